@@ -1,0 +1,144 @@
+/*
+ * eigsol_hip.h — C ABI of the MI355X (gfx950) eigenvalue-solver hot path.
+ *
+ * This is the drop-in boundary for hugoheziyang/PCSC_Eigenvalue_Solver_Project.  The reference has
+ * no FFI: its boundary is the header-only C++ template API, and the seam is the dense/sparse
+ * dispatch inside each entry point.  Every function below replaces the numeric core behind one of
+ * those seams (file:line in the reference):
+ *
+ *   powerMethod<S>                 src/power_method/power_method.hpp:135-148 (impl :47-99)
+ *   shiftedInversePowerMethod<S>   src/power_method/shifted_inverse_power_solver.hpp:112-125 (impl :21-79)
+ *   solve_shifted<S>               src/matrix/solve_shifted.hpp:48-118
+ *   to_hessenberg<S>               src/qr_method/to_hessenberg.hpp:99-119 (impl :23-80)
+ *   qr_eigenvalues<S>              src/qr_method/qr_eigenvalues.hpp:126-147 (impl :40-108)
+ *   Matrix (dense / sparse store)  src/matrix/matrix.hpp:36-246
+ *
+ * The C++ drop-in façade (include/eigsol/...) keeps the reference's names, signatures and
+ * exception messages and calls only this ABI.  Plain pointers and sizes; no torch / HIP types in
+ * the signatures (streams are passed as void*).  Every call returns an eigsol_status; the
+ * detail string of the last failure on the calling thread is eigsol_last_error().
+ *
+ * Scalars: EIGSOL_F64 = double, EIGSOL_C128 = std::complex<double> / double _Complex
+ * (interleaved re, im).  Dense storage is column-major (Matrix::Dense is an Eigen col-major
+ * matrix, matrix.hpp:39-40).  Sparse storage is CSR with int32 indices on the device; the CSC
+ * constructor accepts the reference's canonical Eigen::SparseMatrix<S> (ColMajor, int) layout
+ * (matrix.hpp:43-44).
+ */
+#ifndef EIGSOL_HIP_H
+#define EIGSOL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EIGSOL_ABI_VERSION 1
+
+typedef enum eigsol_status {
+    EIGSOL_OK = 0,
+    EIGSOL_E_NOT_SQUARE = 1,      /* "...: matrix must be square"   power_method.hpp:54 */
+    EIGSOL_E_ZERO_SIZE = 2,       /* "...: matrix has zero size"    power_method.hpp:57 */
+    EIGSOL_E_SCALAR_MISMATCH = 3, /* "...: scalar type mismatch"    power_method.hpp:138 */
+    EIGSOL_E_SIZE_MISMATCH = 4,   /* size mismatch between A and b  solve_shifted.hpp:71 */
+    EIGSOL_E_NOT_DENSE = 5,       /* "only dense matrices"          qr_eigenvalues.hpp:132 */
+    EIGSOL_E_SOLVER = 6,          /* factorisation failed           solve_shifted.hpp:109 */
+    EIGSOL_E_HIP = 7,             /* HIP runtime error */
+    EIGSOL_E_RCCL = 8,            /* RCCL error */
+    EIGSOL_E_INVALID = 9,         /* invalid argument (null pointer, malformed CSR, ...) */
+    EIGSOL_E_NO_DEVICE = 10,      /* no usable gfx950 device */
+    EIGSOL_E_EMPTY = 11,          /* "empty matrix"                 qr_decompose.hpp:39 */
+    EIGSOL_E_UNSUPPORTED = 12     /* structure not supported by the device path */
+} eigsol_status;
+
+typedef enum eigsol_dtype { EIGSOL_F64 = 0, EIGSOL_C128 = 1 } eigsol_dtype;
+
+/* SolverOptions (src/option/solver_option.hpp:14-20). */
+typedef struct eigsol_solver_options {
+    int32_t max_iterations; /* default 1000 */
+    double tolerance;       /* default 1e-10; |a-b| <= tol*(1+|a|), tolerance.hpp:28-33 */
+} eigsol_solver_options;
+
+typedef struct eigsol_ctx eigsol_ctx;     /* one device + one stream (+ optional RCCL communicator) */
+typedef struct eigsol_csr eigsol_csr;     /* device-resident CSR matrix (rows of one rank)          */
+typedef struct eigsol_dense eigsol_dense; /* device-resident column-major dense matrix             */
+typedef struct eigsol_power eigsol_power; /* device-resident power-iteration session               */
+
+/* ---------------------------------------------------------------- library / context */
+int eigsol_abi_version(void);
+const char* eigsol_status_string(int status);
+const char* eigsol_last_error(void);
+int eigsol_device_count(int* count);
+int eigsol_ctx_create(int device, eigsol_ctx** out);
+int eigsol_ctx_destroy(eigsol_ctx* ctx);
+/* Use the caller's hipStream_t (NULL = the context's own stream).  All work is stream-ordered. */
+int eigsol_ctx_set_stream(eigsol_ctx* ctx, void* hip_stream);
+int eigsol_ctx_get_stream(eigsol_ctx* ctx, void** hip_stream);
+int eigsol_ctx_synchronize(eigsol_ctx* ctx);
+
+/* ---------------------------------------------------------------- device memory helpers */
+int eigsol_malloc(eigsol_ctx* ctx, size_t bytes, void** dptr);
+int eigsol_free(eigsol_ctx* ctx, void* dptr);
+int eigsol_memcpy_h2d(eigsol_ctx* ctx, void* dst, const void* src, size_t bytes);
+int eigsol_memcpy_d2h(eigsol_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* ---------------------------------------------------------------- matrices (host in, HBM resident) */
+/* CSR: rowptr[nrows+1], colidx[nnz] (0-based, < ncols), values[nnz].  Columns inside a row are
+ * sorted ascending on upload (the reference's CSC product sums each row in ascending column
+ * order, power_method.hpp:69).  Requires nnz < 2^31 (Eigen StorageIndex = int). */
+int eigsol_csr_create(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
+                      int64_t nnz, const int32_t* rowptr, const int32_t* colidx,
+                      const void* values, eigsol_csr** out);
+/* CSC (Eigen::SparseMatrix<S> compressed storage: outer = column pointers). */
+int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
+                               int64_t nnz, const int32_t* colptr, const int32_t* rowidx,
+                               const void* values, eigsol_csr** out);
+int eigsol_csr_destroy(eigsol_csr* A);
+int eigsol_csr_info(eigsol_csr* A, int64_t* nrows, int64_t* ncols, int64_t* nnz, int* dtype);
+/* y = A*x on device buffers (x: ncols scalars, y: nrows scalars), stream-ordered.  Each row is an
+ * ascending-column sequential sum of products: bitwise equal to the reference's CSC scatter. */
+int eigsol_csr_spmv(eigsol_csr* A, const void* x_dev, void* y_dev);
+
+/* Dense, column-major nrows x ncols (Matrix::Dense<S>). */
+int eigsol_dense_create(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
+                        const void* colmajor, eigsol_dense** out);
+int eigsol_dense_destroy(eigsol_dense* A);
+int eigsol_dense_gemv(eigsol_dense* A, const void* x_dev, void* y_dev);
+
+/* ---------------------------------------------------------------- power method
+ * powerMethod<S>(M, opts) (power_method.hpp:135-148) with an explicit start vector x0 in place
+ * of Vector<S>::Random (power_method.hpp:62; x0 is normalised by the library exactly as
+ * x.normalize()).  The device runs ONE fused product per iteration: the reference's second
+ * product x.dot(A*x) (:81) is the next iteration's y (:69), so the eigenvalue sequence is the
+ * reference's.  Outputs mirror EigenResult<S> (eigen_result.hpp:22-52).
+ * One-shot form: host buffers; lambda_out = 1 scalar, x_out = n scalars (either may be NULL). */
+int eigsol_power_csr(eigsol_csr* A, const eigsol_solver_options* opts, const void* x0,
+                     void* lambda_out, void* x_out, int32_t* iterations, int32_t* converged);
+int eigsol_power_dense(eigsol_dense* A, const eigsol_solver_options* opts, const void* x0,
+                       void* lambda_out, void* x_out, int32_t* iterations, int32_t* converged);
+
+/* Session form (device-resident; what a caller with data already in HBM uses, and what the
+ * benchmark times).  begin() normalises x0 and resets the state; step(k) enqueues k fused
+ * iterations (launches after convergence exit immediately); query() synchronises and reports
+ * whether the reference loop has terminated; finish() writes EigenResult fields.
+ * trace_capacity > 0 records the Rayleigh quotient of every completed iteration on the device. */
+int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power** out);
+int eigsol_power_create_dense(eigsol_dense* A, int32_t trace_capacity, eigsol_power** out);
+int eigsol_power_destroy(eigsol_power* s);
+int eigsol_power_begin(eigsol_power* s, const eigsol_solver_options* opts, const void* x0,
+                       int x0_on_device);
+int eigsol_power_step(eigsol_power* s, int32_t nsteps);
+int eigsol_power_query(eigsol_power* s, int32_t* done, int32_t* launches);
+int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_out_on_device,
+                        int32_t* iterations, int32_t* converged);
+int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int32_t* count);
+/* Device-side description of the hot kernel for roofline accounting: algorithmic bytes moved by
+ * one fused iteration and the grid used. */
+int eigsol_power_kernel_info(eigsol_power* s, double* bytes_per_iteration, int32_t* grid_blocks,
+                             int32_t* tiles);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EIGSOL_HIP_H */

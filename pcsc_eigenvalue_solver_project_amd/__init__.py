@@ -1,0 +1,263 @@
+"""MI355X-native eigenvalue-solver hot path (Python view of the C ABI).
+
+The product is ``libeigsol_hip.so`` (hand-written HIP kernels for gfx950, ``csrc/``) behind the
+C ABI in ``include/eigsol_hip.h`` and the C++ drop-in façade in ``include/eigsol/``.  This package
+is the thin Python view used by the tests and the benchmark; its names follow the reference's
+C++ API (``SolverOptions``, ``EigenResult``, ``power_method`` ≙ ``EigSol::powerMethod``).
+No CPU fallback exists: without the library or a gfx950 device every call raises ``EigSolError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from ._capi import (EIGSOL_C128, EIGSOL_F64, EigSolError, SolverOptionsC, call, check, last_error,
+                    lib)
+
+__all__ = [
+    "EigSolError", "SolverOptions", "EigenResult", "Context", "CsrMatrix", "DenseMatrix",
+    "PowerSession", "power_method", "device_count", "lib", "last_error",
+]
+
+
+@dataclass
+class SolverOptions:
+    """``EigSol::SolverOptions`` (src/option/solver_option.hpp:14-20)."""
+
+    maxIterations: int = 1000
+    tolerance: float = 1e-10
+
+    def to_c(self) -> SolverOptionsC:
+        return SolverOptionsC(int(self.maxIterations), float(self.tolerance))
+
+
+@dataclass
+class EigenResult:
+    """``EigSol::EigenResult<S>`` (src/result/eigen_result.hpp:22-52)."""
+
+    eigenvalue: complex | float
+    eigenvector: np.ndarray
+    iterations: int
+    converged: bool
+
+
+def _dtype_code(dt) -> int:
+    dt = np.dtype(dt)
+    if dt == np.float64:
+        return EIGSOL_F64
+    if dt == np.complex128:
+        return EIGSOL_C128
+    raise EigSolError(3, f"scalar type mismatch: {dt} (supported: float64, complex128)")
+
+
+def _np_dtype(code: int):
+    return np.complex128 if code == EIGSOL_C128 else np.float64
+
+
+def _ptr(a: np.ndarray) -> C.c_void_p:
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    st = lib().eigsol_device_count(C.byref(n))
+    return int(n.value) if st == 0 else 0
+
+
+class Context:
+    """One gfx950 device + one stream (``eigsol_ctx``)."""
+
+    def __init__(self, device: int = 0, stream: Optional[int] = None):
+        h = C.c_void_p()
+        call("eigsol_ctx_create", int(device), C.byref(h))
+        self.handle = h
+        self.device = device
+        if stream is not None:
+            self.set_stream(stream)
+
+    def set_stream(self, stream_ptr: Optional[int]) -> None:
+        call("eigsol_ctx_set_stream", self.handle, C.c_void_p(stream_ptr or 0))
+
+    def synchronize(self) -> None:
+        call("eigsol_ctx_synchronize", self.handle)
+
+    def malloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        call("eigsol_malloc", self.handle, C.c_size_t(nbytes), C.byref(p))
+        return int(p.value or 0)
+
+    def free(self, ptr: int) -> None:
+        call("eigsol_free", self.handle, C.c_void_p(ptr))
+
+    def h2d(self, dptr: int, host: np.ndarray) -> None:
+        host = np.ascontiguousarray(host)
+        call("eigsol_memcpy_h2d", self.handle, C.c_void_p(dptr), _ptr(host), C.c_size_t(host.nbytes))
+
+    def d2h(self, host: np.ndarray, dptr: int) -> np.ndarray:
+        call("eigsol_memcpy_d2h", self.handle, _ptr(host), C.c_void_p(dptr), C.c_size_t(host.nbytes))
+        return host
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib().eigsol_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class CsrMatrix:
+    """Device-resident CSR matrix (``eigsol_csr``)."""
+
+    def __init__(self, ctx: Context, rowptr, colidx, values, shape, layout: str = "csr"):
+        values = np.ascontiguousarray(values)
+        code = _dtype_code(values.dtype)
+        ptr = np.ascontiguousarray(rowptr, dtype=np.int32)
+        idx = np.ascontiguousarray(colidx, dtype=np.int32)
+        nrows, ncols = int(shape[0]), int(shape[1])
+        h = C.c_void_p()
+        fn = "eigsol_csr_create" if layout == "csr" else "eigsol_csr_create_from_csc"
+        call(fn, ctx.handle, code, nrows, ncols, len(idx), _ptr(ptr), _ptr(idx), _ptr(values), C.byref(h))
+        self.ctx, self.handle = ctx, h
+        self.shape = (nrows, ncols)
+        self.nnz = len(idx)
+        self.dtype = _np_dtype(code)
+
+    @classmethod
+    def from_scipy(cls, ctx: Context, M):
+        import scipy.sparse as sp
+        if sp.isspmatrix_csc(M) or isinstance(M, sp.csc_array):
+            M = M.copy()
+            M.sort_indices()
+            return cls(ctx, M.indptr, M.indices, M.data, M.shape, layout="csc")
+        M = sp.csr_matrix(M)
+        M.sort_indices()
+        return cls(ctx, M.indptr, M.indices, M.data, M.shape)
+
+    def spmv(self, x_dev: int, y_dev: int) -> None:
+        call("eigsol_csr_spmv", self.handle, C.c_void_p(x_dev), C.c_void_p(y_dev))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib().eigsol_csr_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DenseMatrix:
+    """Device-resident column-major dense matrix (``eigsol_dense``; ``Matrix::Dense<S>``)."""
+
+    def __init__(self, ctx: Context, A: np.ndarray):
+        A = np.asarray(A)
+        code = _dtype_code(A.dtype)
+        Af = np.asfortranarray(A)
+        h = C.c_void_p()
+        call("eigsol_dense_create", ctx.handle, code, A.shape[0], A.shape[1], _ptr(Af), C.byref(h))
+        self.ctx, self.handle = ctx, h
+        self.shape = A.shape
+        self.dtype = _np_dtype(code)
+
+    def gemv(self, x_dev: int, y_dev: int) -> None:
+        call("eigsol_dense_gemv", self.handle, C.c_void_p(x_dev), C.c_void_p(y_dev))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib().eigsol_dense_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PowerSession:
+    """Device-resident power iteration (``eigsol_power``): begin / step / query / finish."""
+
+    def __init__(self, matrix, trace_capacity: int = 0):
+        h = C.c_void_p()
+        if isinstance(matrix, CsrMatrix):
+            call("eigsol_power_create_csr", matrix.handle, int(trace_capacity), C.byref(h))
+        else:
+            call("eigsol_power_create_dense", matrix.handle, int(trace_capacity), C.byref(h))
+        self.matrix, self.handle = matrix, h
+        self.n = matrix.shape[0]
+        self.dtype = matrix.dtype
+
+    def begin(self, opts: SolverOptions, x0=None, x0_dev: Optional[int] = None) -> None:
+        o = opts.to_c()
+        if x0_dev is not None:
+            call("eigsol_power_begin", self.handle, C.byref(o), C.c_void_p(x0_dev), 1)
+        else:
+            x = np.ascontiguousarray(x0, dtype=self.dtype)
+            self._x0 = x
+            call("eigsol_power_begin", self.handle, C.byref(o), _ptr(x), 0)
+
+    def step(self, n: int) -> None:
+        call("eigsol_power_step", self.handle, int(n))
+
+    def query(self):
+        done, launches = C.c_int32(0), C.c_int32(0)
+        call("eigsol_power_query", self.handle, C.byref(done), C.byref(launches))
+        return bool(done.value), int(launches.value)
+
+    def finish(self, want_vector: bool = True) -> EigenResult:
+        lam = np.zeros(1, dtype=self.dtype)
+        x = np.empty(self.n, dtype=self.dtype) if want_vector else None
+        it, conv = C.c_int32(0), C.c_int32(0)
+        call("eigsol_power_finish", self.handle, _ptr(lam), None if x is None else _ptr(x), 0,
+             C.byref(it), C.byref(conv))
+        ev = complex(lam[0]) if self.dtype == np.complex128 else float(lam[0])
+        return EigenResult(ev, x, int(it.value), bool(conv.value))
+
+    def trace(self, capacity: int) -> np.ndarray:
+        buf = np.zeros(max(capacity, 1), dtype=self.dtype)
+        cnt = C.c_int32(0)
+        call("eigsol_power_trace", self.handle, _ptr(buf), int(capacity), C.byref(cnt))
+        return buf[: cnt.value]
+
+    def kernel_info(self):
+        b, g, t = C.c_double(0), C.c_int32(0), C.c_int32(0)
+        call("eigsol_power_kernel_info", self.handle, C.byref(b), C.byref(g), C.byref(t))
+        return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value}
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib().eigsol_power_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def power_method(matrix, opts: SolverOptions = SolverOptions(), x0=None) -> EigenResult:
+    """``EigSol::powerMethod<S>`` on a device-resident matrix, with an explicit start vector."""
+    if x0 is None:
+        rng = np.random.default_rng(0)
+        x0 = rng.uniform(-1, 1, matrix.shape[0])
+        if matrix.dtype == np.complex128:
+            x0 = x0 + 1j * rng.uniform(-1, 1, matrix.shape[0])
+    x0 = np.ascontiguousarray(x0, dtype=matrix.dtype)
+    lam = np.zeros(1, dtype=matrix.dtype)
+    x = np.empty(matrix.shape[0], dtype=matrix.dtype)
+    it, conv = C.c_int32(0), C.c_int32(0)
+    o = opts.to_c()
+    fn = "eigsol_power_csr" if isinstance(matrix, CsrMatrix) else "eigsol_power_dense"
+    call(fn, matrix.handle, C.byref(o), _ptr(x0), _ptr(lam), _ptr(x), C.byref(it), C.byref(conv))
+    ev = complex(lam[0]) if matrix.dtype == np.complex128 else float(lam[0])
+    return EigenResult(ev, x, int(it.value), bool(conv.value))

@@ -1,0 +1,197 @@
+// Internal header of libeigsol_hip.so (gfx950).  Host + device shared definitions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "eigsol_hip.h"
+
+struct eigsol_ctx;
+struct eigsol_csr;
+struct eigsol_dense;
+
+namespace eigsol {
+
+void ctx_retain(eigsol_ctx* c);
+void ctx_release(eigsol_ctx* c);
+void csr_retain(eigsol_csr* A);
+void csr_release(eigsol_csr* A);
+void dense_retain(eigsol_dense* A);
+void dense_release(eigsol_dense* A);
+
+// ------------------------------------------------------------------ errors
+void set_error(const std::string& msg);
+int fail(int status, const std::string& msg);
+
+#define EIGSOL_HIP(expr)                                                                 \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess)                                                            \
+            return ::eigsol::fail(EIGSOL_E_HIP, std::string(#expr) + ": " +              \
+                                                    hipGetErrorString(_e));              \
+    } while (0)
+
+#define EIGSOL_TRY(expr)                  \
+    do {                                  \
+        int _s = (expr);                  \
+        if (_s != EIGSOL_OK) return _s;   \
+    } while (0)
+
+// ------------------------------------------------------------------ scalars
+// Complex values are (re, im) pairs, 16-byte aligned so one lane loads one value with a single
+// 16-byte load.  Arithmetic mirrors what g++ emits for std::complex<double> in the reference:
+// products (ac-bd, ad+bc) with separate roundings (no FMA contraction: see kernels' pragma).
+struct alignas(16) cplx {
+    double re, im;
+};
+
+__host__ __device__ inline double sq_abs(double a) { return a * a; }
+__host__ __device__ inline double sq_abs(cplx a) { return a.re * a.re + a.im * a.im; }
+
+template <class S> __host__ __device__ inline S s_zero();
+template <> __host__ __device__ inline double s_zero<double>() { return 0.0; }
+template <> __host__ __device__ inline cplx s_zero<cplx>() { return cplx{0.0, 0.0}; }
+
+template <class S> struct dtype_of;
+template <> struct dtype_of<double> { static constexpr int value = EIGSOL_F64; };
+template <> struct dtype_of<cplx> { static constexpr int value = EIGSOL_C128; };
+
+inline size_t scalar_bytes(int dtype) { return dtype == EIGSOL_C128 ? 16 : 8; }
+
+// ------------------------------------------------------------------ power-iteration state
+// Carried state, double-buffered by launch parity (launch with parity p reads st[p], writes st[p^1]).
+struct alignas(16) PowerCarry {
+    double rho_re, rho_im;   // Rayleigh quotient of x_{t-1}  (rho_{t-1})
+    double nrm;              // ||y_{t-1}||  (norm of the launch's input vector)
+    int32_t t;               // launch index that wrote this record
+    int32_t pad;
+};
+
+// Device-resident control block of a session (zeroed / initialised by begin()).
+struct alignas(64) PowerCtl {
+    int32_t done;            // monotonic: set by block 0 of the launch that ends the reference loop
+    uint32_t counter;        // last-arriver ticket for the block-partial reduction
+    int32_t max_iter;
+    int32_t trace_cap;
+    double tol;
+    int32_t nranks;
+    int32_t pad0;
+    // result record (valid once done)
+    double lam_re, lam_im;
+    double final_norm;       // x_final = B[final_parity] / final_norm
+    int32_t iters;
+    int32_t converged;
+    int32_t final_parity;
+    int32_t launches;        // launches that passed the done-check (diagnostic)
+    PowerCarry st[2];
+};
+
+// Reference termination logic of powerMethodImpl (power_method.hpp:68-96) evaluated by the fused
+// device loop.  Launch t computes y_t = A x_t with x_t = y_{t-1}/||y_{t-1}|| (y_{-1} = x0) and the
+// partials of ||y_t||^2 and x_t^H y_t.  Its prologue therefore knows rho_{t-1} = x_{t-1}^H y_{t-1}
+// (the reference's lambdaNew of iteration k = t-2, :81) and ||y_{t-1}|| (the normY of iteration
+// k' = t-1, :72).  Identical on host and device, and evaluated redundantly by every block.
+struct PowerDecision {
+    bool done = false;
+    bool converged = false;
+    bool record = false;     // lambda_k completed: trace[k] = lam
+    int32_t iters = 0;
+    int32_t k = 0;
+    double lam_re = 0.0, lam_im = 0.0;
+};
+
+__host__ __device__ inline double cabs_(double re, double im) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return hypot(re, im);
+#else
+    return std::hypot(re, im);
+#endif
+}
+
+// tolerance.hpp:28-33: |a - b| <= tol * (1 + |a|), a = lambdaNew (power_method.hpp:84).
+__host__ __device__ inline bool close_rel(double are, double aim, double bre, double bim,
+                                          double tol, bool is_complex) {
+    const double dre = are - bre, dim = aim - bim;
+    const double diff = is_complex ? cabs_(dre, dim) : (dre < 0 ? -dre : dre);
+    const double scale = 1.0 + (is_complex ? cabs_(are, aim) : (are < 0 ? -are : are));
+    return diff <= tol * scale;
+}
+
+__host__ __device__ inline PowerDecision power_decide(int32_t t, int32_t max_iter, double tol,
+                                                      bool is_complex, double nrm_tm1,
+                                                      double rho_tm1_re, double rho_tm1_im,
+                                                      double rho_tm2_re, double rho_tm2_im) {
+    PowerDecision d;
+    if (t >= 2) {
+        const int32_t k = t - 2;                 // reference iteration completing now
+        d.record = true;
+        d.k = k;
+        d.lam_re = rho_tm1_re;
+        d.lam_im = rho_tm1_im;
+        if (k >= 1 && close_rel(rho_tm1_re, rho_tm1_im, rho_tm2_re, rho_tm2_im, tol, is_complex)) {
+            d.done = true;                        // :83-90
+            d.converged = true;
+            d.iters = k + 1;
+            return d;
+        }
+        if (k + 1 >= max_iter) {                  // loop bound :68
+            d.done = true;
+            d.iters = k + 1;
+            return d;
+        }
+    }
+    if (t >= 1 && nrm_tm1 == 0.0) {               // normY == 0 :73-76 (iteration k' = t-1)
+        d.done = true;
+        d.iters = t;
+        if (t < 2) { d.lam_re = 0.0; d.lam_im = 0.0; }
+        return d;
+    }
+    return d;
+}
+
+}  // namespace eigsol
+
+// ------------------------------------------------------------------ opaque handle bodies
+// Handles are reference counted: a matrix retains its context and a session retains its matrix,
+// so destroying them in any order (e.g. from garbage-collected bindings) is safe.
+struct eigsol_ctx {
+    std::atomic<int> refs{1};
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;   // active stream (own or caller's)
+    int num_cus = 256;
+    // distributed (filled by eigsol_dist_* when a communicator is attached)
+    void* comm = nullptr;
+    int rank = 0;
+    int nranks = 1;
+};
+
+struct eigsol_csr {
+    std::atomic<int> refs{1};
+    eigsol_ctx* ctx = nullptr;
+    int dtype = EIGSOL_F64;
+    int64_t nrows = 0, ncols = 0, nnz = 0;
+    int32_t* rowptr = nullptr;     // device, nrows+1
+    int32_t* col = nullptr;        // device, nnz (+pad)
+    void* val = nullptr;           // device, nnz (+pad)
+    int32_t* tile_meta = nullptr;  // device, 4 ints per row tile: {r0, r1, e0, e1}
+    int32_t ntiles = 0;
+    int32_t max_tile_rows = 0;
+    int32_t long_tiles = 0;        // tiles holding one row longer than the LDS tile
+};
+
+struct eigsol_dense {
+    std::atomic<int> refs{1};
+    eigsol_ctx* ctx = nullptr;
+    int dtype = EIGSOL_F64;
+    int64_t nrows = 0, ncols = 0;
+    void* a = nullptr;             // device, column-major, leading dimension nrows
+    // GEMV workspace (allocated on first use): per-chunk row partials and per-tile tickets
+    void* ypart = nullptr;
+    uint32_t* tile_cnt = nullptr;
+    int ntr = 0, nchunk = 1, cw = 1;
+};

@@ -1,0 +1,179 @@
+// Device helpers shared by the gfx950 kernels: scalar arithmetic with the reference's rounding,
+// deterministic wave/block reductions and the last-arriver hand-off of block partials.
+#pragma once
+
+#include "internal.hpp"
+
+// Products and sums keep the reference's separate roundings (g++, no -march => no FMA).  This
+// makes every CSR row sum bitwise equal to the reference's CSC scatter (oracle-checked).
+#pragma clang fp contract(off)
+
+namespace eigsol {
+namespace dev {
+
+constexpr int kThreads = 256;   // 4 wave64 per block
+constexpr int kWaves = kThreads / 64;
+
+struct alignas(32) part4 {
+    double a, b, c, d;   // a = sum |y|^2, (b, c) = sum conj(x) y, d unused
+};
+
+__device__ __forceinline__ double mul(double a, double b) { return a * b; }
+__device__ __forceinline__ cplx mul(cplx a, cplx b) {
+    return cplx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+__device__ __forceinline__ double add(double a, double b) { return a + b; }
+__device__ __forceinline__ cplx add(cplx a, cplx b) { return cplx{a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ double sub(double a, double b) { return a - b; }
+__device__ __forceinline__ cplx sub(cplx a, cplx b) { return cplx{a.re - b.re, a.im - b.im}; }
+// x = y / normY (power_method.hpp:78): elementwise division by a real scalar.
+__device__ __forceinline__ double divr(double a, double r) { return a / r; }
+__device__ __forceinline__ cplx divr(cplx a, double r) { return cplx{a.re / r, a.im / r}; }
+// conj(x) * y accumulated into (rr, ri) (Eigen dot conjugates its first argument).
+__device__ __forceinline__ void acc_dot(double& rr, double& /*ri*/, double x, double y) {
+    rr += x * y;
+}
+__device__ __forceinline__ void acc_dot(double& rr, double& ri, cplx x, cplx y) {
+    rr += x.re * y.re + x.im * y.im;
+    ri += x.re * y.im - x.im * y.re;
+}
+__device__ __forceinline__ void set_re_im(double& dst, double re, double /*im*/) { dst = re; }
+__device__ __forceinline__ void set_re_im(cplx& dst, double re, double im) { dst = cplx{re, im}; }
+
+// Deterministic xor-butterfly: every lane ends with the same bits.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Block sum of three doubles in a fixed order; result valid in thread 0.
+__device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double* sm /*3*kWaves*/) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c = wave_sum(c);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sm[w] = a;
+        sm[kWaves + w] = b;
+        sm[2 * kWaves + w] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = sm[0]; b = sm[kWaves]; c = sm[2 * kWaves];
+#pragma unroll
+        for (int i = 1; i < kWaves; ++i) {
+            a += sm[i];
+            b += sm[kWaves + i];
+            c += sm[2 * kWaves + i];
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void st_agent(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// In-launch reduction of per-block partials (MI355X guide §6 Guideline 16, counter form):
+// thread 0 of every block stores its partial write-through (agent-scope sc1 stores), drains
+// them, and takes a ticket; the block that draws G-1 reads every partial with sc1 loads and sums
+// them in block order (deterministic), then publishes the rank partial with plain stores (its
+// consumers run after the kernel boundary).  Must be reached by every block of the grid.
+__device__ __forceinline__ void last_arriver_reduce(double a, double b, double c, part4* blk_part,
+                                                    uint32_t* counter, part4* out, double* sm,
+                                                    int* s_last) {
+    const uint32_t G = gridDim.x;
+    if (threadIdx.x == 0) {
+        part4* p = blk_part + blockIdx.x;
+        st_agent(&p->a, a);
+        st_agent(&p->b, b);
+        st_agent(&p->c, c);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = (tk == G - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    double sa = 0.0, sb = 0.0, sc = 0.0;
+    for (uint32_t i = threadIdx.x; i < G; i += kThreads) {
+        sa += ld_agent(&blk_part[i].a);
+        sb += ld_agent(&blk_part[i].b);
+        sc += ld_agent(&blk_part[i].c);
+    }
+    block_sum3(sa, sb, sc, sm);
+    if (threadIdx.x == 0) {
+        out->a = sa;
+        out->b = sb;
+        out->c = sc;
+        out->d = 0.0;
+        __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Launch prologue of the fused power iteration, evaluated by thread 0 and broadcast through LDS.
+struct alignas(16) Prologue {
+    double nrm;       // ||y_{t-1}||: x_t = y_{t-1} / nrm (nrm == 0 only at t == 0: x0 == 0, kept as is)
+    int32_t go;       // 1: this launch computes; 0: the loop has ended
+    int32_t t;
+};
+
+template <class S>
+__device__ __forceinline__ void power_prologue(PowerCtl* ctl, const part4* rank_part, int nranks,
+                                               int parity, S* trace, Prologue* out) {
+    if (threadIdx.x == 0) {
+        Prologue pr{0.0, 0, 0};
+        const int done = __hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!done) {
+            const PowerCarry in = ctl->st[parity];
+            const int32_t t = in.t + 1;
+            double n2 = 0.0, rr = 0.0, ri = 0.0;
+            for (int r = 0; r < nranks; ++r) {   // rank order: identical on every rank
+                n2 += rank_part[r].a;
+                rr += rank_part[r].b;
+                ri += rank_part[r].c;
+            }
+            const double nrm = sqrt(n2);
+            const bool cplx_ = dtype_of<S>::value == EIGSOL_C128;
+            const PowerDecision d = power_decide(t, ctl->max_iter, ctl->tol, cplx_, nrm, rr, ri,
+                                                 in.rho_re, in.rho_im);
+            if (blockIdx.x == 0) {
+                PowerCarry o;
+                o.rho_re = rr;
+                o.rho_im = ri;
+                o.nrm = nrm;
+                o.t = t;
+                o.pad = 0;
+                ctl->st[parity ^ 1] = o;
+                ctl->launches = t + 1;
+                if (d.record && trace && d.k < ctl->trace_cap) set_re_im(trace[d.k], d.lam_re, d.lam_im);
+                if (d.done) {
+                    ctl->lam_re = d.lam_re;
+                    ctl->lam_im = d.lam_im;
+                    ctl->iters = d.iters;
+                    ctl->converged = d.converged ? 1 : 0;
+                    ctl->final_parity = parity;   // x_final = y_{t-2} / ||y_{t-2}|| in B[t & 1]
+                    ctl->final_norm = in.nrm;
+                    __hip_atomic_store(&ctl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            pr.go = d.done ? 0 : 1;
+            pr.nrm = nrm;
+            pr.t = t;
+        }
+        *out = pr;
+    }
+    __syncthreads();
+}
+
+template <class S>
+__device__ __forceinline__ S scale_in(S y, double nrm) {
+    return nrm > 0.0 ? divr(y, nrm) : y;   // Eigen normalize(): unchanged when the norm is 0
+}
+
+}  // namespace dev
+}  // namespace eigsol

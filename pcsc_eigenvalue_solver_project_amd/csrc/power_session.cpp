@@ -1,0 +1,324 @@
+// Power-iteration session: the host side of the fused device loop (include/eigsol_hip.h).
+//
+// Mirrors powerMethodImpl (src/power_method/power_method.hpp:47-99): begin() plays :60-66
+// (x0 normalisation, lambda = 0, counters), each step() enqueues fused iterations of :68-96,
+// finish() returns the EigenResult fields of :98.  The termination logic runs on the device
+// (power_decide in internal.hpp), so the host only polls a done word between chunks.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace eigsol {
+int csr_grid(eigsol_csr* A, int* grid);
+int csr_power_launch(eigsol_csr* A, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
+                     int nranks, void* my_part, void* blk_part, void* trace, int parity, int grid);
+int dense_grid(eigsol_dense* A, int* grid);
+int dense_power_launch(eigsol_dense* A, void* buf0, void* buf1, PowerCtl* ctl,
+                       const void* rank_part, int nranks, void* my_part, void* blk_part,
+                       void* trace, int parity, int grid);
+int norm_partial_launch(eigsol_ctx* ctx, int dtype, const void* x, int64_t n, PowerCtl* ctl,
+                        void* blk_part, void* out, int grid);
+int scale_out_launch(eigsol_ctx* ctx, int dtype, const void* src, double nrm, void* dst, int64_t n);
+}  // namespace eigsol
+
+using namespace eigsol;
+
+struct eigsol_power {
+    eigsol_ctx* ctx = nullptr;
+    eigsol_csr* csr = nullptr;
+    eigsol_dense* dense = nullptr;
+    int dtype = EIGSOL_F64;
+    int64_t n = 0;            // rows owned (= vector length on one GPU)
+    int64_t nbuf = 0;         // own + ghost entries
+    void* buf[2] = {nullptr, nullptr};
+    PowerCtl* ctl = nullptr;
+    void* rank_part = nullptr;   // part4[nranks]
+    void* my_part = nullptr;     // part4 (== rank_part on one GPU)
+    void* blk_part = nullptr;    // part4[grid]
+    void* trace = nullptr;
+    int32_t trace_cap = 0;
+    int grid = 8;
+    int parity = 0;
+    int launches = 0;
+    bool begun = false;
+    bool trivial = false;     // maxIterations <= 0
+    PowerCtl* host_ctl = nullptr;   // pinned mirror for polling
+    eigsol_solver_options opts{1000, 1e-10};
+};
+
+static constexpr size_t kPart = 32;
+
+static int session_alloc(eigsol_power* s, int32_t trace_cap) {
+    const size_t sb = scalar_bytes(s->dtype);
+    EIGSOL_HIP(hipSetDevice(s->ctx->device));
+    for (int i = 0; i < 2; ++i) EIGSOL_HIP(hipMalloc(&s->buf[i], std::max<int64_t>(s->nbuf, 1) * sb + 64));
+    EIGSOL_HIP(hipMalloc(&s->ctl, sizeof(PowerCtl)));
+    EIGSOL_HIP(hipMalloc(&s->rank_part, kPart * std::max(1, s->ctx->nranks)));
+    s->my_part = s->rank_part;
+    EIGSOL_HIP(hipMalloc(&s->blk_part, kPart * std::max(8, s->grid)));
+    if (trace_cap > 0) EIGSOL_HIP(hipMalloc(&s->trace, (size_t)trace_cap * sb));
+    s->trace_cap = std::max(0, trace_cap);
+    EIGSOL_HIP(hipHostMalloc(&s->host_ctl, sizeof(PowerCtl), hipHostMallocDefault));
+    std::memset(s->host_ctl, 0, sizeof(PowerCtl));
+    EIGSOL_HIP(hipMemsetAsync(s->ctl, 0, sizeof(PowerCtl), s->ctx->stream));
+    EIGSOL_HIP(hipMemsetAsync(s->blk_part, 0, kPart * std::max(8, s->grid), s->ctx->stream));
+    return EIGSOL_OK;
+}
+
+static void session_free(eigsol_power* s) {
+    if (!s) return;
+    hipSetDevice(s->ctx->device);
+    hipStreamSynchronize(s->ctx->stream);
+    hipFree(s->buf[0]);
+    hipFree(s->buf[1]);
+    hipFree(s->ctl);
+    hipFree(s->rank_part);
+    hipFree(s->blk_part);
+    if (s->trace) hipFree(s->trace);
+    if (s->host_ctl) hipHostFree(s->host_ctl);
+    if (s->csr) csr_release(s->csr);
+    if (s->dense) dense_release(s->dense);
+    delete s;
+}
+
+static int launch_iteration(eigsol_power* s) {
+    if (s->csr)
+        return csr_power_launch(s->csr, s->buf[0], s->buf[1], s->ctl, s->rank_part,
+                                s->ctx->nranks, s->my_part, s->blk_part, s->trace, s->parity, s->grid);
+    return dense_power_launch(s->dense, s->buf[0], s->buf[1], s->ctl, s->rank_part, s->ctx->nranks,
+                              s->my_part, s->blk_part, s->trace, s->parity, s->grid);
+}
+
+static int pull_ctl(eigsol_power* s) {
+    EIGSOL_HIP(hipMemcpyAsync(s->host_ctl, s->ctl, sizeof(PowerCtl), hipMemcpyDeviceToHost, s->ctx->stream));
+    EIGSOL_HIP(hipStreamSynchronize(s->ctx->stream));
+    return EIGSOL_OK;
+}
+
+extern "C" {
+
+int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power** out) {
+    if (!A || !out) return fail(EIGSOL_E_INVALID, "eigsol_power_create_csr: null pointer");
+    *out = nullptr;
+    if (A->nrows != A->ncols) return fail(EIGSOL_E_NOT_SQUARE, "powerMethod: matrix must be square");
+    if (A->nrows == 0) return fail(EIGSOL_E_ZERO_SIZE, "powerMethod: matrix has zero size");
+    auto* s = new eigsol_power();
+    s->ctx = A->ctx;
+    s->csr = A;
+    csr_retain(A);
+    s->dtype = A->dtype;
+    s->n = A->nrows;
+    s->nbuf = A->ncols;
+    int rc = csr_grid(A, &s->grid);
+    if (rc == EIGSOL_OK) rc = session_alloc(s, trace_capacity);
+    if (rc != EIGSOL_OK) { session_free(s); return rc; }
+    *out = s;
+    return EIGSOL_OK;
+}
+
+int eigsol_power_create_dense(eigsol_dense* A, int32_t trace_capacity, eigsol_power** out) {
+    if (!A || !out) return fail(EIGSOL_E_INVALID, "eigsol_power_create_dense: null pointer");
+    *out = nullptr;
+    if (A->nrows != A->ncols) return fail(EIGSOL_E_NOT_SQUARE, "powerMethod: matrix must be square");
+    if (A->nrows == 0) return fail(EIGSOL_E_ZERO_SIZE, "powerMethod: matrix has zero size");
+    auto* s = new eigsol_power();
+    s->ctx = A->ctx;
+    s->dense = A;
+    dense_retain(A);
+    s->dtype = A->dtype;
+    s->n = A->nrows;
+    s->nbuf = A->ncols;
+    int rc = dense_grid(A, &s->grid);
+    if (rc == EIGSOL_OK) rc = session_alloc(s, trace_capacity);
+    if (rc != EIGSOL_OK) { session_free(s); return rc; }
+    *out = s;
+    return EIGSOL_OK;
+}
+
+int eigsol_power_destroy(eigsol_power* s) {
+    session_free(s);
+    return EIGSOL_OK;
+}
+
+int eigsol_power_begin(eigsol_power* s, const eigsol_solver_options* opts, const void* x0,
+                       int x0_on_device) {
+    if (!s || !opts || !x0) return fail(EIGSOL_E_INVALID, "eigsol_power_begin: null pointer");
+    EIGSOL_HIP(hipSetDevice(s->ctx->device));
+    hipStream_t st = s->ctx->stream;
+    const size_t sb = scalar_bytes(s->dtype);
+    s->opts = *opts;
+    s->trivial = opts->max_iterations <= 0;
+    // y_{-1} = x0 lives in buf[1] (launch t reads buf[(t-1)&1])
+    EIGSOL_HIP(hipMemcpyAsync(s->buf[1], x0, s->n * sb,
+                              x0_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    PowerCtl init;
+    std::memset(&init, 0, sizeof(init));
+    init.max_iter = opts->max_iterations;
+    init.tol = opts->tolerance;
+    init.trace_cap = s->trace_cap;
+    init.nranks = s->ctx->nranks;
+    init.st[0].t = -1;
+    init.st[1].t = -1;
+    std::memcpy(s->host_ctl, &init, sizeof(init));
+    EIGSOL_HIP(hipMemcpyAsync(s->ctl, s->host_ctl, sizeof(PowerCtl), hipMemcpyHostToDevice, st));
+    // ||x0||^2 partials -> the input norm of launch 0 (x.normalize(), power_method.hpp:62)
+    EIGSOL_TRY(norm_partial_launch(s->ctx, s->dtype, s->buf[1], s->n, s->ctl, s->blk_part, s->my_part, s->grid));
+    EIGSOL_HIP(hipStreamSynchronize(st));   // host_ctl is reused by query()
+    s->parity = 0;
+    s->launches = 0;
+    s->begun = true;
+    return EIGSOL_OK;
+}
+
+int eigsol_power_step(eigsol_power* s, int32_t nsteps) {
+    if (!s || !s->begun) return fail(EIGSOL_E_INVALID, "eigsol_power_step: session not begun");
+    if (s->trivial) return EIGSOL_OK;
+    EIGSOL_HIP(hipSetDevice(s->ctx->device));
+    for (int32_t i = 0; i < nsteps; ++i) {
+        EIGSOL_TRY(launch_iteration(s));
+        s->parity ^= 1;
+        ++s->launches;
+    }
+    return EIGSOL_OK;
+}
+
+int eigsol_power_query(eigsol_power* s, int32_t* done, int32_t* launches) {
+    if (!s || !s->begun) return fail(EIGSOL_E_INVALID, "eigsol_power_query: session not begun");
+    if (s->trivial) {
+        if (done) *done = 1;
+        if (launches) *launches = 0;
+        return EIGSOL_OK;
+    }
+    EIGSOL_HIP(hipSetDevice(s->ctx->device));
+    EIGSOL_TRY(pull_ctl(s));
+    if (done) *done = s->host_ctl->done;
+    if (launches) *launches = s->host_ctl->launches;
+    return EIGSOL_OK;
+}
+
+int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_out_on_device,
+                        int32_t* iterations, int32_t* converged) {
+    if (!s || !s->begun) return fail(EIGSOL_E_INVALID, "eigsol_power_finish: session not begun");
+    EIGSOL_HIP(hipSetDevice(s->ctx->device));
+    hipStream_t st = s->ctx->stream;
+    const size_t sb = scalar_bytes(s->dtype);
+    double lam[2] = {0.0, 0.0};
+    int parity = 1;
+    double fnorm = 0.0;
+    int32_t it = 0, conv = 0;
+    if (s->trivial) {
+        // maxIterations <= 0: lambda = 0, x = normalised x0, 0 iterations (power_method.hpp:61-68)
+        double part[4];
+        EIGSOL_HIP(hipMemcpyAsync(part, s->my_part, sizeof(part), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        fnorm = std::sqrt(part[0]);
+        parity = 1;
+    } else {
+        EIGSOL_TRY(pull_ctl(s));
+        if (!s->host_ctl->done)
+            return fail(EIGSOL_E_INVALID, "eigsol_power_finish: iteration has not terminated");
+        lam[0] = s->host_ctl->lam_re;
+        lam[1] = s->host_ctl->lam_im;
+        parity = s->host_ctl->final_parity;
+        fnorm = s->host_ctl->final_norm;
+        it = s->host_ctl->iters;
+        conv = s->host_ctl->converged;
+    }
+    if (lambda_out) std::memcpy(lambda_out, lam, sb);
+    if (iterations) *iterations = it;
+    if (converged) *converged = conv;
+    if (x_out) {
+        void* src = s->buf[parity];
+        if (x_out_on_device) {
+            EIGSOL_TRY(scale_out_launch(s->ctx, s->dtype, src, fnorm, x_out, s->n));
+            EIGSOL_HIP(hipStreamSynchronize(st));
+        } else {
+            void* tmp = s->buf[parity ^ 1];
+            EIGSOL_TRY(scale_out_launch(s->ctx, s->dtype, src, fnorm, tmp, s->n));
+            EIGSOL_HIP(hipMemcpyAsync(x_out, tmp, s->n * sb, hipMemcpyDeviceToHost, st));
+            EIGSOL_HIP(hipStreamSynchronize(st));
+        }
+    }
+    return EIGSOL_OK;
+}
+
+int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int32_t* count) {
+    if (!s || !s->begun) return fail(EIGSOL_E_INVALID, "eigsol_power_trace: session not begun");
+    int32_t n = 0;
+    if (!s->trivial && s->trace) {
+        EIGSOL_TRY(pull_ctl(s));
+        n = s->host_ctl->done ? s->host_ctl->iters : std::max(0, s->host_ctl->launches - 2);
+        n = std::min(n, s->trace_cap);
+        if (trace_host && capacity > 0) {
+            const int32_t m = std::min(n, capacity);
+            EIGSOL_HIP(hipMemcpy(trace_host, s->trace, (size_t)m * scalar_bytes(s->dtype), hipMemcpyDeviceToHost));
+        }
+    }
+    if (count) *count = n;
+    return EIGSOL_OK;
+}
+
+int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int32_t* tiles) {
+    if (!s) return fail(EIGSOL_E_INVALID, "eigsol_power_kernel_info: null session");
+    const double sb = (double)scalar_bytes(s->dtype);
+    if (s->csr) {
+        // values + int32 columns + int32 row pointers + x read once + y written once
+        const double nnz = (double)s->csr->nnz, n = (double)s->csr->nrows;
+        if (bytes) *bytes = (sb + 4.0) * nnz + 4.0 * (n + 1.0) + 2.0 * sb * n;
+        if (tiles) *tiles = s->csr->ntiles;
+    } else {
+        const double n = (double)s->dense->nrows;
+        if (bytes) *bytes = sb * n * n + 2.0 * sb * n;
+        if (tiles) *tiles = 0;
+    }
+    if (grid) *grid = s->grid;
+    return EIGSOL_OK;
+}
+
+// One-shot solves: begin / step in doubling chunks until the device reports termination / finish.
+static int run_to_completion(eigsol_power* s, const eigsol_solver_options* opts, const void* x0,
+                             void* lambda_out, void* x_out, int32_t* iterations, int32_t* converged) {
+    EIGSOL_TRY(eigsol_power_begin(s, opts, x0, 0));
+    if (!s->trivial) {
+        // Upper bound on launches: maxIterations + 2 (launch maxIter+1 only decides).
+        const int64_t cap = (int64_t)opts->max_iterations + 2;
+        int64_t issued = 0;
+        int32_t chunk = 4;
+        int32_t done = 0;
+        while (!done) {
+            const int32_t k = (int32_t)std::min<int64_t>(chunk, std::max<int64_t>(1, cap - issued));
+            EIGSOL_TRY(eigsol_power_step(s, k));
+            issued += k;
+            EIGSOL_TRY(eigsol_power_query(s, &done, nullptr));
+            chunk = std::min(chunk * 2, 64);
+            if (!done && issued >= cap + 4)
+                return fail(EIGSOL_E_SOLVER, "power iteration did not terminate (internal error)");
+        }
+    }
+    return eigsol_power_finish(s, lambda_out, x_out, 0, iterations, converged);
+}
+
+int eigsol_power_csr(eigsol_csr* A, const eigsol_solver_options* opts, const void* x0,
+                     void* lambda_out, void* x_out, int32_t* iterations, int32_t* converged) {
+    if (!opts || !x0) return fail(EIGSOL_E_INVALID, "eigsol_power_csr: null opts/x0");
+    eigsol_power* s = nullptr;
+    EIGSOL_TRY(eigsol_power_create_csr(A, 0, &s));
+    const int rc = run_to_completion(s, opts, x0, lambda_out, x_out, iterations, converged);
+    session_free(s);
+    return rc;
+}
+
+int eigsol_power_dense(eigsol_dense* A, const eigsol_solver_options* opts, const void* x0,
+                       void* lambda_out, void* x_out, int32_t* iterations, int32_t* converged) {
+    if (!opts || !x0) return fail(EIGSOL_E_INVALID, "eigsol_power_dense: null opts/x0");
+    eigsol_power* s = nullptr;
+    EIGSOL_TRY(eigsol_power_create_dense(A, 0, &s));
+    const int rc = run_to_completion(s, opts, x0, lambda_out, x_out, iterations, converged);
+    session_free(s);
+    return rc;
+}
+
+}  // extern "C"

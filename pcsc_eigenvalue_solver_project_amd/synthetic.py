@@ -1,0 +1,123 @@
+"""Seeded synthetic matrices of SURVEY.md §8(d) (benchmark and parity inputs).
+
+* ``band``    — k distinct columns per row inside a (2w+1)-wide window around the diagonal,
+                values U(-1, 1), one planted diagonal spike A(s, s) = 10 at s = n_global // 2 so the
+                dominant eigenvalue is well separated.  Locality-preserving: row blocks only need a
+                halo of w entries from their neighbours (the multi-GPU headline, §8e).
+* ``uniform`` — k distinct columns uniform over [0, n), values U(0, 1] (nonnegative: Perron root
+                ≈ k/2).  The gather-stress case.
+* ``triu_complex`` — config 5: complex upper-triangular CSR with an explicit diagonal whose
+                entries lie in the annulus 1 <= |z| <= 2, one planted interior eigenvalue
+                d* = 1.5 e^{0.7i} isolated by 0.05 (the eigenvalues are the diagonal).
+
+All generators return CSR arrays (rowptr int32, colidx int32 sorted per row, values) for rows
+[row0, row0 + nrows) of an n_global x n_global matrix.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _distinct_sorted(rng, nrows: int, k: int, span: int) -> np.ndarray:
+    """k strictly increasing integers in [0, span) per row (sorted-sample + arange trick)."""
+    r = rng.integers(0, span - k + 1, size=(nrows, k), dtype=np.int64)
+    r.sort(axis=1)
+    r += np.arange(k, dtype=np.int64)[None, :]
+    return r
+
+
+def band(n_global: int, k: int, w: int = 64, seed: int = 42, row0: int = 0, nrows: int | None = None,
+         spike: float = 10.0):
+    if nrows is None:
+        nrows = n_global - row0
+    width = 2 * w + 1
+    if n_global < width or k > width:
+        raise ValueError("band: n_global must be >= 2w+1 and k <= 2w+1")
+    rng = np.random.default_rng([seed, row0])
+    rows = np.arange(row0, row0 + nrows, dtype=np.int64)
+    start = np.clip(rows - w, 0, n_global - width)
+    cols = start[:, None] + _distinct_sorted(rng, nrows, k, width)
+    vals = rng.uniform(-1.0, 1.0, size=(nrows, k))
+    s = n_global // 2
+    if row0 <= s < row0 + nrows:
+        i = s - row0
+        c0 = min(max(s - k // 2, 0), n_global - k)
+        cols[i] = np.arange(c0, c0 + k)
+        vals[i, s - c0] = spike
+    rowptr = np.arange(0, (nrows + 1) * k, k, dtype=np.int64)
+    return rowptr.astype(np.int32), cols.reshape(-1).astype(np.int32), vals.reshape(-1)
+
+
+def uniform(n_global: int, k: int, seed: int = 42, row0: int = 0, nrows: int | None = None):
+    if nrows is None:
+        nrows = n_global - row0
+    rng = np.random.default_rng([seed, row0, 1])
+    cols = _distinct_sorted(rng, nrows, k, n_global)
+    vals = 1.0 - rng.random(size=(nrows, k))   # (0, 1]
+    rowptr = np.arange(0, (nrows + 1) * k, k, dtype=np.int64)
+    return rowptr.astype(np.int32), cols.reshape(-1).astype(np.int32), vals.reshape(-1)
+
+
+def triu_complex(n: int, k: int, seed: int = 42, target=1.5 * np.exp(0.7j), gap: float = 0.05):
+    """Upper-triangular complex CSR, k nonzeros per row including the diagonal (config 5)."""
+    rng = np.random.default_rng([seed, 5])
+    # diagonal in the annulus, none within `gap` of the target except the planted one
+    r = rng.uniform(1.0, 2.0, n)
+    th = rng.uniform(0, 2 * np.pi, n)
+    d = r * np.exp(1j * th)
+    bad = np.abs(d - target) < gap
+    while bad.any():
+        d[bad] = rng.uniform(1.0, 2.0, bad.sum()) * np.exp(1j * rng.uniform(0, 2 * np.pi, bad.sum()))
+        bad = np.abs(d - target) < gap
+    p = n // 3
+    d[p] = target
+    rows, cols, vals = [], [], []
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    off_k = k - 1
+    all_cols = []
+    all_vals = []
+    for_counts = np.zeros(n, dtype=np.int64)
+    # off-diagonal columns uniform in (i, n): vectorised per row count min(off_k, n-1-i)
+    cnt = np.minimum(off_k, n - 1 - np.arange(n))
+    for_counts[:] = cnt + 1
+    rowptr[1:] = np.cumsum(for_counts)
+    nnz = int(rowptr[-1])
+    colidx = np.empty(nnz, dtype=np.int64)
+    values = np.empty(nnz, dtype=np.complex128)
+    scale = 0.5 / max(off_k, 1)
+    full = cnt == off_k
+    idx_full = np.nonzero(full)[0]
+    if idx_full.size:
+        span = n - 1 - idx_full   # columns in (i, n) -> offsets in [0, span)
+        u = rng.random((idx_full.size, off_k))
+        # distinct offsets: sorted sample with arange trick on the per-row span
+        r_ = np.floor(u * (span[:, None] - off_k + 1)).astype(np.int64)
+        r_.sort(axis=1)
+        r_ += np.arange(off_k)[None, :]
+        oc = idx_full[:, None] + 1 + r_
+        base = rowptr[idx_full]
+        colidx[base[:, None] + np.arange(1, off_k + 1)[None, :]] = oc
+        values[base[:, None] + np.arange(1, off_k + 1)[None, :]] = scale * (
+            rng.uniform(-1, 1, (idx_full.size, off_k)) + 1j * rng.uniform(-1, 1, (idx_full.size, off_k)))
+    for i in np.nonzero(~full)[0]:
+        b = rowptr[i]
+        c = int(cnt[i])
+        colidx[b + 1: b + 1 + c] = np.arange(i + 1, i + 1 + c)
+        values[b + 1: b + 1 + c] = scale * (rng.uniform(-1, 1, c) + 1j * rng.uniform(-1, 1, c))
+    colidx[rowptr[:-1]] = np.arange(n)
+    values[rowptr[:-1]] = d
+    return rowptr.astype(np.int32), colidx.astype(np.int32), values, d
+
+
+def start_vector(n: int, dtype=np.float64, seed: int = 7, row0: int = 0) -> np.ndarray:
+    """x0 of SURVEY §8d: U(-1, 1) per (re, im) component, seed 7 (normalised by the solver)."""
+    rng = np.random.default_rng([seed, row0])
+    x = rng.uniform(-1.0, 1.0, n)
+    if np.dtype(dtype) == np.complex128:
+        x = x + 1j * rng.uniform(-1.0, 1.0, n)
+    return x.astype(dtype)
+
+
+def csr_bytes_per_iteration(n: int, nnz: int, scalar_bytes: int = 8) -> float:
+    """Algorithmic HBM bytes of one fused power iteration."""
+    return (scalar_bytes + 4.0) * nnz + 4.0 * (n + 1) + 2.0 * scalar_bytes * n
