@@ -45,8 +45,11 @@ struct CsrArgs {
     const int32_t* rowptr;
     const int32_t* col;
     const S* val;
-    const int4* tile_meta;   // per tile {r0, r1, e0, e1}
+    const int4* tile_meta;   // per tile {r0, r1, e0, e1}: short tiles first, then long rows
+    const int2* tile_win;    // per short tile: x window [w0, w1] covering its columns and rows
     int32_t ntiles;
+    int32_t nshort;
+    int32_t xlen;            // entries of the input vector (own + ghost)
     int32_t nrows;
     const S* x_plain;        // plain SpMV input (kPower == false)
     S* y_plain;              // plain SpMV output
@@ -80,47 +83,158 @@ struct TileRegs {
     int rp0, rp1;
 };
 
-__device__ __forceinline__ bool short_tile(int4 m, int tn) { return m.w - m.z <= tn; }
-
-// Issue every load of a tile's value/column stream and of the lane's row pointers.
+// Issue every load of a short tile's value/column stream and of the lane's row pointers.
+// Branch-free on purpose: an exec-masked branch around each load makes hipcc wait vmcnt(0) per
+// load (MI355X guide §5 "Projection GEMM" item 4(c)), which serialises the pipeline.  The streams
+// are padded by one tile on the device, and every column index (padding included) is valid.
 template <class S>
 __device__ __forceinline__ void load_tile(const CsrArgs<S>& a, int4 m, TileRegs<S>& R) {
     constexpr int P = TileRegs<S>::P;
     const int tid = threadIdx.x;
-    if (short_tile(m, Tile<S>::kCap)) {
-        if constexpr (std::is_same_v<S, double>) {
-            const int q0 = m.z & ~1;
+    if constexpr (std::is_same_v<S, double>) {
+        const int q0 = m.z & ~1;
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
-                const int q = q0 + 2 * (tid + p * kThreads);
-                if (q < m.w) {
-                    R.s[p].v = *reinterpret_cast<const double2*>(a.val + q);
-                    R.s[p].c = *reinterpret_cast<const int2*>(a.col + q);
-                }
-            }
-        } else {
+        for (int p = 0; p < P; ++p) {
+            const int q = q0 + 2 * (tid + p * kThreads);
+            R.s[p].v = *reinterpret_cast<const double2*>(a.val + q);
+            R.s[p].c = *reinterpret_cast<const int2*>(a.col + q);
+        }
+    } else {
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
-                const int q = m.z + tid + p * kThreads;
-                if (q < m.w) {
-                    R.s[p].v = a.val[q];
-                    R.s[p].c = a.col[q];
-                }
-            }
+        for (int p = 0; p < P; ++p) {
+            const int q = m.z + tid + p * kThreads;
+            R.s[p].v = a.val[q];
+            R.s[p].c = a.col[q];
         }
     }
-    if (tid < m.y - m.x) {
-        R.rp0 = a.rowptr[m.x + tid];
-        R.rp1 = a.rowptr[m.x + tid + 1];
+    const int r = min(m.x + tid, a.nrows - 1);
+    R.rp0 = a.rowptr[r];
+    R.rp1 = a.rowptr[r + 1];
+}
+
+// Gathers of one tile's x entries (all in flight together; unconditional, see load_tile).
+template <class S, int kMode>
+__device__ __forceinline__ void issue_gathers(const TileRegs<S>& R, const S* xin,
+                                              S (&xg)[TileRegs<S>::P][Slot<S>::kNnz]) {
+    constexpr int P = TileRegs<S>::P;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        // The empty asm pins each column's first use here: without it hipcc computes the gather
+        // address as soon as the prefetched column lands (before the previous barrier) and
+        // waits for the whole prefetch there.
+        if constexpr (std::is_same_v<S, double>) {
+            int c0 = R.s[p].c.x, c1 = R.s[p].c.y;
+            asm volatile("" : "+v"(c0), "+v"(c1));
+            xg[p][0] = kMode == 1 ? 1.0 : xin[c0];
+            xg[p][1] = kMode == 1 ? 1.0 : xin[c1];
+        } else {
+            int c0 = R.s[p].c;
+            asm volatile("" : "+v"(c0));
+            xg[p][0] = xin[c0];
+        }
     }
 }
 
+// products a_ij * x_j (x_j = y_j / nrm, the reference's x = y / normY) -> LDS.  Slots outside
+// the tile write to the scratch element `dummy`.
+template <class S, bool kPower, int kMode>
+__device__ __forceinline__ void write_products(const TileRegs<S>& R, int4 m,
+                                               const S (&xg)[TileRegs<S>::P][Slot<S>::kNnz],
+                                               double nrm, double rnrm, S* prod, int dummy) {
+    constexpr int P = TileRegs<S>::P;
+    constexpr int NPS = Slot<S>::kNnz;
+    const int tid = threadIdx.x;
+    const int q0 = std::is_same_v<S, double> ? (m.z & ~1) : m.z;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int qb = q0 + NPS * (tid + p * kThreads);
+        if constexpr (std::is_same_v<S, double>) {
+            double x0 = xg[p][0], x1 = xg[p][1];
+            if constexpr (kPower && kMode == 2) {
+                x0 = x0 * rnrm;
+                x1 = x1 * rnrm;
+            } else if constexpr (kPower) {
+                x0 = scale_in(x0, nrm);
+                x1 = scale_in(x1, nrm);
+            }
+            const int i0 = (qb >= m.z && qb < m.w) ? lds_idx(qb - m.z) : dummy;
+            const int i1 = (qb + 1 < m.w) ? lds_idx(qb + 1 - m.z) : dummy;
+            prod[i0] = R.s[p].v.x * x0;
+            prod[i1] = R.s[p].v.y * x1;
+        } else {
+            S xv = xg[p][0];
+            if constexpr (kPower) xv = scale_in(xv, nrm);
+            const int i0 = qb < m.w ? lds_idx(qb - m.z) : dummy;
+            prod[i0] = mul(R.s[p].v, xv);
+        }
+    }
+}
+
+// Long rows (one row per tile, longer than an LDS tile): strided partial sums and a fixed-order
+// block reduction (deterministic); tiles dealt round-robin over the grid.
 template <class S, bool kPower>
+__device__ __forceinline__ void long_rows_pass(const CsrArgs<S>& a, const S* xin, S* yout,
+                                               double nrm, double& n2, double& rr, double& ri,
+                                               double* sm) {
+    const int tid = threadIdx.x;
+    for (int lt = a.nshort + blockIdx.x; lt < a.ntiles; lt += gridDim.x) {
+        const int4 m = a.tile_meta[lt];
+        double pr = 0.0, pi = 0.0, dummy = 0.0;
+        for (int q = m.z + tid; q < m.w; q += kThreads) {
+            S xv = xin[a.col[q]];
+            if constexpr (kPower) xv = scale_in(xv, nrm);
+            const S pq = mul(a.val[q], xv);
+            if constexpr (std::is_same_v<S, double>) {
+                pr += pq;
+            } else {
+                pr += pq.re;
+                pi += pq.im;
+            }
+        }
+        block_sum3(pr, pi, dummy, sm);
+        if (tid == 0) {
+            S sacc;
+            set_re_im(sacc, pr, pi);
+            yout[m.x] = sacc;
+            if constexpr (kPower) {
+                const S xi = scale_in(xin[m.x], nrm);
+                n2 += sq_abs(sacc);
+                acc_dot(rr, ri, xi, sacc);
+            }
+        }
+    }
+}
+
+// Sequential ascending-column sum of one row's products from LDS (the reference's order).
+template <class S, int kMode = 0>
+__device__ __forceinline__ S row_sum(const S* pb, int k0, int k1) {
+    S sacc = s_zero<S>();
+    if constexpr (kMode == 3) {
+        if (k1 > k0) sacc = pb[lds_idx(k0)];
+    } else {
+        for (int k = k0; k < k1; ++k) sacc = add(sacc, pb[lds_idx(k)]);
+    }
+    return sacc;
+}
+
+// kMode (diagnostic ablations, EIGSOL_CSR_ABLATION): 0 full; 1 no x gather; 2 reciprocal scaling;
+// 3 no phase-2 row sums.  Only mode 0 is a product path.
+//
+// Short tiles run as a software pipeline with ONE barrier per tile and two LDS product buffers:
+//   iteration i:  issue gathers of tile i+1 | issue stream loads of tile i+2
+//                 row sums of tile i (LDS buffer b)          <- overlaps the gathers' latency
+//                 products of tile i+1 -> LDS buffer b^1 ; barrier
+// Buffer b^1 was last read by the row sums of iteration i-1, which precede the barrier that
+// ended iteration i-1, so one barrier per tile orders both hazards.
+template <class S, bool kPower, int kMode = 0>
 __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity) {
     constexpr int TN = Tile<S>::kNnz;
     constexpr int P = TileRegs<S>::P;
     constexpr int NPS = Slot<S>::kNnz;
-    __shared__ S prod[TN + TN / 32];
+    constexpr int LDSN = TN + TN / 32;
+    __shared__ S prod[2 * LDSN];
+    __shared__ int2 rows[2][kThreads];
+    __shared__ S xrows[kPower ? 2 : 1][kThreads];
     __shared__ double sm[3 * kWaves];
     __shared__ Prologue pro;
     __shared__ int s_last;
@@ -138,118 +252,257 @@ __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity)
         xin = a.x_plain;
         yout = a.y_plain;
     }
-    (void)nrm;
+    const double rnrm = nrm > 0.0 ? 1.0 / nrm : 1.0;
+    (void)rnrm;
     const int tid = threadIdx.x;
     double n2 = 0.0, rr = 0.0, ri = 0.0;
 
-    // XCD-contiguous tile ranges: block b works in group b % 8 on tiles of that group's chunk.
+    // XCD-contiguous ranges of short tiles: block b works in group b % 8 on that group's chunk.
     const int nb = gridDim.x >> 3;
-    const int chunk = (a.ntiles + 7) >> 3;
+    const int chunk = (a.nshort + 7) >> 3;
     const int tbeg = (blockIdx.x & 7) * chunk;
-    const int tend = min(a.ntiles, tbeg + chunk);
+    const int tend = min(a.nshort, tbeg + chunk);
     int t = tbeg + (blockIdx.x >> 3);
 
     if (t < tend) {
-        int4 m = a.tile_meta[t];
-        TileRegs<S> R;
-        load_tile(a, m, R);
-        for (;;) {
-            const int tn = t + nb;
-            const bool has_next = tn < tend;
-            int4 mn = m;
-            if (has_next) mn = a.tile_meta[tn];
-            const int nr = m.y - m.x;
-            if (short_tile(m, Tile<S>::kCap)) {
-                // ---- gathers of the current tile, all in flight together
-                S xg[P][NPS];
-                const int q0 = std::is_same_v<S, double> ? (m.z & ~1) : m.z;
-#pragma unroll
-                for (int p = 0; p < P; ++p) {
-                    const int qb = q0 + NPS * (tid + p * kThreads);
-                    if constexpr (std::is_same_v<S, double>) {
-                        if (qb >= m.z && qb < m.w) xg[p][0] = xin[R.s[p].c.x];
-                        if (qb + 1 < m.w) xg[p][NPS - 1] = xin[R.s[p].c.y];
-                    } else {
-                        if (qb < m.w) xg[p][0] = xin[R.s[p].c];
-                    }
+        // Loop-carried per-row state (row pointers, x_i for the Rayleigh term) goes through LDS so
+        // the only registers live across the back-edge are the prefetched stream: keeps hipcc's
+        // s_waitcnt counting exact instead of vmcnt(0) at the first use of a loop-carried value.
+        const int last = tend - 1;
+        int4 mc = a.tile_meta[t];
+        TileRegs<S> Rc;
+        load_tile(a, mc, Rc);
+        S xg[P][NPS];
+        issue_gathers<S, kMode>(Rc, xin, xg);
+        S xrow = s_zero<S>();
+        if constexpr (kPower) xrow = xin[min(mc.x + tid, a.nrows - 1)];
+        int tn = t + nb;
+        int4 mn = a.tile_meta[min(tn, last)];
+        TileRegs<S> Rn;
+        load_tile(a, mn, Rn);
+        write_products<S, kPower, kMode>(Rc, mc, xg, nrm, rnrm, prod, LDSN - 1);
+        rows[0][tid] = make_int2(Rc.rp0, Rc.rp1);
+        if constexpr (kPower) xrows[0][tid] = xrow;
+        __syncthreads();
+        int b = 0;
+        // One pipeline step.  `Rnx` holds the next tile's stream (already in flight), `Rld`
+        // receives the stream two tiles ahead.  The loop is unrolled by two with the register
+        // sets swapping roles, so the prefetch is never copied (a copy would force its wait).
+        auto step = [&](TileRegs<S>& Rnx, TileRegs<S>& Rld) -> bool {
+            const int t2 = tn + nb;
+            // meta first, so its wait does not cover the gathers issued after it
+            const int4 m2 = a.tile_meta[min(t2, last)];
+            issue_gathers<S, kMode>(Rnx, xin, xg);
+            if constexpr (kPower) xrow = xin[min(mn.x + tid, a.nrows - 1)];
+            load_tile(a, m2, Rld);
+            // row sums of the current tile from LDS buffer b (ascending-column sequential sums)
+            if (tid < mc.y - mc.x) {
+                const S* pb = prod + b * LDSN;
+                const int2 rp = rows[b][tid];
+                const int k0 = rp.x - mc.z;
+                const int k1 = rp.y - mc.z;
+                S sacc = s_zero<S>();
+                if constexpr (kMode == 3) {
+                    if (k1 > k0) sacc = pb[lds_idx(k0)];
+                } else {
+                    for (int k = k0; k < k1; ++k) sacc = add(sacc, pb[lds_idx(k)]);
                 }
-                S xrow = s_zero<S>();
-                if (kPower && tid < nr) xrow = xin[m.x + tid];
-                // ---- prefetch the next tile's stream while the gathers are in flight
-                TileRegs<S> Rn;
-                if (has_next) load_tile(a, mn, Rn);
-                // ---- products -> LDS
-#pragma unroll
-                for (int p = 0; p < P; ++p) {
-                    const int qb = q0 + NPS * (tid + p * kThreads);
-                    if constexpr (std::is_same_v<S, double>) {
-                        if (qb >= m.z && qb < m.w) {
-                            double xv = xg[p][0];
-                            if constexpr (kPower) xv = scale_in(xv, nrm);
-                            prod[lds_idx(qb - m.z)] = R.s[p].v.x * xv;
-                        }
-                        if (qb + 1 < m.w) {
-                            double xv = xg[p][NPS - 1];
-                            if constexpr (kPower) xv = scale_in(xv, nrm);
-                            prod[lds_idx(qb + 1 - m.z)] = R.s[p].v.y * xv;
-                        }
-                    } else {
-                        if (qb < m.w) {
-                            S xv = xg[p][0];
-                            if constexpr (kPower) xv = scale_in(xv, nrm);
-                            prod[lds_idx(qb - m.z)] = mul(R.s[p].v, xv);
-                        }
-                    }
+                yout[mc.x + tid] = sacc;
+                if constexpr (kPower) {
+                    const S xi = scale_in(xrows[b][tid], nrm);
+                    n2 += sq_abs(sacc);
+                    acc_dot(rr, ri, xi, sacc);
                 }
-                __syncthreads();
-                // ---- one lane per row: sequential ascending-column sum (reference order)
-                if (tid < nr) {
-                    const int k0 = R.rp0 - m.z;
-                    const int k1 = R.rp1 - m.z;
-                    S sacc = s_zero<S>();
-                    for (int k = k0; k < k1; ++k) sacc = add(sacc, prod[lds_idx(k)]);
-                    yout[m.x + tid] = sacc;
-                    if constexpr (kPower) {
-                        const S xi = scale_in(xrow, nrm);
-                        n2 += sq_abs(sacc);
-                        acc_dot(rr, ri, xi, sacc);
-                    }
-                }
-                __syncthreads();
-                if (!has_next) break;
-                R = Rn;
-            } else {
-                // ---- long row (m.y == m.x + 1): strided partial sums, fixed-order block reduction
-                double pr = 0.0, pi = 0.0, dummy = 0.0;
-                for (int q = m.z + tid; q < m.w; q += kThreads) {
-                    S xv = xin[a.col[q]];
-                    if constexpr (kPower) xv = scale_in(xv, nrm);
-                    const S pq = mul(a.val[q], xv);
-                    if constexpr (std::is_same_v<S, double>) {
-                        pr += pq;
-                    } else {
-                        pr += pq.re;
-                        pi += pq.im;
-                    }
-                }
-                block_sum3(pr, pi, dummy, sm);
-                if (tid == 0) {
-                    S sacc;
-                    set_re_im(sacc, pr, pi);
-                    yout[m.x] = sacc;
-                    if constexpr (kPower) {
-                        const S xi = scale_in(xin[m.x], nrm);
-                        n2 += sq_abs(sacc);
-                        acc_dot(rr, ri, xi, sacc);
-                    }
-                }
-                if (!has_next) break;
-                load_tile(a, mn, R);
             }
-            m = mn;
-            t = tn;
+            if (tn >= tend) return true;
+            write_products<S, kPower, kMode>(Rnx, mn, xg, nrm, rnrm, prod + (b ^ 1) * LDSN, LDSN - 1);
+            rows[b ^ 1][tid] = make_int2(Rnx.rp0, Rnx.rp1);
+            if constexpr (kPower) xrows[b ^ 1][tid] = xrow;
+            // keep the next step's address arithmetic (which waits for the prefetch) below this
+            // barrier: hipcc otherwise hoists it and waits for the prefetched stream here.
+            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+            b ^= 1;
+            mc = mn;
+            mn = m2;
+            tn = t2;
+            return false;
+        };
+        TileRegs<S>& Ra = Rn;
+        TileRegs<S>& Rb = Rc;   // Rc's stream is consumed: reuse its registers
+        for (;;) {
+            if (step(Ra, Rb)) break;
+            if (step(Rb, Ra)) break;
         }
     }
+
+    long_rows_pass<S, kPower>(a, xin, yout, nrm, n2, rr, ri, sm);
+    if constexpr (kPower) {
+        block_sum3(n2, rr, ri, sm);
+        last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+    }
+}
+
+// ============================================================================ windowed pipeline
+// For tiles whose columns (and rows) fall in a window of at most kWin entries — banded and
+// locality-ordered matrices, the multi-GPU headline — the tile's slice of x is staged into LDS with
+// coalesced loads (scaled by 1/||y|| once per element) and the products gather from LDS instead of
+// global memory.  Per step (one tile), two barriers:
+//   issue: stream + window loads of tile i+2          (registers, two tiles ahead)
+//   store window of tile i+1 -> xwin[b^1]            (loaded one step ago)
+//   row sums of tile i (prod, xwin[b])               ; barrier A
+//   products of tile i+1 (xwin[b^1]) -> prod, rows   ; barrier B
+template <class S> struct Win;
+template <> struct Win<double> { static constexpr int kWin = 1024; };
+template <> struct Win<cplx> { static constexpr int kWin = 512; };
+
+template <class S>
+struct WinRegs {
+    static constexpr int K = Win<S>::kWin / kThreads;
+    S v[K];
+};
+
+// Branch-free window load: indices past the end of x are clamped (those slots lie beyond w1).
+template <class S>
+__device__ __forceinline__ void load_window(const S* xin, int2 w, int xlen, WinRegs<S>& W) {
+#pragma unroll
+    for (int k = 0; k < WinRegs<S>::K; ++k) W.v[k] = xin[min(w.x + (int)threadIdx.x + k * kThreads, xlen - 1)];
+}
+
+template <class S, bool kPower>
+__device__ __forceinline__ void store_window(const WinRegs<S>& W, double nrm, S* xw) {
+#pragma unroll
+    for (int k = 0; k < WinRegs<S>::K; ++k) {
+        S v = W.v[k];
+        if constexpr (kPower) v = scale_in(v, nrm);
+        xw[threadIdx.x + k * kThreads] = v;
+    }
+}
+
+// products of a short tile with x read from the LDS window
+template <class S>
+__device__ __forceinline__ void win_products(const TileRegs<S>& R, int4 m, int w0, const S* xw,
+                                             S* prod, int dummy) {
+    constexpr int P = TileRegs<S>::P;
+    constexpr int NPS = Slot<S>::kNnz;
+    const int tid = threadIdx.x;
+    const int q0 = std::is_same_v<S, double> ? (m.z & ~1) : m.z;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int qb = q0 + NPS * (tid + p * kThreads);
+        if constexpr (std::is_same_v<S, double>) {
+            const bool v0 = qb >= m.z && qb < m.w;
+            const bool v1 = qb + 1 < m.w;
+            const double x0 = xw[v0 ? R.s[p].c.x - w0 : 0];
+            const double x1 = xw[v1 ? R.s[p].c.y - w0 : 0];
+            prod[v0 ? lds_idx(qb - m.z) : dummy] = R.s[p].v.x * x0;
+            prod[v1 ? lds_idx(qb + 1 - m.z) : dummy] = R.s[p].v.y * x1;
+        } else {
+            const bool v0 = qb < m.w;
+            const S x0 = xw[v0 ? R.s[p].c - w0 : 0];
+            prod[v0 ? lds_idx(qb - m.z) : dummy] = mul(R.s[p].v, x0);
+        }
+    }
+}
+
+template <class S, bool kPower>
+__global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int parity) {
+    constexpr int TN = Tile<S>::kNnz;
+    constexpr int LDSN = TN + TN / 32;
+    constexpr int KW = Win<S>::kWin;
+    __shared__ S prod[LDSN];
+    __shared__ S xwin[2][KW];
+    __shared__ int2 rows[kThreads];
+    __shared__ double sm[3 * kWaves];
+    __shared__ Prologue pro;
+    __shared__ int s_last;
+
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kPower) {
+        power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro);
+        if (!pro.go) return;
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.x_plain;
+        yout = a.y_plain;
+    }
+    const int tid = threadIdx.x;
+    double n2 = 0.0, rr = 0.0, ri = 0.0;
+
+    const int nb = gridDim.x >> 3;
+    const int chunk = (a.nshort + 7) >> 3;
+    const int tbeg = (blockIdx.x & 7) * chunk;
+    const int tend = min(a.nshort, tbeg + chunk);
+    const int t = tbeg + (blockIdx.x >> 3);
+
+    if (t < tend) {
+        const int last = tend - 1;
+        // fill: tile t (products in LDS), tile t+nb (stream + window in registers)
+        int4 mc = a.tile_meta[t];
+        int2 wc = a.tile_win[t];
+        TileRegs<S> Ra, Rb;
+        WinRegs<S> Wa, Wb;
+        load_tile(a, mc, Rb);
+        load_window(xin, wc, a.xlen, Wb);
+        int tn = t + nb;
+        int4 mn = a.tile_meta[min(tn, last)];
+        int2 wn = a.tile_win[min(tn, last)];
+        load_tile(a, mn, Ra);
+        load_window(xin, wn, a.xlen, Wa);
+        int b = 0;
+        store_window<S, kPower>(Wb, nrm, xwin[0]);
+        __syncthreads();
+        win_products(Rb, mc, wc.x, xwin[0], prod, LDSN - 1);
+        rows[tid] = make_int2(Rb.rp0, Rb.rp1);
+        __syncthreads();
+
+        auto step = [&](TileRegs<S>& Rnx, WinRegs<S>& Wnx, TileRegs<S>& Rld, WinRegs<S>& Wld) -> bool {
+            const int t2 = tn + nb;
+            const int4 m2 = a.tile_meta[min(t2, last)];
+            const int2 w2 = a.tile_win[min(t2, last)];
+            load_tile(a, m2, Rld);
+            load_window(xin, w2, a.xlen, Wld);
+            store_window<S, kPower>(Wnx, nrm, xwin[b ^ 1]);   // unconditional: no branch around the wait
+            // row sums of the current tile (x_i for the Rayleigh term from the scaled window)
+            if (tid < mc.y - mc.x) {
+                const int2 rp = rows[tid];
+                const S sacc = row_sum<S>(prod, rp.x - mc.z, rp.y - mc.z);
+                yout[mc.x + tid] = sacc;
+                if constexpr (kPower) {
+                    const S xi = xwin[b][mc.x + tid - wc.x];
+                    n2 += sq_abs(sacc);
+                    acc_dot(rr, ri, xi, sacc);
+                }
+            }
+            if (tn >= tend) return true;
+            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+            win_products(Rnx, mn, wn.x, xwin[b ^ 1], prod, LDSN - 1);
+            rows[tid] = make_int2(Rnx.rp0, Rnx.rp1);
+            __builtin_amdgcn_sched_barrier(0);
+            __syncthreads();
+            __builtin_amdgcn_sched_barrier(0);
+            b ^= 1;
+            mc = mn;
+            wc = wn;
+            mn = m2;
+            wn = w2;
+            tn = t2;
+            return false;
+        };
+        for (;;) {
+            if (step(Ra, Wa, Rb, Wb)) break;
+            if (step(Rb, Wb, Ra, Wa)) break;
+        }
+    }
+
+    long_rows_pass<S, kPower>(a, xin, yout, nrm, n2, rr, ri, sm);
     if constexpr (kPower) {
         block_sum3(n2, rr, ri, sm);
         last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
@@ -297,50 +550,66 @@ void csr_release(eigsol_csr* A) {
     if (A->col) (void)hipFree(A->col);
     if (A->val) (void)hipFree(A->val);
     if (A->tile_meta) (void)hipFree(A->tile_meta);
+    if (A->tile_win) (void)hipFree(A->tile_win);
     eigsol_ctx* c = A->ctx;
     delete A;
     ctx_release(c);
 }
 
 // ---------------------------------------------------------------- host: CSR build / upload
-static int build_tiles(const int32_t* rowptr, int64_t nrows, int tile_nnz,
-                       std::vector<int32_t>& meta, int32_t& long_tiles, int32_t& max_rows) {
-    std::vector<int32_t> starts;
-    starts.clear();
-    starts.reserve(nrows / 64 + 2);
-    long_tiles = 0;
+// Row tiles: short tiles (consecutive rows, <= kTileRows rows, <= tile_nnz nonzeros) first, in
+// row order, then one tile per long row.  meta = {r0, r1, e0, e1} per tile.
+static int build_tiles(const int32_t* rowptr, const int32_t* col, int64_t nrows, int tile_nnz,
+                       int win_cap, std::vector<int32_t>& meta, std::vector<int32_t>& win,
+                       int32_t& nshort, int32_t& max_rows, int32_t& windowed) {
+    std::vector<int32_t> shorts, longs;
+    shorts.reserve(4 * (nrows / 64 + 2));
     max_rows = 0;
+    auto push = [](std::vector<int32_t>& v, int64_t r0, int64_t r1, const int32_t* rp) {
+        v.push_back((int32_t)r0);
+        v.push_back((int32_t)r1);
+        v.push_back(rp[r0]);
+        v.push_back(rp[r1]);
+    };
     int64_t r = 0;
     while (r < nrows) {
-        starts.push_back((int32_t)r);
         const int64_t len = rowptr[r + 1] - rowptr[r];
         if (len > tile_nnz) {
-            ++long_tiles;
+            push(longs, r, r + 1, rowptr);
             ++r;
-            max_rows = std::max(max_rows, 1);
             continue;
         }
         int64_t nz = len;
         int64_t rr = r + 1;
         while (rr < nrows && rr - r < kTileRows) {
             const int64_t l2 = rowptr[rr + 1] - rowptr[rr];
-            if (nz + l2 > tile_nnz) break;
+            if (l2 > tile_nnz || nz + l2 > tile_nnz) break;
             nz += l2;
             ++rr;
         }
         max_rows = std::max(max_rows, (int32_t)(rr - r));
+        push(shorts, r, rr, rowptr);
         r = rr;
     }
-    starts.push_back((int32_t)nrows);
-    const size_t nt = starts.size() - 1;
-    meta.resize(4 * std::max<size_t>(nt, 1));
-    for (size_t i = 0; i < nt; ++i) {
-        meta[4 * i + 0] = starts[i];
-        meta[4 * i + 1] = starts[i + 1];
-        meta[4 * i + 2] = rowptr[starts[i]];
-        meta[4 * i + 3] = rowptr[starts[i + 1]];
+    nshort = (int32_t)(shorts.size() / 4);
+    // x window of each short tile: [min(first row, min column), max(last row, max column)]
+    win.assign(2 * std::max<int32_t>(nshort, 1), 0);
+    windowed = nshort > 0 ? 1 : 0;
+    for (int32_t i = 0; i < nshort; ++i) {
+        const int32_t r0 = shorts[4 * i], r1 = shorts[4 * i + 1];
+        int32_t w0 = r0, w1 = r1 - 1;
+        for (int32_t k = shorts[4 * i + 2]; k < shorts[4 * i + 3]; ++k) {
+            w0 = std::min(w0, col[k]);
+            w1 = std::max(w1, col[k]);
+        }
+        win[2 * i] = w0;
+        win[2 * i + 1] = w1;
+        if (w1 - w0 + 1 > win_cap) windowed = 0;
     }
-    return (int)nt;
+    meta = std::move(shorts);
+    meta.insert(meta.end(), longs.begin(), longs.end());
+    if (meta.empty()) meta.assign(4, 0);
+    return (int)(nshort + longs.size() / 4);
 }
 
 int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t nnz,
@@ -374,10 +643,13 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
         col_use = col_sorted.data();
         val_use = val_sorted.data();
     }
-    std::vector<int32_t> meta;
-    int32_t long_tiles = 0, max_rows = 0;
-    const int ntiles = build_tiles(rowptr, nrows, dtype == EIGSOL_C128 ? Tile<cplx>::kCap : Tile<double>::kCap,
-                                   meta, long_tiles, max_rows);
+    std::vector<int32_t> meta, win;
+    int32_t nshort = 0, max_rows = 0, windowed = 0;
+    const bool cx = dtype == EIGSOL_C128;
+    const int ntiles = build_tiles(rowptr, col_use, nrows, cx ? Tile<cplx>::kCap : Tile<double>::kCap,
+                                   cx ? Win<cplx>::kWin : Win<double>::kWin, meta, win, nshort,
+                                   max_rows, windowed);
+    if (const char* env = std::getenv("EIGSOL_CSR_NO_WINDOW")) if (std::atoi(env)) windowed = 0;
 
     auto* A = new eigsol_csr();
     A->ctx = ctx;
@@ -387,15 +659,17 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     A->ncols = ncols;
     A->nnz = nnz;
     A->ntiles = ntiles;
-    A->long_tiles = long_tiles;
+    A->nshort = nshort;
+    A->windowed = windowed;
     A->max_tile_rows = max_rows;
-    const size_t pad = 8;   // 16-byte pair loads may touch one element past nnz
+    const size_t pad = (size_t)(dtype == EIGSOL_C128 ? Tile<cplx>::kNnz : Tile<double>::kNnz) + 8;   // branch-free tile loads
     auto cleanup = [&]() { csr_release(A); };
     hipError_t e;
     if ((e = hipMalloc(&A->rowptr, (nrows + 1) * sizeof(int32_t))) != hipSuccess ||
         (e = hipMalloc(&A->col, (nnz + pad) * sizeof(int32_t))) != hipSuccess ||
         (e = hipMalloc(&A->val, (nnz + pad) * sb)) != hipSuccess ||
-        (e = hipMalloc(&A->tile_meta, meta.size() * sizeof(int32_t))) != hipSuccess) {
+        (e = hipMalloc(&A->tile_meta, meta.size() * sizeof(int32_t))) != hipSuccess ||
+        (e = hipMalloc(&A->tile_win, win.size() * sizeof(int32_t))) != hipSuccess) {
         cleanup();
         return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: hipMalloc: ") + hipGetErrorString(e));
     }
@@ -406,6 +680,7 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
         (nnz && (e = hipMemcpyAsync(A->col, col_use, nnz * sizeof(int32_t), hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (nnz && (e = hipMemcpyAsync(A->val, val_use, nnz * sb, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (e = hipMemcpyAsync(A->tile_meta, meta.data(), meta.size() * sizeof(int32_t), hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(A->tile_win, win.data(), win.size() * sizeof(int32_t), hipMemcpyHostToDevice, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess) {
         cleanup();
         return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: upload: ") + hipGetErrorString(e));
@@ -433,12 +708,11 @@ static int validate_compressed(const char* who, int64_t nouter, int64_t ninner, 
 }
 
 // ---------------------------------------------------------------- occupancy-derived grid
-template <class S>
-static int resident_grid(eigsol_ctx* ctx, int64_t ntiles, int* grid) {
-    // Residency from the kernel's own resources (MI355X_MICROARCH.md § Register files: waves per
-    // SIMD = floor(512 / VGPR allocation), 4 waves per block, 160 KiB LDS per CU).
+// Residency from the kernel's own resources (MI355X_MICROARCH.md § Register files: waves per SIMD
+// = floor(512 / VGPR allocation), 4 waves per block, 160 KiB LDS per CU).
+static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, int* grid) {
     hipFuncAttributes fa;
-    EIGSOL_HIP(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(csr_kernel<S, true>)));
+    EIGSOL_HIP(hipFuncGetAttributes(&fa, kernel));
     const int vgpr_alloc = std::max(8, ((fa.numRegs + 7) / 8) * 8);
     const int by_vgpr = std::min(8, 512 / vgpr_alloc) * 4 / kWaves;
     const int by_lds = fa.sharedSizeBytes ? (int)(160 * 1024 / fa.sharedSizeBytes) : 8;
@@ -452,37 +726,84 @@ static int resident_grid(eigsol_ctx* ctx, int64_t ntiles, int* grid) {
     return EIGSOL_OK;
 }
 
+template <class S>
+static const void* power_kernel_ptr(const eigsol_csr* A) {
+    return A->windowed ? reinterpret_cast<const void*>(csr_win_kernel<S, true>)
+                       : reinterpret_cast<const void*>(csr_kernel<S, true>);
+}
+
 int csr_grid(eigsol_csr* A, int* grid) {
-    if (A->dtype == EIGSOL_C128) return resident_grid<cplx>(A->ctx, A->ntiles, grid);
-    return resident_grid<double>(A->ctx, A->ntiles, grid);
+    const void* k = A->dtype == EIGSOL_C128 ? power_kernel_ptr<cplx>(A) : power_kernel_ptr<double>(A);
+    return resident_grid(A->ctx, k, A->ntiles, grid);
+}
+
+template <class S>
+static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
+    CsrArgs<S> a{};
+    a.rowptr = A->rowptr;
+    a.col = A->col;
+    a.val = (const S*)A->val;
+    a.tile_meta = (const int4*)A->tile_meta;
+    a.tile_win = (const int2*)A->tile_win;
+    a.ntiles = A->ntiles;
+    a.nshort = A->nshort;
+    a.xlen = (int32_t)xlen;
+    a.nrows = (int32_t)A->nrows;
+    return a;
 }
 
 template <class S>
 static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int parity, int grid) {
     hipStream_t s = A->ctx->stream;
-    if (power)
-        hipLaunchKernelGGL((csr_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);
-    else
-        hipLaunchKernelGGL((csr_kernel<S, false>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+    static const int mode = [] {
+        const char* e = std::getenv("EIGSOL_CSR_ABLATION");
+        return e ? std::atoi(e) : 0;
+    }();
+    if constexpr (std::is_same_v<S, double>) {
+        if (power && mode > 0 && !A->windowed) {
+            if (mode == 1) hipLaunchKernelGGL((csr_kernel<S, true, 1>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+            else if (mode == 2) hipLaunchKernelGGL((csr_kernel<S, true, 2>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+            else hipLaunchKernelGGL((csr_kernel<S, true, 3>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+            EIGSOL_HIP(hipGetLastError());
+            return EIGSOL_OK;
+        }
+    }
+    if (A->windowed) {
+        if (power) hipLaunchKernelGGL((csr_win_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+        else hipLaunchKernelGGL((csr_win_kernel<S, false>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+    } else {
+        if (power) hipLaunchKernelGGL((csr_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+        else hipLaunchKernelGGL((csr_kernel<S, false>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+    }
     EIGSOL_HIP(hipGetLastError());
     return EIGSOL_OK;
 }
 
-// entry points used by power_session.cpp
-int csr_power_launch(eigsol_csr* A, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
-                     int nranks, void* my_part, void* blk_part, void* trace, int parity, int grid) {
-    if (A->dtype == EIGSOL_C128) {
-        CsrArgs<cplx> a{A->rowptr, A->col, (const cplx*)A->val, (const int4*)A->tile_meta, A->ntiles,
-                        (int32_t)A->nrows, nullptr, nullptr, (cplx*)buf0, (cplx*)buf1, ctl,
-                        (const part4*)rank_part, nranks, (part4*)my_part, (part4*)blk_part,
-                        (cplx*)trace};
-        return launch_csr<cplx>(A, a, true, parity, grid);
-    }
-    CsrArgs<double> a{A->rowptr, A->col, (const double*)A->val, (const int4*)A->tile_meta, A->ntiles,
-                      (int32_t)A->nrows, nullptr, nullptr, (double*)buf0, (double*)buf1, ctl,
-                      (const part4*)rank_part, nranks, (part4*)my_part, (part4*)blk_part,
-                      (double*)trace};
-    return launch_csr<double>(A, a, true, parity, grid);
+template <class S>
+static int power_launch_t(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
+                          const void* rank_part, int nranks, void* my_part, void* blk_part,
+                          void* trace, int parity, int grid) {
+    CsrArgs<S> a = make_args<S>(A, xlen);
+    a.buf0 = (S*)buf0;
+    a.buf1 = (S*)buf1;
+    a.ctl = ctl;
+    a.rank_part = (const part4*)rank_part;
+    a.nranks = nranks;
+    a.my_part = (part4*)my_part;
+    a.blk_part = (part4*)blk_part;
+    a.trace = (S*)trace;
+    return launch_csr<S>(A, a, true, parity, grid);
+}
+
+// entry point used by power_session.cpp (xlen: entries of the y buffers, own + ghost)
+int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
+                     const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
+                     int parity, int grid) {
+    if (A->dtype == EIGSOL_C128)
+        return power_launch_t<cplx>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
+                                    trace, parity, grid);
+    return power_launch_t<double>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
+                                  trace, parity, grid);
 }
 
 int norm_partial_launch(eigsol_ctx* ctx, int dtype, const void* x, int64_t n, PowerCtl* ctl,
@@ -582,16 +903,14 @@ int eigsol_csr_spmv(eigsol_csr* A, const void* x_dev, void* y_dev) {
     int grid = 8;
     EIGSOL_TRY(csr_grid(A, &grid));
     if (A->dtype == EIGSOL_C128) {
-        CsrArgs<cplx> a{};
-        a.rowptr = A->rowptr; a.col = A->col; a.val = (const cplx*)A->val; a.tile_meta = (const int4*)A->tile_meta;
-        a.ntiles = A->ntiles; a.nrows = (int32_t)A->nrows;
-        a.x_plain = (const cplx*)x_dev; a.y_plain = (cplx*)y_dev;
+        CsrArgs<cplx> a = make_args<cplx>(A, A->ncols);
+        a.x_plain = (const cplx*)x_dev;
+        a.y_plain = (cplx*)y_dev;
         return launch_csr<cplx>(A, a, false, 0, grid);
     }
-    CsrArgs<double> a{};
-    a.rowptr = A->rowptr; a.col = A->col; a.val = (const double*)A->val; a.tile_meta = (const int4*)A->tile_meta;
-    a.ntiles = A->ntiles; a.nrows = (int32_t)A->nrows;
-    a.x_plain = (const double*)x_dev; a.y_plain = (double*)y_dev;
+    CsrArgs<double> a = make_args<double>(A, A->ncols);
+    a.x_plain = (const double*)x_dev;
+    a.y_plain = (double*)y_dev;
     return launch_csr<double>(A, a, false, 0, grid);
 }
 

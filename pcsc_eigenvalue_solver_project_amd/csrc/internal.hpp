@@ -179,9 +179,11 @@ struct eigsol_csr {
     int32_t* col = nullptr;        // device, nnz (+pad)
     void* val = nullptr;           // device, nnz (+pad)
     int32_t* tile_meta = nullptr;  // device, 4 ints per row tile: {r0, r1, e0, e1}
+    int32_t* tile_win = nullptr;   // device, 2 ints per short tile: x window [w0, w1]
+    int32_t windowed = 0;          // every short tile's window fits LDS: windowed kernel
     int32_t ntiles = 0;
     int32_t max_tile_rows = 0;
-    int32_t long_tiles = 0;        // tiles holding one row longer than the LDS tile
+    int32_t nshort = 0;            // tiles [0, nshort) are short; the rest hold one long row each
 };
 
 struct eigsol_dense {

@@ -13,8 +13,9 @@
 
 namespace eigsol {
 int csr_grid(eigsol_csr* A, int* grid);
-int csr_power_launch(eigsol_csr* A, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
-                     int nranks, void* my_part, void* blk_part, void* trace, int parity, int grid);
+int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
+                     const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
+                     int parity, int grid);
 int dense_grid(eigsol_dense* A, int* grid);
 int dense_power_launch(eigsol_dense* A, void* buf0, void* buf1, PowerCtl* ctl,
                        const void* rank_part, int nranks, void* my_part, void* blk_part,
@@ -86,7 +87,7 @@ static void session_free(eigsol_power* s) {
 
 static int launch_iteration(eigsol_power* s) {
     if (s->csr)
-        return csr_power_launch(s->csr, s->buf[0], s->buf[1], s->ctl, s->rank_part,
+        return csr_power_launch(s->csr, s->nbuf, s->buf[0], s->buf[1], s->ctl, s->rank_part,
                                 s->ctx->nranks, s->my_part, s->blk_part, s->trace, s->parity, s->grid);
     return dense_power_launch(s->dense, s->buf[0], s->buf[1], s->ctl, s->rank_part, s->ctx->nranks,
                               s->my_part, s->blk_part, s->trace, s->parity, s->grid);
