@@ -180,7 +180,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "csr_kernel<double,true> (fused power iteration)",
+                "kernel": info["kernel"] + ", fused power iteration",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -136,7 +136,8 @@ int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int3
 /* Device-side description of the hot kernel for roofline accounting: algorithmic bytes moved by
  * one fused iteration and the grid used. */
 int eigsol_power_kernel_info(eigsol_power* s, double* bytes_per_iteration, int32_t* grid_blocks,
-                             int32_t* tiles);
+                             int32_t* tiles, int32_t* variant);
+/* variant: 0 = CSR, x gathered from HBM; 1 = CSR, x window staged in LDS; 2 = dense GEMV */
 
 #ifdef __cplusplus
 }

@@ -229,9 +229,12 @@ class PowerSession:
         return buf[: cnt.value]
 
     def kernel_info(self):
-        b, g, t = C.c_double(0), C.c_int32(0), C.c_int32(0)
-        call("eigsol_power_kernel_info", self.handle, C.byref(b), C.byref(g), C.byref(t))
-        return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value}
+        b, g, t, v = C.c_double(0), C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        call("eigsol_power_kernel_info", self.handle, C.byref(b), C.byref(g), C.byref(t), C.byref(v))
+        names = {0: "csr_kernel (x gathered from HBM)", 1: "csr_win_kernel (x window staged in LDS)",
+                 2: "dense_kernel (GEMV)"}
+        return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
+                "variant": v.value, "kernel": names.get(v.value, "?")}
 
     def close(self) -> None:
         if getattr(self, "handle", None):

@@ -84,7 +84,7 @@ SIGNATURES = {
     "eigsol_power_query": [_vp, _pi32, _pi32],
     "eigsol_power_finish": [_vp, _vp, _vp, C.c_int, _pi32, _pi32],
     "eigsol_power_trace": [_vp, _vp, _i32, _pi32],
-    "eigsol_power_kernel_info": [_vp, _pd, _pi32, _pi32],
+    "eigsol_power_kernel_info": [_vp, _pd, _pi32, _pi32, _pi32],
 }
 _RESTYPES = {"eigsol_status_string": C.c_char_p, "eigsol_last_error": C.c_char_p}
 

@@ -40,6 +40,28 @@ constexpr int kTileRows = 256;
 // One pad element every 32 keeps the lane-per-row phase-2 reads spread over the 64 banks.
 __device__ __forceinline__ int lds_idx(int k) { return k + (k >> 5); }
 
+// base + 32-bit element index: lets hipcc use the SGPR-base + 32-bit VGPR-offset form of
+// global_load instead of per-lane 64-bit address arithmetic.  Every stream the kernels index
+// this way is < 4 GiB (checked at upload).
+template <class T>
+__device__ __forceinline__ T ldg(const T* base, uint32_t i) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) +
+                                       (uint64_t)(i * (uint32_t)sizeof(T)));
+}
+
+// Tile metadata is read-only for the whole launch and indexed uniformly: scalar loads (constant
+// address space) keep it off the vector memory counter.
+__device__ __forceinline__ int4 ld_uniform(const int4* p, int i) {
+    using cp = const __attribute__((address_space(4))) int*;
+    const cp q = (cp)(uintptr_t)(p + i);
+    return make_int4(q[0], q[1], q[2], q[3]);
+}
+__device__ __forceinline__ int2 ld_uniform(const int2* p, int i) {
+    using cp = const __attribute__((address_space(4))) int*;
+    const cp q = (cp)(uintptr_t)(p + i);
+    return make_int2(q[0], q[1]);
+}
+
 template <class S>
 struct CsrArgs {
     const int32_t* rowptr;
@@ -95,21 +117,21 @@ __device__ __forceinline__ void load_tile(const CsrArgs<S>& a, int4 m, TileRegs<
         const int q0 = m.z & ~1;
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-            const int q = q0 + 2 * (tid + p * kThreads);
-            R.s[p].v = *reinterpret_cast<const double2*>(a.val + q);
-            R.s[p].c = *reinterpret_cast<const int2*>(a.col + q);
+            const uint32_t q = (uint32_t)(q0 + 2 * (tid + p * kThreads));
+            R.s[p].v = ldg(reinterpret_cast<const double2*>(a.val), q >> 1);
+            R.s[p].c = ldg(reinterpret_cast<const int2*>(a.col), q >> 1);
         }
     } else {
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-            const int q = m.z + tid + p * kThreads;
-            R.s[p].v = a.val[q];
-            R.s[p].c = a.col[q];
+            const uint32_t q = (uint32_t)(m.z + tid + p * kThreads);
+            R.s[p].v = ldg(a.val, q);
+            R.s[p].c = ldg(a.col, q);
         }
     }
-    const int r = min(m.x + tid, a.nrows - 1);
-    R.rp0 = a.rowptr[r];
-    R.rp1 = a.rowptr[r + 1];
+    const uint32_t r = (uint32_t)min(m.x + tid, a.nrows - 1);
+    R.rp0 = ldg(a.rowptr, r);
+    R.rp1 = ldg(a.rowptr, r + 1);
 }
 
 // Gathers of one tile's x entries (all in flight together; unconditional, see load_tile).
@@ -354,8 +376,8 @@ __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity)
 //   row sums of tile i (prod, xwin[b])               ; barrier A
 //   products of tile i+1 (xwin[b^1]) -> prod, rows   ; barrier B
 template <class S> struct Win;
-template <> struct Win<double> { static constexpr int kWin = 1024; };
-template <> struct Win<cplx> { static constexpr int kWin = 512; };
+template <> struct Win<double> { static constexpr int kWin = 512; };
+template <> struct Win<cplx> { static constexpr int kWin = 256; };
 
 template <class S>
 struct WinRegs {
@@ -367,7 +389,8 @@ struct WinRegs {
 template <class S>
 __device__ __forceinline__ void load_window(const S* xin, int2 w, int xlen, WinRegs<S>& W) {
 #pragma unroll
-    for (int k = 0; k < WinRegs<S>::K; ++k) W.v[k] = xin[min(w.x + (int)threadIdx.x + k * kThreads, xlen - 1)];
+    for (int k = 0; k < WinRegs<S>::K; ++k)
+        W.v[k] = ldg(xin, (uint32_t)min(w.x + (int)threadIdx.x + k * kThreads, xlen - 1));
 }
 
 template <class S, bool kPower>
@@ -442,16 +465,19 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
 
     if (t < tend) {
         const int last = tend - 1;
-        // fill: tile t (products in LDS), tile t+nb (stream + window in registers)
-        int4 mc = a.tile_meta[t];
-        int2 wc = a.tile_win[t];
+        // Fill: tile t -> products in LDS; tile t+nb -> stream + window in registers; metadata
+        // of tile t+2nb requested (scalar loads, one step ahead of its use).
+        int4 mc = ld_uniform(a.tile_meta, t);
+        int2 wc = ld_uniform(a.tile_win, t);
+        int tn = t + nb;
+        int4 mn = ld_uniform(a.tile_meta, min(tn, last));
+        int2 wn = ld_uniform(a.tile_win, min(tn, last));
+        int4 m2 = ld_uniform(a.tile_meta, min(tn + nb, last));
+        int2 w2 = ld_uniform(a.tile_win, min(tn + nb, last));
         TileRegs<S> Ra, Rb;
         WinRegs<S> Wa, Wb;
         load_tile(a, mc, Rb);
         load_window(xin, wc, a.xlen, Wb);
-        int tn = t + nb;
-        int4 mn = a.tile_meta[min(tn, last)];
-        int2 wn = a.tile_win[min(tn, last)];
         load_tile(a, mn, Ra);
         load_window(xin, wn, a.xlen, Wa);
         int b = 0;
@@ -461,10 +487,13 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
         rows[tid] = make_int2(Rb.rp0, Rb.rp1);
         __syncthreads();
 
+        // step i: Rnx/Wnx = tile i+1 (in flight since step i-1), Rld/Wld <- tile i+2.  Unrolled
+        // by two with the register sets swapping roles, so the prefetch is never copied (a copy
+        // would force its wait).
         auto step = [&](TileRegs<S>& Rnx, WinRegs<S>& Wnx, TileRegs<S>& Rld, WinRegs<S>& Wld) -> bool {
-            const int t2 = tn + nb;
-            const int4 m2 = a.tile_meta[min(t2, last)];
-            const int2 w2 = a.tile_win[min(t2, last)];
+            const int t3 = tn + 2 * nb;
+            const int4 m3 = ld_uniform(a.tile_meta, min(t3, last));
+            const int2 w3 = ld_uniform(a.tile_win, min(t3, last));
             load_tile(a, m2, Rld);
             load_window(xin, w2, a.xlen, Wld);
             store_window<S, kPower>(Wnx, nrm, xwin[b ^ 1]);   // unconditional: no branch around the wait
@@ -493,7 +522,9 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
             wc = wn;
             mn = m2;
             wn = w2;
-            tn = t2;
+            m2 = m3;
+            w2 = w3;
+            tn += nb;
             return false;
         };
         for (;;) {
@@ -651,6 +682,11 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
                                    max_rows, windowed);
     if (const char* env = std::getenv("EIGSOL_CSR_NO_WINDOW")) if (std::atoi(env)) windowed = 0;
 
+    // the kernels index every stream with 32-bit byte offsets (ldg): one device's rows must keep
+    // values, columns and vectors under 4 GiB each (shard larger matrices over ranks)
+    const size_t tile_pad = (size_t)(dtype == EIGSOL_C128 ? Tile<cplx>::kNnz : Tile<double>::kNnz) + 8;
+    if ((size_t)(nnz + tile_pad) * sb >= (size_t(1) << 32) || (size_t)(std::max(nrows, ncols) + 64) * sb >= (size_t(1) << 32))
+        return fail(EIGSOL_E_UNSUPPORTED, "eigsol_csr_create: a per-device stream exceeds 4 GiB; shard the rows over more ranks");
     auto* A = new eigsol_csr();
     A->ctx = ctx;
     ctx_retain(ctx);

@@ -262,7 +262,8 @@ int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int3
     return EIGSOL_OK;
 }
 
-int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int32_t* tiles) {
+int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int32_t* tiles,
+                             int32_t* variant) {
     if (!s) return fail(EIGSOL_E_INVALID, "eigsol_power_kernel_info: null session");
     const double sb = (double)scalar_bytes(s->dtype);
     if (s->csr) {
@@ -270,10 +271,12 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
         const double nnz = (double)s->csr->nnz, n = (double)s->csr->nrows;
         if (bytes) *bytes = (sb + 4.0) * nnz + 4.0 * (n + 1.0) + 2.0 * sb * n;
         if (tiles) *tiles = s->csr->ntiles;
+        if (variant) *variant = s->csr->windowed ? 1 : 0;
     } else {
         const double n = (double)s->dense->nrows;
         if (bytes) *bytes = sb * n * n + 2.0 * sb * n;
         if (tiles) *tiles = 0;
+        if (variant) *variant = 2;
     }
     if (grid) *grid = s->grid;
     return EIGSOL_OK;
