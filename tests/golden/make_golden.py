@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures in tests/golden/ (committed; run from the repo root).
+
+Independent of the C++ oracle: a literal numpy restatement of the reference's small-case algorithms
+(power_method.hpp:47-99, to_hessenberg.hpp:23-80, qr_decompose.hpp:25-86,
+qr_eigenvalues.hpp:40-108, file_matrix_reader.hpp:33-200) plus LAPACK (numpy.linalg.eigvals) for
+eigenvalues.  The C++ oracle is checked against these vectors, and both against the known answers
+of the reference's own tests (test/*.cpp) and its data files (data/A.txt, data/B.txt, copied here).
+"""
+import json
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# ---------------------------------------------------------------- reader (file_matrix_reader.hpp)
+def read_matrix(path, dtype):
+    tok = open(path).read().split()
+    kind, rows, cols = tok[0], int(tok[1]), int(tok[2])
+    it = iter(tok[3:])
+    cplx = np.dtype(dtype) == np.complex128
+    if kind == "dense":
+        A = np.zeros((rows, cols), dtype=dtype)
+        for r in range(rows):
+            for c in range(cols):
+                A[r, c] = complex(float(next(it)), float(next(it))) if cplx else float(next(it))
+        return A
+    nnz = int(next(it))
+    A = np.zeros((rows, cols), dtype=dtype)
+    for _ in range(nnz):
+        r, c = int(next(it)), int(next(it))
+        A[r, c] = complex(float(next(it)), float(next(it))) if cplx else float(next(it))
+    return A
+
+
+# ---------------------------------------------------------------- restatements (numpy, small n)
+def close_rel(a, b, tol):
+    return abs(a - b) <= tol * (1 + abs(a))
+
+
+def power_method(A, x0, max_iter, tol):
+    x = np.array(x0, dtype=A.dtype)
+    x = x / np.sqrt(np.sum(np.abs(x) ** 2))
+    lam, iters, conv, init, trace = 0.0, 0, False, False, []
+    for k in range(max_iter):
+        y = A @ x
+        ny = np.sqrt(np.sum(np.abs(y) ** 2))
+        if ny == 0:
+            iters = k + 1
+            break
+        x = y / ny
+        lam_new = np.vdot(x, A @ x)
+        if A.dtype != np.complex128:
+            lam_new = lam_new.real
+        trace.append(lam_new)
+        if init and close_rel(lam_new, lam, tol):
+            lam, iters, conv = lam_new, k + 1, True
+            break
+        lam, init, iters = lam_new, True, k + 1
+    return lam, x, iters, conv, trace
+
+
+def householder(x):
+    nx = np.linalg.norm(x)
+    if np.linalg.norm(x[1:]) == 0:
+        return None
+    sign = x[0] / abs(x[0]) if x[0] != 0 else 1.0
+    v = x.copy()
+    v[0] -= -sign * nx
+    nv = np.linalg.norm(v)
+    if nv == 0:
+        return None
+    return v / nv
+
+
+def hessenberg(A):
+    H = np.array(A, dtype=A.dtype)
+    n = H.shape[0]
+    for k in range(n - 2):
+        v = householder(H[k + 1:, k].copy())
+        if v is None:
+            continue
+        H[k + 1:, k:] -= 2 * np.outer(v, v.conj() @ H[k + 1:, k:])
+        H[:, k + 1:] -= 2 * np.outer(H[:, k + 1:] @ v, v.conj())
+    return H
+
+
+def qr_decompose(A):
+    m, n = A.shape
+    R = np.array(A, dtype=A.dtype)
+    Q = np.eye(m, dtype=A.dtype)
+    for k in range(min(m, n)):
+        v = householder(R[k:, k].copy())
+        if v is None:
+            continue
+        R[k:, k:] -= 2 * np.outer(v, v.conj() @ R[k:, k:])
+        Q[:, k:] -= 2 * np.outer(Q[:, k:] @ v, v.conj())
+    return Q, R
+
+
+def qr_eigenvalues(A, max_iter, tol):
+    H = hessenberg(A)
+    n = H.shape[0]
+    it, conv = 0, False
+    for it in range(max_iter):
+        Q, R = qr_decompose(H)
+        H = R @ Q
+        sub = max((abs(H[i, i - 1]) for i in range(1, n)), default=0.0)
+        if sub <= tol * (1 + np.linalg.norm(H)):
+            conv = True
+            break
+    return np.diag(H).copy(), it + 1, conv
+
+
+def cplx_list(a):
+    a = np.asarray(a, dtype=np.complex128).ravel()
+    return [[float(z.real), float(z.imag)] for z in a]
+
+
+def main():
+    out = {}
+    A_d = read_matrix(os.path.join(HERE, "A.txt"), np.float64)     # A.txt parsed as double
+    A_c = read_matrix(os.path.join(HERE, "A.txt"), np.complex128)
+    B_c = read_matrix(os.path.join(HERE, "B.txt"), np.complex128)
+    out["A_double"] = A_d.tolist()
+    out["A_complex"] = cplx_list(A_c.ravel(order="C"))
+    out["B_complex"] = cplx_list(B_c.ravel(order="C"))
+    out["eig_A_double"] = cplx_list(np.sort_complex(np.linalg.eigvals(A_d)))
+    out["eig_A_complex"] = cplx_list(np.sort_complex(np.linalg.eigvals(A_c)))
+    out["eig_B_complex"] = cplx_list(np.sort_complex(np.linalg.eigvals(B_c)))
+
+    # config 1: power method on A.txt (double) from a fixed x0
+    x0 = np.array([0.25, -0.5, 0.75])
+    lam, x, it, conv, tr = power_method(A_d, x0, 1000, 1e-10)
+    out["cfg1_power"] = {"x0": x0.tolist(), "tol": 1e-10, "max_iter": 1000, "lambda": float(lam),
+                         "iterations": it, "converged": conv, "trace": [float(t) for t in tr],
+                         "eigenvector": x.tolist()}
+    # complex A.txt / B.txt power method from fixed complex x0
+    for name, M in (("A_complex", A_c), ("B_complex", B_c)):
+        rng = np.random.default_rng(5)
+        xc = rng.uniform(-1, 1, M.shape[0]) + 1j * rng.uniform(-1, 1, M.shape[0])
+        lam, x, it, conv, tr = power_method(M, xc, 1000, 1e-10)
+        out[f"power_{name}"] = {"x0": cplx_list(xc), "lambda": [lam.real, lam.imag],
+                                "iterations": it, "converged": conv}
+
+    # Householder conventions (qr_algorithms_test.cpp:37-40, :145-148, :182-223)
+    T = np.array([[4.0, 1.0, -2.0], [1.0, 3.0, 0.0], [2.0, 1.0, 1.0]])
+    out["hessenberg_test3"] = hessenberg(T).tolist()
+    Tc = np.array([[4 + 1j, 1, -2 + 2j], [1, 3 - 1j, 1j], [2, 1 + 2j, 1]])
+    out["hessenberg_test3_complex"] = cplx_list(hessenberg(Tc).ravel(order="C"))
+    Q, R = qr_decompose(np.array([[1.0, 2.0], [3.0, 4.0], [5.0, 6.0]]))
+    out["qr_3x2"] = {"Q": Q.tolist(), "R": R.tolist()}
+    Qc, Rc = qr_decompose(np.array([[1 + 1j, 2 - 1j], [0.5, 3 + 2j]]))
+    out["qr_complex_2x2"] = {"Q": cplx_list(Qc.ravel(order="C")), "R": cplx_list(Rc.ravel(order="C"))}
+
+    # unshifted QR iteration counts (reference algorithm)
+    for name, M, tol in (("qr_eig_2x2_1e-12", np.array([[2.0, 1.0], [1.0, 2.0]]), 1e-12),
+                         ("qr_eig_2x2_1e-10", np.array([[2.0, 1.0], [1.0, 2.0]]), 1e-10),
+                         ("qr_eig_A_double", A_d, 1e-10)):
+        ev, it, conv = qr_eigenvalues(M, 1000, tol)
+        out[name] = {"eigenvalues": [float(e) for e in ev], "iterations": it, "converged": conv}
+    ev, it, conv = qr_eigenvalues(A_c, 1000, 1e-10)
+    out["qr_eig_A_complex"] = {"eigenvalues": cplx_list(ev), "iterations": it, "converged": conv}
+
+    # power-iteration lambda trace at n = 2000 (band generator) for the oracle's CSC path
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from pcsc_eigenvalue_solver_project_amd import synthetic as S
+    import scipy.sparse as sp
+    rp, ci, v = S.band(2000, 10)
+    M = sp.csr_matrix((v, ci, rp), shape=(2000, 2000)).toarray()
+    x0 = S.start_vector(2000)
+    lam, x, it, conv, tr = power_method(M, x0, 60, 1e-13)
+    out["band2000_power"] = {"lambda": float(lam), "iterations": it, "converged": conv,
+                             "trace": [float(t) for t in tr]}
+
+    json.dump(out, open(os.path.join(HERE, "golden.json"), "w"), indent=1)
+
+    # config 2 fixture: LAPACK eigenvalues of the seeded 4096^2 N(0,1) matrix
+    n = 4096
+    rng = np.random.default_rng(20251226)
+    A = rng.standard_normal((n, n))
+    ev = np.linalg.eigvals(A)
+    np.save(os.path.join(HERE, "cfg2_eigvals_4096.npy"), ev.astype(np.complex128))
+    # smaller QR fixture (n = 512) for fast parity tests
+    rng = np.random.default_rng(512)
+    A = rng.standard_normal((512, 512))
+    np.save(os.path.join(HERE, "qr512_matrix_seed.npy"), np.array([512], dtype=np.int64))
+    np.save(os.path.join(HERE, "qr512_eigvals.npy"), np.linalg.eigvals(A).astype(np.complex128))
+    print("golden fixtures written")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,52 @@
+"""CPU: the gfx950 C-ABI library loads and exports every symbol include/eigsol_hip.h declares;
+argument validation and no-device behaviour (no compute calls)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import pcsc_eigenvalue_solver_project_amd as E
+from pcsc_eigenvalue_solver_project_amd import _capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "eigsol_hip.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(eigsol_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = C.CDLL(_capi.LIB_PATH)
+    names = declared_symbols()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_every_symbol():
+    assert set(declared_symbols()) <= set(_capi.SIGNATURES)
+
+
+def test_abi_version_and_status_strings():
+    L = E.lib()
+    assert L.eigsol_abi_version() == 1
+    assert L.eigsol_status_string(1) == b"matrix must be square"
+    assert L.eigsol_status_string(2) == b"matrix has zero size"
+
+
+def test_null_arguments_rejected_without_device():
+    L = E.lib()
+    assert L.eigsol_ctx_create(0, None) == _capi.EIGSOL_E_INVALID
+    assert L.eigsol_power_step(None, 1) == _capi.EIGSOL_E_INVALID
+    assert L.eigsol_csr_spmv(None, None, None) == _capi.EIGSOL_E_INVALID
+
+
+def test_no_device_fails_loudly():
+    if E.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(E.EigSolError) as e:
+        E.Context(0)
+    assert e.value.status == _capi.EIGSOL_E_NO_DEVICE
