@@ -109,12 +109,14 @@ def main():
     # A dedicated (non-default) torch stream: the library's work and torch's timing events share it.
     torch_stream = torch.cuda.Stream()
     torch.cuda.set_stream(torch_stream)
-    ctx = E.Context(local_rank, stream=torch_stream.cuda_stream)
     rp, ci, v = gen(kind, n_global, k, row0, rows)
     if world > 1:
+        # one communicator per rank owned by the library (RCCL over xGMI); gloo only ships the id
         from pcsc_eigenvalue_solver_project_amd import dist as D
+        ctx = D.torch_dist_context(local_rank, stream=torch_stream.cuda_stream)
         A, sess = D.sharded_power_session(ctx, rp, ci, v, n_global, row0)
     else:
+        ctx = E.Context(local_rank, stream=torch_stream.cuda_stream)
         A = E.CsrMatrix(ctx, rp, ci, v, (rows, rows))
         sess = E.PowerSession(A)
     nnz = len(ci)

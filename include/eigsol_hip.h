@@ -139,6 +139,28 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes_per_iteration, int32
                              int32_t* tiles, int32_t* variant);
 /* variant: 0 = CSR, x gathered from HBM; 1 = CSR, x window staged in LDS; 2 = dense GEMV */
 
+/* ---------------------------------------------------------------- row-sharded power iteration
+ * One process per GPU; RCCL over xGMI (the reference has no distribution: SURVEY.md §2.1).
+ * Rank r owns global rows [row_begins[r], row_begins[r+1]).  Bootstrap: rank 0 calls
+ * eigsol_dist_get_unique_id, broadcasts the bytes with any transport, every rank calls
+ * eigsol_ctx_create_dist.  eigsol_csr_create_dist is collective; the resulting matrix is used with
+ * the eigsol_power_* session functions unchanged (x0 / x_out hold the rank's own rows).  Each
+ * iteration exchanges only the x entries other ranks read (a halo for banded matrices) plus one
+ * 32-byte all-gather; every rank reaches the same termination decision. */
+int eigsol_dist_unique_id_bytes(void);
+int eigsol_dist_get_unique_id(void* id_out);
+int eigsol_ctx_create_dist(int device, int rank, int nranks, const void* unique_id,
+                           eigsol_ctx** out);
+int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* row_begins,
+                           int64_t nnz_local, const int32_t* rowptr_local,
+                           const int32_t* colidx_global, const void* values, eigsol_csr** out);
+/* Host-only planning used by eigsol_csr_create_dist (no device, no communication): remaps global
+ * columns to the local x-space [ghosts of lower ranks | own rows | ghosts of higher ranks] and
+ * lists the ghosts (ascending global index) with their per-owner counts. */
+int eigsol_ghost_plan(int nranks, const int64_t* row_begins, int rank, int64_t nnz_local,
+                      const int32_t* colidx_global, int32_t* colidx_local, int64_t* nghost,
+                      int64_t* ghost_global, int64_t* recv_counts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,6 +85,11 @@ SIGNATURES = {
     "eigsol_power_finish": [_vp, _vp, _vp, C.c_int, _pi32, _pi32],
     "eigsol_power_trace": [_vp, _vp, _i32, _pi32],
     "eigsol_power_kernel_info": [_vp, _pd, _pi32, _pi32, _pi32],
+    "eigsol_dist_unique_id_bytes": [],
+    "eigsol_dist_get_unique_id": [_vp],
+    "eigsol_ctx_create_dist": [C.c_int, C.c_int, C.c_int, _vp, _ppv],
+    "eigsol_csr_create_dist": [_vp, C.c_int, _vp, _i64, _vp, _vp, _vp, _ppv],
+    "eigsol_ghost_plan": [C.c_int, _vp, C.c_int, _i64, _vp, _vp, _pi64, _vp, _vp],
 }
 _RESTYPES = {"eigsol_status_string": C.c_char_p, "eigsol_last_error": C.c_char_p}
 

@@ -72,6 +72,7 @@ struct CsrArgs {
     int32_t ntiles;
     int32_t nshort;
     int32_t xlen;            // entries of the input vector (own + ghost)
+    int32_t xoff;            // x-space index of local row 0 (lower ghosts precede the own rows)
     int32_t nrows;
     const S* x_plain;        // plain SpMV input (kPower == false)
     S* y_plain;              // plain SpMV output
@@ -219,7 +220,7 @@ __device__ __forceinline__ void long_rows_pass(const CsrArgs<S>& a, const S* xin
             set_re_im(sacc, pr, pi);
             yout[m.x] = sacc;
             if constexpr (kPower) {
-                const S xi = scale_in(xin[m.x], nrm);
+                const S xi = scale_in(xin[m.x + a.xoff], nrm);
                 n2 += sq_abs(sacc);
                 acc_dot(rr, ri, xi, sacc);
             }
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity)
         if (!pro.go) return;
         nrm = pro.nrm;
         xin = parity ? a.buf0 : a.buf1;
-        yout = parity ? a.buf1 : a.buf0;
+        yout = (parity ? a.buf1 : a.buf0) + a.xoff;   // y rows land at their x-space slots
     } else {
         xin = a.x_plain;
         yout = a.y_plain;
@@ -297,7 +298,7 @@ __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity)
         S xg[P][NPS];
         issue_gathers<S, kMode>(Rc, xin, xg);
         S xrow = s_zero<S>();
-        if constexpr (kPower) xrow = xin[min(mc.x + tid, a.nrows - 1)];
+        if constexpr (kPower) xrow = xin[min(mc.x + tid, a.nrows - 1) + a.xoff];
         int tn = t + nb;
         int4 mn = a.tile_meta[min(tn, last)];
         TileRegs<S> Rn;
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity)
             // meta first, so its wait does not cover the gathers issued after it
             const int4 m2 = a.tile_meta[min(t2, last)];
             issue_gathers<S, kMode>(Rnx, xin, xg);
-            if constexpr (kPower) xrow = xin[min(mn.x + tid, a.nrows - 1)];
+            if constexpr (kPower) xrow = xin[min(mn.x + tid, a.nrows - 1) + a.xoff];
             load_tile(a, m2, Rld);
             // row sums of the current tile from LDS buffer b (ascending-column sequential sums)
             if (tid < mc.y - mc.x) {
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
         if (!pro.go) return;
         nrm = pro.nrm;
         xin = parity ? a.buf0 : a.buf1;
-        yout = parity ? a.buf1 : a.buf0;
+        yout = (parity ? a.buf1 : a.buf0) + a.xoff;   // y rows land at their x-space slots
     } else {
         xin = a.x_plain;
         yout = a.y_plain;
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
                 const S sacc = row_sum<S>(prod, rp.x - mc.z, rp.y - mc.z);
                 yout[mc.x + tid] = sacc;
                 if constexpr (kPower) {
-                    const S xi = xwin[b][mc.x + tid - wc.x];
+                    const S xi = xwin[b][mc.x + a.xoff + tid - wc.x];
                     n2 += sq_abs(sacc);
                     acc_dot(rr, ri, xi, sacc);
                 }
@@ -582,6 +583,8 @@ void csr_release(eigsol_csr* A) {
     if (A->val) (void)hipFree(A->val);
     if (A->tile_meta) (void)hipFree(A->tile_meta);
     if (A->tile_win) (void)hipFree(A->tile_win);
+    if (A->send_idx) (void)hipFree(A->send_idx);
+    if (A->send_buf) (void)hipFree(A->send_buf);
     eigsol_ctx* c = A->ctx;
     delete A;
     ctx_release(c);
@@ -590,8 +593,8 @@ void csr_release(eigsol_csr* A) {
 // ---------------------------------------------------------------- host: CSR build / upload
 // Row tiles: short tiles (consecutive rows, <= kTileRows rows, <= tile_nnz nonzeros) first, in
 // row order, then one tile per long row.  meta = {r0, r1, e0, e1} per tile.
-static int build_tiles(const int32_t* rowptr, const int32_t* col, int64_t nrows, int tile_nnz,
-                       int win_cap, std::vector<int32_t>& meta, std::vector<int32_t>& win,
+static int build_tiles(const int32_t* rowptr, const int32_t* col, int64_t nrows, int64_t xoff,
+                       int tile_nnz, int win_cap, std::vector<int32_t>& meta, std::vector<int32_t>& win,
                        int32_t& nshort, int32_t& max_rows, int32_t& windowed) {
     std::vector<int32_t> shorts, longs;
     shorts.reserve(4 * (nrows / 64 + 2));
@@ -627,7 +630,7 @@ static int build_tiles(const int32_t* rowptr, const int32_t* col, int64_t nrows,
     win.assign(2 * std::max<int32_t>(nshort, 1), 0);
     windowed = nshort > 0 ? 1 : 0;
     for (int32_t i = 0; i < nshort; ++i) {
-        const int32_t r0 = shorts[4 * i], r1 = shorts[4 * i + 1];
+        const int32_t r0 = shorts[4 * i] + xoff, r1 = shorts[4 * i + 1] + xoff;   // x-space rows
         int32_t w0 = r0, w1 = r1 - 1;
         for (int32_t k = shorts[4 * i + 2]; k < shorts[4 * i + 3]; ++k) {
             w0 = std::min(w0, col[k]);
@@ -643,8 +646,10 @@ static int build_tiles(const int32_t* rowptr, const int32_t* col, int64_t nrows,
     return (int)(nshort + longs.size() / 4);
 }
 
+// xoff: x-space index of local row 0 (0 on one GPU; the lower-ghost count when row-sharded)
 int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t nnz,
-               const int32_t* rowptr, const int32_t* colidx, const void* values, eigsol_csr** out) {
+               const int32_t* rowptr, const int32_t* colidx, const void* values, eigsol_csr** out,
+               int64_t xoff) {
     const size_t sb = scalar_bytes(dtype);
     // sort columns inside rows when needed (keeps the reference's ascending-column row order)
     std::vector<int32_t> col_sorted;
@@ -677,7 +682,7 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     std::vector<int32_t> meta, win;
     int32_t nshort = 0, max_rows = 0, windowed = 0;
     const bool cx = dtype == EIGSOL_C128;
-    const int ntiles = build_tiles(rowptr, col_use, nrows, cx ? Tile<cplx>::kCap : Tile<double>::kCap,
+    const int ntiles = build_tiles(rowptr, col_use, nrows, xoff, cx ? Tile<cplx>::kCap : Tile<double>::kCap,
                                    cx ? Win<cplx>::kWin : Win<double>::kWin, meta, win, nshort,
                                    max_rows, windowed);
     if (const char* env = std::getenv("EIGSOL_CSR_NO_WINDOW")) if (std::atoi(env)) windowed = 0;
@@ -696,6 +701,7 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     A->nnz = nnz;
     A->ntiles = ntiles;
     A->nshort = nshort;
+    A->xoff = xoff;
     A->windowed = windowed;
     A->max_tile_rows = max_rows;
     const size_t pad = (size_t)(dtype == EIGSOL_C128 ? Tile<cplx>::kNnz : Tile<double>::kNnz) + 8;   // branch-free tile loads
@@ -785,6 +791,7 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     a.nshort = A->nshort;
     a.xlen = (int32_t)xlen;
     a.nrows = (int32_t)A->nrows;
+    a.xoff = (int32_t)A->xoff;
     return a;
 }
 
@@ -885,7 +892,7 @@ int eigsol_csr_create(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_
     EIGSOL_TRY(validate_compressed("eigsol_csr_create", nrows, ncols, nnz, rowptr, colidx));
     if (nnz && !values) return fail(EIGSOL_E_INVALID, "eigsol_csr_create: null values");
     EIGSOL_HIP(hipSetDevice(ctx->device));
-    return csr_upload(ctx, dtype, nrows, ncols, nnz, rowptr, colidx, values, out);
+    return csr_upload(ctx, dtype, nrows, ncols, nnz, rowptr, colidx, values, out, 0);
 }
 
 int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
@@ -914,7 +921,7 @@ int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrow
             std::memcpy(&v[(size_t)d * sb], (const unsigned char*)values + (size_t)k * sb, sb);
         }
     EIGSOL_HIP(hipSetDevice(ctx->device));
-    return csr_upload(ctx, dtype, nrows, ncols, nnz, rp.data(), ci.data(), v.data(), out);
+    return csr_upload(ctx, dtype, nrows, ncols, nnz, rp.data(), ci.data(), v.data(), out, 0);
 }
 
 int eigsol_csr_destroy(eigsol_csr* A) {

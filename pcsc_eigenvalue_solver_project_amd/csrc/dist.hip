@@ -1,0 +1,257 @@
+// Row-sharded (multi-GPU) power iteration: one process per GPU, RCCL over xGMI.
+//
+// The reference is single-threaded (no distribution anywhere); this file adds the
+// scale-out of powerMethodImpl's loop (src/power_method/power_method.hpp:68-96) that north_star
+// asks for.  Rank p owns a contiguous block of rows.  Its CSR keeps global column indices on the
+// host; at setup they are remapped to local columns [own rows | ghosts], where ghosts are the
+// remote x entries the rank reads, grouped by owner rank in ascending global order.  Per
+// iteration, after the fused SpMV launch:
+//   pack      send_buf[k] = y[send_idx[k]]          (the rows each peer reads from us)
+//   group {   ncclSend/ncclRecv per peer with traffic -> the ghost segment of the next input
+//             ncclAllGather of this rank's partial sums (||y||^2, x^H y) }
+// and the next launch sums the P rank partials in rank order, so every rank takes bitwise
+// identical termination decisions without any host round trip.  For banded/locality-ordered
+// matrices a rank only talks to its neighbours (halo of the band width); for unstructured ones
+// the same code degenerates into an all-to-all of the needed entries.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace eigsol {
+
+int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t nnz,
+               const int32_t* rowptr, const int32_t* colidx, const void* values, eigsol_csr** out,
+               int64_t xoff);
+
+#define EIGSOL_RCCL(expr)                                                                       \
+    do {                                                                                        \
+        ncclResult_t _r = (expr);                                                               \
+        if (_r != ncclSuccess)                                                                  \
+            return ::eigsol::fail(EIGSOL_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+void dist_release_comm(eigsol_ctx* ctx) {
+    if (ctx && ctx->comm) {
+        ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
+        ctx->comm = nullptr;
+    }
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void pack_kernel(const S* __restrict__ y, const int32_t* __restrict__ idx,
+                                                   S* __restrict__ out, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256)
+        out[k] = y[idx[k]];
+}
+
+// Halo exchange of the vector `y` (local layout [own | ghosts]) + all-gather of the rank partials
+// (part4 = 4 doubles per rank, in place at rank_part[rank]).  Stream-ordered on ctx->stream.
+int dist_exchange(eigsol_csr* A, void* y, void* rank_part) {
+    eigsol_ctx* ctx = A->ctx;
+    const size_t sb = scalar_bytes(A->dtype);
+    hipStream_t st = ctx->stream;
+    if (A->nsend > 0) {
+        const int grid = (int)std::min<int64_t>(1024, (A->nsend + 255) / 256);
+        if (A->dtype == EIGSOL_C128)
+            hipLaunchKernelGGL(pack_kernel<cplx>, dim3(grid), dim3(256), 0, st, (const cplx*)y,
+                               A->send_idx, (cplx*)A->send_buf, A->nsend);
+        else
+            hipLaunchKernelGGL(pack_kernel<double>, dim3(grid), dim3(256), 0, st, (const double*)y,
+                               A->send_idx, (double*)A->send_buf, A->nsend);
+        EIGSOL_HIP(hipGetLastError());
+    }
+    ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
+    const size_t dpe = sb / 8;   // doubles per scalar
+    char* xs = static_cast<char*>(y);   // x-space: [lower ghosts | own rows | upper ghosts]
+    EIGSOL_RCCL(ncclGroupStart());
+    for (int q = 0; q < ctx->nranks; ++q) {
+        if (q == ctx->rank) continue;
+        if (A->send_counts[q] > 0)
+            EIGSOL_RCCL(ncclSend(static_cast<char*>(A->send_buf) + (size_t)A->send_offs[q] * sb,
+                                 (size_t)A->send_counts[q] * dpe, ncclFloat64, q, comm, st));
+        if (A->recv_counts[q] > 0)
+            EIGSOL_RCCL(ncclRecv(xs + (size_t)(A->recv_offs[q] + (q > ctx->rank ? A->nrows : 0)) * sb,
+                                 (size_t)A->recv_counts[q] * dpe, ncclFloat64, q, comm, st));
+    }
+    double* rp = static_cast<double*>(rank_part);
+    EIGSOL_RCCL(ncclAllGather(rp + 4 * ctx->rank, rp, 4, ncclFloat64, comm, st));
+    EIGSOL_RCCL(ncclGroupEnd());
+    return EIGSOL_OK;
+}
+
+}  // namespace eigsol
+
+using namespace eigsol;
+
+extern "C" {
+
+// Pure host planning (no device, no communication): remap a rank's global column indices to the
+// local x-space [ghosts of lower ranks | own rows | ghosts of higher ranks] — monotone in the global
+// index, so banded row blocks keep compact column windows — and list the ghosts per owner
+// (ascending global index; the lower-rank ghosts come first).  Exported for callers that exchange
+// the request lists with their own transport, and for the CPU tests.
+int eigsol_ghost_plan(int nranks, const int64_t* row_begins, int rank, int64_t nnz_local,
+                      const int32_t* colidx_global, int32_t* colidx_local, int64_t* nghost,
+                      int64_t* ghost_global, int64_t* recv_counts) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || !row_begins || !nghost || !recv_counts ||
+        (nnz_local && (!colidx_global || !colidx_local || !ghost_global)))
+        return fail(EIGSOL_E_INVALID, "eigsol_ghost_plan: invalid argument");
+    for (int q = 0; q < nranks; ++q)
+        if (row_begins[q + 1] < row_begins[q])
+            return fail(EIGSOL_E_INVALID, "eigsol_ghost_plan: row_begins not monotone");
+    const int64_t r0 = row_begins[rank], r1 = row_begins[rank + 1], n_global = row_begins[nranks];
+    std::vector<int64_t> g;
+    g.reserve(64);
+    for (int64_t k = 0; k < nnz_local; ++k) {
+        const int64_t c = colidx_global[k];
+        if (c < 0 || c >= n_global) return fail(EIGSOL_E_INVALID, "eigsol_ghost_plan: column out of range");
+        if (c < r0 || c >= r1) g.push_back(c);
+    }
+    std::sort(g.begin(), g.end());
+    g.erase(std::unique(g.begin(), g.end()), g.end());
+    // owners are contiguous row blocks, so sorting by global index groups ghosts by owner
+    for (int q = 0; q < nranks; ++q) recv_counts[q] = 0;
+    int q = 0;
+    for (int64_t c : g) {
+        while (c >= row_begins[q + 1]) ++q;
+        recv_counts[q]++;
+    }
+    *nghost = (int64_t)g.size();
+    std::copy(g.begin(), g.end(), ghost_global);
+    const int64_t nown = r1 - r0;
+    const int64_t nlow = std::lower_bound(g.begin(), g.end(), r0) - g.begin();
+    for (int64_t k = 0; k < nnz_local; ++k) {
+        const int64_t c = colidx_global[k];
+        if (c >= r0 && c < r1) {
+            colidx_local[k] = (int32_t)(nlow + c - r0);
+        } else {
+            const int64_t pos = std::lower_bound(g.begin(), g.end(), c) - g.begin();
+            colidx_local[k] = (int32_t)(pos < nlow ? pos : nown + pos);
+        }
+    }
+    return EIGSOL_OK;
+}
+
+int eigsol_dist_get_unique_id(void* id_out) {
+    if (!id_out) return fail(EIGSOL_E_INVALID, "eigsol_dist_get_unique_id: null pointer");
+    ncclUniqueId id;
+    EIGSOL_RCCL(ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return EIGSOL_OK;
+}
+
+int eigsol_dist_unique_id_bytes(void) { return NCCL_UNIQUE_ID_BYTES; }
+
+int eigsol_ctx_create_dist(int device, int rank, int nranks, const void* unique_id,
+                           eigsol_ctx** out) {
+    if (!out || !unique_id || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(EIGSOL_E_INVALID, "eigsol_ctx_create_dist: invalid argument");
+    EIGSOL_TRY(eigsol_ctx_create(device, out));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclCommInitRank(&comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        eigsol_ctx_destroy(*out);
+        *out = nullptr;
+        return fail(EIGSOL_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    (*out)->comm = comm;
+    (*out)->rank = rank;
+    (*out)->nranks = nranks;
+    return EIGSOL_OK;
+}
+
+// Collective over the context's communicator: every rank passes its own row block.
+int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* row_begins,
+                           int64_t nnz_local, const int32_t* rowptr_local,
+                           const int32_t* colidx_global, const void* values, eigsol_csr** out) {
+    if (!ctx || !out || !row_begins || !rowptr_local)
+        return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: null argument");
+    if (!ctx->comm) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
+    *out = nullptr;
+    const int P = ctx->nranks, me = ctx->rank;
+    const int64_t n_global = row_begins[P];
+    const int64_t nrows = row_begins[me + 1] - row_begins[me];
+    if (rowptr_local[0] != 0 || rowptr_local[nrows] != nnz_local)
+        return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: rowptr must start at 0 and end at nnz");
+    std::vector<int32_t> col_local(std::max<int64_t>(nnz_local, 1));
+    std::vector<int64_t> ghosts(std::max<int64_t>(nnz_local, 1)), recv(P), nghost(1);
+    EIGSOL_TRY(eigsol_ghost_plan(P, row_begins, me, nnz_local, colidx_global, col_local.data(),
+                                 nghost.data(), ghosts.data(), recv.data()));
+    EIGSOL_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
+    // every rank learns how many entries each peer requests from it (P x P counts)
+    int64_t *d_counts = nullptr, *d_req = nullptr, *d_srcreq = nullptr;
+    EIGSOL_HIP(hipMalloc(&d_counts, sizeof(int64_t) * P * P));
+    EIGSOL_HIP(hipMemcpyAsync(d_counts + (size_t)me * P, recv.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice, st));
+    EIGSOL_RCCL(ncclAllGather(d_counts + (size_t)me * P, d_counts, P, ncclInt64, comm, st));
+    std::vector<int64_t> all(P * P);
+    EIGSOL_HIP(hipMemcpyAsync(all.data(), d_counts, sizeof(int64_t) * P * P, hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipStreamSynchronize(st));
+    hipFree(d_counts);
+    std::vector<int64_t> send(P), soff(P + 1, 0), roff(P + 1, 0);
+    for (int q = 0; q < P; ++q) send[q] = (q == me) ? 0 : all[(size_t)q * P + me];
+    for (int q = 0; q < P; ++q) {
+        soff[q + 1] = soff[q] + send[q];
+        roff[q + 1] = roff[q] + recv[q];
+    }
+    const int64_t nsend = soff[P];
+    // ship the request lists (global indices) to their owners
+    EIGSOL_HIP(hipMalloc(&d_srcreq, sizeof(int64_t) * std::max<int64_t>(nghost[0], 1)));
+    EIGSOL_HIP(hipMalloc(&d_req, sizeof(int64_t) * std::max<int64_t>(nsend, 1)));
+    if (nghost[0])
+        EIGSOL_HIP(hipMemcpyAsync(d_srcreq, ghosts.data(), sizeof(int64_t) * nghost[0], hipMemcpyHostToDevice, st));
+    EIGSOL_RCCL(ncclGroupStart());
+    for (int q = 0; q < P; ++q) {
+        if (q == me) continue;
+        if (recv[q]) EIGSOL_RCCL(ncclSend(d_srcreq + roff[q], recv[q], ncclInt64, q, comm, st));
+        if (send[q]) EIGSOL_RCCL(ncclRecv(d_req + soff[q], send[q], ncclInt64, q, comm, st));
+    }
+    EIGSOL_RCCL(ncclGroupEnd());
+    std::vector<int64_t> req(std::max<int64_t>(nsend, 1));
+    if (nsend) EIGSOL_HIP(hipMemcpyAsync(req.data(), d_req, sizeof(int64_t) * nsend, hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipStreamSynchronize(st));
+    hipFree(d_req);
+    hipFree(d_srcreq);
+    int64_t nlow = 0;
+    for (int q = 0; q < me; ++q) nlow += recv[q];
+    std::vector<int32_t> send_idx(std::max<int64_t>(nsend, 1));
+    for (int64_t k = 0; k < nsend; ++k) {
+        const int64_t loc = req[k] - row_begins[me];
+        if (loc < 0 || loc >= nrows)
+            return fail(EIGSOL_E_RCCL, "eigsol_csr_create_dist: peer requested a row this rank does not own");
+        send_idx[k] = (int32_t)(loc + nlow);   // x-space slot of the requested own row
+    }
+    eigsol_csr* A = nullptr;
+    EIGSOL_TRY(csr_upload(ctx, dtype, nrows, nrows + nghost[0], nnz_local, rowptr_local,
+                          col_local.data(), values, &A, nlow));
+    A->dist = 1;
+    A->n_global = n_global;
+    A->row_begin = row_begins[me];
+    A->nghost = nghost[0];
+    A->send_counts = send;
+    A->recv_counts = recv;
+    A->send_offs.assign(soff.begin(), soff.end() - 1);
+    A->recv_offs.assign(roff.begin(), roff.end() - 1);
+    A->nsend = nsend;
+    const size_t sb = scalar_bytes(dtype);
+    hipError_t e = hipMalloc(&A->send_idx, sizeof(int32_t) * std::max<int64_t>(nsend, 1));
+    if (e == hipSuccess) e = hipMalloc(&A->send_buf, sb * std::max<int64_t>(nsend, 1));
+    if (e == hipSuccess && nsend)
+        e = hipMemcpyAsync(A->send_idx, send_idx.data(), sizeof(int32_t) * nsend, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        eigsol_csr_destroy(A);
+        return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create_dist: ") + hipGetErrorString(e));
+    }
+    *out = A;
+    return EIGSOL_OK;
+}
+
+}  // extern "C"

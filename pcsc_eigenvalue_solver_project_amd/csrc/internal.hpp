@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "eigsol_hip.h"
 
@@ -184,6 +185,15 @@ struct eigsol_csr {
     int32_t ntiles = 0;
     int32_t max_tile_rows = 0;
     int32_t nshort = 0;            // tiles [0, nshort) are short; the rest hold one long row each
+    // Row-sharded (multi-GPU) layout: this rank owns global rows [row_begin, row_begin + nrows);
+    // local columns are [own rows | ghosts grouped by owner rank, ascending global index].
+    int dist = 0;
+    int64_t n_global = 0, row_begin = 0, nghost = 0;
+    int64_t xoff = 0;              // x-space index of local row 0 (= ghosts owned by lower ranks)
+    std::vector<int64_t> send_counts, send_offs, recv_counts, recv_offs;   // per peer (scalars)
+    int32_t* send_idx = nullptr;   // device: local row of every entry sent, grouped by peer
+    void* send_buf = nullptr;      // device: packed halo values
+    int64_t nsend = 0;
 };
 
 struct eigsol_dense {

@@ -23,6 +23,7 @@ int dense_power_launch(eigsol_dense* A, void* buf0, void* buf1, PowerCtl* ctl,
 int norm_partial_launch(eigsol_ctx* ctx, int dtype, const void* x, int64_t n, PowerCtl* ctl,
                         void* blk_part, void* out, int grid);
 int scale_out_launch(eigsol_ctx* ctx, int dtype, const void* src, double nrm, void* dst, int64_t n);
+int dist_exchange(eigsol_csr* A, void* y, void* rank_part);
 }  // namespace eigsol
 
 using namespace eigsol;
@@ -33,7 +34,9 @@ struct eigsol_power {
     eigsol_dense* dense = nullptr;
     int dtype = EIGSOL_F64;
     int64_t n = 0;            // rows owned (= vector length on one GPU)
-    int64_t nbuf = 0;         // own + ghost entries
+    int64_t nbuf = 0;         // own + ghost entries (x-space)
+    int64_t xoff = 0;         // x-space index of own row 0 (row-sharded: lower ghosts first)
+    bool dist = false;
     void* buf[2] = {nullptr, nullptr};
     PowerCtl* ctl = nullptr;
     void* rank_part = nullptr;   // part4[nranks]
@@ -58,7 +61,8 @@ static int session_alloc(eigsol_power* s, int32_t trace_cap) {
     for (int i = 0; i < 2; ++i) EIGSOL_HIP(hipMalloc(&s->buf[i], std::max<int64_t>(s->nbuf, 1) * sb + 64));
     EIGSOL_HIP(hipMalloc(&s->ctl, sizeof(PowerCtl)));
     EIGSOL_HIP(hipMalloc(&s->rank_part, kPart * std::max(1, s->ctx->nranks)));
-    s->my_part = s->rank_part;
+    // rank partials are all-gathered in place: this rank's slot is rank_part[rank]
+    s->my_part = static_cast<char*>(s->rank_part) + kPart * (s->dist ? s->ctx->rank : 0);
     EIGSOL_HIP(hipMalloc(&s->blk_part, kPart * std::max(8, s->grid)));
     if (trace_cap > 0) EIGSOL_HIP(hipMalloc(&s->trace, (size_t)trace_cap * sb));
     s->trace_cap = std::max(0, trace_cap);
@@ -86,6 +90,12 @@ static void session_free(eigsol_power* s) {
 }
 
 static int launch_iteration(eigsol_power* s) {
+    if (s->csr && s->dist) {
+        EIGSOL_TRY(csr_power_launch(s->csr, s->nbuf, s->buf[0], s->buf[1], s->ctl, s->rank_part,
+                                    s->ctx->nranks, s->my_part, s->blk_part, s->trace, s->parity, s->grid));
+        // launch t wrote y_t into buf[t & 1]: halo exchange + all-gather of the rank partials
+        return dist_exchange(s->csr, s->buf[s->parity], s->rank_part);
+    }
     if (s->csr)
         return csr_power_launch(s->csr, s->nbuf, s->buf[0], s->buf[1], s->ctl, s->rank_part,
                                 s->ctx->nranks, s->my_part, s->blk_part, s->trace, s->parity, s->grid);
@@ -104,11 +114,13 @@ extern "C" {
 int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power** out) {
     if (!A || !out) return fail(EIGSOL_E_INVALID, "eigsol_power_create_csr: null pointer");
     *out = nullptr;
-    if (A->nrows != A->ncols) return fail(EIGSOL_E_NOT_SQUARE, "powerMethod: matrix must be square");
-    if (A->nrows == 0) return fail(EIGSOL_E_ZERO_SIZE, "powerMethod: matrix has zero size");
+    if (!A->dist && A->nrows != A->ncols) return fail(EIGSOL_E_NOT_SQUARE, "powerMethod: matrix must be square");
+    if (A->dist ? A->n_global == 0 : A->nrows == 0) return fail(EIGSOL_E_ZERO_SIZE, "powerMethod: matrix has zero size");
     auto* s = new eigsol_power();
     s->ctx = A->ctx;
     s->csr = A;
+    s->dist = A->dist != 0;
+    s->xoff = A->xoff;
     csr_retain(A);
     s->dtype = A->dtype;
     s->n = A->nrows;
@@ -152,8 +164,9 @@ int eigsol_power_begin(eigsol_power* s, const eigsol_solver_options* opts, const
     const size_t sb = scalar_bytes(s->dtype);
     s->opts = *opts;
     s->trivial = opts->max_iterations <= 0;
-    // y_{-1} = x0 lives in buf[1] (launch t reads buf[(t-1)&1])
-    EIGSOL_HIP(hipMemcpyAsync(s->buf[1], x0, s->n * sb,
+    // y_{-1} = x0 lives in buf[1] (launch t reads buf[(t-1)&1]); own rows at x-space offset xoff
+    char* x0dst = static_cast<char*>(s->buf[1]) + (size_t)s->xoff * sb;
+    EIGSOL_HIP(hipMemcpyAsync(x0dst, x0, s->n * sb,
                               x0_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
     PowerCtl init;
     std::memset(&init, 0, sizeof(init));
@@ -166,7 +179,8 @@ int eigsol_power_begin(eigsol_power* s, const eigsol_solver_options* opts, const
     std::memcpy(s->host_ctl, &init, sizeof(init));
     EIGSOL_HIP(hipMemcpyAsync(s->ctl, s->host_ctl, sizeof(PowerCtl), hipMemcpyHostToDevice, st));
     // ||x0||^2 partials -> the input norm of launch 0 (x.normalize(), power_method.hpp:62)
-    EIGSOL_TRY(norm_partial_launch(s->ctx, s->dtype, s->buf[1], s->n, s->ctl, s->blk_part, s->my_part, s->grid));
+    EIGSOL_TRY(norm_partial_launch(s->ctx, s->dtype, x0dst, s->n, s->ctl, s->blk_part, s->my_part, s->grid));
+    if (s->dist) EIGSOL_TRY(dist_exchange(s->csr, s->buf[1], s->rank_part));   // x0 ghosts + partials
     EIGSOL_HIP(hipStreamSynchronize(st));   // host_ctl is reused by query()
     s->parity = 0;
     s->launches = 0;
@@ -212,10 +226,13 @@ int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_ou
     int32_t it = 0, conv = 0;
     if (s->trivial) {
         // maxIterations <= 0: lambda = 0, x = normalised x0, 0 iterations (power_method.hpp:61-68)
-        double part[4];
-        EIGSOL_HIP(hipMemcpyAsync(part, s->my_part, sizeof(part), hipMemcpyDeviceToHost, st));
+        const int P = s->dist ? s->ctx->nranks : 1;
+        std::vector<double> part(4 * P);
+        EIGSOL_HIP(hipMemcpyAsync(part.data(), s->rank_part, sizeof(double) * 4 * P, hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(hipStreamSynchronize(st));
-        fnorm = std::sqrt(part[0]);
+        double n2 = 0.0;
+        for (int r = 0; r < P; ++r) n2 += part[4 * r];   // rank order, as on the device
+        fnorm = std::sqrt(n2);
         parity = 1;
     } else {
         EIGSOL_TRY(pull_ctl(s));
@@ -232,7 +249,7 @@ int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_ou
     if (iterations) *iterations = it;
     if (converged) *converged = conv;
     if (x_out) {
-        void* src = s->buf[parity];
+        void* src = static_cast<char*>(s->buf[parity]) + (size_t)s->xoff * sb;
         if (x_out_on_device) {
             EIGSOL_TRY(scale_out_launch(s->ctx, s->dtype, src, fnorm, x_out, s->n));
             EIGSOL_HIP(hipStreamSynchronize(st));

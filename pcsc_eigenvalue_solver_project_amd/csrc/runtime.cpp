@@ -15,11 +15,14 @@ int fail(int status, const std::string& msg) {
     return status;
 }
 
+void dist_release_comm(eigsol_ctx* ctx);   // dist.hip
+
 void ctx_retain(eigsol_ctx* c) { c->refs.fetch_add(1); }
 
 void ctx_release(eigsol_ctx* ctx) {
     if (!ctx || ctx->refs.fetch_sub(1) != 1) return;
     (void)hipSetDevice(ctx->device);
+    dist_release_comm(ctx);
     if (ctx->own_stream) {
         (void)hipStreamSynchronize(ctx->own_stream);
         (void)hipStreamDestroy(ctx->own_stream);

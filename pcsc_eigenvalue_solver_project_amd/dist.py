@@ -1,0 +1,95 @@
+"""Row-sharded power iteration across GPUs (one process per GPU, RCCL over xGMI).
+
+Python view of ``eigsol_ctx_create_dist`` / ``eigsol_csr_create_dist`` (include/eigsol_hip.h).
+The communicator is owned by the C++ library; ``torch.distributed`` (any backend) is only used to
+broadcast RCCL's 128-byte unique id at start-up.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import CsrMatrix, Context, EigSolError, PowerSession, _dtype_code, _np_dtype, _ptr
+from ._capi import call, lib
+
+
+def ghost_plan(nranks: int, row_begins, rank: int, colidx_global):
+    """Host-only remap of global columns to the local x-space (library function, no device)."""
+    rb = np.ascontiguousarray(row_begins, dtype=np.int64)
+    cg = np.ascontiguousarray(colidx_global, dtype=np.int32)
+    cl = np.empty(max(len(cg), 1), dtype=np.int32)
+    gh = np.empty(max(len(cg), 1), dtype=np.int64)
+    rc = np.zeros(nranks, dtype=np.int64)
+    ng = C.c_int64(0)
+    call("eigsol_ghost_plan", int(nranks), _ptr(rb), int(rank), len(cg), _ptr(cg), _ptr(cl),
+         C.byref(ng), _ptr(gh), _ptr(rc))
+    return cl[: len(cg)], gh[: ng.value], rc
+
+
+class DistContext(Context):
+    """A Context whose communicator spans one rank per GPU."""
+
+    def __init__(self, device: int, rank: int, world: int, unique_id: bytes, stream=None):
+        h = C.c_void_p()
+        uid = (C.c_char * len(unique_id)).from_buffer_copy(unique_id)
+        call("eigsol_ctx_create_dist", int(device), int(rank), int(world), C.cast(uid, C.c_void_p), C.byref(h))
+        self.handle = h
+        self.device = device
+        self.rank, self.world = rank, world
+        if stream is not None:
+            self.set_stream(stream)
+
+
+def unique_id() -> bytes:
+    n = lib().eigsol_dist_unique_id_bytes()
+    buf = (C.c_char * n)()
+    call("eigsol_dist_get_unique_id", C.cast(buf, C.c_void_p))
+    return bytes(buf)
+
+
+def torch_dist_context(device: int, stream=None) -> DistContext:
+    """Bootstrap from an initialised torch.distributed process group (gloo or nccl)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = lib().eigsol_dist_unique_id_bytes()
+    t = torch.zeros(n, dtype=torch.uint8)
+    if rank == 0:
+        t[:] = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
+    dist.broadcast(t, src=0)
+    return DistContext(device, rank, world, bytes(t.numpy().tobytes()), stream=stream)
+
+
+class DistCsrMatrix(CsrMatrix):
+    """This rank's row block of a row-sharded CSR matrix (collective construction)."""
+
+    def __init__(self, ctx: DistContext, row_begins, rowptr_local, colidx_global, values):
+        values = np.ascontiguousarray(values)
+        code = _dtype_code(values.dtype)
+        rb = np.ascontiguousarray(row_begins, dtype=np.int64)
+        rp = np.ascontiguousarray(rowptr_local, dtype=np.int32)
+        cg = np.ascontiguousarray(colidx_global, dtype=np.int32)
+        if len(rb) != ctx.world + 1:
+            raise EigSolError(9, "row_begins must have world + 1 entries")
+        h = C.c_void_p()
+        call("eigsol_csr_create_dist", ctx.handle, code, _ptr(rb), len(cg), _ptr(rp), _ptr(cg),
+             _ptr(values), C.byref(h))
+        self.ctx, self.handle = ctx, h
+        nloc = int(rb[ctx.rank + 1] - rb[ctx.rank])
+        self.shape = (nloc, int(rb[-1]))
+        self.n_global = int(rb[-1])
+        self.nnz = len(cg)
+        self.dtype = _np_dtype(code)
+
+
+def sharded_power_session(ctx: DistContext, rowptr_local, colidx_global, values, n_global: int,
+                          row0: int):
+    """Equal contiguous row blocks (rows_per_rank = n_global / world); returns (matrix, session)."""
+    world = ctx.world
+    rows = n_global // world
+    rb = np.arange(world + 1, dtype=np.int64) * rows
+    rb[-1] = n_global
+    assert rb[ctx.rank] == row0
+    A = DistCsrMatrix(ctx, rb, rowptr_local, colidx_global, values)
+    return A, PowerSession(A)
