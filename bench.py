@@ -57,6 +57,24 @@ def gen(kind, n_global, k, row0, nrows):
     return S.uniform(n_global, k, row0=row0, nrows=nrows)
 
 
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of the same kernel on the same workload, from the committed rocprofv3
+    PMC summary (profiles/, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md); PMC counters
+    cannot be read from inside a timed run, so the profile is a separate pass of this workload."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        kn = d.get("kernel") or ""
+        if "hbm_traffic_bytes_per_launch" in d and kernel.split(" ")[0] in kn:
+            best = {"hbm_traffic_bytes_per_launch": round(d["hbm_traffic_bytes_per_launch"]),
+                    "source": os.path.relpath(f, ROOT)}
+    return best
+
+
 def cpu_baseline(kind, k, budget_s):
     """Reference algorithm (two CSC products per iteration, single thread) on a bounded sample."""
     from oracle import oracle as O
@@ -189,9 +207,15 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None,
                 "event_ms_per_launch": round(ev_ms / args.steps, 5),
+                "algorithmic_bytes_per_launch": bytes_iter,
             },
             "cpu_baseline": None,
         }
+    if rank == 0:
+        pmc = pmc_traffic(args.workload, info["kernel"])
+        if pmc:
+            out["roofline"]["traffic"] = pmc["hbm_traffic_bytes_per_launch"]
+            out["roofline"]["traffic_source"] = pmc["source"]
     if args.extras and world == 1:
         # config 3: 1M x 1M uniform, 16 nnz/row (working set < Infinity Cache: may exceed HBM bound)
         rp3, ci3, v3 = S.uniform(1_000_000, 16)

@@ -1,0 +1,40 @@
+"""GPU: the row-sharded path (eigsol_ctx_create_dist / eigsol_csr_create_dist) on one rank.
+
+A one-GPU box cannot host two RCCL ranks (RCCL refuses two ranks on one device), so the
+multi-rank exchange is covered by tests/test_dist_cpu.py (gloo, world_size 2) and by
+construction; here the distributed constructors, the RCCL communicator, the in-place rank-partial
+all-gather and the session plumbing run for real with nranks = 1 and must reproduce the oracle.
+"""
+import numpy as np
+import pytest
+
+import pcsc_eigenvalue_solver_project_amd as E
+from pcsc_eigenvalue_solver_project_amd import dist as D
+from pcsc_eigenvalue_solver_project_amd import synthetic as S
+from oracle import oracle as O
+from test_gpu_power import _assert_power_parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kind", ["band", "uniform"])
+def test_dist_single_rank_power_parity(kind):
+    n = 20000
+    rp, ci, v = S.band(n, 12) if kind == "band" else S.uniform(n, 8)
+    ctx = D.DistContext(0, 0, 1, D.unique_id())
+    try:
+        A, sess = D.sharded_power_session(ctx, rp, ci, v, n, 0)
+        x0 = S.start_vector(n)
+        opts = E.SolverOptions(300, 1e-12)
+        sess.begin(opts, x0)
+        sess.step(301)
+        assert sess.query()[0]
+        res = sess.finish()
+        cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+        ref = O.power_csc(cp, ri, vv, x0, 300, 1e-12, want_trace=True)
+        assert ref["converged"]
+        _assert_power_parity(res, ref, 1e-12)
+        sess.close()
+        A.close()
+    finally:
+        ctx.close()
