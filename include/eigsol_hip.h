@@ -137,7 +137,39 @@ int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int3
  * one fused iteration and the grid used. */
 int eigsol_power_kernel_info(eigsol_power* s, double* bytes_per_iteration, int32_t* grid_blocks,
                              int32_t* tiles, int32_t* variant);
-/* variant: 0 = CSR, x gathered from HBM; 1 = CSR, x window staged in LDS; 2 = dense GEMV */
+/* variant: 0 = CSR, x gathered from HBM; 1 = CSR, x window staged in LDS; 2 = dense GEMV;
+ *          3 = shifted inverse, sync-free triangular solve (tiles = dependency levels);
+ *          4 = shifted inverse, dense LU substitution */
+
+/* ---------------------------------------------------------------- shifted inverse iteration
+ * shiftedInversePowerMethod<S>(M, ShiftedSolverOptions<S>{sigma, maxIter, tol})
+ * (shifted_inverse_power_solver.hpp:112-125, impl :21-79).  A - sigma I is factored ONCE at
+ * session creation (the reference refactors every iteration, solve_shifted.hpp:75-79,96-106):
+ *   - triangular CSR (upper or lower; a missing diagonal counts as 0, solve_shifted.hpp:100-102):
+ *     the matrix is its own factor; one sync-free level-ordered triangular solve per iteration;
+ *   - dense, and non-triangular CSR small enough to densify: partial-pivot LU on the device.
+ * sigma points at ONE scalar of the matrix dtype.  A zero pivot of a sparse matrix fails with
+ * EIGSOL_E_SOLVER ("solve_shifted: SparseLU factorization failed", solve_shifted.hpp:108-110).
+ * The returned handle is a session: use eigsol_power_begin/step/query/finish/trace/kernel_info.
+ * lambda_k = x_{k+1}^H A x_{k+1} is evaluated as sigma + conj(x_k^H y_k)/||y_k||^2 (A y_k = x_k +
+ * sigma y_k), so an iteration reads only the factor. */
+int eigsol_shifted_create_csr(eigsol_csr* A, const void* sigma, int32_t trace_capacity,
+                              eigsol_power** out);
+int eigsol_shifted_create_dense(eigsol_dense* A, const void* sigma, int32_t trace_capacity,
+                                eigsol_power** out);
+int eigsol_shifted_inverse_csr(eigsol_csr* A, const void* sigma, const eigsol_solver_options* opts,
+                               const void* x0, void* lambda_out, void* x_out, int32_t* iterations,
+                               int32_t* converged);
+int eigsol_shifted_inverse_dense(eigsol_dense* A, const void* sigma,
+                                 const eigsol_solver_options* opts, const void* x0,
+                                 void* lambda_out, void* x_out, int32_t* iterations,
+                                 int32_t* converged);
+/* solve_shifted<S>(M, sigma, b) (solve_shifted.hpp:48-118): x = (A - sigma I)^{-1} b, host
+ * buffers of nb scalars.  Status mirrors the reference's exceptions: NOT_SQUARE, SIZE_MISMATCH,
+ * SOLVER. */
+int eigsol_solve_shifted_csr(eigsol_csr* A, const void* sigma, const void* b, int64_t nb, void* x);
+int eigsol_solve_shifted_dense(eigsol_dense* A, const void* sigma, const void* b, int64_t nb,
+                               void* x);
 
 /* ---------------------------------------------------------------- row-sharded power iteration
  * One process per GPU; RCCL over xGMI (the reference has no distribution: SURVEY.md §2.1).

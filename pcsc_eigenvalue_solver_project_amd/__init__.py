@@ -232,7 +232,8 @@ class PowerSession:
         b, g, t, v = C.c_double(0), C.c_int32(0), C.c_int32(0), C.c_int32(0)
         call("eigsol_power_kernel_info", self.handle, C.byref(b), C.byref(g), C.byref(t), C.byref(v))
         names = {0: "csr_kernel (x gathered from HBM)", 1: "csr_win_kernel (x window staged in LDS)",
-                 2: "dense_kernel (GEMV)"}
+                 2: "dense_kernel (GEMV)", 3: "sptrsv_kernel (sync-free triangular solve)",
+                 4: "dense_lu_solve_kernel (LU substitution)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?")}
 
@@ -264,3 +265,61 @@ def power_method(matrix, opts: SolverOptions = SolverOptions(), x0=None) -> Eige
     call(fn, matrix.handle, C.byref(o), _ptr(x0), _ptr(lam), _ptr(x), C.byref(it), C.byref(conv))
     ev = complex(lam[0]) if matrix.dtype == np.complex128 else float(lam[0])
     return EigenResult(ev, x, int(it.value), bool(conv.value))
+
+
+@dataclass
+class ShiftedSolverOptions(SolverOptions):
+    """``EigSol::ShiftedSolverOptions<S>`` (src/option/shifted_solver_option.hpp:24-68)."""
+
+    shift: complex | float = 0.0
+
+
+def _sigma(shift, dtype) -> np.ndarray:
+    if dtype != np.complex128 and np.iscomplexobj(shift) and complex(shift).imag != 0:
+        raise EigSolError(3, "scalar type mismatch: complex shift for a real matrix")
+    return np.array([shift], dtype=dtype)
+
+
+class ShiftedSession(PowerSession):
+    """Shifted inverse iteration session: A - sigma I factored once on the device
+    (``eigsol_shifted_create_*``); driven with the PowerSession methods."""
+
+    def __init__(self, matrix, shift, trace_capacity: int = 0):
+        h = C.c_void_p()
+        sig = _sigma(shift, matrix.dtype)
+        fn = "eigsol_shifted_create_csr" if isinstance(matrix, CsrMatrix) else "eigsol_shifted_create_dense"
+        call(fn, matrix.handle, _ptr(sig), int(trace_capacity), C.byref(h))
+        self.matrix, self.handle = matrix, h
+        self.n = matrix.shape[0]
+        self.dtype = matrix.dtype
+        self.shift = sig[0]
+
+
+def shifted_inverse_power_method(matrix, opts: ShiftedSolverOptions = ShiftedSolverOptions(),
+                                  x0=None) -> EigenResult:
+    """``EigSol::shiftedInversePowerMethod<S>`` with an explicit start vector."""
+    if x0 is None:
+        rng = np.random.default_rng(0)
+        x0 = rng.uniform(-1, 1, matrix.shape[0])
+        if matrix.dtype == np.complex128:
+            x0 = x0 + 1j * rng.uniform(-1, 1, matrix.shape[0])
+    x0 = np.ascontiguousarray(x0, dtype=matrix.dtype)
+    sig = _sigma(opts.shift, matrix.dtype)
+    lam = np.zeros(1, dtype=matrix.dtype)
+    x = np.empty(matrix.shape[0], dtype=matrix.dtype)
+    it, conv = C.c_int32(0), C.c_int32(0)
+    o = opts.to_c()
+    fn = "eigsol_shifted_inverse_csr" if isinstance(matrix, CsrMatrix) else "eigsol_shifted_inverse_dense"
+    call(fn, matrix.handle, _ptr(sig), C.byref(o), _ptr(x0), _ptr(lam), _ptr(x), C.byref(it), C.byref(conv))
+    ev = complex(lam[0]) if matrix.dtype == np.complex128 else float(lam[0])
+    return EigenResult(ev, x, int(it.value), bool(conv.value))
+
+
+def solve_shifted(matrix, shift, b) -> np.ndarray:
+    """``EigSol::solve_shifted<S>``: x = (A - shift I)^{-1} b on the device."""
+    b = np.ascontiguousarray(b, dtype=matrix.dtype)
+    sig = _sigma(shift, matrix.dtype)
+    x = np.empty(len(b), dtype=matrix.dtype)
+    fn = "eigsol_solve_shifted_csr" if isinstance(matrix, CsrMatrix) else "eigsol_solve_shifted_dense"
+    call(fn, matrix.handle, _ptr(sig), _ptr(b), len(b), _ptr(x))
+    return x

@@ -90,6 +90,12 @@ SIGNATURES = {
     "eigsol_ctx_create_dist": [C.c_int, C.c_int, C.c_int, _vp, _ppv],
     "eigsol_csr_create_dist": [_vp, C.c_int, _vp, _i64, _vp, _vp, _vp, _ppv],
     "eigsol_ghost_plan": [C.c_int, _vp, C.c_int, _i64, _vp, _vp, _pi64, _vp, _vp],
+    "eigsol_shifted_create_csr": [_vp, _vp, _i32, _ppv],
+    "eigsol_shifted_create_dense": [_vp, _vp, _i32, _ppv],
+    "eigsol_shifted_inverse_csr": [_vp, _vp, C.POINTER(SolverOptionsC), _vp, _vp, _vp, _pi32, _pi32],
+    "eigsol_shifted_inverse_dense": [_vp, _vp, C.POINTER(SolverOptionsC), _vp, _vp, _vp, _pi32, _pi32],
+    "eigsol_solve_shifted_csr": [_vp, _vp, _vp, _i64, _vp],
+    "eigsol_solve_shifted_dense": [_vp, _vp, _vp, _i64, _vp],
 }
 _RESTYPES = {"eigsol_status_string": C.c_char_p, "eigsol_last_error": C.c_char_p}
 

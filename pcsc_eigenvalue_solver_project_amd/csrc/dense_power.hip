@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
     double nrm = 0.0;
     if constexpr (kPower) {
         power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro);
-        if (!pro.go) return;
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
         nrm = pro.nrm;
         xin = parity ? a.buf0 : a.buf1;
         yout = parity ? a.buf1 : a.buf0;

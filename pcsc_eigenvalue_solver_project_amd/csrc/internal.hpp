@@ -80,7 +80,7 @@ struct alignas(64) PowerCtl {
     int32_t trace_cap;
     double tol;
     int32_t nranks;
-    int32_t pad0;
+    int32_t ntrace;          // eigenvalue estimates completed so far (trace entries written)
     // result record (valid once done)
     double lam_re, lam_im;
     double final_norm;       // x_final = B[final_parity] / final_norm

@@ -150,6 +150,7 @@ __device__ __forceinline__ void power_prologue(PowerCtl* ctl, const part4* rank_
                 o.pad = 0;
                 ctl->st[parity ^ 1] = o;
                 ctl->launches = t + 1;
+                if (d.record) ctl->ntrace = d.k + 1;
                 if (d.record && trace && d.k < ctl->trace_cap) set_re_im(trace[d.k], d.lam_re, d.lam_im);
                 if (d.done) {
                     ctl->lam_re = d.lam_re;
@@ -173,6 +174,97 @@ __device__ __forceinline__ void power_prologue(PowerCtl* ctl, const part4* rank_
 template <class S>
 __device__ __forceinline__ S scale_in(S y, double nrm) {
     return nrm > 0.0 ? divr(y, nrm) : y;   // Eigen normalize(): unchanged when the norm is 0
+}
+
+}  // namespace dev
+}  // namespace eigsol
+
+namespace eigsol {
+namespace dev {
+
+__device__ __forceinline__ cplx cdiv(cplx a, cplx b) {
+    // textbook quotient with one real division by |b|^2 (b is a pivot, never tiny in practice)
+    const double d = b.re * b.re + b.im * b.im;
+    return cplx{(a.re * b.re + a.im * b.im) / d, (a.im * b.re - a.re * b.im) / d};
+}
+__device__ __forceinline__ double sdiv(double a, double b) { return a / b; }
+__device__ __forceinline__ cplx sdiv(cplx a, cplx b) { return cdiv(a, b); }
+
+// Launch prologue of the fused shifted-inverse iteration (shiftedInversePowerImpl,
+// src/power_method/shifted_inverse_power_solver.hpp:48-76).  Launch t solves (A - sigma I) y_t = x_t
+// with x_t = y_{t-1} / ||y_{t-1}||; its partials are ||y_t||^2 and p_t = x_t^H y_t.  Because
+// A y_t = x_t + sigma y_t, the reference's Rayleigh quotient on A (:62) of x_{t+1} = y_t/||y_t|| is
+//     lambda_t = sigma + conj(p_t) / ||y_t||^2
+// so the prologue of launch t+1 completes reference iteration k = t with no extra product.
+// Carry record: rho = lambda_{t-1} (previous estimate), nrm = ||y_{t-1}||.
+template <class S>
+__device__ __forceinline__ void shift_prologue(PowerCtl* ctl, const part4* rank_part, int parity,
+                                               S* trace, double sig_re, double sig_im,
+                                               Prologue* out) {
+    if (threadIdx.x == 0) {
+        Prologue pr{0.0, 0, 0};
+        const int done = __hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!done) {
+            const PowerCarry in = ctl->st[parity];
+            const int32_t t = in.t + 1;
+            const double n2 = rank_part[0].a, pr_ = rank_part[0].b, pi_ = rank_part[0].c;
+            const double nrm = sqrt(n2);
+            const bool cplx_ = dtype_of<S>::value == EIGSOL_C128;
+            bool fin = false, conv = false, rec = false;
+            int32_t iters = 0, fpar = 0;
+            double lre = in.rho_re, lim = in.rho_im, fnorm = 0.0;
+            if (t >= 1) {
+                const int32_t k = t - 1;
+                if (nrm == 0.0) {                 // normY == 0 (:55-58): x, lambda unchanged
+                    fin = true;
+                    iters = t;
+                    fpar = parity;                // x_{t-1} = y_{t-2} / ||y_{t-2}||
+                    fnorm = in.nrm;
+                    if (t < 2) { lre = 0.0; lim = 0.0; }
+                } else {
+                    lre = sig_re + pr_ / n2;
+                    lim = cplx_ ? sig_im - pi_ / n2 : 0.0;
+                    rec = true;
+                    fpar = parity ^ 1;            // x_{t} = y_{t-1} / ||y_{t-1}||
+                    fnorm = nrm;
+                    if (k >= 1 && close_rel(lre, lim, in.rho_re, in.rho_im, ctl->tol, cplx_)) {
+                        fin = true;               // :64-70
+                        conv = true;
+                        iters = t;
+                    } else if (t >= ctl->max_iter) {
+                        fin = true;               // loop bound :48
+                        iters = t;
+                    }
+                }
+            }
+            if (blockIdx.x == 0) {
+                PowerCarry o;
+                o.rho_re = lre;
+                o.rho_im = lim;
+                o.nrm = nrm;
+                o.t = t;
+                o.pad = 0;
+                ctl->st[parity ^ 1] = o;
+                ctl->launches = t + 1;
+                if (rec) ctl->ntrace = t;
+                if (rec && trace && t - 1 < ctl->trace_cap) set_re_im(trace[t - 1], lre, lim);
+                if (fin) {
+                    ctl->lam_re = lre;
+                    ctl->lam_im = lim;
+                    ctl->iters = iters;
+                    ctl->converged = conv ? 1 : 0;
+                    ctl->final_parity = fpar;
+                    ctl->final_norm = fnorm;
+                    __hip_atomic_store(&ctl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            pr.go = fin ? 0 : 1;
+            pr.nrm = nrm;
+            pr.t = t;
+        }
+        *out = pr;
+    }
+    __syncthreads();
 }
 
 }  // namespace dev

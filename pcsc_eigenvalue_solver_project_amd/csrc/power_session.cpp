@@ -24,6 +24,16 @@ int norm_partial_launch(eigsol_ctx* ctx, int dtype, const void* x, int64_t n, Po
                         void* blk_part, void* out, int grid);
 int scale_out_launch(eigsol_ctx* ctx, int dtype, const void* src, double nrm, void* dst, int64_t n);
 int dist_exchange(eigsol_csr* A, void* y, void* rank_part);
+struct ShiftFactor;
+int shift_factor_csr(eigsol_csr* A, const void* sigma, ShiftFactor** out);
+int shift_factor_dense(eigsol_dense* A, const void* sigma, ShiftFactor** out);
+void shift_factor_free(ShiftFactor* f);
+int shift_grid(const ShiftFactor* f);
+int shift_error(ShiftFactor* f);
+int shift_iter_launch(ShiftFactor* f, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
+                      void* my_part, void* trace, int parity);
+int shift_solve_launch(ShiftFactor* f, const void* b_dev, void* y_dev);
+void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* tiles);
 }  // namespace eigsol
 
 using namespace eigsol;
@@ -32,6 +42,7 @@ struct eigsol_power {
     eigsol_ctx* ctx = nullptr;
     eigsol_csr* csr = nullptr;
     eigsol_dense* dense = nullptr;
+    ShiftFactor* shift = nullptr;   // shifted inverse iteration: factor of A - sigma I
     int dtype = EIGSOL_F64;
     int64_t n = 0;            // rows owned (= vector length on one GPU)
     int64_t nbuf = 0;         // own + ghost entries (x-space)
@@ -84,12 +95,16 @@ static void session_free(eigsol_power* s) {
     hipFree(s->blk_part);
     if (s->trace) hipFree(s->trace);
     if (s->host_ctl) hipHostFree(s->host_ctl);
+    if (s->shift) shift_factor_free(s->shift);
     if (s->csr) csr_release(s->csr);
     if (s->dense) dense_release(s->dense);
     delete s;
 }
 
 static int launch_iteration(eigsol_power* s) {
+    if (s->shift)
+        return shift_iter_launch(s->shift, s->buf[0], s->buf[1], s->ctl, s->rank_part, s->my_part,
+                                 s->trace, s->parity);
     if (s->csr && s->dist) {
         EIGSOL_TRY(csr_power_launch(s->csr, s->nbuf, s->buf[0], s->buf[1], s->ctl, s->rank_part,
                                     s->ctx->nranks, s->my_part, s->blk_part, s->trace, s->parity, s->grid));
@@ -209,6 +224,7 @@ int eigsol_power_query(eigsol_power* s, int32_t* done, int32_t* launches) {
     }
     EIGSOL_HIP(hipSetDevice(s->ctx->device));
     EIGSOL_TRY(pull_ctl(s));
+    if (s->shift) EIGSOL_TRY(shift_error(s->shift));
     if (done) *done = s->host_ctl->done;
     if (launches) *launches = s->host_ctl->launches;
     return EIGSOL_OK;
@@ -268,7 +284,7 @@ int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int3
     int32_t n = 0;
     if (!s->trivial && s->trace) {
         EIGSOL_TRY(pull_ctl(s));
-        n = s->host_ctl->done ? s->host_ctl->iters : std::max(0, s->host_ctl->launches - 2);
+        n = s->host_ctl->ntrace;
         n = std::min(n, s->trace_cap);
         if (trace_host && capacity > 0) {
             const int32_t m = std::min(n, capacity);
@@ -283,7 +299,9 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
                              int32_t* variant) {
     if (!s) return fail(EIGSOL_E_INVALID, "eigsol_power_kernel_info: null session");
     const double sb = (double)scalar_bytes(s->dtype);
-    if (s->csr) {
+    if (s->shift) {
+        shift_info(s->shift, bytes, variant, tiles);
+    } else if (s->csr) {
         // values + int32 columns + int32 row pointers + x read once + y written once
         const double nnz = (double)s->csr->nnz, n = (double)s->csr->nrows;
         if (bytes) *bytes = (sb + 4.0) * nnz + 4.0 * (n + 1.0) + 2.0 * sb * n;
@@ -339,6 +357,116 @@ int eigsol_power_dense(eigsol_dense* A, const eigsol_solver_options* opts, const
     EIGSOL_TRY(eigsol_power_create_dense(A, 0, &s));
     const int rc = run_to_completion(s, opts, x0, lambda_out, x_out, iterations, converged);
     session_free(s);
+    return rc;
+}
+
+
+// ---------------------------------------------------------------- shifted inverse iteration
+// shiftedInversePowerMethod<S> (shifted_inverse_power_solver.hpp:112-125): the session factors
+// A - sigma I once at creation and runs one fused solve launch per iteration.
+static int shifted_create(eigsol_ctx* ctx, eigsol_csr* csr, eigsol_dense* dense, int dtype,
+                          int64_t n, const void* sigma, int32_t trace_capacity, eigsol_power** out) {
+    auto* s = new eigsol_power();
+    s->ctx = ctx;
+    s->dtype = dtype;
+    s->n = n;
+    s->nbuf = n;
+    int rc = csr ? shift_factor_csr(csr, sigma, &s->shift) : shift_factor_dense(dense, sigma, &s->shift);
+    if (rc == EIGSOL_OK) {
+        if (csr) { s->csr = csr; csr_retain(csr); }
+        else { s->dense = dense; dense_retain(dense); }
+        s->grid = std::max(64, shift_grid(s->shift));
+        rc = session_alloc(s, trace_capacity);
+    }
+    if (rc != EIGSOL_OK) { session_free(s); return rc; }
+    *out = s;
+    return EIGSOL_OK;
+}
+
+int eigsol_shifted_create_csr(eigsol_csr* A, const void* sigma, int32_t trace_capacity, eigsol_power** out) {
+    if (!A || !sigma || !out) return fail(EIGSOL_E_INVALID, "eigsol_shifted_create_csr: null pointer");
+    *out = nullptr;
+    if (A->dist || A->nrows != A->ncols)
+        return fail(EIGSOL_E_NOT_SQUARE, "shiftedInversePowerMethod: matrix must be square");
+    if (A->nrows == 0) return fail(EIGSOL_E_ZERO_SIZE, "shiftedInversePowerMethod: matrix has zero size");
+    return shifted_create(A->ctx, A, nullptr, A->dtype, A->nrows, sigma, trace_capacity, out);
+}
+
+int eigsol_shifted_create_dense(eigsol_dense* A, const void* sigma, int32_t trace_capacity, eigsol_power** out) {
+    if (!A || !sigma || !out) return fail(EIGSOL_E_INVALID, "eigsol_shifted_create_dense: null pointer");
+    *out = nullptr;
+    if (A->nrows != A->ncols) return fail(EIGSOL_E_NOT_SQUARE, "shiftedInversePowerMethod: matrix must be square");
+    if (A->nrows == 0) return fail(EIGSOL_E_ZERO_SIZE, "shiftedInversePowerMethod: matrix has zero size");
+    return shifted_create(A->ctx, nullptr, A, A->dtype, A->nrows, sigma, trace_capacity, out);
+}
+
+int eigsol_shifted_inverse_csr(eigsol_csr* A, const void* sigma, const eigsol_solver_options* opts,
+                               const void* x0, void* lambda_out, void* x_out, int32_t* iterations,
+                               int32_t* converged) {
+    if (!opts || !x0) return fail(EIGSOL_E_INVALID, "eigsol_shifted_inverse_csr: null opts/x0");
+    eigsol_power* s = nullptr;
+    EIGSOL_TRY(eigsol_shifted_create_csr(A, sigma, 0, &s));
+    const int rc = run_to_completion(s, opts, x0, lambda_out, x_out, iterations, converged);
+    session_free(s);
+    return rc;
+}
+
+int eigsol_shifted_inverse_dense(eigsol_dense* A, const void* sigma, const eigsol_solver_options* opts,
+                                 const void* x0, void* lambda_out, void* x_out, int32_t* iterations,
+                                 int32_t* converged) {
+    if (!opts || !x0) return fail(EIGSOL_E_INVALID, "eigsol_shifted_inverse_dense: null opts/x0");
+    eigsol_power* s = nullptr;
+    EIGSOL_TRY(eigsol_shifted_create_dense(A, sigma, 0, &s));
+    const int rc = run_to_completion(s, opts, x0, lambda_out, x_out, iterations, converged);
+    session_free(s);
+    return rc;
+}
+
+// solve_shifted<S> (solve_shifted.hpp:48-118): x = (A - sigma I)^{-1} b, host buffers.
+static int solve_once(ShiftFactor* f, eigsol_ctx* ctx, size_t sb, int64_t n, const void* b, void* x) {
+    void* d = nullptr;
+    EIGSOL_HIP(hipMalloc(&d, 2 * n * sb));
+    char* bd = static_cast<char*>(d);
+    char* yd = bd + n * sb;
+    int rc = EIGSOL_OK;
+    if (hipMemcpyAsync(bd, b, n * sb, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "solve_shifted: upload");
+    if (rc == EIGSOL_OK) rc = shift_solve_launch(f, bd, yd);
+    if (rc == EIGSOL_OK && hipMemcpyAsync(x, yd, n * sb, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "solve_shifted: download");
+    if (rc == EIGSOL_OK && hipStreamSynchronize(ctx->stream) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "solve_shifted: synchronize");
+    if (rc == EIGSOL_OK) rc = shift_error(f);
+    hipFree(d);
+    return rc;
+}
+
+int eigsol_solve_shifted_csr(eigsol_csr* A, const void* sigma, const void* b, int64_t nb, void* x) {
+    if (!A || !sigma || !b || !x) return fail(EIGSOL_E_INVALID, "eigsol_solve_shifted_csr: null pointer");
+    if (A->dist || A->nrows != A->ncols)
+        return fail(EIGSOL_E_NOT_SQUARE, "solve_shifted: A must be square (sparse case)");
+    if (A->nrows != nb)
+        return fail(EIGSOL_E_SIZE_MISMATCH, "solve_shifted: size mismatch between A and b (sparse case)");
+    if (nb == 0) return EIGSOL_OK;
+    EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    ShiftFactor* f = nullptr;
+    EIGSOL_TRY(shift_factor_csr(A, sigma, &f));
+    const int rc = solve_once(f, A->ctx, scalar_bytes(A->dtype), nb, b, x);
+    shift_factor_free(f);
+    return rc;
+}
+
+int eigsol_solve_shifted_dense(eigsol_dense* A, const void* sigma, const void* b, int64_t nb, void* x) {
+    if (!A || !sigma || !b || !x) return fail(EIGSOL_E_INVALID, "eigsol_solve_shifted_dense: null pointer");
+    if (A->nrows != A->ncols) return fail(EIGSOL_E_NOT_SQUARE, "solve_shifted: A must be square (dense case)");
+    if (A->nrows != nb)
+        return fail(EIGSOL_E_SIZE_MISMATCH, "solve_shifted: size mismatch between A and b (dense case)");
+    if (nb == 0) return EIGSOL_OK;
+    EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    ShiftFactor* f = nullptr;
+    EIGSOL_TRY(shift_factor_dense(A, sigma, &f));
+    const int rc = solve_once(f, A->ctx, scalar_bytes(A->dtype), nb, b, x);
+    shift_factor_free(f);
     return rc;
 }
 

@@ -1,4 +1,5 @@
 // Context, error reporting and device-memory helpers of the C ABI (include/eigsol_hip.h).
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -28,6 +29,21 @@ void ctx_release(eigsol_ctx* ctx) {
         (void)hipStreamDestroy(ctx->own_stream);
     }
     delete ctx;
+}
+
+// Blocks of `threads` threads resident at once over the whole chip, from the kernel's own VGPR
+// and LDS usage (MI355X_MICROARCH.md § Register files: waves per SIMD = floor(512 / VGPR
+// allocation), at most 8; 160 KiB LDS per CU).
+int resident_blocks(eigsol_ctx* ctx, const void* kernel, int threads, size_t dyn_lds, int* grid) {
+    hipFuncAttributes fa;
+    EIGSOL_HIP(hipFuncGetAttributes(&fa, kernel));
+    const int waves = std::max(1, threads / 64);
+    const int vgpr_alloc = std::max(8, ((fa.numRegs + 7) / 8) * 8);
+    const int by_vgpr = std::max(1, std::min(8, 512 / vgpr_alloc) * 4 / waves);
+    const size_t lds = fa.sharedSizeBytes + dyn_lds;
+    const int by_lds = lds ? (int)std::max<size_t>(1, 160 * 1024 / lds) : 32;
+    *grid = std::max(1, std::min(by_vgpr, by_lds)) * ctx->num_cus;
+    return EIGSOL_OK;
 }
 
 }  // namespace eigsol

@@ -1,0 +1,726 @@
+// Shifted inverse iteration and solve_shifted on gfx950: factor once, solve per iteration.
+//
+// Replaces the numeric core of shiftedInversePowerMethod<S>
+// (src/power_method/shifted_inverse_power_solver.hpp:112-125, impl :21-79) and solve_shifted<S>
+// (src/matrix/solve_shifted.hpp:48-118).  The reference refactors A - sigma I on every iteration
+// (SparseLU with COLAMD, or dense PartialPivLU); the factorisation does not depend on the
+// iterate, so the device path factors once per (A, sigma) and runs ONE solve launch per
+// iteration.  The Rayleigh quotient on A (:62) needs no product with A:
+// A y = x + sigma y, see shift_prologue (kernels_common.hpp).
+//
+// Factor kinds
+//   * triangular CSR (upper or lower; config 5): the factor IS the matrix.  Pivots d_i - sigma
+//     (coeffRef inserts a missing diagonal, solve_shifted.hpp:100-102), rows ordered by dependency
+//     level, and a sync-free triangular solve: each 16-lane group solves one row, waiting on
+//     per-row ready flags (epoch-stamped, so they never need resetting) of the rows it reads.
+//   * dense (Matrix::Dense, and small non-triangular sparse matrices densified on the device):
+//     right-looking partial-pivot LU (the unblocked order of Eigen's PartialPivLU), then a
+//     single-workgroup forward/back substitution per iteration with the vector in LDS.
+// Non-triangular sparse matrices too large to densify are reported as EIGSOL_E_UNSUPPORTED.
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstring>
+#include <vector>
+
+#include "kernels_common.hpp"
+
+namespace eigsol {
+
+struct ShiftFactor {
+    eigsol_ctx* ctx = nullptr;
+    int dtype = EIGSOL_F64;
+    int64_t n = 0;
+    int kind = 0;                 // 0 triangular CSR, 1 dense LU
+    double sig_re = 0.0, sig_im = 0.0;
+    // triangular
+    int upper = 1;
+    int64_t nnz_total = 0;        // nonzeros of A (diagonal included), for roofline accounting
+    int64_t nnz_off = 0;
+    int32_t* rowptr = nullptr;    // off-diagonal CSR, original row numbering
+    int32_t* col = nullptr;
+    void* val = nullptr;
+    void* piv = nullptr;          // d_i - sigma
+    int32_t* order = nullptr;     // positions -> row (-1: level padding)
+    int32_t npos = 0, nchunks = 0, nlevels = 0;
+    int32_t* flags = nullptr;     // ready stamps
+    uint32_t* work = nullptr;     // [0] chunk dispenser, [1] last-arriver ticket
+    int32_t* err = nullptr;
+    void* chunk_part = nullptr;   // part4 per chunk
+    int32_t epoch = 0;
+    int grid = 0;
+    // dense
+    void* lu = nullptr;           // column-major n x n, L (unit) below, U on and above the diagonal
+    int32_t* perm = nullptr;      // P b: b_perm[i] = b[perm[i]]
+    int32_t* zero_pivot = nullptr;
+    size_t lds_bytes = 0;
+};
+
+namespace dev {
+
+constexpr int kTriChunk = 64;    // positions per dispenser grab (one wave)
+constexpr int kRowLanes = 16;    // lanes per row
+constexpr int kSpinLimit = 1 << 21;
+
+template <class S>
+struct TriArgs {
+    const int32_t* rowptr;
+    const int32_t* col;
+    const S* val;
+    const S* piv;
+    const int32_t* order;
+    int32_t npos;
+    int32_t nchunks;
+    int32_t* flags;
+    uint32_t* work;
+    int32_t* err;
+    int32_t epoch;
+    const S* b_plain;   // solve mode
+    S* y_plain;
+    S* buf0;            // iteration mode (same parity convention as the power loop)
+    S* buf1;
+    PowerCtl* ctl;
+    const part4* rank_part;
+    part4* my_part;
+    part4* chunk_part;
+    S* trace;
+    double sig_re, sig_im;
+};
+
+__device__ __forceinline__ void st_coh(double* p, double v) { st_agent(p, v); }
+__device__ __forceinline__ void st_coh(cplx* p, cplx v) {
+    st_agent(&p->re, v.re);
+    st_agent(&p->im, v.im);
+}
+__device__ __forceinline__ double ld_coh(const double* p) { return ld_agent(p); }
+__device__ __forceinline__ cplx ld_coh(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
+__device__ __forceinline__ int ld_flag(const int32_t* p) {
+    return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum over the 16 lanes of a row group (xor butterfly inside the group: every lane gets the sum)
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int off = kRowLanes / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ cplx group_sum(cplx v) { return cplx{group_sum(v.re), group_sum(v.im)}; }
+
+// Sync-free triangular solve.  Positions are dispensed in chunks in increasing order; a row only
+// waits on rows of strictly lower level, i.e. strictly earlier positions, and every level is
+// padded to a multiple of 4 rows so the four row groups of one wave never depend on each other
+// (a wave spinning on a row held by its own lanes could never proceed).  Induction on the
+// earliest unfinished position gives progress without any residency assumption; a bounded spin
+// plus a sticky error word guarantees the grid drains even if that invariant were broken.
+template <class S, bool kIter>
+__global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int parity) {
+    __shared__ Prologue pro;
+    __shared__ int s_last;
+    __shared__ double sm[3 * kWaves];
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kIter) {
+        shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.b_plain;
+        yout = a.y_plain;
+    }
+    const int tid = threadIdx.x;
+    const int lane = tid & (kRowLanes - 1);
+    const int lane64 = tid & 63;
+    const int grp = lane64 / kRowLanes;              // 4 row groups per wave
+    constexpr int kGroups = 64 / kRowLanes;
+    const int epoch = a.epoch;
+    // Each wave takes chunks of kTriChunk positions from the dispenser on its own: no barrier
+    // inside the loop.  The grab and the partial stores are executed by ALL lanes (increment 1
+    // from lane 0 only; identical values stored): a lane-0-only branch at the loop head or latch
+    // lets the structurizer rotate that lane into a separate loop around the shuffles, which then
+    // read a stale chunk index and never exit.
+    auto grab = [&]() -> int {
+        const int old = (int)atomicAdd(&a.work[0], lane64 == 0 ? 1u : 0u);
+        return __builtin_amdgcn_readfirstlane(old);
+    };
+    for (int c = grab(); c < a.nchunks; c = grab()) {
+        double n2 = 0.0, pr = 0.0, pi = 0.0;
+        for (int r = grp; r < kTriChunk; r += kGroups) {
+            const int pos = c * kTriChunk + r;
+            if (pos >= a.npos) break;
+            const int i = a.order[pos];
+            if (i < 0) continue;                     // level padding
+            const int e0 = a.rowptr[i], e1 = a.rowptr[i + 1];
+            S acc = s_zero<S>();
+            for (int e = e0 + lane; e < e1; e += kRowLanes) {
+                const int j = a.col[e];
+                const S v = a.val[e];
+                int f = ld_flag(a.flags + j);
+                int spins = 0;
+                while (f < epoch) {
+                    __builtin_amdgcn_s_sleep(2);
+                    f = ld_flag(a.flags + j);
+                    if (++spins > kSpinLimit || ld_flag(a.err) != 0) {
+                        atomicOr(a.err, 1);
+                        break;
+                    }
+                }
+                acc = add(acc, mul(v, ld_coh(yout + j)));
+            }
+            acc = group_sum(acc);
+            S bi = xin[i];
+            if constexpr (kIter) bi = scale_in(bi, nrm);
+            const S yi = sdiv(sub(bi, acc), a.piv[i]);
+            if (lane == 0) {
+                st_coh(yout + i, yi);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(a.flags + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if constexpr (kIter) {
+                    n2 += sq_abs(yi);
+                    acc_dot(pr, pi, bi, yi);         // p = sum conj(x_i) y_i
+                }
+            }
+        }
+        if constexpr (kIter) {
+            n2 = wave_sum(n2);
+            pr = wave_sum(pr);
+            pi = wave_sum(pi);
+            part4* p = a.chunk_part + c;             // every lane stores the same sums
+            st_agent(&p->a, n2);
+            st_agent(&p->b, pr);
+            st_agent(&p->c, pi);
+        }
+    }
+    __syncthreads();
+    // last arriver: chunk partials in chunk order (deterministic), dispenser reset
+    if (tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(&a.work[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (tk == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if constexpr (kIter) {
+        double sa = 0.0, sb = 0.0, sc = 0.0;
+        for (int i = tid; i < a.nchunks; i += kThreads) {
+            sa += ld_agent(&a.chunk_part[i].a);
+            sb += ld_agent(&a.chunk_part[i].b);
+            sc += ld_agent(&a.chunk_part[i].c);
+        }
+        block_sum3(sa, sb, sc, sm);
+        if (tid == 0) {
+            a.my_part->a = sa;
+            a.my_part->b = sb;
+            a.my_part->c = sc;
+            a.my_part->d = 0.0;
+        }
+    }
+    if (tid == 0) {
+        __hip_atomic_store(&a.work[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.work[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// ------------------------------------------------------------------ dense LU (factor once)
+__device__ __forceinline__ double score(double v) { return fabs(v); }
+__device__ __forceinline__ double score(cplx v) { return hypot(v.re, v.im); }
+
+// Column k: pivot = first row of largest modulus in rows k..n-1, swap full rows, record the
+// transposition, scale the subdiagonal column by the pivot (skipped for a zero pivot, as Eigen's
+// partial_lu_impl does; the first zero pivot is recorded).
+template <class S>
+__global__ __launch_bounds__(1024) void lu_pivot_kernel(S* a, int64_t n, int64_t k, int32_t* piv,
+                                                        int32_t* zero_pivot) {
+    __shared__ double sv[1024];
+    __shared__ int si[1024];
+    __shared__ int s_p;
+    const int tid = threadIdx.x;
+    double best = -1.0;
+    int bi = (int)k;
+    for (int64_t i = k + tid; i < n; i += 1024) {
+        const double s = score(a[k * n + i]);
+        if (s > best) { best = s; bi = (int)i; }
+    }
+    sv[tid] = best;
+    si[tid] = bi;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+        if (tid < off) {
+            const double o = sv[tid + off];
+            const int oi = si[tid + off];
+            if (o > sv[tid] || (o == sv[tid] && oi < si[tid])) { sv[tid] = o; si[tid] = oi; }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        s_p = si[0];
+        piv[k] = si[0];
+        if (sv[0] == 0.0 && *zero_pivot < 0) *zero_pivot = (int)k;
+    }
+    __syncthreads();
+    const int64_t p = s_p;
+    if (p != k)
+        for (int64_t j = tid; j < n; j += 1024) {
+            const S t = a[j * n + k];
+            a[j * n + k] = a[j * n + p];
+            a[j * n + p] = t;
+        }
+    __syncthreads();
+    const S d = a[k * n + k];
+    if (score(d) != 0.0)
+        for (int64_t i = k + 1 + tid; i < n; i += 1024) a[k * n + i] = sdiv(a[k * n + i], d);
+}
+
+// trailing update a_ij -= l_ik u_kj, i, j > k (one thread per element, column-major coalesced)
+template <class S>
+__global__ __launch_bounds__(256) void lu_update_kernel(S* a, int64_t n, int64_t k) {
+    const int64_t m = n - k - 1;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= m * m) return;
+    const int64_t i = k + 1 + idx % m;
+    const int64_t j = k + 1 + idx / m;
+    a[j * n + i] = sub(a[j * n + i], mul(a[k * n + i], a[j * n + k]));
+}
+
+template <class S>
+struct DenseSolveArgs {
+    const S* lu;
+    const int32_t* perm;
+    int64_t n;
+    const S* b_plain;
+    S* y_plain;
+    S* buf0;
+    S* buf1;
+    PowerCtl* ctl;
+    const part4* rank_part;
+    part4* my_part;
+    S* trace;
+    double sig_re, sig_im;
+};
+
+// One workgroup: z = P b (scaled by 1/||y_prev|| in iteration mode), L z = P b (unit lower),
+// U y = z, all in LDS; column-oriented so every column access is coalesced.
+template <class S, bool kIter>
+__global__ __launch_bounds__(1024) void dense_lu_solve_kernel(DenseSolveArgs<S> a, int parity) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    S* z = reinterpret_cast<S*>(lds_raw);
+    __shared__ Prologue pro;
+    __shared__ double sm[3 * 16];
+    const int tid = threadIdx.x;
+    const int64_t n = a.n;
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kIter) {
+        shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.b_plain;
+        yout = a.y_plain;
+    }
+    for (int64_t i = tid; i < n; i += 1024) {
+        S v = xin[a.perm[i]];
+        if constexpr (kIter) v = scale_in(v, nrm);
+        z[i] = v;
+    }
+    __syncthreads();
+    // forward: for each column j, z_i -= L_ij z_j (i > j)
+    for (int64_t j = 0; j < n; ++j) {
+        const S zj = z[j];
+        const S* colj = a.lu + j * n;
+        for (int64_t i = j + 1 + tid; i < n; i += 1024) z[i] = sub(z[i], mul(colj[i], zj));
+        __syncthreads();
+    }
+    // backward: for each column j from the last, z_j /= U_jj, z_i -= U_ij z_j (i < j)
+    for (int64_t j = n - 1; j >= 0; --j) {
+        const S* colj = a.lu + j * n;
+        const S zj = sdiv(z[j], colj[j]);
+        __syncthreads();
+        if (tid == 0) z[j] = zj;
+        for (int64_t i = tid; i < j; i += 1024) z[i] = sub(z[i], mul(colj[i], zj));
+        __syncthreads();
+    }
+    double n2 = 0.0, pr = 0.0, pi = 0.0;
+    for (int64_t i = tid; i < n; i += 1024) {
+        const S yi = z[i];
+        yout[i] = yi;
+        if constexpr (kIter) {
+            S xi = xin[i];
+            xi = scale_in(xi, nrm);
+            n2 += sq_abs(yi);
+            acc_dot(pr, pi, xi, yi);
+        }
+    }
+    if constexpr (kIter) {
+        // 1024 threads = 16 waves: wave sums then a fixed-order sum by thread 0
+        n2 = wave_sum(n2);
+        pr = wave_sum(pr);
+        pi = wave_sum(pi);
+        const int w = tid >> 6;
+        if ((tid & 63) == 0) { sm[w] = n2; sm[16 + w] = pr; sm[32 + w] = pi; }
+        __syncthreads();
+        if (tid == 0) {
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+            for (int i = 0; i < 16; ++i) { s0 += sm[i]; s1 += sm[16 + i]; s2 += sm[32 + i]; }
+            a.my_part->a = s0;
+            a.my_part->b = s1;
+            a.my_part->c = s2;
+            a.my_part->d = 0.0;
+        }
+    }
+}
+
+// CSR (device) -> dense column-major (device), for small non-triangular sparse matrices
+template <class S>
+__global__ void densify_kernel(const int32_t* rowptr, const int32_t* col, const S* val, int64_t n,
+                               S* out) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n) return;
+    for (int e = rowptr[r]; e < rowptr[r + 1]; ++e) out[(int64_t)col[e] * n + r] = val[e];
+}
+
+template <class S>
+__global__ void shift_diag_kernel(S* a, int64_t n, S sigma) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) a[i * n + i] = sub(a[i * n + i], sigma);
+}
+
+}  // namespace dev
+
+// ================================================================== host side
+int resident_blocks(eigsol_ctx* ctx, const void* kernel, int threads, size_t dyn_lds, int* grid);
+
+template <class S>
+static S make_sigma(double re, double im) {
+    if constexpr (std::is_same_v<S, double>) { (void)im; return re; }
+    else return cplx{re, im};
+}
+
+static void shift_free(ShiftFactor* f) {
+    if (!f) return;
+    hipSetDevice(f->ctx->device);
+    hipStreamSynchronize(f->ctx->stream);
+    for (void* p : {(void*)f->rowptr, (void*)f->col, f->val, f->piv, (void*)f->order, (void*)f->flags,
+                    (void*)f->work, (void*)f->err, f->chunk_part, f->lu, (void*)f->perm,
+                    (void*)f->zero_pivot})
+        if (p) hipFree(p);
+    ctx_release(f->ctx);
+    delete f;
+}
+
+void shift_factor_free(ShiftFactor* f) { shift_free(f); }
+
+template <class S>
+static int dense_lu_factor(ShiftFactor* f, bool from_sparse) {
+    hipStream_t st = f->ctx->stream;
+    const int64_t n = f->n;
+    S* a = static_cast<S*>(f->lu);
+    int32_t* piv = nullptr;
+    EIGSOL_HIP(hipMalloc(&piv, n * sizeof(int32_t)));
+    EIGSOL_HIP(hipMalloc(&f->zero_pivot, sizeof(int32_t)));
+    EIGSOL_HIP(hipMemsetAsync(f->zero_pivot, 0xff, sizeof(int32_t), st));
+    hipLaunchKernelGGL((dev::shift_diag_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, a, n,
+                       make_sigma<S>(f->sig_re, f->sig_im));
+    for (int64_t k = 0; k < n; ++k) {
+        hipLaunchKernelGGL((dev::lu_pivot_kernel<S>), dim3(1), dim3(1024), 0, st, a, n, k, piv, f->zero_pivot);
+        const int64_t m = n - k - 1;
+        if (m > 0)
+            hipLaunchKernelGGL((dev::lu_update_kernel<S>), dim3((m * m + 255) / 256), dim3(256), 0, st, a, n, k);
+    }
+    EIGSOL_HIP(hipGetLastError());
+    std::vector<int32_t> hp(n);
+    int32_t zp = -1;
+    EIGSOL_HIP(hipMemcpyAsync(hp.data(), piv, n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipMemcpyAsync(&zp, f->zero_pivot, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipStreamSynchronize(st));
+    hipFree(piv);
+    // a sparse matrix goes through SparseLU in the reference, which reports a singular matrix
+    if (from_sparse && zp >= 0)
+        return fail(EIGSOL_E_SOLVER, "solve_shifted: SparseLU factorization failed");
+    // transpositions -> permutation: (P b)[i] = b[perm[i]]
+    std::vector<int32_t> perm(n);
+    for (int64_t i = 0; i < n; ++i) perm[i] = (int32_t)i;
+    for (int64_t k = 0; k < n; ++k) std::swap(perm[k], perm[hp[k]]);
+    EIGSOL_HIP(hipMalloc(&f->perm, n * sizeof(int32_t)));
+    EIGSOL_HIP(hipMemcpyAsync(f->perm, perm.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    EIGSOL_HIP(hipStreamSynchronize(st));
+    f->kind = 1;
+    f->lds_bytes = (size_t)n * sizeof(S);
+    return EIGSOL_OK;
+}
+
+static constexpr size_t kDenseSolveLds = 144 * 1024;   // vector of the single-CU substitution
+
+static int dense_limits(int dtype, int64_t n, const char* who) {
+    if ((size_t)n * scalar_bytes(dtype) > kDenseSolveLds)
+        return fail(EIGSOL_E_UNSUPPORTED, std::string(who) + ": dense factor of order " +
+                                              std::to_string(n) + " exceeds the single-CU LDS "
+                                              "substitution (n * sizeof(S) <= 144 KiB)");
+    return EIGSOL_OK;
+}
+
+template <class S>
+static int factor_dense_t(eigsol_dense* A, double sre, double sim, ShiftFactor** out) {
+    EIGSOL_TRY(dense_limits(A->dtype, A->nrows, "shifted solve"));
+    auto* f = new ShiftFactor();
+    f->ctx = A->ctx;
+    ctx_retain(f->ctx);
+    f->dtype = A->dtype;
+    f->n = A->nrows;
+    f->sig_re = sre;
+    f->sig_im = sim;
+    const size_t bytes = (size_t)f->n * f->n * sizeof(S);
+    int rc = EIGSOL_OK;
+    if (hipMalloc(&f->lu, bytes) != hipSuccess) rc = fail(EIGSOL_E_HIP, "hipMalloc(LU)");
+    if (rc == EIGSOL_OK && hipMemcpyAsync(f->lu, A->a, bytes, hipMemcpyDeviceToDevice, f->ctx->stream) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "hipMemcpyAsync(LU)");
+    if (rc == EIGSOL_OK) rc = dense_lu_factor<S>(f, false);
+    if (rc != EIGSOL_OK) { shift_free(f); return rc; }
+    *out = f;
+    return EIGSOL_OK;
+}
+
+int shift_factor_dense(eigsol_dense* A, const void* sigma, ShiftFactor** out) {
+    double s[2] = {0.0, 0.0};
+    std::memcpy(s, sigma, scalar_bytes(A->dtype));
+    EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    return A->dtype == EIGSOL_C128 ? factor_dense_t<cplx>(A, s[0], s[1], out)
+                                   : factor_dense_t<double>(A, s[0], 0.0, out);
+}
+
+// Level analysis of a triangular pattern (host, once per matrix): level(i) = 1 + max level of
+// the rows it reads; positions sorted by level, each level padded to a multiple of 4 rows.
+static void level_order(const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int64_t n,
+                        bool upper, std::vector<int32_t>& order, int32_t& nlevels) {
+    std::vector<int32_t> lev(n, 0);
+    int32_t maxl = 0;
+    auto visit = [&](int64_t i) {
+        int32_t l = 0;
+        for (int32_t e = rp[i]; e < rp[i + 1]; ++e) l = std::max(l, lev[ci[e]] + 1);
+        lev[i] = l;
+        maxl = std::max(maxl, l);
+    };
+    if (upper) for (int64_t i = n - 1; i >= 0; --i) visit(i);
+    else for (int64_t i = 0; i < n; ++i) visit(i);
+    nlevels = maxl + 1;
+    std::vector<int64_t> cnt(nlevels + 1, 0);
+    for (int64_t i = 0; i < n; ++i) ++cnt[lev[i] + 1];
+    std::vector<int64_t> start(nlevels + 1, 0);
+    for (int32_t l = 0; l < nlevels; ++l) start[l + 1] = start[l] + ((cnt[l + 1] + 3) / 4) * 4;
+    order.assign(start[nlevels], -1);
+    std::vector<int64_t> fill(start.begin(), start.end() - 1);
+    for (int64_t i = 0; i < n; ++i) order[fill[lev[i]]++] = (int32_t)i;
+}
+
+template <class S>
+static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out) {
+    hipStream_t st = A->ctx->stream;
+    const int64_t n = A->nrows, nnz = A->nnz;
+    std::vector<int32_t> rp(n + 1), ci(nnz);
+    std::vector<S> v(nnz);
+    EIGSOL_HIP(hipMemcpyAsync(rp.data(), A->rowptr, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipMemcpyAsync(ci.data(), A->col, nnz * 4, hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipMemcpyAsync(v.data(), A->val, nnz * sizeof(S), hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipStreamSynchronize(st));
+    bool up = true, lo = true;
+    for (int64_t i = 0; i < n && (up || lo); ++i)
+        for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+            if (ci[e] < i) up = false;
+            if (ci[e] > i) lo = false;
+        }
+    auto* f = new ShiftFactor();
+    f->ctx = A->ctx;
+    ctx_retain(f->ctx);
+    f->dtype = A->dtype;
+    f->n = n;
+    f->sig_re = sre;
+    f->sig_im = sim;
+    f->nnz_total = nnz;
+    int rc = EIGSOL_OK;
+    if (!up && !lo) {
+        // general sparse pattern: densify on the device and LU it (the reference's SparseLU)
+        rc = dense_limits(A->dtype, n, "solve_shifted (non-triangular sparse)");
+        const size_t bytes = (size_t)n * n * sizeof(S);
+        if (rc == EIGSOL_OK && hipMalloc(&f->lu, bytes) != hipSuccess) rc = fail(EIGSOL_E_HIP, "hipMalloc(LU)");
+        if (rc == EIGSOL_OK) {
+            hipMemsetAsync(f->lu, 0, bytes, st);
+            hipLaunchKernelGGL((dev::densify_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st,
+                               A->rowptr, A->col, static_cast<const S*>(A->val), n, static_cast<S*>(f->lu));
+            rc = dense_lu_factor<S>(f, true);
+        }
+        if (rc != EIGSOL_OK) { shift_free(f); return rc; }
+        *out = f;
+        return EIGSOL_OK;
+    }
+    f->upper = up ? 1 : 0;
+    // split diagonal / off-diagonal; pivots d_i - sigma (missing diagonal: 0 - sigma)
+    const S sig = make_sigma<S>(sre, sim);
+    std::vector<int32_t> orp(n + 1, 0), oci;
+    std::vector<S> ov, pv(n);
+    oci.reserve(nnz);
+    ov.reserve(nnz);
+    for (int64_t i = 0; i < n; ++i) {
+        S d = s_zero<S>();
+        for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+            if (ci[e] == i) {
+                if constexpr (std::is_same_v<S, double>) d = d + v[e];
+                else d = cplx{d.re + v[e].re, d.im + v[e].im};
+            } else {
+                oci.push_back(ci[e]);
+                ov.push_back(v[e]);
+            }
+        }
+        if constexpr (std::is_same_v<S, double>) pv[i] = d - sig;
+        else pv[i] = cplx{d.re - sig.re, d.im - sig.im};
+        const bool zero = std::is_same_v<S, double> ? (reinterpret_cast<double*>(&pv[i])[0] == 0.0)
+                                                     : (reinterpret_cast<double*>(&pv[i])[0] == 0.0 &&
+                                                        reinterpret_cast<double*>(&pv[i])[1] == 0.0);
+        if (zero) {
+            shift_free(f);
+            return fail(EIGSOL_E_SOLVER, "solve_shifted: SparseLU factorization failed");
+        }
+        orp[i + 1] = (int32_t)oci.size();
+    }
+    f->nnz_off = (int64_t)oci.size();
+    std::vector<int32_t> order;
+    level_order(orp, oci, n, up, order, f->nlevels);
+    f->npos = (int32_t)order.size();
+    f->nchunks = (f->npos + dev::kTriChunk - 1) / dev::kTriChunk;
+    auto up_ = [&](void** dst, const void* src, size_t bytes) -> int {
+        EIGSOL_HIP(hipMalloc(dst, std::max<size_t>(bytes, 16)));
+        if (bytes && src) EIGSOL_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, st));
+        return EIGSOL_OK;
+    };
+    rc = up_((void**)&f->rowptr, orp.data(), (n + 1) * 4);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->col, oci.data(), oci.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_(&f->val, ov.data(), ov.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_(&f->piv, pv.data(), n * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), order.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->flags, nullptr, n * 4);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->work, nullptr, 64);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->err, nullptr, 64);
+    if (rc == EIGSOL_OK) rc = up_(&f->chunk_part, nullptr, (size_t)f->nchunks * sizeof(dev::part4));
+    if (rc == EIGSOL_OK) {
+        hipMemsetAsync(f->flags, 0, n * 4, st);
+        hipMemsetAsync(f->work, 0, 64, st);
+        hipMemsetAsync(f->err, 0, 64, st);
+        if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "factor upload");
+    }
+    if (rc == EIGSOL_OK)
+        rc = resident_blocks(f->ctx, reinterpret_cast<const void*>(dev::sptrsv_kernel<S, true>),
+                             dev::kThreads, 0, &f->grid);
+    if (rc != EIGSOL_OK) { shift_free(f); return rc; }
+    f->grid = std::max(1, std::min(f->grid, f->nchunks));
+    f->kind = 0;
+    *out = f;
+    return EIGSOL_OK;
+}
+
+int shift_factor_csr(eigsol_csr* A, const void* sigma, ShiftFactor** out) {
+    if (A->dist) return fail(EIGSOL_E_UNSUPPORTED, "shifted inverse iteration: row-sharded matrices are not supported");
+    double s[2] = {0.0, 0.0};
+    std::memcpy(s, sigma, scalar_bytes(A->dtype));
+    EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    return A->dtype == EIGSOL_C128 ? factor_csr_t<cplx>(A, s[0], s[1], out)
+                                   : factor_csr_t<double>(A, s[0], 0.0, out);
+}
+
+int shift_grid(const ShiftFactor* f) { return f->kind == 0 ? f->grid : 1; }
+
+int shift_error(ShiftFactor* f) {
+    if (f->kind != 0) return EIGSOL_OK;
+    int32_t e = 0;
+    EIGSOL_HIP(hipMemcpyAsync(&e, f->err, 4, hipMemcpyDeviceToHost, f->ctx->stream));
+    EIGSOL_HIP(hipStreamSynchronize(f->ctx->stream));
+    if (e) return fail(EIGSOL_E_SOLVER, "triangular solve: dependency wait exceeded its bound (internal error)");
+    return EIGSOL_OK;
+}
+
+template <class S>
+static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, void* buf0, void* buf1,
+                          PowerCtl* ctl, const void* rank_part, void* my_part, void* trace, int parity) {
+    hipStream_t st = f->ctx->stream;
+    if (f->kind == 0) {
+        dev::TriArgs<S> a{};
+        a.rowptr = f->rowptr;
+        a.col = f->col;
+        a.val = static_cast<const S*>(f->val);
+        a.piv = static_cast<const S*>(f->piv);
+        a.order = f->order;
+        a.npos = f->npos;
+        a.nchunks = f->nchunks;
+        a.flags = f->flags;
+        a.work = f->work;
+        a.err = f->err;
+        a.epoch = ++f->epoch;
+        a.b_plain = static_cast<const S*>(b);
+        a.y_plain = static_cast<S*>(y);
+        a.buf0 = static_cast<S*>(buf0);
+        a.buf1 = static_cast<S*>(buf1);
+        a.ctl = ctl;
+        a.rank_part = static_cast<const dev::part4*>(rank_part);
+        a.my_part = static_cast<dev::part4*>(my_part);
+        a.chunk_part = static_cast<dev::part4*>(f->chunk_part);
+        a.trace = static_cast<S*>(trace);
+        a.sig_re = f->sig_re;
+        a.sig_im = f->sig_im;
+        if (iter) hipLaunchKernelGGL((dev::sptrsv_kernel<S, true>), dim3(f->grid), dim3(dev::kThreads), 0, st, a, parity);
+        else hipLaunchKernelGGL((dev::sptrsv_kernel<S, false>), dim3(f->grid), dim3(dev::kThreads), 0, st, a, parity);
+    } else {
+        dev::DenseSolveArgs<S> a{};
+        a.lu = static_cast<const S*>(f->lu);
+        a.perm = f->perm;
+        a.n = f->n;
+        a.b_plain = static_cast<const S*>(b);
+        a.y_plain = static_cast<S*>(y);
+        a.buf0 = static_cast<S*>(buf0);
+        a.buf1 = static_cast<S*>(buf1);
+        a.ctl = ctl;
+        a.rank_part = static_cast<const dev::part4*>(rank_part);
+        a.my_part = static_cast<dev::part4*>(my_part);
+        a.trace = static_cast<S*>(trace);
+        a.sig_re = f->sig_re;
+        a.sig_im = f->sig_im;
+        const void* k = iter ? reinterpret_cast<const void*>(dev::dense_lu_solve_kernel<S, true>)
+                             : reinterpret_cast<const void*>(dev::dense_lu_solve_kernel<S, false>);
+        EIGSOL_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)f->lds_bytes));
+        if (iter) hipLaunchKernelGGL((dev::dense_lu_solve_kernel<S, true>), dim3(1), dim3(1024), f->lds_bytes, st, a, parity);
+        else hipLaunchKernelGGL((dev::dense_lu_solve_kernel<S, false>), dim3(1), dim3(1024), f->lds_bytes, st, a, parity);
+    }
+    EIGSOL_HIP(hipGetLastError());
+    return EIGSOL_OK;
+}
+
+int shift_iter_launch(ShiftFactor* f, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
+                      void* my_part, void* trace, int parity) {
+    return f->dtype == EIGSOL_C128
+               ? shift_launch_t<cplx>(f, true, nullptr, nullptr, buf0, buf1, ctl, rank_part, my_part, trace, parity)
+               : shift_launch_t<double>(f, true, nullptr, nullptr, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+}
+
+int shift_solve_launch(ShiftFactor* f, const void* b_dev, void* y_dev) {
+    return f->dtype == EIGSOL_C128
+               ? shift_launch_t<cplx>(f, false, b_dev, y_dev, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0)
+               : shift_launch_t<double>(f, false, b_dev, y_dev, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+}
+
+// algorithmic bytes of one solve (the SpTRSV counts like the SpMV) and variant
+void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* tiles) {
+    const double sb = (double)scalar_bytes(f->dtype), n = (double)f->n;
+    if (f->kind == 0) {
+        if (bytes) *bytes = (sb + 4.0) * (double)f->nnz_total + 4.0 * (n + 1.0) + 2.0 * sb * n;
+        if (variant) *variant = 3;
+        if (tiles) *tiles = f->nlevels;
+    } else {
+        if (bytes) *bytes = sb * n * n + 2.0 * sb * n;
+        if (variant) *variant = 4;
+        if (tiles) *tiles = 0;
+    }
+}
+
+}  // namespace eigsol

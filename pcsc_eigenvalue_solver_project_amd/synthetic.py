@@ -59,7 +59,10 @@ def uniform(n_global: int, k: int, seed: int = 42, row0: int = 0, nrows: int | N
 
 
 def triu_complex(n: int, k: int, seed: int = 42, target=1.5 * np.exp(0.7j), gap: float = 0.05):
-    """Upper-triangular complex CSR, k nonzeros per row including the diagonal (config 5)."""
+    """Upper-triangular complex CSR, k nonzeros per row including the diagonal (config 5).
+
+    Returns (rowptr, colidx, values, diagonal); the eigenvalues are the diagonal, with the target
+    planted at row n // 3 and no other diagonal entry within `gap` of it."""
     rng = np.random.default_rng([seed, 5])
     # diagonal in the annulus, none within `gap` of the target except the planted one
     r = rng.uniform(1.0, 2.0, n)
@@ -71,16 +74,11 @@ def triu_complex(n: int, k: int, seed: int = 42, target=1.5 * np.exp(0.7j), gap:
         bad = np.abs(d - target) < gap
     p = n // 3
     d[p] = target
-    rows, cols, vals = [], [], []
     rowptr = np.zeros(n + 1, dtype=np.int64)
     off_k = k - 1
-    all_cols = []
-    all_vals = []
-    for_counts = np.zeros(n, dtype=np.int64)
     # off-diagonal columns uniform in (i, n): vectorised per row count min(off_k, n-1-i)
     cnt = np.minimum(off_k, n - 1 - np.arange(n))
-    for_counts[:] = cnt + 1
-    rowptr[1:] = np.cumsum(for_counts)
+    rowptr[1:] = np.cumsum(cnt + 1)
     nnz = int(rowptr[-1])
     colidx = np.empty(nnz, dtype=np.int64)
     values = np.empty(nnz, dtype=np.complex128)

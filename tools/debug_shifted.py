@@ -1,0 +1,24 @@
+import sys, time
+import numpy as np
+import scipy.sparse as sp
+sys.path.insert(0, ".")
+import pcsc_eigenvalue_solver_project_amd as E
+def p(*a):
+    print(time.strftime("%H:%M:%S"), *a, flush=True)
+ctx = E.Context(0)
+A = np.diag([1.0, 3.0, 10.0])
+M = E.CsrMatrix.from_scipy(ctx, sp.csc_matrix(A))
+p("matrix ok")
+x = E.solve_shifted(M, 2.9, np.ones(3))
+p("solve ok", x)
+s = E.ShiftedSession(M, 2.9, trace_capacity=16)
+p("session ok", s.kernel_info())
+s.begin(E.ShiftedSolverOptions(1000, 1e-8, 2.9), np.array([0.3, -0.2, 0.5]))
+p("begin ok")
+s.step(1)
+ctx.synchronize()
+p("step1 ok", s.query())
+s.step(10)
+p("step10", s.query(), s.trace(16))
+r = s.finish()
+p("finish", r)
