@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -44,10 +45,11 @@ struct ShiftFactor {
     int32_t* order = nullptr;     // positions -> row (-1: level padding)
     int32_t npos = 0, nchunks = 0, nlevels = 0;
     int32_t* flags = nullptr;     // ready stamps
-    uint32_t* work = nullptr;     // [0] chunk dispenser, [1] last-arriver ticket
+    uint32_t* work = nullptr;     // 8 chunk dispensers + last-arriver ticket (128 B apart)
     int32_t* err = nullptr;
     void* chunk_part = nullptr;   // part4 per chunk
     int32_t epoch = 0;
+    int32_t nclasses = 1;
     int grid = 0;
     // dense
     void* lu = nullptr;           // column-major n x n, L (unit) below, U on and above the diagonal
@@ -58,9 +60,12 @@ struct ShiftFactor {
 
 namespace dev {
 
-constexpr int kTriChunk = 64;    // positions per dispenser grab (one wave)
+constexpr int kU = 4;            // rows in flight per 16-lane group
+constexpr int kTriChunk = 4 * kU;   // positions per dispenser grab: one wave round (all in flight)
+constexpr int kDispStride = 32;  // dispenser counters 128 B apart; [8 * kDispStride] = ticket
+constexpr int kWaveRows = 4 * kU;   // positions per wave round: levels are padded to this
 constexpr int kRowLanes = 16;    // lanes per row
-constexpr int kSpinLimit = 1 << 21;
+constexpr int kSpinLimit = 1 << 20;   // x (512 cycles + a load) ~ 0.5-1 s
 
 template <class S>
 struct TriArgs {
@@ -75,6 +80,7 @@ struct TriArgs {
     uint32_t* work;
     int32_t* err;
     int32_t epoch;
+    int32_t nclasses;   // dispenser classes: 1, or 8 (blockIdx % 8)
     const S* b_plain;   // solve mode
     S* y_plain;
     S* buf0;            // iteration mode (same parity convention as the power loop)
@@ -108,8 +114,8 @@ __device__ __forceinline__ cplx group_sum(cplx v) { return cplx{group_sum(v.re),
 
 // Sync-free triangular solve.  Positions are dispensed in chunks in increasing order; a row only
 // waits on rows of strictly lower level, i.e. strictly earlier positions, and every level is
-// padded to a multiple of 4 rows so the four row groups of one wave never depend on each other
-// (a wave spinning on a row held by its own lanes could never proceed).  Induction on the
+// padded to a multiple of kWaveRows so the rows one wave holds at a time never depend on each
+// other (a wave spinning on a row held by its own lanes could never proceed).  Induction on the
 // earliest unfinished position gives progress without any residency assumption; a bounded spin
 // plus a sticky error word guarantees the grid drains even if that invariant were broken.
 template <class S, bool kIter>
@@ -141,46 +147,92 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
     // from lane 0 only; identical values stored): a lane-0-only branch at the loop head or latch
     // lets the structurizer rotate that lane into a separate loop around the shuffles, which then
     // read a stale chunk index and never exit.
+    // Eight dispensers (one per residue class of the chunk index, served by the blocks with
+    // blockIdx % 8 == class) so grabs do not serialise on one address; each class is still
+    // dispensed in increasing order, which is all the progress argument needs.
+    const int cls = a.nclasses > 1 ? (blockIdx.x & 7) : 0;
+    uint32_t* disp = a.work + kDispStride * cls;
     auto grab = [&]() -> int {
-        const int old = (int)atomicAdd(&a.work[0], lane64 == 0 ? 1u : 0u);
-        return __builtin_amdgcn_readfirstlane(old);
+        const int old = (int)atomicAdd(disp, lane64 == 0 ? 1u : 0u);
+        return cls + a.nclasses * __builtin_amdgcn_readfirstlane(old);
     };
     for (int c = grab(); c < a.nchunks; c = grab()) {
         double n2 = 0.0, pr = 0.0, pi = 0.0;
-        for (int r = grp; r < kTriChunk; r += kGroups) {
-            const int pos = c * kTriChunk + r;
-            if (pos >= a.npos) break;
-            const int i = a.order[pos];
-            if (i < 0) continue;                     // level padding
-            const int e0 = a.rowptr[i], e1 = a.rowptr[i + 1];
-            S acc = s_zero<S>();
-            for (int e = e0 + lane; e < e1; e += kRowLanes) {
-                const int j = a.col[e];
-                const S v = a.val[e];
-                int f = ld_flag(a.flags + j);
-                int spins = 0;
-                while (f < epoch) {
-                    __builtin_amdgcn_s_sleep(2);
-                    f = ld_flag(a.flags + j);
-                    if (++spins > kSpinLimit || ld_flag(a.err) != 0) {
-                        atomicOr(a.err, 1);
-                        break;
+        // a round: kU rows per 16-lane group, kWaveRows positions per wave, all of one level
+        for (int r0 = 0; r0 < kTriChunk; r0 += kWaveRows) {
+            const int pbase = c * kTriChunk + r0 + grp * kU;
+            int iu[kU], e0[kU], len[kU];
+            int maxlen = 0;
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int pos = pbase + u;
+                const int i = pos < a.npos ? a.order[pos] : -1;
+                iu[u] = i;
+                e0[u] = i >= 0 ? a.rowptr[i] : 0;
+                len[u] = i >= 0 ? a.rowptr[i + 1] - e0[u] : 0;
+                maxlen = max(maxlen, len[u]);
+            }
+            S acc[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) acc[u] = s_zero<S>();
+            for (int k = lane; k < maxlen; k += kRowLanes) {
+                // every load of the kU rows is issued before any wait (clamped, unconditional)
+                int j[kU];
+                S v[kU];
+                bool ok[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    ok[u] = k < len[u];
+                    const int e = ok[u] ? e0[u] + k : 0;
+                    const int jj = a.col[e];
+                    j[u] = ok[u] ? jj : 0;
+                    v[u] = a.val[e];
+                }
+                int f[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) f[u] = ld_flag(a.flags + j[u]);
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    int spins = 0;
+                    while (ok[u] && f[u] < epoch) {
+                        // back off: spinning waves must leave the memory system to the producers
+                        __builtin_amdgcn_s_sleep(8);
+                        f[u] = ld_flag(a.flags + j[u]);
+                        if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag(a.err) != 0)) {
+                            atomicOr(a.err, 1);
+                            break;
+                        }
                     }
                 }
-                acc = add(acc, mul(v, ld_coh(yout + j)));
-            }
-            acc = group_sum(acc);
-            S bi = xin[i];
-            if constexpr (kIter) bi = scale_in(bi, nrm);
-            const S yi = sdiv(sub(bi, acc), a.piv[i]);
-            if (lane == 0) {
-                st_coh(yout + i, yi);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.flags + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if constexpr (kIter) {
-                    n2 += sq_abs(yi);
-                    acc_dot(pr, pi, bi, yi);         // p = sum conj(x_i) y_i
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const S yj = ld_coh(yout + j[u]);
+                    if (ok[u]) acc[u] = add(acc[u], mul(v[u], yj));
                 }
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) acc[u] = group_sum(acc[u]);
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int i = iu[u];
+                if (i < 0) continue;                 // level padding / past the end
+                S bi = xin[i];
+                if constexpr (kIter) bi = scale_in(bi, nrm);
+                const S yi = sdiv(sub(bi, acc[u]), a.piv[i]);
+                if (lane == 0) {
+                    st_coh(yout + i, yi);
+                    if constexpr (kIter) {
+                        n2 += sq_abs(yi);
+                        acc_dot(pr, pi, bi, yi);     // p = sum conj(x_i) y_i
+                    }
+                }
+            }
+            if (lane == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // y visible before its flag
+#pragma unroll
+                for (int u = 0; u < kU; ++u)
+                    if (iu[u] >= 0)
+                        __hip_atomic_store(a.flags + iu[u], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         if constexpr (kIter) {
@@ -197,7 +249,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
     // last arriver: chunk partials in chunk order (deterministic), dispenser reset
     if (tid == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(&a.work[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t tk = __hip_atomic_fetch_add(&a.work[8 * kDispStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (tk == gridDim.x - 1) ? 1 : 0;
     }
     __syncthreads();
@@ -217,10 +269,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
             a.my_part->d = 0.0;
         }
     }
-    if (tid == 0) {
-        __hip_atomic_store(&a.work[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&a.work[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (tid <= 8) __hip_atomic_store(&a.work[tid * kDispStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------ dense LU (factor once)
@@ -494,7 +543,7 @@ int shift_factor_dense(eigsol_dense* A, const void* sigma, ShiftFactor** out) {
 }
 
 // Level analysis of a triangular pattern (host, once per matrix): level(i) = 1 + max level of
-// the rows it reads; positions sorted by level, each level padded to a multiple of 4 rows.
+// the rows it reads; positions sorted by level, each level padded to a multiple of kWaveRows.
 static void level_order(const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int64_t n,
                         bool upper, std::vector<int32_t>& order, int32_t& nlevels) {
     std::vector<int32_t> lev(n, 0);
@@ -511,7 +560,8 @@ static void level_order(const std::vector<int32_t>& rp, const std::vector<int32_
     std::vector<int64_t> cnt(nlevels + 1, 0);
     for (int64_t i = 0; i < n; ++i) ++cnt[lev[i] + 1];
     std::vector<int64_t> start(nlevels + 1, 0);
-    for (int32_t l = 0; l < nlevels; ++l) start[l + 1] = start[l] + ((cnt[l + 1] + 3) / 4) * 4;
+    constexpr int64_t W = dev::kWaveRows;
+    for (int32_t l = 0; l < nlevels; ++l) start[l + 1] = start[l] + ((cnt[l + 1] + W - 1) / W) * W;
     order.assign(start[nlevels], -1);
     std::vector<int64_t> fill(start.begin(), start.end() - 1);
     for (int64_t i = 0; i < n; ++i) order[fill[lev[i]]++] = (int32_t)i;
@@ -602,12 +652,12 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
     if (rc == EIGSOL_OK) rc = up_(&f->piv, pv.data(), n * sizeof(S));
     if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), order.size() * 4);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->flags, nullptr, n * 4);
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->work, nullptr, 64);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->work, nullptr, 2048);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->err, nullptr, 64);
     if (rc == EIGSOL_OK) rc = up_(&f->chunk_part, nullptr, (size_t)f->nchunks * sizeof(dev::part4));
     if (rc == EIGSOL_OK) {
         hipMemsetAsync(f->flags, 0, n * 4, st);
-        hipMemsetAsync(f->work, 0, 64, st);
+        hipMemsetAsync(f->work, 0, 2048, st);
         hipMemsetAsync(f->err, 0, 64, st);
         if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "factor upload");
     }
@@ -615,7 +665,14 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         rc = resident_blocks(f->ctx, reinterpret_cast<const void*>(dev::sptrsv_kernel<S, true>),
                              dev::kThreads, 0, &f->grid);
     if (rc != EIGSOL_OK) { shift_free(f); return rc; }
-    f->grid = std::max(1, std::min(f->grid, f->nchunks));
+    // One block per CU by default: enough waves to cover a dependency level many times over,
+    // few enough that waves parked on later levels do not flood the memory system with polls.
+    int per_cu = 1;
+    if (const char* env = std::getenv("EIGSOL_TRSV_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(env));
+    if (const char* env = std::getenv("EIGSOL_TRSV_CLASSES")) f->nclasses = std::atoi(env) == 8 ? 8 : 1;
+    f->grid = std::min(f->grid, per_cu * f->ctx->num_cus);
+    // at least one block per dispenser class (blockIdx % 8)
+    f->grid = std::max(8, std::min(f->grid, ((f->nchunks + 7) / 8) * 8));
     f->kind = 0;
     *out = f;
     return EIGSOL_OK;
@@ -658,6 +715,7 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.work = f->work;
         a.err = f->err;
         a.epoch = ++f->epoch;
+        a.nclasses = f->nclasses;
         a.b_plain = static_cast<const S*>(b);
         a.y_plain = static_cast<S*>(y);
         a.buf0 = static_cast<S*>(buf0);
