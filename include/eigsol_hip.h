@@ -171,6 +171,32 @@ int eigsol_solve_shifted_csr(eigsol_csr* A, const void* sigma, const void* b, in
 int eigsol_solve_shifted_dense(eigsol_dense* A, const void* sigma, const void* b, int64_t nb,
                                void* x);
 
+/* ---------------------------------------------------------------- QR method (dense)
+ * Host column-major buffers in and out; the work runs on the context's device.
+ * to_hessenberg_dense<S>   (to_hessenberg.hpp:23-80): H = Householder reduction of A (n x n).
+ * qr_decompose_dense<S>    (qr_decompose.hpp:25-86):  A (m x n) = Q (m x m) R (m x n); m or n
+ *                          == 0 fails with EIGSOL_E_EMPTY ("qr_decompose_dense: empty matrix").
+ * qr_eigenvalues_dense<S>  (qr_eigenvalues.hpp:40-108):
+ *   variant EIGSOL_QR_UNSHIFTED — the reference algorithm exactly: Hessenberg, then H <- R Q until
+ *     max|h(i,i-1)| <= tol (1 + ||H||_F); eigenvalues = diag(H) (eig_re_or_c: n scalars of the
+ *     dtype; eig_im unused); iterations = iter + 1 (maxIter + 1 when not converged);
+ *   variant EIGSOL_QR_FRANCIS (north_star; real matrices) — Hessenberg, then Francis multishift
+ *     double-shift sweeps to quasi-triangular form with deflation at unit roundoff.  eig_re_or_c
+ *     receives the real parts (= diag of the standardised real Schur form), eig_im (optional) the
+ *     imaginary parts; iterations = sweeps performed; converged = 0 if a block stalled for
+ *     max(30, maxIterations) sweeps.  Complex matrices use the unshifted variant.
+ * n == 0: iterations 0, converged 1 (qr_eigenvalues.hpp:55-57). */
+#define EIGSOL_QR_FRANCIS 0
+#define EIGSOL_QR_UNSHIFTED 1
+int eigsol_hessenberg_dense(eigsol_ctx* ctx, int dtype, int64_t n, const void* A_colmajor,
+                            void* H_out);
+int eigsol_qr_decompose_dense(eigsol_ctx* ctx, int dtype, int64_t m, int64_t n,
+                              const void* A_colmajor, void* Q_out, void* R_out);
+int eigsol_qr_eigenvalues_dense(eigsol_ctx* ctx, int dtype, int64_t n, const void* A_colmajor,
+                                const eigsol_solver_options* opts, int variant,
+                                void* eig_re_or_c, double* eig_im, int32_t* iterations,
+                                int32_t* converged);
+
 /* ---------------------------------------------------------------- row-sharded power iteration
  * One process per GPU; RCCL over xGMI (the reference has no distribution: SURVEY.md §2.1).
  * Rank r owns global rows [row_begins[r], row_begins[r+1]).  Bootstrap: rank 0 calls

@@ -323,3 +323,66 @@ def solve_shifted(matrix, shift, b) -> np.ndarray:
     fn = "eigsol_solve_shifted_csr" if isinstance(matrix, CsrMatrix) else "eigsol_solve_shifted_dense"
     call(fn, matrix.handle, _ptr(sig), _ptr(b), len(b), _ptr(x))
     return x
+
+
+# ------------------------------------------------------------------------------------ QR method
+@dataclass
+class QRResult:
+    """``EigSol::QRResult<S>`` (src/result/qr_result.hpp:25-43).  For the Francis variant on a
+    real matrix, ``eigenvalues`` holds the real parts (the diagonal of the standardised real Schur
+    form) and ``eigenvalues_complex`` the full complex eigenvalues."""
+
+    eigenvalues: np.ndarray
+    iterations: int
+    converged: bool
+    eigenvalues_complex: Optional[np.ndarray] = None
+
+
+def _square_dense(A, who: str) -> np.ndarray:
+    A = np.asarray(A)
+    if A.ndim != 2 or A.shape[0] != A.shape[1]:
+        raise EigSolError(1, f"{who}: A must be square")
+    return A
+
+
+def to_hessenberg(ctx: Context, A) -> np.ndarray:
+    """``EigSol::to_hessenberg_dense<S>`` (to_hessenberg.hpp:23-80) on the device."""
+    A = _square_dense(A, "to_hessenberg_dense")
+    code = _dtype_code(A.dtype)
+    Af = np.asfortranarray(A)
+    H = np.empty_like(Af, order="F")
+    call("eigsol_hessenberg_dense", ctx.handle, code, A.shape[0], _ptr(Af), _ptr(H))
+    return H
+
+
+def qr_decompose(ctx: Context, A):
+    """``EigSol::qr_decompose_dense<S>`` (qr_decompose.hpp:25-86): returns (Q, R)."""
+    A = np.asarray(A)
+    code = _dtype_code(A.dtype)
+    m, n = A.shape
+    Af = np.asfortranarray(A)
+    Q = np.empty((m, m), dtype=A.dtype, order="F")
+    R = np.empty((m, n), dtype=A.dtype, order="F")
+    call("eigsol_qr_decompose_dense", ctx.handle, code, m, n, _ptr(Af), _ptr(Q), _ptr(R))
+    return Q, R
+
+
+def qr_eigenvalues(ctx: Context, A, opts: SolverOptions = SolverOptions(), variant: str = "francis") -> QRResult:
+    """``EigSol::qr_eigenvalues<S>``.  variant "unshifted" = the reference algorithm
+    (qr_eigenvalues.hpp:40-108); "francis" = implicit multishift sweeps (real matrices)."""
+    A = _square_dense(A, "qr_eigenvalues_dense")
+    code = _dtype_code(A.dtype)
+    n = A.shape[0]
+    Af = np.asfortranarray(A)
+    v = 1 if variant == "unshifted" else 0
+    eig = np.zeros(max(n, 1), dtype=A.dtype)
+    wi = np.zeros(max(n, 1))
+    it, conv = C.c_int32(0), C.c_int32(0)
+    o = opts.to_c()
+    call("eigsol_qr_eigenvalues_dense", ctx.handle, code, n, _ptr(Af), C.byref(o), v, _ptr(eig),
+         _ptr(wi), C.byref(it), C.byref(conv))
+    eig = eig[:n]
+    full = None
+    if v == 0 and A.dtype == np.float64:
+        full = eig + 1j * wi[:n]
+    return QRResult(eig, int(it.value), bool(conv.value), full)

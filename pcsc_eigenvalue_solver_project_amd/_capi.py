@@ -29,6 +29,9 @@ EIGSOL_E_UNSUPPORTED = 12
 EIGSOL_F64 = 0
 EIGSOL_C128 = 1
 
+EIGSOL_QR_FRANCIS = 0
+EIGSOL_QR_UNSHIFTED = 1
+
 
 class EigSolError(RuntimeError):
     """A failing C-ABI call; ``status`` is the eigsol_status code."""
@@ -96,6 +99,10 @@ SIGNATURES = {
     "eigsol_shifted_inverse_dense": [_vp, _vp, C.POINTER(SolverOptionsC), _vp, _vp, _vp, _pi32, _pi32],
     "eigsol_solve_shifted_csr": [_vp, _vp, _vp, _i64, _vp],
     "eigsol_solve_shifted_dense": [_vp, _vp, _vp, _i64, _vp],
+    "eigsol_hessenberg_dense": [_vp, C.c_int, _i64, _vp, _vp],
+    "eigsol_qr_decompose_dense": [_vp, C.c_int, _i64, _i64, _vp, _vp, _vp],
+    "eigsol_qr_eigenvalues_dense": [_vp, C.c_int, _i64, _vp, C.POINTER(SolverOptionsC), C.c_int, _vp,
+                                    _vp, _pi32, _pi32],
 }
 _RESTYPES = {"eigsol_status_string": C.c_char_p, "eigsol_last_error": C.c_char_p}
 
