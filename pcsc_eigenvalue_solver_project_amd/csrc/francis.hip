@@ -46,17 +46,20 @@ struct ChaseArgs {
 };
 
 __global__ __launch_bounds__(1024) void chase_kernel(ChaseArgs a) {
-    __shared__ double h[kWin * kWin];
+    // H window with an odd leading dimension: the left updates walk a row across columns, and a
+    // stride of an even number of doubles would put every lane of a wave on the same LDS bank
+    __shared__ double h[kWin * (kWin + 1)];
     __shared__ double u[kWin * kWin];
     __shared__ double rp[kMaxBulges][6];   // xs, ys, zs, q, r, active (as double)
     __shared__ int rk[kMaxBulges];
     const int W = a.e - a.s;
+    const int ldh = W | 1;
     const int tid = threadIdx.x;
     const int nt = blockDim.x;
-    auto Hw = [&](int i, int j) -> double& { return h[(i - a.s) + (j - a.s) * W]; };
+    auto Hw = [&](int i, int j) -> double& { return h[(i - a.s) + (j - a.s) * ldh]; };
     for (int idx = tid; idx < W * W; idx += nt) {
         const int i = idx % W, j = idx / W;
-        h[idx] = a.H[(a.s + i) + (int64_t)(a.s + j) * a.n];
+        h[i + j * ldh] = a.H[(a.s + i) + (int64_t)(a.s + j) * a.n];
         u[idx] = (i == j) ? 1.0 : 0.0;
     }
     __syncthreads();
@@ -106,98 +109,118 @@ __global__ __launch_bounds__(1024) void chase_kernel(ChaseArgs a) {
             }
         }
         __syncthreads();
-        // ---- left updates: rows k..k+2 of each bulge, window columns j in [k, e)
-        for (int idx = tid; idx < a.nb * W; idx += nt) {
-            const int b = idx / W;
-            if (rp[b][5] == 0.0) continue;
-            const int k = rk[b];
-            const int j = a.s + idx % W;
-            if (j < k) continue;
-            const double xs = rp[b][0], ys = rp[b][1], zs = rp[b][2], q = rp[b][3], r = rp[b][4];
+        // ---- left updates: wave b owns bulge b; rows k..k+2, window columns j in [k, e)
+        const int wv = tid >> 6, ln = tid & 63;
+        if (wv < a.nb && rp[wv][5] != 0.0) {
+            const int k = rk[wv];
+            const double xs = rp[wv][0], ys = rp[wv][1], zs = rp[wv][2], q = rp[wv][3], r = rp[wv][4];
             const bool three = k != ihi - 1;
-            double p = Hw(k, j) + q * Hw(k + 1, j);
-            if (three) { p += r * Hw(k + 2, j); Hw(k + 2, j) -= p * zs; }
-            Hw(k + 1, j) -= p * ys;
-            Hw(k, j) -= p * xs;
+            for (int j = k + ln; j < a.e; j += 64) {
+                double p = Hw(k, j) + q * Hw(k + 1, j);
+                if (three) { p += r * Hw(k + 2, j); Hw(k + 2, j) -= p * zs; }
+                Hw(k + 1, j) -= p * ys;
+                Hw(k, j) -= p * xs;
+            }
         }
         __syncthreads();
-        // ---- right updates: window rows i in [max(l, s), min(k+3, ihi)], and all rows of U
-        for (int idx = tid; idx < a.nb * 2 * W; idx += nt) {
-            const int b = idx / (2 * W);
-            if (rp[b][5] == 0.0) continue;
-            const int k = rk[b];
-            const int rr = idx % (2 * W);
-            const double xs = rp[b][0], ys = rp[b][1], zs = rp[b][2], q = rp[b][3], r = rp[b][4];
+        // ---- right updates: window rows i in [max(l, s), min(k+3, ihi)], then all rows of U
+        if (wv < a.nb && rp[wv][5] != 0.0) {
+            const int k = rk[wv];
+            const double xs = rp[wv][0], ys = rp[wv][1], zs = rp[wv][2], q = rp[wv][3], r = rp[wv][4];
             const bool three = k != ihi - 1;
-            double* c0;
-            double* c1;
-            double* c2;
-            if (rr < W) {
-                const int i = a.s + rr;
-                if (i < l || i > min(k + 3, ihi)) continue;
-                c0 = &Hw(i, k);
-                c1 = &Hw(i, k + 1);
-                c2 = three ? &Hw(i, k + 2) : nullptr;
-            } else {
-                const int i = rr - W;
-                c0 = &u[i + (k - a.s) * W];
-                c1 = &u[i + (k + 1 - a.s) * W];
-                c2 = three ? &u[i + (k + 2 - a.s) * W] : nullptr;
+            const int ilast = min(k + 3, ihi);
+            for (int i = max(l, a.s) + ln; i <= ilast; i += 64) {
+                double p = xs * Hw(i, k) + ys * Hw(i, k + 1);
+                if (three) { p += zs * Hw(i, k + 2); Hw(i, k + 2) -= p * r; }
+                Hw(i, k + 1) -= p * q;
+                Hw(i, k) -= p;
             }
-            double p = xs * *c0 + ys * *c1;
-            if (three) { p += zs * *c2; *c2 -= p * r; }
-            *c1 -= p * q;
-            *c0 -= p;
+            double* u0 = u + (k - a.s) * W;
+            for (int i = ln; i < W; i += 64) {
+                double p = xs * u0[i] + ys * u0[i + W];
+                if (three) { p += zs * u0[i + 2 * W]; u0[i + 2 * W] -= p * r; }
+                u0[i + W] -= p * q;
+                u0[i] -= p;
+            }
         }
         __syncthreads();
     }
     for (int idx = tid; idx < W * W; idx += nt) {
         const int i = idx % W, j = idx / W;
-        a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] = h[idx];
+        a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] = h[i + j * ldh];
         a.U[idx] = u[idx];
     }
 }
 
-// H(s:e, c0:c1) <- U^T H(s:e, c0:c1); 32 columns per block
+// H(s:e, c0:c1) <- U^T H(s:e, c0:c1); 32 columns per block, 8 row groups of 12 rows per thread
+// group: thread (c, g) accumulates Y(12g .. 12g+11, c) over i with U(i, :) read as a broadcast
+// row and X(i, c) from an odd-strided panel (conflict-free).
 __global__ __launch_bounds__(256) void win_left_gemm(double* H, int64_t n, int s, int W, int64_t c0, int64_t c1,
                                                      const double* U) {
-    __shared__ double x[kWin * 32];
-    __shared__ double ut[kWin * kWin];
+    constexpr int LX = kWin + 1;
+    __shared__ double x[32 * LX];
+    __shared__ double ut[kWin * kWin];     // ut[i * kWin + r] = U(i, r)
     const int64_t cb = c0 + (int64_t)blockIdx.x * 32;
     const int nc = (int)min<int64_t>(32, c1 - cb);
     for (int idx = threadIdx.x; idx < W * nc; idx += 256) {
         const int i = idx % W, c = idx / W;
-        x[i + c * W] = H[(s + i) + (cb + c) * n];
+        x[c * LX + i] = H[(s + i) + (cb + c) * n];
     }
-    for (int idx = threadIdx.x; idx < W * W; idx += 256) ut[idx] = U[idx];
+    for (int idx = threadIdx.x; idx < kWin * kWin; idx += 256) {
+        const int i = idx / kWin, r = idx % kWin;
+        ut[idx] = (i < W && r < W) ? U[i + r * W] : 0.0;
+    }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < W * nc; idx += 256) {
-        const int r = idx % W, c = idx / W;
-        double acc = 0.0;
-        for (int i = 0; i < W; ++i) acc += ut[i + r * W] * x[i + c * W];   // U(i, r) X(i, c)
-        H[(s + r) + (cb + c) * n] = acc;
+    const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
+    double acc[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) acc[q] = 0.0;
+    for (int i = 0; i < W; ++i) {
+        const double xv = x[c * LX + i];
+        const double* ur = ut + i * kWin + 12 * g;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) acc[q] += ur[q] * xv;
     }
+    if (c < nc)
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            const int r = 12 * g + q;
+            if (r < W) H[(s + r) + (cb + c) * n] = acc[q];
+        }
 }
 
-// H(r0:r1, s:e) <- H(r0:r1, s:e) U; 32 rows per block
+// H(r0:r1, s:e) <- H(r0:r1, s:e) U; 32 rows per block, thread (r, g) owns Y(r, 12g .. 12g+11)
 __global__ __launch_bounds__(256) void win_right_gemm(double* H, int64_t n, int s, int W, int64_t r0, int64_t r1,
                                                       const double* U) {
-    __shared__ double x[32 * kWin];
-    __shared__ double us[kWin * kWin];
+    __shared__ double x[kWin * 32];        // x[i * 32 + r] = X(r, i)
+    __shared__ double us[kWin * kWin];     // us[i * kWin + j] = U(i, j)
     const int64_t rb = r0 + (int64_t)blockIdx.x * 32;
     const int nr = (int)min<int64_t>(32, r1 - rb);
-    for (int idx = threadIdx.x; idx < nr * W; idx += 256) {
-        const int r = idx % nr, j = idx / nr;
-        x[r + j * 32] = H[(rb + r) + (int64_t)(s + j) * n];
+    for (int idx = threadIdx.x; idx < 32 * W; idx += 256) {
+        const int r = idx & 31, i = idx >> 5;
+        x[i * 32 + r] = r < nr ? H[(rb + r) + (int64_t)(s + i) * n] : 0.0;
     }
-    for (int idx = threadIdx.x; idx < W * W; idx += 256) us[idx] = U[idx];
+    for (int idx = threadIdx.x; idx < kWin * kWin; idx += 256) {
+        const int i = idx / kWin, j = idx % kWin;
+        us[idx] = (i < W && j < W) ? U[i + j * W] : 0.0;
+    }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < nr * W; idx += 256) {
-        const int r = idx % nr, j = idx / nr;
-        double acc = 0.0;
-        for (int i = 0; i < W; ++i) acc += x[r + i * 32] * us[i + j * W];
-        H[(rb + r) + (int64_t)(s + j) * n] = acc;
+    const int r = threadIdx.x & 31, g = threadIdx.x >> 5;
+    double acc[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) acc[q] = 0.0;
+    for (int i = 0; i < W; ++i) {
+        const double xv = x[i * 32 + r];
+        const double* ur = us + i * kWin + 12 * g;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) acc[q] += xv * ur[q];
     }
+    if (r < nr)
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            const int j = 12 * g + q;
+            if (j < W) H[(rb + r) + (int64_t)(s + j) * n] = acc[q];
+        }
 }
 
 // diagonal and subdiagonal of the block [0, ihi]: out[0..n) = h(i,i), out[n..2n) = h(i,i-1)

@@ -564,7 +564,9 @@ static int qr_francis_host(eigsol_ctx* ctx, int64_t n, const double* A, int max_
 int hqr_lds(hipStream_t st, const double* H, int64_t ld, int n, int maxits, double* wr_dev, double* wi_dev,
             int* info_dev) {
     if (n > dev::kHqrMaxN) return fail(EIGSOL_E_UNSUPPORTED, "hqr_lds: n > 128");
-    hipLaunchKernelGGL(dev::hqr_lds_kernel, dim3(1), dim3(1024), 0, st, H, ld, n, wr_dev, wi_dev, maxits, info_dev);
+    // one wave for shift-sized problems (its barriers cost nothing), four waves otherwise
+    const int threads = n <= 64 ? 64 : 256;
+    hipLaunchKernelGGL(dev::hqr_lds_kernel, dim3(1), dim3(threads), 0, st, H, ld, n, wr_dev, wi_dev, maxits, info_dev);
     EIGSOL_HIP(hipGetLastError());
     return EIGSOL_OK;
 }

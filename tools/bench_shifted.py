@@ -1,7 +1,8 @@
 """Config 5 timing: 1M x 1M complex upper-triangular CSR, shifted inverse iteration."""
 import json, sys, time
 import numpy as np
-sys.path.insert(0, ".")
+ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 import torch
 import pcsc_eigenvalue_solver_project_amd as E
 from pcsc_eigenvalue_solver_project_amd import synthetic as S

@@ -1,7 +1,8 @@
 import sys, time
 import numpy as np
 import scipy.sparse as sp
-sys.path.insert(0, ".")
+ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 import pcsc_eigenvalue_solver_project_amd as E
 def p(*a):
     print(time.strftime("%H:%M:%S"), *a, flush=True)
