@@ -1,0 +1,362 @@
+// EigSol drop-in façade — value types (no Eigen dependency).
+//
+// Mirrors the reference's public types so that code written against
+// hugoheziyang/PCSC_Eigenvalue_Solver_Project compiles unchanged for the scalar types the
+// device path supports (double, std::complex<double>):
+//   ScalarConcept / Vector<S>        src/core/types.hpp:16-33
+//   is_close_relative                src/core/tolerance.hpp:28-33
+//   SolverOptions                    src/option/solver_option.hpp:14-20
+//   ShiftedSolverOptions<S>          src/option/shifted_solver_option.hpp:24-68
+//   EigenResult<S>                   src/result/eigen_result.hpp:22-52
+//   QRResult<S>                      src/result/qr_result.hpp:25-43
+// Matrix::Dense<S> / Matrix::Sparse<S> are the column-major DenseMatrix<S> and the CSC
+// SparseMatrix<S> below (the storage Eigen uses for the reference's canonical types,
+// matrix.hpp:39-44), with the subset of Eigen's interface the reference's API and tests use.
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdint>
+#include <deque>
+#include <initializer_list>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+namespace EigSol {
+
+template <typename T>
+struct is_complex_of_floating : std::false_type {};
+template <typename Inner>
+struct is_complex_of_floating<std::complex<Inner>> : std::bool_constant<std::is_floating_point_v<Inner>> {};
+
+template <typename S>
+inline constexpr bool ScalarConcept = std::is_floating_point_v<S> || is_complex_of_floating<S>::value;
+
+// Scalars with a device path (gfx950 kernels compute in fp64 / complex fp64).
+template <typename S>
+inline constexpr bool DeviceScalar = std::is_same_v<S, double> || std::is_same_v<S, std::complex<double>>;
+
+template <typename S>
+struct real_of { using type = S; };
+template <typename R>
+struct real_of<std::complex<R>> { using type = R; };
+
+// ------------------------------------------------------------------------------------- Vector
+template <typename S>
+class Vector {
+    static_assert(ScalarConcept<S>, "EigSol::Vector: scalar must be floating point or complex");
+
+public:
+    using Scalar = S;
+    Vector() = default;
+    explicit Vector(std::size_t n) : d_(n, S(0)) {}
+    Vector(std::initializer_list<S> v) : d_(v) {}
+    explicit Vector(std::vector<S> v) : d_(std::move(v)) {}
+
+    std::size_t size() const { return d_.size(); }
+    S& operator()(std::size_t i) { return d_[i]; }
+    const S& operator()(std::size_t i) const { return d_[i]; }
+    S& operator[](std::size_t i) { return d_[i]; }
+    const S& operator[](std::size_t i) const { return d_[i]; }
+    S* data() { return d_.data(); }
+    const S* data() const { return d_.data(); }
+    auto begin() { return d_.begin(); }
+    auto end() { return d_.end(); }
+    auto begin() const { return d_.begin(); }
+    auto end() const { return d_.end(); }
+    void resize(std::size_t n) { d_.resize(n, S(0)); }
+    const std::vector<S>& std() const { return d_; }
+
+    typename real_of<S>::type squaredNorm() const {
+        typename real_of<S>::type s = 0;
+        for (const S& x : d_) s += std::norm(x);
+        return s;
+    }
+    typename real_of<S>::type norm() const { return std::sqrt(squaredNorm()); }
+    // x^H y (the first argument is conjugated, like Eigen's dot)
+    S dot(const Vector& o) const {
+        S s = S(0);
+        for (std::size_t i = 0; i < d_.size(); ++i) s += conj_(d_[i]) * o.d_[i];
+        return s;
+    }
+    Vector operator-() const {
+        Vector r(*this);
+        for (S& x : r.d_) x = -x;
+        return r;
+    }
+    friend Vector operator-(const Vector& a, const Vector& b) {
+        Vector r(a);
+        for (std::size_t i = 0; i < r.size(); ++i) r.d_[i] -= b.d_[i];
+        return r;
+    }
+    friend Vector operator*(const S& s, const Vector& a) {
+        Vector r(a);
+        for (S& x : r.d_) x *= s;
+        return r;
+    }
+    // comma initialisation: v << 1, 2, 3;
+    struct Filler {
+        Vector* v;
+        std::size_t i;
+        Filler& operator,(const S& x) {
+            (*v)(i++) = x;
+            return *this;
+        }
+    };
+    Filler operator<<(const S& x) {
+        d_.at(0) = x;
+        return Filler{this, 1};
+    }
+
+private:
+    static S conj_(const S& x) {
+        if constexpr (is_complex_of_floating<S>::value) return std::conj(x);
+        else return x;
+    }
+    std::vector<S> d_;
+};
+
+// -------------------------------------------------------------------------------- DenseMatrix
+// Column-major rows x cols (Eigen::Matrix<S, Dynamic, Dynamic> default storage).
+template <typename S>
+class DenseMatrix {
+    static_assert(ScalarConcept<S>, "EigSol::DenseMatrix: scalar must be floating point or complex");
+
+public:
+    using Scalar = S;
+    DenseMatrix() = default;
+    DenseMatrix(std::int64_t rows, std::int64_t cols)
+        : r_(rows), c_(cols), d_(static_cast<std::size_t>(std::max<std::int64_t>(rows * cols, 0)), S(0)) {}
+
+    static DenseMatrix Zero(std::int64_t r, std::int64_t c) { return DenseMatrix(r, c); }
+    static DenseMatrix Identity(std::int64_t r, std::int64_t c) {
+        DenseMatrix m(r, c);
+        for (std::int64_t i = 0; i < std::min(r, c); ++i) m(i, i) = S(1);
+        return m;
+    }
+    std::int64_t rows() const { return r_; }
+    std::int64_t cols() const { return c_; }
+    std::int64_t size() const { return r_ * c_; }
+    S& operator()(std::int64_t i, std::int64_t j) { return d_[static_cast<std::size_t>(i + j * r_)]; }
+    const S& operator()(std::int64_t i, std::int64_t j) const { return d_[static_cast<std::size_t>(i + j * r_)]; }
+    S* data() { return d_.data(); }
+    const S* data() const { return d_.data(); }
+    void setIdentity() { *this = Identity(r_, c_); }
+    void setZero() { std::fill(d_.begin(), d_.end(), S(0)); }
+    void resize(std::int64_t r, std::int64_t c) { *this = DenseMatrix(r, c); }
+
+    DenseMatrix adjoint() const {
+        DenseMatrix t(c_, r_);
+        for (std::int64_t j = 0; j < c_; ++j)
+            for (std::int64_t i = 0; i < r_; ++i) {
+                if constexpr (is_complex_of_floating<S>::value) t(j, i) = std::conj((*this)(i, j));
+                else t(j, i) = (*this)(i, j);
+            }
+        return t;
+    }
+    friend DenseMatrix operator*(const DenseMatrix& a, const DenseMatrix& b) {
+        if (a.c_ != b.r_) throw std::runtime_error("DenseMatrix: product dimension mismatch");
+        DenseMatrix m(a.r_, b.c_);
+        for (std::int64_t j = 0; j < b.c_; ++j)
+            for (std::int64_t k = 0; k < a.c_; ++k) {
+                const S bk = b(k, j);
+                for (std::int64_t i = 0; i < a.r_; ++i) m(i, j) += a(i, k) * bk;
+            }
+        return m;
+    }
+    friend Vector<S> operator*(const DenseMatrix& a, const Vector<S>& x) {
+        if (static_cast<std::size_t>(a.c_) != x.size()) throw std::runtime_error("DenseMatrix: size mismatch");
+        Vector<S> y(static_cast<std::size_t>(a.r_));
+        for (std::int64_t j = 0; j < a.c_; ++j)
+            for (std::int64_t i = 0; i < a.r_; ++i) y(i) += a(i, j) * x(j);
+        return y;
+    }
+    friend DenseMatrix operator-(const DenseMatrix& a, const DenseMatrix& b) {
+        DenseMatrix m(a);
+        for (std::size_t i = 0; i < m.d_.size(); ++i) m.d_[i] -= b.d_[i];
+        return m;
+    }
+    friend DenseMatrix operator*(const S& s, const DenseMatrix& a) {
+        DenseMatrix m(a);
+        for (S& x : m.d_) x *= s;
+        return m;
+    }
+    // comma initialisation in row-major order: A << 1, 2, 3, 4;
+    struct Filler {
+        DenseMatrix* m;
+        std::int64_t k;
+        Filler& operator,(const S& x) {
+            m->set_rowmajor(k++, x);
+            return *this;
+        }
+    };
+    Filler operator<<(const S& x) {
+        set_rowmajor(0, x);
+        return Filler{this, 1};
+    }
+    void setRandom();   // defined in solvers.hpp (uses the façade's documented generator)
+
+private:
+    void set_rowmajor(std::int64_t k, const S& x) {
+        if (k >= size()) throw std::runtime_error("DenseMatrix: too many coefficients in comma initializer");
+        (*this)(k / c_, k % c_) = x;
+    }
+    std::int64_t r_ = 0, c_ = 0;
+    std::vector<S> d_;
+};
+
+// ------------------------------------------------------------------------------- SparseMatrix
+// Compressed sparse column with int32 indices (Eigen::SparseMatrix<S> = ColMajor, int).
+// insert(r, c) builds an uncompressed triplet list (duplicates are summed on compression).
+template <typename S>
+class SparseMatrix {
+    static_assert(ScalarConcept<S>, "EigSol::SparseMatrix: scalar must be floating point or complex");
+
+public:
+    using Scalar = S;
+    using StorageIndex = std::int32_t;
+    SparseMatrix() = default;
+    SparseMatrix(std::int64_t rows, std::int64_t cols) : r_(rows), c_(cols), outer_(cols + 1, 0) {}
+
+    std::int64_t rows() const { return r_; }
+    std::int64_t cols() const { return c_; }
+    std::int64_t nonZeros() const {
+        compress();
+        return static_cast<std::int64_t>(val_.size());
+    }
+    void reserve(std::int64_t) {}
+    S& insert(std::int64_t r, std::int64_t c) {
+        if (r < 0 || r >= r_ || c < 0 || c >= c_) throw std::out_of_range("SparseMatrix::insert: index out of range");
+        pend_.push_back({r, c, S(0)});   // deque: the returned reference stays valid
+        dirty_ = true;
+        return pend_.back().v;
+    }
+    void makeCompressed() const { compress(); }
+    void setIdentity() {
+        pend_.clear();
+        outer_.assign(c_ + 1, 0);
+        inner_.clear();
+        val_.clear();
+        for (std::int64_t i = 0; i < std::min(r_, c_); ++i) insert(i, i) = S(1);
+        compress();
+    }
+    S coeff(std::int64_t r, std::int64_t c) const {
+        compress();
+        for (std::int32_t e = outer_[c]; e < outer_[c + 1]; ++e)
+            if (inner_[e] == r) return val_[e];
+        return S(0);
+    }
+    S& coeffRef(std::int64_t r, std::int64_t c) {
+        compress();
+        for (std::int32_t e = outer_[c]; e < outer_[c + 1]; ++e)
+            if (inner_[e] == r) return val_[e];
+        return insert(r, c);
+    }
+    const std::int32_t* outerIndexPtr() const { compress(); return outer_.data(); }
+    const std::int32_t* innerIndexPtr() const { compress(); return inner_.data(); }
+    const S* valuePtr() const { compress(); return val_.data(); }
+
+    static SparseMatrix fromDense(const DenseMatrix<S>& d) {
+        SparseMatrix s(d.rows(), d.cols());
+        for (std::int64_t j = 0; j < d.cols(); ++j)
+            for (std::int64_t i = 0; i < d.rows(); ++i)
+                if (d(i, j) != S(0)) s.insert(i, j) = d(i, j);
+        s.compress();
+        return s;
+    }
+    DenseMatrix<S> toDense() const {
+        compress();
+        DenseMatrix<S> d(r_, c_);
+        for (std::int64_t j = 0; j < c_; ++j)
+            for (std::int32_t e = outer_[j]; e < outer_[j + 1]; ++e) d(inner_[e], j) += val_[e];
+        return d;
+    }
+
+private:
+    struct Trip {
+        std::int64_t r, c;
+        S v;
+    };
+    void compress() const {
+        if (!dirty_) return;
+        std::vector<Trip> all;
+        all.reserve(val_.size() + pend_.size());
+        for (std::int64_t j = 0; j < c_; ++j)
+            for (std::int32_t e = outer_[j]; e < outer_[j + 1]; ++e) all.push_back({inner_[e], j, val_[e]});
+        for (const Trip& t : pend_) all.push_back(t);
+        std::stable_sort(all.begin(), all.end(),
+                         [](const Trip& a, const Trip& b) { return a.c != b.c ? a.c < b.c : a.r < b.r; });
+        outer_.assign(c_ + 1, 0);
+        inner_.clear();
+        val_.clear();
+        for (std::size_t k = 0; k < all.size(); ++k) {
+            if (!inner_.empty() && k > 0 && all[k].c == all[k - 1].c && all[k].r == all[k - 1].r) {
+                val_.back() += all[k].v;
+                continue;
+            }
+            inner_.push_back(static_cast<std::int32_t>(all[k].r));
+            val_.push_back(all[k].v);
+            ++outer_[all[k].c + 1];
+        }
+        for (std::int64_t j = 0; j < c_; ++j) outer_[j + 1] += outer_[j];
+        pend_.clear();
+        dirty_ = false;
+    }
+    std::int64_t r_ = 0, c_ = 0;
+    mutable std::vector<std::int32_t> outer_, inner_;
+    mutable std::vector<S> val_;
+    mutable std::deque<Trip> pend_;   // stable references for insert()
+    mutable bool dirty_ = false;
+};
+
+// ------------------------------------------------------------------------------- options / results
+template <typename S>
+inline bool is_close_relative(S a, S b, double tol) {
+    const double diff = std::abs(a - b);
+    const double scale = 1.0 + std::abs(a);
+    return diff <= tol * scale;
+}
+
+struct SolverOptions {
+    int maxIterations = 1000;
+    double tolerance = 1e-10;
+};
+
+template <typename S>
+struct ShiftedSolverOptions : public SolverOptions {
+    S shift;
+    ShiftedSolverOptions() : SolverOptions(), shift(S(0)) {}
+    ShiftedSolverOptions(S s) : SolverOptions(), shift(s) {}   // NOLINT: implicit like the reference
+    ShiftedSolverOptions(S s, int maxIter, double tol) : SolverOptions(), shift(s) {
+        maxIterations = maxIter;
+        tolerance = tol;
+    }
+};
+
+template <typename S>
+struct EigenResult {
+    S eigenvalue{};
+    Vector<S> eigenvector;
+    int iterations = 0;
+    bool converged = false;
+    EigenResult() = default;
+    EigenResult(const S& lambda, const Vector<S>& vec, int iters, bool conv)
+        : eigenvalue(lambda), eigenvector(vec), iterations(iters), converged(conv) {}
+};
+
+template <typename S>
+struct QRResult {
+    Vector<S> eigenvalues;
+    int iterations = 0;
+    bool converged = false;
+    // Francis variant on a real matrix: the complex eigenvalues (eigenvalues = their real parts)
+    std::vector<std::complex<double>> eigenvalues_complex;
+    QRResult() = default;
+    QRResult(const Vector<S>& ev, int iters, bool conv) : eigenvalues(ev), iterations(iters), converged(conv) {}
+};
+
+}  // namespace EigSol

@@ -1,0 +1,136 @@
+// EigSol drop-in façade — the type-erased Matrix (src/matrix/matrix.hpp:36-246,
+// src/box/box.hpp:32-81, src/box/box_typed.hpp:27-79) and its device-resident mirror.
+//
+// Same contract as the reference: non-copyable and non-movable, built from a dense matrix, a
+// sparse matrix or a row-major std::vector, queried with isDense() / scalar_type() / type(),
+// unwrapped with cast<T>() (std::bad_cast on the wrong T).  New: the first solver call uploads the
+// matrix to the device (eigsol_dense_create / eigsol_csr_create_from_csc) and the handle is
+// cached for the Matrix's lifetime, so repeated solves do not re-upload.  Mutating the storage
+// obtained through the non-const cast<T>() drops the cached device copy.
+#pragma once
+
+#include <memory>
+#include <typeinfo>
+
+#include "core.hpp"
+#include "device.hpp"
+
+namespace EigSol {
+
+class Box {
+public:
+    Box() = default;
+    Box(const Box&) = delete;
+    Box& operator=(const Box&) = delete;
+    virtual ~Box() = default;
+    virtual const std::type_info& type() const noexcept = 0;
+};
+
+template <typename T>
+class BoxTyped final : public Box {
+public:
+    explicit BoxTyped(T v) : v_(std::move(v)) {}
+    const std::type_info& type() const noexcept override { return typeid(T); }
+    T& get() { return v_; }
+    const T& get() const { return v_; }
+
+private:
+    T v_;
+};
+
+class Matrix {
+public:
+    template <typename S>
+    using Dense = DenseMatrix<S>;
+    template <typename S>
+    using Sparse = SparseMatrix<S>;
+
+    Matrix() = delete;
+    Matrix(const Matrix&) = delete;
+    Matrix& operator=(const Matrix&) = delete;
+    Matrix(Matrix&&) = delete;
+    Matrix& operator=(Matrix&&) = delete;
+
+    template <typename S, typename = std::enable_if_t<ScalarConcept<S>>>
+    explicit Matrix(const DenseMatrix<S>& m)
+        : dense_(true), scalar_(&typeid(S)), box_(std::make_unique<BoxTyped<DenseMatrix<S>>>(m)) {}
+
+    template <typename S, typename = std::enable_if_t<ScalarConcept<S>>>
+    explicit Matrix(const SparseMatrix<S>& m)
+        : dense_(false), scalar_(&typeid(S)), box_(std::make_unique<BoxTyped<SparseMatrix<S>>>(m)) {
+        box_cast<SparseMatrix<S>>().makeCompressed();
+    }
+
+    // row-major data (matrix.hpp:207-232)
+    template <typename S, typename = std::enable_if_t<ScalarConcept<S>>>
+    Matrix(const std::vector<S>& data, std::size_t rows, std::size_t cols) : dense_(true), scalar_(&typeid(S)) {
+        if (rows * cols != data.size()) throw std::runtime_error("Matrix: size mismatch in vector constructor");
+        DenseMatrix<S> m(static_cast<std::int64_t>(rows), static_cast<std::int64_t>(cols));
+        for (std::size_t i = 0; i < data.size(); ++i)
+            m(static_cast<std::int64_t>(i / cols), static_cast<std::int64_t>(i % cols)) = data[i];
+        box_ = std::make_unique<BoxTyped<DenseMatrix<S>>>(std::move(m));
+    }
+
+    bool isDense() const { return dense_; }
+    const std::type_info& scalar_type() const { return *scalar_; }
+    const std::type_info& type() const { return box_->type(); }
+
+    template <typename T>
+    T& cast() {
+        check<T>();
+        dev_.reset();   // the caller may modify the storage
+        return box_cast<T>();
+    }
+    template <typename T>
+    const T& cast() const {
+        check<T>();
+        return static_cast<const BoxTyped<T>*>(box_.get())->get();
+    }
+
+    std::int64_t rows() const { return visit([](const auto& m) { return m.rows(); }); }
+    std::int64_t cols() const { return visit([](const auto& m) { return m.cols(); }); }
+
+    // Device mirror (created on first use by the solvers).
+    template <typename S>
+    const detail::DeviceMatrix& device() const {
+        if (!dev_) {
+            if (dense_) {
+                const auto& d = cast<DenseMatrix<S>>();
+                dev_ = detail::DeviceMatrix::dense(detail::dtype_of<S>(), d.rows(), d.cols(), d.data());
+            } else {
+                const auto& s = cast<SparseMatrix<S>>();
+                dev_ = detail::DeviceMatrix::csc(detail::dtype_of<S>(), s.rows(), s.cols(), s.nonZeros(),
+                                                 s.outerIndexPtr(), s.innerIndexPtr(), s.valuePtr());
+            }
+        }
+        return *dev_;
+    }
+
+private:
+    template <typename T>
+    void check() const {
+        if (box_->type() != typeid(T)) throw std::bad_cast{};
+    }
+    template <typename T>
+    T& box_cast() {
+        return static_cast<BoxTyped<T>*>(box_.get())->get();
+    }
+    template <typename F>
+    std::int64_t visit(F f) const {
+        const std::type_info& t = box_->type();
+        if (t == typeid(DenseMatrix<double>)) return f(cast<DenseMatrix<double>>());
+        if (t == typeid(DenseMatrix<std::complex<double>>)) return f(cast<DenseMatrix<std::complex<double>>>());
+        if (t == typeid(SparseMatrix<double>)) return f(cast<SparseMatrix<double>>());
+        if (t == typeid(SparseMatrix<std::complex<double>>)) return f(cast<SparseMatrix<std::complex<double>>>());
+        if (t == typeid(DenseMatrix<float>)) return f(cast<DenseMatrix<float>>());
+        if (t == typeid(SparseMatrix<float>)) return f(cast<SparseMatrix<float>>());
+        return -1;
+    }
+
+    bool dense_;
+    const std::type_info* scalar_;
+    std::unique_ptr<Box> box_;
+    mutable std::shared_ptr<detail::DeviceMatrix> dev_;
+};
+
+}  // namespace EigSol

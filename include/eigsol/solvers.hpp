@@ -1,0 +1,230 @@
+// EigSol drop-in façade — solver entry points, same names, signatures, check order and exception
+// messages as the reference, numeric core on the gfx950 device through the C ABI.
+//
+//   powerMethod<S>                 src/power_method/power_method.hpp:135-148
+//   shiftedInversePowerMethod<S>   src/power_method/shifted_inverse_power_solver.hpp:112-125
+//   solve_shifted<S>               src/matrix/solve_shifted.hpp:48-118
+//   to_hessenberg<S> / _dense      src/qr_method/to_hessenberg.hpp:23-119
+//   qr_decompose<S> / _dense       src/qr_method/qr_decompose.hpp:25-132
+//   qr_eigenvalues<S> / _dense     src/qr_method/qr_eigenvalues.hpp:40-147
+//
+// Start vector: the reference draws x0 with Eigen's Vector::Random (std::rand, not reproducible
+// across Eigen versions).  Here x0 comes from a documented generator
+// (std::mt19937_64 seeded with EigSol::random_seed(), U(-1, 1) per real/imaginary component);
+// overloads taking an explicit x0 are provided.  Iteration semantics (counts, convergence test,
+// zero-norm and maxIterations <= 0 cases) are the reference's, evaluated on the device.
+#pragma once
+
+#include <random>
+#include <typeinfo>
+#include <utility>
+
+#include "matrix.hpp"
+
+namespace EigSol {
+
+inline std::uint64_t& random_seed() {
+    static std::uint64_t seed = 0x5eed5eedULL;
+    return seed;
+}
+
+template <typename S>
+Vector<S> random_vector(std::size_t n) {
+    static std::mt19937_64 gen(random_seed());
+    std::uniform_real_distribution<double> u(-1.0, 1.0);
+    Vector<S> v(n);
+    for (std::size_t i = 0; i < n; ++i) {
+        if constexpr (is_complex_of_floating<S>::value) {
+            const double re = u(gen);
+            const double im = u(gen);
+            v(i) = S(re, im);
+        } else {
+            v(i) = S(u(gen));
+        }
+    }
+    return v;
+}
+
+template <typename S>
+void DenseMatrix<S>::setRandom() {
+    Vector<S> v = random_vector<S>(static_cast<std::size_t>(size()));
+    std::copy(v.begin(), v.end(), d_.begin());
+}
+
+// QR iteration variant: Francis (implicit multishift sweeps, north_star) or the reference's
+// unshifted H <- RQ iteration (identical iteration counts).
+enum class QRVariant { Francis = EIGSOL_QR_FRANCIS, Unshifted = EIGSOL_QR_UNSHIFTED };
+
+namespace detail {
+
+inline eigsol_solver_options copts(const SolverOptions& o) {
+    eigsol_solver_options c;
+    c.max_iterations = o.maxIterations;
+    c.tolerance = o.tolerance;
+    return c;
+}
+
+template <typename S>
+void require_device_scalar(const char* who) {
+    if constexpr (!DeviceScalar<S>)
+        throw std::runtime_error(std::string(who) + ": scalar type not supported by the device path "
+                                                    "(double, std::complex<double>)");
+}
+
+template <typename S>
+EigenResult<S> power_like(const Matrix& M, const SolverOptions& opts, const Vector<S>* x0, const S* shift,
+                          const char* who) {
+    if (M.scalar_type() != typeid(S)) throw std::runtime_error(std::string(who) + ": scalar type mismatch");
+    const std::int64_t r = M.rows(), c = M.cols();
+    if (r != c) throw std::runtime_error(std::string(who) + ": matrix must be square");
+    if (r == 0) throw std::runtime_error(std::string(who) + ": matrix has zero size");
+    require_device_scalar<S>(who);
+    if constexpr (DeviceScalar<S>) {
+        Vector<S> xs = x0 ? *x0 : random_vector<S>(static_cast<std::size_t>(r));
+        if (xs.size() != static_cast<std::size_t>(r))
+            throw std::runtime_error(std::string(who) + ": start vector size mismatch");
+        const detail::DeviceMatrix& d = M.device<S>();
+        const eigsol_solver_options o = copts(opts);
+        S lam{};
+        Vector<S> x(static_cast<std::size_t>(r));
+        std::int32_t it = 0, conv = 0;
+        int st;
+        if (shift) {
+            st = M.isDense() ? eigsol_shifted_inverse_dense(d.dense(), shift, &o, xs.data(), &lam, x.data(), &it, &conv)
+                             : eigsol_shifted_inverse_csr(d.csr(), shift, &o, xs.data(), &lam, x.data(), &it, &conv);
+        } else {
+            st = M.isDense() ? eigsol_power_dense(d.dense(), &o, xs.data(), &lam, x.data(), &it, &conv)
+                             : eigsol_power_csr(d.csr(), &o, xs.data(), &lam, x.data(), &it, &conv);
+        }
+        check(st, who);
+        return EigenResult<S>(lam, x, it, conv != 0);
+    }
+    return {};
+}
+
+template <typename S>
+void dense_square_check(const DenseMatrix<S>& A, const char* who) {
+    if (A.rows() != A.cols()) throw std::runtime_error(std::string(who) + ": A must be square");
+}
+
+}  // namespace detail
+
+// ------------------------------------------------------------------------------ power methods
+template <typename S>
+EigenResult<S> powerMethod(const Matrix& M, const SolverOptions& opts = SolverOptions{}) {
+    return detail::power_like<S>(M, opts, nullptr, nullptr, "powerMethod");
+}
+template <typename S>
+EigenResult<S> powerMethod(const Matrix& M, const SolverOptions& opts, const Vector<S>& x0) {
+    return detail::power_like<S>(M, opts, &x0, nullptr, "powerMethod");
+}
+
+template <typename S>
+EigenResult<S> shiftedInversePowerMethod(const Matrix& M,
+                                         const ShiftedSolverOptions<S>& opts = ShiftedSolverOptions<S>{}) {
+    return detail::power_like<S>(M, opts, nullptr, &opts.shift, "shiftedInversePowerMethod");
+}
+template <typename S>
+EigenResult<S> shiftedInversePowerMethod(const Matrix& M, const ShiftedSolverOptions<S>& opts, const Vector<S>& x0) {
+    return detail::power_like<S>(M, opts, &x0, &opts.shift, "shiftedInversePowerMethod");
+}
+
+// --------------------------------------------------------------------------------- solve_shifted
+template <typename S>
+Vector<S> solve_shifted(const Matrix& A, const S shift, const Vector<S>& b) {
+    if (A.scalar_type() != typeid(S)) throw std::runtime_error("solve_shifted: scalar type mismatch");
+    const char* kind = A.isDense() ? "dense" : "sparse";
+    if (A.rows() != A.cols())
+        throw std::runtime_error(std::string("solve_shifted: A must be square (") + kind + " case)");
+    if (A.rows() != static_cast<std::int64_t>(b.size()))
+        throw std::runtime_error(std::string("solve_shifted: size mismatch between A and b (") + kind + " case)");
+    detail::require_device_scalar<S>("solve_shifted");
+    Vector<S> x(b.size());
+    if constexpr (DeviceScalar<S>) {
+        if (b.size() == 0) return x;
+        const detail::DeviceMatrix& d = A.device<S>();
+        const std::int64_t n = static_cast<std::int64_t>(b.size());
+        detail::check(A.isDense() ? eigsol_solve_shifted_dense(d.dense(), &shift, b.data(), n, x.data())
+                                  : eigsol_solve_shifted_csr(d.csr(), &shift, b.data(), n, x.data()),
+                      "solve_shifted");
+    }
+    return x;
+}
+
+// ------------------------------------------------------------------------------------ QR method
+template <typename S>
+DenseMatrix<S> to_hessenberg_dense(const DenseMatrix<S>& A) {
+    detail::dense_square_check(A, "to_hessenberg_dense");
+    detail::require_device_scalar<S>("to_hessenberg_dense");
+    DenseMatrix<S> H(A.rows(), A.cols());
+    if constexpr (DeviceScalar<S>) {
+        if (A.rows() > 0)
+            detail::check(eigsol_hessenberg_dense(detail::ctx(), detail::dtype_of<S>(), A.rows(), A.data(), H.data()),
+                          "to_hessenberg_dense");
+    }
+    return H;
+}
+
+template <typename S>
+DenseMatrix<S> to_hessenberg(const Matrix& A) {
+    if (!A.isDense()) throw std::runtime_error("to_hessenberg(Matrix): only dense matrices are supported");
+    if (A.scalar_type() != typeid(S)) throw std::runtime_error("to_hessenberg(Matrix): scalar type mismatch");
+    return to_hessenberg_dense<S>(A.cast<DenseMatrix<S>>());
+}
+
+template <typename S>
+void qr_decompose_dense(const DenseMatrix<S>& A, DenseMatrix<S>& Q, DenseMatrix<S>& R) {
+    if (A.rows() == 0 || A.cols() == 0) throw std::runtime_error("qr_decompose_dense: empty matrix");
+    detail::require_device_scalar<S>("qr_decompose_dense");
+    Q = DenseMatrix<S>(A.rows(), A.rows());
+    R = DenseMatrix<S>(A.rows(), A.cols());
+    if constexpr (DeviceScalar<S>)
+        detail::check(eigsol_qr_decompose_dense(detail::ctx(), detail::dtype_of<S>(), A.rows(), A.cols(), A.data(),
+                                                Q.data(), R.data()),
+                      "qr_decompose_dense");
+}
+
+template <typename S>
+std::pair<DenseMatrix<S>, DenseMatrix<S>> qr_decompose(const Matrix& A) {
+    if (!A.isDense()) throw std::runtime_error("qr_decompose(Matrix): only dense matrices are supported");
+    if (A.scalar_type() != typeid(S)) throw std::runtime_error("qr_decompose(Matrix): scalar type mismatch");
+    DenseMatrix<S> Q, R;
+    qr_decompose_dense<S>(A.cast<DenseMatrix<S>>(), Q, R);
+    return {Q, R};
+}
+
+template <typename S>
+QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& opts,
+                                 QRVariant variant = QRVariant::Francis) {
+    detail::dense_square_check(A, "qr_eigenvalues_dense");
+    const std::int64_t n = A.rows();
+    if (n == 0) return QRResult<S>(Vector<S>(), 0, true);   // qr_eigenvalues.hpp:55-57
+    detail::require_device_scalar<S>("qr_eigenvalues_dense");
+    QRResult<S> res;
+    if constexpr (DeviceScalar<S>) {
+        Vector<S> ev(static_cast<std::size_t>(n));
+        std::vector<double> wi(static_cast<std::size_t>(n), 0.0);
+        std::int32_t it = 0, conv = 0;
+        const eigsol_solver_options o = detail::copts(opts);
+        detail::check(eigsol_qr_eigenvalues_dense(detail::ctx(), detail::dtype_of<S>(), n, A.data(), &o,
+                                                  static_cast<int>(variant), ev.data(), wi.data(), &it, &conv),
+                      "qr_eigenvalues_dense");
+        res = QRResult<S>(ev, it, conv != 0);
+        if constexpr (std::is_same_v<S, double>) {
+            if (variant == QRVariant::Francis) {
+                res.eigenvalues_complex.resize(static_cast<std::size_t>(n));
+                for (std::int64_t i = 0; i < n; ++i) res.eigenvalues_complex[i] = {ev(i), wi[i]};
+            }
+        }
+    }
+    return res;
+}
+
+template <typename S>
+QRResult<S> qr_eigenvalues(const Matrix& A, const SolverOptions& opts, QRVariant variant = QRVariant::Francis) {
+    if (!A.isDense()) throw std::runtime_error("qr_eigenvalues(Matrix): only dense matrices are supported");
+    if (A.scalar_type() != typeid(S)) throw std::runtime_error("qr_eigenvalues(Matrix): scalar type mismatch");
+    return qr_eigenvalues_dense<S>(A.cast<DenseMatrix<S>>(), opts, variant);
+}
+
+}  // namespace EigSol

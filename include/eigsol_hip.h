@@ -183,8 +183,9 @@ int eigsol_solve_shifted_dense(eigsol_dense* A, const void* sigma, const void* b
  *   variant EIGSOL_QR_FRANCIS (north_star; real matrices) — Hessenberg, then Francis multishift
  *     double-shift sweeps to quasi-triangular form with deflation at unit roundoff.  eig_re_or_c
  *     receives the real parts (= diag of the standardised real Schur form), eig_im (optional) the
- *     imaginary parts; iterations = sweeps performed; converged = 0 if a block stalled for
- *     max(30, maxIterations) sweeps.  Complex matrices use the unshifted variant.
+ *     imaginary parts; iterations = the most sweeps any single deflation needed (>= 1), and
+ *     converged = 0 when that exceeded maxIterations (so iterations <= maxIterations exactly when
+ *     converged, as in the reference).  Complex matrices use the unshifted variant.
  * n == 0: iterations 0, converged 1 (qr_eigenvalues.hpp:55-57). */
 #define EIGSOL_QR_FRANCIS 0
 #define EIGSOL_QR_UNSHIFTED 1

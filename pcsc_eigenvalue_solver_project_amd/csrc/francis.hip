@@ -255,15 +255,16 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     int sweeps = 0, failed = 0;
     int ihi = (int)n - 1;
     int stall = 0;               // sweeps on the current bottom block without a deflation
-    const int max_stall = std::max(30, maxits);
+    // `sweeps` tracks the largest number of sweeps any single deflation needed
+    const int max_stall = std::max(1, maxits);
     auto finish_small = [&](int l, int hi) -> int {
         const int m = hi - l + 1;
-        EIGSOL_TRY(hqr_lds(st, H + l + (int64_t)l * n, n, m, std::max(30, maxits), dwr + l, dwi + l, dinfo));
-        int info[2];
+        EIGSOL_TRY(hqr_lds(st, H + l + (int64_t)l * n, n, m, std::max(1, maxits), dwr + l, dwi + l, dinfo));
+        int info[3];
         EIGSOL_HIP(hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(hipStreamSynchronize(st));
         if (info[0]) failed = 1;
-        sweeps += info[1];
+        sweeps = std::max(sweeps, info[1]);
         return EIGSOL_OK;
     };
     while (rc == EIGSOL_OK && ihi >= 0) {
@@ -284,10 +285,11 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         if (N <= kSmall) {
             rc = finish_small(l, ihi);
             ihi = l - 1;
+            sweeps = std::max(sweeps, stall);
             stall = 0;
             continue;
         }
-        if (++stall > max_stall) { failed = 1; break; }
+        if (++stall > max_stall) { failed = 1; sweeps = std::max(sweeps, stall); break; }
         // shifts: eigenvalues of the trailing 2nb x 2nb block
         const int nb = std::min(dev::kMaxBulges, std::max(1, N / 8));
         const int ns = 2 * nb;
@@ -372,7 +374,6 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             t0 = t1;
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "francis: launch"); break; }
-        ++sweeps;
         // a deflation anywhere below resets the stall counter at the next scan
         hipLaunchKernelGGL(dev::diag_sub_kernel, dim3((ihi + 256) / 256), dim3(256), 0, st, H, n, ihi, dds);
         if (hipMemcpyAsync(ds.data(), dds, 2 * n * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -381,7 +382,11 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             break;
         }
         for (int k = ihi; k > l; --k)
-            if (std::fabs(ds[n + k]) <= eps * (std::fabs(ds[k - 1]) + std::fabs(ds[k]))) { stall = 0; break; }
+            if (std::fabs(ds[n + k]) <= eps * (std::fabs(ds[k - 1]) + std::fabs(ds[k]))) {
+                sweeps = std::max(sweeps, stall);
+                stall = 0;
+                break;
+            }
     }
     if (rc == EIGSOL_OK) {
         if (hipMemcpyAsync(wr, dwr, n * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -390,7 +395,9 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             rc = fail(EIGSOL_E_HIP, "francis: download");
     }
     for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo}) (void)hipFree(p);
-    *sweeps_out = sweeps;
+    // iterations reported: sweeps spent on the slowest deflation (>= 1, the final check), so that
+    // iterations <= maxIterations exactly when the iteration converged
+    *sweeps_out = std::max(1, sweeps);
     *fail_out = failed;
     return rc;
 }

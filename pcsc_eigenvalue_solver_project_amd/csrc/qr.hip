@@ -213,6 +213,7 @@ __global__ void diag_kernel(const S* H, int64_t n, S* d) {
 struct HqrCtl {
     int nn, l, m, its, stage, fail;
     int total;          // sweeps performed
+    int maxits;         // most sweeps any single deflation needed
     double t;           // accumulated exceptional shift
     double p, q, r, xs, ys, zs;
 };
@@ -240,6 +241,7 @@ __global__ __launch_bounds__(1024) void hqr_lds_kernel(const double* Hin, int64_
         c.t = 0.0;
         c.fail = 0;
         c.total = 0;
+        c.maxits = 0;
         c.its = 0;
     }
     __syncthreads();
@@ -259,7 +261,9 @@ __global__ __launch_bounds__(1024) void hqr_lds_kernel(const double* Hin, int64_
                 }
                 const double x = A(nn, nn);
                 if (l == nn) {
-                    wr[nn] = x + c.t; wi[nn] = 0.0; c.nn = nn - 1; c.its = 0;
+                    wr[nn] = x + c.t; wi[nn] = 0.0; c.nn = nn - 1;
+                    c.maxits = max(c.maxits, c.its);
+                    c.its = 0;
                     continue;
                 }
                 const double y = A(nn - 1, nn - 1);
@@ -280,6 +284,7 @@ __global__ __launch_bounds__(1024) void hqr_lds_kernel(const double* Hin, int64_
                         wi[nn] = z;
                     }
                     c.nn = nn - 2;
+                    c.maxits = max(c.maxits, c.its);
                     c.its = 0;
                     continue;
                 }
@@ -374,12 +379,14 @@ __global__ __launch_bounds__(1024) void hqr_lds_kernel(const double* Hin, int64_
             __syncthreads();
         }
     }
-    if (tid == 0) { info[0] = c.fail; info[1] = c.total; }
+    if (tid == 0) { info[0] = c.fail; info[1] = max(c.maxits, c.its); info[2] = c.total; }
 }
 
 }  // namespace dev
 
 // ============================================================================ host drivers
+int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n);
+
 namespace {
 
 template <class S>
@@ -428,6 +435,16 @@ int hessenberg_t(hipStream_t st, S* H, int64_t n, QrWork<S>& w) {
     return EIGSOL_OK;
 }
 
+// Real matrices of moderate size use the blocked (panel + GEMM) reduction (hessenberg.hip);
+// complex ones the per-reflector kernels above.
+template <class S>
+int hessenberg_dev(hipStream_t st, S* H, int64_t n, QrWork<S>& w) {
+    if constexpr (std::is_same_v<S, double>) {
+        if (n >= 64 && n <= 16384) return hessenberg_blocked_f64(st, H, n);
+    }
+    return hessenberg_t<S>(st, H, n, w);
+}
+
 // qr_decompose_dense (qr_decompose.hpp:46-85): R = A (m x n) in place, Q (m x m) = I then updated
 template <class S>
 int qr_decompose_t(hipStream_t st, S* R, int64_t m, int64_t n, S* Q, QrWork<S>& w) {
@@ -454,7 +471,7 @@ static int hessenberg_host(eigsol_ctx* ctx, int64_t n, const void* A, void* Hout
     int rc = work_alloc(w, n);
     if (rc == EIGSOL_OK && hipMemcpyAsync(H, A, n * n * sizeof(S), hipMemcpyHostToDevice, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "to_hessenberg: upload");
-    if (rc == EIGSOL_OK) rc = hessenberg_t<S>(st, H, n, w);
+    if (rc == EIGSOL_OK) rc = hessenberg_dev<S>(st, H, n, w);
     if (rc == EIGSOL_OK && hipMemcpyAsync(Hout, H, n * n * sizeof(S), hipMemcpyDeviceToHost, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "to_hessenberg: download");
     if (rc == EIGSOL_OK && hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "to_hessenberg: sync");
@@ -500,7 +517,7 @@ static int qr_unshifted_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_
     int rc = work_alloc(w, n);
     if (rc == EIGSOL_OK && hipMemcpyAsync(H, A, n * n * sizeof(S), hipMemcpyHostToDevice, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: upload");
-    if (rc == EIGSOL_OK) rc = hessenberg_t<S>(st, H, n, w);
+    if (rc == EIGSOL_OK) rc = hessenberg_dev<S>(st, H, n, w);
     int iter = 0;
     bool converged = false;
     const dim3 g((n + 63) / 64, (n + 63) / 64);
@@ -550,7 +567,7 @@ static int qr_francis_host(eigsol_ctx* ctx, int64_t n, const double* A, int max_
     int rc = work_alloc(w, n);
     if (rc == EIGSOL_OK && hipMemcpyAsync(H, A, n * n * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: upload");
-    if (rc == EIGSOL_OK) rc = hessenberg_t<double>(st, H, n, w);
+    if (rc == EIGSOL_OK) rc = hessenberg_dev<double>(st, H, n, w);
     int32_t sweeps = 0, failed = 0;
     if (rc == EIGSOL_OK) rc = francis_large_f64(ctx, H, n, max_iter, wr, wi, &sweeps, &failed);
     if (iters) *iters = sweeps;

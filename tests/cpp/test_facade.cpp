@@ -1,0 +1,334 @@
+// C++ façade tests: the reference's GoogleTest cases (test/*.cpp) restated against
+// <eigsol/eigsol.hpp> with a minimal harness (GoogleTest is not available in this image).
+// Each TEST names the reference case it restates.  Needs a gfx950 device at run time.
+#include <eigsol/eigsol.hpp>
+
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+static int g_fail = 0, g_checks = 0;
+static std::vector<std::pair<std::string, std::function<void()>>>& registry() {
+    static std::vector<std::pair<std::string, std::function<void()>>> r;
+    return r;
+}
+struct Reg {
+    Reg(const char* n, std::function<void()> f) { registry().emplace_back(n, std::move(f)); }
+};
+#define TEST(suite, name)                                   \
+    static void suite##_##name();                           \
+    static Reg reg_##suite##_##name(#suite "." #name, suite##_##name); \
+    static void suite##_##name()
+#define EXPECT_TRUE(c)                                                                   \
+    do {                                                                                 \
+        ++g_checks;                                                                      \
+        if (!(c)) { ++g_fail; std::printf("  FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); } \
+    } while (0)
+#define EXPECT_FALSE(c) EXPECT_TRUE(!(c))
+#define EXPECT_EQ(a, b) EXPECT_TRUE((a) == (b))
+#define EXPECT_GT(a, b) EXPECT_TRUE((a) > (b))
+#define EXPECT_GE(a, b) EXPECT_TRUE((a) >= (b))
+#define EXPECT_LE(a, b) EXPECT_TRUE((a) <= (b))
+#define EXPECT_NEAR(a, b, t) EXPECT_TRUE(std::abs((a) - (b)) <= (t))
+#define EXPECT_THROW(stmt, ex)                      \
+    do {                                            \
+        bool thrown_ = false;                       \
+        try { stmt; } catch (const ex&) { thrown_ = true; } catch (...) {} \
+        EXPECT_TRUE(thrown_);                       \
+    } while (0)
+#define EXPECT_NO_THROW(stmt)                       \
+    do {                                            \
+        bool ok_ = true;                            \
+        try { stmt; } catch (...) { ok_ = false; }  \
+        EXPECT_TRUE(ok_);                           \
+    } while (0)
+
+using DenseMat = EigSol::Matrix::Dense<double>;
+using SparseMat = EigSol::Matrix::Sparse<double>;
+using C = std::complex<double>;
+
+static_assert(!std::is_default_constructible_v<EigSol::Matrix>);
+static_assert(!std::is_copy_constructible_v<EigSol::Matrix>);
+static_assert(!std::is_copy_assignable_v<EigSol::Matrix>);
+static_assert(!std::is_move_constructible_v<EigSol::Matrix>);
+static_assert(!std::is_move_assignable_v<EigSol::Matrix>);
+
+// ---------------------------------------------------------------- matrix_wrapper_test.cpp
+TEST(MatrixWrapperTest, ConstructFromDense) {
+    DenseMat A(2, 2);
+    A << 1.0, 2.0, 3.0, 4.0;
+    EigSol::Matrix M(A);
+    EXPECT_TRUE(M.isDense());
+    EXPECT_TRUE(M.scalar_type() == typeid(double));
+    DenseMat& B = M.cast<DenseMat>();
+    EXPECT_EQ(B(0, 0), 1.0);
+    EXPECT_EQ(B(1, 1), 4.0);
+}
+TEST(MatrixWrapperTest, ConstructFromSparse) {
+    SparseMat S(3, 3);
+    S.insert(0, 0) = 5.0;
+    S.insert(1, 2) = 7.0;
+    EigSol::Matrix M(S);
+    EXPECT_FALSE(M.isDense());
+    SparseMat& T = M.cast<SparseMat>();
+    EXPECT_EQ(T.coeff(0, 0), 5.0);
+    EXPECT_EQ(T.coeff(1, 2), 7.0);
+}
+TEST(MatrixWrapperTest, ConstructFromStdVector) {
+    std::vector<double> v = {1, 2, 3, 4};
+    EigSol::Matrix M(v, 2, 2);
+    DenseMat& A = M.cast<DenseMat>();
+    EXPECT_EQ(A(0, 1), 2.0);
+    EXPECT_EQ(A(1, 0), 3.0);
+    EXPECT_THROW(EigSol::Matrix(v, 3, 2), std::runtime_error);
+}
+TEST(MatrixWrapperTest, CastAndTypeQueries) {
+    EigSol::Matrix M(DenseMat::Identity(3, 3));
+    EXPECT_THROW(M.cast<SparseMat>(), std::bad_cast);
+    EXPECT_NO_THROW(M.cast<DenseMat>());
+    EXPECT_TRUE(M.type() == typeid(DenseMat));
+}
+
+// ---------------------------------------------------------------- power_method_test.cpp
+TEST(PowerMethodTest, DenseSimpleMatrix) {
+    DenseMat A(2, 2);
+    A << 2.0, 0.0, 0.0, 1.0;
+    EigSol::Matrix M(A);
+    EigSol::SolverOptions opts;
+    opts.maxIterations = 1000;
+    opts.tolerance = 1e-10;
+    auto r = EigSol::powerMethod<double>(M, opts);
+    EXPECT_TRUE(r.converged);
+    EXPECT_GT(r.iterations, 0);
+    EXPECT_TRUE(EigSol::is_close_relative(2.0, r.eigenvalue, 1e-5));
+    auto lhs = A * r.eigenvector;
+    for (std::size_t i = 0; i < lhs.size(); ++i)
+        EXPECT_TRUE(EigSol::is_close_relative(lhs(i), r.eigenvalue * r.eigenvector(i), 1e-5));
+}
+TEST(PowerMethodTest, SparseMatrix) {
+    DenseMat Ad(2, 2);
+    Ad << 3.0, 1.0, 0.0, 2.0;
+    EigSol::Matrix M(SparseMat::fromDense(Ad));
+    EigSol::SolverOptions opts;
+    opts.tolerance = 1e-8;
+    auto r = EigSol::powerMethod<double>(M, opts);
+    EXPECT_TRUE(r.converged);
+    EXPECT_TRUE(EigSol::is_close_relative(3.0, r.eigenvalue, 1e-6));
+}
+TEST(PowerMethodTest, ErrorsAndFewIterations) {
+    EigSol::Matrix N(DenseMat(2, 3));
+    EXPECT_THROW(EigSol::powerMethod<double>(N), std::runtime_error);
+    EigSol::Matrix Z(DenseMat(0, 0));
+    EXPECT_THROW(EigSol::powerMethod<double>(Z), std::runtime_error);
+    EXPECT_THROW(EigSol::powerMethod<C>(EigSol::Matrix(DenseMat::Identity(2, 2))), std::runtime_error);
+    DenseMat A(2, 2);
+    A << 5.0, 1.0, 1.0, 4.0;
+    EigSol::Matrix M(A);
+    EigSol::SolverOptions opts;
+    opts.maxIterations = 1;
+    opts.tolerance = 1e-12;
+    auto r = EigSol::powerMethod<double>(M, opts);
+    EXPECT_EQ(r.iterations, opts.maxIterations);
+    try {
+        EigSol::powerMethod<double>(N);
+    } catch (const std::runtime_error& e) {
+        EXPECT_EQ(std::string(e.what()), std::string("powerMethod: matrix must be square"));
+    }
+}
+TEST(PowerMethodTest, DataFileAsDouble) {
+    // main.cpp reads data/A.txt (complex layout) as double: dominant eigenvalue 1 + sqrt(15)
+    EigSol::Matrix A = EigSol::readMatrixFromFile<double>(EIGSOL_TEST_DATA "/A.txt");
+    EigSol::SolverOptions opts;
+    auto r = EigSol::powerMethod<double>(A, opts);
+    EXPECT_TRUE(r.converged);
+    EXPECT_NEAR(r.eigenvalue, 1.0 + std::sqrt(15.0), 1e-8);
+    EXPECT_THROW(EigSol::readMatrixFromFile<double>(EIGSOL_TEST_DATA "/B.txt"), std::runtime_error);
+    EigSol::Matrix B = EigSol::readMatrixFromFile<C>(EIGSOL_TEST_DATA "/B.txt");
+    EXPECT_FALSE(B.isDense());
+    EigSol::ShiftedSolverOptions<C> so(C(2.3, 0.0));
+    auto rs = EigSol::shiftedInversePowerMethod<C>(B, so);
+    EXPECT_TRUE(rs.converged);
+    EXPECT_NEAR(std::abs(rs.eigenvalue - C(3, 2)), 0.0, 1e-6);
+}
+
+// ---------------------------------------------------------------- shifted_inverse_power_method_test.cpp
+TEST(ShiftedInversePowerMethodTest, DenseShifts) {
+    DenseMat A(2, 2);
+    A << 2.0, 0.0, 0.0, 5.0;
+    EigSol::Matrix M(A);
+    for (double sh : {1.9, 4.9}) {
+        EigSol::ShiftedSolverOptions<double> opts;
+        opts.shift = sh;
+        opts.maxIterations = 1000;
+        opts.tolerance = 1e-10;
+        auto r = EigSol::shiftedInversePowerMethod<double>(M, opts);
+        EXPECT_TRUE(r.converged);
+        EXPECT_GT(r.iterations, 0);
+        EXPECT_TRUE(EigSol::is_close_relative(sh < 3 ? 2.0 : 5.0, r.eigenvalue, 1e-5));
+    }
+}
+TEST(ShiftedInversePowerMethodTest, SparseMatrixAndErrors) {
+    DenseMat Ad = DenseMat::Zero(3, 3);
+    Ad(0, 0) = 1.0;
+    Ad(1, 1) = 3.0;
+    Ad(2, 2) = 10.0;
+    EigSol::Matrix M(SparseMat::fromDense(Ad));
+    EigSol::ShiftedSolverOptions<double> opts(2.9, 1000, 1e-8);
+    auto r = EigSol::shiftedInversePowerMethod<double>(M, opts);
+    EXPECT_TRUE(r.converged);
+    EXPECT_TRUE(EigSol::is_close_relative(3.0, r.eigenvalue, 1e-5));
+    EXPECT_THROW(EigSol::shiftedInversePowerMethod<double>(EigSol::Matrix(DenseMat(2, 3)), opts), std::runtime_error);
+    EXPECT_THROW(EigSol::shiftedInversePowerMethod<double>(EigSol::Matrix(DenseMat(0, 0)), opts), std::runtime_error);
+    DenseMat B(2, 2);
+    B << 5.0, 1.0, 1.0, 4.0;
+    EigSol::ShiftedSolverOptions<double> o1(4.0, 1, 1e-12);
+    EXPECT_EQ(EigSol::shiftedInversePowerMethod<double>(EigSol::Matrix(B), o1).iterations, 1);
+}
+
+// ---------------------------------------------------------------- solve_shifted_test.cpp
+TEST(SolveShiftedLinearSystem, DenseAndSparse) {
+    EigSol::Vector<double> b(3);
+    b << 1.0, -2.0, 3.0;
+    auto x = EigSol::solve_shifted<double>(EigSol::Matrix(DenseMat::Identity(3, 3)), 2.0, b);
+    for (int i = 0; i < 3; ++i) EXPECT_NEAR(x(i), -b(i), 1e-12);
+    SparseMat S(3, 3);
+    S.setIdentity();
+    auto xs = EigSol::solve_shifted<double>(EigSol::Matrix(S), 2.0, b);
+    for (int i = 0; i < 3; ++i) EXPECT_NEAR(xs(i), -b(i), 1e-12);
+    DenseMat A(2, 2);
+    A << 3.0, 1.0, 0.0, 4.0;
+    EigSol::Vector<double> b2(2);
+    b2 << 2.0, -1.0;
+    auto x2 = EigSol::solve_shifted<double>(EigSol::Matrix(A), 1.5, b2);
+    DenseMat Ms = A - 1.5 * DenseMat::Identity(2, 2);
+    auto res = Ms * x2 - b2;
+    EXPECT_NEAR(res.norm(), 0.0, 1e-10);
+}
+TEST(SolveShiftedLinearSystem, ComplexAndErrors) {
+    EigSol::Matrix::Dense<C> A(2, 2);
+    A << C(1, 1), C(2, -1), C(0.5, 0), C(3, 2);
+    const C lam(0.7, -0.3);
+    EigSol::Vector<C> b(2);
+    b << C(1, 0), C(-2, 1);
+    auto x = EigSol::solve_shifted<C>(EigSol::Matrix(A), lam, b);
+    auto M = A - lam * EigSol::Matrix::Dense<C>::Identity(2, 2);
+    EXPECT_NEAR((M * x - b).norm(), 0.0, 1e-10);
+    EigSol::Vector<double> ones(2);
+    ones << 1.0, 1.0;
+    DenseMat R(2, 3);
+    EXPECT_THROW(EigSol::solve_shifted<double>(EigSol::Matrix(R), 1.0, ones), std::runtime_error);
+    SparseMat S23(2, 3);
+    S23.insert(0, 0) = 1.0;
+    S23.insert(1, 2) = 2.0;
+    EXPECT_THROW(EigSol::solve_shifted<double>(EigSol::Matrix(S23), 0.5, ones), std::runtime_error);
+    EXPECT_THROW(EigSol::solve_shifted<double>(EigSol::Matrix(DenseMat::Identity(3, 3)), 1.0, ones), std::runtime_error);
+    DenseMat Rr(2, 2);
+    Rr << 1.0, 2.0, 3.0, 4.0;
+    EigSol::Vector<C> bc(2);
+    EXPECT_THROW(EigSol::solve_shifted<C>(EigSol::Matrix(Rr), C(1, 0), bc), std::runtime_error);
+}
+
+// ---------------------------------------------------------------- qr_algorithms_test.cpp
+TEST(ToHessenbergDenseTest, RealAndComplex) {
+    DenseMat A(3, 3);
+    A << 4.0, 1.0, -2.0, 1.0, 3.0, 0.0, 2.0, 1.0, 1.0;
+    DenseMat H = EigSol::to_hessenberg_dense<double>(A);
+    EXPECT_NEAR(H(2, 0), 0.0, 1e-12);
+    EXPECT_NEAR(H(1, 0), -2.2360679774997902, 1e-12);
+    EXPECT_NEAR(H(0, 1), 1.3416407864998736, 1e-12);
+    DenseMat H2 = EigSol::to_hessenberg<double>(EigSol::Matrix(A));
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) EXPECT_NEAR(H(i, j), H2(i, j), 1e-10);
+    EigSol::Matrix::Dense<C> Ac(3, 3);
+    Ac << C(4, 1), C(1, 0), C(-2, 2), C(1, 0), C(3, -1), C(0, 1), C(2, 0), C(1, 2), C(1, 0);
+    auto Hc = EigSol::to_hessenberg_dense<C>(Ac);
+    EXPECT_NEAR(std::abs(Hc(2, 0)), 0.0, 1e-12);
+    EXPECT_THROW(EigSol::to_hessenberg_dense<double>(DenseMat(2, 3)), std::runtime_error);
+    SparseMat S(2, 2);
+    S.setIdentity();
+    EXPECT_THROW(EigSol::to_hessenberg<double>(EigSol::Matrix(S)), std::runtime_error);
+}
+TEST(QRDecomposeDenseTest, RealRectangularAndComplex) {
+    DenseMat A(3, 2);
+    A << 1.0, 2.0, 3.0, 4.0, 5.0, 6.0;
+    DenseMat Q, R;
+    EigSol::qr_decompose_dense<double>(A, Q, R);
+    EXPECT_EQ(Q.rows(), 3);
+    EXPECT_EQ(Q.cols(), 3);
+    EXPECT_EQ(R.rows(), 3);
+    EXPECT_EQ(R.cols(), 2);
+    DenseMat QR = Q * R;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 2; ++j) EXPECT_NEAR(QR(i, j), A(i, j), 1e-10);
+    DenseMat QtQ = Q.adjoint() * Q;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) EXPECT_NEAR(QtQ(i, j), i == j ? 1.0 : 0.0, 1e-10);
+    EXPECT_NEAR(R(0, 0), -5.916079783099616, 1e-12);
+    auto [Q2, R2] = EigSol::qr_decompose<double>(EigSol::Matrix(A));
+    EXPECT_NEAR(Q2(2, 0), Q(2, 0), 1e-12);
+    EigSol::Matrix::Dense<C> B(2, 2);
+    B << C(1, 1), C(2, -1), C(0.5, 0), C(3, 2);
+    EigSol::Matrix::Dense<C> Qc, Rc;
+    EigSol::qr_decompose_dense<C>(B, Qc, Rc);
+    auto QRc = Qc * Rc;
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) EXPECT_NEAR(std::abs(QRc(i, j) - B(i, j)), 0.0, 1e-10);
+    EXPECT_NEAR(std::abs(Rc(1, 0)), 0.0, 1e-10);
+    DenseMat E0(0, 0), q, r;
+    EXPECT_THROW(EigSol::qr_decompose_dense<double>(E0, q, r), std::runtime_error);
+}
+TEST(QREigenvaluesDenseTest, Real2x2BothVariantsAndComplex) {
+    DenseMat A(2, 2);
+    A << 2.0, 1.0, 1.0, 2.0;
+    EigSol::SolverOptions opts;
+    opts.maxIterations = 1000;
+    opts.tolerance = 1e-12;
+    for (auto v : {EigSol::QRVariant::Francis, EigSol::QRVariant::Unshifted}) {
+        auto r = EigSol::qr_eigenvalues_dense<double>(A, opts, v);
+        EXPECT_TRUE(r.converged);
+        EXPECT_EQ(r.eigenvalues.size(), 2u);
+        EXPECT_GE(r.iterations, 1);
+        EXPECT_LE(r.iterations, opts.maxIterations);
+        const double hi = std::max(r.eigenvalues(0), r.eigenvalues(1));
+        const double lo = std::min(r.eigenvalues(0), r.eigenvalues(1));
+        EXPECT_NEAR(hi, 3.0, 1e-8);
+        EXPECT_NEAR(lo, 1.0, 1e-8);
+    }
+    // reference algorithm: 25 iterations at 1e-12 (golden)
+    EXPECT_EQ(EigSol::qr_eigenvalues_dense<double>(A, opts, EigSol::QRVariant::Unshifted).iterations, 25);
+    auto r2 = EigSol::qr_eigenvalues<double>(EigSol::Matrix(A), opts);
+    EXPECT_EQ(r2.eigenvalues.size(), 2u);
+    EigSol::Matrix::Dense<C> Ac(2, 2);
+    Ac << C(2, 0), C(1, 0), C(1, 0), C(2, 0);
+    auto rc = EigSol::qr_eigenvalues_dense<C>(Ac, opts);
+    EXPECT_TRUE(rc.converged);
+    const double hc = std::max(rc.eigenvalues(0).real(), rc.eigenvalues(1).real());
+    EXPECT_NEAR(hc, 3.0, 1e-8);
+    EXPECT_THROW(EigSol::qr_eigenvalues_dense<double>(DenseMat(2, 3), opts), std::runtime_error);
+    // complex-conjugate pair reported through eigenvalues_complex
+    DenseMat Rot(2, 2);
+    Rot << 0.0, -1.0, 1.0, 0.0;
+    auto rr = EigSol::qr_eigenvalues_dense<double>(Rot, opts);
+    EXPECT_TRUE(rr.converged);
+    EXPECT_NEAR(std::abs(std::abs(rr.eigenvalues_complex[0].imag()) - 1.0), 0.0, 1e-12);
+}
+
+int main() {
+    for (auto& [name, fn] : registry()) {
+        const int before = g_fail;
+        try {
+            fn();
+        } catch (const std::exception& e) {
+            ++g_fail;
+            std::printf("  FAIL %s: unexpected exception: %s\n", name.c_str(), e.what());
+        }
+        std::printf("%s %s\n", g_fail == before ? "[ OK ]" : "[FAIL]", name.c_str());
+    }
+    std::printf("%d checks, %d failures\n", g_checks, g_fail);
+    if (g_fail == 0) std::printf("ALL PASSED\n");
+    return g_fail == 0 ? 0 : 1;
+}

@@ -1,0 +1,14 @@
+"""CPU: the C++ drop-in façade (include/eigsol/*.hpp) compiles with -Wall -Wextra -Werror and
+links against libeigsol_hip.so; the reference-style test program builds (it runs under -m gpu)."""
+import os
+
+import pytest
+
+from cpp_build import ROOT, build
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "pcsc_eigenvalue_solver_project_amd", "libeigsol_hip.so")),
+                    reason="library not built")
+def test_facade_compiles_and_links(tmp_path):
+    out = build(os.path.join(ROOT, "tests", "cpp", "test_facade.cpp"), str(tmp_path / "test_facade"))
+    assert os.path.getsize(out) > 0
