@@ -66,6 +66,7 @@ template <class S>
 struct CsrArgs {
     const int32_t* rowptr;
     const int32_t* col;
+    const uint16_t* col16;   // windowed matrices: column - tile window start (< kWin)
     const S* val;
     const int4* tile_meta;   // per tile {r0, r1, e0, e1}: short tiles first, then long rows
     const int2* tile_win;    // per short tile: x window [w0, w1] covering its columns and rows
@@ -430,12 +431,101 @@ __device__ __forceinline__ void win_products(const TileRegs<S>& R, int4 m, int w
     }
 }
 
+// Windowed tiles stream 16-bit window-relative column offsets instead of int32 columns: 10 bytes
+// per nonzero instead of 12 for f64 (the windows are at most kWin = 512 wide by construction).
+// Algorithmic bytes are still counted for the int32 CSR layout; the PMC traffic
+// in profiles/ shows the bytes actually moved.
+template <class S> struct WSlot;
+template <> struct WSlot<double> {
+    static constexpr int kNnz = 2;
+    double2 v;
+    uint32_t c;     // two 16-bit offsets
+};
+template <> struct WSlot<cplx> {
+    static constexpr int kNnz = 1;
+    cplx v;
+    uint32_t c;     // one 16-bit offset
+};
+template <class S>
+struct WTileRegs {
+    static constexpr int P = Tile<S>::kNnz / (WSlot<S>::kNnz * kThreads);
+    WSlot<S> s[P];
+    int rp0, rp1;
+};
+
+template <class S>
+__device__ __forceinline__ void load_tile_w(const CsrArgs<S>& a, int4 m, WTileRegs<S>& R) {
+    constexpr int P = WTileRegs<S>::P;
+    const int tid = threadIdx.x;
+    if constexpr (std::is_same_v<S, double>) {
+        const int q0 = m.z & ~1;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const uint32_t q = (uint32_t)(q0 + 2 * (tid + p * kThreads));
+            R.s[p].v = ldg(reinterpret_cast<const double2*>(a.val), q >> 1);
+            R.s[p].c = ldg(reinterpret_cast<const uint32_t*>(a.col16), q >> 1);
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const uint32_t q = (uint32_t)(m.z + tid + p * kThreads);
+            R.s[p].v = ldg(a.val, q);
+            R.s[p].c = ldg(a.col16, q);
+        }
+    }
+    const uint32_t r = (uint32_t)min(m.x + tid, a.nrows - 1);
+    R.rp0 = ldg(a.rowptr, r);
+    R.rp1 = ldg(a.rowptr, r + 1);
+}
+
+// LDS product index of the windowed kernel: f64 products are written as 16-byte pairs, so the
+// padding (one pair per 32 products, which spreads the lane-per-row reads over the banks) keeps
+// every pair 16-byte aligned; complex products are 16 bytes each.
+template <class S>
+__device__ __forceinline__ int wlds(int k) {
+    if constexpr (std::is_same_v<S, double>) return k + 2 * (k >> 5);
+    else return k + (k >> 5);
+}
+template <class S>
+__device__ __forceinline__ int wbase(int4 m) {
+    return std::is_same_v<S, double> ? (m.z & ~1) : m.z;   // stream index of LDS product slot 0
+}
+
+// Products of a short tile with x from the LDS window, written unconditionally: slots outside the
+// tile's [e0, e1) (the pair partner before e0, the stream beyond e1) hold products no row sum
+// reads, and every 16-bit offset in the stream is a valid window index (< kWin) by construction.
+template <class S>
+__device__ __forceinline__ void win_products_w(const WTileRegs<S>& R, int4 m, const S* xw, S* prod) {
+    constexpr int P = WTileRegs<S>::P;
+    constexpr int NPS = WSlot<S>::kNnz;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int k = NPS * (tid + p * kThreads);   // slot of this lane's first product
+        if constexpr (std::is_same_v<S, double>) {
+            const double x0 = xw[R.s[p].c & 0xffffu];
+            const double x1 = xw[R.s[p].c >> 16];
+            *reinterpret_cast<double2*>(prod + wlds<S>(k)) = make_double2(R.s[p].v.x * x0, R.s[p].v.y * x1);
+        } else {
+            prod[wlds<S>(k)] = mul(R.s[p].v, xw[R.s[p].c]);
+        }
+    }
+    (void)m;
+}
+
+template <class S>
+__device__ __forceinline__ S row_sum_w(const S* pb, int k0, int k1) {
+    S sacc = s_zero<S>();
+    for (int k = k0; k < k1; ++k) sacc = add(sacc, pb[wlds<S>(k)]);
+    return sacc;
+}
+
 template <class S, bool kPower>
 __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int parity) {
     constexpr int TN = Tile<S>::kNnz;
-    constexpr int LDSN = TN + TN / 32;
+    constexpr int LDSN = TN + (std::is_same_v<S, double> ? 2 : 1) * (TN / 32);
     constexpr int KW = Win<S>::kWin;
-    __shared__ S prod[LDSN];
+    __shared__ __align__(16) S prod[LDSN];
     __shared__ S xwin[2][KW];
     __shared__ int2 rows[kThreads];
     __shared__ double sm[3 * kWaves];
@@ -475,33 +565,34 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
         int2 wn = ld_uniform(a.tile_win, min(tn, last));
         int4 m2 = ld_uniform(a.tile_meta, min(tn + nb, last));
         int2 w2 = ld_uniform(a.tile_win, min(tn + nb, last));
-        TileRegs<S> Ra, Rb;
+        WTileRegs<S> Ra, Rb;
         WinRegs<S> Wa, Wb;
-        load_tile(a, mc, Rb);
+        load_tile_w(a, mc, Rb);
         load_window(xin, wc, a.xlen, Wb);
-        load_tile(a, mn, Ra);
+        load_tile_w(a, mn, Ra);
         load_window(xin, wn, a.xlen, Wa);
         int b = 0;
         store_window<S, kPower>(Wb, nrm, xwin[0]);
         __syncthreads();
-        win_products(Rb, mc, wc.x, xwin[0], prod, LDSN - 1);
+        win_products_w(Rb, mc, xwin[0], prod);
         rows[tid] = make_int2(Rb.rp0, Rb.rp1);
         __syncthreads();
 
         // step i: Rnx/Wnx = tile i+1 (in flight since step i-1), Rld/Wld <- tile i+2.  Unrolled
         // by two with the register sets swapping roles, so the prefetch is never copied (a copy
         // would force its wait).
-        auto step = [&](TileRegs<S>& Rnx, WinRegs<S>& Wnx, TileRegs<S>& Rld, WinRegs<S>& Wld) -> bool {
+        auto step = [&](WTileRegs<S>& Rnx, WinRegs<S>& Wnx, WTileRegs<S>& Rld, WinRegs<S>& Wld) -> bool {
             const int t3 = tn + 2 * nb;
             const int4 m3 = ld_uniform(a.tile_meta, min(t3, last));
             const int2 w3 = ld_uniform(a.tile_win, min(t3, last));
-            load_tile(a, m2, Rld);
+            load_tile_w(a, m2, Rld);
             load_window(xin, w2, a.xlen, Wld);
             store_window<S, kPower>(Wnx, nrm, xwin[b ^ 1]);   // unconditional: no branch around the wait
             // row sums of the current tile (x_i for the Rayleigh term from the scaled window)
             if (tid < mc.y - mc.x) {
                 const int2 rp = rows[tid];
-                const S sacc = row_sum<S>(prod, rp.x - mc.z, rp.y - mc.z);
+                const int qb = wbase<S>(mc);
+                const S sacc = row_sum_w<S>(prod, rp.x - qb, rp.y - qb);
                 yout[mc.x + tid] = sacc;
                 if constexpr (kPower) {
                     const S xi = xwin[b][mc.x + a.xoff + tid - wc.x];
@@ -513,7 +604,7 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
             __builtin_amdgcn_sched_barrier(0);
             __syncthreads();
             __builtin_amdgcn_sched_barrier(0);
-            win_products(Rnx, mn, wn.x, xwin[b ^ 1], prod, LDSN - 1);
+            win_products_w(Rnx, mn, xwin[b ^ 1], prod);
             rows[tid] = make_int2(Rnx.rp0, Rnx.rp1);
             __builtin_amdgcn_sched_barrier(0);
             __syncthreads();
@@ -580,6 +671,7 @@ void csr_release(eigsol_csr* A) {
     (void)hipStreamSynchronize(A->ctx->stream);
     if (A->rowptr) (void)hipFree(A->rowptr);
     if (A->col) (void)hipFree(A->col);
+    if (A->col16) (void)hipFree(A->col16);
     if (A->val) (void)hipFree(A->val);
     if (A->tile_meta) (void)hipFree(A->tile_meta);
     if (A->tile_win) (void)hipFree(A->tile_win);
@@ -727,6 +819,20 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
         cleanup();
         return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: upload: ") + hipGetErrorString(e));
     }
+    if (windowed) {
+        // 16-bit window-relative columns of the short tiles (long rows keep using int32 columns)
+        std::vector<uint16_t> c16((size_t)(nnz + pad), 0);
+        for (int32_t t = 0; t < nshort; ++t) {
+            const int32_t w0 = win[2 * t];
+            for (int32_t k = meta[4 * t + 2]; k < meta[4 * t + 3]; ++k) c16[k] = (uint16_t)(col_use[k] - w0);
+        }
+        if ((e = hipMalloc(&A->col16, c16.size() * sizeof(uint16_t))) != hipSuccess ||
+            (e = hipMemcpyAsync(A->col16, c16.data(), c16.size() * sizeof(uint16_t), hipMemcpyHostToDevice, s)) != hipSuccess ||
+            (e = hipStreamSynchronize(s)) != hipSuccess) {
+            cleanup();
+            return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: upload: ") + hipGetErrorString(e));
+        }
+    }
     *out = A;
     return EIGSOL_OK;
 }
@@ -784,6 +890,7 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     CsrArgs<S> a{};
     a.rowptr = A->rowptr;
     a.col = A->col;
+    a.col16 = A->col16;
     a.val = (const S*)A->val;
     a.tile_meta = (const int4*)A->tile_meta;
     a.tile_win = (const int2*)A->tile_win;

@@ -178,6 +178,7 @@ struct eigsol_csr {
     int64_t nrows = 0, ncols = 0, nnz = 0;
     int32_t* rowptr = nullptr;     // device, nrows+1
     int32_t* col = nullptr;        // device, nnz (+pad)
+    uint16_t* col16 = nullptr;     // device, nnz (+pad): windowed tiles' column - window start
     void* val = nullptr;           // device, nnz (+pad)
     int32_t* tile_meta = nullptr;  // device, 4 ints per row tile: {r0, r1, e0, e1}
     int32_t* tile_win = nullptr;   // device, 2 ints per short tile: x window [w0, w1]
