@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libeigsol_hip.so")
+LIB_PATH = os.environ.get("EIGSOL_LIB_PATH") or os.path.join(_HERE, "libeigsol_hip.so")   # override: A/B builds
 
 EIGSOL_OK = 0
 EIGSOL_E_NOT_SQUARE = 1

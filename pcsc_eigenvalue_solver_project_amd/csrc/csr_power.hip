@@ -481,9 +481,12 @@ __device__ __forceinline__ void load_tile_w(const CsrArgs<S>& a, int4 m, WTileRe
 // LDS product index of the windowed kernel: f64 products are written as 16-byte pairs, so the
 // padding (one pair per 32 products, which spreads the lane-per-row reads over the banks) keeps
 // every pair 16-byte aligned; complex products are 16 bytes each.
+#ifndef EIGSOL_WPAD_SHIFT
+#define EIGSOL_WPAD_SHIFT 5
+#endif
 template <class S>
 __device__ __forceinline__ int wlds(int k) {
-    if constexpr (std::is_same_v<S, double>) return k + 2 * (k >> 5);
+    if constexpr (std::is_same_v<S, double>) return k + 2 * (k >> EIGSOL_WPAD_SHIFT);
     else return k + (k >> 5);
 }
 template <class S>
@@ -523,7 +526,7 @@ __device__ __forceinline__ S row_sum_w(const S* pb, int k0, int k1) {
 template <class S, bool kPower>
 __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int parity) {
     constexpr int TN = Tile<S>::kNnz;
-    constexpr int LDSN = TN + (std::is_same_v<S, double> ? 2 : 1) * (TN / 32);
+    constexpr int LDSN = TN + (std::is_same_v<S, double> ? 2 * (TN >> EIGSOL_WPAD_SHIFT) : TN / 32);
     constexpr int KW = Win<S>::kWin;
     __shared__ __align__(16) S prod[LDSN];
     __shared__ S xwin[2][KW];
