@@ -136,7 +136,7 @@ def run_config3(E, S, ctx, torch, stream, opts):
 def run_config2(E, ctx, no_cpu):
     """BASELINE config 2: 4096^2 N(0,1) (seed 20251226), Hessenberg + Francis multishift QR."""
     n = 4096
-    A = np.random.default_rng(20251226).standard_normal((n, n))
+    A = np.asfortranarray(np.random.default_rng(20251226).standard_normal((n, n)))   # column-major, like Matrix::Dense
     E.qr_eigenvalues(ctx, A[:256, :256].copy())          # warm-up (module load)
     t = time.perf_counter()
     r = E.qr_eigenvalues(ctx, A)

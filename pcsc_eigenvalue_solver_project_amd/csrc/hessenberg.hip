@@ -11,6 +11,7 @@
 // ||x(1:)|| == 0), so H matches the unblocked reduction to rounding.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "kernels_common.hpp"
@@ -184,17 +185,258 @@ __global__ __launch_bounds__(256) void hess_y(int n, int i, int nch, const doubl
     }
 }
 
+// ------------------------------------------------------------------ cooperative panel (one launch)
+// The whole panel (32 columns) in ONE cooperative launch of kCoopBlocks co-resident blocks; block
+// b owns rows [b R, (b+1) R).  Per column, three grid barriers separate
+//   P1  right update of column j (own rows, kept in LDS) + partials of V^T a
+//   P2  w = T^T (sum of partials); left update; partial of ||a(j+2:)||^2; x0 = a(j+1)
+//   P3  reflector (every block, redundantly, from the reduced scalars); v and the reduced column
+//       for own rows; partials of t = V^T v
+//   P4  GEMV y = A(:, j+1:n) v for own rows (v staged in LDS), Y(:, i) and the T column
+// (P4 -> the next P1 needs no barrier: P1 reads only own rows and V(j+1, 0:i), published in P3).
+// Everything another block reads is written with agent-scope (sc1) stores and read with sc1 loads,
+// so no L2 writeback/invalidate is needed; partial sums are combined in block order
+// (deterministic).  The barrier spins are bounded: on expiry the kernel sets an error word and
+// drains (the host then reports EIGSOL_E_HIP).
+constexpr int kCoopBlocks = 64;
+constexpr int kCoopThreads = 1024;
+constexpr int kCoopMaxN = 8192;          // v in LDS (64 KiB) and at most 2 rows per lane
+constexpr int kCoopRowsPerLane = 2;
+
+struct CoopArgs {
+    double* A;
+    int n, k, nbp;
+    double* V;
+    double* Y;
+    double* T;
+    double* part;       // [G][kPanel]
+    double* tpart;      // [G]
+    double* x0;         // a(j+1)
+    unsigned* bar;      // barrier counter (zeroed by the host before the launch)
+    int* err;
+};
+
+__device__ __forceinline__ unsigned ld_agent_u32(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned& target, int* err) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's sc1 stores are complete
+    __syncthreads();
+    target += gridDim.x;
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int spins = 0;
+        while (ld_agent_u32(bar) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1 << 24)) { atomicOr(err, 1); break; }
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
+    extern __shared__ double vsh[];          // v (n doubles) for the GEMV
+    __shared__ double xs[kCoopRowsPerLane * 64];    // own rows of the current column
+    __shared__ double ysum[16][kCoopRowsPerLane * 64];
+    __shared__ double red[16 * kPanel];
+    __shared__ double sv[kPanel], sw[kPanel], st[kPanel];
+    __shared__ double s_scal[4];
+    const int n = a.n, k = a.k;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int G = gridDim.x;
+    const int R = (n + G - 1) / G;
+    const int r0 = blockIdx.x * R, r1 = min(n, r0 + R);
+    unsigned target = 0;
+    for (int i = 0; i < a.nbp; ++i) {
+        const int j = k + i;
+        // ---------------- P1
+        if (tid < i) sv[tid] = ld_agent(&a.V[j + (int64_t)tid * n]);
+        __syncthreads();
+        if (wv == 0)
+            for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                const int r = r0 + lane + 64 * q;
+                if (r < r1) {
+                    double x = a.A[r + (int64_t)j * n];
+                    for (int c = 0; c < i; ++c) x -= a.Y[r + (int64_t)c * n] * sv[c];
+                    xs[lane + 64 * q] = x;
+                }
+            }
+        __syncthreads();
+        // partials of w_c = sum_{r >= k+1} V(r, c) x(r): wave wv handles c = wv, wv + 16
+        for (int c = wv; c < i; c += 16) {
+            double p = 0.0;
+            for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                const int r = r0 + lane + 64 * q;
+                if (r < r1 && r >= k + 1) p += a.V[r + (int64_t)c * n] * xs[lane + 64 * q];
+            }
+            p = wave_sum(p);
+            if (lane == 0) st_agent(&a.part[blockIdx.x * kPanel + c], p);
+        }
+        grid_barrier(a.bar, target, a.err);
+        // ---------------- P2
+        if (tid < i) {
+            double w = 0.0;
+            for (int b = 0; b < G; ++b) w += ld_agent(&a.part[b * kPanel + tid]);
+            sw[tid] = w;
+        }
+        __syncthreads();
+        if (tid < i) {
+            double s = 0.0;
+            for (int c = 0; c <= tid; ++c) s += ld_agent(&a.T[c + tid * kPanel]) * sw[c];   // (T^T w)_tid
+            st[tid] = s;
+        }
+        __syncthreads();
+        double tl = 0.0;
+        if (wv == 0)
+            for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                const int r = r0 + lane + 64 * q;
+                if (r < r1) {
+                    double x = xs[lane + 64 * q];
+                    if (r >= k + 1)
+                        for (int c = 0; c < i; ++c) x -= a.V[r + (int64_t)c * n] * st[c];
+                    xs[lane + 64 * q] = x;
+                    if (r >= j + 2) tl += x * x;
+                    if (r == j + 1) st_agent(a.x0, x);
+                }
+            }
+        if (wv == 0) {
+            tl = wave_sum(tl);
+            if (lane == 0) st_agent(&a.tpart[blockIdx.x], tl);
+        }
+        grid_barrier(a.bar, target, a.err);
+        // ---------------- P3
+        if (tid == 0) {
+            double tail = 0.0;
+            for (int b = 0; b < G; ++b) tail += ld_agent(&a.tpart[b]);
+            const double x0 = ld_agent(a.x0);
+            double sk = tail == 0.0 ? 1.0 : 0.0, v0 = 0.0, rv = 0.0, alpha = 0.0;
+            if (sk == 0.0) {
+                const double nx = sqrt(tail + x0 * x0);
+                const double sign = x0 == 0.0 ? 1.0 : (x0 > 0.0 ? 1.0 : -1.0);
+                alpha = -sign * nx;
+                v0 = x0 - alpha;
+                const double vn = sqrt(tail + v0 * v0);
+                if (vn == 0.0) sk = 1.0;
+                else rv = 1.0 / vn;
+            }
+            s_scal[0] = sk; s_scal[1] = v0; s_scal[2] = rv; s_scal[3] = alpha;
+        }
+        __syncthreads();
+        const bool sk = s_scal[0] != 0.0;
+        const double v0 = s_scal[1], rv = s_scal[2], alpha = s_scal[3];
+        if (wv == 0)
+            for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                const int r = r0 + lane + 64 * q;
+                if (r < r1) {
+                    const double x = xs[lane + 64 * q];
+                    double v = 0.0;
+                    if (!sk && r > j) v = (r == j + 1 ? v0 : x) * rv;
+                    st_agent(&a.V[r + (int64_t)i * n], v);
+                    xs[lane + 64 * q] = v;           // keep v for the t partials
+                    double red_col = x;
+                    if (!sk && r == j + 1) red_col = alpha;
+                    if (!sk && r > j + 1) red_col = 0.0;
+                    a.A[r + (int64_t)j * n] = red_col;
+                }
+            }
+        __syncthreads();
+        for (int c = wv; c < i; c += 16) {
+            double p = 0.0;
+            for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                const int r = r0 + lane + 64 * q;
+                if (r < r1) p += a.V[r + (int64_t)c * n] * xs[lane + 64 * q];
+            }
+            p = wave_sum(p);
+            if (lane == 0) st_agent(&a.part[blockIdx.x * kPanel + c], p);
+        }
+        grid_barrier(a.bar, target, a.err);
+        // ---------------- P4
+        for (int r = tid; r < n; r += kCoopThreads) vsh[r] = sk ? 0.0 : ld_agent(&a.V[r + (int64_t)i * n]);
+        if (tid < i) {
+            double t = 0.0;
+            for (int b = 0; b < G; ++b) t += ld_agent(&a.part[b * kPanel + tid]);
+            sv[tid] = sk ? 0.0 : t;
+        }
+        __syncthreads();
+        double yacc[kCoopRowsPerLane];
+#pragma unroll
+        for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] = 0.0;
+        if (!sk) {
+            // 8 columns per step with every load issued before the FMAs (bytes in flight: the
+            // GEMV streams the trailing matrix once per column)
+            const int nq = (r1 - r0 + 63) / 64;
+            int c = j + 1 + wv;
+            for (; c + 16 * 7 < n; c += 16 * 8) {
+                double av[8][kCoopRowsPerLane];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+#pragma unroll
+                    for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                        const int r = min(r0 + lane + 64 * q, r1 - 1);
+                        av[u][q] = q < nq ? a.A[r + (int64_t)(c + 16 * u) * n] : 0.0;
+                    }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const double vc = vsh[c + 16 * u];
+#pragma unroll
+                    for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] += av[u][q] * vc;
+                }
+            }
+            for (; c < n; c += 16) {
+                const double vc = vsh[c];
+#pragma unroll
+                for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                    const int r = min(r0 + lane + 64 * q, r1 - 1);
+                    if (q < nq) yacc[q] += a.A[r + (int64_t)c * n] * vc;
+                }
+            }
+            // rows past r1 were clamped to r1 - 1: their sums are never stored
+        }
+#pragma unroll
+        for (int q = 0; q < kCoopRowsPerLane; ++q) ysum[wv][lane + 64 * q] = yacc[q];
+        __syncthreads();
+        if (wv == 0)
+            for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                const int r = r0 + lane + 64 * q;
+                if (r < r1) {
+                    double y = 0.0;
+                    for (int w = 0; w < 16; ++w) y += ysum[w][lane + 64 * q];
+                    for (int c = 0; c < i; ++c) y -= a.Y[r + (int64_t)c * n] * sv[c];
+                    a.Y[r + (int64_t)i * n] = sk ? 0.0 : 2.0 * y;
+                }
+            }
+        if (blockIdx.x == 0 && tid <= i) {
+            double tc = 2.0;
+            if (tid < i) {
+                double s = 0.0;
+                for (int q = tid; q < i; ++q) s += ld_agent(&a.T[tid + q * kPanel]) * sv[q];
+                tc = -2.0 * s;
+            }
+            st_agent(&a.T[tid + i * kPanel], tc);
+        }
+        __syncthreads();
+        (void)red;
+    }
+}
+
 // C (m x nn, ldc) += alpha * op(A) op(B); op = transpose when TA / TB.  64x64 tiles, 4x4/thread.
+// Split-K: blockIdx.z takes rows [z kc, (z+1) kc) of the K range and, when gridDim.z > 1, writes its
+// partial product to C + z * zstride (beta must be 0 then; gemm_reduce adds the partials in z order).
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_f64(int m, int nn, int kk, double alpha, const double* A, int64_t lda,
-                                                const double* B, int64_t ldb, double beta, double* C, int64_t ldc) {
+                                                const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
+                                                int kc, int64_t zstride) {
     constexpr int TM = 64, KT = 16;
     __shared__ double As[KT][TM + 1];
     __shared__ double Bs[KT][TM + 1];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int i0 = blockIdx.x * TM, j0 = blockIdx.y * TM;
+    const int kb = blockIdx.z * kc;
+    const int ke = min(kk, kb + kc);
+    C += blockIdx.z * zstride;
     double acc[4][4] = {};
-    for (int k0 = 0; k0 < kk; k0 += KT) {
+    for (int k0 = kb; k0 < ke; k0 += KT) {
         for (int e = threadIdx.x; e < KT * TM; e += 256) {
             int r, q;
             // A tile: op(A)(i0 + r, k0 + q)
@@ -202,7 +444,7 @@ __global__ __launch_bounds__(256) void gemm_f64(int m, int nn, int kk, double al
             {
                 const int gi = i0 + r, gk = k0 + q;
                 double val = 0.0;
-                if (gi < m && gk < kk) val = TA ? A[gk + (int64_t)gi * lda] : A[gi + (int64_t)gk * lda];
+                if (gi < m && gk < ke) val = TA ? A[gk + (int64_t)gi * lda] : A[gi + (int64_t)gk * lda];
                 As[q][r] = val;
             }
             // B tile: op(B)(k0 + q, j0 + r)
@@ -210,7 +452,7 @@ __global__ __launch_bounds__(256) void gemm_f64(int m, int nn, int kk, double al
             {
                 const int gk = k0 + q, gj = j0 + r;
                 double val = 0.0;
-                if (gk < kk && gj < nn) val = TB ? B[gj + (int64_t)gk * ldb] : B[gk + (int64_t)gj * ldb];
+                if (gk < ke && gj < nn) val = TB ? B[gj + (int64_t)gk * ldb] : B[gk + (int64_t)gj * ldb];
                 Bs[q][r] = val;
             }
         }
@@ -239,15 +481,45 @@ __global__ __launch_bounds__(256) void gemm_f64(int m, int nn, int kk, double al
         }
 }
 
+// C = beta C + sum_z P[z] (m x nn, P packed with leading dimension m), partials added in z order
+__global__ void gemm_reduce(int m, int nn, int nz, const double* P, double beta, double* C, int64_t ldc) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)m * nn) return;
+    const int i = (int)(idx % m);
+    const int64_t j = idx / m;
+    double s = 0.0;
+    for (int z = 0; z < nz; ++z) s += P[(int64_t)z * m * nn + idx];
+    double* c = C + i + j * ldc;
+    *c = (beta == 0.0 ? 0.0 : beta * *c) + s;
+}
+
 }  // namespace dev
 
 namespace {
 template <bool TA, bool TB>
 void gemm(hipStream_t st, int m, int nn, int kk, double alpha, const double* A, int64_t lda, const double* B,
-          int64_t ldb, double beta, double* C, int64_t ldc) {
+          int64_t ldb, double beta, double* C, int64_t ldc, double* work = nullptr, int64_t work_elems = 0) {
     if (m <= 0 || nn <= 0) return;
-    hipLaunchKernelGGL((dev::gemm_f64<TA, TB>), dim3((m + 63) / 64, (nn + 63) / 64), dim3(256), 0, st, m, nn, kk,
-                       alpha, A, lda, B, ldb, beta, C, ldc);
+    const int bx = (m + 63) / 64, by = (nn + 63) / 64;
+    // split K when the output has too few tiles to fill the chip (e.g. W = V^T A, 32 rows)
+    int nz = 1;
+    if (work && bx * by < 512 && kk >= 512) {
+        nz = std::min(16, std::max(1, 1024 / (bx * by)));
+        nz = std::min<int64_t>(nz, work_elems / ((int64_t)m * nn));
+        nz = std::max(1, std::min(nz, kk / 128));
+    }
+    if (nz <= 1) {
+        hipLaunchKernelGGL((dev::gemm_f64<TA, TB>), dim3(bx, by, 1), dim3(256), 0, st, m, nn, kk, alpha, A, lda, B,
+                           ldb, beta, C, ldc, kk, (int64_t)0);
+        return;
+    }
+    const int kc = ((kk + nz - 1) / nz + 15) / 16 * 16;
+    nz = (kk + kc - 1) / kc;
+    hipLaunchKernelGGL((dev::gemm_f64<TA, TB>), dim3(bx, by, nz), dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb,
+                       0.0, work, (int64_t)m, kc, (int64_t)m * nn);
+    const int64_t tot = (int64_t)m * nn;
+    hipLaunchKernelGGL(dev::gemm_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, m, nn, nz, work, beta,
+                       C, ldc);
 }
 }  // namespace
 
@@ -267,15 +539,45 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
     EIGSOL_HIP(hipMalloc(&yp, (size_t)maxch * n * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&W, (size_t)NB * n * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&W2, (size_t)NB * n * sizeof(double)));
+    double* SK = nullptr;                 // split-K partials of W = V^T A (16 x 32 x n)
+    const int64_t sk_elems = (int64_t)16 * NB * n;
+    EIGSOL_HIP(hipMalloc(&SK, sk_elems * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&skip, 64));
     const size_t lds = (size_t)n * sizeof(double);
+    // one cooperative launch per panel when the device supports it and n fits its LDS staging
+    int coop_ok = 0, dev_id = 0;
+    EIGSOL_HIP(hipGetDevice(&dev_id));
+    EIGSOL_HIP(hipDeviceGetAttribute(&coop_ok, hipDeviceAttributeCooperativeLaunch, dev_id));
+    bool coop = coop_ok && n <= dev::kCoopMaxN && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
+    const size_t coop_lds = (size_t)n * sizeof(double);
+    double *part = nullptr, *tpart = nullptr, *x0s = nullptr;
+    unsigned* bar = nullptr;
+    int* err = nullptr;
+    if (coop) {
+        EIGSOL_HIP(hipMalloc(&part, dev::kCoopBlocks * NB * sizeof(double)));
+        EIGSOL_HIP(hipMalloc(&tpart, dev::kCoopBlocks * sizeof(double)));
+        EIGSOL_HIP(hipMalloc(&x0s, 64));
+        EIGSOL_HIP(hipMalloc(&bar, 64));
+        EIGSOL_HIP(hipMalloc(&err, 64));
+        EIGSOL_HIP(hipMemsetAsync(err, 0, 64, st));
+        EIGSOL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dev::hess_panel_coop),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)coop_lds));
+    }
     EIGSOL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dev::hess_panel_col),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int last = n - 3;   // reflector columns 0 .. n-3 (to_hessenberg.hpp:38)
     for (int k = 0; k <= last; k += NB) {
         const int nbp = std::min(NB, last - k + 1);
         EIGSOL_HIP(hipMemsetAsync(T, 0, NB * NB * sizeof(double), st));
-        for (int i = 0; i < nbp; ++i) {
+        if (coop) {
+            EIGSOL_HIP(hipMemsetAsync(bar, 0, 64, st));
+            dev::CoopArgs ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err};
+            void* kargs[] = {&ca};
+            EIGSOL_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(dev::hess_panel_coop),
+                                                  dim3(dev::kCoopBlocks), dim3(dev::kCoopThreads), kargs,
+                                                  coop_lds, st));
+        }
+        for (int i = 0; !coop && i < nbp; ++i) {
             const int j = k + i;
             hipLaunchKernelGGL(dev::hess_panel_col, dim3(1), dim3(1024), lds, st, A, n, k, j, i, V, Y, T, tv, skip);
             const int c0 = j + 1;
@@ -291,14 +593,22 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
             gemm<false, true>(st, n, mt, nbp, -1.0, Y, n, V + c1, n, 1.0, A + (int64_t)c1 * n, n);
             // left: W = V(k+1:n, :)^T A(k+1:n, c1:n); W2 = T^T W; A(k+1:n, c1:n) -= V W2
             const int rows = n - (k + 1);
-            gemm<true, false>(st, nbp, mt, rows, 1.0, V + (k + 1), n, A + (k + 1) + (int64_t)c1 * n, n, 0.0, W, NB);
+            gemm<true, false>(st, nbp, mt, rows, 1.0, V + (k + 1), n, A + (k + 1) + (int64_t)c1 * n, n, 0.0, W, NB, SK,
+                              sk_elems);
             gemm<true, false>(st, nbp, mt, nbp, 1.0, T, NB, W, NB, 0.0, W2, NB);
             gemm<false, false>(st, rows, mt, nbp, -1.0, V + (k + 1), n, W2, NB, 1.0, A + (k + 1) + (int64_t)c1 * n, n);
         }
     }
     EIGSOL_HIP(hipGetLastError());
-    for (void* p : {(void*)V, (void*)Y, (void*)T, (void*)tv, (void*)yp, (void*)W, (void*)W2, (void*)skip})
-        (void)hipFree(p);
+    int errh = 0;
+    if (coop) {
+        EIGSOL_HIP(hipMemcpyAsync(&errh, err, sizeof(int), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+    }
+    for (void* p : {(void*)V, (void*)Y, (void*)T, (void*)tv, (void*)yp, (void*)W, (void*)W2, (void*)skip,
+                    (void*)part, (void*)tpart, (void*)x0s, (void*)bar, (void*)err, (void*)SK})
+        if (p) (void)hipFree(p);
+    if (errh) return fail(EIGSOL_E_HIP, "blocked Hessenberg: grid barrier timed out (internal error)");
     return EIGSOL_OK;
 }
 

@@ -8,7 +8,7 @@ import pcsc_eigenvalue_solver_project_amd as E
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 ctx = E.Context(0)
 rng = np.random.default_rng(20251226)
-A = rng.standard_normal((n, n))
+A = np.asfortranarray(rng.standard_normal((n, n)))   # column-major, like Matrix::Dense
 # warm (small)
 E.qr_eigenvalues(ctx, A[:300, :300].copy())
 t = time.perf_counter()
