@@ -57,10 +57,25 @@ __global__ __launch_bounds__(1024) void chase_kernel(ChaseArgs a) {
     const int tid = threadIdx.x;
     const int nt = blockDim.x;
     auto Hw = [&](int i, int j) -> double& { return h[(i - a.s) + (j - a.s) * ldh]; };
-    for (int idx = tid; idx < W * W; idx += nt) {
-        const int i = idx % W, j = idx / W;
-        h[i + j * ldh] = a.H[(a.s + i) + (int64_t)(a.s + j) * a.n];
-        u[idx] = (i == j) ? 1.0 : 0.0;
+    {
+        // window load: all global loads first (9 per thread), then the LDS stores
+        constexpr int kPer = (kWin * kWin + 1023) / 1024;
+        double tmp[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int idx = tid + q * 1024;
+            const int i = idx % W, j = idx / W;
+            tmp[q] = idx < W * W ? a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int idx = tid + q * 1024;
+            if (idx < W * W) {
+                const int i = idx % W, j = idx / W;
+                h[i + j * ldh] = tmp[q];
+                u[idx] = (i == j) ? 1.0 : 0.0;
+            }
+        }
     }
     __syncthreads();
     const int l = a.l, ihi = a.ihi;
