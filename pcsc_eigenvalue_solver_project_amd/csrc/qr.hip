@@ -246,26 +246,32 @@ __global__ __launch_bounds__(1024) void hqr_lds_kernel(const double* Hin, int64_
     }
     __syncthreads();
     const double eps = 2.220446049250313e-16;
+    __shared__ int s_l;
     while (true) {
-        // ---- thread 0: deflation / 1x1 / 2x2 handling, shift and starting row m
+        // ---- deflation scan in parallel: the largest l in [1, nn] with a negligible h(l, l-1)
+        if (tid == 0) s_l = 0;
+        __syncthreads();
+        const int nn0 = c.nn;
+        if (nn0 < 0) break;
+        for (int l = 1 + tid; l <= nn0; l += blockDim.x) {
+            const double s0 = fabs(A(l - 1, l - 1)) + fabs(A(l, l));
+            const double sc = s0 == 0.0 ? s_anorm : s0;
+            if (fabs(A(l, l - 1)) <= eps * sc) atomicMax(&s_l, l);
+        }
+        __syncthreads();
+        // ---- thread 0: 1x1 / 2x2 deflation or the next sweep's shift (start row m = l)
         if (tid == 0) {
-            c.stage = 0;   // 0: sweep, 1: done
-            while (true) {
-                int nn = c.nn;
-                if (nn < 0) { c.stage = 1; break; }
-                int l;
-                for (l = nn; l >= 1; --l) {
-                    const double s0 = fabs(A(l - 1, l - 1)) + fabs(A(l, l));
-                    const double s = s0 == 0.0 ? s_anorm : s0;
-                    if (fabs(A(l, l - 1)) <= eps * s) { A(l, l - 1) = 0.0; break; }
-                }
-                const double x = A(nn, nn);
-                if (l == nn) {
-                    wr[nn] = x + c.t; wi[nn] = 0.0; c.nn = nn - 1;
-                    c.maxits = max(c.maxits, c.its);
-                    c.its = 0;
-                    continue;
-                }
+            c.stage = 0;   // 0: sweep, 1: stop, 3: deflated (scan again)
+            const int nn = nn0;
+            const int l = s_l;
+            if (l > 0) A(l, l - 1) = 0.0;
+            const double x = A(nn, nn);
+            if (l == nn) {
+                wr[nn] = x + c.t; wi[nn] = 0.0; c.nn = nn - 1;
+                c.maxits = max(c.maxits, c.its);
+                c.its = 0;
+                c.stage = 3;
+            } else {
                 const double y = A(nn - 1, nn - 1);
                 const double w = A(nn, nn - 1) * A(nn - 1, nn);
                 if (l == nn - 1) {
@@ -286,47 +292,49 @@ __global__ __launch_bounds__(1024) void hqr_lds_kernel(const double* Hin, int64_
                     c.nn = nn - 2;
                     c.maxits = max(c.maxits, c.its);
                     c.its = 0;
-                    continue;
-                }
-                if (c.its >= maxits) { c.fail = 1; c.stage = 1; break; }
-                double xs = x, ys = y, ws = w;
-                if (c.its == 10 || c.its == 20) {   // exceptional shift
-                    c.t += xs;
-                    for (int i = 0; i <= nn; ++i) A(i, i) -= xs;
-                    const double s = fabs(A(nn, nn - 1)) + fabs(A(nn - 1, nn - 2));
-                    ys = xs = 0.75 * s;
-                    ws = -0.4375 * s * s;
-                }
-                ++c.its;
-                ++c.total;
-                int m;
-                double p = 0, q = 0, r = 0;
-                for (m = nn - 2; m >= l; --m) {
+                    c.stage = 3;
+                } else if (c.its >= maxits) {
+                    c.fail = 1;
+                    c.stage = 1;
+                } else {
+                    double xs = x, ys = y, ws = w;
+                    if (c.its == 10 || c.its == 20) {   // exceptional shift
+                        c.t += xs;
+                        for (int i = 0; i <= nn; ++i) A(i, i) -= xs;
+                        const double s = fabs(A(nn, nn - 1)) + fabs(A(nn - 1, nn - 2));
+                        ys = xs = 0.75 * s;
+                        ws = -0.4375 * s * s;
+                    }
+                    ++c.its;
+                    ++c.total;
+                    // the sweep starts at m = l (the textbook's search for two small consecutive
+                    // subdiagonals is an O(n) scalar loop; starting at l is always valid)
+                    const int m = l;
                     const double z = A(m, m);
-                    r = xs - z;
-                    const double s = ys - z;
-                    p = (r * s - ws) / A(m + 1, m) + A(m, m + 1);
-                    q = A(m + 1, m + 1) - z - r - s;
-                    r = A(m + 2, m + 1);
+                    const double r0 = xs - z, s1 = ys - z;
+                    double p = (r0 * s1 - ws) / A(m + 1, m) + A(m, m + 1);
+                    double q = A(m + 1, m + 1) - z - r0 - s1;
+                    double r = A(m + 2, m + 1);
                     const double sc = fabs(p) + fabs(q) + fabs(r);
                     p /= sc; q /= sc; r /= sc;
-                    if (m == l) break;
-                    const double u = fabs(A(m, m - 1)) * (fabs(q) + fabs(r));
-                    const double v = fabs(p) * (fabs(A(m - 1, m - 1)) + fabs(z) + fabs(A(m + 1, m + 1)));
-                    if (u <= eps * v) break;
+                    c.l = l;
+                    c.m = m;
+                    c.p = p; c.q = q; c.r = r;
                 }
-                for (int i = m; i <= nn - 2; ++i) {
-                    A(i + 2, i) = 0.0;
-                    if (i != m) A(i + 2, i - 1) = 0.0;
-                }
-                c.l = l;
-                c.m = m;
-                c.p = p; c.q = q; c.r = r;
-                break;
             }
         }
         __syncthreads();
         if (c.stage == 1) break;
+        if (c.stage == 3) continue;
+        {
+            // clear the sub-subdiagonals of the active block (textbook: before the sweep)
+            const int m = c.m, nn = c.nn;
+            for (int i = m + tid; i <= nn - 2; i += blockDim.x) {
+                A(i + 2, i) = 0.0;
+                if (i != m) A(i + 2, i - 1) = 0.0;
+            }
+            __syncthreads();
+        }
         const int l = c.l, m = c.m, nn = c.nn;
         // ---- the sweep: one 3x3 reflector per k, updates in parallel
         for (int k = m; k <= nn - 1; ++k) {
