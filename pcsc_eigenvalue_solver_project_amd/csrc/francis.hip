@@ -10,7 +10,7 @@
 //
 // Locality: the chain is chased inside an LDS window [s, e) of at most kWin rows/columns with
 // the window's orthogonal factor U accumulated alongside; the parts of the reflectors' updates
-// outside the window are applied afterwards as two small GEMMs,
+// outside the window are applied afterwards as two small GEMMs (one fused launch),
 //     H(s:e, e:ihi]   <- U^T H(s:e, e:ihi]        H[l, s) x [s, e) <- H[l, s) x [s, e) U,
 // so every HBM element of the active block is touched O(1) times per window instead of once per
 // reflector.  Shifts: eigenvalues of the trailing 2nb x 2nb block (in-LDS Francis solver,
@@ -167,75 +167,65 @@ __global__ __launch_bounds__(1024) void chase_kernel(ChaseArgs a) {
     }
 }
 
-// H(s:e, c0:c1) <- U^T H(s:e, c0:c1); 32 columns per block, 8 row groups of 12 rows per thread
-// group: thread (c, g) accumulates Y(12g .. 12g+11, c) over i with U(i, :) read as a broadcast
-// row and X(i, c) from an odd-strided panel (conflict-free).
-__global__ __launch_bounds__(256) void win_left_gemm(double* H, int64_t n, int s, int W, int64_t c0, int64_t c1,
-                                                     const double* U) {
-    constexpr int LX = kWin + 1;
-    __shared__ double x[32 * LX];
-    __shared__ double ut[kWin * kWin];     // ut[i * kWin + r] = U(i, r)
-    const int64_t cb = c0 + (int64_t)blockIdx.x * 32;
-    const int nc = (int)min<int64_t>(32, c1 - cb);
-    for (int idx = threadIdx.x; idx < W * nc; idx += 256) {
-        const int i = idx % W, c = idx / W;
-        x[c * LX + i] = H[(s + i) + (cb + c) * n];
-    }
+// Both delayed updates of a window in ONE launch: blocks [0, nl) take 16-column panels of
+//     H(s:e, c0:c1) <- U^T H(s:e, c0:c1)
+// and blocks [nl, nl + nr) 16-row panels of
+//     H(r0:r1, s:e) <- H(r0:r1, s:e) U.
+// 256 threads = 16 columns (rows) x 16 groups of 6 outputs; U staged in LDS, the panel too.
+__global__ __launch_bounds__(256) void win_gemm_fused(double* H, int64_t n, int s, int W, int64_t c0, int64_t c1,
+                                                      int nl, int64_t r0, int64_t r1, const double* U) {
+    __shared__ double um[kWin * kWin];     // left: um[i * kWin + r] = U(i, r); right: um[i * kWin + j] = U(i, j)
+    __shared__ double x[kWin * 17];          // left: 16 x (kWin + 1) panel; right: kWin x 17
+    const bool left = (int)blockIdx.x < nl;
     for (int idx = threadIdx.x; idx < kWin * kWin; idx += 256) {
         const int i = idx / kWin, r = idx % kWin;
-        ut[idx] = (i < W && r < W) ? U[i + r * W] : 0.0;
+        um[idx] = (i < W && r < W) ? U[i + r * W] : 0.0;
     }
-    __syncthreads();
-    const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
-    double acc[12];
+    const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+    double acc[6];
 #pragma unroll
-    for (int q = 0; q < 12; ++q) acc[q] = 0.0;
-    for (int i = 0; i < W; ++i) {
-        const double xv = x[c * LX + i];
-        const double* ur = ut + i * kWin + 12 * g;
-#pragma unroll
-        for (int q = 0; q < 12; ++q) acc[q] += ur[q] * xv;
-    }
-    if (c < nc)
-#pragma unroll
-        for (int q = 0; q < 12; ++q) {
-            const int r = 12 * g + q;
-            if (r < W) H[(s + r) + (cb + c) * n] = acc[q];
+    for (int q = 0; q < 6; ++q) acc[q] = 0.0;
+    if (left) {
+        const int64_t cb = c0 + (int64_t)blockIdx.x * 16;
+        const int nc = (int)min<int64_t>(16, c1 - cb);
+        for (int idx = threadIdx.x; idx < W * 16; idx += 256) {
+            const int i = idx % W, cc = idx / W;
+            x[cc * (kWin + 1) + i] = cc < nc ? H[(s + i) + (cb + cc) * n] : 0.0;   // column-major panel, odd stride
         }
-}
-
-// H(r0:r1, s:e) <- H(r0:r1, s:e) U; 32 rows per block, thread (r, g) owns Y(r, 12g .. 12g+11)
-__global__ __launch_bounds__(256) void win_right_gemm(double* H, int64_t n, int s, int W, int64_t r0, int64_t r1,
-                                                      const double* U) {
-    __shared__ double x[kWin * 32];        // x[i * 32 + r] = X(r, i)
-    __shared__ double us[kWin * kWin];     // us[i * kWin + j] = U(i, j)
-    const int64_t rb = r0 + (int64_t)blockIdx.x * 32;
-    const int nr = (int)min<int64_t>(32, r1 - rb);
-    for (int idx = threadIdx.x; idx < 32 * W; idx += 256) {
-        const int r = idx & 31, i = idx >> 5;
-        x[i * 32 + r] = r < nr ? H[(rb + r) + (int64_t)(s + i) * n] : 0.0;
-    }
-    for (int idx = threadIdx.x; idx < kWin * kWin; idx += 256) {
-        const int i = idx / kWin, j = idx % kWin;
-        us[idx] = (i < W && j < W) ? U[i + j * W] : 0.0;
-    }
-    __syncthreads();
-    const int r = threadIdx.x & 31, g = threadIdx.x >> 5;
-    double acc[12];
+        __syncthreads();
+        for (int i = 0; i < W; ++i) {
+            const double xv = x[c * (kWin + 1) + i];
+            const double* ur = um + i * kWin + 6 * g;
 #pragma unroll
-    for (int q = 0; q < 12; ++q) acc[q] = 0.0;
-    for (int i = 0; i < W; ++i) {
-        const double xv = x[i * 32 + r];
-        const double* ur = us + i * kWin + 12 * g;
-#pragma unroll
-        for (int q = 0; q < 12; ++q) acc[q] += xv * ur[q];
-    }
-    if (r < nr)
-#pragma unroll
-        for (int q = 0; q < 12; ++q) {
-            const int j = 12 * g + q;
-            if (j < W) H[(rb + r) + (int64_t)(s + j) * n] = acc[q];
+            for (int q = 0; q < 6; ++q) acc[q] += ur[q] * xv;
         }
+        if (c < nc)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const int r = 6 * g + q;
+                if (r < W) H[(s + r) + (cb + c) * n] = acc[q];
+            }
+    } else {
+        const int64_t rb = r0 + (int64_t)(blockIdx.x - nl) * 16;
+        const int nr = (int)min<int64_t>(16, r1 - rb);
+        for (int idx = threadIdx.x; idx < 16 * W; idx += 256) {
+            const int rr = idx & 15, i = idx >> 4;
+            x[i * 17 + rr] = rr < nr ? H[(rb + rr) + (int64_t)(s + i) * n] : 0.0;
+        }
+        __syncthreads();
+        for (int i = 0; i < W; ++i) {
+            const double xv = x[i * 17 + c];
+            const double* ur = um + i * kWin + 6 * g;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) acc[q] += xv * ur[q];
+        }
+        if (c < nr)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const int j = 6 * g + q;
+                if (j < W) H[(rb + c) + (int64_t)(s + j) * n] = acc[q];
+            }
+    }
 }
 
 // diagonal and subdiagonal of the block [0, ihi]: out[0..n) = h(i,i), out[n..2n) = h(i,i-1)
@@ -376,16 +366,11 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             dev::ChaseArgs ca{H, n, s, e, l, ihi, t0, t1, nb, dsh, dU};
             hipLaunchKernelGGL(dev::chase_kernel, dim3(1), dim3(1024), 0, st, ca);
             const int W = e - s;
-            if (e <= ihi) {
-                const int64_t nc = ihi + 1 - e;
-                hipLaunchKernelGGL(dev::win_left_gemm, dim3((nc + 31) / 32), dim3(256), 0, st, H, n, s, W,
-                                   (int64_t)e, (int64_t)ihi + 1, dU);
-            }
-            if (s > l) {
-                const int64_t nr = s - l;
-                hipLaunchKernelGGL(dev::win_right_gemm, dim3((nr + 31) / 32), dim3(256), 0, st, H, n, s, W,
-                                   (int64_t)l, (int64_t)s, dU);
-            }
+            const int nlb = e <= ihi ? (ihi + 1 - e + 15) / 16 : 0;
+            const int nrb = s > l ? (s - l + 15) / 16 : 0;
+            if (nlb + nrb > 0)
+                hipLaunchKernelGGL(dev::win_gemm_fused, dim3(nlb + nrb), dim3(256), 0, st, H, n, s, W, (int64_t)e,
+                                   (int64_t)ihi + 1, nlb, (int64_t)l, (int64_t)s, dU);
             t0 = t1;
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "francis: launch"); break; }
