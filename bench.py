@@ -331,6 +331,7 @@ def main():
         }
     sess.close()
     A.close()
+    ctx.close()
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(kind, k, args.cpu_seconds)

@@ -481,6 +481,82 @@ __global__ __launch_bounds__(256) void gemm_f64(int m, int nn, int kk, double al
         }
 }
 
+// Same contract as gemm_f64, on the fp64 matrix cores: v_mfma_f64_16x16x4_f64.  A 64x64 block
+// tile, four waves of 32x32 (2x2 MFMA tiles).  The product is formed transposed (A operand =
+// B^T fragment, B operand = A^T fragment) so that the f64 C/D layout (col = lane & 15,
+// row = (lane >> 4) + 4 reg, cdna_hip_programming.md) puts C's ROW on the lane: 16 lanes store
+// 128 contiguous bytes of one column.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_mfma_f64(int m, int nn, int kk, double alpha, const double* A,
+                                                     int64_t lda, const double* B, int64_t ldb, double beta,
+                                                     double* C, int64_t ldc, int kc, int64_t zstride) {
+    constexpr int TM = 64, KT = 16;
+    __shared__ double As[KT][TM + 1];   // As[k][row]
+    __shared__ double Bs[KT][TM + 1];   // Bs[k][col]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wy = wave >> 1, wx = wave & 1;
+    const int i0 = blockIdx.x * TM, j0 = blockIdx.y * TM;
+    const int kb = blockIdx.z * kc;
+    const int ke = min(kk, kb + kc);
+    C += blockIdx.z * zstride;
+    dbl4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = kb; k0 < ke; k0 += KT) {
+        for (int e = threadIdx.x; e < KT * TM; e += 256) {
+            int r, q;
+            if (!TA) { r = e % TM; q = e / TM; } else { q = e % KT; r = e / KT; }
+            {
+                const int gi = i0 + r, gk = k0 + q;
+                double val = 0.0;
+                if (gi < m && gk < ke) val = TA ? A[gk + (int64_t)gi * lda] : A[gi + (int64_t)gk * lda];
+                As[q][r] = val;
+            }
+            if (!TB) { q = e % KT; r = e / KT; } else { r = e % TM; q = e / TM; }
+            {
+                const int gk = k0 + q, gj = j0 + r;
+                double val = 0.0;
+                if (gk < ke && gj < nn) val = TB ? B[gj + (int64_t)gk * ldb] : B[gk + (int64_t)gj * ldb];
+                Bs[q][r] = val;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kq = 0; kq < KT; kq += 4) {
+            const int k = kq + (lane >> 4);
+            double bfrag[2], afrag[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                afrag[t] = Bs[k][32 * wx + 16 * t + (lane & 15)];   // B^T fragment (D rows = C columns)
+                bfrag[t] = As[k][32 * wy + 16 * t + (lane & 15)];   // A^T fragment (D cols = C rows)
+            }
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj)
+                    acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(afrag[tj], bfrag[ti], acc[ti][tj], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = i0 + 32 * wy + 16 * ti + (lane & 15);
+                const int gj = j0 + 32 * wx + 16 * tj + (lane >> 4) + 4 * r;
+                if (gi < m && gj < nn) {
+                    double* cp = C + gi + (int64_t)gj * ldc;
+                    *cp = (beta == 0.0 ? 0.0 : beta * *cp) + alpha * acc[ti][tj][r];
+                }
+            }
+}
+
 // C = beta C + sum_z P[z] (m x nn, P packed with leading dimension m), partials added in z order
 __global__ void gemm_reduce(int m, int nn, int nz, const double* P, double beta, double* C, int64_t ldc) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -508,15 +584,17 @@ void gemm(hipStream_t st, int m, int nn, int kk, double alpha, const double* A, 
         nz = std::min<int64_t>(nz, work_elems / ((int64_t)m * nn));
         nz = std::max(1, std::min(nz, kk / 128));
     }
+    static const bool valu = std::getenv("EIGSOL_GEMM_VALU") != nullptr;
+    auto kern = valu ? dev::gemm_f64<TA, TB> : dev::gemm_mfma_f64<TA, TB>;
     if (nz <= 1) {
-        hipLaunchKernelGGL((dev::gemm_f64<TA, TB>), dim3(bx, by, 1), dim3(256), 0, st, m, nn, kk, alpha, A, lda, B,
-                           ldb, beta, C, ldc, kk, (int64_t)0);
+        hipLaunchKernelGGL(kern, dim3(bx, by, 1), dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb, beta, C, ldc,
+                           kk, (int64_t)0);
         return;
     }
     const int kc = ((kk + nz - 1) / nz + 15) / 16 * 16;
     nz = (kk + kc - 1) / kc;
-    hipLaunchKernelGGL((dev::gemm_f64<TA, TB>), dim3(bx, by, nz), dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb,
-                       0.0, work, (int64_t)m, kc, (int64_t)m * nn);
+    hipLaunchKernelGGL(kern, dim3(bx, by, nz), dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb, 0.0, work,
+                       (int64_t)m, kc, (int64_t)m * nn);
     const int64_t tot = (int64_t)m * nn;
     hipLaunchKernelGGL(dev::gemm_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, m, nn, nz, work, beta,
                        C, ldc);

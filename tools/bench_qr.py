@@ -29,3 +29,4 @@ if n == 4096:
     out["max_match_dist"] = float(d.max())
     out["unique_matches"] = int(len(np.unique(j)))
 print(json.dumps(out), flush=True)
+ctx.close()

@@ -41,3 +41,4 @@ ms = e0.elapsed_time(e1) / steps
 b = sess.kernel_info()["bytes_per_iteration"]
 print(json.dumps({"n": n, "ms_per_iteration": ms, "GBps": b / (ms / 1e3) / 1e9, "bytes": b,
                   "levels": sess.kernel_info()["tiles"]}), flush=True)
+ctx.close()

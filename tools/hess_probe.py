@@ -12,3 +12,4 @@ for rep in range(2):
     t = time.perf_counter()
     H = E.to_hessenberg(ctx, A)
     print(json.dumps({"n": n, "rep": rep, "seconds": time.perf_counter() - t}), flush=True)
+ctx.close()

@@ -60,3 +60,4 @@ for L in (64, 256):
 # (d) config 5
 rp, ci, v, _ = S.triu_complex(n, 16)
 run("config5", rp, ci, v, n)
+ctx.close()
