@@ -201,7 +201,10 @@ __global__ __launch_bounds__(256) void hess_y(int n, int i, int nch, const doubl
 constexpr int kCoopBlocks = 64;
 constexpr int kCoopThreads = 1024;
 constexpr int kCoopMaxN = 8192;          // v in LDS (64 KiB) and at most 2 rows per lane
-constexpr int kCoopRowsPerLane = 2;
+#ifndef EIGSOL_GEMV_BATCH
+#define EIGSOL_GEMV_BATCH 16
+#endif
+constexpr int kGemvBatch = EIGSOL_GEMV_BATCH;   // columns per GEMV step (loads in flight per lane)
 
 struct CoopArgs {
     double* A;
@@ -235,13 +238,30 @@ __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned& target, in
     __syncthreads();
 }
 
+template <int kCoopRowsPerLane>
 __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
     extern __shared__ double vsh[];          // v (n doubles) for the GEMV
     __shared__ double xs[kCoopRowsPerLane * 64];    // own rows of the current column
     __shared__ double ysum[16][kCoopRowsPerLane * 64];
-    __shared__ double red[16 * kPanel];
+    __shared__ double red[kCoopBlocks * kPanel];   // gathered block partials
     __shared__ double sv[kPanel], sw[kPanel], st[kPanel];
     __shared__ double s_scal[4];
+    // Block partials of another phase: all threads load them at once (independent sc1 loads),
+    // then thread c sums column c in block order (deterministic).
+    auto gather = [&](const double* src, int cnt, double* dst) {
+        const int nb = (int)gridDim.x;
+        for (int e = threadIdx.x; e < nb * kPanel; e += kCoopThreads) {
+            const int b = e / kPanel, c = e % kPanel;
+            red[e] = c < cnt ? ld_agent(&src[b * kPanel + c]) : 0.0;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < cnt) {
+            double acc = 0.0;
+            for (int b = 0; b < nb; ++b) acc += red[b * kPanel + threadIdx.x];
+            dst[threadIdx.x] = acc;
+        }
+        __syncthreads();
+    };
     const int n = a.n, k = a.k;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int G = gridDim.x;
@@ -275,12 +295,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
         }
         grid_barrier(a.bar, target, a.err);
         // ---------------- P2
-        if (tid < i) {
-            double w = 0.0;
-            for (int b = 0; b < G; ++b) w += ld_agent(&a.part[b * kPanel + tid]);
-            sw[tid] = w;
-        }
-        __syncthreads();
+        gather(a.part, i, sw);
         if (tid < i) {
             double s = 0.0;
             for (int c = 0; c <= tid; ++c) s += ld_agent(&a.T[c + tid * kPanel]) * sw[c];   // (T^T w)_tid
@@ -306,9 +321,11 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
         }
         grid_barrier(a.bar, target, a.err);
         // ---------------- P3
+        if (tid < G) red[tid] = ld_agent(&a.tpart[tid]);
+        __syncthreads();
         if (tid == 0) {
             double tail = 0.0;
-            for (int b = 0; b < G; ++b) tail += ld_agent(&a.tpart[b]);
+            for (int b = 0; b < G; ++b) tail += red[b];
             const double x0 = ld_agent(a.x0);
             double sk = tail == 0.0 ? 1.0 : 0.0, v0 = 0.0, rv = 0.0, alpha = 0.0;
             if (sk == 0.0) {
@@ -353,11 +370,9 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
         grid_barrier(a.bar, target, a.err);
         // ---------------- P4
         for (int r = tid; r < n; r += kCoopThreads) vsh[r] = sk ? 0.0 : ld_agent(&a.V[r + (int64_t)i * n]);
-        if (tid < i) {
-            double t = 0.0;
-            for (int b = 0; b < G; ++b) t += ld_agent(&a.part[b * kPanel + tid]);
-            sv[tid] = sk ? 0.0 : t;
-        }
+        __syncthreads();
+        gather(a.part, i, sv);
+        if (sk && tid < i) sv[tid] = 0.0;
         __syncthreads();
         double yacc[kCoopRowsPerLane];
 #pragma unroll
@@ -367,17 +382,18 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
             // GEMV streams the trailing matrix once per column)
             const int nq = (r1 - r0 + 63) / 64;
             int c = j + 1 + wv;
-            for (; c + 16 * 7 < n; c += 16 * 8) {
-                double av[8][kCoopRowsPerLane];
+            constexpr int kB = kGemvBatch / kCoopRowsPerLane;   // loads in flight per lane
+            for (; c + 16 * (kB - 1) < n; c += 16 * kB) {
+                double av[kB][kCoopRowsPerLane];
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
+                for (int u = 0; u < kB; ++u)
 #pragma unroll
                     for (int q = 0; q < kCoopRowsPerLane; ++q) {
                         const int r = min(r0 + lane + 64 * q, r1 - 1);
                         av[u][q] = q < nq ? a.A[r + (int64_t)(c + 16 * u) * n] : 0.0;
                     }
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
+                for (int u = 0; u < kB; ++u) {
                     const double vc = vsh[c + 16 * u];
 #pragma unroll
                     for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] += av[u][q] * vc;
@@ -628,6 +644,8 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
     EIGSOL_HIP(hipDeviceGetAttribute(&coop_ok, hipDeviceAttributeCooperativeLaunch, dev_id));
     bool coop = coop_ok && n <= dev::kCoopMaxN && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
     const size_t coop_lds = (size_t)n * sizeof(double);
+    const void* coop_kernel = n <= 64 * dev::kCoopBlocks ? reinterpret_cast<const void*>(dev::hess_panel_coop<1>)
+                                                         : reinterpret_cast<const void*>(dev::hess_panel_coop<2>);
     double *part = nullptr, *tpart = nullptr, *x0s = nullptr;
     unsigned* bar = nullptr;
     int* err = nullptr;
@@ -638,8 +656,7 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
         EIGSOL_HIP(hipMalloc(&bar, 64));
         EIGSOL_HIP(hipMalloc(&err, 64));
         EIGSOL_HIP(hipMemsetAsync(err, 0, 64, st));
-        EIGSOL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dev::hess_panel_coop),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)coop_lds));
+        EIGSOL_HIP(hipFuncSetAttribute(coop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)coop_lds));
     }
     EIGSOL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dev::hess_panel_col),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -651,8 +668,7 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
             EIGSOL_HIP(hipMemsetAsync(bar, 0, 64, st));
             dev::CoopArgs ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err};
             void* kargs[] = {&ca};
-            EIGSOL_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(dev::hess_panel_coop),
-                                                  dim3(dev::kCoopBlocks), dim3(dev::kCoopThreads), kargs,
+            EIGSOL_HIP(hipLaunchCooperativeKernel(coop_kernel, dim3(dev::kCoopBlocks), dim3(dev::kCoopThreads), kargs,
                                                   coop_lds, st));
         }
         for (int i = 0; !coop && i < nbp; ++i) {
