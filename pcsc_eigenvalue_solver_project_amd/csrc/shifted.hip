@@ -140,7 +140,6 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
     const int lane = tid & (kRowLanes - 1);
     const int lane64 = tid & 63;
     const int grp = lane64 / kRowLanes;              // 4 row groups per wave
-    constexpr int kGroups = 64 / kRowLanes;
     const int epoch = a.epoch;
     // Each wave takes chunks of kTriChunk positions from the dispenser on its own: no barrier
     // inside the loop.  The grab and the partial stores are executed by ALL lanes (increment 1
@@ -152,11 +151,23 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
     // dispensed in increasing order, which is all the progress argument needs.
     const int cls = a.nclasses > 1 ? (blockIdx.x & 7) : 0;
     uint32_t* disp = a.work + kDispStride * cls;
-    auto grab = [&]() -> int {
-        const int old = (int)atomicAdd(disp, lane64 == 0 ? 1u : 0u);
-        return cls + a.nclasses * __builtin_amdgcn_readfirstlane(old);
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar) index
+    __shared__ int s_grab;
+    // The block takes kWaves consecutive chunks per dispenser grab (one atomic per block, not per
+    // wave) and wave w works on chunk g * kWaves + w.  The grab is executed by all lanes of wave 0
+    // (scalar branch) and broadcast through LDS; the loop bound is block-uniform.
+    auto grab_group = [&]() -> int {
+        __syncthreads();
+        if (wave == 0) {
+            const int old = (int)atomicAdd(disp, lane64 == 0 ? 1u : 0u);
+            s_grab = __builtin_amdgcn_readfirstlane(old);
+        }
+        __syncthreads();
+        return cls + a.nclasses * __builtin_amdgcn_readfirstlane(s_grab);
     };
-    for (int c = grab(); c < a.nchunks; c = grab()) {
+    for (int g = grab_group(); g * kWaves < a.nchunks; g = grab_group()) {
+        const int c = g * kWaves + wave;
+        if (c >= a.nchunks) continue;
         double n2 = 0.0, pr = 0.0, pi = 0.0;
         // a round: kU rows per 16-lane group, kWaveRows positions per wave, all of one level
         for (int r0 = 0; r0 < kTriChunk; r0 += kWaveRows) {
