@@ -206,8 +206,11 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
                 for (int u = 0; u < kU; ++u) {
                     int spins = 0;
                     while (ok[u] && f[u] < epoch) {
-                        // back off: spinning waves must leave the memory system to the producers
-                        __builtin_amdgcn_s_sleep(8);
+                        // back off, exponentially: a wave far ahead of the dependency frontier must
+                        // leave the memory system to the producers
+                        if (spins < 4) __builtin_amdgcn_s_sleep(2);
+                        else if (spins < 16) __builtin_amdgcn_s_sleep(8);
+                        else __builtin_amdgcn_s_sleep(32);
                         f[u] = ld_flag(a.flags + j[u]);
                         if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag(a.err) != 0)) {
                             atomicOr(a.err, 1);
