@@ -11,8 +11,8 @@
 // Factor kinds
 //   * triangular CSR (upper or lower; config 5): the factor IS the matrix.  Pivots d_i - sigma
 //     (coeffRef inserts a missing diagonal, solve_shifted.hpp:100-102), rows ordered by dependency
-//     level, and a sync-free triangular solve: each 16-lane group solves one row, waiting on
-//     per-row ready flags (epoch-stamped, so they never need resetting) of the rows it reads.
+//     level, and a sync-free triangular solve: each 16-lane group solves one row, polling the
+//     solved values of the rows it reads (an unsolved value is a sentinel NaN).
 //   * dense (Matrix::Dense, and small non-triangular sparse matrices densified on the device):
 //     right-looking partial-pivot LU (the unblocked order of Eigen's PartialPivLU), then a
 //     single-workgroup forward/back substitution per iteration with the vector in LDS.
@@ -34,22 +34,21 @@ struct ShiftFactor {
     int64_t n = 0;
     int kind = 0;                 // 0 triangular CSR, 1 dense LU
     double sig_re = 0.0, sig_im = 0.0;
-    // triangular
+    // triangular: everything indexed by solve position (rows sorted by level, levels padded)
     int upper = 1;
     int64_t nnz_total = 0;        // nonzeros of A (diagonal included), for roofline accounting
     int64_t nnz_off = 0;
-    int32_t* rowptr = nullptr;    // off-diagonal CSR, original row numbering
-    int32_t* col = nullptr;
-    void* val = nullptr;
-    void* piv = nullptr;          // d_i - sigma
-    int32_t* order = nullptr;     // positions -> row (-1: level padding)
+    int32_t* order = nullptr;     // position -> row (-1: level padding)
+    int32_t* pptr = nullptr;      // position -> first off-diagonal entry (npos + 1)
+    int32_t* pcol = nullptr;      // off-diagonal columns (original row numbering), position order
+    void* pval = nullptr;
+    void* ppiv = nullptr;         // d_i - sigma, by position
+    void* z[2] = {nullptr, nullptr};   // solve values polled by readers; sentinel = not yet solved
     int32_t npos = 0, nchunks = 0, nlevels = 0;
-    int32_t* flags = nullptr;     // ready stamps
-    uint32_t* work = nullptr;     // 8 chunk dispensers + last-arriver ticket (128 B apart)
+    uint32_t* work = nullptr;     // last-arriver ticket
     int32_t* err = nullptr;
-    void* chunk_part = nullptr;   // part4 per chunk
+    void* wave_part = nullptr;    // part4 per wave
     int32_t epoch = 0;
-    int32_t nclasses = 1;
     int grid = 0;
     // dense
     void* lu = nullptr;           // column-major n x n, L (unit) below, U on and above the diagonal
@@ -60,27 +59,27 @@ struct ShiftFactor {
 
 namespace dev {
 
-constexpr int kU = 4;            // rows in flight per 16-lane group
-constexpr int kTriChunk = 4 * kU;   // positions per dispenser grab: one wave round (all in flight)
-constexpr int kDispStride = 32;  // dispenser counters 128 B apart; [8 * kDispStride] = ticket
-constexpr int kWaveRows = 4 * kU;   // positions per wave round: levels are padded to this
-constexpr int kRowLanes = 16;    // lanes per row
-constexpr int kSpinLimit = 1 << 20;   // x (512 cycles + a load) ~ 0.5-1 s
+constexpr int kRowLanes = 16;    // lanes per row: one row per 16-lane group, 4 rows per wave round
+constexpr int kWaveRows = 4;     // positions per wave round (one chunk): levels are padded to this
+constexpr int kSpinLimit = 1 << 20;   // polls (with back-off) before the wait is declared broken
+// An unsolved entry of z holds this NaN in every 8-byte word.  A solved value never does: the
+// producer maps it to the default quiet NaN (sanitize), so the value itself is the ready flag.
+constexpr unsigned long long kSent = 0x7FF4DEAD7FF4DEADull;
 
 template <class S>
 struct TriArgs {
-    const int32_t* rowptr;
-    const int32_t* col;
-    const S* val;
-    const S* piv;
     const int32_t* order;
-    int32_t npos;
+    const int32_t* pptr;
+    const int32_t* pcol;
+    const S* pval;
+    const S* ppiv;
     int32_t nchunks;
-    int32_t* flags;
+    int64_t n;
+    S* zcur;            // polled by this launch
+    S* znext;           // reset to the sentinel by this launch, for the next one
     uint32_t* work;
     int32_t* err;
-    int32_t epoch;
-    int32_t nclasses;   // dispenser classes: 1, or 8 (blockIdx % 8)
+    part4* wave_part;
     const S* b_plain;   // solve mode
     S* y_plain;
     S* buf0;            // iteration mode (same parity convention as the power loop)
@@ -88,7 +87,6 @@ struct TriArgs {
     PowerCtl* ctl;
     const part4* rank_part;
     part4* my_part;
-    part4* chunk_part;
     S* trace;
     double sig_re, sig_im;
 };
@@ -100,8 +98,27 @@ __device__ __forceinline__ void st_coh(cplx* p, cplx v) {
 }
 __device__ __forceinline__ double ld_coh(const double* p) { return ld_agent(p); }
 __device__ __forceinline__ cplx ld_coh(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
-__device__ __forceinline__ int ld_flag(const int32_t* p) {
+
+__device__ __forceinline__ int ld_flag_err(const int32_t* p) {
     return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool unready(double v) { return (unsigned long long)__double_as_longlong(v) == kSent; }
+__device__ __forceinline__ bool unready(cplx v) { return unready(v.re) || unready(v.im); }
+__device__ __forceinline__ double sanitize(double v) {
+    return unready(v) ? __longlong_as_double(0x7FF8000000000000ll) : v;
+}
+__device__ __forceinline__ cplx sanitize(cplx v) { return cplx{sanitize(v.re), sanitize(v.im)}; }
+template <class S>
+__device__ __forceinline__ S sentinel() {
+    const double s = __longlong_as_double((long long)kSent);
+    if constexpr (std::is_same_v<S, double>) return s;
+    else return cplx{s, s};
+}
+template <class S>
+__device__ __forceinline__ S s_one() {
+    if constexpr (std::is_same_v<S, double>) return 1.0;
+    else return cplx{1.0, 0.0};
 }
 
 // sum over the 16 lanes of a row group (xor butterfly inside the group: every lane gets the sum)
@@ -112,12 +129,44 @@ __device__ __forceinline__ double group_sum(double v) {
 }
 __device__ __forceinline__ cplx group_sum(cplx v) { return cplx{group_sum(v.re), group_sum(v.im)}; }
 
-// Sync-free triangular solve.  Positions are dispensed in chunks in increasing order; a row only
-// waits on rows of strictly lower level, i.e. strictly earlier positions, and every level is
-// padded to a multiple of kWaveRows so the rows one wave holds at a time never depend on each
-// other (a wave spinning on a row held by its own lanes could never proceed).  Induction on the
-// earliest unfinished position gives progress without any residency assumption; a bounded spin
-// plus a sticky error word guarantees the grid drains even if that invariant were broken.
+// poll z[j] until solved (bounded; a broken wait sets the sticky error word and gives up)
+template <class S>
+__device__ __forceinline__ S wait_value(const S* z, int j, int32_t* err) {
+    S y = ld_coh(z + j);
+    int spins = 0;
+    while (unready(y)) {
+        // back off, exponentially: a wave far ahead of the dependency frontier must leave the
+        // memory system to the producers
+        if (spins < 4) __builtin_amdgcn_s_sleep(2);
+        else if (spins < 16) __builtin_amdgcn_s_sleep(8);
+        else __builtin_amdgcn_s_sleep(32);
+        y = ld_coh(z + j);
+        if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(err) != 0)) {
+            atomicOr(err, 1);
+            break;
+        }
+    }
+    return y;
+}
+
+template <class S>
+struct RowMeta {
+    int i, e0, len, j;
+    S v, bi, pv;
+};
+
+// Sync-free triangular solve, static schedule.  Positions (rows sorted by level, every level
+// padded to a multiple of kWaveRows) form chunks of one wave round; chunk c belongs to wave
+// c mod W of the W resident waves, which takes its chunks in increasing order.  A row waits only
+// on rows of strictly lower level, i.e. strictly earlier chunks, and the four rows of a round
+// never depend on each other, so the earliest unfinished chunk can always proceed: progress
+// needs every wave resident (the grid is sized to one residency round); a bounded spin plus a
+// sticky error word guarantees the grid drains even if that were violated.
+// The solved value is its own ready flag (z starts as the sentinel NaN): a dependency costs one
+// coherent load, and the producer publishes with one store.  Each launch resets the other z
+// buffer row by row for the next launch (also when it exits early), so no reset pass exists.
+// The metadata of the next two chunks is in flight while the current one waits.
+// Norm and Rayleigh partials accumulate per wave in a fixed chunk order: deterministic.
 template <class S, bool kIter>
 __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int parity) {
     __shared__ Prologue pro;
@@ -128,7 +177,12 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
     double nrm = 0.0;
     if constexpr (kIter) {
         shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
-        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) {
+            // nothing to solve, but the next launch still expects its z reset
+            for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < a.n; r += (int64_t)gridDim.x * kThreads)
+                a.znext[r] = sentinel<S>();
+            return;
+        }
         nrm = pro.nrm;
         xin = parity ? a.buf0 : a.buf1;
         yout = parity ? a.buf1 : a.buf0;
@@ -138,142 +192,83 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
     }
     const int tid = threadIdx.x;
     const int lane = tid & (kRowLanes - 1);
-    const int lane64 = tid & 63;
-    const int grp = lane64 / kRowLanes;              // 4 row groups per wave
-    const int epoch = a.epoch;
-    // Each wave takes chunks of kTriChunk positions from the dispenser on its own: no barrier
-    // inside the loop.  The grab and the partial stores are executed by ALL lanes (increment 1
-    // from lane 0 only; identical values stored): a lane-0-only branch at the loop head or latch
-    // lets the structurizer rotate that lane into a separate loop around the shuffles, which then
-    // read a stale chunk index and never exit.
-    // Eight dispensers (one per residue class of the chunk index, served by the blocks with
-    // blockIdx % 8 == class) so grabs do not serialise on one address; each class is still
-    // dispensed in increasing order, which is all the progress argument needs.
-    const int cls = a.nclasses > 1 ? (blockIdx.x & 7) : 0;
-    uint32_t* disp = a.work + kDispStride * cls;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar) index
-    __shared__ int s_grab;
-    // The block takes kWaves consecutive chunks per dispenser grab (one atomic per block, not per
-    // wave) and wave w works on chunk g * kWaves + w.  The grab is executed by all lanes of wave 0
-    // (scalar branch) and broadcast through LDS; the loop bound is block-uniform.
-    auto grab_group = [&]() -> int {
-        __syncthreads();
-        if (wave == 0) {
-            const int old = (int)atomicAdd(disp, lane64 == 0 ? 1u : 0u);
-            s_grab = __builtin_amdgcn_readfirstlane(old);
-        }
-        __syncthreads();
-        return cls + a.nclasses * __builtin_amdgcn_readfirstlane(s_grab);
+    const int grp = (tid & 63) / kRowLanes;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W = gridDim.x * kWaves;
+    const int gw = blockIdx.x * kWaves + wave;
+
+    auto fetch1 = [&](int c, RowMeta<S>& m) {   // position-indexed metadata: no dependent loads
+        const bool in = c < a.nchunks;
+        const int pos = (in ? c : 0) * kWaveRows + grp;
+        m.i = in ? a.order[pos] : -1;
+        const int e0 = a.pptr[pos];
+        m.e0 = e0;
+        m.len = in ? a.pptr[pos + 1] - e0 : 0;
+        m.pv = a.ppiv[pos];
     };
-    for (int g = grab_group(); g * kWaves < a.nchunks; g = grab_group()) {
-        const int c = g * kWaves + wave;
-        if (c >= a.nchunks) continue;
-        double n2 = 0.0, pr = 0.0, pi = 0.0;
-        // a round: kU rows per 16-lane group, kWaveRows positions per wave, all of one level
-        for (int r0 = 0; r0 < kTriChunk; r0 += kWaveRows) {
-            const int pbase = c * kTriChunk + r0 + grp * kU;
-            int iu[kU], e0[kU], len[kU];
-            int maxlen = 0;
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int pos = pbase + u;
-                const int i = pos < a.npos ? a.order[pos] : -1;
-                iu[u] = i;
-                e0[u] = i >= 0 ? a.rowptr[i] : 0;
-                len[u] = i >= 0 ? a.rowptr[i + 1] - e0[u] : 0;
-                maxlen = max(maxlen, len[u]);
-            }
-            S acc[kU];
-#pragma unroll
-            for (int u = 0; u < kU; ++u) acc[u] = s_zero<S>();
-            for (int k = lane; k < maxlen; k += kRowLanes) {
-                // every load of the kU rows is issued before any wait (clamped, unconditional)
-                int j[kU];
-                S v[kU];
-                bool ok[kU];
-#pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    ok[u] = k < len[u];
-                    const int e = ok[u] ? e0[u] + k : 0;
-                    const int jj = a.col[e];
-                    j[u] = ok[u] ? jj : 0;
-                    v[u] = a.val[e];
-                }
-                int f[kU];
-#pragma unroll
-                for (int u = 0; u < kU; ++u) f[u] = ld_flag(a.flags + j[u]);
-#pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    int spins = 0;
-                    while (ok[u] && f[u] < epoch) {
-                        // back off, exponentially: a wave far ahead of the dependency frontier must
-                        // leave the memory system to the producers
-                        if (spins < 4) __builtin_amdgcn_s_sleep(2);
-                        else if (spins < 16) __builtin_amdgcn_s_sleep(8);
-                        else __builtin_amdgcn_s_sleep(32);
-                        f[u] = ld_flag(a.flags + j[u]);
-                        if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag(a.err) != 0)) {
-                            atomicOr(a.err, 1);
-                            break;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    const S yj = ld_coh(yout + j[u]);
-                    if (ok[u]) acc[u] = add(acc[u], mul(v[u], yj));
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kU; ++u) acc[u] = group_sum(acc[u]);
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int i = iu[u];
-                if (i < 0) continue;                 // level padding / past the end
-                S bi = xin[i];
-                if constexpr (kIter) bi = scale_in(bi, nrm);
-                const S yi = sdiv(sub(bi, acc[u]), a.piv[i]);
-                if (lane == 0) {
-                    st_coh(yout + i, yi);
-                    if constexpr (kIter) {
-                        n2 += sq_abs(yi);
-                        acc_dot(pr, pi, bi, yi);     // p = sum conj(x_i) y_i
-                    }
-                }
-            }
-            if (lane == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // y visible before its flag
-#pragma unroll
-                for (int u = 0; u < kU; ++u)
-                    if (iu[u] >= 0)
-                        __hip_atomic_store(a.flags + iu[u], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto fetch2 = [&](RowMeta<S>& m) {         // the row's first 16 entries and its right side
+        const bool ok = lane < m.len;
+        const int e = ok ? m.e0 + lane : 0;
+        m.j = ok ? a.pcol[e] : -1;
+        m.v = a.pval[e];
+        m.bi = xin[m.i >= 0 ? m.i : 0];
+    };
+
+    double n2 = 0.0, pr = 0.0, pi = 0.0;
+    RowMeta<S> cur, nxt;
+    fetch1(gw, cur);
+    fetch2(cur);
+    fetch1(gw + W, nxt);
+    for (int c = gw; c < a.nchunks; c += W) {
+        fetch2(nxt);
+        RowMeta<S> nn;
+        fetch1(c + 2 * W, nn);
+        S acc = s_zero<S>();
+        if (cur.j >= 0) acc = mul(cur.v, wait_value(a.zcur, cur.j, a.err));
+        for (int k = lane + kRowLanes; k < cur.len; k += kRowLanes) {   // rows longer than 16
+            const int e = cur.e0 + k;
+            acc = add(acc, mul(a.pval[e], wait_value(a.zcur, a.pcol[e], a.err)));
+        }
+        acc = group_sum(acc);
+        if (cur.i >= 0 && lane == 0) {
+            S bi = cur.bi;
+            if constexpr (kIter) bi = scale_in(bi, nrm);
+            const S yi = sanitize(sdiv(sub(bi, acc), cur.pv));
+            st_coh(a.zcur + cur.i, yi);      // publish: readers poll this very word
+            yout[cur.i] = yi;
+            a.znext[cur.i] = sentinel<S>();
+            if constexpr (kIter) {
+                n2 += sq_abs(yi);
+                acc_dot(pr, pi, bi, yi);     // p = sum conj(x_i) y_i
             }
         }
-        if constexpr (kIter) {
-            n2 = wave_sum(n2);
-            pr = wave_sum(pr);
-            pi = wave_sum(pi);
-            part4* p = a.chunk_part + c;             // every lane stores the same sums
-            st_agent(&p->a, n2);
-            st_agent(&p->b, pr);
-            st_agent(&p->c, pi);
-        }
+        cur = nxt;
+        nxt = nn;
+    }
+    if constexpr (kIter) {
+        n2 = wave_sum(n2);
+        pr = wave_sum(pr);
+        pi = wave_sum(pi);
+        part4* p = a.wave_part + gw;             // every lane stores the same sums
+        st_agent(&p->a, n2);
+        st_agent(&p->b, pr);
+        st_agent(&p->c, pi);
     }
     __syncthreads();
-    // last arriver: chunk partials in chunk order (deterministic), dispenser reset
+    // last arriver: wave partials in wave order (deterministic), ticket reset
     if (tid == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(&a.work[8 * kDispStride], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t tk = __hip_atomic_fetch_add(&a.work[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (tk == gridDim.x - 1) ? 1 : 0;
     }
     __syncthreads();
     if (!s_last) return;
     if constexpr (kIter) {
         double sa = 0.0, sb = 0.0, sc = 0.0;
-        for (int i = tid; i < a.nchunks; i += kThreads) {
-            sa += ld_agent(&a.chunk_part[i].a);
-            sb += ld_agent(&a.chunk_part[i].b);
-            sc += ld_agent(&a.chunk_part[i].c);
+        for (int i = tid; i < W; i += kThreads) {
+            sa += ld_agent(&a.wave_part[i].a);
+            sb += ld_agent(&a.wave_part[i].b);
+            sc += ld_agent(&a.wave_part[i].c);
         }
         block_sum3(sa, sb, sc, sm);
         if (tid == 0) {
@@ -283,7 +278,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
             a.my_part->d = 0.0;
         }
     }
-    if (tid <= 8) __hip_atomic_store(&a.work[tid * kDispStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(&a.work[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------ dense LU (factor once)
@@ -468,8 +463,8 @@ static void shift_free(ShiftFactor* f) {
     if (!f) return;
     hipSetDevice(f->ctx->device);
     hipStreamSynchronize(f->ctx->stream);
-    for (void* p : {(void*)f->rowptr, (void*)f->col, f->val, f->piv, (void*)f->order, (void*)f->flags,
-                    (void*)f->work, (void*)f->err, f->chunk_part, f->lu, (void*)f->perm,
+    for (void* p : {(void*)f->order, (void*)f->pptr, (void*)f->pcol, f->pval, f->ppiv, f->z[0], f->z[1],
+                    (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
                     (void*)f->zero_pivot})
         if (p) hipFree(p);
     ctx_release(f->ctx);
@@ -654,39 +649,60 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
     std::vector<int32_t> order;
     level_order(orp, oci, n, up, order, f->nlevels);
     f->npos = (int32_t)order.size();
-    f->nchunks = (f->npos + dev::kTriChunk - 1) / dev::kTriChunk;
+    f->nchunks = f->npos / dev::kWaveRows;
+    // position-indexed copies: a row's metadata needs no dependent load, and the off-diagonal
+    // entries of consecutive positions are contiguous
+    std::vector<int32_t> pptr(f->npos + 1, 0), pcol;
+    std::vector<S> pval, ppiv(f->npos);
+    pcol.reserve(oci.size());
+    pval.reserve(oci.size());
+    for (int32_t p = 0; p < f->npos; ++p) {
+        const int32_t i = order[p];
+        if (i >= 0) {
+            for (int32_t e = orp[i]; e < orp[i + 1]; ++e) {
+                pcol.push_back(oci[e]);
+                pval.push_back(ov[e]);
+            }
+            ppiv[p] = pv[i];
+        } else {
+            ppiv[p] = make_sigma<S>(1.0, 0.0);
+        }
+        pptr[p + 1] = (int32_t)pcol.size();
+    }
+    std::vector<int32_t>().swap(oci);
+    std::vector<S>().swap(ov);
     auto up_ = [&](void** dst, const void* src, size_t bytes) -> int {
         EIGSOL_HIP(hipMalloc(dst, std::max<size_t>(bytes, 16)));
         if (bytes && src) EIGSOL_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, st));
         return EIGSOL_OK;
     };
-    rc = up_((void**)&f->rowptr, orp.data(), (n + 1) * 4);
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->col, oci.data(), oci.size() * 4);
-    if (rc == EIGSOL_OK) rc = up_(&f->val, ov.data(), ov.size() * sizeof(S));
-    if (rc == EIGSOL_OK) rc = up_(&f->piv, pv.data(), n * sizeof(S));
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), order.size() * 4);
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->flags, nullptr, n * 4);
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->work, nullptr, 2048);
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->err, nullptr, 64);
-    if (rc == EIGSOL_OK) rc = up_(&f->chunk_part, nullptr, (size_t)f->nchunks * sizeof(dev::part4));
-    if (rc == EIGSOL_OK) {
-        hipMemsetAsync(f->flags, 0, n * 4, st);
-        hipMemsetAsync(f->work, 0, 2048, st);
-        hipMemsetAsync(f->err, 0, 64, st);
-        if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "factor upload");
-    }
+    // one residency round of waves (the static schedule needs every wave resident), capped by
+    // the work: two blocks per CU by default
     if (rc == EIGSOL_OK)
         rc = resident_blocks(f->ctx, reinterpret_cast<const void*>(dev::sptrsv_kernel<S, true>),
                              dev::kThreads, 0, &f->grid);
-    if (rc != EIGSOL_OK) { shift_free(f); return rc; }
-    // One block per CU by default: enough waves to cover a dependency level many times over,
-    // few enough that waves parked on later levels do not flood the memory system with polls.
-    int per_cu = 1;
+    int per_cu = 2;
     if (const char* env = std::getenv("EIGSOL_TRSV_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(env));
-    if (const char* env = std::getenv("EIGSOL_TRSV_CLASSES")) f->nclasses = std::atoi(env) == 8 ? 8 : 1;
     f->grid = std::min(f->grid, per_cu * f->ctx->num_cus);
-    // at least one block per dispenser class (blockIdx % 8)
-    f->grid = std::max(8, std::min(f->grid, ((f->nchunks + 7) / 8) * 8));
+    f->grid = std::max(1, std::min(f->grid, (f->nchunks + dev::kWaves - 1) / dev::kWaves));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), order.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->pptr, pptr.data(), pptr.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->pcol, pcol.data(), pcol.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_(&f->pval, pval.data(), pval.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_(&f->ppiv, ppiv.data(), ppiv.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_(&f->z[0], nullptr, n * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_(&f->z[1], nullptr, n * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->work, nullptr, 64);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->err, nullptr, 64);
+    if (rc == EIGSOL_OK) rc = up_(&f->wave_part, nullptr, (size_t)f->grid * dev::kWaves * sizeof(dev::part4));
+    if (rc == EIGSOL_OK) {
+        const uint32_t sent = (uint32_t)(dev::kSent & 0xffffffffu);
+        for (void* zb : f->z) hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st);
+        hipMemsetAsync(f->work, 0, 64, st);
+        hipMemsetAsync(f->err, 0, 64, st);
+        if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "factor upload");
+    }
+    if (rc != EIGSOL_OK) { shift_free(f); return rc; }
     f->kind = 0;
     *out = f;
     return EIGSOL_OK;
@@ -718,18 +734,19 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
     hipStream_t st = f->ctx->stream;
     if (f->kind == 0) {
         dev::TriArgs<S> a{};
-        a.rowptr = f->rowptr;
-        a.col = f->col;
-        a.val = static_cast<const S*>(f->val);
-        a.piv = static_cast<const S*>(f->piv);
         a.order = f->order;
-        a.npos = f->npos;
+        a.pptr = f->pptr;
+        a.pcol = f->pcol;
+        a.pval = static_cast<const S*>(f->pval);
+        a.ppiv = static_cast<const S*>(f->ppiv);
         a.nchunks = f->nchunks;
-        a.flags = f->flags;
+        a.n = f->n;
+        const int e = ++f->epoch;
+        a.zcur = static_cast<S*>(f->z[e & 1]);
+        a.znext = static_cast<S*>(f->z[(e + 1) & 1]);
         a.work = f->work;
         a.err = f->err;
-        a.epoch = ++f->epoch;
-        a.nclasses = f->nclasses;
+        a.wave_part = static_cast<dev::part4*>(f->wave_part);
         a.b_plain = static_cast<const S*>(b);
         a.y_plain = static_cast<S*>(y);
         a.buf0 = static_cast<S*>(buf0);
@@ -737,7 +754,6 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.ctl = ctl;
         a.rank_part = static_cast<const dev::part4*>(rank_part);
         a.my_part = static_cast<dev::part4*>(my_part);
-        a.chunk_part = static_cast<dev::part4*>(f->chunk_part);
         a.trace = static_cast<S*>(trace);
         a.sig_re = f->sig_re;
         a.sig_im = f->sig_im;
