@@ -192,3 +192,75 @@ def test_solve_shifted_triangular_large(ctx):
     A = sp.csr_matrix((v, ci, rp), shape=(n, n))
     r = A @ x - sigma * x - b
     assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(b)
+
+
+def test_session_rebegin_after_early_exit_launches(ctx):
+    """Launches enqueued after convergence exit early; they must still hand the next launch a
+    clean solve buffer (the solved values are the ready flags), so a second begin on the same
+    session reproduces a fresh one."""
+    n = 5000
+    rp, ci, v, _ = S.triu_complex(n, 16, seed=3)
+    target = 1.5 * np.exp(0.7j)
+    sigma = target + 2e-3
+    M = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sess = E.ShiftedSession(M, sigma)
+    opts = E.ShiftedSolverOptions(200, 1e-12, sigma)
+    results = []
+    for seed in (1, 2, 1):
+        x0 = S.start_vector(n, np.complex128, seed=seed)
+        sess.begin(opts, x0)
+        sess.step(60)                                     # far past convergence: no-op launches
+        assert sess.query()[0]
+        results.append(sess.finish())
+        ref = O.shifted_triu_csr(rp, ci, v, sigma, x0, 200, 1e-12, want_trace=True)
+        _parity(results[-1], ref, 1e-12)
+    assert results[0].eigenvalue == results[2].eigenvalue   # deterministic reductions
+    assert results[0].iterations == results[2].iterations
+    np.testing.assert_array_equal(results[0].eigenvector, results[2].eigenvector)
+    sess.close()
+
+
+@pytest.mark.parametrize("upper", [True, False])
+def test_solve_shifted_long_rows(ctx, upper):
+    """Rows longer than one 16-lane pass (up to 200 off-diagonal entries), both orientations."""
+    rng = np.random.default_rng(11)
+    n = 3000
+    rows, cols = [], []
+    for i in range(n):
+        k = int(rng.integers(0, 200)) if i % 7 == 0 else int(rng.integers(0, 12))
+        span = (n - 1 - i) if upper else i
+        k = min(k, span)
+        if k:
+            off = rng.choice(span, size=k, replace=False)
+            cols.append((i + 1 + off) if upper else off)
+            rows.append(np.full(k, i))
+    r = np.concatenate(rows + [np.arange(n)])
+    c = np.concatenate(cols + [np.arange(n)])
+    vals = rng.uniform(-1, 1, len(r)) * 0.02
+    vals[-n:] = rng.uniform(1, 2, n)
+    A = sp.csr_matrix((vals, (r, c)), shape=(n, n))
+    A.sort_indices()
+    b = rng.standard_normal(n)
+    x = E.solve_shifted(E.CsrMatrix.from_scipy(ctx, A), 0.25, b)
+    Ad = A.toarray() - 0.25 * np.eye(n)
+    xr = np.linalg.solve(Ad, b)
+    assert np.linalg.norm(x - xr) <= 1e-11 * np.linalg.norm(xr)
+
+
+def test_solve_shifted_nan_payloads_do_not_stall(ctx):
+    """A right-hand side carrying NaNs, one with the exact bit pattern the solver uses for
+    'not yet solved', still drains: NaN propagates to the dependent rows, the rest is exact."""
+    n = 2000
+    d = np.linspace(1.0, 2.0, n)
+    A = sp.diags([d, np.full(n - 1, 0.1)], [0, 1], format="csr")   # upper bidiagonal
+    b = np.ones(n)
+    sent = np.array([0x7FF4DEAD7FF4DEAD], dtype=np.uint64).view(np.float64)[0]
+    b[1000] = sent
+    b[1500] = np.nan
+    x = E.solve_shifted(E.CsrMatrix.from_scipy(ctx, A), 0.0, b)
+    # row i depends on rows > i: rows <= 1500 see a NaN, rows > 1500 are finite and exact
+    assert np.all(np.isnan(x[:1501]))
+    bb = b.copy()
+    bb[:1501] = 0.0
+    xr = np.linalg.solve(A.toarray(), bb)
+    np.testing.assert_allclose(x[1501:], xr[1501:], rtol=1e-13)
