@@ -139,7 +139,8 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes_per_iteration, int32
                              int32_t* tiles, int32_t* variant);
 /* variant: 0 = CSR, x gathered from HBM; 1 = CSR, x window staged in LDS; 2 = dense GEMV;
  *          3 = shifted inverse, sync-free triangular solve (tiles = dependency levels);
- *          4 = shifted inverse, dense LU substitution */
+ *          4 = shifted inverse, dense LU substitution;
+ *          5 = CSR in 64-row slices, one row per lane (tiles = slices) */
 
 /* ---------------------------------------------------------------- shifted inverse iteration
  * shiftedInversePowerMethod<S>(M, ShiftedSolverOptions<S>{sigma, maxIter, tol})

@@ -233,7 +233,8 @@ class PowerSession:
         call("eigsol_power_kernel_info", self.handle, C.byref(b), C.byref(g), C.byref(t), C.byref(v))
         names = {0: "csr_kernel (x gathered from HBM)", 1: "csr_win_kernel (x window staged in LDS)",
                  2: "dense_kernel (GEMV)", 3: "sptrsv_kernel (sync-free triangular solve)",
-                 4: "dense_lu_solve_kernel (LU substitution)"}
+                 4: "dense_lu_solve_kernel (LU substitution)",
+                 5: "csr_slice_kernel (64-row slices, one row per lane)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?")}
 

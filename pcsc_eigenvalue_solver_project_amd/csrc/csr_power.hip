@@ -68,6 +68,13 @@ struct CsrArgs {
     const int32_t* col;
     const uint16_t* col16;   // windowed matrices: column - tile window start (< kWin)
     const S* val;
+    // sliced layout (csr_slice_kernel): 64 rows per slice, entry (k, lane) at off + 64 k + lane
+    const int4* slice_meta;  // per slice {entry offset, window start (-1: gather slice), K | ragged << 8, window length}
+    const S* sval;
+    const uint32_t* scol8;   // window slices: column - window start, 8 bits, 4 entries per lane-dword
+    const int32_t* scol32;   // gather slices: x-space column
+    const uint8_t* slen;     // row lengths (read for ragged slices only)
+    int32_t nslices;
     const int4* tile_meta;   // per tile {r0, r1, e0, e1}: short tiles first, then long rows
     const int2* tile_win;    // per short tile: x window [w0, w1] covering its columns and rows
     int32_t ntiles;
@@ -635,6 +642,169 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
     }
 }
 
+// ============================================================================ sliced pipeline
+// Rows in slices of 64, one row per lane.  Values are stored slice by slice in (k, lane) order, so
+// every value load is one coalesced 64-lane access and each lane sums its own row in ascending
+// column order (the reference's order) in registers: no LDS product round trip and no block
+// barrier.  A slice whose x window (its columns and its own rows) spans at most kSliceWin entries
+// stages the window, scaled once per element, in a wave-private LDS region, and streams 8-bit
+// window offsets packed four per lane-dword; other slices gather x from global memory with int32
+// columns.  Slices are taken XCD-contiguously like the tiles of the other kernels.
+// meta per slice: {value entry offset, window start (-1: gather slice), K | ragged << 8 | wl << 9,
+//                  column offset (dwords of packed 8-bit offsets, or int32 entries)}
+constexpr int kSliceRows = 64;
+constexpr int kSliceMaxK = 64;
+constexpr int kSliceWin = 256;
+
+template <class S, int KB>
+struct SliceRegs {
+    static constexpr int NW = kSliceWin / 64;
+    S v[KB];
+    uint32_t c[KB];   // window slices: packed 8-bit offsets in c[0 .. KB/4); gather slices: columns
+    S w[NW];
+    int len;          // the lane's row length
+};
+
+// Every load of one slice's first KB entries, its window and the row lengths.  Loads are clamped
+// (to entry K-1, window entry wl-1): same cache lines, no extra bytes, no exec-masked loads.
+template <class S, int KB>
+__device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, int slice, int4 m,
+                                            SliceRegs<S, KB>& R) {
+    const int lane = threadIdx.x & 63;
+    const int K = m.z & 0xff;
+    const uint32_t base = (uint32_t)m.x + (uint32_t)lane;
+    R.len = K;
+    if (m.z & 0x100) R.len = a.slen[min(slice * kSliceRows + lane, a.nrows - 1)];
+    if (m.y >= 0) {
+        // the window always holds the slice's own rows: loaded even for an all-empty slice
+        const int wl = max((m.z >> 9) & 0x1ff, 1);
+#pragma unroll
+        for (int j = 0; j < SliceRegs<S, KB>::NW; ++j)
+            R.w[j] = ldg(xin, (uint32_t)(m.y + min(lane + 64 * j, wl - 1)));
+    }
+    if (K == 0) return;                         // no entries: nothing to stream (uniform)
+#pragma unroll
+    for (int u = 0; u < KB; ++u) R.v[u] = ldg(a.sval, base + 64u * (uint32_t)min(u, K - 1));
+    if (m.y >= 0) {
+        const int nw = (K + 3) >> 2;
+#pragma unroll
+        for (int g = 0; g < KB / 4; ++g)
+            R.c[g] = ldg(a.scol8, (uint32_t)m.w + 64u * (uint32_t)min(g, nw - 1) + (uint32_t)lane);
+    } else {
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+            R.c[u] = (uint32_t)ldg(a.scol32, (uint32_t)m.w + 64u * (uint32_t)min(u, K - 1) + (uint32_t)lane);
+    }
+}
+
+template <class S, bool kPower, int KB>
+__global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int parity) {
+    __shared__ S xw_all[kWaves][kSliceWin];
+    __shared__ double sm[3 * kWaves];
+    __shared__ Prologue pro;
+    __shared__ int s_last;
+
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kPower) {
+        power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = (parity ? a.buf1 : a.buf0) + a.xoff;   // y rows land at their x-space slots
+    } else {
+        xin = a.x_plain;
+        yout = a.y_plain;
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    S* xw = xw_all[wave];
+    double n2 = 0.0, rr = 0.0, ri = 0.0;
+
+    const int wpg = (gridDim.x >> 3) * kWaves;          // waves per XCD group (grid % 8 == 0)
+    const int chunk = (a.nslices + 7) >> 3;
+    const int sbeg = (blockIdx.x & 7) * chunk;
+    const int send = min(a.nslices, sbeg + chunk);
+    int sl = sbeg + (blockIdx.x >> 3) * kWaves + wave;
+    int4 m = ld_uniform(a.slice_meta, min(sl, max(send - 1, 0)));
+    for (; sl < send; sl += wpg) {
+        SliceRegs<S, KB> R;
+        slice_issue<S, KB>(a, xin, sl, m, R);
+        const int4 mc = m;
+        m = ld_uniform(a.slice_meta, min(sl + wpg, send - 1));   // next slice's metadata, early
+        const int K = mc.z & 0xff;
+        const int row = sl * kSliceRows + lane;
+        const bool valid = row < a.nrows;
+        const int rowc = valid ? row : a.nrows - 1;
+        S sacc = s_zero<S>();
+        S xi = s_zero<S>();
+        if (mc.y >= 0) {
+            const int w0 = mc.y, wl = (mc.z >> 9) & 0x1ff;
+#pragma unroll
+            for (int j = 0; j < SliceRegs<S, KB>::NW; ++j) {
+                S v = R.w[j];
+                if constexpr (kPower) v = scale_in(v, nrm);
+                if (lane + 64 * j < wl) xw[lane + 64 * j] = v;
+            }
+            // wave-private region: LDS executes one wave's accesses in order; the fences only
+            // keep the compiler from moving the reads above the stores
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int u = 0; u < KB; ++u) {
+                const S pr = mul(R.v[u], xw[(R.c[u >> 2] >> (8 * (u & 3))) & 0xffu]);
+                if (u < R.len) sacc = add(sacc, pr);
+            }
+            for (int k0 = KB; k0 < K; k0 += 4) {       // rows longer than KB entries
+                const uint32_t cw = ldg(a.scol8, (uint32_t)mc.w + 64u * (uint32_t)(k0 >> 2) + (uint32_t)lane);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const S pr = mul(ldg(a.sval, (uint32_t)mc.x + (uint32_t)lane + 64u * (uint32_t)min(k0 + u, K - 1)),
+                                     xw[(cw >> (8 * u)) & 0xffu]);
+                    if (k0 + u < R.len) sacc = add(sacc, pr);
+                }
+            }
+            if constexpr (kPower) xi = xw[min(max(rowc + a.xoff - w0, 0), wl - 1)];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        } else if (K > 0) {
+            S xv[KB];
+#pragma unroll
+            for (int u = 0; u < KB; ++u) xv[u] = ldg(xin, R.c[u]);
+#pragma unroll
+            for (int u = 0; u < KB; ++u) {
+                S x = xv[u];
+                if constexpr (kPower) x = scale_in(x, nrm);
+                const S pr = mul(R.v[u], x);
+                if (u < R.len) sacc = add(sacc, pr);
+            }
+            for (int k0 = KB; k0 < K; ++k0) {
+                const uint32_t q = (uint32_t)lane + 64u * (uint32_t)k0;
+                S x = ldg(xin, (uint32_t)ldg(a.scol32, (uint32_t)mc.w + q));
+                if constexpr (kPower) x = scale_in(x, nrm);
+                const S pr = mul(ldg(a.sval, (uint32_t)mc.x + q), x);
+                if (k0 < R.len) sacc = add(sacc, pr);
+            }
+            if constexpr (kPower) xi = scale_in(xin[rowc + a.xoff], nrm);
+        } else if constexpr (kPower) {
+            xi = scale_in(xin[rowc + a.xoff], nrm);
+        }
+        if (valid) {
+            yout[row] = sacc;
+            if constexpr (kPower) {
+                n2 += sq_abs(sacc);
+                acc_dot(rr, ri, xi, sacc);
+            }
+        }
+    }
+    if constexpr (kPower) {
+        block_sum3(n2, rr, ri, sm);
+        last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+    }
+}
+
 // ||x||^2 partials of the start vector (x.normalize(), power_method.hpp:62).
 template <class S>
 __global__ __launch_bounds__(kThreads) void norm_partial_kernel(const S* x, int64_t n, PowerCtl* ctl,
@@ -678,6 +848,8 @@ void csr_release(eigsol_csr* A) {
     if (A->val) (void)hipFree(A->val);
     if (A->tile_meta) (void)hipFree(A->tile_meta);
     if (A->tile_win) (void)hipFree(A->tile_win);
+    for (void* q : {(void*)A->slice_meta, A->sval, (void*)A->scol8, (void*)A->scol32, (void*)A->slen})
+        if (q) (void)hipFree(q);
     if (A->send_idx) (void)hipFree(A->send_idx);
     if (A->send_buf) (void)hipFree(A->send_buf);
     eigsol_ctx* c = A->ctx;
@@ -741,6 +913,85 @@ static int build_tiles(const int32_t* rowptr, const int32_t* col, int64_t nrows,
     return (int)(nshort + longs.size() / 4);
 }
 
+// Sliced layout: slices of 64 rows, K_s = longest row of the slice, value entry (k, lane) at
+// off_s + 64 k + lane (padding entries: value 0, masked by the row length).  Columns: window
+// slices hold 8-bit offsets from the window start, entry (k, lane) in byte k % 4 of dword
+// coff_s + 64 (k / 4) + lane; gather slices hold int32 x-space columns at goff_s + 64 k + lane.
+// Used when every row has at most kSliceMaxK entries and padding adds at most 1/8 of the entries.
+struct SliceLayout {
+    std::vector<int32_t> meta;
+    std::vector<unsigned char> val;
+    std::vector<uint32_t> c8;
+    std::vector<int32_t> c32;
+    std::vector<uint8_t> len;
+    int maxk = 0;
+};
+
+static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* values, size_t sb,
+                         int64_t nrows, int64_t nnz, int64_t xoff, SliceLayout& L) {
+    if (nrows == 0) return false;
+    const int64_t ns = (nrows + kSliceRows - 1) / kSliceRows;
+    int64_t total = 0, ctot8 = 0, ctot32 = 0;
+    bool any_ragged = false;
+    L.meta.assign(4 * ns, 0);
+    for (int64_t s = 0; s < ns; ++s) {
+        const int64_t r0 = s * kSliceRows, r1 = std::min<int64_t>(nrows, r0 + kSliceRows);
+        int K = 0, kmin = INT32_MAX;
+        int32_t w0 = (int32_t)(r0 + xoff), w1 = (int32_t)(r1 - 1 + xoff);
+        for (int64_t r = r0; r < r1; ++r) {
+            const int l = rowptr[r + 1] - rowptr[r];
+            if (l > kSliceMaxK) return false;
+            K = std::max(K, l);
+            kmin = std::min(kmin, l);
+            for (int32_t e = rowptr[r]; e < rowptr[r + 1]; ++e) {
+                w0 = std::min(w0, col[e]);
+                w1 = std::max(w1, col[e]);
+            }
+        }
+        const bool ragged = kmin != K || (r1 - r0) != kSliceRows;
+        const int64_t wl = (int64_t)w1 - w0 + 1;
+        const bool win = wl <= kSliceWin;
+        any_ragged |= ragged;
+        L.maxk = std::max(L.maxk, K);
+        L.meta[4 * s] = (int32_t)total;
+        L.meta[4 * s + 1] = win ? w0 : -1;
+        L.meta[4 * s + 2] = K | (ragged ? 0x100 : 0) | (win ? (int32_t)(wl << 9) : 0);
+        L.meta[4 * s + 3] = (int32_t)(win ? ctot8 : ctot32);
+        total += (int64_t)K * kSliceRows;
+        if (win) ctot8 += (int64_t)((K + 3) / 4) * kSliceRows;
+        else ctot32 += (int64_t)K * kSliceRows;
+        if (total > nnz + nnz / 8 + 64 * kSliceRows || total >= (int64_t(1) << 31) / (int64_t)sb) return false;
+    }
+    L.val.assign((size_t)std::max<int64_t>(total, 1) * sb, 0);
+    if (ctot8) L.c8.assign((size_t)ctot8, 0);
+    if (ctot32) L.c32.assign((size_t)ctot32, 0);
+    if (any_ragged) L.len.assign((size_t)nrows, 0);
+    for (int64_t s = 0; s < ns; ++s) {
+        const int64_t r0 = s * kSliceRows, r1 = std::min<int64_t>(nrows, r0 + kSliceRows);
+        const int64_t off = L.meta[4 * s], coff = L.meta[4 * s + 3];
+        const int32_t w0 = L.meta[4 * s + 1];
+        const int K = L.meta[4 * s + 2] & 0xff;
+        for (int64_t r = r0; r < r1; ++r) {
+            const int64_t lane = r - r0;
+            const int l = rowptr[r + 1] - rowptr[r];
+            if (any_ragged) L.len[r] = (uint8_t)l;
+            for (int k = 0; k < l; ++k) {
+                const int32_t e = rowptr[r] + k;
+                const size_t q = (size_t)(off + (int64_t)k * kSliceRows + lane);
+                std::memcpy(&L.val[q * sb], (const unsigned char*)values + (size_t)e * sb, sb);
+                if (w0 >= 0)
+                    L.c8[(size_t)(coff + (int64_t)(k / 4) * kSliceRows + lane)] |= (uint32_t)(col[e] - w0) << (8 * (k % 4));
+                else
+                    L.c32[(size_t)(coff + (int64_t)k * kSliceRows + lane)] = col[e];
+            }
+            // padding: offset 0 is in the window; gather padding reads the row's own x entry
+            if (w0 < 0)
+                for (int k = l; k < K; ++k) L.c32[(size_t)(coff + (int64_t)k * kSliceRows + lane)] = (int32_t)(r + xoff);
+        }
+    }
+    return true;
+}
+
 // xoff: x-space index of local row 0 (0 on one GPU; the lower-ghost count when row-sharded)
 int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t nnz,
                const int32_t* rowptr, const int32_t* colidx, const void* values, eigsol_csr** out,
@@ -781,6 +1032,11 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
                                    cx ? Win<cplx>::kWin : Win<double>::kWin, meta, win, nshort,
                                    max_rows, windowed);
     if (const char* env = std::getenv("EIGSOL_CSR_NO_WINDOW")) if (std::atoi(env)) windowed = 0;
+    SliceLayout SL;
+    bool sliced = true;
+    if (const char* env = std::getenv("EIGSOL_CSR_NO_SLICE")) if (std::atoi(env)) sliced = false;
+    if (sliced)
+        sliced = build_slices(rowptr, col_use, val_use, sb, nrows, nnz, xoff, SL);
 
     // the kernels index every stream with 32-bit byte offsets (ldg): one device's rows must keep
     // values, columns and vectors under 4 GiB each (shard larger matrices over ranks)
@@ -799,6 +1055,9 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     A->xoff = xoff;
     A->windowed = windowed;
     A->max_tile_rows = max_rows;
+    A->sliced = sliced ? 1 : 0;
+    A->nslices = sliced ? (int32_t)(SL.meta.size() / 4) : 0;
+    A->slice_kb = SL.maxk <= 4 ? 4 : SL.maxk <= 8 ? 8 : SL.maxk <= 12 ? 12 : 16;
     const size_t pad = (size_t)(dtype == EIGSOL_C128 ? Tile<cplx>::kNnz : Tile<double>::kNnz) + 8;   // branch-free tile loads
     auto cleanup = [&]() { csr_release(A); };
     hipError_t e;
@@ -822,7 +1081,7 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
         cleanup();
         return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: upload: ") + hipGetErrorString(e));
     }
-    if (windowed) {
+    if (windowed && !sliced) {
         // 16-bit window-relative columns of the short tiles (long rows keep using int32 columns)
         std::vector<uint16_t> c16((size_t)(nnz + pad), 0);
         for (int32_t t = 0; t < nshort; ++t) {
@@ -834,6 +1093,22 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
             (e = hipStreamSynchronize(s)) != hipSuccess) {
             cleanup();
             return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: upload: ") + hipGetErrorString(e));
+        }
+    }
+    if (A->sliced) {
+        auto upl = [&](void** dst, const void* src, size_t bytes) -> hipError_t {
+            hipError_t r = hipMalloc(dst, std::max<size_t>(bytes, 16));
+            if (r == hipSuccess && bytes) r = hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, s);
+            return r;
+        };
+        if ((e = upl((void**)&A->slice_meta, SL.meta.data(), SL.meta.size() * 4)) != hipSuccess ||
+            (e = upl(&A->sval, SL.val.data(), SL.val.size())) != hipSuccess ||
+            (!SL.c8.empty() && (e = upl((void**)&A->scol8, SL.c8.data(), SL.c8.size() * 4)) != hipSuccess) ||
+            (!SL.c32.empty() && (e = upl((void**)&A->scol32, SL.c32.data(), SL.c32.size() * 4)) != hipSuccess) ||
+            (!SL.len.empty() && (e = upl((void**)&A->slen, SL.len.data(), SL.len.size())) != hipSuccess) ||
+            (e = hipStreamSynchronize(s)) != hipSuccess) {
+            cleanup();
+            return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: slice upload: ") + hipGetErrorString(e));
         }
     }
     *out = A;
@@ -879,13 +1154,23 @@ static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, in
 
 template <class S>
 static const void* power_kernel_ptr(const eigsol_csr* A) {
+    if (A->sliced) {
+        switch (A->slice_kb) {
+            case 4: return reinterpret_cast<const void*>(csr_slice_kernel<S, true, 4>);
+            case 8: return reinterpret_cast<const void*>(csr_slice_kernel<S, true, 8>);
+            case 12: return reinterpret_cast<const void*>(csr_slice_kernel<S, true, 12>);
+            default: return reinterpret_cast<const void*>(csr_slice_kernel<S, true, 16>);
+        }
+    }
     return A->windowed ? reinterpret_cast<const void*>(csr_win_kernel<S, true>)
                        : reinterpret_cast<const void*>(csr_kernel<S, true>);
 }
 
 int csr_grid(eigsol_csr* A, int* grid) {
     const void* k = A->dtype == EIGSOL_C128 ? power_kernel_ptr<cplx>(A) : power_kernel_ptr<double>(A);
-    return resident_grid(A->ctx, k, A->ntiles, grid);
+    // work units: tiles (one per block step) or slices (one per wave step)
+    const int64_t units = A->sliced ? (A->nslices + kWaves - 1) / kWaves : A->ntiles;
+    return resident_grid(A->ctx, k, units, grid);
 }
 
 template <class S>
@@ -897,6 +1182,12 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     a.val = (const S*)A->val;
     a.tile_meta = (const int4*)A->tile_meta;
     a.tile_win = (const int2*)A->tile_win;
+    a.slice_meta = (const int4*)A->slice_meta;
+    a.sval = (const S*)A->sval;
+    a.scol8 = A->scol8;
+    a.scol32 = A->scol32;
+    a.slen = A->slen;
+    a.nslices = A->nslices;
     a.ntiles = A->ntiles;
     a.nshort = A->nshort;
     a.xlen = (int32_t)xlen;
@@ -913,7 +1204,7 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
         return e ? std::atoi(e) : 0;
     }();
     if constexpr (std::is_same_v<S, double>) {
-        if (power && mode > 0 && !A->windowed) {
+        if (power && mode > 0 && !A->windowed && !A->sliced) {
             if (mode == 1) hipLaunchKernelGGL((csr_kernel<S, true, 1>), dim3(grid), dim3(kThreads), 0, s, args, parity);
             else if (mode == 2) hipLaunchKernelGGL((csr_kernel<S, true, 2>), dim3(grid), dim3(kThreads), 0, s, args, parity);
             else hipLaunchKernelGGL((csr_kernel<S, true, 3>), dim3(grid), dim3(kThreads), 0, s, args, parity);
@@ -921,7 +1212,18 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
             return EIGSOL_OK;
         }
     }
-    if (A->windowed) {
+    if (A->sliced) {
+#define EIGSOL_SLICE_LAUNCH(KB)                                                                              \
+    if (power) hipLaunchKernelGGL((csr_slice_kernel<S, true, KB>), dim3(grid), dim3(kThreads), 0, s, args, parity); \
+    else hipLaunchKernelGGL((csr_slice_kernel<S, false, KB>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+        switch (A->slice_kb) {
+            case 4: EIGSOL_SLICE_LAUNCH(4) break;
+            case 8: EIGSOL_SLICE_LAUNCH(8) break;
+            case 12: EIGSOL_SLICE_LAUNCH(12) break;
+            default: EIGSOL_SLICE_LAUNCH(16) break;
+        }
+#undef EIGSOL_SLICE_LAUNCH
+    } else if (A->windowed) {
         if (power) hipLaunchKernelGGL((csr_win_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);
         else hipLaunchKernelGGL((csr_win_kernel<S, false>), dim3(grid), dim3(kThreads), 0, s, args, parity);
     } else {

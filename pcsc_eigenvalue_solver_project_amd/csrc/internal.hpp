@@ -186,6 +186,15 @@ struct eigsol_csr {
     int32_t ntiles = 0;
     int32_t max_tile_rows = 0;
     int32_t nshort = 0;            // tiles [0, nshort) are short; the rest hold one long row each
+    // sliced layout (csr_slice_kernel, preferred when every row has <= 64 entries)
+    int32_t sliced = 0;
+    int32_t nslices = 0;
+    int32_t* slice_meta = nullptr; // device, 4 ints per slice
+    void* sval = nullptr;          // device, 64 * K_s entries per slice
+    uint32_t* scol8 = nullptr;     // device (window slices): 8-bit offsets, 4 per lane-dword
+    int32_t slice_kb = 16;         // entries per row held in registers (kernel instantiation)
+    int32_t* scol32 = nullptr;     // device (gather slices)
+    uint8_t* slen = nullptr;       // device, per row (ragged slices)
     // Row-sharded (multi-GPU) layout: this rank owns global rows [row_begin, row_begin + nrows);
     // local columns are [own rows | ghosts grouped by owner rank, ascending global index].
     int dist = 0;

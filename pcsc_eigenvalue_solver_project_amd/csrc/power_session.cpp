@@ -305,8 +305,8 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
         // values + int32 columns + int32 row pointers + x read once + y written once
         const double nnz = (double)s->csr->nnz, n = (double)s->csr->nrows;
         if (bytes) *bytes = (sb + 4.0) * nnz + 4.0 * (n + 1.0) + 2.0 * sb * n;
-        if (tiles) *tiles = s->csr->ntiles;
-        if (variant) *variant = s->csr->windowed ? 1 : 0;
+        if (tiles) *tiles = s->csr->sliced ? s->csr->nslices : s->csr->ntiles;
+        if (variant) *variant = s->csr->sliced ? 5 : (s->csr->windowed ? 1 : 0);
     } else {
         const double n = (double)s->dense->nrows;
         if (bytes) *bytes = sb * n * n + 2.0 * sb * n;

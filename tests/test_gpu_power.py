@@ -249,3 +249,56 @@ def test_data_A_txt_as_double(ctx):
     ref = O.power_dense(Amat, x0, 1000, 1e-10, want_trace=True)
     _assert_power_parity(res, ref, 1e-10)
     assert abs(res.eigenvalue - (1 + np.sqrt(15))) < 1e-8
+
+
+def _slice_mix(n, dtype, seed=21):
+    """Rows shaped to exercise every case of the sliced layout: uniform band slices (8-bit window
+    offsets), a slice of empty rows, a slice with columns spread over the whole matrix (gather
+    slice), ragged slices with a few short rows, and one slice holding a 60-entry row (row
+    longer than the entries a lane keeps in registers)."""
+    rng = np.random.default_rng(seed)
+    rows, cols = [], []
+    for i in range(n):
+        s = i // 64
+        if s == 10:
+            continue                                          # an all-empty slice
+        if s == 20:
+            c = np.sort(rng.choice(n, size=10, replace=False))  # wide window: gather slice
+        elif s == 30 and i % 64 == 5:
+            lo = max(0, min(i - 100, n - 200))
+            c = np.sort(rng.choice(np.arange(lo, lo + 200), size=60, replace=False))
+        else:
+            k = 10 if (s % 7 != 3 or i % 5) else 7               # ragged slices: some 7-entry rows
+            lo = max(0, min(i - 40, n - 81))
+            c = np.sort(rng.choice(np.arange(lo, lo + 81), size=k, replace=False))
+        rows.append(np.full(len(c), i))
+        cols.append(c)
+    rows = np.concatenate(rows)
+    cols = np.concatenate(cols)
+    vals = rng.uniform(-1, 1, len(rows))
+    if dtype == np.complex128:
+        vals = vals + 1j * rng.uniform(-1, 1, len(rows))
+    M = sp.csr_matrix((vals, (rows, cols)), shape=(n, n)).tolil()
+    M[n // 2, n // 2] = 10.0                                  # a dominant eigenvalue near 10
+    M = M.tocsr()
+    M.sort_indices()
+    return M
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_slice_layout_mix_bitwise_and_power(ctx, dtype):
+    n = 64 * 40 + 17                                          # a partial last slice
+    M = _slice_mix(n, dtype)
+    A = E.CsrMatrix.from_scipy(ctx, M)
+    x = S.start_vector(n, dtype)
+    y = _spmv_gpu(ctx, A, x)
+    cp, ri, vv = O.csr_to_csc(M.indptr, M.indices, M.data, n)
+    y_ref = O.spmv_csc(cp, ri, vv, x, n)
+    assert np.array_equal(y, y_ref), np.max(np.abs(y - y_ref))
+    sess = E.PowerSession(A)
+    assert sess.kernel_info()["variant"] == 5                # the sliced kernel ran
+    sess.close()
+    tol = 1e-12
+    res = E.power_method(A, E.SolverOptions(3000, tol), x)
+    ref = O.power_csc(cp, ri, vv, x, 3000, tol, want_trace=True)
+    _assert_power_parity(res, ref, tol)
