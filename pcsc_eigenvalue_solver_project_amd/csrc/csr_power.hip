@@ -658,12 +658,29 @@ constexpr int kSliceWin = 256;
 
 template <class S, int KB>
 struct SliceRegs {
-    static constexpr int NW = kSliceWin / 64;
-    S v[KB];
+    // window loads: f64 in 16-byte pairs (window start even, length even), complex one per lane
+    static constexpr int NW = std::is_same_v<S, double> ? kSliceWin / 128 : kSliceWin / 64;
+    using WT = std::conditional_t<std::is_same_v<S, double>, double2, S>;
+    // f64 values are stored in lane pairs (entries 2j, 2j+1 of a row adjacent): 16-byte loads
+    static constexpr int NV = std::is_same_v<S, double> ? KB / 2 : KB;
+    using VT = std::conditional_t<std::is_same_v<S, double>, double2, S>;
+    VT v[NV];
     uint32_t c[KB];   // window slices: packed 8-bit offsets in c[0 .. KB/4); gather slices: columns
-    S w[NW];
+    WT w[NW];
     int len;          // the lane's row length
 };
+
+template <class S, int KB>
+__device__ __forceinline__ S slice_val(const SliceRegs<S, KB>& R, int u) {
+    if constexpr (std::is_same_v<S, double>) return (u & 1) ? R.v[u >> 1].y : R.v[u >> 1].x;
+    else return R.v[u];
+}
+// stream index of entry (k, lane) of a slice whose values start at off
+template <class S>
+__device__ __forceinline__ uint32_t slice_entry(uint32_t off, int k, int lane) {
+    if constexpr (std::is_same_v<S, double>) return off + 128u * (uint32_t)(k >> 1) + 2u * (uint32_t)lane + (uint32_t)(k & 1);
+    else return off + 64u * (uint32_t)k + (uint32_t)lane;
+}
 
 // Every load of one slice's first KB entries, its window and the row lengths.  Loads are clamped
 // (to entry K-1, window entry wl-1): same cache lines, no extra bytes, no exec-masked loads.
@@ -671,25 +688,36 @@ template <class S, int KB>
 __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, int slice, int4 m,
                                             SliceRegs<S, KB>& R) {
     const int lane = threadIdx.x & 63;
-    const int K = m.z & 0xff;
+    // K = 0 (all rows empty) clamps to entry 0 of the slice: the streams carry one slice of
+    // padding past their end, so even an empty last slice loads in bounds
+    const int K = max(m.z & 0xff, 1);
     const uint32_t base = (uint32_t)m.x + (uint32_t)lane;
-    R.len = K;
+    R.len = m.z & 0xff;
     if (m.z & 0x100) R.len = a.slen[min(slice * kSliceRows + lane, a.nrows - 1)];
-    if (m.y >= 0) {
-        // the window always holds the slice's own rows: loaded even for an all-empty slice
-        const int wl = max((m.z >> 9) & 0x1ff, 1);
+    if constexpr (std::is_same_v<S, double>) {
+        const int K2 = (K + 1) >> 1;
+        const uint32_t b2 = ((uint32_t)m.x >> 1) + (uint32_t)lane;
 #pragma unroll
-        for (int j = 0; j < SliceRegs<S, KB>::NW; ++j)
-            R.w[j] = ldg(xin, (uint32_t)(m.y + min(lane + 64 * j, wl - 1)));
+        for (int j = 0; j < SliceRegs<S, KB>::NV; ++j)
+            R.v[j] = ldg(reinterpret_cast<const double2*>(a.sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
+    } else {
+#pragma unroll
+        for (int u = 0; u < KB; ++u) R.v[u] = ldg(a.sval, base + 64u * (uint32_t)min(u, K - 1));
     }
-    if (K == 0) return;                         // no entries: nothing to stream (uniform)
-#pragma unroll
-    for (int u = 0; u < KB; ++u) R.v[u] = ldg(a.sval, base + 64u * (uint32_t)min(u, K - 1));
     if (m.y >= 0) {
         const int nw = (K + 3) >> 2;
 #pragma unroll
         for (int g = 0; g < KB / 4; ++g)
             R.c[g] = ldg(a.scol8, (uint32_t)m.w + 64u * (uint32_t)min(g, nw - 1) + (uint32_t)lane);
+        // the window always holds the slice's own rows (the Rayleigh term reads them)
+        const int wl = max((m.z >> 9) & 0x1ff, 1);
+#pragma unroll
+        for (int j = 0; j < SliceRegs<S, KB>::NW; ++j)
+            if constexpr (std::is_same_v<S, double>)
+                R.w[j] = ldg(reinterpret_cast<const double2*>(xin),
+                             (uint32_t)((m.y >> 1) + min(lane + 64 * j, (wl >> 1) - 1)));
+            else
+                R.w[j] = ldg(xin, (uint32_t)(m.y + min(lane + 64 * j, wl - 1)));
     } else {
 #pragma unroll
         for (int u = 0; u < KB; ++u)
@@ -697,9 +725,94 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
     }
 }
 
+// Row sums of one slice from its registers (window slices: x from the wave's LDS window).
+template <class S, bool kPower, int KB>
+__device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin, S* yout, double nrm,
+                                              const SliceRegs<S, KB>& R, int4 mc, int sl, S* xw,
+                                              double& n2, double& rr, double& ri) {
+    const int lane = threadIdx.x & 63;
+    const int K = mc.z & 0xff;
+    const int row = sl * kSliceRows + lane;
+    const bool valid = row < a.nrows;
+    const int rowc = valid ? row : a.nrows - 1;
+    S sacc = s_zero<S>();
+    S xi = s_zero<S>();
+    if (mc.y >= 0) {
+        const int w0 = mc.y, wl = (mc.z >> 9) & 0x1ff;
+#pragma unroll
+        for (int j = 0; j < SliceRegs<S, KB>::NW; ++j) {
+            if constexpr (std::is_same_v<S, double>) {
+                double2 v = R.w[j];
+                if constexpr (kPower) {
+                    v.x = scale_in(v.x, nrm);
+                    v.y = scale_in(v.y, nrm);
+                }
+                if (2 * (lane + 64 * j) < wl) *reinterpret_cast<double2*>(xw + 2 * (lane + 64 * j)) = v;
+            } else {
+                S v = R.w[j];
+                if constexpr (kPower) v = scale_in(v, nrm);
+                if (lane + 64 * j < wl) xw[lane + 64 * j] = v;
+            }
+        }
+        // wave-private region: LDS executes one wave's accesses in order; the fences only keep
+        // the compiler from moving the reads above the stores
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const S pr = mul(slice_val(R, u), xw[(R.c[u >> 2] >> (8 * (u & 3))) & 0xffu]);
+            if (u < R.len) sacc = add(sacc, pr);
+        }
+        for (int k0 = KB; k0 < K; k0 += 4) {       // rows longer than KB entries
+            const uint32_t cw = ldg(a.scol8, (uint32_t)mc.w + 64u * (uint32_t)(k0 >> 2) + (uint32_t)lane);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const S pr = mul(ldg(a.sval, slice_entry<S>((uint32_t)mc.x, min(k0 + u, K - 1), lane)),
+                                 xw[(cw >> (8 * u)) & 0xffu]);
+                if (k0 + u < R.len) sacc = add(sacc, pr);
+            }
+        }
+        if constexpr (kPower) xi = xw[min(max(rowc + a.xoff - w0, 0), wl - 1)];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        S xv[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) xv[u] = ldg(xin, R.c[u]);
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            S x = xv[u];
+            if constexpr (kPower) x = scale_in(x, nrm);
+            const S pr = mul(slice_val(R, u), x);
+            if (u < R.len) sacc = add(sacc, pr);
+        }
+        for (int k0 = KB; k0 < K; ++k0) {
+            const uint32_t q = (uint32_t)lane + 64u * (uint32_t)k0;
+            S x = ldg(xin, (uint32_t)ldg(a.scol32, (uint32_t)mc.w + q));
+            if constexpr (kPower) x = scale_in(x, nrm);
+            const S pr = mul(ldg(a.sval, slice_entry<S>((uint32_t)mc.x, k0, lane)), x);
+            if (k0 < R.len) sacc = add(sacc, pr);
+        }
+        if constexpr (kPower) xi = scale_in(xin[rowc + a.xoff], nrm);
+    }
+    if (valid) {
+        yout[row] = sacc;
+        if constexpr (kPower) {
+            n2 += sq_abs(sacc);
+            acc_dot(rr, ri, xi, sacc);
+        }
+    }
+}
+
+#ifndef EIGSOL_SLICE_NS
+#define EIGSOL_SLICE_NS 2
+#endif
+constexpr int kSliceNS = EIGSOL_SLICE_NS;   // slices a wave has in flight at once
+
 template <class S, bool kPower, int KB>
 __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int parity) {
-    __shared__ S xw_all[kWaves][kSliceWin];
+    __shared__ __align__(16) S xw_all[kWaves][kSliceNS][kSliceWin];
     __shared__ double sm[3 * kWaves];
     __shared__ Prologue pro;
     __shared__ int s_last;
@@ -717,87 +830,27 @@ __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int p
         xin = a.x_plain;
         yout = a.y_plain;
     }
-    const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    S* xw = xw_all[wave];
     double n2 = 0.0, rr = 0.0, ri = 0.0;
 
+    // XCD-contiguous slice ranges; each wave takes kSliceNS slices (wpg apart) per round, all
+    // of whose loads are issued before any of them is consumed
     const int wpg = (gridDim.x >> 3) * kWaves;          // waves per XCD group (grid % 8 == 0)
     const int chunk = (a.nslices + 7) >> 3;
     const int sbeg = (blockIdx.x & 7) * chunk;
     const int send = min(a.nslices, sbeg + chunk);
-    int sl = sbeg + (blockIdx.x >> 3) * kWaves + wave;
-    int4 m = ld_uniform(a.slice_meta, min(sl, max(send - 1, 0)));
-    for (; sl < send; sl += wpg) {
-        SliceRegs<S, KB> R;
-        slice_issue<S, KB>(a, xin, sl, m, R);
-        const int4 mc = m;
-        m = ld_uniform(a.slice_meta, min(sl + wpg, send - 1));   // next slice's metadata, early
-        const int K = mc.z & 0xff;
-        const int row = sl * kSliceRows + lane;
-        const bool valid = row < a.nrows;
-        const int rowc = valid ? row : a.nrows - 1;
-        S sacc = s_zero<S>();
-        S xi = s_zero<S>();
-        if (mc.y >= 0) {
-            const int w0 = mc.y, wl = (mc.z >> 9) & 0x1ff;
+    for (int sl = sbeg + (blockIdx.x >> 3) * kWaves + wave; sl < send; sl += kSliceNS * wpg) {
+        SliceRegs<S, KB> R[kSliceNS];
+        int4 mc[kSliceNS];
 #pragma unroll
-            for (int j = 0; j < SliceRegs<S, KB>::NW; ++j) {
-                S v = R.w[j];
-                if constexpr (kPower) v = scale_in(v, nrm);
-                if (lane + 64 * j < wl) xw[lane + 64 * j] = v;
-            }
-            // wave-private region: LDS executes one wave's accesses in order; the fences only
-            // keep the compiler from moving the reads above the stores
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int i = 0; i < kSliceNS; ++i) mc[i] = ld_uniform(a.slice_meta, min(sl + i * wpg, send - 1));
 #pragma unroll
-            for (int u = 0; u < KB; ++u) {
-                const S pr = mul(R.v[u], xw[(R.c[u >> 2] >> (8 * (u & 3))) & 0xffu]);
-                if (u < R.len) sacc = add(sacc, pr);
-            }
-            for (int k0 = KB; k0 < K; k0 += 4) {       // rows longer than KB entries
-                const uint32_t cw = ldg(a.scol8, (uint32_t)mc.w + 64u * (uint32_t)(k0 >> 2) + (uint32_t)lane);
+        for (int i = 0; i < kSliceNS; ++i)   // past the range: reloads the last slice, unused
+            slice_issue<S, KB>(a, xin, min(sl + i * wpg, send - 1), mc[i], R[i]);
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const S pr = mul(ldg(a.sval, (uint32_t)mc.x + (uint32_t)lane + 64u * (uint32_t)min(k0 + u, K - 1)),
-                                     xw[(cw >> (8 * u)) & 0xffu]);
-                    if (k0 + u < R.len) sacc = add(sacc, pr);
-                }
-            }
-            if constexpr (kPower) xi = xw[min(max(rowc + a.xoff - w0, 0), wl - 1)];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-        } else if (K > 0) {
-            S xv[KB];
-#pragma unroll
-            for (int u = 0; u < KB; ++u) xv[u] = ldg(xin, R.c[u]);
-#pragma unroll
-            for (int u = 0; u < KB; ++u) {
-                S x = xv[u];
-                if constexpr (kPower) x = scale_in(x, nrm);
-                const S pr = mul(R.v[u], x);
-                if (u < R.len) sacc = add(sacc, pr);
-            }
-            for (int k0 = KB; k0 < K; ++k0) {
-                const uint32_t q = (uint32_t)lane + 64u * (uint32_t)k0;
-                S x = ldg(xin, (uint32_t)ldg(a.scol32, (uint32_t)mc.w + q));
-                if constexpr (kPower) x = scale_in(x, nrm);
-                const S pr = mul(ldg(a.sval, (uint32_t)mc.x + q), x);
-                if (k0 < R.len) sacc = add(sacc, pr);
-            }
-            if constexpr (kPower) xi = scale_in(xin[rowc + a.xoff], nrm);
-        } else if constexpr (kPower) {
-            xi = scale_in(xin[rowc + a.xoff], nrm);
-        }
-        if (valid) {
-            yout[row] = sacc;
-            if constexpr (kPower) {
-                n2 += sq_abs(sacc);
-                acc_dot(rr, ri, xi, sacc);
-            }
-        }
+        for (int i = 0; i < kSliceNS; ++i)
+            if (i == 0 || sl + i * wpg < send)
+                slice_compute<S, kPower, KB>(a, xin, yout, nrm, R[i], mc[i], sl + i * wpg, xw_all[wave][i], n2, rr, ri);
     }
     if constexpr (kPower) {
         block_sum3(n2, rr, ri, sm);
@@ -928,8 +981,8 @@ struct SliceLayout {
 };
 
 static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* values, size_t sb,
-                         int64_t nrows, int64_t nnz, int64_t xoff, SliceLayout& L) {
-    if (nrows == 0) return false;
+                         int64_t nrows, int64_t nnz, int64_t xoff, int64_t xlen, SliceLayout& L) {
+    if (nrows == 0 || xlen == 0) return false;
     const int64_t ns = (nrows + kSliceRows - 1) / kSliceRows;
     int64_t total = 0, ctot8 = 0, ctot32 = 0;
     bool any_ragged = false;
@@ -949,22 +1002,35 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
             }
         }
         const bool ragged = kmin != K || (r1 - r0) != kSliceRows;
+        // rows past the end of x (rectangular plain SpMV) need no x entry of their own
+        w1 = (int32_t)std::min<int64_t>(w1, xlen - 1);
+        w0 = std::min(w0, w1);
+        bool win = true;
+        if (sb == 8) {
+            // f64 windows load in aligned pairs: even start and even length inside x
+            w0 &= ~1;
+            if (((int64_t)w1 - w0 + 1) & 1) {
+                if (w1 + 1 < xlen) ++w1;
+                else win = false;
+            }
+        }
         const int64_t wl = (int64_t)w1 - w0 + 1;
-        const bool win = wl <= kSliceWin;
+        win = win && wl <= kSliceWin;
         any_ragged |= ragged;
         L.maxk = std::max(L.maxk, K);
         L.meta[4 * s] = (int32_t)total;
         L.meta[4 * s + 1] = win ? w0 : -1;
         L.meta[4 * s + 2] = K | (ragged ? 0x100 : 0) | (win ? (int32_t)(wl << 9) : 0);
         L.meta[4 * s + 3] = (int32_t)(win ? ctot8 : ctot32);
-        total += (int64_t)K * kSliceRows;
+        total += (int64_t)(sb == 8 ? (K + 1) & ~1 : K) * kSliceRows;   // f64: whole lane pairs
         if (win) ctot8 += (int64_t)((K + 3) / 4) * kSliceRows;
         else ctot32 += (int64_t)K * kSliceRows;
         if (total > nnz + nnz / 8 + 64 * kSliceRows || total >= (int64_t(1) << 31) / (int64_t)sb) return false;
     }
-    L.val.assign((size_t)std::max<int64_t>(total, 1) * sb, 0);
-    if (ctot8) L.c8.assign((size_t)ctot8, 0);
-    if (ctot32) L.c32.assign((size_t)ctot32, 0);
+    // one slice of padding past each stream's end (clamped loads of empty slices stay in bounds)
+    L.val.assign((size_t)(total + kSliceRows) * sb, 0);
+    L.c8.assign((size_t)(ctot8 + kSliceRows), 0);
+    L.c32.assign((size_t)(ctot32 + kSliceRows), 0);
     if (any_ragged) L.len.assign((size_t)nrows, 0);
     for (int64_t s = 0; s < ns; ++s) {
         const int64_t r0 = s * kSliceRows, r1 = std::min<int64_t>(nrows, r0 + kSliceRows);
@@ -977,7 +1043,8 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
             if (any_ragged) L.len[r] = (uint8_t)l;
             for (int k = 0; k < l; ++k) {
                 const int32_t e = rowptr[r] + k;
-                const size_t q = (size_t)(off + (int64_t)k * kSliceRows + lane);
+                const size_t q = sb == 8 ? (size_t)(off + (int64_t)(k >> 1) * 2 * kSliceRows + 2 * lane + (k & 1))
+                                         : (size_t)(off + (int64_t)k * kSliceRows + lane);
                 std::memcpy(&L.val[q * sb], (const unsigned char*)values + (size_t)e * sb, sb);
                 if (w0 >= 0)
                     L.c8[(size_t)(coff + (int64_t)(k / 4) * kSliceRows + lane)] |= (uint32_t)(col[e] - w0) << (8 * (k % 4));
@@ -986,7 +1053,8 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
             }
             // padding: offset 0 is in the window; gather padding reads the row's own x entry
             if (w0 < 0)
-                for (int k = l; k < K; ++k) L.c32[(size_t)(coff + (int64_t)k * kSliceRows + lane)] = (int32_t)(r + xoff);
+                for (int k = l; k < K; ++k)
+                    L.c32[(size_t)(coff + (int64_t)k * kSliceRows + lane)] = (int32_t)std::min<int64_t>(r + xoff, xlen - 1);
         }
     }
     return true;
@@ -1036,7 +1104,7 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     bool sliced = true;
     if (const char* env = std::getenv("EIGSOL_CSR_NO_SLICE")) if (std::atoi(env)) sliced = false;
     if (sliced)
-        sliced = build_slices(rowptr, col_use, val_use, sb, nrows, nnz, xoff, SL);
+        sliced = build_slices(rowptr, col_use, val_use, sb, nrows, nnz, xoff, ncols, SL);
 
     // the kernels index every stream with 32-bit byte offsets (ldg): one device's rows must keep
     // values, columns and vectors under 4 GiB each (shard larger matrices over ranks)
@@ -1103,8 +1171,8 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
         };
         if ((e = upl((void**)&A->slice_meta, SL.meta.data(), SL.meta.size() * 4)) != hipSuccess ||
             (e = upl(&A->sval, SL.val.data(), SL.val.size())) != hipSuccess ||
-            (!SL.c8.empty() && (e = upl((void**)&A->scol8, SL.c8.data(), SL.c8.size() * 4)) != hipSuccess) ||
-            (!SL.c32.empty() && (e = upl((void**)&A->scol32, SL.c32.data(), SL.c32.size() * 4)) != hipSuccess) ||
+            (e = upl((void**)&A->scol8, SL.c8.data(), SL.c8.size() * 4)) != hipSuccess ||
+            (e = upl((void**)&A->scol32, SL.c32.data(), SL.c32.size() * 4)) != hipSuccess ||
             (!SL.len.empty() && (e = upl((void**)&A->slen, SL.len.data(), SL.len.size())) != hipSuccess) ||
             (e = hipStreamSynchronize(s)) != hipSuccess) {
             cleanup();

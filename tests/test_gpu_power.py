@@ -302,3 +302,29 @@ def test_slice_layout_mix_bitwise_and_power(ctx, dtype):
     res = E.power_method(A, E.SolverOptions(3000, tol), x)
     ref = O.power_csc(cp, ri, vv, x, 3000, tol, want_trace=True)
     _assert_power_parity(res, ref, tol)
+
+
+@pytest.mark.parametrize("shape", [(300, 200), (200, 301)])
+def test_spmv_rectangular_sliced(ctx, shape):
+    """Plain SpMV of a rectangular matrix (x shorter or longer than y) in the sliced layout: row
+    sums in ascending column order, bitwise."""
+    m, n = shape
+    rng = np.random.default_rng(8)
+    rows, cols = [], []
+    for i in range(m):
+        lo = min(max(0, i * n // m - 20), n - 41)
+        c = np.sort(rng.choice(np.arange(lo, lo + 41), size=8, replace=False))
+        rows.append(np.full(8, i))
+        cols.append(c)
+    M = sp.csr_matrix((rng.uniform(-1, 1, 8 * m), (np.concatenate(rows), np.concatenate(cols))), shape=(m, n))
+    M.sort_indices()
+    A = E.CsrMatrix.from_scipy(ctx, M)
+    x = S.start_vector(n)
+    y = _spmv_gpu(ctx, A, x)
+    y_ref = np.zeros(m)
+    for i in range(m):
+        acc = 0.0
+        for e in range(M.indptr[i], M.indptr[i + 1]):
+            acc += M.data[e] * x[M.indices[e]]
+        y_ref[i] = acc
+    assert np.array_equal(y, y_ref)

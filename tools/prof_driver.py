@@ -16,6 +16,30 @@ p = argparse.ArgumentParser()
 p.add_argument("--workload", default="band10m")
 p.add_argument("--steps", type=int, default=20)
 args = p.parse_args()
+if args.workload == "config5":
+    # shifted inverse iteration on the 1M upper-triangular complex matrix (sptrsv_kernel)
+    import numpy as np
+    n = 1_000_000
+    rp, ci, v, _ = S.triu_complex(n, 16)
+    ctx = E.Context(0)
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 1.5 * np.exp(0.7j) + 1e-3
+    s = E.ShiftedSession(A, sigma)
+    s.begin(E.ShiftedSolverOptions(2**31 - 1, -1.0, sigma), S.start_vector(n, np.complex128))
+    s.step(args.steps)
+    ctx.synchronize()
+    print("done", s.kernel_info())
+    s.close(); A.close(); ctx.close()
+    sys.exit(0)
+if args.workload == "qr4096":
+    import numpy as np
+    n = 4096
+    a = np.asfortranarray(np.random.default_rng(42).standard_normal((n, n)))
+    ctx = E.Context(0)
+    r = E.qr_eigenvalues(ctx, a, E.SolverOptions(1000, 1e-10))
+    print("done", r.iterations, r.converged)
+    ctx.close()
+    sys.exit(0)
 kind, rows, k = {"band10m": ("band", 10_000_000, 10), "uniform1m": ("uniform", 1_000_000, 16),
                  "band1m": ("band", 1_000_000, 16), "uniform10m": ("uniform", 10_000_000, 10)}[args.workload]
 gen = S.band if kind == "band" else S.uniform
@@ -27,3 +51,6 @@ s.begin(E.SolverOptions(2**31 - 1, -1.0), S.start_vector(rows))
 s.step(args.steps)
 ctx.synchronize()
 print("done", s.kernel_info())
+s.close()
+A.close()
+ctx.close()
