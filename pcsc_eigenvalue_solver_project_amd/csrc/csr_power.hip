@@ -656,7 +656,7 @@ constexpr int kSliceRows = 64;
 constexpr int kSliceMaxK = 64;
 constexpr int kSliceWin = 256;
 
-template <class S, int KB>
+template <class S, int KB, bool kG>
 struct SliceRegs {
     // window loads: f64 in 16-byte pairs (window start even, length even), complex one per lane
     static constexpr int NW = std::is_same_v<S, double> ? kSliceWin / 128 : kSliceWin / 64;
@@ -665,13 +665,14 @@ struct SliceRegs {
     static constexpr int NV = std::is_same_v<S, double> ? KB / 2 : KB;
     using VT = std::conditional_t<std::is_same_v<S, double>, double2, S>;
     VT v[NV];
-    uint32_t c[KB];   // window slices: packed 8-bit offsets in c[0 .. KB/4); gather slices: columns
+    // window slices: packed 8-bit offsets in c[0 .. KB/4); gather slices (kG): int32 columns
+    uint32_t c[kG ? KB : KB / 4];
     WT w[NW];
     int len;          // the lane's row length
 };
 
-template <class S, int KB>
-__device__ __forceinline__ S slice_val(const SliceRegs<S, KB>& R, int u) {
+template <class S, int KB, bool kG>
+__device__ __forceinline__ S slice_val(const SliceRegs<S, KB, kG>& R, int u) {
     if constexpr (std::is_same_v<S, double>) return (u & 1) ? R.v[u >> 1].y : R.v[u >> 1].x;
     else return R.v[u];
 }
@@ -684,9 +685,9 @@ __device__ __forceinline__ uint32_t slice_entry(uint32_t off, int k, int lane) {
 
 // Every load of one slice's first KB entries, its window and the row lengths.  Loads are clamped
 // (to entry K-1, window entry wl-1): same cache lines, no extra bytes, no exec-masked loads.
-template <class S, int KB>
+template <class S, int KB, bool kG>
 __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, int slice, int4 m,
-                                            SliceRegs<S, KB>& R) {
+                                            SliceRegs<S, KB, kG>& R) {
     const int lane = threadIdx.x & 63;
     // K = 0 (all rows empty) clamps to entry 0 of the slice: the streams carry one slice of
     // padding past their end, so even an empty last slice loads in bounds
@@ -698,7 +699,7 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
         const int K2 = (K + 1) >> 1;
         const uint32_t b2 = ((uint32_t)m.x >> 1) + (uint32_t)lane;
 #pragma unroll
-        for (int j = 0; j < SliceRegs<S, KB>::NV; ++j)
+        for (int j = 0; j < SliceRegs<S, KB, kG>::NV; ++j)
             R.v[j] = ldg(reinterpret_cast<const double2*>(a.sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
     } else {
 #pragma unroll
@@ -712,13 +713,13 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
         // the window always holds the slice's own rows (the Rayleigh term reads them)
         const int wl = max((m.z >> 9) & 0x1ff, 1);
 #pragma unroll
-        for (int j = 0; j < SliceRegs<S, KB>::NW; ++j)
+        for (int j = 0; j < SliceRegs<S, KB, kG>::NW; ++j)
             if constexpr (std::is_same_v<S, double>)
                 R.w[j] = ldg(reinterpret_cast<const double2*>(xin),
                              (uint32_t)((m.y >> 1) + min(lane + 64 * j, (wl >> 1) - 1)));
             else
                 R.w[j] = ldg(xin, (uint32_t)(m.y + min(lane + 64 * j, wl - 1)));
-    } else {
+    } else if constexpr (kG) {
 #pragma unroll
         for (int u = 0; u < KB; ++u)
             R.c[u] = (uint32_t)ldg(a.scol32, (uint32_t)m.w + 64u * (uint32_t)min(u, K - 1) + (uint32_t)lane);
@@ -726,9 +727,9 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
 }
 
 // Row sums of one slice from its registers (window slices: x from the wave's LDS window).
-template <class S, bool kPower, int KB>
+template <class S, bool kPower, int KB, bool kG>
 __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin, S* yout, double nrm,
-                                              const SliceRegs<S, KB>& R, int4 mc, int sl, S* xw,
+                                              const SliceRegs<S, KB, kG>& R, int4 mc, int sl, S* xw,
                                               double& n2, double& rr, double& ri) {
     const int lane = threadIdx.x & 63;
     const int K = mc.z & 0xff;
@@ -740,7 +741,7 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
     if (mc.y >= 0) {
         const int w0 = mc.y, wl = (mc.z >> 9) & 0x1ff;
 #pragma unroll
-        for (int j = 0; j < SliceRegs<S, KB>::NW; ++j) {
+        for (int j = 0; j < SliceRegs<S, KB, kG>::NW; ++j) {
             if constexpr (std::is_same_v<S, double>) {
                 double2 v = R.w[j];
                 if constexpr (kPower) {
@@ -776,7 +777,7 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
         if constexpr (kPower) xi = xw[min(max(rowc + a.xoff - w0, 0), wl - 1)];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-    } else {
+    } else if constexpr (kG) {
         S xv[KB];
 #pragma unroll
         for (int u = 0; u < KB; ++u) xv[u] = ldg(xin, R.c[u]);
@@ -810,7 +811,7 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
 #endif
 constexpr int kSliceNS = EIGSOL_SLICE_NS;   // slices a wave has in flight at once
 
-template <class S, bool kPower, int KB>
+template <class S, bool kPower, int KB, bool kG>
 __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int parity) {
     __shared__ __align__(16) S xw_all[kWaves][kSliceNS][kSliceWin];
     __shared__ double sm[3 * kWaves];
@@ -840,17 +841,17 @@ __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int p
     const int sbeg = (blockIdx.x & 7) * chunk;
     const int send = min(a.nslices, sbeg + chunk);
     for (int sl = sbeg + (blockIdx.x >> 3) * kWaves + wave; sl < send; sl += kSliceNS * wpg) {
-        SliceRegs<S, KB> R[kSliceNS];
+        SliceRegs<S, KB, kG> R[kSliceNS];
         int4 mc[kSliceNS];
 #pragma unroll
         for (int i = 0; i < kSliceNS; ++i) mc[i] = ld_uniform(a.slice_meta, min(sl + i * wpg, send - 1));
 #pragma unroll
         for (int i = 0; i < kSliceNS; ++i)   // past the range: reloads the last slice, unused
-            slice_issue<S, KB>(a, xin, min(sl + i * wpg, send - 1), mc[i], R[i]);
+            slice_issue<S, KB, kG>(a, xin, min(sl + i * wpg, send - 1), mc[i], R[i]);
 #pragma unroll
         for (int i = 0; i < kSliceNS; ++i)
             if (i == 0 || sl + i * wpg < send)
-                slice_compute<S, kPower, KB>(a, xin, yout, nrm, R[i], mc[i], sl + i * wpg, xw_all[wave][i], n2, rr, ri);
+                slice_compute<S, kPower, KB, kG>(a, xin, yout, nrm, R[i], mc[i], sl + i * wpg, xw_all[wave][i], n2, rr, ri);
     }
     if constexpr (kPower) {
         block_sum3(n2, rr, ri, sm);
@@ -978,6 +979,7 @@ struct SliceLayout {
     std::vector<int32_t> c32;
     std::vector<uint8_t> len;
     int maxk = 0;
+    bool any_gather = false;   // some slice's window does not fit: gather instantiation
 };
 
 static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* values, size_t sb,
@@ -1025,6 +1027,7 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
         total += (int64_t)(sb == 8 ? (K + 1) & ~1 : K) * kSliceRows;   // f64: whole lane pairs
         if (win) ctot8 += (int64_t)((K + 3) / 4) * kSliceRows;
         else ctot32 += (int64_t)K * kSliceRows;
+        L.any_gather |= !win;
         if (total > nnz + nnz / 8 + 64 * kSliceRows || total >= (int64_t(1) << 31) / (int64_t)sb) return false;
     }
     // one slice of padding past each stream's end (clamped loads of empty slices stay in bounds)
@@ -1126,6 +1129,8 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     A->sliced = sliced ? 1 : 0;
     A->nslices = sliced ? (int32_t)(SL.meta.size() / 4) : 0;
     A->slice_kb = SL.maxk <= 4 ? 4 : SL.maxk <= 8 ? 8 : SL.maxk <= 12 ? 12 : 16;
+    A->slice_gather = SL.any_gather ? 1 : 0;
+    if (const char* env = std::getenv("EIGSOL_SLICE_FORCE_GATHER")) if (std::atoi(env)) A->slice_gather = 1;   // A/B
     const size_t pad = (size_t)(dtype == EIGSOL_C128 ? Tile<cplx>::kNnz : Tile<double>::kNnz) + 8;   // branch-free tile loads
     auto cleanup = [&]() { csr_release(A); };
     hipError_t e;
@@ -1204,13 +1209,13 @@ static int validate_compressed(const char* who, int64_t nouter, int64_t ninner, 
 // ---------------------------------------------------------------- occupancy-derived grid
 // Residency from the kernel's own resources (MI355X_MICROARCH.md § Register files: waves per SIMD
 // = floor(512 / VGPR allocation), 4 waves per block, 160 KiB LDS per CU).
-static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, int* grid) {
+static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, int* grid, int cap = 8) {
     hipFuncAttributes fa;
     EIGSOL_HIP(hipFuncGetAttributes(&fa, kernel));
     const int vgpr_alloc = std::max(8, ((fa.numRegs + 7) / 8) * 8);
     const int by_vgpr = std::min(8, 512 / vgpr_alloc) * 4 / kWaves;
     const int by_lds = fa.sharedSizeBytes ? (int)(160 * 1024 / fa.sharedSizeBytes) : 8;
-    int per_cu = std::max(1, std::min({by_vgpr, by_lds, 8}));
+    int per_cu = std::max(1, std::min({by_vgpr, by_lds, cap}));
     if (const char* env = std::getenv("EIGSOL_CSR_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(env));
     int64_t g = (int64_t)per_cu * ctx->num_cus;
     const int64_t need = ((ntiles + 7) / 8) * 8;
@@ -1223,12 +1228,16 @@ static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, in
 template <class S>
 static const void* power_kernel_ptr(const eigsol_csr* A) {
     if (A->sliced) {
+#define EIGSOL_SLICE_PTR(KB)                                                                     \
+    return A->slice_gather ? reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, true>) \
+                           : reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, false>);
         switch (A->slice_kb) {
-            case 4: return reinterpret_cast<const void*>(csr_slice_kernel<S, true, 4>);
-            case 8: return reinterpret_cast<const void*>(csr_slice_kernel<S, true, 8>);
-            case 12: return reinterpret_cast<const void*>(csr_slice_kernel<S, true, 12>);
-            default: return reinterpret_cast<const void*>(csr_slice_kernel<S, true, 16>);
+            case 4: EIGSOL_SLICE_PTR(4)
+            case 8: EIGSOL_SLICE_PTR(8)
+            case 12: EIGSOL_SLICE_PTR(12)
+            default: EIGSOL_SLICE_PTR(16)
         }
+#undef EIGSOL_SLICE_PTR
     }
     return A->windowed ? reinterpret_cast<const void*>(csr_win_kernel<S, true>)
                        : reinterpret_cast<const void*>(csr_kernel<S, true>);
@@ -1238,7 +1247,9 @@ int csr_grid(eigsol_csr* A, int* grid) {
     const void* k = A->dtype == EIGSOL_C128 ? power_kernel_ptr<cplx>(A) : power_kernel_ptr<double>(A);
     // work units: tiles (one per block step) or slices (one per wave step)
     const int64_t units = A->sliced ? (A->nslices + kWaves - 1) / kWaves : A->ntiles;
-    return resident_grid(A->ctx, k, units, grid);
+    // sliced: two blocks (8 waves, 16 slices in flight) per CU measured fastest on band10m;
+    // more concurrent streams per CU cost more than the latency they hide
+    return resident_grid(A->ctx, k, units, grid, A->sliced ? 2 : 8);
 }
 
 template <class S>
@@ -1281,9 +1292,12 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
         }
     }
     if (A->sliced) {
-#define EIGSOL_SLICE_LAUNCH(KB)                                                                              \
-    if (power) hipLaunchKernelGGL((csr_slice_kernel<S, true, KB>), dim3(grid), dim3(kThreads), 0, s, args, parity); \
-    else hipLaunchKernelGGL((csr_slice_kernel<S, false, KB>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+#define EIGSOL_SLICE_LAUNCH2(KB, G)                                                                               \
+    if (power) hipLaunchKernelGGL((csr_slice_kernel<S, true, KB, G>), dim3(grid), dim3(kThreads), 0, s, args, parity); \
+    else hipLaunchKernelGGL((csr_slice_kernel<S, false, KB, G>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+#define EIGSOL_SLICE_LAUNCH(KB)                                  \
+    if (A->slice_gather) { EIGSOL_SLICE_LAUNCH2(KB, true) }      \
+    else { EIGSOL_SLICE_LAUNCH2(KB, false) }
         switch (A->slice_kb) {
             case 4: EIGSOL_SLICE_LAUNCH(4) break;
             case 8: EIGSOL_SLICE_LAUNCH(8) break;
@@ -1291,6 +1305,7 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
             default: EIGSOL_SLICE_LAUNCH(16) break;
         }
 #undef EIGSOL_SLICE_LAUNCH
+#undef EIGSOL_SLICE_LAUNCH2
     } else if (A->windowed) {
         if (power) hipLaunchKernelGGL((csr_win_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);
         else hipLaunchKernelGGL((csr_win_kernel<S, false>), dim3(grid), dim3(kThreads), 0, s, args, parity);

@@ -193,6 +193,7 @@ struct eigsol_csr {
     void* sval = nullptr;          // device, 64 * K_s entries per slice
     uint32_t* scol8 = nullptr;     // device (window slices): 8-bit offsets, 4 per lane-dword
     int32_t slice_kb = 16;         // entries per row held in registers (kernel instantiation)
+    int32_t slice_gather = 0;      // some slices gather x from global memory (kernel instantiation)
     int32_t* scol32 = nullptr;     // device (gather slices)
     uint8_t* slen = nullptr;       // device, per row (ragged slices)
     // Row-sharded (multi-GPU) layout: this rank owns global rows [row_begin, row_begin + nrows);
