@@ -104,6 +104,60 @@ def cpu_baseline(kind, k, budget_s):
     }
 
 
+def host_cpu():
+    """Core model and the CPU share this process may use (the GPU box exports OMP_NUM_THREADS)."""
+    model = "?"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"model": model, "nproc": os.cpu_count(),
+            "threads_allowed": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))}
+
+
+def cpu_allcores(kind, k, budget_s):
+    """Stronger CPU figure: one fused CSR product per iteration on all allowed cores."""
+    from oracle import oracle as O
+    from pcsc_eigenvalue_solver_project_amd import synthetic as S
+    n = 1_000_000
+    rp, ci, v = gen(kind, n, k, 0, n)
+    x0 = S.start_vector(n)
+    th = host_cpu()["threads_allowed"]
+    t = time.perf_counter()
+    O.power_csr_omp(rp, ci, v, x0, 3, th)
+    per_iter = (time.perf_counter() - t) / 3
+    iters = max(5, int(budget_s / max(per_iter, 1e-6)))
+    t = time.perf_counter()
+    O.power_csr_omp(rp, ci, v, x0, iters, th)
+    dt = time.perf_counter() - t
+    return {"value": round(S.csr_bytes_per_iteration(n, len(ci)) * iters / dt / 1e9, 2), "unit": "GB/s",
+            "cores": th, "kind": "port",
+            "sample": f"{kind} {n}x{n}, {k} nnz/row: {iters} fused CSR power iterations, OpenMP rows "
+                      f"(oracle power_csr_omp_f64, -O3), {dt:.1f}s",
+            "ms_per_iteration": round(1e3 * dt / iters, 3)}
+
+
+def measured_hbm(torch, stream):
+    """STREAM-like figures on this GPU (report beside the 8 TB/s spec): a 2 GiB device
+    copy (read + write bytes) and a 2 GiB read-only reduction."""
+    a = torch.empty(2 << 30, dtype=torch.uint8, device="cuda").view(torch.float64)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    a.sum()
+    torch.cuda.synchronize()
+    reps = 10
+    ms_copy = _events(torch, stream, lambda: [b.copy_(a) for _ in range(reps)]) / reps
+    ms_read = _events(torch, stream, lambda: [a.sum() for _ in range(reps)]) / reps
+    nb = a.numel() * 8
+    del a, b
+    return {"copy_GBps": round(2 * nb / ms_copy / 1e6, 1), "read_GBps": round(nb / ms_read / 1e6, 1),
+            "note": "torch copy_ and sum over 2 GiB fp64, HIP events; the roofline peak stays the 8 TB/s spec"}
+
+
 def _events(torch, stream, fn):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -323,6 +377,8 @@ def main():
         if pmc:
             out["roofline"]["traffic"] = pmc["hbm_traffic_bytes_per_launch"]
             out["roofline"]["traffic_source"] = pmc["source"]
+    if world == 1 and rank == 0:
+        out["roofline"]["measured_hbm"] = measured_hbm(torch, torch_stream)
     if not args.no_extras and world == 1:
         out["extras"] = {
             "config3_csr_1Mx16": run_config3(E, S, ctx, torch, torch_stream, opts),
@@ -335,6 +391,8 @@ def main():
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(kind, k, args.cpu_seconds)
+            out["cpu_baseline"]["host"] = host_cpu()
+            out["cpu_allcores"] = cpu_allcores(kind, k, min(args.cpu_seconds, 10.0))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -205,8 +205,13 @@ int eigsol_qr_eigenvalues_dense(eigsol_ctx* ctx, int dtype, int64_t n, const voi
  * eigsol_dist_get_unique_id, broadcasts the bytes with any transport, every rank calls
  * eigsol_ctx_create_dist.  eigsol_csr_create_dist is collective; the resulting matrix is used with
  * the eigsol_power_* session functions unchanged (x0 / x_out hold the rank's own rows).  Each
- * iteration exchanges only the x entries other ranks read (a halo for banded matrices) plus one
- * 32-byte all-gather; every rank reaches the same termination decision. */
+ * iteration exchanges x plus one 32-byte all-gather of rank partials; every rank reaches the same
+ * termination decision.  The x exchange (chosen collectively, eigsol_exchange_mode):
+ *   EIGSOL_EXCHANGE_HALO      only the entries other ranks read, point to point (banded matrices);
+ *   EIGSOL_EXCHANGE_ALLGATHER every rank keeps all of x and the row blocks are all-gathered
+ *                             (unstructured columns, where a rank reads most of x anyway). */
+#define EIGSOL_EXCHANGE_HALO 0
+#define EIGSOL_EXCHANGE_ALLGATHER 1
 int eigsol_dist_unique_id_bytes(void);
 int eigsol_dist_get_unique_id(void* id_out);
 int eigsol_ctx_create_dist(int device, int rank, int nranks, const void* unique_id,
@@ -220,6 +225,13 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
 int eigsol_ghost_plan(int nranks, const int64_t* row_begins, int rank, int64_t nnz_local,
                       const int32_t* colidx_global, int32_t* colidx_local, int64_t* nghost,
                       int64_t* ghost_global, int64_t* recv_counts);
+/* Host-only: the exchange every rank of eigsol_csr_create_dist selects from the P x P ghost counts
+ * (ghost_counts[r * P + q] = entries rank r reads from rank q): all-gather when some rank reads at
+ * least a quarter of the rows it does not own, else halo.  EIGSOL_DIST_EXCHANGE=halo|allgather
+ * overrides. */
+int eigsol_exchange_mode(int nranks, const int64_t* row_begins, const int64_t* ghost_counts, int* mode);
+/* The exchange a row-sharded matrix uses (EIGSOL_EXCHANGE_*) and its number of ghost entries. */
+int eigsol_csr_dist_info(const eigsol_csr* A, int* mode, int64_t* nghost);
 
 #ifdef __cplusplus
 }

@@ -51,6 +51,8 @@ def lib():
             f = getattr(L, "orc_" + name)
             f.argtypes = [_i64, _p, _p, _int, _dbl, _p, _p, _p, _p]
             f.restype = _int
+        L.orc_power_csr_omp_f64.argtypes = [_i64, _p, _p, _p, _p, _int, _int]
+        L.orc_power_csr_omp_f64.restype = _dbl
         L.orc_solve_shifted_dense_f64.argtypes = [_i64, _p, _dbl, _p, _p]
         L.orc_solve_shifted_dense_c128.argtypes = [_i64, _p, _p, _p, _p]
         L.orc_shifted_dense_f64.argtypes = [_i64, _p, _dbl, _p, _int, _dbl, _p, _p, _p, _p]
@@ -148,6 +150,15 @@ def power_csc(colptr, rowidx, vals, x0, max_iterations=1000, tolerance=1e-10, wa
         n, _ptr(cp), _ptr(ri), _ptr(v), _ptr(xx), int(max_iterations), float(tolerance),
         _ptr(lam), _ptr(x), C.byref(it), None if tr is None else _ptr(tr))
     return _result(lam, x, it, conv, tr)
+
+
+def power_csr_omp(rowptr, colidx, vals, x0, iterations, threads):
+    """bench.py's all-cores CPU figure: fused CSR power iteration, OpenMP rows, fixed iteration
+    count; returns the last Rayleigh quotient."""
+    n = len(rowptr) - 1
+    rp, ci, v, xx = _vec(rowptr, np.int32), _vec(colidx, np.int32), _vec(vals, np.float64), _vec(x0, np.float64)
+    return float(lib().orc_power_csr_omp_f64(n, _ptr(rp), _ptr(ci), _ptr(v), _ptr(xx), int(iterations),
+                                             int(threads)))
 
 
 def power_dense(A, x0, max_iterations=1000, tolerance=1e-10, want_trace=False):

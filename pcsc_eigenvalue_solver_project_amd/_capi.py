@@ -93,6 +93,8 @@ SIGNATURES = {
     "eigsol_ctx_create_dist": [C.c_int, C.c_int, C.c_int, _vp, _ppv],
     "eigsol_csr_create_dist": [_vp, C.c_int, _vp, _i64, _vp, _vp, _vp, _ppv],
     "eigsol_ghost_plan": [C.c_int, _vp, C.c_int, _i64, _vp, _vp, _pi64, _vp, _vp],
+    "eigsol_exchange_mode": [C.c_int, _vp, _vp, C.POINTER(C.c_int)],
+    "eigsol_csr_dist_info": [_vp, C.POINTER(C.c_int), _pi64],
     "eigsol_shifted_create_csr": [_vp, _vp, _i32, _ppv],
     "eigsol_shifted_create_dense": [_vp, _vp, _i32, _ppv],
     "eigsol_shifted_inverse_csr": [_vp, _vp, C.POINTER(SolverOptionsC), _vp, _vp, _vp, _pi32, _pi32],

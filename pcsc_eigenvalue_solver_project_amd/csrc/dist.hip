@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -67,6 +68,27 @@ int dist_exchange(eigsol_csr* A, void* y, void* rank_part) {
     ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
     const size_t dpe = sb / 8;   // doubles per scalar
     char* xs = static_cast<char*>(y);   // x-space: [lower ghosts | own rows | upper ghosts]
+    double* rpart = static_cast<double*>(rank_part);
+    if (A->exchange == EIGSOL_EXCHANGE_ALLGATHER) {
+        // x-space = the global index space: every rank's own block lands in place on every rank
+        const std::vector<int64_t>& rb = A->row_begins;
+        const int P = ctx->nranks;
+        bool equal = true;
+        for (int q = 0; q < P; ++q) equal = equal && (rb[q + 1] - rb[q] == rb[1] - rb[0]);
+        EIGSOL_RCCL(ncclGroupStart());
+        if (equal) {
+            EIGSOL_RCCL(ncclAllGather(xs + (size_t)rb[ctx->rank] * sb, xs, (size_t)(rb[1] - rb[0]) * dpe,
+                                      ncclFloat64, comm, st));
+        } else {
+            for (int q = 0; q < P; ++q)
+                if (rb[q + 1] > rb[q])
+                    EIGSOL_RCCL(ncclBroadcast(xs + (size_t)rb[q] * sb, xs + (size_t)rb[q] * sb,
+                                              (size_t)(rb[q + 1] - rb[q]) * dpe, ncclFloat64, q, comm, st));
+        }
+        EIGSOL_RCCL(ncclAllGather(rpart + 4 * ctx->rank, rpart, 4, ncclFloat64, comm, st));
+        EIGSOL_RCCL(ncclGroupEnd());
+        return EIGSOL_OK;
+    }
     EIGSOL_RCCL(ncclGroupStart());
     for (int q = 0; q < ctx->nranks; ++q) {
         if (q == ctx->rank) continue;
@@ -136,6 +158,32 @@ int eigsol_ghost_plan(int nranks, const int64_t* row_begins, int rank, int64_t n
     return EIGSOL_OK;
 }
 
+int eigsol_exchange_mode(int nranks, const int64_t* row_begins, const int64_t* ghost_counts, int* mode) {
+    if (nranks < 1 || !row_begins || !ghost_counts || !mode)
+        return fail(EIGSOL_E_INVALID, "eigsol_exchange_mode: invalid argument");
+    const int64_t n_global = row_begins[nranks];
+    int m = EIGSOL_EXCHANGE_HALO;
+    for (int r = 0; r < nranks; ++r) {
+        int64_t g = 0;
+        for (int q = 0; q < nranks; ++q) g += q == r ? 0 : ghost_counts[(size_t)r * nranks + q];
+        const int64_t remote = n_global - (row_begins[r + 1] - row_begins[r]);
+        if (remote > 0 && 4 * g >= remote) m = EIGSOL_EXCHANGE_ALLGATHER;
+    }
+    if (const char* e = std::getenv("EIGSOL_DIST_EXCHANGE")) {
+        if (!std::strcmp(e, "halo")) m = EIGSOL_EXCHANGE_HALO;
+        else if (!std::strcmp(e, "allgather")) m = EIGSOL_EXCHANGE_ALLGATHER;
+    }
+    *mode = m;
+    return EIGSOL_OK;
+}
+
+int eigsol_csr_dist_info(const eigsol_csr* A, int* mode, int64_t* nghost) {
+    if (!A) return fail(EIGSOL_E_INVALID, "eigsol_csr_dist_info: null matrix");
+    if (mode) *mode = A->dist ? A->exchange : EIGSOL_EXCHANGE_HALO;
+    if (nghost) *nghost = A->dist ? A->nghost : 0;
+    return EIGSOL_OK;
+}
+
 int eigsol_dist_get_unique_id(void* id_out) {
     if (!id_out) return fail(EIGSOL_E_INVALID, "eigsol_dist_get_unique_id: null pointer");
     ncclUniqueId id;
@@ -195,6 +243,26 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     EIGSOL_HIP(hipMemcpyAsync(all.data(), d_counts, sizeof(int64_t) * P * P, hipMemcpyDeviceToHost, st));
     EIGSOL_HIP(hipStreamSynchronize(st));
     hipFree(d_counts);
+    int mode = EIGSOL_EXCHANGE_HALO;
+    EIGSOL_TRY(eigsol_exchange_mode(P, row_begins, all.data(), &mode));   // same decision on every rank
+    if (mode == EIGSOL_EXCHANGE_ALLGATHER) {
+        // replicated x: local columns are the global ones, own rows sit at their global slots
+        eigsol_csr* A = nullptr;
+        EIGSOL_TRY(csr_upload(ctx, dtype, nrows, n_global, nnz_local, rowptr_local, colidx_global, values, &A,
+                              row_begins[me]));
+        A->dist = 1;
+        A->exchange = EIGSOL_EXCHANGE_ALLGATHER;
+        A->n_global = n_global;
+        A->row_begin = row_begins[me];
+        A->nghost = n_global - nrows;
+        A->row_begins.assign(row_begins, row_begins + P + 1);
+        A->send_counts.assign(P, 0);
+        A->recv_counts.assign(P, 0);
+        A->send_offs.assign(P, 0);
+        A->recv_offs.assign(P, 0);
+        *out = A;
+        return EIGSOL_OK;
+    }
     std::vector<int64_t> send(P), soff(P + 1, 0), roff(P + 1, 0);
     for (int q = 0; q < P; ++q) send[q] = (q == me) ? 0 : all[(size_t)q * P + me];
     for (int q = 0; q < P; ++q) {

@@ -202,6 +202,8 @@ struct eigsol_csr {
     int64_t n_global = 0, row_begin = 0, nghost = 0;
     int64_t xoff = 0;              // x-space index of local row 0 (= ghosts owned by lower ranks)
     std::vector<int64_t> send_counts, send_offs, recv_counts, recv_offs;   // per peer (scalars)
+    int exchange = 0;              // EIGSOL_EXCHANGE_HALO / _ALLGATHER
+    std::vector<int64_t> row_begins;   // all ranks' row blocks (all-gather exchange)
     int32_t* send_idx = nullptr;   // device: local row of every entry sent, grouped by peer
     void* send_buf = nullptr;      // device: packed halo values
     int64_t nsend = 0;

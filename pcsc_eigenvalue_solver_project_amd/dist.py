@@ -27,6 +27,19 @@ def ghost_plan(nranks: int, row_begins, rank: int, colidx_global):
     return cl[: len(cg)], gh[: ng.value], rc
 
 
+EXCHANGE_HALO, EXCHANGE_ALLGATHER = 0, 1
+
+
+def exchange_mode(row_begins, ghost_counts) -> int:
+    """The x exchange eigsol_csr_create_dist selects from the P x P ghost counts
+    (``ghost_counts[r, q]`` = entries rank r reads from rank q); library function, no device."""
+    rb = np.ascontiguousarray(row_begins, dtype=np.int64)
+    gc = np.ascontiguousarray(ghost_counts, dtype=np.int64)
+    m = C.c_int(0)
+    call("eigsol_exchange_mode", len(rb) - 1, _ptr(rb), _ptr(gc), C.byref(m))
+    return m.value
+
+
 class DistContext(Context):
     """A Context whose communicator spans one rank per GPU."""
 
@@ -81,6 +94,13 @@ class DistCsrMatrix(CsrMatrix):
         self.n_global = int(rb[-1])
         self.nnz = len(cg)
         self.dtype = _np_dtype(code)
+
+    @property
+    def exchange(self) -> int:
+        """EXCHANGE_HALO or EXCHANGE_ALLGATHER (chosen collectively at construction)."""
+        m, g = C.c_int(0), C.c_int64(0)
+        call("eigsol_csr_dist_info", self.handle, C.byref(m), C.byref(g))
+        return m.value
 
 
 def sharded_power_session(ctx: DistContext, rowptr_local, colidx_global, values, n_global: int,

@@ -162,3 +162,98 @@ def test_ghost_plan_layout_and_errors():
     assert list(cl) == [12, 1, 4, 11, 0, 13, 7]
     with pytest.raises(EigSolError):
         D.ghost_plan(3, rb, 1, np.array([31], dtype=np.int32))
+
+
+def test_exchange_mode_rule():
+    """eigsol_exchange_mode: all-gather once some rank reads >= 1/4 of the rows it does not own."""
+    from pcsc_eigenvalue_solver_project_amd import dist as D
+    from pcsc_eigenvalue_solver_project_amd import synthetic as S
+    n, world = 4000, 4
+    rb = np.linspace(0, n, world + 1).astype(np.int64)
+    for kind, want in (("band", D.EXCHANGE_HALO), ("uniform", D.EXCHANGE_ALLGATHER)):
+        rp, ci, v = S.band(n, 10) if kind == "band" else S.uniform(n, 8)
+        counts = np.zeros((world, world), dtype=np.int64)
+        for r in range(world):
+            lci = ci[rp[rb[r]]:rp[rb[r + 1]]]
+            counts[r] = D.ghost_plan(world, rb, r, lci)[2]
+        assert D.exchange_mode(rb, counts) == want, kind
+    # boundary: one rank reading exactly a quarter of its remote rows flips the decision
+    rb2 = np.array([0, 100, 200], dtype=np.int64)
+    assert D.exchange_mode(rb2, np.array([[0, 24], [0, 0]])) == D.EXCHANGE_HALO
+    assert D.exchange_mode(rb2, np.array([[0, 25], [0, 0]])) == D.EXCHANGE_ALLGATHER
+
+
+def _worker_allgather(rank, world, port, out_q):
+    """The all-gather exchange: replicated x-space (global indices), own block written in place,
+    blocks all-gathered before every product; partials added in rank order."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pcsc_eigenvalue_solver_project_amd import synthetic as S
+        n = 3000
+        rp, ci, v = S.uniform(n, 8)
+        rb = np.linspace(0, n, world + 1).astype(np.int64)
+        r0, r1 = int(rb[rank]), int(rb[rank + 1])
+        Aloc = sp.csr_matrix((v[rp[r0]:rp[r1]], ci[rp[r0]:rp[r1]], (rp[r0:r1 + 1] - rp[r0])), shape=(r1 - r0, n))
+
+        def gather(xs):
+            blocks = [torch.zeros(int(rb[q + 1] - rb[q]), dtype=torch.float64) for q in range(world)]
+            dist.all_gather(blocks, torch.from_numpy(xs[r0:r1].copy()))
+            for q in range(world):
+                xs[rb[q]:rb[q + 1]] = blocks[q].numpy()
+
+        def allsum(val):
+            g = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(g, torch.tensor([val], dtype=torch.float64))
+            return float(sum(t.item() for t in g))          # rank order
+
+        x0 = S.start_vector(n)
+        xs = np.zeros(n)
+        xs[r0:r1] = x0[r0:r1]
+        gather(xs)
+        assert np.array_equal(xs, x0)                        # replicated x bitwise
+        nx = np.sqrt(allsum(float(np.sum(xs[r0:r1] ** 2))))
+        lam, it = 0.0, 0
+        for k in range(200):
+            y = Aloc @ (xs / nx)
+            n2 = allsum(float(np.dot(y, y)))
+            lam_new = allsum(float(np.dot(xs[r0:r1] / nx, y)))
+            it = k + 1
+            xs[r0:r1] = y
+            gather(xs)
+            nx = np.sqrt(n2)
+            if k > 0 and abs(lam_new - lam) <= 1e-12 * (1 + abs(lam_new)):
+                lam = lam_new
+                break
+            lam = lam_new
+        out_q.put((rank, lam, it))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_sharded_allgather_exchange_gloo():
+    import torch.multiprocessing as mp
+    from oracle import oracle as O
+    from pcsc_eigenvalue_solver_project_amd import synthetic as S
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_allgather, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1:] == res[1][1:]                          # identical decisions on every rank
+    n = 3000
+    rp, ci, v = S.uniform(n, 8)
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    ref = O.power_csc(cp, ri, vv, S.start_vector(n), 200, 1e-12)
+    assert abs(res[0][2] - ref["iterations"]) <= 1
+    assert abs(res[0][1] - ref["eigenvalue"]) <= 1e-10 * (1 + abs(ref["eigenvalue"]))

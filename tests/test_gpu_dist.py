@@ -38,3 +38,26 @@ def test_dist_single_rank_power_parity(kind):
         A.close()
     finally:
         ctx.close()
+
+
+def test_dist_single_rank_allgather_exchange(monkeypatch):
+    """The all-gather exchange (in-place ncclAllGather of the row blocks) run for real on one rank."""
+    monkeypatch.setenv("EIGSOL_DIST_EXCHANGE", "allgather")
+    n = 20000
+    rp, ci, v = S.uniform(n, 8)
+    ctx = D.DistContext(0, 0, 1, D.unique_id())
+    try:
+        A, sess = D.sharded_power_session(ctx, rp, ci, v, n, 0)
+        assert A.exchange == D.EXCHANGE_ALLGATHER
+        x0 = S.start_vector(n)
+        sess.begin(E.SolverOptions(300, 1e-12), x0)
+        sess.step(301)
+        assert sess.query()[0]
+        res = sess.finish()
+        cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+        ref = O.power_csc(cp, ri, vv, x0, 300, 1e-12, want_trace=True)
+        _assert_power_parity(res, ref, 1e-12)
+        sess.close()
+        A.close()
+    finally:
+        ctx.close()
