@@ -205,6 +205,13 @@ def run_config2(E, ctx, no_cpu):
         ev = r.eigenvalues_complex
         d, j = cKDTree(np.c_[ref.real, ref.imag]).query(np.c_[ev.real, ev.imag], k=1)
         out["vs_lapack_fixture"] = {"max_abs_diff": float(d.max()), "one_to_one": bool(len(np.unique(j)) == n)}
+    prof = os.path.join(ROOT, "profiles", "r01_qr4096_mfma.json")
+    if os.path.exists(prof):
+        d = json.load(open(prof))
+        out["mfma"] = {"gemm_TFLOPs": round(d["gemm_TFLOPs"], 2), "peak_TFLOPs": d["mfma_peak_TFLOPs"],
+                       "utilisation": round(d["mfma_utilisation"], 4), "gemm_flops": d["gemm_flops"],
+                       "source": "profiles/r01_qr4096_mfma.json (rocprofv3 kernel times of the Hessenberg "
+                                 "trailing-update GEMMs, v_mfma_f64_16x16x4_f64)"}
     if not no_cpu:
         from oracle import oracle as O
         m = 1024
