@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -228,6 +230,330 @@ __global__ __launch_bounds__(256) void win_gemm_fused(double* H, int64_t n, int 
     }
 }
 
+// ------------------------------------------------------------ one-wave Francis double shift
+// The textbook double-shift QR (the oracle's hqr_francis) on an n x n Hessenberg matrix in LDS,
+// run by ONE wave: every lane computes each 3x3 reflector redundantly from the same LDS words, so
+// no step needs a workgroup barrier and scalar values never travel through LDS; a wave's LDS
+// accesses execute in issue order, and compiler barriers keep them in program order.  kSchur:
+// full-row/column updates and the orthogonal factor V accumulated (real Schur form T = V S V^T,
+// block sizes in bs[]); otherwise the eigenvalue-only updates of the active block.  Exceptional
+// shifts at 10 and 20 sweeps are given in unshifted form (no diagonal shifting), every reflector
+// zeroes the bulge entries it consumes.  Eigenvalues go to wr/wi (complex pairs: -im, +im).
+#define EIGSOL_LDS_ORDER() asm volatile("" ::: "memory")
+
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+template <bool kSchur>
+__device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double* wr, double* wi, int* bs,
+                         int& fail, int& total, int& maxsw) {
+    const int lane = threadIdx.x & 63;
+    auto T = [&](int i, int j) -> double& { return t[i + j * LD]; };
+    auto V = [&](int i, int j) -> double& { return v[i + j * LD]; };
+    const double eps = 2.220446049250313e-16;
+    int nn = n - 1, its = 0;
+    fail = 0;
+    total = 0;
+    maxsw = 0;
+    EIGSOL_LDS_ORDER();
+    while (nn >= 0) {
+        int lm = 0;
+        for (int l = 1 + lane; l <= nn; l += 64) {
+            const double s0 = fabs(T(l - 1, l - 1)) + fabs(T(l, l));
+            const double h = T(l, l - 1);
+            if (h == 0.0 || fabs(h) <= eps * s0) lm = l;    // ascending per lane: the last is the max
+        }
+        const int l = __builtin_amdgcn_readfirstlane(wave_max_int(lm));
+        EIGSOL_LDS_ORDER();
+        if (l > 0 && lane == 0) T(l, l - 1) = 0.0;
+        EIGSOL_LDS_ORDER();
+        const double x = T(nn, nn);
+        if (l == nn) {
+            if (lane == 0) {
+                wr[nn] = x;
+                wi[nn] = 0.0;
+                if (kSchur) bs[nn] = 1;
+            }
+            --nn;
+            maxsw = max(maxsw, its);
+            its = 0;
+            EIGSOL_LDS_ORDER();
+            continue;
+        }
+        const double y = T(nn - 1, nn - 1), w = T(nn, nn - 1) * T(nn - 1, nn);
+        if (l == nn - 1) {
+            if (lane == 0) {
+                const double p = 0.5 * (y - x), q = p * p + w, z = sqrt(fabs(q));
+                if (q >= 0.0) {
+                    const double zz = p + (p >= 0 ? fabs(z) : -fabs(z));
+                    wr[nn - 1] = wr[nn] = x + zz;
+                    if (zz != 0.0) wr[nn] = x - w / zz;
+                    wi[nn - 1] = wi[nn] = 0.0;
+                } else {
+                    wr[nn - 1] = wr[nn] = x + p;
+                    wi[nn - 1] = -z;
+                    wi[nn] = z;
+                }
+                if (kSchur) bs[nn] = bs[nn - 1] = 2;
+            }
+            nn -= 2;
+            maxsw = max(maxsw, its);
+            its = 0;
+            EIGSOL_LDS_ORDER();
+            continue;
+        }
+        if (its >= maxits) {
+            fail = 1;
+            break;
+        }
+        double xs = x, ys = y, ws = w;
+        if (its == 10 || its == 20) {
+            const double sc = fabs(T(nn, nn - 1)) + fabs(T(nn - 1, nn - 2));
+            xs = ys = x + 0.75 * sc;
+            ws = -0.4375 * sc * sc;
+        }
+        ++its;
+        ++total;
+        const int m = l;
+        double p0, q0, r0;
+        {
+            const double z = T(m, m), rr = xs - z, ss = ys - z;
+            p0 = (rr * ss - ws) / T(m + 1, m) + T(m, m + 1);
+            q0 = T(m + 1, m + 1) - z - rr - ss;
+            r0 = T(m + 2, m + 1);
+            const double sc = fabs(p0) + fabs(q0) + fabs(r0);
+            p0 /= sc; q0 /= sc; r0 /= sc;
+        }
+        for (int i = m + lane; i <= nn - 2; i += 64) {
+            T(i + 2, i) = 0.0;
+            if (i != m) T(i + 2, i - 1) = 0.0;
+        }
+        EIGSOL_LDS_ORDER();
+        const int jend = kSchur ? n : nn + 1;      // left updates: to the matrix end (Schur) or the block end
+        const int ibeg = kSchur ? 0 : l;           // right updates: from row 0 (Schur) or the block top
+        for (int k = m; k <= nn - 1; ++k) {
+            double p = p0, q = q0, r = r0, xk = 1.0;
+            const bool three = k != nn - 1;
+            if (k != m) {
+                p = T(k, k - 1);
+                q = T(k + 1, k - 1);
+                r = three ? T(k + 2, k - 1) : 0.0;
+                xk = fabs(p) + fabs(q) + fabs(r);
+                if (xk != 0.0) { p /= xk; q /= xk; r /= xk; }
+            }
+            const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(p * p + q * q + r * r);
+            if (sg == 0.0) continue;
+            EIGSOL_LDS_ORDER();
+            if (lane == 0) {
+                if (k == m) {
+                    if (l != m) T(k, k - 1) = -T(k, k - 1);
+                } else {
+                    T(k, k - 1) = -sg * xk;
+                    T(k + 1, k - 1) = 0.0;
+                    if (three) T(k + 2, k - 1) = 0.0;
+                }
+            }
+            p += sg;
+            const double ax = p / sg, ay = q / sg, az = r / sg, bq = q / p, br = r / p;
+            for (int j = k + lane; j < jend; j += 64) {
+                double pp = T(k, j) + bq * T(k + 1, j);
+                if (three) { pp += br * T(k + 2, j); T(k + 2, j) -= pp * az; }
+                T(k + 1, j) -= pp * ay;
+                T(k, j) -= pp * ax;
+            }
+            EIGSOL_LDS_ORDER();
+            const int imax = nn < k + 3 ? nn : k + 3;
+            for (int i = ibeg + lane; i <= imax; i += 64) {
+                double pp = ax * T(i, k) + ay * T(i, k + 1);
+                if (three) { pp += az * T(i, k + 2); T(i, k + 2) -= pp * br; }
+                T(i, k + 1) -= pp * bq;
+                T(i, k) -= pp;
+            }
+            if (kSchur)
+                for (int i = lane; i < n; i += 64) {
+                    double pp = ax * V(i, k) + ay * V(i, k + 1);
+                    if (three) { pp += az * V(i, k + 2); V(i, k + 2) -= pp * br; }
+                    V(i, k + 1) -= pp * bq;
+                    V(i, k) -= pp;
+                }
+            EIGSOL_LDS_ORDER();
+        }
+    }
+    maxsw = max(maxsw, its);
+}
+
+constexpr int kHqrWaveMax = 128;
+
+// eigenvalues of an n x n (n <= 128) Hessenberg block: info = {fail, most sweeps per deflation, total}
+__global__ __launch_bounds__(64) void hqr_wave_kernel(const double* Hin, int64_t ld, int n, double* wr, double* wi,
+                                                      int maxits, int* info) {
+    constexpr int LD = kHqrWaveMax + 1;
+    __shared__ double t[kHqrWaveMax * LD];
+    for (int e = threadIdx.x; e < n * n; e += 64) {
+        const int i = e % n, j = e / n;
+        t[i + j * LD] = Hin[i + (int64_t)j * ld];
+    }
+    __syncthreads();
+    int fail, total, maxsw;
+    wave_hqr<false>(t, nullptr, n, LD, maxits, wr, wi, nullptr, fail, total, maxsw);
+    if (threadIdx.x == 0) {
+        info[0] = fail;
+        info[1] = maxsw;
+        info[2] = total;
+    }
+}
+
+// ------------------------------------------------------------ aggressive early deflation
+// (Braman, Byers & Mathias, 2002; LAPACK xLAQR3's idea, restated for one wave.)
+// The trailing nw x nw window T = H[kw:kw+nw, kw:kw+nw] of the active block is brought to real
+// Schur form T = V S V^T (wave_hqr<true>).  Coupled to the rest of the block only through the
+// spike s = H(kw, kw-1), the similarity turns that entry into the column s V(0, :)^T; trailing
+// Schur blocks whose spike entries are negligible (|s v| <= ulp |lambda|, LAPACK's test) are
+// deflated outright, scanning from the bottom up to the first block that is not.  When some
+// deflate, the undeflated top part with its spike is reduced back to Hessenberg form (Householder,
+// accumulated into V), the window and the new H(kw, kw-1) are written back and the caller applies
+// V to the rows above the window (H[l:kw, kw:kw+nw] V, the only other part an eigenvalue-only
+// iteration reads).  The undeflated eigenvalues are the next sweep's shifts.
+constexpr int kAedMax = 96;
+
+struct AedCtl {
+    int nd;
+    double beta, tau;
+};
+
+__global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, int nw, int spike_valid, int maxits,
+                                                 double* wr, double* wi, double* Vout, int* info) {
+    constexpr int LD = kAedMax + 1;
+    __shared__ double t[kAedMax * LD];
+    __shared__ double v[kAedMax * LD];
+    __shared__ double hv[kAedMax];        // Householder vector
+    __shared__ double sp[kAedMax];
+    __shared__ int bs[kAedMax];           // Schur block size ending at each row (1 or 2)
+    __shared__ AedCtl c;
+    const int tid = threadIdx.x, nt = 64;
+    auto T = [&](int i, int j) -> double& { return t[i + j * LD]; };
+    auto V = [&](int i, int j) -> double& { return v[i + j * LD]; };
+    for (int e = tid; e < nw * nw; e += nt) {
+        const int i = e % nw, j = e / nw;
+        T(i, j) = H[(kw + i) + (int64_t)(kw + j) * n];
+        V(i, j) = i == j ? 1.0 : 0.0;
+    }
+    const double spike = (spike_valid && kw > 0) ? H[kw + (int64_t)(kw - 1) * n] : 0.0;
+    __syncthreads();
+    const double eps = 2.220446049250313e-16;
+    int fail, total, maxsw;
+    // ---------------- phase A: real Schur form with V
+    wave_hqr<true>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw);
+    __syncthreads();
+    // ---------------- phase B: spike test from the bottom
+    if (tid == 0) {
+        int nd = 0;
+        if (!fail) {
+            const double smlnum = 2.2250738585072014e-308 * (nw / eps);
+            int j = nw - 1;
+            while (j >= 0) {
+                const int b = bs[j];
+                double foo, spk;
+                if (b == 1) {
+                    foo = fabs(T(j, j));
+                    if (foo == 0.0) foo = fabs(spike);
+                    spk = fabs(spike * V(0, j));
+                } else {
+                    foo = fabs(T(j, j)) + sqrt(fabs(T(j, j - 1))) * sqrt(fabs(T(j - 1, j)));
+                    if (foo == 0.0) foo = fabs(spike);
+                    spk = fmax(fabs(spike * V(0, j)), fabs(spike * V(0, j - 1)));
+                }
+                if (spk > fmax(smlnum, eps * foo)) break;
+                nd += b;
+                j -= b;
+            }
+        }
+        c.nd = nd;
+        c.beta = 0.0;
+    }
+    __syncthreads();
+    const int nd = c.nd, m = nw - nd;
+    // ---------------- phase C: undeflated part + spike back to Hessenberg form
+    // apply P = I - tau hv hv^T (hv[0..len), hv[0] = 1) to rows/columns [o, o + len)
+    auto reflect = [&](int o, int len, int jlo) {
+        const double tau = c.tau;
+        for (int j = jlo + tid; j < nw; j += nt) {                       // left: T[o:o+len, jlo:nw]
+            double w = 0.0;
+            for (int i = 0; i < len; ++i) w += hv[i] * T(o + i, j);
+            w *= tau;
+            for (int i = 0; i < len; ++i) T(o + i, j) -= w * hv[i];
+        }
+        __syncthreads();
+        for (int i = tid; i < m; i += nt) {                              // right: T[0:m, o:o+len]
+            double w = 0.0;
+            for (int jj = 0; jj < len; ++jj) w += T(i, o + jj) * hv[jj];
+            w *= tau;
+            for (int jj = 0; jj < len; ++jj) T(i, o + jj) -= w * hv[jj];
+        }
+        for (int i = tid; i < nw; i += nt) {                             // V[:, o:o+len]
+            double w = 0.0;
+            for (int jj = 0; jj < len; ++jj) w += V(i, o + jj) * hv[jj];
+            w *= tau;
+            for (int jj = 0; jj < len; ++jj) V(i, o + jj) -= w * hv[jj];
+        }
+        __syncthreads();
+    };
+    // Householder vector of x[0..len) (thread 0): hv[0] = 1, c.tau, returns beta
+    auto house = [&](const double* x, int len) -> double {
+        const double alpha = x[0];
+        double xn = 0.0;
+        for (int i = 1; i < len; ++i) xn += x[i] * x[i];
+        xn = sqrt(xn);
+        hv[0] = 1.0;
+        if (xn == 0.0) {
+            c.tau = 0.0;
+            for (int i = 1; i < len; ++i) hv[i] = 0.0;
+            return alpha;
+        }
+        const double beta = -(alpha >= 0 ? 1.0 : -1.0) * sqrt(alpha * alpha + xn * xn);
+        c.tau = (beta - alpha) / beta;
+        const double sc = 1.0 / (alpha - beta);
+        for (int i = 1; i < len; ++i) hv[i] = x[i] * sc;
+        return beta;
+    };
+    if (nd > 0 && m > 0) {
+        if (tid == 0) {
+            for (int i = 0; i < m; ++i) sp[i] = spike * V(0, i);
+            c.tau = 0.0;
+            c.beta = m > 1 ? house(sp, m) : sp[0];
+        }
+        __syncthreads();
+        if (m > 1 && c.tau != 0.0) reflect(0, m, 0);
+        for (int col = 0; col + 2 < m; ++col) {
+            if (tid == 0) {
+                const double b = house(&T(col + 1, col), m - col - 1);
+                T(col + 1, col) = b;
+                for (int i = col + 2; i < m; ++i) T(i, col) = 0.0;
+            }
+            __syncthreads();
+            if (c.tau != 0.0) reflect(col + 1, m - col - 1, col + 1);
+        }
+    }
+    // ---------------- phase D: write back (only when something deflated)
+    if (nd > 0) {
+        for (int e = tid; e < nw * nw; e += nt) {
+            const int i = e % nw, j = e / nw;
+            H[(kw + i) + (int64_t)(kw + j) * n] = i > j + 1 ? 0.0 : T(i, j);
+            Vout[e] = V(i, j);
+        }
+        if (tid == 0 && spike_valid && kw > 0) H[kw + (int64_t)(kw - 1) * n] = c.beta;
+    }
+    if (tid == 0) {
+        info[0] = fail;
+        info[1] = nd;
+        info[2] = total;
+        info[3] = m;
+    }
+}
+
 // diagonal and subdiagonal of the block [0, ihi]: out[0..n) = h(i,i), out[n..2n) = h(i,i-1)
 __global__ void diag_sub_kernel(const double* H, int64_t n, int ihi, double* out) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -241,7 +567,24 @@ __global__ void zero_entry_kernel(double* H, int64_t n, int i, int j) { H[i + (i
 }  // namespace dev
 
 // ---------------------------------------------------------------------------------- host loop
-static constexpr int kSmall = 128;   // blocks finished by the in-LDS solver
+// eigenvalues of an n <= 128 Hessenberg block in LDS: the one-wave solver (EIGSOL_HQR_WAVE=0: the
+// workgroup solver of qr.hip, for A/B)
+static int hqr_small(hipStream_t st, const double* H, int64_t ld, int n, int maxits, double* wr, double* wi,
+                     int* info) {
+    static const bool wave = [] {
+        const char* e = std::getenv("EIGSOL_HQR_WAVE");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (!wave) return hqr_lds(st, H, ld, n, maxits, wr, wi, info);
+    hipLaunchKernelGGL(dev::hqr_wave_kernel, dim3(1), dim3(64), 0, st, H, ld, n, wr, wi, maxits, info);
+    EIGSOL_HIP(hipGetLastError());
+    return EIGSOL_OK;
+}
+
+static constexpr int kSmallDefault = 128;
+// AED window: 40 measured best at 4096 (32: 2.63 s, 40: 2.58 s, 48: 2.60 s, 64: 2.92 s, 96: 4.28 s, off: 2.89 s);
+// the window's one-wave Schur factorisation costs O(nw^3) latency-bound steps
+static constexpr int kAedDefault = 40;   // blocks finished by the in-LDS solver (EIGSOL_QR_SMALL)
 
 int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double* wr, double* wi,
                       int32_t* sweeps_out, int32_t* fail_out) {
@@ -262,9 +605,20 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     int stall = 0;               // sweeps on the current bottom block without a deflation
     // `sweeps` tracks the largest number of sweeps any single deflation needed
     const int max_stall = std::max(1, maxits);
+    static const int kSmall = [] {
+        const char* e = std::getenv("EIGSOL_QR_SMALL");
+        return e ? std::max(16, std::min(128, std::atoi(e))) : kSmallDefault;
+    }();
+    static const bool stats = std::getenv("EIGSOL_QR_STATS") != nullptr;
+    static const int aed_win = [] {
+        const char* e = std::getenv("EIGSOL_QR_AED");   // AED window (0: off)
+        return e ? std::max(0, std::min(dev::kAedMax, std::atoi(e))) : kAedDefault;
+    }();
+    constexpr int kNibble = 14;   // % of the AED window deflated that skips the sweep (LAPACK's NIBBLE)
+    int st_sweeps = 0, st_windows = 0, st_small = 0, st_small_rows = 0, st_aed = 0, st_aed_defl = 0;
     auto finish_small = [&](int l, int hi) -> int {
         const int m = hi - l + 1;
-        EIGSOL_TRY(hqr_lds(st, H + l + (int64_t)l * n, n, m, std::max(1, maxits), dwr + l, dwi + l, dinfo));
+        EIGSOL_TRY(hqr_small(st, H + l + (int64_t)l * n, n, m, std::max(1, maxits), dwr + l, dwi + l, dinfo));
         int info[3];
         EIGSOL_HIP(hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(hipStreamSynchronize(st));
@@ -288,6 +642,8 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         }
         const int N = ihi - l + 1;
         if (N <= kSmall) {
+            ++st_small;
+            st_small_rows += N;
             rc = finish_small(l, ihi);
             ihi = l - 1;
             sweeps = std::max(sweeps, stall);
@@ -295,17 +651,60 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             continue;
         }
         if (++stall > max_stall) { failed = 1; sweeps = std::max(sweeps, stall); break; }
-        // shifts: eigenvalues of the trailing 2nb x 2nb block
-        const int nb = std::min(dev::kMaxBulges, std::max(1, N / 8));
-        const int ns = 2 * nb;
-        rc = hqr_lds(st, H + (ihi - ns + 1) + (int64_t)(ihi - ns + 1) * n, n, ns, 60, dwr + ihi - ns + 1,
-                     dwi + ihi - ns + 1, dinfo);
-        if (rc != EIGSOL_OK) break;
-        if (hipMemcpyAsync(swr.data(), dwr + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipMemcpyAsync(swi.data(), dwi + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) {
-            rc = fail(EIGSOL_E_HIP, "francis: shifts");
-            break;
+        // aggressive early deflation on the trailing window; its undeflated eigenvalues are the shifts
+        int nb = std::min(dev::kMaxBulges, std::max(1, N / 8));
+        int ns = 2 * nb;
+        bool have_shifts = false;
+        if (aed_win > 0) {
+            const int nw = std::min(aed_win, N);
+            const int kw = ihi - nw + 1;
+            hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(64), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60, dwr, dwi,
+                               dU, dinfo);
+            int info[4];
+            std::vector<double> awr(nw), awi(nw);
+            if (hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(awr.data(), dwr + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(awi.data(), dwi + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
+                rc = fail(EIGSOL_E_HIP, "francis: aed");
+                break;
+            }
+            ++st_aed;
+            if (!info[0]) {
+                const int nd = info[1], m = info[3];
+                if (nd > 0) {
+                    st_aed_defl += nd;
+                    const int nr = kw > l ? (kw - l + 15) / 16 : 0;
+                    if (nr > 0)
+                        hipLaunchKernelGGL(dev::win_gemm_fused, dim3(nr), dim3(256), 0, st, H, n, kw, nw, (int64_t)0,
+                                           (int64_t)0, 0, (int64_t)l, (int64_t)kw, dU);
+                    ihi = kw + m - 1;
+                    sweeps = std::max(sweeps, stall);
+                    stall = 0;
+                    if (100 * nd >= kNibble * nw || m < 4) continue;   // enough deflated: look again first
+                }
+                // shifts: the bottom undeflated eigenvalues of the window
+                const int N2 = ihi - l + 1;
+                nb = std::min({dev::kMaxBulges, std::max(1, N2 / 8), std::max(1, m / 2)});
+                ns = 2 * nb;
+                for (int i = 0; i < ns; ++i) {
+                    swr[i] = awr[m - ns + i];
+                    swi[i] = awi[m - ns + i];
+                }
+                have_shifts = true;
+            }
+        }
+        if (!have_shifts) {
+            // shifts: eigenvalues of the trailing 2nb x 2nb block
+            rc = hqr_small(st, H + (ihi - ns + 1) + (int64_t)(ihi - ns + 1) * n, n, ns, 60, dwr + ihi - ns + 1,
+                           dwi + ihi - ns + 1, dinfo);
+            if (rc != EIGSOL_OK) break;
+            if (hipMemcpyAsync(swr.data(), dwr + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(swi.data(), dwi + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
+                rc = fail(EIGSOL_E_HIP, "francis: shifts");
+                break;
+            }
         }
         // pair the shifts: conjugate pairs stay together, reals are paired in order;
         // every 6th stalled sweep uses exceptional shifts from the bottom subdiagonal
@@ -345,6 +744,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             rc = fail(EIGSOL_E_HIP, "francis: shift upload");
             break;
         }
+        ++st_sweeps;
         // chase the chain window by window
         const int T = (ihi - 1 - l) + 3 * (nb - 1) + 1;
         int t0 = 0;
@@ -363,6 +763,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                 ++t1;
             }
             if (t1 == t0) { rc = fail(EIGSOL_E_SOLVER, "francis: window did not advance (internal error)"); break; }
+            ++st_windows;
             dev::ChaseArgs ca{H, n, s, e, l, ihi, t0, t1, nb, dsh, dU};
             hipLaunchKernelGGL(dev::chase_kernel, dim3(1), dim3(1024), 0, st, ca);
             const int W = e - s;
@@ -394,6 +795,10 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             hipStreamSynchronize(st) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "francis: download");
     }
+    if (stats)
+        std::fprintf(stderr, "francis: n=%lld sweeps=%d windows=%d small_blocks=%d small_rows=%d kSmall=%d aed=%d "
+                     "aed_deflated=%d aed_win=%d\n",
+                     (long long)n, st_sweeps, st_windows, st_small, st_small_rows, kSmall, st_aed, st_aed_defl, aed_win);
     for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo}) (void)hipFree(p);
     // iterations reported: sweeps spent on the slowest deflation (>= 1, the final check), so that
     // iterations <= maxIterations exactly when the iteration converged
