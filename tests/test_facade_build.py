@@ -12,3 +12,11 @@ from cpp_build import ROOT, build
 def test_facade_compiles_and_links(tmp_path):
     out = build(os.path.join(ROOT, "tests", "cpp", "test_facade.cpp"), str(tmp_path / "test_facade"))
     assert os.path.getsize(out) > 0
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "pcsc_eigenvalue_solver_project_amd", "libeigsol_hip.so")),
+                    reason="library not built")
+def test_demo_cli_compiles(tmp_path):
+    """examples/eigsol_demo.cpp (the reference main.cpp's counterpart) builds with -Werror."""
+    out = build(os.path.join(ROOT, "examples", "eigsol_demo.cpp"), str(tmp_path / "eigsol_demo"))
+    assert os.path.getsize(out) > 0
