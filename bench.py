@@ -219,12 +219,32 @@ def run_config2(E, ctx, no_cpu):
         t = time.perf_counter()
         O.hqr_francis(O.hessenberg(B))
         dc = time.perf_counter() - t
+        th = host_cpu()["threads_allowed"]
+        t = time.perf_counter()
+        np.linalg.eigvals(A)
+        dl = time.perf_counter() - t
+        out["cpu_allcores"] = {"value": round(n / dl, 1), "unit": "eigvals/s", "cores": th, "kind": "lapack",
+                               "sample": f"numpy.linalg.eigvals (LAPACK dgeev: dgehrd + multishift dhseqr with AED, "
+                                         f"the implicit-shift algorithm class the device runs) on the same 4096^2 "
+                                         f"matrix, {dl:.2f}s, BLAS threads = OMP_NUM_THREADS"}
         out["cpu_baseline"] = {
             "value": round(m / dc, 1), "unit": "eigvals/s", "cores": 1, "kind": "port",
             "sample": f"{m}x{m} N(0,1): oracle Hessenberg + textbook Francis double shift (oracle/eigsol_oracle.cpp,"
                       f" 1 thread) {dc:.2f}s; n^3 scaling to 4096 gives {round(4096 / (dc * (4096 / m) ** 3), 1)}"
                       f" eigvals/s.  The reference's own unshifted iteration does not converge on this input"}
     return out
+
+
+def run_config1(E, S, ctx):
+    """BASELINE config 1: data/A.txt read as double (the reference's text format), power method."""
+    path = os.path.join(ROOT, "tests", "golden", "A.txt")
+    tok = open(path).read().split()
+    r_, c_ = int(tok[1]), int(tok[2])
+    A = np.array([float(t) for t in tok[3:3 + r_ * c_]]).reshape(r_, c_)   # row by row, like the reader
+    res = E.power_method(E.DenseMatrix(ctx, A), E.SolverOptions(1000, 1e-10), S.start_vector(r_))
+    exact = 1.0 + np.sqrt(15.0)
+    return {"eigenvalue": res.eigenvalue, "iterations": res.iterations, "converged": res.converged,
+            "abs_error_vs_1_plus_sqrt15": abs(res.eigenvalue - exact)}
 
 
 def run_config5(E, S, ctx, torch, stream, no_cpu):
@@ -258,6 +278,17 @@ def run_config5(E, S, ctx, torch, stream, no_cpu):
            "converged": res.converged, "abs_error_vs_planted_eigenvalue": float(abs(res.eigenvalue - target)),
            "analysis_seconds": round(t_factor, 3), "solve_seconds": round(t_solve, 4)}
     sess.close()
+    # the same complex matrix in the fused power iteration: the complex SpMV rate (SURVEY §8d asks
+    # for both the SpMV and the SpTRSV GB/s of config 5)
+    ps = E.PowerSession(A)
+    ps.begin(E.SolverOptions(2**31 - 1, -1.0), x0)
+    ps.step(5)
+    torch.cuda.synchronize()
+    ms_mv = _events(torch, stream, lambda: ps.step(50)) / 50
+    pinfo = ps.kernel_info()
+    out["spmv"] = {"ms_per_iteration": round(ms_mv, 4),
+                   "GB/s": round(pinfo["bytes_per_iteration"] / (ms_mv / 1e3) / 1e9, 2), "kernel": pinfo["kernel"]}
+    ps.close()
     if not no_cpu:
         from oracle import oracle as O
         t = time.perf_counter()
@@ -389,6 +420,7 @@ def main():
     if not args.no_extras and world == 1:
         out["extras"] = {
             "config3_csr_1Mx16": run_config3(E, S, ctx, torch, torch_stream, opts),
+            "config1_A_txt": run_config1(E, S, ctx),
             "config2_qr_4096": run_config2(E, ctx, args.no_cpu_baseline),
             "config5_shifted_inverse_1M": run_config5(E, S, ctx, torch, torch_stream, args.no_cpu_baseline),
         }
