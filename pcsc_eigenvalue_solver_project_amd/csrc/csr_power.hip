@@ -48,6 +48,33 @@ __device__ __forceinline__ T ldg(const T* base, uint32_t i) {
     return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) +
                                        (uint64_t)(i * (uint32_t)sizeof(T)));
 }
+// streaming (read-once) variant: non-temporal, so the matrix stream does not evict the x windows
+#ifndef EIGSOL_STREAM_NT
+#define EIGSOL_STREAM_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ T ldg_stream(const T* base, uint32_t i) {
+    const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (uint64_t)(i * (uint32_t)sizeof(T)));
+#if EIGSOL_STREAM_NT
+    if constexpr (std::is_arithmetic_v<T>) {
+        return __builtin_nontemporal_load(p);
+    } else if constexpr (sizeof(T) == 16) {           // double2, cplx, int4
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+        T r;
+        __builtin_memcpy(&r, &v, 16);
+        return r;
+    } else {                                          // int2 and other 8-byte aggregates
+        static_assert(sizeof(T) == 8, "ldg_stream: unsupported width");
+        const long long v = __builtin_nontemporal_load(reinterpret_cast<const long long*>(p));
+        T r;
+        __builtin_memcpy(&r, &v, 8);
+        return r;
+    }
+#else
+    return *p;
+#endif
+}
 
 // Tile metadata is read-only for the whole launch and indexed uniformly: scalar loads (constant
 // address space) keep it off the vector memory counter.
@@ -127,15 +154,15 @@ __device__ __forceinline__ void load_tile(const CsrArgs<S>& a, int4 m, TileRegs<
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             const uint32_t q = (uint32_t)(q0 + 2 * (tid + p * kThreads));
-            R.s[p].v = ldg(reinterpret_cast<const double2*>(a.val), q >> 1);
-            R.s[p].c = ldg(reinterpret_cast<const int2*>(a.col), q >> 1);
+            R.s[p].v = ldg_stream(reinterpret_cast<const double2*>(a.val), q >> 1);
+            R.s[p].c = ldg_stream(reinterpret_cast<const int2*>(a.col), q >> 1);
         }
     } else {
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             const uint32_t q = (uint32_t)(m.z + tid + p * kThreads);
-            R.s[p].v = ldg(a.val, q);
-            R.s[p].c = ldg(a.col, q);
+            R.s[p].v = ldg_stream(a.val, q);
+            R.s[p].c = ldg_stream(a.col, q);
         }
     }
     const uint32_t r = (uint32_t)min(m.x + tid, a.nrows - 1);
@@ -469,15 +496,15 @@ __device__ __forceinline__ void load_tile_w(const CsrArgs<S>& a, int4 m, WTileRe
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             const uint32_t q = (uint32_t)(q0 + 2 * (tid + p * kThreads));
-            R.s[p].v = ldg(reinterpret_cast<const double2*>(a.val), q >> 1);
-            R.s[p].c = ldg(reinterpret_cast<const uint32_t*>(a.col16), q >> 1);
+            R.s[p].v = ldg_stream(reinterpret_cast<const double2*>(a.val), q >> 1);
+            R.s[p].c = ldg_stream(reinterpret_cast<const uint32_t*>(a.col16), q >> 1);
         }
     } else {
 #pragma unroll
         for (int p = 0; p < P; ++p) {
             const uint32_t q = (uint32_t)(m.z + tid + p * kThreads);
-            R.s[p].v = ldg(a.val, q);
-            R.s[p].c = ldg(a.col16, q);
+            R.s[p].v = ldg_stream(a.val, q);
+            R.s[p].c = ldg_stream(a.col16, q);
         }
     }
     const uint32_t r = (uint32_t)min(m.x + tid, a.nrows - 1);
@@ -700,16 +727,16 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
         const uint32_t b2 = ((uint32_t)m.x >> 1) + (uint32_t)lane;
 #pragma unroll
         for (int j = 0; j < SliceRegs<S, KB, kG>::NV; ++j)
-            R.v[j] = ldg(reinterpret_cast<const double2*>(a.sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
+            R.v[j] = ldg_stream(reinterpret_cast<const double2*>(a.sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
     } else {
 #pragma unroll
-        for (int u = 0; u < KB; ++u) R.v[u] = ldg(a.sval, base + 64u * (uint32_t)min(u, K - 1));
+        for (int u = 0; u < KB; ++u) R.v[u] = ldg_stream(a.sval, base + 64u * (uint32_t)min(u, K - 1));
     }
     if (m.y >= 0) {
         const int nw = (K + 3) >> 2;
 #pragma unroll
         for (int g = 0; g < KB / 4; ++g)
-            R.c[g] = ldg(a.scol8, (uint32_t)m.w + 64u * (uint32_t)min(g, nw - 1) + (uint32_t)lane);
+            R.c[g] = ldg_stream(a.scol8, (uint32_t)m.w + 64u * (uint32_t)min(g, nw - 1) + (uint32_t)lane);
         // the window always holds the slice's own rows (the Rayleigh term reads them)
         const int wl = max((m.z >> 9) & 0x1ff, 1);
 #pragma unroll
@@ -722,7 +749,7 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
     } else if constexpr (kG) {
 #pragma unroll
         for (int u = 0; u < KB; ++u)
-            R.c[u] = (uint32_t)ldg(a.scol32, (uint32_t)m.w + 64u * (uint32_t)min(u, K - 1) + (uint32_t)lane);
+            R.c[u] = (uint32_t)ldg_stream(a.scol32, (uint32_t)m.w + 64u * (uint32_t)min(u, K - 1) + (uint32_t)lane);
     }
 }
 
@@ -798,7 +825,7 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
         if constexpr (kPower) xi = scale_in(xin[rowc + a.xoff], nrm);
     }
     if (valid) {
-        yout[row] = sacc;
+        yout[row] = sacc;   // a non-temporal store measured slower: the next launch reads y as x
         if constexpr (kPower) {
             n2 += sq_abs(sacc);
             acc_dot(rr, ri, xi, sacc);
