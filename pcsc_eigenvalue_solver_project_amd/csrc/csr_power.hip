@@ -40,42 +40,6 @@ constexpr int kTileRows = 256;
 // One pad element every 32 keeps the lane-per-row phase-2 reads spread over the 64 banks.
 __device__ __forceinline__ int lds_idx(int k) { return k + (k >> 5); }
 
-// base + 32-bit element index: lets hipcc use the SGPR-base + 32-bit VGPR-offset form of
-// global_load instead of per-lane 64-bit address arithmetic.  Every stream the kernels index
-// this way is < 4 GiB (checked at upload).
-template <class T>
-__device__ __forceinline__ T ldg(const T* base, uint32_t i) {
-    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) +
-                                       (uint64_t)(i * (uint32_t)sizeof(T)));
-}
-// streaming (read-once) variant: non-temporal, so the matrix stream does not evict the x windows
-#ifndef EIGSOL_STREAM_NT
-#define EIGSOL_STREAM_NT 1
-#endif
-template <class T>
-__device__ __forceinline__ T ldg_stream(const T* base, uint32_t i) {
-    const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + (uint64_t)(i * (uint32_t)sizeof(T)));
-#if EIGSOL_STREAM_NT
-    if constexpr (std::is_arithmetic_v<T>) {
-        return __builtin_nontemporal_load(p);
-    } else if constexpr (sizeof(T) == 16) {           // double2, cplx, int4
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
-        T r;
-        __builtin_memcpy(&r, &v, 16);
-        return r;
-    } else {                                          // int2 and other 8-byte aggregates
-        static_assert(sizeof(T) == 8, "ldg_stream: unsupported width");
-        const long long v = __builtin_nontemporal_load(reinterpret_cast<const long long*>(p));
-        T r;
-        __builtin_memcpy(&r, &v, 8);
-        return r;
-    }
-#else
-    return *p;
-#endif
-}
-
 // Tile metadata is read-only for the whole launch and indexed uniformly: scalar loads (constant
 // address space) keep it off the vector memory counter.
 __device__ __forceinline__ int4 ld_uniform(const int4* p, int i) {

@@ -204,13 +204,13 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
         const int e0 = a.pptr[pos];
         m.e0 = e0;
         m.len = in ? a.pptr[pos + 1] - e0 : 0;
-        m.pv = a.ppiv[pos];
+        m.pv = ldg_stream(a.ppiv, (uint32_t)pos);
     };
     auto fetch2 = [&](RowMeta<S>& m) {         // the row's first 16 entries and its right side
         const bool ok = lane < m.len;
         const int e = ok ? m.e0 + lane : 0;
-        m.j = ok ? a.pcol[e] : -1;
-        m.v = a.pval[e];
+        m.j = ok ? (int)ldg_stream(a.pcol, (uint32_t)e) : -1;
+        m.v = ldg_stream(a.pval, (uint32_t)e);
         m.bi = xin[m.i >= 0 ? m.i : 0];
     };
 
