@@ -36,6 +36,9 @@ namespace dev {
 constexpr int kWin = 96;        // window rows/columns (H window + U: 2 x 72 KiB of LDS)
 constexpr int kMaxBulges = 16;
 
+// compiler-only ordering of LDS accesses (one wave's LDS operations execute in issue order)
+#define EIGSOL_LDS_ORDER() asm volatile("" ::: "memory")
+
 struct ChaseArgs {
     double* H;
     int64_t n;        // leading dimension
@@ -172,6 +175,132 @@ __global__ __launch_bounds__(1024) void chase_kernel(ChaseArgs a) {
     }
 }
 
+// The same chase with two barriers per step and no serial section.  Wave b owns bulge b for the
+// whole window: every lane computes the bulge's reflector redundantly from the same LDS words
+// (column k-1 of the window is only ever written by bulge b's own updates), then
+//   phase A: the left update of rows k..k+2 (columns [k, e)) and the U update (columns k..k+2);
+//   phase B: the right update of columns k..k+2 (rows [max(l, s), min(k+3, ihi)]).
+// Within a phase the bulges touch disjoint words: lefts own disjoint rows, rights disjoint
+// columns, and a left (rows k..k+2, columns >= k) meets neither the reflector column k-1 of its
+// own bulge nor the reflector columns of the others.  The barrier between the phases orders
+// left(b+1) before right(b) on their shared 3 x 3 block; the barrier after phase B orders
+// right(b) before the next step.  Each lane handles at most two columns / rows per phase, all
+// LDS reads issued before the dependent arithmetic.
+__global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs a) {
+    __shared__ double h[kWin * (kWin + 1)];
+    __shared__ double u[kWin * kWin];
+    const int W = a.e - a.s;
+    const int ldh = W | 1;
+    const int tid = threadIdx.x;
+    auto Hw = [&](int i, int j) -> double& { return h[(i - a.s) + (j - a.s) * ldh]; };
+    {
+        constexpr int kPer = (kWin * kWin + 1023) / 1024;
+        double tmp[kPer];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int idx = tid + q * 1024;
+            const int i = idx % W, j = idx / W;
+            tmp[q] = idx < W * W ? a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int idx = tid + q * 1024;
+            if (idx < W * W) {
+                const int i = idx % W, j = idx / W;
+                h[i + j * ldh] = tmp[q];
+                u[idx] = (i == j) ? 1.0 : 0.0;
+            }
+        }
+    }
+    __syncthreads();
+    const int l = a.l, ihi = a.ihi;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
+    const int rlo = max(l, a.s);
+    for (int t = a.t0; t < a.t1; ++t) {
+        const int k = l + t - 3 * wv;
+        bool act = wv < a.nb && k >= l && k <= ihi - 1;     // wave-uniform
+        const bool three = k != ihi - 1;
+        double ax = 0.0, ay = 0.0, az = 0.0, bq = 0.0, br = 0.0;
+        if (act) {
+            double p, q, r, xk = 1.0;
+            if (k == l) {
+                const double sx = a.shifts[2 * wv], sw = a.shifts[2 * wv + 1];
+                const double z = Hw(l, l);
+                const double rr = sx - z;
+                p = (rr * rr - sw) / Hw(l + 1, l) + Hw(l, l + 1);
+                q = Hw(l + 1, l + 1) - z - rr - rr;
+                r = (l + 2 <= ihi) ? Hw(l + 2, l + 1) : 0.0;
+                const double sc = fabs(p) + fabs(q) + fabs(r);
+                if (sc != 0.0) { const double is = 1.0 / sc; p *= is; q *= is; r *= is; }
+            } else {
+                p = Hw(k, k - 1);
+                q = Hw(k + 1, k - 1);
+                r = three ? Hw(k + 2, k - 1) : 0.0;
+                xk = fabs(p) + fabs(q) + fabs(r);
+                if (xk != 0.0) { const double is = 1.0 / xk; p *= is; q *= is; r *= is; }
+            }
+            const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(p * p + q * q + r * r);
+            act = sg != 0.0;
+            if (act) {
+                EIGSOL_LDS_ORDER();
+                if (k != l && ln == 0) {
+                    Hw(k, k - 1) = -sg * xk;
+                    Hw(k + 1, k - 1) = 0.0;
+                    if (three) Hw(k + 2, k - 1) = 0.0;
+                }
+                p += sg;
+                const double isg = 1.0 / sg, ip = 1.0 / p;
+                ax = p * isg; ay = q * isg; az = r * isg; bq = q * ip; br = r * ip;
+                // ---- phase A: left update, columns k + ln and k + ln + 64 of rows k..k+2
+                const int j0 = k + ln, j1 = j0 + 64;
+                const bool c0 = j0 < a.e, c1 = j1 < a.e;
+                double h00 = 0, h01 = 0, h02 = 0, h10 = 0, h11 = 0, h12 = 0;
+                if (c0) { h00 = Hw(k, j0); h01 = Hw(k + 1, j0); if (three) h02 = Hw(k + 2, j0); }
+                if (c1) { h10 = Hw(k, j1); h11 = Hw(k + 1, j1); if (three) h12 = Hw(k + 2, j1); }
+                // U columns k..k+2 (window-relative), rows ln and ln + 64
+                double* u0 = u + (k - a.s) * W;
+                const int i0 = ln, i1 = ln + 64;
+                const bool d0 = i0 < W, d1 = i1 < W;
+                double u00 = 0, u01 = 0, u02 = 0, u10 = 0, u11 = 0, u12 = 0;
+                if (d0) { u00 = u0[i0]; u01 = u0[i0 + W]; if (three) u02 = u0[i0 + 2 * W]; }
+                if (d1) { u10 = u0[i1]; u11 = u0[i1 + W]; if (three) u12 = u0[i1 + 2 * W]; }
+                {
+                    const double p0 = h00 + bq * h01 + (three ? br * h02 : 0.0);
+                    const double p1 = h10 + bq * h11 + (three ? br * h12 : 0.0);
+                    if (c0) { Hw(k, j0) = h00 - p0 * ax; Hw(k + 1, j0) = h01 - p0 * ay; if (three) Hw(k + 2, j0) = h02 - p0 * az; }
+                    if (c1) { Hw(k, j1) = h10 - p1 * ax; Hw(k + 1, j1) = h11 - p1 * ay; if (three) Hw(k + 2, j1) = h12 - p1 * az; }
+                }
+                {
+                    const double p0 = ax * u00 + ay * u01 + (three ? az * u02 : 0.0);
+                    const double p1 = ax * u10 + ay * u11 + (three ? az * u12 : 0.0);
+                    if (d0) { u0[i0] = u00 - p0; u0[i0 + W] = u01 - p0 * bq; if (three) u0[i0 + 2 * W] = u02 - p0 * br; }
+                    if (d1) { u0[i1] = u10 - p1; u0[i1 + W] = u11 - p1 * bq; if (three) u0[i1 + 2 * W] = u12 - p1 * br; }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- phase B: right update, rows rlo + ln and rlo + ln + 64 of columns k..k+2
+        if (act) {
+            const int ilast = min(k + 3, ihi);
+            const int i0 = rlo + ln, i1 = i0 + 64;
+            const bool c0 = i0 <= ilast, c1 = i1 <= ilast;
+            double h00 = 0, h01 = 0, h02 = 0, h10 = 0, h11 = 0, h12 = 0;
+            if (c0) { h00 = Hw(i0, k); h01 = Hw(i0, k + 1); if (three) h02 = Hw(i0, k + 2); }
+            if (c1) { h10 = Hw(i1, k); h11 = Hw(i1, k + 1); if (three) h12 = Hw(i1, k + 2); }
+            const double p0 = ax * h00 + ay * h01 + (three ? az * h02 : 0.0);
+            const double p1 = ax * h10 + ay * h11 + (three ? az * h12 : 0.0);
+            if (c0) { Hw(i0, k) = h00 - p0; Hw(i0, k + 1) = h01 - p0 * bq; if (three) Hw(i0, k + 2) = h02 - p0 * br; }
+            if (c1) { Hw(i1, k) = h10 - p1; Hw(i1, k + 1) = h11 - p1 * bq; if (three) Hw(i1, k + 2) = h12 - p1 * br; }
+        }
+        __syncthreads();
+    }
+    for (int idx = tid; idx < W * W; idx += 1024) {
+        const int i = idx % W, j = idx / W;
+        a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] = h[i + j * ldh];
+        a.U[idx] = u[idx];
+    }
+}
+
 // Both delayed updates of a window in ONE launch: blocks [0, nl) take 16-column panels of
 //     H(s:e, c0:c1) <- U^T H(s:e, c0:c1)
 // and blocks [nl, nl + nr) 16-row panels of
@@ -242,7 +371,6 @@ __global__ __launch_bounds__(256) void win_gemm_fused(double* H, int64_t n, int 
 // block sizes in bs[]); otherwise the eigenvalue-only updates of the active block.  Exceptional
 // shifts at 10 and 20 sweeps are given in unshifted form (no diagonal shifting), every reflector
 // zeroes the bulge entries it consumes.  Eigenvalues go to wr/wi (complex pairs: -im, +im).
-#define EIGSOL_LDS_ORDER() asm volatile("" ::: "memory")
 
 __device__ __forceinline__ int wave_max_int(int v) {
 #pragma unroll
@@ -614,6 +742,12 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         return e ? std::max(16, std::min(128, std::atoi(e))) : kSmallDefault;
     }();
     static const bool stats = std::getenv("EIGSOL_QR_STATS") != nullptr;
+    static const bool chase_v1 = std::getenv("EIGSOL_CHASE_V1") != nullptr;   // A/B: three-barrier chase
+    static const int max_bulges = [] {                 // experiments: cap the bulges per chain
+        const char* e = std::getenv("EIGSOL_QR_NB");
+        return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : dev::kMaxBulges;
+    }();
+    long long st_steps = 0;
     static const int aed_win = [] {
         const char* e = std::getenv("EIGSOL_QR_AED");   // AED window (0: off)
         return e ? std::max(0, std::min(dev::kAedMax, std::atoi(e))) : kAedDefault;
@@ -656,7 +790,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         }
         if (++stall > max_stall) { failed = 1; sweeps = std::max(sweeps, stall); break; }
         // aggressive early deflation on the trailing window; its undeflated eigenvalues are the shifts
-        int nb = std::min(dev::kMaxBulges, std::max(1, N / 8));
+        int nb = std::min(max_bulges, std::max(1, N / 8));
         int ns = 2 * nb;
         bool have_shifts = false;
         if (aed_win > 0) {
@@ -689,7 +823,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                 }
                 // shifts: the bottom undeflated eigenvalues of the window
                 const int N2 = ihi - l + 1;
-                nb = std::min({dev::kMaxBulges, std::max(1, N2 / 8), std::max(1, m / 2)});
+                nb = std::min({max_bulges, std::max(1, N2 / 8), std::max(1, m / 2)});
                 ns = 2 * nb;
                 for (int i = 0; i < ns; ++i) {
                     swr[i] = awr[m - ns + i];
@@ -768,8 +902,10 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             }
             if (t1 == t0) { rc = fail(EIGSOL_E_SOLVER, "francis: window did not advance (internal error)"); break; }
             ++st_windows;
+            st_steps += t1 - t0;
             dev::ChaseArgs ca{H, n, s, e, l, ihi, t0, t1, nb, dsh, dU};
-            hipLaunchKernelGGL(dev::chase_kernel, dim3(1), dim3(1024), 0, st, ca);
+            if (chase_v1) hipLaunchKernelGGL(dev::chase_kernel, dim3(1), dim3(1024), 0, st, ca);
+            else hipLaunchKernelGGL(dev::chase_wave_kernel, dim3(1), dim3(1024), 0, st, ca);
             const int W = e - s;
             const int nlb = e <= ihi ? (ihi + 1 - e + 15) / 16 : 0;
             const int nrb = s > l ? (s - l + 15) / 16 : 0;
@@ -800,9 +936,10 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             rc = fail(EIGSOL_E_HIP, "francis: download");
     }
     if (stats)
-        std::fprintf(stderr, "francis: n=%lld sweeps=%d windows=%d small_blocks=%d small_rows=%d kSmall=%d aed=%d "
-                     "aed_deflated=%d aed_win=%d\n",
-                     (long long)n, st_sweeps, st_windows, st_small, st_small_rows, kSmall, st_aed, st_aed_defl, aed_win);
+        std::fprintf(stderr, "francis: n=%lld sweeps=%d windows=%d steps=%lld small_blocks=%d small_rows=%d kSmall=%d "
+                     "aed=%d aed_deflated=%d aed_win=%d\n",
+                     (long long)n, st_sweeps, st_windows, st_steps, st_small, st_small_rows, kSmall, st_aed, st_aed_defl,
+                     aed_win);
     for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo}) (void)hipFree(p);
     // iterations reported: sweeps spent on the slowest deflation (>= 1, the final check), so that
     // iterations <= maxIterations exactly when the iteration converged
