@@ -10,12 +10,18 @@
 //
 // Locality: the chain is chased inside an LDS window [s, e) of at most kWin rows/columns with
 // the window's orthogonal factor U accumulated alongside; the parts of the reflectors' updates
-// outside the window are applied afterwards as two small GEMMs (one fused launch),
+// outside the window are applied afterwards as small GEMMs on the fp64 matrix cores,
 //     H(s:e, e:ihi]   <- U^T H(s:e, e:ihi]        H[l, s) x [s, e) <- H[l, s) x [s, e) U,
 // so every HBM element of the active block is touched O(1) times per window instead of once per
-// reflector.  Shifts: eigenvalues of the trailing 2nb x 2nb block (in-LDS Francis solver,
-// hqr_lds_kernel); blocks of at most 128 rows are finished entirely in LDS.  Deflation: the
-// conventional criterion |h(k,k-1)| <= eps (|h(k,k)| + |h(k-1,k-1)|).
+// reflector.  Concurrency: the chain is split into C groups of 4+ bulges spaced kWin + 3 nbg
+// rows apart, each chased in its own window by its own workgroup (one CU each) in the same
+// launch; windows never overlap, and their delayed updates commute (left regions own disjoint
+// rows, right regions disjoint columns; a left region of a trailing window meets the right
+// region of a leading one, so all lefts run before all rights).  A chase step costs ~1.15 us
+// with 4 bulges and ~2.05 us with 16 (instruction issue of 16 waves on 4 SIMDs), so 4-bulge
+// groups move 1.8x more bulges per microsecond.  Shifts: the undeflated eigenvalues of the
+// aggressive-early-deflation window (aed_kernel), else the trailing block's; blocks of at most
+// 128 rows are finished entirely in LDS.  Deflation: |h(k,k-1)| <= eps (|h(k,k)| + |h(k-1,k-1)|).
 #include <algorithm>
 #include <cmath>
 #include <complex>
@@ -34,145 +40,38 @@ int hqr_lds(hipStream_t st, const double* H, int64_t ld, int n, int maxits, doub
 namespace dev {
 
 constexpr int kWin = 96;        // window rows/columns (H window + U: 2 x 72 KiB of LDS)
-constexpr int kMaxBulges = 16;
+constexpr int kMaxBulges = 24;   // shifts per sweep / 2 (at most 16 per window: one wave each)
 
 // compiler-only ordering of LDS accesses (one wave's LDS operations execute in issue order)
 #define EIGSOL_LDS_ORDER() asm volatile("" ::: "memory")
 
-struct ChaseArgs {
-    double* H;
-    int64_t n;        // leading dimension
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int kMaxGroups = 6;   // bulge groups chased concurrently, one window (workgroup) each
+
+// One window of a chase round: group g's bulges j = 0..nb-1 sit at rows k = l + t - 3 j for the
+// group-local steps t in [t0, t1); the window [s, e) holds them for the whole round.
+struct ChaseWin {
     int s, e;         // window [s, e)
-    int l, ihi;       // active block
-    int t0, t1;       // chase steps of this window
-    int nb;           // bulges in the chain
+    int t0, t1;       // group-local chase steps of this round
+    int nb;           // bulges of the group
     const double* shifts;   // per bulge: xs (= ys) and ws of the shift pair
     double* U;        // out: (e - s)^2 accumulated factor, column-major
 };
+struct ChaseArgs {
+    double* H;
+    int64_t n;        // leading dimension
+    int l, ihi;       // active block
+    ChaseWin w[kMaxGroups];   // window of workgroup blockIdx.x
+};
 
-__global__ __launch_bounds__(1024) void chase_kernel(ChaseArgs a) {
-    // H window with an odd leading dimension: the left updates walk a row across columns, and a
-    // stride of an even number of doubles would put every lane of a wave on the same LDS bank
-    __shared__ double h[kWin * (kWin + 1)];
-    __shared__ double u[kWin * kWin];
-    __shared__ double rp[kMaxBulges][6];   // xs, ys, zs, q, r, active (as double)
-    __shared__ int rk[kMaxBulges];
-    const int W = a.e - a.s;
-    const int ldh = W | 1;
-    const int tid = threadIdx.x;
-    const int nt = blockDim.x;
-    auto Hw = [&](int i, int j) -> double& { return h[(i - a.s) + (j - a.s) * ldh]; };
-    {
-        // window load: all global loads first (9 per thread), then the LDS stores
-        constexpr int kPer = (kWin * kWin + 1023) / 1024;
-        double tmp[kPer];
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            const int idx = tid + q * 1024;
-            const int i = idx % W, j = idx / W;
-            tmp[q] = idx < W * W ? a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] : 0.0;
-        }
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            const int idx = tid + q * 1024;
-            if (idx < W * W) {
-                const int i = idx % W, j = idx / W;
-                h[i + j * ldh] = tmp[q];
-                u[idx] = (i == j) ? 1.0 : 0.0;
-            }
-        }
-    }
-    __syncthreads();
-    const int l = a.l, ihi = a.ihi;
-    for (int t = a.t0; t < a.t1; ++t) {
-        // ---- reflectors of every active bulge (one thread per bulge)
-        if (tid < a.nb) {
-            const int b = tid;
-            const int k = l + t - 3 * b;
-            const bool live = k >= l && k <= ihi - 1;
-            rk[b] = k;
-            rp[b][5] = 0.0;
-            if (live) {
-                double p, q, r, xs = 1.0;
-                if (k == l) {
-                    // first column of (H - s1)(H - s2) e_l, shift pair given by (xs = ys, ws)
-                    const double sx = a.shifts[2 * b], sw = a.shifts[2 * b + 1];
-                    const double z = Hw(l, l);
-                    const double rr = sx - z, ss = sx - z;
-                    p = (rr * ss - sw) / Hw(l + 1, l) + Hw(l, l + 1);
-                    q = Hw(l + 1, l + 1) - z - rr - ss;
-                    r = (l + 2 <= ihi) ? Hw(l + 2, l + 1) : 0.0;
-                    const double sc = fabs(p) + fabs(q) + fabs(r);
-                    if (sc != 0.0) { const double is = 1.0 / sc; p *= is; q *= is; r *= is; }
-                } else {
-                    p = Hw(k, k - 1);
-                    q = Hw(k + 1, k - 1);
-                    r = (k != ihi - 1) ? Hw(k + 2, k - 1) : 0.0;
-                    xs = fabs(p) + fabs(q) + fabs(r);
-                    if (xs != 0.0) { const double is = 1.0 / xs; p *= is; q *= is; r *= is; }
-                }
-                // scaling by reciprocals: three divisions per reflector instead of eight (the
-                // step's serial latency); the reflector stays orthogonal to rounding
-                const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(p * p + q * q + r * r);
-                if (sg != 0.0) {
-                    if (k != l) {
-                        Hw(k, k - 1) = -sg * xs;
-                        Hw(k + 1, k - 1) = 0.0;
-                        if (k != ihi - 1) Hw(k + 2, k - 1) = 0.0;
-                    }
-                    p += sg;
-                    const double isg = 1.0 / sg, ip = 1.0 / p;
-                    rp[b][0] = p * isg;
-                    rp[b][1] = q * isg;
-                    rp[b][2] = r * isg;
-                    rp[b][3] = q * ip;
-                    rp[b][4] = r * ip;
-                    rp[b][5] = 1.0;
-                }
-            }
-        }
-        __syncthreads();
-        // ---- left updates: wave b owns bulge b; rows k..k+2, window columns j in [k, e)
-        const int wv = tid >> 6, ln = tid & 63;
-        if (wv < a.nb && rp[wv][5] != 0.0) {
-            const int k = rk[wv];
-            const double xs = rp[wv][0], ys = rp[wv][1], zs = rp[wv][2], q = rp[wv][3], r = rp[wv][4];
-            const bool three = k != ihi - 1;
-            for (int j = k + ln; j < a.e; j += 64) {
-                double p = Hw(k, j) + q * Hw(k + 1, j);
-                if (three) { p += r * Hw(k + 2, j); Hw(k + 2, j) -= p * zs; }
-                Hw(k + 1, j) -= p * ys;
-                Hw(k, j) -= p * xs;
-            }
-        }
-        __syncthreads();
-        // ---- right updates: window rows i in [max(l, s), min(k+3, ihi)], then all rows of U
-        if (wv < a.nb && rp[wv][5] != 0.0) {
-            const int k = rk[wv];
-            const double xs = rp[wv][0], ys = rp[wv][1], zs = rp[wv][2], q = rp[wv][3], r = rp[wv][4];
-            const bool three = k != ihi - 1;
-            const int ilast = min(k + 3, ihi);
-            for (int i = max(l, a.s) + ln; i <= ilast; i += 64) {
-                double p = xs * Hw(i, k) + ys * Hw(i, k + 1);
-                if (three) { p += zs * Hw(i, k + 2); Hw(i, k + 2) -= p * r; }
-                Hw(i, k + 1) -= p * q;
-                Hw(i, k) -= p;
-            }
-            double* u0 = u + (k - a.s) * W;
-            for (int i = ln; i < W; i += 64) {
-                double p = xs * u0[i] + ys * u0[i + W];
-                if (three) { p += zs * u0[i + 2 * W]; u0[i + 2 * W] -= p * r; }
-                u0[i + W] -= p * q;
-                u0[i] -= p;
-            }
-        }
-        __syncthreads();
-    }
-    for (int idx = tid; idx < W * W; idx += nt) {
-        const int i = idx % W, j = idx / W;
-        a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] = h[i + j * ldh];
-        a.U[idx] = u[idx];
-    }
+// Reciprocal without the IEEE division sequence: v_rcp_f64 and two Newton steps (within an ulp
+// or two; a Householder reflector built from it is orthogonal to the same order).  x != 0, finite.
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    return __builtin_fma(r, e, r);
 }
 
 // The same chase with two barriers per step and no serial section.  Wave b owns bulge b for the
@@ -186,7 +85,12 @@ __global__ __launch_bounds__(1024) void chase_kernel(ChaseArgs a) {
 // left(b+1) before right(b) on their shared 3 x 3 block; the barrier after phase B orders
 // right(b) before the next step.  Each lane handles at most two columns / rows per phase, all
 // LDS reads issued before the dependent arithmetic.
-__global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs a) {
+// U is only ever right-multiplied, and bulge b touches U's columns k..k+2 for three consecutive
+// steps before bulge b+1 takes them over, so wave b keeps its three columns in registers: per
+// step it loads the new column k+2 (stored by bulge b-1 at the end of its previous phase A) and
+// stores the column it drops, instead of reading and writing all three.
+__global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
+    const ChaseWin a = ca.w[blockIdx.x];
     __shared__ double h[kWin * (kWin + 1)];
     __shared__ double u[kWin * kWin];
     const int W = a.e - a.s;
@@ -200,7 +104,7 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs a) {
         for (int q = 0; q < kPer; ++q) {
             const int idx = tid + q * 1024;
             const int i = idx % W, j = idx / W;
-            tmp[q] = idx < W * W ? a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] : 0.0;
+            tmp[q] = idx < W * W ? ca.H[(a.s + i) + (int64_t)(a.s + j) * ca.n] : 0.0;
         }
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
@@ -213,15 +117,39 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs a) {
         }
     }
     __syncthreads();
-    const int l = a.l, ihi = a.ihi;
+    const int l = ca.l, ihi = ca.ihi;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), ln = tid & 63;
     const int rlo = max(l, a.s);
+    const int i0 = ln, i1 = ln + 64;            // U rows of this lane
+    const bool d0 = i0 < W, d1 = i1 < W;
+    auto live = [&](int t) { const int k = l + t - 3 * wv; return wv < a.nb && k >= l && k <= ihi - 1 && t < a.t1; };
+    // U columns k, k+1, k+2 (window-relative), rows i0 and i1
+    double uc0[2] = {0, 0}, uc1[2] = {0, 0}, uc2[2] = {0, 0};
+    auto uload = [&](double* c, int col) {
+        if (d0) c[0] = u[i0 + col * W];
+        if (d1) c[1] = u[i1 + col * W];
+    };
+    auto ustore = [&](const double* c, int col) {
+        if (d0) u[i0 + col * W] = c[0];
+        if (d1) u[i1 + col * W] = c[1];
+    };
     for (int t = a.t0; t < a.t1; ++t) {
         const int k = l + t - 3 * wv;
-        bool act = wv < a.nb && k >= l && k <= ihi - 1;     // wave-uniform
+        const bool lv = live(t);                           // wave-uniform
         const bool three = k != ihi - 1;
+        bool act = false;
         double ax = 0.0, ay = 0.0, az = 0.0, bq = 0.0, br = 0.0;
-        if (act) {
+        if (lv) {
+            const int kk = k - a.s;
+            if (t == a.t0 || !live(t - 1)) {
+                uload(uc0, kk);
+                uload(uc1, kk + 1);
+                if (three) uload(uc2, kk + 2);
+            } else {
+                uc0[0] = uc1[0]; uc0[1] = uc1[1];
+                uc1[0] = uc2[0]; uc1[1] = uc2[1];
+                if (three) uload(uc2, kk + 2);
+            }
             double p, q, r, xk = 1.0;
             if (k == l) {
                 const double sx = a.shifts[2 * wv], sw = a.shifts[2 * wv + 1];
@@ -231,13 +159,13 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs a) {
                 q = Hw(l + 1, l + 1) - z - rr - rr;
                 r = (l + 2 <= ihi) ? Hw(l + 2, l + 1) : 0.0;
                 const double sc = fabs(p) + fabs(q) + fabs(r);
-                if (sc != 0.0) { const double is = 1.0 / sc; p *= is; q *= is; r *= is; }
+                if (sc != 0.0) { const double is = rcp_nr(sc); p *= is; q *= is; r *= is; }
             } else {
                 p = Hw(k, k - 1);
                 q = Hw(k + 1, k - 1);
                 r = three ? Hw(k + 2, k - 1) : 0.0;
                 xk = fabs(p) + fabs(q) + fabs(r);
-                if (xk != 0.0) { const double is = 1.0 / xk; p *= is; q *= is; r *= is; }
+                if (xk != 0.0) { const double is = rcp_nr(xk); p *= is; q *= is; r *= is; }
             }
             const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(p * p + q * q + r * r);
             act = sg != 0.0;
@@ -249,7 +177,7 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs a) {
                     if (three) Hw(k + 2, k - 1) = 0.0;
                 }
                 p += sg;
-                const double isg = 1.0 / sg, ip = 1.0 / p;
+                const double isg = rcp_nr(sg), ip = rcp_nr(p);
                 ax = p * isg; ay = q * isg; az = r * isg; bq = q * ip; br = r * ip;
                 // ---- phase A: left update, columns k + ln and k + ln + 64 of rows k..k+2
                 const int j0 = k + ln, j1 = j0 + 64;
@@ -257,107 +185,177 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs a) {
                 double h00 = 0, h01 = 0, h02 = 0, h10 = 0, h11 = 0, h12 = 0;
                 if (c0) { h00 = Hw(k, j0); h01 = Hw(k + 1, j0); if (three) h02 = Hw(k + 2, j0); }
                 if (c1) { h10 = Hw(k, j1); h11 = Hw(k + 1, j1); if (three) h12 = Hw(k + 2, j1); }
-                // U columns k..k+2 (window-relative), rows ln and ln + 64
-                double* u0 = u + (k - a.s) * W;
-                const int i0 = ln, i1 = ln + 64;
-                const bool d0 = i0 < W, d1 = i1 < W;
-                double u00 = 0, u01 = 0, u02 = 0, u10 = 0, u11 = 0, u12 = 0;
-                if (d0) { u00 = u0[i0]; u01 = u0[i0 + W]; if (three) u02 = u0[i0 + 2 * W]; }
-                if (d1) { u10 = u0[i1]; u11 = u0[i1 + W]; if (three) u12 = u0[i1 + 2 * W]; }
                 {
                     const double p0 = h00 + bq * h01 + (three ? br * h02 : 0.0);
                     const double p1 = h10 + bq * h11 + (three ? br * h12 : 0.0);
                     if (c0) { Hw(k, j0) = h00 - p0 * ax; Hw(k + 1, j0) = h01 - p0 * ay; if (three) Hw(k + 2, j0) = h02 - p0 * az; }
                     if (c1) { Hw(k, j1) = h10 - p1 * ax; Hw(k + 1, j1) = h11 - p1 * ay; if (three) Hw(k + 2, j1) = h12 - p1 * az; }
                 }
-                {
-                    const double p0 = ax * u00 + ay * u01 + (three ? az * u02 : 0.0);
-                    const double p1 = ax * u10 + ay * u11 + (three ? az * u12 : 0.0);
-                    if (d0) { u0[i0] = u00 - p0; u0[i0 + W] = u01 - p0 * bq; if (three) u0[i0 + 2 * W] = u02 - p0 * br; }
-                    if (d1) { u0[i1] = u10 - p1; u0[i1 + W] = u11 - p1 * bq; if (three) u0[i1 + 2 * W] = u12 - p1 * br; }
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {   // U columns k..k+2 in registers
+                    const double pu = ax * uc0[x] + ay * uc1[x] + (three ? az * uc2[x] : 0.0);
+                    uc0[x] -= pu;
+                    uc1[x] -= pu * bq;
+                    if (three) uc2[x] -= pu * br;
                 }
+            }
+            // drop column k (bulge b+1 loads it next step); at the bulge's last step here, all three
+            ustore(uc0, kk);
+            if (!live(t + 1)) {
+                ustore(uc1, kk + 1);
+                if (three) ustore(uc2, kk + 2);
             }
         }
         __syncthreads();
         // ---- phase B: right update, rows rlo + ln and rlo + ln + 64 of columns k..k+2
         if (act) {
             const int ilast = min(k + 3, ihi);
-            const int i0 = rlo + ln, i1 = i0 + 64;
-            const bool c0 = i0 <= ilast, c1 = i1 <= ilast;
+            const int r0 = rlo + ln, r1 = r0 + 64;
+            const bool c0 = r0 <= ilast, c1 = r1 <= ilast;
             double h00 = 0, h01 = 0, h02 = 0, h10 = 0, h11 = 0, h12 = 0;
-            if (c0) { h00 = Hw(i0, k); h01 = Hw(i0, k + 1); if (three) h02 = Hw(i0, k + 2); }
-            if (c1) { h10 = Hw(i1, k); h11 = Hw(i1, k + 1); if (three) h12 = Hw(i1, k + 2); }
+            if (c0) { h00 = Hw(r0, k); h01 = Hw(r0, k + 1); if (three) h02 = Hw(r0, k + 2); }
+            if (c1) { h10 = Hw(r1, k); h11 = Hw(r1, k + 1); if (three) h12 = Hw(r1, k + 2); }
             const double p0 = ax * h00 + ay * h01 + (three ? az * h02 : 0.0);
             const double p1 = ax * h10 + ay * h11 + (three ? az * h12 : 0.0);
-            if (c0) { Hw(i0, k) = h00 - p0; Hw(i0, k + 1) = h01 - p0 * bq; if (three) Hw(i0, k + 2) = h02 - p0 * br; }
-            if (c1) { Hw(i1, k) = h10 - p1; Hw(i1, k + 1) = h11 - p1 * bq; if (three) Hw(i1, k + 2) = h12 - p1 * br; }
+            if (c0) { Hw(r0, k) = h00 - p0; Hw(r0, k + 1) = h01 - p0 * bq; if (three) Hw(r0, k + 2) = h02 - p0 * br; }
+            if (c1) { Hw(r1, k) = h10 - p1; Hw(r1, k + 1) = h11 - p1 * bq; if (three) Hw(r1, k + 2) = h12 - p1 * br; }
         }
         __syncthreads();
     }
     for (int idx = tid; idx < W * W; idx += 1024) {
         const int i = idx % W, j = idx / W;
-        a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] = h[i + j * ldh];
+        ca.H[(a.s + i) + (int64_t)(a.s + j) * ca.n] = h[i + j * ldh];
         a.U[idx] = u[idx];
     }
 }
 
-// Both delayed updates of a window in ONE launch: blocks [0, nl) take 16-column panels of
-//     H(s:e, c0:c1) <- U^T H(s:e, c0:c1)
-// and blocks [nl, nl + nr) 16-row panels of
-//     H(r0:r1, s:e) <- H(r0:r1, s:e) U.
-// 256 threads = 16 columns (rows) x 16 groups of 6 outputs; U staged in LDS, the panel too.
-__global__ __launch_bounds__(256) void win_gemm_fused(double* H, int64_t n, int s, int W, int64_t c0, int64_t c1,
-                                                      int nl, int64_t r0, int64_t r1, const double* U) {
-    __shared__ double um[kWin * kWin];     // left: um[i * kWin + r] = U(i, r); right: um[i * kWin + j] = U(i, j)
-    __shared__ double x[kWin * 17];          // left: 16 x (kWin + 1) panel; right: kWin x 17
-    const bool left = (int)blockIdx.x < nl;
-    for (int idx = threadIdx.x; idx < kWin * kWin; idx += 256) {
-        const int i = idx / kWin, r = idx % kWin;
-        um[idx] = (i < W && r < W) ? U[i + r * W] : 0.0;
+// The delayed updates of up to kMaxGroups windows on the fp64 matrix cores
+// (v_mfma_f64_16x16x4_f64).  One launch applies one side for every window:
+//   left : H(s:s+W, lo:hi) <- U^T H(s:s+W, lo:hi)      64 columns per workgroup
+//   right: H(lo:hi, s:s+W) <- H(lo:hi, s:s+W) U        64 rows per workgroup
+// Left regions of different windows own disjoint rows and right regions disjoint columns, so a
+// launch is race-free; a left region of a window meets the right region of a window further down
+// the chain, hence lefts and rights are two launches (U_g^T X U_h = (U_g^T X) U_h).
+// U is staged in LDS (odd pitch, zero-padded to kWin), the left panel too; each wave computes a
+// kWin x 16 strip as six 16 x 16 tiles.  D layout of the f64 MFMA: lane L, register r holds
+// D[(L >> 4) + 4 r][L & 15] (cdna_hip_programming.md); D's column index is put on the output's
+// row, so 16 lanes store 128 contiguous bytes of one column.
+struct WinGemm {
+    int s, W;          // window rows/columns [s, s + W)
+    int64_t lo, hi;    // left: columns [lo, hi); right: rows [lo, hi)
+    int blk0;          // first workgroup of this window
+    const double* U;   // W x W, column-major
+};
+struct WinGemmBatch {
+    double* H;
+    int64_t n;
+    int nw;
+    WinGemm w[kMaxGroups + 1];
+};
+constexpr int kUP = kWin + 2;   // LDS pitch of U and of the left panel: (k + 2 i) mod 32 distinct for 32 lanes
+
+template <bool kLeft>
+__global__ __launch_bounds__(256) void win_gemm_mfma(WinGemmBatch b) {
+    __shared__ double us[kWin * kUP];                    // us[k + rho * kUP] = U(k, rho)
+    __shared__ double xs[kLeft ? 64 * kUP : 1];          // left: xs[k + c * kUP] = H(s + k, c0 + c)
+    int g = 0;
+#pragma unroll
+    for (int q = 1; q < kMaxGroups + 1; ++q)
+        if (q < b.nw && (int)blockIdx.x >= b.w[q].blk0) g = q;
+    const WinGemm w = b.w[g];
+    const int W = w.W;
+    const int64_t base = w.lo + (int64_t)((int)blockIdx.x - w.blk0) * 64;
+    const int cnt = (int)min<int64_t>(64, w.hi - base);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    // right: this lane's X(r_j, k) for k = lk, lk + 4, ... (issued first, consumed last)
+    constexpr int kKs = kWin / 4;
+    double xv[kLeft ? 1 : kKs];
+    const int rj = 16 * wave + li;
+    const bool rv = rj < cnt;
+    if constexpr (!kLeft) {
+        const double* xr = b.H + (base + min(rj, max(cnt - 1, 0))) + (int64_t)w.s * b.n;
+#pragma unroll
+        for (int q = 0; q < kKs; ++q) {
+            const int k = 4 * q + lk;
+            xv[q] = xr[(int64_t)min(k, W - 1) * b.n];
+        }
     }
-    const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
-    double acc[6];
+    {
+        // U (and the left panel) into LDS: every global load of the thread issued before any store
+        constexpr int kPU = kWin * kWin / 256;
+        double tu[kPU];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) acc[q] = 0.0;
-    if (left) {
-        const int64_t cb = c0 + (int64_t)blockIdx.x * 16;
-        const int nc = (int)min<int64_t>(16, c1 - cb);
-        for (int idx = threadIdx.x; idx < W * 16; idx += 256) {
-            const int i = idx % W, cc = idx / W;
-            x[cc * (kWin + 1) + i] = cc < nc ? H[(s + i) + (cb + cc) * n] : 0.0;   // column-major panel, odd stride
+        for (int q = 0; q < kPU; ++q) {
+            const int idx = threadIdx.x + 256 * q;
+            const int k = idx % kWin, rho = idx / kWin;
+            tu[q] = w.U[min(k, W - 1) + min(rho, W - 1) * W];
         }
-        __syncthreads();
-        for (int i = 0; i < W; ++i) {
-            const double xv = x[c * (kWin + 1) + i];
-            const double* ur = um + i * kWin + 6 * g;
+        if constexpr (kLeft) {
+            constexpr int kPX = kWin * 64 / 256;
+            double tx[kPX];
 #pragma unroll
-            for (int q = 0; q < 6; ++q) acc[q] += ur[q] * xv;
+            for (int q = 0; q < kPX; ++q) {
+                const int idx = threadIdx.x + 256 * q;
+                const int k = idx % kWin, c = idx / kWin;
+                tx[q] = b.H[(w.s + min(k, W - 1)) + (base + min(c, max(cnt - 1, 0))) * b.n];
+            }
+#pragma unroll
+            for (int q = 0; q < kPX; ++q) {
+                const int idx = threadIdx.x + 256 * q;
+                const int k = idx % kWin, c = idx / kWin;
+                xs[k + c * kUP] = (k < W && c < cnt) ? tx[q] : 0.0;
+            }
         }
-        if (c < nc)
 #pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                const int r = 6 * g + q;
-                if (r < W) H[(s + r) + (cb + c) * n] = acc[q];
+        for (int q = 0; q < kPU; ++q) {
+            const int idx = threadIdx.x + 256 * q;
+            const int k = idx % kWin, rho = idx / kWin;
+            us[k + rho * kUP] = (k < W && rho < W) ? tu[q] : 0.0;
+        }
+    }
+    __syncthreads();
+    dbl4 acc[6];
+#pragma unroll
+    for (int t = 0; t < 6; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+    if constexpr (kLeft) {
+        // D[i][j] = sum_k X(k, c_i) U(k, rho_j): i = column 16 wave + i, j = row 16 t + j
+        const double* xc = xs + (16 * wave + li) * kUP;
+#pragma unroll
+        for (int q = 0; q < kKs; ++q) {     // rows k >= W of both LDS images are zero
+            const int k = 4 * q + lk;
+            const double av = xc[k];
+            double bv[6];
+#pragma unroll
+            for (int t = 0; t < 6; ++t) bv[t] = us[k + (16 * t + li) * kUP];
+#pragma unroll
+            for (int t = 0; t < 6; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * wave + lk + 4 * r, rho = 16 * t + li;
+                if (c < cnt && rho < W) b.H[(w.s + rho) + (base + c) * b.n] = acc[t][r];
             }
     } else {
-        const int64_t rb = r0 + (int64_t)(blockIdx.x - nl) * 16;
-        const int nr = (int)min<int64_t>(16, r1 - rb);
-        for (int idx = threadIdx.x; idx < 16 * W; idx += 256) {
-            const int rr = idx & 15, i = idx >> 4;
-            x[i * 17 + rr] = rr < nr ? H[(rb + rr) + (int64_t)(s + i) * n] : 0.0;
-        }
-        __syncthreads();
-        for (int i = 0; i < W; ++i) {
-            const double xv = x[i * 17 + c];
-            const double* ur = um + i * kWin + 6 * g;
+        // D[i][j] = sum_k U(k, rho_i) X(r_j, k): i = output column rho, j = row 16 wave + j
 #pragma unroll
-            for (int q = 0; q < 6; ++q) acc[q] += xv * ur[q];
-        }
-        if (c < nr)
+        for (int q = 0; q < kKs; ++q) {
+            const int k = 4 * q + lk;
+            const double bv = (rv && k < W) ? xv[q] : 0.0;
+            double av[6];
 #pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                const int j = 6 * g + q;
-                if (j < W) H[(rb + c) + (int64_t)(s + j) * n] = acc[q];
+            for (int t = 0; t < 6; ++t) av[t] = us[k + (16 * t + li) * kUP];
+#pragma unroll
+            for (int t = 0; t < 6; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv, acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rho = 16 * t + lk + 4 * r;
+                if (rv && rho < W) b.H[(base + rj) + (int64_t)(w.s + rho) * b.n] = acc[t][r];
             }
     }
 }
@@ -473,7 +471,7 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
                 q = T(k + 1, k - 1);
                 r = three ? T(k + 2, k - 1) : 0.0;
                 xk = fabs(p) + fabs(q) + fabs(r);
-                if (xk != 0.0) { const double is = 1.0 / xk; p *= is; q *= is; r *= is; }
+                if (xk != 0.0) { const double is = rcp_nr(xk); p *= is; q *= is; r *= is; }
             }
             const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(p * p + q * q + r * r);
             if (sg == 0.0) continue;
@@ -488,7 +486,7 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
                 }
             }
             p += sg;
-            const double isg = 1.0 / sg, ip = 1.0 / p;
+            const double isg = rcp_nr(sg), ip = rcp_nr(p);
             const double ax = p * isg, ay = q * isg, az = r * isg, bq = q * ip, br = r * ip;
             for (int j = k + lane; j < jend; j += 64) {
                 double pp = T(k, j) + bq * T(k + 1, j);
@@ -498,19 +496,19 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
             }
             EIGSOL_LDS_ORDER();
             const int imax = nn < k + 3 ? nn : k + 3;
-            for (int i = ibeg + lane; i <= imax; i += 64) {
-                double pp = ax * T(i, k) + ay * T(i, k + 1);
-                if (three) { pp += az * T(i, k + 2); T(i, k + 2) -= pp * br; }
-                T(i, k + 1) -= pp * bq;
-                T(i, k) -= pp;
+            // right update of T and (Schur) of V in one pass: both columns' loads issued together
+            const int iend = kSchur ? max(imax + 1, n) : imax + 1;
+            for (int i = lane; i + ibeg < iend || i < (kSchur ? n : 0); i += 64) {
+                const int it = ibeg + i;
+                const bool ct = it <= imax, cv = kSchur && i < n;
+                double t0 = 0, t1 = 0, t2 = 0, v0 = 0, v1 = 0, v2 = 0;
+                if (ct) { t0 = T(it, k); t1 = T(it, k + 1); if (three) t2 = T(it, k + 2); }
+                if (cv) { v0 = V(i, k); v1 = V(i, k + 1); if (three) v2 = V(i, k + 2); }
+                const double pt = ax * t0 + ay * t1 + (three ? az * t2 : 0.0);
+                const double pv = ax * v0 + ay * v1 + (three ? az * v2 : 0.0);
+                if (ct) { T(it, k) = t0 - pt; T(it, k + 1) = t1 - pt * bq; if (three) T(it, k + 2) = t2 - pt * br; }
+                if (cv) { V(i, k) = v0 - pv; V(i, k + 1) = v1 - pv * bq; if (three) V(i, k + 2) = v2 - pv * br; }
             }
-            if (kSchur)
-                for (int i = lane; i < n; i += 64) {
-                    double pp = ax * V(i, k) + ay * V(i, k + 1);
-                    if (three) { pp += az * V(i, k + 2); V(i, k + 2) -= pp * br; }
-                    V(i, k + 1) -= pp * bq;
-                    V(i, k) -= pp;
-                }
             EIGSOL_LDS_ORDER();
         }
     }
@@ -714,9 +712,9 @@ static int hqr_small(hipStream_t st, const double* H, int64_t ld, int n, int max
 }
 
 static constexpr int kSmallDefault = 128;
-// AED window: 40 measured best at 4096 (32: 2.63 s, 40: 2.58 s, 48: 2.60 s, 64: 2.92 s, 96: 4.28 s, off: 2.89 s);
-// the window's one-wave Schur factorisation costs O(nw^3) latency-bound steps
-static constexpr int kAedDefault = 40;   // blocks finished by the in-LDS solver (EIGSOL_QR_SMALL)
+// AED window at 4096 with 4-bulge groups (up to 24 bulges per sweep): 40 -> 1.90 s, 48 -> 1.82 s, 56 -> 1.87 s
+// (one chain of 16 bulges: 40 was best); the window's one-wave Schur factorisation costs O(nw^3) latency-bound steps
+static constexpr int kAedDefault = 48;   // EIGSOL_QR_AED overrides (0: off)
 
 int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double* wr, double* wi,
                       int32_t* sweeps_out, int32_t* fail_out) {
@@ -727,7 +725,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     EIGSOL_HIP(hipMalloc(&dwr, n * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&dwi, n * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&dds, 2 * n * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&dU, dev::kWin * dev::kWin * sizeof(double)));
+    EIGSOL_HIP(hipMalloc(&dU, dev::kMaxGroups * dev::kWin * dev::kWin * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&dsh, 4 * dev::kMaxBulges * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&dinfo, 64));
     std::vector<double> ds(2 * n), swr(2 * dev::kMaxBulges), swi(2 * dev::kMaxBulges);
@@ -742,7 +740,10 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         return e ? std::max(16, std::min(128, std::atoi(e))) : kSmallDefault;
     }();
     static const bool stats = std::getenv("EIGSOL_QR_STATS") != nullptr;
-    static const bool chase_v1 = std::getenv("EIGSOL_CHASE_V1") != nullptr;   // A/B: three-barrier chase
+    static const int max_groups = [] {                 // bulge groups chased concurrently (EIGSOL_QR_GROUPS)
+        const char* e = std::getenv("EIGSOL_QR_GROUPS");
+        return e ? std::max(1, std::min(dev::kMaxGroups, std::atoi(e))) : dev::kMaxGroups;
+    }();
     static const int max_bulges = [] {                 // experiments: cap the bulges per chain
         const char* e = std::getenv("EIGSOL_QR_NB");
         return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : dev::kMaxBulges;
@@ -812,10 +813,11 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                 const int nd = info[1], m = info[3];
                 if (nd > 0) {
                     st_aed_defl += nd;
-                    const int nr = kw > l ? (kw - l + 15) / 16 : 0;
-                    if (nr > 0)
-                        hipLaunchKernelGGL(dev::win_gemm_fused, dim3(nr), dim3(256), 0, st, H, n, kw, nw, (int64_t)0,
-                                           (int64_t)0, 0, (int64_t)l, (int64_t)kw, dU);
+                    if (kw > l) {   // rows above the window: H[l, kw) x [kw, kw + nw) V
+                        dev::WinGemmBatch gb{H, n, 1, {}};
+                        gb.w[0] = dev::WinGemm{kw, nw, (int64_t)l, (int64_t)kw, 0, dU};
+                        hipLaunchKernelGGL(dev::win_gemm_mfma<false>, dim3((kw - l + 63) / 64), dim3(256), 0, st, gb);
+                    }
                     ihi = kw + m - 1;
                     sweeps = std::max(sweeps, stall);
                     stall = 0;
@@ -883,35 +885,65 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             break;
         }
         ++st_sweeps;
-        // chase the chain window by window
-        const int T = (ihi - 1 - l) + 3 * (nb - 1) + 1;
+        // chase: C groups of nbg bulges, group g starting G steps after group g-1, each group in its
+        // own LDS window; a round advances every group's window by the same number of steps
+        // groups of >= 4 bulges; the spacing costs (C - 1) G extra steps, kept below N / 4
+        const int C = std::max(1, std::min({max_groups, nb / 4, 1 + N / (4 * (dev::kWin + 12))}));
+        const int nbg = nb / C;
+        const int G = dev::kWin + 3 * nbg;   // group spacing: windows stay disjoint
+        const int Tg = (ihi - 1 - l) + 3 * (nbg - 1) + 1;     // steps of one group
+        const int T = (C - 1) * G + Tg;
         int t0 = 0;
-        while (t0 < T) {
-            int s;
-            if (t0 <= 3 * (nb - 1)) s = std::max(0, l - 1);
-            else s = std::max(0, l + t0 - 3 * (nb - 1) - 1);
-            const int e = std::min(s + dev::kWin, ihi + 1);
-            const int kmax = (e == ihi + 1) ? ihi - 1 : e - 4;
-            int t1 = t0;
-            while (t1 < T) {
-                int blead = std::max(0, (l + t1 - (ihi - 1) + 2) / 3);   // first bulge not yet past ihi-1
-                if (blead >= nb) { t1 = T; break; }
-                const int k = l + t1 - 3 * blead;
-                if (k > kmax) break;
-                ++t1;
+        while (t0 < T && rc == EIGSOL_OK) {
+            dev::ChaseArgs ca{H, n, l, ihi, {}};
+            int t1 = T, nwin = 0;
+            int g_act[dev::kMaxGroups];
+            for (int g = 0; g < C; ++g) {
+                const int tl = t0 - g * G;
+                if (tl < 0) { t1 = std::min(t1, g * G); break; }    // later groups start at a round boundary
+                if (tl >= Tg) continue;                              // group done
+                int s;
+                if (tl <= 3 * (nbg - 1)) s = std::max(0, l - 1);
+                else s = std::max(0, l + tl - 3 * (nbg - 1) - 1);
+                const int e = std::min(s + dev::kWin, ihi + 1);
+                const int kmax = (e == ihi + 1) ? ihi - 1 : e - 4;
+                int tl1 = tl;
+                while (tl1 < Tg) {
+                    const int blead = std::max(0, (l + tl1 - (ihi - 1) + 2) / 3);   // first bulge not past ihi-1
+                    if (blead >= nbg) { tl1 = Tg; break; }
+                    if (l + tl1 - 3 * blead > kmax) break;
+                    ++tl1;
+                }
+                t1 = std::min(t1, tl1 + g * G);
+                ca.w[nwin] = dev::ChaseWin{s, e, tl, 0, nbg, dsh + 2 * g * nbg, dU + (size_t)nwin * dev::kWin * dev::kWin};
+                g_act[nwin++] = g;
             }
-            if (t1 == t0) { rc = fail(EIGSOL_E_SOLVER, "francis: window did not advance (internal error)"); break; }
-            ++st_windows;
+            if (t1 <= t0 || nwin == 0) { rc = fail(EIGSOL_E_SOLVER, "francis: window did not advance (internal error)"); break; }
+            for (int q = 0; q < nwin; ++q) {
+                ca.w[q].t1 = t1 - g_act[q] * G;
+                if (q > 0 && ca.w[q].e > ca.w[q - 1].s) { rc = fail(EIGSOL_E_SOLVER, "francis: windows overlap (internal error)"); break; }
+            }
+            if (rc != EIGSOL_OK) break;
+            st_windows += nwin;
             st_steps += t1 - t0;
-            dev::ChaseArgs ca{H, n, s, e, l, ihi, t0, t1, nb, dsh, dU};
-            if (chase_v1) hipLaunchKernelGGL(dev::chase_kernel, dim3(1), dim3(1024), 0, st, ca);
-            else hipLaunchKernelGGL(dev::chase_wave_kernel, dim3(1), dim3(1024), 0, st, ca);
-            const int W = e - s;
-            const int nlb = e <= ihi ? (ihi + 1 - e + 15) / 16 : 0;
-            const int nrb = s > l ? (s - l + 15) / 16 : 0;
-            if (nlb + nrb > 0)
-                hipLaunchKernelGGL(dev::win_gemm_fused, dim3(nlb + nrb), dim3(256), 0, st, H, n, s, W, (int64_t)e,
-                                   (int64_t)ihi + 1, nlb, (int64_t)l, (int64_t)s, dU);
+            hipLaunchKernelGGL(dev::chase_wave_kernel, dim3(nwin), dim3(1024), 0, st, ca);
+            // delayed updates: every left region, then every right region
+            dev::WinGemmBatch lb{H, n, 0, {}}, rb{H, n, 0, {}};
+            int nlb = 0, nrb = 0;
+            for (int q = 0; q < nwin; ++q) {
+                const dev::ChaseWin& w = ca.w[q];
+                const int W = w.e - w.s;
+                if (w.e <= ihi) {
+                    lb.w[lb.nw++] = dev::WinGemm{w.s, W, (int64_t)w.e, (int64_t)ihi + 1, nlb, w.U};
+                    nlb += (ihi + 1 - w.e + 63) / 64;
+                }
+                if (w.s > l) {
+                    rb.w[rb.nw++] = dev::WinGemm{w.s, W, (int64_t)l, (int64_t)w.s, nrb, w.U};
+                    nrb += (w.s - l + 63) / 64;
+                }
+            }
+            if (nlb > 0) hipLaunchKernelGGL(dev::win_gemm_mfma<true>, dim3(nlb), dim3(256), 0, st, lb);
+            if (nrb > 0) hipLaunchKernelGGL(dev::win_gemm_mfma<false>, dim3(nrb), dim3(256), 0, st, rb);
             t0 = t1;
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "francis: launch"); break; }
