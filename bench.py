@@ -210,8 +210,12 @@ def run_config2(E, ctx, no_cpu):
         d = json.load(open(prof))
         out["mfma"] = {"gemm_TFLOPs": round(d["gemm_TFLOPs"], 2), "peak_TFLOPs": d["mfma_peak_TFLOPs"],
                        "utilisation": round(d["mfma_utilisation"], 4), "gemm_flops": d["gemm_flops"],
+                       "rank_update_TFLOPs": round(d.get("rank_update_TFLOPs") or 0.0, 2),
+                       "rank_update_utilisation": round(d.get("rank_update_mfma_utilisation") or 0.0, 4),
+                       "francis_window_gemm_share": round(d.get("francis_window_gemm_share") or 0.0, 4),
                        "source": "profiles/r01_qr4096_mfma.json (rocprofv3 kernel times of the Hessenberg "
-                                 "trailing-update GEMMs, v_mfma_f64_16x16x4_f64)"}
+                                 "trailing-update GEMMs on v_mfma_f64_16x16x4_f64: the whole set incl. the "
+                                 "split-K W = V^T A, and the single rank-2nb update alone)"}
     if not no_cpu:
         from oracle import oracle as O
         m = 1024
