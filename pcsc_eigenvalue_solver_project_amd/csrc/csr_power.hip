@@ -797,13 +797,30 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
     }
 }
 
-#ifndef EIGSOL_SLICE_NS
-#define EIGSOL_SLICE_NS 2
+// Rounds of slice loads a wave keeps in flight (software pipeline depth) and slices per round,
+// from the size of one slice's registers: band10m (f64, 12 entries per row, 36 VGPRs per slice)
+// measured 205.6 us unpipelined with two slices per round, 194.5 us at depth 1 and 191 us at
+// depth 2 with one slice per round (depth 3+: register pressure, 214 us).  EIGSOL_SLICE_PIPE /
+// EIGSOL_SLICE_NS (compile time) override for A/B builds.
+template <class S, int KB, bool kG>
+struct SlicePlan {
+    static constexpr int bytes = (int)sizeof(SliceRegs<S, KB, kG>);
+#ifdef EIGSOL_SLICE_PIPE
+    static constexpr int pipe = EIGSOL_SLICE_PIPE;
+#else
+    static constexpr int pipe = bytes <= 160 ? 2 : (bytes <= 320 ? 1 : 0);
 #endif
-constexpr int kSliceNS = EIGSOL_SLICE_NS;   // slices a wave has in flight at once
+#ifdef EIGSOL_SLICE_NS
+    static constexpr int ns = EIGSOL_SLICE_NS;
+#else
+    static constexpr int ns = pipe > 0 ? 1 : 2;
+#endif
+};
 
 template <class S, bool kPower, int KB, bool kG>
 __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int parity) {
+    constexpr int kSliceNS = SlicePlan<S, KB, kG>::ns;   // slices per round
+    constexpr int kPipe = SlicePlan<S, KB, kG>::pipe;    // rounds in flight while one computes
     __shared__ __align__(16) S xw_all[kWaves][kSliceNS][kSliceWin];
     __shared__ double sm[3 * kWaves];
     __shared__ Prologue pro;
@@ -831,18 +848,62 @@ __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int p
     const int chunk = (a.nslices + 7) >> 3;
     const int sbeg = (blockIdx.x & 7) * chunk;
     const int send = min(a.nslices, sbeg + chunk);
-    for (int sl = sbeg + (blockIdx.x >> 3) * kWaves + wave; sl < send; sl += kSliceNS * wpg) {
-        SliceRegs<S, KB, kG> R[kSliceNS];
-        int4 mc[kSliceNS];
+    const int step = kSliceNS * wpg;
+    auto issue = [&](SliceRegs<S, KB, kG>(&R)[kSliceNS], int4(&mc)[kSliceNS], int s0) {
 #pragma unroll
-        for (int i = 0; i < kSliceNS; ++i) mc[i] = ld_uniform(a.slice_meta, min(sl + i * wpg, send - 1));
+        for (int i = 0; i < kSliceNS; ++i) mc[i] = ld_uniform(a.slice_meta, min(s0 + i * wpg, send - 1));
 #pragma unroll
         for (int i = 0; i < kSliceNS; ++i)   // past the range: reloads the last slice, unused
-            slice_issue<S, KB, kG>(a, xin, min(sl + i * wpg, send - 1), mc[i], R[i]);
+            slice_issue<S, KB, kG>(a, xin, min(s0 + i * wpg, send - 1), mc[i], R[i]);
+    };
+    auto compute = [&](const SliceRegs<S, KB, kG>(&R)[kSliceNS], const int4(&mc)[kSliceNS], int s0) {
 #pragma unroll
         for (int i = 0; i < kSliceNS; ++i)
-            if (i == 0 || sl + i * wpg < send)
-                slice_compute<S, kPower, KB, kG>(a, xin, yout, nrm, R[i], mc[i], sl + i * wpg, xw_all[wave][i], n2, rr, ri);
+            if (i == 0 || s0 + i * wpg < send)
+                slice_compute<S, kPower, KB, kG>(a, xin, yout, nrm, R[i], mc[i], s0 + i * wpg, xw_all[wave][i], n2, rr, ri);
+    };
+    int sl = sbeg + (blockIdx.x >> 3) * kWaves + wave;
+    if constexpr (kPipe == 1) {
+        // software pipeline, unrolled by two so both register sets have static names: the next
+        // round's loads are in flight while this round computes
+        SliceRegs<S, KB, kG> RA[kSliceNS], RB[kSliceNS];
+        int4 ma[kSliceNS], mb[kSliceNS];
+        if (sl < send) issue(RA, ma, sl);
+        while (sl < send) {
+            if (sl + step < send) issue(RB, mb, sl + step);
+            compute(RA, ma, sl);
+            sl += step;
+            if (sl >= send) break;
+            if (sl + step < send) issue(RA, ma, sl + step);
+            compute(RB, mb, sl);
+            sl += step;
+        }
+    } else if constexpr (kPipe >= 2) {
+        // two rounds in flight while one computes (unrolled by three)
+        SliceRegs<S, KB, kG> RA[kSliceNS], RB[kSliceNS], RC[kSliceNS];
+        int4 ma[kSliceNS], mb[kSliceNS], mcc[kSliceNS];
+        if (sl < send) issue(RA, ma, sl);
+        if (sl + step < send) issue(RB, mb, sl + step);
+        while (sl < send) {
+            if (sl + 2 * step < send) issue(RC, mcc, sl + 2 * step);
+            compute(RA, ma, sl);
+            sl += step;
+            if (sl >= send) break;
+            if (sl + 2 * step < send) issue(RA, ma, sl + 2 * step);
+            compute(RB, mb, sl);
+            sl += step;
+            if (sl >= send) break;
+            if (sl + 2 * step < send) issue(RB, mb, sl + 2 * step);
+            compute(RC, mcc, sl);
+            sl += step;
+        }
+    } else {
+        for (; sl < send; sl += step) {
+            SliceRegs<S, KB, kG> R[kSliceNS];
+            int4 mc[kSliceNS];
+            issue(R, mc, sl);
+            compute(R, mc, sl);
+        }
     }
     if constexpr (kPower) {
         block_sum3(n2, rr, ri, sm);
