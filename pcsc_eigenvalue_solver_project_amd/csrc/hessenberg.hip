@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "kernels_common.hpp"
+#include "mfma_rankk.hpp"
 
 namespace eigsol {
 namespace dev {
@@ -573,69 +574,6 @@ __global__ __launch_bounds__(256) void gemm_mfma_f64(int m, int nn, int kk, doub
             }
 }
 
-// Rank-K update C(m x nn) += alpha L(m x K) R(nn x K)^T, all column-major, K <= kRankMax and a
-// multiple of 4 (smaller K zero-filled), on v_mfma_f64_16x16x4_f64 with every operand fragment
-// loaded straight from global memory into registers (no LDS, no barrier): each wave owns a
-// 32 x 32 tile of C, loads its 32 x K slices of L and R (16 lanes read 128 contiguous bytes of
-// one column) and its C tile, all before the first MFMA.  D layout: lane L, register r holds
-// D[(L >> 4) + 4 r][L & 15]; D's column index is put on C's row for coalesced C traffic.
-constexpr int kRankMax = 64;
-__global__ __launch_bounds__(256) void rankk_mfma_f64(int m, int nn, int K, double alpha, const double* L,
-                                                      int64_t ldl, const double* R, int64_t ldr, double* C,
-                                                      int64_t ldc) {
-    constexpr int KQ = kRankMax / 4;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int li = lane & 15, lk = lane >> 4;
-    const int r0 = blockIdx.x * 64 + 32 * (wave & 1);
-    const int c0 = blockIdx.y * 64 + 32 * (wave >> 1);
-    double ra[2][KQ], lb[2][KQ];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int col = min(c0 + 16 * t + li, nn - 1), row = min(r0 + 16 * t + li, m - 1);
-#pragma unroll
-        for (int q = 0; q < KQ; ++q) {
-            const int k = min(4 * q + lk, K - 1);
-            ra[t][q] = R[col + (int64_t)k * ldr];
-            lb[t][q] = L[row + (int64_t)k * ldl];
-        }
-    }
-    double c[2][2][4];
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-        for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = min(r0 + 16 * ti + li, m - 1), col = min(c0 + 16 * tj + lk + 4 * r, nn - 1);
-                c[ti][tj][r] = C[row + (int64_t)col * ldc];
-            }
-    dbl4 acc[2][2];
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-        for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-        if (4 * q >= K) break;
-        const bool kv = 4 * q + lk < K;
-#pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-            for (int tj = 0; tj < 2; ++tj)
-                acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(kv ? ra[tj][q] : 0.0, kv ? lb[ti][q] : 0.0,
-                                                                  acc[ti][tj], 0, 0, 0);
-    }
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-        for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = r0 + 16 * ti + li, col = c0 + 16 * tj + lk + 4 * r;
-                if (row < m && col < nn) C[row + (int64_t)col * ldc] = c[ti][tj][r] + alpha * acc[ti][tj][r];
-            }
-}
-
 // C = beta C + sum_z P[z] (m x nn, P packed with leading dimension m), partials added in z order
 __global__ void gemm_reduce(int m, int nn, int nz, const double* P, double beta, double* C, int64_t ldc) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -768,8 +706,7 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
             EIGSOL_HIP(hipMemsetAsync(Vz, 0, (size_t)nbp * n * sizeof(double), st));
             EIGSOL_HIP(hipMemcpy2DAsync(Vz + (k + 1), n * sizeof(double), V + (k + 1), n * sizeof(double),
                                         rows * sizeof(double), nbp, hipMemcpyDeviceToDevice, st));
-            hipLaunchKernelGGL(dev::rankk_mfma_f64, dim3((n + 63) / 64, (mt + 63) / 64), dim3(256), 0, st, n, mt,
-                               2 * nbp, -1.0, L, (int64_t)n, R, (int64_t)n, A + (int64_t)c1 * n, (int64_t)n);
+            rankk_update<double, false>(st, n, mt, 2 * nbp, -1.0, L, n, R, n, A + (int64_t)c1 * n, n);
         }
     }
     EIGSOL_HIP(hipGetLastError());

@@ -1,0 +1,117 @@
+// Rank-K update on the fp64 matrix cores (gfx950, v_mfma_f64_16x16x4_f64), shared by the blocked
+// Hessenberg reduction (hessenberg.hip) and the blocked LU of the shifted solve (shifted.hip).
+//
+//   C(m x nn) += alpha * L(m x K) * R^T          R stored nn x K      (kRT = false)
+//   C(m x nn) += alpha * L(m x K) * Rt           Rt stored K x nn     (kRT = true)
+//
+// all column-major; S = double or cplx (interleaved re, im; alpha real).  K <= KMAX, any K
+// (the k-steps past K are masked).  Every operand fragment is loaded straight from global memory
+// into registers — no LDS, no barrier: each wave owns a 32 x 32 tile of C, loads its 32 x K
+// slices of L and R and its C tile, all before the first MFMA.
+//
+// Fragment layout of the f64 MFMA (cdna_hip_programming.md): A operand lane l holds A[l & 15][l >> 4],
+// B operand lane l holds B[l >> 4][l & 15], D lane l register r holds D[(l >> 4) + 4 r][l & 15].
+// The A operand carries R (its row index i = a column of C) and the B operand carries L (its
+// column index j = a row of C), so D's column index lies on C's row: 16 lanes load and store 128
+// contiguous bytes of one column of C.  A complex product takes four real MFMAs:
+//   re += Rre Lre - Rim Lim,   im += Rre Lim + Rim Lre.
+#pragma once
+
+#include "kernels_common.hpp"
+
+namespace eigsol {
+namespace dev {
+
+typedef double mfma_d4 __attribute__((ext_vector_type(4)));
+
+template <class S> struct RankKMax;
+template <> struct RankKMax<double> { static constexpr int value = 64; };
+template <> struct RankKMax<cplx> { static constexpr int value = 32; };
+
+__device__ __forceinline__ double re_of(double v) { return v; }
+__device__ __forceinline__ double im_of(double) { return 0.0; }
+__device__ __forceinline__ double re_of(cplx v) { return v.re; }
+__device__ __forceinline__ double im_of(cplx v) { return v.im; }
+
+template <class S, bool kRT>
+__global__ __launch_bounds__(256) void rankk_mfma(int m, int nn, int K, double alpha, const S* L, int64_t ldl,
+                                                  const S* R, int64_t ldr, S* C, int64_t ldc) {
+    constexpr bool kC = std::is_same_v<S, cplx>;
+    constexpr int KQ = RankKMax<S>::value / 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int r0 = blockIdx.x * 64 + 32 * (wave & 1);
+    const int c0 = blockIdx.y * 64 + 32 * (wave >> 1);
+    S ra[2][KQ], lb[2][KQ];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int col = min(c0 + 16 * t + li, nn - 1), row = min(r0 + 16 * t + li, m - 1);
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+            const int k = min(4 * q + lk, K - 1);
+            ra[t][q] = kRT ? R[k + (int64_t)col * ldr] : R[col + (int64_t)k * ldr];
+            lb[t][q] = L[row + (int64_t)k * ldl];
+        }
+    }
+    S c[2][2][4];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = min(r0 + 16 * ti + li, m - 1), col = min(c0 + 16 * tj + lk + 4 * r, nn - 1);
+                c[ti][tj][r] = C[row + (int64_t)col * ldc];
+            }
+    mfma_d4 are[2][2], aim[2][2];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) are[ti][tj] = aim[ti][tj] = mfma_d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+        if (4 * q >= K) break;
+        const bool kv = 4 * q + lk < K;
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const double rr = kv ? re_of(ra[tj][q]) : 0.0, lr = kv ? re_of(lb[ti][q]) : 0.0;
+                are[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(rr, lr, are[ti][tj], 0, 0, 0);
+                if constexpr (kC) {
+                    const double ri = kv ? im_of(ra[tj][q]) : 0.0, li_ = kv ? im_of(lb[ti][q]) : 0.0;
+                    are[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ri, li_, are[ti][tj], 0, 0, 0);
+                    aim[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(rr, li_, aim[ti][tj], 0, 0, 0);
+                    aim[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(ri, lr, aim[ti][tj], 0, 0, 0);
+                }
+            }
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = r0 + 16 * ti + li, col = c0 + 16 * tj + lk + 4 * r;
+                if (row < m && col < nn) {
+                    if constexpr (kC)
+                        C[row + (int64_t)col * ldc] = cplx{c[ti][tj][r].re + alpha * are[ti][tj][r],
+                                                           c[ti][tj][r].im + alpha * aim[ti][tj][r]};
+                    else
+                        C[row + (int64_t)col * ldc] = c[ti][tj][r] + alpha * are[ti][tj][r];
+                }
+            }
+}
+
+}  // namespace dev
+
+// C += alpha L R^T (or L Rt), stream-ordered; K <= RankKMax<S>::value.
+template <class S, bool kRT>
+inline void rankk_update(hipStream_t st, int m, int nn, int K, double alpha, const S* L, int64_t ldl, const S* R,
+                         int64_t ldr, S* C, int64_t ldc) {
+    if (m <= 0 || nn <= 0 || K <= 0) return;
+    hipLaunchKernelGGL((dev::rankk_mfma<S, kRT>), dim3((m + 63) / 64, (nn + 63) / 64), dim3(256), 0, st, m, nn, K,
+                       alpha, L, ldl, R, ldr, C, ldc);
+}
+
+}  // namespace eigsol

@@ -14,7 +14,8 @@
 //     level, and a sync-free triangular solve: each 16-lane group solves one row, polling the
 //     solved values of the rows it reads (an unsolved value is a sentinel NaN).
 //   * dense (Matrix::Dense, and small non-triangular sparse matrices densified on the device):
-//     right-looking partial-pivot LU (the unblocked order of Eigen's PartialPivLU), then a
+//     right-looking blocked partial-pivot LU (panels of 64 real / 32 complex columns, trailing
+//     update on the fp64 matrix cores; Eigen's PartialPivLU is blocked too), then a
 //     single-workgroup forward/back substitution per iteration with the vector in LDS.
 // Non-triangular sparse matrices too large to densify are reported as EIGSOL_E_UNSUPPORTED.
 #include <algorithm>
@@ -25,6 +26,7 @@
 #include <vector>
 
 #include "kernels_common.hpp"
+#include "mfma_rankk.hpp"
 
 namespace eigsol {
 
@@ -289,8 +291,8 @@ __device__ __forceinline__ double score(cplx v) { return hypot(v.re, v.im); }
 // transposition, scale the subdiagonal column by the pivot (skipped for a zero pivot, as Eigen's
 // partial_lu_impl does; the first zero pivot is recorded).
 template <class S>
-__global__ __launch_bounds__(1024) void lu_pivot_kernel(S* a, int64_t n, int64_t k, int32_t* piv,
-                                                        int32_t* zero_pivot) {
+__global__ __launch_bounds__(1024) void lu_pivot_kernel(S* a, int64_t n, int64_t k, int64_t c0, int64_t c1,
+                                                        int32_t* piv, int32_t* zero_pivot) {
     __shared__ double sv[1024];
     __shared__ int si[1024];
     __shared__ int s_p;
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(1024) void lu_pivot_kernel(S* a, int64_t n, int64_t
     __syncthreads();
     const int64_t p = s_p;
     if (p != k)
-        for (int64_t j = tid; j < n; j += 1024) {
+        for (int64_t j = c0 + tid; j < c1; j += 1024) {
             const S t = a[j * n + k];
             a[j * n + k] = a[j * n + p];
             a[j * n + p] = t;
@@ -331,15 +333,60 @@ __global__ __launch_bounds__(1024) void lu_pivot_kernel(S* a, int64_t n, int64_t
         for (int64_t i = k + 1 + tid; i < n; i += 1024) a[k * n + i] = sdiv(a[k * n + i], d);
 }
 
-// trailing update a_ij -= l_ik u_kj, i, j > k (one thread per element, column-major coalesced)
+// panel update a_ij -= l_ik u_kj, i > k, k < j < c1 (one thread per element, column-major coalesced)
 template <class S>
-__global__ __launch_bounds__(256) void lu_update_kernel(S* a, int64_t n, int64_t k) {
-    const int64_t m = n - k - 1;
+__global__ __launch_bounds__(256) void lu_update_kernel(S* a, int64_t n, int64_t k, int64_t c1) {
+    const int64_t m = n - k - 1, w = c1 - k - 1;
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= m * m) return;
+    if (idx >= m * w) return;
     const int64_t i = k + 1 + idx % m;
     const int64_t j = k + 1 + idx / m;
     a[j * n + i] = sub(a[j * n + i], mul(a[k * n + i], a[j * n + k]));
+}
+
+// the panel's row interchanges (rows j <-> piv[j], j = k0 .. k0 + kb - 1, in order) applied to every
+// column outside the panel; one thread per column
+template <class S>
+__global__ __launch_bounds__(256) void lu_laswp_kernel(S* a, int64_t n, int64_t k0, int kb, const int32_t* piv) {
+    int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= n - kb) return;
+    if (c >= k0) c += kb;
+    S* col = a + c * n;
+    for (int j = 0; j < kb; ++j) {
+        const int64_t r = k0 + j, p = piv[r];
+        if (p != r) {
+            const S t = col[r];
+            col[r] = col[p];
+            col[p] = t;
+        }
+    }
+}
+
+// U12 = L11^{-1} A12: L11 the panel's unit lower kb x kb block (LDS), one thread per column of A12
+template <class S, int NB>
+__global__ __launch_bounds__(256) void lu_trsm_kernel(S* a, int64_t n, int64_t k0, int kb) {
+    __shared__ S l11[NB * NB];
+    for (int e = threadIdx.x; e < kb * kb; e += 256) {
+        const int i = e % kb, j = e / kb;
+        l11[i + j * NB] = a[(k0 + i) + (k0 + j) * n];
+    }
+    __syncthreads();
+    const int64_t c = k0 + kb + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= n) return;
+    S* col = a + c * n + k0;
+    S x[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) x[i] = i < kb ? col[i] : s_zero<S>();
+#pragma unroll
+    for (int j = 0; j < NB - 1; ++j) {
+        if (j < kb) {   // kb < NB only for the last panel
+#pragma unroll
+            for (int i = j + 1; i < NB; ++i) x[i] = sub(x[i], mul(l11[i + j * NB], x[j]));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+        if (i < kb) col[i] = x[i];
 }
 
 template <class S>
@@ -484,11 +531,28 @@ static int dense_lu_factor(ShiftFactor* f, bool from_sparse) {
     EIGSOL_HIP(hipMemsetAsync(f->zero_pivot, 0xff, sizeof(int32_t), st));
     hipLaunchKernelGGL((dev::shift_diag_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, a, n,
                        make_sigma<S>(f->sig_re, f->sig_im));
-    for (int64_t k = 0; k < n; ++k) {
-        hipLaunchKernelGGL((dev::lu_pivot_kernel<S>), dim3(1), dim3(1024), 0, st, a, n, k, piv, f->zero_pivot);
-        const int64_t m = n - k - 1;
-        if (m > 0)
-            hipLaunchKernelGGL((dev::lu_update_kernel<S>), dim3((m * m + 255) / 256), dim3(256), 0, st, a, n, k);
+    // right-looking blocked LU with partial pivoting (LAPACK getrf order): per panel of NB columns,
+    // column-by-column pivoting and rank-1 updates inside the panel, the panel's interchanges on
+    // the other columns, U12 = L11^-1 A12, and A22 -= L21 U12 on the fp64 matrix cores
+    constexpr int NB = dev::RankKMax<S>::value;
+    for (int64_t k0 = 0; k0 < n; k0 += NB) {
+        const int kb = (int)std::min<int64_t>(NB, n - k0);
+        const int64_t c1 = k0 + kb;
+        for (int64_t k = k0; k < c1; ++k) {
+            hipLaunchKernelGGL((dev::lu_pivot_kernel<S>), dim3(1), dim3(1024), 0, st, a, n, k, k0, c1, piv,
+                               f->zero_pivot);
+            const int64_t m = n - k - 1, w = c1 - k - 1;
+            if (m > 0 && w > 0)
+                hipLaunchKernelGGL((dev::lu_update_kernel<S>), dim3((m * w + 255) / 256), dim3(256), 0, st, a, n, k, c1);
+        }
+        if (n - kb > 0)
+            hipLaunchKernelGGL((dev::lu_laswp_kernel<S>), dim3((n - kb + 255) / 256), dim3(256), 0, st, a, n, k0, kb, piv);
+        const int64_t rest = n - c1;
+        if (rest > 0) {
+            hipLaunchKernelGGL((dev::lu_trsm_kernel<S, NB>), dim3((rest + 255) / 256), dim3(256), 0, st, a, n, k0, kb);
+            rankk_update<S, true>(st, (int)rest, (int)rest, kb, -1.0, a + c1 + k0 * n, n, a + k0 + c1 * n, n,
+                                  a + c1 + c1 * n, n);
+        }
     }
     EIGSOL_HIP(hipGetLastError());
     std::vector<int32_t> hp(n);
