@@ -40,13 +40,13 @@ int hqr_lds(hipStream_t st, const double* H, int64_t ld, int n, int maxits, doub
 namespace dev {
 
 constexpr int kWin = 96;        // window rows/columns (H window + U: 2 x 72 KiB of LDS)
-constexpr int kMaxBulges = 24;   // shifts per sweep / 2 (at most 16 per window: one wave each)
+constexpr int kMaxBulges = 32;   // shifts per sweep / 2 (at most 16 per window: one wave each)
 
 // compiler-only ordering of LDS accesses (one wave's LDS operations execute in issue order)
 #define EIGSOL_LDS_ORDER() asm volatile("" ::: "memory")
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
-constexpr int kMaxGroups = 6;   // bulge groups chased concurrently, one window (workgroup) each
+constexpr int kMaxGroups = 8;   // bulge groups chased concurrently, one window (workgroup) each
 
 // One window of a chase round: group g's bulges j = 0..nb-1 sit at rows k = l + t - 3 j for the
 // group-local steps t in [t0, t1); the window [s, e) holds them for the whole round.
@@ -746,7 +746,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     }();
     static const int max_bulges = [] {                 // experiments: cap the bulges per chain
         const char* e = std::getenv("EIGSOL_QR_NB");
-        return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : dev::kMaxBulges;
+        return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : 24;
     }();
     long long st_steps = 0;
     static const int aed_win = [] {
@@ -888,8 +888,9 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         // chase: C groups of nbg bulges, group g starting G steps after group g-1, each group in its
         // own LDS window; a round advances every group's window by the same number of steps
         // groups of >= 4 bulges; the spacing costs (C - 1) G extra steps, kept below N / 4
-        const int C = std::max(1, std::min({max_groups, nb / 4, 1 + N / (4 * (dev::kWin + 12))}));
-        const int nbg = nb / C;
+        const int Nact = ihi - l + 1;   // after the AED's deflations
+        const int C = std::max(1, std::min({max_groups, nb / 4, 1 + Nact / (4 * (dev::kWin + 12))}));
+        const int nbg = std::min(nb / C, 16);   // one wave per bulge: at most 16 per window
         const int G = dev::kWin + 3 * nbg;   // group spacing: windows stay disjoint
         const int Tg = (ihi - 1 - l) + 3 * (nbg - 1) + 1;     // steps of one group
         const int T = (C - 1) * G + Tg;
@@ -918,6 +919,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                 ca.w[nwin] = dev::ChaseWin{s, e, tl, 0, nbg, dsh + 2 * g * nbg, dU + (size_t)nwin * dev::kWin * dev::kWin};
                 g_act[nwin++] = g;
             }
+            if (nwin == 0 && t1 > t0) { t0 = t1; continue; }   // every started group done, the next not yet due
             if (t1 <= t0 || nwin == 0) { rc = fail(EIGSOL_E_SOLVER, "francis: window did not advance (internal error)"); break; }
             for (int q = 0; q < nwin; ++q) {
                 ca.w[q].t1 = t1 - g_act[q] * G;
