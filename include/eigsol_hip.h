@@ -214,6 +214,12 @@ int eigsol_qr_eigenvalues_dense(eigsol_ctx* ctx, int dtype, int64_t n, const voi
 #define EIGSOL_EXCHANGE_ALLGATHER 1
 int eigsol_dist_unique_id_bytes(void);
 int eigsol_dist_get_unique_id(void* id_out);
+/* Test transport: an id that makes eigsol_ctx_create_dist join an in-process loopback world of
+ * nranks ranks instead of an RCCL communicator (one host thread per rank, any devices of this
+ * process, e.g. all on one GPU).  Every exchange of the row-sharded path runs as device copies
+ * between the ranks' buffers, so the whole device-side path (ghost layout, pack, halo and
+ * all-gather slots, rank-order partials) can be tested where RCCL cannot run several ranks. */
+int eigsol_dist_loopback_id(int nranks, void* id_out);
 int eigsol_ctx_create_dist(int device, int rank, int nranks, const void* unique_id,
                            eigsol_ctx** out);
 int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* row_begins,

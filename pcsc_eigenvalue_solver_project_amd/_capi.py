@@ -90,6 +90,7 @@ SIGNATURES = {
     "eigsol_power_kernel_info": [_vp, _pd, _pi32, _pi32, _pi32],
     "eigsol_dist_unique_id_bytes": [],
     "eigsol_dist_get_unique_id": [_vp],
+    "eigsol_dist_loopback_id": [C.c_int, _vp],
     "eigsol_ctx_create_dist": [C.c_int, C.c_int, C.c_int, _vp, _ppv],
     "eigsol_csr_create_dist": [_vp, C.c_int, _vp, _i64, _vp, _vp, _vp, _ppv],
     "eigsol_ghost_plan": [C.c_int, _vp, C.c_int, _i64, _vp, _vp, _pi64, _vp, _vp],

@@ -16,8 +16,15 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
 #include <vector>
 
 #include "internal.hpp"
@@ -35,10 +42,114 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
             return ::eigsol::fail(EIGSOL_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
     } while (0)
 
+// ------------------------------------------------------------------------- loopback world
+// Test transport: P ranks of one process, one host thread each, all on the same device.  Every
+// communication step is a list of sends and receives; a step posts this rank's sends, records an
+// event after everything the sends read, meets the other ranks at a host barrier, copies each
+// receive from the matching send (k-th receive from q = k-th send from q to this rank, NCCL's
+// per-pair order) on its own stream after the sender's event, records a second event, meets them
+// again and waits for every peer's copies before the stream moves on (so no rank overwrites a
+// buffer a peer still reads).  RCCL's collectives are expressed as sends and receives: an in-place
+// all-gather is a send of the own block to, and a receive of every other block from, each peer.
+// It exercises every device-side piece of the row-sharded path except RCCL itself.
+struct LoopSend {
+    int peer;
+    const void* p;
+    size_t bytes;
+};
+struct LoopRecv {
+    int peer;
+    void* p;
+    size_t bytes;
+};
+struct LoopWorld {
+    int P = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    long gen = 0;
+    int joined = 0;
+    std::vector<std::vector<LoopSend>> sends;
+    std::vector<hipEvent_t> ready, done;
+};
+static std::mutex g_loop_m;
+static std::map<std::string, std::shared_ptr<LoopWorld>> g_loop_worlds;
+static const char kLoopMagic[] = "EIGSOL-LOOPBACK:";
+
+static void loop_barrier(LoopWorld* w) {
+    std::unique_lock<std::mutex> lk(w->m);
+    const long g = w->gen;
+    if (++w->arrived == w->P) {
+        w->arrived = 0;
+        ++w->gen;
+        w->cv.notify_all();
+    } else {
+        w->cv.wait(lk, [&] { return w->gen != g; });
+    }
+}
+
+static int loop_step(eigsol_ctx* ctx, const std::vector<LoopSend>& sends, const std::vector<LoopRecv>& recvs) {
+    auto* w = static_cast<LoopWorld*>(ctx->loop);
+    const int me = ctx->rank;
+    hipStream_t st = ctx->stream;
+    {
+        std::lock_guard<std::mutex> lk(w->m);
+        w->sends[me] = sends;
+    }
+    EIGSOL_HIP(hipEventRecord(w->ready[me], st));
+    loop_barrier(w);
+    std::vector<int> seen(w->P, 0);
+    int rc = EIGSOL_OK;
+    for (const LoopRecv& r : recvs) {
+        int k = seen[r.peer]++, idx = -1;
+        const std::vector<LoopSend>& ps = w->sends[r.peer];
+        for (size_t j = 0; j < ps.size(); ++j)
+            if (ps[j].peer == me && k-- == 0) { idx = (int)j; break; }
+        if (idx < 0 || ps[idx].bytes != r.bytes) {
+            rc = fail(EIGSOL_E_RCCL, "loopback: unmatched receive (internal error)");
+            break;
+        }
+        if (hipStreamWaitEvent(st, w->ready[r.peer], 0) != hipSuccess ||
+            (r.bytes && hipMemcpyAsync(r.p, ps[idx].p, r.bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)) {
+            rc = fail(EIGSOL_E_HIP, "loopback: copy");
+            break;
+        }
+    }
+    if (hipEventRecord(w->done[me], st) != hipSuccess && rc == EIGSOL_OK) rc = fail(EIGSOL_E_HIP, "loopback: event");
+    loop_barrier(w);   // every rank reaches it, also after an error, so nobody waits forever
+    for (int q = 0; q < w->P; ++q)
+        if (q != me && hipStreamWaitEvent(st, w->done[q], 0) != hipSuccess && rc == EIGSOL_OK)
+            rc = fail(EIGSOL_E_HIP, "loopback: event wait");
+    return rc;
+}
+
+// in-place all-gather of `count` bytes per rank as loopback sends/receives
+static void loop_allgather(eigsol_ctx* ctx, void* buf, size_t bytes, std::vector<LoopSend>& s,
+                           std::vector<LoopRecv>& r) {
+    char* b = static_cast<char*>(buf);
+    for (int q = 0; q < ctx->nranks; ++q) {
+        if (q == ctx->rank) continue;
+        s.push_back({q, b + (size_t)ctx->rank * bytes, bytes});
+        r.push_back({q, b + (size_t)q * bytes, bytes});
+    }
+}
+
 void dist_release_comm(eigsol_ctx* ctx) {
     if (ctx && ctx->comm) {
         ncclCommDestroy(static_cast<ncclComm_t>(ctx->comm));
         ctx->comm = nullptr;
+    }
+    if (ctx && ctx->loop) {
+        auto* w = static_cast<LoopWorld*>(ctx->loop);
+        std::lock_guard<std::mutex> g(g_loop_m);
+        for (auto it = g_loop_worlds.begin(); it != g_loop_worlds.end(); ++it)
+            if (it->second.get() == w && --w->joined == 0) {
+                for (hipEvent_t e : w->ready) hipEventDestroy(e);
+                for (hipEvent_t e : w->done) hipEventDestroy(e);
+                g_loop_worlds.erase(it);
+                break;
+            }
+        ctx->loop = nullptr;
     }
 }
 
@@ -69,6 +180,30 @@ int dist_exchange(eigsol_csr* A, void* y, void* rank_part) {
     const size_t dpe = sb / 8;   // doubles per scalar
     char* xs = static_cast<char*>(y);   // x-space: [lower ghosts | own rows | upper ghosts]
     double* rpart = static_cast<double*>(rank_part);
+    if (ctx->loop) {
+        std::vector<LoopSend> ls;
+        std::vector<LoopRecv> lr;
+        if (A->exchange == EIGSOL_EXCHANGE_ALLGATHER) {
+            const std::vector<int64_t>& rb = A->row_begins;
+            for (int q = 0; q < ctx->nranks; ++q) {
+                if (q == ctx->rank) continue;
+                ls.push_back({q, xs + (size_t)rb[ctx->rank] * sb, (size_t)(rb[ctx->rank + 1] - rb[ctx->rank]) * sb});
+                lr.push_back({q, xs + (size_t)rb[q] * sb, (size_t)(rb[q + 1] - rb[q]) * sb});
+            }
+        } else {
+            for (int q = 0; q < ctx->nranks; ++q) {
+                if (q == ctx->rank) continue;
+                if (A->send_counts[q] > 0)
+                    ls.push_back({q, static_cast<char*>(A->send_buf) + (size_t)A->send_offs[q] * sb,
+                                  (size_t)A->send_counts[q] * sb});
+                if (A->recv_counts[q] > 0)
+                    lr.push_back({q, xs + (size_t)(A->recv_offs[q] + (q > ctx->rank ? A->nrows : 0)) * sb,
+                                  (size_t)A->recv_counts[q] * sb});
+            }
+        }
+        loop_allgather(ctx, rpart, 4 * sizeof(double), ls, lr);
+        return loop_step(ctx, ls, lr);
+    }
     if (A->exchange == EIGSOL_EXCHANGE_ALLGATHER) {
         // x-space = the global index space: every rank's own block lands in place on every rank
         const std::vector<int64_t>& rb = A->row_begins;
@@ -194,11 +329,51 @@ int eigsol_dist_get_unique_id(void* id_out) {
 
 int eigsol_dist_unique_id_bytes(void) { return NCCL_UNIQUE_ID_BYTES; }
 
+int eigsol_dist_loopback_id(int nranks, void* id_out) {
+    if (!id_out || nranks < 1) return fail(EIGSOL_E_INVALID, "eigsol_dist_loopback_id: invalid argument");
+    static std::atomic<long> serial{0};
+    char buf[NCCL_UNIQUE_ID_BYTES] = {0};
+    std::snprintf(buf, sizeof(buf), "%s%d:%ld:%p", kLoopMagic, nranks, serial.fetch_add(1), (void*)&serial);
+    std::memcpy(id_out, buf, sizeof(buf));
+    return EIGSOL_OK;
+}
+
 int eigsol_ctx_create_dist(int device, int rank, int nranks, const void* unique_id,
                            eigsol_ctx** out) {
     if (!out || !unique_id || nranks < 1 || rank < 0 || rank >= nranks)
         return fail(EIGSOL_E_INVALID, "eigsol_ctx_create_dist: invalid argument");
     EIGSOL_TRY(eigsol_ctx_create(device, out));
+    if (std::strncmp(static_cast<const char*>(unique_id), kLoopMagic, sizeof(kLoopMagic) - 1) == 0) {
+        const std::string key(static_cast<const char*>(unique_id),
+                              strnlen(static_cast<const char*>(unique_id), NCCL_UNIQUE_ID_BYTES));
+        std::shared_ptr<LoopWorld> w;
+        {
+            std::lock_guard<std::mutex> g(g_loop_m);
+            auto& slot = g_loop_worlds[key];
+            if (!slot) {
+                slot = std::make_shared<LoopWorld>();
+                slot->P = nranks;
+                slot->sends.resize(nranks);
+                slot->ready.resize(nranks);
+                slot->done.resize(nranks);
+                for (int q = 0; q < nranks; ++q) {
+                    hipEventCreateWithFlags(&slot->ready[q], hipEventDisableTiming);
+                    hipEventCreateWithFlags(&slot->done[q], hipEventDisableTiming);
+                }
+            }
+            w = slot;
+            ++w->joined;
+        }
+        if (w->P != nranks) {
+            eigsol_ctx_destroy(*out);
+            *out = nullptr;
+            return fail(EIGSOL_E_INVALID, "eigsol_ctx_create_dist: loopback world size mismatch");
+        }
+        (*out)->loop = w.get();
+        (*out)->rank = rank;
+        (*out)->nranks = nranks;
+        return EIGSOL_OK;
+    }
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
     ncclComm_t comm = nullptr;
@@ -220,7 +395,7 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
                            const int32_t* colidx_global, const void* values, eigsol_csr** out) {
     if (!ctx || !out || !row_begins || !rowptr_local)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: null argument");
-    if (!ctx->comm) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
+    if (!ctx->comm && !ctx->loop) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
     *out = nullptr;
     const int P = ctx->nranks, me = ctx->rank;
     const int64_t n_global = row_begins[P];
@@ -238,7 +413,14 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     int64_t *d_counts = nullptr, *d_req = nullptr, *d_srcreq = nullptr;
     EIGSOL_HIP(hipMalloc(&d_counts, sizeof(int64_t) * P * P));
     EIGSOL_HIP(hipMemcpyAsync(d_counts + (size_t)me * P, recv.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice, st));
-    EIGSOL_RCCL(ncclAllGather(d_counts + (size_t)me * P, d_counts, P, ncclInt64, comm, st));
+    if (ctx->loop) {
+        std::vector<LoopSend> ls;
+        std::vector<LoopRecv> lr;
+        loop_allgather(ctx, d_counts, sizeof(int64_t) * P, ls, lr);
+        EIGSOL_TRY(loop_step(ctx, ls, lr));
+    } else {
+        EIGSOL_RCCL(ncclAllGather(d_counts + (size_t)me * P, d_counts, P, ncclInt64, comm, st));
+    }
     std::vector<int64_t> all(P * P);
     EIGSOL_HIP(hipMemcpyAsync(all.data(), d_counts, sizeof(int64_t) * P * P, hipMemcpyDeviceToHost, st));
     EIGSOL_HIP(hipStreamSynchronize(st));
@@ -275,13 +457,24 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     EIGSOL_HIP(hipMalloc(&d_req, sizeof(int64_t) * std::max<int64_t>(nsend, 1)));
     if (nghost[0])
         EIGSOL_HIP(hipMemcpyAsync(d_srcreq, ghosts.data(), sizeof(int64_t) * nghost[0], hipMemcpyHostToDevice, st));
-    EIGSOL_RCCL(ncclGroupStart());
-    for (int q = 0; q < P; ++q) {
-        if (q == me) continue;
-        if (recv[q]) EIGSOL_RCCL(ncclSend(d_srcreq + roff[q], recv[q], ncclInt64, q, comm, st));
-        if (send[q]) EIGSOL_RCCL(ncclRecv(d_req + soff[q], send[q], ncclInt64, q, comm, st));
+    if (ctx->loop) {
+        std::vector<LoopSend> ls;
+        std::vector<LoopRecv> lr;
+        for (int q = 0; q < P; ++q) {
+            if (q == me) continue;
+            if (recv[q]) ls.push_back({q, d_srcreq + roff[q], sizeof(int64_t) * recv[q]});
+            if (send[q]) lr.push_back({q, d_req + soff[q], sizeof(int64_t) * send[q]});
+        }
+        EIGSOL_TRY(loop_step(ctx, ls, lr));
+    } else {
+        EIGSOL_RCCL(ncclGroupStart());
+        for (int q = 0; q < P; ++q) {
+            if (q == me) continue;
+            if (recv[q]) EIGSOL_RCCL(ncclSend(d_srcreq + roff[q], recv[q], ncclInt64, q, comm, st));
+            if (send[q]) EIGSOL_RCCL(ncclRecv(d_req + soff[q], send[q], ncclInt64, q, comm, st));
+        }
+        EIGSOL_RCCL(ncclGroupEnd());
     }
-    EIGSOL_RCCL(ncclGroupEnd());
     std::vector<int64_t> req(std::max<int64_t>(nsend, 1));
     if (nsend) EIGSOL_HIP(hipMemcpyAsync(req.data(), d_req, sizeof(int64_t) * nsend, hipMemcpyDeviceToHost, st));
     EIGSOL_HIP(hipStreamSynchronize(st));

@@ -167,6 +167,7 @@ struct eigsol_ctx {
     int num_cus = 256;
     // distributed (filled by eigsol_dist_* when a communicator is attached)
     void* comm = nullptr;
+    void* loop = nullptr;   // in-process loopback world (tests: several ranks on one device), else null
     int rank = 0;
     int nranks = 1;
 };

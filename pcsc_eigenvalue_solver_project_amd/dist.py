@@ -61,6 +61,14 @@ def unique_id() -> bytes:
     return bytes(buf)
 
 
+def loopback_id(world: int) -> bytes:
+    """Id of an in-process loopback world (tests: ``world`` ranks, one thread each, one device)."""
+    n = lib().eigsol_dist_unique_id_bytes()
+    buf = (C.c_char * n)()
+    call("eigsol_dist_loopback_id", int(world), C.cast(buf, C.c_void_p))
+    return bytes(buf)
+
+
 def torch_dist_context(device: int, stream=None) -> DistContext:
     """Bootstrap from an initialised torch.distributed process group (gloo or nccl)."""
     import torch

@@ -1,9 +1,14 @@
-"""GPU: the row-sharded path (eigsol_ctx_create_dist / eigsol_csr_create_dist) on one rank.
+"""GPU: the row-sharded path (eigsol_ctx_create_dist / eigsol_csr_create_dist).
 
-A one-GPU box cannot host two RCCL ranks (RCCL refuses two ranks on one device), so the
-multi-rank exchange is covered by tests/test_dist_cpu.py (gloo, world_size 2) and by
-construction; here the distributed constructors, the RCCL communicator, the in-place rank-partial
-all-gather and the session plumbing run for real with nranks = 1 and must reproduce the oracle.
+A one-GPU box cannot host two RCCL ranks (RCCL refuses two ranks on one device).  So:
+  * with RCCL, nranks = 1: the distributed constructors, the communicator, the in-place
+    rank-partial all-gather and the session plumbing run for real and must reproduce the oracle;
+  * with the loopback transport (eigsol_dist_loopback_id: 2-3 ranks as threads of this process on
+    one device, every exchange a device copy), the whole device side of the multi-rank path runs:
+    ghost layout with lower and upper ghosts, the pack kernel, halo and all-gather slots, and the
+    rank-order partial sums — eigenvalue bitwise identical on every rank, parity with the oracle
+    on the unsharded matrix (|dlambda| <= 1e-10 (1 + |lambda|), iterations +-1, |x^H x_ref| >= 1 - 1e-10).
+tests/test_dist_cpu.py covers the host planning with gloo, world_size 2.
 """
 import numpy as np
 import pytest
@@ -61,3 +66,73 @@ def test_dist_single_rank_allgather_exchange(monkeypatch):
         A.close()
     finally:
         ctx.close()
+
+
+def _loopback_run(world, kind, n, k, exchange=None, monkeypatch=None):
+    """`world` ranks in threads of this process, one device, joined by the loopback transport."""
+    import threading
+    if exchange:
+        monkeypatch.setenv("EIGSOL_DIST_EXCHANGE", exchange)
+    rp, ci, v = S.band(n, k) if kind == "band" else S.uniform(n, k)
+    x0 = S.start_vector(n)
+    uid = D.loopback_id(world)
+    rows = n // world
+    out, errs = [None] * world, []
+
+    def rank_main(r):
+        try:
+            r0, r1 = r * rows, (n if r == world - 1 else (r + 1) * rows)
+            lrp = (rp[r0:r1 + 1] - rp[r0]).astype(np.int32)
+            lci, lv = ci[rp[r0]:rp[r1]], v[rp[r0]:rp[r1]]
+            ctx = D.DistContext(0, r, world, uid)
+            rb = np.array([q * rows for q in range(world)] + [n], dtype=np.int64)
+            A = D.DistCsrMatrix(ctx, rb, lrp, lci, lv)
+            sess = E.PowerSession(A)
+            sess.begin(E.SolverOptions(300, 1e-12), x0[r0:r1])
+            sess.step(301)
+            assert sess.query()[0]
+            out[r] = (sess.finish(), A.exchange)
+            sess.close()
+            A.close()
+            ctx.close()
+        except Exception as e:          # surfaced after join
+            errs.append(e)
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts), "loopback ranks hung"
+    assert not errs, errs
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    ref = O.power_csc(cp, ri, vv, x0, 300, 1e-12, want_trace=True)
+    assert ref["converged"]
+    lam = [o[0].eigenvalue for o in out]
+    assert all(lv_ == lam[0] for lv_ in lam), lam               # bitwise identical on every rank
+    for o in out:
+        assert o[0].iterations == out[0][0].iterations and o[0].converged
+    x = np.concatenate([o[0].eigenvector for o in out])
+    assert abs(lam[0] - ref["eigenvalue"]) <= 1e-10 * (1 + abs(ref["eigenvalue"]))
+    assert abs(out[0][0].iterations - ref["iterations"]) <= 1
+    assert abs(abs(np.vdot(x, ref["eigenvector"])) - 1) <= 1e-10
+    return [o[1] for o in out]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_loopback_multi_rank_halo(world):
+    """Several ranks on one GPU (loopback transport): ghost layout with lower and upper ghosts,
+    pack kernel, halo slots, rank-order partials — the device side of the multi-GPU path."""
+    modes = _loopback_run(world, "band", 30000, 12)
+    assert all(m == D.EXCHANGE_HALO for m in modes)
+
+
+def test_loopback_multi_rank_allgather(monkeypatch):
+    modes = _loopback_run(2, "uniform", 20000, 8, exchange="allgather", monkeypatch=monkeypatch)
+    assert all(m == D.EXCHANGE_ALLGATHER for m in modes)
+
+
+def test_loopback_uniform_auto_exchange():
+    """Unstructured columns choose the all-gather exchange by themselves (ghost counts)."""
+    modes = _loopback_run(2, "uniform", 20000, 8)
+    assert all(m == D.EXCHANGE_ALLGATHER for m in modes)
