@@ -378,7 +378,7 @@ __device__ __forceinline__ int wave_max_int(int v) {
 
 template <bool kSchur>
 __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double* wr, double* wi, int* bs,
-                         int& fail, int& total, int& maxsw) {
+                         int& fail, int& total, int& maxsw, int* steps_out = nullptr) {
     const int lane = threadIdx.x & 63;
     auto T = [&](int i, int j) -> double& { return t[i + j * LD]; };
     auto V = [&](int i, int j) -> double& { return v[i + j * LD]; };
@@ -463,6 +463,7 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
         EIGSOL_LDS_ORDER();
         const int jend = kSchur ? n : nn + 1;      // left updates: to the matrix end (Schur) or the block end
         const int ibeg = kSchur ? 0 : l;           // right updates: from row 0 (Schur) or the block top
+        if (steps_out) *steps_out += nn - m;
         for (int k = m; k <= nn - 1; ++k) {
             double p = p0, q = q0, r = r0, xk = 1.0;
             const bool three = k != nn - 1;
@@ -576,7 +577,8 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
     const double eps = 2.220446049250313e-16;
     int fail, total, maxsw;
     // ---------------- phase A: real Schur form with V
-    wave_hqr<true>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw);
+    int steps = 0;
+    wave_hqr<true>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
     __syncthreads();
     // ---------------- phase B: spike test from the bottom
     if (tid == 0) {
@@ -681,6 +683,7 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
         info[1] = nd;
         info[2] = total;
         info[3] = m;
+        info[4] = steps;
     }
 }
 
@@ -748,7 +751,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         const char* e = std::getenv("EIGSOL_QR_NB");
         return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : 24;
     }();
-    long long st_steps = 0;
+    long long st_steps = 0, st_aed_steps = 0;
     static const int aed_win = [] {
         const char* e = std::getenv("EIGSOL_QR_AED");   // AED window (0: off)
         return e ? std::max(0, std::min(dev::kAedMax, std::atoi(e))) : kAedDefault;
@@ -799,7 +802,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             const int kw = ihi - nw + 1;
             hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(64), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60, dwr, dwi,
                                dU, dinfo);
-            int info[4];
+            int info[5];
             std::vector<double> awr(nw), awi(nw);
             if (hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipMemcpyAsync(awr.data(), dwr + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -809,6 +812,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                 break;
             }
             ++st_aed;
+            st_aed_steps += info[4];
             if (!info[0]) {
                 const int nd = info[1], m = info[3];
                 if (nd > 0) {
@@ -971,9 +975,9 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     }
     if (stats)
         std::fprintf(stderr, "francis: n=%lld sweeps=%d windows=%d steps=%lld small_blocks=%d small_rows=%d kSmall=%d "
-                     "aed=%d aed_deflated=%d aed_win=%d\n",
+                     "aed=%d aed_deflated=%d aed_win=%d aed_steps=%lld\n",
                      (long long)n, st_sweeps, st_windows, st_steps, st_small, st_small_rows, kSmall, st_aed, st_aed_defl,
-                     aed_win);
+                     aed_win, st_aed_steps);
     for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo}) (void)hipFree(p);
     // iterations reported: sweeps spent on the slowest deflation (>= 1, the final check), so that
     // iterations <= maxIterations exactly when the iteration converged
