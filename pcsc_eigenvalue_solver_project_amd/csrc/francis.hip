@@ -376,7 +376,7 @@ __device__ __forceinline__ int wave_max_int(int v) {
     return v;
 }
 
-template <bool kSchur>
+template <bool kSchur, int NX>
 __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double* wr, double* wi, int* bs,
                          int& fail, int& total, int& maxsw, int* steps_out = nullptr) {
     const int lane = threadIdx.x & 63;
@@ -464,9 +464,12 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
         const int jend = kSchur ? n : nn + 1;      // left updates: to the matrix end (Schur) or the block end
         const int ibeg = kSchur ? 0 : l;           // right updates: from row 0 (Schur) or the block top
         if (steps_out) *steps_out += nn - m;
-        for (int k = m; k <= nn - 1; ++k) {
-            double p = p0, q = q0, r = r0, xk = 1.0;
-            const bool three = k != nn - 1;
+        // one reflector step; `three` is a compile-time constant (only the sweep's last step is a
+        // 2-row reflector), k is wave-uniform, and the updates are explicit FMAs, so the step is
+        // straight-line code on a single wave (its cost is instruction issue)
+        auto step = [&](const int k, auto three_c) {
+            constexpr bool three = decltype(three_c)::value;
+            double p = p0, q = q0, r = three ? r0 : 0.0, xk = 1.0;
             if (k != m) {
                 p = T(k, k - 1);
                 q = T(k + 1, k - 1);
@@ -474,44 +477,60 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
                 xk = fabs(p) + fabs(q) + fabs(r);
                 if (xk != 0.0) { const double is = rcp_nr(xk); p *= is; q *= is; r *= is; }
             }
-            const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(p * p + q * q + r * r);
-            if (sg == 0.0) continue;
+            const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(__builtin_fma(p, p, __builtin_fma(q, q, r * r)));
+            if (sg == 0.0) return;
             EIGSOL_LDS_ORDER();
-            if (lane == 0) {
-                if (k == m) {
-                    if (l != m) T(k, k - 1) = -T(k, k - 1);
-                } else {
-                    T(k, k - 1) = -sg * xk;
-                    T(k + 1, k - 1) = 0.0;
-                    if (three) T(k + 2, k - 1) = 0.0;
-                }
+            if (lane == 0 && k != m) {
+                T(k, k - 1) = -sg * xk;
+                T(k + 1, k - 1) = 0.0;
+                if (three) T(k + 2, k - 1) = 0.0;
             }
             p += sg;
             const double isg = rcp_nr(sg), ip = rcp_nr(p);
             const double ax = p * isg, ay = q * isg, az = r * isg, bq = q * ip, br = r * ip;
-            for (int j = k + lane; j < jend; j += 64) {
-                double pp = T(k, j) + bq * T(k + 1, j);
-                if (three) { pp += br * T(k + 2, j); T(k + 2, j) -= pp * az; }
-                T(k + 1, j) -= pp * ay;
-                T(k, j) -= pp * ax;
+#pragma unroll
+            for (int x = 0; x < NX; ++x) {        // NX = ceil(n / 64): no loop control on the step's path
+                const int j = k + lane + 64 * x;
+                if (j < jend) {
+                    const double t0 = T(k, j), t1 = T(k + 1, j);
+                    double pp = __builtin_fma(bq, t1, t0);
+                    if (three) {
+                        const double t2 = T(k + 2, j);
+                        pp = __builtin_fma(br, t2, pp);
+                        T(k + 2, j) = __builtin_fma(-pp, az, t2);
+                    }
+                    T(k + 1, j) = __builtin_fma(-pp, ay, t1);
+                    T(k, j) = __builtin_fma(-pp, ax, t0);
+                }
             }
             EIGSOL_LDS_ORDER();
             const int imax = nn < k + 3 ? nn : k + 3;
             // right update of T and (Schur) of V in one pass: both columns' loads issued together
-            const int iend = kSchur ? max(imax + 1, n) : imax + 1;
-            for (int i = lane; i + ibeg < iend || i < (kSchur ? n : 0); i += 64) {
+#pragma unroll
+            for (int x = 0; x < NX; ++x) {
+                const int i = lane + 64 * x;
                 const int it = ibeg + i;
                 const bool ct = it <= imax, cv = kSchur && i < n;
                 double t0 = 0, t1 = 0, t2 = 0, v0 = 0, v1 = 0, v2 = 0;
                 if (ct) { t0 = T(it, k); t1 = T(it, k + 1); if (three) t2 = T(it, k + 2); }
                 if (cv) { v0 = V(i, k); v1 = V(i, k + 1); if (three) v2 = V(i, k + 2); }
-                const double pt = ax * t0 + ay * t1 + (three ? az * t2 : 0.0);
-                const double pv = ax * v0 + ay * v1 + (three ? az * v2 : 0.0);
-                if (ct) { T(it, k) = t0 - pt; T(it, k + 1) = t1 - pt * bq; if (three) T(it, k + 2) = t2 - pt * br; }
-                if (cv) { V(i, k) = v0 - pv; V(i, k + 1) = v1 - pv * bq; if (three) V(i, k + 2) = v2 - pv * br; }
+                const double pt = three ? __builtin_fma(az, t2, __builtin_fma(ay, t1, ax * t0)) : __builtin_fma(ay, t1, ax * t0);
+                const double pv = three ? __builtin_fma(az, v2, __builtin_fma(ay, v1, ax * v0)) : __builtin_fma(ay, v1, ax * v0);
+                if (ct) {
+                    T(it, k) = t0 - pt;
+                    T(it, k + 1) = __builtin_fma(-pt, bq, t1);
+                    if (three) T(it, k + 2) = __builtin_fma(-pt, br, t2);
+                }
+                if (cv) {
+                    V(i, k) = v0 - pv;
+                    V(i, k + 1) = __builtin_fma(-pv, bq, v1);
+                    if (three) V(i, k + 2) = __builtin_fma(-pv, br, v2);
+                }
             }
             EIGSOL_LDS_ORDER();
-        }
+        };
+        for (int k = m; k <= nn - 2; ++k) step(__builtin_amdgcn_readfirstlane(k), std::true_type{});
+        step(nn - 1, std::false_type{});
     }
     maxsw = max(maxsw, its);
 }
@@ -529,7 +548,8 @@ __global__ __launch_bounds__(64) void hqr_wave_kernel(const double* Hin, int64_t
     }
     __syncthreads();
     int fail, total, maxsw;
-    wave_hqr<false>(t, nullptr, n, LD, maxits, wr, wi, nullptr, fail, total, maxsw);
+    if (n <= 64) wave_hqr<false, 1>(t, nullptr, n, LD, maxits, wr, wi, nullptr, fail, total, maxsw);
+    else wave_hqr<false, 2>(t, nullptr, n, LD, maxits, wr, wi, nullptr, fail, total, maxsw);
     if (threadIdx.x == 0) {
         info[0] = fail;
         info[1] = maxsw;
@@ -578,7 +598,8 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
     int fail, total, maxsw;
     // ---------------- phase A: real Schur form with V
     int steps = 0;
-    wave_hqr<true>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
+    if (nw <= 64) wave_hqr<true, 1>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
+    else wave_hqr<true, 2>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
     __syncthreads();
     // ---------------- phase B: spike test from the bottom
     if (tid == 0) {
