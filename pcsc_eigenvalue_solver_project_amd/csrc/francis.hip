@@ -133,92 +133,110 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
         if (d0) u[i0 + col * W] = c[0];
         if (d1) u[i1 + col * W] = c[1];
     };
+    double ax = 0.0, ay = 0.0, az = 0.0, bq = 0.0, br = 0.0;
+    // phase A of bulge wv at row k (reflector, left update, U columns); `three` compile-time
+    auto phase_a = [&](const int t, const int k, auto three_c) -> bool {
+        constexpr bool three = decltype(three_c)::value;
+        const int kk = k - a.s;
+        if (t == a.t0 || !live(t - 1)) {
+            uload(uc0, kk);
+            uload(uc1, kk + 1);
+            if (three) uload(uc2, kk + 2);
+        } else {
+            uc0[0] = uc1[0]; uc0[1] = uc1[1];
+            uc1[0] = uc2[0]; uc1[1] = uc2[1];
+            if (three) uload(uc2, kk + 2);
+        }
+        double p, q, r, xk = 1.0;
+        if (k == l) {
+            const double sx = a.shifts[2 * wv], sw = a.shifts[2 * wv + 1];
+            const double z = Hw(l, l);
+            const double rr = sx - z;
+            p = (rr * rr - sw) / Hw(l + 1, l) + Hw(l, l + 1);
+            q = Hw(l + 1, l + 1) - z - rr - rr;
+            r = (three && l + 2 <= ihi) ? Hw(l + 2, l + 1) : 0.0;
+            const double sc = fabs(p) + fabs(q) + fabs(r);
+            if (sc != 0.0) { const double is = rcp_nr(sc); p *= is; q *= is; r *= is; }
+        } else {
+            p = Hw(k, k - 1);
+            q = Hw(k + 1, k - 1);
+            r = three ? Hw(k + 2, k - 1) : 0.0;
+            xk = fabs(p) + fabs(q) + fabs(r);
+            if (xk != 0.0) { const double is = rcp_nr(xk); p *= is; q *= is; r *= is; }
+        }
+        const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(__builtin_fma(p, p, __builtin_fma(q, q, r * r)));
+        const bool act = sg != 0.0;
+        if (act) {
+            EIGSOL_LDS_ORDER();
+            if (k != l && ln == 0) {
+                Hw(k, k - 1) = -sg * xk;
+                Hw(k + 1, k - 1) = 0.0;
+                if (three) Hw(k + 2, k - 1) = 0.0;
+            }
+            p += sg;
+            const double isg = rcp_nr(sg), ip = rcp_nr(p);
+            ax = p * isg; ay = q * isg; az = r * isg; bq = q * ip; br = r * ip;
+            // left update, columns k + ln and k + ln + 64 of rows k..k+2
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const int j = k + ln + 64 * x;
+                if (j < a.e) {
+                    const double h0 = Hw(k, j), h1 = Hw(k + 1, j);
+                    double pp = __builtin_fma(bq, h1, h0);
+                    if (three) {
+                        const double h2 = Hw(k + 2, j);
+                        pp = __builtin_fma(br, h2, pp);
+                        Hw(k + 2, j) = __builtin_fma(-pp, az, h2);
+                    }
+                    Hw(k + 1, j) = __builtin_fma(-pp, ay, h1);
+                    Hw(k, j) = __builtin_fma(-pp, ax, h0);
+                }
+            }
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {   // U columns k..k+2 in registers
+                double pu = __builtin_fma(ay, uc1[x], ax * uc0[x]);
+                if (three) pu = __builtin_fma(az, uc2[x], pu);
+                uc0[x] -= pu;
+                uc1[x] = __builtin_fma(-pu, bq, uc1[x]);
+                if (three) uc2[x] = __builtin_fma(-pu, br, uc2[x]);
+            }
+        }
+        // drop column k (bulge b+1 loads it next step); at the bulge's last step here, all three
+        ustore(uc0, kk);
+        if (!live(t + 1)) {
+            ustore(uc1, kk + 1);
+            if (three) ustore(uc2, kk + 2);
+        }
+        return act;
+    };
+    // phase B: right update, rows rlo + ln and rlo + ln + 64 of columns k..k+2
+    auto phase_b = [&](const int k, auto three_c) {
+        constexpr bool three = decltype(three_c)::value;
+        const int ilast = min(k + 3, ihi);
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            const int i = rlo + ln + 64 * x;
+            if (i <= ilast) {
+                const double h0 = Hw(i, k), h1 = Hw(i, k + 1);
+                double pp = __builtin_fma(ay, h1, ax * h0);
+                double h2 = 0.0;
+                if (three) { h2 = Hw(i, k + 2); pp = __builtin_fma(az, h2, pp); }
+                Hw(i, k) = h0 - pp;
+                Hw(i, k + 1) = __builtin_fma(-pp, bq, h1);
+                if (three) Hw(i, k + 2) = __builtin_fma(-pp, br, h2);
+            }
+        }
+    };
     for (int t = a.t0; t < a.t1; ++t) {
-        const int k = l + t - 3 * wv;
+        const int k = __builtin_amdgcn_readfirstlane(l + t - 3 * wv);
         const bool lv = live(t);                           // wave-uniform
         const bool three = k != ihi - 1;
         bool act = false;
-        double ax = 0.0, ay = 0.0, az = 0.0, bq = 0.0, br = 0.0;
-        if (lv) {
-            const int kk = k - a.s;
-            if (t == a.t0 || !live(t - 1)) {
-                uload(uc0, kk);
-                uload(uc1, kk + 1);
-                if (three) uload(uc2, kk + 2);
-            } else {
-                uc0[0] = uc1[0]; uc0[1] = uc1[1];
-                uc1[0] = uc2[0]; uc1[1] = uc2[1];
-                if (three) uload(uc2, kk + 2);
-            }
-            double p, q, r, xk = 1.0;
-            if (k == l) {
-                const double sx = a.shifts[2 * wv], sw = a.shifts[2 * wv + 1];
-                const double z = Hw(l, l);
-                const double rr = sx - z;
-                p = (rr * rr - sw) / Hw(l + 1, l) + Hw(l, l + 1);
-                q = Hw(l + 1, l + 1) - z - rr - rr;
-                r = (l + 2 <= ihi) ? Hw(l + 2, l + 1) : 0.0;
-                const double sc = fabs(p) + fabs(q) + fabs(r);
-                if (sc != 0.0) { const double is = rcp_nr(sc); p *= is; q *= is; r *= is; }
-            } else {
-                p = Hw(k, k - 1);
-                q = Hw(k + 1, k - 1);
-                r = three ? Hw(k + 2, k - 1) : 0.0;
-                xk = fabs(p) + fabs(q) + fabs(r);
-                if (xk != 0.0) { const double is = rcp_nr(xk); p *= is; q *= is; r *= is; }
-            }
-            const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(p * p + q * q + r * r);
-            act = sg != 0.0;
-            if (act) {
-                EIGSOL_LDS_ORDER();
-                if (k != l && ln == 0) {
-                    Hw(k, k - 1) = -sg * xk;
-                    Hw(k + 1, k - 1) = 0.0;
-                    if (three) Hw(k + 2, k - 1) = 0.0;
-                }
-                p += sg;
-                const double isg = rcp_nr(sg), ip = rcp_nr(p);
-                ax = p * isg; ay = q * isg; az = r * isg; bq = q * ip; br = r * ip;
-                // ---- phase A: left update, columns k + ln and k + ln + 64 of rows k..k+2
-                const int j0 = k + ln, j1 = j0 + 64;
-                const bool c0 = j0 < a.e, c1 = j1 < a.e;
-                double h00 = 0, h01 = 0, h02 = 0, h10 = 0, h11 = 0, h12 = 0;
-                if (c0) { h00 = Hw(k, j0); h01 = Hw(k + 1, j0); if (three) h02 = Hw(k + 2, j0); }
-                if (c1) { h10 = Hw(k, j1); h11 = Hw(k + 1, j1); if (three) h12 = Hw(k + 2, j1); }
-                {
-                    const double p0 = h00 + bq * h01 + (three ? br * h02 : 0.0);
-                    const double p1 = h10 + bq * h11 + (three ? br * h12 : 0.0);
-                    if (c0) { Hw(k, j0) = h00 - p0 * ax; Hw(k + 1, j0) = h01 - p0 * ay; if (three) Hw(k + 2, j0) = h02 - p0 * az; }
-                    if (c1) { Hw(k, j1) = h10 - p1 * ax; Hw(k + 1, j1) = h11 - p1 * ay; if (three) Hw(k + 2, j1) = h12 - p1 * az; }
-                }
-#pragma unroll
-                for (int x = 0; x < 2; ++x) {   // U columns k..k+2 in registers
-                    const double pu = ax * uc0[x] + ay * uc1[x] + (three ? az * uc2[x] : 0.0);
-                    uc0[x] -= pu;
-                    uc1[x] -= pu * bq;
-                    if (three) uc2[x] -= pu * br;
-                }
-            }
-            // drop column k (bulge b+1 loads it next step); at the bulge's last step here, all three
-            ustore(uc0, kk);
-            if (!live(t + 1)) {
-                ustore(uc1, kk + 1);
-                if (three) ustore(uc2, kk + 2);
-            }
-        }
+        if (lv) act = three ? phase_a(t, k, std::true_type{}) : phase_a(t, k, std::false_type{});
         __syncthreads();
-        // ---- phase B: right update, rows rlo + ln and rlo + ln + 64 of columns k..k+2
         if (act) {
-            const int ilast = min(k + 3, ihi);
-            const int r0 = rlo + ln, r1 = r0 + 64;
-            const bool c0 = r0 <= ilast, c1 = r1 <= ilast;
-            double h00 = 0, h01 = 0, h02 = 0, h10 = 0, h11 = 0, h12 = 0;
-            if (c0) { h00 = Hw(r0, k); h01 = Hw(r0, k + 1); if (three) h02 = Hw(r0, k + 2); }
-            if (c1) { h10 = Hw(r1, k); h11 = Hw(r1, k + 1); if (three) h12 = Hw(r1, k + 2); }
-            const double p0 = ax * h00 + ay * h01 + (three ? az * h02 : 0.0);
-            const double p1 = ax * h10 + ay * h11 + (three ? az * h12 : 0.0);
-            if (c0) { Hw(r0, k) = h00 - p0; Hw(r0, k + 1) = h01 - p0 * bq; if (three) Hw(r0, k + 2) = h02 - p0 * br; }
-            if (c1) { Hw(r1, k) = h10 - p1; Hw(r1, k + 1) = h11 - p1 * bq; if (three) Hw(r1, k + 2) = h12 - p1 * br; }
+            if (three) phase_b(k, std::true_type{});
+            else phase_b(k, std::false_type{});
         }
         __syncthreads();
     }
