@@ -4,9 +4,9 @@ summary of tools/prof_driver.py --workload qr4096:
 
   hessenberg : the blocked Hessenberg's trailing updates (hessenberg_blocked_f64): W0 = V^T A
                (split-K), M = V^T Y, W -= M V^T, W2^T = W^T T, and the single rank-2nb update
-               A(:, c1:) -= [Y | V] [V | W2^T]^T (rankk_mfma_f64).  Useful flops only: the rank
+               A(:, c1:) -= [Y | V] [V | W2^T]^T (rankk_mfma<double>).  Useful flops only: the rank
                update's zero rows of V above the panel are not counted.
-  rank_update: rankk_mfma_f64 alone, flops it executes (2 n mt 2nb).
+  rank_update: rankk_mfma<double> alone, flops it executes (2 n mt 2nb).
   francis    : the delayed window updates of the multishift sweeps (win_gemm_mfma); their sizes
                vary per window, so only their kernel time and share of the run are reported.
 
@@ -51,9 +51,9 @@ def main():
         t = float(r["TotalDurationNs"])
         kernels[r["Name"]] = {"calls": int(r["Calls"]), "total_ns": t}
         total_ns += t
-        if "gemm_mfma_f64" in r["Name"] or "gemm_reduce" in r["Name"] or "rankk_mfma_f64" in r["Name"]:
+        if "gemm_mfma_f64" in r["Name"] or "gemm_reduce" in r["Name"] or "rankk_mfma" in r["Name"]:
             hess_ns += t
-        if "rankk_mfma_f64" in r["Name"]:
+        if "rankk_mfma" in r["Name"]:
             rank_ns += t
         if "win_gemm_mfma" in r["Name"]:
             win_ns += t
