@@ -239,6 +239,26 @@ def run_config2(E, ctx, no_cpu):
     return out
 
 
+def run_dense_power(E, S, ctx, torch, stream):
+    """Dense branch of powerMethod (power_method.hpp:141-143): column-major fp64 GEMV fused with the
+    norm and Rayleigh partials, 16384^2 (2 GiB, HBM-bound: 8 n^2 + 16 n bytes per iteration)."""
+    n = 16384
+    A = np.random.default_rng(1).standard_normal((n, n))
+    D = E.DenseMatrix(ctx, A)
+    del A
+    s = E.PowerSession(D)
+    s.begin(E.SolverOptions(2**31 - 1, -1.0), S.start_vector(n))
+    s.step(5)
+    torch.cuda.synchronize()
+    ms = _events(torch, stream, lambda: s.step(50)) / 50
+    info = s.kernel_info()
+    gbs = info["bytes_per_iteration"] / (ms / 1e3) / 1e9
+    s.close()
+    D.close()
+    return {"n": n, "dtype": "f64", "ms_per_iteration": round(ms, 4), "GB/s": round(gbs, 1),
+            "roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "kernel": info["kernel"]}
+
+
 def run_config1(E, S, ctx):
     """BASELINE config 1: data/A.txt read as double (the reference's text format), power method."""
     path = os.path.join(ROOT, "tests", "golden", "A.txt")
@@ -427,6 +447,7 @@ def main():
             "config1_A_txt": run_config1(E, S, ctx),
             "config2_qr_4096": run_config2(E, ctx, args.no_cpu_baseline),
             "config5_shifted_inverse_1M": run_config5(E, S, ctx, torch, torch_stream, args.no_cpu_baseline),
+            "dense_power_16384": run_dense_power(E, S, ctx, torch, torch_stream),
         }
     sess.close()
     A.close()

@@ -93,7 +93,53 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
     const int64_t wc0 = c0 + w * span;
     const int64_t wc1 = min<int64_t>(c1, wc0 + span);
     const bool full = row0 + PL <= a.n;
-    for (int64_t j = wc0; j < wc1; ++j) {
+    int64_t j = wc0;
+    if constexpr (PL == 2) {
+        // batches of kU columns, all loads issued before the FMAs (A read once: non-temporal), the
+        // same per-row summation order as the one-column loop below
+        constexpr int kU = 8;
+        if (full && ((a.n & 1) == 0)) {
+            for (; j + kU <= wc1; j += kU) {
+                S xj[kU];
+                double2 v[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    xj[u] = xin[j + u];
+                    const double* col = a.a + (j + u) * a.n + row0;
+                    typedef double d2v __attribute__((ext_vector_type(2)));
+                    const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(col));
+                    v[u] = double2{t.x, t.y};
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    S x = xj[u];
+                    if constexpr (kPower) x = scale_in(x, nrm);
+                    acc[0] = add(acc[0], mul(v[u].x, x));
+                    acc[1] = add(acc[1], mul(v[u].y, x));
+                }
+            }
+        }
+    }
+    if constexpr (PL == 1) {
+        constexpr int kU = 8;
+        if (row0 < a.n) {
+            for (; j + kU <= wc1; j += kU) {
+                S xj[kU], v[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    xj[u] = xin[j + u];
+                    v[u] = ldg_stream(a.a + (j + u) * a.n, (uint32_t)row0);
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    S x = xj[u];
+                    if constexpr (kPower) x = scale_in(x, nrm);
+                    acc[0] = add(acc[0], mul(v[u], x));
+                }
+            }
+        }
+    }
+    for (; j < wc1; ++j) {
         S xj = xin[j];
         if constexpr (kPower) xj = scale_in(xj, nrm);
         const S* col = a.a + j * a.n;
