@@ -590,7 +590,7 @@ constexpr int kAedMax = 96;
 
 struct AedCtl {
     int nd;
-    double beta, tau;
+    double beta, tau, hbeta;
 };
 
 __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, int nw, int spike_valid, int maxits,
@@ -602,7 +602,7 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
     __shared__ double sp[kAedMax];
     __shared__ int bs[kAedMax];           // Schur block size ending at each row (1 or 2)
     __shared__ AedCtl c;
-    const int tid = threadIdx.x, nt = 64;
+    const int tid = threadIdx.x, nt = 64;   // one wave
     auto T = [&](int i, int j) -> double& { return t[i + j * LD]; };
     auto V = [&](int i, int j) -> double& { return v[i + j * LD]; };
     for (int e = tid; e < nw * nw; e += nt) {
@@ -613,12 +613,16 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
     const double spike = (spike_valid && kw > 0) ? H[kw + (int64_t)(kw - 1) * n] : 0.0;
     __syncthreads();
     const double eps = 2.220446049250313e-16;
-    int fail, total, maxsw;
+    int fail = 0, total = 0, maxsw = 0;
+    const long long tA = wall_clock64();
     // ---------------- phase A: real Schur form with V
     int steps = 0;
-    if (nw <= 64) wave_hqr<true, 1>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
-    else wave_hqr<true, 2>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
+    if (tid < 64) {
+        if (nw <= 64) wave_hqr<true, 1>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
+        else wave_hqr<true, 2>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
+    }
     __syncthreads();
+    const long long tB = wall_clock64();
     // ---------------- phase B: spike test from the bottom
     if (tid == 0) {
         int nd = 0;
@@ -647,67 +651,82 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
     }
     __syncthreads();
     const int nd = c.nd, m = nw - nd;
+    const long long tC = wall_clock64();
     // ---------------- phase C: undeflated part + spike back to Hessenberg form
-    // apply P = I - tau hv hv^T (hv[0..len), hv[0] = 1) to rows/columns [o, o + len)
+    // apply P = I - tau hv hv^T (hv[0..len), hv[0] = 1) to rows/columns [o, o + len); the dot
+    // products run four independent FMA chains so that their LDS reads overlap (one wave: the
+    // step's cost is latency)
+    auto dot4 = [&](auto elem, int len) -> double {
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int i = 0;
+        for (; i + 4 <= len; i += 4) {
+            s0 = __builtin_fma(hv[i], elem(i), s0);
+            s1 = __builtin_fma(hv[i + 1], elem(i + 1), s1);
+            s2 = __builtin_fma(hv[i + 2], elem(i + 2), s2);
+            s3 = __builtin_fma(hv[i + 3], elem(i + 3), s3);
+        }
+        for (; i < len; ++i) s0 = __builtin_fma(hv[i], elem(i), s0);
+        return (s0 + s1) + (s2 + s3);
+    };
     auto reflect = [&](int o, int len, int jlo) {
         const double tau = c.tau;
         for (int j = jlo + tid; j < nw; j += nt) {                       // left: T[o:o+len, jlo:nw]
-            double w = 0.0;
-            for (int i = 0; i < len; ++i) w += hv[i] * T(o + i, j);
-            w *= tau;
-            for (int i = 0; i < len; ++i) T(o + i, j) -= w * hv[i];
+            const double w = tau * dot4([&](int i) { return T(o + i, j); }, len);
+            for (int i = 0; i < len; ++i) T(o + i, j) = __builtin_fma(-w, hv[i], T(o + i, j));
         }
         __syncthreads();
-        for (int i = tid; i < m; i += nt) {                              // right: T[0:m, o:o+len]
-            double w = 0.0;
-            for (int jj = 0; jj < len; ++jj) w += T(i, o + jj) * hv[jj];
-            w *= tau;
-            for (int jj = 0; jj < len; ++jj) T(i, o + jj) -= w * hv[jj];
-        }
-        for (int i = tid; i < nw; i += nt) {                             // V[:, o:o+len]
-            double w = 0.0;
-            for (int jj = 0; jj < len; ++jj) w += V(i, o + jj) * hv[jj];
-            w *= tau;
-            for (int jj = 0; jj < len; ++jj) V(i, o + jj) -= w * hv[jj];
+        for (int i = tid; i < nw; i += nt) {                             // right: T[0:m, o:o+len], V[:, o:o+len]
+            const double wv = tau * dot4([&](int jj) { return V(i, o + jj); }, len);
+            if (i < m) {
+                const double w = tau * dot4([&](int jj) { return T(i, o + jj); }, len);
+                for (int jj = 0; jj < len; ++jj) T(i, o + jj) = __builtin_fma(-w, hv[jj], T(i, o + jj));
+            }
+            for (int jj = 0; jj < len; ++jj) V(i, o + jj) = __builtin_fma(-wv, hv[jj], V(i, o + jj));
         }
         __syncthreads();
     };
-    // Householder vector of x[0..len) (thread 0): hv[0] = 1, c.tau, returns beta
+    // Householder vector of x[0..len) by the whole wave: hv[0] = 1, c.tau; returns beta (every lane)
     auto house = [&](const double* x, int len) -> double {
-        const double alpha = x[0];
-        double xn = 0.0;
-        for (int i = 1; i < len; ++i) xn += x[i] * x[i];
-        xn = sqrt(xn);
-        hv[0] = 1.0;
-        if (xn == 0.0) {
-            c.tau = 0.0;
-            for (int i = 1; i < len; ++i) hv[i] = 0.0;
-            return alpha;
+        if (tid < 64) {
+            const double alpha = x[0];
+            double part = 0.0;
+            for (int i = 1 + tid; i < len; i += 64) part = __builtin_fma(x[i], x[i], part);
+            const double xn = sqrt(wave_sum(part));
+            double beta = alpha, sc = 0.0, tau = 0.0;
+            if (xn != 0.0) {
+                beta = -(alpha >= 0 ? 1.0 : -1.0) * sqrt(alpha * alpha + xn * xn);
+                tau = (beta - alpha) / beta;
+                sc = 1.0 / (alpha - beta);
+            }
+            EIGSOL_LDS_ORDER();
+            for (int i = 1 + tid; i < len; i += 64) hv[i] = x[i] * sc;
+            if (tid == 0) {
+                hv[0] = 1.0;
+                c.tau = tau;
+                c.hbeta = beta;
+            }
         }
-        const double beta = -(alpha >= 0 ? 1.0 : -1.0) * sqrt(alpha * alpha + xn * xn);
-        c.tau = (beta - alpha) / beta;
-        const double sc = 1.0 / (alpha - beta);
-        for (int i = 1; i < len; ++i) hv[i] = x[i] * sc;
-        return beta;
+        __syncthreads();
+        return c.hbeta;
     };
     if (nd > 0 && m > 0) {
-        if (tid == 0) {
-            for (int i = 0; i < m; ++i) sp[i] = spike * V(0, i);
-            c.tau = 0.0;
-            c.beta = m > 1 ? house(sp, m) : sp[0];
-        }
+        for (int i = tid; i < m; i += nt) sp[i] = spike * V(0, i);
+        if (tid == 0) c.tau = 0.0;
+        __syncthreads();
+        const double b0 = m > 1 ? house(sp, m) : sp[0];
+        if (tid == 0) c.beta = b0;
         __syncthreads();
         if (m > 1 && c.tau != 0.0) reflect(0, m, 0);
         for (int col = 0; col + 2 < m; ++col) {
-            if (tid == 0) {
-                const double b = house(&T(col + 1, col), m - col - 1);
-                T(col + 1, col) = b;
-                for (int i = col + 2; i < m; ++i) T(i, col) = 0.0;
-            }
+            const double b = house(&T(col + 1, col), m - col - 1);
+            __syncthreads();   // every wave has read beta before the next house overwrites it
+            if (tid == 0) T(col + 1, col) = b;
+            for (int i = col + 2 + tid; i < m; i += nt) T(i, col) = 0.0;
             __syncthreads();
             if (c.tau != 0.0) reflect(col + 1, m - col - 1, col + 1);
         }
     }
+    const long long tD = wall_clock64();
     // ---------------- phase D: write back (only when something deflated)
     if (nd > 0) {
         for (int e = tid; e < nw * nw; e += nt) {
@@ -723,6 +742,9 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
         info[2] = total;
         info[3] = m;
         info[4] = steps;
+        info[5] = (int)(tB - tA);   // wall-clock ticks (100 MHz) of phases A, B, C
+        info[6] = (int)(tC - tB);
+        info[7] = (int)(tD - tC);
     }
 }
 
@@ -790,7 +812,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         const char* e = std::getenv("EIGSOL_QR_NB");
         return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : 24;
     }();
-    long long st_steps = 0, st_aed_steps = 0;
+    long long st_steps = 0, st_aed_steps = 0, st_aed_ph[3] = {0, 0, 0};
     static const int aed_win = [] {
         const char* e = std::getenv("EIGSOL_QR_AED");   // AED window (0: off)
         return e ? std::max(0, std::min(dev::kAedMax, std::atoi(e))) : kAedDefault;
@@ -841,7 +863,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             const int kw = ihi - nw + 1;
             hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(64), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60, dwr, dwi,
                                dU, dinfo);
-            int info[5];
+            int info[8];
             std::vector<double> awr(nw), awi(nw);
             if (hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipMemcpyAsync(awr.data(), dwr + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -852,6 +874,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             }
             ++st_aed;
             st_aed_steps += info[4];
+            st_aed_ph[0] += info[5]; st_aed_ph[1] += info[6]; st_aed_ph[2] += info[7];
             if (!info[0]) {
                 const int nd = info[1], m = info[3];
                 if (nd > 0) {
@@ -1014,9 +1037,9 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     }
     if (stats)
         std::fprintf(stderr, "francis: n=%lld sweeps=%d windows=%d steps=%lld small_blocks=%d small_rows=%d kSmall=%d "
-                     "aed=%d aed_deflated=%d aed_win=%d aed_steps=%lld\n",
+                     "aed=%d aed_deflated=%d aed_win=%d aed_steps=%lld aed_phase_ms=%.1f/%.1f/%.1f\n",
                      (long long)n, st_sweeps, st_windows, st_steps, st_small, st_small_rows, kSmall, st_aed, st_aed_defl,
-                     aed_win, st_aed_steps);
+                     aed_win, st_aed_steps, st_aed_ph[0] * 1e-5, st_aed_ph[1] * 1e-5, st_aed_ph[2] * 1e-5);
     for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo}) (void)hipFree(p);
     // iterations reported: sweeps spent on the slowest deflation (>= 1, the final check), so that
     // iterations <= maxIterations exactly when the iteration converged
