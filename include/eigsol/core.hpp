@@ -40,6 +40,23 @@ inline constexpr bool ScalarConcept = std::is_floating_point_v<S> || is_complex_
 template <typename S>
 inline constexpr bool DeviceScalar = std::is_same_v<S, double> || std::is_same_v<S, std::complex<double>>;
 
+// float and std::complex<float> run on the same kernels: the matrix, start vector and shift are
+// promoted to double on the host and the results rounded back (a deliberate deviation: the
+// arithmetic is fp64, at least as accurate as the reference's single precision; convergence is
+// tested in fp64 at the requested tolerance).  long double has no device path (no 80-bit on the GPU).
+template <typename S>
+inline constexpr bool PromotedScalar = std::is_same_v<S, float> || std::is_same_v<S, std::complex<float>>;
+template <typename S>
+inline constexpr bool DeviceCapable = DeviceScalar<S> || PromotedScalar<S>;
+template <typename S>
+struct device_scalar { using type = S; };
+template <>
+struct device_scalar<float> { using type = double; };
+template <>
+struct device_scalar<std::complex<float>> { using type = std::complex<double>; };
+template <typename S>
+using device_scalar_t = typename device_scalar<S>::type;
+
 template <typename S>
 struct real_of { using type = S; };
 template <typename R>

@@ -91,16 +91,29 @@ public:
     std::int64_t cols() const { return visit([](const auto& m) { return m.cols(); }); }
 
     // Device mirror (created on first use by the solvers).
+    // float / complex<float> storage is uploaded promoted to double (device_scalar_t).
     template <typename S>
     const detail::DeviceMatrix& device() const {
+        using D = device_scalar_t<S>;
         if (!dev_) {
             if (dense_) {
                 const auto& d = cast<DenseMatrix<S>>();
-                dev_ = detail::DeviceMatrix::dense(detail::dtype_of<S>(), d.rows(), d.cols(), d.data());
+                if constexpr (std::is_same_v<D, S>) {
+                    dev_ = detail::DeviceMatrix::dense(detail::dtype_of<D>(), d.rows(), d.cols(), d.data());
+                } else {
+                    std::vector<D> w(d.data(), d.data() + d.size());
+                    dev_ = detail::DeviceMatrix::dense(detail::dtype_of<D>(), d.rows(), d.cols(), w.data());
+                }
             } else {
                 const auto& s = cast<SparseMatrix<S>>();
-                dev_ = detail::DeviceMatrix::csc(detail::dtype_of<S>(), s.rows(), s.cols(), s.nonZeros(),
-                                                 s.outerIndexPtr(), s.innerIndexPtr(), s.valuePtr());
+                if constexpr (std::is_same_v<D, S>) {
+                    dev_ = detail::DeviceMatrix::csc(detail::dtype_of<D>(), s.rows(), s.cols(), s.nonZeros(),
+                                                     s.outerIndexPtr(), s.innerIndexPtr(), s.valuePtr());
+                } else {
+                    std::vector<D> w(s.valuePtr(), s.valuePtr() + s.nonZeros());
+                    dev_ = detail::DeviceMatrix::csc(detail::dtype_of<D>(), s.rows(), s.cols(), s.nonZeros(),
+                                                     s.outerIndexPtr(), s.innerIndexPtr(), w.data());
+                }
             }
         }
         return *dev_;
@@ -124,6 +137,13 @@ private:
         if (t == typeid(SparseMatrix<std::complex<double>>)) return f(cast<SparseMatrix<std::complex<double>>>());
         if (t == typeid(DenseMatrix<float>)) return f(cast<DenseMatrix<float>>());
         if (t == typeid(SparseMatrix<float>)) return f(cast<SparseMatrix<float>>());
+        if (t == typeid(DenseMatrix<std::complex<float>>)) return f(cast<DenseMatrix<std::complex<float>>>());
+        if (t == typeid(SparseMatrix<std::complex<float>>)) return f(cast<SparseMatrix<std::complex<float>>>());
+        if (t == typeid(DenseMatrix<long double>)) return f(cast<DenseMatrix<long double>>());
+        if (t == typeid(SparseMatrix<long double>)) return f(cast<SparseMatrix<long double>>());
+        if (t == typeid(DenseMatrix<std::complex<long double>>)) return f(cast<DenseMatrix<std::complex<long double>>>());
+        if (t == typeid(SparseMatrix<std::complex<long double>>))
+            return f(cast<SparseMatrix<std::complex<long double>>>());
         return -1;
     }
 

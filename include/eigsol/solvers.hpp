@@ -8,6 +8,9 @@
 //   qr_decompose<S> / _dense       src/qr_method/qr_decompose.hpp:25-132
 //   qr_eigenvalues<S> / _dense     src/qr_method/qr_eigenvalues.hpp:40-147
 //
+// Scalars: double and std::complex<double> natively; float and std::complex<float> promoted to fp64
+// (core.hpp, PromotedScalar); long double throws "scalar type not supported by the device path".
+//
 // Start vector: the reference draws x0 with Eigen's Vector::Random (std::rand, not reproducible
 // across Eigen versions).  Here x0 comes from a documented generator
 // (std::mt19937_64 seeded with EigSol::random_seed(), U(-1, 1) per real/imaginary component);
@@ -66,9 +69,26 @@ inline eigsol_solver_options copts(const SolverOptions& o) {
 
 template <typename S>
 void require_device_scalar(const char* who) {
-    if constexpr (!DeviceScalar<S>)
+    if constexpr (!DeviceCapable<S>)
         throw std::runtime_error(std::string(who) + ": scalar type not supported by the device path "
-                                                    "(double, std::complex<double>)");
+                                                    "(double, std::complex<double>, float, std::complex<float>)");
+}
+
+// element-wise conversions between a scalar type and its device (fp64) type
+template <typename T, typename U>
+Vector<T> convert_vec(const Vector<U>& v) {
+    if constexpr (std::is_same_v<T, U>) return v;
+    else {
+        Vector<T> w(v.size());
+        for (std::size_t i = 0; i < v.size(); ++i) w(i) = static_cast<T>(v(i));
+        return w;
+    }
+}
+template <typename T, typename U>
+DenseMatrix<T> convert_dense(const DenseMatrix<U>& a) {
+    DenseMatrix<T> b(a.rows(), a.cols());
+    for (std::int64_t i = 0; i < a.size(); ++i) b.data()[i] = static_cast<T>(a.data()[i]);
+    return b;
 }
 
 template <typename S>
@@ -79,25 +99,28 @@ EigenResult<S> power_like(const Matrix& M, const SolverOptions& opts, const Vect
     if (r != c) throw std::runtime_error(std::string(who) + ": matrix must be square");
     if (r == 0) throw std::runtime_error(std::string(who) + ": matrix has zero size");
     require_device_scalar<S>(who);
-    if constexpr (DeviceScalar<S>) {
-        Vector<S> xs = x0 ? *x0 : random_vector<S>(static_cast<std::size_t>(r));
-        if (xs.size() != static_cast<std::size_t>(r))
+    if constexpr (DeviceCapable<S>) {
+        using D = device_scalar_t<S>;
+        Vector<S> xs0 = x0 ? *x0 : random_vector<S>(static_cast<std::size_t>(r));
+        if (xs0.size() != static_cast<std::size_t>(r))
             throw std::runtime_error(std::string(who) + ": start vector size mismatch");
+        const Vector<D> xs = convert_vec<D>(xs0);
         const detail::DeviceMatrix& d = M.device<S>();
         const eigsol_solver_options o = copts(opts);
-        S lam{};
-        Vector<S> x(static_cast<std::size_t>(r));
+        D lam{};
+        const D sh = shift ? static_cast<D>(*shift) : D{};
+        Vector<D> x(static_cast<std::size_t>(r));
         std::int32_t it = 0, conv = 0;
         int st;
         if (shift) {
-            st = M.isDense() ? eigsol_shifted_inverse_dense(d.dense(), shift, &o, xs.data(), &lam, x.data(), &it, &conv)
-                             : eigsol_shifted_inverse_csr(d.csr(), shift, &o, xs.data(), &lam, x.data(), &it, &conv);
+            st = M.isDense() ? eigsol_shifted_inverse_dense(d.dense(), &sh, &o, xs.data(), &lam, x.data(), &it, &conv)
+                             : eigsol_shifted_inverse_csr(d.csr(), &sh, &o, xs.data(), &lam, x.data(), &it, &conv);
         } else {
             st = M.isDense() ? eigsol_power_dense(d.dense(), &o, xs.data(), &lam, x.data(), &it, &conv)
                              : eigsol_power_csr(d.csr(), &o, xs.data(), &lam, x.data(), &it, &conv);
         }
         check(st, who);
-        return EigenResult<S>(lam, x, it, conv != 0);
+        return EigenResult<S>(static_cast<S>(lam), convert_vec<S>(x), it, conv != 0);
     }
     return {};
 }
@@ -140,13 +163,18 @@ Vector<S> solve_shifted(const Matrix& A, const S shift, const Vector<S>& b) {
         throw std::runtime_error(std::string("solve_shifted: size mismatch between A and b (") + kind + " case)");
     detail::require_device_scalar<S>("solve_shifted");
     Vector<S> x(b.size());
-    if constexpr (DeviceScalar<S>) {
+    if constexpr (DeviceCapable<S>) {
+        using D = device_scalar_t<S>;
         if (b.size() == 0) return x;
         const detail::DeviceMatrix& d = A.device<S>();
         const std::int64_t n = static_cast<std::int64_t>(b.size());
-        detail::check(A.isDense() ? eigsol_solve_shifted_dense(d.dense(), &shift, b.data(), n, x.data())
-                                  : eigsol_solve_shifted_csr(d.csr(), &shift, b.data(), n, x.data()),
+        const D sh = static_cast<D>(shift);
+        const Vector<D> bd = detail::convert_vec<D>(b);
+        Vector<D> xd(b.size());
+        detail::check(A.isDense() ? eigsol_solve_shifted_dense(d.dense(), &sh, bd.data(), n, xd.data())
+                                  : eigsol_solve_shifted_csr(d.csr(), &sh, bd.data(), n, xd.data()),
                       "solve_shifted");
+        x = detail::convert_vec<S>(xd);
     }
     return x;
 }
@@ -156,6 +184,8 @@ template <typename S>
 DenseMatrix<S> to_hessenberg_dense(const DenseMatrix<S>& A) {
     detail::dense_square_check(A, "to_hessenberg_dense");
     detail::require_device_scalar<S>("to_hessenberg_dense");
+    if constexpr (PromotedScalar<S>)
+        return detail::convert_dense<S>(to_hessenberg_dense(detail::convert_dense<device_scalar_t<S>>(A)));
     DenseMatrix<S> H(A.rows(), A.cols());
     if constexpr (DeviceScalar<S>) {
         if (A.rows() > 0)
@@ -176,6 +206,14 @@ template <typename S>
 void qr_decompose_dense(const DenseMatrix<S>& A, DenseMatrix<S>& Q, DenseMatrix<S>& R) {
     if (A.rows() == 0 || A.cols() == 0) throw std::runtime_error("qr_decompose_dense: empty matrix");
     detail::require_device_scalar<S>("qr_decompose_dense");
+    if constexpr (PromotedScalar<S>) {
+        using D = device_scalar_t<S>;
+        DenseMatrix<D> Qd, Rd;
+        qr_decompose_dense<D>(detail::convert_dense<D>(A), Qd, Rd);
+        Q = detail::convert_dense<S>(Qd);
+        R = detail::convert_dense<S>(Rd);
+        return;
+    }
     Q = DenseMatrix<S>(A.rows(), A.rows());
     R = DenseMatrix<S>(A.rows(), A.cols());
     if constexpr (DeviceScalar<S>)
@@ -200,6 +238,13 @@ QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& o
     const std::int64_t n = A.rows();
     if (n == 0) return QRResult<S>(Vector<S>(), 0, true);   // qr_eigenvalues.hpp:55-57
     detail::require_device_scalar<S>("qr_eigenvalues_dense");
+    if constexpr (PromotedScalar<S>) {
+        using D = device_scalar_t<S>;
+        const QRResult<D> rd = qr_eigenvalues_dense<D>(detail::convert_dense<D>(A), opts, variant);
+        QRResult<S> rs(detail::convert_vec<S>(rd.eigenvalues), rd.iterations, rd.converged);
+        rs.eigenvalues_complex = rd.eigenvalues_complex;
+        return rs;
+    }
     QRResult<S> res;
     if constexpr (DeviceScalar<S>) {
         Vector<S> ev(static_cast<std::size_t>(n));

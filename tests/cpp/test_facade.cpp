@@ -317,6 +317,51 @@ TEST(QREigenvaluesDenseTest, Real2x2BothVariantsAndComplex) {
     EXPECT_NEAR(std::abs(std::abs(rr.eigenvalues_complex[0].imag()) - 1.0), 0.0, 1e-12);
 }
 
+// ---------------------------------------------------------------- single precision (promoted)
+// ScalarConcept admits float and std::complex<float> (types.hpp:28-30): they run on the fp64
+// kernels (promoted on the host, rounded back); long double has no device path.
+TEST(SinglePrecision, PowerShiftedSolveAndQR) {
+    EigSol::Matrix::Dense<float> A(2, 2);
+    A << 2.0f, 0.0f, 0.0f, 1.0f;
+    EigSol::Matrix M(A);
+    auto r = EigSol::powerMethod<float>(M, EigSol::SolverOptions{});
+    EXPECT_TRUE(r.converged);
+    EXPECT_NEAR(r.eigenvalue, 2.0f, 1e-6f);
+    EXPECT_EQ(r.eigenvector.size(), 2u);
+    EigSol::ShiftedSolverOptions<float> so;
+    so.shift = 0.9f;
+    auto rs = EigSol::shiftedInversePowerMethod<float>(M, so);
+    EXPECT_NEAR(rs.eigenvalue, 1.0f, 1e-6f);
+    EigSol::Vector<float> b(2);
+    b << 4.0f, 2.0f;
+    auto x = EigSol::solve_shifted<float>(M, 0.5f, b);   // (A - 0.5 I) x = b
+    EXPECT_NEAR(x(0), 4.0f / 1.5f, 1e-6f);
+    EXPECT_NEAR(x(1), 4.0f, 1e-6f);
+    EigSol::Matrix::Dense<float> B(2, 2);
+    B << 2.0f, 1.0f, 1.0f, 2.0f;
+    auto q = EigSol::qr_eigenvalues<float>(EigSol::Matrix(B), EigSol::SolverOptions{});
+    EXPECT_TRUE(q.converged);
+    std::array<float, 2> ev{q.eigenvalues(0), q.eigenvalues(1)};
+    std::sort(ev.begin(), ev.end());
+    EXPECT_NEAR(ev[0], 1.0f, 1e-5f);
+    EXPECT_NEAR(ev[1], 3.0f, 1e-5f);
+    auto H = EigSol::to_hessenberg<float>(EigSol::Matrix(B));
+    EXPECT_EQ(H.rows(), 2);
+    EigSol::Matrix::Sparse<std::complex<float>> Sc(2, 2);
+    Sc.insert(0, 0) = std::complex<float>(1.0f, 3.0f);
+    Sc.insert(0, 1) = std::complex<float>(3.0f, 5.0f);
+    Sc.insert(1, 1) = std::complex<float>(5.0f, -1.0f);
+    EigSol::Matrix Ms(Sc);
+    auto rc = EigSol::powerMethod<std::complex<float>>(Ms, EigSol::SolverOptions{});
+    EXPECT_NEAR(std::abs(rc.eigenvalue - std::complex<float>(5.0f, -1.0f)), 0.0f, 1e-4f);
+    EXPECT_EQ(Ms.rows(), 2);
+    EigSol::Matrix::Dense<long double> L(1, 1);
+    L << 1.0L;
+    EigSol::Matrix Ml(L);
+    EXPECT_EQ(Ml.rows(), 1);
+    EXPECT_THROW(EigSol::powerMethod<long double>(Ml, EigSol::SolverOptions{}), std::runtime_error);
+}
+
 int main() {
     for (auto& [name, fn] : registry()) {
         const int before = g_fail;
