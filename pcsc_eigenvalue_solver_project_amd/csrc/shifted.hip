@@ -57,6 +57,11 @@ struct ShiftFactor {
     int32_t* perm = nullptr;      // P b: b_perm[i] = b[perm[i]]
     int32_t* zero_pivot = nullptr;
     size_t lds_bytes = 0;
+    // dense, multi-CU substitution (large n): epoch flags per block row, forward results
+    int dense_multi = 0;
+    int32_t* flag_f = nullptr;
+    int32_t* flag_b = nullptr;
+    void* zf = nullptr;
 };
 
 namespace dev {
@@ -480,6 +485,235 @@ __global__ __launch_bounds__(1024) void dense_lu_solve_kernel(DenseSolveArgs<S> 
     }
 }
 
+// ------------------------------------------------------------ multi-CU dense substitution
+// L z = P b (L unit lower), then U y = z, for large dense factors: block rows of kDB rows, one
+// persistent workgroup per resident slot taking block rows round-robin — all its forward rows in
+// increasing order, then all its backward rows in decreasing order.  A block row accumulates the
+// off-diagonal tiles L_rc z_c as the z_c it needs are published (epoch flags: no reset between
+// launches), solves its kDB x kDB triangle in LDS, and publishes.  Forward rows wait only on
+// smaller forward rows and backward rows only on forward rows and larger backward rows, and
+// every workgroup finishes its forward list first, so with all workgroups resident the
+// dependency graph always has a runnable item (bounded spins + an error word besides).
+constexpr int kDB = 64;
+__device__ __forceinline__ double readlane_s(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ cplx readlane_s(cplx v, int src) { return cplx{readlane_s(v.re, src), readlane_s(v.im, src)}; }
+template <class S>
+struct DenseTriArgs {
+    const S* lu;
+    const int32_t* perm;
+    int64_t n;
+    int32_t nblk;
+    int32_t epoch;
+    int32_t* flag_f;     // [nblk] epoch when z of the block row is published
+    int32_t* flag_b;     // [nblk] epoch when y of the block row is published
+    S* z;                // forward results (n)
+    const S* b_plain;
+    S* y_plain;
+    S* buf0;
+    S* buf1;
+    PowerCtl* ctl;
+    const part4* rank_part;
+    part4* my_part;
+    part4* wave_part;    // [grid] workgroup partials
+    uint32_t* work;
+    int32_t* err;
+    S* trace;
+    double sig_re, sig_im;
+};
+
+__device__ __forceinline__ void wait_flag(const int32_t* f, int32_t epoch, int32_t* err) {
+    int spins = 0;
+    while (__hip_atomic_load(const_cast<int32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        // back off: waves far ahead of the chain leave the memory system to the producers
+        if (spins < 4) __builtin_amdgcn_s_sleep(2);
+        else if (spins < 16) __builtin_amdgcn_s_sleep(8);
+        else __builtin_amdgcn_s_sleep(32);
+        if (++spins > (1 << 22)) { atomicOr(err, 1); break; }
+    }
+}
+
+template <class S, bool kIter>
+__global__ __launch_bounds__(256) void dense_trsv_kernel(DenseTriArgs<S> a, int parity) {
+    __shared__ S tri[kDB * (kDB + 1)];     // the block row's diagonal tile (odd pitch)
+    __shared__ S part[4][kDB];             // per-wave partial sums of the off-diagonal tiles
+    __shared__ S zsh[4][kDB];              // per-wave copy of the block of z / y a tile multiplies
+    __shared__ S vec[kDB];
+    __shared__ Prologue pro;
+    __shared__ int s_last;
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kIter) {
+        shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // epoch flags: nothing to reset
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.b_plain;
+        yout = a.y_plain;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t n = a.n;
+    const int G = gridDim.x;
+    double n2 = 0.0, pr = 0.0, pi = 0.0;
+    for (int phase = 0; phase < 2; ++phase) {
+        const bool fwd = phase == 0;
+        // this workgroup's block rows: r = blockIdx.x + k G, forward increasing, backward decreasing
+        const int cnt = a.nblk > (int)blockIdx.x ? (a.nblk - 1 - (int)blockIdx.x) / G + 1 : 0;
+        for (int q = 0; q < cnt; ++q) {
+            const int r = fwd ? (int)blockIdx.x + q * G : (int)blockIdx.x + (cnt - 1 - q) * G;
+            const int64_t r0 = (int64_t)r * kDB;
+            const int rn = (int)min<int64_t>(kDB, n - r0);
+            // diagonal tile into LDS (column-major, pitch kDB + 1): all 16 loads of a thread first
+            {
+                constexpr int kPer = kDB * kDB / 256;
+                S tv[kPer];
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) {
+                    const int e = tid + 256 * q, i = e % kDB, j = e / kDB;
+                    tv[q] = a.lu[(r0 + min(i, rn - 1)) + (r0 + min(j, rn - 1)) * n];
+                }
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) {
+                    const int e = tid + 256 * q, i = e % kDB, j = e / kDB;
+                    tri[i + j * (kDB + 1)] = (i < rn && j < rn) ? tv[q] : s_zero<S>();
+                }
+            }
+            // off-diagonal tiles: forward c < r (L), backward c > r (U); wave wv takes every 4th
+            S acc = s_zero<S>();
+            const int c_beg = fwd ? 0 : r + 1, c_end = fwd ? r : a.nblk;
+            for (int c = c_beg + wv; c < c_end; c += 4) {
+                wait_flag(fwd ? a.flag_f + c : a.flag_b + c, a.epoch, a.err);
+                const int64_t c0 = (int64_t)c * kDB;
+                const int cn = (int)min<int64_t>(kDB, n - c0);
+                const S* src = fwd ? a.z : yout;
+                // the published block of z (or y): one coherent load per lane, broadcast from LDS
+                zsh[wv][lane] = lane < cn ? ld_coh(src + c0 + lane) : s_zero<S>();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const S* tile = a.lu + c0 * n + r0 + min(lane, max(rn - 1, 0));
+                if (cn == kDB) {
+                    // 16 tile columns in flight per lane before the FMAs consume them
+#pragma unroll
+                    for (int j0 = 0; j0 < kDB; j0 += 16) {
+                        S tv[16];
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) tv[u] = tile[(int64_t)(j0 + u) * n];
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) acc = add(acc, mul(tv[u], zsh[wv][j0 + u]));
+                    }
+                } else {
+                    for (int j = 0; j < cn; ++j) acc = add(acc, mul(tile[(int64_t)j * n], zsh[wv][j]));
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
+            part[wv][lane] = lane < rn ? acc : s_zero<S>();
+            __syncthreads();
+            if (wv == 0) {
+                // right-hand side of the block row
+                S rhs = s_zero<S>();
+                if (lane < rn) {
+                    if (fwd) {
+                        rhs = xin[a.perm[r0 + lane]];
+                        if constexpr (kIter) rhs = scale_in(rhs, nrm);
+                    } else {
+                        rhs = ld_coh(a.z + r0 + lane);   // published by this wave, read past L1
+                    }
+                    rhs = sub(rhs, add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane])));
+                }
+                vec[lane] = rhs;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // triangle: forward unit lower (column order), backward upper (reverse column order)
+                // the solved entry travels by v_readlane (wave-uniform j), the tile column from LDS
+                S v = vec[lane];
+                auto step = [&](const int j) {
+                    S zj;
+                    if (!fwd && lane == j) v = sdiv(v, tri[j + j * (kDB + 1)]);
+                    zj = readlane_s(v, j);
+                    const bool below = fwd ? (lane > j) : (lane < j);
+                    const S lij = tri[lane + j * (kDB + 1)];
+                    if (below) v = sub(v, mul(lij, zj));
+                };
+                if (rn == kDB) {
+                    if (fwd) {
+#pragma unroll
+                        for (int j = 0; j < kDB; ++j) step(j);
+                    } else {
+#pragma unroll
+                        for (int j = kDB - 1; j >= 0; --j) step(j);
+                    }
+                } else {
+                    for (int jj = 0; jj < rn; ++jj) step(fwd ? jj : rn - 1 - jj);
+                }
+                if (lane < rn) {
+                    if (fwd) {
+                        st_coh(a.z + r0 + lane, v);
+                    } else {
+                        const S yi = v;
+                        st_coh(yout + r0 + lane, yi);
+                        if constexpr (kIter) {
+                            S xi = xin[r0 + lane];
+                            xi = scale_in(xi, nrm);
+                            n2 += sq_abs(yi);
+                            acc_dot(pr, pi, xi, yi);
+                        }
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store(fwd ? a.flag_f + r : a.flag_b + r, a.epoch, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+        }
+    }
+    // workgroup partials (wave 0 holds them), then the last arriver sums them in workgroup order
+    if (wv == 0) {
+        n2 = wave_sum(n2);
+        pr = wave_sum(pr);
+        pi = wave_sum(pi);
+        if (lane == 0) {
+            part4* p = a.wave_part + blockIdx.x;
+            st_agent(&p->a, n2);
+            st_agent(&p->b, pr);
+            st_agent(&p->c, pi);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(&a.work[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (tk == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if constexpr (kIter) {
+        if (tid == 0) {
+            double sa = 0.0, sb = 0.0, sc = 0.0;
+            for (int i = 0; i < G; ++i) {
+                sa += ld_agent(&a.wave_part[i].a);
+                sb += ld_agent(&a.wave_part[i].b);
+                sc += ld_agent(&a.wave_part[i].c);
+            }
+            a.my_part->a = sa;
+            a.my_part->b = sb;
+            a.my_part->c = sc;
+            a.my_part->d = 0.0;
+        }
+    }
+    if (tid == 0) __hip_atomic_store(&a.work[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // CSR (device) -> dense column-major (device), for small non-triangular sparse matrices
 template <class S>
 __global__ void densify_kernel(const int32_t* rowptr, const int32_t* col, const S* val, int64_t n,
@@ -512,13 +746,20 @@ static void shift_free(ShiftFactor* f) {
     hipStreamSynchronize(f->ctx->stream);
     for (void* p : {(void*)f->order, (void*)f->pptr, (void*)f->pcol, f->pval, f->ppiv, f->z[0], f->z[1],
                     (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
-                    (void*)f->zero_pivot})
+                    (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf})
         if (p) hipFree(p);
     ctx_release(f->ctx);
     delete f;
 }
 
 void shift_factor_free(ShiftFactor* f) { shift_free(f); }
+
+template <class S>
+static int64_t kDenseSingleMax() {
+    const char* e = std::getenv("EIGSOL_DENSE_TRSV_SINGLE_MAX");   // A/B: substitution crossover
+    if (e) return std::atoll(e);
+    return 512;
+}
 
 template <class S>
 static int dense_lu_factor(ShiftFactor* f, bool from_sparse) {
@@ -573,16 +814,35 @@ static int dense_lu_factor(ShiftFactor* f, bool from_sparse) {
     EIGSOL_HIP(hipStreamSynchronize(st));
     f->kind = 1;
     f->lds_bytes = (size_t)n * sizeof(S);
+    if (n > kDenseSingleMax<S>()) {
+        // multi-CU substitution: one persistent workgroup per CU at most (all resident)
+        const int nblk = (int)((n + dev::kDB - 1) / dev::kDB);
+        f->dense_multi = 1;
+        f->grid = std::max(1, std::min(nblk, 32));   // 16384^2 f64: 32 WGs 32 ms, 64: 37 ms, 256: 48 ms per solve
+        if (const char* e = std::getenv("EIGSOL_DENSE_TRSV_GRID")) f->grid = std::max(1, std::min(nblk, std::atoi(e)));
+        f->nchunks = nblk;
+        EIGSOL_HIP(hipMalloc(&f->flag_f, sizeof(int32_t) * nblk));
+        EIGSOL_HIP(hipMalloc(&f->flag_b, sizeof(int32_t) * nblk));
+        EIGSOL_HIP(hipMalloc(&f->zf, sizeof(S) * n));
+        EIGSOL_HIP(hipMalloc(&f->work, 64));
+        EIGSOL_HIP(hipMalloc(&f->err, 64));
+        EIGSOL_HIP(hipMalloc(&f->wave_part, sizeof(dev::part4) * f->grid));
+        EIGSOL_HIP(hipMemsetAsync(f->flag_f, 0, sizeof(int32_t) * nblk, st));
+        EIGSOL_HIP(hipMemsetAsync(f->flag_b, 0, sizeof(int32_t) * nblk, st));
+        EIGSOL_HIP(hipMemsetAsync(f->work, 0, 64, st));
+        EIGSOL_HIP(hipMemsetAsync(f->err, 0, 64, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+    }
     return EIGSOL_OK;
 }
 
-static constexpr size_t kDenseSolveLds = 144 * 1024;   // vector of the single-CU substitution
-
+// dense factors up to this order (vector in one CU's LDS) use the single-workgroup substitution,
+// larger ones the multi-CU block-row substitution (dense_trsv_kernel); their size is bounded by HBM
 static int dense_limits(int dtype, int64_t n, const char* who) {
-    if ((size_t)n * scalar_bytes(dtype) > kDenseSolveLds)
-        return fail(EIGSOL_E_UNSUPPORTED, std::string(who) + ": dense factor of order " +
-                                              std::to_string(n) + " exceeds the single-CU LDS "
-                                              "substitution (n * sizeof(S) <= 144 KiB)");
+    const double bytes = (double)n * (double)n * (double)scalar_bytes(dtype);
+    if (n > INT32_MAX / 2 || bytes > 0.9 * 288e9)
+        return fail(EIGSOL_E_UNSUPPORTED, std::string(who) + ": dense factor of order " + std::to_string(n) +
+                                              " does not fit the device memory");
     return EIGSOL_OK;
 }
 
@@ -781,10 +1041,10 @@ int shift_factor_csr(eigsol_csr* A, const void* sigma, ShiftFactor** out) {
                                    : factor_csr_t<double>(A, s[0], 0.0, out);
 }
 
-int shift_grid(const ShiftFactor* f) { return f->kind == 0 ? f->grid : 1; }
+int shift_grid(const ShiftFactor* f) { return (f->kind == 0 || f->dense_multi) ? f->grid : 1; }
 
 int shift_error(ShiftFactor* f) {
-    if (f->kind != 0) return EIGSOL_OK;
+    if (f->kind != 0 && !f->dense_multi) return EIGSOL_OK;
     int32_t e = 0;
     EIGSOL_HIP(hipMemcpyAsync(&e, f->err, 4, hipMemcpyDeviceToHost, f->ctx->stream));
     EIGSOL_HIP(hipStreamSynchronize(f->ctx->stream));
@@ -823,6 +1083,31 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.sig_im = f->sig_im;
         if (iter) hipLaunchKernelGGL((dev::sptrsv_kernel<S, true>), dim3(f->grid), dim3(dev::kThreads), 0, st, a, parity);
         else hipLaunchKernelGGL((dev::sptrsv_kernel<S, false>), dim3(f->grid), dim3(dev::kThreads), 0, st, a, parity);
+    } else if (f->dense_multi) {
+        dev::DenseTriArgs<S> a{};
+        a.lu = static_cast<const S*>(f->lu);
+        a.perm = f->perm;
+        a.n = f->n;
+        a.nblk = f->nchunks;
+        a.epoch = ++f->epoch;
+        a.flag_f = f->flag_f;
+        a.flag_b = f->flag_b;
+        a.z = static_cast<S*>(f->zf);
+        a.b_plain = static_cast<const S*>(b);
+        a.y_plain = static_cast<S*>(y);
+        a.buf0 = static_cast<S*>(buf0);
+        a.buf1 = static_cast<S*>(buf1);
+        a.ctl = ctl;
+        a.rank_part = static_cast<const dev::part4*>(rank_part);
+        a.my_part = static_cast<dev::part4*>(my_part);
+        a.wave_part = static_cast<dev::part4*>(f->wave_part);
+        a.work = f->work;
+        a.err = f->err;
+        a.trace = static_cast<S*>(trace);
+        a.sig_re = f->sig_re;
+        a.sig_im = f->sig_im;
+        if (iter) hipLaunchKernelGGL((dev::dense_trsv_kernel<S, true>), dim3(f->grid), dim3(256), 0, st, a, parity);
+        else hipLaunchKernelGGL((dev::dense_trsv_kernel<S, false>), dim3(f->grid), dim3(256), 0, st, a, parity);
     } else {
         dev::DenseSolveArgs<S> a{};
         a.lu = static_cast<const S*>(f->lu);

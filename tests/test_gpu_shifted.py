@@ -285,3 +285,43 @@ def test_dense_solve_shifted_blocked_lu(ctx, dtype):
     assert r <= 1e-12 * n * np.linalg.norm(M, 2) * np.linalg.norm(x), r
     xr = np.linalg.solve(M, b)
     assert np.linalg.norm(x - xr) <= (1e-13 * np.linalg.cond(M) + 1e-12) * np.linalg.norm(xr)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_dense_multi_cu_substitution_matches_single_cu(ctx, dtype, monkeypatch):
+    """Dense factors above 2048 rows use the multi-CU block-row substitution (epoch flags, one
+    persistent workgroup per CU): the shifted inverse iteration must reproduce the single-CU
+    substitution's result (EIGSOL_DENSE_TRSV_SINGLE_MAX forces it) to 1e-10, and solve_shifted
+    must be backward stable."""
+    rng = np.random.default_rng(21)
+    n = 3000
+    A = rng.standard_normal((n, n))
+    if dtype == np.complex128:
+        A = A + 1j * rng.standard_normal((n, n))
+    A = (A / np.sqrt(n) + np.diag(np.linspace(1.0, 4.0, n))).astype(dtype)
+    sigma = 2.501 if dtype == np.float64 else 2.501 + 0.01j
+    x0 = S.start_vector(n, dtype)
+    opts = E.ShiftedSolverOptions(300, 1e-12, sigma)
+    multi = E.shifted_inverse_power_method(E.DenseMatrix(ctx, A), opts, x0)
+    monkeypatch.setenv("EIGSOL_DENSE_TRSV_SINGLE_MAX", str(n))
+    single = E.shifted_inverse_power_method(E.DenseMatrix(ctx, A), opts, x0)
+    monkeypatch.delenv("EIGSOL_DENSE_TRSV_SINGLE_MAX")
+    assert multi.converged and single.converged
+    assert abs(multi.eigenvalue - single.eigenvalue) <= 1e-10 * (1 + abs(single.eigenvalue))
+    assert abs(multi.iterations - single.iterations) <= 1
+    assert abs(np.vdot(multi.eigenvector, single.eigenvector)) >= 1 - 1e-10
+    b = rng.standard_normal(n).astype(dtype)
+    x = E.solve_shifted(E.DenseMatrix(ctx, A), sigma, b)
+    M = A - sigma * np.eye(n)
+    assert np.linalg.norm(M @ x - b) <= 1e-12 * n * np.linalg.norm(M, 2) * np.linalg.norm(x)
+
+
+def test_dense_shifted_above_single_cu_limit(ctx):
+    """n = 20000 f64 (3.2 GB): beyond the former single-CU LDS limit (18432); residual check."""
+    rng = np.random.default_rng(5)
+    n = 20000
+    A = rng.standard_normal((n, n)) / np.sqrt(n) + np.eye(n) * 3.0
+    b = rng.standard_normal(n)
+    x = E.solve_shifted(E.DenseMatrix(ctx, A), 0.5, b)
+    r = A @ x - 0.5 * x - b
+    assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(b)
