@@ -487,6 +487,25 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
         // straight-line code on a single wave (its cost is instruction issue)
         auto step = [&](const int k, auto three_c) {
             constexpr bool three = decltype(three_c)::value;
+            // every load that does not depend on this step's reflector is issued first, so its LDS
+            // latency overlaps the reflector's sqrt / reciprocal chain: the left update's rows
+            // k..k+2 and (Schur) V's columns k..k+2 (neither is written before they are used)
+            double l0[NX], l1[NX], l2[NX], w0[NX], w1[NX], w2[NX];
+#pragma unroll
+            for (int x = 0; x < NX; ++x) {
+                const int j = k + lane + 64 * x, i = lane + 64 * x;
+                l0[x] = l1[x] = l2[x] = w0[x] = w1[x] = w2[x] = 0.0;
+                if (j < jend) {
+                    l0[x] = T(k, j);
+                    l1[x] = T(k + 1, j);
+                    if (three) l2[x] = T(k + 2, j);
+                }
+                if (kSchur && i < n) {
+                    w0[x] = V(i, k);
+                    w1[x] = V(i, k + 1);
+                    if (three) w2[x] = V(i, k + 2);
+                }
+            }
             double p = p0, q = q0, r = three ? r0 : 0.0, xk = 1.0;
             if (k != m) {
                 p = T(k, k - 1);
@@ -510,39 +529,36 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
             for (int x = 0; x < NX; ++x) {        // NX = ceil(n / 64): no loop control on the step's path
                 const int j = k + lane + 64 * x;
                 if (j < jend) {
-                    const double t0 = T(k, j), t1 = T(k + 1, j);
-                    double pp = __builtin_fma(bq, t1, t0);
+                    double pp = __builtin_fma(bq, l1[x], l0[x]);
                     if (three) {
-                        const double t2 = T(k + 2, j);
-                        pp = __builtin_fma(br, t2, pp);
-                        T(k + 2, j) = __builtin_fma(-pp, az, t2);
+                        pp = __builtin_fma(br, l2[x], pp);
+                        T(k + 2, j) = __builtin_fma(-pp, az, l2[x]);
                     }
-                    T(k + 1, j) = __builtin_fma(-pp, ay, t1);
-                    T(k, j) = __builtin_fma(-pp, ax, t0);
+                    T(k + 1, j) = __builtin_fma(-pp, ay, l1[x]);
+                    T(k, j) = __builtin_fma(-pp, ax, l0[x]);
                 }
             }
             EIGSOL_LDS_ORDER();
             const int imax = nn < k + 3 ? nn : k + 3;
-            // right update of T and (Schur) of V in one pass: both columns' loads issued together
+            // right update of T (rows through k+3 read after the left update's stores) and of V
 #pragma unroll
             for (int x = 0; x < NX; ++x) {
                 const int i = lane + 64 * x;
                 const int it = ibeg + i;
                 const bool ct = it <= imax, cv = kSchur && i < n;
-                double t0 = 0, t1 = 0, t2 = 0, v0 = 0, v1 = 0, v2 = 0;
+                double t0 = 0, t1 = 0, t2 = 0;
                 if (ct) { t0 = T(it, k); t1 = T(it, k + 1); if (three) t2 = T(it, k + 2); }
-                if (cv) { v0 = V(i, k); v1 = V(i, k + 1); if (three) v2 = V(i, k + 2); }
                 const double pt = three ? __builtin_fma(az, t2, __builtin_fma(ay, t1, ax * t0)) : __builtin_fma(ay, t1, ax * t0);
-                const double pv = three ? __builtin_fma(az, v2, __builtin_fma(ay, v1, ax * v0)) : __builtin_fma(ay, v1, ax * v0);
+                const double pv = three ? __builtin_fma(az, w2[x], __builtin_fma(ay, w1[x], ax * w0[x])) : __builtin_fma(ay, w1[x], ax * w0[x]);
                 if (ct) {
                     T(it, k) = t0 - pt;
                     T(it, k + 1) = __builtin_fma(-pt, bq, t1);
                     if (three) T(it, k + 2) = __builtin_fma(-pt, br, t2);
                 }
                 if (cv) {
-                    V(i, k) = v0 - pv;
-                    V(i, k + 1) = __builtin_fma(-pv, bq, v1);
-                    if (three) V(i, k + 2) = __builtin_fma(-pv, br, v2);
+                    V(i, k) = w0[x] - pv;
+                    V(i, k + 1) = __builtin_fma(-pv, bq, w1[x]);
+                    if (three) V(i, k + 2) = __builtin_fma(-pv, br, w2[x]);
                 }
             }
             EIGSOL_LDS_ORDER();
@@ -778,7 +794,7 @@ static int hqr_small(hipStream_t st, const double* H, int64_t ld, int n, int max
 static constexpr int kSmallDefault = 128;
 // AED window at 4096 with 4-bulge groups (up to 24 bulges per sweep): 40 -> 1.90 s, 48 -> 1.82 s, 56 -> 1.87 s
 // (one chain of 16 bulges: 40 was best); the window's one-wave Schur factorisation costs O(nw^3) latency-bound steps
-static constexpr int kAedDefault = 48;   // EIGSOL_QR_AED overrides (0: off)
+static constexpr int kAedDefault = 64;   // EIGSOL_QR_AED overrides (0: off)
 
 int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double* wr, double* wi,
                       int32_t* sweeps_out, int32_t* fail_out) {
@@ -810,14 +826,17 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     }();
     static const int max_bulges = [] {                 // experiments: cap the bulges per chain
         const char* e = std::getenv("EIGSOL_QR_NB");
-        return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : 24;
+        return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : 28;
     }();
     long long st_steps = 0, st_aed_steps = 0, st_aed_ph[3] = {0, 0, 0};
     static const int aed_win = [] {
         const char* e = std::getenv("EIGSOL_QR_AED");   // AED window (0: off)
         return e ? std::max(0, std::min(dev::kAedMax, std::atoi(e))) : kAedDefault;
     }();
-    constexpr int kNibble = 14;   // % of the AED window deflated that skips the sweep (LAPACK's NIBBLE)
+    static const int kNibble = [] {   // % of the AED window deflated that skips the sweep (LAPACK's NIBBLE)
+        const char* e = std::getenv("EIGSOL_QR_NIBBLE");
+        return e ? std::max(1, std::atoi(e)) : 30;
+    }();
     int st_sweeps = 0, st_windows = 0, st_small = 0, st_small_rows = 0, st_aed = 0, st_aed_defl = 0;
     auto finish_small = [&](int l, int hi) -> int {
         const int m = hi - l + 1;
