@@ -66,6 +66,20 @@ struct ChaseArgs {
 
 // Reciprocal without the IEEE division sequence: v_rcp_f64 and two Newton steps (within an ulp
 // or two; a Householder reflector built from it is orthogonal to the same order).  x != 0, finite.
+// sqrt of a in [2^-4, 2^4] (no range reduction): hardware reciprocal square root, then Goldschmidt /
+// Newton corrections to full double precision (v_sqrt_f64 alone is far from it)
+__device__ __forceinline__ double sqrt_nr(double a) {
+    const double y = __builtin_amdgcn_rsq(a);
+    double s = a * y, h = 0.5 * y;
+    const double r = __builtin_fma(-h, s, 0.5);
+    s = __builtin_fma(s, r, s);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-s, s, a);
+    s = __builtin_fma(d, h, s);
+    d = __builtin_fma(-s, s, a);
+    return __builtin_fma(d, h, s);
+}
+
 __device__ __forceinline__ double rcp_nr(double x) {
     double r = __builtin_amdgcn_rcp(x);
     double e = __builtin_fma(-x, r, 1.0);
@@ -506,19 +520,27 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
                     if (three) w2[x] = V(i, k + 2);
                 }
             }
-            double p = p0, q = q0, r = three ? r0 : 0.0, xk = 1.0;
+            // the bulge column is scaled by a power of two (exact, two instructions instead of a
+            // reciprocal) into [1/2, 1), so the norm's square root needs no range reduction: the
+            // step's serial chain is its latency
+            double p = p0, q = q0, r = three ? r0 : 0.0;
+            int ex = 0;
             if (k != m) {
                 p = T(k, k - 1);
                 q = T(k + 1, k - 1);
                 r = three ? T(k + 2, k - 1) : 0.0;
-                xk = fabs(p) + fabs(q) + fabs(r);
-                if (xk != 0.0) { const double is = rcp_nr(xk); p *= is; q *= is; r *= is; }
+                ex = __builtin_amdgcn_frexp_exp(fmax(fmax(fabs(p), fabs(q)), fabs(r)));
+                p = __builtin_amdgcn_ldexp(p, -ex);
+                q = __builtin_amdgcn_ldexp(q, -ex);
+                r = __builtin_amdgcn_ldexp(r, -ex);
             }
-            const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(__builtin_fma(p, p, __builtin_fma(q, q, r * r)));
+            const double nrm2 = __builtin_fma(p, p, __builtin_fma(q, q, r * r));
+            if (nrm2 == 0.0) return;
+            const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt_nr(nrm2);
             if (sg == 0.0) return;
             EIGSOL_LDS_ORDER();
             if (lane == 0 && k != m) {
-                T(k, k - 1) = -sg * xk;
+                T(k, k - 1) = -__builtin_amdgcn_ldexp(sg, ex);
                 T(k + 1, k - 1) = 0.0;
                 if (three) T(k + 2, k - 1) = 0.0;
             }
