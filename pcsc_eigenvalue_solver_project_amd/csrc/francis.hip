@@ -161,7 +161,22 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
             uc1[0] = uc2[0]; uc1[1] = uc2[1];
             if (three) uload(uc2, kk + 2);
         }
-        double p, q, r, xk = 1.0;
+        // the left update's rows k..k+2 (columns >= k: no other bulge writes them in this phase, and
+        // this step's own stores go to column k-1) are loaded first, so their LDS latency overlaps
+        // the reflector's chain
+        double l0[2], l1[2], l2[2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            const int j = k + ln + 64 * x;
+            l0[x] = l1[x] = l2[x] = 0.0;
+            if (j < a.e) {
+                l0[x] = Hw(k, j);
+                l1[x] = Hw(k + 1, j);
+                if (three) l2[x] = Hw(k + 2, j);
+            }
+        }
+        double p, q, r;
+        int ex = 0;
         if (k == l) {
             const double sx = a.shifts[2 * wv], sw = a.shifts[2 * wv + 1];
             const double z = Hw(l, l);
@@ -172,18 +187,23 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
             const double sc = fabs(p) + fabs(q) + fabs(r);
             if (sc != 0.0) { const double is = rcp_nr(sc); p *= is; q *= is; r *= is; }
         } else {
+            // scaled by a power of two (exact) into [1/2, 1): the norm's square root needs no range
+            // reduction
             p = Hw(k, k - 1);
             q = Hw(k + 1, k - 1);
             r = three ? Hw(k + 2, k - 1) : 0.0;
-            xk = fabs(p) + fabs(q) + fabs(r);
-            if (xk != 0.0) { const double is = rcp_nr(xk); p *= is; q *= is; r *= is; }
+            ex = __builtin_amdgcn_frexp_exp(fmax(fmax(fabs(p), fabs(q)), fabs(r)));
+            p = __builtin_amdgcn_ldexp(p, -ex);
+            q = __builtin_amdgcn_ldexp(q, -ex);
+            r = __builtin_amdgcn_ldexp(r, -ex);
         }
-        const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt(__builtin_fma(p, p, __builtin_fma(q, q, r * r)));
-        const bool act = sg != 0.0;
+        const double nrm2 = __builtin_fma(p, p, __builtin_fma(q, q, r * r));
+        const bool act = nrm2 != 0.0;
         if (act) {
+            const double sg = (p >= 0 ? 1.0 : -1.0) * sqrt_nr(nrm2);
             EIGSOL_LDS_ORDER();
             if (k != l && ln == 0) {
-                Hw(k, k - 1) = -sg * xk;
+                Hw(k, k - 1) = -__builtin_amdgcn_ldexp(sg, ex);
                 Hw(k + 1, k - 1) = 0.0;
                 if (three) Hw(k + 2, k - 1) = 0.0;
             }
@@ -195,15 +215,13 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
             for (int x = 0; x < 2; ++x) {
                 const int j = k + ln + 64 * x;
                 if (j < a.e) {
-                    const double h0 = Hw(k, j), h1 = Hw(k + 1, j);
-                    double pp = __builtin_fma(bq, h1, h0);
+                    double pp = __builtin_fma(bq, l1[x], l0[x]);
                     if (three) {
-                        const double h2 = Hw(k + 2, j);
-                        pp = __builtin_fma(br, h2, pp);
-                        Hw(k + 2, j) = __builtin_fma(-pp, az, h2);
+                        pp = __builtin_fma(br, l2[x], pp);
+                        Hw(k + 2, j) = __builtin_fma(-pp, az, l2[x]);
                     }
-                    Hw(k + 1, j) = __builtin_fma(-pp, ay, h1);
-                    Hw(k, j) = __builtin_fma(-pp, ax, h0);
+                    Hw(k + 1, j) = __builtin_fma(-pp, ay, l1[x]);
+                    Hw(k, j) = __builtin_fma(-pp, ax, l0[x]);
                 }
             }
 #pragma unroll

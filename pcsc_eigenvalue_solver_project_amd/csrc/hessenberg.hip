@@ -199,11 +199,17 @@ __global__ __launch_bounds__(256) void hess_y(int n, int i, int nch, const doubl
 // so no L2 writeback/invalidate is needed; partial sums are combined in block order
 // (deterministic).  The barrier spins are bounded: on expiry the kernel sets an error word and
 // drains (the host then reports EIGSOL_E_HIP).
-constexpr int kCoopBlocks = 64;
+#ifndef EIGSOL_COOP_BLOCKS
+#define EIGSOL_COOP_BLOCKS 64
+#endif
+constexpr int kCoopBlocks = EIGSOL_COOP_BLOCKS;
 constexpr int kCoopThreads = 1024;
 constexpr int kCoopMaxN = 8192;          // v in LDS (64 KiB) and at most 2 rows per lane
 #ifndef EIGSOL_GEMV_BATCH
 #define EIGSOL_GEMV_BATCH 16
+#endif
+#ifndef EIGSOL_HESS_SKIP_GEMV
+#define EIGSOL_HESS_SKIP_GEMV 0   // timing experiments only
 #endif
 constexpr int kGemvBatch = EIGSOL_GEMV_BATCH;   // columns per GEMV step (loads in flight per lane)
 
@@ -378,7 +384,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
         double yacc[kCoopRowsPerLane];
 #pragma unroll
         for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] = 0.0;
-        if (!sk) {
+        if (!sk && !EIGSOL_HESS_SKIP_GEMV) {
             // 8 columns per step with every load issued before the FMAs (bytes in flight: the
             // GEMV streams the trailing matrix once per column)
             const int nq = (r1 - r0 + 63) / 64;
