@@ -107,8 +107,11 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
     const ChaseWin a = ca.w[blockIdx.x];
     __shared__ double h[kWin * (kWin + 1)];
     __shared__ double u[kWin * kWin];
+    __shared__ double trash[4];   // target of the stores of lanes past a row / column range (branch-free)
     const int W = a.e - a.s;
-    const int ldh = W | 1;
+    // compile-time LDS pitches (odd for H): every LDS address is shifts and adds of wave-uniform
+    // and per-lane terms, no integer multiplies on a step's path
+    constexpr int ldh = kWin + 1, ldu = kWin;
     const int tid = threadIdx.x;
     auto Hw = [&](int i, int j) -> double& { return h[(i - a.s) + (j - a.s) * ldh]; };
     {
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
             if (idx < W * W) {
                 const int i = idx % W, j = idx / W;
                 h[i + j * ldh] = tmp[q];
-                u[idx] = (i == j) ? 1.0 : 0.0;
+                u[i + j * ldu] = (i == j) ? 1.0 : 0.0;
             }
         }
     }
@@ -139,13 +142,15 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
     auto live = [&](int t) { const int k = l + t - 3 * wv; return wv < a.nb && k >= l && k <= ihi - 1 && t < a.t1; };
     // U columns k, k+1, k+2 (window-relative), rows i0 and i1
     double uc0[2] = {0, 0}, uc1[2] = {0, 0}, uc2[2] = {0, 0};
+    // U rows past W: clamped loads, stores into `trash`
+    const int i0c = min(i0, W - 1), i1c = min(i1, W - 1);
     auto uload = [&](double* c, int col) {
-        if (d0) c[0] = u[i0 + col * W];
-        if (d1) c[1] = u[i1 + col * W];
+        c[0] = u[i0c + col * ldu];
+        c[1] = u[i1c + col * ldu];
     };
     auto ustore = [&](const double* c, int col) {
-        if (d0) u[i0 + col * W] = c[0];
-        if (d1) u[i1 + col * W] = c[1];
+        *(d0 ? &u[i0 + col * ldu] : &trash[0]) = c[0];
+        *(d1 ? &u[i1 + col * ldu] : &trash[1]) = c[1];
     };
     double ax = 0.0, ay = 0.0, az = 0.0, bq = 0.0, br = 0.0;
     // phase A of bulge wv at row k (reflector, left update, U columns); `three` compile-time
@@ -168,12 +173,10 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
             const int j = k + ln + 64 * x;
-            l0[x] = l1[x] = l2[x] = 0.0;
-            if (j < a.e) {
-                l0[x] = Hw(k, j);
-                l1[x] = Hw(k + 1, j);
-                if (three) l2[x] = Hw(k + 2, j);
-            }
+            const int jc = min(j, a.e - 1);    // clamped: lanes past the window read a valid word
+            l0[x] = Hw(k, jc);
+            l1[x] = Hw(k + 1, jc);
+            l2[x] = three ? Hw(k + 2, jc) : 0.0;
         }
         double p, q, r;
         int ex = 0;
@@ -214,15 +217,14 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
 #pragma unroll
             for (int x = 0; x < 2; ++x) {
                 const int j = k + ln + 64 * x;
-                if (j < a.e) {
-                    double pp = __builtin_fma(bq, l1[x], l0[x]);
-                    if (three) {
-                        pp = __builtin_fma(br, l2[x], pp);
-                        Hw(k + 2, j) = __builtin_fma(-pp, az, l2[x]);
-                    }
-                    Hw(k + 1, j) = __builtin_fma(-pp, ay, l1[x]);
-                    Hw(k, j) = __builtin_fma(-pp, ax, l0[x]);
+                const bool ok = j < a.e;
+                double pp = __builtin_fma(bq, l1[x], l0[x]);
+                if (three) {
+                    pp = __builtin_fma(br, l2[x], pp);
+                    *(ok ? &Hw(k + 2, j) : &trash[2]) = __builtin_fma(-pp, az, l2[x]);
                 }
+                *(ok ? &Hw(k + 1, j) : &trash[1]) = __builtin_fma(-pp, ay, l1[x]);
+                *(ok ? &Hw(k, j) : &trash[0]) = __builtin_fma(-pp, ax, l0[x]);
             }
 #pragma unroll
             for (int x = 0; x < 2; ++x) {   // U columns k..k+2 in registers
@@ -248,15 +250,15 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
 #pragma unroll
         for (int x = 0; x < 2; ++x) {
             const int i = rlo + ln + 64 * x;
-            if (i <= ilast) {
-                const double h0 = Hw(i, k), h1 = Hw(i, k + 1);
-                double pp = __builtin_fma(ay, h1, ax * h0);
-                double h2 = 0.0;
-                if (three) { h2 = Hw(i, k + 2); pp = __builtin_fma(az, h2, pp); }
-                Hw(i, k) = h0 - pp;
-                Hw(i, k + 1) = __builtin_fma(-pp, bq, h1);
-                if (three) Hw(i, k + 2) = __builtin_fma(-pp, br, h2);
-            }
+            const bool ok = i <= ilast;
+            const int ic = min(i, ilast);
+            const double h0 = Hw(ic, k), h1 = Hw(ic, k + 1);
+            double pp = __builtin_fma(ay, h1, ax * h0);
+            double h2 = 0.0;
+            if (three) { h2 = Hw(ic, k + 2); pp = __builtin_fma(az, h2, pp); }
+            *(ok ? &Hw(i, k) : &trash[0]) = h0 - pp;
+            *(ok ? &Hw(i, k + 1) : &trash[1]) = __builtin_fma(-pp, bq, h1);
+            if (three) *(ok ? &Hw(i, k + 2) : &trash[2]) = __builtin_fma(-pp, br, h2);
         }
     };
     for (int t = a.t0; t < a.t1; ++t) {
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(1024) void chase_wave_kernel(ChaseArgs ca) {
     for (int idx = tid; idx < W * W; idx += 1024) {
         const int i = idx % W, j = idx / W;
         ca.H[(a.s + i) + (int64_t)(a.s + j) * ca.n] = h[i + j * ldh];
-        a.U[idx] = u[idx];
+        a.U[idx] = u[i + j * ldu];
     }
 }
 
