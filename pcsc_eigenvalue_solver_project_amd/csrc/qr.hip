@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <limits>
 #include <vector>
 
 #include "kernels_common.hpp"
@@ -390,6 +391,19 @@ __global__ __launch_bounds__(1024) void hqr_lds_kernel(const double* Hin, int64_
     if (tid == 0) { info[0] = c.fail; info[1] = max(c.maxits, c.its); info[2] = c.total; }
 }
 
+// max |a_ij| as the bit pattern of a non-negative double (ordered like the value), for the
+// norm-range check before the Francis path
+__global__ __launch_bounds__(256) void absmax_kernel(const double* A, int64_t cnt, unsigned long long* out) {
+    double m = 0.0;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) m = fmax(m, fabs(A[i]));
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+}
+
+__global__ __launch_bounds__(256) void scale_pow2_kernel(double* A, int64_t cnt, int e) {
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256)
+        A[i] = __builtin_amdgcn_ldexp(A[i], e);
+}
 }  // namespace dev
 
 // ============================================================================ host drivers
@@ -575,9 +589,36 @@ static int qr_francis_host(eigsol_ctx* ctx, int64_t n, const double* A, int max_
     int rc = work_alloc(w, n);
     if (rc == EIGSOL_OK && hipMemcpyAsync(H, A, n * n * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: upload");
+    // LAPACK xGEEV's range guard: a matrix whose largest entry lies outside [smlnum, bignum]
+    // (smlnum = sqrt(safe min) / eps) is scaled into range first, here by an exact power of two, and
+    // the eigenvalues are scaled back; squared norms in the reflectors would under- or overflow
+    // otherwise.  Matrices inside the range are untouched (bit-identical path).
+    int escale = 0;
+    if (rc == EIGSOL_OK) {
+        unsigned long long* dmax = nullptr;
+        unsigned long long bits = 0;
+        EIGSOL_HIP(hipMallocAsync(reinterpret_cast<void**>(&dmax), sizeof(bits), st));
+        EIGSOL_HIP(hipMemsetAsync(dmax, 0, sizeof(bits), st));
+        hipLaunchKernelGGL(dev::absmax_kernel, dim3(1024), dim3(256), 0, st, H, n * n, dmax);
+        EIGSOL_HIP(hipMemcpyAsync(&bits, dmax, sizeof(bits), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipFreeAsync(dmax, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        double amax;
+        std::memcpy(&amax, &bits, sizeof(amax));
+        const double smlnum = std::sqrt(std::numeric_limits<double>::min()) / std::numeric_limits<double>::epsilon();
+        if (std::isfinite(amax) && amax > 0.0 && (amax < smlnum || amax > 1.0 / smlnum)) {
+            escale = -std::ilogb(amax);
+            hipLaunchKernelGGL(dev::scale_pow2_kernel, dim3(1024), dim3(256), 0, st, H, n * n, escale);
+        }
+    }
     if (rc == EIGSOL_OK) rc = hessenberg_dev<double>(st, H, n, w);
     int32_t sweeps = 0, failed = 0;
     if (rc == EIGSOL_OK) rc = francis_large_f64(ctx, H, n, max_iter, wr, wi, &sweeps, &failed);
+    if (rc == EIGSOL_OK && escale != 0)
+        for (int64_t i = 0; i < n; ++i) {
+            wr[i] = std::ldexp(wr[i], -escale);
+            wi[i] = std::ldexp(wi[i], -escale);
+        }
     if (iters) *iters = sweeps;
     if (conv) *conv = failed ? 0 : 1;
     work_free(w);

@@ -158,3 +158,80 @@ def test_francis_qr512_fixture_and_structured(ctx):
     K = Qm @ np.diag(d) @ Qm.T
     r = E.qr_eigenvalues(ctx, K, E.SolverOptions(1000, 1e-10))
     _match(r.eigenvalues_complex, d, 1e-8 * 300)
+
+
+# ---------------------------------------------------------------- Francis edge cases
+# Structures that drive the multishift / AED path through its corner cases: zero and triangular
+# input (every reflector and bulge vanishes), splits in the middle of the matrix (active blocks with
+# l > 0), unit-modulus spectra (a cyclic permutation: every shift is equally good), a repeated
+# eigenvalue cluster, extreme magnitudes (the power-of-two bulge scaling), and orders that are not
+# multiples of the 96-row chase window.  Reference eigenvalues are exact where the structure gives
+# them, LAPACK (numpy.linalg.eigvals) otherwise; tolerance 1e-9 * ||A|| unless stated.
+
+def test_francis_zero_and_triangular(ctx):
+    n = 300
+    r = E.qr_eigenvalues(ctx, np.zeros((n, n)), E.SolverOptions(1000, 1e-10))
+    assert r.converged and np.all(r.eigenvalues_complex == 0)
+    rng = np.random.default_rng(31)
+    U = np.triu(rng.standard_normal((n, n)))
+    r = E.qr_eigenvalues(ctx, U, E.SolverOptions(1000, 1e-10))
+    assert r.converged
+    # already triangular: nothing to chase, the diagonal comes back exactly
+    np.testing.assert_array_equal(np.sort(r.eigenvalues_complex.real), np.sort(np.diag(U)))
+    assert np.all(r.eigenvalues_complex.imag == 0)
+
+
+def test_francis_split_blocks(ctx):
+    rng = np.random.default_rng(32)
+    A1, A2, A3 = (rng.standard_normal((m, m)) for m in (150, 97, 260))
+    n = 150 + 97 + 260
+    A = np.zeros((n, n))
+    A[:150, :150] = A1
+    A[150:247, 150:247] = A2
+    A[247:, 247:] = A3
+    A[:150, 150:] = rng.standard_normal((150, n - 150))   # block upper triangular: same spectrum
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-10))
+    assert r.converged
+    ref = np.concatenate([np.linalg.eigvals(A1), np.linalg.eigvals(A2), np.linalg.eigvals(A3)])
+    _match(r.eigenvalues_complex, ref, 1e-9 * np.linalg.norm(A))
+
+
+def test_francis_roots_of_unity(ctx):
+    n = 300
+    P = np.roll(np.eye(n), 1, axis=0)   # cyclic shift: eigenvalues exp(2 pi i k / n), all |z| = 1
+    r = E.qr_eigenvalues(ctx, P, E.SolverOptions(1000, 1e-10))
+    assert r.converged
+    _match(r.eigenvalues_complex, np.exp(2j * np.pi * np.arange(n) / n), 1e-9 * np.sqrt(n))
+
+
+def test_francis_repeated_cluster(ctx):
+    n = 400
+    rng = np.random.default_rng(33)
+    u = rng.standard_normal(n)
+    S = np.eye(n) + np.outer(u, u)   # eigenvalue 1 (n - 1 times) and 1 + |u|^2
+    Qm, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    A = Qm @ S @ Qm.T
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-10))
+    assert r.converged
+    ref = np.ones(n)
+    ref[0] = 1 + u @ u
+    _match(r.eigenvalues_complex, ref, 1e-9 * np.linalg.norm(A))
+
+
+@pytest.mark.parametrize("scale", [1e-200, 1e140])
+def test_francis_extreme_magnitudes(ctx, scale):
+    n = 256
+    rng = np.random.default_rng(34)
+    A = rng.standard_normal((n, n))
+    r = E.qr_eigenvalues(ctx, A * scale, E.SolverOptions(1000, 1e-10))
+    assert r.converged
+    _match(r.eigenvalues_complex / scale, np.linalg.eigvals(A), 1e-9 * np.linalg.norm(A))
+
+
+@pytest.mark.parametrize("n", [97, 193, 385, 1001])
+def test_francis_window_boundaries(ctx, n):
+    rng = np.random.default_rng(1000 + n)
+    A = rng.standard_normal((n, n))
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-10))
+    assert r.converged
+    _match(r.eigenvalues_complex, np.linalg.eigvals(A), 1e-9 * np.linalg.norm(A))
