@@ -66,8 +66,11 @@ struct ShiftFactor {
 
 namespace dev {
 
-constexpr int kRowLanes = 16;    // lanes per row: one row per 16-lane group, 4 rows per wave round
-constexpr int kWaveRows = 4;     // positions per wave round (one chunk): levels are padded to this
+#ifndef EIGSOL_TRSV_ROW_LANES
+#define EIGSOL_TRSV_ROW_LANES 16
+#endif
+constexpr int kRowLanes = EIGSOL_TRSV_ROW_LANES;   // lanes per row: one row per 16-lane group
+constexpr int kWaveRows = 64 / kRowLanes;          // positions per wave round (one chunk): levels are padded to this
 constexpr int kSpinLimit = 1 << 20;   // polls (with back-off) before the wait is declared broken
 // An unsolved entry of z holds this NaN in every 8-byte word.  A solved value never does: the
 // producer maps it to the default quiet NaN (sanitize), so the value itself is the ready flag.
