@@ -1,0 +1,4 @@
+// Drop-in path for the reference header src/qr_method/qr_decompose.hpp: with -I<repo>/include/eigsol/compat and
+// -I<repo>/include a caller keeps its #include "src/qr_method/qr_decompose.hpp" line unchanged.
+#pragma once
+#include <eigsol/eigsol.hpp>

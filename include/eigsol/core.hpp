@@ -20,11 +20,26 @@
 #include <cstdint>
 #include <deque>
 #include <initializer_list>
+#include <iomanip>
+#include <ios>
+#include <ostream>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
 #include <utility>
 #include <vector>
+
+// Eigen interop (the reference's storage types, matrix.hpp:39-44): compiled only where Eigen's
+// headers are on the include path.  This image has no Eigen, so the conversions below are
+// compile-unverified here.
+#if __has_include(<Eigen/Dense>) && __has_include(<Eigen/Sparse>)
+#include <Eigen/Dense>
+#include <Eigen/Sparse>
+#define EIGSOL_HAVE_EIGEN 1
+#else
+#define EIGSOL_HAVE_EIGEN 0
+#endif
 
 namespace EigSol {
 
@@ -33,8 +48,10 @@ struct is_complex_of_floating : std::false_type {};
 template <typename Inner>
 struct is_complex_of_floating<std::complex<Inner>> : std::bool_constant<std::is_floating_point_v<Inner>> {};
 
+// The reference's concept (src/core/types.hpp:28-30), spelled the same way: a C++20 concept, so
+// reference-style callers written as `template <EigSol::ScalarConcept S>` compile unchanged.
 template <typename S>
-inline constexpr bool ScalarConcept = std::is_floating_point_v<S> || is_complex_of_floating<S>::value;
+concept ScalarConcept = std::is_floating_point_v<S> || is_complex_of_floating<S>::value;
 
 // Scalars with a device path (gfx950 kernels compute in fp64 / complex fp64).
 template <typename S>
@@ -129,6 +146,37 @@ public:
         return Filler{this, 1};
     }
 
+    // Row view for printing, as in the reference demo's `std::cout << v.transpose()` (main.cpp:38):
+    // the entries on one line, separated by spaces, padded to a common width (Eigen's default
+    // IOFormat for a row vector).
+    struct RowView {
+        const Vector* v;
+        friend std::ostream& operator<<(std::ostream& os, const RowView& r) {
+            std::vector<std::string> cells;
+            std::size_t w = 0;
+            for (const S& x : r.v->std()) {
+                std::ostringstream c;
+                c.precision(os.precision());
+                c.flags(os.flags());
+                c << x;
+                cells.push_back(c.str());
+                w = std::max(w, cells.back().size());
+            }
+            for (std::size_t i = 0; i < cells.size(); ++i)
+                os << (i ? " " : "") << std::setw(static_cast<int>(w)) << cells[i];
+            return os;
+        }
+    };
+    RowView transpose() const { return RowView{this}; }
+#if EIGSOL_HAVE_EIGEN
+    // Vector<S> of the reference is Eigen::Matrix<S, Dynamic, 1> (types.hpp:33)
+    operator Eigen::Matrix<S, Eigen::Dynamic, 1>() const {
+        Eigen::Matrix<S, Eigen::Dynamic, 1> e(static_cast<Eigen::Index>(d_.size()));
+        for (std::size_t i = 0; i < d_.size(); ++i) e(static_cast<Eigen::Index>(i)) = d_[i];
+        return e;
+    }
+#endif
+
 private:
     static S conj_(const S& x) {
         if constexpr (is_complex_of_floating<S>::value) return std::conj(x);
@@ -217,6 +265,46 @@ public:
     }
     void setRandom();   // defined in solvers.hpp (uses the façade's documented generator)
 
+#if EIGSOL_HAVE_EIGEN
+    // Matrix::Dense<S> of the reference is Eigen::Matrix<S, Dynamic, Dynamic> (matrix.hpp:39-41):
+    // both are column-major, so the conversion is one copy of the storage.
+    template <typename Derived>
+    static DenseMatrix fromEigen(const Eigen::MatrixBase<Derived>& m) {
+        const Eigen::Matrix<S, Eigen::Dynamic, Eigen::Dynamic> e = m;   // evaluates any expression
+        DenseMatrix d(e.rows(), e.cols());
+        std::copy(e.data(), e.data() + e.size(), d.d_.begin());
+        return d;
+    }
+    operator Eigen::Matrix<S, Eigen::Dynamic, Eigen::Dynamic>() const {
+        Eigen::Matrix<S, Eigen::Dynamic, Eigen::Dynamic> e(r_, c_);
+        std::copy(d_.begin(), d_.end(), e.data());
+        return e;
+    }
+#endif
+
+    // Eigen's default matrix print (main.cpp:117, :123-127): one row per line, columns separated
+    // by a space and right-aligned to the widest entry.
+    friend std::ostream& operator<<(std::ostream& os, const DenseMatrix& m) {
+        std::vector<std::string> cells(m.d_.size());
+        std::size_t w = 0;
+        for (std::int64_t i = 0; i < m.r_; ++i)
+            for (std::int64_t j = 0; j < m.c_; ++j) {
+                std::ostringstream c;
+                c.precision(os.precision());
+                c.flags(os.flags());
+                c << m(i, j);
+                std::string& cell = cells[static_cast<std::size_t>(i + j * m.r_)];
+                cell = c.str();
+                w = std::max(w, cell.size());
+            }
+        for (std::int64_t i = 0; i < m.r_; ++i) {
+            if (i) os << "\n";
+            for (std::int64_t j = 0; j < m.c_; ++j)
+                os << (j ? " " : "") << std::setw(static_cast<int>(w)) << cells[static_cast<std::size_t>(i + j * m.r_)];
+        }
+        return os;
+    }
+
 private:
     void set_rowmajor(std::int64_t k, const S& x) {
         if (k >= size()) throw std::runtime_error("DenseMatrix: too many coefficients in comma initializer");
@@ -285,6 +373,18 @@ public:
         s.compress();
         return s;
     }
+#if EIGSOL_HAVE_EIGEN
+    // Matrix::Sparse<S> of the reference is Eigen::SparseMatrix<S> (ColMajor, int; matrix.hpp:43-44)
+    template <int Options, typename Index>
+    static SparseMatrix fromEigen(const Eigen::SparseMatrix<S, Options, Index>& m) {
+        SparseMatrix s(m.rows(), m.cols());
+        for (Eigen::Index k = 0; k < m.outerSize(); ++k)
+            for (typename Eigen::SparseMatrix<S, Options, Index>::InnerIterator it(m, k); it; ++it)
+                s.insert(it.row(), it.col()) = it.value();
+        s.compress();
+        return s;
+    }
+#endif
     DenseMatrix<S> toDense() const {
         compress();
         DenseMatrix<S> d(r_, c_);

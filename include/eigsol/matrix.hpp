@@ -51,18 +51,29 @@ public:
     Matrix(Matrix&&) = delete;
     Matrix& operator=(Matrix&&) = delete;
 
-    template <typename S, typename = std::enable_if_t<ScalarConcept<S>>>
+    template <ScalarConcept S>
     explicit Matrix(const DenseMatrix<S>& m)
         : dense_(true), scalar_(&typeid(S)), box_(std::make_unique<BoxTyped<DenseMatrix<S>>>(m)) {}
 
-    template <typename S, typename = std::enable_if_t<ScalarConcept<S>>>
+    template <ScalarConcept S>
     explicit Matrix(const SparseMatrix<S>& m)
         : dense_(false), scalar_(&typeid(S)), box_(std::make_unique<BoxTyped<SparseMatrix<S>>>(m)) {
         box_cast<SparseMatrix<S>>().makeCompressed();
     }
 
+#if EIGSOL_HAVE_EIGEN
+    // Eigen inputs, as the reference's constructors take them (matrix.hpp:70-76, :89-94): any dense
+    // expression is evaluated into column-major storage, a sparse matrix is copied entry by entry.
+    template <typename Derived>
+        requires ScalarConcept<typename Derived::Scalar>
+    explicit Matrix(const Eigen::MatrixBase<Derived>& m)
+        : Matrix(DenseMatrix<typename Derived::Scalar>::fromEigen(m)) {}
+    template <ScalarConcept S, int Options, typename Index>
+    explicit Matrix(const Eigen::SparseMatrix<S, Options, Index>& m) : Matrix(SparseMatrix<S>::fromEigen(m)) {}
+#endif
+
     // row-major data (matrix.hpp:207-232)
-    template <typename S, typename = std::enable_if_t<ScalarConcept<S>>>
+    template <ScalarConcept S>
     Matrix(const std::vector<S>& data, std::size_t rows, std::size_t cols) : dense_(true), scalar_(&typeid(S)) {
         if (rows * cols != data.size()) throw std::runtime_error("Matrix: size mismatch in vector constructor");
         DenseMatrix<S> m(static_cast<std::int64_t>(rows), static_cast<std::int64_t>(cols));

@@ -31,9 +31,38 @@ inline std::uint64_t& random_seed() {
     return seed;
 }
 
-template <typename S>
+namespace detail {
+struct RandomState {
+    std::mt19937_64 gen{random_seed()};
+    std::uint64_t seeded = random_seed();
+};
+inline RandomState& random_state() {
+    static RandomState st;
+    return st;
+}
+// One generator for every scalar type; re-seeded whenever EigSol::random_seed() holds a new value
+// since the last draw (so setting the seed between solves takes effect, like std::srand before the
+// reference's Eigen Vector::Random).
+inline std::mt19937_64& random_engine() {
+    RandomState& st = random_state();
+    if (st.seeded != random_seed()) {
+        st.seeded = random_seed();
+        st.gen.seed(st.seeded);
+    }
+    return st.gen;
+}
+}  // namespace detail
+
+// std::srand counterpart: always restarts the start-vector sequence, also for an unchanged seed.
+inline void set_random_seed(std::uint64_t seed) {
+    random_seed() = seed;
+    detail::random_state().seeded = seed;
+    detail::random_state().gen.seed(seed);
+}
+
+template <ScalarConcept S>
 Vector<S> random_vector(std::size_t n) {
-    static std::mt19937_64 gen(random_seed());
+    std::mt19937_64& gen = detail::random_engine();
     std::uniform_real_distribution<double> u(-1.0, 1.0);
     Vector<S> v(n);
     for (std::size_t i = 0; i < n; ++i) {
@@ -54,8 +83,12 @@ void DenseMatrix<S>::setRandom() {
     std::copy(v.begin(), v.end(), d_.begin());
 }
 
-// QR iteration variant: Francis (implicit multishift sweeps, north_star) or the reference's
-// unshifted H <- RQ iteration (identical iteration counts).
+// QR iteration variant: the reference's unshifted H <- RQ iteration (qr_eigenvalues.hpp:62-105,
+// identical iteration counts, `converged` and positional diag(H)) is what the reference-signature
+// overloads run; Francis (implicit multishift sweeps with aggressive early deflation, north_star)
+// is opt-in by passing QRVariant::Francis: it converges on general real matrices, deflates at
+// LAPACK's threshold, reports `iterations` as its sweep count and returns the real parts in
+// `eigenvalues` with the complex eigenvalues in `eigenvalues_complex`.
 enum class QRVariant { Francis = EIGSOL_QR_FRANCIS, Unshifted = EIGSOL_QR_UNSHIFTED };
 
 namespace detail {
@@ -133,27 +166,27 @@ void dense_square_check(const DenseMatrix<S>& A, const char* who) {
 }  // namespace detail
 
 // ------------------------------------------------------------------------------ power methods
-template <typename S>
+template <ScalarConcept S>
 EigenResult<S> powerMethod(const Matrix& M, const SolverOptions& opts = SolverOptions{}) {
     return detail::power_like<S>(M, opts, nullptr, nullptr, "powerMethod");
 }
-template <typename S>
+template <ScalarConcept S>
 EigenResult<S> powerMethod(const Matrix& M, const SolverOptions& opts, const Vector<S>& x0) {
     return detail::power_like<S>(M, opts, &x0, nullptr, "powerMethod");
 }
 
-template <typename S>
+template <ScalarConcept S>
 EigenResult<S> shiftedInversePowerMethod(const Matrix& M,
                                          const ShiftedSolverOptions<S>& opts = ShiftedSolverOptions<S>{}) {
     return detail::power_like<S>(M, opts, nullptr, &opts.shift, "shiftedInversePowerMethod");
 }
-template <typename S>
+template <ScalarConcept S>
 EigenResult<S> shiftedInversePowerMethod(const Matrix& M, const ShiftedSolverOptions<S>& opts, const Vector<S>& x0) {
     return detail::power_like<S>(M, opts, &x0, &opts.shift, "shiftedInversePowerMethod");
 }
 
 // --------------------------------------------------------------------------------- solve_shifted
-template <typename S>
+template <ScalarConcept S>
 Vector<S> solve_shifted(const Matrix& A, const S shift, const Vector<S>& b) {
     if (A.scalar_type() != typeid(S)) throw std::runtime_error("solve_shifted: scalar type mismatch");
     const char* kind = A.isDense() ? "dense" : "sparse";
@@ -180,7 +213,7 @@ Vector<S> solve_shifted(const Matrix& A, const S shift, const Vector<S>& b) {
 }
 
 // ------------------------------------------------------------------------------------ QR method
-template <typename S>
+template <ScalarConcept S>
 DenseMatrix<S> to_hessenberg_dense(const DenseMatrix<S>& A) {
     detail::dense_square_check(A, "to_hessenberg_dense");
     detail::require_device_scalar<S>("to_hessenberg_dense");
@@ -195,14 +228,14 @@ DenseMatrix<S> to_hessenberg_dense(const DenseMatrix<S>& A) {
     return H;
 }
 
-template <typename S>
+template <ScalarConcept S>
 DenseMatrix<S> to_hessenberg(const Matrix& A) {
     if (!A.isDense()) throw std::runtime_error("to_hessenberg(Matrix): only dense matrices are supported");
     if (A.scalar_type() != typeid(S)) throw std::runtime_error("to_hessenberg(Matrix): scalar type mismatch");
     return to_hessenberg_dense<S>(A.cast<DenseMatrix<S>>());
 }
 
-template <typename S>
+template <ScalarConcept S>
 void qr_decompose_dense(const DenseMatrix<S>& A, DenseMatrix<S>& Q, DenseMatrix<S>& R) {
     if (A.rows() == 0 || A.cols() == 0) throw std::runtime_error("qr_decompose_dense: empty matrix");
     detail::require_device_scalar<S>("qr_decompose_dense");
@@ -222,7 +255,7 @@ void qr_decompose_dense(const DenseMatrix<S>& A, DenseMatrix<S>& Q, DenseMatrix<
                       "qr_decompose_dense");
 }
 
-template <typename S>
+template <ScalarConcept S>
 std::pair<DenseMatrix<S>, DenseMatrix<S>> qr_decompose(const Matrix& A) {
     if (!A.isDense()) throw std::runtime_error("qr_decompose(Matrix): only dense matrices are supported");
     if (A.scalar_type() != typeid(S)) throw std::runtime_error("qr_decompose(Matrix): scalar type mismatch");
@@ -231,9 +264,9 @@ std::pair<DenseMatrix<S>, DenseMatrix<S>> qr_decompose(const Matrix& A) {
     return {Q, R};
 }
 
-template <typename S>
+template <ScalarConcept S>
 QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& opts,
-                                 QRVariant variant = QRVariant::Francis) {
+                                 QRVariant variant = QRVariant::Unshifted) {
     detail::dense_square_check(A, "qr_eigenvalues_dense");
     const std::int64_t n = A.rows();
     if (n == 0) return QRResult<S>(Vector<S>(), 0, true);   // qr_eigenvalues.hpp:55-57
@@ -265,8 +298,8 @@ QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& o
     return res;
 }
 
-template <typename S>
-QRResult<S> qr_eigenvalues(const Matrix& A, const SolverOptions& opts, QRVariant variant = QRVariant::Francis) {
+template <ScalarConcept S>
+QRResult<S> qr_eigenvalues(const Matrix& A, const SolverOptions& opts, QRVariant variant = QRVariant::Unshifted) {
     if (!A.isDense()) throw std::runtime_error("qr_eigenvalues(Matrix): only dense matrices are supported");
     if (A.scalar_type() != typeid(S)) throw std::runtime_error("qr_eigenvalues(Matrix): scalar type mismatch");
     return qr_eigenvalues_dense<S>(A.cast<DenseMatrix<S>>(), opts, variant);

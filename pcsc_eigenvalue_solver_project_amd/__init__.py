@@ -14,7 +14,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._capi import (EIGSOL_C128, EIGSOL_F64, EigSolError, SolverOptionsC, call, check, last_error,
+from ._capi import (EIGSOL_C128, EIGSOL_E_SIZE_MISMATCH, EIGSOL_F64, EigSolError, SolverOptionsC, call, check, last_error,
                     lib)
 
 __all__ = [
@@ -59,6 +59,14 @@ def _np_dtype(code: int):
 
 def _ptr(a: np.ndarray) -> C.c_void_p:
     return a.ctypes.data_as(C.c_void_p)
+
+
+def _vector(v, dtype, n: int, what: str) -> np.ndarray:
+    """Host vector of exactly n entries (the C ABI copies n scalars from the pointer)."""
+    v = np.ascontiguousarray(v, dtype=dtype).reshape(-1)
+    if len(v) != n:
+        raise EigSolError(EIGSOL_E_SIZE_MISMATCH, f"{what} has {len(v)} entries, the matrix has {n} rows")
+    return v
 
 
 def device_count() -> int:
@@ -121,6 +129,13 @@ class CsrMatrix:
         ptr = np.ascontiguousarray(rowptr, dtype=np.int32)
         idx = np.ascontiguousarray(colidx, dtype=np.int32)
         nrows, ncols = int(shape[0]), int(shape[1])
+        nouter = nrows if layout == "csr" else ncols
+        if len(ptr) != nouter + 1:
+            raise EigSolError(EIGSOL_E_SIZE_MISMATCH,
+                              f"{layout} pointer array has {len(ptr)} entries, expected {nouter + 1}")
+        if len(values) != len(idx):
+            raise EigSolError(EIGSOL_E_SIZE_MISMATCH,
+                              f"values ({len(values)}) and index array ({len(idx)}) lengths differ")
         h = C.c_void_p()
         fn = "eigsol_csr_create" if layout == "csr" else "eigsol_csr_create_from_csc"
         call(fn, ctx.handle, code, nrows, ncols, len(idx), _ptr(ptr), _ptr(idx), _ptr(values), C.byref(h))
@@ -201,7 +216,7 @@ class PowerSession:
         if x0_dev is not None:
             call("eigsol_power_begin", self.handle, C.byref(o), C.c_void_p(x0_dev), 1)
         else:
-            x = np.ascontiguousarray(x0, dtype=self.dtype)
+            x = _vector(x0, self.dtype, self.n, "x0")
             self._x0 = x
             call("eigsol_power_begin", self.handle, C.byref(o), _ptr(x), 0)
 
@@ -257,7 +272,7 @@ def power_method(matrix, opts: SolverOptions = SolverOptions(), x0=None) -> Eige
         x0 = rng.uniform(-1, 1, matrix.shape[0])
         if matrix.dtype == np.complex128:
             x0 = x0 + 1j * rng.uniform(-1, 1, matrix.shape[0])
-    x0 = np.ascontiguousarray(x0, dtype=matrix.dtype)
+    x0 = _vector(x0, matrix.dtype, matrix.shape[0], "x0")
     lam = np.zeros(1, dtype=matrix.dtype)
     x = np.empty(matrix.shape[0], dtype=matrix.dtype)
     it, conv = C.c_int32(0), C.c_int32(0)
@@ -304,7 +319,7 @@ def shifted_inverse_power_method(matrix, opts: ShiftedSolverOptions = ShiftedSol
         x0 = rng.uniform(-1, 1, matrix.shape[0])
         if matrix.dtype == np.complex128:
             x0 = x0 + 1j * rng.uniform(-1, 1, matrix.shape[0])
-    x0 = np.ascontiguousarray(x0, dtype=matrix.dtype)
+    x0 = _vector(x0, matrix.dtype, matrix.shape[0], "x0")
     sig = _sigma(opts.shift, matrix.dtype)
     lam = np.zeros(1, dtype=matrix.dtype)
     x = np.empty(matrix.shape[0], dtype=matrix.dtype)

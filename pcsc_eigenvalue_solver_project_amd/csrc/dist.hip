@@ -398,8 +398,15 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     if (!ctx->comm && !ctx->loop) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
     *out = nullptr;
     const int P = ctx->nranks, me = ctx->rank;
+    if (row_begins[0] != 0 || nnz_local < 0)
+        return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: row_begins must start at 0 and nnz be >= 0");
+    for (int q = 0; q < P; ++q)
+        if (row_begins[q + 1] < row_begins[q])
+            return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: row_begins not monotone");
     const int64_t n_global = row_begins[P];
     const int64_t nrows = row_begins[me + 1] - row_begins[me];
+    if (n_global > INT32_MAX - 1)
+        return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: dimension exceeds int32 storage index");
     if (rowptr_local[0] != 0 || rowptr_local[nrows] != nnz_local)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: rowptr must start at 0 and end at nnz");
     std::vector<int32_t> col_local(std::max<int64_t>(nnz_local, 1));

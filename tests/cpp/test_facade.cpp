@@ -300,8 +300,12 @@ TEST(QREigenvaluesDenseTest, Real2x2BothVariantsAndComplex) {
     }
     // reference algorithm: 25 iterations at 1e-12 (golden)
     EXPECT_EQ(EigSol::qr_eigenvalues_dense<double>(A, opts, EigSol::QRVariant::Unshifted).iterations, 25);
+    // the reference-signature call runs the reference algorithm (qr_eigenvalues.hpp:62-105)
     auto r2 = EigSol::qr_eigenvalues<double>(EigSol::Matrix(A), opts);
     EXPECT_EQ(r2.eigenvalues.size(), 2u);
+    EXPECT_EQ(r2.iterations, 25);
+    EXPECT_TRUE(r2.converged);
+    EXPECT_EQ(EigSol::qr_eigenvalues_dense<double>(A, opts).iterations, 25);
     EigSol::Matrix::Dense<C> Ac(2, 2);
     Ac << C(2, 0), C(1, 0), C(1, 0), C(2, 0);
     auto rc = EigSol::qr_eigenvalues_dense<C>(Ac, opts);
@@ -312,7 +316,7 @@ TEST(QREigenvaluesDenseTest, Real2x2BothVariantsAndComplex) {
     // complex-conjugate pair reported through eigenvalues_complex
     DenseMat Rot(2, 2);
     Rot << 0.0, -1.0, 1.0, 0.0;
-    auto rr = EigSol::qr_eigenvalues_dense<double>(Rot, opts);
+    auto rr = EigSol::qr_eigenvalues_dense<double>(Rot, opts, EigSol::QRVariant::Francis);
     EXPECT_TRUE(rr.converged);
     EXPECT_NEAR(std::abs(std::abs(rr.eigenvalues_complex[0].imag()) - 1.0), 0.0, 1e-12);
 }
@@ -360,6 +364,32 @@ TEST(SinglePrecision, PowerShiftedSolveAndQR) {
     EigSol::Matrix Ml(L);
     EXPECT_EQ(Ml.rows(), 1);
     EXPECT_THROW(EigSol::powerMethod<long double>(Ml, EigSol::SolverOptions{}), std::runtime_error);
+}
+
+// ---------------------------------------------------------------- reference caller shapes
+// A helper constrained on the concept, as reference callers write it (power_method.hpp:135).
+template <EigSol::ScalarConcept S>
+S dominant_eigenvalue(const EigSol::Matrix& M) {
+    return EigSol::powerMethod<S>(M, EigSol::SolverOptions{}).eigenvalue;
+}
+static_assert(EigSol::ScalarConcept<float> && EigSol::ScalarConcept<std::complex<double>>);
+static_assert(!EigSol::ScalarConcept<int> && !EigSol::ScalarConcept<std::complex<int>>);
+
+TEST(StartVector, SeedChangesTakeEffect) {
+    EigSol::random_seed() = 11;
+    auto a = EigSol::random_vector<double>(5);
+    EigSol::random_seed() = 12;
+    auto b = EigSol::random_vector<double>(5);
+    EigSol::random_seed() = 11;
+    auto c = EigSol::random_vector<double>(5);
+    EXPECT_TRUE(a.std() == c.std());
+    EXPECT_TRUE(a.std() != b.std());
+    EigSol::set_random_seed(11);   // same value again: restarts the sequence like std::srand
+    auto d = EigSol::random_vector<double>(5);
+    EXPECT_TRUE(a.std() == d.std());
+    DenseMat A(2, 2);
+    A << 2.0, 0.0, 0.0, 1.0;
+    EXPECT_NEAR(dominant_eigenvalue<double>(EigSol::Matrix(A)), 2.0, 1e-8);
 }
 
 int main() {

@@ -50,3 +50,33 @@ def test_no_device_fails_loudly():
     with pytest.raises(E.EigSolError) as e:
         E.Context(0)
     assert e.value.status == _capi.EIGSOL_E_NO_DEVICE
+
+
+class _FakeCtx:
+    handle = None
+
+
+class _FakeMatrix:
+    """Shape/dtype stand-in: the length checks raise before any library call."""
+    shape = (8, 8)
+    dtype = __import__("numpy").float64
+    handle = None
+
+
+def test_python_bindings_reject_short_arrays():
+    import numpy as np
+    rp = np.arange(0, 9, dtype=np.int32)
+    ci = np.arange(8, dtype=np.int32)
+    with pytest.raises(E.EigSolError) as e:       # short values
+        E.CsrMatrix(_FakeCtx(), rp, ci, np.ones(7), (8, 8))
+    assert e.value.status == _capi.EIGSOL_E_SIZE_MISMATCH
+    with pytest.raises(E.EigSolError) as e:       # short rowptr
+        E.CsrMatrix(_FakeCtx(), rp[:-1], ci, np.ones(8), (8, 8))
+    assert e.value.status == _capi.EIGSOL_E_SIZE_MISMATCH
+    with pytest.raises(E.EigSolError) as e:       # CSC: colptr length follows ncols
+        E.CsrMatrix(_FakeCtx(), rp, ci, np.ones(8), (8, 9), layout="csc")
+    assert e.value.status == _capi.EIGSOL_E_SIZE_MISMATCH
+    for fn in (E.power_method, E.shifted_inverse_power_method):
+        with pytest.raises(E.EigSolError) as e:   # short x0
+            fn(_FakeMatrix(), x0=np.ones(7))
+        assert e.value.status == _capi.EIGSOL_E_SIZE_MISMATCH

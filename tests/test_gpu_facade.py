@@ -34,3 +34,30 @@ def test_demo_cli_reference_data(tmp_path):
     r = subprocess.run([exe, "--real", os.path.join(data, "A.txt")], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Eigenvalue: 4.87298" in r.stdout
+
+
+def test_reference_shaped_caller(tmp_path):
+    """examples/main_dropin.cpp: the reference demo's code shape (includes "src/...", helpers
+    constrained on EigSol::ScalarConcept, v.transpose() printing, structured bindings of
+    qr_decompose) compiled with -std=c++20 against the compat include tree, run on the reference
+    data: A.txt complex is upper triangular with eigenvalues {1+3i, 2+4i, 5-i}; the reference-
+    signature qr_eigenvalues runs the reference's unshifted iteration (converges on it)."""
+    exe = build(os.path.join(ROOT, "examples", "main_dropin.cpp"), str(tmp_path / "main_dropin"),
+                extra_includes=(os.path.join(ROOT, "include", "eigsol", "compat"),))
+    data = os.path.join(ROOT, "tests", "golden")
+    r = subprocess.run([exe, os.path.join(data, "A.txt"), os.path.join(data, "B.txt")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    assert "Eigenvalue near the shift: (5,-1)" in out or "Eigenvalue near the shift: (5," in out
+    assert "Eigenvalue near the shift: (3,2)" in out or "Eigenvalue near the shift: (3," in out
+    assert "H(A) = " in out and "Q_A * R_A (should approximate A) = " in out
+    qa = out.split("QR eigenvalues for Matrix A")[1]
+    assert "Converged              : true" in qa.splitlines()[1]
+    # diag of the converged H holds the three eigenvalues (positional, like the reference)
+    diag = qa.split("Eigenvalues (diag of H): \n")[1].splitlines()[0]
+    got = sorted(complex(t.replace(",", "+").replace("+-", "-").strip("()") + "j") for t in diag.split())
+    want = sorted([1 + 3j, 2 + 4j, 5 - 1j], key=lambda z: (z.real, z.imag))
+    got = sorted(got, key=lambda z: (z.real, z.imag))
+    assert all(abs(g - w) < 1e-8 for g, w in zip(got, want)), diag
+    assert "only dense matrices" in r.stderr
