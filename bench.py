@@ -5,11 +5,15 @@ metric : "power-iteration SpMV GB/s vs HBM roofline + eigvals/sec (QR), 1/2/4/8 
 step   : one fused power iteration (y = A x / ||.||, ||y||^2, x^H y, device-side convergence
          test) over the workload's CSR matrix — powerMethodImpl's loop body
          (src/power_method/power_method.hpp:68-96) with the redundant second product fused away.
-workload (default): BASELINE config "10M x 10M CSR ~10 nnz/row fp64, power_method row-sharded"
-         — per GPU a 10,000,000-row block of the band generator, weak scaling:
-         N GPUs hold an (N*10M) x (N*10M) matrix, one row block per rank.
-value  : algorithmic bytes (12 nnz + 4 (n+1) + 16 n per iteration) x iterations
-         x ranks / max-over-ranks wall time of the K timed iterations; inputs resident in HBM.
+workload (default): BASELINE config 4 "10M x 10M CSR ~10 nnz/row fp64, power_method row-sharded"
+         — ONE 10,000,000 x 10,000,000 band matrix (SURVEY §8d generator, partition-invariant) split
+         into N contiguous row blocks, one per rank (strong scaling; --scaling weak gives every
+         rank a 10M-row block of an (N*10M)-row matrix instead).  Per iteration the ranks exchange
+         halo rows and partial sums device to device (EIGSOL_TRANSPORT_PEER: the SpMV epilogue
+         stores into the peers' IPC-mapped inboxes over xGMI, the next launch waits on their flags).
+value  : algorithmic bytes (12 nnz + 4 (n+1) + 16 n per iteration, summed over the
+         ranks' blocks) x iterations / max-over-ranks wall time of the K timed iterations; inputs
+         resident in HBM.
 
 Run: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run).
 """
@@ -30,7 +34,7 @@ METRIC = "power-iteration SpMV GB/s vs HBM roofline + eigvals/sec (QR), 1/2/4/8 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 WORKLOADS = {
-    # name: (generator, rows per rank, nnz per row)
+    # name: (generator, rows (global for strong scaling, per rank for weak), nnz per row)
     "band10m": ("band", 10_000_000, 10),
     "uniform10m": ("uniform", 10_000_000, 10),
     "uniform1m": ("uniform", 1_000_000, 16),
@@ -44,6 +48,9 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--workload", default="band10m", choices=sorted(WORKLOADS))
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                   help="strong: one global matrix split over the ranks (BASELINE config 4); "
+                        "weak: a full-size block per rank")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-extras", action="store_true",
@@ -76,11 +83,11 @@ def pmc_traffic(workload, kernel):
     return best
 
 
-def cpu_baseline(kind, k, budget_s):
-    """Reference algorithm (two CSC products per iteration, single thread) on a bounded sample."""
+def cpu_baseline(kind, k, budget_s, n=1_000_000):
+    """Reference algorithm (two CSC products per iteration, single thread) on the same matrix as
+    the GPU run (n = the workload's global size), a bounded number of iterations."""
     from oracle import oracle as O
     from pcsc_eigenvalue_solver_project_amd import synthetic as S
-    n = 1_000_000
     rp, ci, v = gen(kind, n, k, 0, n)
     cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
     x0 = S.start_vector(n)
@@ -97,7 +104,7 @@ def cpu_baseline(kind, k, budget_s):
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{kind} {n}x{n}, {k} nnz/row (same generator), {iters} reference power "
+        "sample": f"the same {kind} {n}x{n} matrix, {k} nnz/row, {iters} reference power "
                   f"iterations (2 CSC-scatter products each, oracle/eigsol_oracle.cpp, -O3, 1 thread), "
                   f"{dt:.1f}s",
         "ms_per_iteration": 1e3 * dt / iters,
@@ -185,6 +192,26 @@ def run_config3(E, S, ctx, torch, stream, opts):
         A.close()
     res["note"] = "212 MB per iteration fits the 256 MB Infinity Cache: can exceed the HBM bound"
     return res
+
+
+def run_uniform10m(E, S, ctx, torch, stream, opts):
+    """Config 4's honest gather figure (SURVEY §8d "uniform also reported"): the same fused
+    iteration on a 10M x 10M matrix with 10 uniform random columns per row, one GPU."""
+    n = 10_000_000
+    rp, ci, v = S.uniform(n, 10)
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    del rp, ci, v
+    s = E.PowerSession(A)
+    s.begin(opts, S.start_vector(n))
+    s.step(5)
+    torch.cuda.synchronize()
+    ms = _events(torch, stream, lambda: s.step(40)) / 40
+    info = s.kernel_info()
+    s.close()
+    A.close()
+    return {"GB/s": round(info["bytes_per_iteration"] / (ms / 1e3) / 1e9, 2), "ms_per_iteration": round(ms, 4),
+            "roofline_frac": round(info["bytes_per_iteration"] / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel": info["kernel"], "bytes_per_iteration": info["bytes_per_iteration"]}
 
 
 def run_config2(E, ctx, no_cpu):
@@ -344,9 +371,14 @@ def main():
     import pcsc_eigenvalue_solver_project_amd as E
     from pcsc_eigenvalue_solver_project_amd import synthetic as S
 
-    kind, rows, k = WORKLOADS[args.workload]
-    n_global = rows * world
-    row0 = rows * rank
+    kind, rows_cfg, k = WORKLOADS[args.workload]
+    if args.scaling == "strong":
+        n_global = rows_cfg
+        rb = np.linspace(0, n_global, world + 1).astype(np.int64)
+    else:
+        n_global = rows_cfg * world
+        rb = np.arange(world + 1, dtype=np.int64) * rows_cfg
+    row0, rows = int(rb[rank]), int(rb[rank + 1] - rb[rank])
     # A dedicated (non-default) torch stream: the library's work and torch's timing events share it.
     torch_stream = torch.cuda.Stream()
     torch.cuda.set_stream(torch_stream)
@@ -355,7 +387,8 @@ def main():
         # one communicator per rank owned by the library (RCCL over xGMI); gloo only ships the id
         from pcsc_eigenvalue_solver_project_amd import dist as D
         ctx = D.torch_dist_context(local_rank, stream=torch_stream.cuda_stream)
-        A, sess = D.sharded_power_session(ctx, rp, ci, v, n_global, row0)
+        A = D.DistCsrMatrix(ctx, rb, rp, ci, v)
+        sess = E.PowerSession(A)
     else:
         ctx = E.Context(local_rank, stream=torch_stream.cuda_stream)
         A = E.CsrMatrix(ctx, rp, ci, v, (rows, rows))
@@ -363,6 +396,7 @@ def main():
     nnz = len(ci)
     del rp, ci, v
     x0 = S.start_vector(rows, np.float64, row0=row0)
+    transport = sess.transport()
     opts = E.SolverOptions(2**31 - 1, -1.0)   # tol < 0: the reference loop never stops early
     sess.begin(opts, x0)
     info = sess.kernel_info()
@@ -386,12 +420,14 @@ def main():
     done, launches = sess.query()
     assert not done, "tol < 0 must never terminate"
     el = torch.tensor([elapsed, ev_ms / 1e3], dtype=torch.float64)
+    tot = torch.tensor([info["bytes_per_iteration"], float(nnz)], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     elapsed_max, ev_max = float(el[0]), float(el[1])
 
     bytes_iter = info["bytes_per_iteration"]          # this rank's algorithmic bytes
-    total_bytes = bytes_iter * args.steps * world
+    total_bytes = float(tot[0]) * args.steps          # all ranks' blocks
     value = total_bytes / elapsed_max / 1e9
     achieved = bytes_iter / (ev_ms / 1e3 / args.steps) / 1e9
 
@@ -406,17 +442,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed_max / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded generators of SURVEY §8d; x0 seed 7)",
             "config": {
-                "workload": f"power_method CSR {args.workload}: {rows} rows x {k} nnz/row per GPU "
-                            f"({kind} columns), global {n_global}x{n_global}",
+                "workload": (f"power_method CSR {args.workload}: one {n_global}x{n_global} matrix, {k} nnz/row "
+                             f"({kind} columns), split into {world} row blocks of ~{rows} rows"
+                             if args.scaling == "strong" else
+                             f"power_method CSR {args.workload}: {rows} rows x {k} nnz/row per GPU "
+                             f"({kind} columns), global {n_global}x{n_global} (weak scaling)"),
                 "rows_per_gpu": rows,
                 "nnz_per_gpu": nnz,
+                "nnz_global": int(tot[1]),
                 "n_global": n_global,
                 "parallelism": f"row-block x{world}" if world > 1 else "single GPU",
+                "exchange": {0: "none (one GPU)", 1: "collective (pack kernel + RCCL group per iteration)",
+                             2: "peer (SpMV epilogue stores halo + partial into the peers' IPC inboxes, "
+                                "epoch flags, no host round trip)"}[transport],
                 "bytes_per_iteration_per_gpu": bytes_iter,
                 "grid_blocks": info["grid"],
                 "row_tiles": info["tiles"],
@@ -444,6 +487,7 @@ def main():
     if not args.no_extras and world == 1:
         out["extras"] = {
             "config3_csr_1Mx16": run_config3(E, S, ctx, torch, torch_stream, opts),
+            "config4_uniform10m": run_uniform10m(E, S, ctx, torch, torch_stream, opts),
             "config1_A_txt": run_config1(E, S, ctx),
             "config2_qr_4096": run_config2(E, ctx, args.no_cpu_baseline),
             "config5_shifted_inverse_1M": run_config5(E, S, ctx, torch, torch_stream, args.no_cpu_baseline),
@@ -454,7 +498,7 @@ def main():
     ctx.close()
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(kind, k, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(kind, k, args.cpu_seconds, n=n_global)
             out["cpu_baseline"]["host"] = host_cpu()
             out["cpu_allcores"] = cpu_allcores(kind, k, min(args.cpu_seconds, 10.0))
         print(json.dumps(out), flush=True)

@@ -239,6 +239,40 @@ int eigsol_exchange_mode(int nranks, const int64_t* row_begins, const int64_t* g
 /* The exchange a row-sharded matrix uses (EIGSOL_EXCHANGE_*) and its number of ghost entries. */
 int eigsol_csr_dist_info(const eigsol_csr* A, int* mode, int64_t* nghost);
 
+/* Host-collective bootstrap, no RCCL communicator: `allgather` gathers bytes_per_rank host bytes
+ * from every rank into recv (rank order) and returns 0 on success; the library calls it for its
+ * setup steps only (ghost plan counts and request lists, inbox addresses / IPC handles, barriers)
+ * and never from a kernel-issuing hot loop.  Any host transport works (MPI, torch.distributed
+ * gloo, sockets).  Row-sharded sessions on such a context use the device-side peer exchange. */
+typedef int (*eigsol_allgather_fn)(const void* send, void* recv, size_t bytes_per_rank, void* user);
+int eigsol_ctx_create_dist_host(int device, int rank, int nranks, eigsol_allgather_fn allgather,
+                                void* user, eigsol_ctx** out);
+
+/* Per-iteration transport of a power session (eigsol_power_transport):
+ *   EIGSOL_TRANSPORT_LOCAL     one GPU, nothing to exchange;
+ *   EIGSOL_TRANSPORT_COLLECTIVE host-enqueued pack kernel + RCCL group (or loopback copies) after
+ *                              every launch (all-gather exchange, non-sliced layouts);
+ *   EIGSOL_TRANSPORT_PEER      device-side: the fused SpMV's epilogue stores the halo rows and the
+ *                              rank partial straight into every peer's inbox (IPC-mapped over xGMI,
+ *                              or same-device pointers in a loopback world) and raises an epoch
+ *                              flag there; the next launch's prologue waits for the peers' flags.
+ *                              No host round trip, no extra launch.  EIGSOL_DIST_TRANSPORT=
+ *                              collective|peer overrides the collective choice (halo matrices in
+ *                              the sliced layout use peer by default). */
+#define EIGSOL_TRANSPORT_LOCAL 0
+#define EIGSOL_TRANSPORT_COLLECTIVE 1
+#define EIGSOL_TRANSPORT_PEER 2
+int eigsol_power_transport(const eigsol_power* s, int* transport);
+
+/* Host-only planning of the peer exchange (no device): this rank's push list.  requests holds
+ * the global rows other ranks read from this rank, grouped by requesting rank in rank order with
+ * counts ghost_counts[q * P + rank] (each group ascending, as eigsol_ghost_plan lists them);
+ * ghost_counts is the all-gathered P x P matrix of eigsol_ghost_plan's recv_counts.  Output: per
+ * request an entry {local row, peer, slot, 0}, where slot indexes the peer's ghost list (its
+ * [lower | upper] ghost order), sorted by local row. */
+int eigsol_peer_plan(int nranks, int rank, const int64_t* row_begins, const int64_t* ghost_counts,
+                     const int64_t* requests, int64_t nreq, int32_t* push_out);
+
 #ifdef __cplusplus
 }
 #endif

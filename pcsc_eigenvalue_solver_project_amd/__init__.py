@@ -243,6 +243,12 @@ class PowerSession:
         call("eigsol_power_trace", self.handle, _ptr(buf), int(capacity), C.byref(cnt))
         return buf[: cnt.value]
 
+    def transport(self) -> int:
+        """EIGSOL_TRANSPORT_LOCAL / _COLLECTIVE / _PEER (per-iteration exchange of this session)."""
+        t = C.c_int(0)
+        call("eigsol_power_transport", self.handle, C.byref(t))
+        return t.value
+
     def kernel_info(self):
         b, g, t, v = C.c_double(0), C.c_int32(0), C.c_int32(0), C.c_int32(0)
         call("eigsol_power_kernel_info", self.handle, C.byref(b), C.byref(g), C.byref(t), C.byref(v))

@@ -29,6 +29,13 @@ EIGSOL_E_UNSUPPORTED = 12
 EIGSOL_F64 = 0
 EIGSOL_C128 = 1
 
+EIGSOL_TRANSPORT_LOCAL = 0
+EIGSOL_TRANSPORT_COLLECTIVE = 1
+EIGSOL_TRANSPORT_PEER = 2
+
+# int (*)(const void* send, void* recv, size_t bytes_per_rank, void* user)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
 EIGSOL_QR_FRANCIS = 0
 EIGSOL_QR_UNSHIFTED = 1
 
@@ -96,6 +103,9 @@ SIGNATURES = {
     "eigsol_ghost_plan": [C.c_int, _vp, C.c_int, _i64, _vp, _vp, _pi64, _vp, _vp],
     "eigsol_exchange_mode": [C.c_int, _vp, _vp, C.POINTER(C.c_int)],
     "eigsol_csr_dist_info": [_vp, C.POINTER(C.c_int), _pi64],
+    "eigsol_ctx_create_dist_host": [C.c_int, C.c_int, C.c_int, _vp, _vp, _ppv],
+    "eigsol_power_transport": [_vp, C.POINTER(C.c_int)],
+    "eigsol_peer_plan": [C.c_int, C.c_int, _vp, _vp, _vp, _i64, _vp],
     "eigsol_shifted_create_csr": [_vp, _vp, _i32, _ppv],
     "eigsol_shifted_create_dense": [_vp, _vp, _i32, _ppv],
     "eigsol_shifted_inverse_csr": [_vp, _vp, C.POINTER(SolverOptionsC), _vp, _vp, _vp, _pi32, _pi32],

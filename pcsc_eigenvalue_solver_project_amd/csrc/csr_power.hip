@@ -83,6 +83,7 @@ struct CsrArgs {
     part4* my_part;
     part4* blk_part;
     S* trace;
+    PeerArgs peer;           // row-sharded session on the device-side peer exchange (kDist kernels)
 };
 
 // Registers holding one tile's stream for one lane: P slots of (values, columns) plus the lane's
@@ -647,6 +648,15 @@ constexpr int kSliceRows = 64;
 constexpr int kSliceMaxK = 64;
 constexpr int kSliceWin = 256;
 
+// x-space entry e of a ghost-reading slice on the peer exchange: own rows from the input vector,
+// ghosts (e < xoff, e >= xoff + nrows) from the inbox's ghost area with system-scope loads.
+template <class S>
+__device__ __forceinline__ S ld_x_peer(const CsrArgs<S>& a, const S* xin, const S* gin, int e) {
+    const bool lo = e < a.xoff, hi = e >= a.xoff + a.nrows;
+    if (lo || hi) return ld_sys_s(gin + (lo ? e : e - a.nrows));
+    return xin[e];
+}
+
 template <class S, int KB, bool kG>
 struct SliceRegs {
     // window loads: f64 in 16-byte pairs (window start even, length even), complex one per lane
@@ -676,9 +686,9 @@ __device__ __forceinline__ uint32_t slice_entry(uint32_t off, int k, int lane) {
 
 // Every load of one slice's first KB entries, its window and the row lengths.  Loads are clamped
 // (to entry K-1, window entry wl-1): same cache lines, no extra bytes, no exec-masked loads.
-template <class S, int KB, bool kG>
+template <class S, int KB, bool kG, bool kDist = false>
 __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, int slice, int4 m,
-                                            SliceRegs<S, KB, kG>& R) {
+                                            SliceRegs<S, KB, kG>& R, const S* gin = nullptr) {
     const int lane = threadIdx.x & 63;
     // K = 0 (all rows empty) clamps to entry 0 of the slice: the streams carry one slice of
     // padding past their end, so even an empty last slice loads in bounds
@@ -703,6 +713,18 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
             R.c[g] = ldg_stream(a.scol8, (uint32_t)m.w + 64u * (uint32_t)min(g, nw - 1) + (uint32_t)lane);
         // the window always holds the slice's own rows (the Rayleigh term reads them)
         const int wl = max((m.z >> 9) & 0x1ff, 1);
+        if (kDist && (m.z & kGhostSliceBit)) {
+#pragma unroll
+            for (int j = 0; j < SliceRegs<S, KB, kG>::NW; ++j) {
+                if constexpr (std::is_same_v<S, double>) {
+                    const int e = m.y + 2 * min(lane + 64 * j, (wl >> 1) - 1);
+                    R.w[j].x = ld_x_peer(a, xin, gin, e);
+                    R.w[j].y = ld_x_peer(a, xin, gin, e + 1);
+                } else {
+                    R.w[j] = ld_x_peer(a, xin, gin, m.y + min(lane + 64 * j, wl - 1));
+                }
+            }
+        } else
 #pragma unroll
         for (int j = 0; j < SliceRegs<S, KB, kG>::NW; ++j)
             if constexpr (std::is_same_v<S, double>)
@@ -718,10 +740,17 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
 }
 
 // Row sums of one slice from its registers (window slices: x from the wave's LDS window).
-template <class S, bool kPower, int KB, bool kG>
+template <class S>
+__device__ __forceinline__ S shfl_s(S v, int src) {
+    if constexpr (std::is_same_v<S, double>) return __shfl(v, src, 64);
+    else return cplx{__shfl(v.re, src, 64), __shfl(v.im, src, 64)};
+}
+
+template <class S, bool kPower, int KB, bool kG, bool kDist = false>
 __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin, S* yout, double nrm,
                                               const SliceRegs<S, KB, kG>& R, int4 mc, int sl, S* xw,
-                                              double& n2, double& rr, double& ri) {
+                                              double& n2, double& rr, double& ri, const S* gin = nullptr,
+                                              int parity = 0) {
     const int lane = threadIdx.x & 63;
     const int K = mc.z & 0xff;
     const int row = sl * kSliceRows + lane;
@@ -770,8 +799,14 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
         __builtin_amdgcn_wave_barrier();
     } else if constexpr (kG) {
         S xv[KB];
+        const bool ghost = kDist && (mc.z & kGhostSliceBit);
+        if (ghost) {
 #pragma unroll
-        for (int u = 0; u < KB; ++u) xv[u] = ldg(xin, R.c[u]);
+            for (int u = 0; u < KB; ++u) xv[u] = ld_x_peer(a, xin, gin, (int)R.c[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < KB; ++u) xv[u] = ldg(xin, R.c[u]);
+        }
 #pragma unroll
         for (int u = 0; u < KB; ++u) {
             S x = xv[u];
@@ -781,7 +816,8 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
         }
         for (int k0 = KB; k0 < K; ++k0) {
             const uint32_t q = (uint32_t)lane + 64u * (uint32_t)k0;
-            S x = ldg(xin, (uint32_t)ldg(a.scol32, (uint32_t)mc.w + q));
+            const uint32_t cc = (uint32_t)ldg(a.scol32, (uint32_t)mc.w + q);
+            S x = ghost ? ld_x_peer(a, xin, gin, (int)cc) : ldg(xin, cc);
             if constexpr (kPower) x = scale_in(x, nrm);
             const S pr = mul(ldg(a.sval, slice_entry<S>((uint32_t)mc.x, k0, lane)), x);
             if (k0 < R.len) sacc = add(sacc, pr);
@@ -793,6 +829,17 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
         if constexpr (kPower) {
             n2 += sq_abs(sacc);
             acc_dot(rr, ri, xi, sacc);
+        }
+    }
+    if constexpr (kDist) {
+        // halo: the rows other ranks read go straight into their inboxes (system-scope stores,
+        // drained before the block's ticket); a slice's entries are contiguous in the push list
+        const int2 pr = ld_uniform(a.peer.slice_push, sl);
+        for (int e0 = pr.x; e0 < pr.y; e0 += 64) {
+            const int e = e0 + lane;
+            const int4 en = a.peer.push[min(e, pr.y - 1)];
+            const S v = shfl_s(sacc, en.x - sl * kSliceRows);
+            if (e < pr.y) st_sys_s(peer_ghosts<S>(a.peer.peers[en.y], parity, a.peer.ghost_stride) + en.z, v);
         }
     }
 }
@@ -817,7 +864,7 @@ struct SlicePlan {
 #endif
 };
 
-template <class S, bool kPower, int KB, bool kG>
+template <class S, bool kPower, int KB, bool kG, bool kDist = false>
 __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int parity) {
     constexpr int kSliceNS = SlicePlan<S, KB, kG>::ns;   // slices per round
     constexpr int kPipe = SlicePlan<S, KB, kG>::pipe;    // rounds in flight while one computes
@@ -829,12 +876,14 @@ __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int p
     const S* xin;
     S* yout;
     double nrm = 0.0;
+    const S* gin = nullptr;   // peer exchange: ghost entries of the input (inbox, previous parity)
     if constexpr (kPower) {
-        power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro);
+        power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro, kDist ? &a.peer : nullptr);
         if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
         nrm = pro.nrm;
         xin = parity ? a.buf0 : a.buf1;
         yout = (parity ? a.buf1 : a.buf0) + a.xoff;   // y rows land at their x-space slots
+        if constexpr (kDist) gin = peer_ghosts<S>(a.peer.inbox, parity ^ 1, a.peer.ghost_stride);
     } else {
         xin = a.x_plain;
         yout = a.y_plain;
@@ -854,13 +903,14 @@ __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int p
         for (int i = 0; i < kSliceNS; ++i) mc[i] = ld_uniform(a.slice_meta, min(s0 + i * wpg, send - 1));
 #pragma unroll
         for (int i = 0; i < kSliceNS; ++i)   // past the range: reloads the last slice, unused
-            slice_issue<S, KB, kG>(a, xin, min(s0 + i * wpg, send - 1), mc[i], R[i]);
+            slice_issue<S, KB, kG, kDist>(a, xin, min(s0 + i * wpg, send - 1), mc[i], R[i], gin);
     };
     auto compute = [&](const SliceRegs<S, KB, kG>(&R)[kSliceNS], const int4(&mc)[kSliceNS], int s0) {
 #pragma unroll
         for (int i = 0; i < kSliceNS; ++i)
             if (i == 0 || s0 + i * wpg < send)
-                slice_compute<S, kPower, KB, kG>(a, xin, yout, nrm, R[i], mc[i], s0 + i * wpg, xw_all[wave][i], n2, rr, ri);
+                slice_compute<S, kPower, KB, kG, kDist>(a, xin, yout, nrm, R[i], mc[i], s0 + i * wpg, xw_all[wave][i],
+                                                        n2, rr, ri, gin, parity);
     };
     int sl = sbeg + (blockIdx.x >> 3) * kWaves + wave;
     if constexpr (kPipe == 1) {
@@ -906,9 +956,31 @@ __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int p
         }
     }
     if constexpr (kPower) {
+        if constexpr (kDist) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // halo stores drained
         block_sum3(n2, rr, ri, sm);
         last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+        if constexpr (kDist) {
+            if (threadIdx.x == 0 && s_last) {
+                const part4 mine = *a.my_part;
+                peer_publish(a.peer, parity, mine, (uint64_t)pro.t + 2);
+            }
+        }
     }
+}
+
+// Start of a peer-exchange session (begin(), after the x0 norm partial): x0's halo rows and the
+// rank partial go to every inbox's parity-1 slots (launch 0 reads them as "launch -1"), then flag
+// epoch 1.  One block.
+template <class S>
+__global__ __launch_bounds__(kThreads) void peer_begin_kernel(PeerArgs pa, const S* x_own, int64_t npush,
+                                                              const part4* mine) {
+    for (int64_t e = threadIdx.x; e < npush; e += kThreads) {
+        const int4 en = pa.push[e];
+        st_sys_s(peer_ghosts<S>(pa.peers[en.y], 1, pa.ghost_stride) + en.z, x_own[en.x]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) peer_publish(pa, 1, *mine, 1);
 }
 
 // ||x||^2 partials of the start vector (x.normalize(), power_method.hpp:62).
@@ -1070,11 +1142,20 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
         }
         const int64_t wl = (int64_t)w1 - w0 + 1;
         win = win && wl <= kSliceWin;
+        // row-sharded x-space: does the slice read ghost entries (x-space indices outside its own
+        // rank's rows)?  Only the peer-exchange kernel looks at the bit.
+        bool ghost = false;
+        if (win) {
+            ghost = w0 < xoff || (int64_t)w1 >= xoff + nrows;
+        } else {
+            for (int64_t e = rowptr[r0]; e < rowptr[r1] && !ghost; ++e)
+                ghost = col[e] < xoff || col[e] >= xoff + nrows;
+        }
         any_ragged |= ragged;
         L.maxk = std::max(L.maxk, K);
         L.meta[4 * s] = (int32_t)total;
         L.meta[4 * s + 1] = win ? w0 : -1;
-        L.meta[4 * s + 2] = K | (ragged ? 0x100 : 0) | (win ? (int32_t)(wl << 9) : 0);
+        L.meta[4 * s + 2] = K | (ragged ? 0x100 : 0) | (win ? (int32_t)(wl << 9) : 0) | (ghost ? kGhostSliceBit : 0);
         L.meta[4 * s + 3] = (int32_t)(win ? ctot8 : ctot32);
         total += (int64_t)(sb == 8 ? (K + 1) & ~1 : K) * kSliceRows;   // f64: whole lane pairs
         if (win) ctot8 += (int64_t)((K + 3) / 4) * kSliceRows;
@@ -1278,10 +1359,13 @@ static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, in
 }
 
 template <class S>
-static const void* power_kernel_ptr(const eigsol_csr* A) {
+static const void* power_kernel_ptr(const eigsol_csr* A, bool peer = false) {
     if (A->sliced) {
-#define EIGSOL_SLICE_PTR(KB)                                                                     \
-    return A->slice_gather ? reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, true>) \
+#define EIGSOL_SLICE_PTR(KB)                                                                                 \
+    if (peer)                                                                                                \
+        return A->slice_gather ? reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, true, true>)   \
+                               : reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, false, true>); \
+    return A->slice_gather ? reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, true>)             \
                            : reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, false>);
         switch (A->slice_kb) {
             case 4: EIGSOL_SLICE_PTR(4)
@@ -1295,8 +1379,8 @@ static const void* power_kernel_ptr(const eigsol_csr* A) {
                        : reinterpret_cast<const void*>(csr_kernel<S, true>);
 }
 
-int csr_grid(eigsol_csr* A, int* grid) {
-    const void* k = A->dtype == EIGSOL_C128 ? power_kernel_ptr<cplx>(A) : power_kernel_ptr<double>(A);
+int csr_grid(eigsol_csr* A, int* grid, bool peer) {
+    const void* k = A->dtype == EIGSOL_C128 ? power_kernel_ptr<cplx>(A, peer) : power_kernel_ptr<double>(A, peer);
     // work units: tiles (one per block step) or slices (one per wave step)
     const int64_t units = A->sliced ? (A->nslices + kWaves - 1) / kWaves : A->ntiles;
     // sliced: two blocks (8 waves, 16 slices in flight) per CU measured fastest on band10m;
@@ -1328,7 +1412,7 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
 }
 
 template <class S>
-static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int parity, int grid) {
+static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int parity, int grid, bool peer = false) {
     hipStream_t s = A->ctx->stream;
     static const int mode = [] {
         const char* e = std::getenv("EIGSOL_CSR_ABLATION");
@@ -1344,8 +1428,10 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
         }
     }
     if (A->sliced) {
-#define EIGSOL_SLICE_LAUNCH2(KB, G)                                                                               \
-    if (power) hipLaunchKernelGGL((csr_slice_kernel<S, true, KB, G>), dim3(grid), dim3(kThreads), 0, s, args, parity); \
+#define EIGSOL_SLICE_LAUNCH2(KB, G)                                                                                     \
+    if (power && peer)                                                                                                  \
+        hipLaunchKernelGGL((csr_slice_kernel<S, true, KB, G, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);   \
+    else if (power) hipLaunchKernelGGL((csr_slice_kernel<S, true, KB, G>), dim3(grid), dim3(kThreads), 0, s, args, parity); \
     else hipLaunchKernelGGL((csr_slice_kernel<S, false, KB, G>), dim3(grid), dim3(kThreads), 0, s, args, parity);
 #define EIGSOL_SLICE_LAUNCH(KB)                                  \
     if (A->slice_gather) { EIGSOL_SLICE_LAUNCH2(KB, true) }      \
@@ -1372,7 +1458,7 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
 template <class S>
 static int power_launch_t(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
                           const void* rank_part, int nranks, void* my_part, void* blk_part,
-                          void* trace, int parity, int grid) {
+                          void* trace, int parity, int grid, const PeerArgs* peer) {
     CsrArgs<S> a = make_args<S>(A, xlen);
     a.buf0 = (S*)buf0;
     a.buf1 = (S*)buf1;
@@ -1382,18 +1468,33 @@ static int power_launch_t(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, P
     a.my_part = (part4*)my_part;
     a.blk_part = (part4*)blk_part;
     a.trace = (S*)trace;
-    return launch_csr<S>(A, a, true, parity, grid);
+    if (peer) a.peer = *peer;
+    return launch_csr<S>(A, a, true, parity, grid, peer != nullptr);
 }
 
 // entry point used by power_session.cpp (xlen: entries of the y buffers, own + ghost)
 int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
                      const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
-                     int parity, int grid) {
+                     int parity, int grid, const PeerArgs* peer) {
+    if (peer && !A->sliced) return fail(EIGSOL_E_UNSUPPORTED, "peer exchange needs the sliced CSR layout");
     if (A->dtype == EIGSOL_C128)
         return power_launch_t<cplx>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
-                                    trace, parity, grid);
+                                    trace, parity, grid, peer);
     return power_launch_t<double>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
-                                  trace, parity, grid);
+                                  trace, parity, grid, peer);
+}
+
+int peer_begin_launch(eigsol_ctx* ctx, int dtype, const PeerArgs& pa, const void* x_own, int64_t npush,
+                      const void* mine) {
+    hipStream_t s = ctx->stream;
+    if (dtype == EIGSOL_C128)
+        hipLaunchKernelGGL(peer_begin_kernel<cplx>, dim3(1), dim3(kThreads), 0, s, pa, (const cplx*)x_own, npush,
+                           (const part4*)mine);
+    else
+        hipLaunchKernelGGL(peer_begin_kernel<double>, dim3(1), dim3(kThreads), 0, s, pa, (const double*)x_own,
+                           npush, (const part4*)mine);
+    EIGSOL_HIP(hipGetLastError());
+    return EIGSOL_OK;
 }
 
 int norm_partial_launch(eigsol_ctx* ctx, int dtype, const void* x, int64_t n, PowerCtl* ctl,
@@ -1491,7 +1592,7 @@ int eigsol_csr_spmv(eigsol_csr* A, const void* x_dev, void* y_dev) {
     if (A->nrows == 0) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
     int grid = 8;
-    EIGSOL_TRY(csr_grid(A, &grid));
+    EIGSOL_TRY(csr_grid(A, &grid, false));
     if (A->dtype == EIGSOL_C128) {
         CsrArgs<cplx> a = make_args<cplx>(A, A->ncols);
         a.x_plain = (const cplx*)x_dev;

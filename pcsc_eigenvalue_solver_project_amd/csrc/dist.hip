@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <cstdio>
@@ -71,6 +72,7 @@ struct LoopWorld {
     int joined = 0;
     std::vector<std::vector<LoopSend>> sends;
     std::vector<hipEvent_t> ready, done;
+    std::vector<std::vector<char>> hbuf;   // host all-gather slots
 };
 static std::mutex g_loop_m;
 static std::map<std::string, std::shared_ptr<LoopWorld>> g_loop_worlds;
@@ -132,6 +134,61 @@ static void loop_allgather(eigsol_ctx* ctx, void* buf, size_t bytes, std::vector
         s.push_back({q, b + (size_t)ctx->rank * bytes, bytes});
         r.push_back({q, b + (size_t)q * bytes, bytes});
     }
+}
+
+// ------------------------------------------------------------------------- host collectives
+// Setup-time all-gather of host bytes over whatever the context was bootstrapped with: the
+// caller's callback (eigsol_ctx_create_dist_host), the loopback world, or RCCL (staged through a
+// device buffer).  Never used per iteration.
+int coll_allgather(eigsol_ctx* ctx, const void* mine, size_t bytes, void* all) {
+    const int P = ctx->nranks, me = ctx->rank;
+    char* out = static_cast<char*>(all);
+    if (P == 1 || bytes == 0) {
+        if (bytes) std::memcpy(out, mine, bytes);
+        return EIGSOL_OK;
+    }
+    if (ctx->hcoll) {
+        if (ctx->hcoll(mine, all, bytes, ctx->hcoll_user) != 0)
+            return fail(EIGSOL_E_RCCL, "host all-gather callback failed");
+        return EIGSOL_OK;
+    }
+    if (ctx->loop) {
+        auto* w = static_cast<LoopWorld*>(ctx->loop);
+        {
+            std::lock_guard<std::mutex> lk(w->m);
+            w->hbuf[me].assign(static_cast<const char*>(mine), static_cast<const char*>(mine) + bytes);
+        }
+        loop_barrier(w);
+        int rc = EIGSOL_OK;
+        for (int q = 0; q < P; ++q) {
+            if (w->hbuf[q].size() != bytes) rc = fail(EIGSOL_E_RCCL, "loopback all-gather: size mismatch");
+            else std::memcpy(out + (size_t)q * bytes, w->hbuf[q].data(), bytes);
+        }
+        loop_barrier(w);   // nobody overwrites a slot another rank still reads
+        return rc;
+    }
+    if (!ctx->comm) return fail(EIGSOL_E_INVALID, "coll_allgather: context has no communicator");
+    char* d = nullptr;
+    EIGSOL_HIP(hipMalloc(&d, bytes * P));
+    hipStream_t st = ctx->stream;
+    int rc = EIGSOL_OK;
+    if (hipMemcpyAsync(d + bytes * me, mine, bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "coll_allgather: upload");
+    ncclResult_t r = rc == EIGSOL_OK ? ncclAllGather(d + bytes * me, d, bytes, ncclChar,
+                                                    static_cast<ncclComm_t>(ctx->comm), st)
+                                     : ncclSuccess;
+    if (r != ncclSuccess) rc = fail(EIGSOL_E_RCCL, std::string("coll_allgather: ") + ncclGetErrorString(r));
+    if (rc == EIGSOL_OK && (hipMemcpyAsync(all, d, bytes * P, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                            hipStreamSynchronize(st) != hipSuccess))
+        rc = fail(EIGSOL_E_HIP, "coll_allgather: download");
+    hipFree(d);
+    return rc;
+}
+
+int coll_barrier(eigsol_ctx* ctx) {
+    const char one = 1;
+    std::vector<char> all(ctx->nranks);
+    return coll_allgather(ctx, &one, 1, all.data());
 }
 
 void dist_release_comm(eigsol_ctx* ctx) {
@@ -354,6 +411,7 @@ int eigsol_ctx_create_dist(int device, int rank, int nranks, const void* unique_
                 slot = std::make_shared<LoopWorld>();
                 slot->P = nranks;
                 slot->sends.resize(nranks);
+                slot->hbuf.resize(nranks);
                 slot->ready.resize(nranks);
                 slot->done.resize(nranks);
                 for (int q = 0; q < nranks; ++q) {
@@ -389,13 +447,16 @@ int eigsol_ctx_create_dist(int device, int rank, int nranks, const void* unique_
     return EIGSOL_OK;
 }
 
-// Collective over the context's communicator: every rank passes its own row block.
+// Collective over the context's communicator: every rank passes its own row block.  The setup
+// exchanges (ghost counts, request lists) are host all-gathers (coll_allgather), so the same code
+// serves RCCL, loopback and host-bootstrapped contexts.
 int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* row_begins,
                            int64_t nnz_local, const int32_t* rowptr_local,
                            const int32_t* colidx_global, const void* values, eigsol_csr** out) {
     if (!ctx || !out || !row_begins || !rowptr_local)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: null argument");
-    if (!ctx->comm && !ctx->loop) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
+    if (!ctx->comm && !ctx->loop && !ctx->hcoll)
+        return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
     *out = nullptr;
     const int P = ctx->nranks, me = ctx->rank;
     if (row_begins[0] != 0 || nnz_local < 0)
@@ -414,24 +475,9 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     EIGSOL_TRY(eigsol_ghost_plan(P, row_begins, me, nnz_local, colidx_global, col_local.data(),
                                  nghost.data(), ghosts.data(), recv.data()));
     EIGSOL_HIP(hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
-    ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
     // every rank learns how many entries each peer requests from it (P x P counts)
-    int64_t *d_counts = nullptr, *d_req = nullptr, *d_srcreq = nullptr;
-    EIGSOL_HIP(hipMalloc(&d_counts, sizeof(int64_t) * P * P));
-    EIGSOL_HIP(hipMemcpyAsync(d_counts + (size_t)me * P, recv.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice, st));
-    if (ctx->loop) {
-        std::vector<LoopSend> ls;
-        std::vector<LoopRecv> lr;
-        loop_allgather(ctx, d_counts, sizeof(int64_t) * P, ls, lr);
-        EIGSOL_TRY(loop_step(ctx, ls, lr));
-    } else {
-        EIGSOL_RCCL(ncclAllGather(d_counts + (size_t)me * P, d_counts, P, ncclInt64, comm, st));
-    }
-    std::vector<int64_t> all(P * P);
-    EIGSOL_HIP(hipMemcpyAsync(all.data(), d_counts, sizeof(int64_t) * P * P, hipMemcpyDeviceToHost, st));
-    EIGSOL_HIP(hipStreamSynchronize(st));
-    hipFree(d_counts);
+    std::vector<int64_t> all((size_t)P * P);
+    EIGSOL_TRY(coll_allgather(ctx, recv.data(), sizeof(int64_t) * P, all.data()));
     int mode = EIGSOL_EXCHANGE_HALO;
     EIGSOL_TRY(eigsol_exchange_mode(P, row_begins, all.data(), &mode));   // same decision on every rank
     if (mode == EIGSOL_EXCHANGE_ALLGATHER) {
@@ -459,34 +505,25 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
         roff[q + 1] = roff[q] + recv[q];
     }
     const int64_t nsend = soff[P];
-    // ship the request lists (global indices) to their owners
-    EIGSOL_HIP(hipMalloc(&d_srcreq, sizeof(int64_t) * std::max<int64_t>(nghost[0], 1)));
-    EIGSOL_HIP(hipMalloc(&d_req, sizeof(int64_t) * std::max<int64_t>(nsend, 1)));
-    if (nghost[0])
-        EIGSOL_HIP(hipMemcpyAsync(d_srcreq, ghosts.data(), sizeof(int64_t) * nghost[0], hipMemcpyHostToDevice, st));
-    if (ctx->loop) {
-        std::vector<LoopSend> ls;
-        std::vector<LoopRecv> lr;
-        for (int q = 0; q < P; ++q) {
-            if (q == me) continue;
-            if (recv[q]) ls.push_back({q, d_srcreq + roff[q], sizeof(int64_t) * recv[q]});
-            if (send[q]) lr.push_back({q, d_req + soff[q], sizeof(int64_t) * send[q]});
-        }
-        EIGSOL_TRY(loop_step(ctx, ls, lr));
-    } else {
-        EIGSOL_RCCL(ncclGroupStart());
-        for (int q = 0; q < P; ++q) {
-            if (q == me) continue;
-            if (recv[q]) EIGSOL_RCCL(ncclSend(d_srcreq + roff[q], recv[q], ncclInt64, q, comm, st));
-            if (send[q]) EIGSOL_RCCL(ncclRecv(d_req + soff[q], send[q], ncclInt64, q, comm, st));
-        }
-        EIGSOL_RCCL(ncclGroupEnd());
+    // request lists (global indices) to their owners: every rank's whole ghost list, padded to the
+    // longest, all-gathered; each rank keeps the part addressed to it (ghost lists are grouped by
+    // owner, so q's requests to me start at sum_{p < me} all[q][p])
+    int64_t maxg = 0;
+    for (int q = 0; q < P; ++q) {
+        int64_t g = 0;
+        for (int p = 0; p < P; ++p) g += all[(size_t)q * P + p];
+        maxg = std::max(maxg, g);
     }
+    std::vector<int64_t> mine(std::max<int64_t>(maxg, 1), -1), lists((size_t)P * std::max<int64_t>(maxg, 1));
+    std::copy(ghosts.begin(), ghosts.begin() + nghost[0], mine.begin());
+    EIGSOL_TRY(coll_allgather(ctx, mine.data(), sizeof(int64_t) * mine.size(), lists.data()));
     std::vector<int64_t> req(std::max<int64_t>(nsend, 1));
-    if (nsend) EIGSOL_HIP(hipMemcpyAsync(req.data(), d_req, sizeof(int64_t) * nsend, hipMemcpyDeviceToHost, st));
-    EIGSOL_HIP(hipStreamSynchronize(st));
-    hipFree(d_req);
-    hipFree(d_srcreq);
+    for (int q = 0; q < P; ++q) {
+        if (q == me || !send[q]) continue;
+        int64_t off = 0;
+        for (int p = 0; p < me; ++p) off += all[(size_t)q * P + p];
+        std::copy_n(lists.begin() + (size_t)q * mine.size() + off, send[q], req.begin() + soff[q]);
+    }
     int64_t nlow = 0;
     for (int q = 0; q < me; ++q) nlow += recv[q];
     std::vector<int32_t> send_idx(std::max<int64_t>(nsend, 1));
@@ -503,12 +540,20 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     A->n_global = n_global;
     A->row_begin = row_begins[me];
     A->nghost = nghost[0];
+    A->row_begins.assign(row_begins, row_begins + P + 1);
     A->send_counts = send;
     A->recv_counts = recv;
     A->send_offs.assign(soff.begin(), soff.end() - 1);
     A->recv_offs.assign(roff.begin(), roff.end() - 1);
     A->nsend = nsend;
+    A->h_send_idx.assign(send_idx.begin(), send_idx.begin() + nsend);
+    A->peer_dst_off.assign(P, 0);
+    for (int q = 0; q < P; ++q)
+        for (int p = 0; p < me; ++p) A->peer_dst_off[q] += all[(size_t)q * P + p];
+    A->ghost_counts = all;
+    A->requests.assign(req.begin(), req.begin() + nsend);
     const size_t sb = scalar_bytes(dtype);
+    hipStream_t st = ctx->stream;
     hipError_t e = hipMalloc(&A->send_idx, sizeof(int32_t) * std::max<int64_t>(nsend, 1));
     if (e == hipSuccess) e = hipMalloc(&A->send_buf, sb * std::max<int64_t>(nsend, 1));
     if (e == hipSuccess && nsend)
@@ -519,6 +564,47 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
         return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create_dist: ") + hipGetErrorString(e));
     }
     *out = A;
+    return EIGSOL_OK;
+}
+
+int eigsol_peer_plan(int nranks, int rank, const int64_t* row_begins, const int64_t* ghost_counts,
+                     const int64_t* requests, int64_t nreq, int32_t* push_out) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || !row_begins || !ghost_counts || nreq < 0 ||
+        (nreq && (!requests || !push_out)))
+        return fail(EIGSOL_E_INVALID, "eigsol_peer_plan: invalid argument");
+    const int P = nranks;
+    const int64_t r0 = row_begins[rank], nrows = row_begins[rank + 1] - r0;
+    std::vector<std::array<int32_t, 4>> ent;
+    ent.reserve(nreq);
+    int64_t k = 0;
+    for (int q = 0; q < P; ++q) {
+        if (q == rank) continue;
+        const int64_t cnt = ghost_counts[(size_t)q * P + rank];
+        int64_t base = 0;   // where this rank's rows start in q's ghost list
+        for (int p = 0; p < rank; ++p) base += ghost_counts[(size_t)q * P + p];
+        for (int64_t j = 0; j < cnt; ++j, ++k) {
+            if (k >= nreq) return fail(EIGSOL_E_INVALID, "eigsol_peer_plan: fewer requests than ghost counts");
+            const int64_t loc = requests[k] - r0;
+            if (loc < 0 || loc >= nrows) return fail(EIGSOL_E_INVALID, "eigsol_peer_plan: request outside own rows");
+            ent.push_back({(int32_t)loc, (int32_t)q, (int32_t)(base + j), 0});
+        }
+    }
+    if (k != nreq) return fail(EIGSOL_E_INVALID, "eigsol_peer_plan: more requests than ghost counts");
+    std::stable_sort(ent.begin(), ent.end(), [](const auto& x, const auto& y) { return x[0] < y[0]; });
+    for (size_t i = 0; i < ent.size(); ++i)
+        for (int c = 0; c < 4; ++c) push_out[4 * i + c] = ent[i][c];
+    return EIGSOL_OK;
+}
+
+int eigsol_ctx_create_dist_host(int device, int rank, int nranks, eigsol_allgather_fn allgather,
+                                void* user, eigsol_ctx** out) {
+    if (!out || !allgather || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(EIGSOL_E_INVALID, "eigsol_ctx_create_dist_host: invalid argument");
+    EIGSOL_TRY(eigsol_ctx_create(device, out));
+    (*out)->hcoll = allgather;
+    (*out)->hcoll_user = user;
+    (*out)->rank = rank;
+    (*out)->nranks = nranks;
     return EIGSOL_OK;
 }
 

@@ -88,6 +88,8 @@ struct alignas(64) PowerCtl {
     int32_t converged;
     int32_t final_parity;
     int32_t launches;        // launches that passed the done-check (diagnostic)
+    int32_t fault;           // row-sharded peer exchange: a wait for a peer timed out (host raises)
+    int32_t pad_;
     PowerCarry st[2];
 };
 
@@ -168,6 +170,10 @@ struct eigsol_ctx {
     // distributed (filled by eigsol_dist_* when a communicator is attached)
     void* comm = nullptr;
     void* loop = nullptr;   // in-process loopback world (tests: several ranks on one device), else null
+    // host-collective bootstrap (eigsol_ctx_create_dist_host): the caller's all-gather of host
+    // bytes, used for setup only; the per-iteration exchange then runs device to device
+    eigsol_allgather_fn hcoll = nullptr;
+    void* hcoll_user = nullptr;
     int rank = 0;
     int nranks = 1;
 };
@@ -208,6 +214,10 @@ struct eigsol_csr {
     int32_t* send_idx = nullptr;   // device: local row of every entry sent, grouped by peer
     void* send_buf = nullptr;      // device: packed halo values
     int64_t nsend = 0;
+    std::vector<int32_t> h_send_idx;     // host copy of send_idx (x-space slots of own rows)
+    std::vector<int64_t> peer_dst_off;   // per peer q: where my rows start in q's ghost list
+    std::vector<int64_t> ghost_counts;   // P x P: [r * P + q] = entries rank r reads from rank q
+    std::vector<int64_t> requests;       // global rows the peers read from this rank (by peer)
 };
 
 struct eigsol_dense {

@@ -115,6 +115,92 @@ __device__ __forceinline__ void last_arriver_reduce(double a, double b, double c
     }
 }
 
+// ------------------------------------------------------------------ device-side peer exchange
+// Every rank of a row-sharded session owns one inbox (fine-grained-free, uncached device memory,
+// exported to the other ranks by IPC handle or, in a loopback world, by plain pointer):
+//   flag[q]          epoch written by rank q: q has delivered everything of its launch flag - 2
+//   part[p][q]       rank q's partial sums of its launch t, p = t & 1
+//   ghosts[p][...]   x-space ghost entries (this rank's [lower | upper] ghost order) of y_t, p = t & 1
+// Producers store with system-scope (sc0 sc1) stores and drain them (s_waitcnt vmcnt(0)) before
+// the block's ticket; the last-arriving block then stores the partial and, after a second drain,
+// the flag.  Consumers poll the flag and read partials and ghosts with system-scope loads only
+// (MI355X_MICROARCH.md, inter-workgroup visibility: every store and every load of the handed-off
+// bytes bypasses the non-coherent caches, so no acquire fence is needed).
+constexpr int kMaxPeerRanks = 64;
+struct alignas(128) PeerInbox {
+    uint64_t flag[kMaxPeerRanks];
+    part4 part[2][kMaxPeerRanks];
+};
+constexpr int kGhostSliceBit = 1 << 20;   // slice meta .z: the slice reads ghost x entries
+
+struct PeerArgs {
+    PeerInbox* const* peers;   // peers[q]: rank q's inbox as mapped in this process (peers[me] = own)
+    PeerInbox* inbox;          // own inbox
+    const int4* push;          // {local row, peer, slot, 0} sorted by row
+    const int2* slice_push;    // per slice: [begin, end) of its rows' entries in push
+    int64_t ghost_stride;      // scalars per parity in a ghost area
+    int32_t me, P;
+};
+
+template <class S>
+__device__ __forceinline__ S* peer_ghosts(PeerInbox* b, int parity, int64_t stride) {
+    return reinterpret_cast<S*>(b + 1) + parity * stride;
+}
+__device__ __forceinline__ double ld_sys(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys_s(const double* p) { return ld_sys(p); }
+__device__ __forceinline__ cplx ld_sys_s(const cplx* p) {
+    return cplx{ld_sys(&p->re), ld_sys(&p->im)};
+}
+__device__ __forceinline__ void st_sys_s(double* p, double v) { st_sys(p, v); }
+__device__ __forceinline__ void st_sys_s(cplx* p, cplx v) {
+    st_sys(&p->re, v.re);
+    st_sys(&p->im, v.im);
+}
+
+// Poll budget of a peer wait: 10 s of the 100 MHz constant clock (s_memrealtime).  A wait that
+// runs out marks the session faulted instead of hanging the GPU.
+constexpr uint64_t kPeerWaitTicks = 1000000000ull;
+
+// Thread 0 only: wait until every peer's flag reached `epoch`; false on timeout.
+__device__ __forceinline__ bool peer_wait(PeerInbox* inbox, int P, int me, uint64_t epoch) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int q = 0; q < P; ++q) {
+        if (q == me) continue;
+        while (ld_sys(&inbox->flag[q]) < epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kPeerWaitTicks) return false;
+        }
+    }
+    return true;
+}
+
+// Thread 0 of the last-arriving block: this rank's partial to part[parity][me] of every inbox,
+// drained, then the epoch flag of every peer.
+__device__ __forceinline__ void peer_publish(const PeerArgs& pa, int parity, const part4& mine,
+                                             uint64_t epoch) {
+    for (int q = 0; q < pa.P; ++q) {
+        part4* d = &pa.peers[q]->part[parity][pa.me];
+        st_sys(&d->a, mine.a);
+        st_sys(&d->b, mine.b);
+        st_sys(&d->c, mine.c);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int q = 0; q < pa.P; ++q)
+        if (q != pa.me) st_sys(&pa.peers[q]->flag[pa.me], epoch);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Launch prologue of the fused power iteration, evaluated by thread 0 and broadcast through LDS.
 struct alignas(16) Prologue {
     double nrm;       // ||y_{t-1}||: x_t = y_{t-1} / nrm (nrm == 0 only at t == 0: x0 == 0, kept as is)
@@ -122,20 +208,37 @@ struct alignas(16) Prologue {
     int32_t t;
 };
 
+// peer != nullptr: row-sharded session on the device-side peer exchange — wait for every peer's
+// flag of the previous launch (epoch t + 1), then read the rank partials from the own inbox.
 template <class S>
 __device__ __forceinline__ void power_prologue(PowerCtl* ctl, const part4* rank_part, int nranks,
-                                               int parity, S* trace, Prologue* out) {
+                                               int parity, S* trace, Prologue* out,
+                                               const PeerArgs* peer = nullptr) {
     if (threadIdx.x == 0) {
         Prologue pr{0.0, 0, 0};
         const int done = __hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!done) {
-            const PowerCarry in = ctl->st[parity];
-            const int32_t t = in.t + 1;
+        const PowerCarry in = ctl->st[parity];
+        const int32_t t = in.t + 1;
+        bool ok = true;
+        if (!done && peer) {
+            ok = peer_wait(peer->inbox, peer->P, peer->me, (uint64_t)t + 1);
+            if (!ok) __hip_atomic_store(&ctl->fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!done && ok) {
             double n2 = 0.0, rr = 0.0, ri = 0.0;
-            for (int r = 0; r < nranks; ++r) {   // rank order: identical on every rank
-                n2 += rank_part[r].a;
-                rr += rank_part[r].b;
-                ri += rank_part[r].c;
+            if (peer) {
+                const part4* rp = peer->inbox->part[parity ^ 1];
+                for (int r = 0; r < nranks; ++r) {   // rank order: identical on every rank
+                    n2 += ld_sys(&rp[r].a);
+                    rr += ld_sys(&rp[r].b);
+                    ri += ld_sys(&rp[r].c);
+                }
+            } else {
+                for (int r = 0; r < nranks; ++r) {   // rank order: identical on every rank
+                    n2 += rank_part[r].a;
+                    rr += rank_part[r].b;
+                    ri += rank_part[r].c;
+                }
             }
             const double nrm = sqrt(n2);
             const bool cplx_ = dtype_of<S>::value == EIGSOL_C128;

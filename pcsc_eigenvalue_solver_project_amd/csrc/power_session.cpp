@@ -9,13 +9,21 @@
 #include <cstring>
 #include <vector>
 
-#include "internal.hpp"
+#include <chrono>
+#include <cstdlib>
+#include <thread>
+
+#include "kernels_common.hpp"
 
 namespace eigsol {
-int csr_grid(eigsol_csr* A, int* grid);
+int csr_grid(eigsol_csr* A, int* grid, bool peer = false);
 int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
                      const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
-                     int parity, int grid);
+                     int parity, int grid, const dev::PeerArgs* peer = nullptr);
+int peer_begin_launch(eigsol_ctx* ctx, int dtype, const dev::PeerArgs& pa, const void* x_own, int64_t npush,
+                      const void* mine);
+int coll_allgather(eigsol_ctx* ctx, const void* mine, size_t bytes, void* all);
+int coll_barrier(eigsol_ctx* ctx);
 int dense_grid(eigsol_dense* A, int* grid);
 int dense_power_launch(eigsol_dense* A, void* buf0, void* buf1, PowerCtl* ctl,
                        const void* rank_part, int nranks, void* my_part, void* blk_part,
@@ -37,6 +45,20 @@ void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* 
 }  // namespace eigsol
 
 using namespace eigsol;
+
+// Device-side peer exchange of a row-sharded session (EIGSOL_TRANSPORT_PEER): the own inbox, the
+// peers' inboxes mapped into this process, and the push plan.
+struct PeerState {
+    dev::PeerArgs args{};
+    void* inbox = nullptr;
+    size_t inbox_bytes = 0;
+    std::vector<void*> opened;    // IPC-opened peer inboxes (closed at destroy)
+    void* peers_dev = nullptr;    // device table of P inbox pointers
+    void* push_dev = nullptr;     // int4 push entries
+    void* slice_push_dev = nullptr;
+    int64_t npush = 0;
+    bool agreed = false;          // every rank finished setup: destroy is collective from here on
+};
 
 struct eigsol_power {
     eigsol_ctx* ctx = nullptr;
@@ -62,6 +84,8 @@ struct eigsol_power {
     bool trivial = false;     // maxIterations <= 0
     PowerCtl* host_ctl = nullptr;   // pinned mirror for polling
     eigsol_solver_options opts{1000, 1e-10};
+    int transport = EIGSOL_TRANSPORT_LOCAL;
+    PeerState* peer = nullptr;
 };
 
 static constexpr size_t kPart = 32;
@@ -84,10 +108,23 @@ static int session_alloc(eigsol_power* s, int32_t trace_cap) {
     return EIGSOL_OK;
 }
 
+static void peer_free(eigsol_power* s) {
+    PeerState* p = s->peer;
+    if (!p) return;
+    // collective: no rank releases its inbox while a peer may still store into it
+    if (p->agreed) (void)coll_barrier(s->ctx);
+    for (void* q : p->opened) (void)hipIpcCloseMemHandle(q);
+    for (void* q : {p->inbox, p->peers_dev, p->push_dev, p->slice_push_dev})
+        if (q) (void)hipFree(q);
+    delete p;
+    s->peer = nullptr;
+}
+
 static void session_free(eigsol_power* s) {
     if (!s) return;
     hipSetDevice(s->ctx->device);
     hipStreamSynchronize(s->ctx->stream);
+    peer_free(s);
     hipFree(s->buf[0]);
     hipFree(s->buf[1]);
     hipFree(s->ctl);
@@ -102,6 +139,9 @@ static void session_free(eigsol_power* s) {
 }
 
 static int launch_iteration(eigsol_power* s) {
+    if (s->peer)   // one launch: the epilogue delivers the halo and the partial to the peers
+        return csr_power_launch(s->csr, s->nbuf, s->buf[0], s->buf[1], s->ctl, s->rank_part, s->ctx->nranks,
+                                s->my_part, s->blk_part, s->trace, s->parity, s->grid, &s->peer->args);
     if (s->shift)
         return shift_iter_launch(s->shift, s->buf[0], s->buf[1], s->ctl, s->rank_part, s->my_part,
                                  s->trace, s->parity);
@@ -124,6 +164,124 @@ static int pull_ctl(eigsol_power* s) {
     return EIGSOL_OK;
 }
 
+// Inbox memory: uncached device memory by default (every access of the handed-off bytes is
+// system-scope anyway); EIGSOL_PEER_MEM=finegrained|coarse for experiments.
+static hipError_t peer_alloc(void** p, size_t bytes) {
+    const char* m = std::getenv("EIGSOL_PEER_MEM");
+    if (m && !std::strcmp(m, "coarse")) return hipMalloc(p, bytes);
+    if (m && !std::strcmp(m, "finegrained")) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
+    return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+}
+
+// Local part of the peer setup (allocation, address exchange, plan upload).  Returns EIGSOL_OK or
+// an error; the caller makes the outcome collective.
+static int peer_setup_local(eigsol_power* s) {
+    eigsol_csr* A = s->csr;
+    eigsol_ctx* ctx = s->ctx;
+    const int P = ctx->nranks, me = ctx->rank;
+    auto* p = new PeerState();
+    s->peer = p;
+    const size_t sb = scalar_bytes(s->dtype);
+    const int64_t stride = ((std::max<int64_t>(A->nghost, 1) + 15) / 16) * 16;
+    p->inbox_bytes = sizeof(dev::PeerInbox) + 2 * (size_t)stride * sb;
+    EIGSOL_HIP(peer_alloc(&p->inbox, p->inbox_bytes));
+    EIGSOL_HIP(hipMemset(p->inbox, 0, p->inbox_bytes));
+    std::vector<void*> table(P, nullptr);
+    if (ctx->loop) {
+        // one process: the other ranks' inboxes are plain device pointers
+        std::vector<uintptr_t> all(P);
+        const uintptr_t mine = reinterpret_cast<uintptr_t>(p->inbox);
+        EIGSOL_TRY(coll_allgather(ctx, &mine, sizeof(mine), all.data()));
+        for (int q = 0; q < P; ++q) table[q] = reinterpret_cast<void*>(all[q]);
+    } else {
+        hipIpcMemHandle_t h;
+        std::memset(&h, 0, sizeof(h));
+        const hipError_t e = hipIpcGetMemHandle(&h, p->inbox);
+        // a rank whose export failed still takes part in the all-gather (zero handle)
+        std::vector<hipIpcMemHandle_t> all(P);
+        EIGSOL_TRY(coll_allgather(ctx, &h, sizeof(h), all.data()));
+        if (e != hipSuccess) return fail(EIGSOL_E_HIP, std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e));
+        for (int q = 0; q < P; ++q) {
+            if (q == me) { table[q] = p->inbox; continue; }
+            void* ptr = nullptr;
+            EIGSOL_HIP(hipIpcOpenMemHandle(&ptr, all[q], hipIpcMemLazyEnablePeerAccess));
+            p->opened.push_back(ptr);
+            table[q] = ptr;
+        }
+    }
+    // push plan: {local row, peer, slot} sorted by row, and each slice's range of it
+    p->npush = A->nsend;
+    std::vector<int32_t> push(4 * std::max<int64_t>(p->npush, 1), 0);
+    EIGSOL_TRY(eigsol_peer_plan(P, me, A->row_begins.data(), A->ghost_counts.data(), A->requests.data(),
+                                A->nsend, push.data()));
+    std::vector<int32_t> sp(2 * std::max<int32_t>(A->nslices, 1), 0);
+    int64_t e = 0;
+    for (int32_t sl = 0; sl < A->nslices; ++sl) {
+        sp[2 * sl] = (int32_t)e;
+        while (e < p->npush && push[4 * e] < (sl + 1) * 64) ++e;
+        sp[2 * sl + 1] = (int32_t)e;
+    }
+    EIGSOL_HIP(hipMalloc(&p->peers_dev, sizeof(void*) * P));
+    EIGSOL_HIP(hipMalloc(&p->push_dev, push.size() * sizeof(int32_t)));
+    EIGSOL_HIP(hipMalloc(&p->slice_push_dev, sp.size() * sizeof(int32_t)));
+    EIGSOL_HIP(hipMemcpy(p->peers_dev, table.data(), sizeof(void*) * P, hipMemcpyHostToDevice));
+    EIGSOL_HIP(hipMemcpy(p->push_dev, push.data(), push.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    EIGSOL_HIP(hipMemcpy(p->slice_push_dev, sp.data(), sp.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    p->args.peers = static_cast<dev::PeerInbox* const*>(p->peers_dev);
+    p->args.inbox = static_cast<dev::PeerInbox*>(p->inbox);
+    p->args.push = static_cast<const int4*>(p->push_dev);
+    p->args.slice_push = static_cast<const int2*>(p->slice_push_dev);
+    p->args.ghost_stride = stride;
+    p->args.me = me;
+    p->args.P = P;
+    EIGSOL_TRY(csr_grid(A, &s->grid, true));
+    if (ctx->loop) {
+        // loopback ranks share one device: each rank's blocks must stay co-resident with the
+        // others' (a waiting launch must not keep a peer's producing launch off the CUs)
+        s->grid = std::max(8, (s->grid / P) / 8 * 8);
+    }
+    return EIGSOL_OK;
+}
+
+// Collective choice of the per-iteration transport of a row-sharded CSR session.
+static int choose_transport(eigsol_power* s) {
+    eigsol_csr* A = s->csr;
+    eigsol_ctx* ctx = s->ctx;
+    const int P = ctx->nranks;
+    const bool host_only = !ctx->comm && !ctx->loop;
+    int cand = (A->sliced && A->exchange == EIGSOL_EXCHANGE_HALO && P <= dev::kMaxPeerRanks) ? 1 : 0;
+    if (const char* e = std::getenv("EIGSOL_DIST_TRANSPORT"))
+        if (!std::strcmp(e, "collective") && !host_only) cand = 0;
+    std::vector<int> all(P);
+    EIGSOL_TRY(coll_allgather(ctx, &cand, sizeof(int), all.data()));
+    bool peer = true;
+    for (int v : all) peer = peer && v;
+    if (!peer) {
+        if (host_only)
+            return fail(EIGSOL_E_UNSUPPORTED, "row-sharded session on a host-bootstrapped context needs the "
+                                              "peer exchange (halo matrix in the sliced layout on every rank)");
+        s->transport = EIGSOL_TRANSPORT_COLLECTIVE;
+        return EIGSOL_OK;
+    }
+    int rc = peer_setup_local(s);
+    int ok = rc == EIGSOL_OK ? 1 : 0;
+    const std::string why = ok ? "" : eigsol_last_error();
+    EIGSOL_TRY(coll_allgather(ctx, &ok, sizeof(int), all.data()));
+    bool all_ok = true;
+    for (int v : all) all_ok = all_ok && v;
+    if (all_ok) {
+        s->peer->agreed = true;
+        s->transport = EIGSOL_TRANSPORT_PEER;
+        return EIGSOL_OK;
+    }
+    peer_free(s);   // not agreed: local teardown only
+    if (host_only)
+        return fail(EIGSOL_E_HIP, "peer exchange setup failed on some rank: " + why);
+    s->transport = EIGSOL_TRANSPORT_COLLECTIVE;   // RCCL / loopback copies
+    EIGSOL_TRY(csr_grid(A, &s->grid));
+    return EIGSOL_OK;
+}
+
 extern "C" {
 
 int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power** out) {
@@ -141,6 +299,7 @@ int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power*
     s->n = A->nrows;
     s->nbuf = A->ncols;
     int rc = csr_grid(A, &s->grid);
+    if (rc == EIGSOL_OK && s->dist) rc = choose_transport(s);
     if (rc == EIGSOL_OK) rc = session_alloc(s, trace_capacity);
     if (rc != EIGSOL_OK) { session_free(s); return rc; }
     *out = s;
@@ -193,9 +352,21 @@ int eigsol_power_begin(eigsol_power* s, const eigsol_solver_options* opts, const
     init.st[1].t = -1;
     std::memcpy(s->host_ctl, &init, sizeof(init));
     EIGSOL_HIP(hipMemcpyAsync(s->ctl, s->host_ctl, sizeof(PowerCtl), hipMemcpyHostToDevice, st));
+    if (s->peer) {
+        // fresh epochs: every rank's previous launches (and their stores into this inbox) are over
+        // before the inbox is cleared, and every inbox is clear before anyone publishes again
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        EIGSOL_TRY(coll_barrier(s->ctx));
+        EIGSOL_HIP(hipMemsetAsync(s->peer->inbox, 0, s->peer->inbox_bytes, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        EIGSOL_TRY(coll_barrier(s->ctx));
+    }
     // ||x0||^2 partials -> the input norm of launch 0 (x.normalize(), power_method.hpp:62)
     EIGSOL_TRY(norm_partial_launch(s->ctx, s->dtype, x0dst, s->n, s->ctl, s->blk_part, s->my_part, s->grid));
-    if (s->dist) EIGSOL_TRY(dist_exchange(s->csr, s->buf[1], s->rank_part));   // x0 ghosts + partials
+    if (s->peer)   // x0 halo + partial into every inbox (parity 1), epoch 1
+        EIGSOL_TRY(peer_begin_launch(s->ctx, s->dtype, s->peer->args, x0dst, s->peer->npush, s->my_part));
+    else if (s->dist)
+        EIGSOL_TRY(dist_exchange(s->csr, s->buf[1], s->rank_part));   // x0 ghosts + partials
     EIGSOL_HIP(hipStreamSynchronize(st));   // host_ctl is reused by query()
     s->parity = 0;
     s->launches = 0;
@@ -225,6 +396,9 @@ int eigsol_power_query(eigsol_power* s, int32_t* done, int32_t* launches) {
     EIGSOL_HIP(hipSetDevice(s->ctx->device));
     EIGSOL_TRY(pull_ctl(s));
     if (s->shift) EIGSOL_TRY(shift_error(s->shift));
+    if (s->host_ctl->fault)
+        return fail(EIGSOL_E_RCCL, "row-sharded peer exchange: a peer's data did not arrive within 10 s "
+                                   "(ranks stepping unevenly, or a peer failed)");
     if (done) *done = s->host_ctl->done;
     if (launches) *launches = s->host_ctl->launches;
     return EIGSOL_OK;
@@ -244,8 +418,28 @@ int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_ou
         // maxIterations <= 0: lambda = 0, x = normalised x0, 0 iterations (power_method.hpp:61-68)
         const int P = s->dist ? s->ctx->nranks : 1;
         std::vector<double> part(4 * P);
-        EIGSOL_HIP(hipMemcpyAsync(part.data(), s->rank_part, sizeof(double) * 4 * P, hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipStreamSynchronize(st));
+        if (s->peer) {
+            // the peers' x0 partials arrive in the inbox (parity 1) with epoch 1
+            dev::PeerInbox box;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (;;) {
+                EIGSOL_HIP(hipMemcpy(&box, s->peer->inbox, sizeof(box), hipMemcpyDeviceToHost));
+                bool all = true;
+                for (int q = 0; q < P; ++q) all = all && (q == s->ctx->rank || box.flag[q] >= 1);
+                if (all) break;
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                    return fail(EIGSOL_E_RCCL, "row-sharded peer exchange: start-vector partials did not arrive");
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+            for (int q = 0; q < P; ++q) {
+                part[4 * q] = box.part[1][q].a;
+                part[4 * q + 1] = box.part[1][q].b;
+                part[4 * q + 2] = box.part[1][q].c;
+            }
+        } else {
+            EIGSOL_HIP(hipMemcpyAsync(part.data(), s->rank_part, sizeof(double) * 4 * P, hipMemcpyDeviceToHost, st));
+            EIGSOL_HIP(hipStreamSynchronize(st));
+        }
         double n2 = 0.0;
         for (int r = 0; r < P; ++r) n2 += part[4 * r];   // rank order, as on the device
         fnorm = std::sqrt(n2);
@@ -292,6 +486,12 @@ int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int3
         }
     }
     if (count) *count = n;
+    return EIGSOL_OK;
+}
+
+int eigsol_power_transport(const eigsol_power* s, int* transport) {
+    if (!s || !transport) return fail(EIGSOL_E_INVALID, "eigsol_power_transport: null pointer");
+    *transport = s->transport;
     return EIGSOL_OK;
 }
 

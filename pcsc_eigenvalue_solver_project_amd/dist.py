@@ -69,6 +69,63 @@ def loopback_id(world: int) -> bytes:
     return bytes(buf)
 
 
+def peer_plan(nranks: int, rank: int, row_begins, ghost_counts, requests) -> np.ndarray:
+    """Host-only push plan of the device-side peer exchange (library function, no device): one row
+    {local row, peer, slot in the peer's ghost list, 0} per request, sorted by local row."""
+    rb = np.ascontiguousarray(row_begins, dtype=np.int64)
+    gc = np.ascontiguousarray(ghost_counts, dtype=np.int64)
+    rq = np.ascontiguousarray(requests, dtype=np.int64)
+    out = np.zeros((max(len(rq), 1), 4), dtype=np.int32)
+    call("eigsol_peer_plan", int(nranks), int(rank), _ptr(rb), _ptr(gc), _ptr(rq), len(rq), _ptr(out))
+    return out[: len(rq)]
+
+
+class HostDistContext(Context):
+    """A row-sharded context bootstrapped by a host all-gather (``eigsol_ctx_create_dist_host``):
+    no RCCL communicator; setup runs over ``allgather(bytes) -> list[bytes]`` (any host transport,
+    e.g. torch.distributed gloo) and the per-iteration exchange is device to device."""
+
+    def __init__(self, device: int, rank: int, world: int, allgather, stream=None):
+        from ._capi import ALLGATHER_FN
+
+        def _cb(send, recv, nbytes, _user):
+            try:
+                mine = C.string_at(send, nbytes)
+                parts = allgather(mine)
+                if len(parts) != world or any(len(p) != nbytes for p in parts):
+                    return 1
+                C.memmove(recv, b"".join(parts), nbytes * world)
+                return 0
+            except Exception:   # noqa: BLE001 - reported to the library as a failed collective
+                return 1
+
+        self._cb = ALLGATHER_FN(_cb)   # kept alive as long as the context
+        h = C.c_void_p()
+        call("eigsol_ctx_create_dist_host", int(device), int(rank), int(world), C.cast(self._cb, C.c_void_p),
+             None, C.byref(h))
+        self.handle = h
+        self.device = device
+        self.rank, self.world = rank, world
+        if stream is not None:
+            self.set_stream(stream)
+
+
+def torch_host_context(device: int, stream=None) -> HostDistContext:
+    """HostDistContext over an initialised torch.distributed process group (gloo: CPU tensors)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(), dist.get_world_size()
+
+    def allgather(b: bytes):
+        n = len(b)
+        mine = torch.frombuffer(bytearray(b), dtype=torch.uint8) if n else torch.zeros(0, dtype=torch.uint8)
+        out = [torch.zeros(n, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(out, mine)
+        return [bytes(t.numpy().tobytes()) for t in out]
+
+    return HostDistContext(device, rank, world, allgather, stream=stream)
+
+
 def torch_dist_context(device: int, stream=None) -> DistContext:
     """Bootstrap from an initialised torch.distributed process group (gloo or nccl)."""
     import torch

@@ -11,7 +11,10 @@
                 d* = 1.5 e^{0.7i} isolated by 0.05 (the eigenvalues are the diagonal).
 
 All generators return CSR arrays (rowptr int32, colidx int32 sorted per row, values) for rows
-[row0, row0 + nrows) of an n_global x n_global matrix.
+[row0, row0 + nrows) of an n_global x n_global matrix.  band / uniform / start_vector draw their
+random numbers in fixed chunks of CHUNK rows seeded by the chunk index, so any row block is
+bitwise the same rows of the unsplit matrix (BASELINE config 4 is one 10M matrix split over the
+ranks: the N-rank matrix is the N = 1 matrix).
 """
 from __future__ import annotations
 
@@ -26,34 +29,63 @@ def _distinct_sorted(rng, nrows: int, k: int, span: int) -> np.ndarray:
     return r
 
 
+CHUNK = 1 << 16   # rows per generator chunk: chunk c is drawn from default_rng([seed, c, tag])
+
+
+def _chunks(row0: int, nrows: int):
+    """(chunk index, first row of the chunk, rows [a, b) of the request inside it)."""
+    c0, c1 = row0 // CHUNK, (row0 + nrows + CHUNK - 1) // CHUNK
+    for c in range(c0, c1):
+        base = c * CHUNK
+        yield c, base, max(row0, base), min(row0 + nrows, base + CHUNK)
+
+
 def band(n_global: int, k: int, w: int = 64, seed: int = 42, row0: int = 0, nrows: int | None = None,
          spike: float = 10.0):
+    """Rows [row0, row0 + nrows) of the band matrix.  Partition-invariant: rows are generated in
+    fixed chunks of CHUNK rows seeded by the chunk index, so the rows of any row block are bitwise
+    the rows of the whole matrix (a matrix split over N ranks is the N = 1 matrix)."""
     if nrows is None:
         nrows = n_global - row0
     width = 2 * w + 1
     if n_global < width or k > width:
         raise ValueError("band: n_global must be >= 2w+1 and k <= 2w+1")
-    rng = np.random.default_rng([seed, row0])
-    rows = np.arange(row0, row0 + nrows, dtype=np.int64)
-    start = np.clip(rows - w, 0, n_global - width)
-    cols = start[:, None] + _distinct_sorted(rng, nrows, k, width)
-    vals = rng.uniform(-1.0, 1.0, size=(nrows, k))
+    cols = np.empty((nrows, k), dtype=np.int64)
+    vals = np.empty((nrows, k), dtype=np.float64)
+    for c, base, a, b in _chunks(row0, nrows):
+        m = min(CHUNK, n_global - base)
+        rng = np.random.default_rng([seed, c, 0])
+        rows = np.arange(base, base + m, dtype=np.int64)
+        start = np.clip(rows - w, 0, n_global - width)
+        cc = start[:, None] + _distinct_sorted(rng, m, k, width)
+        vv = rng.uniform(-1.0, 1.0, size=(m, k))
+        cols[a - row0:b - row0] = cc[a - base:b - base]
+        vals[a - row0:b - row0] = vv[a - base:b - base]
     s = n_global // 2
     if row0 <= s < row0 + nrows:
         i = s - row0
         c0 = min(max(s - k // 2, 0), n_global - k)
         cols[i] = np.arange(c0, c0 + k)
+        vals[i] = 0.0
+        vals[i, :] = np.random.default_rng([seed, s, 2]).uniform(-1.0, 1.0, size=k)
         vals[i, s - c0] = spike
     rowptr = np.arange(0, (nrows + 1) * k, k, dtype=np.int64)
     return rowptr.astype(np.int32), cols.reshape(-1).astype(np.int32), vals.reshape(-1)
 
 
 def uniform(n_global: int, k: int, seed: int = 42, row0: int = 0, nrows: int | None = None):
+    """Rows [row0, row0 + nrows) of the uniform-column matrix (partition-invariant, see band)."""
     if nrows is None:
         nrows = n_global - row0
-    rng = np.random.default_rng([seed, row0, 1])
-    cols = _distinct_sorted(rng, nrows, k, n_global)
-    vals = 1.0 - rng.random(size=(nrows, k))   # (0, 1]
+    cols = np.empty((nrows, k), dtype=np.int64)
+    vals = np.empty((nrows, k), dtype=np.float64)
+    for c, base, a, b in _chunks(row0, nrows):
+        m = min(CHUNK, n_global - base)
+        rng = np.random.default_rng([seed, c, 1])
+        cc = _distinct_sorted(rng, m, k, n_global)
+        vv = 1.0 - rng.random(size=(m, k))   # (0, 1]
+        cols[a - row0:b - row0] = cc[a - base:b - base]
+        vals[a - row0:b - row0] = vv[a - base:b - base]
     rowptr = np.arange(0, (nrows + 1) * k, k, dtype=np.int64)
     return rowptr.astype(np.int32), cols.reshape(-1).astype(np.int32), vals.reshape(-1)
 
@@ -108,11 +140,17 @@ def triu_complex(n: int, k: int, seed: int = 42, target=1.5 * np.exp(0.7j), gap:
 
 
 def start_vector(n: int, dtype=np.float64, seed: int = 7, row0: int = 0) -> np.ndarray:
-    """x0 of SURVEY §8d: U(-1, 1) per (re, im) component, seed 7 (normalised by the solver)."""
-    rng = np.random.default_rng([seed, row0])
-    x = rng.uniform(-1.0, 1.0, n)
-    if np.dtype(dtype) == np.complex128:
-        x = x + 1j * rng.uniform(-1.0, 1.0, n)
+    """x0 of SURVEY §8d: U(-1, 1) per (re, im) component, seed 7 (normalised by the solver).
+    Entries [row0, row0 + n) of the global start vector, drawn in the generators' fixed chunks, so
+    a row block's slice is bitwise the slice of the N = 1 vector."""
+    x = np.empty(n, dtype=np.complex128 if np.dtype(dtype) == np.complex128 else np.float64)
+    for c, base, a, b in _chunks(row0, n):
+        rng = np.random.default_rng([seed, c, 3])
+        re = rng.uniform(-1.0, 1.0, CHUNK)
+        if np.dtype(dtype) == np.complex128:
+            x[a - row0:b - row0] = re[a - base:b - base] + 1j * rng.uniform(-1.0, 1.0, CHUNK)[a - base:b - base]
+        else:
+            x[a - row0:b - row0] = re[a - base:b - base]
     return x.astype(dtype)
 
 

@@ -22,3 +22,10 @@ def ctx():
     c = E.Context(0)
     yield c
     c.close()
+
+
+# Loopback worlds run several ranks' streams on one GPU, and a peer-exchange launch waits inside
+# the kernel for the other ranks' launches: each rank's stream needs a hardware queue of its own
+# (HIP's default of 4 would put two ranks' launches one behind the other in a shared queue).
+# Read by HIP at its initialisation, which happens after conftest is imported.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")

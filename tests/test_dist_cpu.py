@@ -257,3 +257,125 @@ def test_row_sharded_allgather_exchange_gloo():
     ref = O.power_csc(cp, ri, vv, S.start_vector(n), 200, 1e-12)
     assert abs(res[0][2] - ref["iterations"]) <= 1
     assert abs(res[0][1] - ref["eigenvalue"]) <= 1e-10 * (1 + abs(ref["eigenvalue"]))
+
+
+def _worker_peer(rank, world, port, out_q):
+    """The device-side peer exchange's plan and protocol, restated on gloo: every rank's inbox is
+    its ghost list [lower | upper] (parity double-buffered); the push plan from the library
+    (eigsol_peer_plan) says which own row goes to which slot of which peer; each "launch" computes
+    y = A (y_prev / ||y_prev||) reading own rows from its vector and ghosts from its inbox, then
+    pushes its halo rows and its partial sums to the peers (here: gloo all_gather of the (peer,
+    slot, value) triples), and the next launch sums the partials in rank order."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pcsc_eigenvalue_solver_project_amd import dist as D
+        from pcsc_eigenvalue_solver_project_amd import synthetic as S
+        n = 3000
+        rb = np.array([0, 1300, n], dtype=np.int64)           # uneven blocks
+        r0, r1 = int(rb[rank]), int(rb[rank + 1])
+        lrp, lci, lv = S.band(n, 10, row0=r0, nrows=r1 - r0)
+        cl, ghosts, recv = D.ghost_plan(world, rb, rank, lci)
+        nown = r1 - r0
+        nlow = int(np.searchsorted(ghosts, r0))
+
+        def allgather_obj(obj):
+            out = [None] * world
+            dist.all_gather_object(out, obj)
+            return out
+
+        counts = np.array(allgather_obj(recv.tolist()), dtype=np.int64)   # P x P
+        lists = allgather_obj(ghosts.tolist())
+        # requests to me, grouped by requesting rank (rank order), as eigsol_csr_create_dist does
+        req = []
+        for q in range(world):
+            if q == rank:
+                continue
+            off = int(counts[q, :rank].sum())
+            req += lists[q][off:off + int(counts[q, rank])]
+        push = D.peer_plan(world, rank, rb, counts, np.array(req, dtype=np.int64))
+        assert np.all(np.diff(push[:, 0]) >= 0)                # sorted by local row
+        # every entry lands on the peer's ghost slot holding exactly that global row
+        for (row, q, slot, _z) in push:
+            assert lists[q][slot] == r0 + row
+        Aloc = sp.csr_matrix((lv, cl, lrp), shape=(nown, nown + len(ghosts)))
+
+        def xspace(own, inbox):
+            return np.concatenate([inbox[:nlow], own, inbox[nlow:]])
+
+        def exchange(own, part):
+            """push halo rows + partial; returns (my inbox, partials of all ranks in rank order)."""
+            trip = [(int(q), int(slot), float(own[row])) for (row, q, slot, _z) in push]
+            got = allgather_obj((trip, part))
+            inbox = np.full(len(ghosts), np.nan)
+            for q in range(world):
+                for (dst, slot, val) in got[q][0]:
+                    if dst == rank:
+                        inbox[slot] = val
+            assert not np.any(np.isnan(inbox))                   # every ghost delivered
+            return inbox, [got[q][1] for q in range(world)]
+
+        x0 = S.start_vector(nown, row0=r0)
+        inbox, parts = exchange(x0, [float(np.sum(x0 * x0)), 0.0])
+        assert np.array_equal(xspace(x0, inbox)[cl], S.start_vector(n)[lci])   # ghosts bitwise
+        y, rho_prev, lam, it = x0, None, 0.0, 0
+        for t in range(300):
+            n2 = sum(p[0] for p in parts)                         # rank order
+            rho = sum(p[1] for p in parts)
+            nrm = np.sqrt(n2)
+            if t >= 2:                                            # power_decide
+                k = t - 2
+                lam = rho
+                it = k + 1
+                if k >= 1 and abs(rho - rho_prev) <= 1e-12 * (1 + abs(rho)):
+                    break
+            rho_prev = rho
+            xs = xspace(y, inbox) / nrm
+            ynew = Aloc @ xs
+            part = [float(np.dot(ynew, ynew)), float(np.dot(xs[nlow:nlow + nown], ynew))]
+            y = ynew
+            inbox, parts = exchange(y, part)
+        out_q.put((rank, lam, it))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_peer_exchange_plan_and_protocol_gloo():
+    import torch.multiprocessing as mp
+    from oracle import oracle as O
+    from pcsc_eigenvalue_solver_project_amd import synthetic as S
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_peer, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1:] == res[1][1:]                          # identical decisions on every rank
+    n = 3000
+    rp, ci, v = S.band(n, 10)
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    ref = O.power_csc(cp, ri, vv, S.start_vector(n), 300, 1e-12)
+    assert abs(res[0][2] - ref["iterations"]) <= 1
+    assert abs(res[0][1] - ref["eigenvalue"]) <= 1e-10 * (1 + abs(ref["eigenvalue"]))
+
+
+def test_peer_plan_errors():
+    from pcsc_eigenvalue_solver_project_amd import dist as D
+    from pcsc_eigenvalue_solver_project_amd import EigSolError
+    rb = np.array([0, 10, 20], dtype=np.int64)
+    counts = np.array([[0, 2], [3, 0]], dtype=np.int64)     # rank 1 reads 3 rows of rank 0
+    p = D.peer_plan(2, 0, rb, counts, np.array([9, 2, 5], dtype=np.int64))
+    assert p.tolist() == [[2, 1, 1, 0], [5, 1, 2, 0], [9, 1, 0, 0]]
+    with pytest.raises(EigSolError):                         # request outside own rows
+        D.peer_plan(2, 0, rb, counts, np.array([9, 2, 15], dtype=np.int64))
+    with pytest.raises(EigSolError):                         # count mismatch
+        D.peer_plan(2, 0, rb, counts, np.array([9, 2], dtype=np.int64))
