@@ -182,7 +182,14 @@ static int peer_setup_local(eigsol_power* s) {
     auto* p = new PeerState();
     s->peer = p;
     const size_t sb = scalar_bytes(s->dtype);
-    const int64_t stride = ((std::max<int64_t>(A->nghost, 1) + 15) / 16) * 16;
+    // one ghost-area stride for every rank: a pusher addresses the peer's parity-1 area with it
+    int64_t gmax = 1;
+    for (int q = 0; q < P; ++q) {
+        int64_t g = 0;
+        for (int r = 0; r < P; ++r) g += A->ghost_counts[(size_t)q * P + r];
+        gmax = std::max(gmax, g);
+    }
+    const int64_t stride = ((gmax + 15) / 16) * 16;
     p->inbox_bytes = sizeof(dev::PeerInbox) + 2 * (size_t)stride * sb;
     EIGSOL_HIP(peer_alloc(&p->inbox, p->inbox_bytes));
     EIGSOL_HIP(hipMemset(p->inbox, 0, p->inbox_bytes));
