@@ -172,17 +172,18 @@ __device__ __forceinline__ void st_sys_s(cplx* p, cplx v) {
 // runs out marks the session faulted instead of hanging the GPU.
 constexpr uint64_t kPeerWaitTicks = 1000000000ull;
 
-// Thread 0 only: wait until every peer's flag reached `epoch`; false on timeout.
-__device__ __forceinline__ bool peer_wait(PeerInbox* inbox, int P, int me, uint64_t epoch) {
+// Thread 0 only: wait until every peer's flag reached `epoch`; on timeout returns 1 + the peer
+// that did not deliver (0: all delivered).
+__device__ __forceinline__ int peer_wait(PeerInbox* inbox, int P, int me, uint64_t epoch) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (int q = 0; q < P; ++q) {
         if (q == me) continue;
         while (ld_sys(&inbox->flag[q]) < epoch) {
             __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kPeerWaitTicks) return false;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kPeerWaitTicks) return 1 + q;
         }
     }
-    return true;
+    return 0;
 }
 
 // Thread 0 of the last-arriving block: this rank's partial to part[parity][me] of every inbox,
@@ -216,13 +217,19 @@ __device__ __forceinline__ void power_prologue(PowerCtl* ctl, const part4* rank_
                                                const PeerArgs* peer = nullptr) {
     if (threadIdx.x == 0) {
         Prologue pr{0.0, 0, 0};
-        const int done = __hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int done = __hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const PowerCarry in = ctl->st[parity];
         const int32_t t = in.t + 1;
         bool ok = true;
         if (!done && peer) {
-            ok = peer_wait(peer->inbox, peer->P, peer->me, (uint64_t)t + 1);
-            if (!ok) __hip_atomic_store(&ctl->fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // a faulted session stops at once (later launches must not wait again)
+            ok = __hip_atomic_load(&ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+            const int miss = ok ? peer_wait(peer->inbox, peer->P, peer->me, (uint64_t)t + 1) : 0;
+            if (miss) {
+                ok = false;
+                // which peer, at which launch: (peer + 1) | t << 8
+                __hip_atomic_store(&ctl->fault, miss | (t << 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (!done && ok) {
             double n2 = 0.0, rr = 0.0, ri = 0.0;

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <thread>
 
@@ -241,6 +242,12 @@ static int peer_setup_local(eigsol_power* s) {
     p->args.ghost_stride = stride;
     p->args.me = me;
     p->args.P = P;
+    if (std::getenv("EIGSOL_PEER_DEBUG")) {
+        std::fprintf(stderr, "[peer] rank %d/%d inbox %p table", me, P, p->inbox);
+        for (int q = 0; q < P; ++q) std::fprintf(stderr, " %p", table[q]);
+        std::fprintf(stderr, " npush %lld nghost %lld stride %lld slices %d\n", (long long)p->npush,
+                     (long long)A->nghost, (long long)stride, A->nslices);
+    }
     EIGSOL_TRY(csr_grid(A, &s->grid, true));
     if (ctx->loop) {
         // loopback ranks share one device: each rank's blocks must stay co-resident with the
@@ -259,6 +266,13 @@ static int choose_transport(eigsol_power* s) {
     int cand = (A->sliced && A->exchange == EIGSOL_EXCHANGE_HALO && P <= dev::kMaxPeerRanks) ? 1 : 0;
     if (const char* e = std::getenv("EIGSOL_DIST_TRANSPORT"))
         if (!std::strcmp(e, "collective") && !host_only) cand = 0;
+    if (ctx->loop) {
+        // Loopback ranks share one device: a waiting launch sits at the head of its stream's
+        // hardware queue, so every rank needs a queue of its own (HIP maps streams onto
+        // GPU_MAX_HW_QUEUES queues, default 4) or a rank's launch can queue behind a waiting one.
+        const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+        if ((q ? std::atoi(q) : 4) < P + 1) cand = 0;
+    }
     std::vector<int> all(P);
     EIGSOL_TRY(coll_allgather(ctx, &cand, sizeof(int), all.data()));
     bool peer = true;
@@ -403,9 +417,19 @@ int eigsol_power_query(eigsol_power* s, int32_t* done, int32_t* launches) {
     EIGSOL_HIP(hipSetDevice(s->ctx->device));
     EIGSOL_TRY(pull_ctl(s));
     if (s->shift) EIGSOL_TRY(shift_error(s->shift));
-    if (s->host_ctl->fault)
-        return fail(EIGSOL_E_RCCL, "row-sharded peer exchange: a peer's data did not arrive within 10 s "
-                                   "(ranks stepping unevenly, or a peer failed)");
+    if (s->host_ctl->fault) {
+        std::string flags;
+        if (s->peer) {
+            dev::PeerInbox box;
+            if (hipMemcpy(&box, s->peer->inbox, sizeof(box), hipMemcpyDeviceToHost) == hipSuccess)
+                for (int q = 0; q < s->ctx->nranks; ++q) flags += (q ? "," : "") + std::to_string(box.flag[q]);
+        }
+        return fail(EIGSOL_E_RCCL, "row-sharded peer exchange: inbox flags [" + flags + "]; rank " +
+                                       std::to_string(s->ctx->rank) +
+                                       " waited 10 s for peer " + std::to_string((s->host_ctl->fault & 0xff) - 1) +
+                                       " at launch " + std::to_string(s->host_ctl->fault >> 8) +
+                                       " (ranks stepping unevenly, or a peer failed)");
+    }
     if (done) *done = s->host_ctl->done;
     if (launches) *launches = s->host_ctl->launches;
     return EIGSOL_OK;

@@ -27,5 +27,7 @@ def ctx():
 # Loopback worlds run several ranks' streams on one GPU, and a peer-exchange launch waits inside
 # the kernel for the other ranks' launches: each rank's stream needs a hardware queue of its own
 # (HIP's default of 4 would put two ranks' launches one behind the other in a shared queue).
-# Read by HIP at its initialisation, which happens after conftest is imported.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# Read by HIP at its initialisation, which happens after conftest is imported.  The GPU box
+# exports 4, so raise it (16 is within what the pool allows).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"

@@ -1,0 +1,90 @@
+"""Loopback probe of the device-side peer exchange: P ranks (threads) on one GPU, band matrix of
+n rows split in P, fixed number of launches (tol < 0), per-rank wall time per launch and errors.
+Also the exchange latency: tiny blocks (the SpMV is negligible) at P ranks vs the same rows on
+one rank without exchange.
+
+  python tools/peer_probe.py --ranks 1 2 4 8 --n 10000000 --steps 200
+"""
+import argparse
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:   # the box exports 4: one queue per rank
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
+import pcsc_eigenvalue_solver_project_amd as E  # noqa: E402
+from pcsc_eigenvalue_solver_project_amd import dist as D  # noqa: E402
+from pcsc_eigenvalue_solver_project_amd import synthetic as S  # noqa: E402
+
+
+def run(P, rp, ci, v, x0, n, steps, warm):
+    rb = np.linspace(0, n, P + 1).astype(np.int64)
+    uid = D.loopback_id(P) if P > 1 else None
+    res, errs = [None] * P, []
+    gate = threading.Barrier(P)
+
+    def rank_main(r):
+        try:
+            r0, r1 = int(rb[r]), int(rb[r + 1])
+            lrp = (rp[r0:r1 + 1] - rp[r0]).astype(np.int32)
+            if P > 1:
+                ctx = D.DistContext(0, r, P, uid)
+                A = D.DistCsrMatrix(ctx, rb, lrp, ci[rp[r0]:rp[r1]], v[rp[r0]:rp[r1]])
+            else:
+                ctx = E.Context(0)
+                A = E.CsrMatrix(ctx, lrp, ci[rp[r0]:rp[r1]], v[rp[r0]:rp[r1]], (n, n))
+            s = E.PowerSession(A)
+            s.begin(E.SolverOptions(2**31 - 1, -1.0), x0[r0:r1])
+            s.step(warm)
+            s.query()
+            gate.wait()
+            t = time.perf_counter()
+            s.step(steps)
+            s.query()
+            dt = time.perf_counter() - t
+            res[r] = (dt / steps * 1e6, s.transport(), s.kernel_info()["grid"])
+            s.close()
+            A.close()
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errs.append((r, repr(e)))
+            try:
+                gate.abort()
+            except Exception:  # noqa: BLE001
+                pass
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    alive = [i for i, t in enumerate(ts) if t.is_alive()]
+    return res, errs, alive
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warm", type=int, default=20)
+    a = ap.parse_args()
+    rp, ci, v = S.band(a.n, 10)
+    x0 = S.start_vector(a.n)
+    for P in a.ranks:
+        res, errs, alive = run(P, rp, ci, v, x0, a.n, a.steps, a.warm)
+        print(f"P={P} n={a.n}: us/launch per rank {[None if r is None else round(r[0], 1) for r in res]} "
+              f"transport {[None if r is None else r[1] for r in res]} grid {[None if r is None else r[2] for r in res]} "
+              f"errors {errs} hung {alive}", flush=True)
+        if alive:
+            break
+
+
+if __name__ == "__main__":
+    main()
