@@ -105,8 +105,10 @@ def test_config4_strong_split_peer_exchange(world, band10m):
 
 
 def test_peer_exchange_matches_collective_exchange(monkeypatch):
-    """Same split matrix, peer transport vs the host-enqueued pack + copies transport: the same
-    partials in the same rank order, so the eigenvalue and the iteration count agree bitwise."""
+    """Same split matrix, peer transport vs the host-enqueued pack + copies transport.  Every row
+    sum is the same single-lane ascending-column sum, but the two transports launch different grids
+    (loopback peer ranks take 1/P of the chip each), so the in-launch block partials of ||y||^2
+    and x^H y are added in a different order: agreement to rounding, identical iteration count."""
     n = 400_000
     rp, ci, v = S.band(n, 12)
     x0 = S.start_vector(n)
@@ -115,10 +117,12 @@ def test_peer_exchange_matches_collective_exchange(monkeypatch):
                              monkeypatch=monkeypatch)
     assert all(o[1] == _capi.EIGSOL_TRANSPORT_PEER for o in peer)
     assert all(o[1] == _capi.EIGSOL_TRANSPORT_COLLECTIVE for o in coll)
-    assert peer[0][0].eigenvalue == coll[0][0].eigenvalue
+    assert abs(peer[0][0].eigenvalue - coll[0][0].eigenvalue) <= 1e-13 * abs(coll[0][0].eigenvalue)
     assert peer[0][0].iterations == coll[0][0].iterations
-    assert np.array_equal(np.concatenate([o[0].eigenvector for o in peer]),
-                          np.concatenate([o[0].eigenvector for o in coll]))
+    xp = np.concatenate([o[0].eigenvector for o in peer])
+    xc = np.concatenate([o[0].eigenvector for o in coll])
+    assert np.max(np.abs(xp - xc)) <= 1e-13
+    assert abs(abs(np.vdot(xp, xc)) - 1) <= 1e-13
 
 
 def test_peer_exchange_edge_cases():
