@@ -57,7 +57,7 @@ def test_reference_shaped_caller(tmp_path):
     assert "Converged              : true" in qa.splitlines()[1]
     # diag of the converged H holds the three eigenvalues (positional, like the reference)
     diag = qa.split("Eigenvalues (diag of H): \n")[1].splitlines()[0]
-    got = sorted(complex(t.replace(",", "+").replace("+-", "-").strip("()") + "j") for t in diag.split())
+    got = [complex(t.replace(",", "+").replace("+-", "-").strip("()") + "j") for t in diag.split()]
     want = sorted([1 + 3j, 2 + 4j, 5 - 1j], key=lambda z: (z.real, z.imag))
     got = sorted(got, key=lambda z: (z.real, z.imag))
     assert all(abs(g - w) < 1e-8 for g, w in zip(got, want)), diag
