@@ -57,10 +57,13 @@ concept ScalarConcept = std::is_floating_point_v<S> || is_complex_of_floating<S>
 template <typename S>
 inline constexpr bool DeviceScalar = std::is_same_v<S, double> || std::is_same_v<S, std::complex<double>>;
 
-// float and std::complex<float> run on the same kernels: the matrix, start vector and shift are
-// promoted to double on the host and the results rounded back (a deliberate deviation: the
-// arithmetic is fp64, at least as accurate as the reference's single precision; convergence is
-// tested in fp64 at the requested tolerance).  long double has no device path (no 80-bit on the GPU).
+// float and std::complex<float> have native single-precision kernels for the power method (CSR
+// and dense), plain products and the triangular-CSR shifted inverse (values stored and multiplied
+// in single precision, norm/dot partials in double).  The other solvers (dense and general-sparse
+// shifted inverse, solve_shifted on a non-triangular matrix, Hessenberg, QR) promote the matrix,
+// vectors and shift to double on the host and round the results back (a deliberate deviation:
+// fp64 arithmetic, at least as accurate as the reference's single precision).  long double has no
+// device path (no 80-bit arithmetic on the GPU).
 template <typename S>
 inline constexpr bool PromotedScalar = std::is_same_v<S, float> || std::is_same_v<S, std::complex<float>>;
 template <typename S>

@@ -101,33 +101,24 @@ public:
     std::int64_t rows() const { return visit([](const auto& m) { return m.rows(); }); }
     std::int64_t cols() const { return visit([](const auto& m) { return m.cols(); }); }
 
-    // Device mirror (created on first use by the solvers).
-    // float / complex<float> storage is uploaded promoted to double (device_scalar_t).
+    // Device mirror (created on first use by the solvers) in the storage's own precision
+    // (double, float and their complex types all have device storage).
     template <typename S>
     const detail::DeviceMatrix& device() const {
-        using D = device_scalar_t<S>;
-        if (!dev_) {
-            if (dense_) {
-                const auto& d = cast<DenseMatrix<S>>();
-                if constexpr (std::is_same_v<D, S>) {
-                    dev_ = detail::DeviceMatrix::dense(detail::dtype_of<D>(), d.rows(), d.cols(), d.data());
-                } else {
-                    std::vector<D> w(d.data(), d.data() + d.size());
-                    dev_ = detail::DeviceMatrix::dense(detail::dtype_of<D>(), d.rows(), d.cols(), w.data());
-                }
-            } else {
-                const auto& s = cast<SparseMatrix<S>>();
-                if constexpr (std::is_same_v<D, S>) {
-                    dev_ = detail::DeviceMatrix::csc(detail::dtype_of<D>(), s.rows(), s.cols(), s.nonZeros(),
-                                                     s.outerIndexPtr(), s.innerIndexPtr(), s.valuePtr());
-                } else {
-                    std::vector<D> w(s.valuePtr(), s.valuePtr() + s.nonZeros());
-                    dev_ = detail::DeviceMatrix::csc(detail::dtype_of<D>(), s.rows(), s.cols(), s.nonZeros(),
-                                                     s.outerIndexPtr(), s.innerIndexPtr(), w.data());
-                }
-            }
-        }
+        if (!dev_) dev_ = upload<S, S>();
         return *dev_;
+    }
+    // fp64 mirror for the solvers without single-precision kernels (float / complex<float>
+    // storage promoted on upload; the same mirror as device<S>() for double scalars).
+    template <typename S>
+    const detail::DeviceMatrix& device_fp64() const {
+        using D = device_scalar_t<S>;
+        if constexpr (std::is_same_v<D, S>) {
+            return device<S>();
+        } else {
+            if (!dev64_) dev64_ = upload<S, D>();
+            return *dev64_;
+        }
     }
 
 private:
@@ -158,10 +149,33 @@ private:
         return -1;
     }
 
+    template <typename S, typename D>
+    std::shared_ptr<detail::DeviceMatrix> upload() const {
+        if (dense_) {
+            const auto& d = cast<DenseMatrix<S>>();
+            if constexpr (std::is_same_v<D, S>) {
+                return detail::DeviceMatrix::dense(detail::dtype_of<D>(), d.rows(), d.cols(), d.data());
+            } else {
+                std::vector<D> w(d.data(), d.data() + d.size());
+                return detail::DeviceMatrix::dense(detail::dtype_of<D>(), d.rows(), d.cols(), w.data());
+            }
+        }
+        const auto& s = cast<SparseMatrix<S>>();
+        if constexpr (std::is_same_v<D, S>) {
+            return detail::DeviceMatrix::csc(detail::dtype_of<D>(), s.rows(), s.cols(), s.nonZeros(),
+                                             s.outerIndexPtr(), s.innerIndexPtr(), s.valuePtr());
+        } else {
+            std::vector<D> w(s.valuePtr(), s.valuePtr() + s.nonZeros());
+            return detail::DeviceMatrix::csc(detail::dtype_of<D>(), s.rows(), s.cols(), s.nonZeros(),
+                                             s.outerIndexPtr(), s.innerIndexPtr(), w.data());
+        }
+    }
+
     bool dense_;
     const std::type_info* scalar_;
     std::unique_ptr<Box> box_;
     mutable std::shared_ptr<detail::DeviceMatrix> dev_;
+    mutable std::shared_ptr<detail::DeviceMatrix> dev64_;
 };
 
 }  // namespace EigSol

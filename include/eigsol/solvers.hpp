@@ -8,7 +8,8 @@
 //   qr_decompose<S> / _dense       src/qr_method/qr_decompose.hpp:25-132
 //   qr_eigenvalues<S> / _dense     src/qr_method/qr_eigenvalues.hpp:40-147
 //
-// Scalars: double and std::complex<double> natively; float and std::complex<float> promoted to fp64
+// Scalars: double and std::complex<double> natively; float and std::complex<float> natively for the
+// power method and the triangular-CSR shifted inverse, promoted to fp64 for the other solvers
 // (core.hpp, PromotedScalar); long double throws "scalar type not supported by the device path".
 //
 // Start vector: the reference draws x0 with Eigen's Vector::Random (std::rand, not reproducible
@@ -124,6 +125,26 @@ DenseMatrix<T> convert_dense(const DenseMatrix<U>& a) {
     return b;
 }
 
+// One device run in scalar type D (S itself, or its fp64 promotion).
+template <typename D, typename S>
+int power_run(const DeviceMatrix& d, bool dense, const eigsol_solver_options& o, const Vector<S>& xs0,
+              const S* shift, EigenResult<S>& out) {
+    const Vector<D> xs = convert_vec<D>(xs0);
+    const D sh = shift ? static_cast<D>(*shift) : D{};
+    D lam{};
+    Vector<D> x(xs0.size());
+    std::int32_t it = 0, conv = 0;
+    int st;
+    if (shift)
+        st = dense ? eigsol_shifted_inverse_dense(d.dense(), &sh, &o, xs.data(), &lam, x.data(), &it, &conv)
+                   : eigsol_shifted_inverse_csr(d.csr(), &sh, &o, xs.data(), &lam, x.data(), &it, &conv);
+    else
+        st = dense ? eigsol_power_dense(d.dense(), &o, xs.data(), &lam, x.data(), &it, &conv)
+                   : eigsol_power_csr(d.csr(), &o, xs.data(), &lam, x.data(), &it, &conv);
+    if (st == EIGSOL_OK) out = EigenResult<S>(static_cast<S>(lam), convert_vec<S>(x), it, conv != 0);
+    return st;
+}
+
 template <typename S>
 EigenResult<S> power_like(const Matrix& M, const SolverOptions& opts, const Vector<S>* x0, const S* shift,
                           const char* who) {
@@ -132,30 +153,24 @@ EigenResult<S> power_like(const Matrix& M, const SolverOptions& opts, const Vect
     if (r != c) throw std::runtime_error(std::string(who) + ": matrix must be square");
     if (r == 0) throw std::runtime_error(std::string(who) + ": matrix has zero size");
     require_device_scalar<S>(who);
+    EigenResult<S> res;
     if constexpr (DeviceCapable<S>) {
-        using D = device_scalar_t<S>;
         Vector<S> xs0 = x0 ? *x0 : random_vector<S>(static_cast<std::size_t>(r));
         if (xs0.size() != static_cast<std::size_t>(r))
             throw std::runtime_error(std::string(who) + ": start vector size mismatch");
-        const Vector<D> xs = convert_vec<D>(xs0);
-        const detail::DeviceMatrix& d = M.device<S>();
         const eigsol_solver_options o = copts(opts);
-        D lam{};
-        const D sh = shift ? static_cast<D>(*shift) : D{};
-        Vector<D> x(static_cast<std::size_t>(r));
-        std::int32_t it = 0, conv = 0;
-        int st;
-        if (shift) {
-            st = M.isDense() ? eigsol_shifted_inverse_dense(d.dense(), &sh, &o, xs.data(), &lam, x.data(), &it, &conv)
-                             : eigsol_shifted_inverse_csr(d.csr(), &sh, &o, xs.data(), &lam, x.data(), &it, &conv);
-        } else {
-            st = M.isDense() ? eigsol_power_dense(d.dense(), &o, xs.data(), &lam, x.data(), &it, &conv)
-                             : eigsol_power_csr(d.csr(), &o, xs.data(), &lam, x.data(), &it, &conv);
+        // single precision runs natively (power method; shifted inverse on a triangular CSR); the
+        // dense and general-sparse shifted inverse have fp64 factors only
+        const bool native = !PromotedScalar<S> || !shift || !M.isDense();
+        int st = EIGSOL_E_UNSUPPORTED;
+        if (native) st = power_run<S>(M.device<S>(), M.isDense(), o, xs0, shift, res);
+        if constexpr (PromotedScalar<S>) {
+            if (st == EIGSOL_E_UNSUPPORTED && shift)
+                st = power_run<device_scalar_t<S>>(M.device_fp64<S>(), M.isDense(), o, xs0, shift, res);
         }
         check(st, who);
-        return EigenResult<S>(static_cast<S>(lam), convert_vec<S>(x), it, conv != 0);
     }
-    return {};
+    return res;
 }
 
 template <typename S>
@@ -197,17 +212,24 @@ Vector<S> solve_shifted(const Matrix& A, const S shift, const Vector<S>& b) {
     detail::require_device_scalar<S>("solve_shifted");
     Vector<S> x(b.size());
     if constexpr (DeviceCapable<S>) {
-        using D = device_scalar_t<S>;
         if (b.size() == 0) return x;
-        const detail::DeviceMatrix& d = A.device<S>();
         const std::int64_t n = static_cast<std::int64_t>(b.size());
-        const D sh = static_cast<D>(shift);
-        const Vector<D> bd = detail::convert_vec<D>(b);
-        Vector<D> xd(b.size());
-        detail::check(A.isDense() ? eigsol_solve_shifted_dense(d.dense(), &sh, bd.data(), n, xd.data())
-                                  : eigsol_solve_shifted_csr(d.csr(), &sh, bd.data(), n, xd.data()),
-                      "solve_shifted");
-        x = detail::convert_vec<S>(xd);
+        auto run = [&](auto tag, const detail::DeviceMatrix& d) {
+            using D = decltype(tag);
+            const D sh = static_cast<D>(shift);
+            const Vector<D> bd = detail::convert_vec<D>(b);
+            Vector<D> xd(b.size());
+            const int st = A.isDense() ? eigsol_solve_shifted_dense(d.dense(), &sh, bd.data(), n, xd.data())
+                                       : eigsol_solve_shifted_csr(d.csr(), &sh, bd.data(), n, xd.data());
+            if (st == EIGSOL_OK) x = detail::convert_vec<S>(xd);
+            return st;
+        };
+        // single precision: triangular CSR natively, everything else on the fp64 factor
+        int st = EIGSOL_E_UNSUPPORTED;
+        if (!PromotedScalar<S> || !A.isDense()) st = run(S{}, A.device<S>());
+        if constexpr (PromotedScalar<S>)
+            if (st == EIGSOL_E_UNSUPPORTED) st = run(device_scalar_t<S>{}, A.device_fp64<S>());
+        detail::check(st, "solve_shifted");
     }
     return x;
 }

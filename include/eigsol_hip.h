@@ -19,7 +19,8 @@
  * detail string of the last failure on the calling thread is eigsol_last_error().
  *
  * Scalars: EIGSOL_F64 = double, EIGSOL_C128 = std::complex<double> / double _Complex
- * (interleaved re, im).  Dense storage is column-major (Matrix::Dense is an Eigen col-major
+ * (interleaved re, im), EIGSOL_F32 = float, EIGSOL_C64 = std::complex<float> (single-precision
+ * paths listed at eigsol_dtype).  Dense storage is column-major (Matrix::Dense is an Eigen col-major
  * matrix, matrix.hpp:39-40).  Sparse storage is CSR with int32 indices on the device; the CSC
  * constructor accepts the reference's canonical Eigen::SparseMatrix<S> (ColMajor, int) layout
  * (matrix.hpp:43-44).
@@ -52,7 +53,11 @@ typedef enum eigsol_status {
     EIGSOL_E_UNSUPPORTED = 12     /* structure not supported by the device path */
 } eigsol_status;
 
-typedef enum eigsol_dtype { EIGSOL_F64 = 0, EIGSOL_C128 = 1 } eigsol_dtype;
+/* EIGSOL_F32 / EIGSOL_C64: float and std::complex<float> (ScalarConcept, types.hpp:28-30), stored
+ * and multiplied in single precision on the device (CSR / dense power iteration, plain SpMV/GEMV,
+ * triangular-CSR shifted inverse).  Other solvers accept only F64 / C128 (the C++ façade promotes
+ * float input for those). */
+typedef enum eigsol_dtype { EIGSOL_F64 = 0, EIGSOL_C128 = 1, EIGSOL_F32 = 2, EIGSOL_C64 = 3 } eigsol_dtype;
 
 /* SolverOptions (src/option/solver_option.hpp:14-20). */
 typedef struct eigsol_solver_options {

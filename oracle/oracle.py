@@ -37,17 +37,17 @@ def lib():
     if _lib is None:
         build()
         L = C.CDLL(_LIB_PATH)
-        for name in ("spmv_csc_f64", "spmv_csc_c128"):
+        for name in ("spmv_csc_f64", "spmv_csc_c128", "spmv_csc_f32", "spmv_csc_c64"):
             getattr(L, "orc_" + name).argtypes = [_i64, _i64, _p, _p, _p, _p, _p]
-        for name in ("spmv_csr_f64", "spmv_csr_c128"):
+        for name in ("spmv_csr_f64", "spmv_csr_c128", "spmv_csr_f32", "spmv_csr_c64"):
             getattr(L, "orc_" + name).argtypes = [_i64, _p, _p, _p, _p, _p]
-        for name in ("gemv_f64", "gemv_c128"):
+        for name in ("gemv_f64", "gemv_c128", "gemv_f32", "gemv_c64"):
             getattr(L, "orc_" + name).argtypes = [_i64, _i64, _p, _p, _p]
-        for name in ("power_csc_f64", "power_csc_c128"):
+        for name in ("power_csc_f64", "power_csc_c128", "power_csc_f32", "power_csc_c64"):
             f = getattr(L, "orc_" + name)
             f.argtypes = [_i64, _p, _p, _p, _p, _int, _dbl, _p, _p, _p, _p]
             f.restype = _int
-        for name in ("power_dense_f64", "power_dense_c128"):
+        for name in ("power_dense_f64", "power_dense_c128", "power_dense_f32", "power_dense_c64"):
             f = getattr(L, "orc_" + name)
             f.argtypes = [_i64, _p, _p, _int, _dbl, _p, _p, _p, _p]
             f.restype = _int
@@ -64,6 +64,10 @@ def lib():
         L.orc_shifted_triu_csr_f64.argtypes = [_i64, _p, _p, _p, _dbl, _p, _int, _dbl, _p, _p, _p, _p]
         L.orc_shifted_triu_csr_f64.restype = _int
         L.orc_triu_shifted_solve_csr_c128.argtypes = [_i64, _p, _p, _p, _p, _p, _p]
+        for name in ("shifted_triu_csr_f32", "shifted_triu_csr_c64"):
+            f = getattr(L, "orc_" + name)
+            f.argtypes = [_i64, _p, _p, _p, _p, _p, _int, _dbl, _p, _p, _p, _p]
+            f.restype = _int
         for name in ("hessenberg_f64", "hessenberg_c128"):
             getattr(L, "orc_" + name).argtypes = [_i64, _p, _p]
         for name in ("qr_decompose_f64", "qr_decompose_c128"):
@@ -86,8 +90,16 @@ def _is_c(dt) -> bool:
     return np.dtype(dt) == np.complex128
 
 
+_SFX = {np.dtype(np.float64): "f64", np.dtype(np.complex128): "c128", np.dtype(np.float32): "f32",
+        np.dtype(np.complex64): "c64"}
+
+
 def _sfx(dt) -> str:
-    return "c128" if _is_c(dt) else "f64"
+    return _SFX[np.dtype(dt)]
+
+
+def _single(dt) -> bool:
+    return np.dtype(dt) in (np.dtype(np.float32), np.dtype(np.complex64))
 
 
 def _vec(a, dt):
@@ -118,7 +130,7 @@ def spmv_csr(rowptr, colidx, vals, x):
 
 
 def gemv(A, x):
-    dt = np.result_type(A.dtype, np.float64)
+    dt = A.dtype if _single(A.dtype) else np.result_type(A.dtype, np.float64)
     Af, xx = _fortran(A, dt), _vec(x, dt)
     y = np.empty(A.shape[0], dtype=dt)
     getattr(lib(), "orc_gemv_" + _sfx(dt))(A.shape[0], A.shape[1], _ptr(Af), _ptr(xx), _ptr(y))
@@ -129,7 +141,7 @@ def gemv(A, x):
 def _result(lam, x, iters, conv, trace):
     it = int(iters.value)
     return {
-        "eigenvalue": lam[0] if lam.dtype == np.complex128 else float(lam[0]),
+        "eigenvalue": lam[0] if np.iscomplexobj(lam) else float(lam[0]),
         "eigenvector": x,
         "iterations": it,
         "converged": bool(conv),
@@ -162,7 +174,7 @@ def power_csr_omp(rowptr, colidx, vals, x0, iterations, threads):
 
 
 def power_dense(A, x0, max_iterations=1000, tolerance=1e-10, want_trace=False):
-    dt = np.result_type(A.dtype, np.float64)
+    dt = A.dtype if _single(A.dtype) else np.result_type(A.dtype, np.float64)
     n = A.shape[0]
     Af, xx = _fortran(A, dt), _vec(x0, dt)
     lam = np.zeros(1, dtype=dt)
@@ -219,7 +231,12 @@ def shifted_triu_csr(rowptr, colidx, vals, shift, x0, max_iterations=1000, toler
     it = C.c_int(0)
     tr = np.zeros(max(max_iterations, 1), dtype=dt) if want_trace else None
     trp = None if tr is None else _ptr(tr)
-    if _is_c(dt):
+    if _single(dt):
+        s = np.array([shift], dtype=dt)
+        conv = getattr(lib(), "orc_shifted_triu_csr_" + _sfx(dt))(
+            n, _ptr(rp), _ptr(ci), _ptr(v), _ptr(s), _ptr(xx), int(max_iterations), float(tolerance), _ptr(lam),
+            _ptr(x), C.byref(it), trp)
+    elif _is_c(dt):
         s = np.array([complex(shift).real, complex(shift).imag])
         conv = lib().orc_shifted_triu_csr_c128(n, _ptr(rp), _ptr(ci), _ptr(v), _ptr(s), _ptr(xx),
                                                int(max_iterations), float(tolerance), _ptr(lam),

@@ -14,7 +14,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._capi import (EIGSOL_C128, EIGSOL_E_SIZE_MISMATCH, EIGSOL_F64, EigSolError, SolverOptionsC, call, check, last_error,
+from ._capi import (EIGSOL_C64, EIGSOL_C128, EIGSOL_F32, EIGSOL_E_SIZE_MISMATCH, EIGSOL_F64, EigSolError, SolverOptionsC, call, check, last_error,
                     lib)
 
 __all__ = [
@@ -50,11 +50,15 @@ def _dtype_code(dt) -> int:
         return EIGSOL_F64
     if dt == np.complex128:
         return EIGSOL_C128
-    raise EigSolError(3, f"scalar type mismatch: {dt} (supported: float64, complex128)")
+    if dt == np.float32:
+        return EIGSOL_F32
+    if dt == np.complex64:
+        return EIGSOL_C64
+    raise EigSolError(3, f"scalar type mismatch: {dt} (supported: float64, complex128, float32, complex64)")
 
 
 def _np_dtype(code: int):
-    return np.complex128 if code == EIGSOL_C128 else np.float64
+    return {EIGSOL_C128: np.complex128, EIGSOL_F32: np.float32, EIGSOL_C64: np.complex64}.get(code, np.float64)
 
 
 def _ptr(a: np.ndarray) -> C.c_void_p:
@@ -234,7 +238,7 @@ class PowerSession:
         it, conv = C.c_int32(0), C.c_int32(0)
         call("eigsol_power_finish", self.handle, _ptr(lam), None if x is None else _ptr(x), 0,
              C.byref(it), C.byref(conv))
-        ev = complex(lam[0]) if self.dtype == np.complex128 else float(lam[0])
+        ev = complex(lam[0]) if np.iscomplexobj(lam) else float(lam[0])
         return EigenResult(ev, x, int(it.value), bool(conv.value))
 
     def trace(self, capacity: int) -> np.ndarray:
@@ -255,7 +259,8 @@ class PowerSession:
         names = {0: "csr_kernel (x gathered from HBM)", 1: "csr_win_kernel (x window staged in LDS)",
                  2: "dense_kernel (GEMV)", 3: "sptrsv_kernel (sync-free triangular solve)",
                  4: "dense_lu_solve_kernel (LU substitution)",
-                 5: "csr_slice_kernel (64-row slices, one row per lane)"}
+                 5: "csr_slice_kernel (64-row slices, one row per lane)",
+                 6: "csr_row_kernel (one row per lane, single-precision fallback layout)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?")}
 
@@ -276,7 +281,7 @@ def power_method(matrix, opts: SolverOptions = SolverOptions(), x0=None) -> Eige
     if x0 is None:
         rng = np.random.default_rng(0)
         x0 = rng.uniform(-1, 1, matrix.shape[0])
-        if matrix.dtype == np.complex128:
+        if np.issubdtype(matrix.dtype, np.complexfloating):
             x0 = x0 + 1j * rng.uniform(-1, 1, matrix.shape[0])
     x0 = _vector(x0, matrix.dtype, matrix.shape[0], "x0")
     lam = np.zeros(1, dtype=matrix.dtype)
@@ -285,7 +290,7 @@ def power_method(matrix, opts: SolverOptions = SolverOptions(), x0=None) -> Eige
     o = opts.to_c()
     fn = "eigsol_power_csr" if isinstance(matrix, CsrMatrix) else "eigsol_power_dense"
     call(fn, matrix.handle, C.byref(o), _ptr(x0), _ptr(lam), _ptr(x), C.byref(it), C.byref(conv))
-    ev = complex(lam[0]) if matrix.dtype == np.complex128 else float(lam[0])
+    ev = complex(lam[0]) if np.iscomplexobj(lam) else float(lam[0])
     return EigenResult(ev, x, int(it.value), bool(conv.value))
 
 
@@ -297,7 +302,7 @@ class ShiftedSolverOptions(SolverOptions):
 
 
 def _sigma(shift, dtype) -> np.ndarray:
-    if dtype != np.complex128 and np.iscomplexobj(shift) and complex(shift).imag != 0:
+    if not np.issubdtype(dtype, np.complexfloating) and np.iscomplexobj(shift) and complex(shift).imag != 0:
         raise EigSolError(3, "scalar type mismatch: complex shift for a real matrix")
     return np.array([shift], dtype=dtype)
 
@@ -323,7 +328,7 @@ def shifted_inverse_power_method(matrix, opts: ShiftedSolverOptions = ShiftedSol
     if x0 is None:
         rng = np.random.default_rng(0)
         x0 = rng.uniform(-1, 1, matrix.shape[0])
-        if matrix.dtype == np.complex128:
+        if np.issubdtype(matrix.dtype, np.complexfloating):
             x0 = x0 + 1j * rng.uniform(-1, 1, matrix.shape[0])
     x0 = _vector(x0, matrix.dtype, matrix.shape[0], "x0")
     sig = _sigma(opts.shift, matrix.dtype)
@@ -333,7 +338,7 @@ def shifted_inverse_power_method(matrix, opts: ShiftedSolverOptions = ShiftedSol
     o = opts.to_c()
     fn = "eigsol_shifted_inverse_csr" if isinstance(matrix, CsrMatrix) else "eigsol_shifted_inverse_dense"
     call(fn, matrix.handle, _ptr(sig), C.byref(o), _ptr(x0), _ptr(lam), _ptr(x), C.byref(it), C.byref(conv))
-    ev = complex(lam[0]) if matrix.dtype == np.complex128 else float(lam[0])
+    ev = complex(lam[0]) if np.iscomplexobj(lam) else float(lam[0])
     return EigenResult(ev, x, int(it.value), bool(conv.value))
 
 

@@ -28,6 +28,8 @@ EIGSOL_E_UNSUPPORTED = 12
 
 EIGSOL_F64 = 0
 EIGSOL_C128 = 1
+EIGSOL_F32 = 2   # float (single-precision power / SpMV / triangular shifted inverse)
+EIGSOL_C64 = 3   # std::complex<float>
 
 EIGSOL_TRANSPORT_LOCAL = 0
 EIGSOL_TRANSPORT_COLLECTIVE = 1

@@ -657,14 +657,20 @@ __device__ __forceinline__ S ld_x_peer(const CsrArgs<S>& a, const S* xin, const 
     return xin[e];
 }
 
+// Real scalars travel in pairs (double2: 16-byte lane loads; float2: 8-byte), complex ones alone.
+template <class S> struct Pair2 { using type = S; };
+template <> struct Pair2<double> { using type = double2; };
+template <> struct Pair2<float> { using type = float2; };
+template <class S> using pair_t = typename Pair2<S>::type;
+
 template <class S, int KB, bool kG>
 struct SliceRegs {
-    // window loads: f64 in 16-byte pairs (window start even, length even), complex one per lane
-    static constexpr int NW = std::is_same_v<S, double> ? kSliceWin / 128 : kSliceWin / 64;
-    using WT = std::conditional_t<std::is_same_v<S, double>, double2, S>;
-    // f64 values are stored in lane pairs (entries 2j, 2j+1 of a row adjacent): 16-byte loads
-    static constexpr int NV = std::is_same_v<S, double> ? KB / 2 : KB;
-    using VT = std::conditional_t<std::is_same_v<S, double>, double2, S>;
+    // window loads: real in pairs (window start even, length even), complex one per lane
+    static constexpr int NW = is_real_v<S> ? kSliceWin / 128 : kSliceWin / 64;
+    using WT = pair_t<S>;
+    // real values are stored in lane pairs (entries 2j, 2j+1 of a row adjacent): one load per pair
+    static constexpr int NV = is_real_v<S> ? KB / 2 : KB;
+    using VT = pair_t<S>;
     VT v[NV];
     // window slices: packed 8-bit offsets in c[0 .. KB/4); gather slices (kG): int32 columns
     uint32_t c[kG ? KB : KB / 4];
@@ -674,13 +680,13 @@ struct SliceRegs {
 
 template <class S, int KB, bool kG>
 __device__ __forceinline__ S slice_val(const SliceRegs<S, KB, kG>& R, int u) {
-    if constexpr (std::is_same_v<S, double>) return (u & 1) ? R.v[u >> 1].y : R.v[u >> 1].x;
+    if constexpr (is_real_v<S>) return (u & 1) ? R.v[u >> 1].y : R.v[u >> 1].x;
     else return R.v[u];
 }
 // stream index of entry (k, lane) of a slice whose values start at off
 template <class S>
 __device__ __forceinline__ uint32_t slice_entry(uint32_t off, int k, int lane) {
-    if constexpr (std::is_same_v<S, double>) return off + 128u * (uint32_t)(k >> 1) + 2u * (uint32_t)lane + (uint32_t)(k & 1);
+    if constexpr (is_real_v<S>) return off + 128u * (uint32_t)(k >> 1) + 2u * (uint32_t)lane + (uint32_t)(k & 1);
     else return off + 64u * (uint32_t)k + (uint32_t)lane;
 }
 
@@ -696,12 +702,12 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
     const uint32_t base = (uint32_t)m.x + (uint32_t)lane;
     R.len = m.z & 0xff;
     if (m.z & 0x100) R.len = a.slen[min(slice * kSliceRows + lane, a.nrows - 1)];
-    if constexpr (std::is_same_v<S, double>) {
+    if constexpr (is_real_v<S>) {
         const int K2 = (K + 1) >> 1;
         const uint32_t b2 = ((uint32_t)m.x >> 1) + (uint32_t)lane;
 #pragma unroll
         for (int j = 0; j < SliceRegs<S, KB, kG>::NV; ++j)
-            R.v[j] = ldg_stream(reinterpret_cast<const double2*>(a.sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
+            R.v[j] = ldg_stream(reinterpret_cast<const pair_t<S>*>(a.sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
     } else {
 #pragma unroll
         for (int u = 0; u < KB; ++u) R.v[u] = ldg_stream(a.sval, base + 64u * (uint32_t)min(u, K - 1));
@@ -716,7 +722,7 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
         if (kDist && (m.z & kGhostSliceBit)) {
 #pragma unroll
             for (int j = 0; j < SliceRegs<S, KB, kG>::NW; ++j) {
-                if constexpr (std::is_same_v<S, double>) {
+                if constexpr (is_real_v<S>) {
                     const int e = m.y + 2 * min(lane + 64 * j, (wl >> 1) - 1);
                     R.w[j].x = ld_x_peer(a, xin, gin, e);
                     R.w[j].y = ld_x_peer(a, xin, gin, e + 1);
@@ -727,8 +733,8 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
         } else
 #pragma unroll
         for (int j = 0; j < SliceRegs<S, KB, kG>::NW; ++j)
-            if constexpr (std::is_same_v<S, double>)
-                R.w[j] = ldg(reinterpret_cast<const double2*>(xin),
+            if constexpr (is_real_v<S>)
+                R.w[j] = ldg(reinterpret_cast<const pair_t<S>*>(xin),
                              (uint32_t)((m.y >> 1) + min(lane + 64 * j, (wl >> 1) - 1)));
             else
                 R.w[j] = ldg(xin, (uint32_t)(m.y + min(lane + 64 * j, wl - 1)));
@@ -742,8 +748,8 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
 // Row sums of one slice from its registers (window slices: x from the wave's LDS window).
 template <class S>
 __device__ __forceinline__ S shfl_s(S v, int src) {
-    if constexpr (std::is_same_v<S, double>) return __shfl(v, src, 64);
-    else return cplx{__shfl(v.re, src, 64), __shfl(v.im, src, 64)};
+    if constexpr (is_real_v<S>) return __shfl(v, src, 64);
+    else return S{__shfl(v.re, src, 64), __shfl(v.im, src, 64)};
 }
 
 template <class S, bool kPower, int KB, bool kG, bool kDist = false>
@@ -762,13 +768,13 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
         const int w0 = mc.y, wl = (mc.z >> 9) & 0x1ff;
 #pragma unroll
         for (int j = 0; j < SliceRegs<S, KB, kG>::NW; ++j) {
-            if constexpr (std::is_same_v<S, double>) {
-                double2 v = R.w[j];
+            if constexpr (is_real_v<S>) {
+                pair_t<S> v = R.w[j];
                 if constexpr (kPower) {
                     v.x = scale_in(v.x, nrm);
                     v.y = scale_in(v.y, nrm);
                 }
-                if (2 * (lane + 64 * j) < wl) *reinterpret_cast<double2*>(xw + 2 * (lane + 64 * j)) = v;
+                if (2 * (lane + 64 * j) < wl) *reinterpret_cast<pair_t<S>*>(xw + 2 * (lane + 64 * j)) = v;
             } else {
                 S v = R.w[j];
                 if constexpr (kPower) v = scale_in(v, nrm);
@@ -997,6 +1003,50 @@ __global__ __launch_bounds__(kThreads) void norm_partial_kernel(const S* x, int6
     last_arriver_reduce(n2, z1, z2, blk_part, &ctl->counter, out, sm, &s_last);
 }
 
+// Single-precision matrices the sliced layout cannot hold (a row longer than 64 entries, or
+// too much padding): one row per lane, its entries summed sequentially in ascending column order
+// (the reference's CSC scatter order, bitwise), fused power epilogue.  Uncoalesced, but only the
+// fallback layout of the float / complex<float> instantiations.
+template <class S, bool kPower>
+__global__ __launch_bounds__(kThreads) void csr_row_kernel(CsrArgs<S> a, int parity) {
+    __shared__ double sm[3 * kWaves];
+    __shared__ Prologue pro;
+    __shared__ int s_last;
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kPower) {
+        power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = (parity ? a.buf1 : a.buf0) + a.xoff;
+    } else {
+        xin = a.x_plain;
+        yout = a.y_plain;
+    }
+    double n2 = 0.0, rr = 0.0, ri = 0.0;
+    for (int r = blockIdx.x * kThreads + threadIdx.x; r < a.nrows; r += gridDim.x * kThreads) {
+        S acc = s_zero<S>();
+        const int e1 = a.rowptr[r + 1];
+        for (int e = a.rowptr[r]; e < e1; ++e) {
+            S x = xin[a.col[e]];
+            if constexpr (kPower) x = scale_in(x, nrm);
+            acc = add(acc, mul(a.val[e], x));
+        }
+        yout[r] = acc;
+        if constexpr (kPower) {
+            const S xi = scale_in(xin[r + a.xoff], nrm);
+            n2 += sq_abs(acc);
+            acc_dot(rr, ri, xi, acc);
+        }
+    }
+    if constexpr (kPower) {
+        block_sum3(n2, rr, ri, sm);
+        last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+    }
+}
+
 // x_out = src / nrm (the reference's x = y / normY of the final iterate; unchanged if nrm == 0).
 template <class S>
 __global__ __launch_bounds__(kThreads) void scale_out_kernel(const S* src, double nrm, S* dst,
@@ -1106,7 +1156,7 @@ struct SliceLayout {
     bool any_gather = false;   // some slice's window does not fit: gather instantiation
 };
 
-static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* values, size_t sb,
+static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* values, size_t sb, bool pairs,
                          int64_t nrows, int64_t nnz, int64_t xoff, int64_t xlen, SliceLayout& L) {
     if (nrows == 0 || xlen == 0) return false;
     const int64_t ns = (nrows + kSliceRows - 1) / kSliceRows;
@@ -1132,8 +1182,8 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
         w1 = (int32_t)std::min<int64_t>(w1, xlen - 1);
         w0 = std::min(w0, w1);
         bool win = true;
-        if (sb == 8) {
-            // f64 windows load in aligned pairs: even start and even length inside x
+        if (pairs) {
+            // real windows load in aligned pairs: even start and even length inside x
             w0 &= ~1;
             if (((int64_t)w1 - w0 + 1) & 1) {
                 if (w1 + 1 < xlen) ++w1;
@@ -1157,7 +1207,7 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
         L.meta[4 * s + 1] = win ? w0 : -1;
         L.meta[4 * s + 2] = K | (ragged ? 0x100 : 0) | (win ? (int32_t)(wl << 9) : 0) | (ghost ? kGhostSliceBit : 0);
         L.meta[4 * s + 3] = (int32_t)(win ? ctot8 : ctot32);
-        total += (int64_t)(sb == 8 ? (K + 1) & ~1 : K) * kSliceRows;   // f64: whole lane pairs
+        total += (int64_t)(pairs ? (K + 1) & ~1 : K) * kSliceRows;   // real: whole lane pairs
         if (win) ctot8 += (int64_t)((K + 3) / 4) * kSliceRows;
         else ctot32 += (int64_t)K * kSliceRows;
         L.any_gather |= !win;
@@ -1179,7 +1229,7 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
             if (any_ragged) L.len[r] = (uint8_t)l;
             for (int k = 0; k < l; ++k) {
                 const int32_t e = rowptr[r] + k;
-                const size_t q = sb == 8 ? (size_t)(off + (int64_t)(k >> 1) * 2 * kSliceRows + 2 * lane + (k & 1))
+                const size_t q = pairs ? (size_t)(off + (int64_t)(k >> 1) * 2 * kSliceRows + 2 * lane + (k & 1))
                                          : (size_t)(off + (int64_t)k * kSliceRows + lane);
                 std::memcpy(&L.val[q * sb], (const unsigned char*)values + (size_t)e * sb, sb);
                 if (w0 >= 0)
@@ -1240,7 +1290,7 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     bool sliced = true;
     if (const char* env = std::getenv("EIGSOL_CSR_NO_SLICE")) if (std::atoi(env)) sliced = false;
     if (sliced)
-        sliced = build_slices(rowptr, col_use, val_use, sb, nrows, nnz, xoff, ncols, SL);
+        sliced = build_slices(rowptr, col_use, val_use, sb, !dtype_complex(dtype), nrows, nnz, xoff, ncols, SL);
 
     // the kernels index every stream with 32-bit byte offsets (ldg): one device's rows must keep
     // values, columns and vectors under 4 GiB each (shard larger matrices over ranks)
@@ -1358,13 +1408,16 @@ static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, in
     return EIGSOL_OK;
 }
 
+// the device-side peer exchange (row-sharded sessions) is built for the double instantiations
+template <class S> inline constexpr bool kPeerOk = std::is_same_v<S, double> || std::is_same_v<S, cplx>;
+
 template <class S>
 static const void* power_kernel_ptr(const eigsol_csr* A, bool peer = false) {
     if (A->sliced) {
 #define EIGSOL_SLICE_PTR(KB)                                                                                 \
     if (peer)                                                                                                \
-        return A->slice_gather ? reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, true, true>)   \
-                               : reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, false, true>); \
+        return A->slice_gather ? reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, true, kPeerOk<S>>)   \
+                               : reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, false, kPeerOk<S>>); \
     return A->slice_gather ? reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, true>)             \
                            : reinterpret_cast<const void*>(csr_slice_kernel<S, true, KB, false>);
         switch (A->slice_kb) {
@@ -1375,16 +1428,24 @@ static const void* power_kernel_ptr(const eigsol_csr* A, bool peer = false) {
         }
 #undef EIGSOL_SLICE_PTR
     }
-    return A->windowed ? reinterpret_cast<const void*>(csr_win_kernel<S, true>)
-                       : reinterpret_cast<const void*>(csr_kernel<S, true>);
+    if constexpr (std::is_same_v<S, float> || std::is_same_v<S, cplxf>)
+        return reinterpret_cast<const void*>(csr_row_kernel<S, true>);
+    else
+        return A->windowed ? reinterpret_cast<const void*>(csr_win_kernel<S, true>)
+                           : reinterpret_cast<const void*>(csr_kernel<S, true>);
 }
 
 int csr_grid(eigsol_csr* A, int* grid, bool peer) {
-    const void* k = A->dtype == EIGSOL_C128 ? power_kernel_ptr<cplx>(A, peer) : power_kernel_ptr<double>(A, peer);
+    const void* k = A->dtype == EIGSOL_C128  ? power_kernel_ptr<cplx>(A, peer)
+                    : A->dtype == EIGSOL_F32 ? power_kernel_ptr<float>(A, peer)
+                    : A->dtype == EIGSOL_C64 ? power_kernel_ptr<cplxf>(A, peer)
+                                             : power_kernel_ptr<double>(A, peer);
     // work units: tiles (one per block step) or slices (one per wave step)
     const int64_t units = A->sliced ? (A->nslices + kWaves - 1) / kWaves : A->ntiles;
     // sliced: two blocks (8 waves, 16 slices in flight) per CU measured fastest on band10m;
     // more concurrent streams per CU cost more than the latency they hide
+    if (dtype_single(A->dtype) && !A->sliced)   // row-per-lane fallback: rows / threads
+        return resident_grid(A->ctx, k, (A->nrows + kThreads - 1) / kThreads, grid, 8);
     return resident_grid(A->ctx, k, units, grid, A->sliced ? 2 : 8);
 }
 
@@ -1430,7 +1491,7 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
     if (A->sliced) {
 #define EIGSOL_SLICE_LAUNCH2(KB, G)                                                                                     \
     if (power && peer)                                                                                                  \
-        hipLaunchKernelGGL((csr_slice_kernel<S, true, KB, G, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);   \
+        hipLaunchKernelGGL((csr_slice_kernel<S, true, KB, G, kPeerOk<S>>), dim3(grid), dim3(kThreads), 0, s, args, parity); \
     else if (power) hipLaunchKernelGGL((csr_slice_kernel<S, true, KB, G>), dim3(grid), dim3(kThreads), 0, s, args, parity); \
     else hipLaunchKernelGGL((csr_slice_kernel<S, false, KB, G>), dim3(grid), dim3(kThreads), 0, s, args, parity);
 #define EIGSOL_SLICE_LAUNCH(KB)                                  \
@@ -1444,6 +1505,9 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
         }
 #undef EIGSOL_SLICE_LAUNCH
 #undef EIGSOL_SLICE_LAUNCH2
+    } else if constexpr (std::is_same_v<S, float> || std::is_same_v<S, cplxf>) {
+        if (power) hipLaunchKernelGGL((csr_row_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);
+        else hipLaunchKernelGGL((csr_row_kernel<S, false>), dim3(grid), dim3(kThreads), 0, s, args, parity);
     } else if (A->windowed) {
         if (power) hipLaunchKernelGGL((csr_win_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, args, parity);
         else hipLaunchKernelGGL((csr_win_kernel<S, false>), dim3(grid), dim3(kThreads), 0, s, args, parity);
@@ -1477,9 +1541,17 @@ int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerC
                      const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
                      int parity, int grid, const PeerArgs* peer) {
     if (peer && !A->sliced) return fail(EIGSOL_E_UNSUPPORTED, "peer exchange needs the sliced CSR layout");
+    if (peer && dtype_single(A->dtype))
+        return fail(EIGSOL_E_UNSUPPORTED, "peer exchange: single-precision row-sharded sessions are not built");
     if (A->dtype == EIGSOL_C128)
         return power_launch_t<cplx>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
                                     trace, parity, grid, peer);
+    if (A->dtype == EIGSOL_F32)
+        return power_launch_t<float>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
+                                     trace, parity, grid, nullptr);
+    if (A->dtype == EIGSOL_C64)
+        return power_launch_t<cplxf>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
+                                     trace, parity, grid, nullptr);
     return power_launch_t<double>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
                                   trace, parity, grid, peer);
 }
@@ -1487,6 +1559,8 @@ int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerC
 int peer_begin_launch(eigsol_ctx* ctx, int dtype, const PeerArgs& pa, const void* x_own, int64_t npush,
                       const void* mine) {
     hipStream_t s = ctx->stream;
+    if (dtype_single(dtype))
+        return fail(EIGSOL_E_UNSUPPORTED, "peer exchange: single-precision row-sharded sessions are not built");
     if (dtype == EIGSOL_C128)
         hipLaunchKernelGGL(peer_begin_kernel<cplx>, dim3(1), dim3(kThreads), 0, s, pa, (const cplx*)x_own, npush,
                            (const part4*)mine);
@@ -1503,6 +1577,12 @@ int norm_partial_launch(eigsol_ctx* ctx, int dtype, const void* x, int64_t n, Po
     if (dtype == EIGSOL_C128)
         hipLaunchKernelGGL(norm_partial_kernel<cplx>, dim3(grid), dim3(kThreads), 0, s,
                            (const cplx*)x, n, ctl, (part4*)blk_part, (part4*)out);
+    else if (dtype == EIGSOL_F32)
+        hipLaunchKernelGGL(norm_partial_kernel<float>, dim3(grid), dim3(kThreads), 0, s,
+                           (const float*)x, n, ctl, (part4*)blk_part, (part4*)out);
+    else if (dtype == EIGSOL_C64)
+        hipLaunchKernelGGL(norm_partial_kernel<cplxf>, dim3(grid), dim3(kThreads), 0, s,
+                           (const cplxf*)x, n, ctl, (part4*)blk_part, (part4*)out);
     else
         hipLaunchKernelGGL(norm_partial_kernel<double>, dim3(grid), dim3(kThreads), 0, s,
                            (const double*)x, n, ctl, (part4*)blk_part, (part4*)out);
@@ -1516,6 +1596,12 @@ int scale_out_launch(eigsol_ctx* ctx, int dtype, const void* src, double nrm, vo
     if (dtype == EIGSOL_C128)
         hipLaunchKernelGGL(scale_out_kernel<cplx>, dim3(grid), dim3(kThreads), 0, s, (const cplx*)src,
                            nrm, (cplx*)dst, n);
+    else if (dtype == EIGSOL_F32)
+        hipLaunchKernelGGL(scale_out_kernel<float>, dim3(grid), dim3(kThreads), 0, s, (const float*)src,
+                           nrm, (float*)dst, n);
+    else if (dtype == EIGSOL_C64)
+        hipLaunchKernelGGL(scale_out_kernel<cplxf>, dim3(grid), dim3(kThreads), 0, s, (const cplxf*)src,
+                           nrm, (cplxf*)dst, n);
     else
         hipLaunchKernelGGL(scale_out_kernel<double>, dim3(grid), dim3(kThreads), 0, s,
                            (const double*)src, nrm, (double*)dst, n);
@@ -1533,8 +1619,7 @@ int eigsol_csr_create(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_
                       const void* values, eigsol_csr** out) {
     if (!ctx || !out) return fail(EIGSOL_E_INVALID, "eigsol_csr_create: null ctx/out");
     *out = nullptr;
-    if (dtype != EIGSOL_F64 && dtype != EIGSOL_C128)
-        return fail(EIGSOL_E_INVALID, "eigsol_csr_create: unknown dtype");
+    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create: unknown dtype");
     if (nrows > INT32_MAX - 1 || ncols > INT32_MAX - 1)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create: dimension exceeds int32 storage index");
     EIGSOL_TRY(validate_compressed("eigsol_csr_create", nrows, ncols, nnz, rowptr, colidx));
@@ -1548,8 +1633,7 @@ int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrow
                                const void* values, eigsol_csr** out) {
     if (!ctx || !out) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_csc: null ctx/out");
     *out = nullptr;
-    if (dtype != EIGSOL_F64 && dtype != EIGSOL_C128)
-        return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_csc: unknown dtype");
+    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_csc: unknown dtype");
     if (nrows > INT32_MAX - 1 || ncols > INT32_MAX - 1)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_csc: dimension exceeds int32");
     EIGSOL_TRY(validate_compressed("eigsol_csr_create_from_csc", ncols, nrows, nnz, colptr, rowidx));
@@ -1593,16 +1677,19 @@ int eigsol_csr_spmv(eigsol_csr* A, const void* x_dev, void* y_dev) {
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
     int grid = 8;
     EIGSOL_TRY(csr_grid(A, &grid, false));
-    if (A->dtype == EIGSOL_C128) {
-        CsrArgs<cplx> a = make_args<cplx>(A, A->ncols);
-        a.x_plain = (const cplx*)x_dev;
-        a.y_plain = (cplx*)y_dev;
-        return launch_csr<cplx>(A, a, false, 0, grid);
+    auto run = [&](auto tag) {
+        using S = decltype(tag);
+        CsrArgs<S> a = make_args<S>(A, A->ncols);
+        a.x_plain = (const S*)x_dev;
+        a.y_plain = (S*)y_dev;
+        return launch_csr<S>(A, a, false, 0, grid);
+    };
+    switch (A->dtype) {
+        case EIGSOL_C128: return run(cplx{});
+        case EIGSOL_F32: return run(0.0f);
+        case EIGSOL_C64: return run(cplxf{});
+        default: return run(0.0);
     }
-    CsrArgs<double> a = make_args<double>(A, A->ncols);
-    a.x_plain = (const double*)x_dev;
-    a.y_plain = (double*)y_dev;
-    return launch_csr<double>(A, a, false, 0, grid);
 }
 
 }  // extern "C"

@@ -19,9 +19,19 @@
 namespace eigsol {
 namespace dev {
 
-template <class S> struct DenseTile;
-template <> struct DenseTile<double> { static constexpr int kRows = 128; static constexpr int kPerLane = 2; };
-template <> struct DenseTile<cplx> { static constexpr int kRows = 64; static constexpr int kPerLane = 1; };
+// A lane owns 16 bytes of a column: 2 rows (f64, c64), 4 rows (f32) or 1 row (c128).
+template <class S> struct DenseTile {
+    static constexpr int kPerLane = 16 / (int)sizeof(S);
+    static constexpr int kRows = 64 * kPerLane;
+};
+
+// the lane's 16 bytes of a column (non-temporal: A is read once per iteration)
+template <class S, int PL>
+__device__ __forceinline__ void load_col16(const S* p, S (&v)[PL]) {
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+    __builtin_memcpy(&v[0], &t, 16);
+}
 
 template <class S>
 struct DenseArgs {
@@ -50,6 +60,17 @@ __device__ __forceinline__ void st_agent_s(cplx* p, cplx v) {
     st_agent(&p->re, v.re);
     st_agent(&p->im, v.im);
 }
+__device__ __forceinline__ void st_agent_s(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent_s(cplxf* p, cplxf v) {
+    st_agent_s(&p->re, v.re);
+    st_agent_s(&p->im, v.im);
+}
+__device__ __forceinline__ float ld_agent_s(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ cplxf ld_agent_s(const cplxf* p) { return cplxf{ld_agent_s(&p->re), ld_agent_s(&p->im)}; }
 __device__ __forceinline__ double ld_agent_s(const double* p) { return ld_agent(p); }
 __device__ __forceinline__ cplx ld_agent_s(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
 
@@ -92,49 +113,28 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
     const int64_t span = (c1 - c0 + kWaves - 1) / kWaves;
     const int64_t wc0 = c0 + w * span;
     const int64_t wc1 = min<int64_t>(c1, wc0 + span);
-    const bool full = row0 + PL <= a.n;
+    // 16-byte column pieces need the tile inside the matrix and 16-byte aligned columns
+    const bool vec = row0 + PL <= a.n && (a.n % PL) == 0;
     int64_t j = wc0;
-    if constexpr (PL == 2) {
-        // batches of kU columns, all loads issued before the FMAs (A read once: non-temporal), the
-        // same per-row summation order as the one-column loop below
+    {
+        // batches of kU columns, all loads issued before the products (A read once: non-temporal),
+        // the same per-row summation order as the one-column loop below
         constexpr int kU = 8;
-        if (full && ((a.n & 1) == 0)) {
+        if (vec) {
             for (; j + kU <= wc1; j += kU) {
                 S xj[kU];
-                double2 v[kU];
+                S v[kU][PL];
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
                     xj[u] = xin[j + u];
-                    const double* col = a.a + (j + u) * a.n + row0;
-                    typedef double d2v __attribute__((ext_vector_type(2)));
-                    const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(col));
-                    v[u] = double2{t.x, t.y};
+                    load_col16<S, PL>(a.a + (j + u) * a.n + row0, v[u]);
                 }
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
                     S x = xj[u];
                     if constexpr (kPower) x = scale_in(x, nrm);
-                    acc[0] = add(acc[0], mul(v[u].x, x));
-                    acc[1] = add(acc[1], mul(v[u].y, x));
-                }
-            }
-        }
-    }
-    if constexpr (PL == 1) {
-        constexpr int kU = 8;
-        if (row0 < a.n) {
-            for (; j + kU <= wc1; j += kU) {
-                S xj[kU], v[kU];
 #pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    xj[u] = xin[j + u];
-                    v[u] = ldg_stream(a.a + (j + u) * a.n, (uint32_t)row0);
-                }
-#pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    S x = xj[u];
-                    if constexpr (kPower) x = scale_in(x, nrm);
-                    acc[0] = add(acc[0], mul(v[u], x));
+                    for (int p = 0; p < PL; ++p) acc[p] = add(acc[p], mul(v[u][p], x));
                 }
             }
         }
@@ -143,17 +143,15 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
         S xj = xin[j];
         if constexpr (kPower) xj = scale_in(xj, nrm);
         const S* col = a.a + j * a.n;
-        if constexpr (PL == 2) {
-            if (full && ((a.n & 1) == 0)) {
-                const double2 v = *reinterpret_cast<const double2*>(col + row0);
-                acc[0] = add(acc[0], mul(v.x, xj));
-                acc[1] = add(acc[1], mul(v.y, xj));
-            } else {
-                if (row0 < a.n) acc[0] = add(acc[0], mul(col[row0], xj));
-                if (row0 + 1 < a.n) acc[1] = add(acc[1], mul(col[row0 + 1], xj));
-            }
+        if (vec) {
+            S v[PL];
+            load_col16<S, PL>(col + row0, v);
+#pragma unroll
+            for (int p = 0; p < PL; ++p) acc[p] = add(acc[p], mul(v[p], xj));
         } else {
-            if (row0 < a.n) acc[0] = add(acc[0], mul(col[row0], xj));
+#pragma unroll
+            for (int p = 0; p < PL; ++p)
+                if (row0 + p < a.n) acc[p] = add(acc[p], mul(col[row0 + p], xj));
         }
     }
 #pragma unroll
@@ -219,7 +217,7 @@ void dense_release(eigsol_dense* A) {
 }
 
 static void dense_layout(const eigsol_dense* A, int& ntr, int& nchunk, int& cw) {
-    const int R = A->dtype == EIGSOL_C128 ? DenseTile<cplx>::kRows : DenseTile<double>::kRows;
+    const int R = 64 * (16 / (int)scalar_bytes(A->dtype));   // DenseTile<S>::kRows
     ntr = (int)((A->nrows + R - 1) / R);
     const int64_t target = 2048;   // ~8 blocks per CU
     int64_t nch = std::max<int64_t>(1, target / std::max(1, ntr));
@@ -282,11 +280,16 @@ int dense_power_launch(eigsol_dense* A, void* buf0, void* buf1, PowerCtl* ctl,
                        const void* rank_part, int nranks, void* my_part, void* blk_part,
                        void* trace, int parity, int /*grid*/) {
     EIGSOL_TRY(dense_work(A));
-    if (A->dtype == EIGSOL_C128)
-        return dense_launch_t<cplx>(A, true, nullptr, nullptr, buf0, buf1, ctl, rank_part,
-                                    nranks, my_part, blk_part, trace, parity);
-    return dense_launch_t<double>(A, true, nullptr, nullptr, buf0, buf1, ctl, rank_part, nranks,
-                                  my_part, blk_part, trace, parity);
+    auto run = [&](auto tag) {
+        return dense_launch_t<decltype(tag)>(A, true, nullptr, nullptr, buf0, buf1, ctl, rank_part,
+                                             nranks, my_part, blk_part, trace, parity);
+    };
+    switch (A->dtype) {
+        case EIGSOL_C128: return run(cplx{});
+        case EIGSOL_F32: return run(0.0f);
+        case EIGSOL_C64: return run(cplxf{});
+        default: return run(0.0);
+    }
 }
 
 }  // namespace eigsol
@@ -297,8 +300,7 @@ int eigsol_dense_create(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int6
                         const void* colmajor, eigsol_dense** out) {
     if (!ctx || !out) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: null ctx/out");
     *out = nullptr;
-    if (dtype != EIGSOL_F64 && dtype != EIGSOL_C128)
-        return fail(EIGSOL_E_INVALID, "eigsol_dense_create: unknown dtype");
+    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: unknown dtype");
     if (nrows < 0 || ncols < 0) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: negative dimension");
     if (nrows * ncols > 0 && !colmajor) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: null data");
     EIGSOL_HIP(hipSetDevice(ctx->device));
@@ -333,11 +335,16 @@ int eigsol_dense_gemv(eigsol_dense* A, const void* x_dev, void* y_dev) {
     if (A->nrows == 0) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
     EIGSOL_TRY(dense_work(A));
-    if (A->dtype == EIGSOL_C128)
-        return dense_launch_t<cplx>(A, false, x_dev, y_dev, nullptr, nullptr, nullptr, nullptr, 1,
-                                    nullptr, nullptr, nullptr, 0);
-    return dense_launch_t<double>(A, false, x_dev, y_dev, nullptr, nullptr, nullptr, nullptr, 1,
-                                  nullptr, nullptr, nullptr, 0);
+    auto run = [&](auto tag) {
+        return dense_launch_t<decltype(tag)>(A, false, x_dev, y_dev, nullptr, nullptr, nullptr, nullptr, 1,
+                                             nullptr, nullptr, nullptr, 0);
+    };
+    switch (A->dtype) {
+        case EIGSOL_C128: return run(cplx{});
+        case EIGSOL_F32: return run(0.0f);
+        case EIGSOL_C64: return run(cplxf{});
+        default: return run(0.0);
+    }
 }
 
 }  // extern "C"

@@ -458,6 +458,9 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     if (!ctx->comm && !ctx->loop && !ctx->hcoll)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
     *out = nullptr;
+    if (dtype != EIGSOL_F64 && dtype != EIGSOL_C128)
+        return fail(EIGSOL_E_UNSUPPORTED, "eigsol_csr_create_dist: row-sharded matrices are built for double "
+                                          "and complex<double>");
     const int P = ctx->nranks, me = ctx->rank;
     if (row_begins[0] != 0 || nnz_local < 0)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: row_begins must start at 0 and nnz be >= 0");

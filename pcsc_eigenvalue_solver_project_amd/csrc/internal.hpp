@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "eigsol_hip.h"
@@ -43,25 +44,67 @@ int fail(int status, const std::string& msg);
     } while (0)
 
 // ------------------------------------------------------------------ scalars
-// Complex values are (re, im) pairs, 16-byte aligned so one lane loads one value with a single
-// 16-byte load.  Arithmetic mirrors what g++ emits for std::complex<double> in the reference:
-// products (ac-bd, ad+bc) with separate roundings (no FMA contraction: see kernels' pragma).
+// Complex values are (re, im) pairs, aligned to their size so one lane loads one value with a
+// single 16-byte (cplx) or 8-byte (cplxf) load.  Arithmetic mirrors what g++ emits for
+// std::complex<T> in the reference: products (ac-bd, ad+bc) with separate roundings (no FMA
+// contraction: see the kernels' pragma).  float / cplxf are the reference's float and
+// std::complex<float> instantiations (ScalarConcept, types.hpp:28-30): stored and multiplied in
+// single precision; norm and Rayleigh partial sums accumulate in double (every single-precision
+// square and product is exact in double).
 struct alignas(16) cplx {
     double re, im;
+};
+struct alignas(8) cplxf {
+    float re, im;
 };
 
 __host__ __device__ inline double sq_abs(double a) { return a * a; }
 __host__ __device__ inline double sq_abs(cplx a) { return a.re * a.re + a.im * a.im; }
+__host__ __device__ inline double sq_abs(float a) { return (double)a * (double)a; }
+__host__ __device__ inline double sq_abs(cplxf a) {
+    return (double)a.re * (double)a.re + (double)a.im * (double)a.im;
+}
 
 template <class S> __host__ __device__ inline S s_zero();
 template <> __host__ __device__ inline double s_zero<double>() { return 0.0; }
 template <> __host__ __device__ inline cplx s_zero<cplx>() { return cplx{0.0, 0.0}; }
+template <> __host__ __device__ inline float s_zero<float>() { return 0.0f; }
+template <> __host__ __device__ inline cplxf s_zero<cplxf>() { return cplxf{0.0f, 0.0f}; }
 
 template <class S> struct dtype_of;
 template <> struct dtype_of<double> { static constexpr int value = EIGSOL_F64; };
 template <> struct dtype_of<cplx> { static constexpr int value = EIGSOL_C128; };
+template <> struct dtype_of<float> { static constexpr int value = EIGSOL_F32; };
+template <> struct dtype_of<cplxf> { static constexpr int value = EIGSOL_C64; };
 
-inline size_t scalar_bytes(int dtype) { return dtype == EIGSOL_C128 ? 16 : 8; }
+// real scalars are packed in lane pairs by the sliced layout; complex ones one per lane
+template <class S> inline constexpr bool is_real_v = std::is_same_v<S, double> || std::is_same_v<S, float>;
+template <class S> inline constexpr bool is_cplx_v = !is_real_v<S>;
+
+inline bool dtype_complex(int dtype) { return dtype == EIGSOL_C128 || dtype == EIGSOL_C64; }
+inline bool dtype_single(int dtype) { return dtype == EIGSOL_F32 || dtype == EIGSOL_C64; }
+inline bool dtype_valid(int dtype) { return dtype >= EIGSOL_F64 && dtype <= EIGSOL_C64; }
+inline size_t scalar_bytes(int dtype) {
+    return dtype == EIGSOL_C128 ? 16 : dtype == EIGSOL_F32 ? 4 : 8;
+}
+// (re, im) in double -> one scalar of `dtype` at dst (results, traces, shifts)
+inline void store_scalar(void* dst, int dtype, double re, double im) {
+    switch (dtype) {
+        case EIGSOL_F64: *static_cast<double*>(dst) = re; break;
+        case EIGSOL_C128: static_cast<double*>(dst)[0] = re; static_cast<double*>(dst)[1] = im; break;
+        case EIGSOL_F32: *static_cast<float*>(dst) = (float)re; break;
+        default: static_cast<float*>(dst)[0] = (float)re; static_cast<float*>(dst)[1] = (float)im; break;
+    }
+}
+inline void load_scalar(const void* src, int dtype, double& re, double& im) {
+    im = 0.0;
+    switch (dtype) {
+        case EIGSOL_F64: re = *static_cast<const double*>(src); break;
+        case EIGSOL_C128: re = static_cast<const double*>(src)[0]; im = static_cast<const double*>(src)[1]; break;
+        case EIGSOL_F32: re = *static_cast<const float*>(src); break;
+        default: re = static_cast<const float*>(src)[0]; im = static_cast<const float*>(src)[1]; break;
+    }
+}
 
 // ------------------------------------------------------------------ power-iteration state
 // Carried state, double-buffered by launch parity (launch with parity p reads st[p], writes st[p^1]).

@@ -40,6 +40,32 @@ __device__ __forceinline__ void acc_dot(double& rr, double& ri, cplx x, cplx y) 
 __device__ __forceinline__ void set_re_im(double& dst, double re, double /*im*/) { dst = re; }
 __device__ __forceinline__ void set_re_im(cplx& dst, double re, double im) { dst = cplx{re, im}; }
 
+// single precision (float, std::complex<float>): float products and sums, norm / dot partials in
+// double (exact products of floats); x = y / normY divides by the float normY like the reference
+__device__ __forceinline__ float mul(float a, float b) { return a * b; }
+__device__ __forceinline__ cplxf mul(cplxf a, cplxf b) {
+    return cplxf{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+__device__ __forceinline__ float add(float a, float b) { return a + b; }
+__device__ __forceinline__ cplxf add(cplxf a, cplxf b) { return cplxf{a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ float sub(float a, float b) { return a - b; }
+__device__ __forceinline__ cplxf sub(cplxf a, cplxf b) { return cplxf{a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ float divr(float a, double r) { return a / (float)r; }
+__device__ __forceinline__ cplxf divr(cplxf a, double r) {
+    const float f = (float)r;
+    return cplxf{a.re / f, a.im / f};
+}
+__device__ __forceinline__ void acc_dot(double& rr, double& /*ri*/, float x, float y) {
+    rr += (double)x * (double)y;
+}
+__device__ __forceinline__ void acc_dot(double& rr, double& ri, cplxf x, cplxf y) {
+    const double xr = x.re, xi = x.im, yr = y.re, yi = y.im;
+    rr += xr * yr + xi * yi;
+    ri += xr * yi - xi * yr;
+}
+__device__ __forceinline__ void set_re_im(float& dst, double re, double /*im*/) { dst = (float)re; }
+__device__ __forceinline__ void set_re_im(cplxf& dst, double re, double im) { dst = cplxf{(float)re, (float)im}; }
+
 // Deterministic xor-butterfly: every lane ends with the same bits.
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -162,6 +188,17 @@ __device__ __forceinline__ double ld_sys_s(const double* p) { return ld_sys(p); 
 __device__ __forceinline__ cplx ld_sys_s(const cplx* p) {
     return cplx{ld_sys(&p->re), ld_sys(&p->im)};
 }
+__device__ __forceinline__ float ld_sys_s(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ cplxf ld_sys_s(const cplxf* p) { return cplxf{ld_sys_s(&p->re), ld_sys_s(&p->im)}; }
+__device__ __forceinline__ void st_sys_s(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys_s(cplxf* p, cplxf v) {
+    st_sys_s(&p->re, v.re);
+    st_sys_s(&p->im, v.im);
+}
 __device__ __forceinline__ void st_sys_s(double* p, double v) { st_sys(p, v); }
 __device__ __forceinline__ void st_sys_s(cplx* p, cplx v) {
     st_sys(&p->re, v.re);
@@ -248,7 +285,7 @@ __device__ __forceinline__ void power_prologue(PowerCtl* ctl, const part4* rank_
                 }
             }
             const double nrm = sqrt(n2);
-            const bool cplx_ = dtype_of<S>::value == EIGSOL_C128;
+            const bool cplx_ = is_cplx_v<S>;
             const PowerDecision d = power_decide(t, ctl->max_iter, ctl->tol, cplx_, nrm, rr, ri,
                                                  in.rho_re, in.rho_im);
             if (blockIdx.x == 0) {
@@ -335,6 +372,11 @@ __device__ __forceinline__ cplx cdiv(cplx a, cplx b) {
 }
 __device__ __forceinline__ double sdiv(double a, double b) { return a / b; }
 __device__ __forceinline__ cplx sdiv(cplx a, cplx b) { return cdiv(a, b); }
+__device__ __forceinline__ float sdiv(float a, float b) { return a / b; }
+__device__ __forceinline__ cplxf sdiv(cplxf a, cplxf b) {
+    const float d = b.re * b.re + b.im * b.im;
+    return cplxf{(a.re * b.re + a.im * b.im) / d, (a.im * b.re - a.re * b.im) / d};
+}
 
 // Launch prologue of the fused shifted-inverse iteration (shiftedInversePowerImpl,
 // src/power_method/shifted_inverse_power_solver.hpp:48-76).  Launch t solves (A - sigma I) y_t = x_t
@@ -355,7 +397,7 @@ __device__ __forceinline__ void shift_prologue(PowerCtl* ctl, const part4* rank_
             const int32_t t = in.t + 1;
             const double n2 = rank_part[0].a, pr_ = rank_part[0].b, pi_ = rank_part[0].c;
             const double nrm = sqrt(n2);
-            const bool cplx_ = dtype_of<S>::value == EIGSOL_C128;
+            const bool cplx_ = is_cplx_v<S>;
             bool fin = false, conv = false, rec = false;
             int32_t iters = 0, fpar = 0;
             double lre = in.rho_re, lim = in.rho_im, fnorm = 0.0;

@@ -486,7 +486,7 @@ int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_ou
         it = s->host_ctl->iters;
         conv = s->host_ctl->converged;
     }
-    if (lambda_out) std::memcpy(lambda_out, lam, sb);
+    if (lambda_out) store_scalar(lambda_out, s->dtype, lam[0], lam[1]);
     if (iterations) *iterations = it;
     if (converged) *converged = conv;
     if (x_out) {
@@ -537,7 +537,7 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
         const double nnz = (double)s->csr->nnz, n = (double)s->csr->nrows;
         if (bytes) *bytes = (sb + 4.0) * nnz + 4.0 * (n + 1.0) + 2.0 * sb * n;
         if (tiles) *tiles = s->csr->sliced ? s->csr->nslices : s->csr->ntiles;
-        if (variant) *variant = s->csr->sliced ? 5 : (s->csr->windowed ? 1 : 0);
+        if (variant) *variant = s->csr->sliced ? 5 : dtype_single(s->dtype) ? 6 : (s->csr->windowed ? 1 : 0);
     } else {
         const double n = (double)s->dense->nrows;
         if (bytes) *bytes = sb * n * n + 2.0 * sb * n;

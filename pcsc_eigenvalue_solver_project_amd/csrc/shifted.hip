@@ -106,6 +106,17 @@ __device__ __forceinline__ void st_coh(cplx* p, cplx v) {
     st_agent(&p->re, v.re);
     st_agent(&p->im, v.im);
 }
+__device__ __forceinline__ void st_coh(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coh(cplxf* p, cplxf v) {
+    st_coh(&p->re, v.re);
+    st_coh(&p->im, v.im);
+}
+__device__ __forceinline__ float ld_coh(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ cplxf ld_coh(const cplxf* p) { return cplxf{ld_coh(&p->re), ld_coh(&p->im)}; }
 __device__ __forceinline__ double ld_coh(const double* p) { return ld_agent(p); }
 __device__ __forceinline__ cplx ld_coh(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
 
@@ -115,20 +126,30 @@ __device__ __forceinline__ int ld_flag_err(const int32_t* p) {
 
 __device__ __forceinline__ bool unready(double v) { return (unsigned long long)__double_as_longlong(v) == kSent; }
 __device__ __forceinline__ bool unready(cplx v) { return unready(v.re) || unready(v.im); }
+// single precision: every 32-bit word of an unsolved entry holds the low word of kSent (a NaN)
+__device__ __forceinline__ bool unready(float v) { return __float_as_uint(v) == (uint32_t)(kSent & 0xffffffffu); }
+__device__ __forceinline__ bool unready(cplxf v) { return unready(v.re) || unready(v.im); }
 __device__ __forceinline__ double sanitize(double v) {
     return unready(v) ? __longlong_as_double(0x7FF8000000000000ll) : v;
 }
 __device__ __forceinline__ cplx sanitize(cplx v) { return cplx{sanitize(v.re), sanitize(v.im)}; }
+__device__ __forceinline__ float sanitize(float v) { return unready(v) ? __uint_as_float(0x7FC00000u) : v; }
+__device__ __forceinline__ cplxf sanitize(cplxf v) { return cplxf{sanitize(v.re), sanitize(v.im)}; }
 template <class S>
 __device__ __forceinline__ S sentinel() {
     const double s = __longlong_as_double((long long)kSent);
+    const float sf = __uint_as_float((uint32_t)(kSent & 0xffffffffu));
     if constexpr (std::is_same_v<S, double>) return s;
-    else return cplx{s, s};
+    else if constexpr (std::is_same_v<S, cplx>) return cplx{s, s};
+    else if constexpr (std::is_same_v<S, float>) return sf;
+    else return cplxf{sf, sf};
 }
 template <class S>
 __device__ __forceinline__ S s_one() {
     if constexpr (std::is_same_v<S, double>) return 1.0;
-    else return cplx{1.0, 0.0};
+    else if constexpr (std::is_same_v<S, cplx>) return cplx{1.0, 0.0};
+    else if constexpr (std::is_same_v<S, float>) return 1.0f;
+    else return cplxf{1.0f, 0.0f};
 }
 
 // sum over the 16 lanes of a row group (xor butterfly inside the group: every lane gets the sum)
@@ -138,6 +159,12 @@ __device__ __forceinline__ double group_sum(double v) {
     return v;
 }
 __device__ __forceinline__ cplx group_sum(cplx v) { return cplx{group_sum(v.re), group_sum(v.im)}; }
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int off = kRowLanes / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ cplxf group_sum(cplxf v) { return cplxf{group_sum(v.re), group_sum(v.im)}; }
 
 // poll z[j] until solved (bounded; a broken wait sets the sticky error word and gives up)
 template <class S>
@@ -735,12 +762,29 @@ __global__ void shift_diag_kernel(S* a, int64_t n, S sigma) {
 }  // namespace dev
 
 // ================================================================== host side
+// the dense LU (and the densified general-sparse path) is built for the double instantiations
+template <class S> inline constexpr bool kDenseLU = std::is_same_v<S, double> || std::is_same_v<S, cplx>;
 int resident_blocks(eigsol_ctx* ctx, const void* kernel, int threads, size_t dyn_lds, int* grid);
 
 template <class S>
 static S make_sigma(double re, double im) {
     if constexpr (std::is_same_v<S, double>) { (void)im; return re; }
-    else return cplx{re, im};
+    else if constexpr (std::is_same_v<S, cplx>) return cplx{re, im};
+    else if constexpr (std::is_same_v<S, float>) { (void)im; return (float)re; }
+    else return cplxf{(float)re, (float)im};
+}
+// host arithmetic of the factor set-up (pivots d_i - sigma) in the scalar's own precision
+template <class S> static S h_add(S a, S b) {
+    if constexpr (is_real_v<S>) return a + b;
+    else return S{a.re + b.re, a.im + b.im};
+}
+template <class S> static S h_sub(S a, S b) {
+    if constexpr (is_real_v<S>) return a - b;
+    else return S{a.re - b.re, a.im - b.im};
+}
+template <class S> static bool h_zero(S a) {
+    if constexpr (is_real_v<S>) return a == 0;
+    else return a.re == 0 && a.im == 0;
 }
 
 static void shift_free(ShiftFactor* f) {
@@ -871,6 +915,9 @@ static int factor_dense_t(eigsol_dense* A, double sre, double sim, ShiftFactor**
 }
 
 int shift_factor_dense(eigsol_dense* A, const void* sigma, ShiftFactor** out) {
+    if (dtype_single(A->dtype))
+        return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: single-precision dense factors are not built "
+                                          "(the C++ facade promotes them to double)");
     double s[2] = {0.0, 0.0};
     std::memcpy(s, sigma, scalar_bytes(A->dtype));
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
@@ -929,6 +976,11 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
     f->nnz_total = nnz;
     int rc = EIGSOL_OK;
     if (!up && !lo) {
+        if constexpr (!kDenseLU<S>) {
+            shift_free(f);
+            return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: single-precision factors exist for triangular "
+                                              "sparse matrices only");
+        } else {
         // general sparse pattern: densify on the device and LU it (the reference's SparseLU)
         rc = dense_limits(A->dtype, n, "solve_shifted (non-triangular sparse)");
         const size_t bytes = (size_t)n * n * sizeof(S);
@@ -942,6 +994,7 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         if (rc != EIGSOL_OK) { shift_free(f); return rc; }
         *out = f;
         return EIGSOL_OK;
+        }
     }
     f->upper = up ? 1 : 0;
     // split diagonal / off-diagonal; pivots d_i - sigma (missing diagonal: 0 - sigma)
@@ -954,19 +1007,14 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         S d = s_zero<S>();
         for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
             if (ci[e] == i) {
-                if constexpr (std::is_same_v<S, double>) d = d + v[e];
-                else d = cplx{d.re + v[e].re, d.im + v[e].im};
+                d = h_add(d, v[e]);
             } else {
                 oci.push_back(ci[e]);
                 ov.push_back(v[e]);
             }
         }
-        if constexpr (std::is_same_v<S, double>) pv[i] = d - sig;
-        else pv[i] = cplx{d.re - sig.re, d.im - sig.im};
-        const bool zero = std::is_same_v<S, double> ? (reinterpret_cast<double*>(&pv[i])[0] == 0.0)
-                                                     : (reinterpret_cast<double*>(&pv[i])[0] == 0.0 &&
-                                                        reinterpret_cast<double*>(&pv[i])[1] == 0.0);
-        if (zero) {
+        pv[i] = h_sub(d, sig);
+        if (h_zero(pv[i])) {
             shift_free(f);
             return fail(EIGSOL_E_SOLVER, "solve_shifted: SparseLU factorization failed");
         }
@@ -1038,10 +1086,14 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
 int shift_factor_csr(eigsol_csr* A, const void* sigma, ShiftFactor** out) {
     if (A->dist) return fail(EIGSOL_E_UNSUPPORTED, "shifted inverse iteration: row-sharded matrices are not supported");
     double s[2] = {0.0, 0.0};
-    std::memcpy(s, sigma, scalar_bytes(A->dtype));
+    load_scalar(sigma, A->dtype, s[0], s[1]);
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
-    return A->dtype == EIGSOL_C128 ? factor_csr_t<cplx>(A, s[0], s[1], out)
-                                   : factor_csr_t<double>(A, s[0], 0.0, out);
+    switch (A->dtype) {
+        case EIGSOL_C128: return factor_csr_t<cplx>(A, s[0], s[1], out);
+        case EIGSOL_F32: return factor_csr_t<float>(A, s[0], 0.0, out);
+        case EIGSOL_C64: return factor_csr_t<cplxf>(A, s[0], s[1], out);
+        default: return factor_csr_t<double>(A, s[0], 0.0, out);
+    }
 }
 
 int shift_grid(const ShiftFactor* f) { return (f->kind == 0 || f->dense_multi) ? f->grid : 1; }
@@ -1086,6 +1138,8 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.sig_im = f->sig_im;
         if (iter) hipLaunchKernelGGL((dev::sptrsv_kernel<S, true>), dim3(f->grid), dim3(dev::kThreads), 0, st, a, parity);
         else hipLaunchKernelGGL((dev::sptrsv_kernel<S, false>), dim3(f->grid), dim3(dev::kThreads), 0, st, a, parity);
+    } else if constexpr (!kDenseLU<S>) {
+        return fail(EIGSOL_E_UNSUPPORTED, "single-precision dense factor");
     } else if (f->dense_multi) {
         dev::DenseTriArgs<S> a{};
         a.lu = static_cast<const S*>(f->lu);
@@ -1136,17 +1190,27 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
     return EIGSOL_OK;
 }
 
+template <class F>
+static int by_dtype(int dtype, F&& fn) {
+    switch (dtype) {
+        case EIGSOL_C128: return fn(cplx{});
+        case EIGSOL_F32: return fn(0.0f);
+        case EIGSOL_C64: return fn(cplxf{});
+        default: return fn(0.0);
+    }
+}
+
 int shift_iter_launch(ShiftFactor* f, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
                       void* my_part, void* trace, int parity) {
-    return f->dtype == EIGSOL_C128
-               ? shift_launch_t<cplx>(f, true, nullptr, nullptr, buf0, buf1, ctl, rank_part, my_part, trace, parity)
-               : shift_launch_t<double>(f, true, nullptr, nullptr, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+    return by_dtype(f->dtype, [&](auto tag) {
+        return shift_launch_t<decltype(tag)>(f, true, nullptr, nullptr, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+    });
 }
 
 int shift_solve_launch(ShiftFactor* f, const void* b_dev, void* y_dev) {
-    return f->dtype == EIGSOL_C128
-               ? shift_launch_t<cplx>(f, false, b_dev, y_dev, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0)
-               : shift_launch_t<double>(f, false, b_dev, y_dev, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+    return by_dtype(f->dtype, [&](auto tag) {
+        return shift_launch_t<decltype(tag)>(f, false, b_dev, y_dev, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+    });
 }
 
 // algorithmic bytes of one solve (the SpTRSV counts like the SpMV) and variant

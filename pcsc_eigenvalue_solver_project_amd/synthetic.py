@@ -143,11 +143,12 @@ def start_vector(n: int, dtype=np.float64, seed: int = 7, row0: int = 0) -> np.n
     """x0 of SURVEY §8d: U(-1, 1) per (re, im) component, seed 7 (normalised by the solver).
     Entries [row0, row0 + n) of the global start vector, drawn in the generators' fixed chunks, so
     a row block's slice is bitwise the slice of the N = 1 vector."""
-    x = np.empty(n, dtype=np.complex128 if np.dtype(dtype) == np.complex128 else np.float64)
+    cx = np.issubdtype(np.dtype(dtype), np.complexfloating)
+    x = np.empty(n, dtype=np.complex128 if cx else np.float64)
     for c, base, a, b in _chunks(row0, n):
         rng = np.random.default_rng([seed, c, 3])
         re = rng.uniform(-1.0, 1.0, CHUNK)
-        if np.dtype(dtype) == np.complex128:
+        if cx:
             x[a - row0:b - row0] = re[a - base:b - base] + 1j * rng.uniform(-1.0, 1.0, CHUNK)[a - base:b - base]
         else:
             x[a - row0:b - row0] = re[a - base:b - base]
