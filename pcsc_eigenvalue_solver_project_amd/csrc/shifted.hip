@@ -40,14 +40,32 @@ struct ShiftFactor {
     int upper = 1;
     int64_t nnz_total = 0;        // nonzeros of A (diagonal included), for roofline accounting
     int64_t nnz_off = 0;
-    int32_t* order = nullptr;     // position -> row (-1: level padding)
-    int32_t* pptr = nullptr;      // position -> first off-diagonal entry (npos + 1)
-    int32_t* pcol = nullptr;      // off-diagonal columns (original row numbering), position order
-    void* pval = nullptr;
-    void* ppiv = nullptr;         // d_i - sigma, by position
+    int32_t* order = nullptr;     // head position -> row (-1: level padding)
     void* z[2] = {nullptr, nullptr};   // solve values polled by readers; sentinel = not yet solved
     int32_t npos = 0, nchunks = 0, nlevels = 0;
-    uint32_t* work = nullptr;     // last-arriver ticket
+    void* hval = nullptr;         // head, pass-major entries / columns / pivots
+    int32_t* hcol = nullptr;
+    void* hpiv = nullptr;
+    int2* passes = nullptr;       // head passes {first position, end | barrier}
+    int32_t npass = 0, hpos = 0, hlevels = 0;
+    int red_grid = 0;             // blocks of the partials reduction
+    int2* smeta = nullptr;        // tail slices (see sptrsv_slice_kernel)
+    int32_t* trow = nullptr;
+    void* tpiv = nullptr;
+    int32_t* tcol = nullptr;
+    void* tval = nullptr;
+    int32_t nslices = 0;
+    int slice_b = 16;             // entries per lane held in registers (4, 8 or 16)
+    int tail_chunks = 0;          // tail variant: 1 chunk kernel, 0 slice kernel
+    int32_t* porder = nullptr;    // chunk variant (see sptrsv_chunk_kernel)
+    int32_t* pptr = nullptr;
+    int32_t* pcol = nullptr;
+    void* pval = nullptr;
+    void* ppiv = nullptr;
+    int32_t chunk0 = 0;
+    int poll_fast = 0;            // tail polls without back-off (EIGSOL_TRSV_POLL_FAST)
+    int poll_mode = 0;            // EIGSOL_TRSV_POLL_MODE
+    uint32_t* work = nullptr;     // [2]: last-arriver ticket of the partials reduction
     int32_t* err = nullptr;
     void* wave_part = nullptr;    // part4 per wave
     int32_t epoch = 0;
@@ -78,12 +96,26 @@ constexpr unsigned long long kSent = 0x7FF4DEAD7FF4DEADull;
 
 template <class S>
 struct TriArgs {
-    const int32_t* order;
+    const int32_t* order;  // head position -> row
+    const S* hval;         // head, pass-major: entry k of group g of pass q at (q * 64 + g) * 16 + k
+    const int32_t* hcol;   // LDS position of the column (padding: the zero slot hpos)
+    const S* hpiv;         // pivot of group g of pass q at q * 64 + g
+    const int2* passes;    // head passes
+    int32_t npass, hpos;   // head passes, head positions
+    const int2* smeta;     // tail slices: {entry offset, entries per lane}
+    const int32_t* trow;   // row of lane l of slice s at s * 64 + l (-1: padding)
+    const S* tpiv;
+    const int32_t* tcol;   // entry k of lane l of slice s at off + 64 k + l (padding: the zero slot n)
+    const S* tval;
+    int32_t nslices;
+    const int32_t* porder; // chunk variant, position-indexed: row (-1: padding), entries, pivots
     const int32_t* pptr;
     const int32_t* pcol;
     const S* pval;
     const S* ppiv;
-    int32_t nchunks;
+    int32_t chunk0, nchunks;
+    int32_t poll_fast;     // tail: polls re-issued without back-off
+    int32_t poll_mode;     // 0: re-poll every unsolved dependency, 1: one per lane
     int64_t n;
     S* zcur;            // polled by this launch
     S* znext;           // reset to the sentinel by this launch, for the next one
@@ -152,16 +184,44 @@ __device__ __forceinline__ S s_one() {
     else return cplxf{1.0f, 0.0f};
 }
 
-// sum over the 16 lanes of a row group (xor butterfly inside the group: every lane gets the sum)
+// sum over the 16 lanes of a row group.  16 lanes: a DPP butterfly over the lane-index xor
+// masks 15 (row_mirror), 7 (row_half_mirror), 3 and 1 (quad_perm), which span all 16 lanes:
+// four VALU steps instead of four LDS-latency ds_bpermute round trips, and every lane of the
+// group ends with the same bits (each step adds the same two values in both lanes).
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), kCtrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), kCtrl, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+template <int kCtrl>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xf, 0xf, false));
+}
+constexpr int kDppRowMirror = 0x140, kDppRowHalfMirror = 0x141, kDppQuad3210 = 0x1B, kDppQuad1032 = 0xB1;
 __device__ __forceinline__ double group_sum(double v) {
+    if constexpr (kRowLanes == 16) {
+        v += dpp_f64<kDppRowMirror>(v);
+        v += dpp_f64<kDppRowHalfMirror>(v);
+        v += dpp_f64<kDppQuad3210>(v);
+        v += dpp_f64<kDppQuad1032>(v);
+    } else {
 #pragma unroll
-    for (int off = kRowLanes / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        for (int off = kRowLanes / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    }
     return v;
 }
 __device__ __forceinline__ cplx group_sum(cplx v) { return cplx{group_sum(v.re), group_sum(v.im)}; }
 __device__ __forceinline__ float group_sum(float v) {
+    if constexpr (kRowLanes == 16) {
+        v += dpp_f32<kDppRowMirror>(v);
+        v += dpp_f32<kDppRowHalfMirror>(v);
+        v += dpp_f32<kDppQuad3210>(v);
+        v += dpp_f32<kDppQuad1032>(v);
+    } else {
 #pragma unroll
-    for (int off = kRowLanes / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        for (int off = kRowLanes / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    }
     return v;
 }
 __device__ __forceinline__ cplxf group_sum(cplxf v) { return cplxf{group_sum(v.re), group_sum(v.im)}; }
@@ -186,29 +246,130 @@ __device__ __forceinline__ S wait_value(const S* z, int j, int32_t* err) {
     return y;
 }
 
-template <class S>
-struct RowMeta {
-    int i, e0, len, j;
-    S v, bi, pv;
-};
+// ---- head: the narrow leading levels, one workgroup, solved values in LDS.
+// Levels [0, nhl) hold few rows each (the bottom of an upper-triangular DAG: the first 185 of
+// config 5's 372 levels hold 9k of its 1M rows).  Through memory every level costs a coherent
+// store + poll round trip (~1.1 us); here a level is a workgroup barrier and LDS reads.  Every
+// column a head row reads is an earlier head row (lower level), so columns are LDS positions.
+// Pass-major layout built at factor time: pass q (64 rows of one level, one per 16-lane group)
+// stores entry k of its group g at hval/hcol[(q * 64 + g) * 16 + k] (padded: column -1) and the
+// group's pivot at hpiv[q * 64 + g].  No load depends on another, so the loads of the next kHeadDepth
+// passes are in flight (a register ring) while a pass computes: a pass costs its LDS and
+// arithmetic latency, not a memory round trip.  zl starts as the scaled right-hand side.
+// Padding entries read the zero slot zl[hpos] with value zero; the pass count is padded to a
+// multiple of the ring depth with empty passes, so the ring loop is straight-line code.
+constexpr int kHeadThreads = 1024;
+constexpr int kHeadRows = kHeadThreads / kRowLanes;    // rows per pass
+constexpr int kHeadDepth = 8;                          // passes in flight
+constexpr int32_t kPassBarrier = 1 << 30;
 
-// Sync-free triangular solve, static schedule.  Positions (rows sorted by level, every level
-// padded to a multiple of kWaveRows) form chunks of one wave round; chunk c belongs to wave
-// c mod W of the W resident waves, which takes its chunks in increasing order.  A row waits only
-// on rows of strictly lower level, i.e. strictly earlier chunks, and the four rows of a round
-// never depend on each other, so the earliest unfinished chunk can always proceed: progress
-// needs every wave resident (the grid is sized to one residency round); a bounded spin plus a
-// sticky error word guarantees the grid drains even if that were violated.
-// The solved value is its own ready flag (z starts as the sentinel NaN): a dependency costs one
-// coherent load, and the producer publishes with one store.  Each launch resets the other z
-// buffer row by row for the next launch (also when it exits early), so no reset pass exists.
-// The metadata of the next two chunks is in flight while the current one waits.
-// Norm and Rayleigh partials accumulate per wave in a fixed chunk order: deterministic.
 template <class S, bool kIter>
-__global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int parity) {
+__global__ __launch_bounds__(kHeadThreads) void sptrsv_head_kernel(TriArgs<S> a, int parity) {
+    extern __shared__ __align__(16) unsigned char head_lds[];
+    S* zl = reinterpret_cast<S*>(head_lds);
+    // zl[hpos] is a zero (the column of padding entries, whose values are zero too)
+    int2* pl = reinterpret_cast<int2*>(head_lds + (size_t)(a.hpos + 1) * sizeof(S));   // pass table
     __shared__ Prologue pro;
-    __shared__ int s_last;
-    __shared__ double sm[3 * kWaves];
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kIter) {
+        shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // the tail kernel resets z
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.b_plain;
+        yout = a.y_plain;
+    }
+    const int tid = threadIdx.x;
+    const int lane = tid & (kRowLanes - 1);
+    const int grp = tid / kRowLanes;
+    const int npass = a.npass;
+    S rv[kHeadDepth], rp[kHeadDepth];
+    int rc[kHeadDepth];
+    auto load = [&](int q, S& v, int& c, S& p) {
+        const uint32_t e = (uint32_t)(q < npass ? q : 0) * kHeadThreads + (uint32_t)tid;
+        v = ldg_stream(a.hval, e);
+        c = (int)ldg_stream(a.hcol, e);
+        p = ldg_stream(a.hpiv, (uint32_t)(q < npass ? q : 0) * kHeadRows + (uint32_t)grp);
+    };
+#pragma unroll
+    for (int u = 0; u < kHeadDepth; ++u) load(u, rv[u], rc[u], rp[u]);
+    for (int p = tid; p < a.hpos; p += kHeadThreads) {
+        const int i = a.order[p];
+        S b = xin[i >= 0 ? i : 0];
+        if constexpr (kIter) b = scale_in(b, nrm);
+        zl[p] = b;
+    }
+    if (tid == 0) zl[a.hpos] = s_zero<S>();
+    for (int q = tid; q < npass; q += kHeadThreads) pl[q] = a.passes[q];
+    __syncthreads();
+    for (int q0 = 0; q0 < npass; q0 += kHeadDepth) {
+#pragma unroll
+        for (int u = 0; u < kHeadDepth; ++u) {   // straight line: npass is a multiple of the depth
+            const int q = q0 + u;
+            const int2 pb = pl[q];   // LDS: a vector load here would wait for the ring (vmcnt is in order)
+            S acc = group_sum(mul(rv[u], zl[rc[u]]));
+            const int pos = pb.x + grp;
+            if (lane == 0 && pos < (pb.y & ~kPassBarrier)) zl[pos] = sdiv(sub(zl[pos], acc), rp[u]);
+            if (pb.y & kPassBarrier) __syncthreads();
+            load(q + kHeadDepth, rv[u], rc[u], rp[u]);
+            asm volatile("" ::: "memory");   // keep the refills in ring order (vmcnt retires in issue order)
+        }
+    }
+    __syncthreads();
+    // publish: the tail kernel (next in stream order) reads these through z
+    for (int p = tid; p < a.hpos; p += kHeadThreads) {
+        const int i = a.order[p];
+        if (i < 0) continue;
+        const S yi = sanitize(zl[p]);
+        a.zcur[i] = yi;
+        yout[i] = yi;
+        a.znext[i] = sentinel<S>();
+    }
+}
+
+// first poll of a dependency is issued early (ld_coh); this finishes the wait
+template <class S>
+__device__ __forceinline__ S finish_wait(S y, const S* z, int j, int32_t* err, int fast) {
+    int spins = 0;
+    while (unready(y)) {
+        if (spins < fast) {}          // re-poll at once: the value is due within a round trip
+        else if (spins < fast + 4) __builtin_amdgcn_s_sleep(2);
+        else if (spins < fast + 16) __builtin_amdgcn_s_sleep(8);
+        else __builtin_amdgcn_s_sleep(32);
+        y = ld_coh(z + j);
+        if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(err) != 0)) {
+            atomicOr(err, 1);
+            break;
+        }
+    }
+    return y;
+}
+
+// ---- tail: sync-free triangular solve over the remaining (wide) levels, one row per lane.
+// The rows of each tail level are cut into slices of 64 (a level's last slice is padded with
+// empty rows, so a slice never spans two levels and its lanes never wait on each other).  Slice
+// s stores entry k of lane l at off_s + 64 k + l (coalesced), padded to at least B entries per
+// lane with the zero slot z[n] (always 0) and value 0.  A lane computes its row exactly as the
+// reference's back substitution does: s = b_i, s -= a_ij z_j in stored column order, y_i = s / d_i
+// (oracle triu_shifted_solve_csr: bitwise equal when no FMA is contracted).
+// Slices are dealt round-robin to the W waves, each taking its slices in increasing order.  A
+// slice waits only on slices of strictly lower levels, i.e. earlier slices, so the earliest
+// unfinished slice can always proceed provided every wave is resident: the kernel is launched
+// cooperatively, so the runtime guarantees co-residency (or refuses the launch); a bounded spin
+// plus a sticky error word still guarantee the grid drains.  (A ticket dispenser needs no
+// co-residency, but 250k atomics on one word serialise: 3.3 ms against 0.9 ms.)
+// Per slice: the B dependency loads (coherent; the solved value is its own ready flag, z starts
+// as the sentinel NaN) and the B values are issued first, then the columns / row / pivot of the
+// wave's next slice, so waiting on the dependencies does not wait on the prefetch (vmcnt retires
+// in issue order).  Each launch resets the other z buffer row by row for the next launch (also
+// when it exits early).  Norm / Rayleigh partials are reduced afterwards by shift_part_kernel.
+template <class S, int B, bool kIter>
+__global__ __launch_bounds__(kThreads) void sptrsv_slice_kernel(TriArgs<S> a, int parity) {
+    __shared__ Prologue pro;
     const S* xin;
     S* yout;
     double nrm = 0.0;
@@ -227,17 +388,143 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
         xin = a.b_plain;
         yout = a.y_plain;
     }
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int W = gridDim.x * kWaves;
+    const int ns = a.nslices;
+    // consecutive slices (the slices of one level) go to consecutive workgroups, i.e. to
+    // different CUs and XCDs, not to the four waves of one CU
+    int s = wave * gridDim.x + blockIdx.x;
+
+    int K, off, row;
+    S piv;
+    int col[B];
+    auto fetch = [&](int s_, int& K_, int& off_, int* c, int& row_, S& piv_) {
+        const bool in = s_ < ns;
+        const int2 m = a.smeta[in ? s_ : 0];
+        K_ = in ? m.y : 0;
+        off_ = m.x;
+#pragma unroll
+        for (int k = 0; k < B; ++k) c[k] = (int)ldg_stream(a.tcol, (uint32_t)(off_ + 64 * k + lane));
+        const uint32_t r = (uint32_t)((in ? s_ : 0) * 64 + lane);
+        row_ = in ? (int)ldg_stream(a.trow, r) : -1;
+        piv_ = ldg_stream(a.tpiv, r);
+    };
+    fetch(s, K, off, col, row, piv);
+    for (; s < ns; s += W) {
+        S z[B], v[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) z[k] = ld_coh(a.zcur + col[k]);
+#pragma unroll
+        for (int k = 0; k < B; ++k) v[k] = ldg_stream(a.tval, (uint32_t)(off + 64 * k + lane));
+        S bi = xin[row >= 0 ? row : 0];
+        int Kn, offn, rown, coln[B];
+        S pivn;
+        fetch(s + W, Kn, offn, coln, rown, pivn);
+        if constexpr (kIter) bi = scale_in(bi, nrm);
+        S acc = bi;
+        // dependencies not yet solved at the first load: poll them all together (one round trip
+        // per poll round, not one per entry)
+        bool pend = false;
+#pragma unroll
+        for (int k = 0; k < B; ++k) pend = pend || unready(z[k]);
+        int spins = 0;
+        while (pend) {
+            if (spins >= a.poll_fast) {
+                if (spins < a.poll_fast + 8) __builtin_amdgcn_s_sleep(2);
+                else __builtin_amdgcn_s_sleep(16);
+            }
+            if (a.poll_mode == 0) {
+#pragma unroll
+                for (int k = 0; k < B; ++k)
+                    if (unready(z[k])) z[k] = ld_coh(a.zcur + col[k]);
+            } else {   // one poll per lane: its first unsolved dependency
+                int kf = -1;
+#pragma unroll
+                for (int k = B - 1; k >= 0; --k)
+                    if (unready(z[k])) kf = k;
+                S zf = ld_coh(a.zcur + (kf >= 0 ? col[kf] : (int)a.n));
+#pragma unroll
+                for (int k = 0; k < B; ++k)
+                    if (k == kf) z[k] = zf;
+            }
+            pend = false;
+#pragma unroll
+            for (int k = 0; k < B; ++k) pend = pend || unready(z[k]);
+            if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(a.err) != 0)) {
+                atomicOr(a.err, 1);
+                break;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) acc = sub(acc, mul(v[k], z[k]));
+        for (int k = B; k < K; ++k) {   // entries beyond B (long rows): one dependent round trip each
+            const uint32_t e = (uint32_t)(off + 64 * k + lane);
+            const int c = (int)a.tcol[e];
+            acc = sub(acc, mul(a.tval[e], wait_value(a.zcur, c, a.err)));
+        }
+        if (row >= 0) {
+            const S yi = sanitize(sdiv(acc, piv));
+            st_coh(a.zcur + row, yi);        // publish: readers poll this very word
+            yout[row] = yi;
+            a.znext[row] = sentinel<S>();
+        }
+        K = Kn;
+        off = offn;
+        row = rown;
+        piv = pivn;
+#pragma unroll
+        for (int k = 0; k < B; ++k) col[k] = coln[k];
+    }
+}
+
+// ---- tail, chunk variant: sync-free triangular solve, 16 lanes per row, 4 rows per chunk.
+// Positions (level-ordered, every level padded to kWaveRows) form chunks of one wave round;
+// chunk c belongs to wave (c - chunk0) mod W (consecutive chunks on consecutive workgroups), each
+// wave taking its chunks in increasing order, two at a time: the dependency loads of a pair are
+// issued at the end of the previous iteration (speculatively: a sentinel just means poll again),
+// then the first chunk is solved and published, then the second (which may read the first).
+// Progress needs every wave resident: launched cooperatively, like the slice variant.  Chosen
+// for DAGs of many moderately wide levels (config 5: 0.86 ms against 1.3 ms for the slices,
+// which wait on the slowest of 960 dependencies per wave); the slice variant wins on few, very
+// wide levels (one 1M-row level: 74 us against 195 us).
+template <class S>
+struct RowMeta {
+    int i, e0, len, j;
+    S v, bi, pv;
+};
+
+template <class S, bool kIter>
+__global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, int parity) {
+    __shared__ Prologue pro;
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kIter) {
+        shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) {
+            for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < a.n; r += (int64_t)gridDim.x * kThreads)
+                a.znext[r] = sentinel<S>();
+            return;
+        }
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.b_plain;
+        yout = a.y_plain;
+    }
     const int tid = threadIdx.x;
     const int lane = tid & (kRowLanes - 1);
     const int grp = (tid & 63) / kRowLanes;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int W = gridDim.x * kWaves;
-    const int gw = blockIdx.x * kWaves + wave;
+    const int gw = a.chunk0 + wave * gridDim.x + blockIdx.x;
 
     auto fetch1 = [&](int c, RowMeta<S>& m) {   // position-indexed metadata: no dependent loads
         const bool in = c < a.nchunks;
         const int pos = (in ? c : 0) * kWaveRows + grp;
-        m.i = in ? a.order[pos] : -1;
+        m.i = in ? a.porder[pos] : -1;
         const int e0 = a.pptr[pos];
         m.e0 = e0;
         m.len = in ? a.pptr[pos + 1] - e0 : 0;
@@ -250,72 +537,76 @@ __global__ __launch_bounds__(kThreads) void sptrsv_kernel(TriArgs<S> a, int pari
         m.v = ldg_stream(a.pval, (uint32_t)e);
         m.bi = xin[m.i >= 0 ? m.i : 0];
     };
-
-    double n2 = 0.0, pr = 0.0, pi = 0.0;
-    RowMeta<S> cur, nxt;
-    fetch1(gw, cur);
-    fetch2(cur);
-    fetch1(gw + W, nxt);
-    for (int c = gw; c < a.nchunks; c += W) {
-        fetch2(nxt);
-        RowMeta<S> nn;
-        fetch1(c + 2 * W, nn);
+    auto solve = [&](const RowMeta<S>& m, S z0) {
         S acc = s_zero<S>();
-        if (cur.j >= 0) acc = mul(cur.v, wait_value(a.zcur, cur.j, a.err));
-        for (int k = lane + kRowLanes; k < cur.len; k += kRowLanes) {   // rows longer than 16
-            const int e = cur.e0 + k;
+        if (m.j >= 0) acc = mul(m.v, finish_wait(z0, a.zcur, m.j, a.err, a.poll_fast));
+        for (int k = lane + kRowLanes; k < m.len; k += kRowLanes) {   // rows longer than 16
+            const int e = m.e0 + k;
             acc = add(acc, mul(a.pval[e], wait_value(a.zcur, a.pcol[e], a.err)));
         }
         acc = group_sum(acc);
-        if (cur.i >= 0 && lane == 0) {
-            S bi = cur.bi;
+        if (m.i >= 0 && lane == 0) {
+            S bi = m.bi;
             if constexpr (kIter) bi = scale_in(bi, nrm);
-            const S yi = sanitize(sdiv(sub(bi, acc), cur.pv));
-            st_coh(a.zcur + cur.i, yi);      // publish: readers poll this very word
-            yout[cur.i] = yi;
-            a.znext[cur.i] = sentinel<S>();
-            if constexpr (kIter) {
-                n2 += sq_abs(yi);
-                acc_dot(pr, pi, bi, yi);     // p = sum conj(x_i) y_i
-            }
+            const S yi = sanitize(sdiv(sub(bi, acc), m.pv));
+            st_coh(a.zcur + m.i, yi);        // publish: readers poll this very word
+            yout[m.i] = yi;
+            a.znext[m.i] = sentinel<S>();
         }
-        cur = nxt;
-        nxt = nn;
+    };
+
+    RowMeta<S> c0, c1, n0, n1;
+    fetch1(gw, c0);
+    fetch1(gw + W, c1);
+    fetch2(c0);
+    fetch2(c1);
+    fetch1(gw + 2 * W, n0);
+    fetch1(gw + 3 * W, n1);
+    S z0 = c0.j >= 0 ? ld_coh(a.zcur + c0.j) : s_zero<S>();
+    S z1 = c1.j >= 0 ? ld_coh(a.zcur + c1.j) : s_zero<S>();
+    for (int c = gw; c < a.nchunks; c += 2 * W) {
+        fetch2(n0);
+        fetch2(n1);
+        RowMeta<S> m0, m1;
+        fetch1(c + 4 * W, m0);
+        fetch1(c + 5 * W, m1);
+        solve(c0, z0);
+        solve(c1, z1);
+        z0 = n0.j >= 0 ? ld_coh(a.zcur + n0.j) : s_zero<S>();
+        z1 = n1.j >= 0 ? ld_coh(a.zcur + n1.j) : s_zero<S>();
+        c0 = n0;
+        c1 = n1;
+        n0 = m0;
+        n1 = m1;
     }
-    if constexpr (kIter) {
-        n2 = wave_sum(n2);
-        pr = wave_sum(pr);
-        pi = wave_sum(pi);
-        part4* p = a.wave_part + gw;             // every lane stores the same sums
-        st_agent(&p->a, n2);
-        st_agent(&p->b, pr);
-        st_agent(&p->c, pi);
+}
+
+// Norm and Rayleigh partials of a solved iterate, in a fixed order (grid-stride per thread,
+// block sums, last-arriver sum in block order): sum |y_i|^2 and sum conj(x_i) y_i with
+// x = b / ||y_prev|| as the solve used it.  Skipped once the prologue has stopped the loop.
+template <class S>
+__global__ __launch_bounds__(kThreads) void shift_part_kernel(TriArgs<S> a, int parity) {
+    __shared__ double sm[3 * kWaves];
+    __shared__ int s_last;
+    __shared__ int s_go;
+    __shared__ double s_nrm;
+    if (threadIdx.x == 0) {
+        s_go = __hip_atomic_load(&a.ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 0 : 1;
+        s_nrm = a.ctl->st[parity ^ 1].nrm;
     }
     __syncthreads();
-    // last arriver: wave partials in wave order (deterministic), ticket reset
-    if (tid == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(&a.work[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (tk == gridDim.x - 1) ? 1 : 0;
+    if (!s_go) return;
+    const double nrm = s_nrm;
+    const S* xin = parity ? a.buf0 : a.buf1;
+    const S* y = parity ? a.buf1 : a.buf0;
+    double n2 = 0.0, pr = 0.0, pi = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kThreads) {
+        const S yi = y[i];
+        n2 += sq_abs(yi);
+        acc_dot(pr, pi, scale_in(xin[i], nrm), yi);   // p = sum conj(x_i) y_i
     }
-    __syncthreads();
-    if (!s_last) return;
-    if constexpr (kIter) {
-        double sa = 0.0, sb = 0.0, sc = 0.0;
-        for (int i = tid; i < W; i += kThreads) {
-            sa += ld_agent(&a.wave_part[i].a);
-            sb += ld_agent(&a.wave_part[i].b);
-            sc += ld_agent(&a.wave_part[i].c);
-        }
-        block_sum3(sa, sb, sc, sm);
-        if (tid == 0) {
-            a.my_part->a = sa;
-            a.my_part->b = sb;
-            a.my_part->c = sc;
-            a.my_part->d = 0.0;
-        }
-    }
-    if (tid == 0) __hip_atomic_store(&a.work[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    block_sum3(n2, pr, pi, sm);
+    last_arriver_reduce(n2, pr, pi, a.wave_part, a.work + 2, a.my_part, sm, &s_last);
 }
 
 // ------------------------------------------------------------------ dense LU (factor once)
@@ -791,7 +1082,10 @@ static void shift_free(ShiftFactor* f) {
     if (!f) return;
     hipSetDevice(f->ctx->device);
     hipStreamSynchronize(f->ctx->stream);
-    for (void* p : {(void*)f->order, (void*)f->pptr, (void*)f->pcol, f->pval, f->ppiv, f->z[0], f->z[1],
+    for (void* p : {(void*)f->order, f->z[0], f->z[1],
+                    f->hval, (void*)f->hcol, f->hpiv, (void*)f->passes, (void*)f->smeta, (void*)f->trow,
+                    f->tpiv, (void*)f->tcol, f->tval, (void*)f->porder, (void*)f->pptr, (void*)f->pcol, f->pval,
+                    f->ppiv,
                     (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
                     (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf})
         if (p) hipFree(p);
@@ -928,7 +1222,8 @@ int shift_factor_dense(eigsol_dense* A, const void* sigma, ShiftFactor** out) {
 // Level analysis of a triangular pattern (host, once per matrix): level(i) = 1 + max level of
 // the rows it reads; positions sorted by level, each level padded to a multiple of kWaveRows.
 static void level_order(const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int64_t n,
-                        bool upper, std::vector<int32_t>& order, int32_t& nlevels) {
+                        bool upper, std::vector<int32_t>& order, int32_t& nlevels,
+                        std::vector<int64_t>& lstart, std::vector<int64_t>& lcount) {
     std::vector<int32_t> lev(n, 0);
     int32_t maxl = 0;
     auto visit = [&](int64_t i) {
@@ -948,6 +1243,39 @@ static void level_order(const std::vector<int32_t>& rp, const std::vector<int32_
     order.assign(start[nlevels], -1);
     std::vector<int64_t> fill(start.begin(), start.end() - 1);
     for (int64_t i = 0; i < n; ++i) order[fill[lev[i]]++] = (int32_t)i;
+    lstart = start;
+    lcount.assign(cnt.begin() + 1, cnt.end());
+}
+
+// Head of the level order solved by one workgroup from LDS: the longest prefix of levels whose
+// positions fit the LDS budget and whose levels are narrow (a wide level is cheaper spread over
+// the whole GPU).  EIGSOL_TRSV_HEAD_ROWS / EIGSOL_TRSV_HEAD_WIDTH override (0 rows: no head).
+template <class S>
+static int32_t head_levels(const std::vector<int64_t>& lstart, const std::vector<int64_t>& lcount,
+                           const std::vector<int32_t>& lmaxlen, int32_t nlevels) {
+    int64_t cap = (int64_t)(150 * 1024) / (int64_t)sizeof(S);
+    int64_t width = 256;   // config 5: 256 -> 0.861 ms, 1024 -> 0.872 ms per solve
+    if (const char* e = std::getenv("EIGSOL_TRSV_HEAD_ROWS")) cap = std::min<int64_t>(cap, std::atoll(e));
+    if (const char* e = std::getenv("EIGSOL_TRSV_HEAD_WIDTH")) width = std::atoll(e);
+    int32_t h = 0;
+    int64_t npass = 0;   // the pass table shares the LDS budget (8 bytes a pass)
+    while (h < nlevels && lcount[h] <= width && lmaxlen[h] <= dev::kRowLanes) {
+        const int64_t np = npass + (lcount[h] + dev::kHeadRows - 1) / dev::kHeadRows;
+        if ((lstart[h + 1] + 1) * (int64_t)sizeof(S) + (np + dev::kHeadDepth) * 8 > cap * (int64_t)sizeof(S)) break;
+        npass = np;
+        ++h;
+    }
+    return h;
+}
+
+template <class S>
+static const void* slice_kernel_ptr(int b, bool iter) {
+    if (b == 4) return iter ? reinterpret_cast<const void*>(dev::sptrsv_slice_kernel<S, 4, true>)
+                            : reinterpret_cast<const void*>(dev::sptrsv_slice_kernel<S, 4, false>);
+    if (b == 8) return iter ? reinterpret_cast<const void*>(dev::sptrsv_slice_kernel<S, 8, true>)
+                            : reinterpret_cast<const void*>(dev::sptrsv_slice_kernel<S, 8, false>);
+    return iter ? reinterpret_cast<const void*>(dev::sptrsv_slice_kernel<S, 16, true>)
+                : reinterpret_cast<const void*>(dev::sptrsv_slice_kernel<S, 16, false>);
 }
 
 template <class S>
@@ -1022,27 +1350,140 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
     }
     f->nnz_off = (int64_t)oci.size();
     std::vector<int32_t> order;
-    level_order(orp, oci, n, up, order, f->nlevels);
+    std::vector<int64_t> lstart, lcount;
+    level_order(orp, oci, n, up, order, f->nlevels, lstart, lcount);
     f->npos = (int32_t)order.size();
-    f->nchunks = f->npos / dev::kWaveRows;
-    // position-indexed copies: a row's metadata needs no dependent load, and the off-diagonal
-    // entries of consecutive positions are contiguous
-    std::vector<int32_t> pptr(f->npos + 1, 0), pcol;
-    std::vector<S> pval, ppiv(f->npos);
-    pcol.reserve(oci.size());
-    pval.reserve(oci.size());
-    for (int32_t p = 0; p < f->npos; ++p) {
-        const int32_t i = order[p];
-        if (i >= 0) {
-            for (int32_t e = orp[i]; e < orp[i + 1]; ++e) {
-                pcol.push_back(oci[e]);
-                pval.push_back(ov[e]);
-            }
-            ppiv[p] = pv[i];
-        } else {
-            ppiv[p] = make_sigma<S>(1.0, 0.0);
+    std::vector<int32_t> lmaxlen(f->nlevels, 0);   // longest row (off-diagonal entries) per level
+    for (int32_t l = 0; l < f->nlevels; ++l)
+        for (int64_t p = lstart[l]; p < lstart[l] + lcount[l]; ++p)
+            lmaxlen[l] = std::max(lmaxlen[l], orp[order[p] + 1] - orp[order[p]]);
+    f->hlevels = head_levels<S>(lstart, lcount, lmaxlen, f->nlevels);
+    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_FAST")) f->poll_fast = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_MODE")) f->poll_mode = std::atoi(e);
+    f->hpos = (int32_t)lstart[f->hlevels];
+    std::vector<int2> passes;
+    for (int32_t l = 0; l < f->hlevels; ++l) {
+        const int32_t p0 = (int32_t)lstart[l], p1 = (int32_t)(lstart[l] + lcount[l]);
+        for (int32_t p = p0; p < p1; p += dev::kHeadRows) {
+            const int32_t e = std::min(p1, p + dev::kHeadRows);
+            passes.push_back(make_int2(p, e | (e == p1 ? dev::kPassBarrier : 0)));
         }
-        pptr[p + 1] = (int32_t)pcol.size();
+    }
+    while (!passes.empty() && passes.size() % dev::kHeadDepth) passes.push_back(make_int2(0, 0));   // empty
+    f->npass = (int32_t)passes.size();
+    std::vector<int32_t> rowpos;
+    if (f->hpos > 0) {
+        rowpos.assign(n, -1);
+        for (int32_t p = 0; p < f->hpos; ++p)
+            if (order[p] >= 0) rowpos[order[p]] = p;
+    }
+    // head, pass-major (see sptrsv_head_kernel): columns are LDS positions of earlier head rows
+    const size_t hslots = (size_t)f->npass * dev::kHeadThreads;
+    std::vector<int32_t> hcol(hslots, f->hpos);   // padding: the zero slot
+    std::vector<S> hval(hslots, s_zero<S>()), hpiv((size_t)f->npass * dev::kHeadRows, make_sigma<S>(1.0, 0.0));
+    for (int32_t q = 0; q < f->npass; ++q) {
+        const int32_t p0 = passes[q].x, p1 = passes[q].y & ~dev::kPassBarrier;
+        for (int32_t p = p0; p < p1; ++p) {
+            const size_t g = (size_t)q * dev::kHeadRows + (p - p0);
+            const int32_t i = order[p];
+            hpiv[g] = pv[i];
+            for (int32_t e = orp[i]; e < orp[i + 1]; ++e) {
+                hcol[g * dev::kRowLanes + (e - orp[i])] = rowpos[oci[e]];
+                hval[g * dev::kRowLanes + (e - orp[i])] = ov[e];
+            }
+        }
+    }
+    // tail variant: slices (row per lane) for few, very wide levels; chunks (16 lanes per row)
+    // otherwise.  EIGSOL_TRSV_TAIL=slice|chunk overrides.
+    {
+        // slices when most tail rows sit in levels of >= 64k rows (a wave's 64 rows then rarely
+        // wait); measured: one 1M-row level 74 vs 195 us, config 5 (widest level 21k) 1.3 vs 0.86 ms
+        int64_t trows = 0, wide = 0;
+        for (int32_t l = f->hlevels; l < f->nlevels; ++l) {
+            trows += lcount[l];
+            if (lcount[l] >= 65536) wide += lcount[l];
+        }
+        f->tail_chunks = (trows > 0 && 2 * wide < trows) ? 1 : 0;
+        if (const char* e = std::getenv("EIGSOL_TRSV_TAIL")) f->tail_chunks = std::strcmp(e, "slice") ? 1 : 0;
+    }
+    std::vector<int32_t> porder, pptr, pcol;
+    std::vector<S> pval, ppiv;
+    if (f->tail_chunks) {   // position-indexed copies: no dependent metadata loads in the kernel
+        f->chunk0 = f->hpos / dev::kWaveRows;
+        f->nchunks = f->npos / dev::kWaveRows;
+        porder = order;
+        pptr.assign((size_t)f->npos + 1, 0);
+        ppiv.assign((size_t)f->npos, make_sigma<S>(1.0, 0.0));
+        pcol.reserve(oci.size());
+        pval.reserve(oci.size());
+        for (int32_t p = 0; p < f->npos; ++p) {
+            const int32_t i = order[p];
+            if (i >= 0) {
+                for (int32_t e = orp[i]; e < orp[i + 1]; ++e) {
+                    pcol.push_back(oci[e]);
+                    pval.push_back(ov[e]);
+                }
+                ppiv[p] = pv[i];
+            }
+            pptr[p + 1] = (int32_t)pcol.size();
+        }
+    }
+    // tail slices (see sptrsv_slice_kernel): 64 rows of one level each; B = the smallest of
+    // 4 / 8 / 16 that holds the entries of at least 95 % of the slices (longer slices loop)
+    std::vector<int32_t> slen;   // longest row per slice
+    std::vector<int64_t> sfirst;
+    std::vector<int32_t> scount;
+    for (int32_t l = f->tail_chunks ? f->nlevels : f->hlevels; l < f->nlevels; ++l)
+        for (int64_t p = lstart[l]; p < lstart[l] + lcount[l]; p += 64) {
+            const int32_t c = (int32_t)std::min<int64_t>(64, lstart[l] + lcount[l] - p);
+            int32_t K = 0;
+            for (int32_t u = 0; u < c; ++u) K = std::max(K, orp[order[p + u] + 1] - orp[order[p + u]]);
+            sfirst.push_back(p);
+            scount.push_back(c);
+            slen.push_back(K);
+        }
+    f->nslices = (int32_t)slen.size();
+    {
+        std::vector<int32_t> sorted(slen);
+        std::sort(sorted.begin(), sorted.end());
+        const int32_t q95 = sorted.empty() ? 0 : sorted[(size_t)(0.95 * (double)(sorted.size() - 1))];
+        f->slice_b = q95 <= 4 ? 4 : (q95 <= 8 ? 8 : 16);
+        if (const char* e = std::getenv("EIGSOL_TRSV_SLICE_B")) {
+            const int b = std::atoi(e);
+            if (b == 4 || b == 8 || b == 16) f->slice_b = b;
+        }
+    }
+    const int32_t Bs = f->slice_b;
+    // the kernel prefetches "slice 0" for a wave past the last slice: slice 0 always exists (an
+    // empty one when the head holds every level)
+    std::vector<int2> smeta(std::max(1, f->nslices), make_int2(0, Bs));
+    std::vector<int32_t> trow((size_t)std::max(1, f->nslices) * 64, -1);
+    std::vector<S> tpiv((size_t)std::max(1, f->nslices) * 64, make_sigma<S>(1.0, 0.0));
+    int64_t tent = 0;
+    for (int32_t sl = 0; sl < f->nslices; ++sl) tent += 64 * (int64_t)std::max(slen[sl], Bs);
+    tent += 64 * (int64_t)Bs;   // the prefetch of "slice ns" reads slice 0's range: keep it in bounds
+    if (tent * (int64_t)sizeof(S) >= (int64_t)1 << 32) {
+        shift_free(f);
+        return fail(EIGSOL_E_UNSUPPORTED, "triangular solve: factor streams exceed 4 GiB");
+    }
+    std::vector<int32_t> tcol((size_t)tent, (int32_t)n);   // padding: the zero slot z[n]
+    std::vector<S> tval((size_t)tent, s_zero<S>());
+    {
+        int64_t off = 0;
+        for (int32_t sl = 0; sl < f->nslices; ++sl) {
+            const int32_t Kp = std::max(slen[sl], Bs);
+            smeta[sl] = make_int2((int32_t)off, Kp);
+            for (int32_t u = 0; u < scount[sl]; ++u) {
+                const int32_t i = order[sfirst[sl] + u];
+                trow[(size_t)sl * 64 + u] = i;
+                tpiv[(size_t)sl * 64 + u] = pv[i];
+                for (int32_t e = orp[i]; e < orp[i + 1]; ++e) {
+                    tcol[(size_t)(off + 64 * (e - orp[i]) + u)] = oci[e];
+                    tval[(size_t)(off + 64 * (e - orp[i]) + u)] = ov[e];
+                }
+            }
+            off += 64 * (int64_t)Kp;
+        }
     }
     std::vector<int32_t>().swap(oci);
     std::vector<S>().swap(ov);
@@ -1051,28 +1492,51 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         if (bytes && src) EIGSOL_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, st));
         return EIGSOL_OK;
     };
-    // one residency round of waves (the static schedule needs every wave resident), capped by
-    // the work: two blocks per CU by default
-    if (rc == EIGSOL_OK)
-        rc = resident_blocks(f->ctx, reinterpret_cast<const void*>(dev::sptrsv_kernel<S, true>),
-                             dev::kThreads, 0, &f->grid);
+    // tail grid: one residency round (cooperative launch), capped at EIGSOL_TRSV_BLOCKS_PER_CU
+    // blocks per CU and by the work
+    if (rc == EIGSOL_OK) {
+        int per_cu_max = 0;
+        const void* tk = f->tail_chunks ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>)
+                                        : slice_kernel_ptr<S>(Bs, true);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_max, tk, dev::kThreads, 0) != hipSuccess ||
+            per_cu_max < 1)
+            rc = fail(EIGSOL_E_HIP, "triangular solve: occupancy query");
+        f->grid = per_cu_max * f->ctx->num_cus;
+    }
     int per_cu = 2;
     if (const char* env = std::getenv("EIGSOL_TRSV_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(env));
     f->grid = std::min(f->grid, per_cu * f->ctx->num_cus);
-    f->grid = std::max(1, std::min(f->grid, (f->nchunks + dev::kWaves - 1) / dev::kWaves));
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), order.size() * 4);
+    const int64_t units = f->tail_chunks ? (int64_t)f->nchunks - f->chunk0 : f->nslices;
+    f->grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid, (units + dev::kWaves - 1) / dev::kWaves));
+    f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
+                                                                  std::min<int64_t>(1024, (n + 1023) / 1024)));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), (size_t)f->hpos * 4);
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->hcol, hcol.data(), hcol.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_(&f->hval, hval.data(), hval.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_(&f->hpiv, hpiv.data(), hpiv.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->passes, passes.data(), passes.size() * sizeof(int2));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->smeta, smeta.data(), smeta.size() * sizeof(int2));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->trow, trow.data(), trow.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_(&f->tpiv, tpiv.data(), tpiv.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->tcol, tcol.data(), tcol.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_(&f->tval, tval.data(), tval.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->porder, porder.data(), porder.size() * 4);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->pptr, pptr.data(), pptr.size() * 4);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->pcol, pcol.data(), pcol.size() * 4);
     if (rc == EIGSOL_OK) rc = up_(&f->pval, pval.data(), pval.size() * sizeof(S));
     if (rc == EIGSOL_OK) rc = up_(&f->ppiv, ppiv.data(), ppiv.size() * sizeof(S));
-    if (rc == EIGSOL_OK) rc = up_(&f->z[0], nullptr, n * sizeof(S));
-    if (rc == EIGSOL_OK) rc = up_(&f->z[1], nullptr, n * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_(&f->z[0], nullptr, (n + 1) * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_(&f->z[1], nullptr, (n + 1) * sizeof(S));
     if (rc == EIGSOL_OK) rc = up_((void**)&f->work, nullptr, 64);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->err, nullptr, 64);
     if (rc == EIGSOL_OK) rc = up_(&f->wave_part, nullptr, (size_t)f->grid * dev::kWaves * sizeof(dev::part4));
     if (rc == EIGSOL_OK) {
+        // every row starts unsolved (sentinel); the zero slot z[n] stays 0 for good
         const uint32_t sent = (uint32_t)(dev::kSent & 0xffffffffu);
-        for (void* zb : f->z) hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st);
+        for (void* zb : f->z) {
+            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st);
+            hipMemsetAsync(static_cast<char*>(zb) + n * sizeof(S), 0, sizeof(S), st);
+        }
         hipMemsetAsync(f->work, 0, 64, st);
         hipMemsetAsync(f->err, 0, 64, st);
         if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "factor upload");
@@ -1114,11 +1578,6 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
     if (f->kind == 0) {
         dev::TriArgs<S> a{};
         a.order = f->order;
-        a.pptr = f->pptr;
-        a.pcol = f->pcol;
-        a.pval = static_cast<const S*>(f->pval);
-        a.ppiv = static_cast<const S*>(f->ppiv);
-        a.nchunks = f->nchunks;
         a.n = f->n;
         const int e = ++f->epoch;
         a.zcur = static_cast<S*>(f->z[e & 1]);
@@ -1136,8 +1595,43 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.trace = static_cast<S*>(trace);
         a.sig_re = f->sig_re;
         a.sig_im = f->sig_im;
-        if (iter) hipLaunchKernelGGL((dev::sptrsv_kernel<S, true>), dim3(f->grid), dim3(dev::kThreads), 0, st, a, parity);
-        else hipLaunchKernelGGL((dev::sptrsv_kernel<S, false>), dim3(f->grid), dim3(dev::kThreads), 0, st, a, parity);
+        a.hcol = f->hcol;
+        a.hval = static_cast<const S*>(f->hval);
+        a.hpiv = static_cast<const S*>(f->hpiv);
+        a.passes = f->passes;
+        a.npass = f->npass;
+        a.hpos = f->hpos;
+        a.poll_fast = f->poll_fast;
+        a.poll_mode = f->poll_mode;
+        const size_t hl = (size_t)(f->hpos + 1) * sizeof(S) + (size_t)f->npass * sizeof(int2);
+        if (f->hpos > 0) {
+            const void* hk = iter ? reinterpret_cast<const void*>(dev::sptrsv_head_kernel<S, true>)
+                                  : reinterpret_cast<const void*>(dev::sptrsv_head_kernel<S, false>);
+            EIGSOL_HIP(hipFuncSetAttribute(hk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl));
+            if (iter) hipLaunchKernelGGL((dev::sptrsv_head_kernel<S, true>), dim3(1), dim3(dev::kHeadThreads), hl, st, a, parity);
+            else hipLaunchKernelGGL((dev::sptrsv_head_kernel<S, false>), dim3(1), dim3(dev::kHeadThreads), hl, st, a, parity);
+        }
+        // cooperative: the static chunk schedule needs every wave of the grid resident
+        void* kargs[] = {&a, &parity};
+        a.smeta = f->smeta;
+        a.trow = f->trow;
+        a.tpiv = static_cast<const S*>(f->tpiv);
+        a.tcol = f->tcol;
+        a.tval = static_cast<const S*>(f->tval);
+        a.nslices = f->nslices;
+        a.porder = f->porder;
+        a.pptr = f->pptr;
+        a.pcol = f->pcol;
+        a.pval = static_cast<const S*>(f->pval);
+        a.ppiv = static_cast<const S*>(f->ppiv);
+        a.chunk0 = f->chunk0;
+        a.nchunks = f->nchunks;
+        const void* tk = !f->tail_chunks ? slice_kernel_ptr<S>(f->slice_b, iter)
+                         : iter ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>)
+                                : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, false>);
+        EIGSOL_HIP(hipLaunchCooperativeKernel(tk, dim3(f->grid), dim3(dev::kThreads), kargs, 0, st));
+        if (iter)
+            hipLaunchKernelGGL((dev::shift_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a, parity);
     } else if constexpr (!kDenseLU<S>) {
         return fail(EIGSOL_E_UNSUPPORTED, "single-precision dense factor");
     } else if (f->dense_multi) {
@@ -1163,8 +1657,11 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.trace = static_cast<S*>(trace);
         a.sig_re = f->sig_re;
         a.sig_im = f->sig_im;
-        if (iter) hipLaunchKernelGGL((dev::dense_trsv_kernel<S, true>), dim3(f->grid), dim3(256), 0, st, a, parity);
-        else hipLaunchKernelGGL((dev::dense_trsv_kernel<S, false>), dim3(f->grid), dim3(256), 0, st, a, parity);
+        // cooperative: the persistent block-row workgroups wait on each other's epoch flags
+        void* kargs[] = {&a, &parity};
+        const void* dk = iter ? reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, true>)
+                              : reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, false>);
+        EIGSOL_HIP(hipLaunchCooperativeKernel(dk, dim3(f->grid), dim3(256), kargs, 0, st));
     } else {
         dev::DenseSolveArgs<S> a{};
         a.lu = static_cast<const S*>(f->lu);
