@@ -79,6 +79,12 @@ public:
         check(eigsol_csr_create_from_csc(ctx(), dt, r, c, nnz, colptr, rowidx, v, &m->csr_), "eigsol_csr_create_from_csc");
         return m;
     }
+    static std::shared_ptr<DeviceMatrix> coo(eigsol_dtype dt, std::int64_t r, std::int64_t c, std::int64_t nnz,
+                                             const std::int32_t* row, const std::int32_t* col, const void* v) {
+        auto m = std::shared_ptr<DeviceMatrix>(new DeviceMatrix());
+        check(eigsol_csr_create_from_coo(ctx(), dt, r, c, nnz, row, col, v, &m->csr_), "eigsol_csr_create_from_coo");
+        return m;
+    }
     ~DeviceMatrix() {
         if (csr_) eigsol_csr_destroy(csr_);
         if (dense_) eigsol_dense_destroy(dense_);

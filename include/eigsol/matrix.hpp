@@ -7,10 +7,14 @@
 // matrix to the device (eigsol_dense_create / eigsol_csr_create_from_csc) and the handle is
 // cached for the Matrix's lifetime, so repeated solves do not re-upload.  Mutating the storage
 // obtained through the non-const cast<T>() drops the cached device copy.
+// Device-resident construction (the text reader's sparse path): a Matrix built from triplets owns
+// a device CSR from the start (eigsol_csr_create_from_coo, no host CSC); the host Sparse<S> that
+// cast<>() returns is materialised from the device copy the first time a caller asks for it.
 #pragma once
 
 #include <memory>
 #include <typeinfo>
+#include <vector>
 
 #include "core.hpp"
 #include "device.hpp"
@@ -38,6 +42,20 @@ private:
     T v_;
 };
 
+// Entries of a sparse matrix as a reader collects them: position and value per entry, any order,
+// repeated positions summed (in input order) like repeated Sparse<S>::insert()s.
+template <typename S>
+struct SparseTriplets {
+    std::int64_t rows = 0, cols = 0;
+    std::vector<std::int32_t> row, col;
+    std::vector<S> val;
+};
+
+template <typename S>
+inline constexpr bool has_device_storage_v =
+    std::is_same_v<S, double> || std::is_same_v<S, float> || std::is_same_v<S, std::complex<double>> ||
+    std::is_same_v<S, std::complex<float>>;
+
 class Matrix {
 public:
     template <typename S>
@@ -59,6 +77,29 @@ public:
     explicit Matrix(const SparseMatrix<S>& m)
         : dense_(false), scalar_(&typeid(S)), box_(std::make_unique<BoxTyped<SparseMatrix<S>>>(m)) {
         box_cast<SparseMatrix<S>>().makeCompressed();
+    }
+
+    // Triplets straight to the device.  Scalars without device storage (long
+    // double), or a process without a usable device, take the host route (insert + compress);
+    // the solvers then report the missing device on first use, as for any other Matrix.
+    template <ScalarConcept S>
+    explicit Matrix(SparseTriplets<S>&& t) : dense_(false), scalar_(&typeid(S)), rows_(t.rows), cols_(t.cols) {
+        if constexpr (has_device_storage_v<S>) {
+            try {
+                dev_ = detail::DeviceMatrix::coo(detail::dtype_of<S>(), t.rows, t.cols,
+                                                 static_cast<std::int64_t>(t.val.size()), t.row.data(),
+                                                 t.col.data(), t.val.data());
+                type_ = &typeid(SparseMatrix<S>);
+                materialise_ = &Matrix::host_from_device<S>;
+                return;
+            } catch (const std::runtime_error&) {
+                dev_.reset();
+            }
+        }
+        SparseMatrix<S> s(t.rows, t.cols);
+        for (std::size_t k = 0; k < t.val.size(); ++k) s.insert(t.row[k], t.col[k]) = t.val[k];
+        s.makeCompressed();
+        box_ = std::make_unique<BoxTyped<SparseMatrix<S>>>(std::move(s));
     }
 
 #if EIGSOL_HAVE_EIGEN
@@ -84,22 +125,28 @@ public:
 
     bool isDense() const { return dense_; }
     const std::type_info& scalar_type() const { return *scalar_; }
-    const std::type_info& type() const { return box_->type(); }
+    const std::type_info& type() const { return box_ ? box_->type() : *type_; }
+    // true while the only copy of the entries is the device one (the host storage has not been
+    // asked for yet)
+    bool deviceResident() const { return !box_; }
 
     template <typename T>
     T& cast() {
         check<T>();
+        materialise();
         dev_.reset();   // the caller may modify the storage
+        dev64_.reset();
         return box_cast<T>();
     }
     template <typename T>
     const T& cast() const {
         check<T>();
+        materialise();
         return static_cast<const BoxTyped<T>*>(box_.get())->get();
     }
 
-    std::int64_t rows() const { return visit([](const auto& m) { return m.rows(); }); }
-    std::int64_t cols() const { return visit([](const auto& m) { return m.cols(); }); }
+    std::int64_t rows() const { return box_ ? visit([](const auto& m) { return m.rows(); }) : rows_; }
+    std::int64_t cols() const { return box_ ? visit([](const auto& m) { return m.cols(); }) : cols_; }
 
     // Device mirror (created on first use by the solvers) in the storage's own precision
     // (double, float and their complex types all have device storage).
@@ -124,7 +171,24 @@ public:
 private:
     template <typename T>
     void check() const {
-        if (box_->type() != typeid(T)) throw std::bad_cast{};
+        if (type() != typeid(T)) throw std::bad_cast{};
+    }
+    void materialise() const {
+        if (!box_) box_ = materialise_(*dev_);
+    }
+    // host Sparse<S> (CSC) from the device CSR: download, then a counting-sort transpose
+    template <typename S>
+    static std::unique_ptr<Box> host_from_device(const detail::DeviceMatrix& d) {
+        std::int64_t r = 0, c = 0, nnz = 0;
+        detail::check(eigsol_csr_info(d.csr(), &r, &c, &nnz, nullptr), "eigsol_csr_info");
+        std::vector<std::int32_t> rp(r + 1), ci(nnz);
+        std::vector<S> v(nnz);
+        detail::check(eigsol_csr_download(d.csr(), rp.data(), ci.data(), v.data()), "eigsol_csr_download");
+        SparseMatrix<S> s(r, c);
+        for (std::int64_t i = 0; i < r; ++i)
+            for (std::int32_t e = rp[i]; e < rp[i + 1]; ++e) s.insert(i, ci[e]) = v[e];
+        s.makeCompressed();
+        return std::make_unique<BoxTyped<SparseMatrix<S>>>(std::move(s));
     }
     template <typename T>
     T& box_cast() {
@@ -151,6 +215,7 @@ private:
 
     template <typename S, typename D>
     std::shared_ptr<detail::DeviceMatrix> upload() const {
+        materialise();
         if (dense_) {
             const auto& d = cast<DenseMatrix<S>>();
             if constexpr (std::is_same_v<D, S>) {
@@ -173,7 +238,10 @@ private:
 
     bool dense_;
     const std::type_info* scalar_;
-    std::unique_ptr<Box> box_;
+    const std::type_info* type_ = nullptr;   // storage type while box_ is empty
+    std::int64_t rows_ = 0, cols_ = 0;
+    mutable std::unique_ptr<Box> box_;        // empty until a device-resident matrix is cast
+    std::unique_ptr<Box> (*materialise_)(const detail::DeviceMatrix&) = nullptr;
     mutable std::shared_ptr<detail::DeviceMatrix> dev_;
     mutable std::shared_ptr<detail::DeviceMatrix> dev64_;
 };

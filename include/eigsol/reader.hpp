@@ -32,13 +32,20 @@ Matrix readInsideDenseMatrix(std::ifstream& in, int rows, int cols) {
     return Matrix(d);
 }
 
+// Sparse entries go straight to the device: the triplets become a device CSR (no host CSC, SURVEY
+// §8f rank 2) and the Matrix materialises its host Sparse<S> only if a caller casts to it.
 template <typename S>
 Matrix readInsideSparseMatrix(std::ifstream& in, int rows, int cols) {
     if (rows < 0 || cols < 0) throw std::runtime_error("Negative matrix dimensions");
     int nnz = 0;
     if (!(in >> nnz)) throw std::runtime_error("Cannot read number of non-zero entries in the sparse matrix");
     if (nnz <= 0) throw std::runtime_error("number of non-zero entries must be positive in a sparse matrix");
-    SparseMatrix<S> s(rows, cols);
+    SparseTriplets<S> t;
+    t.rows = rows;
+    t.cols = cols;
+    t.row.reserve(nnz);
+    t.col.reserve(nnz);
+    t.val.reserve(nnz);
     for (int k = 0; k < nnz; ++k) {
         int r{}, c{};
         if (!(in >> r >> c)) throw std::runtime_error("Error when trying to read indices in sparse matrix");
@@ -46,15 +53,16 @@ Matrix readInsideSparseMatrix(std::ifstream& in, int rows, int cols) {
         if constexpr (is_complex_of_floating<S>::value) {
             typename S::value_type re{}, im{};
             if (!(in >> re >> im)) throw std::runtime_error("Failed to read scalar entry in sparse matrix");
-            s.insert(r, c) = S(re, im);
+            t.val.push_back(S(re, im));
         } else {
             S v{};
             if (!(in >> v)) throw std::runtime_error("Failed to read scalar entry in sparse matrix");
-            s.insert(r, c) = v;
+            t.val.push_back(v);
         }
+        t.row.push_back(r);
+        t.col.push_back(c);
     }
-    s.makeCompressed();
-    return Matrix(s);
+    return Matrix(std::move(t));
 }
 
 enum class StorageType { Dense, Sparse };

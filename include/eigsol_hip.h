@@ -99,6 +99,16 @@ int eigsol_csr_create(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_
 int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
                                int64_t nnz, const int32_t* colptr, const int32_t* rowidx,
                                const void* values, eigsol_csr** out);
+/* COO triplets (row[k], col[k], values[k]) in any order, the text reader's sparse entries
+ * (file_matrix_reader.hpp:84-132, "row col value" lines): ordered by (row, column) into CSR
+ * directly, with no CSC step; repeated positions are summed in input order (what Matrix::Sparse's
+ * compression does with repeated insert()s). */
+int eigsol_csr_create_from_coo(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
+                               int64_t nnz, const int32_t* rowidx, const int32_t* colidx,
+                               const void* values, eigsol_csr** out);
+/* Copy the device CSR back (rowptr[nrows+1], colidx[nnz], values[nnz]; columns ascending within
+ * each row, duplicates already summed).  Single-device matrices only. */
+int eigsol_csr_download(eigsol_csr* A, int32_t* rowptr, int32_t* colidx, void* values);
 int eigsol_csr_destroy(eigsol_csr* A);
 int eigsol_csr_info(eigsol_csr* A, int64_t* nrows, int64_t* ncols, int64_t* nnz, int* dtype);
 /* y = A*x on device buffers (x: ncols scalars, y: nrows scalars), stream-ordered.  Each row is an

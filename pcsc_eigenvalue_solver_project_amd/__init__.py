@@ -159,6 +159,37 @@ class CsrMatrix:
         M.sort_indices()
         return cls(ctx, M.indptr, M.indices, M.data, M.shape)
 
+    @classmethod
+    def from_coo(cls, ctx: Context, rows, cols, values, shape):
+        """Triplets in any order straight to the device CSR (``eigsol_csr_create_from_coo``):
+        repeated positions are summed in input order, as the reader's Matrix::Sparse does."""
+        values = np.ascontiguousarray(values)
+        code = _dtype_code(values.dtype)
+        r = np.ascontiguousarray(rows, dtype=np.int32)
+        c = np.ascontiguousarray(cols, dtype=np.int32)
+        if not (len(r) == len(c) == len(values)):
+            raise EigSolError(EIGSOL_E_SIZE_MISMATCH,
+                              f"triplet arrays differ in length ({len(r)}, {len(c)}, {len(values)})")
+        h = C.c_void_p()
+        call("eigsol_csr_create_from_coo", ctx.handle, code, int(shape[0]), int(shape[1]), len(r), _ptr(r),
+             _ptr(c), _ptr(values), C.byref(h))
+        self = cls.__new__(cls)
+        self.ctx, self.handle = ctx, h
+        self.shape = (int(shape[0]), int(shape[1]))
+        nnz = C.c_int64()
+        call("eigsol_csr_info", h, None, None, C.byref(nnz), None)
+        self.nnz = nnz.value
+        self.dtype = _np_dtype(code)
+        return self
+
+    def download(self):
+        """(rowptr, colidx, values) of the device CSR (``eigsol_csr_download``)."""
+        rp = np.empty(self.shape[0] + 1, np.int32)
+        ci = np.empty(self.nnz, np.int32)
+        v = np.empty(self.nnz, self.dtype)
+        call("eigsol_csr_download", self.handle, _ptr(rp), _ptr(ci), _ptr(v))
+        return rp, ci, v
+
     def spmv(self, x_dev: int, y_dev: int) -> None:
         call("eigsol_csr_spmv", self.handle, C.c_void_p(x_dev), C.c_void_p(y_dev))
 

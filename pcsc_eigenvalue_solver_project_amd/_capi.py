@@ -80,6 +80,8 @@ SIGNATURES = {
     "eigsol_memcpy_d2h": [_vp, _vp, _vp, C.c_size_t],
     "eigsol_csr_create": [_vp, C.c_int, _i64, _i64, _i64, _vp, _vp, _vp, _ppv],
     "eigsol_csr_create_from_csc": [_vp, C.c_int, _i64, _i64, _i64, _vp, _vp, _vp, _ppv],
+    "eigsol_csr_create_from_coo": [_vp, C.c_int, _i64, _i64, _i64, _vp, _vp, _vp, _ppv],
+    "eigsol_csr_download": [_vp, _vp, _vp, _vp],
     "eigsol_csr_destroy": [_vp],
     "eigsol_csr_info": [_vp, _pi64, _pi64, _pi64, _pint],
     "eigsol_csr_spmv": [_vp, _vp, _vp],

@@ -1656,6 +1656,92 @@ int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrow
     return csr_upload(ctx, dtype, nrows, ncols, nnz, rp.data(), ci.data(), v.data(), out, 0);
 }
 
+int eigsol_csr_create_from_coo(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
+                               int64_t nnz, const int32_t* rowidx, const int32_t* colidx,
+                               const void* values, eigsol_csr** out) {
+    if (!ctx || !out) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: null ctx/out");
+    *out = nullptr;
+    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: unknown dtype");
+    if (nrows < 0 || ncols < 0 || nnz < 0) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: negative dimension");
+    if (nrows > INT32_MAX - 1 || ncols > INT32_MAX - 1 || nnz > INT32_MAX - 16)
+        return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: dimension exceeds int32 storage index");
+    if (nnz && (!rowidx || !colidx || !values)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: null array");
+    for (int64_t k = 0; k < nnz; ++k)
+        if (rowidx[k] < 0 || rowidx[k] >= nrows || colidx[k] < 0 || colidx[k] >= ncols)
+            return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: index out of range");
+    // Two stable counting sorts (by column, then by row) order the triplets by (row, column) and
+    // keep equal positions in input order; duplicates are then summed in input order, which is
+    // what Matrix::Sparse's compression does with repeated insert()s (SparseMatrix::compress).
+    const size_t sb = scalar_bytes(dtype);
+    const auto* vin = static_cast<const unsigned char*>(values);
+    std::vector<int32_t> by_col(nnz), cptr(ncols + 1, 0), rp(nrows + 1, 0);
+    for (int64_t k = 0; k < nnz; ++k) cptr[colidx[k] + 1]++;
+    for (int64_t j = 0; j < ncols; ++j) cptr[j + 1] += cptr[j];
+    for (int64_t k = 0; k < nnz; ++k) by_col[cptr[colidx[k]]++] = (int32_t)k;
+    for (int64_t k = 0; k < nnz; ++k) rp[rowidx[k] + 1]++;
+    for (int64_t i = 0; i < nrows; ++i) rp[i + 1] += rp[i];
+    std::vector<int32_t> perm(nnz), fill(rp.begin(), rp.end() - 1);
+    for (int64_t t = 0; t < nnz; ++t) {
+        const int32_t k = by_col[t];
+        perm[fill[rowidx[k]]++] = k;
+    }
+    std::vector<int32_t>().swap(by_col);
+    std::vector<int32_t> ci;
+    std::vector<unsigned char> v;
+    ci.reserve(nnz);
+    v.reserve((size_t)nnz * sb);
+    std::vector<int32_t> crp(nrows + 1, 0);
+    auto accumulate = [&](unsigned char* dst, const unsigned char* src) {
+        if (dtype == EIGSOL_F64 || dtype == EIGSOL_C128) {
+            for (size_t w = 0; w < sb / 8; ++w) {
+                double a, b;
+                std::memcpy(&a, dst + 8 * w, 8);
+                std::memcpy(&b, src + 8 * w, 8);
+                a += b;
+                std::memcpy(dst + 8 * w, &a, 8);
+            }
+        } else {
+            for (size_t w = 0; w < sb / 4; ++w) {
+                float a, b;
+                std::memcpy(&a, dst + 4 * w, 4);
+                std::memcpy(&b, src + 4 * w, 4);
+                a += b;
+                std::memcpy(dst + 4 * w, &a, 4);
+            }
+        }
+    };
+    for (int64_t i = 0; i < nrows; ++i) {
+        for (int32_t t = rp[i]; t < rp[i + 1]; ++t) {
+            const int32_t k = perm[t];
+            const unsigned char* src = vin + (size_t)k * sb;
+            if ((int64_t)ci.size() > crp[i] && ci.back() == colidx[k]) {
+                accumulate(v.data() + v.size() - sb, src);
+                continue;
+            }
+            ci.push_back(colidx[k]);
+            v.insert(v.end(), src, src + sb);
+        }
+        crp[i + 1] = (int32_t)ci.size();
+    }
+    EIGSOL_HIP(hipSetDevice(ctx->device));
+    return csr_upload(ctx, dtype, nrows, ncols, (int64_t)ci.size(), crp.data(), ci.data(), v.data(), out, 0);
+}
+
+int eigsol_csr_download(eigsol_csr* A, int32_t* rowptr, int32_t* colidx, void* values) {
+    if (!A) return fail(EIGSOL_E_INVALID, "eigsol_csr_download: null matrix");
+    if (A->dist) return fail(EIGSOL_E_UNSUPPORTED, "eigsol_csr_download: row-sharded matrix");
+    if (!rowptr || (A->nnz && (!colidx || !values))) return fail(EIGSOL_E_INVALID, "eigsol_csr_download: null array");
+    EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    hipStream_t s = A->ctx->stream;
+    EIGSOL_HIP(hipMemcpyAsync(rowptr, A->rowptr, (A->nrows + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (A->nnz) {
+        EIGSOL_HIP(hipMemcpyAsync(colidx, A->col, A->nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        EIGSOL_HIP(hipMemcpyAsync(values, A->val, A->nnz * scalar_bytes(A->dtype), hipMemcpyDeviceToHost, s));
+    }
+    EIGSOL_HIP(hipStreamSynchronize(s));
+    return EIGSOL_OK;
+}
+
 int eigsol_csr_destroy(eigsol_csr* A) {
     csr_release(A);
     return EIGSOL_OK;

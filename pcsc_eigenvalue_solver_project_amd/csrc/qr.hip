@@ -531,12 +531,12 @@ static int qr_unshifted_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_
                              void* eig, int32_t* iters, int32_t* conv) {
     hipStream_t st = ctx->stream;
     S *H = nullptr, *Q = nullptr, *R = nullptr, *d = nullptr;
-    EIGSOL_HIP(hipMalloc(&H, n * n * sizeof(S)));
-    EIGSOL_HIP(hipMalloc(&Q, n * n * sizeof(S)));
-    EIGSOL_HIP(hipMalloc(&R, n * n * sizeof(S)));
-    EIGSOL_HIP(hipMalloc(&d, n * sizeof(S)));
+    int rc = EIGSOL_OK;
+    if (hipMalloc(&H, n * n * sizeof(S)) != hipSuccess || hipMalloc(&Q, n * n * sizeof(S)) != hipSuccess ||
+        hipMalloc(&R, n * n * sizeof(S)) != hipSuccess || hipMalloc(&d, n * sizeof(S)) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: hipMalloc");
     QrWork<S> w;
-    int rc = work_alloc(w, n);
+    if (rc == EIGSOL_OK) rc = work_alloc(w, n);
     if (rc == EIGSOL_OK && hipMemcpyAsync(H, A, n * n * sizeof(S), hipMemcpyHostToDevice, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: upload");
     if (rc == EIGSOL_OK) rc = hessenberg_dev<S>(st, H, n, w);
@@ -584,9 +584,10 @@ static int qr_francis_host(eigsol_ctx* ctx, int64_t n, const double* A, int max_
                            double* wi, int32_t* iters, int32_t* conv) {
     hipStream_t st = ctx->stream;
     double* H = nullptr;
-    EIGSOL_HIP(hipMalloc(&H, n * n * sizeof(double)));
+    int rc = EIGSOL_OK;
+    if (hipMalloc(&H, n * n * sizeof(double)) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: hipMalloc");
     QrWork<double> w;
-    int rc = work_alloc(w, n);
+    if (rc == EIGSOL_OK) rc = work_alloc(w, n);
     if (rc == EIGSOL_OK && hipMemcpyAsync(H, A, n * n * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: upload");
     // LAPACK xGEEV's range guard: a matrix whose largest entry lies outside [smlnum, bignum]
@@ -594,15 +595,20 @@ static int qr_francis_host(eigsol_ctx* ctx, int64_t n, const double* A, int max_
     // the eigenvalues are scaled back; squared norms in the reflectors would under- or overflow
     // otherwise.  Matrices inside the range are untouched (bit-identical path).
     int escale = 0;
+    unsigned long long bits = 0;   // max |a_ij| as its bit pattern (nonnegative doubles order as integers)
     if (rc == EIGSOL_OK) {
         unsigned long long* dmax = nullptr;
-        unsigned long long bits = 0;
-        EIGSOL_HIP(hipMallocAsync(reinterpret_cast<void**>(&dmax), sizeof(bits), st));
-        EIGSOL_HIP(hipMemsetAsync(dmax, 0, sizeof(bits), st));
-        hipLaunchKernelGGL(dev::absmax_kernel, dim3(1024), dim3(256), 0, st, H, n * n, dmax);
-        EIGSOL_HIP(hipMemcpyAsync(&bits, dmax, sizeof(bits), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipFreeAsync(dmax, st));
-        EIGSOL_HIP(hipStreamSynchronize(st));
+        if (hipMallocAsync(reinterpret_cast<void**>(&dmax), sizeof(bits), st) != hipSuccess) {
+            rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: hipMallocAsync");
+        } else {
+            hipMemsetAsync(dmax, 0, sizeof(bits), st);
+            hipLaunchKernelGGL(dev::absmax_kernel, dim3(1024), dim3(256), 0, st, H, n * n, dmax);
+            hipMemcpyAsync(&bits, dmax, sizeof(bits), hipMemcpyDeviceToHost, st);
+            (void)hipFreeAsync(dmax, st);
+            if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: norm-range check");
+        }
+    }
+    if (rc == EIGSOL_OK) {
         double amax;
         std::memcpy(&amax, &bits, sizeof(amax));
         const double smlnum = std::sqrt(std::numeric_limits<double>::min()) / std::numeric_limits<double>::epsilon();

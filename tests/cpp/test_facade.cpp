@@ -155,6 +155,43 @@ TEST(PowerMethodTest, DataFileAsDouble) {
     EXPECT_NEAR(std::abs(rs.eigenvalue - C(3, 2)), 0.0, 1e-6);
 }
 
+TEST(ReaderTest, SparseFileStraightToDevice) {
+    // triplets in file order, unsorted, with a repeated position: the device CSR is built from
+    // them directly; the host Sparse<S> appears only when cast<>() asks for it
+    const char* path = "/tmp/eigsol_reader_coo.txt";
+    {
+        std::FILE* f = std::fopen(path, "w");
+        std::fputs("sparse\n4 4\n7\n3 3 1.0\n0 1 2.0\n0 0 4.0\n2 2 0.5\n0 1 0.25\n1 0 1.0\n1 1 3.0\n", f);
+        std::fclose(f);
+    }
+    EigSol::Matrix M = EigSol::readMatrixFromFile<double>(path);
+    EXPECT_FALSE(M.isDense());
+    EXPECT_TRUE(M.deviceResident());
+    EXPECT_TRUE(M.type() == typeid(SparseMat));
+    EXPECT_EQ(M.rows(), 4);
+    EXPECT_EQ(M.cols(), 4);
+    EigSol::SolverOptions opts;
+    opts.tolerance = 1e-12;
+    EigSol::set_random_seed(11);
+    auto r = EigSol::powerMethod<double>(M, opts);
+    EXPECT_TRUE(M.deviceResident());
+    EXPECT_TRUE(r.converged);
+    const SparseMat& S = M.cast<SparseMat>();
+    EXPECT_FALSE(M.deviceResident());
+    EXPECT_EQ(S.nonZeros(), 6);
+    EXPECT_EQ(S.coeff(0, 1), 2.25);
+    EXPECT_EQ(S.coeff(1, 0), 1.0);
+    EXPECT_NEAR(r.eigenvalue, (7.0 + std::sqrt(10.0)) / 2, 1e-9);
+    EXPECT_EQ(S.coeff(3, 3), 1.0);
+    EXPECT_EQ(S.coeff(2, 3), 0.0);
+    EigSol::set_random_seed(11);
+    auto r2 = EigSol::powerMethod<double>(M, opts);   // re-uploaded from the host copy: same run
+    EXPECT_EQ(r2.iterations, r.iterations);
+    EXPECT_EQ(r2.eigenvalue, r.eigenvalue);
+    EXPECT_THROW(M.cast<DenseMat>(), std::bad_cast);
+    std::remove(path);
+}
+
 // ---------------------------------------------------------------- shifted_inverse_power_method_test.cpp
 TEST(ShiftedInversePowerMethodTest, DenseShifts) {
     DenseMat A(2, 2);
