@@ -30,11 +30,19 @@
 
 namespace eigsol {
 
+struct GmresSolver;
+int gmres_create(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const int32_t* ci, const void* v,
+                 double sre, double sim, GmresSolver** out);
+void gmres_free(GmresSolver* g);
+int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev);
+void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps);
+
 struct ShiftFactor {
     eigsol_ctx* ctx = nullptr;
     int dtype = EIGSOL_F64;
     int64_t n = 0;
-    int kind = 0;                 // 0 triangular CSR, 1 dense LU
+    int kind = 0;                 // 0 triangular CSR, 1 dense LU, 2 ILU(0)-preconditioned GMRES
+    GmresSolver* gm = nullptr;    // kind 2 (gmres.hip)
     double sig_re = 0.0, sig_im = 0.0;
     // triangular: everything indexed by solve position (rows sorted by level, levels padded)
     int upper = 1;
@@ -581,6 +589,14 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
     }
 }
 
+// GMRES path: the launch prologue alone (the stop decision and ||y_{t-1}||), the solve follows on
+// the host's word
+template <class S>
+__global__ __launch_bounds__(64) void shift_decide_kernel(TriArgs<S> a, int parity) {
+    __shared__ Prologue pro;
+    shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+}
+
 // Norm and Rayleigh partials of a solved iterate, in a fixed order (grid-stride per thread,
 // block sums, last-arriver sum in block order): sum |y_i|^2 and sum conj(x_i) y_i with
 // x = b / ||y_prev|| as the solve used it.  Skipped once the prologue has stopped the loop.
@@ -1080,6 +1096,7 @@ template <class S> static bool h_zero(S a) {
 
 static void shift_free(ShiftFactor* f) {
     if (!f) return;
+    if (f->gm) gmres_free(f->gm);
     hipSetDevice(f->ctx->device);
     hipStreamSynchronize(f->ctx->stream);
     for (void* p : {(void*)f->order, f->z[0], f->z[1],
@@ -1278,6 +1295,22 @@ static const void* slice_kernel_ptr(int b, bool iter) {
                 : reinterpret_cast<const void*>(dev::sptrsv_slice_kernel<S, 16, false>);
 }
 
+// General (non-triangular) sparse: densified LU up to this order, ILU(0)-preconditioned GMRES above
+// it (EIGSOL_SPARSE_SOLVER=lu|gmres forces one).  The dense LU is a direct factor like the
+// reference's SparseLU; GMRES keeps O(nnz) memory for any order.
+static bool general_sparse_uses_gmres(int64_t n) {
+    if (const char* e = std::getenv("EIGSOL_SPARSE_SOLVER")) {
+        if (!std::strcmp(e, "gmres")) return true;
+        if (!std::strcmp(e, "lu")) return false;
+    }
+    return n > 16384;
+}
+
+template <class S>
+static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<int32_t>& rp,
+                           std::vector<int32_t>& ci, std::vector<S>& v, bool up, double sre, double sim,
+                           ShiftFactor** out);
+
 template <class S>
 static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out) {
     hipStream_t st = A->ctx->stream;
@@ -1294,6 +1327,7 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
             if (ci[e] < i) up = false;
             if (ci[e] > i) lo = false;
         }
+    if (up || lo) return factor_tri_host<S>(A->ctx, A->dtype, n, rp, ci, v, up, sre, sim, out);
     auto* f = new ShiftFactor();
     f->ctx = A->ctx;
     ctx_retain(f->ctx);
@@ -1303,12 +1337,24 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
     f->sig_im = sim;
     f->nnz_total = nnz;
     int rc = EIGSOL_OK;
-    if (!up && !lo) {
+    {
         if constexpr (!kDenseLU<S>) {
             shift_free(f);
             return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: single-precision factors exist for triangular "
                                               "sparse matrices only");
         } else {
+        if (general_sparse_uses_gmres(n)) {
+            rc = gmres_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, &f->gm);
+            f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 1023) / 1024));
+            if (rc == EIGSOL_OK && (hipMalloc(&f->work, 64) != hipSuccess ||
+                                    hipMalloc(&f->wave_part, (size_t)f->red_grid * sizeof(dev::part4)) != hipSuccess ||
+                                    hipMemsetAsync(f->work, 0, 64, st) != hipSuccess))
+                rc = fail(EIGSOL_E_HIP, "solve_shifted: GMRES work buffers");
+            if (rc != EIGSOL_OK) { shift_free(f); return rc; }
+            f->kind = 2;
+            *out = f;
+            return EIGSOL_OK;
+        }
         // general sparse pattern: densify on the device and LU it (the reference's SparseLU)
         rc = dense_limits(A->dtype, n, "solve_shifted (non-triangular sparse)");
         const size_t bytes = (size_t)n * n * sizeof(S);
@@ -1324,6 +1370,24 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         return EIGSOL_OK;
         }
     }
+}
+
+// Triangular CSR (host arrays, columns ascending per row) -> level-ordered factor of A - sigma I.
+template <class S>
+static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<int32_t>& rp,
+                           std::vector<int32_t>& ci, std::vector<S>& v, bool up, double sre, double sim,
+                           ShiftFactor** out) {
+    hipStream_t st = ctx->stream;
+    const int64_t nnz = rp[n];
+    auto* f = new ShiftFactor();
+    f->ctx = ctx;
+    ctx_retain(f->ctx);
+    f->dtype = dtype;
+    f->n = n;
+    f->sig_re = sre;
+    f->sig_im = sim;
+    f->nnz_total = nnz;
+    int rc = EIGSOL_OK;
     f->upper = up ? 1 : 0;
     // split diagonal / off-diagonal; pivots d_i - sigma (missing diagonal: 0 - sigma)
     const S sig = make_sigma<S>(sre, sim);
@@ -1547,6 +1611,22 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
     return EIGSOL_OK;
 }
 
+// triangular factor from host CSR arrays (the ILU(0) factors of the GMRES path, gmres.hip)
+int shift_factor_tri(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<int32_t>& rp, std::vector<int32_t>& ci,
+                     const void* vals, bool up, ShiftFactor** out) {
+    auto run = [&](auto tag) {
+        using S = decltype(tag);
+        std::vector<S> v(static_cast<const S*>(vals), static_cast<const S*>(vals) + rp[n]);
+        return factor_tri_host<S>(ctx, dtype, n, rp, ci, v, up, 0.0, 0.0, out);
+    };
+    switch (dtype) {
+        case EIGSOL_C128: return run(cplx{});
+        case EIGSOL_F32: return run(0.0f);
+        case EIGSOL_C64: return run(cplxf{});
+        default: return run(0.0);
+    }
+}
+
 int shift_factor_csr(eigsol_csr* A, const void* sigma, ShiftFactor** out) {
     if (A->dist) return fail(EIGSOL_E_UNSUPPORTED, "shifted inverse iteration: row-sharded matrices are not supported");
     double s[2] = {0.0, 0.0};
@@ -1575,6 +1655,34 @@ template <class S>
 static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, void* buf0, void* buf1,
                           PowerCtl* ctl, const void* rank_part, void* my_part, void* trace, int parity) {
     hipStream_t st = f->ctx->stream;
+    if (f->kind == 2) {
+        // ILU(0)-preconditioned GMRES: host-driven (one sync per Arnoldi step), so the iteration is
+        // prologue launch -> host reads the stop decision -> solve -> partials launch
+        if (!iter) return gmres_solve(f->gm, b, 0.0, y);
+        dev::TriArgs<S> a{};
+        a.n = f->n;
+        a.work = f->work;
+        a.wave_part = static_cast<dev::part4*>(f->wave_part);
+        a.buf0 = static_cast<S*>(buf0);
+        a.buf1 = static_cast<S*>(buf1);
+        a.ctl = ctl;
+        a.rank_part = static_cast<const dev::part4*>(rank_part);
+        a.my_part = static_cast<dev::part4*>(my_part);
+        a.trace = static_cast<S*>(trace);
+        a.sig_re = f->sig_re;
+        a.sig_im = f->sig_im;
+        hipLaunchKernelGGL((dev::shift_decide_kernel<S>), dim3(1), dim3(64), 0, st, a, parity);
+        int32_t done = 0;
+        double nrm = 0.0;
+        EIGSOL_HIP(hipMemcpyAsync(&done, &ctl->done, sizeof(done), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipMemcpyAsync(&nrm, &ctl->st[parity ^ 1].nrm, sizeof(nrm), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        if (done) return EIGSOL_OK;
+        EIGSOL_TRY(gmres_solve(f->gm, parity ? buf0 : buf1, nrm, parity ? buf1 : buf0));
+        hipLaunchKernelGGL((dev::shift_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a, parity);
+        EIGSOL_HIP(hipGetLastError());
+        return EIGSOL_OK;
+    }
     if (f->kind == 0) {
         dev::TriArgs<S> a{};
         a.order = f->order;
@@ -1713,7 +1821,10 @@ int shift_solve_launch(ShiftFactor* f, const void* b_dev, void* y_dev) {
 // algorithmic bytes of one solve (the SpTRSV counts like the SpMV) and variant
 void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* tiles) {
     const double sb = (double)scalar_bytes(f->dtype), n = (double)f->n;
-    if (f->kind == 0) {
+    if (f->kind == 2) {
+        gmres_info(f->gm, bytes, tiles);
+        if (variant) *variant = 6;
+    } else if (f->kind == 0) {
         if (bytes) *bytes = (sb + 4.0) * (double)f->nnz_total + 4.0 * (n + 1.0) + 2.0 * sb * n;
         if (variant) *variant = 3;
         if (tiles) *tiles = f->nlevels;

@@ -139,6 +139,31 @@ def triu_complex(n: int, k: int, seed: int = 42, target=1.5 * np.exp(0.7j), gap:
     return rowptr.astype(np.int32), colidx.astype(np.int32), values, d
 
 
+def general_complex(n: int, k: int, seed: int = 42, target=1.5 * np.exp(0.7j), gap: float = 0.05, sub: float = 0.3):
+    """Non-triangular complex CSR with known eigenvalues (the general-sparse shifted-inverse case).
+
+    triu_complex plus a subdiagonal entry A(i+1, i) = sub * e^{i phi} for every even i whose row i
+    stores no (i, i+1): the matrix is block upper triangular with 2 x 2 diagonal blocks
+    [[d_i, 0], [c, d_{i+1}]], so its eigenvalues are still the diagonal (planted target included),
+    while no row/column permutation makes the pattern triangular for the solver's test.
+    Returns (rowptr, colidx, values, diagonal)."""
+    rp, ci, v, d = triu_complex(n, k, seed=seed, target=target, gap=gap)
+    rp = rp.astype(np.int64)
+    first_off = np.where(np.diff(rp) > 1, ci[np.minimum(rp[:-1] + 1, len(ci) - 1)], -1)
+    i = np.arange(0, n - 1, 2)
+    add = i[first_off[i] != i + 1]                  # (i, i+1) absent: the 2 x 2 block stays lower triangular
+    phi = np.random.default_rng([seed, 6]).uniform(0, 2 * np.pi, add.size)
+    rows = np.repeat(np.arange(n), np.diff(rp))
+    rows = np.concatenate([rows, add + 1])
+    cols = np.concatenate([ci.astype(np.int64), add])
+    vals = np.concatenate([v, sub * np.exp(1j * phi)])
+    order = np.lexsort((cols, rows))
+    rows, cols, vals = rows[order], cols[order], vals[order]
+    rowptr = np.zeros(n + 1, np.int64)
+    np.add.at(rowptr, rows + 1, 1)
+    return np.cumsum(rowptr).astype(np.int32), cols.astype(np.int32), vals, d
+
+
 def start_vector(n: int, dtype=np.float64, seed: int = 7, row0: int = 0) -> np.ndarray:
     """x0 of SURVEY §8d: U(-1, 1) per (re, im) component, seed 7 (normalised by the solver).
     Entries [row0, row0 + n) of the global start vector, drawn in the generators' fixed chunks, so

@@ -189,6 +189,7 @@ TEST(ReaderTest, SparseFileStraightToDevice) {
     EXPECT_EQ(r2.iterations, r.iterations);
     EXPECT_EQ(r2.eigenvalue, r.eigenvalue);
     EXPECT_THROW(M.cast<DenseMat>(), std::bad_cast);
+    EigSol::set_random_seed(0x5eed5eedULL);   // leave the default sequence to later cases
     std::remove(path);
 }
 
