@@ -291,7 +291,8 @@ class PowerSession:
                  2: "dense_kernel (GEMV)", 3: "sptrsv_kernel (sync-free triangular solve)",
                  4: "dense_lu_solve_kernel (LU substitution)",
                  5: "csr_slice_kernel (64-row slices, one row per lane)",
-                 6: "csr_row_kernel (one row per lane, single-precision fallback layout)"}
+                 6: "csr_row_kernel (one row per lane, single-precision fallback layout)",
+                 7: "ILU(0)-preconditioned GMRES (tiles = Arnoldi steps of the last solve)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?")}
 

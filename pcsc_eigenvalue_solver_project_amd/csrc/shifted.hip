@@ -1823,7 +1823,7 @@ void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* 
     const double sb = (double)scalar_bytes(f->dtype), n = (double)f->n;
     if (f->kind == 2) {
         gmres_info(f->gm, bytes, tiles);
-        if (variant) *variant = 6;
+        if (variant) *variant = 7;
     } else if (f->kind == 0) {
         if (bytes) *bytes = (sb + 4.0) * (double)f->nnz_total + 4.0 * (n + 1.0) + 2.0 * sb * n;
         if (variant) *variant = 3;
