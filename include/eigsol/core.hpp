@@ -62,18 +62,27 @@ inline constexpr bool DeviceScalar = std::is_same_v<S, double> || std::is_same_v
 // in single precision, norm/dot partials in double).  The other solvers (dense and general-sparse
 // shifted inverse, solve_shifted on a non-triangular matrix, Hessenberg, QR) promote the matrix,
 // vectors and shift to double on the host and round the results back (a deliberate deviation:
-// fp64 arithmetic, at least as accurate as the reference's single precision).  long double has no
-// device path (no 80-bit arithmetic on the GPU).
+// fp64 arithmetic, at least as accurate as the reference's single precision).  long double and
+// std::complex<long double> (WideScalar) run on the fp64 kernels too: the GPU has no 80-bit
+// arithmetic, so the matrix, vectors and shift are rounded to double on the host, the device
+// computes in double, and the results are widened back — a documented precision deviation (53-bit
+// against x87's 64-bit significand; identical behaviour for tolerances above ~1e-15).
 template <typename S>
 inline constexpr bool PromotedScalar = std::is_same_v<S, float> || std::is_same_v<S, std::complex<float>>;
 template <typename S>
-inline constexpr bool DeviceCapable = DeviceScalar<S> || PromotedScalar<S>;
+inline constexpr bool WideScalar = std::is_same_v<S, long double> || std::is_same_v<S, std::complex<long double>>;
+template <typename S>
+inline constexpr bool DeviceCapable = DeviceScalar<S> || PromotedScalar<S> || WideScalar<S>;
 template <typename S>
 struct device_scalar { using type = S; };
 template <>
 struct device_scalar<float> { using type = double; };
 template <>
 struct device_scalar<std::complex<float>> { using type = std::complex<double>; };
+template <>
+struct device_scalar<long double> { using type = double; };
+template <>
+struct device_scalar<std::complex<long double>> { using type = std::complex<double>; };
 template <typename S>
 using device_scalar_t = typename device_scalar<S>::type;
 

@@ -10,7 +10,8 @@
 //
 // Scalars: double and std::complex<double> natively; float and std::complex<float> natively for the
 // power method and the triangular-CSR shifted inverse, promoted to fp64 for the other solvers
-// (core.hpp, PromotedScalar); long double throws "scalar type not supported by the device path".
+// (core.hpp, PromotedScalar); long double / std::complex<long double> run on the fp64 kernels
+// (core.hpp, WideScalar).
 //
 // Start vector: the reference draws x0 with Eigen's Vector::Random (std::rand, not reproducible
 // across Eigen versions).  Here x0 comes from a documented generator
@@ -87,7 +88,7 @@ void DenseMatrix<S>::setRandom() {
 // QR iteration variant: the reference's unshifted H <- RQ iteration (qr_eigenvalues.hpp:62-105,
 // identical iteration counts, `converged` and positional diag(H)) is what the reference-signature
 // overloads run; Francis (implicit multishift sweeps with aggressive early deflation, north_star)
-// is opt-in by passing QRVariant::Francis: it converges on general real matrices, deflates at
+// is opt-in by passing QRVariant::Francis: it converges on general real and complex matrices, deflates at
 // LAPACK's threshold, reports `iterations` as its sweep count and returns the real parts in
 // `eigenvalues` with the complex eigenvalues in `eigenvalues_complex`.
 enum class QRVariant { Francis = EIGSOL_QR_FRANCIS, Unshifted = EIGSOL_QR_UNSHIFTED };
@@ -163,7 +164,11 @@ EigenResult<S> power_like(const Matrix& M, const SolverOptions& opts, const Vect
         // dense and general-sparse shifted inverse have fp64 factors only
         const bool native = !PromotedScalar<S> || !shift || !M.isDense();
         int st = EIGSOL_E_UNSUPPORTED;
-        if (native) st = power_run<S>(M.device<S>(), M.isDense(), o, xs0, shift, res);
+        if constexpr (WideScalar<S>) {   // long double: the fp64 kernels (see core.hpp)
+            st = power_run<device_scalar_t<S>>(M.device_fp64<S>(), M.isDense(), o, xs0, shift, res);
+        } else {
+            if (native) st = power_run<S>(M.device<S>(), M.isDense(), o, xs0, shift, res);
+        }
         if constexpr (PromotedScalar<S>) {
             if (st == EIGSOL_E_UNSUPPORTED && shift)
                 st = power_run<device_scalar_t<S>>(M.device_fp64<S>(), M.isDense(), o, xs0, shift, res);
@@ -226,7 +231,11 @@ Vector<S> solve_shifted(const Matrix& A, const S shift, const Vector<S>& b) {
         };
         // single precision: triangular CSR natively, everything else on the fp64 factor
         int st = EIGSOL_E_UNSUPPORTED;
-        if (!PromotedScalar<S> || !A.isDense()) st = run(S{}, A.device<S>());
+        if constexpr (WideScalar<S>) {
+            st = run(device_scalar_t<S>{}, A.device_fp64<S>());
+        } else {
+            if (!PromotedScalar<S> || !A.isDense()) st = run(S{}, A.device<S>());
+        }
         if constexpr (PromotedScalar<S>)
             if (st == EIGSOL_E_UNSUPPORTED) st = run(device_scalar_t<S>{}, A.device_fp64<S>());
         detail::check(st, "solve_shifted");
@@ -239,7 +248,7 @@ template <ScalarConcept S>
 DenseMatrix<S> to_hessenberg_dense(const DenseMatrix<S>& A) {
     detail::dense_square_check(A, "to_hessenberg_dense");
     detail::require_device_scalar<S>("to_hessenberg_dense");
-    if constexpr (PromotedScalar<S>)
+    if constexpr (PromotedScalar<S> || WideScalar<S>)
         return detail::convert_dense<S>(to_hessenberg_dense(detail::convert_dense<device_scalar_t<S>>(A)));
     DenseMatrix<S> H(A.rows(), A.cols());
     if constexpr (DeviceScalar<S>) {
@@ -261,7 +270,7 @@ template <ScalarConcept S>
 void qr_decompose_dense(const DenseMatrix<S>& A, DenseMatrix<S>& Q, DenseMatrix<S>& R) {
     if (A.rows() == 0 || A.cols() == 0) throw std::runtime_error("qr_decompose_dense: empty matrix");
     detail::require_device_scalar<S>("qr_decompose_dense");
-    if constexpr (PromotedScalar<S>) {
+    if constexpr (PromotedScalar<S> || WideScalar<S>) {
         using D = device_scalar_t<S>;
         DenseMatrix<D> Qd, Rd;
         qr_decompose_dense<D>(detail::convert_dense<D>(A), Qd, Rd);
@@ -293,7 +302,7 @@ QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& o
     const std::int64_t n = A.rows();
     if (n == 0) return QRResult<S>(Vector<S>(), 0, true);   // qr_eigenvalues.hpp:55-57
     detail::require_device_scalar<S>("qr_eigenvalues_dense");
-    if constexpr (PromotedScalar<S>) {
+    if constexpr (PromotedScalar<S> || WideScalar<S>) {
         using D = device_scalar_t<S>;
         const QRResult<D> rd = qr_eigenvalues_dense<D>(detail::convert_dense<D>(A), opts, variant);
         QRResult<S> rs(detail::convert_vec<S>(rd.eigenvalues), rd.iterations, rd.converged);
@@ -310,10 +319,11 @@ QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& o
                                                   static_cast<int>(variant), ev.data(), wi.data(), &it, &conv),
                       "qr_eigenvalues_dense");
         res = QRResult<S>(ev, it, conv != 0);
-        if constexpr (std::is_same_v<S, double>) {
-            if (variant == QRVariant::Francis) {
-                res.eigenvalues_complex.resize(static_cast<std::size_t>(n));
-                for (std::int64_t i = 0; i < n; ++i) res.eigenvalues_complex[i] = {ev(i), wi[i]};
+        if (variant == QRVariant::Francis) {
+            res.eigenvalues_complex.resize(static_cast<std::size_t>(n));
+            for (std::int64_t i = 0; i < n; ++i) {
+                if constexpr (std::is_same_v<S, double>) res.eigenvalues_complex[i] = {ev(i), wi[i]};
+                else res.eigenvalues_complex[i] = ev(i);   // complex sweeps return the eigenvalues themselves
             }
         }
     }

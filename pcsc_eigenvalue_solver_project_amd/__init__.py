@@ -428,7 +428,8 @@ def qr_decompose(ctx: Context, A):
 
 def qr_eigenvalues(ctx: Context, A, opts: SolverOptions = SolverOptions(), variant: str = "francis") -> QRResult:
     """``EigSol::qr_eigenvalues<S>``.  variant "unshifted" = the reference algorithm
-    (qr_eigenvalues.hpp:40-108); "francis" = implicit multishift sweeps (real matrices)."""
+    (qr_eigenvalues.hpp:40-108); "francis" = implicit multishift sweeps (real: double-shift
+    bulges, francis.hip; complex: complex two-shift bulges, zfrancis.hip)."""
     A = _square_dense(A, "qr_eigenvalues_dense")
     code = _dtype_code(A.dtype)
     n = A.shape[0]
@@ -444,4 +445,6 @@ def qr_eigenvalues(ctx: Context, A, opts: SolverOptions = SolverOptions(), varia
     full = None
     if v == 0 and A.dtype == np.float64:
         full = eig + 1j * wi[:n]
+    elif v == 0 and A.dtype == np.complex128:
+        full = eig.copy()
     return QRResult(eig, int(it.value), bool(conv.value), full)

@@ -632,6 +632,59 @@ static int qr_francis_host(eigsol_ctx* ctx, int64_t n, const double* A, int max_
     return rc;
 }
 
+// Complex multishift QR (zfrancis.hip): Hessenberg on the device, then complex sweeps; the same
+// norm-range guard as the real path (max |Re|, |Im| of the entries outside [smlnum, 1/smlnum] ->
+// exact power-of-two scaling, eigenvalues scaled back)
+int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_host, int32_t* sweeps_out,
+                       int32_t* fail_out);
+
+static int qr_francis_c128_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_iter, cplx* w,
+                                int32_t* iters, int32_t* conv) {
+    hipStream_t st = ctx->stream;
+    cplx* H = nullptr;
+    int rc = EIGSOL_OK;
+    if (hipMalloc(&H, n * n * sizeof(cplx)) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: hipMalloc");
+    QrWork<cplx> wk;
+    if (rc == EIGSOL_OK) rc = work_alloc(wk, n);
+    if (rc == EIGSOL_OK && hipMemcpyAsync(H, A, n * n * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: upload");
+    int escale = 0;
+    if (rc == EIGSOL_OK) {
+        unsigned long long* dmax = nullptr;
+        unsigned long long bits = 0;
+        if (hipMallocAsync(reinterpret_cast<void**>(&dmax), sizeof(bits), st) != hipSuccess) {
+            rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: hipMallocAsync");
+        } else {
+            double* Hd = reinterpret_cast<double*>(H);
+            hipMemsetAsync(dmax, 0, sizeof(bits), st);
+            hipLaunchKernelGGL(dev::absmax_kernel, dim3(1024), dim3(256), 0, st, Hd, 2 * n * n, dmax);
+            hipMemcpyAsync(&bits, dmax, sizeof(bits), hipMemcpyDeviceToHost, st);
+            (void)hipFreeAsync(dmax, st);
+            if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: norm-range check");
+            double amax;
+            std::memcpy(&amax, &bits, sizeof(amax));
+            const double smlnum = std::sqrt(std::numeric_limits<double>::min()) / std::numeric_limits<double>::epsilon();
+            if (rc == EIGSOL_OK && std::isfinite(amax) && amax > 0.0 && (amax < smlnum || amax > 1.0 / smlnum)) {
+                escale = -std::ilogb(amax);
+                hipLaunchKernelGGL(dev::scale_pow2_kernel, dim3(1024), dim3(256), 0, st, Hd, 2 * n * n, escale);
+            }
+        }
+    }
+    if (rc == EIGSOL_OK) rc = hessenberg_dev<cplx>(st, H, n, wk);
+    int32_t sweeps = 0, failed = 0;
+    if (rc == EIGSOL_OK) rc = francis_large_c128(ctx, H, n, max_iter, w, &sweeps, &failed);
+    if (rc == EIGSOL_OK && escale != 0)
+        for (int64_t i = 0; i < n; ++i) {
+            w[i].re = std::ldexp(w[i].re, -escale);
+            w[i].im = std::ldexp(w[i].im, -escale);
+        }
+    if (iters) *iters = sweeps;
+    if (conv) *conv = failed ? 0 : 1;
+    work_free(wk);
+    (void)hipFree(H);
+    return rc;
+}
+
 // Small problems: the whole matrix in LDS (n <= kHqrMaxN).  Larger: see francis.hip.
 int hqr_lds(hipStream_t st, const double* H, int64_t ld, int n, int maxits, double* wr_dev, double* wi_dev,
             int* info_dev) {
@@ -678,6 +731,9 @@ int eigsol_qr_eigenvalues_dense(eigsol_ctx* ctx, int dtype, int64_t n, const voi
     }
     if (!A_colmajor || !eig_re_or_c) return fail(EIGSOL_E_INVALID, "eigsol_qr_eigenvalues_dense: null pointer");
     EIGSOL_HIP(hipSetDevice(ctx->device));
+    if (variant != EIGSOL_QR_UNSHIFTED && dtype == EIGSOL_C128)
+        return qr_francis_c128_host(ctx, n, A_colmajor, opts->max_iterations, static_cast<cplx*>(eig_re_or_c),
+                                    iterations, converged);
     if (variant == EIGSOL_QR_UNSHIFTED || dtype == EIGSOL_C128)
         return dtype == EIGSOL_C128
                    ? qr_unshifted_host<cplx>(ctx, n, A_colmajor, opts->max_iterations, opts->tolerance,

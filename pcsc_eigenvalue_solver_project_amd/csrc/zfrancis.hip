@@ -1,0 +1,510 @@
+// Complex multishift QR sweeps (eigenvalues only) for std::complex<double> Hessenberg matrices.
+//
+// The reference's qr_eigenvalues_dense<std::complex<double>> (qr_eigenvalues.hpp:40-108) runs the
+// unshifted iteration H <- R Q, which does not converge on general input (a complex N(0,1) matrix
+// has eigenvalues of equal modulus).  This is the complex counterpart of francis.hip: the same
+// small-bulge chase geometry, with complex arithmetic and shifts that need not come in conjugate
+// pairs (LAPACK ZLAQR5's bulges):
+//   * a bulge carries two shifts (s1, s2); its first column is (H - s1)(H - s2) e_l (scaled as in
+//     ZLAQR1), and it is chased down by 3 x 3 complex Householder reflectors Q = I - tau v v^H
+//     (ZLARFG's convention: Q^H (alpha, x) = (beta, 0) with beta real), the last step by a 2 x 2;
+//   * bulges sit 3 rows apart and move together: every bulge's left update (Q^H on rows k..k+2)
+//     runs before any right update (Q on columns k..k+2), which touch disjoint words within a
+//     phase, and associativity makes the simultaneous step the product of the sequential ones;
+//   * the chain is chased inside an LDS window [s, e) of at most 64 rows/columns (complex: H and
+//     its accumulated unitary U take 2 x 64 KiB of LDS), one wave per bulge; the window's updates
+//     outside it are applied afterwards as complex GEMMs over the columns right of the window
+//     (U^H X) and the rows above it (X U);
+//   * shifts: eigenvalues of the trailing 2 nb x 2 nb block; every 6th sweep without a deflation
+//     uses exceptional shifts; active blocks of at most 64 rows are finished in LDS by a one-wave
+//     single-shift QR (the ZLAHQR iteration: Wilkinson shift, exceptional shifts at iterations 10
+//     and 20, Ahues-Tisseur deflation test).
+// Deflation: |h(k,k-1)| <= eps (|h(k,k)| + |h(k-1,k-1)|) with |z| = |Re z| + |Im z| (ZLAHQR's cabs1).
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "kernels_common.hpp"
+
+namespace eigsol {
+namespace dev {
+
+constexpr int kZWin = 64;         // window rows/columns
+constexpr int kZSmall = 64;       // blocks finished by the one-wave solver
+constexpr int kZMaxBulges = 16;   // one wave each
+
+__device__ __forceinline__ cplx cconj(cplx a) { return cplx{a.re, -a.im}; }
+__device__ __forceinline__ double cabs1(cplx a) { return fabs(a.re) + fabs(a.im); }
+__device__ __forceinline__ cplx cscale(cplx a, double s) { return cplx{a.re * s, a.im * s}; }
+__device__ __forceinline__ cplx cmul_conj(cplx a, cplx b) {   // conj(a) * b
+    return cplx{a.re * b.re + a.im * b.im, a.re * b.im - a.im * b.re};
+}
+__device__ __forceinline__ cplx csqrt_(cplx z) {
+    const double r = hypot(z.re, z.im);
+    if (r == 0.0) return cplx{0.0, 0.0};
+    const double t = sqrt(0.5 * (r + fabs(z.re)));
+    return z.re >= 0.0 ? cplx{t, z.im / (2.0 * t)} : cplx{fabs(z.im) / (2.0 * t), copysign(t, z.im)};
+}
+// robust quotient (Smith's algorithm)
+__device__ __forceinline__ cplx cdiv_s(cplx a, cplx b) {
+    if (fabs(b.re) >= fabs(b.im)) {
+        const double r = b.im / b.re, d = b.re + b.im * r;
+        return cplx{(a.re + a.im * r) / d, (a.im - a.re * r) / d};
+    }
+    const double r = b.re / b.im, d = b.re * r + b.im;
+    return cplx{(a.re * r + a.im) / d, (a.im * r - a.re) / d};
+}
+
+// ZLARFG on (alpha, x1, x2) (x2 ignored when !three): Q = I - tau v v^H, v = (1, v1, v2),
+// Q^H (alpha, x1, x2) = (beta, 0, 0).  tau = 0 (Q = I) when x = 0 and alpha is real.  The caller
+// scales the input to O(1).
+__device__ __forceinline__ void zhouse(cplx a, cplx x1, cplx x2, bool three, double& beta, cplx& tau, cplx& v1,
+                                       cplx& v2) {
+    const double xn2 = sq_abs(x1) + (three ? sq_abs(x2) : 0.0);
+    if (xn2 == 0.0 && a.im == 0.0) {
+        beta = a.re;
+        tau = cplx{0.0, 0.0};
+        v1 = v2 = cplx{0.0, 0.0};
+        return;
+    }
+    const double an = sqrt(a.re * a.re + a.im * a.im + xn2);
+    beta = a.re >= 0.0 ? -an : an;
+    tau = cplx{(beta - a.re) / beta, -a.im / beta};
+    const cplx d = cplx{a.re - beta, a.im};
+    v1 = cdiv_s(x1, d);
+    v2 = three ? cdiv_s(x2, d) : cplx{0.0, 0.0};
+}
+
+// ---------------------------------------------------------------- one-wave single-shift QR (n <= 64)
+// Eigenvalues of an n x n Hessenberg block (ZLAHQR without Schur vectors; updates confined to the
+// active block).  info[0] = 1 if some eigenvalue needed more than 30 max(10, n) iterations,
+// info[1] = most iterations any eigenvalue took.
+__global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t ld, int n, cplx* w, int* info) {
+    __shared__ cplx h[kZSmall * (kZSmall + 1)];
+    constexpr int lh = kZSmall + 1;
+    const int ln = threadIdx.x;
+    auto H = [&](int i, int j) -> cplx& { return h[i + j * lh]; };
+    for (int idx = ln; idx < n * n; idx += 64) H(idx % n, idx / n) = Hin[(idx % n) + (int64_t)(idx / n) * ld];
+    __syncthreads();
+    const double ulp = 2.220446049250313e-16, smlnum = 2.2250738585072014e-308 * ((double)n / ulp);
+    const int itmax = 30 * max(10, n);
+    int failed = 0, maxits = 0, i = n - 1;
+    while (i >= 0) {
+        int l = 0, its = 0;
+        for (; its <= itmax; ++its) {
+            int k = i;
+            for (; k > l; --k) {
+                const cplx hk = H(k, k - 1);
+                if (cabs1(hk) <= smlnum) break;
+                double tst = cabs1(H(k - 1, k - 1)) + cabs1(H(k, k));
+                if (tst == 0.0) {
+                    if (k - 2 >= l) tst += fabs(H(k - 1, k - 2).re);
+                    if (k + 1 <= i) tst += fabs(H(k + 1, k).re);
+                }
+                if (cabs1(hk) <= ulp * tst) {
+                    const double ab = fmax(cabs1(hk), cabs1(H(k - 1, k))), ba = fmin(cabs1(hk), cabs1(H(k - 1, k)));
+                    const cplx dd = sub(H(k - 1, k - 1), H(k, k));
+                    const double aa = fmax(cabs1(H(k, k)), cabs1(dd)), bb = fmin(cabs1(H(k, k)), cabs1(dd));
+                    const double s = aa + ab;
+                    if (ba * (ab / s) <= fmax(smlnum, ulp * (bb * (aa / s)))) break;
+                }
+            }
+            l = k;
+            if (l > 0) {
+                __syncthreads();
+                if (ln == 0) H(l, l - 1) = cplx{0.0, 0.0};
+                __syncthreads();
+            }
+            if (l >= i) break;
+            // shift
+            cplx t;
+            if (its == 10) {
+                t = add(cplx{0.75 * fabs(H(l + 1, l).re), 0.0}, H(l, l));
+            } else if (its == 20) {
+                t = add(cplx{0.75 * fabs(H(i, i - 1).re), 0.0}, H(i, i));
+            } else {
+                t = H(i, i);
+                const cplx u = mul(csqrt_(H(i - 1, i)), csqrt_(H(i, i - 1)));
+                double s = cabs1(u);
+                if (s != 0.0) {
+                    const cplx x = cscale(sub(H(i - 1, i - 1), t), 0.5);
+                    const double sx = cabs1(x);
+                    s = fmax(s, sx);
+                    const cplx xs = cscale(x, 1.0 / s), us = cscale(u, 1.0 / s);
+                    cplx y = cscale(csqrt_(add(mul(xs, xs), mul(us, us))), s);
+                    if (sx > 0.0) {
+                        const cplx xn = cscale(x, 1.0 / sx);
+                        if (xn.re * y.re + xn.im * y.im < 0.0) y = cplx{-y.re, -y.im};
+                    }
+                    t = sub(t, mul(u, cdiv_s(u, add(x, y))));
+                }
+            }
+            // single-shift sweep from l
+            for (int kk = l; kk < i; ++kk) {
+                cplx v0, v1;
+                if (kk == l) {
+                    const cplx h11s = sub(H(l, l), t);
+                    const cplx h21 = H(l + 1, l);
+                    const double s = cabs1(h11s) + cabs1(h21);
+                    v0 = s > 0.0 ? cscale(h11s, 1.0 / s) : h11s;
+                    v1 = s > 0.0 ? cscale(h21, 1.0 / s) : h21;
+                } else {
+                    v0 = H(kk, kk - 1);
+                    v1 = H(kk + 1, kk - 1);
+                }
+                double beta;
+                cplx tau, vv, unused;
+                zhouse(v0, v1, cplx{0.0, 0.0}, false, beta, tau, vv, unused);
+                __syncthreads();
+                if (kk > l && ln == 0) {
+                    H(kk, kk - 1) = cplx{beta, 0.0};
+                    H(kk + 1, kk - 1) = cplx{0.0, 0.0};
+                }
+                const cplx ct = cconj(tau);
+                {   // left: rows kk, kk+1, columns kk..i
+                    const int c = kk + ln;
+                    if (c <= i) {
+                        const cplx a0 = H(kk, c), a1 = H(kk + 1, c);
+                        const cplx s = mul(ct, add(a0, cmul_conj(vv, a1)));
+                        H(kk, c) = sub(a0, s);
+                        H(kk + 1, c) = sub(a1, mul(s, vv));
+                    }
+                }
+                __syncthreads();
+                {   // right: columns kk, kk+1, rows l..min(kk+2, i)
+                    const int r = l + ln;
+                    if (r <= min(kk + 2, i)) {
+                        const cplx a0 = H(r, kk), a1 = H(r, kk + 1);
+                        const cplx s = mul(tau, add(a0, mul(a1, vv)));
+                        H(r, kk) = sub(a0, s);
+                        H(r, kk + 1) = sub(a1, mul(s, cconj(vv)));
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        if (its > itmax) {
+            failed = 1;
+            break;
+        }
+        maxits = max(maxits, its);
+        // H(l..i) has deflated to a single eigenvalue at i (l == i)
+        if (ln == 0) w[i] = H(i, i);
+        i = l - 1;
+    }
+    if (failed) {
+        for (int r = ln; r <= i; r += 64) w[r] = H(r, r);   // best effort, flagged as failed
+    }
+    if (ln == 0) {
+        info[0] = failed;
+        info[1] = maxits;
+    }
+}
+
+// ---------------------------------------------------------------- windowed multishift chase
+struct ZChaseArgs {
+    cplx* H;
+    int64_t n;
+    int l, ihi;
+    int s, e;          // window [s, e)
+    int t0, t1;        // chase steps of this launch
+    int nb;            // bulges
+    const cplx* shifts;   // 2 per bulge
+    cplx* U;           // out: (e - s)^2, column-major
+};
+
+__global__ __launch_bounds__(1024) void zchase_kernel(ZChaseArgs a) {
+    __shared__ cplx h[kZWin * (kZWin + 1)];
+    __shared__ cplx u[kZWin * kZWin];
+    constexpr int lh = kZWin + 1, lu = kZWin;
+    const int W = a.e - a.s;
+    const int tid = threadIdx.x;
+    auto Hw = [&](int i, int j) -> cplx& { return h[(i - a.s) + (j - a.s) * lh]; };
+    for (int idx = tid; idx < W * W; idx += 1024) {
+        const int i = idx % W, j = idx / W;
+        h[i + j * lh] = a.H[(a.s + i) + (int64_t)(a.s + j) * a.n];
+        u[i + j * lu] = (i == j) ? cplx{1.0, 0.0} : cplx{0.0, 0.0};
+    }
+    __syncthreads();
+    const int l = a.l, ihi = a.ihi;
+    const int wv = tid >> 6, ln = tid & 63;
+    const int rlo = max(l, a.s);
+    for (int t = a.t0; t < a.t1; ++t) {
+        const int k = l + t - 3 * wv;
+        const bool live = wv < a.nb && k >= l && k <= ihi - 1;
+        const bool three = k != ihi - 1;
+        double beta = 0.0;
+        cplx tau{0.0, 0.0}, v1{0.0, 0.0}, v2{0.0, 0.0};
+        bool act = false;
+        if (live) {
+            cplx p, q, r;
+            int ex = 0;
+            if (k == l) {
+                const cplx s1 = a.shifts[2 * wv], s2 = a.shifts[2 * wv + 1];
+                const cplx h11 = Hw(l, l), h21 = Hw(l + 1, l), h12 = Hw(l, l + 1), h22 = Hw(l + 1, l + 1);
+                const double s = cabs1(sub(h11, s2)) + cabs1(h21);
+                if (s == 0.0) {
+                    p = q = r = cplx{0.0, 0.0};
+                } else {
+                    const cplx h21s = cscale(h21, 1.0 / s);
+                    p = add(mul(h21s, h12), mul(sub(h11, s1), cscale(sub(h11, s2), 1.0 / s)));
+                    q = mul(h21s, sub(add(h11, h22), add(s1, s2)));
+                    r = three ? mul(h21s, Hw(l + 2, l + 1)) : cplx{0.0, 0.0};
+                }
+            } else {
+                p = Hw(k, k - 1);
+                q = Hw(k + 1, k - 1);
+                r = three ? Hw(k + 2, k - 1) : cplx{0.0, 0.0};
+            }
+            const double mx = fmax(fmax(cabs1(p), cabs1(q)), cabs1(r));
+            if (mx > 0.0) {
+                ex = __builtin_amdgcn_frexp_exp(mx);   // exact power-of-two scaling into [1/2, 1)
+                p = cplx{ldexp(p.re, -ex), ldexp(p.im, -ex)};
+                q = cplx{ldexp(q.re, -ex), ldexp(q.im, -ex)};
+                r = cplx{ldexp(r.re, -ex), ldexp(r.im, -ex)};
+                zhouse(p, q, r, three, beta, tau, v1, v2);
+                act = true;
+                if (k != l && ln == 0) {
+                    Hw(k, k - 1) = cplx{ldexp(beta, ex), 0.0};
+                    Hw(k + 1, k - 1) = cplx{0.0, 0.0};
+                    if (three) Hw(k + 2, k - 1) = cplx{0.0, 0.0};
+                }
+                const cplx ct = cconj(tau);
+                // phase A: left update (Q^H on rows k..k+2), columns [k, e)
+                const int c = k + ln;
+                if (c < a.e) {
+                    const cplx x0 = Hw(k, c), x1 = Hw(k + 1, c);
+                    const cplx x2 = three ? Hw(k + 2, c) : cplx{0.0, 0.0};
+                    cplx wsum = add(x0, cmul_conj(v1, x1));
+                    if (three) wsum = add(wsum, cmul_conj(v2, x2));
+                    const cplx s = mul(ct, wsum);
+                    Hw(k, c) = sub(x0, s);
+                    Hw(k + 1, c) = sub(x1, mul(s, v1));
+                    if (three) Hw(k + 2, c) = sub(x2, mul(s, v2));
+                }
+                // U <- U Q on columns k..k+2 (window-relative), every row
+                if (ln < W) {
+                    const int kk = k - a.s;
+                    const cplx y0 = u[ln + kk * lu], y1 = u[ln + (kk + 1) * lu];
+                    const cplx y2 = three ? u[ln + (kk + 2) * lu] : cplx{0.0, 0.0};
+                    cplx wsum = add(y0, mul(y1, v1));
+                    if (three) wsum = add(wsum, mul(y2, v2));
+                    const cplx s = mul(tau, wsum);
+                    u[ln + kk * lu] = sub(y0, s);
+                    u[ln + (kk + 1) * lu] = sub(y1, mul(s, cconj(v1)));
+                    if (three) u[ln + (kk + 2) * lu] = sub(y2, mul(s, cconj(v2)));
+                }
+            }
+        }
+        __syncthreads();
+        if (act) {   // phase B: right update (Q on columns k..k+2), rows [rlo, min(k + 3, ihi)]
+            const int r = rlo + ln;
+            if (r <= min(k + 3, ihi)) {
+                const cplx y0 = Hw(r, k), y1 = Hw(r, k + 1);
+                const cplx y2 = three ? Hw(r, k + 2) : cplx{0.0, 0.0};
+                cplx wsum = add(y0, mul(y1, v1));
+                if (three) wsum = add(wsum, mul(y2, v2));
+                const cplx s = mul(tau, wsum);
+                Hw(r, k) = sub(y0, s);
+                Hw(r, k + 1) = sub(y1, mul(s, cconj(v1)));
+                if (three) Hw(r, k + 2) = sub(y2, mul(s, cconj(v2)));
+            }
+        }
+        __syncthreads();
+    }
+    for (int idx = tid; idx < W * W; idx += 1024) {
+        const int i = idx % W, j = idx / W;
+        a.H[(a.s + i) + (int64_t)(a.s + j) * a.n] = h[i + j * lh];
+        a.U[idx] = u[i + j * lu];
+    }
+}
+
+// Delayed window updates.  left: H(s:s+W, c0:c0+64) <- U^H H(s:s+W, c0:c0+64) (columns [lo, hi));
+// right: H(r0:r0+64, s:s+W) <- H(r0:r0+64, s:s+W) U (rows [lo, hi)).  64 output columns (rows)
+// per workgroup, U and the panel staged in LDS; each thread owns one column (row) and 16 rows
+// (columns) of the output.
+template <bool kLeft>
+__global__ __launch_bounds__(256) void zwin_gemm_kernel(cplx* H, int64_t n, int s, int W, int64_t lo, int64_t hi,
+                                                        const cplx* U) {
+    __shared__ cplx us[kZWin * kZWin];
+    __shared__ cplx xs[kZWin * kZWin];
+    const int tid = threadIdx.x;
+    const int64_t b0 = lo + (int64_t)blockIdx.x * 64;
+    const int nb = (int)std::min<int64_t>(64, hi - b0);
+    for (int idx = tid; idx < W * W; idx += 256) us[idx] = U[idx];
+    for (int idx = tid; idx < W * 64; idx += 256) {
+        if (kLeft) {   // xs[i + j W] = H(s + i, b0 + j)
+            const int i = idx % W, j = idx / W;
+            xs[idx] = j < nb ? H[(s + i) + (b0 + j) * n] : cplx{0.0, 0.0};
+        } else {       // xs[i + j 64] = H(b0 + i, s + j)
+            const int i = idx % 64, j = idx / 64;
+            xs[idx] = i < nb ? H[(b0 + i) + (int64_t)(s + j) * n] : cplx{0.0, 0.0};
+        }
+    }
+    __syncthreads();
+    const int own = tid & 63, grp = tid >> 6;   // 4 groups of 16 outputs
+    cplx acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = cplx{0.0, 0.0};
+    if (kLeft) {   // out(i, own) = sum_r conj(U(r, i)) X(r, own), i = grp*16 + q
+        for (int r = 0; r < W; ++r) {
+            const cplx x = xs[r + own * W];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int i = grp * 16 + q;
+                if (i < W) acc[q] = add(acc[q], cmul_conj(us[r + i * W], x));
+            }
+        }
+        if (own < nb)
+            for (int q = 0; q < 16; ++q) {
+                const int i = grp * 16 + q;
+                if (i < W) H[(s + i) + (b0 + own) * n] = acc[q];
+            }
+    } else {       // out(own, j) = sum_r X(own, r) U(r, j), j = grp*16 + q
+        for (int r = 0; r < W; ++r) {
+            const cplx x = xs[own + r * 64];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int j = grp * 16 + q;
+                if (j < W) acc[q] = add(acc[q], mul(x, us[r + j * W]));
+            }
+        }
+        if (own < nb)
+            for (int q = 0; q < 16; ++q) {
+                const int j = grp * 16 + q;
+                if (j < W) H[(b0 + own) + (int64_t)(s + j) * n] = acc[q];
+            }
+    }
+}
+
+__global__ void zdiag_sub_kernel(const cplx* H, int64_t n, int ihi, cplx* out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i > ihi) return;
+    out[i] = H[i + (int64_t)i * n];
+    out[n + i] = i > 0 ? H[i + (int64_t)(i - 1) * n] : cplx{0.0, 0.0};
+}
+
+}  // namespace dev
+
+static double cabs1_h(const cplx& a) { return std::fabs(a.re) + std::fabs(a.im); }
+
+// eigenvalues of the complex Hessenberg matrix H (device, n x n, leading dimension n; destroyed)
+int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_host, int32_t* sweeps_out,
+                       int32_t* fail_out) {
+    hipStream_t st = ctx->stream;
+    const double eps = 2.220446049250313e-16;
+    cplx *dw = nullptr, *dds = nullptr, *dU = nullptr, *dsh = nullptr;
+    int* dinfo = nullptr;
+    int rc = EIGSOL_OK;
+    if (hipMalloc(&dw, n * sizeof(cplx)) != hipSuccess || hipMalloc(&dds, 2 * n * sizeof(cplx)) != hipSuccess ||
+        hipMalloc(&dU, dev::kZWin * dev::kZWin * sizeof(cplx)) != hipSuccess ||
+        hipMalloc(&dsh, 2 * dev::kZMaxBulges * sizeof(cplx)) != hipSuccess || hipMalloc(&dinfo, 64) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "complex QR: hipMalloc");
+    std::vector<cplx> ds(2 * n), swv(2 * dev::kZMaxBulges);
+    int sweeps = 0, failed = 0, stall = 0;
+    int ihi = (int)n - 1;
+    const int max_stall = std::max(1, maxits);
+    auto small = [&](int l, int hi, cplx* wdst, int info[2]) -> int {
+        hipLaunchKernelGGL(dev::zhqr_wave_kernel, dim3(1), dim3(64), 0, st, H + l + (int64_t)l * n, (int64_t)n,
+                           hi - l + 1, wdst, dinfo);
+        EIGSOL_HIP(hipMemcpyAsync(info, dinfo, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        return EIGSOL_OK;
+    };
+    auto scan = [&]() -> int {
+        hipLaunchKernelGGL(dev::zdiag_sub_kernel, dim3((ihi + 256) / 256), dim3(256), 0, st, H, (int64_t)n, ihi, dds);
+        EIGSOL_HIP(hipMemcpyAsync(ds.data(), dds, 2 * n * sizeof(cplx), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        return EIGSOL_OK;
+    };
+    while (rc == EIGSOL_OK && ihi >= 0) {
+        if ((rc = scan()) != EIGSOL_OK) break;
+        int l = ihi;
+        while (l > 0) {
+            const cplx sd = ds[n + l];
+            if (cabs1_h(sd) <= eps * (cabs1_h(ds[l - 1]) + cabs1_h(ds[l])) || (sd.re == 0.0 && sd.im == 0.0)) break;
+            --l;
+        }
+        const int N = ihi - l + 1;
+        if (N <= dev::kZSmall) {
+            int info[2];
+            if ((rc = small(l, ihi, dw + l, info)) != EIGSOL_OK) break;
+            if (info[0]) failed = 1;
+            sweeps = std::max({sweeps, stall, info[1]});
+            stall = 0;
+            ihi = l - 1;
+            continue;
+        }
+        if (++stall > max_stall) { failed = 1; sweeps = std::max(sweeps, stall); break; }
+        int nb = std::min(dev::kZMaxBulges, std::max(1, N / 16));
+        const int ns = 2 * nb;
+        std::vector<cplx> sh(ns);
+        bool exceptional = stall % 6 == 0;
+        if (!exceptional) {
+            int info[2];
+            if ((rc = small(ihi - ns + 1, ihi, dsh, info)) != EIGSOL_OK) break;   // shifts written to dsh
+            if (info[0]) exceptional = true;
+        }
+        if (exceptional) {
+            for (int b = 0; b < nb; ++b) {
+                const cplx d = ds[ihi - b];
+                const double sc = cabs1_h(ds[n + ihi - b]) + cabs1_h(d) * 1e-3 + 1e-300;
+                sh[2 * b] = cplx{d.re + 0.75 * sc, d.im};
+                sh[2 * b + 1] = cplx{d.re - 0.75 * sc, d.im};
+            }
+            if (hipMemcpyAsync(dsh, sh.data(), ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
+                rc = fail(EIGSOL_E_HIP, "complex QR: shift upload");
+                break;
+            }
+        }
+        // chase the chain of nb bulges down [l, ihi] through successive windows
+        const int T = (ihi - 1 - l) + 3 * (nb - 1) + 1;
+        int t0 = 0;
+        while (t0 < T && rc == EIGSOL_OK) {
+            int s = t0 <= 3 * (nb - 1) ? std::max(0, l - 1) : std::max(0, l + t0 - 3 * (nb - 1) - 1);
+            const int e = std::min(s + dev::kZWin, ihi + 1);
+            const int kmax = (e == ihi + 1) ? ihi - 1 : e - 4;
+            int t1 = t0;
+            while (t1 < T) {
+                const int blead = std::max(0, (l + t1 - (ihi - 1) + 2) / 3);   // first bulge not past ihi-1
+                if (blead >= nb) { t1 = T; break; }
+                if (l + t1 - 3 * blead > kmax) break;
+                ++t1;
+            }
+            if (t1 <= t0) { rc = fail(EIGSOL_E_SOLVER, "complex QR: window did not advance (internal error)"); break; }
+            dev::ZChaseArgs ca{H, (int64_t)n, l, ihi, s, e, t0, t1, nb, dsh, dU};
+            hipLaunchKernelGGL(dev::zchase_kernel, dim3(1), dim3(1024), 0, st, ca);
+            const int W = e - s;
+            if (e <= ihi)
+                hipLaunchKernelGGL(dev::zwin_gemm_kernel<true>, dim3((ihi + 1 - e + 63) / 64), dim3(256), 0, st, H,
+                                   (int64_t)n, s, W, (int64_t)e, (int64_t)ihi + 1, (const cplx*)dU);
+            if (s > l)
+                hipLaunchKernelGGL(dev::zwin_gemm_kernel<false>, dim3((s - l + 63) / 64), dim3(256), 0, st, H,
+                                   (int64_t)n, s, W, (int64_t)l, (int64_t)s, (const cplx*)dU);
+            t0 = t1;
+        }
+        if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "complex QR: launch"); break; }
+        if ((rc = scan()) != EIGSOL_OK) break;
+        for (int k = ihi; k > l; --k)
+            if (cabs1_h(ds[n + k]) <= eps * (cabs1_h(ds[k - 1]) + cabs1_h(ds[k]))) {
+                sweeps = std::max(sweeps, stall);
+                stall = 0;
+                break;
+            }
+    }
+    if (rc == EIGSOL_OK) {
+        if (hipMemcpyAsync(w_host, dw, n * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "complex QR: download");
+    }
+    for (void* p : {(void*)dw, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo})
+        if (p) (void)hipFree(p);
+    *sweeps_out = std::max(1, sweeps);
+    *fail_out = failed;
+    return rc;
+}
+
+}  // namespace eigsol

@@ -361,7 +361,7 @@ TEST(QREigenvaluesDenseTest, Real2x2BothVariantsAndComplex) {
 
 // ---------------------------------------------------------------- single precision (promoted)
 // ScalarConcept admits float and std::complex<float> (types.hpp:28-30): they run on the fp64
-// kernels (promoted on the host, rounded back); long double has no device path.
+// kernels (promoted on the host, rounded back).
 TEST(SinglePrecision, PowerShiftedSolveAndQR) {
     EigSol::Matrix::Dense<float> A(2, 2);
     A << 2.0f, 0.0f, 0.0f, 1.0f;
@@ -397,11 +397,51 @@ TEST(SinglePrecision, PowerShiftedSolveAndQR) {
     auto rc = EigSol::powerMethod<std::complex<float>>(Ms, EigSol::SolverOptions{});
     EXPECT_NEAR(std::abs(rc.eigenvalue - std::complex<float>(5.0f, -1.0f)), 0.0f, 1e-4f);
     EXPECT_EQ(Ms.rows(), 2);
-    EigSol::Matrix::Dense<long double> L(1, 1);
-    L << 1.0L;
+}
+
+// long double / std::complex<long double>: on the fp64 kernels (rounded to double on upload,
+// widened back), every entry point of the reference's API
+TEST(WidePrecision, LongDoubleOnFp64Kernels) {
+    using LD = long double;
+    using CLD = std::complex<long double>;
+    EigSol::Matrix::Dense<LD> L(2, 2);
+    L << 2.0L, 0.0L, 0.0L, 1.0L;
     EigSol::Matrix Ml(L);
-    EXPECT_EQ(Ml.rows(), 1);
-    EXPECT_THROW(EigSol::powerMethod<long double>(Ml, EigSol::SolverOptions{}), std::runtime_error);
+    auto r = EigSol::powerMethod<LD>(Ml, EigSol::SolverOptions{});
+    EXPECT_TRUE(r.converged);
+    EXPECT_NEAR(r.eigenvalue, 2.0L, 1e-8L);
+    EigSol::ShiftedSolverOptions<LD> so(0.9L, 1000, 1e-12);
+    auto rs = EigSol::shiftedInversePowerMethod<LD>(Ml, so);
+    EXPECT_TRUE(rs.converged);
+    EXPECT_NEAR(rs.eigenvalue, 1.0L, 1e-10L);
+    EigSol::Vector<LD> b(2);
+    b << 4.0L, 2.0L;
+    auto x = EigSol::solve_shifted<LD>(Ml, 0.5L, b);
+    EXPECT_NEAR(x(0), 4.0L / 1.5L, 1e-14L);
+    EXPECT_NEAR(x(1), 4.0L, 1e-14L);
+    EigSol::Matrix::Dense<LD> B(2, 2);
+    B << 2.0L, 1.0L, 1.0L, 2.0L;
+    auto q = EigSol::qr_eigenvalues<LD>(EigSol::Matrix(B), EigSol::SolverOptions{1000, 1e-12});
+    EXPECT_TRUE(q.converged);
+    EXPECT_EQ(q.iterations, 25);   // the reference iteration (qr_algorithms_test.cpp): same count
+    auto H = EigSol::to_hessenberg<LD>(EigSol::Matrix(B));
+    EXPECT_EQ(H.rows(), 2);
+    EigSol::Matrix::Sparse<CLD> Sc(3, 3);
+    Sc.insert(0, 0) = CLD(1.0L, 3.0L);
+    Sc.insert(0, 1) = CLD(3.0L, 5.0L);
+    Sc.insert(1, 1) = CLD(5.0L, -1.0L);
+    Sc.insert(2, 2) = CLD(2.0L, 4.0L);
+    EigSol::Matrix Ms(Sc);
+    auto rc = EigSol::powerMethod<CLD>(Ms, EigSol::SolverOptions{});
+    EXPECT_NEAR(std::abs(rc.eigenvalue - CLD(5.0L, -1.0L)), 0.0L, 1e-8L);
+    EigSol::ShiftedSolverOptions<CLD> sc(CLD(2.1L, 3.9L), 1000, 1e-12);
+    auto rsc = EigSol::shiftedInversePowerMethod<CLD>(Ms, sc);
+    EXPECT_NEAR(std::abs(rsc.eigenvalue - CLD(2.0L, 4.0L)), 0.0L, 1e-10L);
+    EigSol::Matrix::Dense<CLD> Dc(2, 2);
+    Dc << CLD(1, 1), CLD(2, 0), CLD(0, 0), CLD(3, -1);
+    auto qc = EigSol::qr_eigenvalues<CLD>(EigSol::Matrix(Dc), EigSol::SolverOptions{}, EigSol::QRVariant::Francis);
+    EXPECT_TRUE(qc.converged);
+    EXPECT_EQ(qc.eigenvalues_complex.size(), 2u);
 }
 
 // ---------------------------------------------------------------- reference caller shapes

@@ -189,6 +189,11 @@ def main():
     A = rng.standard_normal((512, 512))
     np.save(os.path.join(HERE, "qr512_matrix_seed.npy"), np.array([512], dtype=np.int64))
     np.save(os.path.join(HERE, "qr512_eigvals.npy"), np.linalg.eigvals(A).astype(np.complex128))
+    # complex QR fixture (n = 1024): LAPACK zgeev eigenvalues of a seeded complex N(0,1) matrix
+    rng = np.random.default_rng(1024)
+    n = 1024
+    A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    np.save(os.path.join(HERE, "qr_c1024_eigvals.npy"), np.linalg.eigvals(A).astype(np.complex128))
     print("golden fixtures written")
 
 

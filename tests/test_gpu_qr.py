@@ -235,3 +235,48 @@ def test_francis_window_boundaries(ctx, n):
     r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-10))
     assert r.converged
     _match(r.eigenvalues_complex, np.linalg.eigvals(A), 1e-9 * np.linalg.norm(A))
+
+
+# ---------------------------------------------------------------- complex Francis (zfrancis.hip)
+# qr_eigenvalues_dense<std::complex<double>> (qr_eigenvalues.hpp:40-108) with complex two-shift
+# bulges in place of the unshifted loop; eigenvalues matched one-to-one against LAPACK zgeev.
+@pytest.mark.parametrize("n", [2, 7, 40, 64, 65, 97, 200])
+def test_complex_francis_small_and_windows(ctx, n):
+    rng = np.random.default_rng(100 + n)
+    A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12))
+    assert r.converged and 1 <= r.iterations <= 1000
+    _match(r.eigenvalues_complex, np.linalg.eigvals(A), 1e-9 * np.linalg.norm(A))
+
+
+def test_complex_francis_1024_fixture(ctx):
+    rng = np.random.default_rng(1024)
+    n = 1024
+    A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12))
+    assert r.converged
+    _match(r.eigenvalues_complex, np.load(os.path.join(HERE, "golden", "qr_c1024_eigvals.npy")),
+           1e-9 * np.linalg.norm(A))
+
+
+def test_complex_francis_structured(ctx):
+    # Hermitian: real spectrum; unitary diagonal similarity of a triangular matrix: its diagonal;
+    # a real matrix as complex: the real path's conjugate pairs
+    rng = np.random.default_rng(8)
+    n = 150
+    B = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    Hm = B + B.conj().T
+    r = E.qr_eigenvalues(ctx, Hm, E.SolverOptions(1000, 1e-12))
+    assert r.converged
+    _match(r.eigenvalues_complex, np.linalg.eigvalsh(Hm), 1e-9 * np.linalg.norm(Hm))
+    T = np.triu(B)
+    r = E.qr_eigenvalues(ctx, T, E.SolverOptions(1000, 1e-12))
+    _match(r.eigenvalues_complex, np.diag(T), 1e-9 * np.linalg.norm(T))
+    R = rng.standard_normal((n, n))
+    r = E.qr_eigenvalues(ctx, R.astype(np.complex128), E.SolverOptions(1000, 1e-12))
+    _match(r.eigenvalues_complex, np.linalg.eigvals(R), 1e-9 * np.linalg.norm(R))
+    Z = np.zeros((80, 80), np.complex128)
+    r = E.qr_eigenvalues(ctx, Z, E.SolverOptions(1000, 1e-12))
+    assert r.converged and np.all(r.eigenvalues_complex == 0)
+    r = E.qr_eigenvalues(ctx, 1e-200 * B, E.SolverOptions(1000, 1e-12))
+    _match(r.eigenvalues_complex * 1e200, np.linalg.eigvals(B), 1e-9 * np.linalg.norm(B))
