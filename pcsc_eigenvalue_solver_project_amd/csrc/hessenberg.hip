@@ -194,7 +194,10 @@ __global__ __launch_bounds__(256) void hess_y(int n, int i, int nch, const doubl
 //   P3  reflector (every block, redundantly, from the reduced scalars); v and the reduced column
 //       for own rows; partials of t = V^T v
 //   P4  GEMV y = A(:, j+1:n) v for own rows (v staged in LDS), Y(:, i) and the T column
-// (P4 -> the next P1 needs no barrier: P1 reads only own rows and V(j+1, 0:i), published in P3).
+// (P4 -> the next P1 needs no barrier: P1 reads only own rows and V(j+1, 0:i), published in P3.
+// The block partials are double-buffered for the same reason: a block that has finished P4 writes
+// the next column's P1 partials while a slower block may still be gathering P3's, so P1/P2 and
+// P3/P4 use separate halves of `part`.)
 // Everything another block reads is written with agent-scope (sc1) stores and read with sc1 loads,
 // so no L2 writeback/invalidate is needed; partial sums are combined in block order
 // (deterministic).  The barrier spins are bounded: on expiry the kernel sets an error word and
@@ -219,7 +222,7 @@ struct CoopArgs {
     double* V;
     double* Y;
     double* T;
-    double* part;       // [G][kPanel]
+    double* part;       // [2][G][kPanel]: P1 -> P2 partials in the first half, P3 -> P4 in the second
     double* tpart;      // [G]
     double* x0;         // a(j+1)
     unsigned* bar;      // barrier counter (zeroed by the host before the launch)
@@ -372,13 +375,13 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
                 if (r < r1) p += a.V[r + (int64_t)c * n] * xs[lane + 64 * q];
             }
             p = wave_sum(p);
-            if (lane == 0) st_agent(&a.part[blockIdx.x * kPanel + c], p);
+            if (lane == 0) st_agent(&a.part[(G + blockIdx.x) * kPanel + c], p);
         }
         grid_barrier(a.bar, target, a.err);
         // ---------------- P4
         for (int r = tid; r < n; r += kCoopThreads) vsh[r] = sk ? 0.0 : ld_agent(&a.V[r + (int64_t)i * n]);
         __syncthreads();
-        gather(a.part, i, sv);
+        gather(a.part + (size_t)G * kPanel, i, sv);
         if (sk && tid < i) sv[tid] = 0.0;
         __syncthreads();
         double yacc[kCoopRowsPerLane];
@@ -661,7 +664,7 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
     unsigned* bar = nullptr;
     int* err = nullptr;
     if (coop) {
-        EIGSOL_HIP(hipMalloc(&part, dev::kCoopBlocks * NB * sizeof(double)));
+        EIGSOL_HIP(hipMalloc(&part, 2 * dev::kCoopBlocks * NB * sizeof(double)));
         EIGSOL_HIP(hipMalloc(&tpart, dev::kCoopBlocks * sizeof(double)));
         EIGSOL_HIP(hipMalloc(&x0s, 64));
         EIGSOL_HIP(hipMalloc(&bar, 64));
