@@ -1737,7 +1737,13 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         const void* tk = !f->tail_chunks ? slice_kernel_ptr<S>(f->slice_b, iter)
                          : iter ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>)
                                 : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, false>);
-        EIGSOL_HIP(hipLaunchCooperativeKernel(tk, dim3(f->grid), dim3(dev::kThreads), kargs, 0, st));
+        // EIGSOL_TRSV_NO_COOP=1: the same kernel through an ordinary launch, for profiling only
+        // (rocprofv3 7.2 segfaults in its exit-time finaliser after any cooperative launch,
+        // tools/coop_prof_repro.hip); the grid is one residency round, so on an otherwise idle
+        // device every wave is resident anyway
+        static const bool no_coop = std::getenv("EIGSOL_TRSV_NO_COOP") != nullptr;
+        if (no_coop) EIGSOL_HIP(hipLaunchKernel(tk, dim3(f->grid), dim3(dev::kThreads), kargs, 0, st));
+        else EIGSOL_HIP(hipLaunchCooperativeKernel(tk, dim3(f->grid), dim3(dev::kThreads), kargs, 0, st));
         if (iter)
             hipLaunchKernelGGL((dev::shift_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a, parity);
     } else if constexpr (!kDenseLU<S>) {
