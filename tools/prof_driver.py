@@ -31,6 +31,16 @@ if args.workload == "config5":
     print("done", s.kernel_info())
     s.close(); A.close(); ctx.close()
     sys.exit(0)
+if args.workload == "qrc1024":
+    import numpy as np
+    n = 1024
+    rng = np.random.default_rng(1024)
+    a = np.asfortranarray(rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n)))
+    ctx = E.Context(0)
+    r = E.qr_eigenvalues(ctx, a, E.SolverOptions(1000, 1e-12))
+    print("done", r.iterations, r.converged)
+    ctx.close()
+    sys.exit(0)
 if args.workload == "qr4096":
     import numpy as np
     n = 4096
