@@ -322,62 +322,64 @@ __global__ __launch_bounds__(1024) void zchase_kernel(ZChaseArgs a) {
     }
 }
 
-// Delayed window updates.  left: H(s:s+W, c0:c0+64) <- U^H H(s:s+W, c0:c0+64) (columns [lo, hi));
-// right: H(r0:r0+64, s:s+W) <- H(r0:r0+64, s:s+W) U (rows [lo, hi)).  64 output columns (rows)
-// per workgroup, U and the panel staged in LDS; each thread owns one column (row) and 16 rows
-// (columns) of the output.
+// Delayed window updates.  left: H(s:s+W, cols) <- U^H H(s:s+W, cols) for the columns [lo, hi);
+// right: H(rows, s:s+W) <- H(rows, s:s+W) U for the rows [lo, hi).  32 output columns (rows) per
+// workgroup of 128 threads; U and the panel staged in LDS, each thread a 4 x 4 register tile of
+// the output (8 LDS reads per 16 complex multiply-adds; the LDS pitches keep a wave's 16-byte
+// reads on distinct banks).
+constexpr int kZG = 32;   // output columns (left) / rows (right) per workgroup
 template <bool kLeft>
-__global__ __launch_bounds__(256) void zwin_gemm_kernel(cplx* H, int64_t n, int s, int W, int64_t lo, int64_t hi,
+__global__ __launch_bounds__(128) void zwin_gemm_kernel(cplx* H, int64_t n, int s, int W, int64_t lo, int64_t hi,
                                                         const cplx* U) {
-    __shared__ cplx us[kZWin * kZWin];
-    __shared__ cplx xs[kZWin * kZWin];
+    constexpr int LU = kZWin + 1;    // U pitch
+    constexpr int LX = kZWin + 1;    // panel pitch
+    __shared__ cplx us[kZWin * LU];
+    __shared__ cplx xs[kZG * LX];
     const int tid = threadIdx.x;
-    const int64_t b0 = lo + (int64_t)blockIdx.x * 64;
-    const int nb = (int)std::min<int64_t>(64, hi - b0);
-    for (int idx = tid; idx < W * W; idx += 256) us[idx] = U[idx];
-    for (int idx = tid; idx < W * 64; idx += 256) {
-        if (kLeft) {   // xs[i + j W] = H(s + i, b0 + j)
-            const int i = idx % W, j = idx / W;
-            xs[idx] = j < nb ? H[(s + i) + (b0 + j) * n] : cplx{0.0, 0.0};
-        } else {       // xs[i + j 64] = H(b0 + i, s + j)
-            const int i = idx % 64, j = idx / 64;
-            xs[idx] = i < nb ? H[(b0 + i) + (int64_t)(s + j) * n] : cplx{0.0, 0.0};
+    const int64_t b0 = lo + (int64_t)blockIdx.x * kZG;
+    const int nb = (int)std::min<int64_t>(kZG, hi - b0);
+    for (int idx = tid; idx < W * W; idx += 128) us[(idx % W) + (idx / W) * LU] = U[idx];
+    if (kLeft) {   // xs[r + c LX] = H(s + r, b0 + c)
+        for (int idx = tid; idx < W * kZG; idx += 128) {
+            const int r = idx % W, c = idx / W;
+            xs[r + c * LX] = c < nb ? H[(s + r) + (b0 + c) * n] : cplx{0.0, 0.0};
+        }
+    } else {       // xs[r + c LX] = H(b0 + c, s + r)  (row c of the block, transposed)
+        for (int idx = tid; idx < W * kZG; idx += 128) {
+            const int c = idx % kZG, r = idx / kZG;
+            xs[r + c * LX] = c < nb ? H[(b0 + c) + (int64_t)(s + r) * n] : cplx{0.0, 0.0};
         }
     }
     __syncthreads();
-    const int own = tid & 63, grp = tid >> 6;   // 4 groups of 16 outputs
-    cplx acc[16];
+    // output tile: 4 window indices (i0 + 16 a) x 4 block columns/rows (c0 + 8 b)
+    const int i0 = tid & 15, c0 = tid >> 4;   // 16 x 8 threads
+    cplx acc[4][4];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = cplx{0.0, 0.0};
-    if (kLeft) {   // out(i, own) = sum_r conj(U(r, i)) X(r, own), i = grp*16 + q
-        for (int r = 0; r < W; ++r) {
-            const cplx x = xs[r + own * W];
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int i = grp * 16 + q;
-                if (i < W) acc[q] = add(acc[q], cmul_conj(us[r + i * W], x));
-            }
-        }
-        if (own < nb)
-            for (int q = 0; q < 16; ++q) {
-                const int i = grp * 16 + q;
-                if (i < W) H[(s + i) + (b0 + own) * n] = acc[q];
-            }
-    } else {       // out(own, j) = sum_r X(own, r) U(r, j), j = grp*16 + q
-        for (int r = 0; r < W; ++r) {
-            const cplx x = xs[own + r * 64];
+        for (int b = 0; b < 4; ++b) acc[a][b] = cplx{0.0, 0.0};
+    for (int r = 0; r < W; ++r) {
+        cplx uu[4], xx[4];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int j = grp * 16 + q;
-                if (j < W) acc[q] = add(acc[q], mul(x, us[r + j * W]));
-            }
-        }
-        if (own < nb)
-            for (int q = 0; q < 16; ++q) {
-                const int j = grp * 16 + q;
-                if (j < W) H[(b0 + own) + (int64_t)(s + j) * n] = acc[q];
-            }
+        for (int a = 0; a < 4; ++a) uu[a] = kLeft ? us[r + (i0 + 16 * a) * LU] : us[r + (i0 + 16 * a) * LU];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) xx[b] = xs[r + (c0 + 8 * b) * LX];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                acc[a][b] = add(acc[a][b], kLeft ? cmul_conj(uu[a], xx[b]) : mul(xx[b], uu[a]));
     }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int i = i0 + 16 * a, c = c0 + 8 * b;
+            if (i < W && c < nb) {
+                if (kLeft) H[(s + i) + (b0 + c) * n] = acc[a][b];          // (U^H X)(i, c)
+                else H[(b0 + c) + (int64_t)(s + i) * n] = acc[a][b];       // (X U)(c, i)
+            }
+        }
 }
 
 __global__ void zdiag_sub_kernel(const cplx* H, int64_t n, int ihi, cplx* out) {
@@ -439,7 +441,12 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             continue;
         }
         if (++stall > max_stall) { failed = 1; sweeps = std::max(sweeps, stall); break; }
-        int nb = std::min(dev::kZMaxBulges, std::max(1, N / 16));
+        // at most 8 bulges: the chain (3 nb rows) must leave the 64-row window room to advance
+        static const int max_nb = [] {
+            const char* e = std::getenv("EIGSOL_ZQR_NB");
+            return e ? std::max(1, std::min(dev::kZMaxBulges, std::atoi(e))) : 8;
+        }();
+        int nb = std::min(max_nb, std::max(1, N / 16));
         const int ns = 2 * nb;
         std::vector<cplx> sh(ns);
         bool exceptional = stall % 6 == 0;
@@ -479,10 +486,10 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             hipLaunchKernelGGL(dev::zchase_kernel, dim3(1), dim3(1024), 0, st, ca);
             const int W = e - s;
             if (e <= ihi)
-                hipLaunchKernelGGL(dev::zwin_gemm_kernel<true>, dim3((ihi + 1 - e + 63) / 64), dim3(256), 0, st, H,
+                hipLaunchKernelGGL(dev::zwin_gemm_kernel<true>, dim3((ihi + 1 - e + dev::kZG - 1) / dev::kZG), dim3(128), 0, st, H,
                                    (int64_t)n, s, W, (int64_t)e, (int64_t)ihi + 1, (const cplx*)dU);
             if (s > l)
-                hipLaunchKernelGGL(dev::zwin_gemm_kernel<false>, dim3((s - l + 63) / 64), dim3(256), 0, st, H,
+                hipLaunchKernelGGL(dev::zwin_gemm_kernel<false>, dim3((s - l + dev::kZG - 1) / dev::kZG), dim3(128), 0, st, H,
                                    (int64_t)n, s, W, (int64_t)l, (int64_t)s, (const cplx*)dU);
             t0 = t1;
         }
