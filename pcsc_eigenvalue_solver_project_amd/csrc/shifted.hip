@@ -56,6 +56,12 @@ struct ShiftFactor {
     void* hpiv = nullptr;
     int2* passes = nullptr;       // head passes {first position, end | barrier}
     int32_t npass = 0, hpos = 0, hlevels = 0;
+    int wave_head = 1;            // head kernel: 1 one-wave (sptrsv_whead_kernel), 0 one workgroup
+    void* wval = nullptr;         // one-wave head, pass-major (see sptrsv_whead_kernel)
+    int32_t* wcol = nullptr;
+    void* wrp = nullptr;
+    int32_t* wdst = nullptr;
+    int32_t nwpass = 0;
     int red_grid = 0;             // blocks of the partials reduction
     int2* smeta = nullptr;        // tail slices (see sptrsv_slice_kernel)
     int32_t* trow = nullptr;
@@ -110,6 +116,11 @@ struct TriArgs {
     const S* hpiv;         // pivot of group g of pass q at q * 64 + g
     const int2* passes;    // head passes
     int32_t npass, hpos;   // head passes, head positions
+    const S* wval;         // one-wave head: entry k of lane l of pass q at (q * 4 + k) * 64 + l
+    const int32_t* wcol;   // its LDS column position (padding: the zero slot hpos)
+    const S* wrp;          // 1 / pivot of row group g of pass q at q * 16 + g
+    const int32_t* wdst;   // LDS position that group g of pass q solves (-1: none)
+    int32_t nwpass;
     const int2* smeta;     // tail slices: {entry offset, entries per lane}
     const int32_t* trow;   // row of lane l of slice s at s * 64 + l (-1: padding)
     const S* tpiv;
@@ -330,6 +341,116 @@ __global__ __launch_bounds__(kHeadThreads) void sptrsv_head_kernel(TriArgs<S> a,
     __syncthreads();
     // publish: the tail kernel (next in stream order) reads these through z
     for (int p = tid; p < a.hpos; p += kHeadThreads) {
+        const int i = a.order[p];
+        if (i < 0) continue;
+        const S yi = sanitize(zl[p]);
+        a.zcur[i] = yi;
+        yout[i] = yi;
+        a.znext[i] = sentinel<S>();
+    }
+}
+
+// ---- head, one-wave form.  The narrow levels are a chain of short dependent steps; with a
+// workgroup, every pass costs a barrier and the instruction issue of 16 waves (~0.6 us for 64
+// rows).  Here ONE wave solves them with no barrier at all (a wave's LDS operations complete in
+// issue order): 4 lanes per row, 4 entries per lane, 16 rows per pass, and the row's pivot applied
+// as a multiplication by its reciprocal (computed at factor time).  A pass never spans two levels,
+// so the rows of a pass are independent; the entries of the next kWHeadDepth passes are in flight
+// in a register ring.  The other waves only help to stage the right-hand side into LDS and to
+// publish the solved values.
+constexpr int kWHeadThreads = 256;
+constexpr int kWHeadDepth = 8;
+constexpr int kWHeadRows = 16;   // rows per pass
+constexpr int kDppQuad2301 = 0x4E;
+__device__ __forceinline__ double quad_sum(double v) {
+    v += dpp_f64<kDppQuad1032>(v);
+    return v + dpp_f64<kDppQuad2301>(v);
+}
+__device__ __forceinline__ float quad_sum(float v) {
+    v += dpp_f32<kDppQuad1032>(v);
+    return v + dpp_f32<kDppQuad2301>(v);
+}
+__device__ __forceinline__ cplx quad_sum(cplx v) { return cplx{quad_sum(v.re), quad_sum(v.im)}; }
+__device__ __forceinline__ cplxf quad_sum(cplxf v) { return cplxf{quad_sum(v.re), quad_sum(v.im)}; }
+
+template <class S, bool kIter>
+__global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> a, int parity) {
+    extern __shared__ __align__(16) unsigned char head_lds[];
+    S* zl = reinterpret_cast<S*>(head_lds);
+    __shared__ Prologue pro;
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kIter) {
+        shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // the tail kernel resets z
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.b_plain;
+        yout = a.y_plain;
+    }
+    const int tid = threadIdx.x;
+    // right-hand side of the head positions into LDS: 8 positions per thread per round, every
+    // load of a round issued before the first is consumed
+    constexpr int kB = 8;
+    for (int p0 = 0; p0 < a.hpos; p0 += kWHeadThreads * kB) {
+        int ii[kB];
+        S bb[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int p = p0 + u * kWHeadThreads + tid;
+            ii[u] = p < a.hpos ? a.order[p] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) bb[u] = xin[ii[u] >= 0 ? ii[u] : 0];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int p = p0 + u * kWHeadThreads + tid;
+            if (p < a.hpos) {
+                if constexpr (kIter) zl[p] = scale_in(bb[u], nrm);
+                else zl[p] = bb[u];
+            }
+        }
+    }
+    if (tid == 0) zl[a.hpos] = s_zero<S>();
+    __syncthreads();
+    if (tid < 64) {
+        const int lane = tid, grp = lane >> 2, slot = lane & 3;
+        const int nw = a.nwpass;
+        S rv[kWHeadDepth][4], rq[kWHeadDepth];
+        int rc[kWHeadDepth][4], rd[kWHeadDepth];
+        auto load = [&](int q, S* v, int* c, S& r, int& d) {
+            const uint32_t qq = (uint32_t)(q < nw ? q : 0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t e = (qq * 4u + (uint32_t)k) * 64u + (uint32_t)lane;
+                v[k] = ldg(a.wval, e);   // temporal loads: the head's data stays cached between solves
+                c[k] = (int)ldg(a.wcol, e);
+            }
+            r = ldg(a.wrp, qq * (uint32_t)kWHeadRows + (uint32_t)grp);
+            d = q < nw ? (int)ldg(a.wdst, qq * (uint32_t)kWHeadRows + (uint32_t)grp) : -1;
+        };
+#pragma unroll
+        for (int u = 0; u < kWHeadDepth; ++u) load(u, rv[u], rc[u], rq[u], rd[u]);
+        for (int q0 = 0; q0 < nw; q0 += kWHeadDepth) {
+#pragma unroll
+            for (int u = 0; u < kWHeadDepth; ++u) {   // straight line: nw is a multiple of the depth
+                S acc = mul(rv[u][0], zl[rc[u][0]]);
+#pragma unroll
+                for (int k = 1; k < 4; ++k) acc = add(acc, mul(rv[u][k], zl[rc[u][k]]));
+                acc = quad_sum(acc);
+                const int d = rd[u];
+                if (slot == 0 && d >= 0) zl[d] = mul(sub(zl[d], acc), rq[u]);
+                asm volatile("" ::: "memory");   // this pass's store precedes the next pass's reads
+                load(q0 + u + kWHeadDepth, rv[u], rc[u], rq[u], rd[u]);
+            }
+        }
+    }
+    __syncthreads();
+    // publish: the tail kernel (next in stream order) reads these through z
+    for (int p = tid; p < a.hpos; p += kWHeadThreads) {
         const int i = a.order[p];
         if (i < 0) continue;
         const S yi = sanitize(zl[p]);
@@ -1101,6 +1222,7 @@ static void shift_free(ShiftFactor* f) {
     hipStreamSynchronize(f->ctx->stream);
     for (void* p : {(void*)f->order, f->z[0], f->z[1],
                     f->hval, (void*)f->hcol, f->hpiv, (void*)f->passes, (void*)f->smeta, (void*)f->trow,
+                    f->wval, (void*)f->wcol, f->wrp, (void*)f->wdst,
                     f->tpiv, (void*)f->tcol, f->tval, (void*)f->porder, (void*)f->pptr, (void*)f->pcol, f->pval,
                     f->ppiv,
                     (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
@@ -1269,9 +1391,12 @@ static void level_order(const std::vector<int32_t>& rp, const std::vector<int32_
 // the whole GPU).  EIGSOL_TRSV_HEAD_ROWS / EIGSOL_TRSV_HEAD_WIDTH override (0 rows: no head).
 template <class S>
 static int32_t head_levels(const std::vector<int64_t>& lstart, const std::vector<int64_t>& lcount,
-                           const std::vector<int32_t>& lmaxlen, int32_t nlevels) {
+                           const std::vector<int32_t>& lmaxlen, int32_t nlevels, bool wave_head) {
     int64_t cap = (int64_t)(150 * 1024) / (int64_t)sizeof(S);
-    int64_t width = 256;   // config 5: 256 -> 0.861 ms, 1024 -> 0.872 ms per solve
+    // widest head level.  One-workgroup head: config 5 256 -> 0.861 ms, 1024 -> 0.872 ms per solve.
+    // One-wave head (16 rows per pass, ~0.26 us a pass): 64 -> 0.833 ms, 256 -> 0.879 ms (a wider
+    // level is cheaper in the tail, ~1.7 us a level)
+    int64_t width = wave_head ? 64 : 256;
     if (const char* e = std::getenv("EIGSOL_TRSV_HEAD_ROWS")) cap = std::min<int64_t>(cap, std::atoll(e));
     if (const char* e = std::getenv("EIGSOL_TRSV_HEAD_WIDTH")) width = std::atoll(e);
     int32_t h = 0;
@@ -1421,7 +1546,8 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
     for (int32_t l = 0; l < f->nlevels; ++l)
         for (int64_t p = lstart[l]; p < lstart[l] + lcount[l]; ++p)
             lmaxlen[l] = std::max(lmaxlen[l], orp[order[p] + 1] - orp[order[p]]);
-    f->hlevels = head_levels<S>(lstart, lcount, lmaxlen, f->nlevels);
+    if (const char* e = std::getenv("EIGSOL_TRSV_HEAD")) f->wave_head = std::strcmp(e, "block") ? 1 : 0;
+    f->hlevels = head_levels<S>(lstart, lcount, lmaxlen, f->nlevels, f->wave_head != 0);
     if (const char* e = std::getenv("EIGSOL_TRSV_POLL_FAST")) f->poll_fast = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("EIGSOL_TRSV_POLL_MODE")) f->poll_mode = std::atoi(e);
     f->hpos = (int32_t)lstart[f->hlevels];
@@ -1456,6 +1582,52 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
                 hval[g * dev::kRowLanes + (e - orp[i])] = ov[e];
             }
         }
+    }
+    // one-wave head (see sptrsv_whead_kernel): passes of <= 16 rows inside a level, 4 lanes per row,
+    // entry idx of a row at lane 4 g + idx / 4, slot idx % 4; reciprocal pivots.
+    // EIGSOL_TRSV_HEAD=block selects the one-workgroup head.
+    std::vector<S> wval, wrp;
+    std::vector<int32_t> wcol, wdst;
+    if (f->hpos > 0) {
+        auto recip = [](S p) -> S {
+            if constexpr (is_real_v<S>) return (S)1 / p;
+            else {
+                const double d = (double)p.re * (double)p.re + (double)p.im * (double)p.im;
+                S r;
+                r.re = (decltype(p.re))((double)p.re / d);
+                r.im = (decltype(p.im))(-(double)p.im / d);
+                return r;
+            }
+        };
+        int32_t q = 0;
+        for (int32_t l = 0; l < f->hlevels; ++l) {
+            const int32_t p0 = (int32_t)lstart[l], p1 = (int32_t)(lstart[l] + lcount[l]);
+            for (int32_t p = p0; p < p1; p += dev::kWHeadRows, ++q) {
+                wval.resize((size_t)(q + 1) * 256, s_zero<S>());
+                wcol.resize((size_t)(q + 1) * 256, f->hpos);
+                wrp.resize((size_t)(q + 1) * dev::kWHeadRows, make_sigma<S>(1.0, 0.0));
+                wdst.resize((size_t)(q + 1) * dev::kWHeadRows, -1);
+                for (int32_t u = 0; u < std::min(dev::kWHeadRows, p1 - p); ++u) {
+                    const int32_t i = order[p + u];
+                    wrp[(size_t)q * dev::kWHeadRows + u] = recip(pv[i]);
+                    wdst[(size_t)q * dev::kWHeadRows + u] = p + u;
+                    for (int32_t e = orp[i]; e < orp[i + 1]; ++e) {
+                        const int32_t idx = e - orp[i];
+                        const size_t slot = ((size_t)q * 4 + (size_t)(idx % 4)) * 64 + (size_t)(4 * u + idx / 4);
+                        wcol[slot] = rowpos[oci[e]];
+                        wval[slot] = ov[e];
+                    }
+                }
+            }
+        }
+        while (q % dev::kWHeadDepth) {   // empty passes: the ring loop is straight-line code
+            ++q;
+            wval.resize((size_t)q * 256, s_zero<S>());
+            wcol.resize((size_t)q * 256, f->hpos);
+            wrp.resize((size_t)q * dev::kWHeadRows, make_sigma<S>(1.0, 0.0));
+            wdst.resize((size_t)q * dev::kWHeadRows, -1);
+        }
+        f->nwpass = q;
     }
     // tail variant: slices (row per lane) for few, very wide levels; chunks (16 lanes per row)
     // otherwise.  EIGSOL_TRSV_TAIL=slice|chunk overrides.
@@ -1579,6 +1751,10 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
     if (rc == EIGSOL_OK) rc = up_(&f->hval, hval.data(), hval.size() * sizeof(S));
     if (rc == EIGSOL_OK) rc = up_(&f->hpiv, hpiv.data(), hpiv.size() * sizeof(S));
     if (rc == EIGSOL_OK) rc = up_((void**)&f->passes, passes.data(), passes.size() * sizeof(int2));
+    if (rc == EIGSOL_OK) rc = up_(&f->wval, wval.data(), wval.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->wcol, wcol.data(), wcol.size() * 4);
+    if (rc == EIGSOL_OK) rc = up_(&f->wrp, wrp.data(), wrp.size() * sizeof(S));
+    if (rc == EIGSOL_OK) rc = up_((void**)&f->wdst, wdst.data(), wdst.size() * 4);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->smeta, smeta.data(), smeta.size() * sizeof(int2));
     if (rc == EIGSOL_OK) rc = up_((void**)&f->trow, trow.data(), trow.size() * 4);
     if (rc == EIGSOL_OK) rc = up_(&f->tpiv, tpiv.data(), tpiv.size() * sizeof(S));
@@ -1711,8 +1887,21 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.hpos = f->hpos;
         a.poll_fast = f->poll_fast;
         a.poll_mode = f->poll_mode;
+        a.wval = static_cast<const S*>(f->wval);
+        a.wcol = f->wcol;
+        a.wrp = static_cast<const S*>(f->wrp);
+        a.wdst = f->wdst;
+        a.nwpass = f->nwpass;
+        if (f->hpos > 0 && f->wave_head) {
+            const size_t wl = (size_t)(f->hpos + 1) * sizeof(S);
+            const void* hk = iter ? reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, true>)
+                                  : reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, false>);
+            EIGSOL_HIP(hipFuncSetAttribute(hk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wl));
+            if (iter) hipLaunchKernelGGL((dev::sptrsv_whead_kernel<S, true>), dim3(1), dim3(dev::kWHeadThreads), wl, st, a, parity);
+            else hipLaunchKernelGGL((dev::sptrsv_whead_kernel<S, false>), dim3(1), dim3(dev::kWHeadThreads), wl, st, a, parity);
+        }
         const size_t hl = (size_t)(f->hpos + 1) * sizeof(S) + (size_t)f->npass * sizeof(int2);
-        if (f->hpos > 0) {
+        if (f->hpos > 0 && !f->wave_head) {
             const void* hk = iter ? reinterpret_cast<const void*>(dev::sptrsv_head_kernel<S, true>)
                                   : reinterpret_cast<const void*>(dev::sptrsv_head_kernel<S, false>);
             EIGSOL_HIP(hipFuncSetAttribute(hk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl));
