@@ -32,11 +32,17 @@ def ctx():
     c.close()
 
 
-def _power_parity(res, ref):
+def _power_parity(res, ref, tol):
+    """same λ to 1e-10, same iteration count; ±1 only when the oracle's last Δλ sits at
+    the stopping tolerance (a borderline stop decided by the last bits of the norms)."""
     lam, lr = res.eigenvalue, ref["eigenvalue"]
     assert abs(lam - lr) <= 1e-10 * (1 + abs(lr)), (lam, lr)
     assert res.converged == ref["converged"]
-    assert abs(res.iterations - ref["iterations"]) <= 1, (res.iterations, ref["iterations"])
+    if res.iterations != ref["iterations"]:
+        assert abs(res.iterations - ref["iterations"]) == 1, (res.iterations, ref["iterations"])
+        tr = ref["trace"]
+        k = min(res.iterations, ref["iterations"]) - 1
+        assert abs(tr[k] - tr[k - 1]) <= 10 * tol * (1 + abs(tr[k]))
     assert abs(np.vdot(res.eigenvector, ref["eigenvector"])) >= 1 - 1e-10
 
 
@@ -51,9 +57,9 @@ def test_config4_band10m_spmv_bitwise_and_power(ctx):
     assert np.array_equal(y, O.spmv_csc(cp, ri, vv, x, n))
     x0 = S.start_vector(n)
     res = E.power_method(A, E.SolverOptions(100, 1e-10), x0)
-    ref = O.power_csc(cp, ri, vv, x0, 100, 1e-10)
+    ref = O.power_csc(cp, ri, vv, x0, 100, 1e-10, want_trace=True)
     assert ref["converged"]
-    _power_parity(res, ref)
+    _power_parity(res, ref, 1e-10)
     A.close()
 
 
@@ -64,9 +70,9 @@ def test_config3_uniform1m_power(ctx):
     x0 = S.start_vector(n)
     res = E.power_method(A, E.SolverOptions(200, 1e-10), x0)
     cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
-    ref = O.power_csc(cp, ri, vv, x0, 200, 1e-10)
+    ref = O.power_csc(cp, ri, vv, x0, 200, 1e-10, want_trace=True)
     assert ref["converged"]
-    _power_parity(res, ref)
+    _power_parity(res, ref, 1e-10)
     A.close()
 
 

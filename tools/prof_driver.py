@@ -31,6 +31,21 @@ if args.workload == "config5":
     print("done", s.kernel_info())
     s.close(); A.close(); ctx.close()
     sys.exit(0)
+if args.workload == "dense16384":
+    # dense power iteration (GEMV) on a 16384^2 f64 matrix (dense_kernel)
+    import numpy as np
+    n = 16384
+    a = np.asfortranarray(np.random.default_rng(3).standard_normal((n, n)))
+    ctx = E.Context(0)
+    D = E.DenseMatrix(ctx, a)
+    del a
+    s = E.PowerSession(D)
+    s.begin(E.SolverOptions(2**31 - 1, -1.0), S.start_vector(n))
+    s.step(args.steps)
+    ctx.synchronize()
+    print("done", s.kernel_info())
+    s.close(); D.close(); ctx.close()
+    sys.exit(0)
 if args.workload == "qrc1024":
     import numpy as np
     n = 1024
