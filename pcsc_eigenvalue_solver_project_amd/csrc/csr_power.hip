@@ -66,6 +66,9 @@ struct CsrArgs {
     const int32_t* scol32;   // gather slices: x-space column
     const uint8_t* slen;     // row lengths (read for ragged slices only)
     int32_t nslices;
+    int64_t seg_val[kMaxSliceSeg];   // element offset of each stream segment (slice meta .z bits 21..24)
+    int64_t seg_c8[kMaxSliceSeg];
+    int64_t seg_c32[kMaxSliceSeg];
     const int4* tile_meta;   // per tile {r0, r1, e0, e1}: short tiles first, then long rows
     const int2* tile_win;    // per short tile: x window [w0, w1] covering its columns and rows
     int32_t ntiles;
@@ -699,6 +702,10 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
     // K = 0 (all rows empty) clamps to entry 0 of the slice: the streams carry one slice of
     // padding past their end, so even an empty last slice loads in bounds
     const int K = max(m.z & 0xff, 1);
+    const int seg = (m.z >> kSliceSegShift) & (kMaxSliceSeg - 1);   // wave-uniform
+    const S* sval = a.sval + a.seg_val[seg];
+    const uint32_t* scol8 = a.scol8 + a.seg_c8[seg];
+    const int32_t* scol32 = a.scol32 + a.seg_c32[seg];
     const uint32_t base = (uint32_t)m.x + (uint32_t)lane;
     R.len = m.z & 0xff;
     if (m.z & 0x100) R.len = a.slen[min(slice * kSliceRows + lane, a.nrows - 1)];
@@ -707,16 +714,16 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
         const uint32_t b2 = ((uint32_t)m.x >> 1) + (uint32_t)lane;
 #pragma unroll
         for (int j = 0; j < SliceRegs<S, KB, kG>::NV; ++j)
-            R.v[j] = ldg_stream(reinterpret_cast<const pair_t<S>*>(a.sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
+            R.v[j] = ldg_stream(reinterpret_cast<const pair_t<S>*>(sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
     } else {
 #pragma unroll
-        for (int u = 0; u < KB; ++u) R.v[u] = ldg_stream(a.sval, base + 64u * (uint32_t)min(u, K - 1));
+        for (int u = 0; u < KB; ++u) R.v[u] = ldg_stream(sval, base + 64u * (uint32_t)min(u, K - 1));
     }
     if (m.y >= 0) {
         const int nw = (K + 3) >> 2;
 #pragma unroll
         for (int g = 0; g < KB / 4; ++g)
-            R.c[g] = ldg_stream(a.scol8, (uint32_t)m.w + 64u * (uint32_t)min(g, nw - 1) + (uint32_t)lane);
+            R.c[g] = ldg_stream(scol8, (uint32_t)m.w + 64u * (uint32_t)min(g, nw - 1) + (uint32_t)lane);
         // the window always holds the slice's own rows (the Rayleigh term reads them)
         const int wl = max((m.z >> 9) & 0x1ff, 1);
         if (kDist && (m.z & kGhostSliceBit)) {
@@ -741,7 +748,7 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
     } else if constexpr (kG) {
 #pragma unroll
         for (int u = 0; u < KB; ++u)
-            R.c[u] = (uint32_t)ldg_stream(a.scol32, (uint32_t)m.w + 64u * (uint32_t)min(u, K - 1) + (uint32_t)lane);
+            R.c[u] = (uint32_t)ldg_stream(scol32, (uint32_t)m.w + 64u * (uint32_t)min(u, K - 1) + (uint32_t)lane);
     }
 }
 
@@ -759,6 +766,10 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
                                               int parity = 0) {
     const int lane = threadIdx.x & 63;
     const int K = mc.z & 0xff;
+    const int seg = (mc.z >> kSliceSegShift) & (kMaxSliceSeg - 1);
+    const S* sval = a.sval + a.seg_val[seg];
+    const uint32_t* scol8 = a.scol8 + a.seg_c8[seg];
+    const int32_t* scol32 = a.scol32 + a.seg_c32[seg];
     const int row = sl * kSliceRows + lane;
     const bool valid = row < a.nrows;
     const int rowc = valid ? row : a.nrows - 1;
@@ -792,10 +803,10 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
             if (u < R.len) sacc = add(sacc, pr);
         }
         for (int k0 = KB; k0 < K; k0 += 4) {       // rows longer than KB entries
-            const uint32_t cw = ldg(a.scol8, (uint32_t)mc.w + 64u * (uint32_t)(k0 >> 2) + (uint32_t)lane);
+            const uint32_t cw = ldg(scol8, (uint32_t)mc.w + 64u * (uint32_t)(k0 >> 2) + (uint32_t)lane);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const S pr = mul(ldg(a.sval, slice_entry<S>((uint32_t)mc.x, min(k0 + u, K - 1), lane)),
+                const S pr = mul(ldg(sval, slice_entry<S>((uint32_t)mc.x, min(k0 + u, K - 1), lane)),
                                  xw[(cw >> (8 * u)) & 0xffu]);
                 if (k0 + u < R.len) sacc = add(sacc, pr);
             }
@@ -822,10 +833,10 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
         }
         for (int k0 = KB; k0 < K; ++k0) {
             const uint32_t q = (uint32_t)lane + 64u * (uint32_t)k0;
-            const uint32_t cc = (uint32_t)ldg(a.scol32, (uint32_t)mc.w + q);
+            const uint32_t cc = (uint32_t)ldg(scol32, (uint32_t)mc.w + q);
             S x = ghost ? ld_x_peer(a, xin, gin, (int)cc) : ldg(xin, cc);
             if constexpr (kPower) x = scale_in(x, nrm);
-            const S pr = mul(ldg(a.sval, slice_entry<S>((uint32_t)mc.x, k0, lane)), x);
+            const S pr = mul(ldg(sval, slice_entry<S>((uint32_t)mc.x, k0, lane)), x);
             if (k0 < R.len) sacc = add(sacc, pr);
         }
         if constexpr (kPower) xi = scale_in(xin[rowc + a.xoff], nrm);
@@ -1154,7 +1165,17 @@ struct SliceLayout {
     std::vector<uint8_t> len;
     int maxk = 0;
     bool any_gather = false;   // some slice's window does not fit: gather instantiation
+    int nseg = 1;              // stream segments (kSliceSegShift): element offsets of their starts
+    int64_t seg_val[kMaxSliceSeg] = {0}, seg_c8[kMaxSliceSeg] = {0}, seg_c32[kMaxSliceSeg] = {0};
 };
+
+// Largest stream segment in bytes (32-bit offsets inside a segment).  EIGSOL_SLICE_SEG_BYTES
+// lowers it so that tests exercise several segments on small matrices.
+static int64_t slice_seg_bytes() {
+    int64_t lim = (int64_t(1) << 32) - (int64_t(1) << 20);
+    if (const char* e = std::getenv("EIGSOL_SLICE_SEG_BYTES")) lim = std::max<int64_t>(1 << 16, std::min<int64_t>(lim, std::atoll(e)));
+    return lim;
+}
 
 static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* values, size_t sb, bool pairs,
                          int64_t nrows, int64_t nnz, int64_t xoff, int64_t xlen, SliceLayout& L) {
@@ -1162,6 +1183,8 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
     const int64_t ns = (nrows + kSliceRows - 1) / kSliceRows;
     int64_t total = 0, ctot8 = 0, ctot32 = 0;
     bool any_ragged = false;
+    const int64_t seg_lim = slice_seg_bytes();
+    int seg = 0;
     L.meta.assign(4 * ns, 0);
     for (int64_t s = 0; s < ns; ++s) {
         const int64_t r0 = s * kSliceRows, r1 = std::min<int64_t>(nrows, r0 + kSliceRows);
@@ -1203,16 +1226,31 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
         }
         any_ragged |= ragged;
         L.maxk = std::max(L.maxk, K);
-        L.meta[4 * s] = (int32_t)total;
+        const int64_t nv = (int64_t)(pairs ? (K + 1) & ~1 : K) * kSliceRows;   // real: whole lane pairs
+        const int64_t n8 = win ? (int64_t)((K + 3) / 4) * kSliceRows : 0;
+        const int64_t n32 = win ? 0 : (int64_t)K * kSliceRows;
+        // a slice never straddles two segments: start a new one when a stream would pass the limit
+        // (the margin covers the clamped loads of an empty slice)
+        const int64_t pad = 2 * kSliceMaxK * kSliceRows;
+        if ((total - L.seg_val[seg] + nv + pad) * (int64_t)sb > seg_lim ||
+            (ctot8 - L.seg_c8[seg] + n8 + pad) * 4 > seg_lim || (ctot32 - L.seg_c32[seg] + n32 + pad) * 4 > seg_lim) {
+            if (++seg >= kMaxSliceSeg) return false;
+            L.seg_val[seg] = total;
+            L.seg_c8[seg] = ctot8;
+            L.seg_c32[seg] = ctot32;
+        }
+        L.meta[4 * s] = (int32_t)(total - L.seg_val[seg]);
         L.meta[4 * s + 1] = win ? w0 : -1;
-        L.meta[4 * s + 2] = K | (ragged ? 0x100 : 0) | (win ? (int32_t)(wl << 9) : 0) | (ghost ? kGhostSliceBit : 0);
-        L.meta[4 * s + 3] = (int32_t)(win ? ctot8 : ctot32);
-        total += (int64_t)(pairs ? (K + 1) & ~1 : K) * kSliceRows;   // real: whole lane pairs
-        if (win) ctot8 += (int64_t)((K + 3) / 4) * kSliceRows;
-        else ctot32 += (int64_t)K * kSliceRows;
+        L.meta[4 * s + 2] = K | (ragged ? 0x100 : 0) | (win ? (int32_t)(wl << 9) : 0) | (ghost ? kGhostSliceBit : 0) |
+                            (seg << kSliceSegShift);
+        L.meta[4 * s + 3] = (int32_t)(win ? ctot8 - L.seg_c8[seg] : ctot32 - L.seg_c32[seg]);
+        total += nv;
+        ctot8 += n8;
+        ctot32 += n32;
         L.any_gather |= !win;
-        if (total > nnz + nnz / 8 + 64 * kSliceRows || total >= (int64_t(1) << 31) / (int64_t)sb) return false;
+        if (total > nnz + nnz / 8 + 64 * kSliceRows) return false;
     }
+    L.nseg = seg + 1;
     // one slice of padding past each stream's end (clamped loads of empty slices stay in bounds)
     L.val.assign((size_t)(total + kSliceRows) * sb, 0);
     L.c8.assign((size_t)(ctot8 + kSliceRows), 0);
@@ -1220,8 +1258,10 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
     if (any_ragged) L.len.assign((size_t)nrows, 0);
     for (int64_t s = 0; s < ns; ++s) {
         const int64_t r0 = s * kSliceRows, r1 = std::min<int64_t>(nrows, r0 + kSliceRows);
-        const int64_t off = L.meta[4 * s], coff = L.meta[4 * s + 3];
+        const int sg = (L.meta[4 * s + 2] >> kSliceSegShift) & (kMaxSliceSeg - 1);
         const int32_t w0 = L.meta[4 * s + 1];
+        const int64_t off = L.seg_val[sg] + L.meta[4 * s];
+        const int64_t coff = (w0 >= 0 ? L.seg_c8[sg] : L.seg_c32[sg]) + L.meta[4 * s + 3];
         const int K = L.meta[4 * s + 2] & 0xff;
         for (int64_t r = r0; r < r1; ++r) {
             const int64_t lane = r - r0;
@@ -1292,11 +1332,14 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     if (sliced)
         sliced = build_slices(rowptr, col_use, val_use, sb, !dtype_complex(dtype), nrows, nnz, xoff, ncols, SL);
 
-    // the kernels index every stream with 32-bit byte offsets (ldg): one device's rows must keep
-    // values, columns and vectors under 4 GiB each (shard larger matrices over ranks)
+    // the kernels index every stream with 32-bit byte offsets (ldg).  The sliced layout cuts its
+    // streams into < 4 GiB segments, so only the vectors are bounded there (n * sizeof(S) < 4 GiB:
+    // 536M f64 rows); the tile layouts keep the whole value stream under 4 GiB
     const size_t tile_pad = (size_t)(dtype == EIGSOL_C128 ? Tile<cplx>::kNnz : Tile<double>::kNnz) + 8;
-    if ((size_t)(nnz + tile_pad) * sb >= (size_t(1) << 32) || (size_t)(std::max(nrows, ncols) + 64) * sb >= (size_t(1) << 32))
-        return fail(EIGSOL_E_UNSUPPORTED, "eigsol_csr_create: a per-device stream exceeds 4 GiB; shard the rows over more ranks");
+    if ((size_t)(std::max(nrows, ncols) + 64) * sb >= (size_t(1) << 32))
+        return fail(EIGSOL_E_UNSUPPORTED, "eigsol_csr_create: the vectors exceed 4 GiB on one device; shard the rows over more ranks");
+    if (!sliced && (size_t)(nnz + tile_pad) * sb >= (size_t(1) << 32))
+        return fail(EIGSOL_E_UNSUPPORTED, "eigsol_csr_create: a per-device stream exceeds 4 GiB outside the sliced layout; shard the rows over more ranks");
     auto* A = new eigsol_csr();
     A->ctx = ctx;
     ctx_retain(ctx);
@@ -1313,6 +1356,12 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     A->nslices = sliced ? (int32_t)(SL.meta.size() / 4) : 0;
     A->slice_kb = SL.maxk <= 4 ? 4 : SL.maxk <= 8 ? 8 : SL.maxk <= 12 ? 12 : 16;
     A->slice_gather = SL.any_gather ? 1 : 0;
+    A->nseg = SL.nseg;
+    for (int g = 0; g < kMaxSliceSeg; ++g) {
+        A->seg_val[g] = SL.seg_val[g];
+        A->seg_c8[g] = SL.seg_c8[g];
+        A->seg_c32[g] = SL.seg_c32[g];
+    }
     if (const char* env = std::getenv("EIGSOL_SLICE_FORCE_GATHER")) if (std::atoi(env)) A->slice_gather = 1;   // A/B
     const size_t pad = (size_t)(dtype == EIGSOL_C128 ? Tile<cplx>::kNnz : Tile<double>::kNnz) + 8;   // branch-free tile loads
     auto cleanup = [&]() { csr_release(A); };
@@ -1464,6 +1513,11 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     a.scol32 = A->scol32;
     a.slen = A->slen;
     a.nslices = A->nslices;
+    for (int g = 0; g < kMaxSliceSeg; ++g) {
+        a.seg_val[g] = A->seg_val[g];
+        a.seg_c8[g] = A->seg_c8[g];
+        a.seg_c32[g] = A->seg_c32[g];
+    }
     a.ntiles = A->ntiles;
     a.nshort = A->nshort;
     a.xlen = (int32_t)xlen;

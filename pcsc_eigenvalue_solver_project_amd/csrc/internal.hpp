@@ -246,6 +246,8 @@ struct eigsol_csr {
     int32_t slice_gather = 0;      // some slices gather x from global memory (kernel instantiation)
     int32_t* scol32 = nullptr;     // device (gather slices)
     uint8_t* slen = nullptr;       // device, per row (ragged slices)
+    int32_t nseg = 1;              // stream segments (see kSliceSegShift): element offsets of each
+    int64_t seg_val[16] = {0}, seg_c8[16] = {0}, seg_c32[16] = {0};
     // Row-sharded (multi-GPU) layout: this rank owns global rows [row_begin, row_begin + nrows);
     // local columns are [own rows | ghosts grouped by owner rank, ascending global index].
     int dist = 0;

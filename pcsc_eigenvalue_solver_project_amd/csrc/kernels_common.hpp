@@ -158,6 +158,11 @@ struct alignas(128) PeerInbox {
     part4 part[2][kMaxPeerRanks];
 };
 constexpr int kGhostSliceBit = 1 << 20;   // slice meta .z: the slice reads ghost x entries
+// slice meta .z bits 21..24: the slice's stream segment.  Slice streams larger than 4 GiB are cut
+// into segments of < 4 GiB; a slice's 32-bit offsets are relative to its segment's base, so the
+// kernels keep 32-bit address arithmetic for any matrix that fits HBM.
+constexpr int kSliceSegShift = 21;
+constexpr int kMaxSliceSeg = 16;
 
 struct PeerArgs {
     PeerInbox* const* peers;   // peers[q]: rank q's inbox as mapped in this process (peers[me] = own)

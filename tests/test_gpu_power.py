@@ -328,3 +328,34 @@ def test_spmv_rectangular_sliced(ctx, shape):
             acc += M.data[e] * x[M.indices[e]]
         y_ref[i] = acc
     assert np.array_equal(y, y_ref)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_slice_stream_segments_bitwise_and_power(ctx, dtype, monkeypatch):
+    """Slice streams cut into several segments (EIGSOL_SLICE_SEG_BYTES forces 4 MiB segments: 4 to 13 of them here; the
+    default limit is 4 GiB): every product bitwise equal to the CSC scatter, and the power
+    iteration identical to the one-segment layout (same λ bits, same iterate)."""
+    n = 200_000
+    rp, ci, v = S.band(n, 10)
+    rp2, ci2, v2 = S.uniform(n, 16, seed=5)
+    v, v2 = v.astype(dtype), v2.astype(dtype)
+    x0 = S.start_vector(n, dtype)
+    opts = E.SolverOptions(300, 1e-12)
+    ref = {}
+    for key, (a, b, c) in {"band": (rp, ci, v), "uniform": (rp2, ci2, v2)}.items():
+        A = E.CsrMatrix(ctx, a, b, c, (n, n))
+        ref[key] = E.power_method(A, opts, x0)
+        A.close()
+    monkeypatch.setenv("EIGSOL_SLICE_SEG_BYTES", str(1 << 22))
+    for key, (a, b, c) in {"band": (rp, ci, v), "uniform": (rp2, ci2, v2)}.items():
+        A = E.CsrMatrix(ctx, a, b, c, (n, n))
+        s = E.PowerSession(A)
+        assert s.kernel_info()["variant"] == 5
+        s.close()
+        y = _spmv_gpu(ctx, A, x0)
+        cp, ri, vv = O.csr_to_csc(a, b, c, n)
+        assert np.array_equal(y, O.spmv_csc(cp, ri, vv, x0, n))
+        r = E.power_method(A, opts, x0)
+        assert r.iterations == ref[key].iterations and r.eigenvalue == ref[key].eigenvalue
+        assert np.array_equal(r.eigenvector, ref[key].eigenvector)
+        A.close()
