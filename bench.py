@@ -194,6 +194,29 @@ def run_config3(E, S, ctx, torch, stream, opts):
     return res
 
 
+def run_single_band10m(E, S, ctx, torch, stream):
+    """float (ScalarConcept admits it, types.hpp:28-30): the config-4 band matrix stored and multiplied
+    in single precision on the device.  Algorithmic bytes (SURVEY §8d with 4-byte values):
+    8 nnz + 4 (n + 1) + 8 n per fused iteration."""
+    n, k = 10_000_000, 10
+    rp, ci, v = S.band(n, k)
+    A = E.CsrMatrix(ctx, rp, ci, v.astype(np.float32), (n, n))
+    del rp, ci, v
+    sess = E.PowerSession(A)
+    sess.begin(E.SolverOptions(2**31 - 1, -1.0), S.start_vector(n, np.float32))
+    sess.step(10)
+    torch.cuda.synchronize()
+    ms = _events(torch, stream, lambda: sess.step(100)) / 100
+    info = sess.kernel_info()
+    out = {"GB/s": round(info["bytes_per_iteration"] / (ms / 1e3) / 1e9, 2), "ms_per_iteration": round(ms, 4),
+           "bytes_per_iteration": info["bytes_per_iteration"],
+           "roofline_frac": round(info["bytes_per_iteration"] / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+           "kernel": info["kernel"], "dtype": "f32"}
+    sess.close()
+    A.close()
+    return out
+
+
 def run_uniform10m(E, S, ctx, torch, stream, opts):
     """Config 4's honest gather figure (SURVEY §8d "uniform also reported"): the same fused
     iteration on a 10M x 10M matrix with 10 uniform random columns per row, one GPU."""
@@ -550,6 +573,7 @@ def main():
         out["extras"] = {
             "config3_csr_1Mx16": run_config3(E, S, ctx, torch, torch_stream, opts),
             "config4_uniform10m": run_uniform10m(E, S, ctx, torch, torch_stream, opts),
+            "band10m_float32": run_single_band10m(E, S, ctx, torch, torch_stream),
             "config1_A_txt": run_config1(E, S, ctx),
             "config2_qr_4096": run_config2(E, ctx, args.no_cpu_baseline),
             "qr_complex_1024": run_qr_complex(E, ctx, args.no_cpu_baseline),
