@@ -665,15 +665,23 @@ template <class S> struct Pair2 { using type = S; };
 template <> struct Pair2<double> { using type = double2; };
 template <> struct Pair2<float> { using type = float2; };
 template <class S> using pair_t = typename Pair2<S>::type;
+// Value groups of the slice stream: entries of a row held together in one 16-byte lane load
+// (f64: pairs; f32: quads; complex: one entry)
+template <class S> struct VGroup { using type = S; static constexpr int n = 1; };
+template <> struct VGroup<double> { using type = double2; static constexpr int n = 2; };
+template <> struct VGroup<float> { using type = float4; static constexpr int n = 4; };
+template <class S> using vgroup_t = typename VGroup<S>::type;
+template <class S> inline constexpr int kVG = VGroup<S>::n;
 
 template <class S, int KB, bool kG>
 struct SliceRegs {
     // window loads: real in pairs (window start even, length even), complex one per lane
     static constexpr int NW = is_real_v<S> ? kSliceWin / 128 : kSliceWin / 64;
     using WT = pair_t<S>;
-    // real values are stored in lane pairs (entries 2j, 2j+1 of a row adjacent): one load per pair
-    static constexpr int NV = is_real_v<S> ? KB / 2 : KB;
-    using VT = pair_t<S>;
+    // real values are stored in lane groups (entries g j .. g j + g - 1 of a row adjacent, g = 2 for
+    // f64, 4 for f32): one 16-byte load per group
+    static constexpr int NV = (KB + kVG<S> - 1) / kVG<S>;
+    using VT = vgroup_t<S>;
     VT v[NV];
     // window slices: packed 8-bit offsets in c[0 .. KB/4); gather slices (kG): int32 columns
     uint32_t c[kG ? KB : KB / 4];
@@ -683,14 +691,17 @@ struct SliceRegs {
 
 template <class S, int KB, bool kG>
 __device__ __forceinline__ S slice_val(const SliceRegs<S, KB, kG>& R, int u) {
-    if constexpr (is_real_v<S>) return (u & 1) ? R.v[u >> 1].y : R.v[u >> 1].x;
-    else return R.v[u];
+    if constexpr (kVG<S> == 2) return (u & 1) ? R.v[u >> 1].y : R.v[u >> 1].x;
+    else if constexpr (kVG<S> == 4) {
+        const float4 q = R.v[u >> 2];
+        return (u & 3) == 0 ? q.x : (u & 3) == 1 ? q.y : (u & 3) == 2 ? q.z : q.w;
+    } else return R.v[u];
 }
 // stream index of entry (k, lane) of a slice whose values start at off
 template <class S>
 __device__ __forceinline__ uint32_t slice_entry(uint32_t off, int k, int lane) {
-    if constexpr (is_real_v<S>) return off + 128u * (uint32_t)(k >> 1) + 2u * (uint32_t)lane + (uint32_t)(k & 1);
-    else return off + 64u * (uint32_t)k + (uint32_t)lane;
+    constexpr uint32_t g = kVG<S>;
+    return off + 64u * g * (uint32_t)(k / (int)g) + g * (uint32_t)lane + (uint32_t)(k % (int)g);
 }
 
 // Every load of one slice's first KB entries, its window and the row lengths.  Loads are clamped
@@ -710,11 +721,12 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
     R.len = m.z & 0xff;
     if (m.z & 0x100) R.len = a.slen[min(slice * kSliceRows + lane, a.nrows - 1)];
     if constexpr (is_real_v<S>) {
-        const int K2 = (K + 1) >> 1;
-        const uint32_t b2 = ((uint32_t)m.x >> 1) + (uint32_t)lane;
+        constexpr int g = kVG<S>;
+        const int Kg = (K + g - 1) / g;
+        const uint32_t bg = ((uint32_t)m.x / (uint32_t)g) + (uint32_t)lane;
 #pragma unroll
         for (int j = 0; j < SliceRegs<S, KB, kG>::NV; ++j)
-            R.v[j] = ldg_stream(reinterpret_cast<const pair_t<S>*>(sval), b2 + 64u * (uint32_t)min(j, K2 - 1));
+            R.v[j] = ldg_stream(reinterpret_cast<const vgroup_t<S>*>(sval), bg + 64u * (uint32_t)min(j, Kg - 1));
     } else {
 #pragma unroll
         for (int u = 0; u < KB; ++u) R.v[u] = ldg_stream(sval, base + 64u * (uint32_t)min(u, K - 1));
@@ -1177,7 +1189,7 @@ static int64_t slice_seg_bytes() {
     return lim;
 }
 
-static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* values, size_t sb, bool pairs,
+static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* values, size_t sb, int vg,
                          int64_t nrows, int64_t nnz, int64_t xoff, int64_t xlen, SliceLayout& L) {
     if (nrows == 0 || xlen == 0) return false;
     const int64_t ns = (nrows + kSliceRows - 1) / kSliceRows;
@@ -1205,6 +1217,7 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
         w1 = (int32_t)std::min<int64_t>(w1, xlen - 1);
         w0 = std::min(w0, w1);
         bool win = true;
+        const bool pairs = vg > 1;   // real scalars
         if (pairs) {
             // real windows load in aligned pairs: even start and even length inside x
             w0 &= ~1;
@@ -1226,7 +1239,7 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
         }
         any_ragged |= ragged;
         L.maxk = std::max(L.maxk, K);
-        const int64_t nv = (int64_t)(pairs ? (K + 1) & ~1 : K) * kSliceRows;   // real: whole lane pairs
+        const int64_t nv = (int64_t)((K + vg - 1) / vg * vg) * kSliceRows;   // whole lane groups
         const int64_t n8 = win ? (int64_t)((K + 3) / 4) * kSliceRows : 0;
         const int64_t n32 = win ? 0 : (int64_t)K * kSliceRows;
         // a slice never straddles two segments: start a new one when a stream would pass the limit
@@ -1248,7 +1261,8 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
         ctot8 += n8;
         ctot32 += n32;
         L.any_gather |= !win;
-        if (total > nnz + nnz / 8 + 64 * kSliceRows) return false;
+        // padding beyond the lane-group rounding at most 1/8 of the entries
+        if (total > nnz + nnz / 8 + (int64_t)(vg - 1) * kSliceRows * (s + 1) + 64 * kSliceRows) return false;
     }
     L.nseg = seg + 1;
     // one slice of padding past each stream's end (clamped loads of empty slices stay in bounds)
@@ -1269,8 +1283,7 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
             if (any_ragged) L.len[r] = (uint8_t)l;
             for (int k = 0; k < l; ++k) {
                 const int32_t e = rowptr[r] + k;
-                const size_t q = pairs ? (size_t)(off + (int64_t)(k >> 1) * 2 * kSliceRows + 2 * lane + (k & 1))
-                                         : (size_t)(off + (int64_t)k * kSliceRows + lane);
+                const size_t q = (size_t)(off + (int64_t)(k / vg) * vg * kSliceRows + vg * lane + (k % vg));
                 std::memcpy(&L.val[q * sb], (const unsigned char*)values + (size_t)e * sb, sb);
                 if (w0 >= 0)
                     L.c8[(size_t)(coff + (int64_t)(k / 4) * kSliceRows + lane)] |= (uint32_t)(col[e] - w0) << (8 * (k % 4));
@@ -1330,7 +1343,8 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     bool sliced = true;
     if (const char* env = std::getenv("EIGSOL_CSR_NO_SLICE")) if (std::atoi(env)) sliced = false;
     if (sliced)
-        sliced = build_slices(rowptr, col_use, val_use, sb, !dtype_complex(dtype), nrows, nnz, xoff, ncols, SL);
+        sliced = build_slices(rowptr, col_use, val_use, sb,
+                              dtype == EIGSOL_F64 ? 2 : (dtype == EIGSOL_F32 ? 4 : 1), nrows, nnz, xoff, ncols, SL);
 
     // the kernels index every stream with 32-bit byte offsets (ldg).  The sliced layout cuts its
     // streams into < 4 GiB segments, so only the vectors are bounded there (n * sizeof(S) < 4 GiB:
