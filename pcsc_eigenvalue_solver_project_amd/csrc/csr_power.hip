@@ -66,6 +66,7 @@ struct CsrArgs {
     const int32_t* scol32;   // gather slices: x-space column
     const uint8_t* slen;     // row lengths (read for ragged slices only)
     int32_t nslices;
+    int32_t nseg;                    // stream segments; 1: no per-slice segment lookup
     int64_t seg_val[kMaxSliceSeg];   // element offset of each stream segment (slice meta .z bits 21..24)
     int64_t seg_c8[kMaxSliceSeg];
     int64_t seg_c32[kMaxSliceSeg];
@@ -713,10 +714,15 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
     // K = 0 (all rows empty) clamps to entry 0 of the slice: the streams carry one slice of
     // padding past their end, so even an empty last slice loads in bounds
     const int K = max(m.z & 0xff, 1);
-    const int seg = (m.z >> kSliceSegShift) & (kMaxSliceSeg - 1);   // wave-uniform
-    const S* sval = a.sval + a.seg_val[seg];
-    const uint32_t* scol8 = a.scol8 + a.seg_c8[seg];
-    const int32_t* scol32 = a.scol32 + a.seg_c32[seg];
+    const S* sval = a.sval;
+    const uint32_t* scol8 = a.scol8;
+    const int32_t* scol32 = a.scol32;
+    if (a.nseg > 1) {   // a dynamically indexed kernel argument costs a scalar load per slice
+        const int seg = (m.z >> kSliceSegShift) & (kMaxSliceSeg - 1);   // wave-uniform
+        sval += a.seg_val[seg];
+        scol8 += a.seg_c8[seg];
+        scol32 += a.seg_c32[seg];
+    }
     const uint32_t base = (uint32_t)m.x + (uint32_t)lane;
     R.len = m.z & 0xff;
     if (m.z & 0x100) R.len = a.slen[min(slice * kSliceRows + lane, a.nrows - 1)];
@@ -778,10 +784,15 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
                                               int parity = 0) {
     const int lane = threadIdx.x & 63;
     const int K = mc.z & 0xff;
-    const int seg = (mc.z >> kSliceSegShift) & (kMaxSliceSeg - 1);
-    const S* sval = a.sval + a.seg_val[seg];
-    const uint32_t* scol8 = a.scol8 + a.seg_c8[seg];
-    const int32_t* scol32 = a.scol32 + a.seg_c32[seg];
+    const S* sval = a.sval;
+    const uint32_t* scol8 = a.scol8;
+    const int32_t* scol32 = a.scol32;
+    if (a.nseg > 1) {
+        const int seg = (mc.z >> kSliceSegShift) & (kMaxSliceSeg - 1);
+        sval += a.seg_val[seg];
+        scol8 += a.seg_c8[seg];
+        scol32 += a.seg_c32[seg];
+    }
     const int row = sl * kSliceRows + lane;
     const bool valid = row < a.nrows;
     const int rowc = valid ? row : a.nrows - 1;
@@ -1527,6 +1538,7 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     a.scol32 = A->scol32;
     a.slen = A->slen;
     a.nslices = A->nslices;
+    a.nseg = A->nseg;
     for (int g = 0; g < kMaxSliceSeg; ++g) {
         a.seg_val[g] = A->seg_val[g];
         a.seg_c8[g] = A->seg_c8[g];

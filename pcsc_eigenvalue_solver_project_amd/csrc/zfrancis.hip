@@ -34,7 +34,8 @@ namespace dev {
 
 constexpr int kZWin = 64;         // window rows/columns
 constexpr int kZSmall = 64;       // blocks finished by the one-wave solver
-constexpr int kZMaxBulges = 16;   // one wave each
+constexpr int kZMaxBulges = 32;   // per sweep (shifts from a <= 64 block); per window <= 16, one wave each
+constexpr int kZMaxGroups = 4;    // bulge chains chased concurrently, one window (workgroup) each
 
 __device__ __forceinline__ cplx cconj(cplx a) { return cplx{a.re, -a.im}; }
 __device__ __forceinline__ double cabs1(cplx a) { return fabs(a.re) + fabs(a.im); }
@@ -205,18 +206,31 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
 }
 
 // ---------------------------------------------------------------- windowed multishift chase
+struct ZChaseWin {
+    int s, e;          // window [s, e)
+    int t0, t1;        // chase steps of this launch (chain-relative)
+    int nb;            // bulges of the chain
+    const cplx* shifts;   // 2 per bulge
+    cplx* U;           // out: (e - s)^2, column-major
+};
+struct ZChaseBatch {   // one workgroup per window; the windows are disjoint
+    cplx* H;
+    int64_t n;
+    int l, ihi;
+    ZChaseWin w[kZMaxGroups];
+};
 struct ZChaseArgs {
     cplx* H;
     int64_t n;
     int l, ihi;
-    int s, e;          // window [s, e)
-    int t0, t1;        // chase steps of this launch
-    int nb;            // bulges
-    const cplx* shifts;   // 2 per bulge
-    cplx* U;           // out: (e - s)^2, column-major
+    int s, e, t0, t1, nb;
+    const cplx* shifts;
+    cplx* U;
 };
 
-__global__ __launch_bounds__(1024) void zchase_kernel(ZChaseArgs a) {
+__global__ __launch_bounds__(1024) void zchase_kernel(ZChaseBatch b) {
+    const ZChaseWin wd = b.w[blockIdx.x];
+    const ZChaseArgs a{b.H, b.n, b.l, b.ihi, wd.s, wd.e, wd.t0, wd.t1, wd.nb, wd.shifts, wd.U};
     __shared__ cplx h[kZWin * (kZWin + 1)];
     __shared__ cplx u[kZWin * kZWin];
     constexpr int lh = kZWin + 1, lu = kZWin;
@@ -328,15 +342,35 @@ __global__ __launch_bounds__(1024) void zchase_kernel(ZChaseArgs a) {
 // the output (8 LDS reads per 16 complex multiply-adds; the LDS pitches keep a wave's 16-byte
 // reads on distinct banks).
 constexpr int kZG = 32;   // output columns (left) / rows (right) per workgroup
+struct ZWinGemm {
+    int s, W;          // window rows/columns [s, s + W)
+    int64_t lo, hi;    // left: columns [lo, hi); right: rows [lo, hi)
+    int blk0;          // first workgroup of this window
+    const cplx* U;
+};
+struct ZWinGemmBatch {   // left regions of different windows own disjoint rows, right regions disjoint columns
+    cplx* H;
+    int64_t n;
+    int nw;
+    ZWinGemm w[kZMaxGroups];
+};
 template <bool kLeft>
-__global__ __launch_bounds__(128) void zwin_gemm_kernel(cplx* H, int64_t n, int s, int W, int64_t lo, int64_t hi,
-                                                        const cplx* U) {
+__global__ __launch_bounds__(128) void zwin_gemm_kernel(ZWinGemmBatch bt) {
+    int g = 0;
+#pragma unroll
+    for (int q = 1; q < kZMaxGroups; ++q)
+        if (q < bt.nw && (int)blockIdx.x >= bt.w[q].blk0) g = q;
+    cplx* H = bt.H;
+    const int64_t n = bt.n;
+    const int s = bt.w[g].s, W = bt.w[g].W;
+    const int64_t lo = bt.w[g].lo, hi = bt.w[g].hi;
+    const cplx* U = bt.w[g].U;
     constexpr int LU = kZWin + 1;    // U pitch
     constexpr int LX = kZWin + 1;    // panel pitch
     __shared__ cplx us[kZWin * LU];
     __shared__ cplx xs[kZG * LX];
     const int tid = threadIdx.x;
-    const int64_t b0 = lo + (int64_t)blockIdx.x * kZG;
+    const int64_t b0 = lo + (int64_t)(blockIdx.x - bt.w[g].blk0) * kZG;
     const int nb = (int)std::min<int64_t>(kZG, hi - b0);
     for (int idx = tid; idx < W * W; idx += 128) us[(idx % W) + (idx / W) * LU] = U[idx];
     if (kLeft) {   // xs[r + c LX] = H(s + r, b0 + c)
@@ -402,7 +436,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
     int* dinfo = nullptr;
     int rc = EIGSOL_OK;
     if (hipMalloc(&dw, n * sizeof(cplx)) != hipSuccess || hipMalloc(&dds, 2 * n * sizeof(cplx)) != hipSuccess ||
-        hipMalloc(&dU, dev::kZWin * dev::kZWin * sizeof(cplx)) != hipSuccess ||
+        hipMalloc(&dU, (size_t)dev::kZMaxGroups * dev::kZWin * dev::kZWin * sizeof(cplx)) != hipSuccess ||
         hipMalloc(&dsh, 2 * dev::kZMaxBulges * sizeof(cplx)) != hipSuccess || hipMalloc(&dinfo, 64) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "complex QR: hipMalloc");
     std::vector<cplx> ds(2 * n), swv(2 * dev::kZMaxBulges);
@@ -441,12 +475,21 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             continue;
         }
         if (++stall > max_stall) { failed = 1; sweeps = std::max(sweeps, stall); break; }
-        // at most 8 bulges: the chain (3 nb rows) must leave the 64-row window room to advance
+        // up to 16 bulges per sweep (32 shifts, LAPACK's count for n in the low thousands) in C chains
+        // of at most 8 (a chain's 3 nb rows must leave its 64-row window room to advance), the
+        // chains chased concurrently in disjoint windows
         static const int max_nb = [] {
             const char* e = std::getenv("EIGSOL_ZQR_NB");
-            return e ? std::max(1, std::min(dev::kZMaxBulges, std::atoi(e))) : 8;
+            return e ? std::max(1, std::min(dev::kZMaxBulges / 2, std::atoi(e))) : 16;
+        }();
+        static const int max_groups = [] {
+            const char* e = std::getenv("EIGSOL_ZQR_GROUPS");
+            return e ? std::max(1, std::min(dev::kZMaxGroups, std::atoi(e))) : 2;
         }();
         int nb = std::min(max_nb, std::max(1, N / 16));
+        const int C = std::max(1, std::min({max_groups, (nb + 7) / 8, 1 + N / (4 * (dev::kZWin + 12))}));
+        const int nbg = std::max(1, std::min(8, nb / C));
+        nb = nbg * C;
         const int ns = 2 * nb;
         std::vector<cplx> sh(ns);
         bool exceptional = stall % 6 == 0;
@@ -467,30 +510,59 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
                 break;
             }
         }
-        // chase the chain of nb bulges down [l, ihi] through successive windows
-        const int T = (ihi - 1 - l) + 3 * (nb - 1) + 1;
+        // chase: chain g starts G steps after chain g-1 (windows stay disjoint); a round advances
+        // every started chain's window by the same number of steps
+        const int G = dev::kZWin + 3 * nbg;
+        const int Tg = (ihi - 1 - l) + 3 * (nbg - 1) + 1;   // steps of one chain
+        const int T = (C - 1) * G + Tg;
         int t0 = 0;
         while (t0 < T && rc == EIGSOL_OK) {
-            int s = t0 <= 3 * (nb - 1) ? std::max(0, l - 1) : std::max(0, l + t0 - 3 * (nb - 1) - 1);
-            const int e = std::min(s + dev::kZWin, ihi + 1);
-            const int kmax = (e == ihi + 1) ? ihi - 1 : e - 4;
-            int t1 = t0;
-            while (t1 < T) {
-                const int blead = std::max(0, (l + t1 - (ihi - 1) + 2) / 3);   // first bulge not past ihi-1
-                if (blead >= nb) { t1 = T; break; }
-                if (l + t1 - 3 * blead > kmax) break;
-                ++t1;
+            dev::ZChaseBatch cb{H, (int64_t)n, l, ihi, {}};
+            int t1 = T, nwin = 0;
+            int g_act[dev::kZMaxGroups];
+            for (int g = 0; g < C; ++g) {
+                const int tl = t0 - g * G;
+                if (tl < 0) { t1 = std::min(t1, g * G); break; }    // later chains start at a round boundary
+                if (tl >= Tg) continue;                              // chain done
+                const int s = tl <= 3 * (nbg - 1) ? std::max(0, l - 1) : std::max(0, l + tl - 3 * (nbg - 1) - 1);
+                const int e = std::min(s + dev::kZWin, ihi + 1);
+                const int kmax = (e == ihi + 1) ? ihi - 1 : e - 4;
+                int tl1 = tl;
+                while (tl1 < Tg) {
+                    const int blead = std::max(0, (l + tl1 - (ihi - 1) + 2) / 3);   // first bulge not past ihi-1
+                    if (blead >= nbg) { tl1 = Tg; break; }
+                    if (l + tl1 - 3 * blead > kmax) break;
+                    ++tl1;
+                }
+                t1 = std::min(t1, tl1 + g * G);
+                cb.w[nwin] = dev::ZChaseWin{s, e, tl, 0, nbg, dsh + 2 * g * nbg, dU + (size_t)nwin * dev::kZWin * dev::kZWin};
+                g_act[nwin++] = g;
             }
-            if (t1 <= t0) { rc = fail(EIGSOL_E_SOLVER, "complex QR: window did not advance (internal error)"); break; }
-            dev::ZChaseArgs ca{H, (int64_t)n, l, ihi, s, e, t0, t1, nb, dsh, dU};
-            hipLaunchKernelGGL(dev::zchase_kernel, dim3(1), dim3(1024), 0, st, ca);
-            const int W = e - s;
-            if (e <= ihi)
-                hipLaunchKernelGGL(dev::zwin_gemm_kernel<true>, dim3((ihi + 1 - e + dev::kZG - 1) / dev::kZG), dim3(128), 0, st, H,
-                                   (int64_t)n, s, W, (int64_t)e, (int64_t)ihi + 1, (const cplx*)dU);
-            if (s > l)
-                hipLaunchKernelGGL(dev::zwin_gemm_kernel<false>, dim3((s - l + dev::kZG - 1) / dev::kZG), dim3(128), 0, st, H,
-                                   (int64_t)n, s, W, (int64_t)l, (int64_t)s, (const cplx*)dU);
+            if (nwin == 0 && t1 > t0) { t0 = t1; continue; }   // every started chain done, the next not yet due
+            if (t1 <= t0 || nwin == 0) { rc = fail(EIGSOL_E_SOLVER, "complex QR: window did not advance (internal error)"); break; }
+            for (int q = 0; q < nwin; ++q) {
+                cb.w[q].t1 = t1 - g_act[q] * G;
+                if (q > 0 && cb.w[q].e > cb.w[q - 1].s) { rc = fail(EIGSOL_E_SOLVER, "complex QR: windows overlap (internal error)"); break; }
+            }
+            if (rc != EIGSOL_OK) break;
+            hipLaunchKernelGGL(dev::zchase_kernel, dim3(nwin), dim3(1024), 0, st, cb);
+            // delayed updates: every left region, then every right region (U_a^H X U_b = (U_a^H X) U_b)
+            dev::ZWinGemmBatch lb{H, (int64_t)n, 0, {}}, rb{H, (int64_t)n, 0, {}};
+            int nlb = 0, nrb = 0;
+            for (int q = 0; q < nwin; ++q) {
+                const dev::ZChaseWin& w = cb.w[q];
+                const int W = w.e - w.s;
+                if (w.e <= ihi) {
+                    lb.w[lb.nw++] = dev::ZWinGemm{w.s, W, (int64_t)w.e, (int64_t)ihi + 1, nlb, w.U};
+                    nlb += (ihi + 1 - w.e + dev::kZG - 1) / dev::kZG;
+                }
+                if (w.s > l) {
+                    rb.w[rb.nw++] = dev::ZWinGemm{w.s, W, (int64_t)l, (int64_t)w.s, nrb, w.U};
+                    nrb += (w.s - l + dev::kZG - 1) / dev::kZG;
+                }
+            }
+            if (nlb > 0) hipLaunchKernelGGL(dev::zwin_gemm_kernel<true>, dim3(nlb), dim3(128), 0, st, lb);
+            if (nrb > 0) hipLaunchKernelGGL(dev::zwin_gemm_kernel<false>, dim3(nrb), dim3(128), 0, st, rb);
             t0 = t1;
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "complex QR: launch"); break; }
