@@ -59,6 +59,14 @@ __device__ __forceinline__ cplx cdiv_s(cplx a, cplx b) {
     return cplx{(a.re * r + a.im) / d, (a.im * r - a.re) / d};
 }
 
+__device__ __forceinline__ double rcp_nr(double x) {   // x != 0, finite, normal reciprocal
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
 // ZLARFG on (alpha, x1, x2) (x2 ignored when !three): Q = I - tau v v^H, v = (1, v1, v2),
 // Q^H (alpha, x1, x2) = (beta, 0, 0).  tau = 0 (Q = I) when x = 0 and alpha is real.  The caller
 // scales the input to O(1).
@@ -73,16 +81,29 @@ __device__ __forceinline__ void zhouse(cplx a, cplx x1, cplx x2, bool three, dou
     }
     const double an = sqrt(a.re * a.re + a.im * a.im + xn2);
     beta = a.re >= 0.0 ? -an : an;
-    tau = cplx{(beta - a.re) / beta, -a.im / beta};
-    const cplx d = cplx{a.re - beta, a.im};
-    v1 = cdiv_s(x1, d);
-    v2 = three ? cdiv_s(x2, d) : cplx{0.0, 0.0};
+    // the step's serial chain: reciprocals (v_rcp_f64 + two Newton steps, within an ulp or two)
+    // instead of IEEE divisions; x / d by Smith's scaling with one reciprocal of the denominator
+    const double ib = rcp_nr(beta);
+    tau = cplx{(beta - a.re) * ib, -a.im * ib};
+    const cplx d = cplx{a.re - beta, a.im};   // |d| >= |beta| > 0
+    const bool re_big = fabs(d.re) >= fabs(d.im);
+    const double r = re_big ? d.im * rcp_nr(d.re) : d.re * rcp_nr(d.im);
+    const double id = rcp_nr(re_big ? __builtin_fma(d.im, r, d.re) : __builtin_fma(d.re, r, d.im));
+    auto qt = [&](cplx x) -> cplx {
+        return re_big ? cplx{__builtin_fma(x.im, r, x.re) * id, __builtin_fma(-x.re, r, x.im) * id}
+                      : cplx{__builtin_fma(x.re, r, x.im) * id, __builtin_fma(x.im, r, -x.re) * id};
+    };
+    v1 = qt(x1);
+    v2 = three ? qt(x2) : cplx{0.0, 0.0};
 }
 
 // ---------------------------------------------------------------- one-wave single-shift QR (n <= 64)
 // Eigenvalues of an n x n Hessenberg block (ZLAHQR without Schur vectors; updates confined to the
 // active block).  info[0] = 1 if some eigenvalue needed more than 30 max(10, n) iterations,
 // info[1] = most iterations any eigenvalue took.
+// One wave, so no barriers: a wave's LDS operations complete in program order, and the compiler
+// fence keeps the program order.
+#define EIGSOL_ZWAVE_ORDER() asm volatile("" ::: "memory")
 __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t ld, int n, cplx* w, int* info) {
     __shared__ cplx h[kZSmall * (kZSmall + 1)];
     constexpr int lh = kZSmall + 1;
@@ -96,29 +117,34 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
     while (i >= 0) {
         int l = 0, its = 0;
         for (; its <= itmax; ++its) {
-            int k = i;
-            for (; k > l; --k) {
+            // the largest k in (l, i] with a negligible subdiagonal (l if none): the serial downward
+            // scan's answer, one k per lane, then a wave max
+            int kf = l;
+            for (int k = i - ln; k > l; k -= 64) {
                 const cplx hk = H(k, k - 1);
-                if (cabs1(hk) <= smlnum) break;
-                double tst = cabs1(H(k - 1, k - 1)) + cabs1(H(k, k));
-                if (tst == 0.0) {
-                    if (k - 2 >= l) tst += fabs(H(k - 1, k - 2).re);
-                    if (k + 1 <= i) tst += fabs(H(k + 1, k).re);
+                bool neg = cabs1(hk) <= smlnum;
+                if (!neg) {
+                    double tst = cabs1(H(k - 1, k - 1)) + cabs1(H(k, k));
+                    if (tst == 0.0) {
+                        if (k - 2 >= l) tst += fabs(H(k - 1, k - 2).re);
+                        if (k + 1 <= i) tst += fabs(H(k + 1, k).re);
+                    }
+                    if (cabs1(hk) <= ulp * tst) {
+                        const double ab = fmax(cabs1(hk), cabs1(H(k - 1, k))), ba = fmin(cabs1(hk), cabs1(H(k - 1, k)));
+                        const cplx dd = sub(H(k - 1, k - 1), H(k, k));
+                        const double aa = fmax(cabs1(H(k, k)), cabs1(dd)), bb = fmin(cabs1(H(k, k)), cabs1(dd));
+                        const double s = aa + ab;
+                        neg = ba * (ab / s) <= fmax(smlnum, ulp * (bb * (aa / s)));
+                    }
                 }
-                if (cabs1(hk) <= ulp * tst) {
-                    const double ab = fmax(cabs1(hk), cabs1(H(k - 1, k))), ba = fmin(cabs1(hk), cabs1(H(k - 1, k)));
-                    const cplx dd = sub(H(k - 1, k - 1), H(k, k));
-                    const double aa = fmax(cabs1(H(k, k)), cabs1(dd)), bb = fmin(cabs1(H(k, k)), cabs1(dd));
-                    const double s = aa + ab;
-                    if (ba * (ab / s) <= fmax(smlnum, ulp * (bb * (aa / s)))) break;
-                }
+                if (neg) { kf = k; break; }
             }
-            l = k;
-            if (l > 0) {
-                __syncthreads();
-                if (ln == 0) H(l, l - 1) = cplx{0.0, 0.0};
-                __syncthreads();
-            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) kf = max(kf, __shfl_xor(kf, off, 64));
+            l = __builtin_amdgcn_readfirstlane(kf);
+            EIGSOL_ZWAVE_ORDER();
+            if (l > 0 && ln == 0) H(l, l - 1) = cplx{0.0, 0.0};
+            EIGSOL_ZWAVE_ORDER();
             if (l >= i) break;
             // shift
             cplx t;
@@ -159,7 +185,7 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
                 double beta;
                 cplx tau, vv, unused;
                 zhouse(v0, v1, cplx{0.0, 0.0}, false, beta, tau, vv, unused);
-                __syncthreads();
+                EIGSOL_ZWAVE_ORDER();
                 if (kk > l && ln == 0) {
                     H(kk, kk - 1) = cplx{beta, 0.0};
                     H(kk + 1, kk - 1) = cplx{0.0, 0.0};
@@ -174,7 +200,7 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
                         H(kk + 1, c) = sub(a1, mul(s, vv));
                     }
                 }
-                __syncthreads();
+                EIGSOL_ZWAVE_ORDER();
                 {   // right: columns kk, kk+1, rows l..min(kk+2, i)
                     const int r = l + ln;
                     if (r <= min(kk + 2, i)) {
@@ -184,7 +210,7 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
                         H(r, kk + 1) = sub(a1, mul(s, cconj(vv)));
                     }
                 }
-                __syncthreads();
+                EIGSOL_ZWAVE_ORDER();
             }
         }
         if (its > itmax) {
@@ -480,7 +506,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         // chains chased concurrently in disjoint windows
         static const int max_nb = [] {
             const char* e = std::getenv("EIGSOL_ZQR_NB");
-            return e ? std::max(1, std::min(dev::kZMaxBulges / 2, std::atoi(e))) : 16;
+            return e ? std::max(1, std::min(dev::kZMaxBulges, std::atoi(e))) : 16;
         }();
         static const int max_groups = [] {
             const char* e = std::getenv("EIGSOL_ZQR_GROUPS");

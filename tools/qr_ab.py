@@ -9,7 +9,8 @@ from pcsc_eigenvalue_solver_project_amd import synthetic as S
 
 ctx = E.Context(0)
 out = {}
-for n in (60, 128, 512, 4096, -200, -1024):     # negative: complex N(0,1)
+sizes = [int(v) for v in os.environ.get("QR_AB_SIZES", "60,128,512,4096,-200,-1024").split(",")]
+for n in sizes:     # negative: complex N(0,1)
     rng = np.random.default_rng(abs(n))
     A = rng.standard_normal((n, n)) if n > 0 else rng.standard_normal((-n, -n)) + 1j * rng.standard_normal((-n, -n))
     best = 1e9
