@@ -363,11 +363,13 @@ __global__ __launch_bounds__(1024) void zchase_kernel(ZChaseBatch b) {
 }
 
 // Delayed window updates.  left: H(s:s+W, cols) <- U^H H(s:s+W, cols) for the columns [lo, hi);
-// right: H(rows, s:s+W) <- H(rows, s:s+W) U for the rows [lo, hi).  32 output columns (rows) per
-// workgroup of 128 threads; U and the panel staged in LDS, each thread a 4 x 4 register tile of
-// the output (8 LDS reads per 16 complex multiply-adds; the LDS pitches keep a wave's 16-byte
-// reads on distinct banks).
-constexpr int kZG = 32;   // output columns (left) / rows (right) per workgroup
+// right: H(rows, s:s+W) <- H(rows, s:s+W) U for the rows [lo, hi).  8 output columns (rows) per
+// workgroup of 128 threads; U and the panel staged in LDS, each thread a 4 x 1 register tile of
+// the output (the LDS pitches keep a wave's 16-byte reads on distinct banks).  The regions are a
+// few hundred columns, so narrow workgroups are what spreads a launch over the CUs: 32 columns per
+// workgroup 0.436 s, 16: 0.39 s, 8: 0.37 s for the 1024^2 complex QR.
+constexpr int kZG = 8;   // output columns (left) / rows (right) per workgroup
+constexpr int kZB = kZG / 8;   // register-tile columns per thread
 struct ZWinGemm {
     int s, W;          // window rows/columns [s, s + W)
     int64_t lo, hi;    // left: columns [lo, hi); right: rows [lo, hi)
@@ -413,27 +415,27 @@ __global__ __launch_bounds__(128) void zwin_gemm_kernel(ZWinGemmBatch bt) {
     __syncthreads();
     // output tile: 4 window indices (i0 + 16 a) x 4 block columns/rows (c0 + 8 b)
     const int i0 = tid & 15, c0 = tid >> 4;   // 16 x 8 threads
-    cplx acc[4][4];
+    cplx acc[4][kZB];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = cplx{0.0, 0.0};
+        for (int b = 0; b < kZB; ++b) acc[a][b] = cplx{0.0, 0.0};
     for (int r = 0; r < W; ++r) {
-        cplx uu[4], xx[4];
+        cplx uu[4], xx[kZB];
 #pragma unroll
         for (int a = 0; a < 4; ++a) uu[a] = kLeft ? us[r + (i0 + 16 * a) * LU] : us[r + (i0 + 16 * a) * LU];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) xx[b] = xs[r + (c0 + 8 * b) * LX];
+        for (int b = 0; b < kZB; ++b) xx[b] = xs[r + (c0 + 8 * b) * LX];
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
+            for (int b = 0; b < kZB; ++b)
                 acc[a][b] = add(acc[a][b], kLeft ? cmul_conj(uu[a], xx[b]) : mul(xx[b], uu[a]));
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
+        for (int b = 0; b < kZB; ++b) {
             const int i = i0 + 16 * a, c = c0 + 8 * b;
             if (i < W && c < nb) {
                 if (kLeft) H[(s + i) + (b0 + c) * n] = acc[a][b];          // (U^H X)(i, c)
