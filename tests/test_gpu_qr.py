@@ -249,6 +249,21 @@ def test_complex_francis_small_and_windows(ctx, n):
     _match(r.eigenvalues_complex, np.linalg.eigvals(A), 1e-9 * np.linalg.norm(A))
 
 
+@pytest.mark.parametrize("n", [304, 379, 700])
+def test_complex_francis_two_chains(ctx, n):
+    # from N >= 304 a sweep chases two 8-bulge chains concurrently in disjoint windows with batched
+    # window GEMMs; 379 = 304 + 75 ends the second chain's windows off the 64-row grid
+    rng = np.random.default_rng(7 * n)
+    A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12))
+    assert r.converged
+    _match(r.eigenvalues_complex, np.linalg.eigvals(A), 1e-9 * np.linalg.norm(A))
+    B = A + A.conj().T   # Hermitian: real spectrum through the same schedule
+    r = E.qr_eigenvalues(ctx, B, E.SolverOptions(1000, 1e-12))
+    assert r.converged
+    _match(r.eigenvalues_complex, np.linalg.eigvalsh(B), 1e-9 * np.linalg.norm(B))
+
+
 def test_complex_francis_1024_fixture(ctx):
     rng = np.random.default_rng(1024)
     n = 1024
