@@ -444,6 +444,140 @@ __global__ __launch_bounds__(128) void zwin_gemm_kernel(ZWinGemmBatch bt) {
         }
 }
 
+// The same delayed updates on the fp64 matrix cores (v_mfma_f64_16x16x4_f64): a complex tile
+// product is four real ones on split re/im planes.  64 output columns (left) / rows (right) per
+// workgroup of 4 waves, each wave a 16-wide strip against the window's 4 row tiles; U (and the
+// left panel) staged in LDS as re/im planes at a pitch of kZWin + 2 (the real kernel's
+// conflict-free pitch).  D layout: lane L, register r holds D[(L >> 4) + 4 r][L & 15].
+typedef double zdbl4 __attribute__((ext_vector_type(4)));
+constexpr int kZUP = kZWin + 2;
+constexpr int kZMG = 64;   // outputs per workgroup
+constexpr int kZMT = 4 * kZMG;   // threads: one wave per 16 outputs
+template <bool kLeft>
+__global__ __launch_bounds__(kZMT) void zwin_gemm_mfma(ZWinGemmBatch bt) {
+    __shared__ double ur[kZWin * kZUP], ui[kZWin * kZUP];
+    __shared__ double xr_s[kLeft ? kZMG * kZUP : 1], xi_s[kLeft ? kZMG * kZUP : 1];
+    int g = 0;
+#pragma unroll
+    for (int q = 1; q < kZMaxGroups; ++q)
+        if (q < bt.nw && (int)blockIdx.x >= bt.w[q].blk0) g = q;
+    const ZWinGemm w = bt.w[g];
+    const int W = w.W;
+    const int64_t n = bt.n;
+    const int64_t base = w.lo + (int64_t)((int)blockIdx.x - w.blk0) * kZMG;
+    const int cnt = (int)min<int64_t>(kZMG, w.hi - base);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    constexpr int kKs = kZWin / 4;
+    // right: this lane's X(r_j, k), k = lk, lk + 4, ... (issued first, consumed last)
+    cplx xv[kLeft ? 1 : kKs];
+    const int rj = 16 * wave + li;
+    const bool rv = rj < cnt;
+    if constexpr (!kLeft) {
+        const cplx* xrow = bt.H + (base + min(rj, max(cnt - 1, 0))) + (int64_t)w.s * n;
+#pragma unroll
+        for (int q = 0; q < kKs; ++q) xv[q] = xrow[(int64_t)min(4 * q + lk, W - 1) * n];
+    }
+    {
+        constexpr int kPU = kZWin * kZWin / kZMT;
+        cplx tu[kPU];
+#pragma unroll
+        for (int q = 0; q < kPU; ++q) {
+            const int idx = threadIdx.x + kZMT * q;
+            const int k = idx % kZWin, rho = idx / kZWin;
+            tu[q] = w.U[min(k, W - 1) + min(rho, W - 1) * W];
+        }
+        if constexpr (kLeft) {
+            constexpr int kPX = kZWin * kZMG / kZMT;
+            cplx tx[kPX];
+#pragma unroll
+            for (int q = 0; q < kPX; ++q) {
+                const int idx = threadIdx.x + kZMT * q;
+                const int k = idx % kZWin, c = idx / kZWin;
+                tx[q] = bt.H[(w.s + min(k, W - 1)) + (base + min(c, max(cnt - 1, 0))) * n];
+            }
+#pragma unroll
+            for (int q = 0; q < kPX; ++q) {
+                const int idx = threadIdx.x + kZMT * q;
+                const int k = idx % kZWin, c = idx / kZWin;
+                const bool ok = k < W && c < cnt;
+                xr_s[k + c * kZUP] = ok ? tx[q].re : 0.0;
+                xi_s[k + c * kZUP] = ok ? tx[q].im : 0.0;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kPU; ++q) {
+            const int idx = threadIdx.x + kZMT * q;
+            const int k = idx % kZWin, rho = idx / kZWin;
+            const bool ok = k < W && rho < W;
+            ur[k + rho * kZUP] = ok ? tu[q].re : 0.0;
+            ui[k + rho * kZUP] = ok ? tu[q].im : 0.0;
+        }
+    }
+    __syncthreads();
+    constexpr int kT = kZWin / 16;
+    zdbl4 aR[kT], aI[kT];
+#pragma unroll
+    for (int t = 0; t < kT; ++t) aR[t] = aI[t] = zdbl4{0.0, 0.0, 0.0, 0.0};
+    if constexpr (kLeft) {
+        // D[i][j] = sum_k X(k, c_i) conj(U(k, rho_j)): re = Xr Ur + Xi Ui, im = Xi Ur - Xr Ui
+        const int co = (16 * wave + li) * kZUP;
+#pragma unroll
+        for (int q = 0; q < kKs; ++q) {   // rows k >= W of both LDS images are zero
+            const int k = 4 * q + lk;
+            const double xr = xr_s[co + k], xi = xi_s[co + k];
+            double br[kT], bi[kT];
+#pragma unroll
+            for (int t = 0; t < kT; ++t) {
+                br[t] = ur[k + (16 * t + li) * kZUP];
+                bi[t] = ui[k + (16 * t + li) * kZUP];
+            }
+#pragma unroll
+            for (int t = 0; t < kT; ++t) {
+                aR[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr, br[t], aR[t], 0, 0, 0);
+                aR[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xi, bi[t], aR[t], 0, 0, 0);
+                aI[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xi, br[t], aI[t], 0, 0, 0);
+                aI[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-xr, bi[t], aI[t], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int c = 16 * wave + lk + 4 * r, rho = 16 * t + li;
+                if (c < cnt && rho < W) bt.H[(w.s + rho) + (base + c) * n] = cplx{aR[t][r], aI[t][r]};
+            }
+    } else {
+        // D[i][j] = sum_k U(k, rho_i) X(r_j, k): re = Ur Xr - Ui Xi, im = Ur Xi + Ui Xr
+#pragma unroll
+        for (int q = 0; q < kKs; ++q) {
+            const int k = 4 * q + lk;
+            const bool ok = rv && k < W;
+            const double xr = ok ? xv[q].re : 0.0, xi = ok ? xv[q].im : 0.0;
+            double ar[kT], ai[kT];
+#pragma unroll
+            for (int t = 0; t < kT; ++t) {
+                ar[t] = ur[k + (16 * t + li) * kZUP];
+                ai[t] = ui[k + (16 * t + li) * kZUP];
+            }
+#pragma unroll
+            for (int t = 0; t < kT; ++t) {
+                aR[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[t], xr, aR[t], 0, 0, 0);
+                aR[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ai[t], xi, aR[t], 0, 0, 0);
+                aI[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[t], xi, aI[t], 0, 0, 0);
+                aI[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[t], xr, aI[t], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < kT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rho = 16 * t + lk + 4 * r;
+                if (rv && rho < W) bt.H[(base + rj) + (int64_t)(w.s + rho) * n] = cplx{aR[t][r], aI[t][r]};
+            }
+    }
+}
+
 __global__ void zdiag_sub_kernel(const cplx* H, int64_t n, int ihi, cplx* out) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i > ihi) return;
@@ -575,6 +709,12 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             if (rc != EIGSOL_OK) break;
             hipLaunchKernelGGL(dev::zchase_kernel, dim3(nwin), dim3(1024), 0, st, cb);
             // delayed updates: every left region, then every right region (U_a^H X U_b = (U_a^H X) U_b)
+            // on the matrix cores by default; EIGSOL_ZGEMM_VALU=1: the VALU kernel (8-column workgroups)
+            static const bool valu = [] {
+                const char* e = std::getenv("EIGSOL_ZGEMM_VALU");
+                return e && std::atoi(e) != 0;
+            }();
+            const int per = valu ? dev::kZG : dev::kZMG;
             dev::ZWinGemmBatch lb{H, (int64_t)n, 0, {}}, rb{H, (int64_t)n, 0, {}};
             int nlb = 0, nrb = 0;
             for (int q = 0; q < nwin; ++q) {
@@ -582,15 +722,20 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
                 const int W = w.e - w.s;
                 if (w.e <= ihi) {
                     lb.w[lb.nw++] = dev::ZWinGemm{w.s, W, (int64_t)w.e, (int64_t)ihi + 1, nlb, w.U};
-                    nlb += (ihi + 1 - w.e + dev::kZG - 1) / dev::kZG;
+                    nlb += (ihi + 1 - w.e + per - 1) / per;
                 }
                 if (w.s > l) {
                     rb.w[rb.nw++] = dev::ZWinGemm{w.s, W, (int64_t)l, (int64_t)w.s, nrb, w.U};
-                    nrb += (w.s - l + dev::kZG - 1) / dev::kZG;
+                    nrb += (w.s - l + per - 1) / per;
                 }
             }
-            if (nlb > 0) hipLaunchKernelGGL(dev::zwin_gemm_kernel<true>, dim3(nlb), dim3(128), 0, st, lb);
-            if (nrb > 0) hipLaunchKernelGGL(dev::zwin_gemm_kernel<false>, dim3(nrb), dim3(128), 0, st, rb);
+            if (valu) {
+                if (nlb > 0) hipLaunchKernelGGL(dev::zwin_gemm_kernel<true>, dim3(nlb), dim3(128), 0, st, lb);
+                if (nrb > 0) hipLaunchKernelGGL(dev::zwin_gemm_kernel<false>, dim3(nrb), dim3(128), 0, st, rb);
+            } else {
+                if (nlb > 0) hipLaunchKernelGGL(dev::zwin_gemm_mfma<true>, dim3(nlb), dim3(dev::kZMT), 0, st, lb);
+                if (nrb > 0) hipLaunchKernelGGL(dev::zwin_gemm_mfma<false>, dim3(nrb), dim3(dev::kZMT), 0, st, rb);
+            }
             t0 = t1;
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "complex QR: launch"); break; }
