@@ -158,7 +158,8 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes_per_iteration, int32
  *          5 = CSR in 64-row slices, one row per lane (tiles = slices);
  *          6 = CSR one row per lane (single-precision fallback layout);
  *          7 = shifted inverse, ILU(0)-preconditioned GMRES (general sparse; bytes and tiles of the
- *              last solve: algorithmic bytes of all its steps, Arnoldi steps) */
+ *              last solve: algorithmic bytes of all its steps, Arnoldi steps);
+ *          8 = shifted inverse, RCM-banded direct LU (general sparse; tiles = kl + ku) */
 
 /* ---------------------------------------------------------------- shifted inverse iteration
  * shiftedInversePowerMethod<S>(M, ShiftedSolverOptions<S>{sigma, maxIter, tol})
@@ -166,10 +167,13 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes_per_iteration, int32
  * session creation (the reference refactors every iteration, solve_shifted.hpp:75-79,96-106):
  *   - triangular CSR (upper or lower; a missing diagonal counts as 0, solve_shifted.hpp:100-102):
  *     the matrix is its own factor; one sync-free level-ordered triangular solve per iteration;
- *   - dense, and non-triangular CSR up to n = 16384: partial-pivot LU on the device;
- *   - non-triangular CSR above that: ILU(0) on the device + restarted GMRES to a 1e-12 relative
- *     residual (EIGSOL_SPARSE_SOLVER=lu|gmres forces either; a solve that cannot reach 1e-8 fails
- *     with EIGSOL_E_SOLVER).
+ *   - non-triangular CSR: reverse Cuthill-McKee + banded partial-pivot LU on the device (a direct
+ *     factor, like SparseLU) when the band fits; otherwise the densified partial-pivot LU up to
+ *     n = 16384, and ILU(0) + restarted GMRES (1e-12 relative residual) above it.  A GMRES solve
+ *     that stalls above 1e-10 falls back to the densified LU where it fits the device, else fails
+ *     with EIGSOL_E_SOLVER ("solve_shifted: SparseLU solve failed (...)", solve_shifted.hpp:112-114).
+ *     EIGSOL_SPARSE_SOLVER=band|lu|gmres forces a path, EIGSOL_GMRES_FALLBACK=0 disables the fallback;
+ *   - dense: partial-pivot LU on the device.
  * sigma points at ONE scalar of the matrix dtype.  A zero pivot of a sparse matrix fails with
  * EIGSOL_E_SOLVER ("solve_shifted: SparseLU factorization failed", solve_shifted.hpp:108-110).
  * The returned handle is a session: use eigsol_power_begin/step/query/finish/trace/kernel_info.

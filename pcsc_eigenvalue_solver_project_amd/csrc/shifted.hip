@@ -25,6 +25,7 @@
 #include <cstring>
 #include <vector>
 
+#include "band_lu.hpp"
 #include "kernels_common.hpp"
 #include "mfma_rankk.hpp"
 
@@ -41,8 +42,11 @@ struct ShiftFactor {
     eigsol_ctx* ctx = nullptr;
     int dtype = EIGSOL_F64;
     int64_t n = 0;
-    int kind = 0;                 // 0 triangular CSR, 1 dense LU, 2 ILU(0)-preconditioned GMRES
+    int kind = 0;                 // 0 triangular CSR, 1 dense LU, 2 ILU(0)-preconditioned GMRES, 3 band LU
     GmresSolver* gm = nullptr;    // kind 2 (gmres.hip)
+    BandFactor* band = nullptr;   // kind 3 (band_lu.hip)
+    eigsol_csr* src = nullptr;    // kind 2: A, retained for the densified-LU fallback
+    int fell_back = 0;            // kind 1 reached through the GMRES fallback
     double sig_re = 0.0, sig_im = 0.0;
     // triangular: everything indexed by solve position (rows sorted by level, levels padded)
     int upper = 1;
@@ -1218,6 +1222,8 @@ template <class S> static bool h_zero(S a) {
 static void shift_free(ShiftFactor* f) {
     if (!f) return;
     if (f->gm) gmres_free(f->gm);
+    if (f->band) band_free(f->band);
+    if (f->src) csr_release(f->src);
     hipSetDevice(f->ctx->device);
     hipStreamSynchronize(f->ctx->stream);
     for (void* p : {(void*)f->order, f->z[0], f->z[1],
@@ -1420,15 +1426,69 @@ static const void* slice_kernel_ptr(int b, bool iter) {
                 : reinterpret_cast<const void*>(dev::sptrsv_slice_kernel<S, 16, false>);
 }
 
-// General (non-triangular) sparse: densified LU up to this order, ILU(0)-preconditioned GMRES above
-// it (EIGSOL_SPARSE_SOLVER=lu|gmres forces one).  The dense LU is a direct factor like the
-// reference's SparseLU; GMRES keeps O(nnz) memory for any order.
-static bool general_sparse_uses_gmres(int64_t n) {
+// General (non-triangular) sparse solver choice; EIGSOL_SPARSE_SOLVER=band|lu|gmres forces one.
+//   band  - RCM + banded partial-pivot LU (band_lu.hip): a direct factor, like the reference's
+//           SparseLU, chosen when the RCM band fits the solve kernel's LDS window and the device,
+//           and (up to n = 16384) is smaller than the dense matrix;
+//   lu    - the densified partial-pivot LU, up to n = 16384;
+//   gmres - ILU(0) + GMRES for larger patterns whose RCM band is too wide.  A GMRES that stalls
+//           (or an ILU(0) zero pivot) falls back to the densified LU wherever the dense factor fits
+//           the device (EIGSOL_GMRES_FALLBACK=0 disables it); otherwise the solve fails with
+//           EIGSOL_E_SOLVER, as SparseLU reports a failed solve (solve_shifted.hpp:112-114).
+enum SparseSolver { kSolverBand, kSolverLU, kSolverGMRES };
+
+static double device_free_bytes() {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0.0;
+    return (double)fr;
+}
+
+static SparseSolver general_sparse_solver(int64_t n, size_t sb, const BandPlan& plan, bool& forced) {
+    forced = false;
     if (const char* e = std::getenv("EIGSOL_SPARSE_SOLVER")) {
-        if (!std::strcmp(e, "gmres")) return true;
-        if (!std::strcmp(e, "lu")) return false;
+        forced = true;
+        if (!std::strcmp(e, "gmres")) return kSolverGMRES;
+        if (!std::strcmp(e, "lu")) return kSolverLU;
+        if (!std::strcmp(e, "band")) return kSolverBand;
+        forced = false;
     }
-    return n > 16384;
+    const double dense = (double)n * (double)n * (double)sb;
+    const bool band_fits = plan.ok && plan.bytes <= 0.6 * device_free_bytes();
+    if (band_fits && (n > 16384 || plan.bytes < dense)) return kSolverBand;
+    return n > 16384 ? kSolverGMRES : kSolverLU;
+}
+
+static bool gmres_fallback_enabled() {
+    const char* e = std::getenv("EIGSOL_GMRES_FALLBACK");
+    return !(e && !std::strcmp(e, "0"));
+}
+
+// GMRES failed (stalled solve, or ILU(0) zero pivot): switch the factor to the densified LU of A
+// (retained in f->src) when it fits the device; otherwise keep GMRES's error.
+template <class S>
+static int gmres_dense_fallback(ShiftFactor* f, int rc_gmres) {
+    if constexpr (!kDenseLU<S>) {
+        return rc_gmres;
+    } else {
+        const int64_t n = f->n;
+        const double bytes = (double)n * (double)n * (double)sizeof(S);
+        if (!gmres_fallback_enabled() || !f->src || n > INT32_MAX / 2 || bytes > 0.8 * device_free_bytes())
+            return rc_gmres;
+        hipStream_t st = f->ctx->stream;
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        if (f->gm) { gmres_free(f->gm); f->gm = nullptr; }
+        if (f->work) { hipFree(f->work); f->work = nullptr; }
+        if (f->wave_part) { hipFree(f->wave_part); f->wave_part = nullptr; }
+        EIGSOL_HIP(hipMalloc(&f->lu, (size_t)bytes));
+        EIGSOL_HIP(hipMemsetAsync(f->lu, 0, (size_t)bytes, st));
+        hipLaunchKernelGGL((dev::densify_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->src->rowptr,
+                           f->src->col, static_cast<const S*>(f->src->val), n, static_cast<S*>(f->lu));
+        EIGSOL_TRY(dense_lu_factor<S>(f, true));
+        csr_release(f->src);
+        f->src = nullptr;
+        f->fell_back = 1;
+        return EIGSOL_OK;
+    }
 }
 
 template <class S>
@@ -1468,15 +1528,35 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
             return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: single-precision factors exist for triangular "
                                               "sparse matrices only");
         } else {
-        if (general_sparse_uses_gmres(n)) {
+        BandPlan plan;
+        band_plan(A->dtype, n, rp.data(), ci.data(), plan);
+        bool forced = false;
+        const SparseSolver solver = general_sparse_solver(n, sizeof(S), plan, forced);
+        if (solver == kSolverBand) {
+            if (!plan.ok) {
+                shift_free(f);
+                return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: the RCM band (kl " + std::to_string(plan.kl) +
+                                                      ", ku " + std::to_string(plan.ku) +
+                                                      ") is too wide for the band solve");
+            }
+            rc = band_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, plan, &f->band);
+            if (rc != EIGSOL_OK) { shift_free(f); return rc; }
+            f->kind = 3;
+            *out = f;
+            return EIGSOL_OK;
+        }
+        if (solver == kSolverGMRES) {
             rc = gmres_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, &f->gm);
             f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 1023) / 1024));
             if (rc == EIGSOL_OK && (hipMalloc(&f->work, 64) != hipSuccess ||
                                     hipMalloc(&f->wave_part, (size_t)f->red_grid * sizeof(dev::part4)) != hipSuccess ||
                                     hipMemsetAsync(f->work, 0, 64, st) != hipSuccess))
                 rc = fail(EIGSOL_E_HIP, "solve_shifted: GMRES work buffers");
-            if (rc != EIGSOL_OK) { shift_free(f); return rc; }
             f->kind = 2;
+            f->src = A;
+            csr_retain(A);
+            if (rc == EIGSOL_E_SOLVER) rc = gmres_dense_fallback<S>(f, rc);   // ILU(0) zero pivot
+            if (rc != EIGSOL_OK) { shift_free(f); return rc; }
             *out = f;
             return EIGSOL_OK;
         }
@@ -1834,7 +1914,12 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
     if (f->kind == 2) {
         // ILU(0)-preconditioned GMRES: host-driven (one sync per Arnoldi step), so the iteration is
         // prologue launch -> host reads the stop decision -> solve -> partials launch
-        if (!iter) return gmres_solve(f->gm, b, 0.0, y);
+        if (!iter) {
+            const int rc = gmres_solve(f->gm, b, 0.0, y);
+            if (rc != EIGSOL_E_SOLVER) return rc;
+            EIGSOL_TRY(gmres_dense_fallback<S>(f, rc));
+            return shift_launch_t<S>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+        }
         dev::TriArgs<S> a{};
         a.n = f->n;
         a.work = f->work;
@@ -1854,11 +1939,20 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         EIGSOL_HIP(hipMemcpyAsync(&nrm, &ctl->st[parity ^ 1].nrm, sizeof(nrm), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(hipStreamSynchronize(st));
         if (done) return EIGSOL_OK;
-        EIGSOL_TRY(gmres_solve(f->gm, parity ? buf0 : buf1, nrm, parity ? buf1 : buf0));
+        const int rc = gmres_solve(f->gm, parity ? buf0 : buf1, nrm, parity ? buf1 : buf0);
+        if (rc == EIGSOL_E_SOLVER) {
+            // switch to the densified LU and redo this launch on it: the dense kernel's prologue
+            // re-evaluates the same decision from the same carry record (idempotent)
+            EIGSOL_TRY(gmres_dense_fallback<S>(f, rc));
+            return shift_launch_t<S>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+        }
+        EIGSOL_TRY(rc);
         hipLaunchKernelGGL((dev::shift_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a, parity);
         EIGSOL_HIP(hipGetLastError());
         return EIGSOL_OK;
     }
+    if (f->kind == 3)
+        return band_launch(f->band, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
     if (f->kind == 0) {
         dev::TriArgs<S> a{};
         a.order = f->order;
@@ -2019,6 +2113,9 @@ void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* 
     if (f->kind == 2) {
         gmres_info(f->gm, bytes, tiles);
         if (variant) *variant = 7;
+    } else if (f->kind == 3) {
+        band_info(f->band, bytes, tiles);
+        if (variant) *variant = 8;
     } else if (f->kind == 0) {
         if (bytes) *bytes = (sb + 4.0) * (double)f->nnz_total + 4.0 * (n + 1.0) + 2.0 * sb * n;
         if (variant) *variant = 3;

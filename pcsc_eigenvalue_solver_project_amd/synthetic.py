@@ -164,6 +164,39 @@ def general_complex(n: int, k: int, seed: int = 42, target=1.5 * np.exp(0.7j), g
     return np.cumsum(rowptr).astype(np.int32), cols.astype(np.int32), vals, d
 
 
+def convdiff_complex(nx: int, seed: int = 2026, beta: float = 0.1, pert: float = 0.2, permute: bool = True):
+    """General complex sparse matrix whose LU has real fill: a 2-D convection-diffusion 5-point
+    stencil on an nx x nx grid (diagonal 4, neighbours -1 -/+ beta, -1 -/+ beta/2: nonsymmetric),
+    every entry multiplied by 1 + pert * (u + i v), u, v ~ U(-1, 1), then a random symmetric
+    permutation P A P^T (so neither the pattern nor its natural ordering is banded or triangular).
+    n = nx^2, <= 5 entries per row; the spectrum lies around (0, 8) with clustered interior
+    eigenvalues.  Returns (rowptr, colidx, values)."""
+    rng = np.random.default_rng([seed, 9])
+    n = nx * nx
+    idx = np.arange(n, dtype=np.int64)
+    ix, iy = idx % nx, idx // nx
+    rows, cols = [idx], [idx]
+    vals = [4.0 + pert * (rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n))]
+    for dx, dy, c in ((1, 0, -1 - beta), (-1, 0, -1 + beta), (0, 1, -1 - 0.5 * beta), (0, -1, -1 + 0.5 * beta)):
+        m = (ix + dx >= 0) & (ix + dx < nx) & (iy + dy >= 0) & (iy + dy < nx)
+        r = idx[m]
+        rows.append(r)
+        cols.append(r + dx + dy * nx)
+        k = int(m.sum())
+        vals.append(c * (1 + pert * (rng.uniform(-1, 1, k) + 1j * rng.uniform(-1, 1, k))))
+    rows, cols, vals = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
+    if permute:
+        p = rng.permutation(n)            # new index of old row i: inv[i]; P A P^T
+        inv = np.empty(n, np.int64)
+        inv[p] = np.arange(n)
+        rows, cols = inv[rows], inv[cols]
+    order = np.lexsort((cols, rows))
+    rows, cols, vals = rows[order], cols[order], vals[order]
+    rowptr = np.zeros(n + 1, np.int64)
+    np.add.at(rowptr, rows + 1, 1)
+    return np.cumsum(rowptr).astype(np.int32), cols.astype(np.int32), vals
+
+
 def start_vector(n: int, dtype=np.float64, seed: int = 7, row0: int = 0) -> np.ndarray:
     """x0 of SURVEY §8d: U(-1, 1) per (re, im) component, seed 7 (normalised by the solver).
     Entries [row0, row0 + n) of the global start vector, drawn in the generators' fixed chunks, so
