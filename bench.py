@@ -65,21 +65,42 @@ def gen(kind, n_global, k, row0, nrows):
     return S.uniform(n_global, k, row0=row0, nrows=nrows)
 
 
-def pmc_traffic(workload, kernel):
-    """HBM bytes per launch of the same kernel on the same workload, from the committed rocprofv3
-    PMC summary (profiles/, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md); PMC counters
-    cannot be read from inside a timed run, so the profile is a separate pass of this workload."""
+def kernel_key(name):
+    """'void eigsol::dev::csr_slice_kernel<double, true, 12, false, false>(eigsol::dev::CsrArgs<double>, int)'
+    -> 'csr_slice_kernel<double, true, 12, false, false>' (template instantiation, no scope/arguments)."""
+    name = (name or "").strip()
+    if name.startswith("void "):
+        name = name[5:]
+    depth, cut = 0, len(name)
+    for i, ch in enumerate(name):          # drop the argument list: first '(' outside the template brackets
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+    name = name[:cut]
+    head = name.split("<", 1)
+    return head[0].split("::")[-1] + ("<" + head[1] if len(head) > 1 else "")
+
+
+def pmc_traffic(workload, kernel_name):
+    """HBM bytes per launch of the SAME kernel instantiation on the same workload, from the
+    committed rocprofv3 PMC summary (profiles/, FETCH_SIZE x 2 + WRITE_SIZE per MI355X_MICROARCH.md);
+    PMC counters cannot be read from inside a timed run, so the profile is a separate pass of this
+    workload.  A summary whose kernel string is a different instantiation is not used."""
     import glob
     best = None
+    want = kernel_key(kernel_name)
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_*.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        kn = d.get("kernel") or ""
-        if "hbm_traffic_bytes_per_launch" in d and kernel.split(" ")[0] in kn:
+        if "hbm_traffic_bytes_per_launch" in d and want and kernel_key(d.get("kernel")) == want:
             best = {"hbm_traffic_bytes_per_launch": round(d["hbm_traffic_bytes_per_launch"]),
-                    "source": os.path.relpath(f, ROOT)}
+                    "source": os.path.relpath(f, ROOT), "kernel": d.get("kernel")}
     return best
 
 
@@ -255,7 +276,7 @@ def run_config2(E, ctx, no_cpu):
         ev = r.eigenvalues_complex
         d, j = cKDTree(np.c_[ref.real, ref.imag]).query(np.c_[ev.real, ev.imag], k=1)
         out["vs_lapack_fixture"] = {"max_abs_diff": float(d.max()), "one_to_one": bool(len(np.unique(j)) == n)}
-    prof = os.path.join(ROOT, "profiles", "r01_qr4096_mfma.json")
+    prof = os.path.join(ROOT, "profiles", "r03_qr4096_mfma.json")
     if os.path.exists(prof):
         d = json.load(open(prof))
         out["mfma"] = {"gemm_TFLOPs": round(d["gemm_TFLOPs"], 2), "peak_TFLOPs": d["mfma_peak_TFLOPs"],
@@ -263,8 +284,9 @@ def run_config2(E, ctx, no_cpu):
                        "rank_update_TFLOPs": round(d.get("rank_update_TFLOPs") or 0.0, 2),
                        "rank_update_utilisation": round(d.get("rank_update_mfma_utilisation") or 0.0, 4),
                        "francis_window_gemm_share": round(d.get("francis_window_gemm_share") or 0.0, 4),
-                       "source": "profiles/r01_qr4096_mfma.json (rocprofv3 kernel times of the Hessenberg "
-                                 "trailing-update GEMMs on v_mfma_f64_16x16x4_f64: the whole set incl. the "
+                       "source": "profiles/r03_qr4096_mfma.json (rocprofv3 kernel times of the shipped path, "
+                                 "cooperative Hessenberg panel issued by an ordinary launch of the same kernel: "
+                                 "the trailing-update GEMMs on v_mfma_f64_16x16x4_f64, the whole set incl. the "
                                  "split-K W = V^T A, and the single rank-2nb update alone)"}
     if not no_cpu:
         from oracle import oracle as O
@@ -485,6 +507,7 @@ def main():
     opts = E.SolverOptions(2**31 - 1, -1.0)   # tol < 0: the reference loop never stops early
     sess.begin(opts, x0)
     info = sess.kernel_info()
+    kname = sess.kernel_name()
     sess.step(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
@@ -551,7 +574,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": info["kernel"] + ", fused power iteration",
+                "kernel": kname or info["kernel"],
+                "kernel_role": info["kernel"] + ", fused power iteration",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -563,10 +587,11 @@ def main():
             "cpu_baseline": None,
         }
     if rank == 0:
-        pmc = pmc_traffic(args.workload, info["kernel"])
+        pmc = pmc_traffic(args.workload, kname)
         if pmc:
             out["roofline"]["traffic"] = pmc["hbm_traffic_bytes_per_launch"]
             out["roofline"]["traffic_source"] = pmc["source"]
+            out["roofline"]["traffic_kernel"] = pmc["kernel"]
     if world == 1 and rank == 0:
         out["roofline"]["measured_hbm"] = measured_hbm(torch, torch_stream)
     if not args.no_extras and world == 1:

@@ -152,6 +152,10 @@ int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int3
  * one fused iteration and the grid used. */
 int eigsol_power_kernel_info(eigsol_power* s, double* bytes_per_iteration, int32_t* grid_blocks,
                              int32_t* tiles, int32_t* variant);
+/* Demangled name of the kernel a CSR power session launches per iteration (e.g.
+ * "void eigsol::dev::csr_slice_kernel<double, true, 12, false, false>(...)"), the string rocprofv3
+ * reports; empty for other sessions. */
+int eigsol_power_kernel_name(eigsol_power* s, char* buf, size_t capacity);
 /* variant: 0 = CSR, x gathered from HBM; 1 = CSR, x window staged in LDS; 2 = dense GEMV;
  *          3 = shifted inverse, sync-free triangular solve (tiles = dependency levels);
  *          4 = shifted inverse, dense LU substitution;

@@ -297,6 +297,12 @@ class PowerSession:
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?")}
 
+    def kernel_name(self) -> str:
+        """Demangled name of the per-iteration kernel (CSR power sessions), as rocprofv3 reports it."""
+        buf = C.create_string_buffer(512)
+        call("eigsol_power_kernel_name", self.handle, buf, 512)
+        return buf.value.decode()
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             lib().eigsol_power_destroy(self.handle)

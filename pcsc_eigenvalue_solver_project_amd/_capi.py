@@ -99,6 +99,7 @@ SIGNATURES = {
     "eigsol_power_finish": [_vp, _vp, _vp, C.c_int, _pi32, _pi32],
     "eigsol_power_trace": [_vp, _vp, _i32, _pi32],
     "eigsol_power_kernel_info": [_vp, _pd, _pi32, _pi32, _pi32],
+    "eigsol_power_kernel_name": [_vp, C.c_char_p, C.c_size_t],
     "eigsol_dist_unique_id_bytes": [],
     "eigsol_dist_get_unique_id": [_vp],
     "eigsol_dist_loopback_id": [C.c_int, _vp],

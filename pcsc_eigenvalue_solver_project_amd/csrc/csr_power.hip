@@ -1509,6 +1509,13 @@ static const void* power_kernel_ptr(const eigsol_csr* A, bool peer = false) {
                            : reinterpret_cast<const void*>(csr_kernel<S, true>);
 }
 
+const void* csr_power_kernel(const eigsol_csr* A, bool peer) {
+    return A->dtype == EIGSOL_C128  ? power_kernel_ptr<cplx>(A, peer)
+           : A->dtype == EIGSOL_F32 ? power_kernel_ptr<float>(A, peer)
+           : A->dtype == EIGSOL_C64 ? power_kernel_ptr<cplxf>(A, peer)
+                                    : power_kernel_ptr<double>(A, peer);
+}
+
 int csr_grid(eigsol_csr* A, int* grid, bool peer) {
     const void* k = A->dtype == EIGSOL_C128  ? power_kernel_ptr<cplx>(A, peer)
                     : A->dtype == EIGSOL_F32 ? power_kernel_ptr<float>(A, peer)

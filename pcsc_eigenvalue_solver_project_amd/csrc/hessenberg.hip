@@ -682,8 +682,16 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
             EIGSOL_HIP(hipMemsetAsync(bar, 0, 64, st));
             dev::CoopArgs ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err};
             void* kargs[] = {&ca};
-            EIGSOL_HIP(hipLaunchCooperativeKernel(coop_kernel, dim3(dev::kCoopBlocks), dim3(dev::kCoopThreads), kargs,
-                                                  coop_lds, st));
+            // EIGSOL_HESS_COOP_PLAIN=1: the SAME panel kernel through an ordinary launch, for profiling
+            // only (rocprofv3 7.2 crashes at exit after any cooperative launch, tools/coop_prof_repro.hip);
+            // its kCoopBlocks blocks are far fewer than the CUs, so on an idle device all are resident,
+            // and the grid barrier's bounded spin reports a failure instead of hanging otherwise
+            static const bool plain = std::getenv("EIGSOL_HESS_COOP_PLAIN") != nullptr;
+            if (plain)
+                EIGSOL_HIP(hipLaunchKernel(coop_kernel, dim3(dev::kCoopBlocks), dim3(dev::kCoopThreads), kargs, coop_lds, st));
+            else
+                EIGSOL_HIP(hipLaunchCooperativeKernel(coop_kernel, dim3(dev::kCoopBlocks), dim3(dev::kCoopThreads), kargs,
+                                                      coop_lds, st));
         }
         for (int i = 0; !coop && i < nbp; ++i) {
             const int j = k + i;

@@ -14,10 +14,13 @@
 #include <cstdlib>
 #include <thread>
 
+#include <cxxabi.h>
+
 #include "kernels_common.hpp"
 
 namespace eigsol {
 int csr_grid(eigsol_csr* A, int* grid, bool peer = false);
+const void* csr_power_kernel(const eigsol_csr* A, bool peer);
 int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
                      const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
                      int parity, int grid, const dev::PeerArgs* peer = nullptr);
@@ -545,6 +548,22 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
         if (variant) *variant = 2;
     }
     if (grid) *grid = s->grid;
+    return EIGSOL_OK;
+}
+
+// Demangled name of the fused power-iteration kernel a CSR session launches (the string rocprofv3
+// prints for it), so roofline figures can be matched to the exact template instantiation.
+int eigsol_power_kernel_name(eigsol_power* s, char* buf, size_t cap) {
+    if (!s || !buf || cap == 0) return fail(EIGSOL_E_INVALID, "eigsol_power_kernel_name: null argument");
+    buf[0] = 0;
+    if (s->shift || !s->csr) return EIGSOL_OK;   // named for CSR power sessions only
+    const void* k = csr_power_kernel(s->csr, s->transport == EIGSOL_TRANSPORT_PEER);
+    const char* m = k ? hipKernelNameRefByPtr(k, s->ctx->stream) : nullptr;
+    if (!m) return EIGSOL_OK;
+    int st = 0;
+    char* d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+    std::snprintf(buf, cap, "%s", (st == 0 && d) ? d : m);
+    std::free(d);
     return EIGSOL_OK;
 }
 
