@@ -1,14 +1,17 @@
-// Blocked Householder Hessenberg reduction (real, gfx950), the reference's reflector convention.
+// Blocked Householder Hessenberg reduction (gfx950), the reference's reflector convention, for
+// S = double and S = std::complex<double> (cplx).
 //
-// to_hessenberg_dense<S> (src/qr_method/to_hessenberg.hpp:38-77) applies H_j = I - 2 v_j v_j^T
+// to_hessenberg_dense<S> (src/qr_method/to_hessenberg.hpp:38-77) applies H_j = I - 2 v_j v_j^H
 // from both sides for every column j.  Here the reflectors of a panel of nb columns are
-// accumulated in compact-WY form Q = H_k ... H_{k+nb-1} = I - V T V^T (T upper triangular,
+// accumulated in compact-WY form Q = H_k ... H_{k+nb-1} = I - V T V^H (T upper triangular,
 // T(i,i) = 2) together with Y = A V T, and the trailing matrix is updated once per panel:
-//     A <- Q^T (A Q) = (I - V T^T V^T)(A - Y V^T)
-// (the dlahr2/dgehrd organisation).  Per panel column the only full-matrix pass is the GEMV
-// y = A(:, j+1:n) v_j (BLAS-2, half the flops); everything else is three GEMMs per panel.
-// Reflectors are generated exactly as the reference does (alpha = -sign(x0) ||x||, skipped when
-// ||x(1:)|| == 0), so H matches the unblocked reduction to rounding.
+//     A <- Q^H (A Q) = (I - V T^H V^H)(A - Y V^H)
+// (the dlahr2/dgehrd organisation; zlahr2/zgehrd for complex S).  Per panel column the only
+// full-matrix pass is the GEMV y = A(:, j+1:n) v_j (BLAS-2, half the flops); everything else is
+// GEMMs per panel.  Reflectors are generated exactly as the reference does (alpha =
+// -phase(x0) ||x||, phase = x0 / |x0| (1 at x0 = 0), skipped when ||x(1:)|| == 0), so H matches the
+// unblocked reduction to rounding.  For real S every conjugation below is the identity and the
+// arithmetic is the real path's, operation for operation.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -20,91 +23,46 @@
 namespace eigsol {
 namespace dev {
 
-constexpr int kPanel = 32;          // reflectors per panel
+// Per-scalar configuration: panel width (complex panels are half as wide, so the rank-2 nb
+// trailing update stays within rankk_mfma's K <= 32 for cplx), the largest order the per-column
+// panel keeps in LDS, and the largest order of the cooperative panel (v staged in LDS).
+template <class S> struct HessCfg;
+template <> struct HessCfg<double> {
+    static constexpr int NB = 32;
+    static constexpr int kMaxLdsN = 16384;   // 128 KiB
+    static constexpr int kCoopMaxN = 8192;   // v in LDS (64 KiB) and at most 2 rows per lane
+};
+template <> struct HessCfg<cplx> {
+    static constexpr int NB = 16;
+    static constexpr int kMaxLdsN = 8192;    // 128 KiB
+    static constexpr int kCoopMaxN = 4096;   // v (64 KiB) + the partial / row buffers: < 160 KiB
+};
+constexpr int kPanel = 32;          // the widest panel (array bounds)
 constexpr int kGemvCols = 128;      // columns per GEMV partial
-constexpr int kMaxLdsN = 16384;     // panel column kept in LDS (128 KiB)
 
-// block (1024 threads) sum of kPanel partials per thread -> sw[0..cnt)
-__device__ __forceinline__ void block_sum_vec(double (&p)[kPanel], int cnt, double* red /*16*kPanel*/,
-                                              double* sw) {
-    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
-#pragma unroll
-    for (int c = 0; c < kPanel; ++c) {
-        if (c < cnt) {                      // static register index (no scratch)
-            const double s = wave_sum(p[c]);
-            if (ln == 0) red[w * kPanel + c] = s;
-        }
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < cnt) {
-        double s = 0.0;
-        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) s += red[q * kPanel + threadIdx.x];
-        sw[threadIdx.x] = s;
-    }
-    __syncthreads();
+__device__ __forceinline__ double cj(double a) { return a; }
+__device__ __forceinline__ cplx cj(cplx a) { return cplx{a.re, -a.im}; }
+__device__ __forceinline__ double wsum(double v) { return wave_sum(v); }
+__device__ __forceinline__ cplx wsum(cplx v) { return cplx{wave_sum(v.re), wave_sum(v.im)}; }
+__device__ __forceinline__ void st_ag(double* p, double v) { st_agent(p, v); }
+__device__ __forceinline__ void st_ag(cplx* p, cplx v) {
+    st_agent(&p->re, v.re);
+    st_agent(&p->im, v.im);
 }
+__device__ __forceinline__ double ld_ag(const double* p) { return ld_agent(p); }
+__device__ __forceinline__ cplx ld_ag(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
+__device__ __forceinline__ double scal(double a, double s) { return a * s; }
+__device__ __forceinline__ cplx scal(cplx a, double s) { return cplx{a.re * s, a.im * s}; }
+__device__ __forceinline__ double two_x(double a) { return 2.0 * a; }
+__device__ __forceinline__ cplx two_x(cplx a) { return cplx{2.0 * a.re, 2.0 * a.im}; }
+__device__ __forceinline__ double neg2(double a) { return -2.0 * a; }
+__device__ __forceinline__ cplx neg2(cplx a) { return cplx{-2.0 * a.re, -2.0 * a.im}; }
 
-// Panel column j (local index i): apply the panel's earlier reflectors from the right (via Y) and
-// the left (via V, T), generate reflector i from rows j+1.., store the reduced column, and
-// t = V(:, 0:i)^T v_i for the T / Y recursions.
-__global__ __launch_bounds__(1024) void hess_panel_col(double* A, int n, int k, int j, int i, double* V,
-                                                       const double* Y, const double* T, double* tvec,
-                                                       int* skip) {
-    extern __shared__ double a[];          // column j (n doubles)
-    __shared__ double red[16 * kPanel];
-    __shared__ double sw[kPanel];
-    __shared__ double sw2[kPanel];
-    __shared__ double vj[kPanel];
-    __shared__ double s_tail;
-    const int tid = threadIdx.x, nt = blockDim.x;
-    if (tid < i) vj[tid] = V[j + (int64_t)tid * n];   // row j of V
-    __syncthreads();
-    // right: a -= Y(:, 0:i) V(j, 0:i)^T
-    for (int r = tid; r < n; r += nt) {
-        double x = A[r + (int64_t)j * n];
-        for (int c = 0; c < i; ++c) x -= Y[r + (int64_t)c * n] * vj[c];
-        a[r] = x;
-    }
-    __syncthreads();
-    // left: w = V^T a (rows k+1..), w = T^T w, a -= V w
-    if (i > 0) {
-        double p[kPanel];
-#pragma unroll
-        for (int c = 0; c < kPanel; ++c) p[c] = 0.0;
-        for (int r = k + 1 + tid; r < n; r += nt) {
-            const double x = a[r];
-#pragma unroll
-            for (int c = 0; c < kPanel; ++c)
-                if (c < i) p[c] += V[r + (int64_t)c * n] * x;
-        }
-        block_sum_vec(p, i, red, sw);
-        if (tid < i) {
-            double s = 0.0;
-            for (int c = 0; c <= tid; ++c) s += T[c + tid * kPanel] * sw[c];   // (T^T w)_tid
-            sw2[tid] = s;
-        }
-        __syncthreads();
-        for (int r = k + 1 + tid; r < n; r += nt) {
-            double x = a[r];
-            for (int c = 0; c < i; ++c) x -= V[r + (int64_t)c * n] * sw2[c];
-            a[r] = x;
-        }
-        __syncthreads();
-    }
-    // reflector from a(j+1 : n)
-    double tl = 0.0;
-    for (int r = j + 2 + tid; r < n; r += nt) tl += a[r] * a[r];
-    {
-        double pp[kPanel];
-        pp[0] = tl;
-        block_sum_vec(pp, 1, red, sw);
-        if (tid == 0) s_tail = sw[0];
-        __syncthreads();
-    }
-    const double tail = s_tail;
-    const double x0 = a[j + 1];
-    bool sk = tail == 0.0;
-    double v0 = 0.0, rv = 0.0, alpha = 0.0;
+// The reference's reflector from x0 = a(j+1) and tail = ||a(j+2:)||^2 (to_hessenberg.hpp:45-65):
+// alpha = -phase(x0) ||x||, v0 = x0 - alpha, rv = 1 / ||(v0, x(1:))||; sk when skipped.
+__device__ __forceinline__ void hess_reflector(double x0, double tail, bool& sk, double& v0, double& rv, double& alpha) {
+    sk = tail == 0.0;
+    v0 = 0.0; rv = 0.0; alpha = 0.0;
     if (!sk) {
         const double nx = sqrt(tail + x0 * x0);
         const double sign = x0 == 0.0 ? 1.0 : (x0 > 0.0 ? 1.0 : -1.0);
@@ -114,75 +72,276 @@ __global__ __launch_bounds__(1024) void hess_panel_col(double* A, int n, int k, 
         if (vn == 0.0) sk = true;
         else rv = 1.0 / vn;
     }
-    double* vcol = V + (int64_t)i * n;
+}
+__device__ __forceinline__ void hess_reflector(cplx x0, double tail, bool& sk, cplx& v0, double& rv, cplx& alpha) {
+    sk = tail == 0.0;
+    v0 = cplx{0.0, 0.0}; rv = 0.0; alpha = cplx{0.0, 0.0};
+    if (!sk) {
+        const double nx = sqrt(tail + sq_abs(x0));
+        cplx ph{1.0, 0.0};
+        if (x0.re != 0.0 || x0.im != 0.0) {
+            const double ia = 1.0 / hypot(x0.re, x0.im);   // hh_make_kernel's phase (qr.hip)
+            ph = cplx{x0.re * ia, x0.im * ia};
+        }
+        alpha = cplx{-ph.re * nx, -ph.im * nx};
+        v0 = sub(x0, alpha);
+        const double vn = sqrt(tail + sq_abs(v0));
+        if (vn == 0.0) sk = true;
+        else rv = 1.0 / vn;
+    }
+}
+
+// block (1024 threads) sum of NB partials per thread -> sw[0..cnt)
+template <class S, int NB>
+__device__ __forceinline__ void block_sum_vec(S (&p)[NB], int cnt, S* red /*16*NB*/, S* sw) {
+    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+        if (c < cnt) {                      // static register index (no scratch)
+            const S s = wsum(p[c]);
+            if (ln == 0) red[w * NB + c] = s;
+        }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < cnt) {
+        S s = s_zero<S>();
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) s = add(s, red[q * NB + threadIdx.x]);
+        sw[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+// Panel column j (local index i): apply the panel's earlier reflectors from the right (via Y) and
+// the left (via V, T), generate reflector i from rows j+1.., store the reduced column, and
+// t = V(:, 0:i)^H v_i for the T / Y recursions.
+template <class S>
+__global__ __launch_bounds__(1024) void hess_panel_col(S* A, int n, int k, int j, int i, S* V, const S* Y,
+                                                       const S* T, S* tvec, int* skip) {
+    constexpr int NB = HessCfg<S>::NB;
+    extern __shared__ double a_raw[];      // column j (n scalars)
+    S* a = reinterpret_cast<S*>(a_raw);
+    __shared__ S red[16 * NB];
+    __shared__ S sw[NB];
+    __shared__ S sw2[NB];
+    __shared__ S vj[NB];
+    __shared__ double s_tail;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (tid < i) vj[tid] = cj(V[j + (int64_t)tid * n]);   // conj of row j of V
+    __syncthreads();
+    // right: a -= Y(:, 0:i) V(j, 0:i)^H
     for (int r = tid; r < n; r += nt) {
-        double v = 0.0;
-        if (!sk && r > j) v = (r == j + 1 ? v0 : a[r]) * rv;
+        S x = A[r + (int64_t)j * n];
+        for (int c = 0; c < i; ++c) x = sub(x, mul(Y[r + (int64_t)c * n], vj[c]));
+        a[r] = x;
+    }
+    __syncthreads();
+    // left: w = V^H a (rows k+1..), w = T^H w, a -= V w
+    if (i > 0) {
+        S p[NB];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) p[c] = s_zero<S>();
+        for (int r = k + 1 + tid; r < n; r += nt) {
+            const S x = a[r];
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+                if (c < i) p[c] = add(p[c], mul(cj(V[r + (int64_t)c * n]), x));
+        }
+        block_sum_vec<S, NB>(p, i, red, sw);
+        if (tid < i) {
+            S s = s_zero<S>();
+            for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(T[c + tid * NB]), sw[c]));   // (T^H w)_tid
+            sw2[tid] = s;
+        }
+        __syncthreads();
+        for (int r = k + 1 + tid; r < n; r += nt) {
+            S x = a[r];
+            for (int c = 0; c < i; ++c) x = sub(x, mul(V[r + (int64_t)c * n], sw2[c]));
+            a[r] = x;
+        }
+        __syncthreads();
+    }
+    // reflector from a(j+1 : n)
+    double tl = 0.0;
+    for (int r = j + 2 + tid; r < n; r += nt) tl += sq_abs(a[r]);
+    {
+        double pp[kPanel];
+        pp[0] = tl;
+        block_sum_vec<double, kPanel>(pp, 1, reinterpret_cast<double*>(red), reinterpret_cast<double*>(sw));
+        if (tid == 0) s_tail = reinterpret_cast<double*>(sw)[0];
+        __syncthreads();
+    }
+    const double tail = s_tail;
+    const S x0 = a[j + 1];
+    bool sk;
+    S v0, alpha;
+    double rv;
+    hess_reflector(x0, tail, sk, v0, rv, alpha);
+    S* vcol = V + (int64_t)i * n;
+    for (int r = tid; r < n; r += nt) {
+        S v = s_zero<S>();
+        if (!sk && r > j) v = scal(r == j + 1 ? v0 : a[r], rv);
         vcol[r] = v;
     }
     // store the reduced column (alpha on the subdiagonal, zeros below)
     for (int r = tid; r < n; r += nt) {
-        double x = a[r];
+        S x = a[r];
         if (!sk && r == j + 1) x = alpha;
-        if (!sk && r > j + 1) x = 0.0;
+        if (!sk && r > j + 1) x = s_zero<S>();
         A[r + (int64_t)j * n] = x;
     }
     if (tid == 0) *skip = sk ? 1 : 0;
     __syncthreads();
-    // t = V(:, 0:i)^T v (rows j+1..)
+    // t = V(:, 0:i)^H v (rows j+1..)
     if (i > 0) {
-        double p[kPanel];
+        S p[NB];
 #pragma unroll
-        for (int c = 0; c < kPanel; ++c) p[c] = 0.0;
+        for (int c = 0; c < NB; ++c) p[c] = s_zero<S>();
         if (!sk)
             for (int r = j + 1 + tid; r < n; r += nt) {
-                const double v = vcol[r];
+                const S v = vcol[r];
 #pragma unroll
-                for (int c = 0; c < kPanel; ++c)
-                    if (c < i) p[c] += V[r + (int64_t)c * n] * v;
+                for (int c = 0; c < NB; ++c)
+                    if (c < i) p[c] = add(p[c], mul(cj(V[r + (int64_t)c * n]), v));
             }
-        block_sum_vec(p, i, red, sw);
+        block_sum_vec<S, NB>(p, i, red, sw);
         if (tid < i) tvec[tid] = sw[tid];
     }
 }
 
 // y partials: ypart[ch * n + r] = sum_{c in chunk ch} A(r, c) v(c), columns j+1..n-1
-__global__ __launch_bounds__(256) void hess_gemv(const double* A, int n, int c0, const double* v,
-                                                 double* ypart, const int* skip) {
+template <class S>
+__global__ __launch_bounds__(256) void hess_gemv(const S* A, int n, int c0, const S* v, S* ypart, const int* skip) {
     if (*skip) return;
     const int r = blockIdx.x * 256 + threadIdx.x;
     const int ch = blockIdx.y;
     const int cb = c0 + ch * kGemvCols;
     const int ce = min(n, cb + kGemvCols);
     if (r >= n) return;
-    double s = 0.0;
-    for (int c = cb; c < ce; ++c) s += A[r + (int64_t)c * n] * v[c];
+    S s = s_zero<S>();
+    for (int c = cb; c < ce; ++c) s = add(s, mul(A[r + (int64_t)c * n], v[c]));
     ypart[(int64_t)ch * n + r] = s;
 }
 
 // Y(:, i) = 2 (y - Y(:, 0:i) t);  T(0:i, i) = -2 T(0:i, 0:i) t, T(i, i) = 2
-__global__ __launch_bounds__(256) void hess_y(int n, int i, int nch, const double* ypart, const double* tvec,
-                                              double* Y, double* T, const int* skip) {
+template <class S>
+__global__ __launch_bounds__(256) void hess_y(int n, int i, int nch, const S* ypart, const S* tvec, S* Y, S* T,
+                                              const int* skip) {
+    constexpr int NB = HessCfg<S>::NB;
     const int r = blockIdx.x * 256 + threadIdx.x;
     const bool sk = *skip != 0;
     if (r < n) {
-        double y = 0.0;
+        S y = s_zero<S>();
         if (!sk) {
-            for (int ch = 0; ch < nch; ++ch) y += ypart[(int64_t)ch * n + r];
-            for (int c = 0; c < i; ++c) y -= Y[r + (int64_t)c * n] * tvec[c];
+            for (int ch = 0; ch < nch; ++ch) y = add(y, ypart[(int64_t)ch * n + r]);
+            for (int c = 0; c < i; ++c) y = sub(y, mul(Y[r + (int64_t)c * n], tvec[c]));
         }
-        Y[r + (int64_t)i * n] = sk ? 0.0 : 2.0 * y;
+        Y[r + (int64_t)i * n] = sk ? s_zero<S>() : two_x(y);
     }
     if (blockIdx.x == 0 && (int)threadIdx.x <= i) {
         const int c = threadIdx.x;
-        double tc = 2.0;
+        S tc;
+        set_re_im(tc, 2.0, 0.0);
         if (c < i) {
-            double s = 0.0;
+            S s = s_zero<S>();
             if (!sk)
-                for (int q = c; q < i; ++q) s += T[c + q * kPanel] * tvec[q];
-            tc = -2.0 * s;
+                for (int q = c; q < i; ++q) s = add(s, mul(T[c + q * NB], tvec[q]));
+            tc = neg2(s);
         }
-        T[c + i * kPanel] = tc;
+        T[c + i * NB] = tc;
+    }
+}
+
+// ------------------------------------------------------------------ blocked Householder QR
+// qr_decompose_dense<S> (src/qr_method/qr_decompose.hpp:46-85) in compact-WY form: the panel's
+// reflectors H_i = I - 2 v_i v_i^H (the reference's convention, reflector from the diagonal row
+// down) give Q_p = H_k ... H_{k+nb-1} = I - V T V^H; per panel R(k:, c1:) <- Q_p^H R(k:, c1:)
+// and Q(:, k:) <- Q(:, k:) Q_p are GEMMs.  Panel column j (local i), one workgroup with the column
+// in LDS: apply the panel's earlier reflectors (a -= V T^H V^H a, rows k..), generate reflector i
+// from rows j.., store R's column (alpha on the diagonal, exact zeros below), V(:, i) and the
+// T column (T(0:i, i) = -2 T(0:i, 0:i) V(:, 0:i)^H v_i, T(i, i) = 2).
+template <class S>
+__global__ __launch_bounds__(1024) void qr_panel_col(S* R, int m, int k, int j, int i, S* V, S* T) {
+    constexpr int NB = 32;
+    extern __shared__ double qa_raw[];     // column j (m scalars)
+    S* a = reinterpret_cast<S*>(qa_raw);
+    __shared__ S red[16 * NB];
+    __shared__ S sw[NB];
+    __shared__ S sw2[NB];
+    __shared__ double s_tail;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int r = tid; r < m; r += nt) a[r] = R[r + (int64_t)j * m];
+    __syncthreads();
+    if (i > 0) {   // a(k:) -= V T^H V^H a(k:)
+        S p[NB];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) p[c] = s_zero<S>();
+        for (int r = k + tid; r < m; r += nt) {
+            const S x = a[r];
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+                if (c < i) p[c] = add(p[c], mul(cj(V[r + (int64_t)c * m]), x));
+        }
+        block_sum_vec<S, NB>(p, i, red, sw);
+        if (tid < i) {
+            S s = s_zero<S>();
+            for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(T[c + tid * NB]), sw[c]));
+            sw2[tid] = s;
+        }
+        __syncthreads();
+        for (int r = k + tid; r < m; r += nt) {
+            S x = a[r];
+            for (int c = 0; c < i; ++c) x = sub(x, mul(V[r + (int64_t)c * m], sw2[c]));
+            a[r] = x;
+        }
+        __syncthreads();
+    }
+    double tl = 0.0;
+    for (int r = j + 1 + tid; r < m; r += nt) tl += sq_abs(a[r]);
+    {
+        double pp[kPanel];
+        pp[0] = tl;
+        block_sum_vec<double, kPanel>(pp, 1, reinterpret_cast<double*>(red), reinterpret_cast<double*>(sw));
+        if (tid == 0) s_tail = reinterpret_cast<double*>(sw)[0];
+        __syncthreads();
+    }
+    const double tail = s_tail;
+    bool sk;
+    S v0, alpha;
+    double rv;
+    hess_reflector(a[j], tail, sk, v0, rv, alpha);
+    S* vcol = V + (int64_t)i * m;
+    for (int r = tid; r < m; r += nt) {
+        S v = s_zero<S>();
+        if (!sk && r >= j) v = scal(r == j ? v0 : a[r], rv);
+        vcol[r] = v;
+        S x = a[r];
+        if (!sk && r == j) x = alpha;
+        if (!sk && r > j) x = s_zero<S>();
+        R[r + (int64_t)j * m] = x;
+    }
+    __syncthreads();
+    // t = V(:, 0:i)^H v (rows j..), then the T column
+    S p[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) p[c] = s_zero<S>();
+    if (!sk && i > 0)
+        for (int r = j + tid; r < m; r += nt) {
+            const S v = vcol[r];
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+                if (c < i) p[c] = add(p[c], mul(cj(V[r + (int64_t)c * m]), v));
+        }
+    if (i > 0) block_sum_vec<S, NB>(p, i, red, sw);
+    if (tid <= i) {
+        S tc;
+        set_re_im(tc, 2.0, 0.0);
+        if (tid < i) {
+            S s2 = s_zero<S>();
+            if (!sk)
+                for (int q = tid; q < i; ++q) s2 = add(s2, mul(T[tid + q * NB], sw[q]));
+            tc = neg2(s2);
+        }
+        T[tid + i * NB] = tc;
     }
 }
 
@@ -207,7 +366,6 @@ __global__ __launch_bounds__(256) void hess_y(int n, int i, int nch, const doubl
 #endif
 constexpr int kCoopBlocks = EIGSOL_COOP_BLOCKS;
 constexpr int kCoopThreads = 1024;
-constexpr int kCoopMaxN = 8192;          // v in LDS (64 KiB) and at most 2 rows per lane
 #ifndef EIGSOL_GEMV_BATCH
 #define EIGSOL_GEMV_BATCH 16
 #endif
@@ -216,15 +374,16 @@ constexpr int kCoopMaxN = 8192;          // v in LDS (64 KiB) and at most 2 rows
 #endif
 constexpr int kGemvBatch = EIGSOL_GEMV_BATCH;   // columns per GEMV step (loads in flight per lane)
 
+template <class S>
 struct CoopArgs {
-    double* A;
+    S* A;
     int n, k, nbp;
-    double* V;
-    double* Y;
-    double* T;
-    double* part;       // [2][G][kPanel]: P1 -> P2 partials in the first half, P3 -> P4 in the second
+    S* V;
+    S* Y;
+    S* T;
+    S* part;            // [2][G][NB]: P1 -> P2 partials in the first half, P3 -> P4 in the second
     double* tpart;      // [G]
-    double* x0;         // a(j+1)
+    S* x0;              // a(j+1)
     unsigned* bar;      // barrier counter (zeroed by the host before the launch)
     int* err;
 };
@@ -248,26 +407,30 @@ __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned& target, in
     __syncthreads();
 }
 
-template <int kCoopRowsPerLane>
-__global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
-    extern __shared__ double vsh[];          // v (n doubles) for the GEMV
-    __shared__ double xs[kCoopRowsPerLane * 64];    // own rows of the current column
-    __shared__ double ysum[16][kCoopRowsPerLane * 64];
-    __shared__ double red[kCoopBlocks * kPanel];   // gathered block partials
-    __shared__ double sv[kPanel], sw[kPanel], st[kPanel];
-    __shared__ double s_scal[4];
+template <class S, int kCoopRowsPerLane>
+__global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
+    constexpr int NB = HessCfg<S>::NB;
+    extern __shared__ double vsh_raw[];      // v (n scalars) for the GEMV
+    S* vsh = reinterpret_cast<S*>(vsh_raw);
+    __shared__ S xs[kCoopRowsPerLane * 64];    // own rows of the current column
+    __shared__ S ysum[16][kCoopRowsPerLane * 64];
+    __shared__ S red[kCoopBlocks * NB];   // gathered block partials
+    __shared__ S sv[NB], sw[NB], st[NB];
+    __shared__ S s_scal[3];
+    __shared__ double s_rv;
+    __shared__ int s_sk;
     // Block partials of another phase: all threads load them at once (independent sc1 loads),
     // then thread c sums column c in block order (deterministic).
-    auto gather = [&](const double* src, int cnt, double* dst) {
+    auto gather = [&](const S* src, int cnt, S* dst) {
         const int nb = (int)gridDim.x;
-        for (int e = threadIdx.x; e < nb * kPanel; e += kCoopThreads) {
-            const int b = e / kPanel, c = e % kPanel;
-            red[e] = c < cnt ? ld_agent(&src[b * kPanel + c]) : 0.0;
+        for (int e = threadIdx.x; e < nb * NB; e += kCoopThreads) {
+            const int b = e / NB, c = e % NB;
+            red[e] = c < cnt ? ld_ag(&src[b * NB + c]) : s_zero<S>();
         }
         __syncthreads();
         if ((int)threadIdx.x < cnt) {
-            double acc = 0.0;
-            for (int b = 0; b < nb; ++b) acc += red[b * kPanel + threadIdx.x];
+            S acc = s_zero<S>();
+            for (int b = 0; b < nb; ++b) acc = add(acc, red[b * NB + threadIdx.x]);
             dst[threadIdx.x] = acc;
         }
         __syncthreads();
@@ -281,34 +444,34 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
     for (int i = 0; i < a.nbp; ++i) {
         const int j = k + i;
         // ---------------- P1
-        if (tid < i) sv[tid] = ld_agent(&a.V[j + (int64_t)tid * n]);
+        if (tid < i) sv[tid] = cj(ld_ag(&a.V[j + (int64_t)tid * n]));
         __syncthreads();
         if (wv == 0)
             for (int q = 0; q < kCoopRowsPerLane; ++q) {
                 const int r = r0 + lane + 64 * q;
                 if (r < r1) {
-                    double x = a.A[r + (int64_t)j * n];
-                    for (int c = 0; c < i; ++c) x -= a.Y[r + (int64_t)c * n] * sv[c];
+                    S x = a.A[r + (int64_t)j * n];
+                    for (int c = 0; c < i; ++c) x = sub(x, mul(a.Y[r + (int64_t)c * n], sv[c]));
                     xs[lane + 64 * q] = x;
                 }
             }
         __syncthreads();
-        // partials of w_c = sum_{r >= k+1} V(r, c) x(r): wave wv handles c = wv, wv + 16
+        // partials of w_c = sum_{r >= k+1} conj(V(r, c)) x(r): wave wv handles c = wv, wv + 16
         for (int c = wv; c < i; c += 16) {
-            double p = 0.0;
+            S p = s_zero<S>();
             for (int q = 0; q < kCoopRowsPerLane; ++q) {
                 const int r = r0 + lane + 64 * q;
-                if (r < r1 && r >= k + 1) p += a.V[r + (int64_t)c * n] * xs[lane + 64 * q];
+                if (r < r1 && r >= k + 1) p = add(p, mul(cj(a.V[r + (int64_t)c * n]), xs[lane + 64 * q]));
             }
-            p = wave_sum(p);
-            if (lane == 0) st_agent(&a.part[blockIdx.x * kPanel + c], p);
+            p = wsum(p);
+            if (lane == 0) st_ag(&a.part[blockIdx.x * NB + c], p);
         }
         grid_barrier(a.bar, target, a.err);
         // ---------------- P2
         gather(a.part, i, sw);
         if (tid < i) {
-            double s = 0.0;
-            for (int c = 0; c <= tid; ++c) s += ld_agent(&a.T[c + tid * kPanel]) * sw[c];   // (T^T w)_tid
+            S s = s_zero<S>();
+            for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(ld_ag(&a.T[c + tid * NB])), sw[c]));   // (T^H w)_tid
             st[tid] = s;
         }
         __syncthreads();
@@ -317,12 +480,12 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
             for (int q = 0; q < kCoopRowsPerLane; ++q) {
                 const int r = r0 + lane + 64 * q;
                 if (r < r1) {
-                    double x = xs[lane + 64 * q];
+                    S x = xs[lane + 64 * q];
                     if (r >= k + 1)
-                        for (int c = 0; c < i; ++c) x -= a.V[r + (int64_t)c * n] * st[c];
+                        for (int c = 0; c < i; ++c) x = sub(x, mul(a.V[r + (int64_t)c * n], st[c]));
                     xs[lane + 64 * q] = x;
-                    if (r >= j + 2) tl += x * x;
-                    if (r == j + 1) st_agent(a.x0, x);
+                    if (r >= j + 2) tl += sq_abs(x);
+                    if (r == j + 1) st_ag(a.x0, x);
                 }
             }
         if (wv == 0) {
@@ -331,90 +494,89 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
         }
         grid_barrier(a.bar, target, a.err);
         // ---------------- P3
-        if (tid < G) red[tid] = ld_agent(&a.tpart[tid]);
+        double* redd = reinterpret_cast<double*>(red);
+        if (tid < G) redd[tid] = ld_agent(&a.tpart[tid]);
         __syncthreads();
         if (tid == 0) {
             double tail = 0.0;
-            for (int b = 0; b < G; ++b) tail += red[b];
-            const double x0 = ld_agent(a.x0);
-            double sk = tail == 0.0 ? 1.0 : 0.0, v0 = 0.0, rv = 0.0, alpha = 0.0;
-            if (sk == 0.0) {
-                const double nx = sqrt(tail + x0 * x0);
-                const double sign = x0 == 0.0 ? 1.0 : (x0 > 0.0 ? 1.0 : -1.0);
-                alpha = -sign * nx;
-                v0 = x0 - alpha;
-                const double vn = sqrt(tail + v0 * v0);
-                if (vn == 0.0) sk = 1.0;
-                else rv = 1.0 / vn;
-            }
-            s_scal[0] = sk; s_scal[1] = v0; s_scal[2] = rv; s_scal[3] = alpha;
+            for (int b = 0; b < G; ++b) tail += redd[b];
+            const S x0 = ld_ag(a.x0);
+            bool sk;
+            S v0, alpha;
+            double rv;
+            hess_reflector(x0, tail, sk, v0, rv, alpha);
+            s_sk = sk ? 1 : 0;
+            s_scal[1] = v0;
+            s_rv = rv;
+            s_scal[2] = alpha;
         }
         __syncthreads();
-        const bool sk = s_scal[0] != 0.0;
-        const double v0 = s_scal[1], rv = s_scal[2], alpha = s_scal[3];
+        const bool sk = s_sk != 0;
+        const S v0 = s_scal[1], alpha = s_scal[2];
+        const double rv = s_rv;
         if (wv == 0)
             for (int q = 0; q < kCoopRowsPerLane; ++q) {
                 const int r = r0 + lane + 64 * q;
                 if (r < r1) {
-                    const double x = xs[lane + 64 * q];
-                    double v = 0.0;
-                    if (!sk && r > j) v = (r == j + 1 ? v0 : x) * rv;
-                    st_agent(&a.V[r + (int64_t)i * n], v);
+                    const S x = xs[lane + 64 * q];
+                    S v = s_zero<S>();
+                    if (!sk && r > j) v = scal(r == j + 1 ? v0 : x, rv);
+                    st_ag(&a.V[r + (int64_t)i * n], v);
                     xs[lane + 64 * q] = v;           // keep v for the t partials
-                    double red_col = x;
+                    S red_col = x;
                     if (!sk && r == j + 1) red_col = alpha;
-                    if (!sk && r > j + 1) red_col = 0.0;
+                    if (!sk && r > j + 1) red_col = s_zero<S>();
                     a.A[r + (int64_t)j * n] = red_col;
                 }
             }
         __syncthreads();
         for (int c = wv; c < i; c += 16) {
-            double p = 0.0;
+            S p = s_zero<S>();
             for (int q = 0; q < kCoopRowsPerLane; ++q) {
                 const int r = r0 + lane + 64 * q;
-                if (r < r1) p += a.V[r + (int64_t)c * n] * xs[lane + 64 * q];
+                if (r < r1) p = add(p, mul(cj(a.V[r + (int64_t)c * n]), xs[lane + 64 * q]));
             }
-            p = wave_sum(p);
-            if (lane == 0) st_agent(&a.part[(G + blockIdx.x) * kPanel + c], p);
+            p = wsum(p);
+            if (lane == 0) st_ag(&a.part[(G + blockIdx.x) * NB + c], p);
         }
         grid_barrier(a.bar, target, a.err);
         // ---------------- P4
-        for (int r = tid; r < n; r += kCoopThreads) vsh[r] = sk ? 0.0 : ld_agent(&a.V[r + (int64_t)i * n]);
+        for (int r = tid; r < n; r += kCoopThreads) vsh[r] = sk ? s_zero<S>() : ld_ag(&a.V[r + (int64_t)i * n]);
         __syncthreads();
-        gather(a.part + (size_t)G * kPanel, i, sv);
-        if (sk && tid < i) sv[tid] = 0.0;
+        gather(a.part + (size_t)G * NB, i, sv);
+        if (sk && tid < i) sv[tid] = s_zero<S>();
         __syncthreads();
-        double yacc[kCoopRowsPerLane];
+        S yacc[kCoopRowsPerLane];
 #pragma unroll
-        for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] = 0.0;
+        for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] = s_zero<S>();
         if (!sk && !EIGSOL_HESS_SKIP_GEMV) {
-            // 8 columns per step with every load issued before the FMAs (bytes in flight: the
+            // kB columns per step with every load issued before the FMAs (bytes in flight: the
             // GEMV streams the trailing matrix once per column)
             const int nq = (r1 - r0 + 63) / 64;
             int c = j + 1 + wv;
-            constexpr int kB = kGemvBatch / kCoopRowsPerLane;   // loads in flight per lane
+            constexpr int kB = kGemvBatch * (int)sizeof(double) / (int)sizeof(S) / kCoopRowsPerLane;
             for (; c + 16 * (kB - 1) < n; c += 16 * kB) {
-                double av[kB][kCoopRowsPerLane];
+                S av[kB][kCoopRowsPerLane];
 #pragma unroll
                 for (int u = 0; u < kB; ++u)
 #pragma unroll
                     for (int q = 0; q < kCoopRowsPerLane; ++q) {
                         const int r = min(r0 + lane + 64 * q, r1 - 1);
-                        av[u][q] = q < nq ? a.A[r + (int64_t)(c + 16 * u) * n] : 0.0;
+                        av[u][q] = q < nq ? a.A[r + (int64_t)(c + 16 * u) * n] : s_zero<S>();
                     }
 #pragma unroll
                 for (int u = 0; u < kB; ++u) {
-                    const double vc = vsh[c + 16 * u];
+                    const S vc = vsh[c + 16 * u];
 #pragma unroll
-                    for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] += av[u][q] * vc;
+                    for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] = add(yacc[q], mul(av[u][q], vc));
                 }
             }
             for (; c < n; c += 16) {
-                const double vc = vsh[c];
+                const S vc = vsh[c];
 #pragma unroll
                 for (int q = 0; q < kCoopRowsPerLane; ++q) {
                     const int r = min(r0 + lane + 64 * q, r1 - 1);
-                    if (q < nq) yacc[q] += a.A[r + (int64_t)c * n] * vc;
+                    if (q < nq) yacc[q] = add(yacc[q], mul(a.A[r + (int64_t)c * n], vc));
                 }
             }
             // rows past r1 were clamped to r1 - 1: their sums are never stored
@@ -426,23 +588,23 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs a) {
             for (int q = 0; q < kCoopRowsPerLane; ++q) {
                 const int r = r0 + lane + 64 * q;
                 if (r < r1) {
-                    double y = 0.0;
-                    for (int w = 0; w < 16; ++w) y += ysum[w][lane + 64 * q];
-                    for (int c = 0; c < i; ++c) y -= a.Y[r + (int64_t)c * n] * sv[c];
-                    a.Y[r + (int64_t)i * n] = sk ? 0.0 : 2.0 * y;
+                    S y = s_zero<S>();
+                    for (int w = 0; w < 16; ++w) y = add(y, ysum[w][lane + 64 * q]);
+                    for (int c = 0; c < i; ++c) y = sub(y, mul(a.Y[r + (int64_t)c * n], sv[c]));
+                    a.Y[r + (int64_t)i * n] = sk ? s_zero<S>() : two_x(y);
                 }
             }
         if (blockIdx.x == 0 && tid <= i) {
-            double tc = 2.0;
+            S tc;
+            set_re_im(tc, 2.0, 0.0);
             if (tid < i) {
-                double s = 0.0;
-                for (int q = tid; q < i; ++q) s += ld_agent(&a.T[tid + q * kPanel]) * sv[q];
-                tc = -2.0 * s;
+                S s = s_zero<S>();
+                for (int q = tid; q < i; ++q) s = add(s, mul(ld_ag(&a.T[tid + q * NB]), sv[q]));
+                tc = neg2(s);
             }
-            st_agent(&a.T[tid + i * kPanel], tc);
+            st_ag(&a.T[tid + i * NB], tc);
         }
         __syncthreads();
-        (void)red;
     }
 }
 
@@ -583,88 +745,187 @@ __global__ __launch_bounds__(256) void gemm_mfma_f64(int m, int nn, int kk, doub
             }
 }
 
+// Complex counterpart of gemm_mfma_f64: C = beta C + alpha op(A) op(B), op = conjugate transpose
+// when TA / TB (alpha, beta real).  The tiles are staged as re / im planes and a complex tile
+// product is four real MFMAs: re += Ar Br - Ai Bi, im += Ar Bi + Ai Br.
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_mfma_c128(int m, int nn, int kk, double alpha, const cplx* A,
+                                                      int64_t lda, const cplx* B, int64_t ldb, double beta,
+                                                      cplx* C, int64_t ldc, int kc, int64_t zstride) {
+    constexpr int TM = 64, KT = 16;
+    __shared__ double Ar[KT][TM + 1], Ai[KT][TM + 1];   // [k][row]
+    __shared__ double Br[KT][TM + 1], Bi[KT][TM + 1];   // [k][col]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wy = wave >> 1, wx = wave & 1;
+    const int i0 = blockIdx.x * TM, j0 = blockIdx.y * TM;
+    const int kb = blockIdx.z * kc;
+    const int ke = min(kk, kb + kc);
+    C += blockIdx.z * zstride;
+    dbl4 accR[2][2], accI[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) accR[a][b] = accI[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = kb; k0 < ke; k0 += KT) {
+        for (int e = threadIdx.x; e < KT * TM; e += 256) {
+            int r, q;
+            if (!TA) { r = e % TM; q = e / TM; } else { q = e % KT; r = e / KT; }
+            {
+                const int gi = i0 + r, gk = k0 + q;
+                cplx val{0.0, 0.0};
+                if (gi < m && gk < ke) val = TA ? cj(A[gk + (int64_t)gi * lda]) : A[gi + (int64_t)gk * lda];
+                Ar[q][r] = val.re;
+                Ai[q][r] = val.im;
+            }
+            if (!TB) { q = e % KT; r = e / KT; } else { r = e % TM; q = e / TM; }
+            {
+                const int gk = k0 + q, gj = j0 + r;
+                cplx val{0.0, 0.0};
+                if (gk < ke && gj < nn) val = TB ? cj(B[gj + (int64_t)gk * ldb]) : B[gk + (int64_t)gj * ldb];
+                Br[q][r] = val.re;
+                Bi[q][r] = val.im;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kq = 0; kq < KT; kq += 4) {
+            const int k = kq + (lane >> 4);
+            double bR[2], bI[2], aR[2], aI[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                bR[t] = Br[k][32 * wx + 16 * t + (lane & 15)];
+                bI[t] = Bi[k][32 * wx + 16 * t + (lane & 15)];
+                aR[t] = Ar[k][32 * wy + 16 * t + (lane & 15)];
+                aI[t] = Ai[k][32 * wy + 16 * t + (lane & 15)];
+            }
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj) {
+                    accR[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(bR[tj], aR[ti], accR[ti][tj], 0, 0, 0);
+                    accR[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(-bI[tj], aI[ti], accR[ti][tj], 0, 0, 0);
+                    accI[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(bI[tj], aR[ti], accI[ti][tj], 0, 0, 0);
+                    accI[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(bR[tj], aI[ti], accI[ti][tj], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = i0 + 32 * wy + 16 * ti + (lane & 15);
+                const int gj = j0 + 32 * wx + 16 * tj + (lane >> 4) + 4 * r;
+                if (gi < m && gj < nn) {
+                    cplx* cp = C + gi + (int64_t)gj * ldc;
+                    const cplx old = beta == 0.0 ? cplx{0.0, 0.0} : cplx{beta * cp->re, beta * cp->im};
+                    *cp = cplx{old.re + alpha * accR[ti][tj][r], old.im + alpha * accI[ti][tj][r]};
+                }
+            }
+}
+
 // C = beta C + sum_z P[z] (m x nn, P packed with leading dimension m), partials added in z order
-__global__ void gemm_reduce(int m, int nn, int nz, const double* P, double beta, double* C, int64_t ldc) {
+template <class S>
+__global__ void gemm_reduce(int m, int nn, int nz, const S* P, double beta, S* C, int64_t ldc) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (int64_t)m * nn) return;
     const int i = (int)(idx % m);
     const int64_t j = idx / m;
-    double s = 0.0;
-    for (int z = 0; z < nz; ++z) s += P[(int64_t)z * m * nn + idx];
-    double* c = C + i + j * ldc;
-    *c = (beta == 0.0 ? 0.0 : beta * *c) + s;
+    S s = s_zero<S>();
+    for (int z = 0; z < nz; ++z) s = add(s, P[(int64_t)z * m * nn + idx]);
+    S* c = C + i + j * ldc;
+    *c = add(beta == 0.0 ? s_zero<S>() : scal(*c, beta), s);
+}
+
+// dst(0:rows, 0:cols) = conj(src(...)), column-major
+__global__ void conj_copy2d(cplx* dst, int64_t ldd, const cplx* src, int64_t lds, int rows, int cols) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)rows * cols) return;
+    const int i = (int)(idx % rows);
+    const int64_t j = idx / rows;
+    dst[i + j * ldd] = cj(src[i + j * lds]);
 }
 
 }  // namespace dev
 
 namespace {
-template <bool TA, bool TB>
-void gemm(hipStream_t st, int m, int nn, int kk, double alpha, const double* A, int64_t lda, const double* B,
-          int64_t ldb, double beta, double* C, int64_t ldc, double* work = nullptr, int64_t work_elems = 0) {
+template <class S, bool TA, bool TB>
+void gemm(hipStream_t st, int m, int nn, int kk, double alpha, const S* A, int64_t lda, const S* B, int64_t ldb,
+          double beta, S* C, int64_t ldc, S* work = nullptr, int64_t work_elems = 0) {
     if (m <= 0 || nn <= 0) return;
     const int bx = (m + 63) / 64, by = (nn + 63) / 64;
-    // split K when the output has too few tiles to fill the chip (e.g. W = V^T A, 32 rows)
+    // split K when the output has too few tiles to fill the chip (e.g. W = V^H A, nb rows)
     int nz = 1;
     if (work && bx * by < 512 && kk >= 512) {
         nz = std::min(16, std::max(1, 1024 / (bx * by)));
         nz = std::min<int64_t>(nz, work_elems / ((int64_t)m * nn));
         nz = std::max(1, std::min(nz, kk / 128));
     }
-    static const bool valu = std::getenv("EIGSOL_GEMM_VALU") != nullptr;
-    auto kern = valu ? dev::gemm_f64<TA, TB> : dev::gemm_mfma_f64<TA, TB>;
+    auto launch = [&](dim3 g, double be, S* Cp, int64_t ldcp, int kc, int64_t zs) {
+        if constexpr (std::is_same_v<S, double>) {
+            static const bool valu = std::getenv("EIGSOL_GEMM_VALU") != nullptr;
+            auto kern = valu ? dev::gemm_f64<TA, TB> : dev::gemm_mfma_f64<TA, TB>;
+            hipLaunchKernelGGL(kern, g, dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb, be, Cp, ldcp, kc, zs);
+        } else {
+            hipLaunchKernelGGL((dev::gemm_mfma_c128<TA, TB>), g, dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb,
+                               be, Cp, ldcp, kc, zs);
+        }
+    };
     if (nz <= 1) {
-        hipLaunchKernelGGL(kern, dim3(bx, by, 1), dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb, beta, C, ldc,
-                           kk, (int64_t)0);
+        launch(dim3(bx, by, 1), beta, C, ldc, kk, (int64_t)0);
         return;
     }
     const int kc = ((kk + nz - 1) / nz + 15) / 16 * 16;
     nz = (kk + kc - 1) / kc;
-    hipLaunchKernelGGL(kern, dim3(bx, by, nz), dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb, 0.0, work,
-                       (int64_t)m, kc, (int64_t)m * nn);
+    launch(dim3(bx, by, nz), 0.0, work, (int64_t)m, kc, (int64_t)m * nn);
     const int64_t tot = (int64_t)m * nn;
-    hipLaunchKernelGGL(dev::gemm_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, m, nn, nz, work, beta,
-                       C, ldc);
+    hipLaunchKernelGGL((dev::gemm_reduce<S>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, m, nn, nz, work,
+                       beta, C, ldc);
 }
-}  // namespace
 
 // In place on the device matrix A (n x n, column-major, ld = n).
-int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
+template <class S>
+int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
+    constexpr bool kC = std::is_same_v<S, cplx>;
+    using Cfg = dev::HessCfg<S>;
     const int n = (int)n64;
     if (n < 3) return EIGSOL_OK;
-    if (n > dev::kMaxLdsN) return fail(EIGSOL_E_UNSUPPORTED, "blocked Hessenberg: n > 16384");
-    constexpr int NB = dev::kPanel;
+    if (n > Cfg::kMaxLdsN) return fail(EIGSOL_E_UNSUPPORTED, "blocked Hessenberg: n above the LDS panel limit");
+    constexpr int NB = Cfg::NB;
     const int maxch = (n + dev::kGemvCols - 1) / dev::kGemvCols;
-    double *V = nullptr, *Y = nullptr, *T = nullptr, *tv = nullptr, *yp = nullptr, *W = nullptr, *W2 = nullptr;
+    S *V = nullptr, *Y = nullptr, *T = nullptr, *tv = nullptr, *yp = nullptr, *W = nullptr;
     int* skip = nullptr;
-    EIGSOL_HIP(hipMalloc(&V, (size_t)n * NB * sizeof(double)));
-    double *L = nullptr, *R = nullptr, *M = nullptr;
-    EIGSOL_HIP(hipMalloc(&L, (size_t)n * 2 * NB * sizeof(double)));   // [Y | V zero above the panel]
-    EIGSOL_HIP(hipMalloc(&R, (size_t)n * 2 * NB * sizeof(double)));   // [V(c1:, :) | W2^T]
-    EIGSOL_HIP(hipMalloc(&M, (size_t)NB * NB * sizeof(double)));      // V^T Y
+    EIGSOL_HIP(hipMalloc(&V, (size_t)n * NB * sizeof(S)));
+    S *L = nullptr, *R = nullptr, *M = nullptr;
+    EIGSOL_HIP(hipMalloc(&L, (size_t)n * 2 * NB * sizeof(S)));   // [Y | V zero above the panel]
+    EIGSOL_HIP(hipMalloc(&R, (size_t)n * 2 * NB * sizeof(S)));   // conj of [V(c1:, :) | W2^H]
+    EIGSOL_HIP(hipMalloc(&M, (size_t)NB * NB * sizeof(S)));      // V^H Y
     Y = L;
-    EIGSOL_HIP(hipMalloc(&T, NB * NB * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&tv, NB * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&yp, (size_t)maxch * n * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&W, (size_t)NB * n * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&W2, (size_t)NB * n * sizeof(double)));
-    double* SK = nullptr;                 // split-K partials of W = V^T A (16 x 32 x n)
+    EIGSOL_HIP(hipMalloc(&T, NB * NB * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&tv, NB * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&yp, (size_t)maxch * n * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&W, (size_t)NB * n * sizeof(S)));
+    S* SK = nullptr;                      // split-K partials of W = V^H A (16 x NB x n)
     const int64_t sk_elems = (int64_t)16 * NB * n;
-    EIGSOL_HIP(hipMalloc(&SK, sk_elems * sizeof(double)));
+    EIGSOL_HIP(hipMalloc(&SK, sk_elems * sizeof(S)));
     EIGSOL_HIP(hipMalloc(&skip, 64));
-    const size_t lds = (size_t)n * sizeof(double);
+    const size_t lds = (size_t)n * sizeof(S);
     // one cooperative launch per panel when the device supports it and n fits its LDS staging
     int coop_ok = 0, dev_id = 0;
     EIGSOL_HIP(hipGetDevice(&dev_id));
     EIGSOL_HIP(hipDeviceGetAttribute(&coop_ok, hipDeviceAttributeCooperativeLaunch, dev_id));
-    bool coop = coop_ok && n <= dev::kCoopMaxN && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
-    const size_t coop_lds = (size_t)n * sizeof(double);
-    const void* coop_kernel = n <= 64 * dev::kCoopBlocks ? reinterpret_cast<const void*>(dev::hess_panel_coop<1>)
-                                                         : reinterpret_cast<const void*>(dev::hess_panel_coop<2>);
-    double *part = nullptr, *tpart = nullptr, *x0s = nullptr;
+    bool coop = coop_ok && n <= Cfg::kCoopMaxN && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
+    const size_t coop_lds = (size_t)n * sizeof(S);
+    const void* coop_kernel = n <= 64 * dev::kCoopBlocks ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1>)
+                                                         : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 2>);
+    S *part = nullptr, *x0s = nullptr;
+    double* tpart = nullptr;
     unsigned* bar = nullptr;
     int* err = nullptr;
     if (coop) {
-        EIGSOL_HIP(hipMalloc(&part, 2 * dev::kCoopBlocks * NB * sizeof(double)));
+        EIGSOL_HIP(hipMalloc(&part, 2 * dev::kCoopBlocks * NB * sizeof(S)));
         EIGSOL_HIP(hipMalloc(&tpart, dev::kCoopBlocks * sizeof(double)));
         EIGSOL_HIP(hipMalloc(&x0s, 64));
         EIGSOL_HIP(hipMalloc(&bar, 64));
@@ -672,15 +933,15 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
         EIGSOL_HIP(hipMemsetAsync(err, 0, 64, st));
         EIGSOL_HIP(hipFuncSetAttribute(coop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)coop_lds));
     }
-    EIGSOL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dev::hess_panel_col),
+    EIGSOL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dev::hess_panel_col<S>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int last = n - 3;   // reflector columns 0 .. n-3 (to_hessenberg.hpp:38)
     for (int k = 0; k <= last; k += NB) {
         const int nbp = std::min(NB, last - k + 1);
-        EIGSOL_HIP(hipMemsetAsync(T, 0, NB * NB * sizeof(double), st));
+        EIGSOL_HIP(hipMemsetAsync(T, 0, NB * NB * sizeof(S), st));
         if (coop) {
             EIGSOL_HIP(hipMemsetAsync(bar, 0, 64, st));
-            dev::CoopArgs ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err};
+            dev::CoopArgs<S> ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err};
             void* kargs[] = {&ca};
             // EIGSOL_HESS_COOP_PLAIN=1: the SAME panel kernel through an ordinary launch, for profiling
             // only (rocprofv3 7.2 crashes at exit after any cooperative launch, tools/coop_prof_repro.hip);
@@ -695,35 +956,46 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
         }
         for (int i = 0; !coop && i < nbp; ++i) {
             const int j = k + i;
-            hipLaunchKernelGGL(dev::hess_panel_col, dim3(1), dim3(1024), lds, st, A, n, k, j, i, V, Y, T, tv, skip);
+            hipLaunchKernelGGL(dev::hess_panel_col<S>, dim3(1), dim3(1024), lds, st, A, n, k, j, i, V, Y, T, tv, skip);
             const int c0 = j + 1;
             const int nch = (n - c0 + dev::kGemvCols - 1) / dev::kGemvCols;
-            hipLaunchKernelGGL(dev::hess_gemv, dim3((n + 255) / 256, nch), dim3(256), 0, st, A, n, c0,
+            hipLaunchKernelGGL(dev::hess_gemv<S>, dim3((n + 255) / 256, nch), dim3(256), 0, st, A, n, c0,
                                V + (int64_t)i * n, yp, skip);
-            hipLaunchKernelGGL(dev::hess_y, dim3((n + 255) / 256), dim3(256), 0, st, n, i, nch, yp, tv, Y, T, skip);
+            hipLaunchKernelGGL(dev::hess_y<S>, dim3((n + 255) / 256), dim3(256), 0, st, n, i, nch, yp, tv, Y, T, skip);
         }
         const int c1 = k + nbp;           // first trailing column
         const int mt = n - c1;
         if (mt > 0) {
-            // A <- Q^T A Q with Q = I - V T V^T, in one pass over the trailing columns:
-            //   right: A Q = A - Y V^T (Y = A V T from the panel);
-            //   left:  Q^T (A Q) = A Q - V W2, W2 = T^T V^T (A Q) = T^T (V^T A - (V^T Y) V^T);
-            // so A(:, c1:) -= [Y | V] [V(c1:, :) | W2^T]^T, one rank-2nbp update (V is zero above
-            // row k+1), with W0 = V^T A read from A before it.
+            // A <- Q^H A Q with Q = I - V T V^H, in one pass over the trailing columns:
+            //   right: A Q = A - Y V^H (Y = A V T from the panel);
+            //   left:  Q^H (A Q) = A Q - V W2, W2 = T^H V^H (A Q) = T^H (V^H A - (V^H Y) V^H);
+            // so A(:, c1:) -= [Y | V] [V(c1:, :) | W2^H]^H, one rank-2nbp update (V is zero above
+            // row k+1), with W0 = V^H A read from A before it.  The update kernel forms L Rc^T, so
+            // R holds the conjugate of [V(c1:, :) | W2^H] = [conj V(c1:, :) | W2^T].
             const int rows = n - (k + 1);
-            double* Vz = L + (int64_t)nbp * n;     // L = [Y | Vz], Y already in place
-            double* R2 = R + (int64_t)nbp * n;     // R = [V(c1:, :) | W2^T]
-            gemm<true, false>(st, nbp, mt, rows, 1.0, V + (k + 1), n, A + (k + 1) + (int64_t)c1 * n, n, 0.0, W, NB,
-                              SK, sk_elems);
-            gemm<true, false>(st, nbp, nbp, rows, 1.0, V + (k + 1), n, L + (k + 1), n, 0.0, M, NB, SK, sk_elems);
-            EIGSOL_HIP(hipMemcpy2DAsync(R, n * sizeof(double), V + c1, n * sizeof(double), mt * sizeof(double), nbp,
+            S* Vz = L + (int64_t)nbp * n;     // L = [Y | Vz], Y already in place
+            S* R2 = R + (int64_t)nbp * n;
+            gemm<S, true, false>(st, nbp, mt, rows, 1.0, V + (k + 1), n, A + (k + 1) + (int64_t)c1 * n, n, 0.0, W, NB,
+                                 SK, sk_elems);
+            gemm<S, true, false>(st, nbp, nbp, rows, 1.0, V + (k + 1), n, L + (k + 1), n, 0.0, M, NB, SK, sk_elems);
+            if constexpr (kC) {
+                gemm<S, false, true>(st, nbp, mt, nbp, -1.0, M, NB, V + c1, n, 1.0, W, NB);          // W = V^H (A Q)
+                const int64_t cnt = (int64_t)mt * nbp;
+                hipLaunchKernelGGL(dev::conj_copy2d, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, R,
+                                   (int64_t)n, V + c1, (int64_t)n, mt, nbp);                          // conj V(c1:, :)
+                gemm<S, true, false>(st, mt, nbp, nbp, 1.0, W, NB, T, NB, 0.0, R2, n);               // W^H T
+                hipLaunchKernelGGL(dev::conj_copy2d, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, R2,
+                                   (int64_t)n, R2, (int64_t)n, mt, nbp);                              // W2^T
+            } else {
+                EIGSOL_HIP(hipMemcpy2DAsync(R, n * sizeof(S), V + c1, n * sizeof(S), mt * sizeof(S), nbp,
+                                            hipMemcpyDeviceToDevice, st));
+                gemm<S, false, true>(st, nbp, mt, nbp, -1.0, M, NB, R, n, 1.0, W, NB);              // W = V^T (A Q)
+                gemm<S, true, false>(st, mt, nbp, nbp, 1.0, W, NB, T, NB, 0.0, R2, n);              // W2^T = W^T T
+            }
+            EIGSOL_HIP(hipMemsetAsync(Vz, 0, (size_t)nbp * n * sizeof(S), st));
+            EIGSOL_HIP(hipMemcpy2DAsync(Vz + (k + 1), n * sizeof(S), V + (k + 1), n * sizeof(S), rows * sizeof(S), nbp,
                                         hipMemcpyDeviceToDevice, st));
-            gemm<false, true>(st, nbp, mt, nbp, -1.0, M, NB, R, n, 1.0, W, NB);              // W = V^T (A Q)
-            gemm<true, false>(st, mt, nbp, nbp, 1.0, W, NB, T, NB, 0.0, R2, n);              // W2^T = W^T T
-            EIGSOL_HIP(hipMemsetAsync(Vz, 0, (size_t)nbp * n * sizeof(double), st));
-            EIGSOL_HIP(hipMemcpy2DAsync(Vz + (k + 1), n * sizeof(double), V + (k + 1), n * sizeof(double),
-                                        rows * sizeof(double), nbp, hipMemcpyDeviceToDevice, st));
-            rankk_update<double, false>(st, n, mt, 2 * nbp, -1.0, L, n, R, n, A + (int64_t)c1 * n, n);
+            rankk_update<S, false>(st, n, mt, 2 * nbp, -1.0, L, n, R, n, A + (int64_t)c1 * n, n);
         }
     }
     EIGSOL_HIP(hipGetLastError());
@@ -732,11 +1004,67 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n64) {
         EIGSOL_HIP(hipMemcpyAsync(&errh, err, sizeof(int), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(hipStreamSynchronize(st));
     }
-    for (void* p : {(void*)V, (void*)L, (void*)R, (void*)M, (void*)T, (void*)tv, (void*)yp, (void*)W, (void*)W2, (void*)skip,
+    for (void* p : {(void*)V, (void*)L, (void*)R, (void*)M, (void*)T, (void*)tv, (void*)yp, (void*)W, (void*)skip,
                     (void*)part, (void*)tpart, (void*)x0s, (void*)bar, (void*)err, (void*)SK})
         if (p) (void)hipFree(p);
     if (errh) return fail(EIGSOL_E_HIP, "blocked Hessenberg: grid barrier timed out (internal error)");
     return EIGSOL_OK;
 }
+
+// qr_decompose_dense (qr_decompose.hpp:46-85) blocked: R (m x n, in place) and Q (m x m, set here).
+// Panels of 32 reflectors; m up to the LDS column limit (else the caller uses the per-reflector
+// kernels).
+template <class S>
+int qr_blocked(hipStream_t st, S* R, int m, int n, S* Q) {
+    constexpr bool kC = std::is_same_v<S, cplx>;
+    constexpr int NB = 32;
+    if (m > dev::HessCfg<S>::kMaxLdsN) return fail(EIGSOL_E_UNSUPPORTED, "blocked QR: m above the LDS panel limit");
+    const int kmax = std::min(m, n);
+    S *V = nullptr, *Vc = nullptr, *T = nullptr, *W = nullptr, *W2 = nullptr, *Z = nullptr, *Z2 = nullptr, *SK = nullptr;
+    const int64_t sk_elems = (int64_t)16 * NB * std::max(m, n);
+    EIGSOL_HIP(hipMalloc(&V, (size_t)m * NB * sizeof(S)));
+    if (kC) EIGSOL_HIP(hipMalloc(&Vc, (size_t)m * NB * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&T, NB * NB * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&W, (size_t)NB * std::max(n, 1) * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&W2, (size_t)NB * std::max(n, 1) * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&Z, (size_t)m * NB * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&Z2, (size_t)m * NB * sizeof(S)));
+    EIGSOL_HIP(hipMalloc(&SK, sk_elems * sizeof(S)));
+    EIGSOL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dev::qr_panel_col<S>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)(m * sizeof(S))));
+    for (int k = 0; k < kmax; k += NB) {
+        const int nbp = std::min(NB, kmax - k);
+        EIGSOL_HIP(hipMemsetAsync(T, 0, NB * NB * sizeof(S), st));
+        for (int i = 0; i < nbp; ++i)
+            hipLaunchKernelGGL(dev::qr_panel_col<S>, dim3(1), dim3(1024), m * sizeof(S), st, R, m, k, k + i, i, V, T);
+        const int rows = m - k, c1 = k + nbp, mt = n - c1;
+        if (mt > 0) {   // R(k:, c1:) <- (I - V T^H V^H) R(k:, c1:)
+            gemm<S, true, false>(st, nbp, mt, rows, 1.0, V + k, m, R + k + (int64_t)c1 * m, m, 0.0, W, NB, SK, sk_elems);
+            gemm<S, true, false>(st, nbp, mt, nbp, 1.0, T, NB, W, NB, 0.0, W2, NB);
+            rankk_update<S, true>(st, rows, mt, nbp, -1.0, V + k, m, W2, NB, R + k + (int64_t)c1 * m, m);
+        }
+        // Q(:, k:) <- Q(:, k:) (I - V T V^H)
+        gemm<S, false, false>(st, m, nbp, rows, 1.0, Q + (int64_t)k * m, m, V + k, m, 0.0, Z, m, SK, sk_elems);
+        gemm<S, false, false>(st, m, nbp, nbp, 1.0, Z, m, T, NB, 0.0, Z2, m);
+        const S* Vr = V;
+        if constexpr (kC) {
+            const int64_t cnt = (int64_t)m * nbp;
+            hipLaunchKernelGGL(dev::conj_copy2d, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, Vc, (int64_t)m, V,
+                               (int64_t)m, m, nbp);
+            Vr = Vc;
+        }
+        rankk_update<S, false>(st, m, rows, nbp, -1.0, Z2, m, Vr + k, m, Q + (int64_t)k * m, m);
+    }
+    EIGSOL_HIP(hipGetLastError());
+    for (void* p : {(void*)V, (void*)Vc, (void*)T, (void*)W, (void*)W2, (void*)Z, (void*)Z2, (void*)SK})
+        if (p) (void)hipFree(p);
+    return EIGSOL_OK;
+}
+}  // namespace
+
+int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n) { return hessenberg_blocked<double>(st, A, n); }
+int hessenberg_blocked_c128(hipStream_t st, cplx* A, int64_t n) { return hessenberg_blocked<cplx>(st, A, n); }
+int qr_blocked_f64(hipStream_t st, double* R, int64_t m, int64_t n, double* Q) { return qr_blocked<double>(st, R, (int)m, (int)n, Q); }
+int qr_blocked_c128(hipStream_t st, cplx* R, int64_t m, int64_t n, cplx* Q) { return qr_blocked<cplx>(st, R, (int)m, (int)n, Q); }
 
 }  // namespace eigsol

@@ -90,6 +90,7 @@ struct eigsol_power {
     eigsol_solver_options opts{1000, 1e-10};
     int transport = EIGSOL_TRANSPORT_LOCAL;
     PeerState* peer = nullptr;
+    int same_device = 1;      // ranks (of any process) sharing this rank's device
 };
 
 static constexpr size_t kPart = 32;
@@ -256,16 +257,54 @@ static int peer_setup_local(eigsol_power* s) {
         // loopback ranks share one device: each rank's blocks must stay co-resident with the
         // others' (a waiting launch must not keep a peer's producing launch off the CUs)
         s->grid = std::max(8, (s->grid / P) / 8 * 8);
+    } else if (s->same_device > 1) {
+        // ranks of other processes on this device (choose_transport's device-identity gather):
+        // the same co-residency rule, split among the ranks that share the CUs
+        s->grid = std::max(8, (s->grid / s->same_device) / 8 * 8);
     }
     return EIGSOL_OK;
 }
 
+// Frees the per-session device buffers only (a session falling back from the peer transport
+// re-allocates them for the collective grid).
+static void session_bufs_free(eigsol_power* s) {
+    for (void** q : {&s->buf[0], &s->buf[1], reinterpret_cast<void**>(&s->ctl), &s->rank_part, &s->blk_part,
+                     &s->trace}) {
+        if (*q) (void)hipFree(*q);
+        *q = nullptr;
+    }
+    if (s->host_ctl) (void)hipHostFree(s->host_ctl);
+    s->host_ctl = nullptr;
+}
+
+// Number of ranks (this one included) whose device has this rank's PCI bus id.  Host-collective
+// (every rank calls it).  Loopback worlds share one device by construction and return 1.
+static int ranks_on_my_device(eigsol_ctx* ctx, int& out) {
+    out = 1;
+    if (ctx->loop || ctx->nranks <= 1) return EIGSOL_OK;
+    char id[64];
+    std::memset(id, 0, sizeof(id));
+    if (hipDeviceGetPCIBusId(id, (int)sizeof(id) - 1, ctx->device) != hipSuccess)
+        std::snprintf(id, sizeof(id), "unknown-%p", static_cast<void*>(ctx));   // unique: counted alone
+    std::vector<char> all((size_t)ctx->nranks * sizeof(id));
+    EIGSOL_TRY(coll_allgather(ctx, id, sizeof(id), all.data()));
+    int same = 0;
+    for (int q = 0; q < ctx->nranks; ++q)
+        if (!std::memcmp(all.data() + (size_t)q * sizeof(id), id, sizeof(id))) ++same;
+    out = std::max(1, same);
+    return EIGSOL_OK;
+}
+
 // Collective choice of the per-iteration transport of a row-sharded CSR session.
-static int choose_transport(eigsol_power* s) {
+// The session buffers are allocated inside the agreement (peer path), so that a rank whose
+// allocation fails makes every rank fail or fall back together: a peer session's teardown is
+// collective, and a rank tearing down alone would leave the others in an unmatched barrier.
+static int choose_transport(eigsol_power* s, int32_t trace_cap) {
     eigsol_csr* A = s->csr;
     eigsol_ctx* ctx = s->ctx;
     const int P = ctx->nranks;
     const bool host_only = !ctx->comm && !ctx->loop;
+    EIGSOL_TRY(ranks_on_my_device(ctx, s->same_device));
     int cand = (A->sliced && A->exchange == EIGSOL_EXCHANGE_HALO && P <= dev::kMaxPeerRanks) ? 1 : 0;
     if (const char* e = std::getenv("EIGSOL_DIST_TRANSPORT"))
         if (!std::strcmp(e, "collective") && !host_only) cand = 0;
@@ -288,6 +327,7 @@ static int choose_transport(eigsol_power* s) {
         return EIGSOL_OK;
     }
     int rc = peer_setup_local(s);
+    if (rc == EIGSOL_OK) rc = session_alloc(s, trace_cap);
     int ok = rc == EIGSOL_OK ? 1 : 0;
     const std::string why = ok ? "" : eigsol_last_error();
     EIGSOL_TRY(coll_allgather(ctx, &ok, sizeof(int), all.data()));
@@ -299,6 +339,7 @@ static int choose_transport(eigsol_power* s) {
         return EIGSOL_OK;
     }
     peer_free(s);   // not agreed: local teardown only
+    session_bufs_free(s);
     if (host_only)
         return fail(EIGSOL_E_HIP, "peer exchange setup failed on some rank: " + why);
     s->transport = EIGSOL_TRANSPORT_COLLECTIVE;   // RCCL / loopback copies
@@ -323,8 +364,8 @@ int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power*
     s->n = A->nrows;
     s->nbuf = A->ncols;
     int rc = csr_grid(A, &s->grid);
-    if (rc == EIGSOL_OK && s->dist) rc = choose_transport(s);
-    if (rc == EIGSOL_OK) rc = session_alloc(s, trace_capacity);
+    if (rc == EIGSOL_OK && s->dist) rc = choose_transport(s, trace_capacity);
+    if (rc == EIGSOL_OK && !s->buf[0]) rc = session_alloc(s, trace_capacity);
     if (rc != EIGSOL_OK) { session_free(s); return rc; }
     *out = s;
     return EIGSOL_OK;

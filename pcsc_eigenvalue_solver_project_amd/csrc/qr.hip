@@ -16,6 +16,7 @@
 // The matrix stays in HBM (a 4096^2 fp64 matrix is 128 MiB, inside the 256 MiB Infinity Cache).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -408,6 +409,9 @@ __global__ __launch_bounds__(256) void scale_pow2_kernel(double* A, int64_t cnt,
 
 // ============================================================================ host drivers
 int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n);
+int hessenberg_blocked_c128(hipStream_t st, cplx* A, int64_t n);
+int qr_blocked_f64(hipStream_t st, double* R, int64_t m, int64_t n, double* Q);
+int qr_blocked_c128(hipStream_t st, cplx* R, int64_t m, int64_t n, cplx* Q);
 
 namespace {
 
@@ -457,20 +461,34 @@ int hessenberg_t(hipStream_t st, S* H, int64_t n, QrWork<S>& w) {
     return EIGSOL_OK;
 }
 
-// Real matrices of moderate size use the blocked (panel + GEMM) reduction (hessenberg.hip);
-// complex ones the per-reflector kernels above.
+// Matrices of moderate size use the blocked (panel + GEMM) reduction (hessenberg.hip): real up to
+// n = 16384, complex up to 8192 (the panel column in LDS); others the per-reflector kernels above
+// (EIGSOL_HESS_UNBLOCKED=1 forces those, for A/B).
 template <class S>
 int hessenberg_dev(hipStream_t st, S* H, int64_t n, QrWork<S>& w) {
-    if constexpr (std::is_same_v<S, double>) {
-        if (n >= 64 && n <= 16384) return hessenberg_blocked_f64(st, H, n);
+    static const bool unblocked = std::getenv("EIGSOL_HESS_UNBLOCKED") != nullptr;
+    if (!unblocked) {
+        if constexpr (std::is_same_v<S, double>) {
+            if (n >= 64 && n <= 16384) return hessenberg_blocked_f64(st, H, n);
+        } else {
+            if (n >= 64 && n <= 8192) return hessenberg_blocked_c128(st, H, n);
+        }
     }
     return hessenberg_t<S>(st, H, n, w);
 }
 
 // qr_decompose_dense (qr_decompose.hpp:46-85): R = A (m x n) in place, Q (m x m) = I then updated
+// Blocked (compact WY, hessenberg.hip) from min(m, n) >= 64 while a column fits the panel
+// kernel's LDS; EIGSOL_QR_UNBLOCKED=1 forces the per-reflector kernels (A/B).
 template <class S>
 int qr_decompose_t(hipStream_t st, S* R, int64_t m, int64_t n, S* Q, QrWork<S>& w) {
     hipLaunchKernelGGL((dev::set_identity_kernel<S>), dim3((m * m + 255) / 256), dim3(256), 0, st, Q, m);
+    static const bool unblocked = std::getenv("EIGSOL_QR_UNBLOCKED") != nullptr;
+    const int64_t lds_max = std::is_same_v<S, double> ? 16384 : 8192;
+    if (!unblocked && std::min(m, n) >= 64 && m <= lds_max && n <= INT32_MAX / 2) {
+        if constexpr (std::is_same_v<S, double>) return qr_blocked_f64(st, R, m, n, Q);
+        else return qr_blocked_c128(st, R, m, n, Q);
+    }
     const int64_t kmax = std::min(m, n);
     for (int64_t k = 0; k < kmax; ++k) {
         const int64_t rows = m - k;

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -104,16 +105,27 @@ __device__ __forceinline__ void zhouse(cplx a, cplx x1, cplx x2, bool three, dou
 // One wave, so no barriers: a wave's LDS operations complete in program order, and the compiler
 // fence keeps the program order.
 #define EIGSOL_ZWAVE_ORDER() asm volatile("" ::: "memory")
-__global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t ld, int n, cplx* w, int* info) {
-    __shared__ cplx h[kZSmall * (kZSmall + 1)];
+// kSchur = false: eigenvalues only, updates confined to the active block (ZLAHQR with WANTT =
+// WANTZ = false).  kSchur = true: the full Schur form T = V^H H V of the n x n block (left updates
+// to column n-1, right updates from row 0, V accumulated: WANTT = WANTZ = true), for the AED.
+// w[i] = the eigenvalue deflated at row i; failed / maxits / steps as for the kernel below.
+// AED early stop (kSchur, spk >= 0 = cabs1 of the window's spike): when an eigenvalue deflates at
+// the bottom row i its Schur vector column V(:, i) is final (later sweeps touch columns < i only),
+// so the AED spike test is taken right there; the first eigenvalue that fails it ends the
+// factorisation (stop = i; the rows above stay unreduced).  stop = -1: ran to completion.
+template <bool kSchur>
+__device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& maxits, int& steps,
+                          double spk = -1.0, int* stop = nullptr) {
     constexpr int lh = kZSmall + 1;
     const int ln = threadIdx.x;
     auto H = [&](int i, int j) -> cplx& { return h[i + j * lh]; };
-    for (int idx = ln; idx < n * n; idx += 64) H(idx % n, idx / n) = Hin[(idx % n) + (int64_t)(idx / n) * ld];
-    __syncthreads();
+    auto V = [&](int i, int j) -> cplx& { return v[i + j * lh]; };
     const double ulp = 2.220446049250313e-16, smlnum = 2.2250738585072014e-308 * ((double)n / ulp);
     const int itmax = 30 * max(10, n);
-    int failed = 0, maxits = 0, i = n - 1;
+    int i = n - 1;
+    failed = 0;
+    maxits = 0;
+    steps = 0;
     while (i >= 0) {
         int l = 0, its = 0;
         for (; its <= itmax; ++its) {
@@ -170,6 +182,7 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
                 }
             }
             // single-shift sweep from l
+            steps += i - l;
             for (int kk = l; kk < i; ++kk) {
                 cplx v0, v1;
                 if (kk == l) {
@@ -191,9 +204,9 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
                     H(kk + 1, kk - 1) = cplx{0.0, 0.0};
                 }
                 const cplx ct = cconj(tau);
-                {   // left: rows kk, kk+1, columns kk..i
+                {   // left: rows kk, kk+1, columns kk..i (Schur: ..n-1)
                     const int c = kk + ln;
-                    if (c <= i) {
+                    if (c <= (kSchur ? n - 1 : i)) {
                         const cplx a0 = H(kk, c), a1 = H(kk + 1, c);
                         const cplx s = mul(ct, add(a0, cmul_conj(vv, a1)));
                         H(kk, c) = sub(a0, s);
@@ -201,13 +214,19 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
                     }
                 }
                 EIGSOL_ZWAVE_ORDER();
-                {   // right: columns kk, kk+1, rows l..min(kk+2, i)
-                    const int r = l + ln;
+                {   // right: columns kk, kk+1, rows l..min(kk+2, i) (Schur: from row 0; and V)
+                    const int r = (kSchur ? 0 : l) + ln;
                     if (r <= min(kk + 2, i)) {
                         const cplx a0 = H(r, kk), a1 = H(r, kk + 1);
                         const cplx s = mul(tau, add(a0, mul(a1, vv)));
                         H(r, kk) = sub(a0, s);
                         H(r, kk + 1) = sub(a1, mul(s, cconj(vv)));
+                    }
+                    if (kSchur && ln < n) {
+                        const cplx a0 = V(ln, kk), a1 = V(ln, kk + 1);
+                        const cplx s = mul(tau, add(a0, mul(a1, vv)));
+                        V(ln, kk) = sub(a0, s);
+                        V(ln, kk + 1) = sub(a1, mul(s, cconj(vv)));
                     }
                 }
                 EIGSOL_ZWAVE_ORDER();
@@ -220,14 +239,175 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
         maxits = max(maxits, its);
         // H(l..i) has deflated to a single eigenvalue at i (l == i)
         if (ln == 0) w[i] = H(i, i);
+        if (kSchur && spk >= 0.0) {
+            double foo = cabs1(H(i, i));
+            if (foo == 0.0) foo = spk;
+            if (spk * cabs1(V(0, i)) > fmax(smlnum, ulp * foo)) {
+                *stop = i;
+                return;
+            }
+        }
         i = l - 1;
     }
+    if (stop) *stop = -1;
     if (failed) {
         for (int r = ln; r <= i; r += 64) w[r] = H(r, r);   // best effort, flagged as failed
     }
+}
+
+// Eigenvalues of an n x n Hessenberg block (n <= 64) in LDS.
+__global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t ld, int n, cplx* w, int* info) {
+    __shared__ cplx h[kZSmall * (kZSmall + 1)];
+    constexpr int lh = kZSmall + 1;
+    const int ln = threadIdx.x;
+    for (int idx = ln; idx < n * n; idx += 64) h[(idx % n) + (idx / n) * lh] = Hin[(idx % n) + (int64_t)(idx / n) * ld];
+    __syncthreads();
+    int failed, maxits, steps;
+    zwave_hqr<false>(h, nullptr, n, w, failed, maxits, steps);
     if (ln == 0) {
         info[0] = failed;
         info[1] = maxits;
+    }
+}
+
+// ---------------------------------------------------------------- complex aggressive early deflation
+// (ZLAQR3's idea, restated for one wave, as francis.hip's aed_kernel is for the real case.)  The
+// trailing nw x nw window T = H[kw:kw+nw, kw:kw+nw] of the active block is brought to complex
+// Schur form T = V S V^H (zwave_hqr<true>).  The window is coupled to the rest of the block only
+// through the spike s = H(kw, kw-1), which the similarity turns into the column s conj(V(0, :))^T;
+// trailing eigenvalues whose spike entry is negligible (cabs1(s) cabs1(V(0, j)) <=
+// max(smlnum, ulp cabs1(S(j, j))), ZLAQR3's test; no reordering) deflate outright, scanning from
+// the bottom to the first that does not.  When some deflate, the undeflated top part with its
+// spike is reduced back to Hessenberg form by complex Householder reflectors (ZLARFG convention,
+// accumulated into V), the window and the new spike are written back, and the caller applies V to
+// the rows of the block above the window (H[l:kw, kw:kw+nw] V).  w[kw + i] = S(i, i): the
+// deflated eigenvalues are final, the undeflated ones are the next sweep's shifts.
+// info = {fail, deflated, iterations, undeflated, steps}.
+struct ZAedCtl {
+    cplx tau, spike;
+    double beta;
+};
+__global__ __launch_bounds__(64) void zaed_kernel(cplx* Hg, int64_t n, int kw, int nw, int spike_valid, int early,
+                                                  cplx* w, cplx* Vout, int* info) {
+    constexpr int lh = kZSmall + 1;
+    __shared__ cplx t[kZSmall * lh];
+    __shared__ cplx v[kZSmall * lh];
+    __shared__ cplx hv[kZSmall];
+    __shared__ cplx sp[kZSmall];
+    __shared__ ZAedCtl c;
+    const int ln = threadIdx.x;
+    auto T = [&](int i, int j) -> cplx& { return t[i + j * lh]; };
+    auto V = [&](int i, int j) -> cplx& { return v[i + j * lh]; };
+    for (int e = ln; e < nw * nw; e += 64) {
+        const int i = e % nw, j = e / nw;
+        T(i, j) = Hg[(kw + i) + (int64_t)(kw + j) * n];
+        V(i, j) = i == j ? cplx{1.0, 0.0} : cplx{0.0, 0.0};
+    }
+    const cplx spike = (spike_valid && kw > 0) ? Hg[kw + (int64_t)(kw - 1) * n] : cplx{0.0, 0.0};
+    __syncthreads();
+    int fail, maxsw, steps, stop = -1;
+    zwave_hqr<true>(t, v, nw, w + kw, fail, maxsw, steps, early ? cabs1(spike) : -1.0, &stop);
+    __syncthreads();
+    // spike test, one window row per lane; deflated = the trailing run of negligible entries
+    const double ulp = 2.220446049250313e-16, smlnum = 2.2250738585072014e-308 * ((double)nw / ulp);
+    int nd = 0;
+    if (early) {
+        nd = fail ? 0 : nw - 1 - stop;   // the spike test ran inside the factorisation
+    } else if (!fail) {
+        bool keep = false;
+        if (ln < nw) {
+            double foo = cabs1(T(ln, ln));
+            if (foo == 0.0) foo = cabs1(spike);
+            keep = cabs1(spike) * cabs1(V(0, ln)) > fmax(smlnum, ulp * foo);
+        }
+        const unsigned long long km = __ballot(keep);
+        nd = km ? nw - 1 - (63 - __clzll(km)) : nw;
+    }
+    const int m = nw - nd;
+    // undeflated part + spike back to Hessenberg form.  Q = I - tau hv hv^H (hv[0] = 1) applied
+    // as Q^H T on rows [o, o + len) (columns [jlo, nw)), then T Q on T's rows [0, m) and V Q
+    auto reflect = [&](int o, int len, int jlo) {
+        const cplx tau = c.tau, ctau = cconj(tau);
+        for (int j = jlo + ln; j < nw; j += 64) {
+            cplx s{0.0, 0.0};
+            for (int i = 0; i < len; ++i) s = add(s, cmul_conj(hv[i], T(o + i, j)));
+            const cplx wv = mul(ctau, s);
+            for (int i = 0; i < len; ++i) T(o + i, j) = sub(T(o + i, j), mul(hv[i], wv));
+        }
+        __syncthreads();
+        if (ln < nw) {
+            cplx s{0.0, 0.0};
+            for (int jj = 0; jj < len; ++jj) s = add(s, mul(V(ln, o + jj), hv[jj]));
+            const cplx wv = mul(tau, s);
+            for (int jj = 0; jj < len; ++jj) V(ln, o + jj) = sub(V(ln, o + jj), mul(wv, cconj(hv[jj])));
+        }
+        if (ln < m) {
+            cplx s{0.0, 0.0};
+            for (int jj = 0; jj < len; ++jj) s = add(s, mul(T(ln, o + jj), hv[jj]));
+            const cplx wv = mul(tau, s);
+            for (int jj = 0; jj < len; ++jj) T(ln, o + jj) = sub(T(ln, o + jj), mul(wv, cconj(hv[jj])));
+        }
+        __syncthreads();
+    };
+    // ZLARFG of x[0..len) by the wave: hv, c.tau (0: Q = I), c.beta (real)
+    auto house = [&](const cplx* x, int len) {
+        const cplx alpha = x[0];
+        double part = 0.0;
+        for (int i = 1 + ln; i < len; i += 64) part += sq_abs(x[i]);
+        const double xn2 = wave_sum(part);
+        cplx tau{0.0, 0.0}, sc{0.0, 0.0};
+        double beta = alpha.re;
+        if (xn2 != 0.0 || alpha.im != 0.0) {
+            beta = -copysign(sqrt(sq_abs(alpha) + xn2), alpha.re);
+            tau = cplx{(beta - alpha.re) / beta, -alpha.im / beta};
+            sc = cdiv_s(cplx{1.0, 0.0}, cplx{alpha.re - beta, alpha.im});
+        }
+        __syncthreads();   // x may alias a T column the stores below do not touch; order the reads
+        for (int i = 1 + ln; i < len; i += 64) hv[i] = mul(x[i], sc);
+        if (ln == 0) {
+            hv[0] = cplx{1.0, 0.0};
+            c.tau = tau;
+            c.beta = beta;
+        }
+        __syncthreads();
+    };
+    if (nd > 0 && m > 0) {
+        for (int i = ln; i < m; i += 64) sp[i] = mul(spike, cconj(V(0, i)));
+        __syncthreads();
+        if (m > 1) {
+            house(sp, m);
+            if (ln == 0) c.spike = cplx{c.beta, 0.0};
+            __syncthreads();
+            if (c.tau.re != 0.0 || c.tau.im != 0.0) reflect(0, m, 0);
+        } else {
+            if (ln == 0) c.spike = sp[0];
+            __syncthreads();
+        }
+        for (int col = 0; col + 2 < m; ++col) {
+            house(&T(col + 1, col), m - col - 1);
+            if (ln == 0) T(col + 1, col) = cplx{c.beta, 0.0};
+            for (int i = col + 2 + ln; i < m; i += 64) T(i, col) = cplx{0.0, 0.0};
+            __syncthreads();
+            if (c.tau.re != 0.0 || c.tau.im != 0.0) reflect(col + 1, m - col - 1, col + 1);
+        }
+    } else if (ln == 0) {
+        c.spike = cplx{0.0, 0.0};
+    }
+    __syncthreads();
+    if (nd > 0) {
+        for (int e = ln; e < nw * nw; e += 64) {
+            const int i = e % nw, j = e / nw;
+            Hg[(kw + i) + (int64_t)(kw + j) * n] = i > j + 1 ? cplx{0.0, 0.0} : T(i, j);
+            Vout[e] = V(i, j);
+        }
+        if (ln == 0 && spike_valid && kw > 0) Hg[kw + (int64_t)(kw - 1) * n] = c.spike;
+    }
+    if (ln == 0) {
+        info[0] = fail;
+        info[1] = nd;
+        info[2] = maxsw;
+        info[3] = m;
+        info[4] = steps;
     }
 }
 
@@ -589,6 +769,9 @@ __global__ void zdiag_sub_kernel(const cplx* H, int64_t n, int ihi, cplx* out) {
 
 static double cabs1_h(const cplx& a) { return std::fabs(a.re) + std::fabs(a.im); }
 
+// AED window (EIGSOL_ZQR_AED overrides, 0: off)
+static constexpr int kZAedDefault = 48;
+
 // eigenvalues of the complex Hessenberg matrix H (device, n x n, leading dimension n; destroyed)
 int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_host, int32_t* sweeps_out,
                        int32_t* fail_out) {
@@ -601,8 +784,13 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         hipMalloc(&dU, (size_t)dev::kZMaxGroups * dev::kZWin * dev::kZWin * sizeof(cplx)) != hipSuccess ||
         hipMalloc(&dsh, 2 * dev::kZMaxBulges * sizeof(cplx)) != hipSuccess || hipMalloc(&dinfo, 64) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "complex QR: hipMalloc");
-    std::vector<cplx> ds(2 * n), swv(2 * dev::kZMaxBulges);
+    cplx* dV = nullptr;   // the AED window's unitary factor
+    if (rc == EIGSOL_OK && hipMalloc(&dV, (size_t)dev::kZSmall * dev::kZSmall * sizeof(cplx)) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "complex QR: hipMalloc");
+    std::vector<cplx> ds(2 * n), aw(dev::kZSmall);
     int sweeps = 0, failed = 0, stall = 0;
+    int st_sweeps = 0, st_aed = 0, st_aed_defl = 0, st_small = 0;
+    static const bool stats = std::getenv("EIGSOL_QR_STATS") != nullptr;
     int ihi = (int)n - 1;
     const int max_stall = std::max(1, maxits);
     auto small = [&](int l, int hi, cplx* wdst, int info[2]) -> int {
@@ -629,6 +817,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         const int N = ihi - l + 1;
         if (N <= dev::kZSmall) {
             int info[2];
+            ++st_small;
             if ((rc = small(l, ihi, dw + l, info)) != EIGSOL_OK) break;
             if (info[0]) failed = 1;
             sweeps = std::max({sweeps, stall, info[1]});
@@ -648,14 +837,71 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             const char* e = std::getenv("EIGSOL_ZQR_GROUPS");
             return e ? std::max(1, std::min(dev::kZMaxGroups, std::atoi(e))) : 2;
         }();
-        int nb = std::min(max_nb, std::max(1, N / 16));
-        const int C = std::max(1, std::min({max_groups, (nb + 7) / 8, 1 + N / (4 * (dev::kZWin + 12))}));
+        // aggressive early deflation on the trailing window; its undeflated eigenvalues are the shifts
+        static const int aed_win = [] {
+            const char* e = std::getenv("EIGSOL_ZQR_AED");   // AED window (0: off)
+            return e ? std::max(0, std::min(dev::kZSmall, std::atoi(e))) : kZAedDefault;
+        }();
+        static const int nibble = [] {   // % of the window deflated that skips the sweep (LAPACK's NIBBLE)
+            const char* e = std::getenv("EIGSOL_ZQR_NIBBLE");
+            return e ? std::max(1, std::atoi(e)) : 14;
+        }();
+        // EIGSOL_ZQR_AED_FULL=1: the window's whole Schur form (LAPACK's AED, the undeflated
+        // eigenvalues become the shifts); default: early stop at the first undeflatable eigenvalue,
+        // shifts from the trailing block afterwards
+        static const bool aed_full = [] {
+            const char* e = std::getenv("EIGSOL_ZQR_AED_FULL");
+            return e && std::atoi(e) != 0;
+        }();
+        int m_aed = 0;
+        if (aed_win >= 4) {
+            const int nw = std::min(aed_win, N);
+            const int kw = ihi - nw + 1;
+            hipLaunchKernelGGL(dev::zaed_kernel, dim3(1), dim3(64), 0, st, H, (int64_t)n, kw, nw, kw > l ? 1 : 0,
+                               aed_full ? 0 : 1, dw, dV, dinfo);
+            int info[5];
+            if (hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(aw.data(), dw + kw, nw * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
+                rc = fail(EIGSOL_E_HIP, "complex QR: aed");
+                break;
+            }
+            ++st_aed;
+            if (!info[0]) {
+                const int nd = info[1];
+                m_aed = aed_full ? info[3] : 0;   // early-stopped windows carry no shifts
+                if (nd > 0) {
+                    st_aed_defl += nd;
+                    if (kw > l) {   // rows of the block above the window: H[l, kw) x [kw, kw + nw) V
+                        dev::ZWinGemmBatch rb{H, (int64_t)n, 1, {}};
+                        rb.w[0] = dev::ZWinGemm{kw, nw, (int64_t)l, (int64_t)kw, 0, dV};
+                        hipLaunchKernelGGL(dev::zwin_gemm_mfma<false>, dim3((kw - l + dev::kZMG - 1) / dev::kZMG),
+                                           dim3(dev::kZMT), 0, st, rb);
+                    }
+                    const int m = info[3];
+                    ihi = kw + m - 1;
+                    sweeps = std::max(sweeps, stall);
+                    stall = 0;
+                    if (100 * nd >= nibble * nw || m < 2 || ihi - l + 1 <= dev::kZSmall) continue;
+                }
+            }
+        }
+        const int Nact = ihi - l + 1;   // after the AED's deflations
+        int nb = std::min(max_nb, std::max(1, Nact / 16));
+        if (m_aed >= 2) nb = std::min(nb, m_aed / 2);
+        const int C = std::max(1, std::min({max_groups, (nb + 7) / 8, 1 + Nact / (4 * (dev::kZWin + 12))}));
         const int nbg = std::max(1, std::min(8, nb / C));
         nb = nbg * C;
         const int ns = 2 * nb;
         std::vector<cplx> sh(ns);
         bool exceptional = stall % 6 == 0;
-        if (!exceptional) {
+        if (!exceptional && m_aed >= 2) {   // the bottom undeflated eigenvalues of the AED window
+            for (int i = 0; i < ns; ++i) sh[i] = aw[m_aed - ns + i];
+            if (hipMemcpyAsync(dsh, sh.data(), ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
+                rc = fail(EIGSOL_E_HIP, "complex QR: shift upload");
+                break;
+            }
+        } else if (!exceptional) {
             int info[2];
             if ((rc = small(ihi - ns + 1, ihi, dsh, info)) != EIGSOL_OK) break;   // shifts written to dsh
             if (info[0]) exceptional = true;
@@ -672,6 +918,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
                 break;
             }
         }
+        ++st_sweeps;
         // chase: chain g starts G steps after chain g-1 (windows stay disjoint); a round advances
         // every started chain's window by the same number of steps
         const int G = dev::kZWin + 3 * nbg;
@@ -752,7 +999,10 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             hipStreamSynchronize(st) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "complex QR: download");
     }
-    for (void* p : {(void*)dw, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo})
+    if (stats)
+        std::fprintf(stderr, "complex francis: n=%lld sweeps=%d small_blocks=%d aed=%d aed_deflated=%d\n", (long long)n,
+                     st_sweeps, st_small, st_aed, st_aed_defl);
+    for (void* p : {(void*)dw, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo, (void*)dV})
         if (p) (void)hipFree(p);
     *sweeps_out = std::max(1, sweeps);
     *fail_out = failed;

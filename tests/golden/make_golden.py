@@ -195,8 +195,18 @@ def main():
     n = 1024
     A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
     np.save(os.path.join(HERE, "qr_c1024_eigvals.npy"), np.linalg.eigvals(A).astype(np.complex128))
+    complex4096_fixture()
     convdiff_fixture()
     print("golden fixtures written")
+
+
+def complex4096_fixture():
+    """Complex QR at the config-2 order: LAPACK zgeev eigenvalues of the seeded
+    4096^2 complex N(0,1) matrix (seed 4096, real then imaginary parts, as bench.py draws it)."""
+    n = 4096
+    rng = np.random.default_rng(4096)
+    A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    np.save(os.path.join(HERE, "qr_c4096_eigvals.npy"), np.linalg.eigvals(A).astype(np.complex128))
 
 
 def shifted_inverse_loop(A, sigma, x0, max_iter, tol):

@@ -95,6 +95,26 @@ def test_qr_decompose_parity(ctx):
     np.testing.assert_allclose(Q @ R, A, atol=1e-11)
 
 
+@pytest.mark.parametrize("shape,cplx", [((200, 333), False), ((130, 130), True), ((257, 100), True)])
+def test_qr_decompose_blocked_parity(ctx, shape, cplx):
+    """Blocked compact-WY QR (hessenberg.hip qr_blocked: 32-reflector panels, GEMM trailing and Q
+    updates) against the reference's per-reflector loop (qr_decompose.hpp:46-85, oracle):
+    wide, square complex and tall complex shapes with partial last panels, and a zero column
+    (x.tail().norm() == 0: the step is skipped, qr_decompose.hpp:55-57)."""
+    rng = np.random.default_rng(sum(shape))
+    m, n = shape
+    A = rng.standard_normal((m, n))
+    if cplx:
+        A = A + 1j * rng.standard_normal((m, n))
+    A[:, 40] = 0.0
+    Q, R = E.qr_decompose(ctx, A)
+    Qo, Ro = O.qr_decompose(A)
+    sc = np.linalg.norm(A)
+    assert np.abs(Q - Qo).max() <= 1e-12 * m and np.abs(R - Ro).max() <= 1e-12 * sc
+    assert np.abs(Q @ R - A).max() <= 1e-12 * sc
+    assert np.abs(Q.conj().T @ Q - np.eye(m)).max() <= 1e-12 * m
+
+
 def test_kat_qr_eigenvalues_unshifted_matches_reference_counts(ctx):
     A = np.array([[2.0, 1.0], [1.0, 2.0]])
     r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12), variant="unshifted")
@@ -295,3 +315,32 @@ def test_complex_francis_structured(ctx):
     assert r.converged and np.all(r.eigenvalues_complex == 0)
     r = E.qr_eigenvalues(ctx, 1e-200 * B, E.SolverOptions(1000, 1e-12))
     _match(r.eigenvalues_complex * 1e200, np.linalg.eigvals(B), 1e-9 * np.linalg.norm(B))
+
+
+@pytest.mark.parametrize("coop", [True, False])
+def test_complex_hessenberg_blocked(ctx, coop, monkeypatch):
+    """Blocked complex reduction (hessenberg.hip, compact WY with 16-column panels, complex MFMA
+    GEMMs and the rank-32 trailing update) against the reference's per-column reflectors
+    (to_hessenberg.hpp:38-77, oracle restatement): the cooperative panel and the per-column panel
+    kernels, with a partial last panel (n - 2 = 298 reflector columns)."""
+    if not coop:
+        monkeypatch.setenv("EIGSOL_HESS_NO_COOP", "1")
+    rng = np.random.default_rng(300)
+    n = 300
+    A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    H = E.to_hessenberg(ctx, A)
+    scale = np.linalg.norm(A)
+    assert np.abs(H - O.hessenberg(A)).max() <= 1e-12 * scale
+    assert np.abs(np.tril(H, -2)).max() == 0.0
+
+
+def test_complex_francis_4096_fixture(ctx):
+    """Complex QR at the config-2 order: blocked complex Hessenberg, complex AED and multishift
+    sweeps, matched one-to-one against LAPACK zgeev (tests/golden/qr_c4096_eigvals.npy)."""
+    rng = np.random.default_rng(4096)
+    n = 4096
+    A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12))
+    assert r.converged
+    _match(r.eigenvalues_complex, np.load(os.path.join(HERE, "golden", "qr_c4096_eigvals.npy")),
+           1e-9 * np.linalg.norm(A))
