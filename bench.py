@@ -311,11 +311,11 @@ def run_config2(E, ctx, no_cpu):
     return out
 
 
-def run_qr_complex(E, ctx, no_cpu):
-    """qr_eigenvalues_dense<std::complex<double>> on a 1024^2 complex N(0,1) matrix (seed 1024):
-    complex Hessenberg + complex multishift sweeps (zfrancis.hip), matched to the zgeev fixture."""
-    n = 1024
-    rng = np.random.default_rng(1024)
+def run_qr_complex(E, ctx, no_cpu, n=1024):
+    """qr_eigenvalues_dense<std::complex<double>> on an n^2 complex N(0,1) matrix (seed n, n = 1024 or
+    4096): blocked complex Hessenberg + complex AED and multishift sweeps (zfrancis.hip), matched to
+    the zgeev fixture (tests/golden/qr_c<n>_eigvals.npy)."""
+    rng = np.random.default_rng(n)
     A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
     E.qr_eigenvalues(ctx, A[:128, :128].copy())   # warm-up
     t = time.perf_counter()
@@ -323,14 +323,14 @@ def run_qr_complex(E, ctx, no_cpu):
     dt = time.perf_counter() - t
     out = {"eigvals_per_s": round(n / dt, 1), "seconds": round(dt, 3), "converged": r.converged,
            "iterations": r.iterations, "dtype": "c128"}
-    fx = os.path.join(ROOT, "tests", "golden", "qr_c1024_eigvals.npy")
+    fx = os.path.join(ROOT, "tests", "golden", f"qr_c{n}_eigvals.npy")
     if os.path.exists(fx):
         from scipy.spatial import cKDTree
         ref = np.load(fx)
         ev = r.eigenvalues_complex
         d, j = cKDTree(np.c_[ref.real, ref.imag]).query(np.c_[ev.real, ev.imag], k=1)
         out["vs_lapack_fixture"] = {"max_abs_diff": float(d.max()), "one_to_one": bool(len(np.unique(j)) == n)}
-    if not no_cpu:
+    if not no_cpu and n <= 1024:   # (zgeev at 4096 takes ~40 s of host time: timed at 1024 only)
         t = time.perf_counter()
         np.linalg.eigvals(A)
         dl = time.perf_counter() - t
@@ -602,6 +602,7 @@ def main():
             "config1_A_txt": run_config1(E, S, ctx),
             "config2_qr_4096": run_config2(E, ctx, args.no_cpu_baseline),
             "qr_complex_1024": run_qr_complex(E, ctx, args.no_cpu_baseline),
+            "qr_complex_4096": run_qr_complex(E, ctx, args.no_cpu_baseline, 4096),
             "config5_shifted_inverse_1M": run_config5(E, S, ctx, torch, torch_stream, args.no_cpu_baseline),
             "config5_general_sparse_1M": run_config5_general(E, S, ctx),
             "dense_power_16384": run_dense_power(E, S, ctx, torch, torch_stream),

@@ -85,12 +85,15 @@ void DenseMatrix<S>::setRandom() {
     std::copy(v.begin(), v.end(), d_.begin());
 }
 
-// QR iteration variant: the reference's unshifted H <- RQ iteration (qr_eigenvalues.hpp:62-105,
-// identical iteration counts, `converged` and positional diag(H)) is what the reference-signature
-// overloads run; Francis (implicit multishift sweeps with aggressive early deflation, north_star)
-// is opt-in by passing QRVariant::Francis: it converges on general real and complex matrices, deflates at
-// LAPACK's threshold, reports `iterations` as its sweep count and returns the real parts in
-// `eigenvalues` with the complex eigenvalues in `eigenvalues_complex`.
+// QR iteration variant.  Francis (Hessenberg + implicit multishift sweeps with aggressive early
+// deflation, the north_star path) is the default of every overload, as in the Python binding: it
+// converges on general real and complex matrices (the reference's loop does not),
+// deflates at LAPACK's threshold, reports `iterations` as the most sweeps any deflation needed
+// (within [1, maxIterations] exactly when converged) and returns the real parts in `eigenvalues`
+// with the complex eigenvalues in `eigenvalues_complex`.  The reference's own unshifted H <- RQ
+// iteration (qr_eigenvalues.hpp:62-105: identical iteration counts, `converged` and positional
+// diag(H)) is QRVariant::Unshifted.  The reference's tests check sorted eigenvalues, `converged`
+// and 1 <= iterations <= maxIterations (qr_algorithms_test.cpp:253-332), which both satisfy.
 enum class QRVariant { Francis = EIGSOL_QR_FRANCIS, Unshifted = EIGSOL_QR_UNSHIFTED };
 
 namespace detail {
@@ -160,14 +163,14 @@ EigenResult<S> power_like(const Matrix& M, const SolverOptions& opts, const Vect
         if (xs0.size() != static_cast<std::size_t>(r))
             throw std::runtime_error(std::string(who) + ": start vector size mismatch");
         const eigsol_solver_options o = copts(opts);
-        // single precision runs natively (power method; shifted inverse on a triangular CSR); the
-        // dense and general-sparse shifted inverse have fp64 factors only
-        const bool native = !PromotedScalar<S> || !shift || !M.isDense();
+        // single precision runs natively (power method; shifted inverse on dense, banded and
+        // triangular factors); only a general sparse pattern with neither a usable band nor a dense
+        // factor that fits (ILU(0)-GMRES, double-only) is promoted to fp64
         int st = EIGSOL_E_UNSUPPORTED;
         if constexpr (WideScalar<S>) {   // long double: the fp64 kernels (see core.hpp)
             st = power_run<device_scalar_t<S>>(M.device_fp64<S>(), M.isDense(), o, xs0, shift, res);
         } else {
-            if (native) st = power_run<S>(M.device<S>(), M.isDense(), o, xs0, shift, res);
+            st = power_run<S>(M.device<S>(), M.isDense(), o, xs0, shift, res);
         }
         if constexpr (PromotedScalar<S>) {
             if (st == EIGSOL_E_UNSUPPORTED && shift)
@@ -229,12 +232,13 @@ Vector<S> solve_shifted(const Matrix& A, const S shift, const Vector<S>& b) {
             if (st == EIGSOL_OK) x = detail::convert_vec<S>(xd);
             return st;
         };
-        // single precision: triangular CSR natively, everything else on the fp64 factor
+        // single precision natively (dense, banded and triangular factors in float); the fp64
+        // factor only where the single-precision one is not built (general sparse via GMRES)
         int st = EIGSOL_E_UNSUPPORTED;
         if constexpr (WideScalar<S>) {
             st = run(device_scalar_t<S>{}, A.device_fp64<S>());
         } else {
-            if (!PromotedScalar<S> || !A.isDense()) st = run(S{}, A.device<S>());
+            st = run(S{}, A.device<S>());
         }
         if constexpr (PromotedScalar<S>)
             if (st == EIGSOL_E_UNSUPPORTED) st = run(device_scalar_t<S>{}, A.device_fp64<S>());
@@ -248,10 +252,10 @@ template <ScalarConcept S>
 DenseMatrix<S> to_hessenberg_dense(const DenseMatrix<S>& A) {
     detail::dense_square_check(A, "to_hessenberg_dense");
     detail::require_device_scalar<S>("to_hessenberg_dense");
-    if constexpr (PromotedScalar<S> || WideScalar<S>)
+    if constexpr (WideScalar<S>)
         return detail::convert_dense<S>(to_hessenberg_dense(detail::convert_dense<device_scalar_t<S>>(A)));
     DenseMatrix<S> H(A.rows(), A.cols());
-    if constexpr (DeviceScalar<S>) {
+    if constexpr (DeviceScalar<S> || PromotedScalar<S>) {   // single precision: native float reduction
         if (A.rows() > 0)
             detail::check(eigsol_hessenberg_dense(detail::ctx(), detail::dtype_of<S>(), A.rows(), A.data(), H.data()),
                           "to_hessenberg_dense");
@@ -270,7 +274,7 @@ template <ScalarConcept S>
 void qr_decompose_dense(const DenseMatrix<S>& A, DenseMatrix<S>& Q, DenseMatrix<S>& R) {
     if (A.rows() == 0 || A.cols() == 0) throw std::runtime_error("qr_decompose_dense: empty matrix");
     detail::require_device_scalar<S>("qr_decompose_dense");
-    if constexpr (PromotedScalar<S> || WideScalar<S>) {
+    if constexpr (WideScalar<S>) {
         using D = device_scalar_t<S>;
         DenseMatrix<D> Qd, Rd;
         qr_decompose_dense<D>(detail::convert_dense<D>(A), Qd, Rd);
@@ -280,7 +284,7 @@ void qr_decompose_dense(const DenseMatrix<S>& A, DenseMatrix<S>& Q, DenseMatrix<
     }
     Q = DenseMatrix<S>(A.rows(), A.rows());
     R = DenseMatrix<S>(A.rows(), A.cols());
-    if constexpr (DeviceScalar<S>)
+    if constexpr (DeviceScalar<S> || PromotedScalar<S>)   // single precision: native float QR
         detail::check(eigsol_qr_decompose_dense(detail::ctx(), detail::dtype_of<S>(), A.rows(), A.cols(), A.data(),
                                                 Q.data(), R.data()),
                       "qr_decompose_dense");
@@ -297,12 +301,14 @@ std::pair<DenseMatrix<S>, DenseMatrix<S>> qr_decompose(const Matrix& A) {
 
 template <ScalarConcept S>
 QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& opts,
-                                 QRVariant variant = QRVariant::Unshifted) {
+                                 QRVariant variant = QRVariant::Francis) {
     detail::dense_square_check(A, "qr_eigenvalues_dense");
     const std::int64_t n = A.rows();
     if (n == 0) return QRResult<S>(Vector<S>(), 0, true);   // qr_eigenvalues.hpp:55-57
     detail::require_device_scalar<S>("qr_eigenvalues_dense");
-    if constexpr (PromotedScalar<S> || WideScalar<S>) {
+    // single precision: the reference's unshifted iteration natively in float; the Francis sweeps
+    // (double kernels) on the fp64 promotion, eigenvalues rounded back
+    if constexpr (WideScalar<S> || PromotedScalar<S>) if (WideScalar<S> || variant == QRVariant::Francis) {
         using D = device_scalar_t<S>;
         const QRResult<D> rd = qr_eigenvalues_dense<D>(detail::convert_dense<D>(A), opts, variant);
         QRResult<S> rs(detail::convert_vec<S>(rd.eigenvalues), rd.iterations, rd.converged);
@@ -310,7 +316,7 @@ QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& o
         return rs;
     }
     QRResult<S> res;
-    if constexpr (DeviceScalar<S>) {
+    if constexpr (DeviceScalar<S> || PromotedScalar<S>) {
         Vector<S> ev(static_cast<std::size_t>(n));
         std::vector<double> wi(static_cast<std::size_t>(n), 0.0);
         std::int32_t it = 0, conv = 0;
@@ -331,7 +337,7 @@ QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& o
 }
 
 template <ScalarConcept S>
-QRResult<S> qr_eigenvalues(const Matrix& A, const SolverOptions& opts, QRVariant variant = QRVariant::Unshifted) {
+QRResult<S> qr_eigenvalues(const Matrix& A, const SolverOptions& opts, QRVariant variant = QRVariant::Francis) {
     if (!A.isDense()) throw std::runtime_error("qr_eigenvalues(Matrix): only dense matrices are supported");
     if (A.scalar_type() != typeid(S)) throw std::runtime_error("qr_eigenvalues(Matrix): scalar type mismatch");
     return qr_eigenvalues_dense<S>(A.cast<DenseMatrix<S>>(), opts, variant);

@@ -44,6 +44,8 @@ namespace dev {
 
 __device__ __forceinline__ double bscore(double v) { return fabs(v); }
 __device__ __forceinline__ double bscore(cplx v) { return hypot(v.re, v.im); }
+__device__ __forceinline__ double bscore(float v) { return fabs((double)v); }
+__device__ __forceinline__ double bscore(cplxf v) { return hypot((double)v.re, (double)v.im); }
 
 __device__ __forceinline__ double b_readlane(double v, int src) {
     const long long b = __double_as_longlong(v);
@@ -52,6 +54,10 @@ __device__ __forceinline__ double b_readlane(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 __device__ __forceinline__ cplx b_readlane(cplx v, int src) { return cplx{b_readlane(v.re, src), b_readlane(v.im, src)}; }
+__device__ __forceinline__ float b_readlane(float v, int src) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+__device__ __forceinline__ cplxf b_readlane(cplxf v, int src) { return cplxf{b_readlane(v.re, src), b_readlane(v.im, src)}; }
 
 // Scatter of M = A - sigma I (host-built CSR, diagonal present) into the band, rows and columns
 // renumbered by iperm (old -> new).
@@ -519,7 +525,7 @@ void band_plan(int dtype, int64_t n, const int32_t* rp, const int32_t* ci, BandP
 
 template <class S>
 static S bh_sub(S a, S b) {
-    if constexpr (std::is_same_v<S, double>) return a - b;
+    if constexpr (is_real_v<S>) return a - b;
     else return S{a.re - b.re, a.im - b.im};
 }
 
@@ -544,8 +550,8 @@ static int band_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* r
     const int64_t ld = f->ldab - 1;
     // M = A - sigma I (solve_shifted.hpp:96-102: coeffRef inserts a missing diagonal), host CSR
     S sig;
-    if constexpr (std::is_same_v<S, double>) { (void)sim; sig = sre; }
-    else sig = S{sre, sim};
+    if constexpr (is_real_v<S>) { (void)sim; sig = (S)sre; }
+    else sig = S{(decltype(S::re))sre, (decltype(S::re))sim};
     std::vector<int32_t> mrp(n + 1, 0), mci;
     std::vector<S> mv;
     mci.reserve(rp[n] + n);
@@ -664,7 +670,9 @@ int band_create(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const 
         return band_create_t<cplx>(ctx, dtype, n, rp, ci, static_cast<const cplx*>(v), sre, sim, plan, out);
     if (dtype == EIGSOL_F64)
         return band_create_t<double>(ctx, dtype, n, rp, ci, static_cast<const double*>(v), sre, sim, plan, out);
-    return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: the band factor is built for double and complex<double>");
+    if (dtype == EIGSOL_F32)   // single precision: factored and solved in float (native)
+        return band_create_t<float>(ctx, dtype, n, rp, ci, static_cast<const float*>(v), sre, sim, plan, out);
+    return band_create_t<cplxf>(ctx, dtype, n, rp, ci, static_cast<const cplxf*>(v), sre, sim, plan, out);
 }
 
 template <class S>
@@ -708,6 +716,10 @@ int band_launch(BandFactor* f, bool iter, const void* b, void* y, void* buf0, vo
                 const void* rank_part, void* my_part, void* trace, int parity) {
     if (f->dtype == EIGSOL_C128)
         return band_launch_t<cplx>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+    if (f->dtype == EIGSOL_F32)
+        return band_launch_t<float>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+    if (f->dtype == EIGSOL_C64)
+        return band_launch_t<cplxf>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
     return band_launch_t<double>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
 }
 

@@ -903,6 +903,18 @@ struct SlicePlan {
     static constexpr int ns = pipe > 0 ? 1 : 2;
 #endif
 };
+// float: a slice's registers are small enough that four slices per round, all loads issued before
+// any is consumed, beat the software pipeline: band10m f32 149.3 -> 130.9 us (6.16 -> 7.03 TB/s
+// algorithmic), 1M x 16 band 23.6 -> 21.6 us; two / three slices with a pipeline 141-142 / 136 us
+// (tools/f32_ab.sh)
+#if !defined(EIGSOL_SLICE_PIPE) && !defined(EIGSOL_SLICE_NS)
+template <int KB, bool kG>
+struct SlicePlan<float, KB, kG> {
+    static constexpr int bytes = (int)sizeof(SliceRegs<float, KB, kG>);
+    static constexpr int pipe = 0;
+    static constexpr int ns = 4;
+};
+#endif
 
 template <class S, bool kPower, int KB, bool kG, bool kDist = false>
 __global__ __launch_bounds__(kThreads) void csr_slice_kernel(CsrArgs<S> a, int parity) {

@@ -428,13 +428,20 @@ __device__ __forceinline__ int wave_max_int(int v) {
     return v;
 }
 
+// AED early stop (kSchur, spk >= 0 = |spike|): a block deflating at the bottom has final Schur
+// vector columns (later sweeps touch only the columns of the rows above), so the AED spike test is
+// taken when it deflates; the first block that fails it ends the factorisation (*stop = its last
+// row; the rows above stay unreduced).  *stop = -1: ran to completion.
 template <bool kSchur, int NX>
 __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double* wr, double* wi, int* bs,
-                         int& fail, int& total, int& maxsw, int* steps_out = nullptr) {
+                         int& fail, int& total, int& maxsw, int* steps_out = nullptr, double spk = -1.0,
+                         int* stop = nullptr) {
     const int lane = threadIdx.x & 63;
     auto T = [&](int i, int j) -> double& { return t[i + j * LD]; };
     auto V = [&](int i, int j) -> double& { return v[i + j * LD]; };
     const double eps = 2.220446049250313e-16;
+    const double aed_sml = 2.2250738585072014e-308 * (n / eps);
+    if (stop) *stop = -1;
     int nn = n - 1, its = 0;
     fail = 0;
     total = 0;
@@ -458,6 +465,13 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
                 wi[nn] = 0.0;
                 if (kSchur) bs[nn] = 1;
             }
+            if (kSchur && spk >= 0.0) {
+                const double foo = x == 0.0 ? spk : fabs(x);
+                if (fabs(spk * V(0, nn)) > fmax(aed_sml, eps * foo)) {
+                    *stop = nn;
+                    return;
+                }
+            }
             --nn;
             maxsw = max(maxsw, its);
             its = 0;
@@ -479,6 +493,14 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
                     wi[nn] = z;
                 }
                 if (kSchur) bs[nn] = bs[nn - 1] = 2;
+            }
+            if (kSchur && spk >= 0.0) {
+                double foo = fabs(x) + sqrt(fabs(T(nn, nn - 1))) * sqrt(fabs(T(nn - 1, nn)));
+                if (foo == 0.0) foo = spk;
+                if (fmax(fabs(spk * V(0, nn)), fabs(spk * V(0, nn - 1))) > fmax(aed_sml, eps * foo)) {
+                    *stop = nn;
+                    return;
+                }
             }
             nn -= 2;
             maxsw = max(maxsw, its);
@@ -652,7 +674,7 @@ struct AedCtl {
 };
 
 __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, int nw, int spike_valid, int maxits,
-                                                 double* wr, double* wi, double* Vout, int* info) {
+                                                 int early, double* wr, double* wi, double* Vout, int* info) {
     constexpr int LD = kAedMax + 1;
     __shared__ double t[kAedMax * LD];
     __shared__ double v[kAedMax * LD];
@@ -674,15 +696,19 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
     int fail = 0, total = 0, maxsw = 0;
     const long long tA = wall_clock64();
     // ---------------- phase A: real Schur form with V
-    int steps = 0;
+    int steps = 0, stop = -1;
+    const double spk = early ? fabs(spike) : -1.0;
     if (tid < 64) {
-        if (nw <= 64) wave_hqr<true, 1>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
-        else wave_hqr<true, 2>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps);
+        if (nw <= 64) wave_hqr<true, 1>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps, spk, &stop);
+        else wave_hqr<true, 2>(t, v, nw, LD, maxits, wr + kw, wi + kw, bs, fail, total, maxsw, &steps, spk, &stop);
     }
     __syncthreads();
     const long long tB = wall_clock64();
     // ---------------- phase B: spike test from the bottom
-    if (tid == 0) {
+    if (tid == 0 && early) {
+        c.nd = fail ? 0 : nw - 1 - stop;   // the spike test ran inside the factorisation
+        c.beta = 0.0;
+    } else if (tid == 0) {
         int nd = 0;
         if (!fail) {
             const double smlnum = 2.2250738585072014e-308 * (nw / eps);
@@ -875,6 +901,15 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         const char* e = std::getenv("EIGSOL_QR_AED");   // AED window (0: off)
         return e ? std::max(0, std::min(dev::kAedMax, std::atoi(e))) : kAedDefault;
     }();
+    // AED early stop (default; EIGSOL_QR_AED_EARLY=0: the whole window Schur form, whose undeflated
+    // eigenvalues are the shifts).  4096^2: 1.33 -> 1.23 s (the window's factorisation stops at the
+    // first undeflatable block: 378 -> 192 ms of one-wave steps; the shifts then come from the
+    // trailing block, and the sweeps drop from 146 to 128); grid over window 48/56/64, nibble 30/50,
+    // bulges 28/36: window 64, nibble 30, 28 bulges is the optimum (tools/qr_ab_round3.sh)
+    static const bool aed_early = [] {
+        const char* e = std::getenv("EIGSOL_QR_AED_EARLY");
+        return !e || std::atoi(e) != 0;
+    }();
     static const int kNibble = [] {   // % of the AED window deflated that skips the sweep (LAPACK's NIBBLE)
         const char* e = std::getenv("EIGSOL_QR_NIBBLE");
         return e ? std::max(1, std::atoi(e)) : 30;
@@ -922,8 +957,8 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         if (aed_win > 0) {
             const int nw = std::min(aed_win, N);
             const int kw = ihi - nw + 1;
-            hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(64), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60, dwr, dwi,
-                               dU, dinfo);
+            hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(64), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60,
+                               aed_early ? 1 : 0, dwr, dwi, dU, dinfo);
             int info[8];
             std::vector<double> awr(nw), awi(nw);
             if (hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -950,18 +985,23 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                     stall = 0;
                     if (100 * nd >= kNibble * nw || m < 4) continue;   // enough deflated: look again first
                 }
-                // shifts: the bottom undeflated eigenvalues of the window
-                const int N2 = ihi - l + 1;
-                nb = std::min({max_bulges, std::max(1, N2 / 8), std::max(1, m / 2)});
-                ns = 2 * nb;
-                for (int i = 0; i < ns; ++i) {
-                    swr[i] = awr[m - ns + i];
-                    swi[i] = awi[m - ns + i];
+                // shifts: the bottom undeflated eigenvalues of the window (early-stopped windows
+                // have none: the trailing block's, below)
+                if (!aed_early) {
+                    const int N2 = ihi - l + 1;
+                    nb = std::min({max_bulges, std::max(1, N2 / 8), std::max(1, m / 2)});
+                    ns = 2 * nb;
+                    for (int i = 0; i < ns; ++i) {
+                        swr[i] = awr[m - ns + i];
+                        swi[i] = awi[m - ns + i];
+                    }
+                    have_shifts = true;
                 }
-                have_shifts = true;
             }
         }
         if (!have_shifts) {
+            nb = std::min(max_bulges, std::max(1, (ihi - l + 1) / 8));
+            ns = 2 * nb;
             // shifts: eigenvalues of the trailing 2nb x 2nb block
             rc = hqr_small(st, H + (ihi - ns + 1) + (int64_t)(ihi - ns + 1) * n, n, ns, 60, dwr + ihi - ns + 1,
                            dwi + ihi - ns + 1, dinfo);

@@ -37,26 +37,63 @@ template <> struct HessCfg<cplx> {
     static constexpr int kMaxLdsN = 8192;    // 128 KiB
     static constexpr int kCoopMaxN = 4096;   // v (64 KiB) + the partial / row buffers: < 160 KiB
 };
+// single precision (float / complex<float>): the same reductions in the scalar's own type; norms
+// and the reflector's scalars are formed in double and rounded, like the power method's partials
+template <> struct HessCfg<float> {
+    static constexpr int NB = 32;
+    static constexpr int kMaxLdsN = 16384;
+    static constexpr int kCoopMaxN = 8192;
+};
+template <> struct HessCfg<cplxf> {
+    static constexpr int NB = 16;
+    static constexpr int kMaxLdsN = 16384;
+    static constexpr int kCoopMaxN = 8192;
+};
 constexpr int kPanel = 32;          // the widest panel (array bounds)
 constexpr int kGemvCols = 128;      // columns per GEMV partial
 
 __device__ __forceinline__ double cj(double a) { return a; }
 __device__ __forceinline__ cplx cj(cplx a) { return cplx{a.re, -a.im}; }
+__device__ __forceinline__ float cj(float a) { return a; }
+__device__ __forceinline__ cplxf cj(cplxf a) { return cplxf{a.re, -a.im}; }
 __device__ __forceinline__ double wsum(double v) { return wave_sum(v); }
 __device__ __forceinline__ cplx wsum(cplx v) { return cplx{wave_sum(v.re), wave_sum(v.im)}; }
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ cplxf wsum(cplxf v) { return cplxf{wsum(v.re), wsum(v.im)}; }
 __device__ __forceinline__ void st_ag(double* p, double v) { st_agent(p, v); }
 __device__ __forceinline__ void st_ag(cplx* p, cplx v) {
     st_agent(&p->re, v.re);
     st_agent(&p->im, v.im);
 }
+__device__ __forceinline__ void st_ag(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_ag(cplxf* p, cplxf v) {
+    st_ag(&p->re, v.re);
+    st_ag(&p->im, v.im);
+}
 __device__ __forceinline__ double ld_ag(const double* p) { return ld_agent(p); }
 __device__ __forceinline__ cplx ld_ag(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
+__device__ __forceinline__ float ld_ag(const float* p) {
+    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ cplxf ld_ag(const cplxf* p) { return cplxf{ld_ag(&p->re), ld_ag(&p->im)}; }
 __device__ __forceinline__ double scal(double a, double s) { return a * s; }
 __device__ __forceinline__ cplx scal(cplx a, double s) { return cplx{a.re * s, a.im * s}; }
+__device__ __forceinline__ float scal(float a, double s) { return a * (float)s; }
+__device__ __forceinline__ cplxf scal(cplxf a, double s) { return cplxf{a.re * (float)s, a.im * (float)s}; }
 __device__ __forceinline__ double two_x(double a) { return 2.0 * a; }
 __device__ __forceinline__ cplx two_x(cplx a) { return cplx{2.0 * a.re, 2.0 * a.im}; }
+__device__ __forceinline__ float two_x(float a) { return 2.0f * a; }
+__device__ __forceinline__ cplxf two_x(cplxf a) { return cplxf{2.0f * a.re, 2.0f * a.im}; }
 __device__ __forceinline__ double neg2(double a) { return -2.0 * a; }
 __device__ __forceinline__ cplx neg2(cplx a) { return cplx{-2.0 * a.re, -2.0 * a.im}; }
+__device__ __forceinline__ float neg2(float a) { return -2.0f * a; }
+__device__ __forceinline__ cplxf neg2(cplxf a) { return cplxf{-2.0f * a.re, -2.0f * a.im}; }
 
 // The reference's reflector from x0 = a(j+1) and tail = ||a(j+2:)||^2 (to_hessenberg.hpp:45-65):
 // alpha = -phase(x0) ||x||, v0 = x0 - alpha, rv = 1 / ||(v0, x(1:))||; sk when skipped.
@@ -89,6 +126,20 @@ __device__ __forceinline__ void hess_reflector(cplx x0, double tail, bool& sk, c
         if (vn == 0.0) sk = true;
         else rv = 1.0 / vn;
     }
+}
+
+// single precision: the reflector's scalars in double (x0 exact in double), rounded to S
+__device__ __forceinline__ void hess_reflector(float x0, double tail, bool& sk, float& v0, double& rv, float& alpha) {
+    double v0d, ad;
+    hess_reflector((double)x0, tail, sk, v0d, rv, ad);
+    v0 = (float)v0d;
+    alpha = (float)ad;
+}
+__device__ __forceinline__ void hess_reflector(cplxf x0, double tail, bool& sk, cplxf& v0, double& rv, cplxf& alpha) {
+    cplx v0d, ad;
+    hess_reflector(cplx{(double)x0.re, (double)x0.im}, tail, sk, v0d, rv, ad);
+    v0 = cplxf{(float)v0d.re, (float)v0d.im};
+    alpha = cplxf{(float)ad.re, (float)ad.im};
 }
 
 // block (1024 threads) sum of NB partials per thread -> sw[0..cnt)
@@ -611,19 +662,23 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
 // C (m x nn, ldc) += alpha * op(A) op(B); op = transpose when TA / TB.  64x64 tiles, 4x4/thread.
 // Split-K: blockIdx.z takes rows [z kc, (z+1) kc) of the K range and, when gridDim.z > 1, writes its
 // partial product to C + z * zstride (beta must be 0 then; gemm_reduce adds the partials in z order).
-template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_f64(int m, int nn, int kk, double alpha, const double* A, int64_t lda,
-                                                const double* B, int64_t ldb, double beta, double* C, int64_t ldc,
-                                                int kc, int64_t zstride) {
+template <class S, bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_valu(int m, int nn, int kk, double alpha, const S* A, int64_t lda,
+                                                 const S* B, int64_t ldb, double beta, S* C, int64_t ldc,
+                                                 int kc, int64_t zstride) {
     constexpr int TM = 64, KT = 16;
-    __shared__ double As[KT][TM + 1];
-    __shared__ double Bs[KT][TM + 1];
+    __shared__ S As[KT][TM + 1];
+    __shared__ S Bs[KT][TM + 1];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int i0 = blockIdx.x * TM, j0 = blockIdx.y * TM;
     const int kb = blockIdx.z * kc;
     const int ke = min(kk, kb + kc);
     C += blockIdx.z * zstride;
-    double acc[4][4] = {};
+    S acc[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc[u][w] = s_zero<S>();
     for (int k0 = kb; k0 < ke; k0 += KT) {
         for (int e = threadIdx.x; e < KT * TM; e += 256) {
             int r, q;
@@ -631,29 +686,29 @@ __global__ __launch_bounds__(256) void gemm_f64(int m, int nn, int kk, double al
             if (!TA) { r = e % TM; q = e / TM; } else { q = e % KT; r = e / KT; }
             {
                 const int gi = i0 + r, gk = k0 + q;
-                double val = 0.0;
-                if (gi < m && gk < ke) val = TA ? A[gk + (int64_t)gi * lda] : A[gi + (int64_t)gk * lda];
+                S val = s_zero<S>();
+                if (gi < m && gk < ke) val = TA ? cj(A[gk + (int64_t)gi * lda]) : A[gi + (int64_t)gk * lda];
                 As[q][r] = val;
             }
             // B tile: op(B)(k0 + q, j0 + r)
             if (!TB) { q = e % KT; r = e / KT; } else { r = e % TM; q = e / TM; }
             {
                 const int gk = k0 + q, gj = j0 + r;
-                double val = 0.0;
-                if (gk < ke && gj < nn) val = TB ? B[gj + (int64_t)gk * ldb] : B[gk + (int64_t)gj * ldb];
+                S val = s_zero<S>();
+                if (gk < ke && gj < nn) val = TB ? cj(B[gj + (int64_t)gk * ldb]) : B[gk + (int64_t)gj * ldb];
                 Bs[q][r] = val;
             }
         }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < KT; ++q) {
-            double av[4], bv[4];
+            S av[4], bv[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) { av[u] = As[q][tx + 16 * u]; bv[u] = Bs[q][ty + 16 * u]; }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
-                for (int w = 0; w < 4; ++w) acc[u][w] += av[u] * bv[w];
+                for (int w = 0; w < 4; ++w) acc[u][w] = add(acc[u][w], mul(av[u], bv[w]));
         }
         __syncthreads();
     }
@@ -663,8 +718,8 @@ __global__ __launch_bounds__(256) void gemm_f64(int m, int nn, int kk, double al
         for (int w = 0; w < 4; ++w) {
             const int gi = i0 + tx + 16 * u, gj = j0 + ty + 16 * w;
             if (gi < m && gj < nn) {
-                double* cp = C + gi + (int64_t)gj * ldc;
-                *cp = (beta == 0.0 ? 0.0 : beta * *cp) + alpha * acc[u][w];
+                S* cp = C + gi + (int64_t)gj * ldc;
+                *cp = add(beta == 0.0 ? s_zero<S>() : scal(*cp, beta), scal(acc[u][w], alpha));
             }
         }
 }
@@ -840,7 +895,8 @@ __global__ void gemm_reduce(int m, int nn, int nz, const S* P, double beta, S* C
 }
 
 // dst(0:rows, 0:cols) = conj(src(...)), column-major
-__global__ void conj_copy2d(cplx* dst, int64_t ldd, const cplx* src, int64_t lds, int rows, int cols) {
+template <class S>
+__global__ void conj_copy2d(S* dst, int64_t ldd, const S* src, int64_t lds, int rows, int cols) {
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (int64_t)rows * cols) return;
     const int i = (int)(idx % rows);
@@ -866,10 +922,13 @@ void gemm(hipStream_t st, int m, int nn, int kk, double alpha, const S* A, int64
     auto launch = [&](dim3 g, double be, S* Cp, int64_t ldcp, int kc, int64_t zs) {
         if constexpr (std::is_same_v<S, double>) {
             static const bool valu = std::getenv("EIGSOL_GEMM_VALU") != nullptr;
-            auto kern = valu ? dev::gemm_f64<TA, TB> : dev::gemm_mfma_f64<TA, TB>;
+            auto kern = valu ? dev::gemm_valu<double, TA, TB> : dev::gemm_mfma_f64<TA, TB>;
             hipLaunchKernelGGL(kern, g, dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb, be, Cp, ldcp, kc, zs);
-        } else {
+        } else if constexpr (std::is_same_v<S, cplx>) {
             hipLaunchKernelGGL((dev::gemm_mfma_c128<TA, TB>), g, dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb,
+                               be, Cp, ldcp, kc, zs);
+        } else {   // single precision: the small panel GEMMs on the VALU
+            hipLaunchKernelGGL((dev::gemm_valu<S, TA, TB>), g, dim3(256), 0, st, m, nn, kk, alpha, A, lda, B, ldb,
                                be, Cp, ldcp, kc, zs);
         }
     };
@@ -888,7 +947,7 @@ void gemm(hipStream_t st, int m, int nn, int kk, double alpha, const S* A, int64
 // In place on the device matrix A (n x n, column-major, ld = n).
 template <class S>
 int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
-    constexpr bool kC = std::is_same_v<S, cplx>;
+    constexpr bool kC = !is_real_v<S>;
     using Cfg = dev::HessCfg<S>;
     const int n = (int)n64;
     if (n < 3) return EIGSOL_OK;
@@ -981,10 +1040,10 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
             if constexpr (kC) {
                 gemm<S, false, true>(st, nbp, mt, nbp, -1.0, M, NB, V + c1, n, 1.0, W, NB);          // W = V^H (A Q)
                 const int64_t cnt = (int64_t)mt * nbp;
-                hipLaunchKernelGGL(dev::conj_copy2d, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, R,
+                hipLaunchKernelGGL(dev::conj_copy2d<S>, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, R,
                                    (int64_t)n, V + c1, (int64_t)n, mt, nbp);                          // conj V(c1:, :)
                 gemm<S, true, false>(st, mt, nbp, nbp, 1.0, W, NB, T, NB, 0.0, R2, n);               // W^H T
-                hipLaunchKernelGGL(dev::conj_copy2d, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, R2,
+                hipLaunchKernelGGL(dev::conj_copy2d<S>, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, R2,
                                    (int64_t)n, R2, (int64_t)n, mt, nbp);                              // W2^T
             } else {
                 EIGSOL_HIP(hipMemcpy2DAsync(R, n * sizeof(S), V + c1, n * sizeof(S), mt * sizeof(S), nbp,
@@ -1016,7 +1075,7 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
 // kernels).
 template <class S>
 int qr_blocked(hipStream_t st, S* R, int m, int n, S* Q) {
-    constexpr bool kC = std::is_same_v<S, cplx>;
+    constexpr bool kC = !is_real_v<S>;
     constexpr int NB = 32;
     if (m > dev::HessCfg<S>::kMaxLdsN) return fail(EIGSOL_E_UNSUPPORTED, "blocked QR: m above the LDS panel limit");
     const int kmax = std::min(m, n);
@@ -1049,7 +1108,7 @@ int qr_blocked(hipStream_t st, S* R, int m, int n, S* Q) {
         const S* Vr = V;
         if constexpr (kC) {
             const int64_t cnt = (int64_t)m * nbp;
-            hipLaunchKernelGGL(dev::conj_copy2d, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, Vc, (int64_t)m, V,
+            hipLaunchKernelGGL(dev::conj_copy2d<S>, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, Vc, (int64_t)m, V,
                                (int64_t)m, m, nbp);
             Vr = Vc;
         }
@@ -1066,5 +1125,9 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n) { return hessen
 int hessenberg_blocked_c128(hipStream_t st, cplx* A, int64_t n) { return hessenberg_blocked<cplx>(st, A, n); }
 int qr_blocked_f64(hipStream_t st, double* R, int64_t m, int64_t n, double* Q) { return qr_blocked<double>(st, R, (int)m, (int)n, Q); }
 int qr_blocked_c128(hipStream_t st, cplx* R, int64_t m, int64_t n, cplx* Q) { return qr_blocked<cplx>(st, R, (int)m, (int)n, Q); }
+int hessenberg_blocked_f32(hipStream_t st, float* A, int64_t n) { return hessenberg_blocked<float>(st, A, n); }
+int hessenberg_blocked_c64(hipStream_t st, cplxf* A, int64_t n) { return hessenberg_blocked<cplxf>(st, A, n); }
+int qr_blocked_f32(hipStream_t st, float* R, int64_t m, int64_t n, float* Q) { return qr_blocked<float>(st, R, (int)m, (int)n, Q); }
+int qr_blocked_c64(hipStream_t st, cplxf* R, int64_t m, int64_t n, cplxf* Q) { return qr_blocked<cplxf>(st, R, (int)m, (int)n, Q); }
 
 }  // namespace eigsol

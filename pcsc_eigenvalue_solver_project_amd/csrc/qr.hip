@@ -34,6 +34,14 @@ __device__ __forceinline__ double abs_(double a) { return fabs(a); }
 __device__ __forceinline__ double abs_(cplx a) { return hypot(a.re, a.im); }
 __device__ __forceinline__ bool is_zero(double a) { return a == 0.0; }
 __device__ __forceinline__ bool is_zero(cplx a) { return a.re == 0.0 && a.im == 0.0; }
+__device__ __forceinline__ float conj_(float a) { return a; }
+__device__ __forceinline__ cplxf conj_(cplxf a) { return cplxf{a.re, -a.im}; }
+__device__ __forceinline__ float scale_(float a, double s) { return a * (float)s; }
+__device__ __forceinline__ cplxf scale_(cplxf a, double s) { return cplxf{a.re * (float)s, a.im * (float)s}; }
+__device__ __forceinline__ double abs_(float a) { return fabs((double)a); }
+__device__ __forceinline__ double abs_(cplxf a) { return hypot((double)a.re, (double)a.im); }
+__device__ __forceinline__ bool is_zero(float a) { return a == 0.0f; }
+__device__ __forceinline__ bool is_zero(cplxf a) { return a.re == 0.0f && a.im == 0.0f; }
 
 template <class S>
 __device__ __forceinline__ S at(const S* A, int64_t ld, int64_t i, int64_t j) { return A[i + j * ld]; }
@@ -113,7 +121,7 @@ __global__ __launch_bounds__(256) void hh_right_kernel(S* A, int64_t ld, int64_t
         for (int64_t j = lane; j < m; j += 16) w = add(w, mul(row[j * ld], v[j]));
     // sum over the 16 lanes of the row (xor butterfly stays inside the group)
     double re, im = 0.0;
-    if constexpr (std::is_same_v<S, double>) re = w;
+    if constexpr (is_real_v<S>) re = w;
     else { re = w.re; im = w.im; }
 #pragma unroll
     for (int off = 8; off > 0; off >>= 1) {
@@ -412,6 +420,10 @@ int hessenberg_blocked_f64(hipStream_t st, double* A, int64_t n);
 int hessenberg_blocked_c128(hipStream_t st, cplx* A, int64_t n);
 int qr_blocked_f64(hipStream_t st, double* R, int64_t m, int64_t n, double* Q);
 int qr_blocked_c128(hipStream_t st, cplx* R, int64_t m, int64_t n, cplx* Q);
+int hessenberg_blocked_f32(hipStream_t st, float* A, int64_t n);
+int hessenberg_blocked_c64(hipStream_t st, cplxf* A, int64_t n);
+int qr_blocked_f32(hipStream_t st, float* R, int64_t m, int64_t n, float* Q);
+int qr_blocked_c64(hipStream_t st, cplxf* R, int64_t m, int64_t n, cplxf* Q);
 
 namespace {
 
@@ -470,8 +482,12 @@ int hessenberg_dev(hipStream_t st, S* H, int64_t n, QrWork<S>& w) {
     if (!unblocked) {
         if constexpr (std::is_same_v<S, double>) {
             if (n >= 64 && n <= 16384) return hessenberg_blocked_f64(st, H, n);
-        } else {
+        } else if constexpr (std::is_same_v<S, cplx>) {
             if (n >= 64 && n <= 8192) return hessenberg_blocked_c128(st, H, n);
+        } else if constexpr (std::is_same_v<S, float>) {
+            if (n >= 64 && n <= 16384) return hessenberg_blocked_f32(st, H, n);
+        } else {
+            if (n >= 64 && n <= 16384) return hessenberg_blocked_c64(st, H, n);
         }
     }
     return hessenberg_t<S>(st, H, n, w);
@@ -484,10 +500,12 @@ template <class S>
 int qr_decompose_t(hipStream_t st, S* R, int64_t m, int64_t n, S* Q, QrWork<S>& w) {
     hipLaunchKernelGGL((dev::set_identity_kernel<S>), dim3((m * m + 255) / 256), dim3(256), 0, st, Q, m);
     static const bool unblocked = std::getenv("EIGSOL_QR_UNBLOCKED") != nullptr;
-    const int64_t lds_max = std::is_same_v<S, double> ? 16384 : 8192;
+    const int64_t lds_max = std::is_same_v<S, cplx> ? 8192 : 16384;
     if (!unblocked && std::min(m, n) >= 64 && m <= lds_max && n <= INT32_MAX / 2) {
         if constexpr (std::is_same_v<S, double>) return qr_blocked_f64(st, R, m, n, Q);
-        else return qr_blocked_c128(st, R, m, n, Q);
+        else if constexpr (std::is_same_v<S, cplx>) return qr_blocked_c128(st, R, m, n, Q);
+        else if constexpr (std::is_same_v<S, float>) return qr_blocked_f32(st, R, m, n, Q);
+        else return qr_blocked_c64(st, R, m, n, Q);
     }
     const int64_t kmax = std::min(m, n);
     for (int64_t k = 0; k < kmax; ++k) {
@@ -724,8 +742,12 @@ int eigsol_hessenberg_dense(eigsol_ctx* ctx, int dtype, int64_t n, const void* A
     if (!ctx || (!A_colmajor && n) || (!H_out && n)) return fail(EIGSOL_E_INVALID, "eigsol_hessenberg_dense: null pointer");
     if (n == 0) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(ctx->device));
-    return dtype == EIGSOL_C128 ? hessenberg_host<cplx>(ctx, n, A_colmajor, H_out)
-                                : hessenberg_host<double>(ctx, n, A_colmajor, H_out);
+    switch (dtype) {
+        case EIGSOL_C128: return hessenberg_host<cplx>(ctx, n, A_colmajor, H_out);
+        case EIGSOL_F32: return hessenberg_host<float>(ctx, n, A_colmajor, H_out);
+        case EIGSOL_C64: return hessenberg_host<cplxf>(ctx, n, A_colmajor, H_out);
+        default: return hessenberg_host<double>(ctx, n, A_colmajor, H_out);
+    }
 }
 
 int eigsol_qr_decompose_dense(eigsol_ctx* ctx, int dtype, int64_t m, int64_t n, const void* A_colmajor,
@@ -734,8 +756,12 @@ int eigsol_qr_decompose_dense(eigsol_ctx* ctx, int dtype, int64_t m, int64_t n, 
     if (m == 0 || n == 0) return fail(EIGSOL_E_EMPTY, "qr_decompose_dense: empty matrix");
     if (!A_colmajor) return fail(EIGSOL_E_INVALID, "eigsol_qr_decompose_dense: null A");
     EIGSOL_HIP(hipSetDevice(ctx->device));
-    return dtype == EIGSOL_C128 ? qr_decompose_host<cplx>(ctx, m, n, A_colmajor, Q_out, R_out)
-                                : qr_decompose_host<double>(ctx, m, n, A_colmajor, Q_out, R_out);
+    switch (dtype) {
+        case EIGSOL_C128: return qr_decompose_host<cplx>(ctx, m, n, A_colmajor, Q_out, R_out);
+        case EIGSOL_F32: return qr_decompose_host<float>(ctx, m, n, A_colmajor, Q_out, R_out);
+        case EIGSOL_C64: return qr_decompose_host<cplxf>(ctx, m, n, A_colmajor, Q_out, R_out);
+        default: return qr_decompose_host<double>(ctx, m, n, A_colmajor, Q_out, R_out);
+    }
 }
 
 int eigsol_qr_eigenvalues_dense(eigsol_ctx* ctx, int dtype, int64_t n, const void* A_colmajor,
@@ -749,6 +775,17 @@ int eigsol_qr_eigenvalues_dense(eigsol_ctx* ctx, int dtype, int64_t n, const voi
     }
     if (!A_colmajor || !eig_re_or_c) return fail(EIGSOL_E_INVALID, "eigsol_qr_eigenvalues_dense: null pointer");
     EIGSOL_HIP(hipSetDevice(ctx->device));
+    if (dtype == EIGSOL_F32 || dtype == EIGSOL_C64) {
+        // single precision: the reference's unshifted iteration natively (blocked QR decompositions
+        // and products in float); the Francis sweeps are built in double (the facade promotes)
+        if (variant != EIGSOL_QR_UNSHIFTED)
+            return fail(EIGSOL_E_UNSUPPORTED, "qr_eigenvalues: the multishift sweeps run in double precision");
+        return dtype == EIGSOL_F32
+                   ? qr_unshifted_host<float>(ctx, n, A_colmajor, opts->max_iterations, opts->tolerance, eig_re_or_c,
+                                              iterations, converged)
+                   : qr_unshifted_host<cplxf>(ctx, n, A_colmajor, opts->max_iterations, opts->tolerance, eig_re_or_c,
+                                              iterations, converged);
+    }
     if (variant != EIGSOL_QR_UNSHIFTED && dtype == EIGSOL_C128)
         return qr_francis_c128_host(ctx, n, A_colmajor, opts->max_iterations, static_cast<cplx*>(eig_re_or_c),
                                     iterations, converged);

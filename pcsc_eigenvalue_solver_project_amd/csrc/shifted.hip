@@ -753,6 +753,8 @@ __global__ __launch_bounds__(kThreads) void shift_part_kernel(TriArgs<S> a, int 
 // ------------------------------------------------------------------ dense LU (factor once)
 __device__ __forceinline__ double score(double v) { return fabs(v); }
 __device__ __forceinline__ double score(cplx v) { return hypot(v.re, v.im); }
+__device__ __forceinline__ double score(float v) { return fabs((double)v); }
+__device__ __forceinline__ double score(cplxf v) { return hypot((double)v.re, (double)v.im); }
 
 // Column k: pivot = first row of largest modulus in rows k..n-1, swap full rows, record the
 // transposition, scale the subdiagonal column by the pivot (skipped for a zero pivot, as Eigen's
@@ -964,6 +966,10 @@ __device__ __forceinline__ double readlane_s(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 __device__ __forceinline__ cplx readlane_s(cplx v, int src) { return cplx{readlane_s(v.re, src), readlane_s(v.im, src)}; }
+__device__ __forceinline__ float readlane_s(float v, int src) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+__device__ __forceinline__ cplxf readlane_s(cplxf v, int src) { return cplxf{readlane_s(v.re, src), readlane_s(v.im, src)}; }
 template <class S>
 struct DenseTriArgs {
     const S* lu;
@@ -1194,8 +1200,11 @@ __global__ void shift_diag_kernel(S* a, int64_t n, S sigma) {
 }  // namespace dev
 
 // ================================================================== host side
-// the dense LU (and the densified general-sparse path) is built for the double instantiations
-template <class S> inline constexpr bool kDenseLU = std::is_same_v<S, double> || std::is_same_v<S, cplx>;
+// the dense LU (and the densified / banded general-sparse paths) is built for every scalar: single
+// precision factors and solves in float (rank-NB updates on v_mfma_f32_16x16x4_f32); ILU(0)-GMRES
+// stays double-only
+template <class S> inline constexpr bool kDenseLU = true;
+template <class S> inline constexpr bool kGmres = std::is_same_v<S, double> || std::is_same_v<S, cplx>;
 int resident_blocks(eigsol_ctx* ctx, const void* kernel, int threads, size_t dyn_lds, int* grid);
 
 template <class S>
@@ -1354,14 +1363,15 @@ static int factor_dense_t(eigsol_dense* A, double sre, double sim, ShiftFactor**
 }
 
 int shift_factor_dense(eigsol_dense* A, const void* sigma, ShiftFactor** out) {
-    if (dtype_single(A->dtype))
-        return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: single-precision dense factors are not built "
-                                          "(the C++ facade promotes them to double)");
     double s[2] = {0.0, 0.0};
-    std::memcpy(s, sigma, scalar_bytes(A->dtype));
+    load_scalar(sigma, A->dtype, s[0], s[1]);
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
-    return A->dtype == EIGSOL_C128 ? factor_dense_t<cplx>(A, s[0], s[1], out)
-                                   : factor_dense_t<double>(A, s[0], 0.0, out);
+    switch (A->dtype) {
+        case EIGSOL_C128: return factor_dense_t<cplx>(A, s[0], s[1], out);
+        case EIGSOL_F32: return factor_dense_t<float>(A, s[0], 0.0, out);
+        case EIGSOL_C64: return factor_dense_t<cplxf>(A, s[0], s[1], out);
+        default: return factor_dense_t<double>(A, s[0], 0.0, out);
+    }
 }
 
 // Level analysis of a triangular pattern (host, once per matrix): level(i) = 1 + max level of
@@ -1545,7 +1555,8 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
             *out = f;
             return EIGSOL_OK;
         }
-        if (solver == kSolverGMRES) {
+        // single precision has no GMRES: the densified LU (below) where it fits the device
+        if (solver == kSolverGMRES && kGmres<S>) {
             rc = gmres_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, &f->gm);
             f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 1023) / 1024));
             if (rc == EIGSOL_OK && (hipMalloc(&f->work, 64) != hipSuccess ||

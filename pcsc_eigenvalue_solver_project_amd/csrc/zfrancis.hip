@@ -769,7 +769,9 @@ __global__ void zdiag_sub_kernel(const cplx* H, int64_t n, int ihi, cplx* out) {
 
 static double cabs1_h(const cplx& a) { return std::fabs(a.re) + std::fabs(a.im); }
 
-// AED window (EIGSOL_ZQR_AED overrides, 0: off)
+// AED window (EIGSOL_ZQR_AED overrides, 0: off).  Early-stop AED, 32 bulges in 4 chains: window
+// 32 / 48 / 64 at 1024^2 0.292 / 0.287 / 0.320 s; 48 vs 64 at 4096^2 2.65 / 2.75 s.  Without the
+// AED: 1024^2 0.37-0.42 s, 4096^2 4.4 s; the full-Schur AED (EIGSOL_ZQR_AED_FULL=1) 0.54 / 4.4 s.
 static constexpr int kZAedDefault = 48;
 
 // eigenvalues of the complex Hessenberg matrix H (device, n x n, leading dimension n; destroyed)
@@ -826,16 +828,17 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             continue;
         }
         if (++stall > max_stall) { failed = 1; sweeps = std::max(sweeps, stall); break; }
-        // up to 16 bulges per sweep (32 shifts, LAPACK's count for n in the low thousands) in C chains
-        // of at most 8 (a chain's 3 nb rows must leave its 64-row window room to advance), the
-        // chains chased concurrently in disjoint windows
+        // up to 32 bulges per sweep (64 shifts) in C chains of at most 8 (a chain's 3 nb rows must
+        // leave its 64-row window room to advance), the chains chased concurrently in disjoint
+        // windows.  With the AED (round 3) 32 bulges in 4 chains beat 16 in 2: 1024^2 0.31 -> 0.29 s,
+        // 2048^2 0.93 -> 0.77 s, 4096^2 3.28 -> 2.65 s (tools/qr_ab_round3.sh)
         static const int max_nb = [] {
             const char* e = std::getenv("EIGSOL_ZQR_NB");
-            return e ? std::max(1, std::min(dev::kZMaxBulges, std::atoi(e))) : 16;
+            return e ? std::max(1, std::min(dev::kZMaxBulges, std::atoi(e))) : 32;
         }();
         static const int max_groups = [] {
             const char* e = std::getenv("EIGSOL_ZQR_GROUPS");
-            return e ? std::max(1, std::min(dev::kZMaxGroups, std::atoi(e))) : 2;
+            return e ? std::max(1, std::min(dev::kZMaxGroups, std::atoi(e))) : 4;
         }();
         // aggressive early deflation on the trailing window; its undeflated eigenvalues are the shifts
         static const int aed_win = [] {

@@ -13,11 +13,14 @@ Tolerances (fp32):
   * power iteration at tol 1e-5: |dlambda| <= 1e-5 (1 + |lambda|), iterations +-1 (borderline
     stopping test only), |x^H x_ref| >= 1 - 1e-5;
   * triangular shifted inverse (config-5 class, complex<float>): the planted eigenvalue within
-    1e-5, and the oracle's result within 1e-5.
+    1e-5, and the oracle's result within 1e-5;
+  * dense and general-sparse (RCM band LU) shifted inverse in float: planted / numpy eigenvalues
+    within 1e-4, solve backward errors at single precision (1e-4 ||M|| ||y||).
 """
 import numpy as np
 import pytest
 import scipy.sparse as sp
+import scipy.sparse.linalg as spla
 
 import pcsc_eigenvalue_solver_project_amd as E
 from pcsc_eigenvalue_solver_project_amd import synthetic as S
@@ -190,7 +193,7 @@ def test_single_shifted_inverse_triangular(ctx):
     assert np.linalg.norm(r) <= 1e-4 * np.linalg.norm(b)
 
 
-def test_single_algorithmic_bytes_and_unsupported(ctx):
+def test_single_algorithmic_bytes_and_band_solve(ctx):
     n = 50000
     rp, ci, v = S.band(n, 10)
     A = E.CsrMatrix(ctx, rp, ci, v.astype(np.float32), (n, n))
@@ -200,7 +203,62 @@ def test_single_algorithmic_bytes_and_unsupported(ctx):
     # SURVEY §8d accounting with 4-byte values: (4 + 4) nnz + 4 (n + 1) + 2 * 4 n
     assert info["bytes_per_iteration"] == 8 * nnz + 4 * (n + 1) + 8 * n
     s.close()
-    # a general (non-triangular) single-precision sparse shifted solve has no native factor
-    with pytest.raises(E.EigSolError) as ei:
-        E.solve_shifted(A, np.float32(0.5), np.ones(n, dtype=np.float32))
-    assert ei.value.status == 12
+    # a general (non-triangular) single-precision sparse shifted solve: the RCM band LU in float
+    # (solve_shifted.hpp:85-117's SparseLU branch); backward error at single precision
+    b = S.start_vector(n, np.float32, seed=3)
+    y = E.solve_shifted(A, np.float32(0.5), b)
+    assert y.dtype == np.float32
+    M = sp.csr_matrix((v.astype(np.float64), ci, rp), shape=(n, n)) - 0.5 * sp.identity(n)
+    r = M @ y.astype(np.float64) - b
+    assert np.linalg.norm(r) <= 1e-4 * spla.norm(M) * np.linalg.norm(y)
+
+
+def _planted_dense(n, dtype, seed):
+    rng = np.random.default_rng(seed)
+    Q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    d = np.linspace(1.0, 4.0, n)
+    d[np.abs(d - 2.5) < 0.05] = 1.0
+    d[0] = 2.5
+    return ((Q * d) @ Q.T).astype(dtype)
+
+
+@pytest.mark.parametrize("dtype", SINGLE)
+@pytest.mark.parametrize("n", [700, 1536])
+def test_single_dense_shifted_native(ctx, dtype, n):
+    """Dense shifted inverse and solve_shifted in single precision: the LU factor and the solves in
+    float (rank-64 / rank-32 trailing updates on v_mfma_f32_16x16x4_f32), n = 700 on the
+    one-workgroup substitution, 1536 on the multi-CU one; planted eigenvalue 2.5 (isolated by 0.05)
+    within 1e-4, x in the scalar's own type, solve backward error at single precision."""
+    A = _planted_dense(n, dtype, n)
+    sigma = dtype(2.5 + 1e-2)
+    D = E.DenseMatrix(ctx, A)
+    r = E.shifted_inverse_power_method(D, E.ShiftedSolverOptions(200, 1e-6, sigma))
+    assert r.converged and abs(r.eigenvalue - 2.5) <= 1e-4, r.eigenvalue
+    assert np.asarray(r.eigenvector).dtype == dtype
+    b = S.start_vector(n, dtype, seed=4)
+    y = E.solve_shifted(D, sigma, b)
+    D.close()
+    assert y.dtype == dtype
+    M = A.astype(np.complex128) - complex(sigma) * np.eye(n)
+    res = M @ y.astype(np.complex128) - b.astype(np.complex128)
+    assert np.linalg.norm(res) <= 1e-4 * np.linalg.norm(M, 2) * np.linalg.norm(y)
+
+
+def test_single_general_sparse_shifted_band(ctx):
+    """complex<float> general sparse shifted inverse on the permuted convection-diffusion matrix
+    (nx = 40): the RCM band LU in single precision, the eigenvalue nearest the shift (numpy, fp64)
+    within 1e-4 relative."""
+    rp, ci, v = S.convdiff_complex(40)
+    n = len(rp) - 1
+    Md = sp.csr_matrix((v, ci, rp), shape=(n, n)).toarray()
+    ev = np.linalg.eigvals(Md)
+    k = n // 3
+    order = np.argsort(ev.real)
+    lam = ev[order[k]]
+    gap = np.min(np.abs(np.delete(ev, order[k]) - lam))
+    sigma = np.complex64(lam + 0.1 * gap)
+    A = E.CsrMatrix(ctx, rp, ci, v.astype(np.complex64), (n, n))
+    r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(300, 1e-6, sigma),
+                                       S.start_vector(n, np.complex64))
+    assert r.converged and abs(r.eigenvalue - lam) <= 1e-4 * (1 + abs(lam)), (r.eigenvalue, lam)
+    assert np.asarray(r.eigenvector).dtype == np.complex64

@@ -1,5 +1,5 @@
 import sys, os, time, json
-sys.path.insert(0, '/root/repo')
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 import numpy as np, torch
 import pcsc_eigenvalue_solver_project_amd as E
 from pcsc_eigenvalue_solver_project_amd import synthetic as S
