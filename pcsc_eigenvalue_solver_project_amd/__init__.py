@@ -440,8 +440,15 @@ def qr_eigenvalues(ctx: Context, A, opts: SolverOptions = SolverOptions(), varia
     A = _square_dense(A, "qr_eigenvalues_dense")
     code = _dtype_code(A.dtype)
     n = A.shape[0]
-    Af = np.asfortranarray(A)
     v = 1 if variant == "unshifted" else 0
+    if v == 0 and A.dtype in (np.float32, np.complex64):
+        # single precision: the multishift sweeps are double kernels (as in the C++ facade, the
+        # matrix is promoted and the eigenvalues rounded back); "unshifted" runs natively in float
+        wide = np.float64 if A.dtype == np.float32 else np.complex128
+        r = qr_eigenvalues(ctx, A.astype(wide), opts, variant)
+        return QRResult(r.eigenvalues.astype(A.dtype), r.iterations, r.converged,
+                        None if r.eigenvalues_complex is None else r.eigenvalues_complex.astype(np.complex64))
+    Af = np.asfortranarray(A)
     eig = np.zeros(max(n, 1), dtype=A.dtype)
     wi = np.zeros(max(n, 1))
     it, conv = C.c_int32(0), C.c_int32(0)

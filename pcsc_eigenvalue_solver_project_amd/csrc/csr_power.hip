@@ -1495,7 +1495,7 @@ static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, in
 }
 
 // the device-side peer exchange (row-sharded sessions) is built for the double instantiations
-template <class S> inline constexpr bool kPeerOk = std::is_same_v<S, double> || std::is_same_v<S, cplx>;
+template <class S> inline constexpr bool kPeerOk = true;   // every scalar type has the peer kernels
 
 template <class S>
 static const void* power_kernel_ptr(const eigsol_csr* A, bool peer = false) {
@@ -1640,8 +1640,6 @@ int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerC
                      const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
                      int parity, int grid, const PeerArgs* peer) {
     if (peer && !A->sliced) return fail(EIGSOL_E_UNSUPPORTED, "peer exchange needs the sliced CSR layout");
-    if (peer && dtype_single(A->dtype))
-        return fail(EIGSOL_E_UNSUPPORTED, "peer exchange: single-precision row-sharded sessions are not built");
     if (A->dtype == EIGSOL_C128)
         return power_launch_t<cplx>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
                                     trace, parity, grid, peer);
@@ -1658,10 +1656,14 @@ int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerC
 int peer_begin_launch(eigsol_ctx* ctx, int dtype, const PeerArgs& pa, const void* x_own, int64_t npush,
                       const void* mine) {
     hipStream_t s = ctx->stream;
-    if (dtype_single(dtype))
-        return fail(EIGSOL_E_UNSUPPORTED, "peer exchange: single-precision row-sharded sessions are not built");
     if (dtype == EIGSOL_C128)
         hipLaunchKernelGGL(peer_begin_kernel<cplx>, dim3(1), dim3(kThreads), 0, s, pa, (const cplx*)x_own, npush,
+                           (const part4*)mine);
+    else if (dtype == EIGSOL_F32)
+        hipLaunchKernelGGL(peer_begin_kernel<float>, dim3(1), dim3(kThreads), 0, s, pa, (const float*)x_own, npush,
+                           (const part4*)mine);
+    else if (dtype == EIGSOL_C64)
+        hipLaunchKernelGGL(peer_begin_kernel<cplxf>, dim3(1), dim3(kThreads), 0, s, pa, (const cplxf*)x_own, npush,
                            (const part4*)mine);
     else
         hipLaunchKernelGGL(peer_begin_kernel<double>, dim3(1), dim3(kThreads), 0, s, pa, (const double*)x_own,

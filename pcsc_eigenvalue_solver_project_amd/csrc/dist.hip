@@ -225,16 +225,24 @@ int dist_exchange(eigsol_csr* A, void* y, void* rank_part) {
     hipStream_t st = ctx->stream;
     if (A->nsend > 0) {
         const int grid = (int)std::min<int64_t>(1024, (A->nsend + 255) / 256);
-        if (A->dtype == EIGSOL_C128)
+        // the pack moves whole scalars: 16-byte complex<double> as cplx, 8-byte scalars
+        // (double, complex<float>) as double, float as float
+        if (sb == 16)
             hipLaunchKernelGGL(pack_kernel<cplx>, dim3(grid), dim3(256), 0, st, (const cplx*)y,
                                A->send_idx, (cplx*)A->send_buf, A->nsend);
-        else
+        else if (sb == 8)
             hipLaunchKernelGGL(pack_kernel<double>, dim3(grid), dim3(256), 0, st, (const double*)y,
                                A->send_idx, (double*)A->send_buf, A->nsend);
+        else
+            hipLaunchKernelGGL(pack_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)y,
+                               A->send_idx, (float*)A->send_buf, A->nsend);
         EIGSOL_HIP(hipGetLastError());
     }
     ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
-    const size_t dpe = sb / 8;   // doubles per scalar
+    // RCCL element type of the vector payload: fp64 words for double / complex<double>, fp32 words
+    // for float / complex<float> (the rank partials are always 4 doubles)
+    const ncclDataType_t vty = dtype_single(A->dtype) ? ncclFloat32 : ncclFloat64;
+    const size_t dpe = dtype_single(A->dtype) ? sb / 4 : sb / 8;   // RCCL elements per scalar
     char* xs = static_cast<char*>(y);   // x-space: [lower ghosts | own rows | upper ghosts]
     double* rpart = static_cast<double*>(rank_part);
     if (ctx->loop) {
@@ -270,12 +278,12 @@ int dist_exchange(eigsol_csr* A, void* y, void* rank_part) {
         EIGSOL_RCCL(ncclGroupStart());
         if (equal) {
             EIGSOL_RCCL(ncclAllGather(xs + (size_t)rb[ctx->rank] * sb, xs, (size_t)(rb[1] - rb[0]) * dpe,
-                                      ncclFloat64, comm, st));
+                                      vty, comm, st));
         } else {
             for (int q = 0; q < P; ++q)
                 if (rb[q + 1] > rb[q])
                     EIGSOL_RCCL(ncclBroadcast(xs + (size_t)rb[q] * sb, xs + (size_t)rb[q] * sb,
-                                              (size_t)(rb[q + 1] - rb[q]) * dpe, ncclFloat64, q, comm, st));
+                                              (size_t)(rb[q + 1] - rb[q]) * dpe, vty, q, comm, st));
         }
         EIGSOL_RCCL(ncclAllGather(rpart + 4 * ctx->rank, rpart, 4, ncclFloat64, comm, st));
         EIGSOL_RCCL(ncclGroupEnd());
@@ -286,10 +294,10 @@ int dist_exchange(eigsol_csr* A, void* y, void* rank_part) {
         if (q == ctx->rank) continue;
         if (A->send_counts[q] > 0)
             EIGSOL_RCCL(ncclSend(static_cast<char*>(A->send_buf) + (size_t)A->send_offs[q] * sb,
-                                 (size_t)A->send_counts[q] * dpe, ncclFloat64, q, comm, st));
+                                 (size_t)A->send_counts[q] * dpe, vty, q, comm, st));
         if (A->recv_counts[q] > 0)
             EIGSOL_RCCL(ncclRecv(xs + (size_t)(A->recv_offs[q] + (q > ctx->rank ? A->nrows : 0)) * sb,
-                                 (size_t)A->recv_counts[q] * dpe, ncclFloat64, q, comm, st));
+                                 (size_t)A->recv_counts[q] * dpe, vty, q, comm, st));
     }
     double* rp = static_cast<double*>(rank_part);
     EIGSOL_RCCL(ncclAllGather(rp + 4 * ctx->rank, rp, 4, ncclFloat64, comm, st));
@@ -458,9 +466,8 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     if (!ctx->comm && !ctx->loop && !ctx->hcoll)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
     *out = nullptr;
-    if (dtype != EIGSOL_F64 && dtype != EIGSOL_C128)
-        return fail(EIGSOL_E_UNSUPPORTED, "eigsol_csr_create_dist: row-sharded matrices are built for double "
-                                          "and complex<double>");
+    if (dtype != EIGSOL_F64 && dtype != EIGSOL_C128 && dtype != EIGSOL_F32 && dtype != EIGSOL_C64)
+        return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: unknown dtype");
     const int P = ctx->nranks, me = ctx->rank;
     if (row_begins[0] != 0 || nnz_local < 0)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: row_begins must start at 0 and nnz be >= 0");

@@ -49,7 +49,6 @@ template <> struct HessCfg<cplxf> {
     static constexpr int kMaxLdsN = 16384;
     static constexpr int kCoopMaxN = 8192;
 };
-constexpr int kPanel = 32;          // the widest panel (array bounds)
 constexpr int kGemvCols = 128;      // columns per GEMV partial
 
 __device__ __forceinline__ double cj(double a) { return a; }
@@ -175,6 +174,7 @@ __global__ __launch_bounds__(1024) void hess_panel_col(S* A, int n, int k, int j
     __shared__ S sw[NB];
     __shared__ S sw2[NB];
     __shared__ S vj[NB];
+    __shared__ double rtl[17];   // block sum of the tail norm (its own scratch: red holds S)
     __shared__ double s_tail;
     const int tid = threadIdx.x, nt = blockDim.x;
     if (tid < i) vj[tid] = cj(V[j + (int64_t)tid * n]);   // conj of row j of V
@@ -215,10 +215,9 @@ __global__ __launch_bounds__(1024) void hess_panel_col(S* A, int n, int k, int j
     double tl = 0.0;
     for (int r = j + 2 + tid; r < n; r += nt) tl += sq_abs(a[r]);
     {
-        double pp[kPanel];
-        pp[0] = tl;
-        block_sum_vec<double, kPanel>(pp, 1, reinterpret_cast<double*>(red), reinterpret_cast<double*>(sw));
-        if (tid == 0) s_tail = reinterpret_cast<double*>(sw)[0];
+        double pp[1] = {tl};
+        block_sum_vec<double, 1>(pp, 1, rtl, rtl + 16);
+        if (tid == 0) s_tail = rtl[16];
         __syncthreads();
     }
     const double tail = s_tail;
@@ -318,6 +317,7 @@ __global__ __launch_bounds__(1024) void qr_panel_col(S* R, int m, int k, int j, 
     __shared__ S red[16 * NB];
     __shared__ S sw[NB];
     __shared__ S sw2[NB];
+    __shared__ double rtl[17];   // block sum of the tail norm (its own scratch: red holds S)
     __shared__ double s_tail;
     const int tid = threadIdx.x, nt = blockDim.x;
     for (int r = tid; r < m; r += nt) a[r] = R[r + (int64_t)j * m];
@@ -349,10 +349,9 @@ __global__ __launch_bounds__(1024) void qr_panel_col(S* R, int m, int k, int j, 
     double tl = 0.0;
     for (int r = j + 1 + tid; r < m; r += nt) tl += sq_abs(a[r]);
     {
-        double pp[kPanel];
-        pp[0] = tl;
-        block_sum_vec<double, kPanel>(pp, 1, reinterpret_cast<double*>(red), reinterpret_cast<double*>(sw));
-        if (tid == 0) s_tail = reinterpret_cast<double*>(sw)[0];
+        double pp[1] = {tl};
+        block_sum_vec<double, 1>(pp, 1, rtl, rtl + 16);
+        if (tid == 0) s_tail = rtl[16];
         __syncthreads();
     }
     const double tail = s_tail;

@@ -179,3 +179,34 @@ def test_two_processes_ipc_inboxes(tmp_path):
     ref = O.power_csc(cp, ri, vv, x0, 300, TOL)
     assert abs(res[0]["lambda"] - ref["eigenvalue"]) <= 1e-10 * (1 + abs(ref["eigenvalue"]))
     assert abs(res[0]["iterations"] - ref["iterations"]) <= 1
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.complex64])
+def test_single_precision_row_sharded(dtype, monkeypatch):
+    """float / complex<float> row-sharded sessions (4-byte / 8-byte values on the peer exchange and
+    the RCCL-typed collective one): every rank's eigenvalue bitwise identical, the two transports
+    agreeing, and parity with the single-precision oracle of the unsharded loop (power_method.hpp:
+    68-96 in float, norm / dot partials in double) at the single-precision tolerance
+    |dlambda| <= 1e-5 (1 + |lambda|), iterations +-1, |x^H x_ref| >= 1 - 1e-5."""
+    n = 400_000
+    rp, ci, v = S.band(n, 10)
+    v = v.astype(dtype)
+    if np.issubdtype(dtype, np.complexfloating):
+        v = (v + 0.1j * np.random.default_rng(3).uniform(-1, 1, len(v))).astype(dtype)
+    x0 = S.start_vector(n, dtype)
+    tol = 1e-5
+    peer = loopback_peer_run(4, rp, ci, v, x0, n, E.SolverOptions(300, tol))
+    assert all(o[1] == _capi.EIGSOL_TRANSPORT_PEER for o in peer)
+    lam = [o[0].eigenvalue for o in peer]
+    assert all(l_ == lam[0] for l_ in lam), lam
+    coll = loopback_peer_run(4, rp, ci, v, x0, n, E.SolverOptions(300, tol), transport="collective",
+                             monkeypatch=monkeypatch)
+    assert all(o[1] == _capi.EIGSOL_TRANSPORT_COLLECTIVE for o in coll)
+    assert abs(coll[0][0].eigenvalue - lam[0]) <= 1e-6 * (1 + abs(lam[0]))
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    ref = O.power_csc(cp, ri, vv, x0, 300, tol)
+    assert abs(lam[0] - ref["eigenvalue"]) <= 1e-5 * (1 + abs(ref["eigenvalue"]))
+    assert abs(peer[0][0].iterations - ref["iterations"]) <= 1
+    x = np.concatenate([o[0].eigenvector for o in peer]).astype(np.complex128)
+    assert x.dtype == np.complex128 and peer[0][0].eigenvector.dtype == dtype
+    assert abs(abs(np.vdot(x, ref["eigenvector"].astype(np.complex128))) - 1) <= 1e-5

@@ -262,3 +262,55 @@ def test_single_general_sparse_shifted_band(ctx):
                                        S.start_vector(n, np.complex64))
     assert r.converged and abs(r.eigenvalue - lam) <= 1e-4 * (1 + abs(lam)), (r.eigenvalue, lam)
     assert np.asarray(r.eigenvector).dtype == np.complex64
+
+
+@pytest.mark.parametrize("dtype", SINGLE)
+def test_single_hessenberg_and_qr_decompose_native(ctx, dtype):
+    """to_hessenberg / qr_decompose in the scalar's own precision (the blocked compact-WY kernels
+    instantiated for float and complex<float>: f32 panels, VALU panel GEMMs, rank-2nb updates on
+    v_mfma_f32_16x16x4_f32) against the fp64 restatement of the reference's loops
+    (to_hessenberg.hpp:38-77, qr_decompose.hpp:46-85): H within 2e-5 ||A||, zero below the
+    subdiagonal; Q R = A and Q^H Q = I at single precision."""
+    rng = np.random.default_rng(77)
+    n = 200
+    A = rng.standard_normal((n, n))
+    if np.issubdtype(dtype, np.complexfloating):
+        A = A + 1j * rng.standard_normal((n, n))
+    A = A.astype(dtype)
+    H = E.to_hessenberg(ctx, A)
+    assert H.dtype == dtype
+    sc = np.linalg.norm(A.astype(np.complex128))
+    assert np.abs(H - O.hessenberg(A.astype(np.complex128 if np.iscomplexobj(A) else np.float64))).max() <= 2e-5 * sc
+    assert np.abs(np.tril(H, -2)).max() == 0.0
+    B = A[:, :150]
+    Q, R = E.qr_decompose(ctx, B)
+    assert Q.dtype == dtype and R.dtype == dtype
+    Qd, Rd = Q.astype(np.complex128), R.astype(np.complex128)
+    assert np.abs(Qd @ Rd - B).max() <= 2e-5 * sc
+    assert np.abs(Qd.conj().T @ Qd - np.eye(n)).max() <= 2e-5 * n
+    assert np.abs(np.tril(R, -1)).max() == 0.0
+
+
+@pytest.mark.parametrize("dtype", SINGLE)
+def test_single_qr_eigenvalues(ctx, dtype):
+    """qr_eigenvalues<float / complex<float>>: the reference's unshifted iteration natively in float
+    (qr_eigenvalues.hpp:62-105) on the reference test's 2 x 2 (eigenvalues 3 and 1), and the default
+    Francis path (fp64 sweeps on the promoted matrix, eigenvalues rounded to the scalar type) on a
+    120 x 120 matrix, matched to LAPACK within 1e-5 ||A||."""
+    A = np.array([[2.0, 1.0], [1.0, 2.0]], dtype=dtype)
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-6), variant="unshifted")
+    assert r.converged and 1 <= r.iterations <= 1000
+    assert r.eigenvalues.dtype == dtype
+    ev = np.sort(np.asarray(r.eigenvalues).real)
+    assert abs(ev[0] - 1) <= 1e-5 and abs(ev[1] - 3) <= 1e-5
+    rng = np.random.default_rng(8)
+    B = rng.standard_normal((120, 120))
+    if np.issubdtype(dtype, np.complexfloating):
+        B = B + 1j * rng.standard_normal((120, 120))
+    B = B.astype(dtype)
+    r = E.qr_eigenvalues(ctx, B, E.SolverOptions(1000, 1e-6))
+    assert r.converged and r.eigenvalues.dtype == dtype
+    ref = np.linalg.eigvals(B.astype(np.complex128))
+    got = np.asarray(r.eigenvalues_complex, np.complex128)
+    d = np.abs(got[:, None] - ref[None, :]).min(axis=1)
+    assert d.max() <= 1e-5 * np.linalg.norm(B.astype(np.complex128))
