@@ -293,7 +293,8 @@ class PowerSession:
                  5: "csr_slice_kernel (64-row slices, one row per lane)",
                  6: "csr_row_kernel (one row per lane, single-precision fallback layout)",
                  7: "ILU(0)-preconditioned GMRES (tiles = Arnoldi steps of the last solve)",
-                 8: "band_solve_kernel (RCM-banded LU; tiles = kl + ku)"}
+                 8: "band_solve_kernel (RCM-banded LU; tiles = kl + ku)",
+                 9: "csr_kernel column-block passes (x blocks L2-resident; tiles = blocks)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?")}
 

@@ -88,6 +88,8 @@ struct CsrArgs {
     part4* blk_part;
     S* trace;
     PeerArgs peer;           // row-sharded session on the device-side peer exchange (kDist kernels)
+    int32_t cb_carry;        // column-block pass > 0 (csr_kernel): row sums start from y's partials
+    int32_t cb_epi;          // last (or only) pass: fused power epilogue (norm / Rayleigh partials)
 };
 
 // Registers holding one tile's stream for one lane: P slots of (values, columns) plus the lane's
@@ -328,7 +330,8 @@ __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity)
                 const int2 rp = rows[b][tid];
                 const int k0 = rp.x - mc.z;
                 const int k1 = rp.y - mc.z;
-                S sacc = s_zero<S>();
+                // column-block passes continue the previous block's partial (same summation order)
+                S sacc = a.cb_carry ? yout[mc.x + tid] : s_zero<S>();
                 if constexpr (kMode == 3) {
                     if (k1 > k0) sacc = pb[lds_idx(k0)];
                 } else {
@@ -336,9 +339,11 @@ __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity)
                 }
                 yout[mc.x + tid] = sacc;
                 if constexpr (kPower) {
-                    const S xi = scale_in(xrows[b][tid], nrm);
-                    n2 += sq_abs(sacc);
-                    acc_dot(rr, ri, xi, sacc);
+                    if (a.cb_epi) {
+                        const S xi = scale_in(xrows[b][tid], nrm);
+                        n2 += sq_abs(sacc);
+                        acc_dot(rr, ri, xi, sacc);
+                    }
                 }
             }
             if (tn >= tend) return true;
@@ -364,10 +369,12 @@ __global__ __launch_bounds__(kThreads) void csr_kernel(CsrArgs<S> a, int parity)
         }
     }
 
-    long_rows_pass<S, kPower>(a, xin, yout, nrm, n2, rr, ri, sm);
+    long_rows_pass<S, kPower>(a, xin, yout, nrm, n2, rr, ri, sm);   // (column blocks have no long rows)
     if constexpr (kPower) {
-        block_sum3(n2, rr, ri, sm);
-        last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+        if (a.cb_epi) {   // launch-uniform
+            block_sum3(n2, rr, ri, sm);
+            last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+        }
     }
 }
 
@@ -631,10 +638,12 @@ __global__ __launch_bounds__(kThreads) void csr_win_kernel(CsrArgs<S> a, int par
         }
     }
 
-    long_rows_pass<S, kPower>(a, xin, yout, nrm, n2, rr, ri, sm);
+    long_rows_pass<S, kPower>(a, xin, yout, nrm, n2, rr, ri, sm);   // (column blocks have no long rows)
     if constexpr (kPower) {
-        block_sum3(n2, rr, ri, sm);
-        last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+        if (a.cb_epi) {   // launch-uniform
+            block_sum3(n2, rr, ri, sm);
+            last_arriver_reduce(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+        }
     }
 }
 
@@ -1126,6 +1135,7 @@ void csr_release(eigsol_csr* A) {
         if (q) (void)hipFree(q);
     if (A->send_idx) (void)hipFree(A->send_idx);
     if (A->send_buf) (void)hipFree(A->send_buf);
+    for (eigsol_csr* B : A->cblk) csr_release(B);
     eigsol_ctx* c = A->ctx;
     delete A;
     ctx_release(c);
@@ -1323,6 +1333,9 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
 }
 
 // xoff: x-space index of local row 0 (0 on one GPU; the lower-ghost count when row-sharded)
+static int build_col_blocks(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, const void* val);
+static thread_local int g_upload_plain = 0;   // > 0: building a column block (tiles only, no blocks)
+
 int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t nnz,
                const int32_t* rowptr, const int32_t* colidx, const void* values, eigsol_csr** out,
                int64_t xoff) {
@@ -1363,7 +1376,8 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
                                    max_rows, windowed);
     if (const char* env = std::getenv("EIGSOL_CSR_NO_WINDOW")) if (std::atoi(env)) windowed = 0;
     SliceLayout SL;
-    bool sliced = true;
+    bool sliced = g_upload_plain == 0;
+    if (g_upload_plain) windowed = 0;
     if (const char* env = std::getenv("EIGSOL_CSR_NO_SLICE")) if (std::atoi(env)) sliced = false;
     if (sliced)
         sliced = build_slices(rowptr, col_use, val_use, sb,
@@ -1453,7 +1467,75 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
             return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: slice upload: ") + hipGetErrorString(e));
         }
     }
+    const int rcb = build_col_blocks(A, rowptr, col_use, val_use);
+    if (rcb != EIGSOL_OK) {
+        cleanup();
+        return rcb;
+    }
     *out = A;
+    return EIGSOL_OK;
+}
+
+// Column blocks for gather-bound products (uniform columns): when the matrix gathers x (gather
+// slices or plain tiles) and x is larger than kCblkMinBytes, split the columns into blocks of about
+// kCblkBytes of x (one XCD's L2 is 4 MB) so that each pass's gathers hit L2.  Rows keep their
+// ascending column order across the passes, so every row sum is the reference's, bit for bit.
+// EIGSOL_CSR_CBLK=0 disables; EIGSOL_CSR_CBLK_BYTES sets the block size of x in bytes;
+// EIGSOL_CSR_CBLK_MIN the x size from which blocks are built.
+static int build_col_blocks(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, const void* val) {
+    if (g_upload_plain || A->xoff != 0 || A->dist) return EIGSOL_OK;
+    if (A->dtype != EIGSOL_F64 && A->dtype != EIGSOL_C128) return EIGSOL_OK;
+    if (const char* e = std::getenv("EIGSOL_CSR_CBLK")) if (!std::atoi(e)) return EIGSOL_OK;
+    const bool gathers = A->sliced ? A->slice_gather != 0 : !A->windowed;
+    if (!gathers || A->nrows != A->ncols || A->nnz == 0) return EIGSOL_OK;
+    const size_t sb = scalar_bytes(A->dtype);
+    double blk_bytes = 2.0 * 1024 * 1024, min_bytes = 6.0 * 1024 * 1024;
+    if (const char* e = std::getenv("EIGSOL_CSR_CBLK_BYTES")) blk_bytes = std::max(1024.0, std::atof(e));
+    if (const char* e = std::getenv("EIGSOL_CSR_CBLK_MIN")) min_bytes = std::atof(e);
+    const double xbytes = (double)A->ncols * (double)sb;
+    if (xbytes < min_bytes) return EIGSOL_OK;
+    const int B = (int)std::ceil(xbytes / blk_bytes);
+    // every pass visits every row: blocks pay only while rows keep >= 2 entries per block on average
+    const double avg = (double)A->nnz / (double)A->nrows;
+    if (B < 2 || B > 64 || avg < 2.0 * B) return EIGSOL_OK;
+    const int64_t n = A->nrows, nc = A->ncols;
+    auto blk_of = [&](int32_t c) { return (int)(((int64_t)c * B) / nc); };
+    // one pass over the entries, in row order: each block's rows stay ascending
+    std::vector<std::vector<int32_t>> rp(B, std::vector<int32_t>(n + 1, 0)), ci(B);
+    std::vector<std::vector<unsigned char>> vv(B);
+    for (int b = 0; b < B; ++b) {
+        ci[b].reserve((size_t)(A->nnz / B + 16));
+        vv[b].reserve((size_t)(A->nnz / B + 16) * sb);
+    }
+    const int tile_cap = A->dtype == EIGSOL_C128 ? Tile<cplx>::kCap : Tile<double>::kCap;
+    for (int64_t i = 0; i < n; ++i) {
+        for (int32_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+            const int b = blk_of(col[k]);
+            ci[b].push_back(col[k]);
+            const unsigned char* src = (const unsigned char*)val + (size_t)k * sb;
+            vv[b].insert(vv[b].end(), src, src + sb);
+        }
+        for (int b = 0; b < B; ++b) {
+            rp[b][i + 1] = (int32_t)ci[b].size();
+            if (rp[b][i + 1] - rp[b][i] > tile_cap / 2) return EIGSOL_OK;   // a long row: keep one pass
+        }
+    }
+    for (int b = 0; b < B; ++b) {
+        if (ci[b].empty()) { ci[b].push_back(0); vv[b].resize(sb, 0); }
+        eigsol_csr* Bm = nullptr;
+        ++g_upload_plain;
+        const int rc = csr_upload(A->ctx, A->dtype, n, nc, rp[b][n], rp[b].data(), ci[b].data(), vv[b].data(), &Bm, 0);
+        --g_upload_plain;
+        if (rc != EIGSOL_OK) {
+            for (eigsol_csr* q : A->cblk) csr_release(q);
+            A->cblk.clear();
+            return rc;
+        }
+        A->cblk.push_back(Bm);
+        std::vector<int32_t>().swap(rp[b]);
+        std::vector<int32_t>().swap(ci[b]);
+        std::vector<unsigned char>().swap(vv[b]);
+    }
     return EIGSOL_OK;
 }
 
@@ -1499,6 +1581,8 @@ template <class S> inline constexpr bool kPeerOk = true;   // every scalar type 
 
 template <class S>
 static const void* power_kernel_ptr(const eigsol_csr* A, bool peer = false) {
+    if constexpr (std::is_same_v<S, double> || std::is_same_v<S, cplx>)
+        if (!A->cblk.empty() && !peer) return reinterpret_cast<const void*>(csr_kernel<S, true>);
     if (A->sliced) {
 #define EIGSOL_SLICE_PTR(KB)                                                                                 \
     if (peer)                                                                                                \
@@ -1534,7 +1618,12 @@ int csr_grid(eigsol_csr* A, int* grid, bool peer) {
                     : A->dtype == EIGSOL_C64 ? power_kernel_ptr<cplxf>(A, peer)
                                              : power_kernel_ptr<double>(A, peer);
     // work units: tiles (one per block step) or slices (one per wave step)
-    const int64_t units = A->sliced ? (A->nslices + kWaves - 1) / kWaves : A->ntiles;
+    int64_t units = A->sliced ? (A->nslices + kWaves - 1) / kWaves : A->ntiles;
+    if (!A->cblk.empty() && !peer) {   // column blocks: csr_kernel passes over the blocks' tiles
+        units = 0;
+        for (const eigsol_csr* B : A->cblk) units = std::max<int64_t>(units, B->ntiles);
+        return resident_grid(A->ctx, k, units, grid, 8);
+    }
     // sliced: two blocks (8 waves, 16 slices in flight) per CU measured fastest on band10m;
     // more concurrent streams per CU cost more than the latency they hide
     if (dtype_single(A->dtype) && !A->sliced)   // row-per-lane fallback: rows / threads
@@ -1568,12 +1657,39 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     a.xlen = (int32_t)xlen;
     a.nrows = (int32_t)A->nrows;
     a.xoff = (int32_t)A->xoff;
+    a.cb_carry = 0;
+    a.cb_epi = 1;
     return a;
 }
 
 template <class S>
 static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int parity, int grid, bool peer = false) {
     hipStream_t s = A->ctx->stream;
+    if constexpr (std::is_same_v<S, double> || std::is_same_v<S, cplx>) {
+        if (!A->cblk.empty() && !peer) {
+            // column blocks: one csr_kernel pass per block, partials carried in y (stream order)
+            const int B = (int)A->cblk.size();
+            for (int b = 0; b < B; ++b) {
+                CsrArgs<S> ab = make_args<S>(A->cblk[b], args.xlen);
+                ab.x_plain = args.x_plain;
+                ab.y_plain = args.y_plain;
+                ab.buf0 = args.buf0;
+                ab.buf1 = args.buf1;
+                ab.ctl = args.ctl;
+                ab.rank_part = args.rank_part;
+                ab.nranks = args.nranks;
+                ab.my_part = args.my_part;
+                ab.blk_part = args.blk_part;
+                ab.trace = args.trace;
+                ab.cb_carry = b > 0;
+                ab.cb_epi = b == B - 1;
+                if (power) hipLaunchKernelGGL((csr_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, ab, parity);
+                else hipLaunchKernelGGL((csr_kernel<S, false>), dim3(grid), dim3(kThreads), 0, s, ab, parity);
+            }
+            EIGSOL_HIP(hipGetLastError());
+            return EIGSOL_OK;
+        }
+    }
     static const int mode = [] {
         const char* e = std::getenv("EIGSOL_CSR_ABLATION");
         return e ? std::atoi(e) : 0;

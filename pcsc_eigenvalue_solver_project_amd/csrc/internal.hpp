@@ -263,6 +263,11 @@ struct eigsol_csr {
     std::vector<int64_t> peer_dst_off;   // per peer q: where my rows start in q's ghost list
     std::vector<int64_t> ghost_counts;   // P x P: [r * P + q] = entries rank r reads from rank q
     std::vector<int64_t> requests;       // global rows the peers read from this rank (by peer)
+    // Column blocks (gathered x larger than an XCD's L2): B sub-matrices holding the entries of
+    // columns [c_b, c_{b+1}), all rows, tile layout; a product is B passes of csr_kernel, each
+    // adding its block's entries to the row partials of the previous pass (the ascending-column
+    // order of every row sum is kept), the last with the fused power epilogue.  Empty: off.
+    std::vector<eigsol_csr*> cblk;
 };
 
 struct eigsol_dense {

@@ -582,6 +582,10 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
         if (bytes) *bytes = (sb + 4.0) * nnz + 4.0 * (n + 1.0) + 2.0 * sb * n;
         if (tiles) *tiles = s->csr->sliced ? s->csr->nslices : s->csr->ntiles;
         if (variant) *variant = s->csr->sliced ? 5 : dtype_single(s->dtype) ? 6 : (s->csr->windowed ? 1 : 0);
+        if (!s->csr->cblk.empty() && !s->peer) {   // column-blocked passes (tiles = blocks)
+            if (variant) *variant = 9;
+            if (tiles) *tiles = (int32_t)s->csr->cblk.size();
+        }
     } else {
         const double n = (double)s->dense->nrows;
         if (bytes) *bytes = sb * n * n + 2.0 * sb * n;

@@ -359,3 +359,35 @@ def test_slice_stream_segments_bitwise_and_power(ctx, dtype, monkeypatch):
         assert r.iterations == ref[key].iterations and r.eigenvalue == ref[key].eigenvalue
         assert np.array_equal(r.eigenvector, ref[key].eigenvector)
         A.close()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_column_blocked_gather_bitwise_and_power(ctx, dtype, monkeypatch):
+    """Column-blocked gathers (uniform columns, x larger than an XCD's L2: csr_kernel passes over
+    column blocks, each continuing the previous block's row partials): the product is bitwise the
+    reference's CSC scatter (power_method.hpp:69, every row still summed in ascending column
+    order), and the power iteration keeps the oracle parity of test_power_csr_parity.  Blocks are
+    forced on a small matrix (x = 1.6 MB, 512 KB blocks: 4 passes; ~1 % of the rows have no entry
+    in a given block)."""
+    monkeypatch.setenv("EIGSOL_CSR_CBLK_MIN", "0")
+    monkeypatch.setenv("EIGSOL_CSR_CBLK_BYTES", str(512 * 1024))
+    n = 200_000
+    rp, ci, v = S.uniform(n, 16)
+    v = v.astype(dtype)
+    if dtype == np.complex128:
+        v = v + 1j * np.random.default_rng(1).uniform(-1, 1, len(v))
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    s = E.PowerSession(A)
+    info = s.kernel_info()
+    s.close()
+    assert info["variant"] == 9 and info["tiles"] >= 2, info
+    x = S.start_vector(n, dtype)
+    y = _spmv_gpu(ctx, A, x)
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    assert np.array_equal(y, O.spmv_csc(cp, ri, vv, x, n))
+    tol = 1e-12
+    res = E.power_method(A, E.SolverOptions(1000, tol), x)
+    ref = O.power_csc(cp, ri, vv, x, 1000, tol, want_trace=True)
+    assert ref["converged"]
+    _assert_power_parity(res, ref, tol)
+    A.close()

@@ -269,8 +269,11 @@ def test_single_hessenberg_and_qr_decompose_native(ctx, dtype):
     """to_hessenberg / qr_decompose in the scalar's own precision (the blocked compact-WY kernels
     instantiated for float and complex<float>: f32 panels, VALU panel GEMMs, rank-2nb updates on
     v_mfma_f32_16x16x4_f32) against the fp64 restatement of the reference's loops
-    (to_hessenberg.hpp:38-77, qr_decompose.hpp:46-85): H within 2e-5 ||A||, zero below the
-    subdiagonal; Q R = A and Q^H Q = I at single precision."""
+    (to_hessenberg.hpp:38-77, qr_decompose.hpp:46-85): |H| within 2e-5 ||A||, zero below the
+    subdiagonal; Q R = A and Q^H Q = I at single precision.  H is compared entrywise in modulus:
+    the reference's reflector takes its sign / phase from x0, and where |x0| / ||x|| is below the
+    single-precision rounding (column 89 of this matrix: 3.4e-7) float and double legitimately
+    choose opposite reflectors, i.e. H_f32 = D H_f64 D^H with a diagonal unitary D."""
     rng = np.random.default_rng(77)
     n = 200
     A = rng.standard_normal((n, n))
@@ -280,7 +283,8 @@ def test_single_hessenberg_and_qr_decompose_native(ctx, dtype):
     H = E.to_hessenberg(ctx, A)
     assert H.dtype == dtype
     sc = np.linalg.norm(A.astype(np.complex128))
-    assert np.abs(H - O.hessenberg(A.astype(np.complex128 if np.iscomplexobj(A) else np.float64))).max() <= 2e-5 * sc
+    Hr = O.hessenberg(A.astype(np.complex128 if np.iscomplexobj(A) else np.float64))
+    assert np.abs(np.abs(H) - np.abs(Hr)).max() <= 2e-5 * sc
     assert np.abs(np.tril(H, -2)).max() == 0.0
     B = A[:, :150]
     Q, R = E.qr_decompose(ctx, B)
