@@ -1480,16 +1480,21 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
 // slices or plain tiles) and x is larger than kCblkMinBytes, split the columns into blocks of about
 // kCblkBytes of x (one XCD's L2 is 4 MB) so that each pass's gathers hit L2.  Rows keep their
 // ascending column order across the passes, so every row sum is the reference's, bit for bit.
-// EIGSOL_CSR_CBLK=0 disables; EIGSOL_CSR_CBLK_BYTES sets the block size of x in bytes;
-// EIGSOL_CSR_CBLK_MIN the x size from which blocks are built.
+// EIGSOL_CSR_CBLK=0 disables (=2 skips the entries-per-block rule); EIGSOL_CSR_CBLK_BYTES sets the block size of x in bytes;
+// EIGSOL_CSR_CBLK_MIN the x size from which blocks are built.  Measured on config 3's 1M x 16 uniform
+// matrix (x 8 MB, tools/cblk_ab.sh): 1 block 166 us, 2 blocks (4 MB) 140 us, 3 blocks 181 us,
+// 4 blocks 233 us, 8 blocks 430 us -- each pass re-reads and re-writes y and walks every row, so
+// only a split into blocks of a whole L2 pays, and only for rows with >= 8 entries per block.
 static int build_col_blocks(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, const void* val) {
     if (g_upload_plain || A->xoff != 0 || A->dist) return EIGSOL_OK;
     if (A->dtype != EIGSOL_F64 && A->dtype != EIGSOL_C128) return EIGSOL_OK;
-    if (const char* e = std::getenv("EIGSOL_CSR_CBLK")) if (!std::atoi(e)) return EIGSOL_OK;
+    int mode = 1;   // EIGSOL_CSR_CBLK: 0 off, 1 by the rules below, 2 regardless of row lengths (tests)
+    if (const char* e = std::getenv("EIGSOL_CSR_CBLK")) mode = std::atoi(e);
+    if (!mode) return EIGSOL_OK;
     const bool gathers = A->sliced ? A->slice_gather != 0 : !A->windowed;
     if (!gathers || A->nrows != A->ncols || A->nnz == 0) return EIGSOL_OK;
     const size_t sb = scalar_bytes(A->dtype);
-    double blk_bytes = 2.0 * 1024 * 1024, min_bytes = 6.0 * 1024 * 1024;
+    double blk_bytes = 4.0 * 1024 * 1024, min_bytes = 6.0 * 1024 * 1024;
     if (const char* e = std::getenv("EIGSOL_CSR_CBLK_BYTES")) blk_bytes = std::max(1024.0, std::atof(e));
     if (const char* e = std::getenv("EIGSOL_CSR_CBLK_MIN")) min_bytes = std::atof(e);
     const double xbytes = (double)A->ncols * (double)sb;
@@ -1497,7 +1502,7 @@ static int build_col_blocks(eigsol_csr* A, const int32_t* rowptr, const int32_t*
     const int B = (int)std::ceil(xbytes / blk_bytes);
     // every pass visits every row: blocks pay only while rows keep >= 2 entries per block on average
     const double avg = (double)A->nnz / (double)A->nrows;
-    if (B < 2 || B > 64 || avg < 2.0 * B) return EIGSOL_OK;
+    if (B < 2 || B > 64 || (mode != 2 && avg < 8.0 * B)) return EIGSOL_OK;
     const int64_t n = A->nrows, nc = A->ncols;
     auto blk_of = [&](int32_t c) { return (int)(((int64_t)c * B) / nc); };
     // one pass over the entries, in row order: each block's rows stay ascending
@@ -1576,8 +1581,8 @@ static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, in
     return EIGSOL_OK;
 }
 
-// the device-side peer exchange (row-sharded sessions) is built for the double instantiations
-template <class S> inline constexpr bool kPeerOk = true;   // every scalar type has the peer kernels
+// the device-side peer exchange (row-sharded sessions): every scalar type has the peer kernels
+template <class S> inline constexpr bool kPeerOk = true;
 
 template <class S>
 static const void* power_kernel_ptr(const eigsol_csr* A, bool peer = false) {
@@ -1761,10 +1766,10 @@ int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerC
                                     trace, parity, grid, peer);
     if (A->dtype == EIGSOL_F32)
         return power_launch_t<float>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
-                                     trace, parity, grid, nullptr);
+                                     trace, parity, grid, peer);
     if (A->dtype == EIGSOL_C64)
         return power_launch_t<cplxf>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
-                                     trace, parity, grid, nullptr);
+                                     trace, parity, grid, peer);
     return power_launch_t<double>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
                                   trace, parity, grid, peer);
 }

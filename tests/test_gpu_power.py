@@ -370,6 +370,7 @@ def test_column_blocked_gather_bitwise_and_power(ctx, dtype, monkeypatch):
     forced on a small matrix (x = 1.6 MB, 512 KB blocks: 4 passes; ~1 % of the rows have no entry
     in a given block)."""
     monkeypatch.setenv("EIGSOL_CSR_CBLK_MIN", "0")
+    monkeypatch.setenv("EIGSOL_CSR_CBLK", "2")
     monkeypatch.setenv("EIGSOL_CSR_CBLK_BYTES", str(512 * 1024))
     n = 200_000
     rp, ci, v = S.uniform(n, 16)
