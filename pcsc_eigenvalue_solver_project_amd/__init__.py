@@ -294,7 +294,8 @@ class PowerSession:
                  6: "csr_row_kernel (one row per lane, single-precision fallback layout)",
                  7: "ILU(0)-preconditioned GMRES (tiles = Arnoldi steps of the last solve)",
                  8: "band_solve_kernel (RCM-banded LU; tiles = kl + ku)",
-                 9: "csr_kernel column-block passes (x blocks L2-resident; tiles = blocks)"}
+                 9: "csr_kernel column-block passes (x blocks L2-resident; tiles = blocks)",
+                 10: "csr_bin_kernel (column-binned row chunks, row sums in LDS; tiles = chunks)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?")}
 

@@ -90,6 +90,14 @@ struct CsrArgs {
     PeerArgs peer;           // row-sharded session on the device-side peer exchange (kDist kernels)
     int32_t cb_carry;        // column-block pass > 0 (csr_kernel): row sums start from y's partials
     int32_t cb_epi;          // last (or only) pass: fused power epilogue (norm / Rayleigh partials)
+    // column-binned layout (csr_bin_kernel): entries as (row in chunk << cbits | column in block)
+    const uint32_t* bpk;
+    const S* bval;
+    const int4* bstep;       // per step {first level, levels | barrier << 8, first run, block}
+    const int2* blev;        // per level {entry offset, runs}
+    const int32_t* bchunk;   // per chunk: its steps [bchunk[c], bchunk[c + 1])
+    int32_t nchunks;
+    int32_t bcbits;          // log2 of the columns per block
 };
 
 // Registers holding one tile's stream for one lane: P slots of (values, columns) plus the lane's
@@ -1102,6 +1110,155 @@ __global__ __launch_bounds__(kThreads) void csr_row_kernel(CsrArgs<S> a, int par
     }
 }
 
+// Column-binned SpMV for gather-bound matrices (uniform columns, x larger than the L2s).  Rows go
+// in chunks of kBinRows<S> whose row sums live in LDS, and a chunk's entries are grouped by column
+// block.  A workgroup walks its chunk block by block, so the resident workgroups sweep x together
+// and each block's gathers hit the L2 after the first touch, instead of one cache line fetched from
+// the Infinity Cache per gathered word.  Inside a block, a row's entries form one run (its entries
+// are ascending); runs are sorted longest first and run i belongs to lane i % kNT of the step that
+// covers it.  Level l of the block holds the l-th entry of every run longer than l, so the lanes'
+// loads of one level are contiguous (16-byte-free but coalesced), and a lane adds its run's entries
+// to the row sum in register, in ascending column order.  A row has one run per block, so only the
+// block boundaries need a barrier; every row is summed in ascending column order across blocks --
+// the reference's CSC scatter order, bit for bit.  Entries pack (row in chunk, column in block) in
+// 32 bits: 12 bytes per f64 entry, the CSR stream's size, and no row pointers.
+// kKB: KB of LDS row sums per workgroup (16: more workgroups per CU, for matrices with few row
+// chunks; 64: more rows per chunk, hence more runs per step); kNT threads per workgroup.
+// Step (int4): {index of its first level in the level table, levels | barrier << 8, first run, block};
+// level table (int2): {entry offset, runs at this level}.  A step covers runs [first, first + kNT)
+// and at most kBinLev levels; the host cuts longer runs into several steps (same lanes, no barrier).
+template <class S, int kKB> inline constexpr int kBinRows = kKB * 1024 / (int)sizeof(S);
+constexpr int kBinLev = 4;
+#ifndef EIGSOL_BIN_COND
+#define EIGSOL_BIN_COND 1
+#endif
+constexpr bool kBinCondLoads = EIGSOL_BIN_COND;   // levels >= 1: loads only in waves that use them
+
+template <class S>
+struct BinRegs {
+    uint32_t pk[kBinLev];
+    S v[kBinLev];
+    S x[kBinLev];
+    int c[kBinLev];   // runs at each level (wave-uniform)
+    int nl, bar, i;   // levels, barrier after, this lane's run
+    uint32_t xb;
+};
+
+// LDS-only barrier: the row sums are the only data the waves share, so only the LDS counter is
+// drained; loads of later steps stay in flight across it (__syncthreads would drain them too).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <class S, bool kPower, int kKB, int kNT>
+__global__ __launch_bounds__(kNT) void csr_bin_kernel(CsrArgs<S> a, int parity) {
+    constexpr int kRows = kBinRows<S, kKB>;
+    __shared__ S acc[kRows + 1];
+    __shared__ double sm[3 * (kNT / 64)];
+    __shared__ Prologue pro;
+    __shared__ int s_last;
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kPower) {
+        power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.x_plain;
+        yout = a.y_plain;
+    }
+    const int cb = a.bcbits;
+    const uint32_t cmask = (1u << cb) - 1u;
+    const int tid = threadIdx.x;
+    const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+    // three steps in flight: entries of step s+2 loading, x of step s+1 gathering, step s adding.
+    // Level 0 loads are unconditional (clamped); levels >= 1, which few runs reach, are loaded only
+    // by waves with a lane there (10M uniform: 0.89 ms against 1.29 ms with every level loaded).
+    auto load_pv = [&](BinRegs<S>& R, int st) {
+        const int4 m = ld_uniform(a.bstep, st);
+        R.nl = m.y & 0xff;
+        R.bar = m.y & 0x100;
+        R.i = m.z + tid;
+        R.xb = (uint32_t)m.w << cb;
+#pragma unroll
+        for (int l = 0; l < kBinLev; ++l) {
+            const int2 lv = ld_uniform(a.blev, m.x + min(l, R.nl - 1));
+            R.c[l] = l < R.nl ? lv.y : 0;
+            const uint32_t e = (uint32_t)lv.x + (uint32_t)min(R.i, lv.y - 1);
+            if (kBinCondLoads && l > 0 && m.z + wbase >= R.c[l]) continue;   // no lane of this wave at level l
+            R.pk[l] = ldg_stream(a.bpk, e);
+            R.v[l] = ldg_stream(a.bval, e);
+        }
+    };
+    auto load_x = [&](BinRegs<S>& R) {
+#pragma unroll
+        for (int l = 0; l < kBinLev; ++l) {
+            if (kBinCondLoads && l > 0 && (R.i - tid) + wbase >= R.c[l]) continue;
+            R.x[l] = ldg(xin, R.xb + (R.pk[l] & cmask));
+        }
+    };
+    auto apply = [&](const BinRegs<S>& R) {
+        // lanes without a run add into the spare slot acc[kRows]
+        const int r = R.i < R.c[0] ? (int)(R.pk[0] >> cb) : kRows;
+        S sum = acc[r];
+#pragma unroll
+        for (int l = 0; l < kBinLev; ++l) {
+            if (l > 0 && (R.i - tid) + wbase >= R.c[l]) break;   // no lane of this wave at level l
+            S xv = R.x[l];
+            if constexpr (kPower) xv = scale_in(xv, nrm);
+            const S t = add(sum, mul(R.v[l], xv));
+            sum = R.i < R.c[l] ? t : sum;
+        }
+        acc[r] = sum;
+        if (R.bar) lds_barrier();   // the next block's runs may belong to other lanes
+    };
+    double n2 = 0.0, rr = 0.0, ri = 0.0;
+    for (int c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
+        const int r0 = c * kRows;
+        const int nr = min(kRows, a.nrows - r0);
+        for (int i = tid; i < nr; i += kNT) acc[i] = s_zero<S>();
+        __syncthreads();
+        const int s0 = a.bchunk[c], s1 = a.bchunk[c + 1];
+        if (s0 < s1) {
+            const int sl = s1 - 1;
+            BinRegs<S> RA, RB, RC;
+            load_pv(RA, s0);
+            load_pv(RB, min(s0 + 1, sl));
+            load_x(RA);
+            for (int st = s0;; st += 3) {
+                load_pv(RC, min(st + 2, sl));
+                load_x(RB);
+                apply(RA);
+                if (st + 1 > sl) break;
+                load_pv(RA, min(st + 3, sl));
+                load_x(RC);
+                apply(RB);
+                if (st + 2 > sl) break;
+                load_pv(RB, min(st + 4, sl));
+                load_x(RA);
+                apply(RC);
+                if (st + 3 > sl) break;
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < nr; i += kNT) {
+            const S y = acc[i];
+            yout[r0 + i] = y;
+            if constexpr (kPower) {
+                const S xi = scale_in(xin[r0 + i], nrm);
+                n2 += sq_abs(y);
+                acc_dot(rr, ri, xi, y);
+            }
+        }
+        __syncthreads();   // the next chunk clears acc
+    }
+    if constexpr (kPower) {
+        block_sum3<kNT>(n2, rr, ri, sm);
+        last_arriver_reduce<kNT>(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+    }
+}
+
 // x_out = src / nrm (the reference's x = y / normY of the final iterate; unchanged if nrm == 0).
 template <class S>
 __global__ __launch_bounds__(kThreads) void scale_out_kernel(const S* src, double nrm, S* dst,
@@ -1136,6 +1293,8 @@ void csr_release(eigsol_csr* A) {
     if (A->send_idx) (void)hipFree(A->send_idx);
     if (A->send_buf) (void)hipFree(A->send_buf);
     for (eigsol_csr* B : A->cblk) csr_release(B);
+    for (void* q : {(void*)A->bpk, A->bval, (void*)A->bstep, (void*)A->blev, (void*)A->bchunk})
+        if (q) (void)hipFree(q);
     eigsol_ctx* c = A->ctx;
     delete A;
     ctx_release(c);
@@ -1334,6 +1493,7 @@ static bool build_slices(const int32_t* rowptr, const int32_t* col, const void* 
 
 // xoff: x-space index of local row 0 (0 on one GPU; the lower-ghost count when row-sharded)
 static int build_col_blocks(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, const void* val);
+static int build_bins(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, const void* val);
 static thread_local int g_upload_plain = 0;   // > 0: building a column block (tiles only, no blocks)
 
 int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t nnz,
@@ -1467,7 +1627,8 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
             return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: slice upload: ") + hipGetErrorString(e));
         }
     }
-    const int rcb = build_col_blocks(A, rowptr, col_use, val_use);
+    int rcb = build_bins(A, rowptr, col_use, val_use);
+    if (rcb == EIGSOL_OK && !A->binned) rcb = build_col_blocks(A, rowptr, col_use, val_use);
     if (rcb != EIGSOL_OK) {
         cleanup();
         return rcb;
@@ -1544,6 +1705,142 @@ static int build_col_blocks(eigsol_csr* A, const int32_t* rowptr, const int32_t*
     return EIGSOL_OK;
 }
 
+// Column-binned layout (csr_bin_kernel) for gather-bound matrices: built for square matrices
+// that gather x (gather slices or plain tiles) when x exceeds EIGSOL_CSR_BIN_MIN bytes (default
+// 4 MB: one XCD's L2).  EIGSOL_CSR_BIN=0 disables, =2 builds regardless of x's size (tests);
+// EIGSOL_CSR_BIN_BYTES (default 2 MB) is the x block a chunk's steps gather from.
+static int build_bins(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, const void* val) {
+    if (g_upload_plain || A->xoff != 0 || A->dist) return EIGSOL_OK;
+    int mode = 1;
+    if (const char* e = std::getenv("EIGSOL_CSR_BIN")) mode = std::atoi(e);
+    if (!mode) return EIGSOL_OK;
+    const bool gathers = A->sliced ? A->slice_gather != 0 : !A->windowed;
+    if (!gathers || A->nrows != A->ncols || A->nnz == 0) return EIGSOL_OK;
+    const size_t sb = scalar_bytes(A->dtype);
+    double blk_bytes = 2.0 * 1024 * 1024, min_bytes = 4.0 * 1024 * 1024;
+    if (const char* e = std::getenv("EIGSOL_CSR_BIN_BYTES")) blk_bytes = std::max(1024.0, std::atof(e));
+    if (const char* e = std::getenv("EIGSOL_CSR_BIN_MIN")) min_bytes = std::atof(e);
+    if (mode != 2 && (double)A->ncols * (double)sb < min_bytes) return EIGSOL_OK;
+    // KB of row sums per workgroup: 64 where that still leaves >= 1024 chunks, else 16
+    // (EIGSOL_CSR_BIN_LDS); threads per workgroup 1024 or 256 (EIGSOL_CSR_BIN_NT)
+    int lds_kb = (double)A->nrows * (double)sb >= 1024.0 * 65536.0 ? 64 : 16;
+    if (const char* e = std::getenv("EIGSOL_CSR_BIN_LDS")) lds_kb = std::atoi(e) == 64 ? 64 : 16;
+    int nt = sb >= 16 ? 256 : 1024;   // complex<double>: the 1024-thread instantiation spills
+    if (const char* e = std::getenv("EIGSOL_CSR_BIN_NT")) {
+        const int v = std::atoi(e);
+        nt = v == 256 ? 256 : v == 512 ? 512 : 1024;
+    }
+    const int R = lds_kb * 1024 / (int)sb;   // kBinRows<S, lds_kb>
+    int rbits = 0;
+    while ((1 << rbits) < R) ++rbits;
+    int cbits = 0;
+    while (cbits < 31 && (double)(int64_t(2) << cbits) * (double)sb <= blk_bytes) ++cbits;
+    cbits = std::min(cbits, 32 - rbits);
+    const int64_t n = A->nrows, nc = A->ncols;
+    const int64_t nblk = (nc + (int64_t(1) << cbits) - 1) >> cbits;
+    if (nblk > 65535 || (double)A->nnz * (double)sb >= 4294967296.0) return EIGSOL_OK;   // 32-bit byte offsets
+    const int64_t nchunks = (n + R - 1) / R;
+    std::vector<uint32_t> pk((size_t)A->nnz);
+    std::vector<unsigned char> bv((size_t)A->nnz * sb);
+    std::vector<int32_t> steps, levtab, chunk((size_t)nchunks + 1, 0);
+    struct Run { int32_t blk, row, start, len; };
+    std::vector<Run> runs, sorted;
+    std::vector<int64_t> bcnt;
+    std::vector<int32_t> lcnt;
+    const uint32_t cm = (1u << cbits) - 1u;
+    int64_t out = 0;
+    for (int64_t c = 0; c < nchunks; ++c) {
+        const int64_t r0 = c * R, r1 = std::min(n, r0 + R);
+        // runs: a row's entries inside one column block (contiguous: the row is ascending)
+        runs.clear();
+        for (int64_t i = r0; i < r1; ++i)
+            for (int32_t k = rowptr[i]; k < rowptr[i + 1];) {
+                const int32_t b = col[k] >> cbits;
+                int32_t k2 = k + 1;
+                while (k2 < rowptr[i + 1] && (col[k2] >> cbits) == b) ++k2;
+                runs.push_back({b, (int32_t)(i - r0), k, k2 - k});
+                k = k2;
+            }
+        // by block (stable: row order)
+        bcnt.assign((size_t)nblk + 1, 0);
+        for (const Run& q : runs) ++bcnt[(size_t)q.blk + 1];
+        for (int64_t b = 0; b < nblk; ++b) bcnt[b + 1] += bcnt[b];
+        sorted.resize(runs.size());
+        {
+            std::vector<int64_t> pos(bcnt.begin(), bcnt.end() - 1);
+            for (const Run& q : runs) sorted[(size_t)pos[(size_t)q.blk]++] = q;
+        }
+        for (int64_t b = 0; b < nblk; ++b) {
+            const int64_t q0 = bcnt[b], q1 = bcnt[b + 1];
+            if (q0 == q1) continue;
+            // longest runs first (stable: row order among equal lengths)
+            int32_t maxlen = 0;
+            for (int64_t q = q0; q < q1; ++q) maxlen = std::max(maxlen, sorted[q].len);
+            if (maxlen > 1) {
+                if (maxlen <= 256) {
+                    lcnt.assign((size_t)maxlen + 2, 0);
+                    for (int64_t q = q0; q < q1; ++q) ++lcnt[(size_t)(maxlen - sorted[q].len) + 1];
+                    for (int32_t l = 0; l <= maxlen; ++l) lcnt[l + 1] += lcnt[l];
+                    runs.assign(sorted.begin() + q0, sorted.begin() + q1);
+                    for (const Run& q : runs) sorted[(size_t)(q0 + lcnt[(size_t)(maxlen - q.len)]++)] = q;
+                } else {
+                    std::stable_sort(sorted.begin() + q0, sorted.begin() + q1,
+                                     [](const Run& x, const Run& y) { return x.len > y.len; });
+                }
+            }
+            // levels: level l holds the l-th entry of the c_l runs longer than l
+            const int32_t lbase = (int32_t)(levtab.size() / 2);
+            int64_t cl = q1 - q0;   // runs longer than l (prefix of the sorted runs)
+            for (int32_t l = 0; l < maxlen; ++l) {
+                while (cl > 0 && sorted[q0 + cl - 1].len <= l) --cl;
+                levtab.push_back((int32_t)out);
+                levtab.push_back((int32_t)cl);
+                for (int64_t i = 0; i < cl; ++i) {
+                    const Run& q = sorted[q0 + i];
+                    const int64_t k = q.start + l;
+                    pk[out] = ((uint32_t)q.row << cbits) | ((uint32_t)col[k] & cm);
+                    std::memcpy(&bv[(size_t)out * sb], (const unsigned char*)val + (size_t)k * sb, sb);
+                    ++out;
+                }
+            }
+            // steps: runs [r, r + nt) x levels [l0, l0 + kBinLev); one barrier after the block
+            const size_t sfirst = steps.size();
+            for (int64_t r = 0; r < q1 - q0; r += nt) {
+                int32_t lr = 0;   // levels holding runs >= r
+                while (lr < maxlen && levtab[2 * (lbase + lr) + 1] > r) ++lr;
+                for (int32_t l0 = 0; l0 < lr; l0 += kBinLev) {
+                    steps.push_back(lbase + l0);
+                    steps.push_back(std::min(kBinLev, lr - l0));
+                    steps.push_back((int32_t)r);
+                    steps.push_back((int32_t)b);
+                }
+            }
+            if (steps.size() > sfirst) steps[steps.size() - 3] |= 0x100;
+        }
+        chunk[(size_t)c + 1] = (int32_t)(steps.size() / 4);
+    }
+    A->nchunks = (int32_t)nchunks;
+    A->bcbits = cbits;
+    A->nbsteps = (int32_t)(steps.size() / 4);
+    hipStream_t s = A->ctx->stream;
+    auto upl = [&](void** dst, const void* src, size_t bytes) -> hipError_t {
+        hipError_t r = hipMalloc(dst, std::max<size_t>(bytes, 16));
+        if (r == hipSuccess && bytes) r = hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, s);
+        return r;
+    };
+    hipError_t e;
+    if ((e = upl((void**)&A->bpk, pk.data(), pk.size() * 4)) != hipSuccess ||
+        (e = upl(&A->bval, bv.data(), bv.size())) != hipSuccess ||
+        (e = upl((void**)&A->bstep, steps.data(), steps.size() * 4)) != hipSuccess ||
+        (e = upl((void**)&A->blev, levtab.data(), levtab.size() * 4)) != hipSuccess ||
+        (e = upl((void**)&A->bchunk, chunk.data(), chunk.size() * 4)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: binned upload: ") + hipGetErrorString(e));
+    A->binned = lds_kb;
+    A->bin_nt = nt;
+    return EIGSOL_OK;
+}
+
 static int validate_compressed(const char* who, int64_t nouter, int64_t ninner, int64_t nnz,
                                const int32_t* ptr, const int32_t* idx) {
     if (nouter < 0 || ninner < 0 || nnz < 0)
@@ -1565,11 +1862,12 @@ static int validate_compressed(const char* who, int64_t nouter, int64_t ninner, 
 // ---------------------------------------------------------------- occupancy-derived grid
 // Residency from the kernel's own resources (MI355X_MICROARCH.md § Register files: waves per SIMD
 // = floor(512 / VGPR allocation), 4 waves per block, 160 KiB LDS per CU).
-static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, int* grid, int cap = 8) {
+static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, int* grid, int cap = 8,
+                         int waves = kWaves) {
     hipFuncAttributes fa;
     EIGSOL_HIP(hipFuncGetAttributes(&fa, kernel));
     const int vgpr_alloc = std::max(8, ((fa.numRegs + 7) / 8) * 8);
-    const int by_vgpr = std::min(8, 512 / vgpr_alloc) * 4 / kWaves;
+    const int by_vgpr = std::max(1, std::min(8, 512 / vgpr_alloc) * 4 / waves);
     const int by_lds = fa.sharedSizeBytes ? (int)(160 * 1024 / fa.sharedSizeBytes) : 8;
     int per_cu = std::max(1, std::min({by_vgpr, by_lds, cap}));
     if (const char* env = std::getenv("EIGSOL_CSR_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(env));
@@ -1584,8 +1882,21 @@ static int resident_grid(eigsol_ctx* ctx, const void* kernel, int64_t ntiles, in
 // the device-side peer exchange (row-sharded sessions): every scalar type has the peer kernels
 template <class S> inline constexpr bool kPeerOk = true;
 
+template <class S, bool kPower, int kKB>
+static const void* bin_kernel_ptr_kb(int nt) {
+    return nt == 1024  ? reinterpret_cast<const void*>(csr_bin_kernel<S, kPower, kKB, 1024>)
+           : nt == 512 ? reinterpret_cast<const void*>(csr_bin_kernel<S, kPower, kKB, 512>)
+                       : reinterpret_cast<const void*>(csr_bin_kernel<S, kPower, kKB, 256>);
+}
+template <class S, bool kPower>
+static const void* bin_kernel_ptr(const eigsol_csr* A) {
+    return A->binned == 64 ? bin_kernel_ptr_kb<S, kPower, 64>(A->bin_nt) : bin_kernel_ptr_kb<S, kPower, 16>(A->bin_nt);
+}
+
 template <class S>
 static const void* power_kernel_ptr(const eigsol_csr* A, bool peer = false) {
+    if (A->binned && !peer)
+        return bin_kernel_ptr<S, true>(A);
     if constexpr (std::is_same_v<S, double> || std::is_same_v<S, cplx>)
         if (!A->cblk.empty() && !peer) return reinterpret_cast<const void*>(csr_kernel<S, true>);
     if (A->sliced) {
@@ -1624,6 +1935,7 @@ int csr_grid(eigsol_csr* A, int* grid, bool peer) {
                                              : power_kernel_ptr<double>(A, peer);
     // work units: tiles (one per block step) or slices (one per wave step)
     int64_t units = A->sliced ? (A->nslices + kWaves - 1) / kWaves : A->ntiles;
+    if (A->binned && !peer) return resident_grid(A->ctx, k, A->nchunks, grid, 8, A->bin_nt / 64);
     if (!A->cblk.empty() && !peer) {   // column blocks: csr_kernel passes over the blocks' tiles
         units = 0;
         for (const eigsol_csr* B : A->cblk) units = std::max<int64_t>(units, B->ntiles);
@@ -1664,12 +1976,28 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     a.xoff = (int32_t)A->xoff;
     a.cb_carry = 0;
     a.cb_epi = 1;
+    a.bpk = A->bpk;
+    a.bval = (const S*)A->bval;
+    a.bstep = (const int4*)A->bstep;
+    a.blev = (const int2*)A->blev;
+    a.bchunk = A->bchunk;
+    a.nchunks = A->nchunks;
+    a.bcbits = A->bcbits;
     return a;
 }
 
 template <class S>
 static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int parity, int grid, bool peer = false) {
     hipStream_t s = A->ctx->stream;
+    if (A->binned && !peer) {
+        const void* k = power ? bin_kernel_ptr<S, true>(A) : bin_kernel_ptr<S, false>(A);
+        CsrArgs<S> av = args;
+        int pv = parity;
+        void* argv[] = {&av, &pv};
+        EIGSOL_HIP(hipLaunchKernel(k, dim3(grid), dim3(A->bin_nt), argv, 0, s));
+        EIGSOL_HIP(hipGetLastError());
+        return EIGSOL_OK;
+    }
     if constexpr (std::is_same_v<S, double> || std::is_same_v<S, cplx>) {
         if (!A->cblk.empty() && !peer) {
             // column blocks: one csr_kernel pass per block, partials carried in y (stream order)

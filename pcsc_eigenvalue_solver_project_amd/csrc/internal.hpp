@@ -268,6 +268,16 @@ struct eigsol_csr {
     // adding its block's entries to the row partials of the previous pass (the ascending-column
     // order of every row sum is kept), the last with the fused power epilogue.  Empty: off.
     std::vector<eigsol_csr*> cblk;
+    // Column-binned layout (csr_bin_kernel; preferred over cblk where it is built): chunks of
+    // kBinRows rows, entries ordered (column block, level, row), packed (row << bcbits | column).
+    int32_t binned = 0;            // 0: not built; else KB of LDS row sums (kernel instantiation)
+    int32_t bin_nt = 256;          // threads per workgroup (kernel instantiation)
+    int32_t nchunks = 0, bcbits = 0, nbsteps = 0;
+    uint32_t* bpk = nullptr;
+    void* bval = nullptr;
+    int32_t* bstep = nullptr;      // 4 ints per step
+    int32_t* blev = nullptr;       // 2 ints per level
+    int32_t* bchunk = nullptr;     // nchunks + 1
 };
 
 struct eigsol_dense {

@@ -74,24 +74,26 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Block sum of three doubles in a fixed order; result valid in thread 0.
-__device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double* sm /*3*kWaves*/) {
+template <int NT = kThreads>
+__device__ __forceinline__ void block_sum3(double& a, double& b, double& c, double* sm /*3*NT/64*/) {
+    constexpr int W = NT / 64;
     a = wave_sum(a);
     b = wave_sum(b);
     c = wave_sum(c);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         sm[w] = a;
-        sm[kWaves + w] = b;
-        sm[2 * kWaves + w] = c;
+        sm[W + w] = b;
+        sm[2 * W + w] = c;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        a = sm[0]; b = sm[kWaves]; c = sm[2 * kWaves];
+        a = sm[0]; b = sm[W]; c = sm[2 * W];
 #pragma unroll
-        for (int i = 1; i < kWaves; ++i) {
+        for (int i = 1; i < W; ++i) {
             a += sm[i];
-            b += sm[kWaves + i];
-            c += sm[2 * kWaves + i];
+            b += sm[W + i];
+            c += sm[2 * W + i];
         }
     }
     __syncthreads();
@@ -109,6 +111,7 @@ __device__ __forceinline__ double ld_agent(const double* p) {
 // them, and takes a ticket; the block that draws G-1 reads every partial with sc1 loads and sums
 // them in block order (deterministic), then publishes the rank partial with plain stores (its
 // consumers run after the kernel boundary).  Must be reached by every block of the grid.
+template <int NT = kThreads>
 __device__ __forceinline__ void last_arriver_reduce(double a, double b, double c, part4* blk_part,
                                                     uint32_t* counter, part4* out, double* sm,
                                                     int* s_last) {
@@ -126,12 +129,12 @@ __device__ __forceinline__ void last_arriver_reduce(double a, double b, double c
     __syncthreads();
     if (!*s_last) return;
     double sa = 0.0, sb = 0.0, sc = 0.0;
-    for (uint32_t i = threadIdx.x; i < G; i += kThreads) {
+    for (uint32_t i = threadIdx.x; i < G; i += NT) {
         sa += ld_agent(&blk_part[i].a);
         sb += ld_agent(&blk_part[i].b);
         sc += ld_agent(&blk_part[i].c);
     }
-    block_sum3(sa, sb, sc, sm);
+    block_sum3<NT>(sa, sb, sc, sm);
     if (threadIdx.x == 0) {
         out->a = sa;
         out->b = sb;

@@ -586,6 +586,10 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
             if (variant) *variant = 9;
             if (tiles) *tiles = (int32_t)s->csr->cblk.size();
         }
+        if (s->csr->binned && !s->peer) {   // column-binned chunks (tiles = chunks)
+            if (variant) *variant = 10;
+            if (tiles) *tiles = s->csr->nchunks;
+        }
     } else {
         const double n = (double)s->dense->nrows;
         if (bytes) *bytes = sb * n * n + 2.0 * sb * n;

@@ -392,3 +392,54 @@ def test_column_blocked_gather_bitwise_and_power(ctx, dtype, monkeypatch):
     assert ref["converged"]
     _assert_power_parity(res, ref, tol)
     A.close()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128, np.float32, np.complex64])
+def test_column_binned_gather_bitwise_and_power(ctx, dtype, monkeypatch):
+    """Column-binned gathers (csr_bin_kernel: row chunks whose sums live in LDS, entries ordered by
+    column block, then level, then row): the product is bitwise the reference's CSC scatter
+    (power_method.hpp:69; every row summed in ascending column order across levels and blocks)
+    and the power iteration keeps the oracle parity of test_power_csr_parity.  Forced on a small
+    matrix with 64 KB blocks (many blocks, several levels per block), plus a dense row (2000
+    entries: thousands of one-entry levels) and empty rows."""
+    monkeypatch.setenv("EIGSOL_CSR_BIN", "2")
+    monkeypatch.setenv("EIGSOL_CSR_BIN_BYTES", str(64 * 1024))
+    n = 150_000
+    rp, ci, v = S.uniform(n, 16)
+    # row 7: 2000 ascending columns; rows 100..199: empty
+    lens = np.diff(rp).astype(np.int64)
+    rows = [ci[rp[i]:rp[i + 1]] for i in range(n)]
+    vals = [v[rp[i]:rp[i + 1]] for i in range(n)]
+    rng = np.random.default_rng(11)
+    rows[7] = np.sort(rng.choice(n, 2000, replace=False)).astype(np.int32)
+    vals[7] = rng.uniform(-1, 1, 2000)
+    for i in range(100, 200):
+        rows[i] = rows[i][:0]
+        vals[i] = vals[i][:0]
+    lens = np.array([len(r) for r in rows], dtype=np.int64)
+    rp = np.zeros(n + 1, dtype=np.int32)
+    np.cumsum(lens, out=rp[1:])
+    ci = np.concatenate(rows).astype(np.int32)
+    v = np.concatenate(vals).astype(dtype)
+    if np.issubdtype(dtype, np.complexfloating):
+        v = (v + 1j * np.random.default_rng(1).uniform(-1, 1, len(v))).astype(dtype)
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    s = E.PowerSession(A)
+    info = s.kernel_info()
+    s.close()
+    assert info["variant"] == 10 and info["tiles"] >= 2, info
+    x = S.start_vector(n, dtype)
+    y = _spmv_gpu(ctx, A, x)
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    assert np.array_equal(y, O.spmv_csc(cp, ri, vv, x, n))
+    single = dtype in (np.float32, np.complex64)
+    tol = 1e-5 if single else 1e-12
+    res = E.power_method(A, E.SolverOptions(1000, tol), x)
+    ref = O.power_csc(cp, ri, vv, x, 1000, tol, want_trace=True)
+    assert ref["converged"]
+    if single:
+        assert abs(res.eigenvalue - ref["eigenvalue"]) <= 1e-5 * (1 + abs(ref["eigenvalue"]))
+        assert abs(res.iterations - ref["iterations"]) <= 1
+    else:
+        _assert_power_parity(res, ref, tol)
+    A.close()
