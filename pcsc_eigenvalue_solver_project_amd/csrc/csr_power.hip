@@ -1708,7 +1708,7 @@ static int build_col_blocks(eigsol_csr* A, const int32_t* rowptr, const int32_t*
 // Column-binned layout (csr_bin_kernel) for gather-bound matrices: built for square matrices
 // that gather x (gather slices or plain tiles) when x exceeds EIGSOL_CSR_BIN_MIN bytes (default
 // 4 MB: one XCD's L2).  EIGSOL_CSR_BIN=0 disables, =2 builds regardless of x's size (tests);
-// EIGSOL_CSR_BIN_BYTES (default 2 MB) is the x block a chunk's steps gather from.
+// EIGSOL_CSR_BIN_BYTES (default 1 MB) is the x block a chunk's steps gather from.
 static int build_bins(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, const void* val) {
     if (g_upload_plain || A->xoff != 0 || A->dist) return EIGSOL_OK;
     int mode = 1;
@@ -1717,14 +1717,21 @@ static int build_bins(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, 
     const bool gathers = A->sliced ? A->slice_gather != 0 : !A->windowed;
     if (!gathers || A->nrows != A->ncols || A->nnz == 0) return EIGSOL_OK;
     const size_t sb = scalar_bytes(A->dtype);
-    double blk_bytes = 2.0 * 1024 * 1024, min_bytes = 4.0 * 1024 * 1024;
+    // complex<double>: the 16-byte gathers already fetch 4 entries per 64-byte line and its
+    // kernel runs at 3 waves per SIMD; config 5's triangular product measured 0.198 ms sliced
+    // against 0.356 ms binned, so it keeps the slices
+    if (sb > 8 && mode != 2) return EIGSOL_OK;
+    double blk_bytes = 1024.0 * 1024, min_bytes = 4.0 * 1024 * 1024;
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_BYTES")) blk_bytes = std::max(1024.0, std::atof(e));
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_MIN")) min_bytes = std::atof(e);
     if (mode != 2 && (double)A->ncols * (double)sb < min_bytes) return EIGSOL_OK;
     // KB of row sums per workgroup: 64 where that still leaves >= 1024 chunks, else 16
     // (EIGSOL_CSR_BIN_LDS); threads per workgroup 1024 or 256 (EIGSOL_CSR_BIN_NT)
     int lds_kb = (double)A->nrows * (double)sb >= 1024.0 * 65536.0 ? 64 : 16;
-    if (const char* e = std::getenv("EIGSOL_CSR_BIN_LDS")) lds_kb = std::atoi(e) == 64 ? 64 : 16;
+    if (const char* e = std::getenv("EIGSOL_CSR_BIN_LDS")) {
+        const int v = std::atoi(e);
+        lds_kb = v == 128 ? 128 : v == 64 ? 64 : 16;
+    }
     int nt = sb >= 16 ? 256 : 1024;   // complex<double>: the 1024-thread instantiation spills
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_NT")) {
         const int v = std::atoi(e);
@@ -1890,7 +1897,9 @@ static const void* bin_kernel_ptr_kb(int nt) {
 }
 template <class S, bool kPower>
 static const void* bin_kernel_ptr(const eigsol_csr* A) {
-    return A->binned == 64 ? bin_kernel_ptr_kb<S, kPower, 64>(A->bin_nt) : bin_kernel_ptr_kb<S, kPower, 16>(A->bin_nt);
+    return A->binned == 128  ? bin_kernel_ptr_kb<S, kPower, 128>(A->bin_nt)
+           : A->binned == 64 ? bin_kernel_ptr_kb<S, kPower, 64>(A->bin_nt)
+                             : bin_kernel_ptr_kb<S, kPower, 16>(A->bin_nt);
 }
 
 template <class S>
