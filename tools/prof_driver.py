@@ -46,10 +46,10 @@ if args.workload == "dense16384":
     print("done", s.kernel_info())
     s.close(); D.close(); ctx.close()
     sys.exit(0)
-if args.workload == "qrc1024":
+if args.workload in ("qrc1024", "qrc4096"):
     import numpy as np
-    n = 1024
-    rng = np.random.default_rng(1024)
+    n = 1024 if args.workload == "qrc1024" else 4096
+    rng = np.random.default_rng(n)
     a = np.asfortranarray(rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n)))
     ctx = E.Context(0)
     r = E.qr_eigenvalues(ctx, a, E.SolverOptions(1000, 1e-12))
