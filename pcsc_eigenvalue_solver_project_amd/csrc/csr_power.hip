@@ -1163,7 +1163,7 @@ __global__ __launch_bounds__(kNT) void csr_bin_kernel(CsrArgs<S> a, int parity) 
         if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
         nrm = pro.nrm;
         xin = parity ? a.buf0 : a.buf1;
-        yout = parity ? a.buf1 : a.buf0;
+        yout = (parity ? a.buf1 : a.buf0) + a.xoff;   // y rows land at their x-space slots (row shards)
     } else {
         xin = a.x_plain;
         yout = a.y_plain;
@@ -1246,7 +1246,7 @@ __global__ __launch_bounds__(kNT) void csr_bin_kernel(CsrArgs<S> a, int parity) 
             const S y = acc[i];
             yout[r0 + i] = y;
             if constexpr (kPower) {
-                const S xi = scale_in(xin[r0 + i], nrm);
+                const S xi = scale_in(xin[r0 + i + a.xoff], nrm);
                 n2 += sq_abs(y);
                 acc_dot(rr, ri, xi, y);
             }
@@ -1705,17 +1705,18 @@ static int build_col_blocks(eigsol_csr* A, const int32_t* rowptr, const int32_t*
     return EIGSOL_OK;
 }
 
-// Column-binned layout (csr_bin_kernel) for gather-bound matrices: built for square matrices
-// that gather x (gather slices or plain tiles) when x exceeds EIGSOL_CSR_BIN_MIN bytes (default
-// 4 MB: one XCD's L2).  EIGSOL_CSR_BIN=0 disables, =2 builds regardless of x's size (tests);
+// Column-binned layout (csr_bin_kernel) for gather-bound matrices: built for matrices (square,
+// rectangular or row shards) that gather x (gather slices or plain tiles) when x exceeds
+// EIGSOL_CSR_BIN_MIN bytes (default 4 MB: one XCD's L2).  EIGSOL_CSR_BIN=0 disables, =2 builds regardless of x's size (tests);
 // EIGSOL_CSR_BIN_BYTES (default 1 MB) is the x block a chunk's steps gather from.
 static int build_bins(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, const void* val) {
-    if (g_upload_plain || A->xoff != 0 || A->dist) return EIGSOL_OK;
+    if (g_upload_plain) return EIGSOL_OK;
     int mode = 1;
     if (const char* e = std::getenv("EIGSOL_CSR_BIN")) mode = std::atoi(e);
     if (!mode) return EIGSOL_OK;
+    // gathering products of any shape: square matrices, row shards (x-space columns, rows at xoff)
     const bool gathers = A->sliced ? A->slice_gather != 0 : !A->windowed;
-    if (!gathers || A->nrows != A->ncols || A->nnz == 0) return EIGSOL_OK;
+    if (!gathers || A->nnz == 0) return EIGSOL_OK;
     const size_t sb = scalar_bytes(A->dtype);
     // complex<double>: the 16-byte gathers already fetch 4 entries per 64-byte line and its
     // kernel runs at 3 waves per SIMD; config 5's triangular product measured 0.198 ms sliced

@@ -68,7 +68,7 @@ def test_dist_single_rank_allgather_exchange(monkeypatch):
         ctx.close()
 
 
-def _loopback_run(world, kind, n, k, exchange=None, monkeypatch=None):
+def _loopback_run(world, kind, n, k, exchange=None, monkeypatch=None, variants=None):
     """`world` ranks in threads of this process, one device, joined by the loopback transport."""
     import threading
     if exchange:
@@ -88,6 +88,8 @@ def _loopback_run(world, kind, n, k, exchange=None, monkeypatch=None):
             rb = np.array([q * rows for q in range(world)] + [n], dtype=np.int64)
             A = D.DistCsrMatrix(ctx, rb, lrp, lci, lv)
             sess = E.PowerSession(A)
+            if variants is not None:
+                variants.append(sess.kernel_info()["variant"])
             sess.begin(E.SolverOptions(300, 1e-12), x0[r0:r1])
             sess.step(301)
             assert sess.query()[0]
@@ -127,9 +129,17 @@ def test_loopback_multi_rank_halo(world):
     assert all(m == D.EXCHANGE_HALO for m in modes)
 
 
-def test_loopback_multi_rank_allgather(monkeypatch):
-    modes = _loopback_run(2, "uniform", 20000, 8, exchange="allgather", monkeypatch=monkeypatch)
+@pytest.mark.parametrize("binned", [False, True])
+def test_loopback_multi_rank_allgather(monkeypatch, binned):
+    """binned: the column-binned kernel on the shards (x-space columns, own rows at xoff; forced on
+    this small matrix with 32 KB x blocks), every rank's eigenvalue still bitwise identical."""
+    if binned:
+        monkeypatch.setenv("EIGSOL_CSR_BIN", "2")
+        monkeypatch.setenv("EIGSOL_CSR_BIN_BYTES", str(32 * 1024))
+    variants = []
+    modes = _loopback_run(2, "uniform", 20000, 8, exchange="allgather", monkeypatch=monkeypatch, variants=variants)
     assert all(m == D.EXCHANGE_ALLGATHER for m in modes)
+    assert all(v == (10 if binned else 5) for v in variants), variants
 
 
 def test_loopback_uniform_auto_exchange():

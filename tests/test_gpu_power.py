@@ -443,3 +443,12 @@ def test_column_binned_gather_bitwise_and_power(ctx, dtype, monkeypatch):
     else:
         _assert_power_parity(res, ref, tol)
     A.close()
+    # rectangular product (2n columns): rows chunked by n, columns blocked over 2n
+    rp2, ci2, v2 = S.uniform(n, 12, seed=3)
+    ci2 = (ci2.astype(np.int64) * 2 + (np.arange(len(ci2)) & 1)).astype(np.int32)
+    v2 = v2.astype(dtype)
+    B = E.CsrMatrix(ctx, rp2, ci2, v2, (n, 2 * n))
+    xb = S.start_vector(2 * n, dtype)
+    cp2, ri2, vv2 = O.csr_to_csc(rp2, ci2, v2, 2 * n)
+    assert np.array_equal(_spmv_gpu(ctx, B, xb), O.spmv_csc(cp2, ri2, vv2, xb, n))
+    B.close()
