@@ -295,7 +295,9 @@ class PowerSession:
                  7: "ILU(0)-preconditioned GMRES (tiles = Arnoldi steps of the last solve)",
                  8: "band_solve_kernel (RCM-banded LU; tiles = kl + ku)",
                  9: "csr_kernel column-block passes (x blocks L2-resident; tiles = blocks)",
-                 10: "csr_bin_kernel (column-binned row chunks, row sums in LDS; tiles = chunks)"}
+                 10: "csr_bin_kernel (column-binned row chunks, row sums in LDS; tiles = chunks)",
+                 11: "csr_bin_kernel in two row halves per iteration, the first half's all-gather "
+                     "overlapped with the second half (row-sharded; tiles = chunks)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?")}
 

@@ -98,6 +98,8 @@ struct CsrArgs {
     const int32_t* bchunk;   // per chunk: its steps [bchunk[c], bchunk[c + 1])
     int32_t nchunks;
     int32_t bcbits;          // log2 of the columns per block
+    int32_t cbeg, cend;      // chunks of this launch (an iteration split in two row parts)
+    int32_t cont;            // second part: read the first part's decision, add to its partial
 };
 
 // Registers holding one tile's stream for one lane: P slots of (values, columns) plus the lane's
@@ -1159,7 +1161,7 @@ __global__ __launch_bounds__(kNT) void csr_bin_kernel(CsrArgs<S> a, int parity) 
     S* yout;
     double nrm = 0.0;
     if constexpr (kPower) {
-        power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro);
+        power_prologue<S>(a.ctl, a.rank_part, a.nranks, parity, a.trace, &pro, nullptr, a.cont != 0);
         if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // block-uniform exit
         nrm = pro.nrm;
         xin = parity ? a.buf0 : a.buf1;
@@ -1214,7 +1216,7 @@ __global__ __launch_bounds__(kNT) void csr_bin_kernel(CsrArgs<S> a, int parity) 
         if (R.bar) lds_barrier();   // the next block's runs may belong to other lanes
     };
     double n2 = 0.0, rr = 0.0, ri = 0.0;
-    for (int c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
+    for (int c = a.cbeg + blockIdx.x; c < a.cend; c += gridDim.x) {
         const int r0 = c * kRows;
         const int nr = min(kRows, a.nrows - r0);
         for (int i = tid; i < nr; i += kNT) acc[i] = s_zero<S>();
@@ -1255,7 +1257,7 @@ __global__ __launch_bounds__(kNT) void csr_bin_kernel(CsrArgs<S> a, int parity) 
     }
     if constexpr (kPower) {
         block_sum3<kNT>(n2, rr, ri, sm);
-        last_arriver_reduce<kNT>(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last);
+        last_arriver_reduce<kNT>(n2, rr, ri, a.blk_part, &a.ctl->counter, a.my_part, sm, &s_last, a.cont != 0);
     }
 }
 
@@ -1993,6 +1995,9 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     a.bchunk = A->bchunk;
     a.nchunks = A->nchunks;
     a.bcbits = A->bcbits;
+    a.cbeg = 0;
+    a.cend = A->nchunks;
+    a.cont = 0;
     return a;
 }
 
@@ -2077,11 +2082,19 @@ static int launch_csr(eigsol_csr* A, const CsrArgs<S>& args, bool power, int par
     return EIGSOL_OK;
 }
 
+// First chunk of the second row part of an iteration split in two (binned layout).
+static int32_t bin_split_chunk(const eigsol_csr* A) { return (A->nchunks + 1) / 2; }
+
 template <class S>
 static int power_launch_t(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
                           const void* rank_part, int nranks, void* my_part, void* blk_part,
-                          void* trace, int parity, int grid, const PeerArgs* peer) {
+                          void* trace, int parity, int grid, const PeerArgs* peer, int part) {
     CsrArgs<S> a = make_args<S>(A, xlen);
+    if (part >= 0) {   // one of the two row parts of a split iteration (binned layout only)
+        a.cbeg = part == 0 ? 0 : bin_split_chunk(A);
+        a.cend = part == 0 ? bin_split_chunk(A) : A->nchunks;
+        a.cont = part;
+    }
     a.buf0 = (S*)buf0;
     a.buf1 = (S*)buf1;
     a.ctl = ctl;
@@ -2097,19 +2110,27 @@ static int power_launch_t(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, P
 // entry point used by power_session.cpp (xlen: entries of the y buffers, own + ghost)
 int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
                      const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
-                     int parity, int grid, const PeerArgs* peer) {
+                     int parity, int grid, const PeerArgs* peer, int part) {
     if (peer && !A->sliced) return fail(EIGSOL_E_UNSUPPORTED, "peer exchange needs the sliced CSR layout");
+    if (part >= 0 && (peer || !A->binned)) return fail(EIGSOL_E_INVALID, "split iteration needs the binned layout");
     if (A->dtype == EIGSOL_C128)
         return power_launch_t<cplx>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
-                                    trace, parity, grid, peer);
+                                    trace, parity, grid, peer, part);
     if (A->dtype == EIGSOL_F32)
         return power_launch_t<float>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
-                                     trace, parity, grid, peer);
+                                     trace, parity, grid, peer, part);
     if (A->dtype == EIGSOL_C64)
         return power_launch_t<cplxf>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
-                                     trace, parity, grid, peer);
+                                     trace, parity, grid, peer, part);
     return power_launch_t<double>(A, xlen, buf0, buf1, ctl, rank_part, nranks, my_part, blk_part,
-                                  trace, parity, grid, peer);
+                                  trace, parity, grid, peer, part);
+}
+
+// Own rows in the first part of a split iteration (binned layout): whole chunks of the first half.
+int64_t csr_bin_split_row(const eigsol_csr* A) {
+    if (!A->binned) return A->nrows;
+    const int64_t rows = (int64_t)A->binned * 1024 / (int64_t)scalar_bytes(A->dtype);   // kBinRows
+    return std::min<int64_t>(A->nrows, (int64_t)bin_split_chunk(A) * rows);
 }
 
 int peer_begin_launch(eigsol_ctx* ctx, int dtype, const PeerArgs& pa, const void* x_own, int64_t npush,

@@ -305,6 +305,60 @@ int dist_exchange(eigsol_csr* A, void* y, void* rank_part) {
     return EIGSOL_OK;
 }
 
+// All-gather exchange of an iteration split in two row parts (binned shards): part 0 moves rows
+// [rb_q, rb_q + split[q]) of every rank q, part 1 the rest and the rank partials.  With RCCL the
+// parts run on `comm` after an event on the compute stream, so part 0's transfer overlaps the
+// second part's product; after part 1 the compute stream waits for `comm`.  The loopback world
+// copies on the compute stream (same data movement, no overlap).
+int dist_exchange_part(eigsol_csr* A, void* y, void* rank_part, int part, const std::vector<int64_t>& split,
+                       hipStream_t comm_st, hipEvent_t* ev) {
+    eigsol_ctx* ctx = A->ctx;
+    const size_t sb = scalar_bytes(A->dtype);
+    const int P = ctx->nranks, me = ctx->rank;
+    const std::vector<int64_t>& rb = A->row_begins;
+    char* xs = static_cast<char*>(y);
+    double* rpart = static_cast<double*>(rank_part);
+    auto seg = [&](int q, int64_t& lo, int64_t& hi) {
+        lo = part == 0 ? rb[q] : rb[q] + split[q];
+        hi = part == 0 ? rb[q] + split[q] : rb[q + 1];
+    };
+    if (ctx->loop) {
+        std::vector<LoopSend> ls;
+        std::vector<LoopRecv> lr;
+        int64_t mlo, mhi;
+        seg(me, mlo, mhi);
+        for (int q = 0; q < P; ++q) {
+            if (q == me) continue;
+            int64_t lo, hi;
+            seg(q, lo, hi);
+            ls.push_back({q, xs + (size_t)mlo * sb, (size_t)(mhi - mlo) * sb});
+            lr.push_back({q, xs + (size_t)lo * sb, (size_t)(hi - lo) * sb});
+        }
+        if (part == 1) loop_allgather(ctx, rpart, 4 * sizeof(double), ls, lr);
+        return loop_step(ctx, ls, lr);
+    }
+    ncclComm_t comm = static_cast<ncclComm_t>(ctx->comm);
+    const ncclDataType_t vty = dtype_single(A->dtype) ? ncclFloat32 : ncclFloat64;
+    const size_t dpe = dtype_single(A->dtype) ? sb / 4 : sb / 8;
+    EIGSOL_HIP(hipEventRecord(ev[part], ctx->stream));
+    EIGSOL_HIP(hipStreamWaitEvent(comm_st, ev[part], 0));
+    EIGSOL_RCCL(ncclGroupStart());
+    for (int q = 0; q < P; ++q) {
+        int64_t lo, hi;
+        seg(q, lo, hi);
+        if (hi > lo)
+            EIGSOL_RCCL(ncclBroadcast(xs + (size_t)lo * sb, xs + (size_t)lo * sb, (size_t)(hi - lo) * dpe, vty, q,
+                                      comm, comm_st));
+    }
+    if (part == 1) EIGSOL_RCCL(ncclAllGather(rpart + 4 * me, rpart, 4, ncclFloat64, comm, comm_st));
+    EIGSOL_RCCL(ncclGroupEnd());
+    if (part == 1) {
+        EIGSOL_HIP(hipEventRecord(ev[2], comm_st));
+        EIGSOL_HIP(hipStreamWaitEvent(ctx->stream, ev[2], 0));
+    }
+    return EIGSOL_OK;
+}
+
 }  // namespace eigsol
 
 using namespace eigsol;

@@ -93,17 +93,23 @@ __global__ __launch_bounds__(kThreads) void gm_dots_kernel(const S* V, int64_t l
     }
 }
 
-// out[c] = sum of the G block partials in block order (deterministic)
-__global__ __launch_bounds__(64) void gm_reduce_kernel(const double* part, int G, int k, double* out) {
-    const int c = threadIdx.x;
-    if (c >= k) return;
-    double rr = 0.0, ri = 0.0;
-    for (int b = 0; b < G; ++b) {
+// out[c] = sum of the G block partials (one workgroup per column c; thread t sums blocks t, t + 256,
+// ... in order, then a fixed-order block reduction: deterministic for a given G).  Round 2's
+// one-wave version summed the G = 489 partials of a 1M vector one after another per lane:
+// 64 us per call, 14 % of a GMRES iteration.
+__global__ __launch_bounds__(kThreads) void gm_reduce_kernel(const double* part, int G, int k, double* out) {
+    __shared__ double sm[3 * kWaves];
+    const int c = blockIdx.x;
+    double rr = 0.0, ri = 0.0, dummy = 0.0;
+    for (int b = threadIdx.x; b < G; b += kThreads) {
         rr += part[((int64_t)b * k + c) * 2];
         ri += part[((int64_t)b * k + c) * 2 + 1];
     }
-    out[2 * c] = rr;
-    out[2 * c + 1] = ri;
+    block_sum3(rr, ri, dummy, sm);
+    if (threadIdx.x == 0) {
+        out[2 * c] = rr;
+        out[2 * c + 1] = ri;
+    }
 }
 
 template <class S>
@@ -342,11 +348,11 @@ static int cgs2(GmresSolver* g, S* V, int k, S* w, std::vector<hc>& h, double& w
     for (int pass = 0; pass < 2; ++pass) {
         double* hp = g->hdev + pass * stride;
         hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, V, n, k, w, n, g->part);
-        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(64), 0, st, g->part, g->G, k, hp);
+        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(k), dim3(dev::kThreads), 0, st, g->part, g->G, k, hp);
         hipLaunchKernelGGL((dev::gm_combine_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, V, n, k, hp, w, n, 0);
     }
     hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
-    hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(64), 0, st, g->part, g->G, 1, g->hdev + 2 * stride);
+    hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev + 2 * stride);
     std::vector<double> hb(2 * stride + 2);
     EIGSOL_HIP(hipMemcpyAsync(hb.data(), g->hdev, hb.size() * sizeof(double), hipMemcpyDeviceToHost, st));
     EIGSOL_HIP(hipStreamSynchronize(st));
@@ -378,7 +384,7 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y) {
     auto norm_of = [&](S* v, double& out) -> int {
         double hb[2];
         hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, v, n, 1, v, n, g->part);
-        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(64), 0, st, g->part, g->G, 1, g->hdev);
+        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev);
         EIGSOL_HIP(hipMemcpyAsync(hb, g->hdev, sizeof(hb), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(hipStreamSynchronize(st));
         out = std::sqrt(hb[0]);

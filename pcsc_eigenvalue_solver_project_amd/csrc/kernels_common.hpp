@@ -111,10 +111,12 @@ __device__ __forceinline__ double ld_agent(const double* p) {
 // them, and takes a ticket; the block that draws G-1 reads every partial with sc1 loads and sums
 // them in block order (deterministic), then publishes the rank partial with plain stores (its
 // consumers run after the kernel boundary).  Must be reached by every block of the grid.
+// accum: add to *out instead of overwriting it (the second launch of an iteration split in two
+// row parts; the first part's launch wrote *out, so the sum order is fixed: part 0, then part 1).
 template <int NT = kThreads>
 __device__ __forceinline__ void last_arriver_reduce(double a, double b, double c, part4* blk_part,
                                                     uint32_t* counter, part4* out, double* sm,
-                                                    int* s_last) {
+                                                    int* s_last, bool accum = false) {
     const uint32_t G = gridDim.x;
     if (threadIdx.x == 0) {
         part4* p = blk_part + blockIdx.x;
@@ -136,6 +138,11 @@ __device__ __forceinline__ void last_arriver_reduce(double a, double b, double c
     }
     block_sum3<NT>(sa, sb, sc, sm);
     if (threadIdx.x == 0) {
+        if (accum) {
+            sa = out->a + sa;
+            sb = out->b + sb;
+            sc = out->c + sc;
+        }
         out->a = sa;
         out->b = sb;
         out->c = sc;
@@ -256,10 +263,28 @@ struct alignas(16) Prologue {
 
 // peer != nullptr: row-sharded session on the device-side peer exchange — wait for every peer's
 // flag of the previous launch (epoch t + 1), then read the rank partials from the own inbox.
+//
+// cont: the second launch of an iteration split in two row parts (row-sharded sessions that
+// overlap the first part's all-gather with the second part's product): the first launch's
+// prologue already decided and advanced the carry, so this one only reads its decision.
 template <class S>
 __device__ __forceinline__ void power_prologue(PowerCtl* ctl, const part4* rank_part, int nranks,
                                                int parity, S* trace, Prologue* out,
-                                               const PeerArgs* peer = nullptr) {
+                                               const PeerArgs* peer = nullptr, bool cont = false) {
+    if (cont) {
+        if (threadIdx.x == 0) {
+            Prologue pr{0.0, 0, 0};
+            if (!__hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                const PowerCarry o = ctl->st[parity ^ 1];
+                pr.go = 1;
+                pr.nrm = o.nrm;
+                pr.t = o.t;
+            }
+            *out = pr;
+        }
+        __syncthreads();
+        return;
+    }
     if (threadIdx.x == 0) {
         Prologue pr{0.0, 0, 0};
         int done = __hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -23,7 +23,10 @@ int csr_grid(eigsol_csr* A, int* grid, bool peer = false);
 const void* csr_power_kernel(const eigsol_csr* A, bool peer);
 int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerCtl* ctl,
                      const void* rank_part, int nranks, void* my_part, void* blk_part, void* trace,
-                     int parity, int grid, const dev::PeerArgs* peer = nullptr);
+                     int parity, int grid, const dev::PeerArgs* peer = nullptr, int part = -1);
+int64_t csr_bin_split_row(const eigsol_csr* A);
+int dist_exchange_part(eigsol_csr* A, void* y, void* rank_part, int part, const std::vector<int64_t>& split,
+                       hipStream_t comm_st, hipEvent_t* ev);
 int peer_begin_launch(eigsol_ctx* ctx, int dtype, const dev::PeerArgs& pa, const void* x_own, int64_t npush,
                       const void* mine);
 int coll_allgather(eigsol_ctx* ctx, const void* mine, size_t bytes, void* all);
@@ -91,6 +94,13 @@ struct eigsol_power {
     int transport = EIGSOL_TRANSPORT_LOCAL;
     PeerState* peer = nullptr;
     int same_device = 1;      // ranks (of any process) sharing this rank's device
+    // Split iteration (row-sharded, all-gather exchange, binned layout): two launches over the
+    // first and second halves of the own chunks; the first half's all-gather runs on `comm`
+    // while the second half computes.  split_rows[q]: rank q's rows in its first half.
+    bool split = false;
+    std::vector<int64_t> split_rows;
+    hipStream_t comm = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
 };
 
 static constexpr size_t kPart = 32;
@@ -129,6 +139,12 @@ static void session_free(eigsol_power* s) {
     if (!s) return;
     hipSetDevice(s->ctx->device);
     hipStreamSynchronize(s->ctx->stream);
+    if (s->comm) {
+        hipStreamSynchronize(s->comm);
+        hipStreamDestroy(s->comm);
+    }
+    for (hipEvent_t e : s->ev)
+        if (e) hipEventDestroy(e);
     peer_free(s);
     hipFree(s->buf[0]);
     hipFree(s->buf[1]);
@@ -150,6 +166,17 @@ static int launch_iteration(eigsol_power* s) {
     if (s->shift)
         return shift_iter_launch(s->shift, s->buf[0], s->buf[1], s->ctl, s->rank_part, s->my_part,
                                  s->trace, s->parity);
+    if (s->csr && s->dist && s->split) {
+        // launch t writes y_t into buf[t & 1]: the first half's rows go out while the second half computes
+        for (int part = 0; part < 2; ++part) {
+            EIGSOL_TRY(csr_power_launch(s->csr, s->nbuf, s->buf[0], s->buf[1], s->ctl, s->rank_part,
+                                        s->ctx->nranks, s->my_part, s->blk_part, s->trace, s->parity, s->grid,
+                                        nullptr, part));
+            EIGSOL_TRY(dist_exchange_part(s->csr, s->buf[s->parity], s->rank_part, part, s->split_rows, s->comm,
+                                          s->ev));
+        }
+        return EIGSOL_OK;
+    }
     if (s->csr && s->dist) {
         EIGSOL_TRY(csr_power_launch(s->csr, s->nbuf, s->buf[0], s->buf[1], s->ctl, s->rank_part,
                                     s->ctx->nranks, s->my_part, s->blk_part, s->trace, s->parity, s->grid));
@@ -347,6 +374,30 @@ static int choose_transport(eigsol_power* s, int32_t trace_cap) {
     return EIGSOL_OK;
 }
 
+// Collective: split every iteration in two row parts when every rank's shard is binned, uses the
+// all-gather exchange and has >= 2 chunks (EIGSOL_DIST_SPLIT=0 disables).  The first part's
+// all-gather then overlaps the second part's product (RCCL on a stream of its own).
+static int choose_split(eigsol_power* s) {
+    eigsol_csr* A = s->csr;
+    eigsol_ctx* ctx = s->ctx;
+    const int P = ctx->nranks;
+    int cand = (A->binned && A->nchunks >= 2 && A->exchange == EIGSOL_EXCHANGE_ALLGATHER &&
+                (ctx->comm || ctx->loop)) ? 1 : 0;
+    if (const char* e = std::getenv("EIGSOL_DIST_SPLIT")) if (!std::atoi(e)) cand = 0;
+    std::vector<int> all(P);
+    EIGSOL_TRY(coll_allgather(ctx, &cand, sizeof(int), all.data()));
+    for (int v : all) if (!v) return EIGSOL_OK;
+    const int64_t mine = csr_bin_split_row(A);
+    s->split_rows.assign(P, 0);
+    EIGSOL_TRY(coll_allgather(ctx, &mine, sizeof(mine), s->split_rows.data()));
+    if (!ctx->loop) {
+        EIGSOL_HIP(hipStreamCreateWithFlags(&s->comm, hipStreamNonBlocking));
+        for (hipEvent_t& e : s->ev) EIGSOL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    s->split = true;
+    return EIGSOL_OK;
+}
+
 extern "C" {
 
 int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power** out) {
@@ -365,6 +416,7 @@ int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power*
     s->nbuf = A->ncols;
     int rc = csr_grid(A, &s->grid);
     if (rc == EIGSOL_OK && s->dist) rc = choose_transport(s, trace_capacity);
+    if (rc == EIGSOL_OK && s->dist && s->transport == EIGSOL_TRANSPORT_COLLECTIVE) rc = choose_split(s);
     if (rc == EIGSOL_OK && !s->buf[0]) rc = session_alloc(s, trace_capacity);
     if (rc != EIGSOL_OK) { session_free(s); return rc; }
     *out = s;
@@ -587,7 +639,7 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
             if (tiles) *tiles = (int32_t)s->csr->cblk.size();
         }
         if (s->csr->binned && !s->peer) {   // column-binned chunks (tiles = chunks)
-            if (variant) *variant = 10;
+            if (variant) *variant = s->split ? 11 : 10;
             if (tiles) *tiles = s->csr->nchunks;
         }
     } else {

@@ -45,15 +45,23 @@ def test_dist_single_rank_power_parity(kind):
         ctx.close()
 
 
-def test_dist_single_rank_allgather_exchange(monkeypatch):
-    """The all-gather exchange (in-place ncclAllGather of the row blocks) run for real on one rank."""
+@pytest.mark.parametrize("split", [False, True])
+def test_dist_single_rank_allgather_exchange(monkeypatch, split):
+    """The all-gather exchange (in-place ncclAllGather of the row blocks) run for real on one rank;
+    split: the binned shard's two-part iteration, its RCCL broadcasts on the session's own stream
+    behind events (forced binned layout, 16 KB x blocks)."""
     monkeypatch.setenv("EIGSOL_DIST_EXCHANGE", "allgather")
+    if split:
+        monkeypatch.setenv("EIGSOL_CSR_BIN", "2")
+        monkeypatch.setenv("EIGSOL_CSR_BIN_BYTES", str(16 * 1024))
+        monkeypatch.setenv("EIGSOL_CSR_BIN_LDS", "16")
     n = 20000
     rp, ci, v = S.uniform(n, 8)
     ctx = D.DistContext(0, 0, 1, D.unique_id())
     try:
         A, sess = D.sharded_power_session(ctx, rp, ci, v, n, 0)
         assert A.exchange == D.EXCHANGE_ALLGATHER
+        assert sess.kernel_info()["variant"] == (11 if split else 5)
         x0 = S.start_vector(n)
         sess.begin(E.SolverOptions(300, 1e-12), x0)
         sess.step(301)
@@ -129,20 +137,38 @@ def test_loopback_multi_rank_halo(world):
     assert all(m == D.EXCHANGE_HALO for m in modes)
 
 
-@pytest.mark.parametrize("binned", [False, True])
-def test_loopback_multi_rank_allgather(monkeypatch, binned):
+@pytest.mark.parametrize("world,layout", [(2, "sliced"), (2, "binned"), (2, "split"), (3, "split")])
+def test_loopback_multi_rank_allgather(monkeypatch, world, layout):
     """binned: the column-binned kernel on the shards (x-space columns, own rows at xoff; forced on
-    this small matrix with 32 KB x blocks), every rank's eigenvalue still bitwise identical."""
-    if binned:
+    this small matrix with 16 KB x blocks); split (the default for binned all-gather shards): every
+    iteration in two launches over the halves of the own chunks, the first half's rows exchanged
+    before the second half runs, the second launch reading the first one's decision and adding to
+    its partial.  Every rank's eigenvalue bitwise identical, oracle parity as above."""
+    if layout != "sliced":
         monkeypatch.setenv("EIGSOL_CSR_BIN", "2")
-        monkeypatch.setenv("EIGSOL_CSR_BIN_BYTES", str(32 * 1024))
+        monkeypatch.setenv("EIGSOL_CSR_BIN_BYTES", str(16 * 1024))
+        monkeypatch.setenv("EIGSOL_CSR_BIN_LDS", "16")
+    if layout == "binned":
+        monkeypatch.setenv("EIGSOL_DIST_SPLIT", "0")
     variants = []
-    modes = _loopback_run(2, "uniform", 20000, 8, exchange="allgather", monkeypatch=monkeypatch, variants=variants)
+    modes = _loopback_run(world, "uniform", 30000, 8, exchange="allgather", monkeypatch=monkeypatch,
+                          variants=variants)
     assert all(m == D.EXCHANGE_ALLGATHER for m in modes)
-    assert all(v == (10 if binned else 5) for v in variants), variants
+    assert all(v == {"sliced": 5, "binned": 10, "split": 11}[layout] for v in variants), variants
 
 
 def test_loopback_uniform_auto_exchange():
     """Unstructured columns choose the all-gather exchange by themselves (ghost counts)."""
     modes = _loopback_run(2, "uniform", 20000, 8)
     assert all(m == D.EXCHANGE_ALLGATHER for m in modes)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_loopback_uniform_split_default(world):
+    """Uniform columns at 2M rows (x = 16 MB: the binned layout by default, so every shard runs the
+    split iteration with its first half's all-gather ahead of the second half), 2/4/8 ranks against
+    the unsharded reference loop (oracle, power_method.hpp:68-96)."""
+    variants = []
+    modes = _loopback_run(world, "uniform", 2_000_000, 10, variants=variants)
+    assert all(m == D.EXCHANGE_ALLGATHER for m in modes)
+    assert all(v == 11 for v in variants), variants

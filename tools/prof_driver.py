@@ -31,6 +31,23 @@ if args.workload == "config5":
     print("done", s.kernel_info())
     s.close(); A.close(); ctx.close()
     sys.exit(0)
+if args.workload == "gmres1m":
+    # general-sparse shifted inverse (ILU(0) + GMRES) on config 5's matrix made non-triangular
+    import numpy as np
+    n = 1_000_000
+    rp, ci, v, _ = S.general_complex(n, 16)
+    ctx = E.Context(0)
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 1.5 * np.exp(0.7j) + 1e-3
+    s = E.ShiftedSession(A, sigma)
+    s.begin(E.ShiftedSolverOptions(1000, 1e-12, sigma), S.start_vector(n, np.complex128))
+    done = False
+    while not done:
+        s.step(1)
+        done = s.query()[0]
+    print("done", s.finish().iterations, s.kernel_info())
+    s.close(); A.close(); ctx.close()
+    sys.exit(0)
 if args.workload == "dense16384":
     # dense power iteration (GEMV) on a 16384^2 f64 matrix (dense_kernel)
     import numpy as np
