@@ -297,9 +297,12 @@ class PowerSession:
                  9: "csr_kernel column-block passes (x blocks L2-resident; tiles = blocks)",
                  10: "csr_bin_kernel (column-binned row chunks, row sums in LDS; tiles = chunks)",
                  11: "csr_bin_kernel in two row halves per iteration, the first half's all-gather "
-                     "overlapped with the second half (row-sharded; tiles = chunks)"}
+                     "overlapped with the second half (row-sharded; tiles = chunks)",
+                 12: "sptrsv pair kernel (sync-free triangular solve, two iterations per launch: the second "
+                     "solve one wave round behind the first)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
-                "variant": v.value, "kernel": names.get(v.value, "?")}
+                "variant": v.value, "kernel": names.get(v.value, "?"),
+                "iterations_per_launch": 2 if v.value == 12 else 1}
 
     def kernel_name(self) -> str:
         """Demangled name of the per-iteration kernel (CSR power sessions), as rocprofv3 reports it."""

@@ -83,6 +83,15 @@ struct ShiftFactor {
     int32_t chunk0 = 0;
     int poll_fast = 0;            // tail polls without back-off (EIGSOL_TRSV_POLL_FAST)
     int poll_mode = 0;            // EIGSOL_TRSV_POLL_MODE
+    // pair launches (sptrsv_chunk_pair_kernel; EIGSOL_TRSV_PAIR=0 disables): two iterations per
+    // launch, the second solve one wave round behind the first
+    int pair = 0;
+    int grid_pair = 0;
+    void* aux = nullptr;          // w1 of the pair launch (n scalars)
+    void* z2[2] = {nullptr, nullptr};   // the second solve's polled values
+    int32_t epoch2 = 0;
+    void* pair_part = nullptr;    // part4: {||w2||^2, w1^H w2}
+    void* pair_blk = nullptr;     // part4 per block of the pair partials reduction
     uint32_t* work = nullptr;     // [2]: last-arriver ticket of the partials reduction
     int32_t* err = nullptr;
     void* wave_part = nullptr;    // part4 per wave
@@ -154,7 +163,19 @@ struct TriArgs {
     part4* my_part;
     S* trace;
     double sig_re, sig_im;
+    // pair launches
+    S* aux;             // w1
+    S* z2cur;           // the second solve's polled values
+    S* z2next;
+    part4* pair2;       // {||w2||^2, w1^H w2}
+    part4* pair_blk;
 };
+
+// multiplication by an exact power of two (the pair launch's scaling of w1)
+__device__ __forceinline__ double scale_r(double v, double s) { return v * s; }
+__device__ __forceinline__ cplx scale_r(cplx v, double s) { return cplx{v.re * s, v.im * s}; }
+__device__ __forceinline__ float scale_r(float v, double s) { return v * (float)s; }
+__device__ __forceinline__ cplxf scale_r(cplxf v, double s) { return cplxf{v.re * (float)s, v.im * (float)s}; }
 
 __device__ __forceinline__ void st_coh(double* p, double v) { st_agent(p, v); }
 __device__ __forceinline__ void st_coh(cplx* p, cplx v) {
@@ -174,6 +195,41 @@ __device__ __forceinline__ float ld_coh(const float* p) {
 __device__ __forceinline__ cplxf ld_coh(const cplxf* p) { return cplxf{ld_coh(&p->re), ld_coh(&p->im)}; }
 __device__ __forceinline__ double ld_coh(const double* p) { return ld_agent(p); }
 __device__ __forceinline__ cplx ld_coh(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
+
+// Indexed coherent access to a solve buffer (uniform base, element index): complex values move as
+// ONE device-coherent (sc1) buffer load / store of 16 (8) bytes instead of two 8 (4) byte atomics,
+// which halves the dependency polls' memory requests.  A torn read (one half still the sentinel)
+// is simply unready: both halves are checked.  Buffer offsets are 32-bit (solve buffers < 4 GiB).
+constexpr int kBufSc1 = 16;   // buffer cache policy: sc1 (device scope), as the agent-scope atomics use
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, -1, 0x00020000);
+}
+template <class S>
+__device__ __forceinline__ S ld_cohi(const S* base, int j) {
+    if constexpr (std::is_same_v<S, cplx>) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(coh_rsrc(base), (uint32_t)j * 16u, 0, kBufSc1);
+        return __builtin_bit_cast(cplx, v);
+    } else if constexpr (std::is_same_v<S, cplxf>) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(coh_rsrc(base), (uint32_t)j * 8u, 0, kBufSc1);
+        return __builtin_bit_cast(cplxf, v);
+    } else {
+        return ld_coh(base + j);
+    }
+}
+template <class S>
+__device__ __forceinline__ void st_cohi(S* base, int i, S v) {
+    if constexpr (std::is_same_v<S, cplx>) {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), coh_rsrc(base), (uint32_t)i * 16u, 0,
+                                               kBufSc1);
+    } else if constexpr (std::is_same_v<S, cplxf>) {
+        typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), coh_rsrc(base), (uint32_t)i * 8u, 0,
+                                              kBufSc1);
+    } else {
+        st_coh(base + i, v);
+    }
+}
 
 __device__ __forceinline__ int ld_flag_err(const int32_t* p) {
     return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -252,7 +308,7 @@ __device__ __forceinline__ cplxf group_sum(cplxf v) { return cplxf{group_sum(v.r
 // poll z[j] until solved (bounded; a broken wait sets the sticky error word and gives up)
 template <class S>
 __device__ __forceinline__ S wait_value(const S* z, int j, int32_t* err) {
-    S y = ld_coh(z + j);
+    S y = ld_cohi(z, j);
     int spins = 0;
     while (unready(y)) {
         // back off, exponentially: a wave far ahead of the dependency frontier must leave the
@@ -260,7 +316,7 @@ __device__ __forceinline__ S wait_value(const S* z, int j, int32_t* err) {
         if (spins < 4) __builtin_amdgcn_s_sleep(2);
         else if (spins < 16) __builtin_amdgcn_s_sleep(8);
         else __builtin_amdgcn_s_sleep(32);
-        y = ld_coh(z + j);
+        y = ld_cohi(z, j);
         if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(err) != 0)) {
             atomicOr(err, 1);
             break;
@@ -377,20 +433,28 @@ __device__ __forceinline__ float quad_sum(float v) {
 __device__ __forceinline__ cplx quad_sum(cplx v) { return cplx{quad_sum(v.re), quad_sum(v.im)}; }
 __device__ __forceinline__ cplxf quad_sum(cplxf v) { return cplxf{quad_sum(v.re), quad_sum(v.im)}; }
 
-template <class S, bool kIter>
+// kPair: the pair launch's head (shift_pair_prologue): the head is solved twice from LDS, the
+// second time on s * (the first solution), published to z2cur and B[parity].
+template <class S, bool kIter, bool kPair = false>
 __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> a, int parity) {
     extern __shared__ __align__(16) unsigned char head_lds[];
     S* zl = reinterpret_cast<S*>(head_lds);
     __shared__ Prologue pro;
     const S* xin;
     S* yout;
-    double nrm = 0.0;
+    S* yout2 = nullptr;
+    double nrm = 0.0, s2 = 1.0;
     if constexpr (kIter) {
-        shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if constexpr (kPair)
+            shift_pair_prologue<S>(a.ctl, a.rank_part, a.pair2, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        else
+            shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
         if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // the tail kernel resets z
         nrm = pro.nrm;
+        s2 = pro.s;
         xin = parity ? a.buf0 : a.buf1;
-        yout = parity ? a.buf1 : a.buf0;
+        yout = kPair ? a.aux : (parity ? a.buf1 : a.buf0);
+        yout2 = parity ? a.buf1 : a.buf0;
     } else {
         xin = a.b_plain;
         yout = a.y_plain;
@@ -420,6 +484,7 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
     }
     if (tid == 0) zl[a.hpos] = s_zero<S>();
     __syncthreads();
+  for (int rep = 0; rep < (kPair ? 2 : 1); ++rep) {
     if (tid < 64) {
         const int lane = tid, grp = lane >> 2, slot = lane & 3;
         const int nw = a.nwpass;
@@ -454,14 +519,20 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
     }
     __syncthreads();
     // publish: the tail kernel (next in stream order) reads these through z
+    S* zc = rep ? a.z2cur : a.zcur;
+    S* zn = rep ? a.z2next : a.znext;
+    S* yo = rep ? yout2 : yout;
     for (int p = tid; p < a.hpos; p += kWHeadThreads) {
         const int i = a.order[p];
         if (i < 0) continue;
         const S yi = sanitize(zl[p]);
-        a.zcur[i] = yi;
-        yout[i] = yi;
-        a.znext[i] = sentinel<S>();
+        zc[i] = yi;
+        yo[i] = yi;
+        zn[i] = sentinel<S>();
+        if (kPair && rep == 0) zl[p] = scale_r(yi, s2);   // the second solve's right-hand side
     }
+    if (kPair && rep == 0) __syncthreads();
+  }
 }
 
 // first poll of a dependency is issued early (ld_coh); this finishes the wait
@@ -473,7 +544,7 @@ __device__ __forceinline__ S finish_wait(S y, const S* z, int j, int32_t* err, i
         else if (spins < fast + 4) __builtin_amdgcn_s_sleep(2);
         else if (spins < fast + 16) __builtin_amdgcn_s_sleep(8);
         else __builtin_amdgcn_s_sleep(32);
-        y = ld_coh(z + j);
+        y = ld_cohi(z, j);
         if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(err) != 0)) {
             atomicOr(err, 1);
             break;
@@ -682,7 +753,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
             S bi = m.bi;
             if constexpr (kIter) bi = scale_in(bi, nrm);
             const S yi = sanitize(sdiv(sub(bi, acc), m.pv));
-            st_coh(a.zcur + m.i, yi);        // publish: readers poll this very word
+            st_cohi(a.zcur, m.i, yi);        // publish: readers poll this very word
             yout[m.i] = yi;
             a.znext[m.i] = sentinel<S>();
         }
@@ -695,8 +766,8 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
     fetch2(c1);
     fetch1(gw + 2 * W, n0);
     fetch1(gw + 3 * W, n1);
-    S z0 = c0.j >= 0 ? ld_coh(a.zcur + c0.j) : s_zero<S>();
-    S z1 = c1.j >= 0 ? ld_coh(a.zcur + c1.j) : s_zero<S>();
+    S z0 = c0.j >= 0 ? ld_cohi(a.zcur, c0.j) : s_zero<S>();
+    S z1 = c1.j >= 0 ? ld_cohi(a.zcur, c1.j) : s_zero<S>();
     for (int c = gw; c < a.nchunks; c += 2 * W) {
         fetch2(n0);
         fetch2(n1);
@@ -705,13 +776,292 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
         fetch1(c + 5 * W, m1);
         solve(c0, z0);
         solve(c1, z1);
-        z0 = n0.j >= 0 ? ld_coh(a.zcur + n0.j) : s_zero<S>();
-        z1 = n1.j >= 0 ? ld_coh(a.zcur + n1.j) : s_zero<S>();
+        z0 = n0.j >= 0 ? ld_cohi(a.zcur, n0.j) : s_zero<S>();
+        z1 = n1.j >= 0 ? ld_cohi(a.zcur, n1.j) : s_zero<S>();
         c0 = n0;
         c1 = n1;
         n0 = m0;
         n1 = m1;
     }
+}
+
+// ---- tail of a pair launch (shift_pair_prologue): the chunk schedule above solving two systems
+// at once.  A wave solves its chunks of round r for w1 (as sptrsv_chunk_kernel does), then its
+// chunks of round r - 1 for w2 = (A - sigma I)^{-1} (s w1): the second solve reuses the row
+// metadata and entries the wave loaded for the first one a round earlier (the matrix is read once
+// for both solves), and its right-hand side s w1_i is the wave's own result of that round, still
+// in registers.  Its dependencies are the second solve's values of lower positions, polled in
+// z2cur.  No deadlock: first solves never wait on second ones, and every wave takes its second
+// solves in increasing position order, each after its own first solve of the same chunk.
+// A level of the first solve costs what it costs alone; the second trails it by one round, so a
+// launch costs about one solve plus one round, for two reference iterations.
+template <class S>
+__global__ __launch_bounds__(kThreads) void sptrsv_chunk_pair_kernel(TriArgs<S> a, int parity) {
+    __shared__ Prologue pro;
+    shift_pair_prologue<S>(a.ctl, a.rank_part, a.pair2, parity, a.trace, a.sig_re, a.sig_im, &pro);
+    if (!__builtin_amdgcn_readfirstlane(pro.go)) {
+        for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < a.n; r += (int64_t)gridDim.x * kThreads) {
+            a.znext[r] = sentinel<S>();
+            a.z2next[r] = sentinel<S>();
+        }
+        return;
+    }
+    const double nrm = pro.nrm, s2 = pro.s;
+    const S* xin = parity ? a.buf0 : a.buf1;
+    S* w1out = a.aux;
+    S* w2out = parity ? a.buf1 : a.buf0;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kRowLanes - 1);
+    const int grp = (tid & 63) / kRowLanes;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W = gridDim.x * kWaves;
+    const int gw = a.chunk0 + wave * gridDim.x + blockIdx.x;
+
+    auto fetch1 = [&](int c, RowMeta<S>& m) {
+        const bool in = c < a.nchunks;
+        const int pos = (in ? c : 0) * kWaveRows + grp;
+        m.i = in ? a.porder[pos] : -1;
+        const int e0 = a.pptr[pos];
+        m.e0 = e0;
+        m.len = in ? a.pptr[pos + 1] - e0 : 0;
+        m.pv = ldg_stream(a.ppiv, (uint32_t)pos);
+    };
+    auto fetch2 = [&](RowMeta<S>& m) {
+        const bool ok = lane < m.len;
+        const int e = ok ? m.e0 + lane : 0;
+        m.j = ok ? (int)ldg_stream(a.pcol, (uint32_t)e) : -1;
+        m.v = ldg_stream(a.pval, (uint32_t)e);
+        m.bi = xin[m.i >= 0 ? m.i : 0];
+    };
+    // first solve: returns w1_i in every lane of the row's group
+    auto solve1 = [&](const RowMeta<S>& m, S z0) -> S {
+        S acc = s_zero<S>();
+        if (m.j >= 0) acc = mul(m.v, finish_wait(z0, a.zcur, m.j, a.err, a.poll_fast));
+        for (int k = lane + kRowLanes; k < m.len; k += kRowLanes) {
+            const int e = m.e0 + k;
+            acc = add(acc, mul(a.pval[e], wait_value(a.zcur, a.pcol[e], a.err)));
+        }
+        acc = group_sum(acc);
+        const S yi = sanitize(sdiv(sub(scale_in(m.bi, nrm), acc), m.pv));
+        if (m.i >= 0 && lane == 0) {
+            st_cohi(a.zcur, m.i, yi);
+            w1out[m.i] = yi;
+            a.znext[m.i] = sentinel<S>();
+        }
+        return yi;
+    };
+    auto solve2 = [&](const RowMeta<S>& m, S u0, S rhs) {
+        S acc = s_zero<S>();
+        if (m.j >= 0) acc = mul(m.v, finish_wait(u0, a.z2cur, m.j, a.err, a.poll_fast));
+        for (int k = lane + kRowLanes; k < m.len; k += kRowLanes) {
+            const int e = m.e0 + k;
+            acc = add(acc, mul(a.pval[e], wait_value(a.z2cur, a.pcol[e], a.err)));
+        }
+        acc = group_sum(acc);
+        if (m.i >= 0 && lane == 0) {
+            const S yi = sanitize(sdiv(sub(rhs, acc), m.pv));
+            st_cohi(a.z2cur, m.i, yi);
+            w2out[m.i] = yi;
+            a.z2next[m.i] = sentinel<S>();
+        }
+    };
+
+    RowMeta<S> c0, c1, n0, n1, q0, q1;
+    q0.i = q1.i = -1;
+    q0.j = q1.j = -1;
+    q0.e0 = q1.e0 = 0;
+    q0.len = q1.len = 0;
+    q0.v = q1.v = q0.bi = q1.bi = q0.pv = q1.pv = s_zero<S>();
+    S r0 = s_zero<S>(), r1 = s_zero<S>();
+    fetch1(gw, c0);
+    fetch1(gw + W, c1);
+    fetch2(c0);
+    fetch2(c1);
+    fetch1(gw + 2 * W, n0);
+    fetch1(gw + 3 * W, n1);
+    S z0 = c0.j >= 0 ? ld_cohi(a.zcur, c0.j) : s_zero<S>();
+    S z1 = c1.j >= 0 ? ld_cohi(a.zcur, c1.j) : s_zero<S>();
+    for (int c = gw; c < a.nchunks; c += 2 * W) {
+        fetch2(n0);
+        fetch2(n1);
+        RowMeta<S> m0, m1;
+        fetch1(c + 4 * W, m0);
+        fetch1(c + 5 * W, m1);
+        // the second solve's first polls, issued before the first solve waits
+        S u0 = q0.j >= 0 ? ld_cohi(a.z2cur, q0.j) : s_zero<S>();
+        S u1 = q1.j >= 0 ? ld_cohi(a.z2cur, q1.j) : s_zero<S>();
+        const S y0 = solve1(c0, z0);
+        const S y1 = solve1(c1, z1);
+        solve2(q0, u0, r0);
+        solve2(q1, u1, r1);
+        q0 = c0;
+        q1 = c1;
+        r0 = scale_r(y0, s2);
+        r1 = scale_r(y1, s2);
+        z0 = n0.j >= 0 ? ld_cohi(a.zcur, n0.j) : s_zero<S>();
+        z1 = n1.j >= 0 ? ld_cohi(a.zcur, n1.j) : s_zero<S>();
+        c0 = n0;
+        c1 = n1;
+        n0 = m0;
+        n1 = m1;
+    }
+    {
+        S u0 = q0.j >= 0 ? ld_cohi(a.z2cur, q0.j) : s_zero<S>();
+        S u1 = q1.j >= 0 ? ld_cohi(a.z2cur, q1.j) : s_zero<S>();
+        solve2(q0, u0, r0);
+        solve2(q1, u1, r1);
+    }
+}
+
+// ---- tail of a pair launch, role split: the grid is two copies of the single-solve grid.  Blocks
+// [0, G) run sptrsv_chunk_kernel's schedule for w1; blocks [G, 2G) run the same schedule for
+// w2 = (A - sigma I)^{-1} (s w1), taking each row's right-hand side s w1_i from the first solve's
+// polled value (its ready flag) and their dependencies from z2cur.  A wave of either solve waits
+// only on its own solve's chains, so the second solve trails the first by about one dependency
+// round trip instead of adding its own chain waits to the first solve's waves (the interleaved
+// schedule above: 0.69 ms per iteration on config 5 against 0.83 for one solve per launch).
+// The matrix is read once per solve.  No deadlock: first-solve waves never wait on the second
+// solve, and every wave is resident (cooperative launch).
+template <class S>
+__global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> a, int parity) {
+    __shared__ Prologue pro;
+    shift_pair_prologue<S>(a.ctl, a.rank_part, a.pair2, parity, a.trace, a.sig_re, a.sig_im, &pro);
+    if (!__builtin_amdgcn_readfirstlane(pro.go)) {
+        for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < a.n; r += (int64_t)gridDim.x * kThreads) {
+            a.znext[r] = sentinel<S>();
+            a.z2next[r] = sentinel<S>();
+        }
+        return;
+    }
+    const int G = (int)gridDim.x / 2;
+    const int role = __builtin_amdgcn_readfirstlane((int)blockIdx.x >= G ? 1 : 0);
+    const int blk = (int)blockIdx.x - role * G;
+    const double nrm = pro.nrm, s2 = pro.s;
+    const S* xin = parity ? a.buf0 : a.buf1;
+    S* yout = role ? (parity ? a.buf1 : a.buf0) : a.aux;
+    S* zdep = role ? a.z2cur : a.zcur;      // dependencies and publication
+    S* zn = role ? a.z2next : a.znext;
+    const int tid = threadIdx.x;
+    const int lane = tid & (kRowLanes - 1);
+    const int grp = (tid & 63) / kRowLanes;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W = G * kWaves;
+    const int gw = a.chunk0 + wave * G + blk;
+
+    auto fetch1 = [&](int c, RowMeta<S>& m) {
+        const bool in = c < a.nchunks;
+        const int pos = (in ? c : 0) * kWaveRows + grp;
+        m.i = in ? a.porder[pos] : -1;
+        const int e0 = a.pptr[pos];
+        m.e0 = e0;
+        m.len = in ? a.pptr[pos + 1] - e0 : 0;
+        m.pv = ldg_stream(a.ppiv, (uint32_t)pos);
+    };
+    auto fetch2 = [&](RowMeta<S>& m) {
+        const bool ok = lane < m.len;
+        const int e = ok ? m.e0 + lane : 0;
+        m.j = ok ? (int)ldg_stream(a.pcol, (uint32_t)e) : -1;
+        m.v = ldg_stream(a.pval, (uint32_t)e);
+        // second solve: the first solve's value of the row, possibly not yet solved (polled below)
+        m.bi = role ? ld_cohi(a.zcur, (m.i >= 0 ? m.i : (int)a.n)) : xin[m.i >= 0 ? m.i : 0];
+    };
+    auto solve = [&](const RowMeta<S>& m, S z0) {
+        S acc = s_zero<S>();
+        S bv = m.bi;
+        if (role) {
+            // the dependency and (lane 0) the first solve's value of the row are polled in the same
+            // loop: waiting for them one after the other would add a round trip to every level
+            const bool nb = lane == 0 && m.i >= 0;
+            S zv = m.j >= 0 ? z0 : s_zero<S>();
+            int spins = 0;
+            while (unready(zv) || (nb && unready(bv))) {
+                if (spins < 4) __builtin_amdgcn_s_sleep(2);
+                else if (spins < 16) __builtin_amdgcn_s_sleep(8);
+                else __builtin_amdgcn_s_sleep(32);
+                if (unready(zv)) zv = ld_cohi(zdep, m.j);
+                if (nb && unready(bv)) bv = ld_cohi(a.zcur, m.i);
+                if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(a.err) != 0)) {
+                    atomicOr(a.err, 1);
+                    break;
+                }
+            }
+            if (m.j >= 0) acc = mul(m.v, zv);
+        } else if (m.j >= 0) {
+            acc = mul(m.v, finish_wait(z0, zdep, m.j, a.err, a.poll_fast));
+        }
+        for (int k = lane + kRowLanes; k < m.len; k += kRowLanes) {
+            const int e = m.e0 + k;
+            acc = add(acc, mul(a.pval[e], wait_value(zdep, a.pcol[e], a.err)));
+        }
+        acc = group_sum(acc);
+        if (m.i >= 0 && lane == 0) {
+            S bi;
+            if (role) bi = scale_r(bv, s2);
+            else bi = scale_in(m.bi, nrm);
+            const S yi = sanitize(sdiv(sub(bi, acc), m.pv));
+            st_cohi(zdep, m.i, yi);
+            yout[m.i] = yi;
+            zn[m.i] = sentinel<S>();
+        }
+    };
+
+    RowMeta<S> c0, c1, n0, n1;
+    fetch1(gw, c0);
+    fetch1(gw + W, c1);
+    fetch2(c0);
+    fetch2(c1);
+    fetch1(gw + 2 * W, n0);
+    fetch1(gw + 3 * W, n1);
+    S z0 = c0.j >= 0 ? ld_cohi(zdep, c0.j) : s_zero<S>();
+    S z1 = c1.j >= 0 ? ld_cohi(zdep, c1.j) : s_zero<S>();
+    for (int c = gw; c < a.nchunks; c += 2 * W) {
+        fetch2(n0);
+        fetch2(n1);
+        RowMeta<S> m0, m1;
+        fetch1(c + 4 * W, m0);
+        fetch1(c + 5 * W, m1);
+        solve(c0, z0);
+        solve(c1, z1);
+        z0 = n0.j >= 0 ? ld_cohi(zdep, n0.j) : s_zero<S>();
+        z1 = n1.j >= 0 ? ld_cohi(zdep, n1.j) : s_zero<S>();
+        c0 = n0;
+        c1 = n1;
+        n0 = m0;
+        n1 = m1;
+    }
+}
+
+// Partials of a pair launch: {||w1||^2, x^H w1} -> my_part, {||w2||^2, w1^H w2} -> pair2, each in
+// a fixed order (grid-stride per thread, block sums, last-arriver sum in block order).
+template <class S>
+__global__ __launch_bounds__(kThreads) void shift_pair_part_kernel(TriArgs<S> a, int parity) {
+    __shared__ double sm[3 * kWaves];
+    __shared__ int s_last, s_last2;
+    __shared__ int s_go;
+    __shared__ double s_nrm;
+    if (threadIdx.x == 0) {
+        s_go = __hip_atomic_load(&a.ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 0 : 1;
+        s_nrm = a.ctl->st[parity ^ 1].nrm;
+    }
+    __syncthreads();
+    if (!s_go) return;
+    const double nrm = s_nrm;
+    const S* xin = parity ? a.buf0 : a.buf1;
+    const S* w1 = a.aux;
+    const S* w2 = parity ? a.buf1 : a.buf0;
+    double n21 = 0.0, pr = 0.0, pi = 0.0, n22 = 0.0, qr = 0.0, qi = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kThreads) {
+        const S y1 = w1[i];
+        const S y2 = w2[i];
+        n21 += sq_abs(y1);
+        acc_dot(pr, pi, scale_in(xin[i], nrm), y1);
+        n22 += sq_abs(y2);
+        acc_dot(qr, qi, y1, y2);
+    }
+    block_sum3(n21, pr, pi, sm);
+    last_arriver_reduce(n21, pr, pi, a.wave_part, a.work + 2, a.my_part, sm, &s_last);
+    block_sum3(n22, qr, qi, sm);
+    last_arriver_reduce(n22, qr, qi, a.pair_blk, a.work + 3, a.pair2, sm, &s_last2);
 }
 
 // GMRES path: the launch prologue alone (the stop decision and ||y_{t-1}||), the solve follows on
@@ -1241,7 +1591,8 @@ static void shift_free(ShiftFactor* f) {
                     f->tpiv, (void*)f->tcol, f->tval, (void*)f->porder, (void*)f->pptr, (void*)f->pcol, f->pval,
                     f->ppiv,
                     (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
-                    (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf})
+                    (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf,
+                    f->aux, f->z2[0], f->z2[1], f->pair_part, f->pair_blk})
         if (p) hipFree(p);
     ctx_release(f->ctx);
     delete f;
@@ -1835,6 +2186,31 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
     f->grid = std::min(f->grid, per_cu * f->ctx->num_cus);
     const int64_t units = f->tail_chunks ? (int64_t)f->nchunks - f->chunk0 : f->nslices;
     f->grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid, (units + dev::kWaves - 1) / dev::kWaves));
+    // pair launches: chunk tail with the one-wave head (or none); EIGSOL_TRSV_PAIR=0 disables
+    // (1: interleaved schedule, sptrsv_chunk_pair_kernel; 2: role split, sptrsv_chunk_role_kernel,
+    // when twice the single grid is resident; EIGSOL_TRSV_PAIR=1|2 forces one)
+    if (rc == EIGSOL_OK && f->tail_chunks && (f->hpos == 0 || f->wave_head)) {
+        const char* e = std::getenv("EIGSOL_TRSV_PAIR");
+        const int want = e ? std::atoi(e) : 2;
+        int per_cu_pair = 0, per_cu_role = 0;
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu_role, reinterpret_cast<const void*>(dev::sptrsv_chunk_role_kernel<S>), dev::kThreads, 0);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu_pair, reinterpret_cast<const void*>(dev::sptrsv_chunk_pair_kernel<S>), dev::kThreads, 0);
+        // role split: one block per CU per solve by default (config 5: 0.539 ms per iteration
+        // against 0.555 with two, the single-solve optimum; the two solves' polls share the
+        // memory system); EIGSOL_TRSV_PAIR_BLOCKS_PER_CU overrides
+        int role_per_cu = 1;
+        if (const char* env = std::getenv("EIGSOL_TRSV_PAIR_BLOCKS_PER_CU")) role_per_cu = std::max(1, std::atoi(env));
+        const int gr = std::min(f->grid, role_per_cu * f->ctx->num_cus);
+        if (want == 2 && per_cu_role * f->ctx->num_cus >= 2 * gr) {
+            f->pair = 2;
+            f->grid_pair = 2 * gr;
+        } else if (want >= 1 && per_cu_pair >= 1) {
+            f->pair = 1;
+            f->grid_pair = std::min(f->grid, per_cu_pair * f->ctx->num_cus);
+        }
+    }
     f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
                                                                   std::min<int64_t>(1024, (n + 1023) / 1024)));
     if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), (size_t)f->hpos * 4);
@@ -1918,6 +2294,28 @@ int shift_error(ShiftFactor* f) {
     return EIGSOL_OK;
 }
 
+// buffers of the pair launches, allocated by the first iteration launch (plain solves, e.g. the
+// GMRES path's ILU(0) factors, never need them)
+template <class S>
+static int pair_alloc(ShiftFactor* f) {
+    if (f->aux) return EIGSOL_OK;
+    hipStream_t st = f->ctx->stream;
+    const int64_t n = f->n;
+    EIGSOL_HIP(hipMalloc(&f->aux, (size_t)std::max<int64_t>(n, 1) * sizeof(S)));
+    for (void*& zb : f->z2) {
+        EIGSOL_HIP(hipMalloc(&zb, (size_t)(n + 1) * sizeof(S)));
+        const uint32_t sent = (uint32_t)(dev::kSent & 0xffffffffu);
+        EIGSOL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st));
+        EIGSOL_HIP(hipMemsetAsync(static_cast<char*>(zb) + n * sizeof(S), 0, sizeof(S), st));
+    }
+    EIGSOL_HIP(hipMalloc(&f->pair_part, sizeof(dev::part4)));
+    EIGSOL_HIP(hipMemsetAsync(f->pair_part, 0, sizeof(dev::part4), st));
+    EIGSOL_HIP(hipMalloc(&f->pair_blk, (size_t)std::max(1, f->red_grid) * sizeof(dev::part4)));
+    return EIGSOL_OK;
+}
+
+void* shift_aux(const ShiftFactor* f) { return f->aux; }
+
 template <class S>
 static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, void* buf0, void* buf1,
                           PowerCtl* ctl, const void* rank_part, void* my_part, void* trace, int parity) {
@@ -1997,7 +2395,23 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.wrp = static_cast<const S*>(f->wrp);
         a.wdst = f->wdst;
         a.nwpass = f->nwpass;
-        if (f->hpos > 0 && f->wave_head) {
+        const bool pair = iter && f->pair;
+        if (pair) {
+            EIGSOL_TRY(pair_alloc<S>(f));
+            const int e2 = ++f->epoch2;
+            a.z2cur = static_cast<S*>(f->z2[e2 & 1]);
+            a.z2next = static_cast<S*>(f->z2[(e2 + 1) & 1]);
+            a.aux = static_cast<S*>(f->aux);
+            a.pair2 = static_cast<dev::part4*>(f->pair_part);
+            a.pair_blk = static_cast<dev::part4*>(f->pair_blk);
+        }
+        if (f->hpos > 0 && f->wave_head && pair) {
+            const size_t wl = (size_t)(f->hpos + 1) * sizeof(S);
+            const void* hk = reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, true, true>);
+            EIGSOL_HIP(hipFuncSetAttribute(hk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wl));
+            hipLaunchKernelGGL((dev::sptrsv_whead_kernel<S, true, true>), dim3(1), dim3(dev::kWHeadThreads), wl, st, a,
+                               parity);
+        } else if (f->hpos > 0 && f->wave_head) {
             const size_t wl = (size_t)(f->hpos + 1) * sizeof(S);
             const void* hk = iter ? reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, true>)
                                   : reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, false>);
@@ -2028,17 +2442,23 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.ppiv = static_cast<const S*>(f->ppiv);
         a.chunk0 = f->chunk0;
         a.nchunks = f->nchunks;
-        const void* tk = !f->tail_chunks ? slice_kernel_ptr<S>(f->slice_b, iter)
+        const void* tk = (pair && f->pair == 2) ? reinterpret_cast<const void*>(dev::sptrsv_chunk_role_kernel<S>)
+                         : pair ? reinterpret_cast<const void*>(dev::sptrsv_chunk_pair_kernel<S>)
+                         : !f->tail_chunks ? slice_kernel_ptr<S>(f->slice_b, iter)
                          : iter ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>)
                                 : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, false>);
+        const int tgrid = pair ? f->grid_pair : f->grid;
         // EIGSOL_TRSV_NO_COOP=1: the same kernel through an ordinary launch, for profiling only
         // (rocprofv3 7.2 segfaults in its exit-time finaliser after any cooperative launch,
         // tools/coop_prof_repro.hip); the grid is one residency round, so on an otherwise idle
         // device every wave is resident anyway
         static const bool no_coop = std::getenv("EIGSOL_TRSV_NO_COOP") != nullptr;
-        if (no_coop) EIGSOL_HIP(hipLaunchKernel(tk, dim3(f->grid), dim3(dev::kThreads), kargs, 0, st));
-        else EIGSOL_HIP(hipLaunchCooperativeKernel(tk, dim3(f->grid), dim3(dev::kThreads), kargs, 0, st));
-        if (iter)
+        if (no_coop) EIGSOL_HIP(hipLaunchKernel(tk, dim3(tgrid), dim3(dev::kThreads), kargs, 0, st));
+        else EIGSOL_HIP(hipLaunchCooperativeKernel(tk, dim3(tgrid), dim3(dev::kThreads), kargs, 0, st));
+        if (pair)
+            hipLaunchKernelGGL((dev::shift_pair_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a,
+                               parity);
+        else if (iter)
             hipLaunchKernelGGL((dev::shift_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a, parity);
     } else if constexpr (!kDenseLU<S>) {
         return fail(EIGSOL_E_UNSUPPORTED, "single-precision dense factor");
@@ -2129,7 +2549,7 @@ void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* 
         if (variant) *variant = 8;
     } else if (f->kind == 0) {
         if (bytes) *bytes = (sb + 4.0) * (double)f->nnz_total + 4.0 * (n + 1.0) + 2.0 * sb * n;
-        if (variant) *variant = 3;
+        if (variant) *variant = f->pair ? 12 : 3;   // 12: two iterations per launch
         if (tiles) *tiles = f->nlevels;
     } else {
         if (bytes) *bytes = sb * n * n + 2.0 * sb * n;

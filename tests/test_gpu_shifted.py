@@ -129,8 +129,80 @@ def test_triu_complex_parity_config5_class(ctx):
     m = min(len(tr), len(ref["trace"]))
     np.testing.assert_allclose(tr[:m], ref["trace"][:m], rtol=1e-9)
     info = sess.kernel_info()
-    assert info["variant"] == 3 and info["tiles"] > 1
+    assert info["variant"] in (3, 12) and info["tiles"] > 1
     sess.close()
+
+
+def _triu_run(ctx, monkeypatch, pair, n, x0, opts, sigma, seed=42, trace=64):
+    monkeypatch.setenv("EIGSOL_TRSV_PAIR", str(int(pair)))
+    rp, ci, v, _ = S.triu_complex(n, 16, seed=seed)
+    M = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sess = E.ShiftedSession(M, sigma, trace_capacity=trace)
+    assert sess.kernel_info()["variant"] == (12 if pair else 3)
+    sess.begin(opts, x0)
+    sess.step(400)
+    assert sess.query()[0]
+    res = sess.finish()
+    tr = sess.trace(trace)
+    sess.close()
+    M.close()
+    return res, tr
+
+
+@pytest.mark.parametrize("mode", [1, 2])   # 1 interleaved schedule, 2 role split
+def test_pair_launches_match_single_launches(ctx, monkeypatch, mode):
+    """Pair launches (two reference iterations per launch, the second solve on the unnormalised
+    first solution, shift_pair_prologue) against one iteration per launch: the same iteration
+    count, every Rayleigh quotient of the trace within 1e-12 relative (the second solve differs
+    from the reference's only by where the division by ||y|| is rounded), the same eigenvector."""
+    n = 20000
+    target = 1.5 * np.exp(0.7j)
+    sigma = target + 1e-3
+    x0 = S.start_vector(n, np.complex128)
+    opts = E.ShiftedSolverOptions(200, 1e-12, sigma)
+    single, ts = _triu_run(ctx, monkeypatch, False, n, x0, opts, sigma)
+    pair, tp = _triu_run(ctx, monkeypatch, mode, n, x0, opts, sigma)
+    assert pair.converged and single.converged
+    assert pair.iterations == single.iterations
+    assert len(tp) == len(ts) == single.iterations
+    np.testing.assert_allclose(tp, ts, rtol=1e-12)
+    assert abs(pair.eigenvalue - single.eigenvalue) <= 1e-12 * abs(single.eigenvalue)
+    assert abs(np.vdot(pair.eigenvector, single.eigenvector)) >= 1 - 1e-12
+    assert abs(np.linalg.norm(pair.eigenvector) - 1) <= 1e-12
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("max_iter", [1, 2, 3, 4])
+def test_pair_launches_stop_at_max_iterations(ctx, monkeypatch, max_iter, mode):
+    """The loop bound (shifted_inverse_power_solver.hpp:48) falls on either solve of a pair:
+    odd counts end on the first solve (the factor's w1 buffer holds x), even ones on the second."""
+    n = 3000
+    sigma = 0.2 + 0.1j
+    x0 = S.start_vector(n, np.complex128, seed=4)
+    opts = E.ShiftedSolverOptions(max_iter, 1e-15, sigma)
+    single, ts = _triu_run(ctx, monkeypatch, False, n, x0, opts, sigma, seed=4)
+    pair, tp = _triu_run(ctx, monkeypatch, mode, n, x0, opts, sigma, seed=4)
+    assert pair.iterations == single.iterations == max_iter
+    assert not pair.converged and not single.converged
+    np.testing.assert_allclose(tp, ts, rtol=1e-12)
+    assert abs(np.vdot(pair.eigenvector, single.eigenvector)) >= 1 - 1e-12
+    rp, ci, v, _ = S.triu_complex(n, 16, seed=4)
+    ref = O.shifted_triu_csr(rp, ci, v, sigma, x0, max_iter, 1e-15, want_trace=True)
+    assert ref["iterations"] == max_iter
+    np.testing.assert_allclose(pair.eigenvalue, ref["eigenvalue"], rtol=1e-12)
+    assert abs(np.vdot(pair.eigenvector, ref["eigenvector"])) >= 1 - 1e-12
+
+
+def test_pair_launches_zero_start_vector(ctx, monkeypatch):
+    """normY == 0 at the first iteration (shifted_inverse_power_solver.hpp:55-58): x0 = 0 gives
+    y = 0, one iteration, lambda = 0, x unchanged, on both launch shapes."""
+    n = 3000
+    x0 = np.zeros(n, np.complex128)
+    opts = E.ShiftedSolverOptions(50, 1e-12, 0.3 + 0.2j)
+    for pair in (0, 1, 2):
+        res, _ = _triu_run(ctx, monkeypatch, pair, n, x0, opts, 0.3 + 0.2j)
+        assert res.iterations == 1 and not res.converged and res.eigenvalue == 0
+        assert not np.any(res.eigenvector)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.complex128])

@@ -33,7 +33,7 @@ for spec in (sys.argv[1:] or [""]):
     s.step(steps)
     e1.record(st)
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
+    ms = e0.elapsed_time(e1) / (steps * s.kernel_info()["iterations_per_launch"])
     s.close()
     r = E.shifted_inverse_power_method(M, E.ShiftedSolverOptions(100, 1e-12, target + 1e-3), x0)
     print(json.dumps({"variant": spec or "default", "ms": round(ms, 4), "lambda_err": abs(r.eigenvalue - target),
