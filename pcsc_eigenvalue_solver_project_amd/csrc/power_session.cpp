@@ -338,10 +338,14 @@ static int choose_transport(eigsol_power* s, int32_t trace_cap) {
         if (!std::strcmp(e, "collective") && !host_only) cand = 0;
     if (ctx->loop) {
         // Loopback ranks share one device: a waiting launch sits at the head of its stream's
-        // hardware queue, so every rank needs a queue of its own (HIP maps streams onto
-        // GPU_MAX_HW_QUEUES queues, default 4) or a rank's launch can queue behind a waiting one.
+        // hardware queue, so every rank needs a queue of its own, or a rank's launch can queue
+        // behind a waiting one (a 10 s peer-wait fault).  HIP maps streams onto GPU_MAX_HW_QUEUES
+        // queues (default 4) by use, so other live streams of the process can pair two ranks on
+        // one queue whatever the count: the peer transport of a loopback world is opt-in
+        // (EIGSOL_DIST_TRANSPORT=peer, for protocol tests and probes), the collective one the default.
+        const char* t = std::getenv("EIGSOL_DIST_TRANSPORT");
         const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-        if ((q ? std::atoi(q) : 4) < P + 1) cand = 0;
+        if (!(t && !std::strcmp(t, "peer")) || (q ? std::atoi(q) : 4) < P + 1) cand = 0;
     }
     std::vector<int> all(P);
     EIGSOL_TRY(coll_allgather(ctx, &cand, sizeof(int), all.data()));

@@ -754,8 +754,10 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
             if constexpr (kIter) bi = scale_in(bi, nrm);
             const S yi = sanitize(sdiv(sub(bi, acc), m.pv));
             st_cohi(a.zcur, m.i, yi);        // publish: readers poll this very word
-            yout[m.i] = yi;
-            a.znext[m.i] = sentinel<S>();
+            if constexpr (!kIter) {          // iteration: shift_part_kernel<S, true> moves y out
+                yout[m.i] = yi;
+                a.znext[m.i] = sentinel<S>();
+            }
         }
     };
 
@@ -808,8 +810,6 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_pair_kernel(TriArgs<S> 
     }
     const double nrm = pro.nrm, s2 = pro.s;
     const S* xin = parity ? a.buf0 : a.buf1;
-    S* w1out = a.aux;
-    S* w2out = parity ? a.buf1 : a.buf0;
     const int tid = threadIdx.x;
     const int lane = tid & (kRowLanes - 1);
     const int grp = (tid & 63) / kRowLanes;
@@ -843,11 +843,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_pair_kernel(TriArgs<S> 
         }
         acc = group_sum(acc);
         const S yi = sanitize(sdiv(sub(scale_in(m.bi, nrm), acc), m.pv));
-        if (m.i >= 0 && lane == 0) {
-            st_cohi(a.zcur, m.i, yi);
-            w1out[m.i] = yi;
-            a.znext[m.i] = sentinel<S>();
-        }
+        if (m.i >= 0 && lane == 0) st_cohi(a.zcur, m.i, yi);   // moved out by shift_pair_part_kernel
         return yi;
     };
     auto solve2 = [&](const RowMeta<S>& m, S u0, S rhs) {
@@ -861,8 +857,6 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_pair_kernel(TriArgs<S> 
         if (m.i >= 0 && lane == 0) {
             const S yi = sanitize(sdiv(sub(rhs, acc), m.pv));
             st_cohi(a.z2cur, m.i, yi);
-            w2out[m.i] = yi;
-            a.z2next[m.i] = sentinel<S>();
         }
     };
 
@@ -938,9 +932,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> 
     const int blk = (int)blockIdx.x - role * G;
     const double nrm = pro.nrm, s2 = pro.s;
     const S* xin = parity ? a.buf0 : a.buf1;
-    S* yout = role ? (parity ? a.buf1 : a.buf0) : a.aux;
     S* zdep = role ? a.z2cur : a.zcur;      // dependencies and publication
-    S* zn = role ? a.z2next : a.znext;
     const int tid = threadIdx.x;
     const int lane = tid & (kRowLanes - 1);
     const int grp = (tid & 63) / kRowLanes;
@@ -999,9 +991,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> 
             if (role) bi = scale_r(bv, s2);
             else bi = scale_in(m.bi, nrm);
             const S yi = sanitize(sdiv(sub(bi, acc), m.pv));
-            st_cohi(zdep, m.i, yi);
-            yout[m.i] = yi;
-            zn[m.i] = sentinel<S>();
+            st_cohi(zdep, m.i, yi);        // moved out by shift_pair_part_kernel
         }
     };
 
@@ -1047,12 +1037,18 @@ __global__ __launch_bounds__(kThreads) void shift_pair_part_kernel(TriArgs<S> a,
     if (!s_go) return;
     const double nrm = s_nrm;
     const S* xin = parity ? a.buf0 : a.buf1;
-    const S* w1 = a.aux;
-    const S* w2 = parity ? a.buf1 : a.buf0;
+    S* w1 = a.aux;
+    S* w2 = parity ? a.buf1 : a.buf0;
     double n21 = 0.0, pr = 0.0, pi = 0.0, n22 = 0.0, qr = 0.0, qi = 0.0;
+    // the solves left w1, w2 only in their polled buffers: move them out and reset the next
+    // launch's buffers here, in coalesced streams
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kThreads) {
-        const S y1 = w1[i];
-        const S y2 = w2[i];
+        const S y1 = a.zcur[i];
+        const S y2 = a.z2cur[i];
+        w1[i] = y1;
+        w2[i] = y2;
+        a.znext[i] = sentinel<S>();
+        a.z2next[i] = sentinel<S>();
         n21 += sq_abs(y1);
         acc_dot(pr, pi, scale_in(xin[i], nrm), y1);
         n22 += sq_abs(y2);
@@ -1075,7 +1071,10 @@ __global__ __launch_bounds__(64) void shift_decide_kernel(TriArgs<S> a, int pari
 // Norm and Rayleigh partials of a solved iterate, in a fixed order (grid-stride per thread,
 // block sums, last-arriver sum in block order): sum |y_i|^2 and sum conj(x_i) y_i with
 // x = b / ||y_prev|| as the solve used it.  Skipped once the prologue has stopped the loop.
-template <class S>
+// kFromZ (triangular factors): the solve left y only in the polled buffer zcur; this kernel also
+// moves it to B[parity] and resets znext to the sentinel for the next launch (coalesced streams,
+// instead of two scattered 16-byte stores per row inside the latency-bound solve)
+template <class S, bool kFromZ = false>
 __global__ __launch_bounds__(kThreads) void shift_part_kernel(TriArgs<S> a, int parity) {
     __shared__ double sm[3 * kWaves];
     __shared__ int s_last;
@@ -1089,10 +1088,17 @@ __global__ __launch_bounds__(kThreads) void shift_part_kernel(TriArgs<S> a, int 
     if (!s_go) return;
     const double nrm = s_nrm;
     const S* xin = parity ? a.buf0 : a.buf1;
-    const S* y = parity ? a.buf1 : a.buf0;
+    S* y = parity ? a.buf1 : a.buf0;
     double n2 = 0.0, pr = 0.0, pi = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kThreads) {
-        const S yi = y[i];
+        S yi;
+        if constexpr (kFromZ) {
+            yi = a.zcur[i];
+            y[i] = yi;
+            a.znext[i] = sentinel<S>();
+        } else {
+            yi = y[i];
+        }
         n2 += sq_abs(yi);
         acc_dot(pr, pi, scale_in(xin[i], nrm), yi);   // p = sum conj(x_i) y_i
     }
@@ -2458,8 +2464,9 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         if (pair)
             hipLaunchKernelGGL((dev::shift_pair_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a,
                                parity);
-        else if (iter)
-            hipLaunchKernelGGL((dev::shift_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a, parity);
+        else if (iter)   // every tail kernel publishes y in zcur (the chunk tail only there)
+            hipLaunchKernelGGL((dev::shift_part_kernel<S, true>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a,
+                               parity);
     } else if constexpr (!kDenseLU<S>) {
         return fail(EIGSOL_E_UNSUPPORTED, "single-precision dense factor");
     } else if (f->dense_multi) {

@@ -49,10 +49,21 @@ def _split(rp, ci, v, r0, r1):
     return (rp[r0:r1 + 1] - rp[r0]).astype(np.int32), ci[rp[r0]:rp[r1]], v[rp[r0]:rp[r1]]
 
 
-def loopback_peer_run(world, rp, ci, v, x0, n, opts, steps=None, transport=None, monkeypatch=None):
-    """`world` ranks in threads, row blocks of n/world rows; returns per-rank (result, transport)."""
-    if transport and monkeypatch is not None:
-        monkeypatch.setenv("EIGSOL_DIST_TRANSPORT", transport)
+def loopback_peer_run(world, rp, ci, v, x0, n, opts, steps=None, transport="peer", monkeypatch=None):
+    """`world` ranks in threads, row blocks of n/world rows; returns per-rank (result, transport).
+    A loopback world takes the peer transport only on request (EIGSOL_DIST_TRANSPORT=peer)."""
+    saved = os.environ.get("EIGSOL_DIST_TRANSPORT")
+    os.environ["EIGSOL_DIST_TRANSPORT"] = transport
+    try:
+        return _loopback_run(world, rp, ci, v, x0, n, opts, steps)
+    finally:
+        if saved is None:
+            os.environ.pop("EIGSOL_DIST_TRANSPORT", None)
+        else:
+            os.environ["EIGSOL_DIST_TRANSPORT"] = saved
+
+
+def _loopback_run(world, rp, ci, v, x0, n, opts, steps):
     uid = D.loopback_id(world)
     rb = np.linspace(0, n, world + 1).astype(np.int64)
     out, errs = [None] * world, []

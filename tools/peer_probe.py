@@ -15,6 +15,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("EIGSOL_DIST_TRANSPORT", "peer")   # loopback worlds: the peer exchange is opt-in
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:   # the box exports 4: one queue per rank
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
