@@ -169,8 +169,8 @@ struct GmresSolver {
     ShiftFactor* L = nullptr;
     ShiftFactor* U = nullptr;
     void* V = nullptr;          // n x (m + 1), column-major
+    void* Z = nullptr;          // n x m: K^-1 v_j of every Arnoldi step (flexible GMRES: no final preconditioner)
     void* t1 = nullptr;
-    void* t2 = nullptr;
     void* w = nullptr;
     void* x = nullptr;
     double* part = nullptr;
@@ -189,7 +189,7 @@ void gmres_free(GmresSolver* g) {
     if (g->L) shift_factor_free(g->L);
     if (g->U) shift_factor_free(g->U);
     if (g->M) csr_release(g->M);
-    for (void* p : {g->V, g->t1, g->t2, g->w, g->x, (void*)g->part, (void*)g->hdev})
+    for (void* p : {g->V, g->Z, g->t1, g->w, g->x, (void*)g->part, (void*)g->hdev})
         if (p) hipFree(p);
     ctx_release(g->ctx);
     delete g;
@@ -312,8 +312,9 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     const size_t sb = sizeof(S);
     g->G = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 2047) / 2048));
     if (rc == EIGSOL_OK &&
-        (hipMalloc(&g->V, (size_t)n * (g->m + 1) * sb) != hipSuccess || hipMalloc(&g->t1, n * sb) != hipSuccess ||
-         hipMalloc(&g->t2, n * sb) != hipSuccess || hipMalloc(&g->w, n * sb) != hipSuccess ||
+        (hipMalloc(&g->V, (size_t)n * (g->m + 1) * sb) != hipSuccess || hipMalloc(&g->Z, (size_t)n * g->m * sb) != hipSuccess ||
+         hipMalloc(&g->t1, n * sb) != hipSuccess ||
+         hipMalloc(&g->w, n * sb) != hipSuccess ||
          hipMalloc(&g->x, n * sb) != hipSuccess ||
          hipMalloc(&g->part, (size_t)g->G * (g->m + 1) * 2 * sizeof(double)) != hipSuccess ||
          hipMalloc(&g->hdev, (size_t)(g->m + 2) * 6 * sizeof(double)) != hipSuccess))
@@ -370,10 +371,10 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y) {
     const int m = g->m;
     const int gb = (int)std::min<int64_t>(2048, (n + dev::kThreads - 1) / dev::kThreads);
     S* V = static_cast<S*>(g->V);
+    S* Z = static_cast<S*>(g->Z);
     S* w = static_cast<S*>(g->w);
     S* x = static_cast<S*>(g->x);
     S* t1 = static_cast<S*>(g->t1);
-    S* t2 = static_cast<S*>(g->t2);
     double lb = 0.0, ub = 0.0, mb = 0.0;
     shift_info(g->L, &lb, nullptr, nullptr);
     shift_info(g->U, &ub, nullptr, nullptr);
@@ -412,8 +413,9 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y) {
             int k = 0;
             for (int j = 0; j < m; ++j) {
                 S* vj = V + (int64_t)j * n;
-                EIGSOL_TRY(precond(vj, t2));
-                EIGSOL_TRY(eigsol_csr_spmv(g->M, t2, w));
+                S* zj = Z + (int64_t)j * n;
+                EIGSOL_TRY(precond(vj, zj));   // kept: x += Z y at the cycle's end needs no preconditioner
+                EIGSOL_TRY(eigsol_csr_spmv(g->M, zj, w));
                 double hn = 0.0;
                 EIGSOL_TRY(cgs2<S>(g, V, j + 1, w, h, hn));
                 bytes += lb + ub + mb + 2.0 * (3.0 * (j + 1) + 2.0) * sb * (double)n;
@@ -448,7 +450,8 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y) {
                                        V + (int64_t)(j + 1) * n, n);
                 if (est <= g->rtol * bnorm || hn == 0.0) break;
             }
-            // y_k = R^-1 g (upper triangular, k x k), x += K^-1 V_k y_k
+            // y_k = R^-1 g (upper triangular, k x k), x += Z_k y_k (= K^-1 V_k y_k: the preconditioner is
+            // fixed, so flexible GMRES's update is right-preconditioned GMRES's, one application fewer)
             std::vector<hc> yk(k);
             for (int i = k - 1; i >= 0; --i) {
                 hc s = gv[i];
@@ -458,14 +461,13 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y) {
             std::vector<double> yb(2 * k);
             for (int i = 0; i < k; ++i) { yb[2 * i] = yk[i].real(); yb[2 * i + 1] = yk[i].imag(); }
             EIGSOL_HIP(hipMemcpyAsync(g->hdev, yb.data(), yb.size() * sizeof(double), hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL((dev::gm_combine_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, V, n, k, g->hdev, w, n, 1);
-            EIGSOL_TRY(precond(w, t2));
-            hipLaunchKernelGGL((dev::gm_axpy_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, x, t2, n);
+            hipLaunchKernelGGL((dev::gm_combine_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, Z, n, k, g->hdev, w, n, 1);
+            hipLaunchKernelGGL((dev::gm_axpy_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, x, w, n);
             // true residual r = b - M x (the next cycle's start)
             EIGSOL_TRY(eigsol_csr_spmv(g->M, x, t1));
             hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, t1, w, n);
             EIGSOL_TRY(norm_of(w, beta));
-            bytes += lb + ub + 2.0 * mb + (double)k * sb * (double)n;
+            bytes += mb + 2.0 * (double)k * sb * (double)n;
             relres = beta / bnorm;
             ++cycles;
             hist.push_back(relres);
