@@ -87,6 +87,7 @@ struct ShiftFactor {
     // launch, the second solve one wave round behind the first
     int pair = 0;
     int grid_pair = 0;
+    int hconc = 0;                // pair head: both solves' values fit the LDS (sptrsv_whead_kernel)
     void* aux = nullptr;          // w1 of the pair launch (n scalars)
     void* z2[2] = {nullptr, nullptr};   // the second solve's polled values
     int32_t epoch2 = 0;
@@ -169,6 +170,7 @@ struct TriArgs {
     S* z2next;
     part4* pair2;       // {||w2||^2, w1^H w2}
     part4* pair_blk;
+    int32_t hconc;      // pair head: both solves concurrently (two LDS value arrays)
 };
 
 // multiplication by an exact power of two (the pair launch's scaling of w1)
@@ -482,12 +484,26 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
             }
         }
     }
-    if (tid == 0) zl[a.hpos] = s_zero<S>();
+    // pair launch, concurrent head (a.hconc: both solves' values fit the LDS): wave 0 solves the
+    // first system in zl, wave 1 the second in zl2, one pass behind: before pass q it waits for
+    // wave 0's progress word (LDS operations of one wave execute in order, so a progress value
+    // q + 1 means pass q's values are in zl), then takes its right-hand side s * w1 from zl.
+    S* zl2 = zl + (a.hpos + 1);
+    volatile int* prog = reinterpret_cast<volatile int*>(zl2 + (a.hpos + 1));
+    const bool conc = kPair && a.hconc;
+    if (tid == 0) {
+        zl[a.hpos] = s_zero<S>();
+        if (conc) {
+            zl2[a.hpos] = s_zero<S>();
+            *prog = 0;
+        }
+    }
     __syncthreads();
-  for (int rep = 0; rep < (kPair ? 2 : 1); ++rep) {
-    if (tid < 64) {
-        const int lane = tid, grp = lane >> 2, slot = lane & 3;
+    // which 0: values in zl, right-hand side in place; which 1: values in zl2, rhs s * zl
+    auto passes = [&](const int which) {
+        const int lane = tid & 63, grp = lane >> 2, slot = lane & 3;
         const int nw = a.nwpass;
+        S* zs = which ? zl2 : zl;
         S rv[kWHeadDepth][4], rq[kWHeadDepth];
         int rc[kWHeadDepth][4], rd[kWHeadDepth];
         auto load = [&](int q, S* v, int* c, S& r, int& d) {
@@ -506,32 +522,46 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
         for (int q0 = 0; q0 < nw; q0 += kWHeadDepth) {
 #pragma unroll
             for (int u = 0; u < kWHeadDepth; ++u) {   // straight line: nw is a multiple of the depth
-                S acc = mul(rv[u][0], zl[rc[u][0]]);
+                if (which) {
+                    while (*prog <= q0 + u) __builtin_amdgcn_s_sleep(1);
+                    asm volatile("" ::: "memory");
+                }
+                S acc = mul(rv[u][0], zs[rc[u][0]]);
 #pragma unroll
-                for (int k = 1; k < 4; ++k) acc = add(acc, mul(rv[u][k], zl[rc[u][k]]));
+                for (int k = 1; k < 4; ++k) acc = add(acc, mul(rv[u][k], zs[rc[u][k]]));
                 acc = quad_sum(acc);
                 const int d = rd[u];
-                if (slot == 0 && d >= 0) zl[d] = mul(sub(zl[d], acc), rq[u]);
+                if (slot == 0 && d >= 0) {
+                    const S rhs = which ? scale_r(sanitize(zl[d]), s2) : zs[d];
+                    zs[d] = mul(sub(rhs, acc), rq[u]);
+                }
                 asm volatile("" ::: "memory");   // this pass's store precedes the next pass's reads
+                if (conc && !which && lane == 0) *prog = q0 + u + 1;
                 load(q0 + u + kWHeadDepth, rv[u], rc[u], rq[u], rd[u]);
             }
         }
+    };
+  for (int rep = 0; rep < (kPair ? 2 : 1); ++rep) {
+    if (!conc || rep == 0) {
+        if (tid < 64) passes(0);
+        else if (conc && tid < 128) passes(1);
+        __syncthreads();
     }
-    __syncthreads();
     // publish: the tail kernel (next in stream order) reads these through z
     S* zc = rep ? a.z2cur : a.zcur;
     S* zn = rep ? a.z2next : a.znext;
     S* yo = rep ? yout2 : yout;
+    const S* zsrc = (conc && rep) ? zl2 : zl;
     for (int p = tid; p < a.hpos; p += kWHeadThreads) {
         const int i = a.order[p];
         if (i < 0) continue;
-        const S yi = sanitize(zl[p]);
+        const S yi = sanitize(zsrc[p]);
         zc[i] = yi;
         yo[i] = yi;
         zn[i] = sentinel<S>();
-        if (kPair && rep == 0) zl[p] = scale_r(yi, s2);   // the second solve's right-hand side
+        if (kPair && !conc && rep == 0) zl[p] = scale_r(yi, s2);   // the second solve's right-hand side
     }
-    if (kPair && rep == 0) __syncthreads();
+    if (kPair && !conc && rep == 0) __syncthreads();
   }
 }
 
@@ -2209,6 +2239,9 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
         int role_per_cu = 1;
         if (const char* env = std::getenv("EIGSOL_TRSV_PAIR_BLOCKS_PER_CU")) role_per_cu = std::max(1, std::atoi(env));
         const int gr = std::min(f->grid, role_per_cu * f->ctx->num_cus);
+        const char* hc = std::getenv("EIGSOL_TRSV_PAIR_HEAD");   // seq: the two head solves one after the other
+        f->hconc = (!(hc && !std::strcmp(hc, "seq")) &&
+                    2 * (size_t)(f->hpos + 1) * sizeof(S) + 16 <= (size_t)160 * 1024) ? 1 : 0;
         if (want == 2 && per_cu_role * f->ctx->num_cus >= 2 * gr) {
             f->pair = 2;
             f->grid_pair = 2 * gr;
@@ -2412,7 +2445,8 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
             a.pair_blk = static_cast<dev::part4*>(f->pair_blk);
         }
         if (f->hpos > 0 && f->wave_head && pair) {
-            const size_t wl = (size_t)(f->hpos + 1) * sizeof(S);
+            a.hconc = f->hconc;
+            const size_t wl = (size_t)(f->hpos + 1) * sizeof(S) * (f->hconc ? 2 : 1) + (f->hconc ? 16 : 0);
             const void* hk = reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, true, true>);
             EIGSOL_HIP(hipFuncSetAttribute(hk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wl));
             hipLaunchKernelGGL((dev::sptrsv_whead_kernel<S, true, true>), dim3(1), dim3(dev::kWHeadThreads), wl, st, a,

@@ -397,3 +397,20 @@ def test_dense_shifted_above_single_cu_limit(ctx):
     x = E.solve_shifted(E.DenseMatrix(ctx, A), 0.5, b)
     r = A @ x - 0.5 * x - b
     assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(b)
+
+
+def test_pair_head_concurrent_matches_sequential(ctx, monkeypatch):
+    """The pair launch's head solves its two systems in two waves at once (the second one pass
+    behind the first, through an LDS progress word) or one after the other
+    (EIGSOL_TRSV_PAIR_HEAD=seq): the same operations in the same order, so bitwise the same."""
+    n = 20000
+    target = 1.5 * np.exp(0.7j)
+    sigma = target + 1e-3
+    x0 = S.start_vector(n, np.complex128)
+    opts = E.ShiftedSolverOptions(200, 1e-12, sigma)
+    conc, tc = _triu_run(ctx, monkeypatch, 2, n, x0, opts, sigma)
+    monkeypatch.setenv("EIGSOL_TRSV_PAIR_HEAD", "seq")
+    seq, ts = _triu_run(ctx, monkeypatch, 2, n, x0, opts, sigma)
+    assert conc.iterations == seq.iterations and conc.eigenvalue == seq.eigenvalue
+    np.testing.assert_array_equal(tc, ts)
+    np.testing.assert_array_equal(conc.eigenvector, seq.eigenvector)
