@@ -648,7 +648,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_slice_kernel(TriArgs<S> a, in
     for (; s < ns; s += W) {
         S z[B], v[B];
 #pragma unroll
-        for (int k = 0; k < B; ++k) z[k] = ld_coh(a.zcur + col[k]);
+        for (int k = 0; k < B; ++k) z[k] = ld_cohi(a.zcur, col[k]);
 #pragma unroll
         for (int k = 0; k < B; ++k) v[k] = ldg_stream(a.tval, (uint32_t)(off + 64 * k + lane));
         S bi = xin[row >= 0 ? row : 0];
@@ -671,13 +671,13 @@ __global__ __launch_bounds__(kThreads) void sptrsv_slice_kernel(TriArgs<S> a, in
             if (a.poll_mode == 0) {
 #pragma unroll
                 for (int k = 0; k < B; ++k)
-                    if (unready(z[k])) z[k] = ld_coh(a.zcur + col[k]);
+                    if (unready(z[k])) z[k] = ld_cohi(a.zcur, col[k]);
             } else {   // one poll per lane: its first unsolved dependency
                 int kf = -1;
 #pragma unroll
                 for (int k = B - 1; k >= 0; --k)
                     if (unready(z[k])) kf = k;
-                S zf = ld_coh(a.zcur + (kf >= 0 ? col[kf] : (int)a.n));
+                S zf = ld_cohi(a.zcur, kf >= 0 ? col[kf] : (int)a.n);
 #pragma unroll
                 for (int k = 0; k < B; ++k)
                     if (k == kf) z[k] = zf;
@@ -699,7 +699,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_slice_kernel(TriArgs<S> a, in
         }
         if (row >= 0) {
             const S yi = sanitize(sdiv(acc, piv));
-            st_coh(a.zcur + row, yi);        // publish: readers poll this very word
+            st_cohi(a.zcur, row, yi);        // publish: readers poll this very word
             yout[row] = yi;
             a.znext[row] = sentinel<S>();
         }
