@@ -298,11 +298,15 @@ class PowerSession:
                  10: "csr_bin_kernel (column-binned row chunks, row sums in LDS; tiles = chunks)",
                  11: "csr_bin_kernel in two row halves per iteration, the first half's all-gather "
                      "overlapped with the second half (row-sharded; tiles = chunks)",
-                 12: "sptrsv pair kernel (sync-free triangular solve, two iterations per launch: the second "
-                     "solve one wave round behind the first)"}
+                 12: "sptrsv multi-solve kernel (sync-free triangular solves, 2 iterations per launch, "
+                     "solve j one dependency round behind solve j-1)",
+                 13: "sptrsv multi-solve kernel (sync-free triangular solves, 3 iterations per launch, "
+                     "solve j one dependency round behind solve j-1)",
+                 14: "sptrsv multi-solve kernel (sync-free triangular solves, 4 iterations per launch, "
+                     "solve j one dependency round behind solve j-1)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?"),
-                "iterations_per_launch": 2 if v.value == 12 else 1}
+                "iterations_per_launch": v.value - 10 if 12 <= v.value <= 14 else 1}
 
     def kernel_name(self) -> str:
         """Demangled name of the per-iteration kernel (CSR power sessions), as rocprofv3 reports it."""

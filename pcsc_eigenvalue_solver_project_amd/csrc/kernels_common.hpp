@@ -259,7 +259,7 @@ struct alignas(16) Prologue {
     double nrm;       // ||y_{t-1}||: x_t = y_{t-1} / nrm (nrm == 0 only at t == 0: x0 == 0, kept as is)
     int32_t go;       // 1: this launch computes; 0: the loop has ended
     int32_t t;
-    double s;         // pair launches (shift_pair_prologue): the power of two scaling the second solve
+    double s;         // multi-solve launches (shift_multi_prologue): the power of two scaling solves 1..K-1
 };
 
 // peer != nullptr: row-sharded session on the device-side peer exchange — wait for every peer's
@@ -489,27 +489,29 @@ __device__ __forceinline__ void shift_prologue(PowerCtl* ctl, const part4* rank_
     __syncthreads();
 }
 
-// Pair launches (triangular factors, sptrsv pair mode): launch t runs reference iterations
-// k1 = 2t and k2 = 2t + 1 together.  It solves w1 = (A - sigma I)^{-1} x with x = v / ||v|| (v the
-// previous launch's w2) exactly as a single launch does, and, one wave round behind it in the
-// same kernels, w2 = (A - sigma I)^{-1} (s w1) with s = 2^-e an exact power of two near 1 / ||w1||
-// (e from the previous launch's growth ||w1||; s = 1 at t = 0).  The reference's iterate of k2
-// is y = (A - sigma I)^{-1} (w1 / ||w1||) = w2 / (s ||w1||): the second solve defers the
-// normalisation to after the solve (linearity), which is what lets it start before ||w1|| exists.
-// It differs from the reference's y only by the rounding of that division (the
-// factor paths are tolerance parity).  Partials of launch t: part1 = {||w1||^2, x^H w1},
-// part2 = {||w2||^2, w1^H w2}; the Rayleigh quotients are
-//     lambda_k1 = sigma + conj(x^H w1) / ||w1||^2,   lambda_k2 = sigma + s conj(w1^H w2) / ||w2||^2
+// Multi-solve launches (triangular factors; shifted.hip, sptrsv_chunk_role_kernel): launch t runs
+// reference iterations k_j = K t + j, j = 0..K-1, together.  Solve 0 is w_0 = (A - sigma I)^{-1} x
+// with x = v / ||v|| (v the previous launch's last solution), exactly as a single launch does;
+// solve j >= 1 is w_j = (A - sigma I)^{-1} (s w_{j-1}) with s = 2^-e an exact power of two near
+// 1 / ||w_0|| (e from the previous launch's growth ||w_0||; s = 1 at t = 0).  The reference's
+// iterate of k_j (j >= 1) is y = (A - sigma I)^{-1} (w_{j-1} / ||w_{j-1}||) = w_j / (s ||w_{j-1}||):
+// solve j defers the normalisation to after the solve (linearity), which is what lets it start
+// before ||w_{j-1}|| exists, one dependency round behind solve j - 1.  It differs from the
+// reference's y only by the rounding of that division (the factor paths are
+// tolerance parity).  Partials of solve j: {||w_j||^2, w_{j-1}^H w_j} (w_{-1} = x; j = 0 in
+// part0, j >= 1 in kpart[j - 1]); the Rayleigh quotients are
+//     lambda_k0 = sigma + conj(x^H w_0) / ||w_0||^2,   lambda_kj = sigma + s conj(w_{j-1}^H w_j) / ||w_j||^2
 // and the prologue of launch t+1 applies the reference's tests (normY == 0, is_close_relative,
-// maxIterations; shifted_inverse_power_solver.hpp:48-76) to k1, then to k2, in that order, so the
-// iteration count is the reference's.  The work of k2 is discarded when the loop ends at k1.
-// Final iterate: k1 -> the factor's w1 buffer (final_parity 2), k2 -> B[parity ^ 1] (w2), a zero
-// norm -> the previous input B[parity].  Carry: rho = last lambda, nrm = ||v|| (this launch's
-// input norm), pad = e (this launch's exponent, read back for lambda_k2).
+// maxIterations; shifted_inverse_power_solver.hpp:48-76) to k_0, k_1, ... in order, so the
+// iteration count is the reference's; the work past the stopping iteration is discarded.
+// Final iterate x: w_j / ||w_j|| (final_parity 2 + j: the factor's buffer aux[j], j < K - 1;
+// B[parity ^ 1] for j = K - 1); a zero norm at k_j keeps the previous x (w_{j-1}, or the
+// previous input B[parity]).  Carry: rho = last lambda, nrm = ||v|| (this launch's input norm),
+// pad = e (this launch's exponent, read back for the lambdas).
 template <class S>
-__device__ __forceinline__ void shift_pair_prologue(PowerCtl* ctl, const part4* part1, const part4* part2,
-                                                    int parity, S* trace, double sig_re, double sig_im,
-                                                    Prologue* out) {
+__device__ __forceinline__ void shift_multi_prologue(PowerCtl* ctl, const part4* part0, const part4* kpart, int K,
+                                                     int parity, S* trace, double sig_re, double sig_im,
+                                                     Prologue* out) {
     if (threadIdx.x == 0) {
         Prologue pr{0.0, 0, 0, 1.0};
         const int done = __hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -521,60 +523,46 @@ __device__ __forceinline__ void shift_pair_prologue(PowerCtl* ctl, const part4* 
             int32_t iters = 0, fpar = 0, ntr = -1, e = 0;
             double lre = in.rho_re, lim = in.rho_im, fnorm = 0.0, nrm;
             if (t == 0) {
-                nrm = sqrt(part1[0].a);   // ||x0||^2 from begin()
+                nrm = sqrt(part0[0].a);   // ||x0||^2 from begin()
             } else {
-                const int32_t k1 = 2 * (t - 1), k2 = k1 + 1;
-                const double n21 = part1[0].a, p1r = part1[0].b, p1i = part1[0].c;
-                const double n22 = part2[0].a, qr = part2[0].b, qi = part2[0].c;
                 const double s_prev = ldexp(1.0, -in.pad);
-                nrm = sqrt(n22);
-                if (n21 == 0.0) {                         // normY == 0 at k1 (:55-58)
-                    fin = true;
-                    iters = k1 + 1;
-                    fpar = parity;                        // x unchanged: the previous launch's input
-                    fnorm = in.nrm;
-                    if (k1 == 0) { lre = 0.0; lim = 0.0; }
-                } else {
-                    const double l1r = sig_re + p1r / n21;
-                    const double l1i = cplx_ ? sig_im - p1i / n21 : 0.0;
-                    ntr = k1 + 1;
-                    if (trace && k1 < ctl->trace_cap && blockIdx.x == 0) set_re_im(trace[k1], l1r, l1i);
-                    fpar = 2;
-                    fnorm = sqrt(n21);
-                    if (k1 >= 1 && close_rel(l1r, l1i, lre, lim, ctl->tol, cplx_)) {
+                double prev_n = in.nrm;   // norm of the previous x's buffer
+                int prev_par = parity;    // ... and its final_parity code
+                for (int j = 0; j < K && !fin; ++j) {
+                    const part4 pj = j ? kpart[j - 1] : part0[0];
+                    const int32_t k = K * (t - 1) + j;
+                    const int code = j == K - 1 ? (parity ^ 1) : 2 + j;
+                    if (pj.a == 0.0) {                    // normY == 0 (:55-58): x, lambda unchanged
+                        fin = true;
+                        iters = k + 1;
+                        fpar = prev_par;
+                        fnorm = prev_n;
+                        if (k == 0) { lre = 0.0; lim = 0.0; }
+                        break;
+                    }
+                    const double sc = j ? s_prev : 1.0;
+                    const double lr = sig_re + sc * pj.b / pj.a;
+                    const double li = cplx_ ? sig_im - sc * pj.c / pj.a : 0.0;
+                    ntr = k + 1;
+                    if (trace && k < ctl->trace_cap && blockIdx.x == 0) set_re_im(trace[k], lr, li);
+                    fpar = code;
+                    fnorm = sqrt(pj.a);
+                    if (k >= 1 && close_rel(lr, li, lre, lim, ctl->tol, cplx_)) {
                         fin = true;                       // :64-70
                         conv = true;
-                        iters = k1 + 1;
-                    } else if (k1 + 1 >= ctl->max_iter) {
+                        iters = k + 1;
+                    } else if (k + 1 >= ctl->max_iter) {
                         fin = true;                       // loop bound :48
-                        iters = k1 + 1;
+                        iters = k + 1;
                     }
-                    lre = l1r;
-                    lim = l1i;
-                    if (!fin && n22 == 0.0) {             // normY == 0 at k2: x stays x_k1
-                        fin = true;
-                        iters = k2 + 1;
-                    } else if (!fin) {
-                        const double l2r = sig_re + s_prev * qr / n22;
-                        const double l2i = cplx_ ? sig_im - s_prev * qi / n22 : 0.0;
-                        ntr = k2 + 1;
-                        if (trace && k2 < ctl->trace_cap && blockIdx.x == 0) set_re_im(trace[k2], l2r, l2i);
-                        fpar = parity ^ 1;
-                        fnorm = nrm;
-                        if (close_rel(l2r, l2i, lre, lim, ctl->tol, cplx_)) {
-                            fin = true;
-                            conv = true;
-                            iters = k2 + 1;
-                        } else if (k2 + 1 >= ctl->max_iter) {
-                            fin = true;
-                            iters = k2 + 1;
-                        }
-                        lre = l2r;
-                        lim = l2i;
-                    }
+                    lre = lr;
+                    lim = li;
+                    prev_n = fnorm;
+                    prev_par = code;
                 }
+                nrm = sqrt((K > 1 ? kpart[K - 2] : part0[0]).a);
                 // growth of the previous launch's first solve from a unit input
-                const double g = sqrt(n21);
+                const double g = sqrt(part0[0].a);
                 if (g > 0.0 && g < INFINITY) e = min(max(ilogb(g), -900), 900);
                 if constexpr (!std::is_same_v<S, double> && !std::is_same_v<S, cplx>)
                     e = min(max(e, -100), 100);

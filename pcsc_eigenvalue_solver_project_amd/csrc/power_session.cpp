@@ -44,7 +44,7 @@ int shift_factor_csr(eigsol_csr* A, const void* sigma, ShiftFactor** out);
 int shift_factor_dense(eigsol_dense* A, const void* sigma, ShiftFactor** out);
 void shift_factor_free(ShiftFactor* f);
 int shift_grid(const ShiftFactor* f);
-void* shift_aux(const ShiftFactor* f);
+void* shift_aux(const ShiftFactor* f, int j);
 int shift_error(ShiftFactor* f);
 int shift_iter_launch(ShiftFactor* f, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
                       void* my_part, void* trace, int parity);
@@ -591,9 +591,10 @@ int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_ou
     if (iterations) *iterations = it;
     if (converged) *converged = conv;
     if (x_out) {
-        // final_parity 2: a pair launch's first solve (the triangular factor's w1 buffer)
-        void* src = parity == 2 ? shift_aux(s->shift) : static_cast<char*>(s->buf[parity]) + (size_t)s->xoff * sb;
-        if (parity == 2) parity = 1;   // scratch below: buf[0]
+        // final_parity 2 + j: solve j of a multi-solve launch (the triangular factor's buffer aux[j])
+        void* src = parity >= 2 ? shift_aux(s->shift, parity - 2)
+                                : static_cast<char*>(s->buf[parity]) + (size_t)s->xoff * sb;
+        if (parity >= 2) parity = 1;   // scratch below: buf[0]
         if (x_out_on_device) {
             EIGSOL_TRY(scale_out_launch(s->ctx, s->dtype, src, fnorm, x_out, s->n));
             EIGSOL_HIP(hipStreamSynchronize(st));

@@ -38,6 +38,11 @@ void gmres_free(GmresSolver* g);
 int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev);
 void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps);
 
+namespace dev {
+constexpr int kMaxMulti = 4;      // solves per multi-solve launch (one head wave each)
+}
+static constexpr int kMultiDefault = 2;   // EIGSOL_TRSV_MULTI
+
 struct ShiftFactor {
     eigsol_ctx* ctx = nullptr;
     int dtype = EIGSOL_F64;
@@ -83,16 +88,16 @@ struct ShiftFactor {
     int32_t chunk0 = 0;
     int poll_fast = 0;            // tail polls without back-off (EIGSOL_TRSV_POLL_FAST)
     int poll_mode = 0;            // EIGSOL_TRSV_POLL_MODE
-    // pair launches (sptrsv_chunk_pair_kernel; EIGSOL_TRSV_PAIR=0 disables): two iterations per
-    // launch, the second solve one wave round behind the first
-    int pair = 0;
-    int grid_pair = 0;
-    int hconc = 0;                // pair head: both solves' values fit the LDS (sptrsv_whead_kernel)
-    void* aux = nullptr;          // w1 of the pair launch (n scalars)
-    void* z2[2] = {nullptr, nullptr};   // the second solve's polled values
-    int32_t epoch2 = 0;
-    void* pair_part = nullptr;    // part4: {||w2||^2, w1^H w2}
-    void* pair_blk = nullptr;     // part4 per block of the pair partials reduction
+    // multi-solve launches (sptrsv_chunk_role_kernel; EIGSOL_TRSV_MULTI=K, 1 disables): K reference
+    // iterations per launch, solve j one dependency round behind solve j - 1
+    int multi = 1;
+    int grid_multi = 0;
+    int hconc = 0;                // multi head: every solve's values fit the LDS (sptrsv_whead_kernel)
+    void* aux[dev::kMaxMulti - 1] = {};           // w_0 .. w_{K-2} (n scalars each)
+    void* zm[dev::kMaxMulti][2] = {};             // solve j >= 1: polled values (zm[0] unused: z)
+    int32_t epoch_m = 0;
+    void* kpart = nullptr;        // part4 per solve j >= 1: {||w_j||^2, w_{j-1}^H w_j}
+    void* kblk = nullptr;         // part4 per block of those reductions
     uint32_t* work = nullptr;     // [2]: last-arriver ticket of the partials reduction
     int32_t* err = nullptr;
     void* wave_part = nullptr;    // part4 per wave
@@ -164,13 +169,14 @@ struct TriArgs {
     part4* my_part;
     S* trace;
     double sig_re, sig_im;
-    // pair launches
-    S* aux;             // w1
-    S* z2cur;           // the second solve's polled values
-    S* z2next;
-    part4* pair2;       // {||w2||^2, w1^H w2}
-    part4* pair_blk;
-    int32_t hconc;      // pair head: both solves concurrently (two LDS value arrays)
+    // multi-solve launches (K solves; solve 0 polls zcur)
+    int32_t K;
+    S* zk[kMaxMulti];   // solve j's polled values (zk[0] = zcur)
+    S* zkn[kMaxMulti];  // ... and the next launch's buffers (zkn[0] = znext)
+    S* aux[kMaxMulti - 1];   // w_0 .. w_{K-2}
+    part4* kpart;       // solves 1..K-1: {||w_j||^2, w_{j-1}^H w_j}
+    part4* kblk;        // (K - 1) x red_grid block partials
+    int32_t hconc;      // multi head: the K solves concurrently (K LDS value arrays)
 };
 
 // multiplication by an exact power of two (the pair launch's scaling of w1)
@@ -435,28 +441,28 @@ __device__ __forceinline__ float quad_sum(float v) {
 __device__ __forceinline__ cplx quad_sum(cplx v) { return cplx{quad_sum(v.re), quad_sum(v.im)}; }
 __device__ __forceinline__ cplxf quad_sum(cplxf v) { return cplxf{quad_sum(v.re), quad_sum(v.im)}; }
 
-// kPair: the pair launch's head (shift_pair_prologue): the head is solved twice from LDS, the
-// second time on s * (the first solution), published to z2cur and B[parity].
-template <class S, bool kIter, bool kPair = false>
+// kMulti: the multi-solve launch's head (shift_multi_prologue): the head is solved K times from
+// LDS, solve j on s * (solve j-1's solution); solve j is published to zk[j] and, for the last
+// one, to B[parity] (the earlier ones to aux[j]).
+template <class S, bool kIter, bool kMulti = false>
 __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> a, int parity) {
     extern __shared__ __align__(16) unsigned char head_lds[];
     S* zl = reinterpret_cast<S*>(head_lds);
     __shared__ Prologue pro;
     const S* xin;
     S* yout;
-    S* yout2 = nullptr;
     double nrm = 0.0, s2 = 1.0;
+    const int K = kMulti ? a.K : 1;
     if constexpr (kIter) {
-        if constexpr (kPair)
-            shift_pair_prologue<S>(a.ctl, a.rank_part, a.pair2, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if constexpr (kMulti)
+            shift_multi_prologue<S>(a.ctl, a.rank_part, a.kpart, a.K, parity, a.trace, a.sig_re, a.sig_im, &pro);
         else
             shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
         if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // the tail kernel resets z
         nrm = pro.nrm;
         s2 = pro.s;
         xin = parity ? a.buf0 : a.buf1;
-        yout = kPair ? a.aux : (parity ? a.buf1 : a.buf0);
-        yout2 = parity ? a.buf1 : a.buf0;
+        yout = parity ? a.buf1 : a.buf0;
     } else {
         xin = a.b_plain;
         yout = a.y_plain;
@@ -484,26 +490,29 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
             }
         }
     }
-    // pair launch, concurrent head (a.hconc: both solves' values fit the LDS): wave 0 solves the
-    // first system in zl, wave 1 the second in zl2, one pass behind: before pass q it waits for
-    // wave 0's progress word (LDS operations of one wave execute in order, so a progress value
-    // q + 1 means pass q's values are in zl), then takes its right-hand side s * w1 from zl.
-    S* zl2 = zl + (a.hpos + 1);
-    volatile int* prog = reinterpret_cast<volatile int*>(zl2 + (a.hpos + 1));
-    const bool conc = kPair && a.hconc;
+    // multi-solve launch, concurrent head (a.hconc: every solve's values fit the LDS): wave j
+    // solves system j in its own LDS array, one pass behind wave j - 1: before pass q it waits
+    // for wave j - 1's progress word (LDS operations of one wave execute in order, so a progress
+    // value q + 1 means pass q's values are in place), then takes its right-hand side s w_{j-1}
+    // from wave j - 1's array.
+    const int64_t pitch = a.hpos + 1;
+    volatile int* prog = reinterpret_cast<volatile int*>(zl + K * pitch);
+    const bool conc = kMulti && a.hconc;
     if (tid == 0) {
         zl[a.hpos] = s_zero<S>();
-        if (conc) {
-            zl2[a.hpos] = s_zero<S>();
-            *prog = 0;
-        }
+        if (conc)
+            for (int j = 1; j < K; ++j) {
+                zl[j * pitch + a.hpos] = s_zero<S>();
+                prog[j - 1] = 0;
+            }
     }
     __syncthreads();
-    // which 0: values in zl, right-hand side in place; which 1: values in zl2, rhs s * zl
+    // which 0: values in zl, right-hand side in place; which j >= 1: values in array j, rhs s * array j-1
     auto passes = [&](const int which) {
         const int lane = tid & 63, grp = lane >> 2, slot = lane & 3;
         const int nw = a.nwpass;
-        S* zs = which ? zl2 : zl;
+        S* zs = zl + which * pitch;
+        const S* zp = zl + (which ? which - 1 : 0) * pitch;
         S rv[kWHeadDepth][4], rq[kWHeadDepth];
         int rc[kWHeadDepth][4], rd[kWHeadDepth];
         auto load = [&](int q, S* v, int* c, S& r, int& d) {
@@ -523,7 +532,7 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
 #pragma unroll
             for (int u = 0; u < kWHeadDepth; ++u) {   // straight line: nw is a multiple of the depth
                 if (which) {
-                    while (*prog <= q0 + u) __builtin_amdgcn_s_sleep(1);
+                    while (prog[which - 1] <= q0 + u) __builtin_amdgcn_s_sleep(1);
                     asm volatile("" ::: "memory");
                 }
                 S acc = mul(rv[u][0], zs[rc[u][0]]);
@@ -532,26 +541,26 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
                 acc = quad_sum(acc);
                 const int d = rd[u];
                 if (slot == 0 && d >= 0) {
-                    const S rhs = which ? scale_r(sanitize(zl[d]), s2) : zs[d];
+                    const S rhs = which ? scale_r(sanitize(zp[d]), s2) : zs[d];
                     zs[d] = mul(sub(rhs, acc), rq[u]);
                 }
                 asm volatile("" ::: "memory");   // this pass's store precedes the next pass's reads
-                if (conc && !which && lane == 0) *prog = q0 + u + 1;
+                if (conc && which + 1 < K && lane == 0) prog[which] = q0 + u + 1;
                 load(q0 + u + kWHeadDepth, rv[u], rc[u], rq[u], rd[u]);
             }
         }
     };
-  for (int rep = 0; rep < (kPair ? 2 : 1); ++rep) {
+  for (int rep = 0; rep < K; ++rep) {
     if (!conc || rep == 0) {
-        if (tid < 64) passes(0);
-        else if (conc && tid < 128) passes(1);
+        const int w = tid >> 6;
+        if (w == 0 || (conc && w < K)) passes(w);
         __syncthreads();
     }
     // publish: the tail kernel (next in stream order) reads these through z
-    S* zc = rep ? a.z2cur : a.zcur;
-    S* zn = rep ? a.z2next : a.znext;
-    S* yo = rep ? yout2 : yout;
-    const S* zsrc = (conc && rep) ? zl2 : zl;
+    S* zc = rep ? a.zk[rep] : a.zcur;
+    S* zn = rep ? a.zkn[rep] : a.znext;
+    S* yo = rep == K - 1 ? yout : a.aux[rep];
+    const S* zsrc = zl + (conc ? rep : 0) * pitch;
     for (int p = tid; p < a.hpos; p += kWHeadThreads) {
         const int i = a.order[p];
         if (i < 0) continue;
@@ -559,9 +568,9 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
         zc[i] = yi;
         yo[i] = yi;
         zn[i] = sentinel<S>();
-        if (kPair && !conc && rep == 0) zl[p] = scale_r(yi, s2);   // the second solve's right-hand side
+        if (kMulti && !conc && rep + 1 < K) zl[p] = scale_r(yi, s2);   // the next solve's right-hand side
     }
-    if (kPair && !conc && rep == 0) __syncthreads();
+    if (kMulti && !conc && rep + 1 < K) __syncthreads();
   }
 }
 
@@ -817,152 +826,33 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
     }
 }
 
-// ---- tail of a pair launch (shift_pair_prologue): the chunk schedule above solving two systems
-// at once.  A wave solves its chunks of round r for w1 (as sptrsv_chunk_kernel does), then its
-// chunks of round r - 1 for w2 = (A - sigma I)^{-1} (s w1): the second solve reuses the row
-// metadata and entries the wave loaded for the first one a round earlier (the matrix is read once
-// for both solves), and its right-hand side s w1_i is the wave's own result of that round, still
-// in registers.  Its dependencies are the second solve's values of lower positions, polled in
-// z2cur.  No deadlock: first solves never wait on second ones, and every wave takes its second
-// solves in increasing position order, each after its own first solve of the same chunk.
-// A level of the first solve costs what it costs alone; the second trails it by one round, so a
-// launch costs about one solve plus one round, for two reference iterations.
-template <class S>
-__global__ __launch_bounds__(kThreads) void sptrsv_chunk_pair_kernel(TriArgs<S> a, int parity) {
-    __shared__ Prologue pro;
-    shift_pair_prologue<S>(a.ctl, a.rank_part, a.pair2, parity, a.trace, a.sig_re, a.sig_im, &pro);
-    if (!__builtin_amdgcn_readfirstlane(pro.go)) {
-        for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < a.n; r += (int64_t)gridDim.x * kThreads) {
-            a.znext[r] = sentinel<S>();
-            a.z2next[r] = sentinel<S>();
-        }
-        return;
-    }
-    const double nrm = pro.nrm, s2 = pro.s;
-    const S* xin = parity ? a.buf0 : a.buf1;
-    const int tid = threadIdx.x;
-    const int lane = tid & (kRowLanes - 1);
-    const int grp = (tid & 63) / kRowLanes;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int W = gridDim.x * kWaves;
-    const int gw = a.chunk0 + wave * gridDim.x + blockIdx.x;
-
-    auto fetch1 = [&](int c, RowMeta<S>& m) {
-        const bool in = c < a.nchunks;
-        const int pos = (in ? c : 0) * kWaveRows + grp;
-        m.i = in ? a.porder[pos] : -1;
-        const int e0 = a.pptr[pos];
-        m.e0 = e0;
-        m.len = in ? a.pptr[pos + 1] - e0 : 0;
-        m.pv = ldg_stream(a.ppiv, (uint32_t)pos);
-    };
-    auto fetch2 = [&](RowMeta<S>& m) {
-        const bool ok = lane < m.len;
-        const int e = ok ? m.e0 + lane : 0;
-        m.j = ok ? (int)ldg_stream(a.pcol, (uint32_t)e) : -1;
-        m.v = ldg_stream(a.pval, (uint32_t)e);
-        m.bi = xin[m.i >= 0 ? m.i : 0];
-    };
-    // first solve: returns w1_i in every lane of the row's group
-    auto solve1 = [&](const RowMeta<S>& m, S z0) -> S {
-        S acc = s_zero<S>();
-        if (m.j >= 0) acc = mul(m.v, finish_wait(z0, a.zcur, m.j, a.err, a.poll_fast));
-        for (int k = lane + kRowLanes; k < m.len; k += kRowLanes) {
-            const int e = m.e0 + k;
-            acc = add(acc, mul(a.pval[e], wait_value(a.zcur, a.pcol[e], a.err)));
-        }
-        acc = group_sum(acc);
-        const S yi = sanitize(sdiv(sub(scale_in(m.bi, nrm), acc), m.pv));
-        if (m.i >= 0 && lane == 0) st_cohi(a.zcur, m.i, yi);   // moved out by shift_pair_part_kernel
-        return yi;
-    };
-    auto solve2 = [&](const RowMeta<S>& m, S u0, S rhs) {
-        S acc = s_zero<S>();
-        if (m.j >= 0) acc = mul(m.v, finish_wait(u0, a.z2cur, m.j, a.err, a.poll_fast));
-        for (int k = lane + kRowLanes; k < m.len; k += kRowLanes) {
-            const int e = m.e0 + k;
-            acc = add(acc, mul(a.pval[e], wait_value(a.z2cur, a.pcol[e], a.err)));
-        }
-        acc = group_sum(acc);
-        if (m.i >= 0 && lane == 0) {
-            const S yi = sanitize(sdiv(sub(rhs, acc), m.pv));
-            st_cohi(a.z2cur, m.i, yi);
-        }
-    };
-
-    RowMeta<S> c0, c1, n0, n1, q0, q1;
-    q0.i = q1.i = -1;
-    q0.j = q1.j = -1;
-    q0.e0 = q1.e0 = 0;
-    q0.len = q1.len = 0;
-    q0.v = q1.v = q0.bi = q1.bi = q0.pv = q1.pv = s_zero<S>();
-    S r0 = s_zero<S>(), r1 = s_zero<S>();
-    fetch1(gw, c0);
-    fetch1(gw + W, c1);
-    fetch2(c0);
-    fetch2(c1);
-    fetch1(gw + 2 * W, n0);
-    fetch1(gw + 3 * W, n1);
-    S z0 = c0.j >= 0 ? ld_cohi(a.zcur, c0.j) : s_zero<S>();
-    S z1 = c1.j >= 0 ? ld_cohi(a.zcur, c1.j) : s_zero<S>();
-    for (int c = gw; c < a.nchunks; c += 2 * W) {
-        fetch2(n0);
-        fetch2(n1);
-        RowMeta<S> m0, m1;
-        fetch1(c + 4 * W, m0);
-        fetch1(c + 5 * W, m1);
-        // the second solve's first polls, issued before the first solve waits
-        S u0 = q0.j >= 0 ? ld_cohi(a.z2cur, q0.j) : s_zero<S>();
-        S u1 = q1.j >= 0 ? ld_cohi(a.z2cur, q1.j) : s_zero<S>();
-        const S y0 = solve1(c0, z0);
-        const S y1 = solve1(c1, z1);
-        solve2(q0, u0, r0);
-        solve2(q1, u1, r1);
-        q0 = c0;
-        q1 = c1;
-        r0 = scale_r(y0, s2);
-        r1 = scale_r(y1, s2);
-        z0 = n0.j >= 0 ? ld_cohi(a.zcur, n0.j) : s_zero<S>();
-        z1 = n1.j >= 0 ? ld_cohi(a.zcur, n1.j) : s_zero<S>();
-        c0 = n0;
-        c1 = n1;
-        n0 = m0;
-        n1 = m1;
-    }
-    {
-        S u0 = q0.j >= 0 ? ld_cohi(a.z2cur, q0.j) : s_zero<S>();
-        S u1 = q1.j >= 0 ? ld_cohi(a.z2cur, q1.j) : s_zero<S>();
-        solve2(q0, u0, r0);
-        solve2(q1, u1, r1);
-    }
-}
-
-// ---- tail of a pair launch, role split: the grid is two copies of the single-solve grid.  Blocks
-// [0, G) run sptrsv_chunk_kernel's schedule for w1; blocks [G, 2G) run the same schedule for
-// w2 = (A - sigma I)^{-1} (s w1), taking each row's right-hand side s w1_i from the first solve's
-// polled value (its ready flag) and their dependencies from z2cur.  A wave of either solve waits
-// only on its own solve's chains, so the second solve trails the first by about one dependency
-// round trip instead of adding its own chain waits to the first solve's waves (the interleaved
-// schedule above: 0.69 ms per iteration on config 5 against 0.83 for one solve per launch).
-// The matrix is read once per solve.  No deadlock: first-solve waves never wait on the second
-// solve, and every wave is resident (cooperative launch).
+// ---- tail of a multi-solve launch (shift_multi_prologue), role split: the grid is K copies of
+// the single-solve grid.  Blocks [jG, (j+1)G) run sptrsv_chunk_kernel's schedule for solve j:
+// w_0 = (A - sigma I)^{-1} x, w_j = (A - sigma I)^{-1} (s w_{j-1}), taking each row's right-hand
+// side s (w_{j-1})_i from solve j-1's polled value (its ready flag) and their dependencies from
+// zk[j].  A wave waits only on its own solve's chains (and on the row of the solve before), so
+// solve j trails solve j-1 by about one dependency round trip.  The matrix is read once per
+// solve.  No deadlock: solve j-1 never waits on solve j, and every wave is resident (cooperative
+// launch).  Measured on config 5 (pair launches, K = 2): 0.539 ms per iteration at one workgroup
+// per CU per solve against 0.555 at two, and 0.58 ms for an interleaved schedule (each wave
+// solving its chunks of round r for w_0, then those of round r - 1 for w_1: a wave's second-solve
+// waits then add to its first-solve waits).
 template <class S>
 __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> a, int parity) {
     __shared__ Prologue pro;
-    shift_pair_prologue<S>(a.ctl, a.rank_part, a.pair2, parity, a.trace, a.sig_re, a.sig_im, &pro);
+    shift_multi_prologue<S>(a.ctl, a.rank_part, a.kpart, a.K, parity, a.trace, a.sig_re, a.sig_im, &pro);
     if (!__builtin_amdgcn_readfirstlane(pro.go)) {
-        for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < a.n; r += (int64_t)gridDim.x * kThreads) {
-            a.znext[r] = sentinel<S>();
-            a.z2next[r] = sentinel<S>();
-        }
+        for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < a.n; r += (int64_t)gridDim.x * kThreads)
+            for (int j = 0; j < a.K; ++j) a.zkn[j][r] = sentinel<S>();
         return;
     }
-    const int G = (int)gridDim.x / 2;
-    const int role = __builtin_amdgcn_readfirstlane((int)blockIdx.x >= G ? 1 : 0);
+    const int G = (int)gridDim.x / a.K;
+    const int role = __builtin_amdgcn_readfirstlane((int)blockIdx.x / G);
     const int blk = (int)blockIdx.x - role * G;
     const double nrm = pro.nrm, s2 = pro.s;
     const S* xin = parity ? a.buf0 : a.buf1;
-    S* zdep = role ? a.z2cur : a.zcur;      // dependencies and publication
+    S* zdep = a.zk[role];                          // dependencies and publication
+    const S* zrhs = a.zk[role ? role - 1 : 0];     // solve j >= 1: the previous solve's values
     const int tid = threadIdx.x;
     const int lane = tid & (kRowLanes - 1);
     const int grp = (tid & 63) / kRowLanes;
@@ -985,7 +875,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> 
         m.j = ok ? (int)ldg_stream(a.pcol, (uint32_t)e) : -1;
         m.v = ldg_stream(a.pval, (uint32_t)e);
         // second solve: the first solve's value of the row, possibly not yet solved (polled below)
-        m.bi = role ? ld_cohi(a.zcur, (m.i >= 0 ? m.i : (int)a.n)) : xin[m.i >= 0 ? m.i : 0];
+        m.bi = role ? ld_cohi(zrhs, (m.i >= 0 ? m.i : (int)a.n)) : xin[m.i >= 0 ? m.i : 0];
     };
     auto solve = [&](const RowMeta<S>& m, S z0) {
         S acc = s_zero<S>();
@@ -1001,7 +891,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> 
                 else if (spins < 16) __builtin_amdgcn_s_sleep(8);
                 else __builtin_amdgcn_s_sleep(32);
                 if (unready(zv)) zv = ld_cohi(zdep, m.j);
-                if (nb && unready(bv)) bv = ld_cohi(a.zcur, m.i);
+                if (nb && unready(bv)) bv = ld_cohi(zrhs, m.i);
                 if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(a.err) != 0)) {
                     atomicOr(a.err, 1);
                     break;
@@ -1021,7 +911,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> 
             if (role) bi = scale_r(bv, s2);
             else bi = scale_in(m.bi, nrm);
             const S yi = sanitize(sdiv(sub(bi, acc), m.pv));
-            st_cohi(zdep, m.i, yi);        // moved out by shift_pair_part_kernel
+            st_cohi(zdep, m.i, yi);        // moved out by shift_multi_part_kernel
         }
     };
 
@@ -1032,18 +922,27 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> 
     fetch2(c1);
     fetch1(gw + 2 * W, n0);
     fetch1(gw + 3 * W, n1);
+    // EIGSOL_TRSV_POLL_MODE bit 1: the second chunk's first polls are issued after the first
+    // chunk is solved instead of a round ahead (fewer polls of still-unsolved values); bit 2: both
+    // chunks' first polls at the top of the round
+    const int late = a.poll_mode;
     S z0 = c0.j >= 0 ? ld_cohi(zdep, c0.j) : s_zero<S>();
     S z1 = c1.j >= 0 ? ld_cohi(zdep, c1.j) : s_zero<S>();
     for (int c = gw; c < a.nchunks; c += 2 * W) {
+        if (late & 4) {
+            z0 = c0.j >= 0 ? ld_cohi(zdep, c0.j) : s_zero<S>();
+            z1 = c1.j >= 0 ? ld_cohi(zdep, c1.j) : s_zero<S>();
+        }
         fetch2(n0);
         fetch2(n1);
         RowMeta<S> m0, m1;
         fetch1(c + 4 * W, m0);
         fetch1(c + 5 * W, m1);
         solve(c0, z0);
+        if (late & 2) z1 = c1.j >= 0 ? ld_cohi(zdep, c1.j) : s_zero<S>();
         solve(c1, z1);
-        z0 = n0.j >= 0 ? ld_cohi(zdep, n0.j) : s_zero<S>();
-        z1 = n1.j >= 0 ? ld_cohi(zdep, n1.j) : s_zero<S>();
+        if (!(late & 4)) z0 = n0.j >= 0 ? ld_cohi(zdep, n0.j) : s_zero<S>();
+        if (!(late & 6)) z1 = n1.j >= 0 ? ld_cohi(zdep, n1.j) : s_zero<S>();
         c0 = n0;
         c1 = n1;
         n0 = m0;
@@ -1051,12 +950,15 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> 
     }
 }
 
-// Partials of a pair launch: {||w1||^2, x^H w1} -> my_part, {||w2||^2, w1^H w2} -> pair2, each in
-// a fixed order (grid-stride per thread, block sums, last-arriver sum in block order).
+// Partials of a multi-solve launch, solve j: {||w_j||^2, w_{j-1}^H w_j} (w_{-1} = x) -> my_part
+// (j = 0) or kpart[j - 1], each in a fixed order (grid-stride per thread, block sums, last-arriver
+// sum in block order).  The solves left w_j only in their polled buffers: this kernel moves them
+// out (aux[j], the last one to B[parity]) and resets the next launch's buffers, in coalesced
+// streams.
 template <class S>
-__global__ __launch_bounds__(kThreads) void shift_pair_part_kernel(TriArgs<S> a, int parity) {
+__global__ __launch_bounds__(kThreads) void shift_multi_part_kernel(TriArgs<S> a, int parity) {
     __shared__ double sm[3 * kWaves];
-    __shared__ int s_last, s_last2;
+    __shared__ int s_last[kMaxMulti];
     __shared__ int s_go;
     __shared__ double s_nrm;
     if (threadIdx.x == 0) {
@@ -1066,28 +968,32 @@ __global__ __launch_bounds__(kThreads) void shift_pair_part_kernel(TriArgs<S> a,
     __syncthreads();
     if (!s_go) return;
     const double nrm = s_nrm;
+    const int K = a.K;
     const S* xin = parity ? a.buf0 : a.buf1;
-    S* w1 = a.aux;
-    S* w2 = parity ? a.buf1 : a.buf0;
-    double n21 = 0.0, pr = 0.0, pi = 0.0, n22 = 0.0, qr = 0.0, qi = 0.0;
-    // the solves left w1, w2 only in their polled buffers: move them out and reset the next
-    // launch's buffers here, in coalesced streams
+    S* wlast = parity ? a.buf1 : a.buf0;
+    double n2[kMaxMulti] = {}, dr[kMaxMulti] = {}, di[kMaxMulti] = {};
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kThreads) {
-        const S y1 = a.zcur[i];
-        const S y2 = a.z2cur[i];
-        w1[i] = y1;
-        w2[i] = y2;
-        a.znext[i] = sentinel<S>();
-        a.z2next[i] = sentinel<S>();
-        n21 += sq_abs(y1);
-        acc_dot(pr, pi, scale_in(xin[i], nrm), y1);
-        n22 += sq_abs(y2);
-        acc_dot(qr, qi, y1, y2);
+        S prev = scale_in(xin[i], nrm);
+#pragma unroll
+        for (int j = 0; j < kMaxMulti; ++j) {
+            if (j < K) {
+                const S y = a.zk[j][i];
+                (j == K - 1 ? wlast : a.aux[j])[i] = y;
+                a.zkn[j][i] = sentinel<S>();
+                n2[j] += sq_abs(y);
+                acc_dot(dr[j], di[j], prev, y);
+                prev = y;
+            }
+        }
     }
-    block_sum3(n21, pr, pi, sm);
-    last_arriver_reduce(n21, pr, pi, a.wave_part, a.work + 2, a.my_part, sm, &s_last);
-    block_sum3(n22, qr, qi, sm);
-    last_arriver_reduce(n22, qr, qi, a.pair_blk, a.work + 3, a.pair2, sm, &s_last2);
+#pragma unroll
+    for (int j = 0; j < kMaxMulti; ++j) {
+        if (j < K) {
+            block_sum3(n2[j], dr[j], di[j], sm);
+            last_arriver_reduce(n2[j], dr[j], di[j], j ? a.kblk + (size_t)(j - 1) * gridDim.x : a.wave_part,
+                                a.work + 2 + j, j ? a.kpart + (j - 1) : a.my_part, sm, &s_last[j]);
+        }
+    }
 }
 
 // GMRES path: the launch prologue alone (the stop decision and ||y_{t-1}||), the solve follows on
@@ -1628,8 +1534,12 @@ static void shift_free(ShiftFactor* f) {
                     f->ppiv,
                     (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
                     (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf,
-                    f->aux, f->z2[0], f->z2[1], f->pair_part, f->pair_blk})
+                    f->kpart, f->kblk})
         if (p) hipFree(p);
+    for (int j = 0; j < dev::kMaxMulti; ++j) {
+        if (j < dev::kMaxMulti - 1 && f->aux[j]) hipFree(f->aux[j]);
+        for (void* zb : f->zm[j]) if (zb) hipFree(zb);
+    }
     ctx_release(f->ctx);
     delete f;
 }
@@ -2222,32 +2132,26 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
     f->grid = std::min(f->grid, per_cu * f->ctx->num_cus);
     const int64_t units = f->tail_chunks ? (int64_t)f->nchunks - f->chunk0 : f->nslices;
     f->grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid, (units + dev::kWaves - 1) / dev::kWaves));
-    // pair launches: chunk tail with the one-wave head (or none); EIGSOL_TRSV_PAIR=0 disables
-    // (1: interleaved schedule, sptrsv_chunk_pair_kernel; 2: role split, sptrsv_chunk_role_kernel,
-    // when twice the single grid is resident; EIGSOL_TRSV_PAIR=1|2 forces one)
+    // multi-solve launches: chunk tail with the one-wave head (or none), K solves per launch
+    // (EIGSOL_TRSV_MULTI=K, 1..4; 1 = one iteration per launch) on K copies of the grid at one
+    // workgroup per CU per solve (EIGSOL_TRSV_MULTI_BLOCKS_PER_CU), when they are co-resident
     if (rc == EIGSOL_OK && f->tail_chunks && (f->hpos == 0 || f->wave_head)) {
-        const char* e = std::getenv("EIGSOL_TRSV_PAIR");
-        const int want = e ? std::atoi(e) : 2;
-        int per_cu_pair = 0, per_cu_role = 0;
+        const char* e = std::getenv("EIGSOL_TRSV_MULTI");
+        const int want = std::max(1, std::min(dev::kMaxMulti, e ? std::atoi(e) : kMultiDefault));
+        int per_cu_role = 0;
         hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu_role, reinterpret_cast<const void*>(dev::sptrsv_chunk_role_kernel<S>), dev::kThreads, 0);
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu_pair, reinterpret_cast<const void*>(dev::sptrsv_chunk_pair_kernel<S>), dev::kThreads, 0);
-        // role split: one block per CU per solve by default (config 5: 0.539 ms per iteration
-        // against 0.555 with two, the single-solve optimum; the two solves' polls share the
-        // memory system); EIGSOL_TRSV_PAIR_BLOCKS_PER_CU overrides
         int role_per_cu = 1;
-        if (const char* env = std::getenv("EIGSOL_TRSV_PAIR_BLOCKS_PER_CU")) role_per_cu = std::max(1, std::atoi(env));
+        if (const char* env = std::getenv("EIGSOL_TRSV_MULTI_BLOCKS_PER_CU")) role_per_cu = std::max(1, std::atoi(env));
         const int gr = std::min(f->grid, role_per_cu * f->ctx->num_cus);
-        const char* hc = std::getenv("EIGSOL_TRSV_PAIR_HEAD");   // seq: the two head solves one after the other
-        f->hconc = (!(hc && !std::strcmp(hc, "seq")) &&
-                    2 * (size_t)(f->hpos + 1) * sizeof(S) + 16 <= (size_t)160 * 1024) ? 1 : 0;
-        if (want == 2 && per_cu_role * f->ctx->num_cus >= 2 * gr) {
-            f->pair = 2;
-            f->grid_pair = 2 * gr;
-        } else if (want >= 1 && per_cu_pair >= 1) {
-            f->pair = 1;
-            f->grid_pair = std::min(f->grid, per_cu_pair * f->ctx->num_cus);
+        int K = want;
+        while (K > 1 && per_cu_role * f->ctx->num_cus < K * gr) --K;
+        if (K > 1) {
+            f->multi = K;
+            f->grid_multi = K * gr;
+            const char* hc = std::getenv("EIGSOL_TRSV_MULTI_HEAD");   // seq: the head solves one after another
+            f->hconc = (!(hc && !std::strcmp(hc, "seq")) &&
+                        (size_t)K * (size_t)(f->hpos + 1) * sizeof(S) + 16 <= (size_t)160 * 1024) ? 1 : 0;
         }
     }
     f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
@@ -2333,27 +2237,30 @@ int shift_error(ShiftFactor* f) {
     return EIGSOL_OK;
 }
 
-// buffers of the pair launches, allocated by the first iteration launch (plain solves, e.g. the
+// buffers of the multi-solve launches, allocated by the first iteration launch (plain solves, e.g. the
 // GMRES path's ILU(0) factors, never need them)
 template <class S>
-static int pair_alloc(ShiftFactor* f) {
-    if (f->aux) return EIGSOL_OK;
+static int multi_alloc(ShiftFactor* f) {
+    if (f->kpart) return EIGSOL_OK;
     hipStream_t st = f->ctx->stream;
     const int64_t n = f->n;
-    EIGSOL_HIP(hipMalloc(&f->aux, (size_t)std::max<int64_t>(n, 1) * sizeof(S)));
-    for (void*& zb : f->z2) {
-        EIGSOL_HIP(hipMalloc(&zb, (size_t)(n + 1) * sizeof(S)));
-        const uint32_t sent = (uint32_t)(dev::kSent & 0xffffffffu);
-        EIGSOL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st));
-        EIGSOL_HIP(hipMemsetAsync(static_cast<char*>(zb) + n * sizeof(S), 0, sizeof(S), st));
-    }
-    EIGSOL_HIP(hipMalloc(&f->pair_part, sizeof(dev::part4)));
-    EIGSOL_HIP(hipMemsetAsync(f->pair_part, 0, sizeof(dev::part4), st));
-    EIGSOL_HIP(hipMalloc(&f->pair_blk, (size_t)std::max(1, f->red_grid) * sizeof(dev::part4)));
+    const int K = f->multi;
+    for (int j = 0; j + 1 < K; ++j) EIGSOL_HIP(hipMalloc(&f->aux[j], (size_t)std::max<int64_t>(n, 1) * sizeof(S)));
+    for (int j = 1; j < K; ++j)
+        for (void*& zb : f->zm[j]) {
+            EIGSOL_HIP(hipMalloc(&zb, (size_t)(n + 1) * sizeof(S)));
+            const uint32_t sent = (uint32_t)(dev::kSent & 0xffffffffu);
+            EIGSOL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st));
+            EIGSOL_HIP(hipMemsetAsync(static_cast<char*>(zb) + n * sizeof(S), 0, sizeof(S), st));
+        }
+    EIGSOL_HIP(hipMalloc(&f->kpart, (size_t)(K - 1) * sizeof(dev::part4)));
+    EIGSOL_HIP(hipMemsetAsync(f->kpart, 0, (size_t)(K - 1) * sizeof(dev::part4), st));
+    EIGSOL_HIP(hipMalloc(&f->kblk, (size_t)(K - 1) * std::max(1, f->red_grid) * sizeof(dev::part4)));
     return EIGSOL_OK;
 }
 
-void* shift_aux(const ShiftFactor* f) { return f->aux; }
+// the final iterate of a multi-solve launch that stopped on solve j < K - 1 (final_parity 2 + j)
+void* shift_aux(const ShiftFactor* f, int j) { return (j >= 0 && j < dev::kMaxMulti - 1) ? f->aux[j] : nullptr; }
 
 template <class S>
 static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, void* buf0, void* buf1,
@@ -2434,19 +2341,25 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.wrp = static_cast<const S*>(f->wrp);
         a.wdst = f->wdst;
         a.nwpass = f->nwpass;
-        const bool pair = iter && f->pair;
+        const bool pair = iter && f->multi > 1;   // multi-solve launch
+        a.K = 1;
+        a.zk[0] = a.zcur;
+        a.zkn[0] = a.znext;
         if (pair) {
-            EIGSOL_TRY(pair_alloc<S>(f));
-            const int e2 = ++f->epoch2;
-            a.z2cur = static_cast<S*>(f->z2[e2 & 1]);
-            a.z2next = static_cast<S*>(f->z2[(e2 + 1) & 1]);
-            a.aux = static_cast<S*>(f->aux);
-            a.pair2 = static_cast<dev::part4*>(f->pair_part);
-            a.pair_blk = static_cast<dev::part4*>(f->pair_blk);
+            EIGSOL_TRY(multi_alloc<S>(f));
+            const int em = ++f->epoch_m;   // its own epoch: plain solves in between never skip a reset
+            a.K = f->multi;
+            for (int j = 1; j < f->multi; ++j) {
+                a.zk[j] = static_cast<S*>(f->zm[j][em & 1]);
+                a.zkn[j] = static_cast<S*>(f->zm[j][(em + 1) & 1]);
+            }
+            for (int j = 0; j + 1 < f->multi; ++j) a.aux[j] = static_cast<S*>(f->aux[j]);
+            a.kpart = static_cast<dev::part4*>(f->kpart);
+            a.kblk = static_cast<dev::part4*>(f->kblk);
         }
         if (f->hpos > 0 && f->wave_head && pair) {
             a.hconc = f->hconc;
-            const size_t wl = (size_t)(f->hpos + 1) * sizeof(S) * (f->hconc ? 2 : 1) + (f->hconc ? 16 : 0);
+            const size_t wl = (size_t)(f->hpos + 1) * sizeof(S) * (f->hconc ? f->multi : 1) + (f->hconc ? 16 : 0);
             const void* hk = reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, true, true>);
             EIGSOL_HIP(hipFuncSetAttribute(hk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)wl));
             hipLaunchKernelGGL((dev::sptrsv_whead_kernel<S, true, true>), dim3(1), dim3(dev::kWHeadThreads), wl, st, a,
@@ -2482,12 +2395,11 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.ppiv = static_cast<const S*>(f->ppiv);
         a.chunk0 = f->chunk0;
         a.nchunks = f->nchunks;
-        const void* tk = (pair && f->pair == 2) ? reinterpret_cast<const void*>(dev::sptrsv_chunk_role_kernel<S>)
-                         : pair ? reinterpret_cast<const void*>(dev::sptrsv_chunk_pair_kernel<S>)
+        const void* tk = pair ? reinterpret_cast<const void*>(dev::sptrsv_chunk_role_kernel<S>)
                          : !f->tail_chunks ? slice_kernel_ptr<S>(f->slice_b, iter)
                          : iter ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>)
                                 : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, false>);
-        const int tgrid = pair ? f->grid_pair : f->grid;
+        const int tgrid = pair ? f->grid_multi : f->grid;
         // EIGSOL_TRSV_NO_COOP=1: the same kernel through an ordinary launch, for profiling only
         // (rocprofv3 7.2 segfaults in its exit-time finaliser after any cooperative launch,
         // tools/coop_prof_repro.hip); the grid is one residency round, so on an otherwise idle
@@ -2496,7 +2408,7 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         if (no_coop) EIGSOL_HIP(hipLaunchKernel(tk, dim3(tgrid), dim3(dev::kThreads), kargs, 0, st));
         else EIGSOL_HIP(hipLaunchCooperativeKernel(tk, dim3(tgrid), dim3(dev::kThreads), kargs, 0, st));
         if (pair)
-            hipLaunchKernelGGL((dev::shift_pair_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a,
+            hipLaunchKernelGGL((dev::shift_multi_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a,
                                parity);
         else if (iter)   // every tail kernel publishes y in zcur (the chunk tail only there)
             hipLaunchKernelGGL((dev::shift_part_kernel<S, true>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a,
@@ -2590,7 +2502,7 @@ void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* 
         if (variant) *variant = 8;
     } else if (f->kind == 0) {
         if (bytes) *bytes = (sb + 4.0) * (double)f->nnz_total + 4.0 * (n + 1.0) + 2.0 * sb * n;
-        if (variant) *variant = f->pair ? 12 : 3;   // 12: two iterations per launch
+        if (variant) *variant = f->multi > 1 ? 10 + f->multi : 3;   // 12/13/14: 2/3/4 iterations per launch
         if (tiles) *tiles = f->nlevels;
     } else {
         if (bytes) *bytes = sb * n * n + 2.0 * sb * n;
