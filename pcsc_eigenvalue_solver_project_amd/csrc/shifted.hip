@@ -41,7 +41,7 @@ void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps);
 namespace dev {
 constexpr int kMaxMulti = 4;      // solves per multi-solve launch (one head wave each)
 }
-static constexpr int kMultiDefault = 2;   // EIGSOL_TRSV_MULTI
+static constexpr int kMultiDefault = 4;   // EIGSOL_TRSV_MULTI (config 5 per iteration: K = 1 0.674, 2 0.502, 3 0.439, 4 0.414 ms)
 
 struct ShiftFactor {
     eigsol_ctx* ctx = nullptr;
@@ -87,7 +87,7 @@ struct ShiftFactor {
     void* ppiv = nullptr;
     int32_t chunk0 = 0;
     int poll_fast = 0;            // tail polls without back-off (EIGSOL_TRSV_POLL_FAST)
-    int poll_mode = 0;            // EIGSOL_TRSV_POLL_MODE
+    int poll_mode = 2;            // EIGSOL_TRSV_POLL_MODE (bit 0: slice tail, one re-poll per lane; bit 1: chunk tails, the second chunk's first polls after the first chunk: config 5 0.698 -> 0.674 ms, K = 4 0.419 -> 0.414)
     // multi-solve launches (sptrsv_chunk_role_kernel; EIGSOL_TRSV_MULTI=K, 1 disables): K reference
     // iterations per launch, solve j one dependency round behind solve j - 1
     int multi = 1;
@@ -153,7 +153,7 @@ struct TriArgs {
     const S* ppiv;
     int32_t chunk0, nchunks;
     int32_t poll_fast;     // tail: polls re-issued without back-off
-    int32_t poll_mode;     // 0: re-poll every unsolved dependency, 1: one per lane
+    int32_t poll_mode;     // bit 0: slice tail re-polls one dependency per lane; bit 1: late second-chunk polls
     int64_t n;
     S* zcur;            // polled by this launch
     S* znext;           // reset to the sentinel by this launch, for the next one
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_slice_kernel(TriArgs<S> a, in
                 if (spins < a.poll_fast + 8) __builtin_amdgcn_s_sleep(2);
                 else __builtin_amdgcn_s_sleep(16);
             }
-            if (a.poll_mode == 0) {
+            if (!(a.poll_mode & 1)) {
 #pragma unroll
                 for (int k = 0; k < B; ++k)
                     if (unready(z[k])) z[k] = ld_cohi(a.zcur, col[k]);
@@ -807,6 +807,8 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
     fetch2(c1);
     fetch1(gw + 2 * W, n0);
     fetch1(gw + 3 * W, n1);
+    // EIGSOL_TRSV_POLL_MODE bit 1: the second chunk's first polls after the first chunk is solved
+    const int late = a.poll_mode & 2;
     S z0 = c0.j >= 0 ? ld_cohi(a.zcur, c0.j) : s_zero<S>();
     S z1 = c1.j >= 0 ? ld_cohi(a.zcur, c1.j) : s_zero<S>();
     for (int c = gw; c < a.nchunks; c += 2 * W) {
@@ -816,9 +818,10 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
         fetch1(c + 4 * W, m0);
         fetch1(c + 5 * W, m1);
         solve(c0, z0);
+        if (late) z1 = c1.j >= 0 ? ld_cohi(a.zcur, c1.j) : s_zero<S>();
         solve(c1, z1);
         z0 = n0.j >= 0 ? ld_cohi(a.zcur, n0.j) : s_zero<S>();
-        z1 = n1.j >= 0 ? ld_cohi(a.zcur, n1.j) : s_zero<S>();
+        if (!late) z1 = n1.j >= 0 ? ld_cohi(a.zcur, n1.j) : s_zero<S>();
         c0 = n0;
         c1 = n1;
         n0 = m0;

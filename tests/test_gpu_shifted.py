@@ -133,6 +133,200 @@ def test_triu_complex_parity_config5_class(ctx):
     sess.close()
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_dense_parity(ctx, dtype):
+    rng = np.random.default_rng(3)
+    n = 120
+    A = rng.standard_normal((n, n))
+    if dtype == np.complex128:
+        A = A + 1j * rng.standard_normal((n, n))
+    A = A + np.diag(np.arange(n, dtype=float))            # well separated eigenvalues
+    ev = np.linalg.eigvals(A)
+    tgt = ev[np.argmin(np.abs(ev - 40.3))]
+    sigma = (tgt + 0.05) if dtype == np.complex128 else float(np.real(tgt)) + 0.05
+    x0 = S.start_vector(n, dtype)
+    res = E.shifted_inverse_power_method(E.DenseMatrix(ctx, A.astype(dtype)),
+                                         E.ShiftedSolverOptions(500, 1e-12, sigma), x0)
+    ref = O.shifted_dense(A.astype(dtype), sigma, x0, 500, 1e-12, want_trace=True)
+    _parity(res, ref, 1e-12)
+
+
+def test_lower_triangular_and_general_sparse(ctx):
+    rng = np.random.default_rng(5)
+    n = 400
+    # lower triangular f64 with a real diagonal: eigenvalues are the diagonal
+    d = rng.uniform(1, 2, n)
+    d[123] = 3.5
+    L = sp.tril(sp.random(n, n, density=0.02, random_state=6), k=-1) * 0.1 + sp.diags(d)
+    L = L.tocsr()
+    x0 = S.start_vector(n)
+    res = E.shifted_inverse_power_method(E.CsrMatrix.from_scipy(ctx, L), E.ShiftedSolverOptions(300, 1e-12, 3.49), x0)
+    ref = O.shifted_dense(L.toarray(), 3.49, x0, 300, 1e-12, want_trace=True)
+    _parity(res, ref, 1e-12)
+    assert abs(res.eigenvalue - 3.5) <= 1e-9
+    # general (non-triangular) sparse: densified on the device, LU with partial pivoting
+    G = (sp.random(n, n, density=0.03, random_state=7) + sp.diags(np.arange(n, dtype=float))).tocsr()
+    ev = np.linalg.eigvals(G.toarray())
+    tgt = float(np.real(ev[np.argmin(np.abs(ev - 200.2))]))
+    res = E.shifted_inverse_power_method(E.CsrMatrix.from_scipy(ctx, G), E.ShiftedSolverOptions(300, 1e-12, tgt + 0.03), x0)
+    ref = O.shifted_dense(G.toarray(), tgt + 0.03, x0, 300, 1e-12, want_trace=True)
+    _parity(res, ref, 1e-12)
+
+
+def test_sparse_zero_pivot_fails_like_sparselu(ctx):
+    A = sp.csr_matrix(np.triu(np.array([[2.0, 1.0, 0.0], [0.0, 3.0, 1.0], [0.0, 0.0, 4.0]])))
+    with pytest.raises(E.EigSolError) as ei:
+        E.solve_shifted(E.CsrMatrix.from_scipy(ctx, A), 3.0, np.ones(3))
+    assert ei.value.status == 6 and "SparseLU" in str(ei.value)
+
+
+def test_solve_shifted_triangular_large(ctx):
+    n = 50000
+    rp, ci, v, _ = S.triu_complex(n, 16, seed=9)
+    rng = np.random.default_rng(1)
+    b = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+    sigma = 0.3 + 0.1j
+    x = E.solve_shifted(E.CsrMatrix(ctx, rp, ci, v, (n, n)), sigma, b)
+    xr = O.triu_shifted_solve_csr(rp, ci, v, sigma, b)
+    assert np.linalg.norm(x - xr) <= 1e-10 * np.linalg.norm(xr)
+    A = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    r = A @ x - sigma * x - b
+    assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(b)
+
+
+def test_session_rebegin_after_early_exit_launches(ctx):
+    """Launches enqueued after convergence exit early; they must still hand the next launch a
+    clean solve buffer (the solved values are the ready flags), so a second begin on the same
+    session reproduces a fresh one."""
+    n = 5000
+    rp, ci, v, _ = S.triu_complex(n, 16, seed=3)
+    target = 1.5 * np.exp(0.7j)
+    sigma = target + 2e-3
+    M = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sess = E.ShiftedSession(M, sigma)
+    opts = E.ShiftedSolverOptions(200, 1e-12, sigma)
+    results = []
+    for seed in (1, 2, 1):
+        x0 = S.start_vector(n, np.complex128, seed=seed)
+        sess.begin(opts, x0)
+        sess.step(60)                                     # far past convergence: no-op launches
+        assert sess.query()[0]
+        results.append(sess.finish())
+        ref = O.shifted_triu_csr(rp, ci, v, sigma, x0, 200, 1e-12, want_trace=True)
+        _parity(results[-1], ref, 1e-12)
+    assert results[0].eigenvalue == results[2].eigenvalue   # deterministic reductions
+    assert results[0].iterations == results[2].iterations
+    np.testing.assert_array_equal(results[0].eigenvector, results[2].eigenvector)
+    sess.close()
+
+
+@pytest.mark.parametrize("upper", [True, False])
+def test_solve_shifted_long_rows(ctx, upper):
+    """Rows longer than one 16-lane pass (up to 200 off-diagonal entries), both orientations."""
+    rng = np.random.default_rng(11)
+    n = 3000
+    rows, cols = [], []
+    for i in range(n):
+        k = int(rng.integers(0, 200)) if i % 7 == 0 else int(rng.integers(0, 12))
+        span = (n - 1 - i) if upper else i
+        k = min(k, span)
+        if k:
+            off = rng.choice(span, size=k, replace=False)
+            cols.append((i + 1 + off) if upper else off)
+            rows.append(np.full(k, i))
+    r = np.concatenate(rows + [np.arange(n)])
+    c = np.concatenate(cols + [np.arange(n)])
+    vals = rng.uniform(-1, 1, len(r)) * 0.02
+    vals[-n:] = rng.uniform(1, 2, n)
+    A = sp.csr_matrix((vals, (r, c)), shape=(n, n))
+    A.sort_indices()
+    b = rng.standard_normal(n)
+    x = E.solve_shifted(E.CsrMatrix.from_scipy(ctx, A), 0.25, b)
+    Ad = A.toarray() - 0.25 * np.eye(n)
+    xr = np.linalg.solve(Ad, b)
+    assert np.linalg.norm(x - xr) <= 1e-11 * np.linalg.norm(xr)
+
+
+def test_solve_shifted_nan_payloads_do_not_stall(ctx):
+    """A right-hand side carrying NaNs, one with the exact bit pattern the solver uses for
+    'not yet solved', still drains: NaN propagates to the dependent rows, the rest is exact."""
+    n = 2000
+    d = np.linspace(1.0, 2.0, n)
+    A = sp.diags([d, np.full(n - 1, 0.1)], [0, 1], format="csr")   # upper bidiagonal
+    b = np.ones(n)
+    sent = np.array([0x7FF4DEAD7FF4DEAD], dtype=np.uint64).view(np.float64)[0]
+    b[1000] = sent
+    b[1500] = np.nan
+    x = E.solve_shifted(E.CsrMatrix.from_scipy(ctx, A), 0.0, b)
+    # row i depends on rows > i: rows <= 1500 see a NaN, rows > 1500 are finite and exact
+    assert np.all(np.isnan(x[:1501]))
+    bb = b.copy()
+    bb[:1501] = 0.0
+    xr = np.linalg.solve(A.toarray(), bb)
+    np.testing.assert_allclose(x[1501:], xr[1501:], rtol=1e-13)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_dense_solve_shifted_blocked_lu(ctx, dtype):
+    """Blocked LU (panels of 64 real / 32 complex columns, MFMA trailing update) on a matrix that
+    needs row interchanges in every panel, with a ragged last panel: backward-stable residual
+    ||(A - sigma I) x - b|| <= 1e-12 ||A|| ||x|| n, and x against LAPACK (numpy.linalg.solve)."""
+    rng = np.random.default_rng(11)
+    n = 1000
+    A = rng.standard_normal((n, n))
+    if dtype == np.complex128:
+        A = A + 1j * rng.standard_normal((n, n))
+    A = A.astype(dtype)
+    sigma = 0.25 if dtype == np.float64 else 0.25 - 0.5j
+    b = rng.standard_normal(n).astype(dtype)
+    x = E.solve_shifted(E.DenseMatrix(ctx, A), sigma, b)
+    M = A - sigma * np.eye(n)
+    r = np.linalg.norm(M @ x - b)
+    assert r <= 1e-12 * n * np.linalg.norm(M, 2) * np.linalg.norm(x), r
+    xr = np.linalg.solve(M, b)
+    assert np.linalg.norm(x - xr) <= (1e-13 * np.linalg.cond(M) + 1e-12) * np.linalg.norm(xr)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_dense_multi_cu_substitution_matches_single_cu(ctx, dtype, monkeypatch):
+    """Dense factors above 2048 rows use the multi-CU block-row substitution (epoch flags, one
+    persistent workgroup per CU): the shifted inverse iteration must reproduce the single-CU
+    substitution's result (EIGSOL_DENSE_TRSV_SINGLE_MAX forces it) to 1e-10, and solve_shifted
+    must be backward stable."""
+    rng = np.random.default_rng(21)
+    n = 3000
+    A = rng.standard_normal((n, n))
+    if dtype == np.complex128:
+        A = A + 1j * rng.standard_normal((n, n))
+    A = (A / np.sqrt(n) + np.diag(np.linspace(1.0, 4.0, n))).astype(dtype)
+    sigma = 2.501 if dtype == np.float64 else 2.501 + 0.01j
+    x0 = S.start_vector(n, dtype)
+    opts = E.ShiftedSolverOptions(300, 1e-12, sigma)
+    multi = E.shifted_inverse_power_method(E.DenseMatrix(ctx, A), opts, x0)
+    monkeypatch.setenv("EIGSOL_DENSE_TRSV_SINGLE_MAX", str(n))
+    single = E.shifted_inverse_power_method(E.DenseMatrix(ctx, A), opts, x0)
+    monkeypatch.delenv("EIGSOL_DENSE_TRSV_SINGLE_MAX")
+    assert multi.converged and single.converged
+    assert abs(multi.eigenvalue - single.eigenvalue) <= 1e-10 * (1 + abs(single.eigenvalue))
+    assert abs(multi.iterations - single.iterations) <= 1
+    assert abs(np.vdot(multi.eigenvector, single.eigenvector)) >= 1 - 1e-10
+    b = rng.standard_normal(n).astype(dtype)
+    x = E.solve_shifted(E.DenseMatrix(ctx, A), sigma, b)
+    M = A - sigma * np.eye(n)
+    assert np.linalg.norm(M @ x - b) <= 1e-12 * n * np.linalg.norm(M, 2) * np.linalg.norm(x)
+
+
+def test_dense_shifted_above_single_cu_limit(ctx):
+    """n = 20000 f64 (3.2 GB): beyond the former single-CU LDS limit (18432); residual check."""
+    rng = np.random.default_rng(5)
+    n = 20000
+    A = rng.standard_normal((n, n)) / np.sqrt(n) + np.eye(n) * 3.0
+    b = rng.standard_normal(n)
+    x = E.solve_shifted(E.DenseMatrix(ctx, A), 0.5, b)
+    r = A @ x - 0.5 * x - b
+    assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(b)
+
+
 def _triu_run(ctx, monkeypatch, K, n, x0, opts, sigma, seed=42, trace=64):
     """K reference iterations per launch (EIGSOL_TRSV_MULTI; 1 = one per launch)."""
     monkeypatch.setenv("EIGSOL_TRSV_MULTI", str(int(K)))
