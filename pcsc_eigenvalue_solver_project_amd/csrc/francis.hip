@@ -435,7 +435,7 @@ __device__ __forceinline__ int wave_max_int(int v) {
 template <bool kSchur, int NX>
 __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double* wr, double* wi, int* bs,
                          int& fail, int& total, int& maxsw, int* steps_out = nullptr, double spk = -1.0,
-                         int* stop = nullptr) {
+                         int* stop = nullptr, double dtol = 2.220446049250313e-16) {
     const int lane = threadIdx.x & 63;
     auto T = [&](int i, int j) -> double& { return t[i + j * LD]; };
     auto V = [&](int i, int j) -> double& { return v[i + j * LD]; };
@@ -452,7 +452,7 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
         for (int l = 1 + lane; l <= nn; l += 64) {
             const double s0 = fabs(T(l - 1, l - 1)) + fabs(T(l, l));
             const double h = T(l, l - 1);
-            if (h == 0.0 || fabs(h) <= eps * s0) lm = l;    // ascending per lane: the last is the max
+            if (h == 0.0 || fabs(h) <= dtol * s0) lm = l;   // ascending per lane: the last is the max
         }
         const int l = __builtin_amdgcn_readfirstlane(wave_max_int(lm));
         EIGSOL_LDS_ORDER();
@@ -636,8 +636,10 @@ __device__ void wave_hqr(double* t, double* v, int n, int LD, int maxits, double
 constexpr int kHqrWaveMax = 128;
 
 // eigenvalues of an n x n (n <= 128) Hessenberg block: info = {fail, most sweeps per deflation, total}
+// dtol: relative subdiagonal below which the block splits (eps: LAPACK's test; the sweeps' shifts
+// are computed with a looser one, EIGSOL_QR_SHIFT_TOL)
 __global__ __launch_bounds__(64) void hqr_wave_kernel(const double* Hin, int64_t ld, int n, double* wr, double* wi,
-                                                      int maxits, int* info) {
+                                                      int maxits, int* info, double dtol) {
     constexpr int LD = kHqrWaveMax + 1;
     __shared__ double t[kHqrWaveMax * LD];
     for (int e = threadIdx.x; e < n * n; e += 64) {
@@ -646,8 +648,8 @@ __global__ __launch_bounds__(64) void hqr_wave_kernel(const double* Hin, int64_t
     }
     __syncthreads();
     int fail, total, maxsw;
-    if (n <= 64) wave_hqr<false, 1>(t, nullptr, n, LD, maxits, wr, wi, nullptr, fail, total, maxsw);
-    else wave_hqr<false, 2>(t, nullptr, n, LD, maxits, wr, wi, nullptr, fail, total, maxsw);
+    if (n <= 64) wave_hqr<false, 1>(t, nullptr, n, LD, maxits, wr, wi, nullptr, fail, total, maxsw, nullptr, -1.0, nullptr, dtol);
+    else wave_hqr<false, 2>(t, nullptr, n, LD, maxits, wr, wi, nullptr, fail, total, maxsw, nullptr, -1.0, nullptr, dtol);
     if (threadIdx.x == 0) {
         info[0] = fail;
         info[1] = maxsw;
@@ -848,13 +850,13 @@ __global__ void zero_entry_kernel(double* H, int64_t n, int i, int j) { H[i + (i
 // eigenvalues of an n <= 128 Hessenberg block in LDS: the one-wave solver (EIGSOL_HQR_WAVE=0: the
 // workgroup solver of qr.hip, for A/B)
 static int hqr_small(hipStream_t st, const double* H, int64_t ld, int n, int maxits, double* wr, double* wi,
-                     int* info) {
+                     int* info, double dtol = 2.220446049250313e-16) {
     static const bool wave = [] {
         const char* e = std::getenv("EIGSOL_HQR_WAVE");
         return !e || std::atoi(e) != 0;
     }();
     if (!wave) return hqr_lds(st, H, ld, n, maxits, wr, wi, info);
-    hipLaunchKernelGGL(dev::hqr_wave_kernel, dim3(1), dim3(64), 0, st, H, ld, n, wr, wi, maxits, info);
+    hipLaunchKernelGGL(dev::hqr_wave_kernel, dim3(1), dim3(64), 0, st, H, ld, n, wr, wi, maxits, info, dtol);
     EIGSOL_HIP(hipGetLastError());
     return EIGSOL_OK;
 }
@@ -909,6 +911,12 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     static const bool aed_early = [] {
         const char* e = std::getenv("EIGSOL_QR_AED_EARLY");
         return !e || std::atoi(e) != 0;
+    }();
+    // the shifts' QR splits at a looser relative subdiagonal than the eigenvalues' (shifts need no
+    // full accuracy); EIGSOL_QR_SHIFT_TOL
+    static const double shift_tol = [] {
+        const char* e = std::getenv("EIGSOL_QR_SHIFT_TOL");
+        return e ? std::max(2.220446049250313e-16, std::atof(e)) : 2.220446049250313e-16;
     }();
     static const int kNibble = [] {   // % of the AED window deflated that skips the sweep (LAPACK's NIBBLE)
         const char* e = std::getenv("EIGSOL_QR_NIBBLE");
@@ -1004,7 +1012,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             ns = 2 * nb;
             // shifts: eigenvalues of the trailing 2nb x 2nb block
             rc = hqr_small(st, H + (ihi - ns + 1) + (int64_t)(ihi - ns + 1) * n, n, ns, 60, dwr + ihi - ns + 1,
-                           dwi + ihi - ns + 1, dinfo);
+                           dwi + ihi - ns + 1, dinfo, shift_tol);
             if (rc != EIGSOL_OK) break;
             if (hipMemcpyAsync(swr.data(), dwr + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipMemcpyAsync(swi.data(), dwi + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
