@@ -306,24 +306,32 @@ struct WinGemmBatch {
 };
 constexpr int kUP = kWin + 2;   // LDS pitch of U and of the left panel: (k + 2 i) mod 32 distinct for 32 lanes
 
-template <bool kLeft>
+// kTile columns (left) / rows (right) of the off-window region per workgroup.  64: each wave owns
+// 16 of them and all six 16-row tiles of U; 32: waves (w & 1) own 16 of them and (w >> 1) three of
+// the six U tiles, so twice as many workgroups share a launch's MFMA work (a launch covers only a
+// few thousand columns, fewer workgroups than CUs at 64).  The k order of every output element is
+// the same for both tilings (bitwise the same updates).
+template <bool kLeft, int kTile = 64>
 __global__ __launch_bounds__(256) void win_gemm_mfma(WinGemmBatch b) {
+    constexpr int kT = kTile == 64 ? 6 : 3;                // U row tiles per wave
     __shared__ double us[kWin * kUP];                    // us[k + rho * kUP] = U(k, rho)
-    __shared__ double xs[kLeft ? 64 * kUP : 1];          // left: xs[k + c * kUP] = H(s + k, c0 + c)
+    __shared__ double xs[kLeft ? kTile * kUP : 1];       // left: xs[k + c * kUP] = H(s + k, c0 + c)
     int g = 0;
 #pragma unroll
     for (int q = 1; q < kMaxGroups + 1; ++q)
         if (q < b.nw && (int)blockIdx.x >= b.w[q].blk0) g = q;
     const WinGemm w = b.w[g];
     const int W = w.W;
-    const int64_t base = w.lo + (int64_t)((int)blockIdx.x - w.blk0) * 64;
-    const int cnt = (int)min<int64_t>(64, w.hi - base);
+    const int64_t base = w.lo + (int64_t)((int)blockIdx.x - w.blk0) * kTile;
+    const int cnt = (int)min<int64_t>(kTile, w.hi - base);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, lk = lane >> 4;
+    const int ct = kTile == 64 ? wave : (wave & 1);      // this wave's 16 columns / rows of the tile
+    const int t0 = kTile == 64 ? 0 : 3 * (wave >> 1);    // ... and its first U row tile
     // right: this lane's X(r_j, k) for k = lk, lk + 4, ... (issued first, consumed last)
     constexpr int kKs = kWin / 4;
     double xv[kLeft ? 1 : kKs];
-    const int rj = 16 * wave + li;
+    const int rj = 16 * ct + li;
     const bool rv = rj < cnt;
     if constexpr (!kLeft) {
         const double* xr = b.H + (base + min(rj, max(cnt - 1, 0))) + (int64_t)w.s * b.n;
@@ -344,7 +352,7 @@ __global__ __launch_bounds__(256) void win_gemm_mfma(WinGemmBatch b) {
             tu[q] = w.U[min(k, W - 1) + min(rho, W - 1) * W];
         }
         if constexpr (kLeft) {
-            constexpr int kPX = kWin * 64 / 256;
+            constexpr int kPX = kWin * kTile / 256;
             double tx[kPX];
 #pragma unroll
             for (int q = 0; q < kPX; ++q) {
@@ -367,46 +375,46 @@ __global__ __launch_bounds__(256) void win_gemm_mfma(WinGemmBatch b) {
         }
     }
     __syncthreads();
-    dbl4 acc[6];
+    dbl4 acc[kT];
 #pragma unroll
-    for (int t = 0; t < 6; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < kT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
     if constexpr (kLeft) {
-        // D[i][j] = sum_k X(k, c_i) U(k, rho_j): i = column 16 wave + i, j = row 16 t + j
-        const double* xc = xs + (16 * wave + li) * kUP;
+        // D[i][j] = sum_k X(k, c_i) U(k, rho_j): i = column 16 ct + i, j = row 16 (t0 + t) + j
+        const double* xc = xs + (16 * ct + li) * kUP;
 #pragma unroll
         for (int q = 0; q < kKs; ++q) {     // rows k >= W of both LDS images are zero
             const int k = 4 * q + lk;
             const double av = xc[k];
-            double bv[6];
+            double bv[kT];
 #pragma unroll
-            for (int t = 0; t < 6; ++t) bv[t] = us[k + (16 * t + li) * kUP];
+            for (int t = 0; t < kT; ++t) bv[t] = us[k + (16 * (t0 + t) + li) * kUP];
 #pragma unroll
-            for (int t = 0; t < 6; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], acc[t], 0, 0, 0);
+            for (int t = 0; t < kT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[t], acc[t], 0, 0, 0);
         }
 #pragma unroll
-        for (int t = 0; t < 6; ++t)
+        for (int t = 0; t < kT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int c = 16 * wave + lk + 4 * r, rho = 16 * t + li;
+                const int c = 16 * ct + lk + 4 * r, rho = 16 * (t0 + t) + li;
                 if (c < cnt && rho < W) b.H[(w.s + rho) + (base + c) * b.n] = acc[t][r];
             }
     } else {
-        // D[i][j] = sum_k U(k, rho_i) X(r_j, k): i = output column rho, j = row 16 wave + j
+        // D[i][j] = sum_k U(k, rho_i) X(r_j, k): i = output column rho, j = row 16 ct + j
 #pragma unroll
         for (int q = 0; q < kKs; ++q) {
             const int k = 4 * q + lk;
             const double bv = (rv && k < W) ? xv[q] : 0.0;
-            double av[6];
+            double av[kT];
 #pragma unroll
-            for (int t = 0; t < 6; ++t) av[t] = us[k + (16 * t + li) * kUP];
+            for (int t = 0; t < kT; ++t) av[t] = us[k + (16 * (t0 + t) + li) * kUP];
 #pragma unroll
-            for (int t = 0; t < 6; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv, acc[t], 0, 0, 0);
+            for (int t = 0; t < kT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t], bv, acc[t], 0, 0, 0);
         }
 #pragma unroll
-        for (int t = 0; t < 6; ++t)
+        for (int t = 0; t < kT; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int rho = 16 * t + lk + 4 * r;
+                const int rho = 16 * (t0 + t) + lk + 4 * r;
                 if (rv && rho < W) b.H[(base + rj) + (int64_t)(w.s + rho) * b.n] = acc[t][r];
             }
     }
@@ -918,6 +926,13 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         const char* e = std::getenv("EIGSOL_QR_SHIFT_TOL");
         return e ? std::max(2.220446049250313e-16, std::atof(e)) : 2.220446049250313e-16;
     }();
+    // window-GEMM tile (EIGSOL_QR_GEMM_TILE = 32 | 64; default: 32 when a launch's 64-wide tiles
+    // would not cover the CUs)
+    static const int gemm_tile = [] {
+        const char* e = std::getenv("EIGSOL_QR_GEMM_TILE");
+        const int v = e ? std::atoi(e) : 0;
+        return (v == 32 || v == 64) ? v : 0;
+    }();
     static const int kNibble = [] {   // % of the AED window deflated that skips the sweep (LAPACK's NIBBLE)
         const char* e = std::getenv("EIGSOL_QR_NIBBLE");
         return e ? std::max(1, std::atoi(e)) : 30;
@@ -1104,23 +1119,35 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             st_windows += nwin;
             st_steps += t1 - t0;
             hipLaunchKernelGGL(dev::chase_wave_kernel, dim3(nwin), dim3(1024), 0, st, ca);
-            // delayed updates: every left region, then every right region
+            // delayed updates: every left region, then every right region; tiles of gemm_tile
+            // columns / rows per workgroup (32 when 64-wide tiles would leave CUs idle)
             dev::WinGemmBatch lb{H, n, 0, {}}, rb{H, n, 0, {}};
-            int nlb = 0, nrb = 0;
+            int nlb = 0, nrb = 0, span = 0;
+            for (int q = 0; q < nwin; ++q) {
+                const dev::ChaseWin& w = ca.w[q];
+                if (w.e <= ihi) span += ihi + 1 - w.e;
+                if (w.s > l) span += w.s - l;
+            }
+            const int tile = gemm_tile > 0 ? gemm_tile : (span / 64 < ctx->num_cus ? 32 : 64);
             for (int q = 0; q < nwin; ++q) {
                 const dev::ChaseWin& w = ca.w[q];
                 const int W = w.e - w.s;
                 if (w.e <= ihi) {
                     lb.w[lb.nw++] = dev::WinGemm{w.s, W, (int64_t)w.e, (int64_t)ihi + 1, nlb, w.U};
-                    nlb += (ihi + 1 - w.e + 63) / 64;
+                    nlb += (ihi + 1 - w.e + tile - 1) / tile;
                 }
                 if (w.s > l) {
                     rb.w[rb.nw++] = dev::WinGemm{w.s, W, (int64_t)l, (int64_t)w.s, nrb, w.U};
-                    nrb += (w.s - l + 63) / 64;
+                    nrb += (w.s - l + tile - 1) / tile;
                 }
             }
-            if (nlb > 0) hipLaunchKernelGGL(dev::win_gemm_mfma<true>, dim3(nlb), dim3(256), 0, st, lb);
-            if (nrb > 0) hipLaunchKernelGGL(dev::win_gemm_mfma<false>, dim3(nrb), dim3(256), 0, st, rb);
+            if (tile == 32) {
+                if (nlb > 0) hipLaunchKernelGGL((dev::win_gemm_mfma<true, 32>), dim3(nlb), dim3(256), 0, st, lb);
+                if (nrb > 0) hipLaunchKernelGGL((dev::win_gemm_mfma<false, 32>), dim3(nrb), dim3(256), 0, st, rb);
+            } else {
+                if (nlb > 0) hipLaunchKernelGGL(dev::win_gemm_mfma<true>, dim3(nlb), dim3(256), 0, st, lb);
+                if (nrb > 0) hipLaunchKernelGGL(dev::win_gemm_mfma<false>, dim3(nrb), dim3(256), 0, st, rb);
+            }
             t0 = t1;
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "francis: launch"); break; }
