@@ -418,3 +418,23 @@ def test_multi_head_concurrent_matches_sequential(ctx, monkeypatch, K):
     assert conc.iterations == seq.iterations and conc.eigenvalue == seq.eigenvalue
     np.testing.assert_array_equal(tc, ts)
     np.testing.assert_array_equal(conc.eigenvector, seq.eigenvector)
+
+
+@pytest.mark.parametrize("K", [1, 4])
+def test_multi_launches_without_head(ctx, monkeypatch, K):
+    """A factor with no narrow leading levels (one 5000-row level: no head kernel) on either
+    launch shape: the eigenvalue nearest the shift, exactly, and the same iteration count."""
+    monkeypatch.setenv("EIGSOL_TRSV_MULTI", str(K))
+    n = 5000
+    rng = np.random.default_rng(11)
+    d = rng.uniform(1.0, 2.0, n) * np.exp(1j * rng.uniform(0, 2 * np.pi, n))
+    d[1234] = 0.5 + 0.25j
+    A = sp.csr_matrix(sp.diags(d))
+    M = E.CsrMatrix.from_scipy(ctx, A)
+    x0 = S.start_vector(n, np.complex128, seed=3)
+    res = E.shifted_inverse_power_method(M, E.ShiftedSolverOptions(100, 1e-12, 0.5 + 0.26j), x0)
+    ref = O.shifted_triu_csr(A.indptr.astype(np.int32), A.indices.astype(np.int32), A.data.astype(np.complex128),
+                             0.5 + 0.26j, x0, 100, 1e-12, want_trace=True)
+    assert res.converged and abs(res.eigenvalue - (0.5 + 0.25j)) <= 1e-12
+    assert abs(res.iterations - ref["iterations"]) <= 1
+    assert abs(np.vdot(res.eigenvector, ref["eigenvector"])) >= 1 - 1e-10
