@@ -2248,17 +2248,20 @@ static int multi_alloc(ShiftFactor* f) {
     hipStream_t st = f->ctx->stream;
     const int64_t n = f->n;
     const int K = f->multi;
-    for (int j = 0; j + 1 < K; ++j) EIGSOL_HIP(hipMalloc(&f->aux[j], (size_t)std::max<int64_t>(n, 1) * sizeof(S)));
+    // buffer by buffer, so that a call after a failed allocation resumes instead of leaking
+    for (int j = 0; j + 1 < K; ++j)
+        if (!f->aux[j]) EIGSOL_HIP(hipMalloc(&f->aux[j], (size_t)std::max<int64_t>(n, 1) * sizeof(S)));
     for (int j = 1; j < K; ++j)
         for (void*& zb : f->zm[j]) {
+            if (zb) continue;
             EIGSOL_HIP(hipMalloc(&zb, (size_t)(n + 1) * sizeof(S)));
             const uint32_t sent = (uint32_t)(dev::kSent & 0xffffffffu);
             EIGSOL_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st));
             EIGSOL_HIP(hipMemsetAsync(static_cast<char*>(zb) + n * sizeof(S), 0, sizeof(S), st));
         }
-    EIGSOL_HIP(hipMalloc(&f->kpart, (size_t)(K - 1) * sizeof(dev::part4)));
+    if (!f->kblk) EIGSOL_HIP(hipMalloc(&f->kblk, (size_t)(K - 1) * std::max(1, f->red_grid) * sizeof(dev::part4)));
+    EIGSOL_HIP(hipMalloc(&f->kpart, (size_t)(K - 1) * sizeof(dev::part4)));   // last: marks the set complete
     EIGSOL_HIP(hipMemsetAsync(f->kpart, 0, (size_t)(K - 1) * sizeof(dev::part4), st));
-    EIGSOL_HIP(hipMalloc(&f->kblk, (size_t)(K - 1) * std::max(1, f->red_grid) * sizeof(dev::part4)));
     return EIGSOL_OK;
 }
 
