@@ -466,6 +466,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
     __shared__ S ysum[16][kCoopRowsPerLane * 64];
     __shared__ S red[kCoopBlocks * NB];   // gathered block partials
     __shared__ S sv[NB], sw[NB], st[NB];
+    __shared__ S Tl[NB * NB];   // this block's copy of T (every block forms each column from the same sums)
     __shared__ S s_scal[3];
     __shared__ double s_rv;
     __shared__ int s_sk;
@@ -491,6 +492,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
     const int R = (n + G - 1) / G;
     const int r0 = blockIdx.x * R, r1 = min(n, r0 + R);
     unsigned target = 0;
+    for (int e = tid; e < NB * NB; e += kCoopThreads) Tl[e] = s_zero<S>();
     for (int i = 0; i < a.nbp; ++i) {
         const int j = k + i;
         // ---------------- P1
@@ -521,7 +523,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
         gather(a.part, i, sw);
         if (tid < i) {
             S s = s_zero<S>();
-            for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(ld_ag(&a.T[c + tid * NB])), sw[c]));   // (T^H w)_tid
+            for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(Tl[c + tid * NB]), sw[c]));   // (T^H w)_tid
             st[tid] = s;
         }
         __syncthreads();
@@ -591,7 +593,16 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
         }
         grid_barrier(a.bar, target, a.err);
         // ---------------- P4
-        for (int r = tid; r < n; r += kCoopThreads) vsh[r] = sk ? s_zero<S>() : ld_ag(&a.V[r + (int64_t)i * n]);
+        // v into LDS: four independent coherent loads per thread in flight (clamped rows, so no
+        // predicated load waits for the one before it)
+        for (int rb = tid; rb < n; rb += 4 * kCoopThreads) {
+            S t4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t4[u] = ld_ag(&a.V[min(rb + u * kCoopThreads, n - 1) + (int64_t)i * n]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (rb + u * kCoopThreads < n) vsh[rb + u * kCoopThreads] = sk ? s_zero<S>() : t4[u];
+        }
         __syncthreads();
         gather(a.part + (size_t)G * NB, i, sv);
         if (sk && tid < i) sv[tid] = s_zero<S>();
@@ -644,15 +655,18 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
                     a.Y[r + (int64_t)i * n] = sk ? s_zero<S>() : two_x(y);
                 }
             }
-        if (blockIdx.x == 0 && tid <= i) {
+        // T column i in every block, from the LDS copy and the gathered sums (the same values and
+        // order in every block); block 0 also publishes it for the trailing update
+        if (tid <= i) {
             S tc;
             set_re_im(tc, 2.0, 0.0);
             if (tid < i) {
                 S s = s_zero<S>();
-                for (int q = tid; q < i; ++q) s = add(s, mul(ld_ag(&a.T[tid + q * NB]), sv[q]));
+                for (int q = tid; q < i; ++q) s = add(s, mul(Tl[tid + q * NB], sv[q]));
                 tc = neg2(s);
             }
-            st_ag(&a.T[tid + i * NB], tc);
+            Tl[tid + i * NB] = tc;
+            if (blockIdx.x == 0) a.T[tid + i * NB] = tc;
         }
         __syncthreads();
     }
