@@ -62,11 +62,11 @@ inline constexpr bool DeviceScalar = std::is_same_v<S, double> || std::is_same_v
 // in single precision, norm/dot partials in double).  The other solvers (dense and general-sparse
 // shifted inverse, solve_shifted on a non-triangular matrix, Hessenberg, QR) promote the matrix,
 // vectors and shift to double on the host and round the results back (a deliberate deviation:
-// fp64 arithmetic, at least as accurate as the reference's single precision).  long double and
-// std::complex<long double> (WideScalar) run on the fp64 kernels too: the GPU has no 80-bit
-// arithmetic, so the matrix, vectors and shift are rounded to double on the host, the device
-// computes in double, and the results are widened back — a documented precision deviation (53-bit
-// against x87's 64-bit significand; identical behaviour for tolerances above ~1e-15).
+// fp64 arithmetic, at least as accurate as the reference's single precision).
+// long double and std::complex<long double> (WideScalar) run on the device in double-double
+// (EIGSOL_DD / EIGSOL_CDD, a 106-bit significand against the x87 format's 64): values cross the C
+// ABI as exact {hi, lo} double pairs (to_wire below), so nothing is rounded on the way in; the
+// results come back rounded to the nearest long double.
 template <typename S>
 inline constexpr bool PromotedScalar = std::is_same_v<S, float> || std::is_same_v<S, std::complex<float>>;
 template <typename S>
@@ -79,10 +79,6 @@ template <>
 struct device_scalar<float> { using type = double; };
 template <>
 struct device_scalar<std::complex<float>> { using type = std::complex<double>; };
-template <>
-struct device_scalar<long double> { using type = double; };
-template <>
-struct device_scalar<std::complex<long double>> { using type = std::complex<double>; };
 template <typename S>
 using device_scalar_t = typename device_scalar<S>::type;
 
@@ -90,6 +86,46 @@ template <typename S>
 struct real_of { using type = S; };
 template <typename R>
 struct real_of<std::complex<R>> { using type = R; };
+
+// ------------------------------------------------------------------ double-double wire format
+// long double (x87: 64-bit significand) as the unevaluated sum of two doubles.  hi = v rounded to
+// double, lo = v - hi (exact in long double, at most 11 significant bits): exact for every finite
+// v inside the double exponent range; beyond it the conversion throws instead of rounding.
+struct DDWire {
+    double hi, lo;
+};
+struct CDDWire {
+    DDWire re, im;
+};
+inline DDWire to_wire(long double v) {
+    const double hi = static_cast<double>(v);
+    if (std::isfinite(v) && !std::isfinite(hi))
+        throw std::runtime_error("EigSol: long double value outside the double-double range (|v| >= 1.8e308)");
+    return DDWire{hi, static_cast<double>(v - static_cast<long double>(hi))};
+}
+inline CDDWire to_wire(const std::complex<long double>& v) { return CDDWire{to_wire(v.real()), to_wire(v.imag())}; }
+inline long double from_wire(const DDWire& w) { return static_cast<long double>(w.hi) + static_cast<long double>(w.lo); }
+inline std::complex<long double> from_wire(const CDDWire& w) {
+    return std::complex<long double>(from_wire(w.re), from_wire(w.im));
+}
+template <typename S>
+struct wire_of { using type = S; };
+template <>
+struct wire_of<long double> { using type = DDWire; };
+template <>
+struct wire_of<std::complex<long double>> { using type = CDDWire; };
+template <typename S>
+using wire_t = typename wire_of<S>::type;
+template <typename S>
+std::vector<wire_t<S>> to_wire_vec(const S* v, std::size_t n) {
+    if constexpr (std::is_same_v<wire_t<S>, S>) {
+        return std::vector<S>(v, v + n);   // the device types travel as they are
+    } else {
+        std::vector<wire_t<S>> w(n);
+        for (std::size_t i = 0; i < n; ++i) w[i] = to_wire(v[i]);
+        return w;
+    }
+}
 
 // ------------------------------------------------------------------------------------- Vector
 template <typename S>

@@ -31,12 +31,15 @@ inline void check(int status, const char* what) {
 template <typename S>
 constexpr eigsol_dtype dtype_of() {
     static_assert(std::is_same_v<S, double> || std::is_same_v<S, std::complex<double>> ||
-                      std::is_same_v<S, float> || std::is_same_v<S, std::complex<float>>,
-                  "the device path supports double, float and their complex types");
+                      std::is_same_v<S, float> || std::is_same_v<S, std::complex<float>> ||
+                      std::is_same_v<S, long double> || std::is_same_v<S, std::complex<long double>>,
+                  "the device path supports double, float, long double and their complex types");
     if constexpr (std::is_same_v<S, double>) return EIGSOL_F64;
     else if constexpr (std::is_same_v<S, std::complex<double>>) return EIGSOL_C128;
     else if constexpr (std::is_same_v<S, float>) return EIGSOL_F32;
-    else return EIGSOL_C64;
+    else if constexpr (std::is_same_v<S, std::complex<float>>) return EIGSOL_C64;
+    else if constexpr (std::is_same_v<S, long double>) return EIGSOL_DD;   // double-double on the wire
+    else return EIGSOL_CDD;
 }
 
 class Context {

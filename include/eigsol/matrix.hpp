@@ -54,7 +54,7 @@ struct SparseTriplets {
 template <typename S>
 inline constexpr bool has_device_storage_v =
     std::is_same_v<S, double> || std::is_same_v<S, float> || std::is_same_v<S, std::complex<double>> ||
-    std::is_same_v<S, std::complex<float>>;
+    std::is_same_v<S, std::complex<float>> || WideScalar<S>;   // long double: double-double on the device
 
 class Matrix {
 public:
@@ -79,16 +79,22 @@ public:
         box_cast<SparseMatrix<S>>().makeCompressed();
     }
 
-    // Triplets straight to the device.  Scalars without device storage (long
-    // double), or a process without a usable device, take the host route (insert + compress);
-    // the solvers then report the missing device on first use, as for any other Matrix.
+    // Triplets straight to the device.  A process without a usable device takes
+    // the host route (insert + compress); the solvers then report the missing device on first use,
+    // as for any other Matrix.
     template <ScalarConcept S>
     explicit Matrix(SparseTriplets<S>&& t) : dense_(false), scalar_(&typeid(S)), rows_(t.rows), cols_(t.cols) {
         if constexpr (has_device_storage_v<S>) {
             try {
-                dev_ = detail::DeviceMatrix::coo(detail::dtype_of<S>(), t.rows, t.cols,
-                                                 static_cast<std::int64_t>(t.val.size()), t.row.data(),
-                                                 t.col.data(), t.val.data());
+                const std::int64_t nnz = static_cast<std::int64_t>(t.val.size());
+                if constexpr (WideScalar<S>) {   // exact double-double pairs
+                    const std::vector<wire_t<S>> w = to_wire_vec(t.val.data(), t.val.size());
+                    dev_ = detail::DeviceMatrix::coo(detail::dtype_of<S>(), t.rows, t.cols, nnz, t.row.data(),
+                                                     t.col.data(), w.data());
+                } else {
+                    dev_ = detail::DeviceMatrix::coo(detail::dtype_of<S>(), t.rows, t.cols, nnz, t.row.data(),
+                                                     t.col.data(), t.val.data());
+                }
                 type_ = &typeid(SparseMatrix<S>);
                 materialise_ = &Matrix::host_from_device<S>;
                 return;
@@ -149,7 +155,7 @@ public:
     std::int64_t cols() const { return box_ ? visit([](const auto& m) { return m.cols(); }) : cols_; }
 
     // Device mirror (created on first use by the solvers) in the storage's own precision
-    // (double, float and their complex types all have device storage).
+    // (double, float, long double and their complex types all have device storage).
     template <typename S>
     const detail::DeviceMatrix& device() const {
         if (!dev_) dev_ = upload<S, S>();
@@ -182,11 +188,14 @@ private:
         std::int64_t r = 0, c = 0, nnz = 0;
         detail::check(eigsol_csr_info(d.csr(), &r, &c, &nnz, nullptr), "eigsol_csr_info");
         std::vector<std::int32_t> rp(r + 1), ci(nnz);
-        std::vector<S> v(nnz);
+        std::vector<wire_t<S>> v(nnz);
         detail::check(eigsol_csr_download(d.csr(), rp.data(), ci.data(), v.data()), "eigsol_csr_download");
         SparseMatrix<S> s(r, c);
         for (std::int64_t i = 0; i < r; ++i)
-            for (std::int32_t e = rp[i]; e < rp[i + 1]; ++e) s.insert(i, ci[e]) = v[e];
+            for (std::int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+                if constexpr (WideScalar<S>) s.insert(i, ci[e]) = from_wire(v[e]);
+                else s.insert(i, ci[e]) = v[e];
+            }
         s.makeCompressed();
         return std::make_unique<BoxTyped<SparseMatrix<S>>>(std::move(s));
     }
@@ -216,6 +225,17 @@ private:
     template <typename S, typename D>
     std::shared_ptr<detail::DeviceMatrix> upload() const {
         materialise();
+        if constexpr (WideScalar<S>) {   // long double: exact double-double pairs (core.hpp, to_wire)
+            if (dense_) {
+                const auto& d = cast<DenseMatrix<S>>();
+                const auto w = to_wire_vec(d.data(), static_cast<std::size_t>(d.size()));
+                return detail::DeviceMatrix::dense(detail::dtype_of<S>(), d.rows(), d.cols(), w.data());
+            }
+            const auto& sm = cast<SparseMatrix<S>>();
+            const auto w = to_wire_vec(sm.valuePtr(), static_cast<std::size_t>(sm.nonZeros()));
+            return detail::DeviceMatrix::csc(detail::dtype_of<S>(), sm.rows(), sm.cols(), sm.nonZeros(),
+                                             sm.outerIndexPtr(), sm.innerIndexPtr(), w.data());
+        }
         if (dense_) {
             const auto& d = cast<DenseMatrix<S>>();
             if constexpr (std::is_same_v<D, S>) {

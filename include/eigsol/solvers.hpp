@@ -10,8 +10,9 @@
 //
 // Scalars: double and std::complex<double> natively; float and std::complex<float> natively for the
 // power method and the triangular-CSR shifted inverse, promoted to fp64 for the other solvers
-// (core.hpp, PromotedScalar); long double / std::complex<long double> run on the fp64 kernels
-// (core.hpp, WideScalar).
+// (core.hpp, PromotedScalar); long double / std::complex<long double> in double-double on the
+// device (core.hpp, WideScalar: every solver; qr_eigenvalues runs the reference's unshifted
+// iteration for them).
 //
 // Start vector: the reference draws x0 with Eigen's Vector::Random (std::rand, not reproducible
 // across Eigen versions).  Here x0 comes from a documented generator
@@ -129,6 +130,31 @@ DenseMatrix<T> convert_dense(const DenseMatrix<U>& a) {
     return b;
 }
 
+// long double: the same run with the vectors, the shift and the results as double-double pairs
+template <typename S>
+int power_run_wide(const DeviceMatrix& d, bool dense, const eigsol_solver_options& o, const Vector<S>& xs0,
+                   const S* shift, EigenResult<S>& out) {
+    using Wt = wire_t<S>;
+    const std::vector<Wt> xw = to_wire_vec(xs0.data(), xs0.size());
+    const Wt sh = shift ? to_wire(*shift) : to_wire(S(0));
+    Wt lam{};
+    std::vector<Wt> x(xs0.size());
+    std::int32_t it = 0, conv = 0;
+    int st;
+    if (shift)
+        st = dense ? eigsol_shifted_inverse_dense(d.dense(), &sh, &o, xw.data(), &lam, x.data(), &it, &conv)
+                   : eigsol_shifted_inverse_csr(d.csr(), &sh, &o, xw.data(), &lam, x.data(), &it, &conv);
+    else
+        st = dense ? eigsol_power_dense(d.dense(), &o, xw.data(), &lam, x.data(), &it, &conv)
+                   : eigsol_power_csr(d.csr(), &o, xw.data(), &lam, x.data(), &it, &conv);
+    if (st == EIGSOL_OK) {
+        Vector<S> xs(x.size());
+        for (std::size_t i = 0; i < x.size(); ++i) xs(i) = from_wire(x[i]);
+        out = EigenResult<S>(from_wire(lam), xs, it, conv != 0);
+    }
+    return st;
+}
+
 // One device run in scalar type D (S itself, or its fp64 promotion).
 template <typename D, typename S>
 int power_run(const DeviceMatrix& d, bool dense, const eigsol_solver_options& o, const Vector<S>& xs0,
@@ -167,8 +193,8 @@ EigenResult<S> power_like(const Matrix& M, const SolverOptions& opts, const Vect
         // triangular factors); only a general sparse pattern with neither a usable band nor a dense
         // factor that fits (ILU(0)-GMRES, double-only) is promoted to fp64
         int st = EIGSOL_E_UNSUPPORTED;
-        if constexpr (WideScalar<S>) {   // long double: the fp64 kernels (see core.hpp)
-            st = power_run<device_scalar_t<S>>(M.device_fp64<S>(), M.isDense(), o, xs0, shift, res);
+        if constexpr (WideScalar<S>) {   // long double: double-double kernels (see core.hpp)
+            st = power_run_wide<S>(M.device<S>(), M.isDense(), o, xs0, shift, res);
         } else {
             st = power_run<S>(M.device<S>(), M.isDense(), o, xs0, shift, res);
         }
@@ -235,8 +261,15 @@ Vector<S> solve_shifted(const Matrix& A, const S shift, const Vector<S>& b) {
         // single precision natively (dense, banded and triangular factors in float); the fp64
         // factor only where the single-precision one is not built (general sparse via GMRES)
         int st = EIGSOL_E_UNSUPPORTED;
-        if constexpr (WideScalar<S>) {
-            st = run(device_scalar_t<S>{}, A.device_fp64<S>());
+        if constexpr (WideScalar<S>) {   // double-double pairs in and out
+            const detail::DeviceMatrix& d = A.device<S>();
+            const wire_t<S> sh = to_wire(shift);
+            const auto bw = to_wire_vec(b.data(), b.size());
+            std::vector<wire_t<S>> xw(b.size());
+            st = A.isDense() ? eigsol_solve_shifted_dense(d.dense(), &sh, bw.data(), n, xw.data())
+                             : eigsol_solve_shifted_csr(d.csr(), &sh, bw.data(), n, xw.data());
+            if (st == EIGSOL_OK)
+                for (std::size_t i = 0; i < xw.size(); ++i) x(i) = from_wire(xw[i]);
         } else {
             st = run(S{}, A.device<S>());
         }
@@ -252,9 +285,17 @@ template <ScalarConcept S>
 DenseMatrix<S> to_hessenberg_dense(const DenseMatrix<S>& A) {
     detail::dense_square_check(A, "to_hessenberg_dense");
     detail::require_device_scalar<S>("to_hessenberg_dense");
-    if constexpr (WideScalar<S>)
-        return detail::convert_dense<S>(to_hessenberg_dense(detail::convert_dense<device_scalar_t<S>>(A)));
     DenseMatrix<S> H(A.rows(), A.cols());
+    if constexpr (WideScalar<S>) {   // double-double reflectors
+        if (A.rows() > 0) {
+            const auto aw = to_wire_vec(A.data(), static_cast<std::size_t>(A.size()));
+            std::vector<wire_t<S>> hw(aw.size());
+            detail::check(eigsol_hessenberg_dense(detail::ctx(), detail::dtype_of<S>(), A.rows(), aw.data(), hw.data()),
+                          "to_hessenberg_dense");
+            for (std::size_t i = 0; i < hw.size(); ++i) H.data()[i] = from_wire(hw[i]);
+        }
+        return H;
+    }
     if constexpr (DeviceScalar<S> || PromotedScalar<S>) {   // single precision: native float reduction
         if (A.rows() > 0)
             detail::check(eigsol_hessenberg_dense(detail::ctx(), detail::dtype_of<S>(), A.rows(), A.data(), H.data()),
@@ -274,12 +315,16 @@ template <ScalarConcept S>
 void qr_decompose_dense(const DenseMatrix<S>& A, DenseMatrix<S>& Q, DenseMatrix<S>& R) {
     if (A.rows() == 0 || A.cols() == 0) throw std::runtime_error("qr_decompose_dense: empty matrix");
     detail::require_device_scalar<S>("qr_decompose_dense");
-    if constexpr (WideScalar<S>) {
-        using D = device_scalar_t<S>;
-        DenseMatrix<D> Qd, Rd;
-        qr_decompose_dense<D>(detail::convert_dense<D>(A), Qd, Rd);
-        Q = detail::convert_dense<S>(Qd);
-        R = detail::convert_dense<S>(Rd);
+    if constexpr (WideScalar<S>) {   // double-double reflectors
+        const auto aw = to_wire_vec(A.data(), static_cast<std::size_t>(A.size()));
+        std::vector<wire_t<S>> qw(static_cast<std::size_t>(A.rows() * A.rows())), rw(aw.size());
+        detail::check(eigsol_qr_decompose_dense(detail::ctx(), detail::dtype_of<S>(), A.rows(), A.cols(), aw.data(),
+                                                qw.data(), rw.data()),
+                      "qr_decompose_dense");
+        Q = DenseMatrix<S>(A.rows(), A.rows());
+        R = DenseMatrix<S>(A.rows(), A.cols());
+        for (std::size_t i = 0; i < qw.size(); ++i) Q.data()[i] = from_wire(qw[i]);
+        for (std::size_t i = 0; i < rw.size(); ++i) R.data()[i] = from_wire(rw[i]);
         return;
     }
     Q = DenseMatrix<S>(A.rows(), A.rows());
@@ -306,9 +351,25 @@ QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& o
     const std::int64_t n = A.rows();
     if (n == 0) return QRResult<S>(Vector<S>(), 0, true);   // qr_eigenvalues.hpp:55-57
     detail::require_device_scalar<S>("qr_eigenvalues_dense");
+    if constexpr (WideScalar<S>) {
+        // long double: the reference's own algorithm (unshifted H <- R Q, qr_eigenvalues.hpp:62-105)
+        // in double-double, for either variant: the multishift sweeps are fp64 kernels, and running
+        // them would round the matrix to double
+        (void)variant;
+        const auto aw = to_wire_vec(A.data(), static_cast<std::size_t>(A.size()));
+        std::vector<wire_t<S>> ew(static_cast<std::size_t>(n));
+        std::int32_t it = 0, conv = 0;
+        const eigsol_solver_options o = detail::copts(opts);
+        detail::check(eigsol_qr_eigenvalues_dense(detail::ctx(), detail::dtype_of<S>(), n, aw.data(), &o,
+                                                  EIGSOL_QR_UNSHIFTED, ew.data(), nullptr, &it, &conv),
+                      "qr_eigenvalues_dense");
+        Vector<S> ev(static_cast<std::size_t>(n));
+        for (std::int64_t i = 0; i < n; ++i) ev(i) = from_wire(ew[static_cast<std::size_t>(i)]);
+        return QRResult<S>(ev, it, conv != 0);
+    }
     // single precision: the reference's unshifted iteration natively in float; the Francis sweeps
     // (double kernels) on the fp64 promotion, eigenvalues rounded back
-    if constexpr (WideScalar<S> || PromotedScalar<S>) if (WideScalar<S> || variant == QRVariant::Francis) {
+    if constexpr (PromotedScalar<S>) if (variant == QRVariant::Francis) {
         using D = device_scalar_t<S>;
         const QRResult<D> rd = qr_eigenvalues_dense<D>(detail::convert_dense<D>(A), opts, variant);
         QRResult<S> rs(detail::convert_vec<S>(rd.eigenvalues), rd.iterations, rd.converged);

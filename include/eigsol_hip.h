@@ -20,7 +20,8 @@
  *
  * Scalars: EIGSOL_F64 = double, EIGSOL_C128 = std::complex<double> / double _Complex
  * (interleaved re, im), EIGSOL_F32 = float, EIGSOL_C64 = std::complex<float> (single-precision
- * paths listed at eigsol_dtype).  Dense storage is column-major (Matrix::Dense is an Eigen col-major
+ * paths listed at eigsol_dtype), EIGSOL_DD / EIGSOL_CDD = long double / std::complex<long double>
+ * carried as double-double (see eigsol_dtype).  Dense storage is column-major (Matrix::Dense is an Eigen col-major
  * matrix, matrix.hpp:39-40).  Sparse storage is CSR with int32 indices on the device; the CSC
  * constructor accepts the reference's canonical Eigen::SparseMatrix<S> (ColMajor, int) layout
  * (matrix.hpp:43-44).
@@ -56,8 +57,24 @@ typedef enum eigsol_status {
 /* EIGSOL_F32 / EIGSOL_C64: float and std::complex<float> (ScalarConcept, types.hpp:28-30), stored
  * and multiplied in single precision on the device (CSR / dense power iteration, plain SpMV/GEMV,
  * triangular-CSR shifted inverse).  Other solvers accept only F64 / C128 (the C++ façade promotes
- * float input for those). */
-typedef enum eigsol_dtype { EIGSOL_F64 = 0, EIGSOL_C128 = 1, EIGSOL_F32 = 2, EIGSOL_C64 = 3 } eigsol_dtype;
+ * float input for those).
+ * EIGSOL_DD / EIGSOL_CDD: long double and std::complex<long double> (types.hpp:28-30; the x87
+ * 80-bit format, 64-bit significand, under g++ on x86-64).  A value is a double-double: two doubles
+ * {hi, lo} whose unevaluated sum is the value, |lo| <= ulp(hi)/2 (106-bit significand); complex
+ * values are {re.hi, re.lo, im.hi, im.lo}.  Every finite long double inside the double exponent
+ * range converts exactly (hi = (double)v, lo = (double)(v - hi)).  Computed in double-double on the
+ * device: CSR / dense products, the power method, the shifted inverse and solve_shifted (the fp64
+ * factor of A - sigma I refined to double-double accuracy by residuals computed in double-double),
+ * to_hessenberg, qr_decompose and the reference's unshifted qr_eigenvalues; the Francis variant
+ * (fp64 kernels) and the row-sharded path return EIGSOL_E_UNSUPPORTED. */
+typedef enum eigsol_dtype {
+    EIGSOL_F64 = 0,
+    EIGSOL_C128 = 1,
+    EIGSOL_F32 = 2,
+    EIGSOL_C64 = 3,
+    EIGSOL_DD = 4,
+    EIGSOL_CDD = 5
+} eigsol_dtype;
 
 /* SolverOptions (src/option/solver_option.hpp:14-20). */
 typedef struct eigsol_solver_options {
@@ -163,7 +180,11 @@ int eigsol_power_kernel_name(eigsol_power* s, char* buf, size_t capacity);
  *          6 = CSR one row per lane (single-precision fallback layout);
  *          7 = shifted inverse, ILU(0)-preconditioned GMRES (general sparse; bytes and tiles of the
  *              last solve: algorithmic bytes of all its steps, Arnoldi steps);
- *          8 = shifted inverse, RCM-banded direct LU (general sparse; tiles = kl + ku) */
+ *          8 = shifted inverse, RCM-banded direct LU (general sparse; tiles = kl + ku);
+ *          15 = double-double CSR product (EIGSOL_DD / EIGSOL_CDD power method, one row per lane);
+ *          16 = double-double dense GEMV (row tiles x column chunks);
+ *          17 = double-double shifted inverse: fp64 factor + residual refinement in double-double
+ *               (tiles = refinement steps of the last solve, bytes = all of its passes) */
 
 /* ---------------------------------------------------------------- shifted inverse iteration
  * shiftedInversePowerMethod<S>(M, ShiftedSolverOptions<S>{sigma, maxIter, tol})

@@ -78,6 +78,22 @@ def lib():
             f.restype = _int
         L.orc_hqr_francis_f64.argtypes = [_i64, _p, _p, _p]
         L.orc_hqr_francis_f64.restype = _int
+        # long double / std::complex<long double> (x87): the same restatements at extended precision
+        for sfx in ("f80", "c80"):
+            getattr(L, "orc_spmv_csc_" + sfx).argtypes = [_i64, _i64, _p, _p, _p, _p, _p]
+            getattr(L, "orc_spmv_csr_" + sfx).argtypes = [_i64, _p, _p, _p, _p, _p]
+            getattr(L, "orc_gemv_" + sfx).argtypes = [_i64, _i64, _p, _p, _p]
+            for name, args in (("power_csc_", [_i64, _p, _p, _p, _p, _int, _dbl, _p, _p, _p, _p]),
+                               ("power_dense_", [_i64, _p, _p, _int, _dbl, _p, _p, _p, _p]),
+                               ("shifted_triu_csr_", [_i64, _p, _p, _p, _p, _p, _int, _dbl, _p, _p, _p, _p]),
+                               ("shifted_dense_", [_i64, _p, _p, _p, _int, _dbl, _p, _p, _p, _p]),
+                               ("qr_eigenvalues_", [_i64, _p, _int, _dbl, _p, _p])):
+                f = getattr(L, "orc_" + name + sfx)
+                f.argtypes = args
+                f.restype = _int
+            getattr(L, "orc_solve_shifted_dense_" + sfx).argtypes = [_i64, _p, _p, _p, _p]
+            getattr(L, "orc_hessenberg_" + sfx).argtypes = [_i64, _p, _p]
+            getattr(L, "orc_qr_decompose_" + sfx).argtypes = [_i64, _i64, _p, _p, _p]
         _lib = L
     return _lib
 
@@ -90,8 +106,13 @@ def _is_c(dt) -> bool:
     return np.dtype(dt) == np.complex128
 
 
+def _wide(dt) -> bool:
+    """long double / std::complex<long double> (numpy longdouble is the x87 80-bit format here)."""
+    return np.dtype(dt) in (np.dtype(np.longdouble), np.dtype(np.clongdouble))
+
+
 _SFX = {np.dtype(np.float64): "f64", np.dtype(np.complex128): "c128", np.dtype(np.float32): "f32",
-        np.dtype(np.complex64): "c64"}
+        np.dtype(np.complex64): "c64", np.dtype(np.longdouble): "f80", np.dtype(np.clongdouble): "c80"}
 
 
 def _sfx(dt) -> str:
@@ -141,7 +162,7 @@ def gemv(A, x):
 def _result(lam, x, iters, conv, trace):
     it = int(iters.value)
     return {
-        "eigenvalue": lam[0] if np.iscomplexobj(lam) else float(lam[0]),
+        "eigenvalue": lam[0] if (np.iscomplexobj(lam) or _wide(lam.dtype)) else float(lam[0]),
         "eigenvector": x,
         "iterations": it,
         "converged": bool(conv),
@@ -192,7 +213,10 @@ def solve_shifted_dense(A, shift, b):
     n = A.shape[0]
     Af, bb = _fortran(A, dt), _vec(b, dt)
     x = np.empty(n, dtype=dt)
-    if _is_c(dt):
+    if _wide(dt):
+        s = np.array([shift], dtype=dt)
+        getattr(lib(), "orc_solve_shifted_dense_" + _sfx(dt))(n, _ptr(Af), _ptr(s), _ptr(bb), _ptr(x))
+    elif _is_c(dt):
         s = np.array([complex(shift).real, complex(shift).imag])
         lib().orc_solve_shifted_dense_c128(n, _ptr(Af), _ptr(s), _ptr(bb), _ptr(x))
     else:
@@ -210,7 +234,11 @@ def shifted_dense(A, shift, x0, max_iterations=1000, tolerance=1e-10, want_trace
     it = C.c_int(0)
     tr = np.zeros(max(max_iterations, 1), dtype=dt) if want_trace else None
     trp = None if tr is None else _ptr(tr)
-    if _is_c(dt):
+    if _wide(dt):
+        s = np.array([shift], dtype=dt)
+        conv = getattr(lib(), "orc_shifted_dense_" + _sfx(dt))(n, _ptr(Af), _ptr(s), _ptr(xx), int(max_iterations),
+                                                              float(tolerance), _ptr(lam), _ptr(x), C.byref(it), trp)
+    elif _is_c(dt):
         s = np.array([complex(shift).real, complex(shift).imag])
         conv = lib().orc_shifted_dense_c128(n, _ptr(Af), _ptr(s), _ptr(xx), int(max_iterations),
                                             float(tolerance), _ptr(lam), _ptr(x), C.byref(it), trp)
@@ -231,7 +259,7 @@ def shifted_triu_csr(rowptr, colidx, vals, shift, x0, max_iterations=1000, toler
     it = C.c_int(0)
     tr = np.zeros(max(max_iterations, 1), dtype=dt) if want_trace else None
     trp = None if tr is None else _ptr(tr)
-    if _single(dt):
+    if _single(dt) or _wide(dt):
         s = np.array([shift], dtype=dt)
         conv = getattr(lib(), "orc_shifted_triu_csr_" + _sfx(dt))(
             n, _ptr(rp), _ptr(ci), _ptr(v), _ptr(s), _ptr(xx), int(max_iterations), float(tolerance), _ptr(lam),

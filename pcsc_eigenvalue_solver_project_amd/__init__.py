@@ -14,8 +14,8 @@ from typing import Optional
 
 import numpy as np
 
-from ._capi import (EIGSOL_C64, EIGSOL_C128, EIGSOL_F32, EIGSOL_E_SIZE_MISMATCH, EIGSOL_F64, EigSolError, SolverOptionsC, call, check, last_error,
-                    lib)
+from ._capi import (EIGSOL_C64, EIGSOL_C128, EIGSOL_CDD, EIGSOL_DD, EIGSOL_E_INVALID, EIGSOL_E_SIZE_MISMATCH, EIGSOL_F32,
+                    EIGSOL_F64, EigSolError, SolverOptionsC, call, check, last_error, lib)
 
 __all__ = [
     "EigSolError", "SolverOptions", "EigenResult", "Context", "CsrMatrix", "DenseMatrix",
@@ -54,15 +54,75 @@ def _dtype_code(dt) -> int:
         return EIGSOL_F32
     if dt == np.complex64:
         return EIGSOL_C64
-    raise EigSolError(3, f"scalar type mismatch: {dt} (supported: float64, complex128, float32, complex64)")
+    if dt == np.longdouble:
+        return EIGSOL_DD
+    if dt == np.clongdouble:
+        return EIGSOL_CDD
+    raise EigSolError(3, f"scalar type mismatch: {dt} (supported: float64, complex128, float32, complex64, "
+                         "longdouble, clongdouble)")
 
 
 def _np_dtype(code: int):
-    return {EIGSOL_C128: np.complex128, EIGSOL_F32: np.float32, EIGSOL_C64: np.complex64}.get(code, np.float64)
+    return {EIGSOL_C128: np.complex128, EIGSOL_F32: np.float32, EIGSOL_C64: np.complex64,
+            EIGSOL_DD: np.longdouble, EIGSOL_CDD: np.clongdouble}.get(code, np.float64)
 
 
 def _ptr(a: np.ndarray) -> C.c_void_p:
     return a.ctypes.data_as(C.c_void_p)
+
+
+def is_wide(dtype) -> bool:
+    """long double / std::complex<long double>: crosses the C ABI as double-double pairs."""
+    return np.dtype(dtype) in (np.dtype(np.longdouble), np.dtype(np.clongdouble))
+
+
+def to_wire(a, dtype) -> np.ndarray:
+    """Host scalars of ``dtype`` in the C ABI's layout (a contiguous buffer, flattened in C order).
+    long double values become exact double-double pairs {hi = (double) v, lo = (double)(v - hi)}:
+    the x87 64-bit significand fits in hi's 53 bits plus lo's 11, so nothing is rounded."""
+    a = np.ascontiguousarray(a, dtype=dtype)
+    if not is_wide(dtype):
+        return a
+    flat = a.reshape(-1)
+    parts = [flat.real, flat.imag] if np.iscomplexobj(flat) else [flat]
+    cols = []
+    for p in parts:
+        with np.errstate(over="ignore"):
+            hi = p.astype(np.float64)
+        if np.any(np.isinf(hi) & np.isfinite(p)):
+            raise EigSolError(EIGSOL_E_INVALID, "long double value outside the double exponent range "
+                                                "(double-double carries |v| < 1.8e308)")
+        lo = (p - hi.astype(np.longdouble)).astype(np.float64)
+        cols += [hi, lo]
+    return np.ascontiguousarray(np.stack(cols, axis=-1))
+
+
+def wire_buffer(dtype, n: int) -> np.ndarray:
+    """Output buffer for n scalars of ``dtype`` in the C ABI's layout."""
+    if not is_wide(dtype):
+        return np.empty(max(n, 0), dtype=dtype)
+    return np.zeros((max(n, 0), 4 if np.dtype(dtype) == np.clongdouble else 2), dtype=np.float64)
+
+
+def from_wire(w: np.ndarray, dtype) -> np.ndarray:
+    """Inverse of to_wire (double-double hi + lo rounded to the nearest long double)."""
+    if not is_wide(dtype):
+        return w
+    w = np.asarray(w, dtype=np.float64).reshape(-1, 4 if np.dtype(dtype) == np.clongdouble else 2)
+    re = w[:, 0].astype(np.longdouble) + w[:, 1].astype(np.longdouble)
+    if np.dtype(dtype) == np.longdouble:
+        return re
+    z = np.empty(len(w), dtype=np.clongdouble)
+    z.real = re
+    z.imag = w[:, 2].astype(np.longdouble) + w[:, 3].astype(np.longdouble)
+    return z
+
+
+def _scalar(v, dtype):
+    """eigenvalue as a Python / numpy scalar (long double kept at its precision)."""
+    if is_wide(dtype):
+        return v
+    return complex(v) if np.iscomplexobj(v) else float(v)
 
 
 def _vector(v, dtype, n: int, what: str) -> np.ndarray:
@@ -70,7 +130,7 @@ def _vector(v, dtype, n: int, what: str) -> np.ndarray:
     v = np.ascontiguousarray(v, dtype=dtype).reshape(-1)
     if len(v) != n:
         raise EigSolError(EIGSOL_E_SIZE_MISMATCH, f"{what} has {len(v)} entries, the matrix has {n} rows")
-    return v
+    return to_wire(v, dtype)
 
 
 def device_count() -> int:
@@ -142,7 +202,8 @@ class CsrMatrix:
                               f"values ({len(values)}) and index array ({len(idx)}) lengths differ")
         h = C.c_void_p()
         fn = "eigsol_csr_create" if layout == "csr" else "eigsol_csr_create_from_csc"
-        call(fn, ctx.handle, code, nrows, ncols, len(idx), _ptr(ptr), _ptr(idx), _ptr(values), C.byref(h))
+        vw = to_wire(values, values.dtype)
+        call(fn, ctx.handle, code, nrows, ncols, len(idx), _ptr(ptr), _ptr(idx), _ptr(vw), C.byref(h))
         self.ctx, self.handle = ctx, h
         self.shape = (nrows, ncols)
         self.nnz = len(idx)
@@ -171,8 +232,9 @@ class CsrMatrix:
             raise EigSolError(EIGSOL_E_SIZE_MISMATCH,
                               f"triplet arrays differ in length ({len(r)}, {len(c)}, {len(values)})")
         h = C.c_void_p()
+        vw = to_wire(values, values.dtype)
         call("eigsol_csr_create_from_coo", ctx.handle, code, int(shape[0]), int(shape[1]), len(r), _ptr(r),
-             _ptr(c), _ptr(values), C.byref(h))
+             _ptr(c), _ptr(vw), C.byref(h))
         self = cls.__new__(cls)
         self.ctx, self.handle = ctx, h
         self.shape = (int(shape[0]), int(shape[1]))
@@ -186,9 +248,9 @@ class CsrMatrix:
         """(rowptr, colidx, values) of the device CSR (``eigsol_csr_download``)."""
         rp = np.empty(self.shape[0] + 1, np.int32)
         ci = np.empty(self.nnz, np.int32)
-        v = np.empty(self.nnz, self.dtype)
+        v = wire_buffer(self.dtype, self.nnz)
         call("eigsol_csr_download", self.handle, _ptr(rp), _ptr(ci), _ptr(v))
-        return rp, ci, v
+        return rp, ci, from_wire(v, self.dtype)
 
     def spmv(self, x_dev: int, y_dev: int) -> None:
         call("eigsol_csr_spmv", self.handle, C.c_void_p(x_dev), C.c_void_p(y_dev))
@@ -211,7 +273,7 @@ class DenseMatrix:
     def __init__(self, ctx: Context, A: np.ndarray):
         A = np.asarray(A)
         code = _dtype_code(A.dtype)
-        Af = np.asfortranarray(A)
+        Af = to_wire(np.asfortranarray(A).ravel(order="F"), A.dtype)   # column-major
         h = C.c_void_p()
         call("eigsol_dense_create", ctx.handle, code, A.shape[0], A.shape[1], _ptr(Af), C.byref(h))
         self.ctx, self.handle = ctx, h
@@ -264,19 +326,19 @@ class PowerSession:
         return bool(done.value), int(launches.value)
 
     def finish(self, want_vector: bool = True) -> EigenResult:
-        lam = np.zeros(1, dtype=self.dtype)
-        x = np.empty(self.n, dtype=self.dtype) if want_vector else None
+        lam = wire_buffer(self.dtype, 1)
+        x = wire_buffer(self.dtype, self.n) if want_vector else None
         it, conv = C.c_int32(0), C.c_int32(0)
         call("eigsol_power_finish", self.handle, _ptr(lam), None if x is None else _ptr(x), 0,
              C.byref(it), C.byref(conv))
-        ev = complex(lam[0]) if np.iscomplexobj(lam) else float(lam[0])
-        return EigenResult(ev, x, int(it.value), bool(conv.value))
+        ev = _scalar(from_wire(lam, self.dtype)[0], self.dtype)
+        return EigenResult(ev, None if x is None else from_wire(x, self.dtype), int(it.value), bool(conv.value))
 
     def trace(self, capacity: int) -> np.ndarray:
-        buf = np.zeros(max(capacity, 1), dtype=self.dtype)
+        buf = wire_buffer(self.dtype, max(capacity, 1))
         cnt = C.c_int32(0)
         call("eigsol_power_trace", self.handle, _ptr(buf), int(capacity), C.byref(cnt))
-        return buf[: cnt.value]
+        return from_wire(buf, self.dtype)[: cnt.value]
 
     def transport(self) -> int:
         """EIGSOL_TRANSPORT_LOCAL / _COLLECTIVE / _PEER (per-iteration exchange of this session)."""
@@ -303,7 +365,11 @@ class PowerSession:
                  13: "sptrsv multi-solve kernel (sync-free triangular solves, 3 iterations per launch, "
                      "solve j one dependency round behind solve j-1)",
                  14: "sptrsv multi-solve kernel (sync-free triangular solves, 4 iterations per launch, "
-                     "solve j one dependency round behind solve j-1)"}
+                     "solve j one dependency round behind solve j-1)",
+                 15: "wide spmv_kernel (double-double CSR product, one row per lane)",
+                 16: "wide gemv kernels (double-double dense product)",
+                 17: "wide shifted inverse (fp64 factor + double-double residual refinement; "
+                     "tiles = refinement steps of the last solve)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?"),
                 "iterations_per_launch": v.value - 10 if 12 <= v.value <= 14 else 1}
@@ -334,14 +400,14 @@ def power_method(matrix, opts: SolverOptions = SolverOptions(), x0=None) -> Eige
         if np.issubdtype(matrix.dtype, np.complexfloating):
             x0 = x0 + 1j * rng.uniform(-1, 1, matrix.shape[0])
     x0 = _vector(x0, matrix.dtype, matrix.shape[0], "x0")
-    lam = np.zeros(1, dtype=matrix.dtype)
-    x = np.empty(matrix.shape[0], dtype=matrix.dtype)
+    lam = wire_buffer(matrix.dtype, 1)
+    x = wire_buffer(matrix.dtype, matrix.shape[0])
     it, conv = C.c_int32(0), C.c_int32(0)
     o = opts.to_c()
     fn = "eigsol_power_csr" if isinstance(matrix, CsrMatrix) else "eigsol_power_dense"
     call(fn, matrix.handle, C.byref(o), _ptr(x0), _ptr(lam), _ptr(x), C.byref(it), C.byref(conv))
-    ev = complex(lam[0]) if np.iscomplexobj(lam) else float(lam[0])
-    return EigenResult(ev, x, int(it.value), bool(conv.value))
+    ev = _scalar(from_wire(lam, matrix.dtype)[0], matrix.dtype)
+    return EigenResult(ev, from_wire(x, matrix.dtype), int(it.value), bool(conv.value))
 
 
 @dataclass
@@ -354,7 +420,7 @@ class ShiftedSolverOptions(SolverOptions):
 def _sigma(shift, dtype) -> np.ndarray:
     if not np.issubdtype(dtype, np.complexfloating) and np.iscomplexobj(shift) and complex(shift).imag != 0:
         raise EigSolError(3, "scalar type mismatch: complex shift for a real matrix")
-    return np.array([shift], dtype=dtype)
+    return to_wire(np.array([shift], dtype=dtype), dtype)
 
 
 class ShiftedSession(PowerSession):
@@ -369,7 +435,7 @@ class ShiftedSession(PowerSession):
         self.matrix, self.handle = matrix, h
         self.n = matrix.shape[0]
         self.dtype = matrix.dtype
-        self.shift = sig[0]
+        self.shift = from_wire(sig, matrix.dtype)[0]
 
 
 def shifted_inverse_power_method(matrix, opts: ShiftedSolverOptions = ShiftedSolverOptions(),
@@ -382,24 +448,26 @@ def shifted_inverse_power_method(matrix, opts: ShiftedSolverOptions = ShiftedSol
             x0 = x0 + 1j * rng.uniform(-1, 1, matrix.shape[0])
     x0 = _vector(x0, matrix.dtype, matrix.shape[0], "x0")
     sig = _sigma(opts.shift, matrix.dtype)
-    lam = np.zeros(1, dtype=matrix.dtype)
-    x = np.empty(matrix.shape[0], dtype=matrix.dtype)
+    lam = wire_buffer(matrix.dtype, 1)
+    x = wire_buffer(matrix.dtype, matrix.shape[0])
     it, conv = C.c_int32(0), C.c_int32(0)
     o = opts.to_c()
     fn = "eigsol_shifted_inverse_csr" if isinstance(matrix, CsrMatrix) else "eigsol_shifted_inverse_dense"
     call(fn, matrix.handle, _ptr(sig), C.byref(o), _ptr(x0), _ptr(lam), _ptr(x), C.byref(it), C.byref(conv))
-    ev = complex(lam[0]) if np.iscomplexobj(lam) else float(lam[0])
-    return EigenResult(ev, x, int(it.value), bool(conv.value))
+    ev = _scalar(from_wire(lam, matrix.dtype)[0], matrix.dtype)
+    return EigenResult(ev, from_wire(x, matrix.dtype), int(it.value), bool(conv.value))
 
 
 def solve_shifted(matrix, shift, b) -> np.ndarray:
     """``EigSol::solve_shifted<S>``: x = (A - shift I)^{-1} b on the device."""
-    b = np.ascontiguousarray(b, dtype=matrix.dtype)
+    b = np.ascontiguousarray(b, dtype=matrix.dtype).reshape(-1)
+    nb = len(b)
     sig = _sigma(shift, matrix.dtype)
-    x = np.empty(len(b), dtype=matrix.dtype)
+    x = wire_buffer(matrix.dtype, nb)
+    bw = to_wire(b, matrix.dtype)
     fn = "eigsol_solve_shifted_csr" if isinstance(matrix, CsrMatrix) else "eigsol_solve_shifted_dense"
-    call(fn, matrix.handle, _ptr(sig), _ptr(b), len(b), _ptr(x))
-    return x
+    call(fn, matrix.handle, _ptr(sig), _ptr(bw), nb, _ptr(x))
+    return from_wire(x, matrix.dtype)
 
 
 # ------------------------------------------------------------------------------------ QR method
@@ -426,9 +494,14 @@ def to_hessenberg(ctx: Context, A) -> np.ndarray:
     """``EigSol::to_hessenberg_dense<S>`` (to_hessenberg.hpp:23-80) on the device."""
     A = _square_dense(A, "to_hessenberg_dense")
     code = _dtype_code(A.dtype)
+    n = A.shape[0]
+    if is_wide(A.dtype):
+        Hw = wire_buffer(A.dtype, n * n)
+        call("eigsol_hessenberg_dense", ctx.handle, code, n, _ptr(to_wire(A.ravel(order="F"), A.dtype)), _ptr(Hw))
+        return from_wire(Hw, A.dtype).reshape((n, n), order="F")
     Af = np.asfortranarray(A)
     H = np.empty_like(Af, order="F")
-    call("eigsol_hessenberg_dense", ctx.handle, code, A.shape[0], _ptr(Af), _ptr(H))
+    call("eigsol_hessenberg_dense", ctx.handle, code, n, _ptr(Af), _ptr(H))
     return H
 
 
@@ -437,6 +510,11 @@ def qr_decompose(ctx: Context, A):
     A = np.asarray(A)
     code = _dtype_code(A.dtype)
     m, n = A.shape
+    if is_wide(A.dtype):
+        Qw, Rw = wire_buffer(A.dtype, m * m), wire_buffer(A.dtype, m * n)
+        call("eigsol_qr_decompose_dense", ctx.handle, code, m, n, _ptr(to_wire(A.ravel(order="F"), A.dtype)),
+             _ptr(Qw), _ptr(Rw))
+        return (from_wire(Qw, A.dtype).reshape((m, m), order="F"), from_wire(Rw, A.dtype).reshape((m, n), order="F"))
     Af = np.asfortranarray(A)
     Q = np.empty((m, m), dtype=A.dtype, order="F")
     R = np.empty((m, n), dtype=A.dtype, order="F")
@@ -452,6 +530,15 @@ def qr_eigenvalues(ctx: Context, A, opts: SolverOptions = SolverOptions(), varia
     code = _dtype_code(A.dtype)
     n = A.shape[0]
     v = 1 if variant == "unshifted" else 0
+    if is_wide(A.dtype):
+        # long double: the reference's unshifted iteration in double-double (the multishift sweeps
+        # are fp64 kernels; the C++ facade makes the same choice)
+        eig = wire_buffer(A.dtype, max(n, 1))
+        it, conv = C.c_int32(0), C.c_int32(0)
+        o = opts.to_c()
+        call("eigsol_qr_eigenvalues_dense", ctx.handle, code, n, _ptr(to_wire(A.ravel(order="F"), A.dtype)),
+             C.byref(o), 1, _ptr(eig), None, C.byref(it), C.byref(conv))
+        return QRResult(from_wire(eig, A.dtype)[:n], int(it.value), bool(conv.value), None)
     if v == 0 and A.dtype in (np.float32, np.complex64):
         # single precision: the multishift sweeps are double kernels (as in the C++ facade, the
         # matrix is promoted and the eigenvalues rounded back); "unshifted" runs natively in float

@@ -30,6 +30,8 @@ EIGSOL_F64 = 0
 EIGSOL_C128 = 1
 EIGSOL_F32 = 2   # float (single-precision power / SpMV / triangular shifted inverse)
 EIGSOL_C64 = 3   # std::complex<float>
+EIGSOL_DD = 4    # long double, carried as double-double {hi, lo} (numpy longdouble: x87 80-bit)
+EIGSOL_CDD = 5   # std::complex<long double>: {re.hi, re.lo, im.hi, im.lo}
 
 EIGSOL_TRANSPORT_LOCAL = 0
 EIGSOL_TRANSPORT_COLLECTIVE = 1

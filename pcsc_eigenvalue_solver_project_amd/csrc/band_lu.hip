@@ -532,6 +532,10 @@ static S bh_sub(S a, S b) {
 template <class S>
 static int band_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const int32_t* ci, const S* v,
                          double sre, double sim, BandPlan& plan, BandFactor** out) {
+    // M = A - sigma I gains up to n inserted diagonal entries; its row pointers are int32
+    if ((int64_t)rp[n] + n > (int64_t)INT32_MAX)
+        return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: A - sigma I has more than 2^31 - 1 entries (int32 storage "
+                                          "index) for the band factor");
     hipStream_t st = ctx->stream;
     auto* f = new BandFactor();
     f->ctx = ctx;

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "kernels_common.hpp"
+#include "wide.hpp"
 
 namespace eigsol {
 namespace dev {
@@ -1295,6 +1296,7 @@ void csr_release(eigsol_csr* A) {
     if (A->send_idx) (void)hipFree(A->send_idx);
     if (A->send_buf) (void)hipFree(A->send_buf);
     for (eigsol_csr* B : A->cblk) csr_release(B);
+    if (A->shadow) csr_release(A->shadow);
     for (void* q : {(void*)A->bpk, A->bval, (void*)A->bstep, (void*)A->blev, (void*)A->bchunk})
         if (q) (void)hipFree(q);
     eigsol_ctx* c = A->ctx;
@@ -2190,6 +2192,17 @@ int scale_out_launch(eigsol_ctx* ctx, int dtype, const void* src, double nrm, vo
     return EIGSOL_OK;
 }
 
+int wide_csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* rowptr,
+                    const int32_t* colidx, const void* values, eigsol_csr** out);   // wide.hip
+int wide_csr_spmv(eigsol_csr* A, const void* x, void* y);
+
+// the row-ordered CSR of any dtype: the fp64 / fp32 layouts, or the double-double plain CSR
+static int upload_any(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t nnz, const int32_t* rowptr,
+                      const int32_t* colidx, const void* values, eigsol_csr** out) {
+    if (dtype_wide(dtype)) return wide_csr_upload(ctx, dtype, nrows, ncols, nnz, rowptr, colidx, values, out);
+    return csr_upload(ctx, dtype, nrows, ncols, nnz, rowptr, colidx, values, out, 0);
+}
+
 }  // namespace eigsol
 
 // ---------------------------------------------------------------- C ABI
@@ -2200,13 +2213,13 @@ int eigsol_csr_create(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_
                       const void* values, eigsol_csr** out) {
     if (!ctx || !out) return fail(EIGSOL_E_INVALID, "eigsol_csr_create: null ctx/out");
     *out = nullptr;
-    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create: unknown dtype");
+    if (!dtype_valid(dtype) && !dtype_wide(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create: unknown dtype");
     if (nrows > INT32_MAX - 1 || ncols > INT32_MAX - 1)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create: dimension exceeds int32 storage index");
     EIGSOL_TRY(validate_compressed("eigsol_csr_create", nrows, ncols, nnz, rowptr, colidx));
     if (nnz && !values) return fail(EIGSOL_E_INVALID, "eigsol_csr_create: null values");
     EIGSOL_HIP(hipSetDevice(ctx->device));
-    return csr_upload(ctx, dtype, nrows, ncols, nnz, rowptr, colidx, values, out, 0);
+    return upload_any(ctx, dtype, nrows, ncols, nnz, rowptr, colidx, values, out);
 }
 
 int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
@@ -2214,7 +2227,7 @@ int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrow
                                const void* values, eigsol_csr** out) {
     if (!ctx || !out) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_csc: null ctx/out");
     *out = nullptr;
-    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_csc: unknown dtype");
+    if (!dtype_valid(dtype) && !dtype_wide(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_csc: unknown dtype");
     if (nrows > INT32_MAX - 1 || ncols > INT32_MAX - 1)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_csc: dimension exceeds int32");
     EIGSOL_TRY(validate_compressed("eigsol_csr_create_from_csc", ncols, nrows, nnz, colptr, rowidx));
@@ -2234,7 +2247,7 @@ int eigsol_csr_create_from_csc(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrow
             std::memcpy(&v[(size_t)d * sb], (const unsigned char*)values + (size_t)k * sb, sb);
         }
     EIGSOL_HIP(hipSetDevice(ctx->device));
-    return csr_upload(ctx, dtype, nrows, ncols, nnz, rp.data(), ci.data(), v.data(), out, 0);
+    return upload_any(ctx, dtype, nrows, ncols, nnz, rp.data(), ci.data(), v.data(), out);
 }
 
 int eigsol_csr_create_from_coo(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int64_t ncols,
@@ -2242,7 +2255,7 @@ int eigsol_csr_create_from_coo(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrow
                                const void* values, eigsol_csr** out) {
     if (!ctx || !out) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: null ctx/out");
     *out = nullptr;
-    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: unknown dtype");
+    if (!dtype_valid(dtype) && !dtype_wide(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: unknown dtype");
     if (nrows < 0 || ncols < 0 || nnz < 0) return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: negative dimension");
     if (nrows > INT32_MAX - 1 || ncols > INT32_MAX - 1 || nnz > INT32_MAX - 16)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_from_coo: dimension exceeds int32 storage index");
@@ -2273,7 +2286,15 @@ int eigsol_csr_create_from_coo(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrow
     v.reserve((size_t)nnz * sb);
     std::vector<int32_t> crp(nrows + 1, 0);
     auto accumulate = [&](unsigned char* dst, const unsigned char* src) {
-        if (dtype == EIGSOL_F64 || dtype == EIGSOL_C128) {
+        if (dtype_wide(dtype)) {   // double-double pairs: the sum in double-double
+            for (size_t w = 0; w < sb / 16; ++w) {
+                dd a, b;
+                std::memcpy(&a, dst + 16 * w, 16);
+                std::memcpy(&b, src + 16 * w, 16);
+                a = dd_add(a, b);
+                std::memcpy(dst + 16 * w, &a, 16);
+            }
+        } else if (dtype == EIGSOL_F64 || dtype == EIGSOL_C128) {
             for (size_t w = 0; w < sb / 8; ++w) {
                 double a, b;
                 std::memcpy(&a, dst + 8 * w, 8);
@@ -2305,7 +2326,7 @@ int eigsol_csr_create_from_coo(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrow
         crp[i + 1] = (int32_t)ci.size();
     }
     EIGSOL_HIP(hipSetDevice(ctx->device));
-    return csr_upload(ctx, dtype, nrows, ncols, (int64_t)ci.size(), crp.data(), ci.data(), v.data(), out, 0);
+    return upload_any(ctx, dtype, nrows, ncols, (int64_t)ci.size(), crp.data(), ci.data(), v.data(), out);
 }
 
 int eigsol_csr_download(eigsol_csr* A, int32_t* rowptr, int32_t* colidx, void* values) {
@@ -2342,6 +2363,7 @@ int eigsol_csr_spmv(eigsol_csr* A, const void* x_dev, void* y_dev) {
         return fail(EIGSOL_E_INVALID, "eigsol_csr_spmv: null pointer");
     if (A->nrows == 0) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    if (dtype_wide(A->dtype)) return wide_csr_spmv(A, x_dev, y_dev);
     int grid = 8;
     EIGSOL_TRY(csr_grid(A, &grid, false));
     auto run = [&](auto tag) {

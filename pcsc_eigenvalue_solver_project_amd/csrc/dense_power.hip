@@ -211,6 +211,7 @@ void dense_release(eigsol_dense* A) {
     if (A->ypart) (void)hipFree(A->ypart);
     if (A->tile_cnt) (void)hipFree(A->tile_cnt);
     if (A->a) (void)hipFree(A->a);
+    if (A->shadow) dense_release(A->shadow);
     eigsol_ctx* c = A->ctx;
     delete A;
     ctx_release(c);
@@ -292,6 +293,8 @@ int dense_power_launch(eigsol_dense* A, void* buf0, void* buf1, PowerCtl* ctl,
     }
 }
 
+int wide_dense_gemv(eigsol_dense* A, const void* x, void* y);   // wide.hip
+
 }  // namespace eigsol
 
 extern "C" {
@@ -300,7 +303,7 @@ int eigsol_dense_create(eigsol_ctx* ctx, eigsol_dtype dtype, int64_t nrows, int6
                         const void* colmajor, eigsol_dense** out) {
     if (!ctx || !out) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: null ctx/out");
     *out = nullptr;
-    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: unknown dtype");
+    if (!dtype_valid(dtype) && !dtype_wide(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: unknown dtype");
     if (nrows < 0 || ncols < 0) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: negative dimension");
     if (nrows * ncols > 0 && !colmajor) return fail(EIGSOL_E_INVALID, "eigsol_dense_create: null data");
     EIGSOL_HIP(hipSetDevice(ctx->device));
@@ -334,6 +337,7 @@ int eigsol_dense_gemv(eigsol_dense* A, const void* x_dev, void* y_dev) {
         return fail(EIGSOL_E_INVALID, "eigsol_dense_gemv: null pointer");
     if (A->nrows == 0) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    if (dtype_wide(A->dtype)) return wide_dense_gemv(A, x_dev, y_dev);
     EIGSOL_TRY(dense_work(A));
     auto run = [&](auto tag) {
         return dense_launch_t<decltype(tag)>(A, false, x_dev, y_dev, nullptr, nullptr, nullptr, nullptr, 1,

@@ -520,6 +520,8 @@ int eigsol_csr_create_dist(eigsol_ctx* ctx, eigsol_dtype dtype, const int64_t* r
     if (!ctx->comm && !ctx->loop && !ctx->hcoll)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: context has no communicator");
     *out = nullptr;
+    if (dtype_wide(dtype))
+        return fail(EIGSOL_E_UNSUPPORTED, "eigsol_csr_create_dist: the row-sharded path has no double-double kernels");
     if (dtype != EIGSOL_F64 && dtype != EIGSOL_C128 && dtype != EIGSOL_F32 && dtype != EIGSOL_C64)
         return fail(EIGSOL_E_INVALID, "eigsol_csr_create_dist: unknown dtype");
     const int P = ctx->nranks, me = ctx->rank;

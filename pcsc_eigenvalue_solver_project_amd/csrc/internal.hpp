@@ -81,11 +81,14 @@ template <> struct dtype_of<cplxf> { static constexpr int value = EIGSOL_C64; };
 template <class S> inline constexpr bool is_real_v = std::is_same_v<S, double> || std::is_same_v<S, float>;
 template <class S> inline constexpr bool is_cplx_v = !is_real_v<S>;
 
-inline bool dtype_complex(int dtype) { return dtype == EIGSOL_C128 || dtype == EIGSOL_C64; }
+inline bool dtype_complex(int dtype) { return dtype == EIGSOL_C128 || dtype == EIGSOL_C64 || dtype == EIGSOL_CDD; }
 inline bool dtype_single(int dtype) { return dtype == EIGSOL_F32 || dtype == EIGSOL_C64; }
+// the fp64 / fp32 kernel families (every layout, factor and QR kernel); EIGSOL_DD / EIGSOL_CDD
+// (long double carried as double-double) have their own kernels in wide.hip
 inline bool dtype_valid(int dtype) { return dtype >= EIGSOL_F64 && dtype <= EIGSOL_C64; }
+inline bool dtype_wide(int dtype) { return dtype == EIGSOL_DD || dtype == EIGSOL_CDD; }
 inline size_t scalar_bytes(int dtype) {
-    return dtype == EIGSOL_C128 ? 16 : dtype == EIGSOL_F32 ? 4 : 8;
+    return dtype == EIGSOL_CDD ? 32 : (dtype == EIGSOL_C128 || dtype == EIGSOL_DD) ? 16 : dtype == EIGSOL_F32 ? 4 : 8;
 }
 // (re, im) in double -> one scalar of `dtype` at dst (results, traces, shifts)
 inline void store_scalar(void* dst, int dtype, double re, double im) {
@@ -278,6 +281,9 @@ struct eigsol_csr {
     int32_t* bstep = nullptr;      // 4 ints per step
     int32_t* blev = nullptr;       // 2 ints per level
     int32_t* bchunk = nullptr;     // nchunks + 1
+    // extended precision (EIGSOL_DD / EIGSOL_CDD, wide.hip): plain CSR in rowptr / col / val (dd
+    // values), plus the matrix rounded to fp64 for the shifted solves' factor (built on first use)
+    eigsol_csr* shadow = nullptr;
 };
 
 struct eigsol_dense {
@@ -290,4 +296,5 @@ struct eigsol_dense {
     void* ypart = nullptr;
     uint32_t* tile_cnt = nullptr;
     int ntr = 0, nchunk = 1, cw = 1;
+    eigsol_dense* shadow = nullptr;   // extended precision: the matrix rounded to fp64 (see eigsol_csr)
 };

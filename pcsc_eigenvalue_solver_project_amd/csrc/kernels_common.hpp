@@ -489,11 +489,13 @@ __device__ __forceinline__ void shift_prologue(PowerCtl* ctl, const part4* rank_
     __syncthreads();
 }
 
-// Multi-solve launches (triangular factors; shifted.hip, sptrsv_chunk_role_kernel): launch t runs
-// reference iterations k_j = K t + j, j = 0..K-1, together.  Solve 0 is w_0 = (A - sigma I)^{-1} x
+// Multi-solve launches (triangular factors; shifted.hip, sptrsv_chunk_role_kernel): launch 0 is an
+// ordinary single solve (reference iteration 0), launch t >= 1 runs reference iterations
+// k_j = 1 + K (t - 1) + j, j = 0..K-1, together.  Solve 0 is w_0 = (A - sigma I)^{-1} x
 // with x = v / ||v|| (v the previous launch's last solution), exactly as a single launch does;
 // solve j >= 1 is w_j = (A - sigma I)^{-1} (s w_{j-1}) with s = 2^-e an exact power of two near
-// 1 / ||w_0|| (e from the previous launch's growth ||w_0||; s = 1 at t = 0).  The reference's
+// 1 / ||w_0|| (e from the previous launch's growth ||w_0||, which launch 0 measures, so the chain
+// stays near unit size instead of growing as ||w_0||^K).  The reference's
 // iterate of k_j (j >= 1) is y = (A - sigma I)^{-1} (w_{j-1} / ||w_{j-1}||) = w_j / (s ||w_{j-1}||):
 // solve j defers the normalisation to after the solve (linearity), which is what lets it start
 // before ||w_{j-1}|| exists, one dependency round behind solve j - 1.  It differs from the
@@ -525,13 +527,18 @@ __device__ __forceinline__ void shift_multi_prologue(PowerCtl* ctl, const part4*
             if (t == 0) {
                 nrm = sqrt(part0[0].a);   // ||x0||^2 from begin()
             } else {
+                // launch 0 of a multi-solve session is an ordinary single solve (shift_launch_t): with
+                // no growth estimate yet, a chain of K solves would grow as g^K and could overflow
+                const bool prev_single = t == 1;
+                const int Kp = prev_single ? 1 : K;
+                const int32_t kbase = prev_single ? 0 : 1 + K * (t - 2);
                 const double s_prev = ldexp(1.0, -in.pad);
                 double prev_n = in.nrm;   // norm of the previous x's buffer
                 int prev_par = parity;    // ... and its final_parity code
-                for (int j = 0; j < K && !fin; ++j) {
+                for (int j = 0; j < Kp && !fin; ++j) {
                     const part4 pj = j ? kpart[j - 1] : part0[0];
-                    const int32_t k = K * (t - 1) + j;
-                    const int code = j == K - 1 ? (parity ^ 1) : 2 + j;
+                    const int32_t k = kbase + j;
+                    const int code = j == Kp - 1 ? (parity ^ 1) : 2 + j;
                     if (pj.a == 0.0) {                    // normY == 0 (:55-58): x, lambda unchanged
                         fin = true;
                         iters = k + 1;
@@ -560,7 +567,7 @@ __device__ __forceinline__ void shift_multi_prologue(PowerCtl* ctl, const part4*
                     prev_n = fnorm;
                     prev_par = code;
                 }
-                nrm = sqrt((K > 1 ? kpart[K - 2] : part0[0]).a);
+                nrm = sqrt((Kp > 1 ? kpart[Kp - 2] : part0[0]).a);
                 // growth of the previous launch's first solve from a unit input
                 const double g = sqrt(part0[0].a);
                 if (g > 0.0 && g < INFINITY) e = min(max(ilogb(g), -900), 900);

@@ -47,9 +47,21 @@ int shift_grid(const ShiftFactor* f);
 void* shift_aux(const ShiftFactor* f, int j);
 int shift_error(ShiftFactor* f);
 int shift_iter_launch(ShiftFactor* f, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
-                      void* my_part, void* trace, int parity);
+                      void* my_part, void* trace, int parity, int first);
 int shift_solve_launch(ShiftFactor* f, const void* b_dev, void* y_dev);
 void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* tiles);
+// extended precision (EIGSOL_DD / EIGSOL_CDD, wide.hip): the same session interface, host-driven
+struct WideSession;
+int wide_session_create(eigsol_ctx* ctx, eigsol_csr* csr, eigsol_dense* dense, const void* sigma, int32_t trace_cap,
+                        WideSession** out);
+void wide_session_free(WideSession* s);
+int wide_begin(WideSession* s, const eigsol_solver_options* opts, const void* x0, int on_dev);
+int wide_step(WideSession* s, int32_t nsteps);
+int wide_query(WideSession* s, int32_t* done, int32_t* launches);
+int wide_finish(WideSession* s, void* lambda_out, void* x_out, int x_on_dev, int32_t* iterations, int32_t* converged);
+int wide_trace(WideSession* s, void* trace_host, int32_t capacity, int32_t* count);
+void wide_info(const WideSession* s, double* bytes, int32_t* variant, int32_t* tiles, int32_t* grid);
+int wide_solve_shifted(eigsol_csr* csr, eigsol_dense* dense, const void* sigma, const void* b, int64_t nb, void* x);
 }  // namespace eigsol
 
 using namespace eigsol;
@@ -102,6 +114,7 @@ struct eigsol_power {
     std::vector<int64_t> split_rows;
     hipStream_t comm = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    WideSession* wide = nullptr;   // EIGSOL_DD / EIGSOL_CDD: the double-double session (wide.hip)
 };
 
 static constexpr size_t kPart = 32;
@@ -138,6 +151,11 @@ static void peer_free(eigsol_power* s) {
 
 static void session_free(eigsol_power* s) {
     if (!s) return;
+    if (s->wide) {
+        wide_session_free(s->wide);
+        delete s;
+        return;
+    }
     hipSetDevice(s->ctx->device);
     hipStreamSynchronize(s->ctx->stream);
     if (s->comm) {
@@ -166,7 +184,7 @@ static int launch_iteration(eigsol_power* s) {
                                 s->my_part, s->blk_part, s->trace, s->parity, s->grid, &s->peer->args);
     if (s->shift)
         return shift_iter_launch(s->shift, s->buf[0], s->buf[1], s->ctl, s->rank_part, s->my_part,
-                                 s->trace, s->parity);
+                                 s->trace, s->parity, s->launches == 0);
     if (s->csr && s->dist && s->split) {
         // launch t writes y_t into buf[t & 1]: the first half's rows go out while the second half computes
         for (int part = 0; part < 2; ++part) {
@@ -403,6 +421,22 @@ static int choose_split(eigsol_power* s) {
     return EIGSOL_OK;
 }
 
+// a session handle around a double-double session (power method when sigma is null)
+static int wide_wrap(eigsol_ctx* ctx, eigsol_csr* csr, eigsol_dense* dense, const void* sigma, int32_t trace_cap,
+                     eigsol_power** out) {
+    EIGSOL_HIP(hipSetDevice(ctx->device));
+    WideSession* w = nullptr;
+    EIGSOL_TRY(wide_session_create(ctx, csr, dense, sigma, trace_cap, &w));
+    auto* s = new eigsol_power();
+    s->ctx = ctx;
+    s->dtype = csr ? csr->dtype : dense->dtype;
+    s->n = csr ? csr->nrows : dense->nrows;
+    s->nbuf = s->n;
+    s->wide = w;
+    *out = s;
+    return EIGSOL_OK;
+}
+
 extern "C" {
 
 int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power** out) {
@@ -410,6 +444,7 @@ int eigsol_power_create_csr(eigsol_csr* A, int32_t trace_capacity, eigsol_power*
     *out = nullptr;
     if (!A->dist && A->nrows != A->ncols) return fail(EIGSOL_E_NOT_SQUARE, "powerMethod: matrix must be square");
     if (A->dist ? A->n_global == 0 : A->nrows == 0) return fail(EIGSOL_E_ZERO_SIZE, "powerMethod: matrix has zero size");
+    if (dtype_wide(A->dtype)) return wide_wrap(A->ctx, A, nullptr, nullptr, trace_capacity, out);
     auto* s = new eigsol_power();
     s->ctx = A->ctx;
     s->csr = A;
@@ -433,6 +468,7 @@ int eigsol_power_create_dense(eigsol_dense* A, int32_t trace_capacity, eigsol_po
     *out = nullptr;
     if (A->nrows != A->ncols) return fail(EIGSOL_E_NOT_SQUARE, "powerMethod: matrix must be square");
     if (A->nrows == 0) return fail(EIGSOL_E_ZERO_SIZE, "powerMethod: matrix has zero size");
+    if (dtype_wide(A->dtype)) return wide_wrap(A->ctx, nullptr, A, nullptr, trace_capacity, out);
     auto* s = new eigsol_power();
     s->ctx = A->ctx;
     s->dense = A;
@@ -455,6 +491,7 @@ int eigsol_power_destroy(eigsol_power* s) {
 int eigsol_power_begin(eigsol_power* s, const eigsol_solver_options* opts, const void* x0,
                        int x0_on_device) {
     if (!s || !opts || !x0) return fail(EIGSOL_E_INVALID, "eigsol_power_begin: null pointer");
+    if (s->wide) return wide_begin(s->wide, opts, x0, x0_on_device);
     EIGSOL_HIP(hipSetDevice(s->ctx->device));
     hipStream_t st = s->ctx->stream;
     const size_t sb = scalar_bytes(s->dtype);
@@ -497,6 +534,7 @@ int eigsol_power_begin(eigsol_power* s, const eigsol_solver_options* opts, const
 }
 
 int eigsol_power_step(eigsol_power* s, int32_t nsteps) {
+    if (s && s->wide) return wide_step(s->wide, nsteps);
     if (!s || !s->begun) return fail(EIGSOL_E_INVALID, "eigsol_power_step: session not begun");
     if (s->trivial) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(s->ctx->device));
@@ -509,6 +547,7 @@ int eigsol_power_step(eigsol_power* s, int32_t nsteps) {
 }
 
 int eigsol_power_query(eigsol_power* s, int32_t* done, int32_t* launches) {
+    if (s && s->wide) return wide_query(s->wide, done, launches);
     if (!s || !s->begun) return fail(EIGSOL_E_INVALID, "eigsol_power_query: session not begun");
     if (s->trivial) {
         if (done) *done = 1;
@@ -538,6 +577,7 @@ int eigsol_power_query(eigsol_power* s, int32_t* done, int32_t* launches) {
 
 int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_out_on_device,
                         int32_t* iterations, int32_t* converged) {
+    if (s && s->wide) return wide_finish(s->wide, lambda_out, x_out, x_out_on_device, iterations, converged);
     if (!s || !s->begun) return fail(EIGSOL_E_INVALID, "eigsol_power_finish: session not begun");
     EIGSOL_HIP(hipSetDevice(s->ctx->device));
     hipStream_t st = s->ctx->stream;
@@ -609,6 +649,7 @@ int eigsol_power_finish(eigsol_power* s, void* lambda_out, void* x_out, int x_ou
 }
 
 int eigsol_power_trace(eigsol_power* s, void* trace_host, int32_t capacity, int32_t* count) {
+    if (s && s->wide) return wide_trace(s->wide, trace_host, capacity, count);
     if (!s || !s->begun) return fail(EIGSOL_E_INVALID, "eigsol_power_trace: session not begun");
     int32_t n = 0;
     if (!s->trivial && s->trace) {
@@ -633,6 +674,10 @@ int eigsol_power_transport(const eigsol_power* s, int* transport) {
 int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int32_t* tiles,
                              int32_t* variant) {
     if (!s) return fail(EIGSOL_E_INVALID, "eigsol_power_kernel_info: null session");
+    if (s->wide) {
+        wide_info(s->wide, bytes, variant, tiles, grid);
+        return EIGSOL_OK;
+    }
     const double sb = (double)scalar_bytes(s->dtype);
     if (s->shift) {
         shift_info(s->shift, bytes, variant, tiles);
@@ -665,7 +710,7 @@ int eigsol_power_kernel_info(eigsol_power* s, double* bytes, int32_t* grid, int3
 int eigsol_power_kernel_name(eigsol_power* s, char* buf, size_t cap) {
     if (!s || !buf || cap == 0) return fail(EIGSOL_E_INVALID, "eigsol_power_kernel_name: null argument");
     buf[0] = 0;
-    if (s->shift || !s->csr) return EIGSOL_OK;   // named for CSR power sessions only
+    if (s->wide || s->shift || !s->csr) return EIGSOL_OK;   // named for CSR power sessions only
     const void* k = csr_power_kernel(s->csr, s->transport == EIGSOL_TRANSPORT_PEER);
     const char* m = k ? hipKernelNameRefByPtr(k, s->ctx->stream) : nullptr;
     if (!m) return EIGSOL_OK;
@@ -725,6 +770,7 @@ int eigsol_power_dense(eigsol_dense* A, const eigsol_solver_options* opts, const
 // A - sigma I once at creation and runs one fused solve launch per iteration.
 static int shifted_create(eigsol_ctx* ctx, eigsol_csr* csr, eigsol_dense* dense, int dtype,
                           int64_t n, const void* sigma, int32_t trace_capacity, eigsol_power** out) {
+    if (dtype_wide(dtype)) return wide_wrap(ctx, csr, dense, sigma, trace_capacity, out);
     auto* s = new eigsol_power();
     s->ctx = ctx;
     s->dtype = dtype;
@@ -808,6 +854,7 @@ int eigsol_solve_shifted_csr(eigsol_csr* A, const void* sigma, const void* b, in
         return fail(EIGSOL_E_SIZE_MISMATCH, "solve_shifted: size mismatch between A and b (sparse case)");
     if (nb == 0) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    if (dtype_wide(A->dtype)) return wide_solve_shifted(A, nullptr, sigma, b, nb, x);
     ShiftFactor* f = nullptr;
     EIGSOL_TRY(shift_factor_csr(A, sigma, &f));
     const int rc = solve_once(f, A->ctx, scalar_bytes(A->dtype), nb, b, x);
@@ -822,6 +869,7 @@ int eigsol_solve_shifted_dense(eigsol_dense* A, const void* sigma, const void* b
         return fail(EIGSOL_E_SIZE_MISMATCH, "solve_shifted: size mismatch between A and b (dense case)");
     if (nb == 0) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(A->ctx->device));
+    if (dtype_wide(A->dtype)) return wide_solve_shifted(nullptr, A, sigma, b, nb, x);
     ShiftFactor* f = nullptr;
     EIGSOL_TRY(shift_factor_dense(A, sigma, &f));
     const int rc = solve_once(f, A->ctx, scalar_bytes(A->dtype), nb, b, x);

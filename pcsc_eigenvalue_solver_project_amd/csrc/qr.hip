@@ -732,6 +732,11 @@ int hqr_lds(hipStream_t st, const double* H, int64_t ld, int n, int maxits, doub
     return EIGSOL_OK;
 }
 
+int wide_hessenberg(eigsol_ctx* ctx, int dtype, int64_t n, const void* A, void* H);   // wide.hip
+int wide_qr_decompose(eigsol_ctx* ctx, int dtype, int64_t m, int64_t n, const void* A, void* Q, void* R);
+int wide_qr_eigenvalues(eigsol_ctx* ctx, int dtype, int64_t n, const void* A, const eigsol_solver_options* opts,
+                        int variant, void* eig, int32_t* iters, int32_t* conv);
+
 }  // namespace eigsol
 
 using namespace eigsol;
@@ -742,6 +747,8 @@ int eigsol_hessenberg_dense(eigsol_ctx* ctx, int dtype, int64_t n, const void* A
     if (!ctx || (!A_colmajor && n) || (!H_out && n)) return fail(EIGSOL_E_INVALID, "eigsol_hessenberg_dense: null pointer");
     if (n == 0) return EIGSOL_OK;
     EIGSOL_HIP(hipSetDevice(ctx->device));
+    if (dtype_wide(dtype)) return wide_hessenberg(ctx, dtype, n, A_colmajor, H_out);
+    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_hessenberg_dense: unknown dtype");
     switch (dtype) {
         case EIGSOL_C128: return hessenberg_host<cplx>(ctx, n, A_colmajor, H_out);
         case EIGSOL_F32: return hessenberg_host<float>(ctx, n, A_colmajor, H_out);
@@ -756,6 +763,8 @@ int eigsol_qr_decompose_dense(eigsol_ctx* ctx, int dtype, int64_t m, int64_t n, 
     if (m == 0 || n == 0) return fail(EIGSOL_E_EMPTY, "qr_decompose_dense: empty matrix");
     if (!A_colmajor) return fail(EIGSOL_E_INVALID, "eigsol_qr_decompose_dense: null A");
     EIGSOL_HIP(hipSetDevice(ctx->device));
+    if (dtype_wide(dtype)) return wide_qr_decompose(ctx, dtype, m, n, A_colmajor, Q_out, R_out);
+    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_qr_decompose_dense: unknown dtype");
     switch (dtype) {
         case EIGSOL_C128: return qr_decompose_host<cplx>(ctx, m, n, A_colmajor, Q_out, R_out);
         case EIGSOL_F32: return qr_decompose_host<float>(ctx, m, n, A_colmajor, Q_out, R_out);
@@ -775,6 +784,9 @@ int eigsol_qr_eigenvalues_dense(eigsol_ctx* ctx, int dtype, int64_t n, const voi
     }
     if (!A_colmajor || !eig_re_or_c) return fail(EIGSOL_E_INVALID, "eigsol_qr_eigenvalues_dense: null pointer");
     EIGSOL_HIP(hipSetDevice(ctx->device));
+    if (dtype_wide(dtype))
+        return wide_qr_eigenvalues(ctx, dtype, n, A_colmajor, opts, variant, eig_re_or_c, iterations, converged);
+    if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_qr_eigenvalues_dense: unknown dtype");
     if (dtype == EIGSOL_F32 || dtype == EIGSOL_C64) {
         // single precision: the reference's unshifted iteration natively (blocked QR decompositions
         // and products in float); the Francis sweeps are built in double (the facade promotes)

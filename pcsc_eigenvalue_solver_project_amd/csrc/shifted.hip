@@ -1786,14 +1786,46 @@ static int gmres_dense_fallback(ShiftFactor* f, int rc_gmres) {
             return rc_gmres;
         hipStream_t st = f->ctx->stream;
         EIGSOL_HIP(hipStreamSynchronize(st));
+        // The densified LU is built in a scratch factor and moved into f only once it exists: a
+        // failed allocation or a zero pivot leaves f a working GMRES factor (later launches and
+        // shift_info still see f->gm) and frees the scratch.
+        auto* g = new ShiftFactor();
+        g->ctx = f->ctx;
+        ctx_retain(g->ctx);
+        g->dtype = f->dtype;
+        g->n = n;
+        g->sig_re = f->sig_re;
+        g->sig_im = f->sig_im;
+        int rc = EIGSOL_OK;
+        if (hipMalloc(&g->lu, (size_t)bytes) != hipSuccess || hipMemsetAsync(g->lu, 0, (size_t)bytes, st) != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "GMRES fallback: hipMalloc(dense LU)");
+        if (rc == EIGSOL_OK) {
+            hipLaunchKernelGGL((dev::densify_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->src->rowptr,
+                               f->src->col, static_cast<const S*>(f->src->val), n, static_cast<S*>(g->lu));
+            rc = dense_lu_factor<S>(g, true);
+        }
+        if (rc != EIGSOL_OK) {
+            shift_free(g);
+            return rc;
+        }
         if (f->gm) { gmres_free(f->gm); f->gm = nullptr; }
-        if (f->work) { hipFree(f->work); f->work = nullptr; }
-        if (f->wave_part) { hipFree(f->wave_part); f->wave_part = nullptr; }
-        EIGSOL_HIP(hipMalloc(&f->lu, (size_t)bytes));
-        EIGSOL_HIP(hipMemsetAsync(f->lu, 0, (size_t)bytes, st));
-        hipLaunchKernelGGL((dev::densify_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->src->rowptr,
-                           f->src->col, static_cast<const S*>(f->src->val), n, static_cast<S*>(f->lu));
-        EIGSOL_TRY(dense_lu_factor<S>(f, true));
+        for (void* p : {(void*)f->work, (void*)f->err, f->wave_part}) if (p) hipFree(p);
+        f->kind = g->kind;
+        f->lu = g->lu;
+        f->perm = g->perm;
+        f->zero_pivot = g->zero_pivot;
+        f->lds_bytes = g->lds_bytes;
+        f->dense_multi = g->dense_multi;
+        f->grid = g->grid;
+        f->nchunks = g->nchunks;
+        f->flag_f = g->flag_f;
+        f->flag_b = g->flag_b;
+        f->zf = g->zf;
+        f->work = g->work;
+        f->err = g->err;
+        f->wave_part = g->wave_part;
+        ctx_release(g->ctx);
+        delete g;   // its buffers now belong to f
         csr_release(f->src);
         f->src = nullptr;
         f->fell_back = 1;
@@ -2153,8 +2185,15 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
             f->multi = K;
             f->grid_multi = K * gr;
             const char* hc = std::getenv("EIGSOL_TRSV_MULTI_HEAD");   // seq: the head solves one after another
+            // the dynamic LDS of the concurrent head shares the CU's 160 KiB with the kernel's static
+            // __shared__ state (its prologue record)
+            hipFuncAttributes fa{};
+            size_t static_lds = 256;
+            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, true, true>)) ==
+                hipSuccess)
+                static_lds = fa.sharedSizeBytes;
             f->hconc = (!(hc && !std::strcmp(hc, "seq")) &&
-                        (size_t)K * (size_t)(f->hpos + 1) * sizeof(S) + 16 <= (size_t)160 * 1024) ? 1 : 0;
+                        (size_t)K * (size_t)(f->hpos + 1) * sizeof(S) + 16 + static_lds <= (size_t)160 * 1024) ? 1 : 0;
         }
     }
     f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
@@ -2270,7 +2309,8 @@ void* shift_aux(const ShiftFactor* f, int j) { return (j >= 0 && j < dev::kMaxMu
 
 template <class S>
 static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, void* buf0, void* buf1,
-                          PowerCtl* ctl, const void* rank_part, void* my_part, void* trace, int parity) {
+                          PowerCtl* ctl, const void* rank_part, void* my_part, void* trace, int parity,
+                          bool first = false) {
     hipStream_t st = f->ctx->stream;
     if (f->kind == 2) {
         // ILU(0)-preconditioned GMRES: host-driven (one sync per Arnoldi step), so the iteration is
@@ -2347,7 +2387,9 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.wrp = static_cast<const S*>(f->wrp);
         a.wdst = f->wdst;
         a.nwpass = f->nwpass;
-        const bool pair = iter && f->multi > 1;   // multi-solve launch
+        // multi-solve launch; a session's launch 0 is a single solve (it measures the growth that
+        // scales the chained solves of the later launches, shift_multi_prologue)
+        const bool pair = iter && f->multi > 1 && !first;
         a.K = 1;
         a.zk[0] = a.zcur;
         a.zkn[0] = a.znext;
@@ -2386,6 +2428,8 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
             if (iter) hipLaunchKernelGGL((dev::sptrsv_head_kernel<S, true>), dim3(1), dim3(dev::kHeadThreads), hl, st, a, parity);
             else hipLaunchKernelGGL((dev::sptrsv_head_kernel<S, false>), dim3(1), dim3(dev::kHeadThreads), hl, st, a, parity);
         }
+        // a head that failed to launch would leave the tail polling for values nobody writes
+        EIGSOL_HIP(hipGetLastError());
         // cooperative: the static chunk schedule needs every wave of the grid resident
         void* kargs[] = {&a, &parity};
         a.smeta = f->smeta;
@@ -2485,9 +2529,10 @@ static int by_dtype(int dtype, F&& fn) {
 }
 
 int shift_iter_launch(ShiftFactor* f, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
-                      void* my_part, void* trace, int parity) {
+                      void* my_part, void* trace, int parity, int first) {
     return by_dtype(f->dtype, [&](auto tag) {
-        return shift_launch_t<decltype(tag)>(f, true, nullptr, nullptr, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+        return shift_launch_t<decltype(tag)>(f, true, nullptr, nullptr, buf0, buf1, ctl, rank_part, my_part, trace, parity,
+                                             first != 0);
     });
 }
 

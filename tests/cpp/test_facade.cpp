@@ -402,26 +402,31 @@ TEST(SinglePrecision, PowerShiftedSolveAndQR) {
     EXPECT_EQ(Ms.rows(), 2);
 }
 
-// long double / std::complex<long double>: on the fp64 kernels (rounded to double on upload,
-// widened back), every entry point of the reference's API
-TEST(WidePrecision, LongDoubleOnFp64Kernels) {
+// long double / std::complex<long double>: double-double on the device (EIGSOL_DD / EIGSOL_CDD),
+// every entry point of the reference's API, at more than double precision
+TEST(WidePrecision, LongDoubleInDoubleDouble) {
     using LD = long double;
     using CLD = std::complex<long double>;
+    const LD tiny = std::ldexp(1.0L, -60);   // below double resolution at 1, inside the x87 significand
     EigSol::Matrix::Dense<LD> L(2, 2);
-    L << 2.0L, 0.0L, 0.0L, 1.0L;
+    L << 1.0L + tiny, 0.0L, 0.0L, 0.5L;
     EigSol::Matrix Ml(L);
-    auto r = EigSol::powerMethod<LD>(Ml, EigSol::SolverOptions{});
+    EigSol::Vector<LD> x0(2);
+    x0 << 0.8L, 0.6L;
+    auto r = EigSol::powerMethod<LD>(Ml, EigSol::SolverOptions{1000, 1e-20}, x0);
     EXPECT_TRUE(r.converged);
-    EXPECT_NEAR(r.eigenvalue, 2.0L, 1e-8L);
-    EigSol::ShiftedSolverOptions<LD> so(0.9L, 1000, 1e-12);
-    auto rs = EigSol::shiftedInversePowerMethod<LD>(Ml, so);
+    EXPECT_NEAR(r.eigenvalue, 1.0L + tiny, std::ldexp(1.0L, -62));   // fp64 would return exactly 1
+    EXPECT_TRUE(r.eigenvalue != 1.0L);
+    EigSol::ShiftedSolverOptions<LD> so(0.45L, 1000, 1e-18);
+    auto rs = EigSol::shiftedInversePowerMethod<LD>(Ml, so, x0);
     EXPECT_TRUE(rs.converged);
-    EXPECT_NEAR(rs.eigenvalue, 1.0L, 1e-10L);
+    EXPECT_NEAR(rs.eigenvalue, 0.5L, std::ldexp(1.0L, -62));
     EigSol::Vector<LD> b(2);
     b << 4.0L, 2.0L;
-    auto x = EigSol::solve_shifted<LD>(Ml, 0.5L, b);
-    EXPECT_NEAR(x(0), 4.0L / 1.5L, 1e-14L);
-    EXPECT_NEAR(x(1), 4.0L, 1e-14L);
+    auto x = EigSol::solve_shifted<LD>(Ml, 0.0L, b);
+    EXPECT_NEAR(x(0), 4.0L / (1.0L + tiny), std::ldexp(1.0L, -61));
+    EXPECT_TRUE(x(0) != 4.0L);
+    EXPECT_NEAR(x(1), 4.0L, 1e-18L);
     EigSol::Matrix::Dense<LD> B(2, 2);
     B << 2.0L, 1.0L, 1.0L, 2.0L;
     auto q = EigSol::qr_eigenvalues<LD>(EigSol::Matrix(B), EigSol::SolverOptions{1000, 1e-12},
@@ -440,12 +445,16 @@ TEST(WidePrecision, LongDoubleOnFp64Kernels) {
     EXPECT_NEAR(std::abs(rc.eigenvalue - CLD(5.0L, -1.0L)), 0.0L, 1e-8L);
     EigSol::ShiftedSolverOptions<CLD> sc(CLD(2.1L, 3.9L), 1000, 1e-12);
     auto rsc = EigSol::shiftedInversePowerMethod<CLD>(Ms, sc);
-    EXPECT_NEAR(std::abs(rsc.eigenvalue - CLD(2.0L, 4.0L)), 0.0L, 1e-10L);
+    EXPECT_NEAR(std::abs(rsc.eigenvalue - CLD(2.0L, 4.0L)), 0.0L, 1e-18L);
     EigSol::Matrix::Dense<CLD> Dc(2, 2);
     Dc << CLD(1, 1), CLD(2, 0), CLD(0, 0), CLD(3, -1);
+    // long double runs the reference's unshifted iteration for either variant (triangular input:
+    // converged at the first check, the diagonal)
     auto qc = EigSol::qr_eigenvalues<CLD>(EigSol::Matrix(Dc), EigSol::SolverOptions{}, EigSol::QRVariant::Francis);
     EXPECT_TRUE(qc.converged);
-    EXPECT_EQ(qc.eigenvalues_complex.size(), 2u);
+    EXPECT_EQ(qc.iterations, 1);
+    EXPECT_NEAR(std::abs(qc.eigenvalues(0) - CLD(1, 1)), 0.0L, 1e-18L);
+    EXPECT_NEAR(std::abs(qc.eigenvalues(1) - CLD(3, -1)), 0.0L, 1e-18L);
 }
 
 // ---------------------------------------------------------------- reference caller shapes

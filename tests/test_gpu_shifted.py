@@ -438,3 +438,37 @@ def test_multi_launches_without_head(ctx, monkeypatch, K):
     assert res.converged and abs(res.eigenvalue - (0.5 + 0.25j)) <= 1e-12
     assert abs(res.iterations - ref["iterations"]) <= 1
     assert abs(np.vdot(res.eigenvector, ref["eigenvector"])) >= 1 - 1e-10
+
+
+@pytest.mark.parametrize("dtype", [np.complex64, np.complex128])
+def test_multi_launches_large_per_solve_growth(ctx, monkeypatch, dtype):
+    """A pivot of 1e-11 makes every solve grow its input ~1e11-fold.  Launch 0 of a multi-solve
+    session is a single solve that measures that growth, so the chained solves of the later launches
+    are scaled by ~1e-11 and stay near unit size (a chain of four unscaled solves would reach ~1e44,
+    past the float range).  The eigenvalue is the tiny pivot itself, matched to the oracle with the
+    same iteration count (shifted_inverse_power_solver.hpp:48-76)."""
+    monkeypatch.setenv("EIGSOL_TRSV_MULTI", "4")
+    n = 20000
+    rp, ci, v, _ = S.triu_complex(n, 16, seed=42)
+    tiny = 1e-11 * np.exp(0.3j)
+    v = v.copy()
+    v[rp[n // 3]] = tiny
+    v = v.astype(dtype)
+    M = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    x0 = S.start_vector(n, dtype)
+    opts = E.ShiftedSolverOptions(50, 1e-6, 0.0)
+    sess = E.ShiftedSession(M, 0.0, trace_capacity=64)
+    assert sess.kernel_info()["iterations_per_launch"] == 4
+    sess.begin(opts, x0)
+    sess.step(60)
+    assert sess.query()[0]
+    res = sess.finish()
+    sess.close()
+    ref = O.shifted_triu_csr(rp, ci, v, 0.0, x0, 50, 1e-6, want_trace=True)
+    assert res.converged and ref["converged"]
+    assert res.iterations == ref["iterations"]
+    lam = complex(res.eigenvalue)
+    assert np.isfinite(lam) and abs(lam - complex(v[rp[n // 3]])) <= 1e-4 * abs(tiny), lam
+    x = res.eigenvector.astype(np.complex128)
+    assert np.all(np.isfinite(x)) and abs(np.linalg.norm(x) - 1) <= 1e-5
+    assert abs(np.vdot(x, ref["eigenvector"].astype(np.complex128))) >= 1 - 1e-5
