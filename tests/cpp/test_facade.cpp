@@ -443,8 +443,9 @@ TEST(WidePrecision, LongDoubleInDoubleDouble) {
     EigSol::Matrix Ms(Sc);
     auto rc = EigSol::powerMethod<CLD>(Ms, EigSol::SolverOptions{});
     EXPECT_NEAR(std::abs(rc.eigenvalue - CLD(5.0L, -1.0L)), 0.0L, 1e-8L);
-    EigSol::ShiftedSolverOptions<CLD> sc(CLD(2.1L, 3.9L), 1000, 1e-12);
+    EigSol::ShiftedSolverOptions<CLD> sc(CLD(2.1L, 3.9L), 1000, 1e-20);
     auto rsc = EigSol::shiftedInversePowerMethod<CLD>(Ms, sc);
+    EXPECT_TRUE(rsc.converged);
     EXPECT_NEAR(std::abs(rsc.eigenvalue - CLD(2.0L, 4.0L)), 0.0L, 1e-18L);
     EigSol::Matrix::Dense<CLD> Dc(2, 2);
     Dc << CLD(1, 1), CLD(2, 0), CLD(0, 0), CLD(3, -1);

@@ -10,7 +10,9 @@ miss these bounds by orders of magnitude.
 Tolerances (eps = 2^-63, the x87 unit roundoff is eps/2):
   * products (CSR, dense): |y - y_ref| <= 64 eps (|A| |x|) per row (the x87 row sum's rounding);
   * power / shifted inverse: |lambda - lambda_ref| <= 1e-17 (1 + |lambda_ref|), equal
-    iteration counts, |x^H x_ref| >= 1 - 1e-17, lambda traces within 1e-17 (1 + |lambda|);
+    iteration counts, |x^H x_ref| >= 1 - 1e-17, lambda traces within 1e-17 (1 + |lambda|), or on
+    non-normal matrices whose iterations amplify rounding, within 1/512 of the fp64 oracle's drift
+    from the x87 one (the x87 oracle's own rounding error there);
   * solve_shifted: within 2e-16 ||x|| of the x87 LU solution at a well-conditioned shift (fp64: 20x worse);
   * Hessenberg / QR decomposition: entrywise within 1e-16 ||A||_F of the long-double oracle (an
     fp64 reduction misses this by ~50x); unshifted QR iteration: the reference's iteration counts
@@ -128,7 +130,16 @@ def test_wide_power_csr_parity(ctx, dt, kind):
     assert isinstance(lam, (np.longdouble, np.clongdouble))
     assert abs(lam - lr) <= 1e-17 * (1 + abs(lr)), (lam, lr)
     assert len(tr) == res.iterations
-    assert np.max(np.abs((tr - ref["trace"]).astype(CLD))) <= 1e-17 * (1 + abs(lr))
+    # lambda trace: the band matrices are non-normal and their Rayleigh quotients pass through
+    # iterations that amplify rounding ~1e4-fold (the fp64 oracle drifts from the x87 one by ~1e-12
+    # there); there the difference is the x87 oracle's own rounding, bounded by its share of the fp64
+    # spread (2^-64 / 2^-53 = 1/2048, with a 4x margin)
+    d64 = np.complex128 if dt == CLD else np.float64
+    r64 = O.power_csc(cp, ri, vv.astype(d64), x0.astype(d64), 500, tol, want_trace=True)
+    m = min(len(tr), len(r64["trace"]))
+    spread64 = float(np.max(np.abs((r64["trace"][:m].astype(dt) - ref["trace"][:m]).astype(CLD))))
+    diff = float(np.max(np.abs((tr - ref["trace"]).astype(CLD))))
+    assert diff <= max(1e-17 * float(1 + abs(lr)), 2e-3 * spread64), (diff, spread64)
     x, xr = res.eigenvector, ref["eigenvector"]
     assert x.dtype == dt
     assert abs(abs(_cdot(x, xr)) - 1) <= 1e-17
