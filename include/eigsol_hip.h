@@ -322,6 +322,18 @@ int eigsol_power_transport(const eigsol_power* s, int* transport);
  * [lower | upper] ghost order), sorted by local row. */
 int eigsol_peer_plan(int nranks, int rank, const int64_t* row_begins, const int64_t* ghost_counts,
                      const int64_t* requests, int64_t nreq, int32_t* push_out);
+/* This context's place in the world: device, rank, ranks, and how it exchanges (0 none, 1 RCCL
+ * communicator, 2 in-process loopback world, 3 caller's host all-gather + device peer inboxes). */
+int eigsol_ctx_info(eigsol_ctx* ctx, int* device, int* rank, int* nranks, int* comm_kind);
+
+/* ---------------------------------------------------------------- measurement
+ * The device's practical HBM bandwidth ("verify the spec with a STREAM-like kernel
+ * on the box"): hand-written gfx950 streams over `bytes` (use >= 2 GiB: beyond the 256 MB
+ * Infinity Cache) with 16-byte non-temporal loads / stores, four in flight per lane, timed with HIP
+ * events over `reps` launches on the context's stream, best over 1/2/4/8 workgroups per CU.
+ * read = load only, copy = load + store (both directions counted), write = store only (GB/s). */
+int eigsol_hbm_probe(eigsol_ctx* ctx, size_t bytes, int reps, double* read_gbps, double* copy_gbps,
+                     double* write_gbps, int* best_blocks_per_cu);
 
 #ifdef __cplusplus
 }

@@ -123,6 +123,8 @@ SIGNATURES = {
     "eigsol_qr_decompose_dense": [_vp, C.c_int, _i64, _i64, _vp, _vp, _vp],
     "eigsol_qr_eigenvalues_dense": [_vp, C.c_int, _i64, _vp, C.POINTER(SolverOptionsC), C.c_int, _vp,
                                     _vp, _pi32, _pi32],
+    "eigsol_hbm_probe": [_vp, C.c_size_t, C.c_int, _pd, _pd, _pd, _pint],
+    "eigsol_ctx_info": [_vp, _pint, _pint, _pint, _pint],
 }
 _RESTYPES = {"eigsol_status_string": C.c_char_p, "eigsol_last_error": C.c_char_p}
 

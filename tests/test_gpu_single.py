@@ -270,10 +270,11 @@ def test_single_hessenberg_and_qr_decompose_native(ctx, dtype):
     instantiated for float and complex<float>: f32 panels, VALU panel GEMMs, rank-2nb updates on
     v_mfma_f32_16x16x4_f32) against the fp64 restatement of the reference's loops
     (to_hessenberg.hpp:38-77, qr_decompose.hpp:46-85): |H| within 2e-5 ||A||, zero below the
-    subdiagonal; Q R = A and Q^H Q = I at single precision.  H is compared entrywise in modulus:
-    the reference's reflector takes its sign / phase from x0, and where |x0| / ||x|| is below the
-    single-precision rounding (column 89 of this matrix: 3.4e-7) float and double legitimately
-    choose opposite reflectors, i.e. H_f32 = D H_f64 D^H with a diagonal unitary D."""
+    subdiagonal; Q R = A and Q^H Q = I at single precision.  The reference's reflector takes its
+    sign / phase from x0, and where |x0| / ||x|| is below the single-precision rounding (column 89
+    of this matrix: 3.4e-7) float and double legitimately choose opposite reflectors, so H is
+    checked as H_f32 = D H_f64 D^H entrywise, with the diagonal unitary D (D_0 = 1, +-1 for real
+    matrices) recovered from the subdiagonal phases."""
     rng = np.random.default_rng(77)
     n = 200
     A = rng.standard_normal((n, n))
@@ -284,7 +285,15 @@ def test_single_hessenberg_and_qr_decompose_native(ctx, dtype):
     assert H.dtype == dtype
     sc = np.linalg.norm(A.astype(np.complex128))
     Hr = O.hessenberg(A.astype(np.complex128 if np.iscomplexobj(A) else np.float64))
-    assert np.abs(np.abs(H) - np.abs(Hr)).max() <= 2e-5 * sc
+    Hd, Hrc = H.astype(np.complex128), Hr.astype(np.complex128)
+    d = np.ones(n, np.complex128)
+    for i in range(n - 1):   # h(i+1, i) = d(i+1) h_ref(i+1, i) conj(d(i))
+        a, b = Hd[i + 1, i], Hrc[i + 1, i]
+        d[i + 1] = d[i] * (a / abs(a)) / (b / abs(b))
+    if not np.iscomplexobj(A):
+        assert np.all(np.abs(np.abs(d.real) - 1) <= 1e-6) and np.all(np.abs(d.imag) <= 1e-6)
+        d = np.sign(d.real)
+    assert np.abs(d[:, None] * Hrc * np.conj(d)[None, :] - Hd).max() <= 2e-5 * sc
     assert np.abs(np.tril(H, -2)).max() == 0.0
     B = A[:, :150]
     Q, R = E.qr_decompose(ctx, B)
