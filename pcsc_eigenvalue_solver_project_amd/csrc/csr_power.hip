@@ -98,6 +98,7 @@ struct CsrArgs {
     const int2* blev;        // per level {entry offset, runs}
     const int32_t* bchunk;   // per chunk: its steps [bchunk[c], bchunk[c + 1])
     int32_t nchunks;
+    int32_t brows;           // rows per chunk (<= kBinRows of the instantiation)
     int32_t bcbits;          // log2 of the columns per block
     int32_t cbeg, cend;      // chunks of this launch (an iteration split in two row parts)
     int32_t cont;            // second part: read the first part's decision, add to its partial
@@ -1132,6 +1133,9 @@ __global__ __launch_bounds__(kThreads) void csr_row_kernel(CsrArgs<S> a, int par
 // and at most kBinLev levels; the host cuts longer runs into several steps (same lanes, no barrier).
 template <class S, int kKB> inline constexpr int kBinRows = kKB * 1024 / (int)sizeof(S);
 constexpr int kBinLev = 4;
+// the largest row-sum array one workgroup can hold beside its other LDS (160 KiB per CU): one
+// workgroup per CU, e.g. 10M f64 rows in two exact rounds of 19532-row chunks over 256 CUs
+constexpr int kBinKBMax = 153;
 #ifndef EIGSOL_BIN_COND
 #define EIGSOL_BIN_COND 1
 #endif
@@ -1218,8 +1222,8 @@ __global__ __launch_bounds__(kNT) void csr_bin_kernel(CsrArgs<S> a, int parity) 
     };
     double n2 = 0.0, rr = 0.0, ri = 0.0;
     for (int c = a.cbeg + blockIdx.x; c < a.cend; c += gridDim.x) {
-        const int r0 = c * kRows;
-        const int nr = min(kRows, a.nrows - r0);
+        const int r0 = c * a.brows;
+        const int nr = min(a.brows, a.nrows - r0);
         for (int i = tid; i < nr; i += kNT) acc[i] = s_zero<S>();
         __syncthreads();
         const int s0 = a.bchunk[c], s1 = a.bchunk[c + 1];
@@ -1731,18 +1735,34 @@ static int build_bins(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, 
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_MIN")) min_bytes = std::atof(e);
     if (mode != 2 && (double)A->ncols * (double)sb < min_bytes) return EIGSOL_OK;
     // KB of row sums per workgroup: 64 where that still leaves >= 1024 chunks, else 16
-    // (EIGSOL_CSR_BIN_LDS); threads per workgroup 1024 or 256 (EIGSOL_CSR_BIN_NT)
+    // (EIGSOL_CSR_BIN_LDS = 16 | 64 | 128 | 153); threads per workgroup 1024 or 256 (EIGSOL_CSR_BIN_NT)
     int lds_kb = (double)A->nrows * (double)sb >= 1024.0 * 65536.0 ? 64 : 16;
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_LDS")) {
         const int v = std::atoi(e);
-        lds_kb = v == 128 ? 128 : v == 64 ? 64 : 16;
+        lds_kb = v == kBinKBMax ? kBinKBMax : v == 128 ? 128 : v == 64 ? 64 : 16;
     }
     int nt = sb >= 16 ? 256 : 1024;   // complex<double>: the 1024-thread instantiation spills
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_NT")) {
         const int v = std::atoi(e);
         nt = v == 256 ? 256 : v == 512 ? 512 : 1024;
     }
-    const int R = lds_kb * 1024 / (int)sb;   // kBinRows<S, lds_kb>
+    const int Rmax = lds_kb * 1024 / (int)sb;   // kBinRows<S, lds_kb>
+    int R = Rmax;
+    // Balanced chunks (EIGSOL_CSR_BIN_BALANCE, default on): the resident workgroups take the chunks
+    // round-robin, so R rows per chunk are chosen to make the chunk count an exact multiple of the
+    // grid (every workgroup gets the same number of equal chunks) with the fewest rounds that fit
+    // the LDS; otherwise a partial last round leaves part of the chip idle while every round still
+    // sweeps x (10M uniform at 64 KB: 1221 chunks over 512 workgroups, the third round 38 % full)
+    int balance = 1;
+    if (const char* e = std::getenv("EIGSOL_CSR_BIN_BALANCE")) balance = std::atoi(e);
+    if (balance) {
+        const int per_cu = std::max(1, std::min(2, (160 * 1024) / (lds_kb * 1024 + 2048)));
+        const int64_t G = (int64_t)per_cu * A->ctx->num_cus;
+        const int64_t rounds = std::max<int64_t>(1, (A->nrows + G * Rmax - 1) / (G * Rmax));
+        int64_t r = (A->nrows + rounds * G - 1) / (rounds * G);
+        r = ((r + 63) / 64) * 64;
+        R = (int)std::max<int64_t>(64, std::min<int64_t>(Rmax, r));
+    }
     int rbits = 0;
     while ((1 << rbits) < R) ++rbits;
     int cbits = 0;
@@ -1850,6 +1870,7 @@ static int build_bins(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, 
         return fail(EIGSOL_E_HIP, std::string("eigsol_csr_create: binned upload: ") + hipGetErrorString(e));
     A->binned = lds_kb;
     A->bin_nt = nt;
+    A->bin_rows = R;
     return EIGSOL_OK;
 }
 
@@ -1902,9 +1923,10 @@ static const void* bin_kernel_ptr_kb(int nt) {
 }
 template <class S, bool kPower>
 static const void* bin_kernel_ptr(const eigsol_csr* A) {
-    return A->binned == 128  ? bin_kernel_ptr_kb<S, kPower, 128>(A->bin_nt)
-           : A->binned == 64 ? bin_kernel_ptr_kb<S, kPower, 64>(A->bin_nt)
-                             : bin_kernel_ptr_kb<S, kPower, 16>(A->bin_nt);
+    return A->binned == kBinKBMax ? bin_kernel_ptr_kb<S, kPower, kBinKBMax>(A->bin_nt)
+           : A->binned == 128     ? bin_kernel_ptr_kb<S, kPower, 128>(A->bin_nt)
+           : A->binned == 64      ? bin_kernel_ptr_kb<S, kPower, 64>(A->bin_nt)
+                                  : bin_kernel_ptr_kb<S, kPower, 16>(A->bin_nt);
 }
 
 template <class S>
@@ -1996,6 +2018,7 @@ static CsrArgs<S> make_args(const eigsol_csr* A, int64_t xlen) {
     a.blev = (const int2*)A->blev;
     a.bchunk = A->bchunk;
     a.nchunks = A->nchunks;
+    a.brows = A->bin_rows;
     a.bcbits = A->bcbits;
     a.cbeg = 0;
     a.cend = A->nchunks;
@@ -2131,7 +2154,7 @@ int csr_power_launch(eigsol_csr* A, int64_t xlen, void* buf0, void* buf1, PowerC
 // Own rows in the first part of a split iteration (binned layout): whole chunks of the first half.
 int64_t csr_bin_split_row(const eigsol_csr* A) {
     if (!A->binned) return A->nrows;
-    const int64_t rows = (int64_t)A->binned * 1024 / (int64_t)scalar_bytes(A->dtype);   // kBinRows
+    const int64_t rows = A->bin_rows;   // rows per chunk
     return std::min<int64_t>(A->nrows, (int64_t)bin_split_chunk(A) * rows);
 }
 

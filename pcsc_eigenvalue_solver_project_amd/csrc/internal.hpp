@@ -275,6 +275,7 @@ struct eigsol_csr {
     // kBinRows rows, entries ordered (column block, level, row), packed (row << bcbits | column).
     int32_t binned = 0;            // 0: not built; else KB of LDS row sums (kernel instantiation)
     int32_t bin_nt = 256;          // threads per workgroup (kernel instantiation)
+    int32_t bin_rows = 0;          // rows per chunk (<= the instantiation's LDS row sums)
     int32_t nchunks = 0, bcbits = 0, nbsteps = 0;
     uint32_t* bpk = nullptr;
     void* bval = nullptr;

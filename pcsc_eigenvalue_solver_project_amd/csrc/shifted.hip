@@ -35,7 +35,7 @@ struct GmresSolver;
 int gmres_create(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const int32_t* ci, const void* v,
                  double sre, double sim, GmresSolver** out);
 void gmres_free(GmresSolver* g);
-int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev);
+int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev, const double* guess = nullptr);
 void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps);
 
 namespace dev {
@@ -2335,12 +2335,29 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.sig_im = f->sig_im;
         hipLaunchKernelGGL((dev::shift_decide_kernel<S>), dim3(1), dim3(64), 0, st, a, parity);
         int32_t done = 0;
-        double nrm = 0.0;
+        PowerCarry cr{};
         EIGSOL_HIP(hipMemcpyAsync(&done, &ctl->done, sizeof(done), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipMemcpyAsync(&nrm, &ctl->st[parity ^ 1].nrm, sizeof(nrm), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipMemcpyAsync(&cr, &ctl->st[parity ^ 1], sizeof(cr), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(hipStreamSynchronize(st));
         if (done) return EIGSOL_OK;
-        const int rc = gmres_solve(f->gm, parity ? buf0 : buf1, nrm, parity ? buf1 : buf0);
+        // warm start from the latest eigenvalue estimate: y ~ x / (lambda - sigma) (gmres.hip)
+        // EIGSOL_GMRES_WARM=0 starts every solve from zero
+        static const bool warm = [] {
+            const char* e = std::getenv("EIGSOL_GMRES_WARM");
+            return !e || std::atoi(e) != 0;
+        }();
+        double guess[2] = {0.0, 0.0};
+        bool use_guess = false;
+        if (warm && cr.t >= 1) {
+            const double dre = cr.rho_re - f->sig_re, dim = dtype_complex(f->dtype) ? cr.rho_im - f->sig_im : 0.0;
+            const double d2 = dre * dre + dim * dim;
+            if (d2 > 0.0 && std::isfinite(d2)) {
+                guess[0] = dre / d2;
+                guess[1] = -dim / d2;
+                use_guess = true;
+            }
+        }
+        const int rc = gmres_solve(f->gm, parity ? buf0 : buf1, cr.nrm, parity ? buf1 : buf0, use_guess ? guess : nullptr);
         if (rc == EIGSOL_E_SOLVER) {
             // switch to the densified LU and redo this launch on it: the dense kernel's prologue
             // re-evaluates the same decision from the same carry record (idempotent)
