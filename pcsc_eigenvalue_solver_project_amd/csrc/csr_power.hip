@@ -1734,9 +1734,12 @@ static int build_bins(eigsol_csr* A, const int32_t* rowptr, const int32_t* col, 
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_BYTES")) blk_bytes = std::max(1024.0, std::atof(e));
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_MIN")) min_bytes = std::atof(e);
     if (mode != 2 && (double)A->ncols * (double)sb < min_bytes) return EIGSOL_OK;
-    // KB of row sums per workgroup: 64 where that still leaves >= 1024 chunks, else 16
-    // (EIGSOL_CSR_BIN_LDS = 16 | 64 | 128 | 153); threads per workgroup 1024 or 256 (EIGSOL_CSR_BIN_NT)
-    int lds_kb = (double)A->nrows * (double)sb >= 1024.0 * 65536.0 ? 64 : 16;
+    // KB of row sums per workgroup: 153 (one workgroup per CU) where the rows' sums exceed 64 MB,
+    // else 16 (EIGSOL_CSR_BIN_LDS = 16 | 64 | 128 | 153); threads per workgroup 1024 or 256
+    // (EIGSOL_CSR_BIN_NT).  Round 4 A/B (tools/bin_balance_ab.py, balanced chunks): 10M x 10 uniform
+    // 16 / 64 / 128 / 153 KB 1.733 / 0.859 / 0.761 / 0.751 ms (fewer chunk rounds: fewer sweeps of x);
+    // 1M x 16 0.123 / 0.123 / 0.125 / 0.125 ms
+    int lds_kb = (double)A->nrows * (double)sb >= 1024.0 * 65536.0 ? kBinKBMax : 16;
     if (const char* e = std::getenv("EIGSOL_CSR_BIN_LDS")) {
         const int v = std::atoi(e);
         lds_kb = v == kBinKBMax ? kBinKBMax : v == 128 ? 128 : v == 64 ? 64 : 16;

@@ -886,7 +886,20 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     EIGSOL_HIP(hipMalloc(&dU, dev::kMaxGroups * dev::kWin * dev::kWin * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&dsh, 4 * dev::kMaxBulges * sizeof(double)));
     EIGSOL_HIP(hipMalloc(&dinfo, 64));
-    std::vector<double> ds(2 * n), swr(2 * dev::kMaxBulges), swi(2 * dev::kMaxBulges);
+    // every per-sweep transfer goes through pinned host memory: a pageable hipMemcpyAsync is staged
+    // by the runtime and waited for with a sleeping wait, ~1 ms per copy (round-4 kernel trace,
+    // tools/gap_analysis.py), more than a sweep's kernels at the end of the iteration
+    struct Staging {
+        int info[8];
+        double awr[dev::kAedMax], awi[dev::kAedMax];
+        double swr[2 * dev::kMaxBulges], swi[2 * dev::kMaxBulges], sh[2 * dev::kMaxBulges];
+    };
+    Staging* hp = nullptr;
+    double* ds = nullptr;   // deflation scans: diagonal [0, n), subdiagonal [n, 2n)
+    EIGSOL_HIP(hipHostMalloc(&hp, sizeof(Staging), hipHostMallocDefault));
+    EIGSOL_HIP(hipHostMalloc(&ds, 2 * n * sizeof(double), hipHostMallocDefault));
+    double* const swr = hp->swr;
+    double* const swi = hp->swi;
     int rc = EIGSOL_OK;
     int sweeps = 0, failed = 0;
     int ihi = (int)n - 1;
@@ -941,21 +954,27 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     auto finish_small = [&](int l, int hi) -> int {
         const int m = hi - l + 1;
         EIGSOL_TRY(hqr_small(st, H + l + (int64_t)l * n, n, m, std::max(1, maxits), dwr + l, dwi + l, dinfo));
-        int info[3];
-        EIGSOL_HIP(hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipStreamSynchronize(st));
+        int* info = hp->info;
+        EIGSOL_HIP(hipMemcpyAsync(info, dinfo, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(stream_wait(st));
         if (info[0]) failed = 1;
         sweeps = std::max(sweeps, info[1]);
         return EIGSOL_OK;
     };
-    while (rc == EIGSOL_OK && ihi >= 0) {
-        // deflation scan of [0, ihi]
+    // deflation scan of [0, ihi]: diagonal and subdiagonal into pinned host memory (only the
+    // ihi + 1 leading entries of each half travel)
+    auto scan = [&]() -> int {
         hipLaunchKernelGGL(dev::diag_sub_kernel, dim3((ihi + 256) / 256), dim3(256), 0, st, H, n, ihi, dds);
-        if (hipMemcpyAsync(ds.data(), dds, 2 * n * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) {
-            rc = fail(EIGSOL_E_HIP, "francis: deflation scan");
-            break;
-        }
+        if (hipMemcpyAsync(ds, dds, (ihi + 1) * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(ds + n, dds + n, (ihi + 1) * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            stream_wait(st) != hipSuccess)
+            return fail(EIGSOL_E_HIP, "francis: deflation scan");
+        return EIGSOL_OK;
+    };
+    bool scanned = false;   // the previous sweep's closing scan is still current (nothing ran since)
+    while (rc == EIGSOL_OK && ihi >= 0) {
+        if (!scanned && (rc = scan()) != EIGSOL_OK) break;
+        scanned = false;
         int l = ihi;
         while (l > 0) {
             const double s0 = std::fabs(ds[l - 1]) + std::fabs(ds[l]);
@@ -982,12 +1001,13 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             const int kw = ihi - nw + 1;
             hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(64), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60,
                                aed_early ? 1 : 0, dwr, dwi, dU, dinfo);
-            int info[8];
-            std::vector<double> awr(nw), awi(nw);
-            if (hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(awr.data(), dwr + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(awi.data(), dwi + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess) {
+            int* info = hp->info;
+            double* const awr = hp->awr;
+            double* const awi = hp->awi;
+            if (hipMemcpyAsync(info, dinfo, 8 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(awr, dwr + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(awi, dwi + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                stream_wait(st) != hipSuccess) {
                 rc = fail(EIGSOL_E_HIP, "francis: aed");
                 break;
             }
@@ -1029,16 +1049,16 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             rc = hqr_small(st, H + (ihi - ns + 1) + (int64_t)(ihi - ns + 1) * n, n, ns, 60, dwr + ihi - ns + 1,
                            dwi + ihi - ns + 1, dinfo, shift_tol);
             if (rc != EIGSOL_OK) break;
-            if (hipMemcpyAsync(swr.data(), dwr + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(swi.data(), dwi + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess) {
+            if (hipMemcpyAsync(swr, dwr + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(swi, dwi + ihi - ns + 1, ns * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                stream_wait(st) != hipSuccess) {
                 rc = fail(EIGSOL_E_HIP, "francis: shifts");
                 break;
             }
         }
         // pair the shifts: conjugate pairs stay together, reals are paired in order;
         // every 6th stalled sweep uses exceptional shifts from the bottom subdiagonal
-        std::vector<double> sh(2 * nb);
+        double* const sh = hp->sh;   // 2 nb values; the chase reads them from dsh
         if (stall % 6 == 0) {
             for (int b = 0; b < nb; ++b) {
                 const double sc = std::fabs(ds[n + ihi - b]) + std::fabs(ds[ihi - b]) + 1e-300;
@@ -1070,7 +1090,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                 sh[2 * b + 1] = 0.0;
             }
         }
-        if (hipMemcpyAsync(dsh, sh.data(), 2 * nb * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess) {
+        if (hipMemcpyAsync(dsh, sh, 2 * nb * sizeof(double), hipMemcpyHostToDevice, st) != hipSuccess) {
             rc = fail(EIGSOL_E_HIP, "francis: shift upload");
             break;
         }
@@ -1151,13 +1171,9 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
             t0 = t1;
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "francis: launch"); break; }
-        // a deflation anywhere below resets the stall counter at the next scan
-        hipLaunchKernelGGL(dev::diag_sub_kernel, dim3((ihi + 256) / 256), dim3(256), 0, st, H, n, ihi, dds);
-        if (hipMemcpyAsync(ds.data(), dds, 2 * n * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) {
-            rc = fail(EIGSOL_E_HIP, "francis: deflation scan");
-            break;
-        }
+        // a deflation anywhere below resets the stall counter; the scan also serves the next pass
+        if ((rc = scan()) != EIGSOL_OK) break;
+        scanned = true;
         for (int k = ihi; k > l; --k)
             if (std::fabs(ds[n + k]) <= eps * (std::fabs(ds[k - 1]) + std::fabs(ds[k]))) {
                 sweeps = std::max(sweeps, stall);
@@ -1168,7 +1184,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     if (rc == EIGSOL_OK) {
         if (hipMemcpyAsync(wr, dwr, n * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipMemcpyAsync(wi, dwi, n * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
+            stream_wait(st) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "francis: download");
     }
     if (stats)
@@ -1177,6 +1193,8 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                      (long long)n, st_sweeps, st_windows, st_steps, st_small, st_small_rows, kSmall, st_aed, st_aed_defl,
                      aed_win, st_aed_steps, st_aed_ph[0] * 1e-5, st_aed_ph[1] * 1e-5, st_aed_ph[2] * 1e-5);
     for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo}) (void)hipFree(p);
+    (void)hipHostFree(ds);
+    (void)hipHostFree(hp);
     // iterations reported: sweeps spent on the slowest deflation (>= 1, the final check), so that
     // iterations <= maxIterations exactly when the iteration converged
     *sweeps_out = std::max(1, sweeps);

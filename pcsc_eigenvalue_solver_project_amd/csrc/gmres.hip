@@ -182,6 +182,7 @@ struct GmresSolver {
     void* x = nullptr;
     double* part = nullptr;
     double* hdev = nullptr;
+    double* hpin = nullptr;     // pinned host mirror of hdev: a pageable copy costs a sleeping wait (~1 ms)
     int G = 1;
     int64_t nnzM = 0;
     int last_steps = 0;
@@ -198,6 +199,7 @@ void gmres_free(GmresSolver* g) {
     if (g->M) csr_release(g->M);
     for (void* p : {g->V, g->Z, g->t1, g->w, g->x, (void*)g->part, (void*)g->hdev})
         if (p) hipFree(p);
+    if (g->hpin) hipHostFree(g->hpin);
     ctx_release(g->ctx);
     delete g;
 }
@@ -292,7 +294,7 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
         }
         hipMemcpyAsync(&zpiv, d_z, 4, hipMemcpyDeviceToHost, st);
         hipMemcpyAsync(lu.data(), d_v, g->nnzM * sizeof(S), hipMemcpyDeviceToHost, st);
-        if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) factorization");
+        if (stream_wait(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) factorization");
     }
     for (void* p : {(void*)d_rp, (void*)d_ci, (void*)d_v, (void*)d_dpos, (void*)d_rows, (void*)d_z})
         if (p) hipFree(p);
@@ -324,7 +326,8 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
          hipMalloc(&g->w, n * sb) != hipSuccess ||
          hipMalloc(&g->x, n * sb) != hipSuccess ||
          hipMalloc(&g->part, (size_t)g->G * (g->m + 1) * 2 * sizeof(double)) != hipSuccess ||
-         hipMalloc(&g->hdev, (size_t)(g->m + 2) * 6 * sizeof(double)) != hipSuccess))
+         hipMalloc(&g->hdev, (size_t)(g->m + 2) * 6 * sizeof(double)) != hipSuccess ||
+         hipHostMalloc(&g->hpin, (size_t)(g->m + 2) * 6 * sizeof(double), hipHostMallocDefault) != hipSuccess))
         rc = fail(EIGSOL_E_HIP, "solve_shifted: GMRES workspace");
     if (rc != EIGSOL_OK) {
         gmres_free(g);
@@ -361,9 +364,9 @@ static int cgs2(GmresSolver* g, S* V, int k, S* w, std::vector<hc>& h, double& w
     }
     hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
     hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev + 2 * stride);
-    std::vector<double> hb(2 * stride + 2);
-    EIGSOL_HIP(hipMemcpyAsync(hb.data(), g->hdev, hb.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-    EIGSOL_HIP(hipStreamSynchronize(st));
+    const double* hb = g->hpin;
+    EIGSOL_HIP(hipMemcpyAsync(g->hpin, g->hdev, (2 * stride + 2) * sizeof(double), hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(stream_wait(st));
     h.assign(k, hc(0.0, 0.0));
     for (int c = 0; c < k; ++c)
         h[c] = hc(hb[2 * c], hb[2 * c + 1]) + hc(hb[stride + 2 * c], hb[stride + 2 * c + 1]);
@@ -390,12 +393,11 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
     double bytes = 0.0;
     int steps = 0;
     auto norm_of = [&](S* v, double& out) -> int {
-        double hb[2];
         hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, v, n, 1, v, n, g->part);
         hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev);
-        EIGSOL_HIP(hipMemcpyAsync(hb, g->hdev, sizeof(hb), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipStreamSynchronize(st));
-        out = std::sqrt(hb[0]);
+        EIGSOL_HIP(hipMemcpyAsync(g->hpin, g->hdev, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(stream_wait(st));
+        out = std::sqrt(g->hpin[0]);
         return EIGSOL_OK;
     };
     auto precond = [&](const S* in, S* out) -> int {   // out = U^-1 L^-1 in
@@ -483,9 +485,9 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
                 for (int c = i + 1; c < k; ++c) s -= H[(size_t)c * (m + 1) + i] * yk[c];
                 yk[i] = s / H[(size_t)i * (m + 1) + i];
             }
-            std::vector<double> yb(2 * k);
+            double* yb = g->hpin;   // read by the copy before the next host write (norm_of syncs below)
             for (int i = 0; i < k; ++i) { yb[2 * i] = yk[i].real(); yb[2 * i + 1] = yk[i].imag(); }
-            EIGSOL_HIP(hipMemcpyAsync(g->hdev, yb.data(), yb.size() * sizeof(double), hipMemcpyHostToDevice, st));
+            EIGSOL_HIP(hipMemcpyAsync(g->hdev, yb, 2 * k * sizeof(double), hipMemcpyHostToDevice, st));
             hipLaunchKernelGGL((dev::gm_combine_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, Z, n, k, g->hdev, w, n, 1);
             hipLaunchKernelGGL((dev::gm_axpy_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, x, w, n);
             // true residual r = b - M x (the next cycle's start)

@@ -37,6 +37,12 @@ int fail(int status, const std::string& msg);
                                                     hipGetErrorString(_e));              \
     } while (0)
 
+// Host wait for a stream inside a host-driven iteration (QR sweeps, GMRES steps):
+// hipStreamSynchronize, or with EIGSOL_SYNC_SPIN=1 a busy poll of hipStreamQuery.  Round-4 A/B
+// (tools/sync_ab.sh): QR 4096^2 real 1.187 / 1.208 s, complex 2.77 / 2.58 s, GMRES 1M 9.11 / 9.20
+// ms per iteration (sync / spin) - within the run-to-run spread, so the default does not spin.
+hipError_t stream_wait(hipStream_t st);
+
 #define EIGSOL_TRY(expr)                  \
     do {                                  \
         int _s = (expr);                  \

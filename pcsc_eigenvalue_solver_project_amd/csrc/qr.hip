@@ -432,6 +432,7 @@ struct QrWork {
     S* v = nullptr;
     int* skip = nullptr;
     double* red = nullptr;
+    double* hred = nullptr;   // pinned host copy of red (a pageable copy sleeps ~1 ms per iteration)
 };
 
 template <class S>
@@ -439,6 +440,7 @@ int work_alloc(QrWork<S>& w, int64_t n) {
     EIGSOL_HIP(hipMalloc(&w.v, std::max<int64_t>(n, 1) * sizeof(S)));
     EIGSOL_HIP(hipMalloc(&w.skip, 64));
     EIGSOL_HIP(hipMalloc(&w.red, 64));
+    EIGSOL_HIP(hipHostMalloc(&w.hred, 64, hipHostMallocDefault));
     return EIGSOL_OK;
 }
 template <class S>
@@ -446,6 +448,7 @@ void work_free(QrWork<S>& w) {
     if (w.v) (void)hipFree(w.v);
     if (w.skip) (void)hipFree(w.skip);
     if (w.red) (void)hipFree(w.red);
+    if (w.hred) (void)hipHostFree(w.hred);
 }
 
 // one reflector: x = A(r0 : r0+m, col); left on A(r0 : r0+m, lc0 : lc1); right on B(0 : nr, r0 : r0+m)
@@ -532,7 +535,7 @@ static int hessenberg_host(eigsol_ctx* ctx, int64_t n, const void* A, void* Hout
     if (rc == EIGSOL_OK) rc = hessenberg_dev<S>(st, H, n, w);
     if (rc == EIGSOL_OK && hipMemcpyAsync(Hout, H, n * n * sizeof(S), hipMemcpyDeviceToHost, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "to_hessenberg: download");
-    if (rc == EIGSOL_OK && hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "to_hessenberg: sync");
+    if (rc == EIGSOL_OK && stream_wait(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "to_hessenberg: sync");
     work_free(w);
     (void)hipFree(H);
     return rc;
@@ -553,7 +556,7 @@ static int qr_decompose_host(eigsol_ctx* ctx, int64_t m, int64_t n, const void* 
         rc = fail(EIGSOL_E_HIP, "qr_decompose: download Q");
     if (rc == EIGSOL_OK && Rout && hipMemcpyAsync(Rout, R, m * n * sizeof(S), hipMemcpyDeviceToHost, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "qr_decompose: download R");
-    if (rc == EIGSOL_OK && hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_decompose: sync");
+    if (rc == EIGSOL_OK && stream_wait(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_decompose: sync");
     work_free(w);
     (void)hipFree(R);
     (void)hipFree(Q);
@@ -588,9 +591,9 @@ static int qr_unshifted_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_
         if (rc != EIGSOL_OK) break;
         hipLaunchKernelGGL((dev::gemm_nn_kernel<S>), g, dim3(256), 0, st, R, Q, H, n);
         hipLaunchKernelGGL((dev::subdiag_frob_kernel<S>), dim3(1), dim3(1024), 0, st, H, n, w.red);
-        double red[2];
-        if (hipMemcpyAsync(red, w.red, sizeof(red), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) {
+        const double* red = w.hred;
+        if (hipMemcpyAsync(w.hred, w.red, 2 * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            stream_wait(st) != hipSuccess) {
             rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: convergence check");
             break;
         }
@@ -602,7 +605,7 @@ static int qr_unshifted_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_
     if (rc == EIGSOL_OK) {
         hipLaunchKernelGGL((dev::diag_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, H, n, d);
         if (hipMemcpyAsync(eig, d, n * sizeof(S), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
+            stream_wait(st) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: download");
     }
     if (iters) *iters = iter + 1;
@@ -641,7 +644,7 @@ static int qr_francis_host(eigsol_ctx* ctx, int64_t n, const double* A, int max_
             hipLaunchKernelGGL(dev::absmax_kernel, dim3(1024), dim3(256), 0, st, H, n * n, dmax);
             hipMemcpyAsync(&bits, dmax, sizeof(bits), hipMemcpyDeviceToHost, st);
             (void)hipFreeAsync(dmax, st);
-            if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: norm-range check");
+            if (stream_wait(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: norm-range check");
         }
     }
     if (rc == EIGSOL_OK) {
@@ -696,7 +699,7 @@ static int qr_francis_c128_host(eigsol_ctx* ctx, int64_t n, const void* A, int m
             hipLaunchKernelGGL(dev::absmax_kernel, dim3(1024), dim3(256), 0, st, Hd, 2 * n * n, dmax);
             hipMemcpyAsync(&bits, dmax, sizeof(bits), hipMemcpyDeviceToHost, st);
             (void)hipFreeAsync(dmax, st);
-            if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: norm-range check");
+            if (stream_wait(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: norm-range check");
             double amax;
             std::memcpy(&amax, &bits, sizeof(amax));
             const double smlnum = std::sqrt(std::numeric_limits<double>::min()) / std::numeric_limits<double>::epsilon();

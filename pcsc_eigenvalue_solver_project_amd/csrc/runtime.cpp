@@ -1,5 +1,6 @@
 // Context, error reporting and device-memory helpers of the C ABI (include/eigsol_hip.h).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -17,6 +18,18 @@ int fail(int status, const std::string& msg) {
 }
 
 void dist_release_comm(eigsol_ctx* ctx);   // dist.hip
+
+hipError_t stream_wait(hipStream_t st) {
+    static const bool spin = [] {
+        const char* e = std::getenv("EIGSOL_SYNC_SPIN");
+        return e && std::atoi(e) != 0;
+    }();
+    if (!spin) return hipStreamSynchronize(st);
+    hipError_t e;
+    while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    }
+    return e;
+}
 
 void ctx_retain(eigsol_ctx* c) { c->refs.fetch_add(1); }
 

@@ -43,6 +43,8 @@ constexpr int kMaxMulti = 4;      // solves per multi-solve launch (one head wav
 }
 static constexpr int kMultiDefault = 4;   // EIGSOL_TRSV_MULTI (config 5 per iteration: K = 1 0.674, 2 0.502, 3 0.439, 4 0.414 ms)
 
+constexpr size_t kPinBytes = 256;   // ShiftFactor::hpin
+
 struct ShiftFactor {
     eigsol_ctx* ctx = nullptr;
     int dtype = EIGSOL_F64;
@@ -50,6 +52,7 @@ struct ShiftFactor {
     int kind = 0;                 // 0 triangular CSR, 1 dense LU, 2 ILU(0)-preconditioned GMRES, 3 band LU
     GmresSolver* gm = nullptr;    // kind 2 (gmres.hip)
     BandFactor* band = nullptr;   // kind 3 (band_lu.hip)
+    void* hpin = nullptr;         // pinned host scratch for per-solve readbacks (pageable copies sleep ~1 ms)
     eigsol_csr* src = nullptr;    // kind 2: A, retained for the densified-LU fallback
     int fell_back = 0;            // kind 1 reached through the GMRES fallback
     double sig_re = 0.0, sig_im = 0.0;
@@ -1543,6 +1546,7 @@ static void shift_free(ShiftFactor* f) {
         if (j < dev::kMaxMulti - 1 && f->aux[j]) hipFree(f->aux[j]);
         for (void* zb : f->zm[j]) if (zb) hipFree(zb);
     }
+    if (f->hpin) hipHostFree(f->hpin);
     ctx_release(f->ctx);
     delete f;
 }
@@ -2272,9 +2276,11 @@ int shift_grid(const ShiftFactor* f) { return (f->kind == 0 || f->dense_multi) ?
 
 int shift_error(ShiftFactor* f) {
     if (f->kind != 0 && !f->dense_multi) return EIGSOL_OK;
-    int32_t e = 0;
-    EIGSOL_HIP(hipMemcpyAsync(&e, f->err, 4, hipMemcpyDeviceToHost, f->ctx->stream));
-    EIGSOL_HIP(hipStreamSynchronize(f->ctx->stream));
+    if (!f->hpin) EIGSOL_HIP(hipHostMalloc(&f->hpin, kPinBytes, hipHostMallocDefault));
+    int32_t* he = static_cast<int32_t*>(f->hpin);
+    EIGSOL_HIP(hipMemcpyAsync(he, f->err, 4, hipMemcpyDeviceToHost, f->ctx->stream));
+    EIGSOL_HIP(stream_wait(f->ctx->stream));
+    const int32_t e = *he;
     if (e) return fail(EIGSOL_E_SOLVER, "triangular solve: dependency wait exceeded its bound (internal error)");
     return EIGSOL_OK;
 }
@@ -2334,17 +2340,27 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.sig_re = f->sig_re;
         a.sig_im = f->sig_im;
         hipLaunchKernelGGL((dev::shift_decide_kernel<S>), dim3(1), dim3(64), 0, st, a, parity);
-        int32_t done = 0;
-        PowerCarry cr{};
-        EIGSOL_HIP(hipMemcpyAsync(&done, &ctl->done, sizeof(done), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipMemcpyAsync(&cr, &ctl->st[parity ^ 1], sizeof(cr), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipStreamSynchronize(st));
+        struct Decision {
+            PowerCarry cr;
+            int32_t done;
+        };
+        static_assert(sizeof(Decision) <= kPinBytes, "pinned scratch");
+        if (!f->hpin) EIGSOL_HIP(hipHostMalloc(&f->hpin, kPinBytes, hipHostMallocDefault));
+        Decision* hd = static_cast<Decision*>(f->hpin);
+        EIGSOL_HIP(hipMemcpyAsync(&hd->done, &ctl->done, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipMemcpyAsync(&hd->cr, &ctl->st[parity ^ 1], sizeof(PowerCarry), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(stream_wait(st));
+        const int32_t done = hd->done;
+        const PowerCarry cr = hd->cr;
         if (done) return EIGSOL_OK;
-        // warm start from the latest eigenvalue estimate: y ~ x / (lambda - sigma) (gmres.hip)
-        // EIGSOL_GMRES_WARM=0 starts every solve from zero
+        // EIGSOL_GMRES_WARM=1: warm start from the latest eigenvalue estimate, y ~ x / (lambda - sigma)
+        // (gmres.hip).  Off by default: round-4 A/B on config 5's matrix made general (tools/gmres_warm_ab.py)
+        // gave 54 against 55 Arnoldi steps over the run and 9.1 against 8.9 ms per iteration - the
+        // guess only beats x0 = 0 once the iterate's residual is below |lambda - sigma|, i.e. in the
+        // last one or two iterations
         static const bool warm = [] {
             const char* e = std::getenv("EIGSOL_GMRES_WARM");
-            return !e || std::atoi(e) != 0;
+            return e && std::atoi(e) != 0;
         }();
         double guess[2] = {0.0, 0.0};
         bool use_guess = false;

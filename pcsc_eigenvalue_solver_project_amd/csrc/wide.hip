@@ -500,7 +500,7 @@ static int csr_shadow(eigsol_csr* A) {
     if (hipMemcpyAsync(rp.data(), A->rowptr, (n + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
         (nnz && hipMemcpyAsync(ci.data(), A->col, nnz * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess) ||
         (nnz && hipMemcpyAsync(hv.data(), dv, hv.size() * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess) ||
-        hipStreamSynchronize(st) != hipSuccess)
+        stream_wait(st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "double-double matrix: fp64 shadow download");
     (void)hipFree(dv);
     EIGSOL_TRY(rc);
@@ -531,7 +531,7 @@ static int dense_shadow(eigsol_dense* A) {
             hipLaunchKernelGGL((wdev::hi_kernel<dd>), dim3(nblk(cnt)), dim3(wdev::kT), 0, st, cnt,
                                static_cast<const dd*>(A->a), static_cast<double*>(B->a));
     }
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+    if (hipGetLastError() != hipSuccess || stream_wait(st) != hipSuccess) {
         dense_release(B);
         return fail(EIGSOL_E_HIP, "double-double matrix: fp64 shadow");
     }
@@ -558,8 +558,8 @@ struct WideSession {
     double* d64 = nullptr;  // fp64 correction
     dd* part = nullptr;     // reduction partials (3 per block)
     double* dpart = nullptr;
-    std::vector<dd> hpart;
-    std::vector<double> hdpart;
+    dd* hpart = nullptr;       // pinned host copies of part / dpart (a pageable copy sleeps ~1 ms)
+    double* hdpart = nullptr;
     // reference loop state (power_method.hpp:60-96 / shifted_inverse_power_solver.hpp:36-76)
     eigsol_solver_options opts{1000, 1e-10};
     bool begun = false, done = false, converged = false, initialized = false;
@@ -579,6 +579,8 @@ void wide_session_free(WideSession* s) {
     hipStreamSynchronize(s->ctx->stream);
     for (void* p : {s->x, s->y, s->z, s->r, (void*)s->r64, (void*)s->d64, (void*)s->part, (void*)s->dpart})
         if (p) hipFree(p);
+    for (void* p : {(void*)s->hpart, (void*)s->hdpart})
+        if (p) hipHostFree(p);
     if (s->f) shift_factor_free(s->f);
     if (s->csr) csr_release(s->csr);
     if (s->dense) dense_release(s->dense);
@@ -599,8 +601,8 @@ static int reduce(WideSession* s, const void* a, const void* w, dd& n2, cdd& dot
     hipLaunchKernelGGL((wdev::dot_kernel<T>), dim3(g), dim3(wdev::kT), 0, st, s->n, static_cast<const T*>(a),
                        static_cast<const T*>(w), s->part);
     EIGSOL_HIP(hipGetLastError());
-    EIGSOL_HIP(hipMemcpyAsync(s->hpart.data(), s->part, 3 * g * sizeof(dd), hipMemcpyDeviceToHost, st));
-    EIGSOL_HIP(hipStreamSynchronize(st));
+    EIGSOL_HIP(hipMemcpyAsync(s->hpart, s->part, 3 * g * sizeof(dd), hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(stream_wait(st));
     n2 = dd{0.0, 0.0};
     dot = cdd{};
     for (unsigned b = 0; b < g; ++b) {
@@ -637,8 +639,8 @@ static int refine_solve(WideSession* s, const void* b, void* y) {
         hipLaunchKernelGGL((wdev::accum_kernel<T>), dim3(g), dim3(wdev::kT), 0, st, n, static_cast<T*>(y), s->d64,
                            1.0, s->dpart);
         EIGSOL_HIP(hipGetLastError());
-        EIGSOL_HIP(hipMemcpyAsync(s->hdpart.data(), s->dpart, 2 * g * sizeof(double), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipStreamSynchronize(st));
+        EIGSOL_HIP(hipMemcpyAsync(s->hdpart, s->dpart, 2 * g * sizeof(double), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(stream_wait(st));
         ++s->refine_steps;
         s->solve_bytes += fbytes + rbytes;
         double nd = 0.0, ny = 0.0;
@@ -686,14 +688,14 @@ int wide_session_create(eigsol_ctx* ctx, eigsol_csr* csr, eigsol_dense* dense, c
     if (rc == EIGSOL_OK &&
         (hipMalloc(&s->x, vb) != hipSuccess || hipMalloc(&s->y, vb) != hipSuccess || hipMalloc(&s->z, vb) != hipSuccess ||
          hipMalloc(&s->part, 3 * g * sizeof(dd)) != hipSuccess ||
+         hipHostMalloc(&s->hpart, 3 * g * sizeof(dd), hipHostMallocDefault) != hipSuccess ||
+         hipHostMalloc(&s->hdpart, 2 * g * sizeof(double), hipHostMallocDefault) != hipSuccess ||
          (s->shifted && (hipMalloc(&s->r, vb) != hipSuccess ||
                          hipMalloc(&s->r64, (size_t)std::max<int64_t>(s->n, 1) * (s->dtype == EIGSOL_CDD ? 16 : 8)) != hipSuccess ||
                          hipMalloc(&s->d64, (size_t)std::max<int64_t>(s->n, 1) * (s->dtype == EIGSOL_CDD ? 16 : 8)) != hipSuccess ||
                          hipMalloc(&s->dpart, 2 * g * sizeof(double)) != hipSuccess))))
         rc = fail(EIGSOL_E_HIP, "double-double session: hipMalloc");
     if (rc != EIGSOL_OK) { wide_session_free(s); return rc; }
-    s->hpart.resize(3 * g);
-    s->hdpart.resize(2 * g);
     *out = s;
     return EIGSOL_OK;
 }
@@ -721,7 +723,7 @@ static int begin_t(WideSession* s, const eigsol_solver_options* opts, const void
         EIGSOL_TRY(apply<T>(s, s->x, s->y, nullptr, W<T>::zero(), 1));
         EIGSOL_TRY(reduce<T>(s, s->y, nullptr, s->pend_n2, dummy));
     }
-    EIGSOL_HIP(hipStreamSynchronize(st));
+    EIGSOL_HIP(stream_wait(st));
     s->begun = true;
     return EIGSOL_OK;
 }
@@ -845,7 +847,7 @@ int wide_solve_shifted(eigsol_csr* csr, eigsol_dense* dense, const void* sigma, 
     if (rc == EIGSOL_OK)
         rc = by_wide(s->dtype, [&](auto tag) { return refine_solve<decltype(tag)>(s, s->x, s->y); });
     if (rc == EIGSOL_OK && (hipMemcpyAsync(x, s->y, nb * s->sb, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                            hipStreamSynchronize(st) != hipSuccess))
+                            stream_wait(st) != hipSuccess))
         rc = fail(EIGSOL_E_HIP, "solve_shifted: download");
     wide_session_free(s);
     return rc;
@@ -918,7 +920,7 @@ int whessenberg_host(eigsol_ctx* ctx, int64_t n, const void* A, void* Hout) {
         rc = fail(EIGSOL_E_HIP, "to_hessenberg: upload");
     if (rc == EIGSOL_OK) rc = whessenberg<T>(st, H, n, w);
     if (rc == EIGSOL_OK && (hipMemcpyAsync(Hout, H, n * n * sizeof(T), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                            hipStreamSynchronize(st) != hipSuccess))
+                            stream_wait(st) != hipSuccess))
         rc = fail(EIGSOL_E_HIP, "to_hessenberg: download");
     wqr_free(w);
     (void)hipFree(H);
@@ -943,7 +945,7 @@ int wqr_decompose_host(eigsol_ctx* ctx, int64_t m, int64_t n, const void* A, voi
         rc = fail(EIGSOL_E_HIP, "qr_decompose: download Q");
     if (rc == EIGSOL_OK && Rout && hipMemcpyAsync(Rout, R, m * n * sizeof(T), hipMemcpyDeviceToHost, st) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "qr_decompose: download R");
-    if (rc == EIGSOL_OK && hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_decompose: sync");
+    if (rc == EIGSOL_OK && stream_wait(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "qr_decompose: sync");
     wqr_free(w);
     (void)hipFree(R);
     (void)hipFree(Q);
@@ -980,7 +982,7 @@ int wqr_unshifted_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_iter, 
         hipLaunchKernelGGL((wdev::subdiag_frob_kernel<T>), dim3(1), dim3(wdev::kT), 0, st, H, n, w.red);
         dd red[2];
         if (hipMemcpyAsync(red, w.red, sizeof(red), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) {
+            stream_wait(st) != hipSuccess) {
             rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: convergence check");
             break;
         }
@@ -994,7 +996,7 @@ int wqr_unshifted_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_iter, 
     if (rc == EIGSOL_OK) {
         hipLaunchKernelGGL((wdev::diag_kernel<T>), dim3(nblk(n)), dim3(wdev::kT), 0, st, H, n, d);
         if (hipMemcpyAsync(eig, d, n * sizeof(T), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
+            stream_wait(st) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: download");
     }
     if (iters) *iters = iter + 1;

@@ -789,7 +789,20 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
     cplx* dV = nullptr;   // the AED window's unitary factor
     if (rc == EIGSOL_OK && hipMalloc(&dV, (size_t)dev::kZSmall * dev::kZSmall * sizeof(cplx)) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "complex QR: hipMalloc");
-    std::vector<cplx> ds(2 * n), aw(dev::kZSmall);
+    // every per-sweep transfer goes through pinned host memory: a pageable hipMemcpyAsync is staged
+    // by the runtime and waited for with a sleeping wait, ~1 ms per copy (round-4 kernel trace of
+    // 4096^2: 1.12 s of 2.8 s idle after such copies, tools/gap_analysis.py)
+    struct Staging {
+        int info[8];
+        cplx aw[dev::kZSmall];
+        cplx sh[2 * dev::kZMaxBulges];
+    };
+    Staging* hp = nullptr;
+    cplx* ds = nullptr;   // deflation scans: diagonal [0, n), subdiagonal [n, 2n)
+    if (rc == EIGSOL_OK && (hipHostMalloc(&hp, sizeof(Staging), hipHostMallocDefault) != hipSuccess ||
+                            hipHostMalloc(&ds, 2 * n * sizeof(cplx), hipHostMallocDefault) != hipSuccess))
+        rc = fail(EIGSOL_E_HIP, "complex QR: hipHostMalloc");
+    cplx* const aw = hp ? hp->aw : nullptr;
     int sweeps = 0, failed = 0, stall = 0;
     int st_sweeps = 0, st_aed = 0, st_aed_defl = 0, st_small = 0;
     static const bool stats = std::getenv("EIGSOL_QR_STATS") != nullptr;
@@ -798,18 +811,23 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
     auto small = [&](int l, int hi, cplx* wdst, int info[2]) -> int {
         hipLaunchKernelGGL(dev::zhqr_wave_kernel, dim3(1), dim3(64), 0, st, H + l + (int64_t)l * n, (int64_t)n,
                            hi - l + 1, wdst, dinfo);
-        EIGSOL_HIP(hipMemcpyAsync(info, dinfo, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipStreamSynchronize(st));
+        EIGSOL_HIP(hipMemcpyAsync(hp->info, dinfo, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(stream_wait(st));
+        info[0] = hp->info[0];
+        info[1] = hp->info[1];
         return EIGSOL_OK;
     };
-    auto scan = [&]() -> int {
+    auto scan = [&]() -> int {   // only the ihi + 1 leading entries of each half travel
         hipLaunchKernelGGL(dev::zdiag_sub_kernel, dim3((ihi + 256) / 256), dim3(256), 0, st, H, (int64_t)n, ihi, dds);
-        EIGSOL_HIP(hipMemcpyAsync(ds.data(), dds, 2 * n * sizeof(cplx), hipMemcpyDeviceToHost, st));
-        EIGSOL_HIP(hipStreamSynchronize(st));
+        EIGSOL_HIP(hipMemcpyAsync(ds, dds, (ihi + 1) * sizeof(cplx), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipMemcpyAsync(ds + n, dds + n, (ihi + 1) * sizeof(cplx), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(stream_wait(st));
         return EIGSOL_OK;
     };
+    bool scanned = false;   // the previous sweep's closing scan is still current (nothing ran since)
     while (rc == EIGSOL_OK && ihi >= 0) {
-        if ((rc = scan()) != EIGSOL_OK) break;
+        if (!scanned && (rc = scan()) != EIGSOL_OK) break;
+        scanned = false;
         int l = ihi;
         while (l > 0) {
             const cplx sd = ds[n + l];
@@ -862,10 +880,10 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             const int kw = ihi - nw + 1;
             hipLaunchKernelGGL(dev::zaed_kernel, dim3(1), dim3(64), 0, st, H, (int64_t)n, kw, nw, kw > l ? 1 : 0,
                                aed_full ? 0 : 1, dw, dV, dinfo);
-            int info[5];
-            if (hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipMemcpyAsync(aw.data(), dw + kw, nw * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess) {
+            int* info = hp->info;
+            if (hipMemcpyAsync(info, dinfo, 5 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(aw, dw + kw, nw * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                stream_wait(st) != hipSuccess) {
                 rc = fail(EIGSOL_E_HIP, "complex QR: aed");
                 break;
             }
@@ -896,11 +914,11 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         const int nbg = std::max(1, std::min(8, nb / C));
         nb = nbg * C;
         const int ns = 2 * nb;
-        std::vector<cplx> sh(ns);
+        cplx* const sh = hp->sh;   // ns values; the chase reads them from dsh
         bool exceptional = stall % 6 == 0;
         if (!exceptional && m_aed >= 2) {   // the bottom undeflated eigenvalues of the AED window
             for (int i = 0; i < ns; ++i) sh[i] = aw[m_aed - ns + i];
-            if (hipMemcpyAsync(dsh, sh.data(), ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
+            if (hipMemcpyAsync(dsh, sh, ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
                 rc = fail(EIGSOL_E_HIP, "complex QR: shift upload");
                 break;
             }
@@ -916,7 +934,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
                 sh[2 * b] = cplx{d.re + 0.75 * sc, d.im};
                 sh[2 * b + 1] = cplx{d.re - 0.75 * sc, d.im};
             }
-            if (hipMemcpyAsync(dsh, sh.data(), ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
+            if (hipMemcpyAsync(dsh, sh, ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
                 rc = fail(EIGSOL_E_HIP, "complex QR: shift upload");
                 break;
             }
@@ -990,6 +1008,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(EIGSOL_E_HIP, "complex QR: launch"); break; }
         if ((rc = scan()) != EIGSOL_OK) break;
+        scanned = true;
         for (int k = ihi; k > l; --k)
             if (cabs1_h(ds[n + k]) <= eps * (cabs1_h(ds[k - 1]) + cabs1_h(ds[k]))) {
                 sweeps = std::max(sweeps, stall);
@@ -999,7 +1018,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
     }
     if (rc == EIGSOL_OK) {
         if (hipMemcpyAsync(w_host, dw, n * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
+            stream_wait(st) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "complex QR: download");
     }
     if (stats)
@@ -1007,6 +1026,8 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
                      st_sweeps, st_small, st_aed, st_aed_defl);
     for (void* p : {(void*)dw, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo, (void*)dV})
         if (p) (void)hipFree(p);
+    if (ds) (void)hipHostFree(ds);
+    if (hp) (void)hipHostFree(hp);
     *sweeps_out = std::max(1, sweeps);
     *fail_out = failed;
     return rc;

@@ -8,7 +8,10 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 ctx = E.Context(0)
 rng = np.random.default_rng(n)
 A = rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))
-E.qr_eigenvalues(ctx, A[:128, :128].copy())
+# column-major before the clock starts, like tools/bench_qr.py (Matrix::Dense is column-major; a
+# C-ordered 4096^2 complex input costs ~1.1 s of numpy transposition inside the timed call)
+A = np.asfortranarray(A)
+E.qr_eigenvalues(ctx, np.asfortranarray(A[:512, :512]))   # warm-up: every kernel of the path loaded
 t = time.perf_counter()
 r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12))
 dt = time.perf_counter() - t
