@@ -184,7 +184,10 @@ int eigsol_power_kernel_name(eigsol_power* s, char* buf, size_t capacity);
  *          15 = double-double CSR product (EIGSOL_DD / EIGSOL_CDD power method, one row per lane);
  *          16 = double-double dense GEMV (row tiles x column chunks);
  *          17 = double-double shifted inverse: fp64 factor + residual refinement in double-double
- *               (tiles = refinement steps of the last solve, bytes = all of its passes) */
+ *               (tiles = refinement steps of the last solve, bytes = all of its passes);
+ *          18 = shifted inverse, general sparse: GMRES preconditioned by the exact sparse LU of
+ *               A - sigma I (symbolic fill without pivoting, used when the filled pattern holds at most
+ *               EIGSOL_LU_FILL_CAP x nnz entries; tiles and bytes as for 7) */
 
 /* ---------------------------------------------------------------- shifted inverse iteration
  * shiftedInversePowerMethod<S>(M, ShiftedSolverOptions<S>{sigma, maxIter, tol})

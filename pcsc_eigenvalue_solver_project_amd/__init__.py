@@ -369,7 +369,9 @@ class PowerSession:
                  15: "wide spmv_kernel (double-double CSR product, one row per lane)",
                  16: "wide gemv kernels (double-double dense product)",
                  17: "wide shifted inverse (fp64 factor + double-double residual refinement; "
-                     "tiles = refinement steps of the last solve)"}
+                     "tiles = refinement steps of the last solve)",
+                 18: "GMRES over the exact sparse LU (complete fill, no pivoting; tiles = Arnoldi "
+                     "steps of the last solve)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?"),
                 "iterations_per_launch": v.value - 10 if 12 <= v.value <= 14 else 1}

@@ -7,8 +7,13 @@
 // here the solve is iterative to a stated residual, with memory O(nnz + n m):
 //   * M = A - sigma I is built once (diagonal inserted where missing) and uploaded as a CSR; its
 //     SpMV is the library's sliced kernel;
-//   * ILU(0) of M on the device: rows in dependency levels of the strict lower pattern (a level's
-//     rows only read earlier levels), one thread per row in IKJ order, one launch per level;
+//   * the preconditioner K is an incomplete or a complete LU of M on the device: rows in dependency
+//     levels of the strict lower pattern (a level's rows only read earlier levels), one thread per
+//     row in IKJ order, one launch per level.  The pattern it factors on is M's closed under fill
+//     (the symbolic LU without pivoting, so the factors are M's exact LU and GMRES converges in one
+//     step) when that pattern holds at most EIGSOL_LU_FILL_CAP (default 3) x nnz(M) entries;
+//     otherwise M's own pattern (ILU(0)).  Over the exact LU a solve is x = U^-1 L^-1 b and its
+//     true residual; GMRES cycles run only if that misses the tolerance (refinement);
 //   * the factors L (unit lower) and U are solved with the sync-free level-ordered triangular
 //     solve of the config-5 path (shifted.hip), i.e. K^-1 v = U^-1 (L^-1 v);
 //   * GMRES(m) with right preconditioning, x0 = 0, classical Gram-Schmidt with one
@@ -186,6 +191,8 @@ struct GmresSolver {
     int G = 1;
     int64_t nnzM = 0;
     int last_steps = 0;
+    int complete = 0;           // 1: K is M's exact LU (complete fill), 0: ILU(0)
+    int64_t nnzK = 0;           // entries of the factored pattern
     double last_bytes = 0.0;
     double last_relres = 0.0;
 };
@@ -208,6 +215,57 @@ template <class S>
 static S h_sub(S a, S b) {
     if constexpr (std::is_same_v<S, double>) return a - b;
     else return S{a.re - b.re, a.im - b.im};
+}
+
+// Symbolic LU of the pattern (rp, ci) without pivoting, up-looking: row i's pattern is its own
+// columns plus, for every k < i in it (ascending, fill included), row k's columns past k.  Rows are
+// sorted, the diagonal present.  Returns false (and stops early) once the pattern would exceed cap
+// entries.
+static bool lu_fill_pattern(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int64_t cap,
+                            std::vector<int32_t>& frp, std::vector<int32_t>& fci, std::vector<int32_t>& fdpos) {
+    frp.assign(n + 1, 0);
+    fci.clear();
+    fdpos.assign(n, 0);
+    std::vector<int32_t> mark(n, -1), lcols, ucols, heap;
+    auto cmp = [](int32_t a, int32_t b) { return a > b; };   // min-heap
+    for (int64_t i = 0; i < n; ++i) {
+        lcols.clear();
+        ucols.clear();
+        heap.clear();
+        for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+            const int32_t c = ci[e];
+            mark[c] = (int32_t)i;
+            if (c < i) heap.push_back(c);
+            else ucols.push_back(c);
+        }
+        std::make_heap(heap.begin(), heap.end(), cmp);
+        while (!heap.empty()) {
+            std::pop_heap(heap.begin(), heap.end(), cmp);
+            const int32_t k = heap.back();
+            heap.pop_back();
+            lcols.push_back(k);
+            for (int32_t e = fdpos[k] + 1; e < frp[k + 1]; ++e) {
+                const int32_t j = fci[e];
+                if (mark[j] == (int32_t)i) continue;
+                mark[j] = (int32_t)i;
+                if (j < i) {
+                    heap.push_back(j);
+                    std::push_heap(heap.begin(), heap.end(), cmp);
+                } else {
+                    ucols.push_back(j);
+                }
+            }
+            if ((int64_t)fci.size() + (int64_t)lcols.size() + (int64_t)ucols.size() + (int64_t)heap.size() > cap)
+                return false;
+        }
+        std::sort(ucols.begin(), ucols.end());
+        fdpos[i] = (int32_t)(fci.size() + lcols.size());
+        fci.insert(fci.end(), lcols.begin(), lcols.end());
+        fci.insert(fci.end(), ucols.begin(), ucols.end());
+        if ((int64_t)fci.size() > cap) return false;
+        frp[i + 1] = (int32_t)fci.size();
+    }
+    return true;
 }
 
 template <class S>
@@ -255,6 +313,32 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     }
     g->nnzM = (int64_t)mci.size();
     int rc = csr_upload(ctx, dtype, n, n, g->nnzM, mrp.data(), mci.data(), mv.data(), &g->M, 0);
+    // complete fill where affordable: M's values on the closed pattern, zeros at the fill
+    // positions; the factorization below then produces the exact LU (round 4: the 1M config-5
+    // matrix made general fills 16.5M -> ~24M entries and GMRES needs one step per solve instead of
+    // 7-10 over ILU(0))
+    {
+        double ratio = 3.0;
+        if (const char* e = std::getenv("EIGSOL_LU_FILL_CAP")) ratio = std::atof(e);
+        std::vector<int32_t> frp, fci, fdpos;
+        if (ratio >= 1.0 && lu_fill_pattern(n, mrp, mci, std::min<int64_t>(INT32_MAX - 1, (int64_t)(ratio * (double)g->nnzM)),
+                                            frp, fci, fdpos)) {
+            std::vector<S> fv(fci.size(), s_zero<S>());
+            for (int64_t i = 0; i < n; ++i) {   // both rows sorted: merge M's entries into the pattern
+                int32_t p = frp[i];
+                for (int32_t e = mrp[i]; e < mrp[i + 1]; ++e) {
+                    while (fci[p] < mci[e]) ++p;
+                    fv[p] = mv[e];
+                }
+            }
+            mrp.swap(frp);
+            mci.swap(fci);
+            mv.swap(fv);
+            dpos.swap(fdpos);
+            g->complete = 1;
+        }
+    }
+    g->nnzK = (int64_t)mci.size();
     // ILU(0) levels: level(i) = 1 + max level of the rows its strict lower part reads
     std::vector<int32_t> lev(n, 0), lcount;
     for (int64_t i = 0; i < n; ++i) {
@@ -273,17 +357,17 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     int32_t *d_rp = nullptr, *d_ci = nullptr, *d_dpos = nullptr, *d_rows = nullptr, *d_z = nullptr;
     S* d_v = nullptr;
     if (rc == EIGSOL_OK &&
-        (hipMalloc(&d_rp, (n + 1) * 4) != hipSuccess || hipMalloc(&d_ci, std::max<int64_t>(1, g->nnzM) * 4) != hipSuccess ||
-         hipMalloc(&d_v, std::max<int64_t>(1, g->nnzM) * sizeof(S)) != hipSuccess ||
+        (hipMalloc(&d_rp, (n + 1) * 4) != hipSuccess || hipMalloc(&d_ci, std::max<int64_t>(1, g->nnzK) * 4) != hipSuccess ||
+         hipMalloc(&d_v, std::max<int64_t>(1, g->nnzK) * sizeof(S)) != hipSuccess ||
          hipMalloc(&d_dpos, n * 4) != hipSuccess || hipMalloc(&d_rows, n * 4) != hipSuccess ||
          hipMalloc(&d_z, 4) != hipSuccess))
         rc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) buffers");
     int32_t zpiv = 0;
-    std::vector<S> lu(g->nnzM);
+    std::vector<S> lu(g->nnzK);
     if (rc == EIGSOL_OK) {
         hipMemcpyAsync(d_rp, mrp.data(), (n + 1) * 4, hipMemcpyHostToDevice, st);
-        hipMemcpyAsync(d_ci, mci.data(), g->nnzM * 4, hipMemcpyHostToDevice, st);
-        hipMemcpyAsync(d_v, mv.data(), g->nnzM * sizeof(S), hipMemcpyHostToDevice, st);
+        hipMemcpyAsync(d_ci, mci.data(), g->nnzK * 4, hipMemcpyHostToDevice, st);
+        hipMemcpyAsync(d_v, mv.data(), g->nnzK * sizeof(S), hipMemcpyHostToDevice, st);
         hipMemcpyAsync(d_dpos, dpos.data(), n * 4, hipMemcpyHostToDevice, st);
         hipMemcpyAsync(d_rows, rows.data(), n * 4, hipMemcpyHostToDevice, st);
         hipMemsetAsync(d_z, 0, 4, st);
@@ -293,12 +377,14 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
                                d_dpos, d_v, d_rows + lstart[l], cnt, d_z);
         }
         hipMemcpyAsync(&zpiv, d_z, 4, hipMemcpyDeviceToHost, st);
-        hipMemcpyAsync(lu.data(), d_v, g->nnzM * sizeof(S), hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(lu.data(), d_v, g->nnzK * sizeof(S), hipMemcpyDeviceToHost, st);
         if (stream_wait(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) factorization");
     }
     for (void* p : {(void*)d_rp, (void*)d_ci, (void*)d_v, (void*)d_dpos, (void*)d_rows, (void*)d_z})
         if (p) hipFree(p);
-    if (rc == EIGSOL_OK && zpiv) rc = fail(EIGSOL_E_SOLVER, "solve_shifted: ILU(0) factorization met a zero pivot");
+    if (rc == EIGSOL_OK && zpiv)
+        rc = fail(EIGSOL_E_SOLVER, g->complete ? "solve_shifted: sparse LU (complete fill, no pivoting) met a zero pivot"
+                                               : "solve_shifted: ILU(0) factorization met a zero pivot");
     if (rc == EIGSOL_OK) {
         // split: L = strict lower + unit diagonal (columns ascending: the lower part, then i), U =
         // diagonal + strict upper
@@ -428,9 +514,18 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
             beta = bnorm;
         }
     }
+    // exact LU (complete fill): x = U^-1 L^-1 r0 directly; GMRES cycles below only if its true
+    // residual misses rtol_true (iterative refinement on the same factors)
+    if (g->complete && !guess && bnorm > 0.0) {
+        EIGSOL_TRY(precond(w, x));
+        EIGSOL_TRY(eigsol_csr_spmv(g->M, x, t1));
+        hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, t1, w, n);
+        EIGSOL_TRY(norm_of(w, beta));
+        bytes += lb + ub + mb + 3.0 * sb * (double)n;
+    }
     double relres = beta / (bnorm > 0.0 ? bnorm : 1.0);
     int cycles = 0;
-    if (bnorm > 0.0 && beta > 0.0) {
+    if (bnorm > 0.0 && beta > 0.0 && relres > g->rtol_true) {
         std::vector<double> hist;
         std::vector<hc> H((size_t)(m + 1) * m), cs(m), sn(m), gv(m + 1), h;
         for (int cycle = 0; cycle < g->max_cycles; ++cycle) {
@@ -524,6 +619,8 @@ int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev, con
         return gmres_solve_t<cplx>(g, static_cast<const cplx*>(b_dev), bdiv, static_cast<cplx*>(y_dev), guess);
     return gmres_solve_t<double>(g, static_cast<const double*>(b_dev), bdiv, static_cast<double*>(y_dev), guess);
 }
+
+int gmres_complete(const GmresSolver* g) { return g->complete; }
 
 void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps) {
     if (bytes) *bytes = g->last_bytes;

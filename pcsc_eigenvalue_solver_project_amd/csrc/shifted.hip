@@ -37,6 +37,7 @@ int gmres_create(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const
 void gmres_free(GmresSolver* g);
 int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev, const double* guess = nullptr);
 void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps);
+int gmres_complete(const GmresSolver* g);
 
 namespace dev {
 constexpr int kMaxMulti = 4;      // solves per multi-solve launch (one head wave each)
@@ -83,6 +84,7 @@ struct ShiftFactor {
     int32_t nslices = 0;
     int slice_b = 16;             // entries per lane held in registers (4, 8 or 16)
     int tail_chunks = 0;          // tail variant: 1 chunk kernel, 0 slice kernel
+    int chunk_two = 0;            // chunk kernel with two entries per lane (tail rows longer than 16)
     int32_t* porder = nullptr;    // chunk variant (see sptrsv_chunk_kernel)
     int32_t* pptr = nullptr;
     int32_t* pcol = nullptr;
@@ -736,11 +738,13 @@ __global__ __launch_bounds__(kThreads) void sptrsv_slice_kernel(TriArgs<S> a, in
 // wide levels (one 1M-row level: 74 us against 195 us).
 template <class S>
 struct RowMeta {
-    int i, e0, len, j;
-    S v, bi, pv;
+    int i, e0, len, j, j2;
+    S v, v2, bi, pv;
 };
 
-template <class S, bool kIter>
+// kTwo: rows of up to 2 x 16 entries (e.g. an LU factor with fill) keep a second entry per lane,
+// whose dependency is polled together with the first instead of one round trip later
+template <class S, bool kIter, bool kTwo = false>
 __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, int parity) {
     __shared__ Prologue pro;
     const S* xin;
@@ -781,12 +785,20 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
         const int e = ok ? m.e0 + lane : 0;
         m.j = ok ? (int)ldg_stream(a.pcol, (uint32_t)e) : -1;
         m.v = ldg_stream(a.pval, (uint32_t)e);
+        if constexpr (kTwo) {
+            const bool ok2 = lane + kRowLanes < m.len;
+            const int e2 = ok2 ? m.e0 + lane + kRowLanes : 0;
+            m.j2 = ok2 ? (int)ldg_stream(a.pcol, (uint32_t)e2) : -1;
+            m.v2 = ldg_stream(a.pval, (uint32_t)e2);
+        }
         m.bi = xin[m.i >= 0 ? m.i : 0];
     };
-    auto solve = [&](const RowMeta<S>& m, S z0) {
+    auto solve = [&](const RowMeta<S>& m, S z0, S z0b) {
         S acc = s_zero<S>();
         if (m.j >= 0) acc = mul(m.v, finish_wait(z0, a.zcur, m.j, a.err, a.poll_fast));
-        for (int k = lane + kRowLanes; k < m.len; k += kRowLanes) {   // rows longer than 16
+        if constexpr (kTwo)
+            if (m.j2 >= 0) acc = add(acc, mul(m.v2, finish_wait(z0b, a.zcur, m.j2, a.err, a.poll_fast)));
+        for (int k = lane + (kTwo ? 2 : 1) * kRowLanes; k < m.len; k += kRowLanes) {   // rows longer than 16 / 32
             const int e = m.e0 + k;
             acc = add(acc, mul(a.pval[e], wait_value(a.zcur, a.pcol[e], a.err)));
         }
@@ -812,19 +824,31 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_kernel(TriArgs<S> a, in
     fetch1(gw + 3 * W, n1);
     // EIGSOL_TRSV_POLL_MODE bit 1: the second chunk's first polls after the first chunk is solved
     const int late = a.poll_mode & 2;
-    S z0 = c0.j >= 0 ? ld_cohi(a.zcur, c0.j) : s_zero<S>();
-    S z1 = c1.j >= 0 ? ld_cohi(a.zcur, c1.j) : s_zero<S>();
+    auto first_poll = [&](int j) { return j >= 0 ? ld_cohi(a.zcur, j) : s_zero<S>(); };
+    S z0 = first_poll(c0.j), z1 = first_poll(c1.j);
+    S z0b = s_zero<S>(), z1b = s_zero<S>();
+    if constexpr (kTwo) {
+        z0b = first_poll(c0.j2);
+        z1b = first_poll(c1.j2);
+    }
     for (int c = gw; c < a.nchunks; c += 2 * W) {
         fetch2(n0);
         fetch2(n1);
         RowMeta<S> m0, m1;
         fetch1(c + 4 * W, m0);
         fetch1(c + 5 * W, m1);
-        solve(c0, z0);
-        if (late) z1 = c1.j >= 0 ? ld_cohi(a.zcur, c1.j) : s_zero<S>();
-        solve(c1, z1);
-        z0 = n0.j >= 0 ? ld_cohi(a.zcur, n0.j) : s_zero<S>();
-        if (!late) z1 = n1.j >= 0 ? ld_cohi(a.zcur, n1.j) : s_zero<S>();
+        solve(c0, z0, z0b);
+        if (late) {
+            z1 = first_poll(c1.j);
+            if constexpr (kTwo) z1b = first_poll(c1.j2);
+        }
+        solve(c1, z1, z1b);
+        z0 = first_poll(n0.j);
+        if constexpr (kTwo) z0b = first_poll(n0.j2);
+        if (!late) {
+            z1 = first_poll(n1.j);
+            if constexpr (kTwo) z1b = first_poll(n1.j2);
+        }
         c0 = n0;
         c1 = n1;
         n0 = m0;
@@ -2079,9 +2103,11 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
         ppiv.assign((size_t)f->npos, make_sigma<S>(1.0, 0.0));
         pcol.reserve(oci.size());
         pval.reserve(oci.size());
+        int32_t longest = 0;
         for (int32_t p = 0; p < f->npos; ++p) {
             const int32_t i = order[p];
             if (i >= 0) {
+                if (p >= f->hpos) longest = std::max(longest, orp[i + 1] - orp[i]);
                 for (int32_t e = orp[i]; e < orp[i + 1]; ++e) {
                     pcol.push_back(oci[e]);
                     pval.push_back(ov[e]);
@@ -2090,6 +2116,10 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
             }
             pptr[p + 1] = (int32_t)pcol.size();
         }
+        // rows past 16 entries: the second entry of every lane is polled with the first
+        // (EIGSOL_TRSV_TWO=0|1 overrides; round 4, the exact LU's U of config 5 made general)
+        f->chunk_two = longest > dev::kRowLanes ? 1 : 0;
+        if (const char* e = std::getenv("EIGSOL_TRSV_TWO")) f->chunk_two = std::atoi(e) != 0;
     }
     // tail slices (see sptrsv_slice_kernel): 64 rows of one level each; B = the smallest of
     // 4 / 8 / 16 that holds the entries of at least 95 % of the slices (longer slices loop)
@@ -2159,7 +2189,8 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
     // blocks per CU and by the work
     if (rc == EIGSOL_OK) {
         int per_cu_max = 0;
-        const void* tk = f->tail_chunks ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>)
+        const void* tk = f->tail_chunks ? (f->chunk_two ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true, true>)
+                                                        : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>))
                                         : slice_kernel_ptr<S>(Bs, true);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_max, tk, dev::kThreads, 0) != hipSuccess ||
             per_cu_max < 1)
@@ -2480,6 +2511,8 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.nchunks = f->nchunks;
         const void* tk = pair ? reinterpret_cast<const void*>(dev::sptrsv_chunk_role_kernel<S>)
                          : !f->tail_chunks ? slice_kernel_ptr<S>(f->slice_b, iter)
+                         : f->chunk_two ? (iter ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true, true>)
+                                                : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, false, true>))
                          : iter ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>)
                                 : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, false>);
         const int tgrid = pair ? f->grid_multi : f->grid;
@@ -2580,7 +2613,7 @@ void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* 
     const double sb = (double)scalar_bytes(f->dtype), n = (double)f->n;
     if (f->kind == 2) {
         gmres_info(f->gm, bytes, tiles);
-        if (variant) *variant = 7;
+        if (variant) *variant = gmres_complete(f->gm) ? 18 : 7;
     } else if (f->kind == 3) {
         band_info(f->band, bytes, tiles);
         if (variant) *variant = 8;

@@ -9,7 +9,10 @@
 * the 1M-row config-5-class matrix made non-triangular (synthetic.general_complex: eigenvalues are
   the diagonal, so the planted eigenvalue is the exact answer): λ within 1e-9 of it, and
   ||A x - λ x|| / ||x|| <= 1e-8 on the host;
-* solve_shifted on the same matrix: ||(A - σI) y - b|| <= 1e-10 ||b||.
+* solve_shifted on the same matrix: ||(A - σI) y - b|| <= 1e-10 ||b||;
+* the preconditioner: the exact sparse LU (complete fill, variant 18) where the filled pattern fits
+  EIGSOL_LU_FILL_CAP x nnz — a direct solve checked by its true residual — and ILU(0) (variant 7) otherwise, both
+  to the same parity.
 EIGSOL_SPARSE_SOLVER=gmres forces the GMRES path below the densify threshold (n > 16384 uses it
 by default)."""
 import os
@@ -63,6 +66,45 @@ def test_gmres_shifted_parity_with_reference_loop(ctx, gmres_env):
     A.close()
 
 
+@pytest.mark.parametrize("cap", ["3", "0"])
+def test_gmres_complete_and_incomplete_lu_parity(ctx, gmres_env, cap):
+    """The same reference loop over the exact LU (cap 3: general_complex fills ~1.4x) and ILU(0)
+    (cap 0): λ, iteration count and x against the oracle's direct-LU loop; over the exact factor a
+    solve is direct (its true residual meets 1e-12 without an Arnoldi step)."""
+    os.environ["EIGSOL_LU_FILL_CAP"] = cap
+    try:
+        n = 600   # the oracle's dense LU loop is O(n^3) per iteration on one core
+        rp, ci, v, d = S.general_complex(n, 12)
+        sigma = TARGET + 1e-3
+        A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+        x0 = S.start_vector(n, np.complex128)
+        s = E.ShiftedSession(A, sigma)
+        s.begin(E.ShiftedSolverOptions(200, 1e-12, sigma), x0)
+        done = False
+        while not done:
+            s.step(1)
+            done, _ = s.query()
+        info = s.kernel_info()
+        r = s.finish()
+        s.close()
+        assert info["variant"] == (18 if cap == "3" else 7), info
+        if cap == "3":
+            assert info["tiles"] == 0, info      # Arnoldi steps of the last solve: the direct solve met 1e-12
+        D = sp.csr_matrix((v, ci, rp), shape=(n, n)).toarray()
+        ref = O.shifted_dense(D, sigma, x0, 200, 1e-12)
+        lam = ref["eigenvalue"]
+        assert r.converged and ref["converged"]
+        assert abs(r.eigenvalue - lam) <= 1e-10 * (1 + abs(lam)), (r.eigenvalue, lam)
+        assert abs(r.iterations - ref["iterations"]) <= 1
+        assert abs(abs(np.vdot(r.eigenvector, ref["eigenvector"])) - 1) <= 1e-10
+        b = S.start_vector(n, np.complex128, seed=3)
+        y = E.solve_shifted(A, sigma, b)
+        assert np.linalg.norm(D @ y - sigma * y - b) <= 1e-11 * np.linalg.norm(b)
+        A.close()
+    finally:
+        os.environ.pop("EIGSOL_LU_FILL_CAP", None)
+
+
 def test_gmres_real_matrix_solve(ctx, gmres_env):
     """f64: a nonsymmetric diagonally dominant sparse matrix; solve_shifted vs a dense solve."""
     n = 3000
@@ -83,8 +125,16 @@ def test_gmres_general_sparse_1m(ctx):
     rp, ci, v, _ = S.general_complex(n, 16)
     sigma = TARGET + 1e-3
     A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
-    r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(100, 1e-12, sigma),
-                                       S.start_vector(n, np.complex128))
+    s = E.ShiftedSession(A, sigma)
+    s.begin(E.ShiftedSolverOptions(100, 1e-12, sigma), S.start_vector(n, np.complex128))
+    done = False
+    while not done:
+        s.step(1)
+        done, _ = s.query()
+    info = s.kernel_info()
+    r = s.finish()
+    s.close()
+    assert info["variant"] == 18 and info["tiles"] == 0, info   # exact LU: a direct solve, no Arnoldi step
     assert r.converged and abs(r.eigenvalue - TARGET) <= 1e-9, r.eigenvalue
     M = sp.csr_matrix((v, ci, rp), shape=(n, n))
     x = r.eigenvector

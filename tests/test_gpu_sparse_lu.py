@@ -173,6 +173,7 @@ def test_gmres_stagnation_reports_solve_failure(ctx, convdiff, env):
     fx, rp, ci, v, _ = convdiff
     env("EIGSOL_SPARSE_SOLVER", "gmres")
     env("EIGSOL_GMRES_FALLBACK", "0")
+    env("EIGSOL_LU_FILL_CAP", "0")       # ILU(0): the incomplete factor is what stagnates
     n = fx["n"]
     A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
     with pytest.raises(E.EigSolError) as ei:
@@ -184,6 +185,7 @@ def test_gmres_stagnation_reports_solve_failure(ctx, convdiff, env):
 def test_gmres_stagnation_falls_back_to_dense_lu(ctx, convdiff, env):
     fx, rp, ci, v, xref = convdiff
     env("EIGSOL_SPARSE_SOLVER", "gmres")
+    env("EIGSOL_LU_FILL_CAP", "0")
     n = fx["n"]
     A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
     sigma = complex(*fx["sigma"])
