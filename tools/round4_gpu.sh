@@ -22,7 +22,7 @@ else
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/uni_fetch -o run -- python3 $R/tools/prof_driver.py --workload uniform10m --steps 20 > $OUT/uni_fetch.log 2>&1 || { echo "uniform fetch failed"; exit 1; }
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/uni_write -o run -- python3 $R/tools/prof_driver.py --workload uniform10m --steps 20 > $OUT/uni_write.log 2>&1 || { echo "uniform write failed"; exit 1; }
   cd $R
-  timeout -k 10 120 python -u tools/bench_qr.py 4096 > $OUT/qr_time.log 2>&1 || { echo "qr timing failed"; exit 1; }
-  timeout -k 10 120 python -u tools/bench_qrc.py 4096 > $OUT/qrc_time.log 2>&1 || { echo "qrc timing failed"; exit 1; }
+  EIGSOL_QR_STATS=1 timeout -k 10 120 python -u tools/bench_qr.py 4096 > $OUT/qr_time.log 2>&1 || { echo "qr timing failed"; exit 1; }
+  EIGSOL_QR_STATS=1 timeout -k 10 120 python -u tools/bench_qrc.py 4096 > $OUT/qrc_time.log 2>&1 || { echo "qrc timing failed"; exit 1; }
   echo "part b ok"
 fi
