@@ -171,8 +171,8 @@ def cpu_allcores(kind, k, budget_s, n, mat=None):
 
 def measured_hbm(torch, stream, ctx=None):
     """STREAM-like figures on this GPU (report beside the 8 TB/s spec): the library's
-    hand-written gfx950 streaming kernels (eigsol_hbm_probe: dwordx4 non-temporal, 2 GiB, best of
-    1/2/4/8 workgroups per CU) and, for comparison, a torch copy_ and a torch read-only reduction."""
+    hand-written gfx950 streaming kernels (eigsol_hbm_probe: non-temporal dwordx4 and dwordx2 reads,
+    dwordx4 copy / write, 2 GiB, best of 1/2/4/8 workgroups per CU) and, for comparison, a torch copy_ and a torch read-only reduction."""
     a = torch.empty(2 << 30, dtype=torch.uint8, device="cuda").view(torch.float64)
     b = torch.empty_like(a)
     a.fill_(1.0)
@@ -195,7 +195,8 @@ def measured_hbm(torch, stream, ctx=None):
         if st == 0:
             out.update({"kernel_read_GBps": round(rd.value, 1), "kernel_copy_GBps": round(cp.value, 1),
                         "kernel_write_GBps": round(wr.value, 1), "kernel_read_blocks_per_cu": bpc.value,
-                        "kernel": "eigsol::pdev::read_kernel / copy_kernel / write_kernel (probe.hip, libeigsol_hip.so)"})
+                        "kernel": "eigsol::pdev::read_kernel, read8_kernel / copy_kernel / write_kernel (probe.hip, "
+                                  "libeigsol_hip.so)"})
     out["note"] = ("practical ceilings of this box; the roofline peak stays the 8 TB/s spec.  The headline's "
                    "actual DRAM rate (PMC traffic / event time) is compared against kernel_read_GBps below")
     return out

@@ -2,10 +2,12 @@
 // box's practical HBM ceiling, SURVEY §8d "verify with a STREAM-like kernel on the box").
 //
 // Hand-written gfx950 streams over one buffer of `bytes` (>= 2 GiB, so neither the 4 MB L2s nor
-// the 256 MB Infinity Cache hold it): 16-byte (dwordx4) non-temporal loads / stores, four in
-// flight per lane, grid-stride over 256-thread workgroups.  Three shapes:
-//   read  - load only (the loads feed an xor reduction that is stored only if it matches a
-//           sentinel, so the compiler keeps every load and nothing is written);
+// the 256 MB Infinity Cache hold it): non-temporal loads / stores, four in flight per lane,
+// grid-stride over 256-thread workgroups.  Three shapes:
+//   read  - load only, 16-byte (dwordx4) and 8-byte (dwordx2) loads, the better of the two (the
+//           loads feed an xor reduction that is stored only if it matches a sentinel, so the
+//           compiler keeps every load and nothing is written; round 4, tools/width_probe.hip:
+//           8-byte loads at 4 workgroups per CU read 7.3 TB/s, 16-byte ones 6.9 TB/s);
 //   copy  - load + store to a second buffer (read + write bytes counted);
 //   write - store only.
 // Each is timed with HIP events on the context's stream over `reps` launches, for grids of 1, 2,
@@ -19,6 +21,7 @@ namespace eigsol {
 namespace pdev {
 
 using u4 = __attribute__((ext_vector_type(4))) unsigned int;
+using u2 = __attribute__((ext_vector_type(2))) unsigned int;
 
 constexpr int kT = 256;
 constexpr int kU = 4;   // 16-byte accesses in flight per lane
@@ -38,6 +41,23 @@ __global__ __launch_bounds__(kT) void read_kernel(const u4* __restrict__ a, size
     }
     const unsigned int r = acc.x ^ acc.y ^ acc.z ^ acc.w;
     if (r == 0x9e3779b9u) out[0] = r;   // never true for the probe's zero-filled buffer
+}
+
+__global__ __launch_bounds__(kT) void read8_kernel(const u2* __restrict__ a, size_t n8, unsigned int* out) {
+    const size_t stride = (size_t)gridDim.x * kT * kU;
+    u2 acc = {0u, 0u};
+    for (size_t base = (size_t)blockIdx.x * kT * kU + threadIdx.x; base < n8; base += stride) {
+        u2 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const size_t i = base + (size_t)u * kT;
+            v[u] = i < n8 ? __builtin_nontemporal_load(a + i) : u2{0u, 0u};
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) acc ^= v[u];
+    }
+    const unsigned int r = acc.x ^ acc.y;
+    if (r == 0x9e3779b9u) out[0] = r;
 }
 
 __global__ __launch_bounds__(kT) void copy_kernel(const u4* __restrict__ a, u4* __restrict__ b, size_t n16) {
@@ -97,11 +117,14 @@ int eigsol_hbm_probe(eigsol_ctx* ctx, size_t bytes, int reps, double* read_gbps,
         auto* bp = static_cast<pdev::u4*>(b);
         for (int bpc : {1, 2, 4, 8}) {
             const unsigned grid = (unsigned)(bpc * ctx->num_cus);
-            for (int kind = 0; kind < 3 && rc == EIGSOL_OK; ++kind) {
+            for (int kind = 0; kind < 4 && rc == EIGSOL_OK; ++kind) {   // read16, copy, write, read8
                 auto launch = [&]() {
                     if (kind == 0)
                         hipLaunchKernelGGL(pdev::read_kernel, dim3(grid), dim3(pdev::kT), 0, st, ap, n16,
                                            static_cast<unsigned int*>(o));
+                    else if (kind == 3)
+                        hipLaunchKernelGGL(pdev::read8_kernel, dim3(grid), dim3(pdev::kT), 0, st,
+                                           reinterpret_cast<const pdev::u2*>(ap), 2 * n16, static_cast<unsigned int*>(o));
                     else if (kind == 1)
                         hipLaunchKernelGGL(pdev::copy_kernel, dim3(grid), dim3(pdev::kT), 0, st, ap, bp, n16);
                     else
@@ -119,9 +142,10 @@ int eigsol_hbm_probe(eigsol_ctx* ctx, size_t bytes, int reps, double* read_gbps,
                 }
                 const double moved = (double)(n16 * 16) * (kind == 1 ? 2.0 : 1.0) * reps;
                 const double gbps = moved / (ms * 1e-3) / 1e9;
-                if (gbps > best[kind]) {
-                    best[kind] = gbps;
-                    if (kind == 0) best_bpc = bpc;
+                const int slot = kind == 3 ? 0 : kind;   // read: the better load width
+                if (gbps > best[slot]) {
+                    best[slot] = gbps;
+                    if (slot == 0) best_bpc = bpc;
                 }
             }
         }
