@@ -28,5 +28,6 @@ if n == 4096:
     d, j = tree.query(np.c_[ev.real, ev.imag], k=1)
     out["max_match_dist"] = float(d.max())
     out["unique_matches"] = int(len(np.unique(j)))
+out["env"] = {k: v for k, v in os.environ.items() if k.startswith("EIGSOL")}
 print(json.dumps(out), flush=True)
 ctx.close()
