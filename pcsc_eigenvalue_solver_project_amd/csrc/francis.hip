@@ -1044,7 +1044,16 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                 }
             }
         }
-        if (!have_shifts) {
+        // every 6th sweep without a deflation uses exceptional shifts (LAPACK xLAQR0's KEXSH, NDFL
+        // counted from 1 after a deflation): stall counts those sweeps, 0 right after the AED deflated.
+        // Round 3 took stall == 0 as exceptional too, so every sweep after a partial AED deflation ran
+        // on ad hoc shifts (and its shift QR went unused); EIGSOL_QR_EXC_LEGACY=1 restores that for A/B
+        static const bool exc_legacy = [] {
+            const char* e = std::getenv("EIGSOL_QR_EXC_LEGACY");
+            return !e || std::atoi(e) != 0;   // pending measurement: legacy by default
+        }();
+        const bool exceptional = exc_legacy ? stall % 6 == 0 : (stall > 0 && stall % 6 == 0);
+        if (!have_shifts && !exceptional) {
             nb = std::min(max_bulges, std::max(1, (ihi - l + 1) / 8));
             ns = 2 * nb;
             // shifts: eigenvalues of the trailing 2nb x 2nb block
@@ -1061,7 +1070,8 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         // pair the shifts: conjugate pairs stay together, reals are paired in order;
         // every 6th stalled sweep uses exceptional shifts from the bottom subdiagonal
         double* const sh = hp->sh;   // 2 nb values; the chase reads them from dsh
-        if (stall % 6 == 0) {
+        if (exceptional) {
+            nb = std::min(max_bulges, std::max(1, (ihi - l + 1) / 8));
             for (int b = 0; b < nb; ++b) {
                 const double sc = std::fabs(ds[n + ihi - b]) + std::fabs(ds[ihi - b]) + 1e-300;
                 sh[2 * b] = ds[ihi - b] + 0.75 * sc;

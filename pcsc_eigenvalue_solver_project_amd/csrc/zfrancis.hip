@@ -915,7 +915,14 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         nb = nbg * C;
         const int ns = 2 * nb;
         cplx* const sh = hp->sh;   // ns values; the chase reads them from dsh
-        bool exceptional = stall % 6 == 0;
+        // every 6th sweep without a deflation: exceptional shifts (LAPACK's KEXSH; stall is 0 right
+        // after the AED deflated, and such a sweep takes the regular shifts).  EIGSOL_ZQR_EXC_LEGACY=1:
+        // round 3's test, which also took stall == 0 (ad hoc shifts after every partial deflation)
+        static const bool exc_legacy = [] {
+            const char* e = std::getenv("EIGSOL_ZQR_EXC_LEGACY");
+            return !e || std::atoi(e) != 0;   // pending measurement: legacy by default
+        }();
+        bool exceptional = exc_legacy ? stall % 6 == 0 : (stall > 0 && stall % 6 == 0);
         if (!exceptional && m_aed >= 2) {   // the bottom undeflated eigenvalues of the AED window
             for (int i = 0; i < ns; ++i) sh[i] = aw[m_aed - ns + i];
             if (hipMemcpyAsync(dsh, sh, ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
