@@ -332,11 +332,23 @@ int eigsol_ctx_info(eigsol_ctx* ctx, int* device, int* rank, int* nranks, int* c
 /* ---------------------------------------------------------------- measurement
  * The device's practical HBM bandwidth ("verify the spec with a STREAM-like kernel
  * on the box"): hand-written gfx950 streams over `bytes` (use >= 2 GiB: beyond the 256 MB
- * Infinity Cache) with 16-byte non-temporal loads / stores, four in flight per lane, timed with HIP
- * events over `reps` launches on the context's stream, best over 1/2/4/8 workgroups per CU.
- * read = load only, copy = load + store (both directions counted), write = store only (GB/s). */
+ * Infinity Cache) with non-temporal loads / stores, four in flight per lane, timed with HIP events
+ * over `reps` launches on the context's stream, best over 1/2/4/8 workgroups per CU.
+ * read = load only (16- and 8-byte loads, the better), copy = load + store (both directions
+ * counted), write = store only (GB/s). */
 int eigsol_hbm_probe(eigsol_ctx* ctx, size_t bytes, int reps, double* read_gbps, double* copy_gbps,
                      double* write_gbps, int* best_blocks_per_cu);
+
+/* ---------------------------------------------------------------- sparse LU analysis (host only)
+ * The symbolic factorization the general-sparse shifted solve runs before choosing the exact LU
+ * over ILU(0) (variant 18 vs 7): the pattern of A with its diagonal inserted, closed under fill
+ * for LU without pivoting (row i = its own columns plus, for every k < i in it in ascending order,
+ * fill included, row k's columns past k).  Stops once the pattern would pass `cap` entries.
+ * *nnz_out = the filled pattern's entries, or -1 when it exceeds cap; *lower_levels_out (optional)
+ * = dependency levels of its strict lower part (the numeric factorization's launches).  Rows must
+ * be sorted; needs no device. */
+int eigsol_sparse_lu_fill(int64_t n, const int32_t* rowptr, const int32_t* colidx, int64_t cap, int64_t* nnz_out,
+                          int32_t* lower_levels_out);
 
 #ifdef __cplusplus
 }

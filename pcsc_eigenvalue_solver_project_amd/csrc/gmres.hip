@@ -628,3 +628,50 @@ void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps) {
 }
 
 }  // namespace eigsol
+
+extern "C" int eigsol_sparse_lu_fill(int64_t n, const int32_t* rowptr, const int32_t* colidx, int64_t cap,
+                                     int64_t* nnz_out, int32_t* lower_levels_out) {
+    using namespace eigsol;
+    if (n < 0 || (n > 0 && (!rowptr || !colidx)) || !nnz_out || n > INT32_MAX - 1)
+        return fail(EIGSOL_E_INVALID, "eigsol_sparse_lu_fill: bad arguments");
+    // A's pattern with the diagonal inserted (the shifted matrix A - sigma I always stores it)
+    std::vector<int32_t> mrp(n + 1, 0), mci;
+    mci.reserve((size_t)rowptr[n] + n);
+    for (int64_t i = 0; i < n; ++i) {
+        bool have = false;
+        for (int32_t e = rowptr[i]; e <= rowptr[i + 1]; ++e) {
+            const bool end = e == rowptr[i + 1];
+            if (!have && (end || colidx[e] >= i)) {
+                mci.push_back((int32_t)i);
+                have = true;
+                if (!end && colidx[e] == i) continue;
+            }
+            if (end) break;
+            if (colidx[e] < 0 || colidx[e] >= n)
+                return fail(EIGSOL_E_INVALID, "eigsol_sparse_lu_fill: column index out of range");
+            if (e > rowptr[i] && colidx[e] <= colidx[e - 1])
+                return fail(EIGSOL_E_INVALID, "eigsol_sparse_lu_fill: rows must be sorted without repeats");
+            mci.push_back(colidx[e]);
+        }
+        mrp[i + 1] = (int32_t)mci.size();
+    }
+    std::vector<int32_t> frp, fci, fdpos;
+    if (!lu_fill_pattern(n, mrp, mci, std::min<int64_t>(cap, INT32_MAX - 1), frp, fci, fdpos)) {
+        *nnz_out = -1;
+        if (lower_levels_out) *lower_levels_out = 0;
+        return EIGSOL_OK;
+    }
+    *nnz_out = (int64_t)fci.size();
+    if (lower_levels_out) {
+        std::vector<int32_t> lev(n, 0);
+        int32_t top = n ? 1 : 0;
+        for (int64_t i = 0; i < n; ++i) {
+            int32_t l = 0;
+            for (int32_t e = frp[i]; e < fdpos[i]; ++e) l = std::max(l, lev[fci[e]] + 1);
+            lev[i] = l;
+            top = std::max(top, l + 1);
+        }
+        *lower_levels_out = top;
+    }
+    return EIGSOL_OK;
+}

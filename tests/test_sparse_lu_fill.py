@@ -1,0 +1,126 @@
+"""Host-only symbolic analysis behind the general-sparse shifted solve (gmres.hip, C ABI
+eigsol_sparse_lu_fill): the pattern of A (diagonal inserted) closed under fill for LU without
+pivoting, which decides between the exact sparse LU (variant 18) and ILU(0) (variant 7).
+
+Checked on the CPU, no device: the library's count against a Python restatement of the up-looking
+symbolic factorization, the closure property against a dense no-pivot LU of random values on the
+same pattern (every structurally possible nonzero of L and U lies in the pattern), the cap, the
+lower-part dependency levels, and argument errors."""
+import ctypes as C
+import heapq
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from pcsc_eigenvalue_solver_project_amd import synthetic as S
+from pcsc_eigenvalue_solver_project_amd._capi import lib
+
+
+def _pattern(rp, ci, n):
+    """Python restatement: rows of the filled pattern (sorted), diagonal included."""
+    rows, mark = [], np.full(n, -1)
+    for i in range(n):
+        cols = set(int(c) for c in ci[rp[i]:rp[i + 1]])
+        cols.add(i)
+        for c in cols:
+            mark[c] = i
+        heap = [c for c in cols if c < i]
+        heapq.heapify(heap)
+        upper = [c for c in cols if c >= i]
+        lower = []
+        while heap:
+            k = heapq.heappop(heap)
+            lower.append(k)
+            for j in rows[k]:
+                if j <= k or mark[j] == i:
+                    continue
+                mark[j] = i
+                if j < i:
+                    heapq.heappush(heap, j)
+                else:
+                    upper.append(j)
+        rows.append(sorted(lower) + sorted(upper))
+    return rows
+
+
+def _call(rp, ci, n, cap):
+    rp = np.ascontiguousarray(rp, dtype=np.int32)
+    ci = np.ascontiguousarray(ci, dtype=np.int32)
+    nnz, lev = C.c_int64(0), C.c_int32(0)
+    st = lib().eigsol_sparse_lu_fill(n, rp.ctypes.data, ci.ctypes.data, cap, C.byref(nnz), C.byref(lev))
+    assert st == 0
+    return nnz.value, lev.value
+
+
+def _levels(rows, n):
+    lev = [0] * n
+    for i in range(n):
+        lev[i] = max([lev[k] + 1 for k in rows[i] if k < i], default=0)
+    return max(lev) + 1 if n else 0
+
+
+@pytest.mark.parametrize("case", ["general_complex", "random", "arrow", "lower_bidiagonal"])
+def test_fill_matches_restatement(case):
+    if case == "general_complex":
+        rp, ci, _, _ = S.general_complex(1500, 8)
+        n = 1500
+    elif case == "random":
+        n = 300
+        M = sp.random(n, n, density=0.01, random_state=3, format="csr")
+        M.sort_indices()
+        rp, ci = M.indptr, M.indices
+    elif case == "arrow":   # dense last row and column: fill stays in them
+        n = 200
+        r = np.r_[np.arange(n), np.full(n, n - 1), np.arange(n)]
+        c = np.r_[np.full(n, n - 1), np.arange(n), np.arange(n)]
+        M = sp.csr_matrix((np.ones(3 * n), (r, c)), shape=(n, n))
+        M.sort_indices()
+        rp, ci = M.indptr, M.indices
+    else:                   # no fill at all
+        n = 400
+        M = sp.diags([np.ones(n), np.ones(n - 1)], [0, -1], format="csr")
+        M.sort_indices()
+        rp, ci = M.indptr, M.indices
+    rows = _pattern(rp, ci, n)
+    want = sum(len(r) for r in rows)
+    got, lev = _call(rp, ci, n, 10**9)
+    assert got == want
+    assert lev == _levels(rows, n)
+    if case == "lower_bidiagonal":
+        assert got == 2 * n - 1 and lev == n
+
+
+def test_pattern_is_closed_under_lu_fill():
+    """Dense LU without pivoting of random values on the pattern: no nonzero outside it."""
+    n = 160
+    M = sp.random(n, n, density=0.03, random_state=11, format="csr")
+    M.sort_indices()
+    rows = _pattern(M.indptr, M.indices, n)
+    inside = np.zeros((n, n), dtype=bool)
+    for i, r in enumerate(rows):
+        inside[i, r] = True
+    A = np.zeros((n, n))
+    A[M.nonzero()] = np.random.default_rng(0).uniform(1, 2, M.nnz)
+    A[np.arange(n), np.arange(n)] += 4.0 * n   # strong diagonal: the no-pivot LU exists
+    LU = A.copy()
+    for k in range(n - 1):
+        LU[k + 1:, k] /= LU[k, k]
+        LU[k + 1:, k + 1:] -= np.outer(LU[k + 1:, k], LU[k, k + 1:])
+    assert not (np.abs(LU[~inside]) > 0).any()
+    got, _ = _call(M.indptr, M.indices, n, 10**9)
+    assert got == int(inside.sum())
+
+
+def test_cap_and_errors():
+    rp, ci, _, _ = S.general_complex(1000, 8)
+    full, _ = _call(rp, ci, 1000, 10**9)
+    assert _call(rp, ci, 1000, full)[0] == full
+    assert _call(rp, ci, 1000, full - 1)[0] == -1
+    out = C.c_int64(0)
+    bad = np.array([0, 2, 2], np.int32), np.array([1, 0], np.int32)   # unsorted row
+    assert lib().eigsol_sparse_lu_fill(2, bad[0].ctypes.data, bad[1].ctypes.data, 100, C.byref(out), None) == 9
+    oor = np.array([0, 1], np.int32), np.array([5], np.int32)         # column out of range
+    assert lib().eigsol_sparse_lu_fill(1, oor[0].ctypes.data, oor[1].ctypes.data, 100, C.byref(out), None) == 9
+    assert lib().eigsol_sparse_lu_fill(-1, None, None, 100, C.byref(out), None) == 9
+    assert _call(np.zeros(1, np.int32), np.zeros(0, np.int32), 0, 10) == (0, 0)
