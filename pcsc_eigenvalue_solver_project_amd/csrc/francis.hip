@@ -40,7 +40,8 @@ int hqr_lds(hipStream_t st, const double* H, int64_t ld, int n, int maxits, doub
 namespace dev {
 
 constexpr int kWin = 96;        // window rows/columns (H window + U: 2 x 72 KiB of LDS)
-constexpr int kMaxBulges = 32;   // shifts per sweep / 2 (at most 16 per window: one wave each)
+constexpr int kMaxBulges = 48;   // shifts per sweep / 2 (at most 16 per window: one wave each; the
+                                 // shifts' block of 2 nb <= 96 rows fits the one-wave solver)
 
 // compiler-only ordering of LDS accesses (one wave's LDS operations execute in issue order)
 #define EIGSOL_LDS_ORDER() asm volatile("" ::: "memory")
@@ -917,7 +918,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     }();
     static const int max_bulges = [] {                 // experiments: cap the bulges per chain
         const char* e = std::getenv("EIGSOL_QR_NB");
-        return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : 28;
+        return e ? std::max(1, std::min(dev::kMaxBulges, std::atoi(e))) : 32;
     }();
     long long st_steps = 0, st_aed_steps = 0, st_aed_ph[3] = {0, 0, 0};
     static const int aed_win = [] {
@@ -1050,7 +1051,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         // on ad hoc shifts (and its shift QR went unused); EIGSOL_QR_EXC_LEGACY=1 restores that for A/B
         static const bool exc_legacy = [] {
             const char* e = std::getenv("EIGSOL_QR_EXC_LEGACY");
-            return !e || std::atoi(e) != 0;   // pending measurement: legacy by default
+            return e && std::atoi(e) != 0;
         }();
         const bool exceptional = exc_legacy ? stall % 6 == 0 : (stall > 0 && stall % 6 == 0);
         if (!have_shifts && !exceptional) {

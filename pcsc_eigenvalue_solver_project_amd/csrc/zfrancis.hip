@@ -920,7 +920,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         // round 3's test, which also took stall == 0 (ad hoc shifts after every partial deflation)
         static const bool exc_legacy = [] {
             const char* e = std::getenv("EIGSOL_ZQR_EXC_LEGACY");
-            return !e || std::atoi(e) != 0;   // pending measurement: legacy by default
+            return e && std::atoi(e) != 0;
         }();
         bool exceptional = exc_legacy ? stall % 6 == 0 : (stall > 0 && stall % 6 == 0);
         if (!exceptional && m_aed >= 2) {   // the bottom undeflated eigenvalues of the AED window
