@@ -113,9 +113,11 @@ __device__ __forceinline__ void zhouse(cplx a, cplx x1, cplx x2, bool three, dou
 // the bottom row i its Schur vector column V(:, i) is final (later sweeps touch columns < i only),
 // so the AED spike test is taken right there; the first eigenvalue that fails it ends the
 // factorisation (stop = i; the rows above stay unreduced).  stop = -1: ran to completion.
+// dtol: relative subdiagonal at which the block splits (ulp: ZLAHQR's test; the sweeps' shifts are
+// computed with a looser one, EIGSOL_ZQR_SHIFT_TOL)
 template <bool kSchur>
 __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& maxits, int& steps,
-                          double spk = -1.0, int* stop = nullptr) {
+                          double spk = -1.0, int* stop = nullptr, double dtol = 2.220446049250313e-16) {
     constexpr int lh = kZSmall + 1;
     const int ln = threadIdx.x;
     auto H = [&](int i, int j) -> cplx& { return h[i + j * lh]; };
@@ -141,12 +143,12 @@ __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& ma
                         if (k - 2 >= l) tst += fabs(H(k - 1, k - 2).re);
                         if (k + 1 <= i) tst += fabs(H(k + 1, k).re);
                     }
-                    if (cabs1(hk) <= ulp * tst) {
+                    if (cabs1(hk) <= dtol * tst) {
                         const double ab = fmax(cabs1(hk), cabs1(H(k - 1, k))), ba = fmin(cabs1(hk), cabs1(H(k - 1, k)));
                         const cplx dd = sub(H(k - 1, k - 1), H(k, k));
                         const double aa = fmax(cabs1(H(k, k)), cabs1(dd)), bb = fmin(cabs1(H(k, k)), cabs1(dd));
                         const double s = aa + ab;
-                        neg = ba * (ab / s) <= fmax(smlnum, ulp * (bb * (aa / s)));
+                        neg = ba * (ab / s) <= fmax(smlnum, dtol * (bb * (aa / s)));
                     }
                 }
                 if (neg) { kf = k; break; }
@@ -256,14 +258,15 @@ __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& ma
 }
 
 // Eigenvalues of an n x n Hessenberg block (n <= 64) in LDS.
-__global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t ld, int n, cplx* w, int* info) {
+__global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t ld, int n, cplx* w, int* info,
+                                                       double dtol) {
     __shared__ cplx h[kZSmall * (kZSmall + 1)];
     constexpr int lh = kZSmall + 1;
     const int ln = threadIdx.x;
     for (int idx = ln; idx < n * n; idx += 64) h[(idx % n) + (idx / n) * lh] = Hin[(idx % n) + (int64_t)(idx / n) * ld];
     __syncthreads();
     int failed, maxits, steps;
-    zwave_hqr<false>(h, nullptr, n, w, failed, maxits, steps);
+    zwave_hqr<false>(h, nullptr, n, w, failed, maxits, steps, -1.0, nullptr, dtol);
     if (ln == 0) {
         info[0] = failed;
         info[1] = maxits;
@@ -808,9 +811,15 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
     static const bool stats = std::getenv("EIGSOL_QR_STATS") != nullptr;
     int ihi = (int)n - 1;
     const int max_stall = std::max(1, maxits);
-    auto small = [&](int l, int hi, cplx* wdst, int info[2]) -> int {
+    // the shifts' QR splits at a looser relative subdiagonal than the eigenvalues' (EIGSOL_ZQR_SHIFT_TOL;
+    // the real path's round-4 grid, francis.hip, put its optimum at 1e-4)
+    static const double shift_tol = [] {
+        const char* e = std::getenv("EIGSOL_ZQR_SHIFT_TOL");
+        return e ? std::max(2.220446049250313e-16, std::atof(e)) : 2.220446049250313e-16;
+    }();
+    auto small = [&](int l, int hi, cplx* wdst, int info[2], double dtol = 2.220446049250313e-16) -> int {
         hipLaunchKernelGGL(dev::zhqr_wave_kernel, dim3(1), dim3(64), 0, st, H + l + (int64_t)l * n, (int64_t)n,
-                           hi - l + 1, wdst, dinfo);
+                           hi - l + 1, wdst, dinfo, dtol);
         EIGSOL_HIP(hipMemcpyAsync(hp->info, dinfo, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(stream_wait(st));
         info[0] = hp->info[0];
@@ -931,7 +940,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             }
         } else if (!exceptional) {
             int info[2];
-            if ((rc = small(ihi - ns + 1, ihi, dsh, info)) != EIGSOL_OK) break;   // shifts written to dsh
+            if ((rc = small(ihi - ns + 1, ihi, dsh, info, shift_tol)) != EIGSOL_OK) break;   // shifts written to dsh
             if (info[0]) exceptional = true;
         }
         if (exceptional) {

@@ -16,8 +16,8 @@ t = time.perf_counter()
 r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12))
 dt = time.perf_counter() - t
 ok = ""
-if n == 1024:
-    ref = np.load(os.path.join(ROOT, "tests", "golden", "qr_c1024_eigvals.npy"))
+if n in (1024, 4096):
+    ref = np.load(os.path.join(ROOT, "tests", "golden", f"qr_c{n}_eigvals.npy"))
     from scipy.spatial import cKDTree
     d, j = cKDTree(np.c_[ref.real, ref.imag]).query(np.c_[r.eigenvalues_complex.real, r.eigenvalues_complex.imag], k=1)
     ok = f" max_diff={d.max():.2e} one_to_one={len(np.unique(j)) == n}"

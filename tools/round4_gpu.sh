@@ -14,6 +14,11 @@ if [ "$part" = a ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/headline -o run -- python3 $R/bench.py --no-extras --no-cpu-baseline > $OUT/headline.log 2>&1 || { echo "headline profile failed"; exit 1; }
   echo "part a ok"
+elif [ "$part" = q ]; then
+  cd /tmp && export TMPDIR=/tmp
+  EIGSOL_HESS_COOP_PLAIN=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/qr4096 -o run -- python3 $R/tools/prof_driver.py --workload qr4096 > $OUT/qr4096.log 2>&1 || { echo "qr4096 profile failed"; exit 1; }
+  EIGSOL_HESS_COOP_PLAIN=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/qrc4096 -o run -- python3 $R/tools/prof_driver.py --workload qrc4096 > $OUT/qrc4096.log 2>&1 || { echo "qrc4096 profile failed"; exit 1; }
+  echo "part q ok"
 else
   cd /tmp && export TMPDIR=/tmp
   EIGSOL_HESS_COOP_PLAIN=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/qr4096 -o run -- python3 $R/tools/prof_driver.py --workload qr4096 > $OUT/qr4096.log 2>&1 || { echo "qr4096 profile failed"; exit 1; }
