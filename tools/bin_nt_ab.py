@@ -12,9 +12,10 @@ n, k = 10_000_000, 10
 rp, ci, v = S.uniform(n, k)
 x = S.start_vector(n)
 ref = None
-for nt in ("1024", "512", "256", "1024"):
+for nt, xb in (("1024", "1048576"), ("1024", "524288"), ("1024", "2097152"), ("1024", "4194304"), ("1024", "1048576")):
     os.environ["EIGSOL_CSR_BIN_LDS"] = "153"
     os.environ["EIGSOL_CSR_BIN_NT"] = nt
+    os.environ["EIGSOL_CSR_BIN_BYTES"] = xb
     A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
     xd, yd = ctx.malloc(8 * n), ctx.malloc(8 * n)
     ctx.h2d(xd, x)
@@ -33,6 +34,6 @@ for nt in ("1024", "512", "256", "1024"):
         e0.record(st); s.step(40); e1.record(st); torch.cuda.synchronize()
         best = min(best, e0.elapsed_time(e1) / 40)
     info = s.kernel_info()
-    print(json.dumps({"nt": nt, "ms": round(best, 4), "GBps": round(info["bytes_per_iteration"] / best / 1e6, 1),
+    print(json.dumps({"nt": nt, "x_block_bytes": xb, "ms": round(best, 4), "GBps": round(info["bytes_per_iteration"] / best / 1e6, 1),
                       "chunks": info["tiles"], "grid": info["grid"], "bitwise_same_as_first": same}), flush=True)
     s.close(); A.close()
