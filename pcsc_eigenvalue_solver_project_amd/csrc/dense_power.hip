@@ -33,6 +33,16 @@ __device__ __forceinline__ void load_col16(const S* p, S (&v)[PL]) {
     __builtin_memcpy(&v[0], &t, 16);
 }
 
+// one 8-byte scalar, non-temporal (the bits through a double: cplxf is a struct)
+template <class S>
+__device__ __forceinline__ S load8_nt(const S* p) {
+    static_assert(sizeof(S) == 8, "8-byte scalars");
+    const double t = __builtin_nontemporal_load(reinterpret_cast<const double*>(p));
+    S v;
+    __builtin_memcpy(&v, &t, 8);
+    return v;
+}
+
 template <class S>
 struct DenseArgs {
     const S* a;            // column-major, leading dimension n
@@ -74,7 +84,11 @@ __device__ __forceinline__ cplxf ld_agent_s(const cplxf* p) { return cplxf{ld_ag
 __device__ __forceinline__ double ld_agent_s(const double* p) { return ld_agent(p); }
 __device__ __forceinline__ cplx ld_agent_s(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
 
-template <class S, bool kPower>
+// kSplit (8-byte scalars, PL = 2): lane l owns rows l and l + 64 of the tile instead of 2l and
+// 2l + 1, loaded by two 8-byte loads per column whose wave-instructions each cover 512 contiguous
+// bytes (round 4, tools/width_probe.hip: 8-byte non-temporal streams read 7.3 TB/s at 4 workgroups
+// per CU, 16-byte ones 6.7-6.9).  Every row is still summed over the columns in the same order.
+template <class S, bool kPower, bool kSplit = false>
 __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int parity) {
     constexpr int R = DenseTile<S>::kRows;
     constexpr int PL = DenseTile<S>::kPerLane;
@@ -102,7 +116,10 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
     // block -> (row tile, column chunk); chunks of one tile are consecutive block ids
     const int rt = blockIdx.x / a.nchunk;
     const int ch = blockIdx.x % a.nchunk;
-    const int64_t row0 = (int64_t)rt * R + (int64_t)lane * PL;
+    static_assert(!kSplit || PL == 2, "split rows: two 8-byte rows per lane");
+    const int64_t row0 = kSplit ? (int64_t)rt * R + lane : (int64_t)rt * R + (int64_t)lane * PL;
+    // row of the lane's p-th value
+    auto lrow = [&](int p) -> int64_t { return kSplit ? row0 + 64 * p : row0 + p; };
     const int64_t c0 = (int64_t)ch * a.cw;
     const int64_t c1 = min<int64_t>(a.ncols, c0 + a.cw);
 
@@ -114,7 +131,7 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
     const int64_t wc0 = c0 + w * span;
     const int64_t wc1 = min<int64_t>(c1, wc0 + span);
     // 16-byte column pieces need the tile inside the matrix and 16-byte aligned columns
-    const bool vec = row0 + PL <= a.n && (a.n % PL) == 0;
+    const bool vec = kSplit ? lrow(PL - 1) < a.n : (row0 + PL <= a.n && (a.n % PL) == 0);
     int64_t j = wc0;
     {
         // batches of kU columns, all loads issued before the products (A read once: non-temporal),
@@ -127,7 +144,12 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
                     xj[u] = xin[j + u];
-                    load_col16<S, PL>(a.a + (j + u) * a.n + row0, v[u]);
+                    if constexpr (kSplit) {
+#pragma unroll
+                        for (int p = 0; p < PL; ++p) v[u][p] = load8_nt(a.a + (j + u) * a.n + lrow(p));
+                    } else {
+                        load_col16<S, PL>(a.a + (j + u) * a.n + row0, v[u]);
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < kU; ++u) {
@@ -145,17 +167,22 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
         const S* col = a.a + j * a.n;
         if (vec) {
             S v[PL];
-            load_col16<S, PL>(col + row0, v);
+            if constexpr (kSplit) {
+#pragma unroll
+                for (int p = 0; p < PL; ++p) v[p] = load8_nt(col + lrow(p));
+            } else {
+                load_col16<S, PL>(col + row0, v);
+            }
 #pragma unroll
             for (int p = 0; p < PL; ++p) acc[p] = add(acc[p], mul(v[p], xj));
         } else {
 #pragma unroll
             for (int p = 0; p < PL; ++p)
-                if (row0 + p < a.n) acc[p] = add(acc[p], mul(col[row0 + p], xj));
+                if (lrow(p) < a.n) acc[p] = add(acc[p], mul(col[lrow(p)], xj));
         }
     }
 #pragma unroll
-    for (int p = 0; p < PL; ++p) wpart[w][lane * PL + p] = acc[p];
+    for (int p = 0; p < PL; ++p) wpart[w][kSplit ? lane + 64 * p : lane * PL + p] = acc[p];
     __syncthreads();
     // fixed-order wave combine, then publish the chunk partial write-through
     if (threadIdx.x < R) {
@@ -220,7 +247,11 @@ void dense_release(eigsol_dense* A) {
 static void dense_layout(const eigsol_dense* A, int& ntr, int& nchunk, int& cw) {
     const int R = 64 * (16 / (int)scalar_bytes(A->dtype));   // DenseTile<S>::kRows
     ntr = (int)((A->nrows + R - 1) / R);
-    const int64_t target = 2048;   // ~8 blocks per CU
+    // ~4 blocks per CU (EIGSOL_DENSE_TARGET overrides).  Round 4 (tools/dense_ab.sh, 16384^2): f64
+    // 2048 / 1024 / 512 blocks 0.350 / 0.321 / 0.358 ms, c64 0.368 / 0.349 / 0.324 ms; the 8-byte
+    // split-row loads (EIGSOL_DENSE_SPLIT=1, bitwise the same products) 0.343 / 0.337 / 0.316 ms f64
+    int64_t target = 1024;
+    if (const char* e = std::getenv("EIGSOL_DENSE_TARGET")) target = std::max<int64_t>(8, std::atoll(e));
     int64_t nch = std::max<int64_t>(1, target / std::max(1, ntr));
     nch = std::min<int64_t>(nch, std::max<int64_t>(1, (A->ncols + 15) / 16));
     nchunk = (int)nch;
@@ -269,6 +300,21 @@ static int dense_launch_t(eigsol_dense* A, bool power, const void* x, void* y,
     a.trace = (S*)trace;
     const int grid = A->ntr * A->nchunk;
     hipStream_t s = A->ctx->stream;
+    // EIGSOL_DENSE_SPLIT=1: the 8-byte split-row loads for 8-byte scalars (A/B)
+    static const bool split = [] {
+        const char* e = std::getenv("EIGSOL_DENSE_SPLIT");
+        return e && std::atoi(e) != 0;
+    }();
+    if constexpr (sizeof(S) == 8) {
+        if (split) {
+            if (power)
+                hipLaunchKernelGGL((dense_kernel<S, true, true>), dim3(grid), dim3(kThreads), 0, s, a, parity);
+            else
+                hipLaunchKernelGGL((dense_kernel<S, false, true>), dim3(grid), dim3(kThreads), 0, s, a, parity);
+            EIGSOL_HIP(hipGetLastError());
+            return EIGSOL_OK;
+        }
+    }
     if (power)
         hipLaunchKernelGGL((dense_kernel<S, true>), dim3(grid), dim3(kThreads), 0, s, a, parity);
     else
