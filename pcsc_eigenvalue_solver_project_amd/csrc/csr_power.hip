@@ -1980,11 +1980,13 @@ int csr_grid(eigsol_csr* A, int* grid, bool peer) {
         for (const eigsol_csr* B : A->cblk) units = std::max<int64_t>(units, B->ntiles);
         return resident_grid(A->ctx, k, units, grid, 8);
     }
-    // sliced: two blocks (8 waves, 16 slices in flight) per CU measured fastest on band10m;
-    // more concurrent streams per CU cost more than the latency they hide
+    // sliced: two blocks (8 waves, 16 slices in flight) per CU measured fastest on band10m f64
+    // (round 4, tools/slice_grid_ab.py: 2 / 3 / 4 / 6 blocks 188.8 / 201.9 / 226.6 / 225.1 us); more
+    // concurrent streams per CU cost more than the latency they hide.  float (four slices per round,
+    // no pipeline) peaks at three: 128.8 / 125.8 / 128.8 / 156.2 us
     if (dtype_single(A->dtype) && !A->sliced)   // row-per-lane fallback: rows / threads
         return resident_grid(A->ctx, k, (A->nrows + kThreads - 1) / kThreads, grid, 8);
-    return resident_grid(A->ctx, k, units, grid, A->sliced ? 2 : 8);
+    return resident_grid(A->ctx, k, units, grid, A->sliced ? (A->dtype == EIGSOL_F32 ? 3 : 2) : 8);
 }
 
 template <class S>
