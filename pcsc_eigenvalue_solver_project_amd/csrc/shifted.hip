@@ -1002,6 +1002,7 @@ __global__ __launch_bounds__(kThreads) void shift_multi_part_kernel(TriArgs<S> a
     const S* xin = parity ? a.buf0 : a.buf1;
     S* wlast = parity ? a.buf1 : a.buf0;
     double n2[kMaxMulti] = {}, dr[kMaxMulti] = {}, di[kMaxMulti] = {};
+#pragma unroll 2
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * kThreads) {
         S prev = scale_in(xin[i], nrm);
 #pragma unroll
@@ -2231,8 +2232,10 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
                         (size_t)K * (size_t)(f->hpos + 1) * sizeof(S) + 16 + static_lds <= (size_t)160 * 1024) ? 1 : 0;
         }
     }
-    f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
-                                                                  std::min<int64_t>(1024, (n + 1023) / 1024)));
+    int64_t red_cap = 1024;   // EIGSOL_TRSV_PART_GRID: A/B of the partials kernels' grid
+    if (const char* e = std::getenv("EIGSOL_TRSV_PART_GRID")) red_cap = std::max<int64_t>(8, std::atoll(e));
+    f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(f->grid * dev::kWaves, red_cap),
+                                                                  std::min<int64_t>(red_cap, (n + 1023) / 1024)));
     if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), (size_t)f->hpos * 4);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->hcol, hcol.data(), hcol.size() * 4);
     if (rc == EIGSOL_OK) rc = up_(&f->hval, hval.data(), hval.size() * sizeof(S));
