@@ -2234,7 +2234,8 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
     }
     int64_t red_cap = 1024;   // EIGSOL_TRSV_PART_GRID: A/B of the partials kernels' grid
     if (const char* e = std::getenv("EIGSOL_TRSV_PART_GRID")) red_cap = std::max<int64_t>(8, std::atoll(e));
-    f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(f->grid * dev::kWaves, red_cap),
+    // never above grid * kWaves: wave_part (below) holds that many block partials
+    f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
                                                                   std::min<int64_t>(red_cap, (n + 1023) / 1024)));
     if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), (size_t)f->hpos * 4);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->hcol, hcol.data(), hcol.size() * 4);
