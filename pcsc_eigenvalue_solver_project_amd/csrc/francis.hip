@@ -684,7 +684,12 @@ struct AedCtl {
     double beta, tau, hbeta;
 };
 
-__global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, int nw, int spike_valid, int maxits,
+// 256 threads: wave 0 runs the one-wave Schur factorisation (phase A) and the Householder vectors;
+// the reflector applications of phase C take four lanes per row / column, each one of the
+// original four FMA chains of the dot products, combined in the same order (round 4: bitwise the
+// one-wave kernel's results, phase C ~3x shorter)
+constexpr int kAedThreads = 256;
+__global__ __launch_bounds__(kAedThreads) void aed_kernel(double* H, int64_t n, int kw, int nw, int spike_valid, int maxits,
                                                  int early, double* wr, double* wi, double* Vout, int* info) {
     constexpr int LD = kAedMax + 1;
     __shared__ double t[kAedMax * LD];
@@ -693,7 +698,8 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
     __shared__ double sp[kAedMax];
     __shared__ int bs[kAedMax];           // Schur block size ending at each row (1 or 2)
     __shared__ AedCtl c;
-    const int tid = threadIdx.x, nt = 64;   // one wave
+    const int tid = threadIdx.x, nt = kAedThreads;
+    const int grp = tid >> 2, q = tid & 3;   // phase C: 64 groups of four lanes (one wave holds 16 groups)
     auto T = [&](int i, int j) -> double& { return t[i + j * LD]; };
     auto V = [&](int i, int j) -> double& { return v[i + j * LD]; };
     for (int e = tid; e < nw * nw; e += nt) {
@@ -763,20 +769,34 @@ __global__ __launch_bounds__(64) void aed_kernel(double* H, int64_t n, int kw, i
         for (; i < len; ++i) s0 = __builtin_fma(hv[i], elem(i), s0);
         return (s0 + s1) + (s2 + s3);
     };
+    (void)dot4;
+    // lane q of a group runs chain q of dot4 (chain 0 also takes the tail), the four chains meet
+    // as (s0 + s1) + (s2 + s3): dot4's value, bit for bit
+    auto dotq = [&](auto elem, int len) -> double {
+        const int full = len & ~3;
+        double sq = 0.0;
+        for (int i = q; i < full; i += 4) sq = __builtin_fma(hv[i], elem(i), sq);
+        if (q == 0)
+            for (int i = full; i < len; ++i) sq = __builtin_fma(hv[i], elem(i), sq);
+        const double o1 = __shfl_xor(sq, 1, 64);
+        const double pr = (q & 1) ? o1 + sq : sq + o1;
+        const double o2 = __shfl_xor(pr, 2, 64);
+        return (q & 2) ? o2 + pr : pr + o2;
+    };
     auto reflect = [&](int o, int len, int jlo) {
         const double tau = c.tau;
-        for (int j = jlo + tid; j < nw; j += nt) {                       // left: T[o:o+len, jlo:nw]
-            const double w = tau * dot4([&](int i) { return T(o + i, j); }, len);
-            for (int i = 0; i < len; ++i) T(o + i, j) = __builtin_fma(-w, hv[i], T(o + i, j));
+        for (int j = jlo + grp; j < nw; j += nt / 4) {                   // left: T[o:o+len, jlo:nw]
+            const double w = tau * dotq([&](int i) { return T(o + i, j); }, len);
+            for (int i = q; i < len; i += 4) T(o + i, j) = __builtin_fma(-w, hv[i], T(o + i, j));
         }
         __syncthreads();
-        for (int i = tid; i < nw; i += nt) {                             // right: T[0:m, o:o+len], V[:, o:o+len]
-            const double wv = tau * dot4([&](int jj) { return V(i, o + jj); }, len);
+        for (int i = grp; i < nw; i += nt / 4) {                         // right: T[0:m, o:o+len], V[:, o:o+len]
+            const double wv = tau * dotq([&](int jj) { return V(i, o + jj); }, len);
             if (i < m) {
-                const double w = tau * dot4([&](int jj) { return T(i, o + jj); }, len);
-                for (int jj = 0; jj < len; ++jj) T(i, o + jj) = __builtin_fma(-w, hv[jj], T(i, o + jj));
+                const double w = tau * dotq([&](int jj) { return T(i, o + jj); }, len);
+                for (int jj = q; jj < len; jj += 4) T(i, o + jj) = __builtin_fma(-w, hv[jj], T(i, o + jj));
             }
-            for (int jj = 0; jj < len; ++jj) V(i, o + jj) = __builtin_fma(-wv, hv[jj], V(i, o + jj));
+            for (int jj = q; jj < len; jj += 4) V(i, o + jj) = __builtin_fma(-wv, hv[jj], V(i, o + jj));
         }
         __syncthreads();
     };
@@ -1002,7 +1022,7 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         if (aed_win > 0) {
             const int nw = std::min(aed_win, N);
             const int kw = ihi - nw + 1;
-            hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(64), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60,
+            hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(dev::kAedThreads), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60,
                                aed_early ? 1 : 0, dwr, dwi, dU, dinfo);
             int* info = hp->info;
             double* const awr = hp->awr;
