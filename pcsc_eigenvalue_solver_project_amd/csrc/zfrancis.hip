@@ -289,128 +289,156 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
 struct ZAedCtl {
     cplx tau, spike;
     double beta;
+    int fail, maxsw, steps, nd;
 };
-__global__ __launch_bounds__(64) void zaed_kernel(cplx* Hg, int64_t n, int kw, int nw, int spike_valid, int early,
-                                                  cplx* w, cplx* Vout, int* info) {
+// 256 threads: wave 0 runs the one-wave Schur factorisation, the spike test and the Householder
+// vectors; the reflector applications of the back-reduction take four lanes per row / column (each
+// sums every fourth term, the four partial sums meet as (s0 + s1) + (s2 + s3)).  Round 4: the
+// one-wave version summed each dot product in one chain.
+constexpr int kZAedThreads = 256;
+__device__ __forceinline__ cplx quad_sum(cplx sq, int q) {   // (s0 + s1) + (s2 + s3) over the 4-lane group
+    const cplx o1{__shfl_xor(sq.re, 1, 64), __shfl_xor(sq.im, 1, 64)};
+    const cplx pr = (q & 1) ? add(o1, sq) : add(sq, o1);
+    const cplx o2{__shfl_xor(pr.re, 2, 64), __shfl_xor(pr.im, 2, 64)};
+    return (q & 2) ? add(o2, pr) : add(pr, o2);
+}
+__global__ __launch_bounds__(kZAedThreads) void zaed_kernel(cplx* Hg, int64_t n, int kw, int nw, int spike_valid,
+                                                            int early, cplx* w, cplx* Vout, int* info) {
     constexpr int lh = kZSmall + 1;
+    constexpr int NT = kZAedThreads;
     __shared__ cplx t[kZSmall * lh];
     __shared__ cplx v[kZSmall * lh];
     __shared__ cplx hv[kZSmall];
     __shared__ cplx sp[kZSmall];
     __shared__ ZAedCtl c;
-    const int ln = threadIdx.x;
+    const int tid = threadIdx.x, ln = tid & 63, wv0 = tid < 64;
+    const int grp = tid >> 2, q = tid & 3;   // 64 groups of four lanes
     auto T = [&](int i, int j) -> cplx& { return t[i + j * lh]; };
     auto V = [&](int i, int j) -> cplx& { return v[i + j * lh]; };
-    for (int e = ln; e < nw * nw; e += 64) {
+    for (int e = tid; e < nw * nw; e += NT) {
         const int i = e % nw, j = e / nw;
         T(i, j) = Hg[(kw + i) + (int64_t)(kw + j) * n];
         V(i, j) = i == j ? cplx{1.0, 0.0} : cplx{0.0, 0.0};
     }
     const cplx spike = (spike_valid && kw > 0) ? Hg[kw + (int64_t)(kw - 1) * n] : cplx{0.0, 0.0};
     __syncthreads();
-    int fail, maxsw, steps, stop = -1;
-    zwave_hqr<true>(t, v, nw, w + kw, fail, maxsw, steps, early ? cabs1(spike) : -1.0, &stop);
-    __syncthreads();
-    // spike test, one window row per lane; deflated = the trailing run of negligible entries
-    const double ulp = 2.220446049250313e-16, smlnum = 2.2250738585072014e-308 * ((double)nw / ulp);
-    int nd = 0;
-    if (early) {
-        nd = fail ? 0 : nw - 1 - stop;   // the spike test ran inside the factorisation
-    } else if (!fail) {
-        bool keep = false;
-        if (ln < nw) {
-            double foo = cabs1(T(ln, ln));
-            if (foo == 0.0) foo = cabs1(spike);
-            keep = cabs1(spike) * cabs1(V(0, ln)) > fmax(smlnum, ulp * foo);
+    if (wv0) {
+        int fail, maxsw, steps, stop = -1;
+        zwave_hqr<true>(t, v, nw, w + kw, fail, maxsw, steps, early ? cabs1(spike) : -1.0, &stop);
+        // spike test, one window row per lane; deflated = the trailing run of negligible entries
+        const double ulp = 2.220446049250313e-16, smlnum = 2.2250738585072014e-308 * ((double)nw / ulp);
+        int nd = 0;
+        if (early) {
+            nd = fail ? 0 : nw - 1 - stop;   // the spike test ran inside the factorisation
+        } else if (!fail) {
+            bool keep = false;
+            if (ln < nw) {
+                double foo = cabs1(T(ln, ln));
+                if (foo == 0.0) foo = cabs1(spike);
+                keep = cabs1(spike) * cabs1(V(0, ln)) > fmax(smlnum, ulp * foo);
+            }
+            const unsigned long long km = __ballot(keep);
+            nd = km ? nw - 1 - (63 - __clzll(km)) : nw;
         }
-        const unsigned long long km = __ballot(keep);
-        nd = km ? nw - 1 - (63 - __clzll(km)) : nw;
+        if (ln == 0) {
+            c.fail = fail;
+            c.maxsw = maxsw;
+            c.steps = steps;
+            c.nd = nd;
+        }
     }
+    __syncthreads();
+    const int nd = c.nd;
     const int m = nw - nd;
     // undeflated part + spike back to Hessenberg form.  Q = I - tau hv hv^H (hv[0] = 1) applied
     // as Q^H T on rows [o, o + len) (columns [jlo, nw)), then T Q on T's rows [0, m) and V Q
     auto reflect = [&](int o, int len, int jlo) {
         const cplx tau = c.tau, ctau = cconj(tau);
-        for (int j = jlo + ln; j < nw; j += 64) {
-            cplx s{0.0, 0.0};
-            for (int i = 0; i < len; ++i) s = add(s, cmul_conj(hv[i], T(o + i, j)));
-            const cplx wv = mul(ctau, s);
-            for (int i = 0; i < len; ++i) T(o + i, j) = sub(T(o + i, j), mul(hv[i], wv));
+        for (int j = jlo + grp; j < nw; j += NT / 4) {
+            cplx sq{0.0, 0.0};
+            for (int i = q; i < len; i += 4) sq = add(sq, cmul_conj(hv[i], T(o + i, j)));
+            const cplx wv = mul(ctau, quad_sum(sq, q));
+            for (int i = q; i < len; i += 4) T(o + i, j) = sub(T(o + i, j), mul(hv[i], wv));
         }
         __syncthreads();
-        if (ln < nw) {
-            cplx s{0.0, 0.0};
-            for (int jj = 0; jj < len; ++jj) s = add(s, mul(V(ln, o + jj), hv[jj]));
-            const cplx wv = mul(tau, s);
-            for (int jj = 0; jj < len; ++jj) V(ln, o + jj) = sub(V(ln, o + jj), mul(wv, cconj(hv[jj])));
+        if (grp < nw) {
+            cplx sq{0.0, 0.0};
+            for (int jj = q; jj < len; jj += 4) sq = add(sq, mul(V(grp, o + jj), hv[jj]));
+            const cplx wv = mul(tau, quad_sum(sq, q));
+            for (int jj = q; jj < len; jj += 4) V(grp, o + jj) = sub(V(grp, o + jj), mul(wv, cconj(hv[jj])));
         }
-        if (ln < m) {
-            cplx s{0.0, 0.0};
-            for (int jj = 0; jj < len; ++jj) s = add(s, mul(T(ln, o + jj), hv[jj]));
-            const cplx wv = mul(tau, s);
-            for (int jj = 0; jj < len; ++jj) T(ln, o + jj) = sub(T(ln, o + jj), mul(wv, cconj(hv[jj])));
+        if (grp < m) {
+            cplx sq{0.0, 0.0};
+            for (int jj = q; jj < len; jj += 4) sq = add(sq, mul(T(grp, o + jj), hv[jj]));
+            const cplx wv = mul(tau, quad_sum(sq, q));
+            for (int jj = q; jj < len; jj += 4) T(grp, o + jj) = sub(T(grp, o + jj), mul(wv, cconj(hv[jj])));
         }
         __syncthreads();
     };
-    // ZLARFG of x[0..len) by the wave: hv, c.tau (0: Q = I), c.beta (real)
+    // ZLARFG of x[0..len) by wave 0: hv, c.tau (0: Q = I), c.beta (real); every thread calls it
     auto house = [&](const cplx* x, int len) {
-        const cplx alpha = x[0];
-        double part = 0.0;
-        for (int i = 1 + ln; i < len; i += 64) part += sq_abs(x[i]);
-        const double xn2 = wave_sum(part);
         cplx tau{0.0, 0.0}, sc{0.0, 0.0};
-        double beta = alpha.re;
-        if (xn2 != 0.0 || alpha.im != 0.0) {
-            beta = -copysign(sqrt(sq_abs(alpha) + xn2), alpha.re);
-            tau = cplx{(beta - alpha.re) / beta, -alpha.im / beta};
-            sc = cdiv_s(cplx{1.0, 0.0}, cplx{alpha.re - beta, alpha.im});
+        double beta = 0.0;
+        if (wv0) {
+            const cplx alpha = x[0];
+            double part = 0.0;
+            for (int i = 1 + ln; i < len; i += 64) part += sq_abs(x[i]);
+            const double xn2 = wave_sum(part);
+            beta = alpha.re;
+            if (xn2 != 0.0 || alpha.im != 0.0) {
+                beta = -copysign(sqrt(sq_abs(alpha) + xn2), alpha.re);
+                tau = cplx{(beta - alpha.re) / beta, -alpha.im / beta};
+                sc = cdiv_s(cplx{1.0, 0.0}, cplx{alpha.re - beta, alpha.im});
+            }
         }
         __syncthreads();   // x may alias a T column the stores below do not touch; order the reads
-        for (int i = 1 + ln; i < len; i += 64) hv[i] = mul(x[i], sc);
-        if (ln == 0) {
-            hv[0] = cplx{1.0, 0.0};
-            c.tau = tau;
-            c.beta = beta;
+        if (wv0) {
+            for (int i = 1 + ln; i < len; i += 64) hv[i] = mul(x[i], sc);
+            if (ln == 0) {
+                hv[0] = cplx{1.0, 0.0};
+                c.tau = tau;
+                c.beta = beta;
+            }
         }
         __syncthreads();
     };
     if (nd > 0 && m > 0) {
-        for (int i = ln; i < m; i += 64) sp[i] = mul(spike, cconj(V(0, i)));
+        for (int i = tid; i < m; i += NT) sp[i] = mul(spike, cconj(V(0, i)));
         __syncthreads();
         if (m > 1) {
             house(sp, m);
-            if (ln == 0) c.spike = cplx{c.beta, 0.0};
+            if (tid == 0) c.spike = cplx{c.beta, 0.0};
             __syncthreads();
             if (c.tau.re != 0.0 || c.tau.im != 0.0) reflect(0, m, 0);
         } else {
-            if (ln == 0) c.spike = sp[0];
+            if (tid == 0) c.spike = sp[0];
             __syncthreads();
         }
         for (int col = 0; col + 2 < m; ++col) {
             house(&T(col + 1, col), m - col - 1);
-            if (ln == 0) T(col + 1, col) = cplx{c.beta, 0.0};
-            for (int i = col + 2 + ln; i < m; i += 64) T(i, col) = cplx{0.0, 0.0};
+            if (tid == 0) T(col + 1, col) = cplx{c.beta, 0.0};
+            for (int i = col + 2 + tid; i < m; i += NT) T(i, col) = cplx{0.0, 0.0};
             __syncthreads();
             if (c.tau.re != 0.0 || c.tau.im != 0.0) reflect(col + 1, m - col - 1, col + 1);
         }
-    } else if (ln == 0) {
+    } else if (tid == 0) {
         c.spike = cplx{0.0, 0.0};
     }
     __syncthreads();
     if (nd > 0) {
-        for (int e = ln; e < nw * nw; e += 64) {
+        for (int e = tid; e < nw * nw; e += NT) {
             const int i = e % nw, j = e / nw;
             Hg[(kw + i) + (int64_t)(kw + j) * n] = i > j + 1 ? cplx{0.0, 0.0} : T(i, j);
             Vout[e] = V(i, j);
         }
-        if (ln == 0 && spike_valid && kw > 0) Hg[kw + (int64_t)(kw - 1) * n] = c.spike;
+        if (tid == 0 && spike_valid && kw > 0) Hg[kw + (int64_t)(kw - 1) * n] = c.spike;
     }
-    if (ln == 0) {
-        info[0] = fail;
+    if (tid == 0) {
+        info[0] = c.fail;
         info[1] = nd;
-        info[2] = maxsw;
+        info[2] = c.maxsw;
         info[3] = m;
-        info[4] = steps;
+        info[4] = c.steps;
     }
 }
 
@@ -887,7 +915,7 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         if (aed_win >= 4) {
             const int nw = std::min(aed_win, N);
             const int kw = ihi - nw + 1;
-            hipLaunchKernelGGL(dev::zaed_kernel, dim3(1), dim3(64), 0, st, H, (int64_t)n, kw, nw, kw > l ? 1 : 0,
+            hipLaunchKernelGGL(dev::zaed_kernel, dim3(1), dim3(dev::kZAedThreads), 0, st, H, (int64_t)n, kw, nw, kw > l ? 1 : 0,
                                aed_full ? 0 : 1, dw, dV, dinfo);
             int* info = hp->info;
             if (hipMemcpyAsync(info, dinfo, 5 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
