@@ -32,6 +32,8 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <exception>
+#include <string>
 #include <vector>
 
 #include "kernels_common.hpp"
@@ -632,8 +634,11 @@ void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps) {
 extern "C" int eigsol_sparse_lu_fill(int64_t n, const int32_t* rowptr, const int32_t* colidx, int64_t cap,
                                      int64_t* nnz_out, int32_t* lower_levels_out) {
     using namespace eigsol;
-    if (n < 0 || (n > 0 && (!rowptr || !colidx)) || !nnz_out || n > INT32_MAX - 1)
+    if (n < 0 || (n > 0 && (!rowptr || !colidx)) || !nnz_out || n > INT32_MAX - 1 || (rowptr && rowptr[0] != 0))
         return fail(EIGSOL_E_INVALID, "eigsol_sparse_lu_fill: bad arguments");
+    for (int64_t i = 0; i < n; ++i)
+        if (rowptr[i + 1] < rowptr[i]) return fail(EIGSOL_E_INVALID, "eigsol_sparse_lu_fill: row pointers not monotone");
+    try {
     // A's pattern with the diagonal inserted (the shifted matrix A - sigma I always stores it)
     std::vector<int32_t> mrp(n + 1, 0), mci;
     mci.reserve((size_t)rowptr[n] + n);
@@ -674,4 +679,7 @@ extern "C" int eigsol_sparse_lu_fill(int64_t n, const int32_t* rowptr, const int
         *lower_levels_out = top;
     }
     return EIGSOL_OK;
+    } catch (const std::exception& ex) {   // host allocation: no exception crosses the C ABI
+        return fail(EIGSOL_E_INVALID, std::string("eigsol_sparse_lu_fill: ") + ex.what());
+    }
 }

@@ -123,4 +123,6 @@ def test_cap_and_errors():
     oor = np.array([0, 1], np.int32), np.array([5], np.int32)         # column out of range
     assert lib().eigsol_sparse_lu_fill(1, oor[0].ctypes.data, oor[1].ctypes.data, 100, C.byref(out), None) == 9
     assert lib().eigsol_sparse_lu_fill(-1, None, None, 100, C.byref(out), None) == 9
+    nonmono = np.array([0, 2, 1], np.int32), np.array([0, 1], np.int32)   # row pointers not monotone
+    assert lib().eigsol_sparse_lu_fill(2, nonmono[0].ctypes.data, nonmono[1].ctypes.data, 100, C.byref(out), None) == 9
     assert _call(np.zeros(1, np.int32), np.zeros(0, np.int32), 0, 10) == (0, 0)
