@@ -12,7 +12,10 @@
 * solve_shifted on the same matrix: ||(A - σI) y - b|| <= 1e-10 ||b||;
 * the preconditioner: the exact sparse LU (complete fill, variant 18) where the filled pattern fits
   EIGSOL_LU_FILL_CAP x nnz — a direct solve checked by its true residual — and ILU(0) (variant 7) otherwise, both
-  to the same parity.
+  to the same parity;
+* the exact LU has no pivoting: a band matrix whose no-pivot LU meets 1e-9 pivots (growth ~1e9) is
+  solved to 1e-10 ||b|| through the residual check + GMRES refinement, and one with exactly zero
+  pivots through the densified partial-pivot LU fallback, both at the oracle's λ and iteration count.
 EIGSOL_SPARSE_SOLVER=gmres forces the GMRES path below the densify threshold (n > 16384 uses it
 by default)."""
 import os
@@ -142,4 +145,58 @@ def test_gmres_general_sparse_1m(ctx):
     b = S.start_vector(n, np.complex128, seed=11)
     y = E.solve_shifted(A, sigma, b)
     assert np.linalg.norm(M @ y - sigma * y - b) <= 1e-10 * np.linalg.norm(b)
+    A.close()
+
+
+def _small_pivot_matrix(n, sigma, pivot, seed):
+    """Nonsymmetric sparse f64 matrix whose LU of A - σI without pivoting meets 40 pivots of size
+    `pivot`: rows with no entry left of the diagonal have u_ii = a_ii - σ exactly, and a unit
+    coupling to the next row makes l_{i+1,i} = 1 / pivot (growth 1 / pivot). The matrix itself is
+    well conditioned (each pair [[pivot, 1], [1, ·]] has determinant ≈ -1)."""
+    rng = np.random.default_rng(seed)
+    # random entries within 4 of the diagonal: the filled pattern stays inside the band (< 3 x nnz)
+    offs = [o for o in range(-4, 5) if o]
+    M = sp.diags([rng.standard_normal(n - abs(o)) * (rng.random(n - abs(o)) < 0.5) for o in offs] +
+                 [3.0 + rng.random(n)], offs + [0]).tolil()
+    for i in rng.choice(np.arange(10, n - 1, 7), 40, replace=False):
+        M[i, :i] = 0.0
+        M[i, i] = sigma + pivot
+        M[i, i + 1] = 1.0
+        M[i + 1, i] = 1.0
+    M = sp.csr_matrix(M)
+    M.eliminate_zeros()
+    M.sort_indices()
+    return M
+
+
+@pytest.mark.parametrize("pivot", [1e-9, 0.0])
+def test_exact_lu_small_and_zero_pivots(ctx, gmres_env, pivot):
+    """No-pivot LU over the filled pattern (variant 18) when its pivots are tiny: the direct solve is
+    checked by its true residual and refined by GMRES over the same factor; an exactly zero pivot
+    falls back to the densified partial-pivot LU. Either way the solve meets 1e-10 ||b|| and the
+    shifted inverse iteration matches the oracle's reference loop (shifted_dense)."""
+    n, sigma = 600, 0.5   # the oracle refactors densely every iteration
+    M = _small_pivot_matrix(n, sigma, pivot, 13)
+    D = M.toarray()
+    A = E.CsrMatrix.from_scipy(ctx, M)
+    b = np.random.default_rng(2).standard_normal(n)
+    y = E.solve_shifted(A, sigma, b)
+    assert np.linalg.norm(D @ y - sigma * y - b) <= 1e-10 * np.linalg.norm(b)
+    s = E.ShiftedSession(A, sigma)
+    x0 = S.start_vector(n)
+    s.begin(E.ShiftedSolverOptions(300, 1e-12, sigma), x0)
+    done = False
+    while not done:
+        s.step(1)
+        done, _ = s.query()
+    info = s.kernel_info()
+    r = s.finish()
+    s.close()
+    if pivot:
+        assert info["variant"] == 18, info
+    ref = O.shifted_dense(D, sigma, x0, 300, 1e-12)
+    assert r.converged == ref["converged"]
+    lam = ref["eigenvalue"]
+    assert abs(r.eigenvalue - lam) <= 1e-10 * (1 + abs(lam)), (r.eigenvalue, lam)
+    assert abs(r.iterations - ref["iterations"]) <= 1
     A.close()
