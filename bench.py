@@ -15,7 +15,10 @@ value  : algorithmic bytes (12 nnz + 4 (n+1) + 16 n per iteration, 
          ranks' blocks) x iterations / max-over-ranks wall time of the K timed iterations; inputs
          resident in HBM.
 
-Run: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run).
+Run: python bench.py [--gpus N --steps K --warmup W].  N>1 runs one rank per GPU: either launched
+by torch.distributed.run (WORLD_SIZE set), or, when started directly, bench.py starts the N ranks
+itself as a child torch.distributed.run over 127.0.0.1 before importing torch and relays rank 0's
+line and exit code.
 """
 from __future__ import annotations
 
@@ -490,14 +493,45 @@ def run_config5_general(E, S, ctx, torch, stream):
     return out
 
 
+def launcher_cmd(argv, n, port, python=None):
+    """The child command that starts N ranks of this script, one per GPU of this node (the
+    contract's own form: torch.distributed.run over 127.0.0.1, arguments forwarded unchanged)."""
+    return [python or sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(argv, n, cmd=None):
+    """`python bench.py --gpus N` with N > 1 outside torch.distributed.run: start the N ranks as a
+    CHILD process (never exec: nothing here has imported torch or touched a GPU), relay rank 0's
+    JSON line to stdout and everything else to stderr as it arrives, and return the child's exit
+    code."""
+    import socket
+    import subprocess
+    if cmd is None:
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        cmd = launcher_cmd(argv, n, port)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this host driver
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    for line in p.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            print(s, flush=True)
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    return p.wait()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("bench.py --gpus N>1 must run under torch.distributed.run")
     import torch
     import torch.distributed as dist
 
@@ -563,6 +597,11 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     elapsed_max, ev_max = float(el[0]), float(el[1])
+    transport_names = {0: "none", 1: "collective", 2: "peer"}
+    transports = [transport_names[transport]]
+    if world > 1:
+        transports = [None] * world
+        dist.all_gather_object(transports, transport_names[transport])
 
     bytes_iter = info["bytes_per_iteration"]          # this rank's algorithmic bytes
     total_bytes = float(tot[0]) * args.steps          # all ranks' blocks
@@ -627,7 +666,7 @@ def main():
         dv, rk, nr, ck = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         if E.lib().eigsol_ctx_info(ctx.handle, C.byref(dv), C.byref(rk), C.byref(nr), C.byref(ck)) == 0:
             out["config"]["communicator"] = {
-                "library_ranks": nr.value, "library_rank": rk.value,
+                "library_ranks": nr.value, "library_rank": rk.value, "transport_per_rank": transports,
                 "kind": {0: "none (one GPU)", 1: "RCCL communicator", 2: "loopback", 3: "host all-gather + peer inboxes"}[ck.value],
                 "note": "from eigsol_ctx_info: the ranks the library itself exchanges with (no 8-GPU run of "
                         "this line has been recorded by the builder; the driver's SCALE record is the measurement)"}

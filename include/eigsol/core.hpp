@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <limits>
 #include <cstdint>
 #include <deque>
 #include <initializer_list>
@@ -97,6 +98,12 @@ struct DDWire {
 struct CDDWire {
     DDWire re, im;
 };
+// Exact for the x87 80-bit format (64-bit significand: hi holds 53 bits, lo the remaining 11) as long
+// as lo's bits stay above the subnormal grid, i.e. |v| >= ~2^-1010 (1e-304); below that the pair is
+// the double-double nearest v.  A long double with a wider significand (IEEE binary128, e.g. aarch64)
+// does not fit {hi, lo} and is refused at compile time.
+static_assert(std::numeric_limits<long double>::digits == 64,
+              "EigSol: the double-double wire format assumes the x87 80-bit long double");
 inline DDWire to_wire(long double v) {
     const double hi = static_cast<double>(v);
     if (std::isfinite(v) && !std::isfinite(hi))

@@ -14,7 +14,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._capi import (EIGSOL_C64, EIGSOL_C128, EIGSOL_CDD, EIGSOL_DD, EIGSOL_E_INVALID, EIGSOL_E_SIZE_MISMATCH, EIGSOL_F32,
+from ._capi import (EIGSOL_C64, EIGSOL_C128, EIGSOL_CDD, EIGSOL_DD, EIGSOL_E_INVALID, EIGSOL_E_SIZE_MISMATCH, EIGSOL_E_UNSUPPORTED, EIGSOL_F32,
                     EIGSOL_F64, EigSolError, SolverOptionsC, call, check, last_error, lib)
 
 __all__ = [
@@ -78,11 +78,17 @@ def is_wide(dtype) -> bool:
 
 def to_wire(a, dtype) -> np.ndarray:
     """Host scalars of ``dtype`` in the C ABI's layout (a contiguous buffer, flattened in C order).
-    long double values become exact double-double pairs {hi = (double) v, lo = (double)(v - hi)}:
-    the x87 64-bit significand fits in hi's 53 bits plus lo's 11, so nothing is rounded."""
+    long double values become double-double pairs {hi = (double) v, lo = (double)(v - hi)}.  Exact
+    for the x87 format (64-bit significand: 53 bits in hi, 11 in lo) while lo is a normal double,
+    i.e. |v| >= ~2^-1010 (1e-304); below that lo falls under the subnormal grid, the pair is the nearest double-double and a
+    RuntimeWarning says so.  A long double with another significand (IEEE binary128 on aarch64)
+    is refused: its values do not fit {hi, lo}."""
     a = np.ascontiguousarray(a, dtype=dtype)
     if not is_wide(dtype):
         return a
+    if np.finfo(np.longdouble).nmant != 63:
+        raise EigSolError(EIGSOL_E_UNSUPPORTED, "long double is not the x87 80-bit format on this platform; "
+                                                "the double-double wire format cannot carry it exactly")
     flat = a.reshape(-1)
     parts = [flat.real, flat.imag] if np.iscomplexobj(flat) else [flat]
     cols = []
@@ -93,6 +99,10 @@ def to_wire(a, dtype) -> np.ndarray:
             raise EigSolError(EIGSOL_E_INVALID, "long double value outside the double exponent range "
                                                 "(double-double carries |v| < 1.8e308)")
         lo = (p - hi.astype(np.longdouble)).astype(np.float64)
+        if np.any(hi.astype(np.longdouble) + lo.astype(np.longdouble) != p):
+            import warnings
+            warnings.warn("long double values below ~2^-1010 (1e-304) lose low bits in the double-double wire format "
+                          "(the low part falls under the subnormal grid)", RuntimeWarning, stacklevel=2)
         cols += [hi, lo]
     return np.ascontiguousarray(np.stack(cols, axis=-1))
 

@@ -901,12 +901,12 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     const double eps = 2.220446049250313e-16;
     double *dwr = nullptr, *dwi = nullptr, *dds = nullptr, *dU = nullptr, *dsh = nullptr;
     int* dinfo = nullptr;
-    EIGSOL_HIP(hipMalloc(&dwr, n * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&dwi, n * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&dds, 2 * n * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&dU, dev::kMaxGroups * dev::kWin * dev::kWin * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&dsh, 4 * dev::kMaxBulges * sizeof(double)));
-    EIGSOL_HIP(hipMalloc(&dinfo, 64));
+    int rc = EIGSOL_OK;
+    if (hipMalloc(&dwr, n * sizeof(double)) != hipSuccess || hipMalloc(&dwi, n * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dds, 2 * n * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dU, dev::kMaxGroups * dev::kWin * dev::kWin * sizeof(double)) != hipSuccess ||
+        hipMalloc(&dsh, 4 * dev::kMaxBulges * sizeof(double)) != hipSuccess || hipMalloc(&dinfo, 64) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "francis: device workspace");
     // every per-sweep transfer goes through pinned host memory: a pageable hipMemcpyAsync is staged
     // by the runtime and waited for with a sleeping wait, ~1 ms per copy (round-4 kernel trace,
     // tools/gap_analysis.py), more than a sweep's kernels at the end of the iteration
@@ -917,11 +917,13 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     };
     Staging* hp = nullptr;
     double* ds = nullptr;   // deflation scans: diagonal [0, n), subdiagonal [n, 2n)
-    EIGSOL_HIP(hipHostMalloc(&hp, sizeof(Staging), hipHostMallocDefault));
-    EIGSOL_HIP(hipHostMalloc(&ds, 2 * n * sizeof(double), hipHostMallocDefault));
-    double* const swr = hp->swr;
-    double* const swi = hp->swi;
-    int rc = EIGSOL_OK;
+    // on any allocation failure rc is set, the loop below never runs and the common cleanup at the
+    // end frees whatever was allocated
+    if (rc == EIGSOL_OK && (hipHostMalloc(&hp, sizeof(Staging), hipHostMallocDefault) != hipSuccess ||
+                            hipHostMalloc(&ds, 2 * n * sizeof(double), hipHostMallocDefault) != hipSuccess))
+        rc = fail(EIGSOL_E_HIP, "francis: pinned staging");
+    double* const swr = hp ? hp->swr : nullptr;
+    double* const swi = hp ? hp->swi : nullptr;
     int sweeps = 0, failed = 0;
     int ihi = (int)n - 1;
     int stall = 0;               // sweeps on the current bottom block without a deflation
@@ -1226,8 +1228,8 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                      (long long)n, st_sweeps, st_windows, st_steps, st_small, st_small_rows, kSmall, st_aed, st_aed_defl,
                      aed_win, st_aed_steps, st_aed_ph[0] * 1e-5, st_aed_ph[1] * 1e-5, st_aed_ph[2] * 1e-5);
     for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo}) (void)hipFree(p);
-    (void)hipHostFree(ds);
-    (void)hipHostFree(hp);
+    if (ds) (void)hipHostFree(ds);
+    if (hp) (void)hipHostFree(hp);
     // iterations reported: sweeps spent on the slowest deflation (>= 1, the final check), so that
     // iterations <= maxIterations exactly when the iteration converged
     *sweeps_out = std::max(1, sweeps);

@@ -318,7 +318,11 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     // complete fill where affordable: M's values on the closed pattern, zeros at the fill
     // positions; the factorization below then produces the exact LU (round 4: the 1M config-5
     // matrix made general fills 16.5M -> ~24M entries and GMRES needs one step per solve instead of
-    // 7-10 over ILU(0))
+    // 7-10 over ILU(0)).  M's own pattern is kept aside: the exact LU without pivoting meets a zero
+    // pivot whenever a leading minor of M is singular, where ILU(0)'s (dropped-fill) pivots may all
+    // be nonzero, so that case retries ILU(0) before reporting SparseLU's failure
+    std::vector<int32_t> orp, oci, odpos;
+    std::vector<S> ov;
     {
         double ratio = 3.0;
         if (const char* e = std::getenv("EIGSOL_LU_FILL_CAP")) ratio = std::atof(e);
@@ -337,53 +341,77 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
             mci.swap(fci);
             mv.swap(fv);
             dpos.swap(fdpos);
+            orp.swap(frp);
+            oci.swap(fci);
+            ov.swap(fv);
+            odpos.swap(fdpos);
             g->complete = 1;
         }
     }
-    g->nnzK = (int64_t)mci.size();
-    // ILU(0) levels: level(i) = 1 + max level of the rows its strict lower part reads
-    std::vector<int32_t> lev(n, 0), lcount;
-    for (int64_t i = 0; i < n; ++i) {
-        int32_t l = 0;
-        for (int32_t e = mrp[i]; e < dpos[i]; ++e) l = std::max(l, lev[mci[e]] + 1);
-        lev[i] = l;
-        if ((int32_t)lcount.size() <= l) lcount.resize(l + 1, 0);
-        ++lcount[l];
-    }
-    std::vector<int32_t> lstart(lcount.size() + 1, 0), rows(n);
-    for (size_t l = 0; l < lcount.size(); ++l) lstart[l + 1] = lstart[l] + lcount[l];
-    {
-        std::vector<int32_t> fill(lstart.begin(), lstart.end() - 1);
-        for (int64_t i = 0; i < n; ++i) rows[fill[lev[i]]++] = (int32_t)i;
-    }
-    int32_t *d_rp = nullptr, *d_ci = nullptr, *d_dpos = nullptr, *d_rows = nullptr, *d_z = nullptr;
-    S* d_v = nullptr;
-    if (rc == EIGSOL_OK &&
-        (hipMalloc(&d_rp, (n + 1) * 4) != hipSuccess || hipMalloc(&d_ci, std::max<int64_t>(1, g->nnzK) * 4) != hipSuccess ||
-         hipMalloc(&d_v, std::max<int64_t>(1, g->nnzK) * sizeof(S)) != hipSuccess ||
-         hipMalloc(&d_dpos, n * 4) != hipSuccess || hipMalloc(&d_rows, n * 4) != hipSuccess ||
-         hipMalloc(&d_z, 4) != hipSuccess))
-        rc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) buffers");
     int32_t zpiv = 0;
-    std::vector<S> lu(g->nnzK);
-    if (rc == EIGSOL_OK) {
-        hipMemcpyAsync(d_rp, mrp.data(), (n + 1) * 4, hipMemcpyHostToDevice, st);
-        hipMemcpyAsync(d_ci, mci.data(), g->nnzK * 4, hipMemcpyHostToDevice, st);
-        hipMemcpyAsync(d_v, mv.data(), g->nnzK * sizeof(S), hipMemcpyHostToDevice, st);
-        hipMemcpyAsync(d_dpos, dpos.data(), n * 4, hipMemcpyHostToDevice, st);
-        hipMemcpyAsync(d_rows, rows.data(), n * 4, hipMemcpyHostToDevice, st);
-        hipMemsetAsync(d_z, 0, 4, st);
-        for (size_t l = 0; l < lcount.size(); ++l) {
-            const int32_t cnt = lcount[l];
-            hipLaunchKernelGGL((dev::ilu0_level_kernel<S>), dim3((cnt + 255) / 256), dim3(256), 0, st, d_rp, d_ci,
-                               d_dpos, d_v, d_rows + lstart[l], cnt, d_z);
+    std::vector<S> lu;
+    // IKJ factorization on the current pattern (mrp/mci/mv/dpos), level by level on the device
+    auto factor = [&]() -> int {
+        g->nnzK = (int64_t)mci.size();
+        // ILU(0) levels: level(i) = 1 + max level of the rows its strict lower part reads
+        std::vector<int32_t> lev(n, 0), lcount;
+        for (int64_t i = 0; i < n; ++i) {
+            int32_t l = 0;
+            for (int32_t e = mrp[i]; e < dpos[i]; ++e) l = std::max(l, lev[mci[e]] + 1);
+            lev[i] = l;
+            if ((int32_t)lcount.size() <= l) lcount.resize(l + 1, 0);
+            ++lcount[l];
         }
-        hipMemcpyAsync(&zpiv, d_z, 4, hipMemcpyDeviceToHost, st);
-        hipMemcpyAsync(lu.data(), d_v, g->nnzK * sizeof(S), hipMemcpyDeviceToHost, st);
-        if (stream_wait(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) factorization");
+        std::vector<int32_t> lstart(lcount.size() + 1, 0), rows(n);
+        for (size_t l = 0; l < lcount.size(); ++l) lstart[l + 1] = lstart[l] + lcount[l];
+        {
+            std::vector<int32_t> fill(lstart.begin(), lstart.end() - 1);
+            for (int64_t i = 0; i < n; ++i) rows[fill[lev[i]]++] = (int32_t)i;
+        }
+        int frc = EIGSOL_OK;
+        int32_t *d_rp = nullptr, *d_ci = nullptr, *d_dpos = nullptr, *d_rows = nullptr, *d_z = nullptr;
+        S* d_v = nullptr;
+        if (hipMalloc(&d_rp, (n + 1) * 4) != hipSuccess || hipMalloc(&d_ci, std::max<int64_t>(1, g->nnzK) * 4) != hipSuccess ||
+            hipMalloc(&d_v, std::max<int64_t>(1, g->nnzK) * sizeof(S)) != hipSuccess ||
+            hipMalloc(&d_dpos, n * 4) != hipSuccess || hipMalloc(&d_rows, n * 4) != hipSuccess ||
+            hipMalloc(&d_z, 4) != hipSuccess)
+            frc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) buffers");
+        zpiv = 0;
+        lu.assign(g->nnzK, s_zero<S>());
+        if (frc == EIGSOL_OK) {
+            hipMemcpyAsync(d_rp, mrp.data(), (n + 1) * 4, hipMemcpyHostToDevice, st);
+            hipMemcpyAsync(d_ci, mci.data(), g->nnzK * 4, hipMemcpyHostToDevice, st);
+            hipMemcpyAsync(d_v, mv.data(), g->nnzK * sizeof(S), hipMemcpyHostToDevice, st);
+            hipMemcpyAsync(d_dpos, dpos.data(), n * 4, hipMemcpyHostToDevice, st);
+            hipMemcpyAsync(d_rows, rows.data(), n * 4, hipMemcpyHostToDevice, st);
+            hipMemsetAsync(d_z, 0, 4, st);
+            for (size_t l = 0; l < lcount.size(); ++l) {
+                const int32_t cnt = lcount[l];
+                hipLaunchKernelGGL((dev::ilu0_level_kernel<S>), dim3((cnt + 255) / 256), dim3(256), 0, st, d_rp, d_ci,
+                                   d_dpos, d_v, d_rows + lstart[l], cnt, d_z);
+            }
+            hipMemcpyAsync(&zpiv, d_z, 4, hipMemcpyDeviceToHost, st);
+            hipMemcpyAsync(lu.data(), d_v, g->nnzK * sizeof(S), hipMemcpyDeviceToHost, st);
+            if (stream_wait(st) != hipSuccess) frc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) factorization");
+        }
+        for (void* p : {(void*)d_rp, (void*)d_ci, (void*)d_v, (void*)d_dpos, (void*)d_rows, (void*)d_z})
+            if (p) hipFree(p);
+        return frc;
+    };
+    if (rc == EIGSOL_OK) rc = factor();
+    if (rc == EIGSOL_OK && zpiv && g->complete) {
+        // the exact LU met a zero pivot: ILU(0) on M's own pattern (GMRES then iterates over it)
+        mrp.swap(orp);
+        mci.swap(oci);
+        mv.swap(ov);
+        dpos.swap(odpos);
+        g->complete = 0;
+        rc = factor();
     }
-    for (void* p : {(void*)d_rp, (void*)d_ci, (void*)d_v, (void*)d_dpos, (void*)d_rows, (void*)d_z})
-        if (p) hipFree(p);
+    std::vector<int32_t>().swap(orp);
+    std::vector<int32_t>().swap(oci);
+    std::vector<int32_t>().swap(odpos);
+    std::vector<S>().swap(ov);
     if (rc == EIGSOL_OK && zpiv)
         rc = fail(EIGSOL_E_SOLVER, g->complete ? "solve_shifted: sparse LU (complete fill, no pivoting) met a zero pivot"
                                                : "solve_shifted: ILU(0) factorization met a zero pivot");

@@ -220,22 +220,34 @@ __global__ __launch_bounds__(kT) void accum_kernel(int64_t n, T* __restrict__ y,
 // ------------------------------------------------------------------ Householder (QR method)
 // reflector of x = A(r0 : r0+m, col) (to_hessenberg.hpp:42-66, qr_decompose.hpp:51-74):
 // skip when ||x(1:)|| == 0 or ||v|| == 0; alpha = -sign ||x||, sign = x0 / |x0| (1 for x0 == 0),
-// v = (x - alpha e1) / ||x - alpha e1||
+// v = (x - alpha e1) / ||x - alpha e1||.  The column is scaled by the power of two 2^-e that brings
+// its largest entry to [1, 2) before any square is formed (exact, so inside the double range the
+// reflector is bitwise the unscaled one); v is scale-free, so entries near 1e+-170, whose squares
+// leave the double range but not the x87 long double's, still give the reference's reflector.
 template <class T>
 __global__ __launch_bounds__(1024) void hh_make_kernel(const T* A, int64_t ld, int64_t r0, int64_t col, int64_t m,
                                                        T* v, int* skip) {
     using O = wide_ops<T>;
     __shared__ dd sm[16];
     const T* x = A + r0 + col * ld;
+    double mx = 0.0;
+    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) mx = fmax(mx, O::maxabs(x[i]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6].hi = mx;
+    __syncthreads();
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) mx = fmax(mx, sm[w].hi);
+    __syncthreads();
+    const int e = (mx > 0.0 && mx <= 1.7976931348623157e308) ? ilogb(mx) : 0;
     dd t[1] = {dd{0.0, 0.0}};
-    for (int64_t i = 1 + threadIdx.x; i < m; i += blockDim.x) t[0] = dd_add(t[0], O::abs2(x[i]));
+    for (int64_t i = 1 + threadIdx.x; i < m; i += blockDim.x) t[0] = dd_add(t[0], O::abs2(O::ldexp(x[i], -e)));
     block_sum<1>(t, sm);
     const dd tail = t[0];
     if (tail.hi == 0.0) {
         if (threadIdx.x == 0) *skip = 1;
         return;
     }
-    const T x0 = x[0];
+    const T x0 = O::ldexp(x[0], -e);
     const dd nx = dd_sqrt(dd_add(tail, O::abs2(x0)));
     const T sign = O::is_zero(x0) ? O::one() : O::div_r(x0, O::abs(x0));
     const T v0 = O::add(x0, O::mul_r(sign, nx));   // x0 - alpha
@@ -244,7 +256,7 @@ __global__ __launch_bounds__(1024) void hh_make_kernel(const T* A, int64_t ld, i
         if (threadIdx.x == 0) *skip = 1;
         return;
     }
-    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) v[i] = O::div_r(i == 0 ? v0 : x[i], vn);
+    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) v[i] = O::div_r(i == 0 ? v0 : O::ldexp(x[i], -e), vn);
     if (threadIdx.x == 0) *skip = 0;
 }
 

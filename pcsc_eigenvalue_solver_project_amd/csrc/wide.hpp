@@ -128,10 +128,28 @@ EIGSOL_HD cdd cdd_mul(cdd a, cdd b) {
 EIGSOL_HD cdd cdd_mul_r(cdd a, dd r) { EIGSOL_EXACT return cdd{dd_mul(a.re, r), dd_mul(a.im, r)}; }
 EIGSOL_HD cdd cdd_div_r(cdd a, dd r) { EIGSOL_EXACT return cdd{dd_div(a.re, r), dd_div(a.im, r)}; }
 EIGSOL_HD dd cdd_abs2(cdd a) { EIGSOL_EXACT return dd_add(dd_mul(a.re, a.re), dd_mul(a.im, a.im)); }
-EIGSOL_HD dd cdd_abs(cdd a) { EIGSOL_EXACT return dd_sqrt(cdd_abs2(a)); }
-EIGSOL_HD cdd cdd_div(cdd a, cdd b) {   // a conj(b) / |b|^2
-    const dd d = cdd_abs2(b);
-    return cdd_div_r(cdd_mul(a, cdd_conj(b)), d);
+// exact scaling by 2^e (both parts; exact while lo stays a normal number)
+EIGSOL_HD dd dd_ldexp(dd a, int e) { EIGSOL_EXACT return dd{std::ldexp(a.hi, e), std::ldexp(a.lo, e)}; }
+EIGSOL_HD cdd cdd_ldexp(cdd a, int e) { EIGSOL_EXACT return cdd{dd_ldexp(a.re, e), dd_ldexp(a.im, e)}; }
+// exponent that brings max(|re|, |im|) to [1, 2); 0 for zero or non-finite values (left unscaled)
+EIGSOL_HD int cdd_scale_exp(cdd a) {
+    const double m = std::fmax(std::fabs(a.re.hi), std::fabs(a.im.hi));
+    return (m > 0.0 && m <= 1.7976931348623157e308) ? std::ilogb(m) : 0;
+}
+// |z| without forming |z|^2 at the input's scale: hypot-style, so |z| near 1e+-170 neither
+// overflows nor underflows (the x87 long double it stands for has a far wider exponent range)
+EIGSOL_HD dd cdd_abs(cdd a) {
+    EIGSOL_EXACT
+    const int e = cdd_scale_exp(a);
+    return dd_ldexp(dd_sqrt(cdd_abs2(cdd_ldexp(a, -e))), e);
+}
+// a / b = a conj(b') / |b'|^2 * 2^-e with b' = b 2^-e of modulus ~1 (scaled division)
+EIGSOL_HD cdd cdd_div(cdd a, cdd b) {
+    EIGSOL_EXACT
+    const int e = cdd_scale_exp(b);
+    const cdd bs = cdd_ldexp(b, -e);
+    const dd d = cdd_abs2(bs);
+    return cdd_ldexp(cdd_div_r(cdd_mul(a, cdd_conj(bs)), d), -e);
 }
 EIGSOL_HD bool cdd_is_zero(cdd a) { EIGSOL_EXACT return a.re.hi == 0.0 && a.im.hi == 0.0; }
 
@@ -156,6 +174,8 @@ template <> struct wide_ops<dd> {
     EIGSOL_HD static dd imag(dd) { EIGSOL_EXACT return dd{0.0, 0.0}; }
     EIGSOL_HD static dd make(dd re, dd) { EIGSOL_EXACT return re; }
     EIGSOL_HD static double hi(dd a) { EIGSOL_EXACT return a.hi; }
+    EIGSOL_HD static dd ldexp(dd a, int e) { EIGSOL_EXACT return dd_ldexp(a, e); }
+    EIGSOL_HD static double maxabs(dd a) { return std::fabs(a.hi); }
 };
 template <> struct wide_ops<cdd> {
     static constexpr bool complex = true;
@@ -176,6 +196,8 @@ template <> struct wide_ops<cdd> {
     EIGSOL_HD static dd imag(cdd a) { EIGSOL_EXACT return a.im; }
     EIGSOL_HD static cdd make(dd re, dd im) { EIGSOL_EXACT return cdd{re, im}; }
     EIGSOL_HD static double hi(cdd a) { EIGSOL_EXACT return a.re.hi; }
+    EIGSOL_HD static cdd ldexp(cdd a, int e) { EIGSOL_EXACT return cdd_ldexp(a, e); }
+    EIGSOL_HD static double maxabs(cdd a) { return std::fmax(std::fabs(a.re.hi), std::fabs(a.im.hi)); }
 };
 
 }  // namespace eigsol

@@ -63,6 +63,34 @@ def test_config4_band10m_spmv_bitwise_and_power(ctx):
     A.close()
 
 
+@pytest.mark.timeout(600)
+def test_config4_uniform10m_binned_bitwise_and_power(ctx):
+    """Config 4's uniform-column form at full size (10M x 10M, 10 uniform columns per row): the
+    shipped default layout is the column-binned kernel with 153 KB of row sums per workgroup
+    (csr_bin_kernel<double, true, 153, 1024>), which this matrix selects on its own (row sums
+    80 MB > 64 MB).  One fused product bitwise equal to the oracle's CSC scatter (the reference's
+    order, power_method.hpp:69,81) and the power iteration's lambda / iterations / eigenvector
+    parity with the oracle's reference loop."""
+    n = 10_000_000
+    rp, ci, v = S.uniform(n, 10)
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    s = E.PowerSession(A)
+    info, kname = s.kernel_info(), s.kernel_name()
+    s.close()
+    assert info["variant"] == 10 and "csr_bin_kernel<double, true, 153, 1024>" in kname, (info, kname)
+    x = S.start_vector(n)
+    y = _spmv_gpu(ctx, A, x)
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    del rp, ci, v
+    assert np.array_equal(y, O.spmv_csc(cp, ri, vv, x, n))
+    del y
+    res = E.power_method(A, E.SolverOptions(100, 1e-10), x)
+    ref = O.power_csc(cp, ri, vv, x, 100, 1e-10, want_trace=True)
+    assert ref["converged"]
+    _power_parity(res, ref, 1e-10)
+    A.close()
+
+
 def test_config3_uniform1m_power(ctx):
     n = 1_000_000
     rp, ci, v = S.uniform(n, 16)

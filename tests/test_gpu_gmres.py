@@ -169,6 +169,45 @@ def _small_pivot_matrix(n, sigma, pivot, seed):
     return M
 
 
+def test_exact_lu_zero_pivot_retries_ilu0(ctx, gmres_env, monkeypatch):
+    """A − σI whose leading 3 × 3 minors are singular in every 4 × 4 diagonal block, while the blocks
+    themselves are not: the exact LU without pivoting meets u_22 = 0 (the fill u_12 = −1 cancels
+    a_22 − σ = −1), whereas ILU(0) drops that fill and keeps every pivot nonzero (u_22 = −1,
+    u_33 = 3.5).  Above the densify threshold with the dense fallback disabled, the factor must
+    retry ILU(0) on M's own pattern (variant 7) and GMRES must still solve to 1e-10 ||b|| and drive
+    the shifted inverse iteration to the block's exact eigenvalue."""
+    monkeypatch.setenv("EIGSOL_GMRES_FALLBACK", "0")
+    nb = 6000
+    n = 4 * nb                                   # > 16384: no densified LU either
+    sigma = 0.25
+    M1 = np.array([[1, 0, 1, 0], [1, 1, 0, 0], [0, 1, -1, 1], [0, 0, 0.5, 3]], float)
+    scale = np.r_[1.0, 4.0 + np.random.default_rng(3).random(nb - 1)]   # block 0: the smallest |λ(M)|
+    A = sp.block_diag([s * M1 for s in scale], format="csr") + sigma * sp.identity(n, format="csr")
+    A = sp.csr_matrix(A)
+    A.eliminate_zeros()
+    A.sort_indices()
+    D = E.CsrMatrix.from_scipy(ctx, A)
+    b = np.random.default_rng(4).standard_normal(n)
+    y = E.solve_shifted(D, sigma, b)
+    assert np.linalg.norm(A @ y - sigma * y - b) <= 1e-10 * np.linalg.norm(b)
+    s = E.ShiftedSession(D, sigma)
+    s.begin(E.ShiftedSolverOptions(200, 1e-12, sigma), S.start_vector(n))
+    done = False
+    while not done:
+        s.step(1)
+        done, _ = s.query()
+    info = s.kernel_info()
+    r = s.finish()
+    s.close()
+    assert info["variant"] == 7, info            # ILU(0) after the exact LU's zero pivot
+    ev = np.linalg.eigvals(M1)
+    exact = sigma + ev[np.argmin(np.abs(ev))].real
+    assert r.converged and abs(r.eigenvalue - exact) <= 1e-9, (r.eigenvalue, exact)
+    x = r.eigenvector
+    assert np.linalg.norm(A @ x - r.eigenvalue * x) <= 1e-8 * np.linalg.norm(x)
+    D.close()
+
+
 @pytest.mark.parametrize("pivot", [1e-9, 0.0])
 def test_exact_lu_small_and_zero_pivots(ctx, gmres_env, pivot):
     """No-pivot LU over the filled pattern (variant 18) when its pivots are tiny: the direct solve is

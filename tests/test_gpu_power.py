@@ -444,6 +444,63 @@ def test_column_binned_gather_bitwise_and_power(ctx, dtype, monkeypatch):
         _assert_power_parity(res, ref, tol)
     A.close()
     # rectangular product (2n columns): rows chunked by n, columns blocked over 2n
+    _rect_binned(ctx, dtype, n)
+
+
+@pytest.mark.parametrize("lds", [64, 128, 153])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_column_binned_lds_instantiations(ctx, dtype, lds, monkeypatch):
+    """The large-LDS instantiations of csr_bin_kernel (64 / 128 / 153 KB of row sums per workgroup,
+    the last one the default for matrices whose row sums exceed 64 MB, i.e. config 4's
+    uniform10m) forced on a small matrix with balanced chunks (chunk rows chosen so the chunk
+    count is a multiple of the grid), an empty row range, a 3000-entry row and a row longer than
+    one x block: bitwise the reference's CSC scatter (power_method.hpp:69,81) and power parity."""
+    monkeypatch.setenv("EIGSOL_CSR_BIN", "2")
+    monkeypatch.setenv("EIGSOL_CSR_BIN_LDS", str(lds))
+    monkeypatch.setenv("EIGSOL_CSR_BIN_BALANCE", "1")
+    monkeypatch.setenv("EIGSOL_CSR_BIN_BYTES", str(256 * 1024))
+    n = 400_000
+    rp, ci, v = S.uniform(n, 10, seed=5)
+    rows = [ci[rp[i]:rp[i + 1]] for i in range(n)]
+    vals = [v[rp[i]:rp[i + 1]] for i in range(n)]
+    rng = np.random.default_rng(17)
+    rows[3] = np.sort(rng.choice(n, 3000, replace=False)).astype(np.int32)
+    vals[3] = rng.uniform(0, 1, 3000)
+    rows[n - 1] = np.arange(0, n, 40, dtype=np.int32)         # spans every x block
+    vals[n - 1] = rng.uniform(0, 1, len(rows[n - 1]))
+    for i in range(5000, 5100):
+        rows[i] = rows[i][:0]
+        vals[i] = vals[i][:0]
+    lens = np.array([len(r) for r in rows], dtype=np.int64)
+    rp = np.zeros(n + 1, dtype=np.int32)
+    np.cumsum(lens, out=rp[1:])
+    ci = np.concatenate(rows).astype(np.int32)
+    v = np.concatenate(vals).astype(dtype)
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    s = E.PowerSession(A)
+    info = s.kernel_info()
+    kname = s.kernel_name()
+    s.close()
+    assert info["variant"] == 10, info
+    assert f", {lds}, " in kname, kname
+    x = S.start_vector(n, dtype)
+    y = _spmv_gpu(ctx, A, x)
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    assert np.array_equal(y, O.spmv_csc(cp, ri, vv, x, n))
+    single = dtype == np.float32
+    tol = 1e-5 if single else 1e-12
+    res = E.power_method(A, E.SolverOptions(1000, tol), x)
+    ref = O.power_csc(cp, ri, vv, x, 1000, tol, want_trace=True)
+    assert ref["converged"]
+    if single:
+        assert abs(res.eigenvalue - ref["eigenvalue"]) <= 1e-5 * (1 + abs(ref["eigenvalue"]))
+        assert abs(res.iterations - ref["iterations"]) <= 1
+    else:
+        _assert_power_parity(res, ref, tol)
+    A.close()
+
+
+def _rect_binned(ctx, dtype, n):
     rp2, ci2, v2 = S.uniform(n, 12, seed=3)
     ci2 = (ci2.astype(np.int64) * 2 + (np.arange(len(ci2)) & 1)).astype(np.int32)
     v2 = v2.astype(dtype)

@@ -472,3 +472,45 @@ def test_multi_launches_large_per_solve_growth(ctx, monkeypatch, dtype):
     x = res.eigenvector.astype(np.complex128)
     assert np.all(np.isfinite(x)) and abs(np.linalg.norm(x) - 1) <= 1e-5
     assert abs(np.vdot(x, ref["eigenvector"].astype(np.complex128))) >= 1 - 1e-5
+
+
+@pytest.mark.parametrize("K", [1, 2])
+def test_chunk_two_entries_per_lane_bitwise(ctx, monkeypatch, K):
+    """Tail rows longer than 16 entries select the chunk kernel that polls each lane's second entry
+    together with the first (sptrsv_chunk_kernel<S, kIter, true>, chosen automatically).
+    Forced on (EIGSOL_TRSV_TWO=1) and off (=0) on one triangular factor with 28-entry rows: the
+    single-solve instantiation (solve_shifted) gives bitwise-equal solutions and the iterative one
+    (one iteration per launch, K = 1) bitwise-equal lambda traces, iteration counts and
+    eigenvectors — the per-lane summation order is the same (entries lane, lane + 16, lane + 32,
+    ...), only the dependency polls move.  K = 2 runs the multi-solve role kernel, which has no
+    two-entry form: the setting must not change it either."""
+    n = 60000
+    rp, ci, v, _ = S.triu_complex(n, 28, seed=9)
+    target = 1.5 * np.exp(0.7j)
+    sigma = target + 1e-3
+    x0 = S.start_vector(n, np.complex128, seed=5)
+    b = S.start_vector(n, np.complex128, seed=6)
+    monkeypatch.setenv("EIGSOL_TRSV_MULTI", str(K))
+    monkeypatch.setenv("EIGSOL_TRSV_TAIL", "chunk")
+    out = {}
+    for two in ("0", "1"):
+        monkeypatch.setenv("EIGSOL_TRSV_TWO", two)
+        M = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+        y = E.solve_shifted(M, sigma, b)
+        sess = E.ShiftedSession(M, sigma, trace_capacity=128)
+        sess.begin(E.ShiftedSolverOptions(100, 1e-12, sigma), x0)
+        sess.step(120)
+        assert sess.query()[0]
+        r = sess.finish()
+        tr = sess.trace(128)
+        sess.close()
+        M.close()
+        out[two] = (y, r, tr)
+    (y0, r0, t0), (y1, r1, t1) = out["0"], out["1"]
+    Msp = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    assert np.linalg.norm(Msp @ y1 - sigma * y1 - b) <= 1e-10 * np.linalg.norm(b)
+    assert np.array_equal(y0, y1)
+    assert r0.converged and r1.converged and r0.iterations == r1.iterations
+    assert np.array_equal(t0, t1) and r0.eigenvalue == r1.eigenvalue
+    assert np.array_equal(r0.eigenvector, r1.eigenvector)
+    assert abs(r1.eigenvalue - target) <= 1e-10

@@ -318,6 +318,27 @@ def test_wide_hessenberg_and_qr_decompose(ctx):
     assert float(np.max(np.abs(Hc - O.hessenberg(Ac[:30, :30])))) <= 1e-16 * nc
 
 
+@pytest.mark.parametrize("scale", [1e-170, 1e170])
+def test_wide_hessenberg_qr_extreme_scales(ctx, scale):
+    """Entries near 1e+-170, whose squares leave the double range (the x87 long double's does not):
+    the reflector's norms and the complex modulus / division are formed on a power-of-two-scaled
+    column (exact), so Hessenberg and QR decomposition stay within 1e-16 ||A||_F of the x87 oracle
+    at that scale, with no overflow, underflow or NaN."""
+    rng = np.random.default_rng(77)
+    s = LD(scale)
+    for dt in (LD, CLD):
+        base = rng.standard_normal((24, 24)) + (1j * rng.standard_normal((24, 24)) if dt == CLD else 0)
+        A = (_wide(base, dt, seed=78) * s).astype(dt)
+        nrm = float(np.linalg.norm(base)) * scale
+        H = E.to_hessenberg(ctx, A)
+        assert np.all(np.isfinite(H.astype(np.complex128 if dt == CLD else np.float64) / scale))
+        assert float(np.max(np.abs(H - O.hessenberg(A)))) <= 1e-16 * nrm
+        Q, R = E.qr_decompose(ctx, A[:, :16].copy())
+        Qr, Rr = O.qr_decompose(A[:, :16].copy())
+        assert float(np.max(np.abs(Q - Qr))) <= 1e-16
+        assert float(np.max(np.abs(R - Rr))) <= 1e-16 * nrm
+
+
 def test_wide_qr_eigenvalues_reference_iteration(ctx):
     """qr_eigenvalues<long double>: the reference's unshifted iteration (qr_eigenvalues.hpp:62-105)
     with its iteration counts; the Francis variant is refused at the C ABI (fp64 kernels) and the

@@ -1,0 +1,45 @@
+"""CPU: the double-double wire format of long double / std::complex<long double> (to_wire /
+from_wire, the C ABI's EIGSOL_DD / EIGSOL_CDD layout).  Exact for x87 values whose low part is a
+double above the subnormal grid; below ~2^-1010 (1e-304) it is not, the pair is the nearest double-double and
+a RuntimeWarning says so."""
+import warnings
+
+import numpy as np
+import pytest
+
+import pcsc_eigenvalue_solver_project_amd as E
+
+LD, CLD = np.longdouble, np.clongdouble
+x87 = np.finfo(LD).nmant == 63
+
+
+@pytest.mark.skipif(not x87, reason="long double is not the x87 format here")
+@pytest.mark.parametrize("scale", [1.0, 1e-250, 1e250, 1e-300])
+def test_round_trip_exact_in_normal_range(scale):
+    rng = np.random.default_rng(1)
+    x = (rng.uniform(-1, 1, 500).astype(LD) * (LD(1) + LD(2) ** -60)) * LD(scale)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        w = E.to_wire(x, LD)
+    assert np.all(E.from_wire(w, LD) == x)
+    z = np.empty(500, CLD)
+    z.real, z.imag = x, -x
+    assert np.all(E.from_wire(E.to_wire(z, CLD), CLD) == z)
+
+
+@pytest.mark.skipif(not x87, reason="long double is not the x87 format here")
+def test_round_trip_near_1e_minus_306_warns_and_is_nearest():
+    x = (np.linspace(1, 2, 101).astype(LD) * (LD(1) + LD(2) ** -62)) * LD(1e-306)
+    with pytest.warns(RuntimeWarning, match="subnormal grid"):
+        w = E.to_wire(x, LD)
+    back = E.from_wire(w, LD)
+    # the only loss is the low part's rounding to the subnormal grid (2^-1074)
+    assert float(np.max(np.abs(back - x))) <= 2.0 ** -1074
+    assert np.any(back != x)
+
+
+def test_out_of_range_refused():
+    if not x87:
+        pytest.skip("long double is not the x87 format here")
+    with pytest.raises(E.EigSolError):
+        E.to_wire(np.array([LD(10) ** 400], LD), LD)
