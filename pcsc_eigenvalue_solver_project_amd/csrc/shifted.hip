@@ -1520,6 +1520,220 @@ __global__ void shift_diag_kernel(S* a, int64_t n, S sigma) {
     if (i < n) a[i * n + i] = sub(a[i * n + i], sigma);
 }
 
+// ---- on-device analysis of a triangular CSR (factor_tri_device): the same level order and the same
+// position-indexed chunk layout the host build produces, without moving the matrix off the device.
+
+// Per row: pivot d_i - sigma (the diagonal entries summed in stored order, 0 where there is none),
+// off-diagonal count, and the triangularity / zero-pivot flags (flags[0]: an entry left of the
+// diagonal, [1]: right of it, [2]: a zero pivot), one atomic per wave.
+template <class S>
+__global__ __launch_bounds__(256) void tri_rows_kernel(const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                       const S* __restrict__ val, int64_t n, S sig,
+                                                       S* __restrict__ pv, int32_t* __restrict__ offlen,
+                                                       int32_t* __restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool lo = false, hi = false, zp = false;
+    if (i < n) {
+        S d = s_zero<S>();
+        int32_t off = 0;
+        for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+            const int32_t c = ci[e];
+            if (c == i) d = add(d, val[e]);
+            else {
+                ++off;
+                lo |= c < i;
+                hi |= c > i;
+            }
+        }
+        const S p = sub(d, sig);
+        pv[i] = p;
+        offlen[i] = off;
+        if constexpr (std::is_same_v<S, double> || std::is_same_v<S, float>) zp = p == 0;
+        else zp = p.re == 0 && p.im == 0;
+    }
+    const uint64_t bl = __ballot(lo), bh = __ballot(hi), bz = __ballot(zp);
+    if ((threadIdx.x & 63) == 0) {
+        if (bl) atomicOr(flags + 0, 1);
+        if (bh) atomicOr(flags + 1, 1);
+        if (bz) atomicOr(flags + 2, 1);
+    }
+}
+
+// Dependency levels, sync-free: level(i) = 1 + max level of the rows row i reads (0 for none).
+// Rows are claimed in dependency order through a ticket (upper: row n-1 first), four rows per wave
+// (16 lanes per row); a row's dependencies always hold smaller tickets, claimed by waves that are
+// already running, so every wait ends.  A wave re-polls its unfinished rows' dependencies
+// (agent-scope loads, -1 = not yet known) and publishes a row as soon as all of them are known,
+// inside the loop (a divergent group must never wait on a row its own wave publishes after the
+// loop).  Per level: row count and longest row (atomics); maxlev = the deepest level.  A wait past
+// ~2 s of the 100 MHz constant clock sets err and publishes level 0, so a broken analysis ends
+// (the host then builds on the CPU).
+__global__ __launch_bounds__(256) void tri_level_kernel(const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                        const int32_t* __restrict__ offlen, int64_t n, int upper,
+                                                        int32_t* lev, uint32_t* ticket, int32_t* lcnt,
+                                                        int32_t* lmax, int32_t* maxlev, int32_t* err) {
+    const int lane = threadIdx.x & (kRowLanes - 1);
+    const int grp = (threadIdx.x & 63) / kRowLanes;
+    for (;;) {
+        uint32_t t0 = 0;
+        if ((threadIdx.x & 63) == 0) t0 = atomicAdd(ticket, (uint32_t)kWaveRows);
+        t0 = __shfl(t0, 0, 64);
+        if ((int64_t)t0 >= n) return;
+        const int64_t t = (int64_t)t0 + grp;
+        const bool live = t < n;
+        const int64_t i = live ? (upper ? n - 1 - t : t) : 0;
+        const int32_t e0 = live ? rp[i] : 0, e1 = live ? rp[i + 1] : 0;
+        bool done = !live;
+        const long long t_start = wall_clock64();
+        for (;;) {
+            int32_t m = -1;
+            bool ready = true;
+            if (!done)
+                for (int32_t e = e0 + lane; e < e1; e += kRowLanes) {
+                    const int32_t c = ci[e];
+                    if (c == i) continue;
+                    const int32_t l = __hip_atomic_load(lev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (l < 0) ready = false;
+                    m = max(m, l);
+                }
+            // the row's 16 lanes: all ready (ballot), and the largest dependency level (every lane
+            // shuffles: a shuffle under a divergent mask would read inactive lanes' stale registers)
+#pragma unroll
+            for (int off = kRowLanes / 2; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off, 64));
+            const uint64_t unready = __ballot(!ready);
+            ready = ((unready >> (grp * kRowLanes)) & ((1ull << kRowLanes) - 1)) == 0;
+            bool timeout = false;
+            if (!done && !ready && wall_clock64() - t_start > 200000000ll) {
+                timeout = true;
+                ready = true;
+                m = -1;
+            }
+            if (!done && ready) {
+                if (lane == 0) {
+                    if (timeout) atomicOr(err, 1);
+                    const int32_t l = m + 1;
+                    __hip_atomic_store(lev + i, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    atomicAdd(lcnt + l, 1);
+                    atomicMax(lmax + l, offlen[i]);
+                    atomicMax(maxlev, l);
+                }
+                done = true;
+            }
+            if (__ballot(!done) == 0) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+// position -> row: the rows sorted by level (stable: ascending row inside a level) placed at their
+// level's padded start; padding positions stay -1
+__global__ __launch_bounds__(256) void tri_order_kernel(const int32_t* __restrict__ lev_sorted,
+                                                        const int32_t* __restrict__ rows_sorted, int64_t n,
+                                                        const int32_t* __restrict__ ustart,
+                                                        const int32_t* __restrict__ pstart, int32_t* __restrict__ order) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    const int32_t l = lev_sorted[k];
+    order[pstart[l] + (k - ustart[l])] = rows_sorted[k];
+}
+
+// per position: its row's off-diagonal count (plen[npos] = 0 closes the scan) and its pivot
+template <class S>
+__global__ __launch_bounds__(256) void tri_poslen_kernel(const int32_t* __restrict__ order, int64_t npos,
+                                                         const int32_t* __restrict__ offlen, const S* __restrict__ pv,
+                                                         S one, int32_t* __restrict__ plen, S* __restrict__ ppiv) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p > npos) return;
+    if (p == npos) {
+        plen[p] = 0;
+        return;
+    }
+    const int32_t i = order[p];
+    plen[p] = i >= 0 ? offlen[i] : 0;
+    ppiv[p] = i >= 0 ? pv[i] : one;
+}
+
+// the position-ordered off-diagonal CSR: 16 lanes per position copy its row's entries (diagonal
+// skipped, stored order kept) to pptr[p]
+template <class S>
+__global__ __launch_bounds__(256) void tri_gather_kernel(const int32_t* __restrict__ order, int64_t npos,
+                                                         const int32_t* __restrict__ pptr,
+                                                         const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                         const S* __restrict__ val, const int32_t* __restrict__ offlen,
+                                                         int32_t* __restrict__ pcol, S* __restrict__ pval) {
+    const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kRowLanes;
+    const int lane = threadIdx.x & (kRowLanes - 1);
+    if (p >= npos) return;
+    const int32_t i = order[p];
+    if (i < 0) return;
+    const int32_t e0 = rp[i], len = rp[i + 1] - e0, nd = len - offlen[i], base = pptr[p];
+    for (int32_t k = lane; k < len; k += kRowLanes) {
+        const int32_t c = ci[e0 + k];
+        if (c == i) continue;
+        const int32_t o = base + (c < i ? k : k - nd);
+        pcol[o] = c;
+        pval[o] = val[e0 + k];
+    }
+}
+
+// head rows: row -> head position (their columns become LDS positions)
+__global__ __launch_bounds__(256) void tri_rowpos_kernel(const int32_t* __restrict__ order, int32_t hpos,
+                                                         int32_t* __restrict__ rowpos) {
+    const int32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= hpos) return;
+    const int32_t i = order[p];
+    if (i >= 0) rowpos[i] = p;
+}
+
+// 1 / pivot as the host build forms it (complex: in double, no contraction), for bitwise-equal heads
+__device__ __forceinline__ double head_recip(double p) { return 1.0 / p; }
+__device__ __forceinline__ float head_recip(float p) { return 1.0f / p; }
+__device__ __forceinline__ cplx head_recip(cplx p) {
+#pragma clang fp contract(off)
+    const double d = p.re * p.re + p.im * p.im;
+    return cplx{p.re / d, -p.im / d};
+}
+__device__ __forceinline__ cplxf head_recip(cplxf p) {
+#pragma clang fp contract(off)
+    const double re = p.re, im = p.im;
+    const double d = re * re + im * im;
+    return cplxf{(float)(re / d), (float)(-im / d)};
+}
+
+// one-wave head, pass-major (see sptrsv_whead_kernel): thread (q, u) fills row u of pass q; the
+// arrays arrive pre-filled with the padding (values 0, columns hpos, pivots 1, targets -1)
+template <class S>
+__global__ __launch_bounds__(256) void tri_whead_kernel(const int2* __restrict__ ptab, int32_t nreal,
+                                                        const int32_t* __restrict__ order, const int32_t* __restrict__ rp,
+                                                        const int32_t* __restrict__ ci, const S* __restrict__ val,
+                                                        const S* __restrict__ pv, const int32_t* __restrict__ rowpos,
+                                                        S* __restrict__ wval, int32_t* __restrict__ wcol,
+                                                        S* __restrict__ wrp, int32_t* __restrict__ wdst) {
+    const int32_t g = blockIdx.x * 256 + threadIdx.x;
+    const int32_t q = g / kWHeadRows, u = g % kWHeadRows;
+    if (q >= nreal) return;
+    const int2 pt = ptab[q];   // {first position, rows}
+    if (u >= pt.y) return;
+    const int32_t p = pt.x + u;
+    const int32_t i = order[p];
+    wrp[(size_t)q * kWHeadRows + u] = head_recip(pv[i]);
+    wdst[(size_t)q * kWHeadRows + u] = p;
+    int32_t idx = 0;
+    for (int32_t e = rp[i]; e < rp[i + 1]; ++e) {
+        const int32_t c = ci[e];
+        if (c == i) continue;
+        const size_t slot = ((size_t)q * 4 + (size_t)(idx % 4)) * 64 + (size_t)(4 * u + idx / 4);
+        wcol[slot] = rowpos[c];
+        wval[slot] = val[e];
+        ++idx;
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void fill_kernel(T* __restrict__ a, int64_t n, T v) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) a[k] = v;
+}
+
 }  // namespace dev
 
 // ================================================================== host side
@@ -1868,9 +2082,19 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
                            ShiftFactor** out);
 
 template <class S>
+static int factor_tri_device(eigsol_csr* A, double sre, double sim, ShiftFactor** out, bool& declined);
+
+template <class S>
 static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out) {
     hipStream_t st = A->ctx->stream;
     const int64_t n = A->nrows, nnz = A->nnz;
+    // triangular matrices: analysis and layout on the device (EIGSOL_TRSV_HOST=1: the host build)
+    const char* host_env = std::getenv("EIGSOL_TRSV_HOST");
+    if (n > 0 && !(host_env && std::atoi(host_env))) {
+        bool declined = false;
+        const int rc = factor_tri_device<S>(A, sre, sim, out, declined);
+        if (!declined) return rc;
+    }
     std::vector<int32_t> rp(n + 1), ci(nnz);
     std::vector<S> v(nnz);
     EIGSOL_HIP(hipMemcpyAsync(rp.data(), A->rowptr, (n + 1) * 4, hipMemcpyDeviceToHost, st));
@@ -1947,6 +2171,97 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         return EIGSOL_OK;
         }
     }
+}
+
+template <class S>
+static void tri_dump(const ShiftFactor* f);
+
+static int dev_upload(hipStream_t st, void** dst, const void* src, size_t bytes) {
+    EIGSOL_HIP(hipMalloc(dst, std::max<size_t>(bytes, 16)));
+    if (bytes && src) EIGSOL_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, st));
+    return EIGSOL_OK;
+}
+
+// Launch geometry of a level-ordered triangular factor (host- or device-built): the tail grid (one
+// residency round, cooperative launch), the multi-solve set-up and the partials grid.  Needs the
+// layout fields (tail variant, chunk_two, slice_b, head, chunks / slices) already set.
+template <class S>
+static int tri_launch_setup(ShiftFactor* f) {
+    int rc = EIGSOL_OK;
+    // tail grid: one residency round (cooperative launch), capped at EIGSOL_TRSV_BLOCKS_PER_CU
+    // blocks per CU and by the work
+    {
+        int per_cu_max = 0;
+        const void* tk = f->tail_chunks ? (f->chunk_two ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true, true>)
+                                                        : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>))
+                                        : slice_kernel_ptr<S>(f->slice_b, true);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_max, tk, dev::kThreads, 0) != hipSuccess ||
+            per_cu_max < 1)
+            rc = fail(EIGSOL_E_HIP, "triangular solve: occupancy query");
+        f->grid = per_cu_max * f->ctx->num_cus;
+    }
+    int per_cu = 2;
+    if (const char* env = std::getenv("EIGSOL_TRSV_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(env));
+    f->grid = std::min(f->grid, per_cu * f->ctx->num_cus);
+    const int64_t units = f->tail_chunks ? (int64_t)f->nchunks - f->chunk0 : f->nslices;
+    f->grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid, (units + dev::kWaves - 1) / dev::kWaves));
+    // multi-solve launches: chunk tail with the one-wave head (or none), K solves per launch
+    // (EIGSOL_TRSV_MULTI=K, 1..4; 1 = one iteration per launch) on K copies of the grid at one
+    // workgroup per CU per solve (EIGSOL_TRSV_MULTI_BLOCKS_PER_CU), when they are co-resident
+    if (rc == EIGSOL_OK && f->tail_chunks && (f->hpos == 0 || f->wave_head)) {
+        const char* e = std::getenv("EIGSOL_TRSV_MULTI");
+        const int want = std::max(1, std::min(dev::kMaxMulti, e ? std::atoi(e) : kMultiDefault));
+        int per_cu_role = 0;
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu_role, reinterpret_cast<const void*>(dev::sptrsv_chunk_role_kernel<S>), dev::kThreads, 0);
+        int role_per_cu = 1;
+        if (const char* env = std::getenv("EIGSOL_TRSV_MULTI_BLOCKS_PER_CU")) role_per_cu = std::max(1, std::atoi(env));
+        const int gr = std::min(f->grid, role_per_cu * f->ctx->num_cus);
+        int K = want;
+        while (K > 1 && per_cu_role * f->ctx->num_cus < K * gr) --K;
+        if (K > 1) {
+            f->multi = K;
+            f->grid_multi = K * gr;
+            const char* hc = std::getenv("EIGSOL_TRSV_MULTI_HEAD");   // seq: the head solves one after another
+            // the dynamic LDS of the concurrent head shares the CU's 160 KiB with the kernel's static
+            // __shared__ state (its prologue record)
+            hipFuncAttributes fa{};
+            size_t static_lds = 256;
+            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, true, true>)) ==
+                hipSuccess)
+                static_lds = fa.sharedSizeBytes;
+            f->hconc = (!(hc && !std::strcmp(hc, "seq")) &&
+                        (size_t)K * (size_t)(f->hpos + 1) * sizeof(S) + 16 + static_lds <= (size_t)160 * 1024) ? 1 : 0;
+        }
+    }
+    int64_t red_cap = 1024;   // EIGSOL_TRSV_PART_GRID: A/B of the partials kernels' grid
+    if (const char* e = std::getenv("EIGSOL_TRSV_PART_GRID")) red_cap = std::max<int64_t>(8, std::atoll(e));
+    // never above grid * kWaves: wave_part (below) holds that many block partials
+    f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
+                                                                  std::min<int64_t>(red_cap, (f->n + 1023) / 1024)));
+    return rc;
+}
+
+// Solve state of a triangular factor: the two polled value buffers (every row unsolved: the
+// sentinel; the zero slot z[n] stays 0 for good), the ticket / error words and the wave partials.
+template <class S>
+static int tri_state_alloc(ShiftFactor* f) {
+    hipStream_t st = f->ctx->stream;
+    const int64_t n = f->n;
+    EIGSOL_TRY(dev_upload(st, &f->z[0], nullptr, (n + 1) * sizeof(S)));
+    EIGSOL_TRY(dev_upload(st, &f->z[1], nullptr, (n + 1) * sizeof(S)));
+    EIGSOL_TRY(dev_upload(st, (void**)&f->work, nullptr, 64));
+    EIGSOL_TRY(dev_upload(st, (void**)&f->err, nullptr, 64));
+    EIGSOL_TRY(dev_upload(st, &f->wave_part, nullptr, (size_t)f->grid * dev::kWaves * sizeof(dev::part4)));
+    const uint32_t sent = (uint32_t)(dev::kSent & 0xffffffffu);
+    for (void* zb : f->z) {
+        hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st);
+        hipMemsetAsync(static_cast<char*>(zb) + n * sizeof(S), 0, sizeof(S), st);
+    }
+    hipMemsetAsync(f->work, 0, 64, st);
+    hipMemsetAsync(f->err, 0, 64, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(EIGSOL_E_HIP, "factor upload");
+    return EIGSOL_OK;
 }
 
 // Triangular CSR (host arrays, columns ascending per row) -> level-ordered factor of A - sigma I.
@@ -2181,62 +2496,8 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
     }
     std::vector<int32_t>().swap(oci);
     std::vector<S>().swap(ov);
-    auto up_ = [&](void** dst, const void* src, size_t bytes) -> int {
-        EIGSOL_HIP(hipMalloc(dst, std::max<size_t>(bytes, 16)));
-        if (bytes && src) EIGSOL_HIP(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, st));
-        return EIGSOL_OK;
-    };
-    // tail grid: one residency round (cooperative launch), capped at EIGSOL_TRSV_BLOCKS_PER_CU
-    // blocks per CU and by the work
-    if (rc == EIGSOL_OK) {
-        int per_cu_max = 0;
-        const void* tk = f->tail_chunks ? (f->chunk_two ? reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true, true>)
-                                                        : reinterpret_cast<const void*>(dev::sptrsv_chunk_kernel<S, true>))
-                                        : slice_kernel_ptr<S>(Bs, true);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_max, tk, dev::kThreads, 0) != hipSuccess ||
-            per_cu_max < 1)
-            rc = fail(EIGSOL_E_HIP, "triangular solve: occupancy query");
-        f->grid = per_cu_max * f->ctx->num_cus;
-    }
-    int per_cu = 2;
-    if (const char* env = std::getenv("EIGSOL_TRSV_BLOCKS_PER_CU")) per_cu = std::max(1, std::atoi(env));
-    f->grid = std::min(f->grid, per_cu * f->ctx->num_cus);
-    const int64_t units = f->tail_chunks ? (int64_t)f->nchunks - f->chunk0 : f->nslices;
-    f->grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid, (units + dev::kWaves - 1) / dev::kWaves));
-    // multi-solve launches: chunk tail with the one-wave head (or none), K solves per launch
-    // (EIGSOL_TRSV_MULTI=K, 1..4; 1 = one iteration per launch) on K copies of the grid at one
-    // workgroup per CU per solve (EIGSOL_TRSV_MULTI_BLOCKS_PER_CU), when they are co-resident
-    if (rc == EIGSOL_OK && f->tail_chunks && (f->hpos == 0 || f->wave_head)) {
-        const char* e = std::getenv("EIGSOL_TRSV_MULTI");
-        const int want = std::max(1, std::min(dev::kMaxMulti, e ? std::atoi(e) : kMultiDefault));
-        int per_cu_role = 0;
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu_role, reinterpret_cast<const void*>(dev::sptrsv_chunk_role_kernel<S>), dev::kThreads, 0);
-        int role_per_cu = 1;
-        if (const char* env = std::getenv("EIGSOL_TRSV_MULTI_BLOCKS_PER_CU")) role_per_cu = std::max(1, std::atoi(env));
-        const int gr = std::min(f->grid, role_per_cu * f->ctx->num_cus);
-        int K = want;
-        while (K > 1 && per_cu_role * f->ctx->num_cus < K * gr) --K;
-        if (K > 1) {
-            f->multi = K;
-            f->grid_multi = K * gr;
-            const char* hc = std::getenv("EIGSOL_TRSV_MULTI_HEAD");   // seq: the head solves one after another
-            // the dynamic LDS of the concurrent head shares the CU's 160 KiB with the kernel's static
-            // __shared__ state (its prologue record)
-            hipFuncAttributes fa{};
-            size_t static_lds = 256;
-            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(dev::sptrsv_whead_kernel<S, true, true>)) ==
-                hipSuccess)
-                static_lds = fa.sharedSizeBytes;
-            f->hconc = (!(hc && !std::strcmp(hc, "seq")) &&
-                        (size_t)K * (size_t)(f->hpos + 1) * sizeof(S) + 16 + static_lds <= (size_t)160 * 1024) ? 1 : 0;
-        }
-    }
-    int64_t red_cap = 1024;   // EIGSOL_TRSV_PART_GRID: A/B of the partials kernels' grid
-    if (const char* e = std::getenv("EIGSOL_TRSV_PART_GRID")) red_cap = std::max<int64_t>(8, std::atoll(e));
-    // never above grid * kWaves: wave_part (below) holds that many block partials
-    f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
-                                                                  std::min<int64_t>(red_cap, (n + 1023) / 1024)));
+    auto up_ = [&](void** dst, const void* src, size_t bytes) -> int { return dev_upload(st, dst, src, bytes); };
+    if (rc == EIGSOL_OK) rc = tri_launch_setup<S>(f);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->order, order.data(), (size_t)f->hpos * 4);
     if (rc == EIGSOL_OK) rc = up_((void**)&f->hcol, hcol.data(), hcol.size() * 4);
     if (rc == EIGSOL_OK) rc = up_(&f->hval, hval.data(), hval.size() * sizeof(S));
@@ -2256,26 +2517,270 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
     if (rc == EIGSOL_OK) rc = up_((void**)&f->pcol, pcol.data(), pcol.size() * 4);
     if (rc == EIGSOL_OK) rc = up_(&f->pval, pval.data(), pval.size() * sizeof(S));
     if (rc == EIGSOL_OK) rc = up_(&f->ppiv, ppiv.data(), ppiv.size() * sizeof(S));
-    if (rc == EIGSOL_OK) rc = up_(&f->z[0], nullptr, (n + 1) * sizeof(S));
-    if (rc == EIGSOL_OK) rc = up_(&f->z[1], nullptr, (n + 1) * sizeof(S));
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->work, nullptr, 64);
-    if (rc == EIGSOL_OK) rc = up_((void**)&f->err, nullptr, 64);
-    if (rc == EIGSOL_OK) rc = up_(&f->wave_part, nullptr, (size_t)f->grid * dev::kWaves * sizeof(dev::part4));
-    if (rc == EIGSOL_OK) {
-        // every row starts unsolved (sentinel); the zero slot z[n] stays 0 for good
-        const uint32_t sent = (uint32_t)(dev::kSent & 0xffffffffu);
-        for (void* zb : f->z) {
-            hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(zb), (int)sent, n * sizeof(S) / 4, st);
-            hipMemsetAsync(static_cast<char*>(zb) + n * sizeof(S), 0, sizeof(S), st);
-        }
-        hipMemsetAsync(f->work, 0, 64, st);
-        hipMemsetAsync(f->err, 0, 64, st);
-        if (hipStreamSynchronize(st) != hipSuccess) rc = fail(EIGSOL_E_HIP, "factor upload");
-    }
+    if (rc == EIGSOL_OK) rc = tri_state_alloc<S>(f);
     if (rc != EIGSOL_OK) { shift_free(f); return rc; }
     f->kind = 0;
+    tri_dump<S>(f);
     *out = f;
     return EIGSOL_OK;
+}
+
+// EIGSOL_TRSV_DUMP=prefix (debugging): the built factor's position-indexed arrays, downloaded and
+// written to prefix_<name>.bin (host and device builds compare byte for byte)
+template <class S>
+static void tri_dump(const ShiftFactor* f) {
+    const char* pre = std::getenv("EIGSOL_TRSV_DUMP");
+    if (!pre || f->kind != 0) return;
+    hipStreamSynchronize(f->ctx->stream);
+    auto put = [&](const char* name, const void* d, size_t bytes) {
+        std::vector<unsigned char> h(bytes);
+        if (bytes && hipMemcpy(h.data(), d, bytes, hipMemcpyDeviceToHost) != hipSuccess) return;
+        const std::string path = std::string(pre) + "_" + name + ".bin";
+        if (FILE* fp = std::fopen(path.c_str(), "wb")) {
+            std::fwrite(h.data(), 1, bytes, fp);
+            std::fclose(fp);
+        }
+    };
+    const int32_t meta[12] = {f->nlevels, f->npos, f->hpos, f->hlevels, f->nwpass, f->chunk0, f->nchunks, f->chunk_two,
+                              f->tail_chunks, f->grid, f->multi, (int32_t)f->nnz_off};
+    if (FILE* fp = std::fopen((std::string(pre) + "_meta.bin").c_str(), "wb")) {
+        std::fwrite(meta, sizeof(meta), 1, fp);
+        std::fclose(fp);
+    }
+    put("porder", f->porder, (size_t)f->npos * 4);
+    put("pptr", f->pptr, ((size_t)f->npos + 1) * 4);
+    put("pcol", f->pcol, (size_t)f->nnz_off * 4);
+    put("pval", f->pval, (size_t)f->nnz_off * sizeof(S));
+    put("ppiv", f->ppiv, (size_t)f->npos * sizeof(S));
+    put("order", f->order, (size_t)f->hpos * 4);
+    put("wval", f->wval, (size_t)f->nwpass * 256 * sizeof(S));
+    put("wcol", f->wcol, (size_t)f->nwpass * 256 * 4);
+    put("wrp", f->wrp, (size_t)f->nwpass * 16 * sizeof(S));
+    put("wdst", f->wdst, (size_t)f->nwpass * 16 * 4);
+}
+
+hipError_t tri_sort_rows_by_level(hipStream_t st, const int32_t* lev, int32_t* lev_out, int32_t* rows_out, int64_t n,
+                                  int bits);
+hipError_t tri_exclusive_scan(hipStream_t st, const int32_t* in, int32_t* out, int64_t n);
+
+// Triangular CSR already on the device -> the level-ordered factor of A - sigma I, built on the device
+// (round 5; the host build of config 5's 1M-row factor took 0.37 s, most of it moving 320 MB of
+// matrix down and the layout back up).  The result is the host build's layout bit for bit: the
+// same levels, positions sorted by level with ascending rows inside a level (stable radix sort),
+// the same padding, the same position-indexed chunk CSR and the same one-wave head.  Only the small
+// per-level tables (counts, longest rows) travel to the host, which takes the same head / tail
+// decisions as factor_tri_host.  declined = true (nothing built) for a matrix that is not
+// triangular or a layout this build does not produce (slice tail, one-workgroup head): the caller
+// then takes the host path.
+template <class S>
+static int factor_tri_device(eigsol_csr* A, double sre, double sim, ShiftFactor** out, bool& declined) {
+    declined = false;
+    eigsol_ctx* ctx = A->ctx;
+    hipStream_t st = ctx->stream;
+    const int64_t n = A->nrows, nnz = A->nnz;
+    const S* val = static_cast<const S*>(A->val);
+    std::vector<void*> scratch;
+    auto dalloc = [&](void** p, size_t bytes) -> int {
+        EIGSOL_HIP(hipMalloc(p, std::max<size_t>(bytes, 16)));
+        scratch.push_back(*p);
+        return EIGSOL_OK;
+    };
+    int32_t* hostw = nullptr;   // pinned: flags[0..2], maxlev, err, nnz_off
+    ShiftFactor* f = nullptr;
+    auto finish = [&](int rc) {
+        hipStreamSynchronize(st);
+        for (void* p : scratch) hipFree(p);
+        if (hostw) hipHostFree(hostw);
+        if (rc != EIGSOL_OK || declined) {
+            if (f) shift_free(f);
+            return rc;
+        }
+        *out = f;
+        return rc;
+    };
+    constexpr int64_t W = dev::kWaveRows;
+    S* pv = nullptr;
+    int32_t *offlen = nullptr, *lev = nullptr, *lcnt = nullptr, *lmax = nullptr, *words = nullptr;
+    int rc = EIGSOL_OK;
+    if ((rc = dalloc((void**)&pv, n * sizeof(S))) || (rc = dalloc((void**)&offlen, n * 4)) ||
+        (rc = dalloc((void**)&lev, n * 4)) || (rc = dalloc((void**)&lcnt, (n + 1) * 4)) ||
+        (rc = dalloc((void**)&lmax, (n + 1) * 4)) || (rc = dalloc((void**)&words, 64)))
+        return finish(rc);
+    if (hipHostMalloc(&hostw, 64, hipHostMallocDefault) != hipSuccess) return finish(fail(EIGSOL_E_HIP, "hipHostMalloc"));
+    // words: [0..2] flags, [3] deepest level, [4] err, [5] ticket
+    hipMemsetAsync(words, 0, 64, st);
+    hipMemsetAsync(lev, 0xFF, n * 4, st);
+    hipMemsetAsync(lcnt, 0, (n + 1) * 4, st);
+    hipMemsetAsync(lmax, 0, (n + 1) * 4, st);
+    const unsigned gb = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL((dev::tri_rows_kernel<S>), dim3(gb), dim3(256), 0, st, A->rowptr, A->col, val, n,
+                       make_sigma<S>(sre, sim), pv, offlen, words);
+    EIGSOL_HIP(hipMemcpyAsync(hostw, words, 64, hipMemcpyDeviceToHost, st));
+    if (hipStreamSynchronize(st) != hipSuccess) return finish(fail(EIGSOL_E_HIP, "triangular analysis: row scan"));
+    const bool up = !hostw[0], lo = !hostw[1];
+    if (!up && !lo) {
+        declined = true;
+        return finish(EIGSOL_OK);
+    }
+    if (hostw[2]) return finish(fail(EIGSOL_E_SOLVER, "solve_shifted: SparseLU factorization failed"));
+    hipLaunchKernelGGL(dev::tri_level_kernel, dim3(std::max(1, 4 * ctx->num_cus)), dim3(256), 0, st, A->rowptr, A->col,
+                       offlen, n, up ? 1 : 0, lev, reinterpret_cast<uint32_t*>(words + 5), lcnt, lmax, words + 3,
+                       words + 4);
+    EIGSOL_HIP(hipMemcpyAsync(hostw, words, 64, hipMemcpyDeviceToHost, st));
+    if (hipStreamSynchronize(st) != hipSuccess) return finish(fail(EIGSOL_E_HIP, "triangular analysis: levels"));
+    if (hostw[4]) {   // a dependency wait ran out of time: build on the host instead
+        declined = true;
+        return finish(EIGSOL_OK);
+    }
+    const int32_t nlevels = hostw[3] + 1;
+    std::vector<int32_t> hcnt(nlevels), hmax(nlevels);
+    EIGSOL_HIP(hipMemcpyAsync(hcnt.data(), lcnt, nlevels * 4, hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipMemcpyAsync(hmax.data(), lmax, nlevels * 4, hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipStreamSynchronize(st));
+    std::vector<int64_t> lstart(nlevels + 1, 0), lcount(hcnt.begin(), hcnt.end());
+    for (int32_t l = 0; l < nlevels; ++l) lstart[l + 1] = lstart[l] + ((lcount[l] + W - 1) / W) * W;
+    f = new ShiftFactor();
+    f->ctx = ctx;
+    ctx_retain(ctx);
+    f->dtype = A->dtype;
+    f->n = n;
+    f->sig_re = sre;
+    f->sig_im = sim;
+    f->nnz_total = nnz;
+    f->upper = up ? 1 : 0;
+    f->nlevels = nlevels;
+    f->npos = (int32_t)lstart[nlevels];
+    if (const char* e = std::getenv("EIGSOL_TRSV_HEAD")) f->wave_head = std::strcmp(e, "block") ? 1 : 0;
+    f->hlevels = head_levels<S>(lstart, lcount, hmax, f->nlevels, f->wave_head != 0);
+    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_FAST")) f->poll_fast = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_MODE")) f->poll_mode = std::atoi(e);
+    f->hpos = (int32_t)lstart[f->hlevels];
+    {   // tail variant: the rule of factor_tri_host
+        int64_t trows = 0, wide = 0;
+        for (int32_t l = f->hlevels; l < f->nlevels; ++l) {
+            trows += lcount[l];
+            if (lcount[l] >= 65536) wide += lcount[l];
+        }
+        f->tail_chunks = (trows > 0 && 2 * wide < trows) ? 1 : 0;
+        if (const char* e = std::getenv("EIGSOL_TRSV_TAIL")) f->tail_chunks = std::strcmp(e, "slice") ? 1 : 0;
+    }
+    if (!f->tail_chunks || (f->hpos > 0 && !f->wave_head)) {
+        declined = true;
+        return finish(EIGSOL_OK);
+    }
+    // positions: rows sorted by level, at each level's padded start
+    int bits = 1;
+    while (bits < 31 && (int64_t(1) << bits) <= (int64_t)(nlevels - 1)) ++bits;
+    int32_t *lev_s = nullptr, *rows_s = nullptr, *ustart = nullptr, *pstart = nullptr, *plen = nullptr;
+    if ((rc = dalloc((void**)&lev_s, n * 4)) || (rc = dalloc((void**)&rows_s, n * 4)) ||
+        (rc = dalloc((void**)&ustart, (size_t)nlevels * 4)) || (rc = dalloc((void**)&pstart, (size_t)nlevels * 4)) ||
+        (rc = dalloc((void**)&plen, ((size_t)f->npos + 1) * 4)))
+        return finish(rc);
+    if (tri_sort_rows_by_level(st, lev, lev_s, rows_s, n, bits) != hipSuccess)
+        return finish(fail(EIGSOL_E_HIP, "triangular analysis: level sort"));
+    std::vector<int32_t> hu(nlevels), hp(nlevels);
+    {
+        int64_t u = 0;
+        for (int32_t l = 0; l < nlevels; ++l) {
+            hu[l] = (int32_t)u;
+            hp[l] = (int32_t)lstart[l];
+            u += lcount[l];
+        }
+    }
+    EIGSOL_HIP(hipMemcpyAsync(ustart, hu.data(), (size_t)nlevels * 4, hipMemcpyHostToDevice, st));
+    EIGSOL_HIP(hipMemcpyAsync(pstart, hp.data(), (size_t)nlevels * 4, hipMemcpyHostToDevice, st));
+    const int64_t npos = f->npos;
+    EIGSOL_TRY(dev_upload(st, (void**)&f->porder, nullptr, (size_t)npos * 4));
+    EIGSOL_HIP(hipMemsetAsync(f->porder, 0xFF, (size_t)npos * 4, st));
+    hipLaunchKernelGGL(dev::tri_order_kernel, dim3(gb), dim3(256), 0, st, lev_s, rows_s, n, ustart, pstart, f->porder);
+    EIGSOL_TRY(dev_upload(st, (void**)&f->order, nullptr, (size_t)f->hpos * 4));
+    if (f->hpos > 0)
+        EIGSOL_HIP(hipMemcpyAsync(f->order, f->porder, (size_t)f->hpos * 4, hipMemcpyDeviceToDevice, st));
+    // position-indexed chunk CSR: pivots, row pointers (scan of the off-diagonal counts), entries
+    const S one = make_sigma<S>(1.0, 0.0);
+    EIGSOL_TRY(dev_upload(st, &f->ppiv, nullptr, (size_t)npos * sizeof(S)));
+    EIGSOL_TRY(dev_upload(st, (void**)&f->pptr, nullptr, ((size_t)npos + 1) * 4));
+    hipLaunchKernelGGL((dev::tri_poslen_kernel<S>), dim3((unsigned)((npos + 256) / 256)), dim3(256), 0, st, f->porder,
+                       npos, offlen, pv, one, plen, static_cast<S*>(f->ppiv));
+    if (tri_exclusive_scan(st, plen, f->pptr, npos) != hipSuccess)
+        return finish(fail(EIGSOL_E_HIP, "triangular analysis: row pointer scan"));
+    EIGSOL_HIP(hipMemcpyAsync(hostw + 5, f->pptr + npos, 4, hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(hipStreamSynchronize(st));
+    f->nnz_off = hostw[5];
+    EIGSOL_TRY(dev_upload(st, (void**)&f->pcol, nullptr, (size_t)f->nnz_off * 4));
+    EIGSOL_TRY(dev_upload(st, &f->pval, nullptr, (size_t)f->nnz_off * sizeof(S)));
+    hipLaunchKernelGGL((dev::tri_gather_kernel<S>), dim3((unsigned)((npos * dev::kRowLanes + 255) / 256)), dim3(256), 0,
+                       st, f->porder, npos, f->pptr, A->rowptr, A->col, val, offlen, f->pcol, static_cast<S*>(f->pval));
+    f->chunk0 = f->hpos / dev::kWaveRows;
+    f->nchunks = f->npos / dev::kWaveRows;
+    {   // rows past 16 entries in the tail: the second entry of every lane is polled with the first
+        int32_t longest = 0;
+        for (int32_t l = f->hlevels; l < f->nlevels; ++l) longest = std::max(longest, hmax[l]);
+        f->chunk_two = longest > dev::kRowLanes ? 1 : 0;
+        if (const char* e = std::getenv("EIGSOL_TRSV_TWO")) f->chunk_two = std::atoi(e) != 0;
+    }
+    // one-wave head: passes of <= 16 rows inside a level, padded to the ring depth
+    std::vector<int2> ptab;
+    for (int32_t l = 0; l < f->hlevels; ++l) {
+        const int32_t p0 = (int32_t)lstart[l], p1 = (int32_t)(lstart[l] + lcount[l]);
+        for (int32_t p = p0; p < p1; p += dev::kWHeadRows) ptab.push_back(make_int2(p, std::min(dev::kWHeadRows, p1 - p)));
+    }
+    const int32_t nreal = (int32_t)ptab.size();
+    int32_t nw = nreal;
+    while (nw % dev::kWHeadDepth) ++nw;
+    f->nwpass = f->hpos > 0 ? nw : 0;
+    const size_t wslots = (size_t)f->nwpass * 256, wrows = (size_t)f->nwpass * dev::kWHeadRows;
+    EIGSOL_TRY(dev_upload(st, &f->wval, nullptr, wslots * sizeof(S)));
+    EIGSOL_TRY(dev_upload(st, (void**)&f->wcol, nullptr, wslots * 4));
+    EIGSOL_TRY(dev_upload(st, &f->wrp, nullptr, wrows * sizeof(S)));
+    EIGSOL_TRY(dev_upload(st, (void**)&f->wdst, nullptr, wrows * 4));
+    if (f->nwpass > 0) {
+        int32_t* rowpos = nullptr;
+        int2* dtab = nullptr;
+        if ((rc = dalloc((void**)&rowpos, n * 4)) || (rc = dalloc((void**)&dtab, (size_t)nreal * sizeof(int2))))
+            return finish(rc);
+        EIGSOL_HIP(hipMemcpyAsync(dtab, ptab.data(), (size_t)nreal * sizeof(int2), hipMemcpyHostToDevice, st));
+        EIGSOL_HIP(hipMemsetAsync(rowpos, 0xFF, n * 4, st));
+        EIGSOL_HIP(hipMemsetAsync(f->wval, 0, wslots * sizeof(S), st));
+        EIGSOL_HIP(hipMemsetAsync(f->wdst, 0xFF, wrows * 4, st));
+        hipLaunchKernelGGL((dev::fill_kernel<int32_t>), dim3(256), dim3(256), 0, st, f->wcol, (int64_t)wslots, f->hpos);
+        hipLaunchKernelGGL((dev::fill_kernel<S>), dim3(64), dim3(256), 0, st, static_cast<S*>(f->wrp), (int64_t)wrows, one);
+        hipLaunchKernelGGL(dev::tri_rowpos_kernel, dim3((unsigned)((f->hpos + 255) / 256)), dim3(256), 0, st, f->porder,
+                           f->hpos, rowpos);
+        hipLaunchKernelGGL((dev::tri_whead_kernel<S>), dim3((unsigned)((nreal * dev::kWHeadRows + 255) / 256)), dim3(256),
+                           0, st, dtab, nreal, f->porder, A->rowptr, A->col, val, pv, rowpos, static_cast<S*>(f->wval),
+                           f->wcol, static_cast<S*>(f->wrp), f->wdst);
+    }
+    // the one-workgroup head's tables stay empty (npass = 0: that head is not built here)
+    EIGSOL_TRY(dev_upload(st, (void**)&f->hcol, nullptr, 0));
+    EIGSOL_TRY(dev_upload(st, &f->hval, nullptr, 0));
+    EIGSOL_TRY(dev_upload(st, &f->hpiv, nullptr, 0));
+    EIGSOL_TRY(dev_upload(st, (void**)&f->passes, nullptr, 0));
+    // slice tail: none (nslices = 0), but the empty slice 0 the slice kernels may prefetch exists
+    {
+        f->slice_b = 4;
+        if (const char* e = std::getenv("EIGSOL_TRSV_SLICE_B")) {
+            const int b = std::atoi(e);
+            if (b == 4 || b == 8 || b == 16) f->slice_b = b;
+        }
+        const int32_t Bs = f->slice_b;
+        f->nslices = 0;
+        const std::vector<int2> smeta(1, make_int2(0, Bs));
+        const std::vector<int32_t> trow(64, -1), tcol((size_t)64 * Bs, (int32_t)n);
+        const std::vector<S> tpiv(64, one), tval((size_t)64 * Bs, s_zero<S>());
+        EIGSOL_TRY(dev_upload(st, (void**)&f->smeta, smeta.data(), smeta.size() * sizeof(int2)));
+        EIGSOL_TRY(dev_upload(st, (void**)&f->trow, trow.data(), trow.size() * 4));
+        EIGSOL_TRY(dev_upload(st, &f->tpiv, tpiv.data(), tpiv.size() * sizeof(S)));
+        EIGSOL_TRY(dev_upload(st, (void**)&f->tcol, tcol.data(), tcol.size() * 4));
+        EIGSOL_TRY(dev_upload(st, &f->tval, tval.data(), tval.size() * sizeof(S)));
+        EIGSOL_HIP(hipStreamSynchronize(st));   // the small host vectors above go out of scope
+    }
+    if (hipGetLastError() != hipSuccess) return finish(fail(EIGSOL_E_HIP, "triangular analysis: launch"));
+    if ((rc = tri_launch_setup<S>(f)) != EIGSOL_OK) return finish(rc);
+    if ((rc = tri_state_alloc<S>(f)) != EIGSOL_OK) return finish(rc);
+    f->kind = 0;
+    tri_dump<S>(f);
+    return finish(EIGSOL_OK);
 }
 
 // triangular factor from host CSR arrays (the ILU(0) factors of the GMRES path, gmres.hip)
