@@ -10,6 +10,7 @@ column-major matrix, ``matrix.hpp:39-40``); complex values are interleaved (re, 
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import subprocess
@@ -32,11 +33,35 @@ def build(force: bool = False) -> str:
     return _LIB_PATH
 
 
+_AS_SHIPPED_PATH = os.path.join(_HERE, "build", "liboracle_O0.so")
+
+
+@contextlib.contextmanager
+def as_shipped():
+    """Inside the block, every oracle call runs the same restatement compiled at -O0 without -march
+    (the reference's CMake sets no build type, so it ships unoptimised) - the
+    secondary CPU baseline; never a checker."""
+    global _lib
+    if not os.path.exists(_AS_SHIPPED_PATH):
+        subprocess.run(["make", "-C", _HERE, "O0"], check=True, stdout=subprocess.DEVNULL)
+    saved = lib()
+    _lib = _configure(C.CDLL(_AS_SHIPPED_PATH))
+    try:
+        yield
+    finally:
+        _lib = saved
+
+
 def lib():
     global _lib
     if _lib is None:
         build()
-        L = C.CDLL(_LIB_PATH)
+        _lib = _configure(C.CDLL(_LIB_PATH))
+    return _lib
+
+
+def _configure(L):
+    if True:
         for name in ("spmv_csc_f64", "spmv_csc_c128", "spmv_csc_f32", "spmv_csc_c64"):
             getattr(L, "orc_" + name).argtypes = [_i64, _i64, _p, _p, _p, _p, _p]
         for name in ("spmv_csr_f64", "spmv_csr_c128", "spmv_csr_f32", "spmv_csr_c64"):
@@ -94,8 +119,7 @@ def lib():
             getattr(L, "orc_solve_shifted_dense_" + sfx).argtypes = [_i64, _p, _p, _p, _p]
             getattr(L, "orc_hessenberg_" + sfx).argtypes = [_i64, _p, _p]
             getattr(L, "orc_qr_decompose_" + sfx).argtypes = [_i64, _i64, _p, _p, _p]
-        _lib = L
-    return _lib
+    return L
 
 
 def _ptr(a: np.ndarray):
