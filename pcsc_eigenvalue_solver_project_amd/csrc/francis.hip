@@ -689,8 +689,27 @@ struct AedCtl {
 // original four FMA chains of the dot products, combined in the same order (round 4: bitwise the
 // one-wave kernel's results, phase C ~3x shorter)
 constexpr int kAedThreads = 256;
+// Concurrent shifts (ShiftJob, round 5): a second workgroup of the same launch computes the
+// eigenvalues of the trailing ns x ns block of the active block as it stands BEFORE the AED -- the
+// block the next sweep's shift QR would read when the AED deflates nothing -- on its own wave while
+// workgroup 0 runs the AED.  It copies the block into its LDS first and raises flag = epoch;
+// workgroup 0 writes the window back only after seeing the flag, so the copy is the pre-AED state.
+struct ShiftJob {
+    int kb, ns;                // block [kb, kb + ns) of H
+    double dtol;               // split tolerance of the shifts' QR (EIGSOL_QR_SHIFT_TOL)
+    double *wr, *wi;           // ns eigenvalues
+    int* info;                 // {fail, most sweeps per deflation, total, wait timed out}
+    unsigned* flag;
+    unsigned epoch;
+};
+
+__device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
+    return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(kAedThreads) void aed_kernel(double* H, int64_t n, int kw, int nw, int spike_valid, int maxits,
-                                                 int early, double* wr, double* wi, double* Vout, int* info) {
+                                                 int early, double* wr, double* wi, double* Vout, int* info,
+                                                 ShiftJob sj) {
     constexpr int LD = kAedMax + 1;
     __shared__ double t[kAedMax * LD];
     __shared__ double v[kAedMax * LD];
@@ -699,6 +718,26 @@ __global__ __launch_bounds__(kAedThreads) void aed_kernel(double* H, int64_t n, 
     __shared__ int bs[kAedMax];           // Schur block size ending at each row (1 or 2)
     __shared__ AedCtl c;
     const int tid = threadIdx.x, nt = kAedThreads;
+    if (blockIdx.x == 1) {   // the concurrent shifts (ShiftJob)
+        const int ns = sj.ns;
+        for (int e = tid; e < ns * ns; e += nt) {
+            const int i = e % ns, j = e / ns;
+            t[i + j * LD] = H[(sj.kb + i) + (int64_t)(sj.kb + j) * n];
+        }
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(sj.flag, sj.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid < 64) {
+            int fail = 0, total = 0, maxsw = 0;
+            if (ns <= 64) wave_hqr<false, 1>(t, nullptr, ns, LD, maxits, sj.wr, sj.wi, nullptr, fail, total, maxsw, nullptr, -1.0, nullptr, sj.dtol);
+            else wave_hqr<false, 2>(t, nullptr, ns, LD, maxits, sj.wr, sj.wi, nullptr, fail, total, maxsw, nullptr, -1.0, nullptr, sj.dtol);
+            if (tid == 0) {
+                sj.info[0] = fail;
+                sj.info[1] = maxsw;
+                sj.info[2] = total;
+            }
+        }
+        return;
+    }
     const int grp = tid >> 2, q = tid & 3;   // phase C: 64 groups of four lanes (one wave holds 16 groups)
     auto T = [&](int i, int j) -> double& { return t[i + j * LD]; };
     auto V = [&](int i, int j) -> double& { return v[i + j * LD]; };
@@ -842,7 +881,22 @@ __global__ __launch_bounds__(kAedThreads) void aed_kernel(double* H, int64_t n, 
         }
     }
     const long long tD = wall_clock64();
-    // ---------------- phase D: write back (only when something deflated)
+    // ---------------- phase D: write back (only when something deflated), after the concurrent
+    // shifts' workgroup has copied its pre-AED block (a bounded wait: ~1 s of the constant clock)
+    if (gridDim.x > 1) {
+        if (tid == 0) {
+            int timed_out = 0;
+            if (nd > 0) {
+                const long long t0 = wall_clock64();
+                while (ld_flag(sj.flag) != sj.epoch) {
+                    if (wall_clock64() - t0 > 100000000ll) { timed_out = 1; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            sj.info[3] = timed_out;
+        }
+        __syncthreads();
+    }
     if (nd > 0) {
         for (int e = tid; e < nw * nw; e += nt) {
             const int i = e % nw, j = e / nw;
@@ -901,18 +955,27 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     const double eps = 2.220446049250313e-16;
     double *dwr = nullptr, *dwi = nullptr, *dds = nullptr, *dU = nullptr, *dsh = nullptr;
     int* dinfo = nullptr;
+    double* dsw = nullptr;      // concurrent shifts (ShiftJob): re, im
+    int* dsinfo = nullptr;
+    unsigned* dflag = nullptr;
+    unsigned flag_epoch = 0;
     int rc = EIGSOL_OK;
-    if (hipMalloc(&dwr, n * sizeof(double)) != hipSuccess || hipMalloc(&dwi, n * sizeof(double)) != hipSuccess ||
+    if (hipMalloc(&dsw, 2 * dev::kAedMax * sizeof(double)) != hipSuccess || hipMalloc(&dsinfo, 64) != hipSuccess ||
+        hipMalloc(&dflag, 64) != hipSuccess || hipMemsetAsync(dflag, 0, 64, st) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "francis: device workspace");
+    if (rc == EIGSOL_OK && (hipMalloc(&dwr, n * sizeof(double)) != hipSuccess || hipMalloc(&dwi, n * sizeof(double)) != hipSuccess ||
         hipMalloc(&dds, 2 * n * sizeof(double)) != hipSuccess ||
         hipMalloc(&dU, dev::kMaxGroups * dev::kWin * dev::kWin * sizeof(double)) != hipSuccess ||
-        hipMalloc(&dsh, 4 * dev::kMaxBulges * sizeof(double)) != hipSuccess || hipMalloc(&dinfo, 64) != hipSuccess)
+        hipMalloc(&dsh, 4 * dev::kMaxBulges * sizeof(double)) != hipSuccess || hipMalloc(&dinfo, 64) != hipSuccess))
         rc = fail(EIGSOL_E_HIP, "francis: device workspace");
     // every per-sweep transfer goes through pinned host memory: a pageable hipMemcpyAsync is staged
     // by the runtime and waited for with a sleeping wait, ~1 ms per copy (round-4 kernel trace,
     // tools/gap_analysis.py), more than a sweep's kernels at the end of the iteration
     struct Staging {
         int info[8];
+        int cinfo[4];
         double awr[dev::kAedMax], awi[dev::kAedMax];
+        double cwr[2 * dev::kAedMax];   // concurrent shifts: re [0, kAedMax), im [kAedMax, 2 kAedMax)
         double swr[2 * dev::kMaxBulges], swi[2 * dev::kMaxBulges], sh[2 * dev::kMaxBulges];
     };
     Staging* hp = nullptr;
@@ -975,7 +1038,18 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         const char* e = std::getenv("EIGSOL_QR_NIBBLE");
         return e ? std::max(1, std::atoi(e)) : 30;
     }();
-    int st_sweeps = 0, st_windows = 0, st_small = 0, st_small_rows = 0, st_aed = 0, st_aed_defl = 0;
+    int st_sweeps = 0, st_windows = 0, st_small = 0, st_small_rows = 0, st_aed = 0, st_aed_defl = 0, st_conc = 0;
+    // concurrent shifts (EIGSOL_QR_CONC): 0 off (the shift QR after the AED, one wave), 1 when the AED
+    // deflates nothing (bitwise the sequential sweeps), 2 (default) also after a small deflation
+    // (LAPACK xLAQR0's undeflated window eigenvalues).  Round 5 (tools/qr_conc_ab.sh, 4096^2, two
+    // seeds): only 2 of 115 sweeps follow an AED that deflated nothing, so mode 1 is mode 0 (0.946 /
+    // 0.949 s); mode 2 runs 141 sweeps instead of 115 but skips their 0.79 ms shift QRs, whose
+    // eigenvalue QR of the window hides under the AED (~1.1 ms): 0.946 -> 0.928 s and 0.948 ->
+    // 0.930 s (seed 7), one-to-one with LAPACK (3.3e-12)
+    static const int conc_mode = [] {
+        const char* e = std::getenv("EIGSOL_QR_CONC");
+        return e ? std::atoi(e) : 2;
+    }();
     auto finish_small = [&](int l, int hi) -> int {
         const int m = hi - l + 1;
         EIGSOL_TRY(hqr_small(st, H + l + (int64_t)l * n, n, m, std::max(1, maxits), dwr + l, dwi + l, dinfo));
@@ -1024,18 +1098,28 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         if (aed_win > 0) {
             const int nw = std::min(aed_win, N);
             const int kw = ihi - nw + 1;
-            hipLaunchKernelGGL(dev::aed_kernel, dim3(1), dim3(dev::kAedThreads), 0, st, H, n, kw, nw, kw > l ? 1 : 0, 60,
-                               aed_early ? 1 : 0, dwr, dwi, dU, dinfo);
+            // concurrent shifts: the pre-AED trailing ns block's eigenvalues on a second workgroup
+            // (ShiftJob); used when the AED deflates nothing (the very block the sequential shift QR
+            // would read, so the sweep is bitwise the same) and, LAPACK xLAQR0-style, when it
+            // deflated a few and the block is the window itself (the undeflated window eigenvalues)
+            const bool conc = conc_mode > 0 && ns <= dev::kAedMax && ns >= 2;
+            dev::ShiftJob sj{ihi - ns + 1, ns, shift_tol, dsw, dsw + dev::kAedMax, dsinfo, dflag, ++flag_epoch};
+            hipLaunchKernelGGL(dev::aed_kernel, dim3(conc ? 2 : 1), dim3(dev::kAedThreads), 0, st, H, n, kw, nw,
+                               kw > l ? 1 : 0, 60, aed_early ? 1 : 0, dwr, dwi, dU, dinfo, sj);
             int* info = hp->info;
             double* const awr = hp->awr;
             double* const awi = hp->awi;
             if (hipMemcpyAsync(info, dinfo, 8 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipMemcpyAsync(awr, dwr + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipMemcpyAsync(awi, dwi + kw, nw * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                (conc && (hipMemcpyAsync(hp->cinfo, dsinfo, 4 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                          hipMemcpyAsync(hp->cwr, dsw, 2 * dev::kAedMax * sizeof(double), hipMemcpyDeviceToHost, st) !=
+                              hipSuccess)) ||
                 stream_wait(st) != hipSuccess) {
                 rc = fail(EIGSOL_E_HIP, "francis: aed");
                 break;
             }
+            const bool conc_ok = conc && !hp->cinfo[0] && !hp->cinfo[3];
             ++st_aed;
             st_aed_steps += info[4];
             st_aed_ph[0] += info[5]; st_aed_ph[1] += info[6]; st_aed_ph[2] += info[7];
@@ -1052,6 +1136,45 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
                     sweeps = std::max(sweeps, stall);
                     stall = 0;
                     if (100 * nd >= kNibble * nw || m < 4) continue;   // enough deflated: look again first
+                }
+                if (conc_ok && nd == 0) {   // the block the shift QR below would solve, already solved
+                    for (int i = 0; i < ns; ++i) {
+                        swr[i] = hp->cwr[i];
+                        swi[i] = hp->cwr[dev::kAedMax + i];
+                    }
+                    have_shifts = true;
+                    ++st_conc;
+                } else if (conc_ok && conc_mode > 1 && nd > 0 && ns == nw && m >= ns / 2) {
+                    // the window's undeflated eigenvalues (LAPACK xLAQR0): the window's spectrum with
+                    // each deflated eigenvalue's nearest match removed; the last (ns - nd) rounded to
+                    // an even count
+                    std::vector<int> used(ns, 0);
+                    for (int j = m; j < nw; ++j) {
+                        int best = -1;
+                        double bd = 0.0;
+                        for (int i = 0; i < ns; ++i) {
+                            if (used[i]) continue;
+                            const double d = std::hypot(hp->cwr[i] - awr[j], hp->cwr[dev::kAedMax + i] - awi[j]);
+                            if (best < 0 || d < bd) { best = i; bd = d; }
+                        }
+                        if (best >= 0) used[best] = 1;
+                    }
+                    int k = 0;
+                    for (int i = 0; i < ns; ++i)
+                        if (!used[i]) {
+                            swr[k] = hp->cwr[i];
+                            swi[k] = hp->cwr[dev::kAedMax + i];
+                            ++k;
+                        }
+                    const int N2 = ihi - l + 1;
+                    nb = std::min({max_bulges, std::max(1, N2 / 8), std::max(1, k / 2)});
+                    ns = 2 * nb;
+                    for (int i = 0; i < ns; ++i) {   // the bottom ns of the undeflated ones
+                        swr[i] = swr[k - ns + i];
+                        swi[i] = swi[k - ns + i];
+                    }
+                    have_shifts = true;
+                    ++st_conc;
                 }
                 // shifts: the bottom undeflated eigenvalues of the window (early-stopped windows
                 // have none: the trailing block's, below)
@@ -1224,10 +1347,12 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
     }
     if (stats)
         std::fprintf(stderr, "francis: n=%lld sweeps=%d windows=%d steps=%lld small_blocks=%d small_rows=%d kSmall=%d "
-                     "aed=%d aed_deflated=%d aed_win=%d aed_steps=%lld aed_phase_ms=%.1f/%.1f/%.1f\n",
+                     "aed=%d aed_deflated=%d aed_win=%d aed_steps=%lld aed_phase_ms=%.1f/%.1f/%.1f conc_shifts=%d\n",
                      (long long)n, st_sweeps, st_windows, st_steps, st_small, st_small_rows, kSmall, st_aed, st_aed_defl,
-                     aed_win, st_aed_steps, st_aed_ph[0] * 1e-5, st_aed_ph[1] * 1e-5, st_aed_ph[2] * 1e-5);
-    for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo}) (void)hipFree(p);
+                     aed_win, st_aed_steps, st_aed_ph[0] * 1e-5, st_aed_ph[1] * 1e-5, st_aed_ph[2] * 1e-5, st_conc);
+    for (void* p : {(void*)dwr, (void*)dwi, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo, (void*)dsw, (void*)dsinfo,
+                    (void*)dflag})
+        (void)hipFree(p);
     if (ds) (void)hipHostFree(ds);
     if (hp) (void)hipHostFree(hp);
     // iterations reported: sweeps spent on the slowest deflation (>= 1, the final check), so that

@@ -302,8 +302,21 @@ __device__ __forceinline__ cplx quad_sum(cplx sq, int q) {   // (s0 + s1) + (s2 
     const cplx o2{__shfl_xor(pr.re, 2, 64), __shfl_xor(pr.im, 2, 64)};
     return (q & 2) ? add(o2, pr) : add(pr, o2);
 }
+// Concurrent shifts (round 5, as francis.hip's ShiftJob): workgroup 1 of the launch copies the
+// pre-AED trailing ns x ns block [kb, kb + ns) into its LDS, raises flag = epoch, and computes its
+// eigenvalues on one wave while workgroup 0 runs the AED; workgroup 0 writes the window back only
+// after the flag.
+struct ZShiftJob {
+    int kb, ns;
+    double dtol;
+    cplx* w;
+    int* info;            // {fail, most sweeps per deflation, -, wait timed out}
+    unsigned* flag;
+    unsigned epoch;
+};
+
 __global__ __launch_bounds__(kZAedThreads) void zaed_kernel(cplx* Hg, int64_t n, int kw, int nw, int spike_valid,
-                                                            int early, cplx* w, cplx* Vout, int* info) {
+                                                            int early, cplx* w, cplx* Vout, int* info, ZShiftJob sj) {
     constexpr int lh = kZSmall + 1;
     constexpr int NT = kZAedThreads;
     __shared__ cplx t[kZSmall * lh];
@@ -312,6 +325,21 @@ __global__ __launch_bounds__(kZAedThreads) void zaed_kernel(cplx* Hg, int64_t n,
     __shared__ cplx sp[kZSmall];
     __shared__ ZAedCtl c;
     const int tid = threadIdx.x, ln = tid & 63, wv0 = tid < 64;
+    if (blockIdx.x == 1) {   // the concurrent shifts
+        const int ns = sj.ns;
+        for (int e = tid; e < ns * ns; e += NT) t[(e % ns) + (e / ns) * lh] = Hg[(sj.kb + e % ns) + (int64_t)(sj.kb + e / ns) * n];
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(sj.flag, sj.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (wv0) {
+            int fail, maxsw, steps;
+            zwave_hqr<false>(t, nullptr, ns, sj.w, fail, maxsw, steps, -1.0, nullptr, sj.dtol);
+            if (ln == 0) {
+                sj.info[0] = fail;
+                sj.info[1] = maxsw;
+            }
+        }
+        return;
+    }
     const int grp = tid >> 2, q = tid & 3;   // 64 groups of four lanes
     auto T = [&](int i, int j) -> cplx& { return t[i + j * lh]; };
     auto V = [&](int i, int j) -> cplx& { return v[i + j * lh]; };
@@ -425,6 +453,20 @@ __global__ __launch_bounds__(kZAedThreads) void zaed_kernel(cplx* Hg, int64_t n,
         c.spike = cplx{0.0, 0.0};
     }
     __syncthreads();
+    if (gridDim.x > 1) {   // the concurrent shifts' copy is taken before the write-back (bounded wait)
+        if (tid == 0) {
+            int timed_out = 0;
+            if (nd > 0) {
+                const long long t0 = wall_clock64();
+                while (__hip_atomic_load(sj.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != sj.epoch) {
+                    if (wall_clock64() - t0 > 100000000ll) { timed_out = 1; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            sj.info[3] = timed_out;
+        }
+        __syncthreads();
+    }
     if (nd > 0) {
         for (int e = tid; e < nw * nw; e += NT) {
             const int i = e % nw, j = e / nw;
@@ -820,12 +862,21 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
     cplx* dV = nullptr;   // the AED window's unitary factor
     if (rc == EIGSOL_OK && hipMalloc(&dV, (size_t)dev::kZSmall * dev::kZSmall * sizeof(cplx)) != hipSuccess)
         rc = fail(EIGSOL_E_HIP, "complex QR: hipMalloc");
+    cplx* dsw = nullptr;       // concurrent shifts
+    int* dsinfo = nullptr;
+    unsigned* dflag = nullptr;
+    unsigned flag_epoch = 0;
+    if (rc == EIGSOL_OK && (hipMalloc(&dsw, dev::kZSmall * sizeof(cplx)) != hipSuccess || hipMalloc(&dsinfo, 64) != hipSuccess ||
+                            hipMalloc(&dflag, 64) != hipSuccess || hipMemsetAsync(dflag, 0, 64, st) != hipSuccess))
+        rc = fail(EIGSOL_E_HIP, "complex QR: hipMalloc");
     // every per-sweep transfer goes through pinned host memory: a pageable hipMemcpyAsync is staged
     // by the runtime and waited for with a sleeping wait, ~1 ms per copy (round-4 kernel trace of
     // 4096^2: 1.12 s of 2.8 s idle after such copies, tools/gap_analysis.py)
     struct Staging {
         int info[8];
+        int cinfo[4];
         cplx aw[dev::kZSmall];
+        cplx cw[dev::kZSmall];   // concurrent shifts
         cplx sh[2 * dev::kZMaxBulges];
     };
     Staging* hp = nullptr;
@@ -835,7 +886,18 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         rc = fail(EIGSOL_E_HIP, "complex QR: hipHostMalloc");
     cplx* const aw = hp ? hp->aw : nullptr;
     int sweeps = 0, failed = 0, stall = 0;
-    int st_sweeps = 0, st_aed = 0, st_aed_defl = 0, st_small = 0;
+    int st_sweeps = 0, st_aed = 0, st_aed_defl = 0, st_small = 0, st_conc = 0;
+    // concurrent shifts (EIGSOL_ZQR_CONC): 0 off (default), 1 when the AED deflates nothing (bitwise
+    // the sequential sweeps), 2 also after a deflation (the pre-AED block's spectrum without the
+    // deflated eigenvalues, LAPACK xLAQR0's undeflated shifts).  Measured and left off (round 5,
+    // tools/zqr_conc_ab.sh, 4096^2): a launch ends with its slower workgroup, and the 64 x 64
+    // complex shift QR (~2.5 ms) outlasts the AED (~1 ms), so every AED - also the 70 % after which
+    // the sweep is skipped - waits for it: 1.569 s -> 2.285 s (mode 1, same 122 sweeps, bitwise the
+    // same eigenvalues), 2.085 s (mode 2, 131 sweeps)
+    static const int conc_mode = [] {
+        const char* e = std::getenv("EIGSOL_ZQR_CONC");
+        return e ? std::atoi(e) : 0;
+    }();
     static const bool stats = std::getenv("EIGSOL_QR_STATS") != nullptr;
     int ihi = (int)n - 1;
     const int max_stall = std::max(1, maxits);
@@ -911,20 +973,57 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             const char* e = std::getenv("EIGSOL_ZQR_AED_FULL");
             return e && std::atoi(e) != 0;
         }();
+        // bulges of a sweep on an active block of Nact rows (C chains of nbg): the shift count 2 nb
+        auto plan = [&](int Nact, int cap, int& C, int& nbg) {
+            int nb = std::min(max_nb, std::max(1, Nact / 16));
+            if (cap >= 2) nb = std::min(nb, cap / 2);
+            C = std::max(1, std::min({max_groups, (nb + 7) / 8, 1 + Nact / (4 * (dev::kZWin + 12))}));
+            nbg = std::max(1, std::min(8, nb / C));
+            return nbg * C;
+        };
         int m_aed = 0;
+        int conc_n = 0;            // candidate shifts from the concurrent workgroup (in hp->cw)
         if (aed_win >= 4) {
             const int nw = std::min(aed_win, N);
             const int kw = ihi - nw + 1;
-            hipLaunchKernelGGL(dev::zaed_kernel, dim3(1), dim3(dev::kZAedThreads), 0, st, H, (int64_t)n, kw, nw, kw > l ? 1 : 0,
-                               aed_full ? 0 : 1, dw, dV, dinfo);
+            int C0, nbg0;
+            const int ns0 = 2 * plan(N, 0, C0, nbg0);   // the shift block if the AED deflates nothing
+            const bool conc = conc_mode > 0 && !aed_full && ns0 >= 2 && ns0 <= dev::kZSmall;
+            dev::ZShiftJob sj{ihi - ns0 + 1, ns0, shift_tol, dsw, dsinfo, dflag, ++flag_epoch};
+            hipLaunchKernelGGL(dev::zaed_kernel, dim3(conc ? 2 : 1), dim3(dev::kZAedThreads), 0, st, H, (int64_t)n, kw, nw,
+                               kw > l ? 1 : 0, aed_full ? 0 : 1, dw, dV, dinfo, sj);
             int* info = hp->info;
             if (hipMemcpyAsync(info, dinfo, 5 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipMemcpyAsync(aw, dw + kw, nw * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                (conc && (hipMemcpyAsync(hp->cinfo, dsinfo, 4 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                          hipMemcpyAsync(hp->cw, dsw, ns0 * sizeof(cplx), hipMemcpyDeviceToHost, st) != hipSuccess)) ||
                 stream_wait(st) != hipSuccess) {
                 rc = fail(EIGSOL_E_HIP, "complex QR: aed");
                 break;
             }
             ++st_aed;
+            const bool conc_ok = conc && !hp->cinfo[0] && !hp->cinfo[3];
+            if (conc_ok && !info[0] && info[1] == 0) conc_n = ns0;   // pre-AED block = post-AED block
+            if (conc_ok && conc_mode > 1 && !info[0] && info[1] > 0 && ns0 >= nw) {
+                // the deflated eigenvalues (bottom of the window) removed from the block's spectrum by
+                // nearest match; the rest keep their order
+                const int nd = info[1];
+                std::vector<int> used(ns0, 0);
+                for (int j = nw - nd; j < nw; ++j) {
+                    int best = -1;
+                    double bd = 0.0;
+                    for (int i = 0; i < ns0; ++i) {
+                        if (used[i]) continue;
+                        const double d = std::hypot(hp->cw[i].re - aw[j].re, hp->cw[i].im - aw[j].im);
+                        if (best < 0 || d < bd) { best = i; bd = d; }
+                    }
+                    if (best >= 0) used[best] = 1;
+                }
+                int k = 0;
+                for (int i = 0; i < ns0; ++i)
+                    if (!used[i]) hp->cw[k++] = hp->cw[i];
+                conc_n = k;
+            }
             if (!info[0]) {
                 const int nd = info[1];
                 m_aed = aed_full ? info[3] : 0;   // early-stopped windows carry no shifts
@@ -945,11 +1044,8 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             }
         }
         const int Nact = ihi - l + 1;   // after the AED's deflations
-        int nb = std::min(max_nb, std::max(1, Nact / 16));
-        if (m_aed >= 2) nb = std::min(nb, m_aed / 2);
-        const int C = std::max(1, std::min({max_groups, (nb + 7) / 8, 1 + Nact / (4 * (dev::kZWin + 12))}));
-        const int nbg = std::max(1, std::min(8, nb / C));
-        nb = nbg * C;
+        int C, nbg;
+        int nb = plan(Nact, m_aed >= 2 ? m_aed : (conc_n >= 2 ? conc_n : 0), C, nbg);
         const int ns = 2 * nb;
         cplx* const sh = hp->sh;   // ns values; the chase reads them from dsh
         // every 6th sweep without a deflation: exceptional shifts (LAPACK's KEXSH; stall is 0 right
@@ -962,6 +1058,13 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         bool exceptional = exc_legacy ? stall % 6 == 0 : (stall > 0 && stall % 6 == 0);
         if (!exceptional && m_aed >= 2) {   // the bottom undeflated eigenvalues of the AED window
             for (int i = 0; i < ns; ++i) sh[i] = aw[m_aed - ns + i];
+            if (hipMemcpyAsync(dsh, sh, ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
+                rc = fail(EIGSOL_E_HIP, "complex QR: shift upload");
+                break;
+            }
+        } else if (!exceptional && conc_n >= ns) {   // the concurrent workgroup's (bottom ns of them)
+            for (int i = 0; i < ns; ++i) sh[i] = hp->cw[conc_n - ns + i];
+            ++st_conc;
             if (hipMemcpyAsync(dsh, sh, ns * sizeof(cplx), hipMemcpyHostToDevice, st) != hipSuccess) {
                 rc = fail(EIGSOL_E_HIP, "complex QR: shift upload");
                 break;
@@ -1066,9 +1169,10 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             rc = fail(EIGSOL_E_HIP, "complex QR: download");
     }
     if (stats)
-        std::fprintf(stderr, "complex francis: n=%lld sweeps=%d small_blocks=%d aed=%d aed_deflated=%d\n", (long long)n,
-                     st_sweeps, st_small, st_aed, st_aed_defl);
-    for (void* p : {(void*)dw, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo, (void*)dV})
+        std::fprintf(stderr, "complex francis: n=%lld sweeps=%d small_blocks=%d aed=%d aed_deflated=%d conc_shifts=%d\n",
+                     (long long)n, st_sweeps, st_small, st_aed, st_aed_defl, st_conc);
+    for (void* p : {(void*)dw, (void*)dds, (void*)dU, (void*)dsh, (void*)dinfo, (void*)dV, (void*)dsw, (void*)dsinfo,
+                    (void*)dflag})
         if (p) (void)hipFree(p);
     if (ds) (void)hipHostFree(ds);
     if (hp) (void)hipHostFree(hp);
