@@ -705,8 +705,8 @@ struct SliceRegs {
     static constexpr int NV = (KB + kVG<S> - 1) / kVG<S>;
     using VT = vgroup_t<S>;
     VT v[NV];
-    // window slices: packed 8-bit offsets in c[0 .. KB/4); gather slices (kG): int32 columns
-    uint32_t c[kG ? KB : KB / 4];
+    // window slices: packed 8-bit offsets in c[0 .. ceil(KB/4)); gather slices (kG): int32 columns
+    uint32_t c[kG ? KB : (KB + 3) / 4];
     WT w[NW];
     int len;          // the lane's row length
 };
@@ -761,7 +761,7 @@ __device__ __forceinline__ void slice_issue(const CsrArgs<S>& a, const S* xin, i
     if (m.y >= 0) {
         const int nw = (K + 3) >> 2;
 #pragma unroll
-        for (int g = 0; g < KB / 4; ++g)
+        for (int g = 0; g < (KB + 3) / 4; ++g)
             R.c[g] = ldg_stream(scol8, (uint32_t)m.w + 64u * (uint32_t)min(g, nw - 1) + (uint32_t)lane);
         // the window always holds the slice's own rows (the Rayleigh term reads them)
         const int wl = max((m.z >> 9) & 0x1ff, 1);
@@ -846,13 +846,13 @@ __device__ __forceinline__ void slice_compute(const CsrArgs<S>& a, const S* xin,
             const S pr = mul(slice_val(R, u), xw[(R.c[u >> 2] >> (8 * (u & 3))) & 0xffu]);
             if (u < R.len) sacc = add(sacc, pr);
         }
-        for (int k0 = KB; k0 < K; k0 += 4) {       // rows longer than KB entries
+        for (int k0 = KB & ~3; k0 < K; k0 += 4) {  // rows longer than KB entries (offset words of 4)
             const uint32_t cw = ldg(scol8, (uint32_t)mc.w + 64u * (uint32_t)(k0 >> 2) + (uint32_t)lane);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const S pr = mul(ldg(sval, slice_entry<S>((uint32_t)mc.x, min(k0 + u, K - 1), lane)),
                                  xw[(cw >> (8 * u)) & 0xffu]);
-                if (k0 + u < R.len) sacc = add(sacc, pr);
+                if (k0 + u >= KB && k0 + u < R.len) sacc = add(sacc, pr);
             }
         }
         if constexpr (kPower) xi = xw[min(max(rowc + a.xoff - w0, 0), wl - 1)];
@@ -1573,6 +1573,9 @@ int csr_upload(eigsol_ctx* ctx, int dtype, int64_t nrows, int64_t ncols, int64_t
     A->max_tile_rows = max_rows;
     A->sliced = sliced ? 1 : 0;
     A->nslices = sliced ? (int32_t)(SL.meta.size() / 4) : 0;
+    // register capacity KB of a row: 4 / 8 / 12 / 16.  Measured and rejected (round 5,
+    // tools/kb10_ab.sh): KB = 10 for the headline's 10-entry rows (five 16-byte value loads per
+    // lane instead of six, the sixth a clamped repeat): 192.0 -> 263.9 us per launch
     A->slice_kb = SL.maxk <= 4 ? 4 : SL.maxk <= 8 ? 8 : SL.maxk <= 12 ? 12 : 16;
     A->slice_gather = SL.any_gather ? 1 : 0;
     A->nseg = SL.nseg;
