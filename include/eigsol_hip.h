@@ -350,6 +350,16 @@ int eigsol_hbm_probe(eigsol_ctx* ctx, size_t bytes, int reps, double* read_gbps,
 int eigsol_sparse_lu_fill(int64_t n, const int32_t* rowptr, const int32_t* colidx, int64_t cap, int64_t* nnz_out,
                           int32_t* lower_levels_out);
 
+/* The nested-dissection multifrontal plan of the general-sparse shifted solve (variant 19; host
+ * only): the ordering of the pattern of A + A^T and the supernodal structure.  perm_out (n
+ * entries, new -> old) and fronts_out (4 int32 per front: first column, pivots, struct size,
+ * parent front or -1; fronts in postorder) may be null; fronts_cap = room in fronts_out (fronts).
+ * stats_out[8] = fronts, tree heights, largest front order, most pivots of a front, stored factor
+ * entries, sum of squared front orders, factorization flops (complex arithmetic if is_complex),
+ * 1.0 when the plan is consistent.  Call once with fronts_out = null to size it. */
+int eigsol_mf_analyze(int64_t n, const int32_t* rowptr, const int32_t* colidx, int32_t leaf, int32_t is_complex,
+                      int32_t* perm_out, int32_t* fronts_out, int64_t fronts_cap, double* stats_out);
+
 #ifdef __cplusplus
 }
 #endif

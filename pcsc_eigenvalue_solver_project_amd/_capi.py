@@ -126,6 +126,7 @@ SIGNATURES = {
     "eigsol_hbm_probe": [_vp, C.c_size_t, C.c_int, _pd, _pd, _pd, _pint],
     "eigsol_ctx_info": [_vp, _pint, _pint, _pint, _pint],
     "eigsol_sparse_lu_fill": [_i64, _vp, _vp, _i64, _pi64, _pi32],
+    "eigsol_mf_analyze": [_i64, _vp, _vp, _i32, _i32, _vp, _vp, _i64, _pd],
 }
 _RESTYPES = {"eigsol_status_string": C.c_char_p, "eigsol_last_error": C.c_char_p}
 

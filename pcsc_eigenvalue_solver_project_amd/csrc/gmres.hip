@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "kernels_common.hpp"
+#include "multifrontal.hpp"
 
 namespace eigsol {
 
@@ -193,7 +194,8 @@ struct GmresSolver {
     int G = 1;
     int64_t nnzM = 0;
     int last_steps = 0;
-    int complete = 0;           // 1: K is M's exact LU (complete fill), 0: ILU(0)
+    int complete = 0;           // 1: K is M's exact LU (complete fill), 2: the multifrontal LU, 0: ILU(0)
+    MfFactor* mf = nullptr;     // complete == 2 (multifrontal.hip)
     int64_t nnzK = 0;           // entries of the factored pattern
     double last_bytes = 0.0;
     double last_relres = 0.0;
@@ -205,6 +207,7 @@ void gmres_free(GmresSolver* g) {
     hipStreamSynchronize(g->ctx->stream);
     if (g->L) shift_factor_free(g->L);
     if (g->U) shift_factor_free(g->U);
+    if (g->mf) mf_free(g->mf);
     if (g->M) csr_release(g->M);
     for (void* p : {g->V, g->Z, g->t1, g->w, g->x, (void*)g->part, (void*)g->hdev})
         if (p) hipFree(p);
@@ -348,6 +351,19 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
             g->complete = 1;
         }
     }
+    // the exact LU's fill passes the cap: the nested-dissection multifrontal LU (its own ordering,
+    // dense fronts on the matrix cores) where its plan fits the device; ILU(0) otherwise.
+    // EIGSOL_MF=0 skips it; a fill cap below 1 (ILU(0) forced) skips it too
+    {
+        double ratio = 3.0;
+        if (const char* e = std::getenv("EIGSOL_LU_FILL_CAP")) ratio = std::atof(e);
+        const char* me = std::getenv("EIGSOL_MF");
+        if (rc == EIGSOL_OK && !g->complete && ratio >= 1.0 && !(me && !std::strcmp(me, "0"))) {
+            const int mrc = mf_create(ctx, dtype, n, mrp, mci, mv.data(), &g->mf);
+            if (mrc == EIGSOL_OK) g->complete = 2;
+            else if (mrc == EIGSOL_E_HIP) rc = mrc;   // a zero pivot or a declined plan: ILU(0) below
+        }
+    }
     int32_t zpiv = 0;
     std::vector<S> lu;
     // IKJ factorization on the current pattern (mrp/mci/mv/dpos), level by level on the device
@@ -398,7 +414,7 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
             if (p) hipFree(p);
         return frc;
     };
-    if (rc == EIGSOL_OK) rc = factor();
+    if (rc == EIGSOL_OK && !g->mf) rc = factor();
     if (rc == EIGSOL_OK && zpiv && g->complete) {
         // the exact LU met a zero pivot: ILU(0) on M's own pattern (GMRES then iterates over it)
         mrp.swap(orp);
@@ -415,7 +431,7 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     if (rc == EIGSOL_OK && zpiv)
         rc = fail(EIGSOL_E_SOLVER, g->complete ? "solve_shifted: sparse LU (complete fill, no pivoting) met a zero pivot"
                                                : "solve_shifted: ILU(0) factorization met a zero pivot");
-    if (rc == EIGSOL_OK) {
+    if (rc == EIGSOL_OK && !g->mf) {
         // split: L = strict lower + unit diagonal (columns ascending: the lower part, then i), U =
         // diagonal + strict upper
         std::vector<int32_t> lrp(n + 1, 0), lci, urp(n + 1, 0), uci;
@@ -502,8 +518,11 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
     S* x = static_cast<S*>(g->x);
     S* t1 = static_cast<S*>(g->t1);
     double lb = 0.0, ub = 0.0, mb = 0.0;
-    shift_info(g->L, &lb, nullptr, nullptr);
-    shift_info(g->U, &ub, nullptr, nullptr);
+    if (g->mf) lb = mf_stats(g->mf).solve_bytes;
+    else {
+        shift_info(g->L, &lb, nullptr, nullptr);
+        shift_info(g->U, &ub, nullptr, nullptr);
+    }
     const double sb = (double)sizeof(S);
     mb = (sb + 4.0) * (double)g->nnzM + 4.0 * (double)(n + 1) + 2.0 * sb * (double)n;
     double bytes = 0.0;
@@ -517,6 +536,7 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
         return EIGSOL_OK;
     };
     auto precond = [&](const S* in, S* out) -> int {   // out = U^-1 L^-1 in
+        if (g->mf) return mf_solve(g->mf, in, out);
         EIGSOL_TRY(shift_solve_launch(g->L, in, t1));
         return shift_solve_launch(g->U, t1, out);
     };
@@ -629,8 +649,8 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
         }
     }
     EIGSOL_HIP(hipMemcpyAsync(y, x, n * sizeof(S), hipMemcpyDeviceToDevice, st));
-    EIGSOL_TRY(shift_error(g->L));
-    EIGSOL_TRY(shift_error(g->U));
+    if (g->L) EIGSOL_TRY(shift_error(g->L));
+    if (g->U) EIGSOL_TRY(shift_error(g->U));
     g->last_steps = steps;
     g->last_bytes = bytes;
     g->last_relres = relres;

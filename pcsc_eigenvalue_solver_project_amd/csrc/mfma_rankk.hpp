@@ -61,9 +61,11 @@ template <> struct MfmaOf<float> {
 template <> struct MfmaOf<cplx> : MfmaOf<double> {};
 template <> struct MfmaOf<cplxf> : MfmaOf<float> {};
 
+// One 64 x 64 tile (tile row bx, tile column by) of the update, by a 256-thread workgroup; shared by
+// rankk_mfma (one launch per update) and batched callers (multifrontal.hip: many fronts per launch).
 template <class S, bool kRT>
-__global__ __launch_bounds__(256) void rankk_mfma(int m, int nn, int K, double alpha, const S* L, int64_t ldl,
-                                                  const S* R, int64_t ldr, S* C, int64_t ldc) {
+__device__ __forceinline__ void rankk_tile(int bx, int by, int m, int nn, int K, double alpha, const S* L, int64_t ldl,
+                                           const S* R, int64_t ldr, S* C, int64_t ldc) {
     constexpr bool kC = std::is_same_v<S, cplx> || std::is_same_v<S, cplxf>;
     using M = MfmaOf<S>;
     using Real = typename M::real;
@@ -71,8 +73,8 @@ __global__ __launch_bounds__(256) void rankk_mfma(int m, int nn, int K, double a
     constexpr int KQ = RankKMax<S>::value / 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, lk = lane >> 4;
-    const int r0 = blockIdx.x * 64 + 32 * (wave & 1);
-    const int c0 = blockIdx.y * 64 + 32 * (wave >> 1);
+    const int r0 = bx * 64 + 32 * (wave & 1);
+    const int c0 = by * 64 + 32 * (wave >> 1);
     S ra[2][KQ], lb[2][KQ];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -135,6 +137,12 @@ __global__ __launch_bounds__(256) void rankk_mfma(int m, int nn, int K, double a
                         C[row + (int64_t)col * ldc] = c[ti][tj][r] + al * are[ti][tj][r];
                 }
             }
+}
+
+template <class S, bool kRT>
+__global__ __launch_bounds__(256) void rankk_mfma(int m, int nn, int K, double alpha, const S* L, int64_t ldl,
+                                                  const S* R, int64_t ldr, S* C, int64_t ldc) {
+    rankk_tile<S, kRT>(blockIdx.x, blockIdx.y, m, nn, K, alpha, L, ldl, R, ldr, C, ldc);
 }
 
 }  // namespace dev

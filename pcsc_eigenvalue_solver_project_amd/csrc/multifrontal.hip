@@ -1,0 +1,1086 @@
+// Nested-dissection multifrontal LU of M = A - sigma I on gfx950, for general sparse patterns whose
+// LU has real fill (a 2-D or 3-D mesh under any numbering).
+//
+// Replaces the SparseLU branch of solve_shifted<S> (src/matrix/solve_shifted.hpp:85-117: M = A,
+// M(i, i) -= sigma with coeffRef inserting a missing diagonal :96-102, analyzePattern + factorize
+// :104-106, solve :112-115).  SparseLU orders columns with COLAMD and factors supernodes on one
+// core; here the order is a nested dissection of the pattern of M + M^T and the factorization is
+// multifrontal, so that the work is dense blocks on the matrix cores and independent fronts run
+// side by side:
+//   * ordering (host): recursive bisection of the graph by breadth-first level structures from a
+//     pseudo-peripheral vertex; the median level, thinned to the vertices that touch the next
+//     level, is the separator; pieces of at most EIGSOL_MF_LEAF (64) vertices are leaves;
+//     disconnected pieces are split into components and the small ones packed together.  The
+//     tree is numbered in postorder, so every supernode (a leaf or a separator) owns a contiguous
+//     range of columns and its descendants come before it;
+//   * symbolic (host): struct(s) = the indices past s's columns that s's rows reach in M + M^T or
+//     through a child's struct; the front of s is the dense (ns + ms)^2 matrix on the index list
+//     [s's columns, struct(s)], column-major, resident in HBM for the factor's lifetime;
+//   * numeric (device, by tree height, all fronts of a height in the same launches): M's entries
+//     scattered into their fronts once; per height the children's Schur blocks extend-added into
+//     their parents (one launch per child rank, so the sum order is fixed); then panels of NB
+//     pivots: one workgroup per front factors its panel with partial pivoting restricted to the
+//     front's own pivot rows (no delayed pivots; a zero pivot fails the factor), swaps whole rows
+//     (LAPACK getrf style) and solves U12 = L11^-1 A12; one batched launch runs every front's
+//     trailing update A22 -= L21 U12 on the fp64 matrix cores (rankk_tile, 64 x 64 tiles, all
+//     fronts of the height in one grid).  The trailing block left after the last panel is the
+//     Schur complement the parent receives;
+//   * solve: gather b into the new numbering; forward by height (one workgroup per front: the
+//     children's contribution vectors extend-added in a fixed order, the pivot permutation, the
+//     unit-lower L11 solve by 64-row blocks - the block's triangle on one wave by lane broadcasts,
+//     the rows below as a GEMV by the workgroup - and the front's own contribution L21 y); then
+//     backward from the root (x of struct(s) gathered from the ancestors, y - U12 x, the U11
+//     solve by blocks from the bottom); scatter back.  Every sum has a fixed order: the solve is
+//     deterministic.
+// The pivoting is restricted to each front, so the factor is the exact LU of a row-permuted M
+// only when no pivot is tiny; gmres.hip therefore treats it like the no-pivot exact LU: the solve
+// is checked by its true residual and refined by GMRES cycles on the same factor when it misses.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "kernels_common.hpp"
+#include "mfma_rankk.hpp"
+#include "multifrontal.hpp"
+
+namespace eigsol {
+
+namespace dev {
+
+struct MfFront {
+    int64_t off;    // front at F + off: d x d, column-major, leading dimension d
+    int64_t uoff;   // forward contribution vector (ms entries) at u + uoff
+    int64_t sof;    // struct indices (new numbering) at sidx + sof; their positions in the parent's list at cmap + sof
+    int32_t d, ns, c0, ms;
+    int32_t ch0, ch1;   // children chl[ch0 .. ch1) (fixed order)
+    int32_t parent;
+    int32_t pad;
+};
+
+__device__ __forceinline__ double mf_rl(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ cplx mf_rl(cplx v, int src) { return cplx{mf_rl(v.re, src), mf_rl(v.im, src)}; }
+
+// M's entries into their fronts: F[dst[e]] = v[e] (every destination distinct)
+template <class S>
+__global__ __launch_bounds__(256) void mf_scatter_kernel(const int64_t* dst, const S* v, int64_t nnz, S* F) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e < nnz) F[dst[e]] = v[e];
+}
+
+// extend-add of one child's Schur block into its parent: tab = (child, first column) pairs, 64
+// columns per workgroup; children of one parent are in different launches (fixed order)
+template <class S>
+__global__ __launch_bounds__(256) void mf_extend_kernel(const MfFront* fr, const int32_t* tab, const int32_t* cmap,
+                                                        S* F) {
+    const int32_t c = tab[2 * blockIdx.x], col0 = tab[2 * blockIdx.x + 1];
+    const MfFront fc = fr[c];
+    const MfFront fp = fr[fc.parent];
+    const int32_t* map = cmap + fc.sof;
+    const S* src = F + fc.off + (int64_t)fc.ns * (fc.d + 1);
+    S* dst = F + fp.off;
+    const int cend = min(fc.ms, col0 + 64);
+    for (int cc = col0; cc < cend; ++cc) {
+        const int64_t pc = (int64_t)map[cc] * fp.d;
+        const S* sc = src + (int64_t)cc * fc.d;
+        for (int r = threadIdx.x; r < fc.ms; r += 256) {
+            const int64_t o = pc + map[r];
+            dst[o] = add(dst[o], sc[r]);
+        }
+    }
+}
+
+// Panel q of every front in list[0 .. gridDim.x): pivots k0 .. k0 + kb - 1 (k0 = q NB), each the
+// first row of largest modulus among the front's remaining pivot rows [k, ns); the whole row
+// swapped (all d columns), the column below the diagonal scaled, the panel's other columns
+// rank-1 updated; then U12 = L11^-1 A12 on the columns right of the panel (one column per thread).
+template <class S, int NB>
+__global__ __launch_bounds__(256) void mf_panel_kernel(const MfFront* fr, const int32_t* list, int q, S* F,
+                                                       int32_t* piv, int32_t* zpiv) {
+    __shared__ double sv[4];
+    __shared__ int si[4];
+    __shared__ int s_p;
+    __shared__ S l11[NB * NB];
+    const MfFront f = fr[list[blockIdx.x]];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int d = f.d, ns = f.ns;
+    const int k0 = q * NB, kb = min(NB, ns - k0), c1 = k0 + kb;
+    S* A = F + f.off;
+    for (int k = k0; k < c1; ++k) {
+        double best = -1.0;
+        int bi = k;
+        for (int i = k + tid; i < ns; i += 256) {
+            const double s = sq_abs(A[i + (int64_t)k * d]);
+            if (s > best) { best = s; bi = i; }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ob = __shfl_xor(best, off, 64);
+            const int oi = __shfl_xor(bi, off, 64);
+            if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        }
+        if (lane == 0) { sv[wv] = best; si[wv] = bi; }
+        __syncthreads();
+        if (tid == 0) {
+            double b = sv[0];
+            int p = si[0];
+            for (int w = 1; w < 4; ++w)
+                if (sv[w] > b || (sv[w] == b && si[w] < p)) { b = sv[w]; p = si[w]; }
+            s_p = p;
+            piv[f.c0 + k] = p;
+            if (!(b > 0.0)) atomicOr(zpiv, 1);
+        }
+        __syncthreads();
+        const int p = s_p;
+        if (p != k)
+            for (int j = tid; j < d; j += 256) {
+                const S t = A[k + (int64_t)j * d];
+                A[k + (int64_t)j * d] = A[p + (int64_t)j * d];
+                A[p + (int64_t)j * d] = t;
+            }
+        __syncthreads();
+        const S dk = A[k + (int64_t)k * d];
+        if (sq_abs(dk) > 0.0)
+            for (int i = k + 1 + tid; i < d; i += 256) A[i + (int64_t)k * d] = sdiv(A[i + (int64_t)k * d], dk);
+        __syncthreads();
+        const int m = d - k - 1, w = c1 - k - 1;
+        for (int e = tid; e < m * w; e += 256) {
+            const int i = k + 1 + e % m, j = k + 1 + e / m;
+            A[i + (int64_t)j * d] = sub(A[i + (int64_t)j * d], mul(A[i + (int64_t)k * d], A[k + (int64_t)j * d]));
+        }
+        __syncthreads();
+    }
+    for (int e = tid; e < kb * kb; e += 256) {
+        const int i = e % kb, j = e / kb;
+        l11[i + j * NB] = A[(k0 + i) + (int64_t)(k0 + j) * d];
+    }
+    __syncthreads();
+    for (int c = c1 + tid; c < d; c += 256) {
+        S* col = A + (int64_t)c * d + k0;
+        S x[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) x[i] = i < kb ? col[i] : s_zero<S>();
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j) {
+            if (j < kb) {
+#pragma unroll
+                for (int i = j + 1; i < NB; ++i) x[i] = sub(x[i], mul(l11[i + j * NB], x[j]));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+            if (i < kb) col[i] = x[i];
+    }
+}
+
+// trailing update of panel q, every front of the launch: tab = (front, tile row, tile column)
+template <class S, int NB>
+__global__ __launch_bounds__(256) void mf_gemm_kernel(const MfFront* fr, const int32_t* tab, int q, S* F) {
+    const int32_t s = tab[3 * blockIdx.x], tr = tab[3 * blockIdx.x + 1], tc = tab[3 * blockIdx.x + 2];
+    const MfFront f = fr[s];
+    const int d = f.d, k0 = q * NB, kb = min(NB, f.ns - k0), c1 = k0 + kb, m = d - c1;
+    S* A = F + f.off;
+    rankk_tile<S, true>(tr, tc, m, m, kb, -1.0, A + c1 + (int64_t)k0 * d, d, A + k0 + (int64_t)c1 * d, d,
+                        A + c1 + (int64_t)c1 * d, d);
+}
+
+// ---------------------------------------------------------------- solve
+// w = b in the new numbering
+template <class S>
+__global__ __launch_bounds__(256) void mf_gather_kernel(const int32_t* perm, const S* b, S* w, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) w[i] = b[perm[i]];
+}
+template <class S>
+__global__ __launch_bounds__(256) void mf_scatter_out_kernel(const int32_t* perm, const S* x, S* out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[perm[i]] = x[i];
+}
+
+// forward: fronts list[0 .. gridDim.x) of one height.  LDS: r (ns), y (ns), acc (ms).
+template <class S>
+__global__ __launch_bounds__(256) void mf_fwd_kernel(const MfFront* fr, const int32_t* list, const int32_t* chl,
+                                                     const S* F, const int32_t* cmap, const int32_t* pinv, S* w,
+                                                     S* u) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const MfFront f = fr[list[blockIdx.x]];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int d = f.d, ns = f.ns, ms = f.ms;
+    S* r = reinterpret_cast<S*>(lds_raw);
+    S* y = r + ns;
+    S* acc = y + ns;
+    for (int t = tid; t < ns; t += 256) r[t] = w[f.c0 + t];
+    for (int t = tid; t < ms; t += 256) acc[t] = s_zero<S>();
+    __syncthreads();
+    for (int k = f.ch0; k < f.ch1; ++k) {
+        const MfFront c = fr[chl[k]];
+        const int32_t* map = cmap + c.sof;
+        const S* uc = u + c.uoff;
+        for (int t = tid; t < c.ms; t += 256) {
+            const int pos = map[t];
+            const S v = uc[t];
+            if (pos < ns) r[pos] = sub(r[pos], v);
+            else acc[pos - ns] = add(acc[pos - ns], v);
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < ns; t += 256) y[t] = r[pinv[f.c0 + t]];
+    __syncthreads();
+    const S* A = F + f.off;
+    for (int jb = 0; jb < ns; jb += 64) {
+        const int bw = min(64, ns - jb);
+        if (wv == 0) {
+            S v = lane < bw ? y[jb + lane] : s_zero<S>();
+            const int row = jb + min(lane, bw - 1);
+            for (int j0 = 0; j0 < bw; j0 += 16) {
+                S lv[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) lv[t] = A[row + (int64_t)(jb + min(j0 + t, bw - 1)) * d];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int j = j0 + t;
+                    if (j < bw) {
+                        const S yj = mf_rl(v, j);
+                        if (lane > j) v = sub(v, mul(lv[t], yj));
+                    }
+                }
+            }
+            if (lane < bw) y[jb + lane] = v;
+        }
+        __syncthreads();
+        for (int i = jb + bw + tid; i < d; i += 256) {
+            S s = s_zero<S>();
+            const S* Ai = A + i + (int64_t)jb * d;
+            for (int j0 = 0; j0 < bw; j0 += 16) {
+                S lv[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) lv[t] = Ai[(int64_t)min(j0 + t, bw - 1) * d];
+#pragma unroll
+                for (int t = 0; t < 16; ++t)
+                    if (j0 + t < bw) s = add(s, mul(lv[t], y[jb + j0 + t]));
+            }
+            if (i < ns) y[i] = sub(y[i], s);
+            else acc[i - ns] = add(acc[i - ns], s);
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < ns; t += 256) w[f.c0 + t] = y[t];
+    for (int t = tid; t < ms; t += 256) u[f.uoff + t] = acc[t];
+}
+
+// backward: fronts list[0 .. gridDim.x) of one height (their ancestors solved).  LDS: t (ns), xs (ms).
+template <class S>
+__global__ __launch_bounds__(256) void mf_bwd_kernel(const MfFront* fr, const int32_t* list, const S* F,
+                                                     const int32_t* sidx, const S* w, S* x) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const MfFront f = fr[list[blockIdx.x]];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int d = f.d, ns = f.ns, ms = f.ms;
+    S* t = reinterpret_cast<S*>(lds_raw);
+    S* xs = t + ns;
+    for (int q = tid; q < ms; q += 256) xs[q] = x[sidx[f.sof + q]];
+    __syncthreads();
+    const S* A = F + f.off;
+    for (int k = tid; k < ns; k += 256) {
+        S s = s_zero<S>();
+        const S* Ak = A + k + (int64_t)ns * d;
+        int q0 = 0;
+        for (; q0 + 8 <= ms; q0 += 8) {
+            S uv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) uv[e] = Ak[(int64_t)(q0 + e) * d];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s = add(s, mul(uv[e], xs[q0 + e]));
+        }
+        for (; q0 < ms; ++q0) s = add(s, mul(Ak[(int64_t)q0 * d], xs[q0]));
+        t[k] = sub(w[f.c0 + k], s);
+    }
+    __syncthreads();
+    for (int jb = ((ns - 1) / 64) * 64; jb >= 0; jb -= 64) {
+        const int bw = min(64, ns - jb);
+        if (wv == 0) {
+            S v = lane < bw ? t[jb + lane] : s_zero<S>();
+            const int row = jb + min(lane, bw - 1);
+            for (int j1 = bw; j1 > 0; j1 -= 16) {
+                S uv[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) uv[e] = A[row + (int64_t)(jb + max(j1 - 1 - e, 0)) * d];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int j = j1 - 1 - e;
+                    if (j >= 0) {
+                        if (lane == j) v = sdiv(v, uv[e]);
+                        const S xj = mf_rl(v, j);
+                        if (lane < j) v = sub(v, mul(uv[e], xj));
+                    }
+                }
+            }
+            if (lane < bw) t[jb + lane] = v;
+        }
+        __syncthreads();
+        for (int i = tid; i < jb; i += 256) {
+            S s = s_zero<S>();
+            const S* Ai = A + i + (int64_t)jb * d;
+            for (int j0 = 0; j0 < bw; j0 += 16) {
+                S uv[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) uv[e] = Ai[(int64_t)min(j0 + e, bw - 1) * d];
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (j0 + e < bw) s = add(s, mul(uv[e], t[jb + j0 + e]));
+            }
+            t[i] = sub(t[i], s);
+        }
+        __syncthreads();
+    }
+    for (int k = tid; k < ns; k += 256) x[f.c0 + k] = t[k];
+}
+
+}  // namespace dev
+
+// ================================================================== host side
+struct MfFactor {
+    eigsol_ctx* ctx = nullptr;
+    int dtype = EIGSOL_F64;
+    int64_t n = 0;
+    int nb = 32;
+    int64_t nfront = 0;
+    dev::MfFront* fronts = nullptr;
+    int32_t* chl = nullptr;
+    int32_t* sidx = nullptr;
+    int32_t* cmap = nullptr;
+    int32_t* perm = nullptr;   // new -> old
+    int32_t* pinv = nullptr;   // composite pivot permutation, per front local
+    int32_t* lists = nullptr;  // fronts by height, each height's list by descending ns
+    void* F = nullptr;
+    void* u = nullptr;
+    void* w = nullptr;
+    void* x = nullptr;
+    std::vector<int64_t> hstart;      // lists[hstart[h] .. hstart[h + 1])
+    std::vector<int32_t> lds_fwd, lds_bwd;   // dynamic LDS bytes per height
+    MfStats st;
+};
+
+void mf_free(MfFactor* f) {
+    if (!f) return;
+    hipSetDevice(f->ctx->device);
+    hipStreamSynchronize(f->ctx->stream);
+    for (void* p : {(void*)f->fronts, (void*)f->chl, (void*)f->sidx, (void*)f->cmap, (void*)f->perm, (void*)f->pinv,
+                    (void*)f->lists, f->F, f->u, f->w, f->x})
+        if (p) hipFree(p);
+    ctx_release(f->ctx);
+    delete f;
+}
+
+const MfStats& mf_stats(const MfFactor* f) { return f->st; }
+
+namespace {
+
+struct SymGraph {
+    std::vector<int64_t> ptr;
+    std::vector<int32_t> adj;
+};
+
+// pattern of M + M^T without the diagonal, each list sorted and unique
+void sym_graph(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, SymGraph& g) {
+    std::vector<int64_t> deg(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int32_t e = rp[i]; e < rp[i + 1]; ++e)
+            if (ci[e] != i) { ++deg[i + 1]; ++deg[ci[e] + 1]; }
+    std::vector<int64_t> p(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) p[i + 1] = p[i] + deg[i + 1];
+    std::vector<int32_t> adj(p[n]);
+    {
+        std::vector<int64_t> fill(p.begin(), p.end() - 1);
+        for (int64_t i = 0; i < n; ++i)
+            for (int32_t e = rp[i]; e < rp[i + 1]; ++e)
+                if (ci[e] != i) { adj[fill[i]++] = ci[e]; adj[fill[ci[e]]++] = (int32_t)i; }
+    }
+    g.ptr.assign(n + 1, 0);
+    int64_t o = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        auto b = adj.begin() + p[i], e = adj.begin() + p[i + 1];
+        std::sort(b, e);
+        const int64_t u = std::unique(b, e) - b;
+        std::copy(b, b + u, adj.begin() + o);
+        o += u;
+        g.ptr[i + 1] = o;
+    }
+    adj.resize(o);
+    g.adj.swap(adj);
+}
+
+struct NdNode {
+    std::vector<int32_t> members;
+    int32_t parent;
+};
+
+// Nested dissection of the vertices of g: tree nodes (leaves and separators) with parents.
+void nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNode>& tree) {
+    struct Task {
+        std::vector<int32_t> nodes;
+        int32_t parent;
+    };
+    std::vector<Task> stack;
+    {
+        Task t;
+        t.nodes.resize(n);
+        std::iota(t.nodes.begin(), t.nodes.end(), 0);
+        t.parent = -1;
+        stack.push_back(std::move(t));
+    }
+    std::vector<int64_t> inset(n, -1), seen(n, -1);
+    std::vector<int32_t> level(n, 0), q;
+    int64_t stamp = 0, bstamp = 0;
+    // BFS inside the current task's set from root: q holds the visit order, level[] the levels
+    auto bfs = [&](int32_t root, int64_t tag) -> int32_t {
+        const int64_t b = ++bstamp;
+        q.clear();
+        q.push_back(root);
+        seen[root] = b;
+        level[root] = 0;
+        int32_t depth = 0;
+        for (size_t h = 0; h < q.size(); ++h) {
+            const int32_t v = q[h];
+            for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
+                const int32_t w = g.adj[e];
+                if (inset[w] != tag || seen[w] == b) continue;
+                seen[w] = b;
+                level[w] = level[v] + 1;
+                depth = std::max(depth, level[w]);
+                q.push_back(w);
+            }
+        }
+        return depth;
+    };
+    auto sub_degree = [&](int32_t v, int64_t tag) {
+        int32_t dgr = 0;
+        for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) dgr += inset[g.adj[e]] == tag;
+        return dgr;
+    };
+    while (!stack.empty()) {
+        Task t = std::move(stack.back());
+        stack.pop_back();
+        const int64_t sz = (int64_t)t.nodes.size();
+        if (sz == 0) continue;
+        if (sz <= leaf) {
+            tree.push_back(NdNode{std::move(t.nodes), t.parent});
+            continue;
+        }
+        const int64_t tag = ++stamp;
+        for (int32_t v : t.nodes) inset[v] = tag;
+        bfs(t.nodes[0], tag);
+        if ((int64_t)q.size() < sz) {
+            // disconnected: components; the small ones packed into leaves, the others new tasks
+            std::vector<std::vector<int32_t>> comps;
+            const int64_t b0 = bstamp;   // the first component's BFS; every later one has a larger stamp
+            comps.push_back(q);
+            for (int32_t v : t.nodes) {
+                if (seen[v] >= b0) continue;
+                bfs(v, tag);
+                comps.push_back(q);
+            }
+            std::vector<int32_t> pack;
+            for (auto& c : comps) {
+                if ((int64_t)c.size() > leaf) {
+                    stack.push_back(Task{std::move(c), t.parent});
+                    continue;
+                }
+                if ((int64_t)(pack.size() + c.size()) > leaf) {
+                    tree.push_back(NdNode{std::move(pack), t.parent});
+                    pack.clear();
+                }
+                pack.insert(pack.end(), c.begin(), c.end());
+            }
+            if (!pack.empty()) tree.push_back(NdNode{std::move(pack), t.parent});
+            continue;
+        }
+        // pseudo-peripheral root (George-Liu): restart from a minimum-degree vertex of the last
+        // level while the eccentricity grows
+        int32_t root = t.nodes[0];
+        int32_t ecc = bfs(root, tag);
+        for (int round = 0; round < 2; ++round) {
+            int32_t best = -1, bd = INT32_MAX;
+            for (size_t h = q.size(); h-- > 0;) {
+                const int32_t v = q[h];
+                if (level[v] != ecc) break;
+                const int32_t dv = sub_degree(v, tag);
+                if (dv < bd) { bd = dv; best = v; }
+            }
+            const int32_t e2 = bfs(best, tag);
+            if (e2 <= ecc) {
+                if (e2 < ecc) ecc = bfs(root, tag);   // restore the levels of the better root
+                break;
+            }
+            root = best;
+            ecc = e2;
+        }
+        const int32_t nlev = ecc + 1;
+        if (nlev < 3) {   // no level structure to cut: one dense front
+            tree.push_back(NdNode{std::move(t.nodes), t.parent});
+            continue;
+        }
+        std::vector<int64_t> cnt(nlev, 0);
+        for (int32_t v : t.nodes) ++cnt[level[v]];
+        int32_t m = 1;
+        {
+            int64_t cum = 0;
+            for (int32_t l = 0; l < nlev; ++l) {
+                if (2 * (cum + cnt[l] / 2) >= sz) { m = l; break; }
+                cum += cnt[l];
+            }
+            m = std::max(1, std::min(nlev - 2, m));
+        }
+        // separator: the vertices of level m that touch level m + 1; the rest of level m joins A
+        std::vector<int32_t> A, B, Sep;
+        for (int32_t v : t.nodes) {
+            const int32_t l = level[v];
+            if (l < m) A.push_back(v);
+            else if (l > m) B.push_back(v);
+            else {
+                bool touch = false;
+                for (int64_t e = g.ptr[v]; e < g.ptr[v + 1] && !touch; ++e)
+                    touch = inset[g.adj[e]] == tag && level[g.adj[e]] == m + 1;
+                (touch ? Sep : A).push_back(v);
+            }
+        }
+        const int32_t id = (int32_t)tree.size();
+        tree.push_back(NdNode{std::move(Sep), t.parent});
+        std::vector<int32_t>().swap(t.nodes);
+        stack.push_back(Task{std::move(A), id});
+        stack.push_back(Task{std::move(B), id});
+    }
+}
+
+// The ordering and symbolic structure (host only): fronts in postorder with their columns,
+// structs, children, parent maps; per-height lists; work and size figures.
+struct MfPlan {
+    int64_t nt = 0;
+    std::vector<int32_t> perm, iperm, snode, chl, sidx, cmap, height, lists;
+    std::vector<int64_t> sof, hstart;
+    std::vector<dev::MfFront> fr;
+    int32_t H = 0;
+    int64_t maxd = 0, maxns = 0, uo = 0;
+    double fe = 0.0, fac = 0.0, flops = 0.0;
+};
+
+// returns false on an internal inconsistency (a struct entry outside the ancestors)
+bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int leaf, bool cplx_flops,
+             MfPlan& P) {
+    static const bool dbg = std::getenv("EIGSOL_MF_DEBUG") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!dbg) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[mf] %s %.3f s\n", what, std::chrono::duration<double>(t - tp).count());
+        tp = t;
+    };
+    // the graph relabelled in breadth-first order (neighbours get nearby labels: the many BFS
+    // passes of the dissection then walk memory locally whatever the caller's numbering)
+    SymGraph g;
+    std::vector<int32_t> ord(n);   // label -> caller's index
+    {
+        SymGraph g0;
+        sym_graph(n, rp, ci, g0);
+        std::vector<char> done(n, 0);
+        int64_t head = 0, tail = 0;
+        for (int64_t s0 = 0; s0 < n; ++s0) {
+            if (done[s0]) continue;
+            done[s0] = 1;
+            ord[tail++] = (int32_t)s0;
+            while (head < tail) {
+                const int32_t v = ord[head++];
+                for (int64_t e = g0.ptr[v]; e < g0.ptr[v + 1]; ++e)
+                    if (!done[g0.adj[e]]) { done[g0.adj[e]] = 1; ord[tail++] = g0.adj[e]; }
+            }
+        }
+        std::vector<int32_t> lab(n);
+        for (int64_t k = 0; k < n; ++k) lab[ord[k]] = (int32_t)k;
+        g.ptr.assign(n + 1, 0);
+        g.adj.resize(g0.adj.size());
+        for (int64_t k = 0; k < n; ++k) {
+            const int32_t v = ord[k];
+            int64_t o = g.ptr[k];
+            for (int64_t e = g0.ptr[v]; e < g0.ptr[v + 1]; ++e) g.adj[o++] = lab[g0.adj[e]];
+            std::sort(g.adj.begin() + g.ptr[k], g.adj.begin() + o);
+            g.ptr[k + 1] = o;
+        }
+    }
+    lap("graph");
+    std::vector<NdNode> tree;
+    nested_dissection(n, g, leaf, tree);
+    lap("dissection");
+    // postorder numbering: children before parents, each tree node one contiguous column range
+    const int64_t nt = (int64_t)tree.size();
+    P.nt = nt;
+    std::vector<int32_t> post;   // tree node of each front (postorder)
+    post.reserve(nt);
+    {
+        std::vector<std::vector<int32_t>> kids(nt);
+        std::vector<int32_t> roots;
+        for (int64_t i = 0; i < nt; ++i) {
+            if (tree[i].parent < 0) roots.push_back((int32_t)i);
+            else kids[tree[i].parent].push_back((int32_t)i);
+        }
+        std::vector<std::pair<int32_t, size_t>> st;
+        for (int32_t r : roots) {
+            st.push_back({r, 0});
+            while (!st.empty()) {
+                auto& top = st.back();
+                if (top.second < kids[top.first].size()) {
+                    const int32_t c = kids[top.first][top.second++];
+                    st.push_back({c, 0});
+                } else {
+                    post.push_back(top.first);
+                    st.pop_back();
+                }
+            }
+        }
+    }
+    std::vector<int32_t> front_of_node(nt);
+    for (int64_t s = 0; s < nt; ++s) front_of_node[post[s]] = (int32_t)s;
+    P.perm.assign(n, 0);
+    P.iperm.assign(n, 0);
+    P.snode.assign(n, 0);
+    P.fr.assign(nt, dev::MfFront{});
+    auto& fr = P.fr;
+    {
+        int32_t c = 0;
+        for (int64_t s = 0; s < nt; ++s) {
+            const NdNode& nd = tree[post[s]];
+            fr[s].c0 = c;
+            fr[s].ns = (int32_t)nd.members.size();
+            fr[s].parent = nd.parent < 0 ? -1 : front_of_node[nd.parent];
+            for (int32_t v : nd.members) {
+                P.perm[c] = v;
+                P.iperm[v] = c;
+                P.snode[c] = (int32_t)s;
+                ++c;
+            }
+        }
+    }
+    std::vector<NdNode>().swap(tree);
+    // children lists (postorder, i.e. the fixed extend-add order)
+    auto& chl = P.chl;
+    {
+        std::vector<std::vector<int32_t>> ch(nt);
+        for (int64_t s = 0; s < nt; ++s)
+            if (fr[s].parent >= 0) ch[fr[s].parent].push_back((int32_t)s);
+        for (int64_t s = 0; s < nt; ++s) {
+            fr[s].ch0 = (int32_t)chl.size();
+            chl.insert(chl.end(), ch[s].begin(), ch[s].end());
+            fr[s].ch1 = (int32_t)chl.size();
+        }
+    }
+    // symbolic: struct(s) = indices >= c1 reached from s's rows in M + M^T or through a child's struct
+    auto& sidx = P.sidx;
+    auto& sof = P.sof;
+    sof.assign(nt + 1, 0);
+    {
+        std::vector<int64_t> mark(n, -1);
+        std::vector<int32_t> lst;
+        for (int64_t s = 0; s < nt; ++s) {
+            const int32_t c0 = fr[s].c0, c1 = c0 + fr[s].ns;
+            lst.clear();
+            for (int32_t i = c0; i < c1; ++i) {
+                const int32_t v = P.perm[i];
+                for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
+                    const int32_t j = P.iperm[g.adj[e]];
+                    if (j >= c1 && mark[j] != s) { mark[j] = s; lst.push_back(j); }
+                }
+            }
+            for (int32_t k = fr[s].ch0; k < fr[s].ch1; ++k) {
+                const int32_t c = chl[k];
+                for (int64_t e = sof[c]; e < sof[c + 1]; ++e) {
+                    const int32_t j = sidx[e];
+                    if (j >= c1 && mark[j] != s) { mark[j] = s; lst.push_back(j); }
+                }
+            }
+            std::sort(lst.begin(), lst.end());
+            sidx.insert(sidx.end(), lst.begin(), lst.end());
+            sof[s + 1] = (int64_t)sidx.size();
+            fr[s].ms = (int32_t)lst.size();
+            fr[s].sof = sof[s];
+            fr[s].d = fr[s].ns + fr[s].ms;
+        }
+    }
+    std::vector<int64_t>().swap(g.ptr);
+    std::vector<int32_t>().swap(g.adj);
+    // labels -> the caller's indices
+    for (int64_t c = 0; c < n; ++c) {
+        P.perm[c] = ord[P.perm[c]];
+        P.iperm[P.perm[c]] = (int32_t)c;
+    }
+    lap("symbolic");
+    // sizes and work
+    for (int64_t s = 0; s < nt; ++s) {
+        const double d = fr[s].d, ns = fr[s].ns;
+        fr[s].off = (int64_t)P.fe;
+        fr[s].uoff = P.uo;
+        P.uo += fr[s].ms;
+        P.fe += d * d;
+        P.fac += ns * (2.0 * d - ns);
+        // sum_{k < ns} 2 (d - k - 1)^2 multiply-adds ~ 2 (ns d^2 - ns^2 d + ns^3 / 3)
+        P.flops += 2.0 * (ns * d * d - ns * ns * d + ns * ns * ns / 3.0);
+        P.maxd = std::max<int64_t>(P.maxd, fr[s].d);
+        P.maxns = std::max<int64_t>(P.maxns, fr[s].ns);
+    }
+    if (cplx_flops) P.flops *= 4.0;
+    // heights and the per-height front lists (descending ns: each panel's fronts are a prefix)
+    P.height.assign(nt, 0);
+    P.H = 0;
+    for (int64_t s = 0; s < nt; ++s) {
+        for (int32_t k = fr[s].ch0; k < fr[s].ch1; ++k) P.height[s] = std::max(P.height[s], P.height[chl[k]] + 1);
+        P.H = std::max(P.H, P.height[s]);
+    }
+    P.hstart.assign(P.H + 2, 0);
+    {
+        std::vector<std::vector<int32_t>> byh(P.H + 1);
+        for (int64_t s = 0; s < nt; ++s) byh[P.height[s]].push_back((int32_t)s);
+        for (int32_t h = 0; h <= P.H; ++h) {
+            std::stable_sort(byh[h].begin(), byh[h].end(), [&](int32_t a, int32_t b) { return fr[a].ns > fr[b].ns; });
+            P.lists.insert(P.lists.end(), byh[h].begin(), byh[h].end());
+            P.hstart[h + 1] = (int64_t)P.lists.size();
+        }
+    }
+    lap("heights");
+    // parent positions of every child's struct entries
+    P.cmap.assign(sidx.size(), 0);
+    for (int64_t s = 0; s < nt; ++s) {
+        const int32_t p = fr[s].parent;
+        if (p < 0) {
+            if (fr[s].ms) return false;   // a root reaches nothing past itself
+            continue;
+        }
+        const int32_t pc0 = fr[p].c0, pc1 = pc0 + fr[p].ns;
+        const int32_t* ps = sidx.data() + sof[p];
+        const int32_t pm = fr[p].ms;
+        int32_t cur = 0;
+        for (int64_t e = sof[s]; e < sof[s + 1]; ++e) {
+            const int32_t j = sidx[e];
+            if (j < pc0) return false;   // struct(s) must lie in the ancestors
+            if (j < pc1) P.cmap[e] = j - pc0;
+            else {
+                while (cur < pm && ps[cur] < j) ++cur;   // both ascending
+                if (cur == pm || ps[cur] != j) return false;
+                P.cmap[e] = fr[p].ns + cur;
+            }
+        }
+    }
+    return true;
+}
+
+template <class S>
+int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
+                const S* vals, MfFactor** out) {
+    *out = nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    constexpr int NB = dev::RankKMax<S>::value;
+    const int64_t sb = (int64_t)sizeof(S);
+    int leaf = 64;
+    if (const char* e = std::getenv("EIGSOL_MF_LEAF")) leaf = std::max(4, std::atoi(e));
+    MfPlan P;
+    if (!mf_plan(n, rp, ci, leaf, is_cplx_v<S>, P)) return EIGSOL_E_UNSUPPORTED;
+    const int64_t nt = P.nt;
+    auto& fr = P.fr;
+    const auto& chl = P.chl;
+    const auto& sidx = P.sidx;
+    const auto& sof = P.sof;
+    const auto& lists = P.lists;
+    const auto& hstart = P.hstart;
+    const int32_t H = P.H;
+    const double fe = P.fe, fac = P.fac;
+    const int64_t uo = P.uo;
+    MfStats stt;
+    stt.fronts = nt;
+    stt.heights = H + 1;
+    stt.max_front = P.maxd;
+    stt.max_pivots = P.maxns;
+    stt.front_entries = fe;
+    stt.factor_entries = fac;
+    stt.flops = P.flops;
+    // bounds: device memory for the fronts, the solve kernels' LDS, the work
+    size_t fr_b = 0, tot_b = 0;
+    hipMemGetInfo(&fr_b, &tot_b);
+    double cap = 0.45 * (double)fr_b;
+    if (const char* e = std::getenv("EIGSOL_MF_MAX_GB")) cap = std::min(cap, std::atof(e) * 1073741824.0);
+    const double lds_max = 120.0 * 1024.0;
+    if (fe * (double)sb > cap || (double)(P.maxns + P.maxd) * (double)sb > lds_max || P.flops > 4e13)
+        return EIGSOL_E_UNSUPPORTED;
+    // destinations of M's entries (the caller's numbering) in the fronts
+    const int64_t nnz = rp[n];
+    std::vector<int64_t> dst(nnz);
+    auto pos_in = [&](int32_t s, int32_t j) -> int64_t {
+        const int32_t c0 = fr[s].c0;
+        if (j < c0 + fr[s].ns) return j - c0;
+        const int32_t* b = sidx.data() + sof[s];
+        const int64_t k = std::lower_bound(b, b + fr[s].ms, j) - b;
+        return (k < fr[s].ms && b[k] == j) ? fr[s].ns + k : -1;
+    };
+    for (int64_t r = 0; r < n; ++r)
+        for (int32_t e = rp[r]; e < rp[r + 1]; ++e) {
+            const int32_t i = P.iperm[r], j = P.iperm[ci[e]];
+            const int32_t s = P.snode[std::min(i, j)];
+            const int64_t pi = pos_in(s, i), pj = pos_in(s, j);
+            if (pi < 0 || pj < 0) return EIGSOL_E_UNSUPPORTED;   // not in the front: an inconsistent plan
+            dst[e] = fr[s].off + pi + pj * (int64_t)fr[s].d;
+        }
+    // launch tables: extend-add (child, first column) per (height, child rank); trailing-update
+    // tiles (front, tile row, tile column) per (height, panel)
+    struct Launch {
+        int kind;   // 0 extend, 1 panel, 2 gemm
+        int32_t h, q;
+        int64_t off, cnt;
+    };
+    std::vector<Launch> plan;
+    std::vector<int32_t> tab;
+    for (int32_t h = 0; h <= H; ++h) {
+        const int32_t* L = lists.data() + hstart[h];
+        const int64_t cnt = hstart[h + 1] - hstart[h];
+        int32_t maxch = 0, maxq = 0;
+        for (int64_t t = 0; t < cnt; ++t) {
+            maxch = std::max(maxch, fr[L[t]].ch1 - fr[L[t]].ch0);
+            maxq = std::max(maxq, (fr[L[t]].ns + NB - 1) / NB);
+        }
+        for (int32_t j = 0; j < maxch; ++j) {
+            const int64_t o = (int64_t)tab.size();
+            for (int64_t t = 0; t < cnt; ++t) {
+                const dev::MfFront& p = fr[L[t]];
+                if (p.ch1 - p.ch0 <= j) continue;
+                const int32_t c = chl[p.ch0 + j];
+                for (int32_t c0 = 0; c0 < fr[c].ms; c0 += 64) { tab.push_back(c); tab.push_back(c0); }
+            }
+            const int64_t k = ((int64_t)tab.size() - o) / 2;
+            if (k) plan.push_back(Launch{0, h, j, o, k});
+        }
+        for (int32_t q = 0; q < maxq; ++q) {
+            int64_t np = 0;
+            while (np < cnt && fr[L[np]].ns > q * NB) ++np;
+            plan.push_back(Launch{1, h, q, hstart[h], np});
+            const int64_t o = (int64_t)tab.size();
+            for (int64_t t = 0; t < np; ++t) {
+                const dev::MfFront& f = fr[L[t]];
+                const int32_t c1 = std::min(f.ns, (q + 1) * NB), m = f.d - c1;
+                const int32_t nt64 = (m + 63) / 64;
+                for (int32_t a = 0; a < nt64; ++a)
+                    for (int32_t b = 0; b < nt64; ++b) { tab.push_back(L[t]); tab.push_back(a); tab.push_back(b); }
+            }
+            const int64_t k = ((int64_t)tab.size() - o) / 3;
+            if (k) plan.push_back(Launch{2, h, q, o, k});
+        }
+    }
+    stt.order_seconds = std::chrono::duration<double>(clk::now() - t0).count();
+    // ---- device
+    auto* f = new MfFactor();
+    f->ctx = ctx;
+    ctx_retain(ctx);
+    f->dtype = dtype;
+    f->n = n;
+    f->nb = NB;
+    f->nfront = nt;
+    f->hstart = hstart;
+    f->lds_fwd.assign(H + 1, 0);
+    f->lds_bwd.assign(H + 1, 0);
+    for (int32_t h = 0; h <= H; ++h)
+        for (int64_t t = hstart[h]; t < hstart[h + 1]; ++t) {
+            const dev::MfFront& q = fr[lists[t]];
+            f->lds_fwd[h] = std::max<int32_t>(f->lds_fwd[h], (int32_t)((2 * q.ns + q.ms) * sb));
+            f->lds_bwd[h] = std::max<int32_t>(f->lds_bwd[h], (int32_t)((q.ns + q.ms) * sb));
+        }
+    hipStream_t st = ctx->stream;
+    int rc = EIGSOL_OK;
+    int32_t *d_tab = nullptr, *d_piv = nullptr, *d_z = nullptr;
+    int64_t* d_dst = nullptr;
+    S* d_v = nullptr;
+    auto dm = [&](void** p, size_t bytes) {
+        if (rc == EIGSOL_OK && hipMalloc(p, std::max<size_t>(bytes, 16)) != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal buffers (" + std::to_string(bytes >> 20) + " MiB)");
+    };
+    dm((void**)&f->fronts, nt * sizeof(dev::MfFront));
+    dm((void**)&f->chl, chl.size() * 4);
+    dm((void**)&f->sidx, sidx.size() * 4);
+    dm((void**)&f->cmap, P.cmap.size() * 4);
+    dm((void**)&f->perm, n * 4);
+    dm((void**)&f->pinv, n * 4);
+    dm((void**)&f->lists, lists.size() * 4);
+    dm(&f->F, (size_t)fe * sb);
+    dm(&f->u, (size_t)uo * sb);
+    dm(&f->w, n * sb);
+    dm(&f->x, n * sb);
+    dm((void**)&d_tab, tab.size() * 4);
+    dm((void**)&d_piv, n * 4);
+    dm((void**)&d_z, 4);
+    dm((void**)&d_dst, nnz * 8);
+    dm((void**)&d_v, nnz * sb);
+    std::vector<int32_t> hpiv(n);
+    int32_t hz = 0;
+    if (rc == EIGSOL_OK) {
+        const auto t1 = clk::now();
+        auto up = [&](void* d, const void* h, size_t b) {
+            if (b) hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, st);
+        };
+        up(f->fronts, fr.data(), nt * sizeof(dev::MfFront));
+        up(f->chl, chl.data(), chl.size() * 4);
+        up(f->sidx, sidx.data(), sidx.size() * 4);
+        up(f->cmap, P.cmap.data(), P.cmap.size() * 4);
+        up(f->perm, P.perm.data(), n * 4);
+        up(f->lists, lists.data(), lists.size() * 4);
+        up(d_tab, tab.data(), tab.size() * 4);
+        up(d_dst, dst.data(), nnz * 8);
+        up(d_v, vals, nnz * sb);
+        hipMemsetAsync(f->F, 0, (size_t)fe * sb, st);
+        hipMemsetAsync(d_z, 0, 4, st);
+        S* F = static_cast<S*>(f->F);
+        if (nnz)
+            hipLaunchKernelGGL((dev::mf_scatter_kernel<S>), dim3((nnz + 255) / 256), dim3(256), 0, st, d_dst, d_v, nnz, F);
+        for (const Launch& l : plan) {
+            if (l.kind == 0)
+                hipLaunchKernelGGL((dev::mf_extend_kernel<S>), dim3(l.cnt), dim3(256), 0, st, f->fronts, d_tab + l.off,
+                                   f->cmap, F);
+            else if (l.kind == 1)
+                hipLaunchKernelGGL((dev::mf_panel_kernel<S, NB>), dim3(l.cnt), dim3(256), 0, st, f->fronts,
+                                   f->lists + l.off, l.q, F, d_piv, d_z);
+            else
+                hipLaunchKernelGGL((dev::mf_gemm_kernel<S, NB>), dim3(l.cnt), dim3(256), 0, st, f->fronts, d_tab + l.off,
+                                   l.q, F);
+        }
+        hipMemcpyAsync(hpiv.data(), d_piv, n * 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&hz, d_z, 4, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal factorization");
+        stt.numeric_seconds = std::chrono::duration<double>(clk::now() - t1).count();
+    }
+    for (void* p : {(void*)d_tab, (void*)d_piv, (void*)d_z, (void*)d_dst, (void*)d_v})
+        if (p) hipFree(p);
+    if (rc == EIGSOL_OK && hz) rc = fail(EIGSOL_E_SOLVER, "solve_shifted: multifrontal LU met a zero pivot");
+    if (rc == EIGSOL_OK) {
+        // composite interchange of every front: row t of the factored front is row q[t] of the assembled one
+        std::vector<int32_t> pinv(n);
+        for (int64_t s = 0; s < nt; ++s) {
+            const int32_t c0 = fr[s].c0, ns = fr[s].ns;
+            int32_t* qv = pinv.data() + c0;
+            for (int32_t t = 0; t < ns; ++t) qv[t] = t;
+            for (int32_t k = 0; k < ns; ++k) std::swap(qv[k], qv[hpiv[c0 + k]]);
+        }
+        if (hipMemcpyAsync(f->pinv, pinv.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal pivots");
+    }
+    if (rc == EIGSOL_OK) {
+        int32_t mx = 0;
+        for (int32_t b : f->lds_fwd) mx = std::max(mx, b);
+        for (int32_t b : f->lds_bwd) mx = std::max(mx, b);
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal solve LDS");
+    }
+    if (rc != EIGSOL_OK) {
+        mf_free(f);
+        return rc;
+    }
+    stt.solve_bytes = fac * (double)sb + 2.0 * (double)uo * (double)sb + 6.0 * (double)n * (double)sb;
+    f->st = stt;
+    *out = f;
+    return EIGSOL_OK;
+}
+
+template <class S>
+int mf_solve_t(MfFactor* f, const S* b, S* out) {
+    hipStream_t st = f->ctx->stream;
+    const int64_t n = f->n;
+    if (n == 0) return EIGSOL_OK;
+    S* w = static_cast<S*>(f->w);
+    S* x = static_cast<S*>(f->x);
+    const S* F = static_cast<const S*>(f->F);
+    hipLaunchKernelGGL((dev::mf_gather_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, b, w, n);
+    const int32_t H = (int32_t)f->hstart.size() - 2;
+    for (int32_t h = 0; h <= H; ++h) {
+        const int64_t cnt = f->hstart[h + 1] - f->hstart[h];
+        hipLaunchKernelGGL((dev::mf_fwd_kernel<S>), dim3(cnt), dim3(256), f->lds_fwd[h], st, f->fronts,
+                           f->lists + f->hstart[h], f->chl, F, f->cmap, f->pinv, w, static_cast<S*>(f->u));
+    }
+    for (int32_t h = H; h >= 0; --h) {
+        const int64_t cnt = f->hstart[h + 1] - f->hstart[h];
+        hipLaunchKernelGGL((dev::mf_bwd_kernel<S>), dim3(cnt), dim3(256), f->lds_bwd[h], st, f->fronts,
+                           f->lists + f->hstart[h], F, f->sidx, w, x);
+    }
+    hipLaunchKernelGGL((dev::mf_scatter_out_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, x, out, n);
+    EIGSOL_HIP(hipGetLastError());
+    return EIGSOL_OK;
+}
+
+}  // namespace
+
+int mf_create(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
+              const void* v, MfFactor** out) {
+    *out = nullptr;
+    try {
+        if (dtype == EIGSOL_C128) return mf_create_t<cplx>(ctx, dtype, n, rp, ci, static_cast<const cplx*>(v), out);
+        if (dtype == EIGSOL_F64) return mf_create_t<double>(ctx, dtype, n, rp, ci, static_cast<const double*>(v), out);
+    } catch (const std::exception& ex) {   // host allocation of the plan
+        return fail(EIGSOL_E_UNSUPPORTED, std::string("solve_shifted: multifrontal plan: ") + ex.what());
+    }
+    return EIGSOL_E_UNSUPPORTED;
+}
+
+int mf_solve(MfFactor* f, const void* b, void* x) {
+    if (f->dtype == EIGSOL_C128) return mf_solve_t<cplx>(f, static_cast<const cplx*>(b), static_cast<cplx*>(x));
+    return mf_solve_t<double>(f, static_cast<const double*>(b), static_cast<double*>(x));
+}
+
+}  // namespace eigsol
+
+// Host-only analysis of the multifrontal plan (ordering + symbolic), for tests and tools: perm_out
+// (n entries, new -> old) and fronts_out (4 per front: first column, pivots, struct size, parent)
+// may be null; stats_out[8] = fronts, heights, max front, max pivots, factor entries, front
+// entries, flops (complex scalars if is_complex), 1 if the plan is consistent.
+extern "C" int eigsol_mf_analyze(int64_t n, const int32_t* rowptr, const int32_t* colidx, int32_t leaf,
+                                 int32_t is_complex, int32_t* perm_out, int32_t* fronts_out, int64_t fronts_cap,
+                                 double* stats_out) {
+    using namespace eigsol;
+    if (n < 0 || n > INT32_MAX - 1 || (n > 0 && (!rowptr || !colidx)) || !stats_out || leaf < 1 ||
+        (rowptr && rowptr[0] != 0))
+        return fail(EIGSOL_E_INVALID, "eigsol_mf_analyze: bad arguments");
+    for (int64_t i = 0; i < n; ++i) {
+        if (rowptr[i + 1] < rowptr[i]) return fail(EIGSOL_E_INVALID, "eigsol_mf_analyze: row pointers not monotone");
+        for (int32_t e = rowptr[i]; e < rowptr[i + 1]; ++e)
+            if (colidx[e] < 0 || colidx[e] >= n) return fail(EIGSOL_E_INVALID, "eigsol_mf_analyze: column index out of range");
+    }
+    try {
+        std::vector<int32_t> rp(rowptr, rowptr + n + 1), ci(colidx, colidx + (n ? rowptr[n] : 0));
+        MfPlan P;
+        const bool ok = mf_plan(n, rp, ci, leaf, is_complex != 0, P);
+        stats_out[0] = (double)P.nt;
+        stats_out[1] = (double)(P.H + 1);
+        stats_out[2] = (double)P.maxd;
+        stats_out[3] = (double)P.maxns;
+        stats_out[4] = P.fac;
+        stats_out[5] = P.fe;
+        stats_out[6] = P.flops;
+        stats_out[7] = ok ? 1.0 : 0.0;
+        if (perm_out && n) std::copy(P.perm.begin(), P.perm.end(), perm_out);
+        if (fronts_out) {
+            if (fronts_cap < P.nt) return fail(EIGSOL_E_INVALID, "eigsol_mf_analyze: fronts_out too small");
+            for (int64_t s = 0; s < P.nt; ++s) {
+                fronts_out[4 * s] = P.fr[s].c0;
+                fronts_out[4 * s + 1] = P.fr[s].ns;
+                fronts_out[4 * s + 2] = P.fr[s].ms;
+                fronts_out[4 * s + 3] = P.fr[s].parent;
+            }
+        }
+        return EIGSOL_OK;
+    } catch (const std::exception& ex) {
+        return fail(EIGSOL_E_INVALID, std::string("eigsol_mf_analyze: ") + ex.what());
+    }
+}

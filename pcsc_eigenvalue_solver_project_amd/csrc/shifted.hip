@@ -1996,14 +1996,21 @@ static double device_free_bytes() {
     return (double)fr;
 }
 
+static bool general_sparse_forced(SparseSolver& out) {
+    if (const char* e = std::getenv("EIGSOL_SPARSE_SOLVER")) {
+        if (!std::strcmp(e, "gmres")) { out = kSolverGMRES; return true; }
+        if (!std::strcmp(e, "lu")) { out = kSolverLU; return true; }
+        if (!std::strcmp(e, "band")) { out = kSolverBand; return true; }
+    }
+    return false;
+}
+
 static SparseSolver general_sparse_solver(int64_t n, size_t sb, const BandPlan& plan, bool& forced) {
     forced = false;
-    if (const char* e = std::getenv("EIGSOL_SPARSE_SOLVER")) {
+    SparseSolver fs;
+    if (general_sparse_forced(fs)) {
         forced = true;
-        if (!std::strcmp(e, "gmres")) return kSolverGMRES;
-        if (!std::strcmp(e, "lu")) return kSolverLU;
-        if (!std::strcmp(e, "band")) return kSolverBand;
-        forced = false;
+        return fs;
     }
     const double dense = (double)n * (double)n * (double)sb;
     const bool band_fits = plan.ok && plan.bytes <= 0.6 * device_free_bytes();
@@ -2123,10 +2130,18 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
             return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: single-precision factors exist for triangular "
                                               "sparse matrices only");
         } else {
+        // past n = 16384 the double / complex<double> factors take the GMRES family's direct
+        // factors (exact no-pivot LU where the fill stays within 3 x nnz, else the nested-dissection
+        // multifrontal LU, gmres.hip / multifrontal.hip; ILU(0) + GMRES when neither fits): the band
+        // factor runs one panel kernel per 64 columns on one workgroup (round 5, config5_convdiff_1M:
+        // 13.8 s, 1.37 s per solve).  The band stays for smaller orders, single precision, or forced.
         BandPlan plan;
-        band_plan(A->dtype, n, rp.data(), ci.data(), plan);
+        SparseSolver fs = kSolverBand;
+        const bool pre_forced = general_sparse_forced(fs);
+        const bool large_gmres = !pre_forced && n > 16384 && kGmres<S>;
+        if (!large_gmres && !(pre_forced && fs != kSolverBand)) band_plan(A->dtype, n, rp.data(), ci.data(), plan);
         bool forced = false;
-        const SparseSolver solver = general_sparse_solver(n, sizeof(S), plan, forced);
+        const SparseSolver solver = large_gmres ? kSolverGMRES : general_sparse_solver(n, sizeof(S), plan, forced);
         if (solver == kSolverBand) {
             if (!plan.ok) {
                 shift_free(f);
@@ -3122,7 +3137,10 @@ void shift_info(const ShiftFactor* f, double* bytes, int32_t* variant, int32_t* 
     const double sb = (double)scalar_bytes(f->dtype), n = (double)f->n;
     if (f->kind == 2) {
         gmres_info(f->gm, bytes, tiles);
-        if (variant) *variant = gmres_complete(f->gm) ? 18 : 7;
+        if (variant) {
+            const int c = gmres_complete(f->gm);
+            *variant = c == 2 ? 19 : c ? 18 : 7;   // 19: nested-dissection multifrontal LU
+        }
     } else if (f->kind == 3) {
         band_info(f->band, bytes, tiles);
         if (variant) *variant = 8;

@@ -1,0 +1,223 @@
+"""General-sparse shifted solve on the nested-dissection multifrontal LU (multifrontal.hip, variant
+19), the default direct factor past n = 16384 when the natural-order LU's fill passes 3 x nnz.
+
+Reference path: solve_shifted<S> (src/matrix/solve_shifted.hpp:85-117, SparseLU) inside
+shiftedInversePowerImpl (src/power_method/shifted_inverse_power_solver.hpp:21-79).
+
+Fixture: tests/golden/convdiff141.json + convdiff141_eigvec.npy (scipy SuperLU, a direct sparse LU
+like the reference's; made by tests/golden/make_golden.py convdiff): the permuted complex 2-D
+convection-diffusion matrix, n = 19881, whose LU has real fill.
+
+Tolerances: lambda within 1e-10 (1 + |lambda|); iterations equal, or +-1 when the last
+step sits at the tolerance; |x^H x_ref| >= 1 - 1e-10; solve residuals ||(A - sigma I) y - b|| <=
+1e-11 ||b|| (+ 1e-13 (||M||_1 + |sigma|) ||y|| next to an eigenvalue) (the factor's solve is checked by its true residual and refined by GMRES cycles when it
+misses 1e-12, gmres.hip).  Smaller systems reach this path with EIGSOL_SPARSE_SOLVER=gmres and
+EIGSOL_LU_FILL_CAP=1 (the exact natural-order LU refused for any fill)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import pcsc_eigenvalue_solver_project_amd as E
+from oracle import oracle as O
+from pcsc_eigenvalue_solver_project_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = E.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture
+def env():
+    saved = {}
+
+    def set_(k, val):
+        saved.setdefault(k, os.environ.get(k))
+        os.environ[k] = val
+
+    yield set_
+    for k, val in saved.items():
+        if val is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = val
+
+
+def _variant(A, sigma):
+    sess = E.ShiftedSession(A, sigma)
+    info = sess.kernel_info()
+    sess.close()
+    return info["variant"]
+
+
+def _mf_env(env):
+    env("EIGSOL_SPARSE_SOLVER", "gmres")
+    env("EIGSOL_LU_FILL_CAP", "1")
+    env("EIGSOL_GMRES_FALLBACK", "0")
+
+
+def test_convdiff_fixture_default_is_multifrontal(ctx):
+    fx = json.load(open(os.path.join(GOLD, "convdiff141.json")))
+    rp, ci, v = S.convdiff_complex(fx["nx"], seed=fx["seed"])
+    xref = np.load(os.path.join(GOLD, "convdiff141_eigvec.npy"))
+    n = fx["n"]
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = complex(*fx["sigma"])
+    assert _variant(A, sigma) == 19
+    r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(fx["max_iter"], fx["tol"], sigma),
+                                       S.start_vector(n, np.complex128))
+    lam = complex(*fx["lambda"])
+    assert r.converged and fx["converged"]
+    assert abs(r.eigenvalue - lam) <= 1e-10 * (1 + abs(lam)), (r.eigenvalue, lam)
+    if r.iterations != fx["iterations"]:
+        tr = fx["trace"]
+        last = abs(complex(*tr[-1]) - complex(*tr[-2])) / (1 + abs(complex(*tr[-1])))
+        assert abs(r.iterations - fx["iterations"]) == 1 and 1e-13 <= last <= 1e-11, (r.iterations, last)
+    assert abs(abs(np.vdot(r.eigenvector, xref)) - 1) <= 1e-10
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    assert np.linalg.norm(M @ r.eigenvector - r.eigenvalue * r.eigenvector) <= 1e-9
+    A.close()
+
+
+@pytest.mark.parametrize("nx", [141, 300])
+def test_multifrontal_solve_residual_and_determinism(ctx, nx):
+    rp, ci, v = S.convdiff_complex(nx, seed=4)
+    n = nx * nx
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    for sigma in (4.0 + 0.5j, 0.5 - 0.25j, 7.9 + 0.0j):
+        assert _variant(A, sigma) == 19
+        b = S.start_vector(n, np.complex128, seed=11)
+        y = E.solve_shifted(A, sigma, b)
+        # backward-error scale: sigma = 7.9 sits next to an eigenvalue (||y|| ~ 1e8; SuperLU's own
+        # solve leaves ~1e-7 there), so the residual is bounded by eps-size multiples of ||M|| ||y||
+        scale = 1e-11 * np.linalg.norm(b) + 1e-13 * (abs(M).sum(0).max() + abs(sigma)) * np.linalg.norm(y)
+        assert np.linalg.norm(M @ y - sigma * y - b) <= scale
+        y2 = E.solve_shifted(A, sigma, b)
+        assert np.array_equal(y, y2)                       # fixed-order sums: bitwise repeatable
+    A.close()
+
+
+def test_multifrontal_real_parity_with_reference_loop(ctx, env):
+    """f64: the real part of the permuted stencil (n = 900) against the oracle's restatement of the
+    reference loop with a direct dense solve per iteration."""
+    _mf_env(env)
+    rp, ci, v = S.convdiff_complex(30, seed=5)
+    v = np.ascontiguousarray(v.real)
+    n = 900
+    D = sp.csr_matrix((v, ci, rp), shape=(n, n)).toarray()
+    ev = np.linalg.eigvals(D)
+    re = np.sort(ev.real[np.abs(ev.imag) < 1e-12])
+    i = len(re) // 3
+    sigma = re[i] + 0.1 * min(re[i + 1] - re[i], re[i] - re[i - 1])
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    assert _variant(A, sigma) == 19
+    x0 = S.start_vector(n)
+    r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(500, 1e-12, sigma), x0)
+    ref = O.shifted_dense(D, sigma, x0, 500, 1e-12)
+    assert r.converged and ref["converged"]
+    lam = ref["eigenvalue"]
+    assert abs(r.eigenvalue - lam) <= 1e-10 * (1 + abs(lam)), (r.eigenvalue, lam)
+    assert abs(r.iterations - ref["iterations"]) <= 1
+    assert abs(abs(np.vdot(r.eigenvector, ref["eigenvector"])) - 1) <= 1e-10
+    b = S.start_vector(n, seed=3)
+    y = E.solve_shifted(A, sigma, b)
+    assert np.linalg.norm(D @ y - sigma * y - b) <= 1e-10 * np.linalg.norm(b) * np.linalg.norm(y)
+    A.close()
+
+
+def test_multifrontal_components_missing_diagonal_and_dense_rows(ctx, env):
+    """Two disconnected stencils, isolated rows without a stored diagonal (coeffRef inserts
+    0 - sigma, solve_shifted.hpp:100-102), a row and a column coupling many vertices (a wide
+    separator), and a nonsymmetric pattern: against a dense solve."""
+    _mf_env(env)
+    rp1, ci1, v1 = S.convdiff_complex(20, seed=1)
+    rp2, ci2, v2 = S.convdiff_complex(15, seed=2)
+    M1 = sp.csr_matrix((v1, ci1, rp1), shape=(400, 400))
+    M2 = sp.csr_matrix((v2, ci2, rp2), shape=(225, 225))
+    Z = sp.csr_matrix((5, 5), dtype=np.complex128)
+    M = sp.block_diag([M1, Z, M2], format="lil")
+    n = M.shape[0]
+    rng = np.random.default_rng(3)
+    hub = 17
+    for j in rng.choice(n, 60, replace=False):
+        M[hub, j] = 0.05 * (rng.standard_normal() + 1j * rng.standard_normal())
+    for i in rng.choice(n, 40, replace=False):
+        M[i, 500] = 0.05 * (rng.standard_normal() + 1j * rng.standard_normal())
+    M = sp.csr_matrix(M)
+    M.sort_indices()
+    A = E.CsrMatrix.from_scipy(ctx, M)
+    sigma = 0.3 + 0.2j
+    assert _variant(A, sigma) == 19
+    b = S.start_vector(n, np.complex128, seed=4)
+    y = E.solve_shifted(A, sigma, b)
+    ref = np.linalg.solve(M.toarray() - sigma * np.eye(n), b)
+    assert np.linalg.norm(y - ref) <= 1e-11 * np.linalg.norm(ref)
+    A.close()
+
+
+@pytest.mark.parametrize("leaf", ["4", "16", "200"])
+def test_multifrontal_leaf_sizes(ctx, env, leaf):
+    """The leaf size only changes the tree: tiny leaves (many fronts, many heights) and one big
+    leaf (the whole matrix as one front) give the same solution within the residual bound."""
+    _mf_env(env)
+    env("EIGSOL_MF_LEAF", leaf)
+    rp, ci, v = S.convdiff_complex(14, seed=8)
+    n = 196
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 2.0 + 0.1j
+    assert _variant(A, sigma) == 19
+    b = S.start_vector(n, np.complex128, seed=2)
+    y = E.solve_shifted(A, sigma, b)
+    assert np.linalg.norm(M @ y - sigma * y - b) <= 1e-11 * np.linalg.norm(b)
+    A.close()
+
+
+def test_multifrontal_needs_front_pivoting(ctx, env):
+    """Zero diagonal entries of A - sigma I (the no-pivot LU would divide by zero): the partial
+    pivoting inside each front handles them."""
+    _mf_env(env)
+    rp, ci, v = S.convdiff_complex(25, seed=6)
+    n = 625
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n)).tolil()
+    sigma = 1.5 + 0.0j
+    for i in range(0, n, 7):
+        M[i, i] = sigma                    # (A - sigma I)(i, i) = 0
+    M = sp.csr_matrix(M)
+    M.sort_indices()
+    A = E.CsrMatrix.from_scipy(ctx, M)
+    assert _variant(A, sigma) == 19
+    b = S.start_vector(n, np.complex128, seed=9)
+    y = E.solve_shifted(A, sigma, b)
+    ref = np.linalg.solve(M.toarray() - sigma * np.eye(n), b)
+    assert np.linalg.norm(y - ref) <= 1e-10 * np.linalg.norm(ref)
+    A.close()
+
+
+def test_multifrontal_singular_falls_back_or_fails(ctx, env):
+    """A zero row in A - sigma I: the front's pivot column is zero (the multifrontal factor
+    reports a zero pivot), ILU(0) meets it too, and with the dense fallback off the solve reports
+    SparseLU's failed factorization (solve_shifted.hpp:108-110)."""
+    _mf_env(env)
+    rp, ci, v = S.convdiff_complex(20, seed=3)
+    M = sp.csr_matrix((v, ci, rp), shape=(400, 400)).tolil()
+    sigma = 2.0 + 0.0j
+    M[17, :] = 0
+    M[17, 17] = sigma
+    M = sp.csr_matrix(M)
+    M.eliminate_zeros()
+    M.sort_indices()
+    A = E.CsrMatrix.from_scipy(ctx, M)
+    with pytest.raises(E.EigSolError) as ei:
+        E.solve_shifted(A, sigma, np.ones(400, np.complex128))
+    assert ei.value.status == 6
+    A.close()

@@ -74,8 +74,9 @@ def _check_fixture(r, fx, xref):
     assert abs(abs(np.vdot(r.eigenvector, xref)) - 1) <= 1e-10
 
 
-def test_band_lu_convdiff_fixture(ctx, convdiff):
+def test_band_lu_convdiff_fixture(ctx, convdiff, env):
     fx, rp, ci, v, xref = convdiff
+    env("EIGSOL_SPARSE_SOLVER", "band")   # n = 19881 > 16384 defaults to the multifrontal LU (test_gpu_multifrontal.py)
     n = fx["n"]
     A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
     sigma = complex(*fx["sigma"])
@@ -92,8 +93,9 @@ def test_band_lu_convdiff_fixture(ctx, convdiff):
     A.close()
 
 
-def test_band_lu_solve_shifted_residual(ctx, convdiff):
+def test_band_lu_solve_shifted_residual(ctx, convdiff, env):
     fx, rp, ci, v, _ = convdiff
+    env("EIGSOL_SPARSE_SOLVER", "band")
     n = fx["n"]
     A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
     M = sp.csr_matrix((v, ci, rp), shape=(n, n))
