@@ -404,12 +404,13 @@ def _convdiff_run(E, ctx, torch, stream, A, sigma, x0, max_iter):
     ms = _events(torch, stream, lambda: sess.step(3)) / 3
     sess.close()
     paths = {7: "ILU(0) + restarted GMRES", 8: "RCM + banded partial-pivot LU",
-             18: "exact sparse LU (complete fill, no pivoting) + residual check", 4: "densified partial-pivot LU"}
+             18: "exact sparse LU (complete fill, no pivoting) + residual check", 4: "densified partial-pivot LU",
+             19: "nested-dissection multifrontal LU (front-restricted pivoting) + residual check"}
     return res, {"solver_path": paths.get(info0["variant"], str(info0["variant"])), "variant": info0["variant"],
                  "factor_seconds": round(t_factor, 3), "ms_per_iteration": round(ms, 3),
                  "iterations": res.iterations, "converged": res.converged,
                  "eigenvalue": [float(np.real(res.eigenvalue)), float(np.imag(res.eigenvalue))],
-                 "arnoldi_steps_last_solve": info["tiles"] if info["variant"] in (7, 18) else None,
+                 "arnoldi_steps_last_solve": info["tiles"] if info["variant"] in (7, 18, 19) else None,
                  "band_kl_plus_ku": info["tiles"] if info["variant"] == 8 else None,
                  "solve_seconds": round(t_solve, 3), "end_to_end_seconds": round(t_e2e, 3)}
 
@@ -419,8 +420,9 @@ def run_config5_convdiff(E, S, ctx, torch, stream, nx=1000, max_iter=8):
     synthetic.convdiff_complex(1000), a 2-D convection-diffusion stencil on a 1000 x 1000 grid with
     complex perturbations under a random symmetric permutation (n = 1M, ~5M nnz; neither banded nor
     triangular as stored; the exact LU's fill passes the 3 x nnz cap).  Reported for the path the
-    library chooses by default (a direct factor, like the reference's SparseLU: here the RCM band LU,
-    bandwidth ~ the grid side) and for ILU(0) + GMRES forced (EIGSOL_SPARSE_SOLVER=gmres): set-up
+    library chooses by default (a direct factor, like the reference's SparseLU: since round 5 the
+    nested-dissection multifrontal LU, multifrontal.hip; round 5's first figure was the RCM band LU:
+    13.8 s set-up, 1.37 s per iteration) and for ILU(0) + GMRES forced (EIGSOL_LU_FILL_CAP=0): set-up
     time, steady-state ms per iteration, Arnoldi steps / band width, and the end-to-end time of a run
     of at most max_iter iterations (sigma sits inside a clustered spectrum, so the iteration itself
     converges slowly: `converged` says whether it did).  solve_shifted.hpp:85-117 is the reference
@@ -433,18 +435,18 @@ def run_config5_convdiff(E, S, ctx, torch, stream, nx=1000, max_iter=8):
     A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
     M = sp.csr_matrix((v, ci, rp), shape=(n, n))
     out = {"n": n, "nnz": int(len(ci)), "sigma": [sigma.real, sigma.imag]}
-    for label, forced in (("default", None), ("gmres_forced", "gmres")):
-        old = os.environ.get("EIGSOL_SPARSE_SOLVER")
-        if forced:
-            os.environ["EIGSOL_SPARSE_SOLVER"] = forced
+    for label, forced in (("default", None), ("ilu0_gmres_forced", {"EIGSOL_SPARSE_SOLVER": "gmres",
+                                                                     "EIGSOL_LU_FILL_CAP": "0"})):
+        old = {k: os.environ.get(k) for k in (forced or {})}
+        os.environ.update(forced or {})
         try:
             res, d = _convdiff_run(E, ctx, torch, stream, A, sigma, x0, max_iter)
         finally:
-            if forced:
-                if old is None:
-                    os.environ.pop("EIGSOL_SPARSE_SOLVER", None)
+            for k, val in old.items():
+                if val is None:
+                    os.environ.pop(k, None)
                 else:
-                    os.environ["EIGSOL_SPARSE_SOLVER"] = old
+                    os.environ[k] = val
         x = res.eigenvector
         d["eigen_residual"] = float(np.linalg.norm(M @ x - res.eigenvalue * x) / np.linalg.norm(x))
         out[label] = d

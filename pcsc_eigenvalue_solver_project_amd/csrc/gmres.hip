@@ -27,6 +27,7 @@
 // EIGSOL_E_SOLVER as SparseLU's failed solve (solve_shifted.hpp:112-114); shifted.hip then falls
 // back to the densified LU wherever it fits the device.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <complex>
 #include <cstdlib>
@@ -277,6 +278,14 @@ template <class S>
 static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const int32_t* ci, const S* v,
                           double sre, double sim, GmresSolver** out) {
     hipStream_t st = ctx->stream;
+    static const bool dbg = std::getenv("EIGSOL_MF_DEBUG") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!dbg) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[gmres] %s %.3f s\n", what, std::chrono::duration<double>(t - tp).count());
+        tp = t;
+    };
     auto* g = new GmresSolver();
     g->ctx = ctx;
     ctx_retain(ctx);
@@ -317,7 +326,9 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
         mrp[i + 1] = (int32_t)mci.size();
     }
     g->nnzM = (int64_t)mci.size();
+    lap("build M");
     int rc = csr_upload(ctx, dtype, n, n, g->nnzM, mrp.data(), mci.data(), mv.data(), &g->M, 0);
+    lap("upload M");
     // complete fill where affordable: M's values on the closed pattern, zeros at the fill
     // positions; the factorization below then produces the exact LU (round 4: the 1M config-5
     // matrix made general fills 16.5M -> ~24M entries and GMRES needs one step per solve instead of
@@ -359,7 +370,9 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
         if (const char* e = std::getenv("EIGSOL_LU_FILL_CAP")) ratio = std::atof(e);
         const char* me = std::getenv("EIGSOL_MF");
         if (rc == EIGSOL_OK && !g->complete && ratio >= 1.0 && !(me && !std::strcmp(me, "0"))) {
+            lap("exact-LU fill attempt");
             const int mrc = mf_create(ctx, dtype, n, mrp, mci, mv.data(), &g->mf);
+            lap("multifrontal create");
             if (mrc == EIGSOL_OK) g->complete = 2;
             else if (mrc == EIGSOL_E_HIP) rc = mrc;   // a zero pivot or a declined plan: ILU(0) below
         }

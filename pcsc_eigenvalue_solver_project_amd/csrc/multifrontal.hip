@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -58,7 +59,8 @@ struct MfFront {
     int32_t d, ns, c0, ms;
     int32_t ch0, ch1;   // children chl[ch0 .. ch1) (fixed order)
     int32_t parent;
-    int32_t pad;
+    int32_t flag0;  // large fronts: first of the front's pivot-block flags; -1: solved by one workgroup
+    int64_t zoff;   // large fronts: assembled right-hand side (d entries) at z + zoff
 };
 
 __device__ __forceinline__ double mf_rl(double v, int src) {
@@ -344,6 +346,261 @@ __global__ __launch_bounds__(256) void mf_bwd_kernel(const MfFront* fr, const in
     for (int k = tid; k < ns; k += 256) x[f.c0 + k] = t[k];
 }
 
+// ---- large fronts: one workgroup per 64-row block, sync-free (the dense path's blocked TRSV,
+// shifted.hip dense_trsv_kernel, on a front).  Pivot block k of a front publishes its solved 64
+// values with write-through stores and raises flag[flag0 + k] to the solve's epoch; a row block
+// waits for the flags of the blocks it multiplies.  Blocks a row block waits for have lower
+// workgroup indices (forward: ascending pivot blocks, then the struct rows; backward: descending),
+// and the launches are small (hundreds of workgroups, all resident), so every wait ends.
+// back-off: short sleeps (the chain's hand-off latency is what a solve waits on; the pollers are
+// a few hundred workgroups), or the dense TRSV's growing sleeps (EIGSOL_MF_BACKOFF=1)
+__device__ __forceinline__ void mf_wait(const int32_t* f, int32_t epoch, int32_t* err, int bo) {
+    int spins = 0;
+    while (__hip_atomic_load(const_cast<int32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        if (!bo) __builtin_amdgcn_s_sleep(1);
+        else if (spins < 4) __builtin_amdgcn_s_sleep(2);
+        else if (spins < 16) __builtin_amdgcn_s_sleep(8);
+        else __builtin_amdgcn_s_sleep(32);
+        if (++spins > (1 << 24)) { atomicOr(err, 1); break; }
+    }
+}
+__device__ __forceinline__ void mf_st(double* p, double v) { st_agent(p, v); }
+__device__ __forceinline__ void mf_st(cplx* p, cplx v) {
+    st_agent(&p->re, v.re);
+    st_agent(&p->im, v.im);
+}
+__device__ __forceinline__ double mf_ld(const double* p) { return ld_agent(p); }
+__device__ __forceinline__ cplx mf_ld(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
+
+// z (d entries per large front) = the permuted pivot right-hand side, then the children's
+// contributions to the struct rows; one workgroup per front.  LDS: r (ns)
+template <class S>
+__global__ __launch_bounds__(256) void mf_big_asm_kernel(const MfFront* fr, const int32_t* list, const int32_t* chl,
+                                                         const int32_t* cmap, const int32_t* pinv, const S* w,
+                                                         const S* u, S* z) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const MfFront f = fr[list[blockIdx.x]];
+    const int tid = threadIdx.x, ns = f.ns, ms = f.ms;
+    S* r = reinterpret_cast<S*>(lds_raw);
+    S* zs = z + f.zoff;
+    for (int t = tid; t < ns; t += 256) r[t] = w[f.c0 + t];
+    for (int t = tid; t < ms; t += 256) zs[ns + t] = s_zero<S>();
+    __syncthreads();
+    for (int k = f.ch0; k < f.ch1; ++k) {
+        const MfFront c = fr[chl[k]];
+        const int32_t* map = cmap + c.sof;
+        const S* uc = u + c.uoff;
+        for (int t = tid; t < c.ms; t += 256) {
+            const int pos = map[t];
+            const S v = uc[t];
+            if (pos < ns) r[pos] = sub(r[pos], v);
+            else zs[pos] = add(zs[pos], v);   // each position once per child: no race
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < ns; t += 256) zs[t] = r[pinv[f.c0 + t]];
+}
+
+template <class S>
+__device__ __forceinline__ S mf_rls(S v, int j) { return mf_rl(v, j); }
+
+// Inverted diagonal blocks of the large fronts (one workgroup per pivot block, after the
+// factorization): Tinv + 8192 k holds inv(L_kk) (unit lower), then inv(U_kk), 64 x 64 column-major,
+// the identity past a partial block's rn rows.  The solves then apply a diagonal block as a
+// 64 x 64 product split over the four waves instead of a 64-step dependent chain on one wave.
+template <class S>
+__global__ __launch_bounds__(256) void mf_inv_kernel(const MfFront* fr, const int32_t* tab, const S* F, S* Tinv) {
+    __shared__ S T[64 * 65];
+    __shared__ S X[64 * 65];
+    const int s = tab[2 * blockIdx.x], k = tab[2 * blockIdx.x + 1];
+    const MfFront f = fr[s];
+    const int tid = threadIdx.x, d = f.d;
+    const int r0 = 64 * k, rn = min(64, f.ns - r0);
+    const S* A = F + f.off;
+    S one;
+    set_re_im(one, 1.0, 0.0);
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int i = e & 63, j = e >> 6;
+        T[i + j * 65] = (i < rn && j < rn) ? A[(r0 + i) + (int64_t)(r0 + j) * d] : (i == j ? one : s_zero<S>());
+    }
+    __syncthreads();
+    S* out = Tinv + (int64_t)(f.flag0 + k) * 8192;
+    // inv(L): thread t < 64 solves column t by forward substitution (unit diagonal)
+    if (tid < 64) {
+        const int t = tid;
+        for (int i = 0; i < 64; ++i) {
+            S v = i == t ? one : s_zero<S>();
+            for (int j = t; j < i; ++j) v = sub(v, mul(T[i + j * 65], X[j + t * 65]));
+            X[i + t * 65] = i < t ? s_zero<S>() : v;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) out[e] = X[(e & 63) + (e >> 6) * 65];
+    __syncthreads();
+    // inv(U): back substitution, column t
+    if (tid < 64) {
+        const int t = tid;
+        for (int i = 63; i >= 0; --i) {
+            S v = i == t ? one : s_zero<S>();
+            for (int j = i + 1; j <= t; ++j) v = sub(v, mul(T[i + j * 65], X[j + t * 65]));
+            X[i + t * 65] = i > t ? s_zero<S>() : sdiv(v, T[i + i * 65]);
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) out[4096 + e] = X[(e & 63) + (e >> 6) * 65];
+}
+
+// acc += tile(row, c0 .. c0 + 16) * yv over the columns below lim (tile values already loaded)
+template <class S>
+__device__ __forceinline__ void mf_acc16(S& acc, const S (&tv)[16], const S* yv, int c0, int lim) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+        if (c0 + t < lim) acc = add(acc, mul(tv[t], yv[t]));
+}
+
+// forward, large fronts: tab = (front, row block) pairs; row block k < nblk: pivot rows
+// [64 k, 64 k + 64) (applies inv(L_kk), publishes, raises the flag); k >= nblk: struct rows (their
+// contribution u = children's part + L21 y).  Every wave takes 16 columns of each column block:
+// its tile values are loaded before the block's flag is awaited.
+template <class S>
+__global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, const int32_t* tab, const S* F,
+                                                         const S* Tinv, const S* z, S* w, S* u, int32_t* flag,
+                                                         int32_t epoch, int32_t* err, int bo) {
+    __shared__ S part[4][64];
+    __shared__ S ysh[4][16];
+    __shared__ S vsh[64];
+    const int s = tab[2 * blockIdx.x], rb = tab[2 * blockIdx.x + 1];
+    const MfFront f = fr[s];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int d = f.d, ns = f.ns;
+    const int nblk = (ns + 63) / 64;
+    const bool piv = rb < nblk;
+    const int r0 = piv ? 64 * rb : ns + 64 * (rb - nblk);
+    const int rn = min(64, (piv ? ns : d) - r0);
+    const S* A = F + f.off;
+    const int row = r0 + min(lane, rn - 1);
+    S iv[16];
+    if (piv) {
+        const S* ti = Tinv + (int64_t)(f.flag0 + rb) * 8192 + lane + (16 * wv) * 64;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) iv[t] = ti[t * 64];
+    }
+    S acc = s_zero<S>();
+    const int cend = piv ? rb : nblk;
+    for (int c = 0; c < cend; ++c) {
+        const int c0 = 64 * c + 16 * wv;
+        S tv[16];
+        const S* tile = A + row;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) tv[t] = tile[(int64_t)min(c0 + t, ns - 1) * d];
+        if (lane == 0) mf_wait(flag + f.flag0 + c, epoch, err, bo);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_ld(w + f.c0 + c0 + lane) : s_zero<S>();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        mf_acc16(acc, tv, ysh[wv], c0, ns);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    part[wv][lane] = acc;
+    __syncthreads();
+    const S sum = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+    const S zr = lane < rn ? z[f.zoff + r0 + lane] : s_zero<S>();
+    if (!piv) {
+        if (wv == 0 && lane < rn) u[f.uoff + (r0 - ns) + lane] = add(zr, sum);
+        return;
+    }
+    if (wv == 0) vsh[lane] = lane < rn ? sub(zr, sum) : s_zero<S>();
+    __syncthreads();
+    S p = s_zero<S>();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) p = add(p, mul(iv[t], vsh[16 * wv + t]));
+    part[wv][lane] = p;
+    __syncthreads();
+    if (wv != 0) return;
+    const S y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+    if (lane < rn) mf_st(w + f.c0 + r0 + lane, y);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// backward, large fronts: tab = (front, pivot block) pairs, blocks descending within a front:
+// t = y - U12 x(struct) - U[rows, later blocks] x, then inv(U_kk) t (publish, flag)
+template <class S>
+__global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, const int32_t* tab, const S* F,
+                                                         const S* Tinv, const int32_t* sidx, const S* w, S* x,
+                                                         int32_t* flag, int32_t epoch, int32_t* err, int bo) {
+    __shared__ S part[4][64];
+    __shared__ S ysh[4][16];
+    __shared__ S vsh[64];
+    const int s = tab[2 * blockIdx.x], rb = tab[2 * blockIdx.x + 1];
+    const MfFront f = fr[s];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int d = f.d, ns = f.ns, ms = f.ms;
+    const int nblk = (ns + 63) / 64;
+    const int r0 = 64 * rb, rn = min(64, ns - r0);
+    const S* A = F + f.off;
+    const int row = r0 + min(lane, rn - 1);
+    S iv[16];
+    {
+        const S* ti = Tinv + (int64_t)(f.flag0 + rb) * 8192 + 4096 + lane + (16 * wv) * 64;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) iv[t] = ti[t * 64];
+    }
+    S acc = s_zero<S>();
+    // U12 x(struct): 16-column chunks, wave wv every 4th (the ancestors' x: earlier launches)
+    for (int q0 = 16 * wv; q0 < ms; q0 += 64) {
+        S tv[16];
+        const S* tile = A + row + (int64_t)ns * d;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) tv[t] = tile[(int64_t)min(q0 + t, ms - 1) * d];
+        if (lane < 16) ysh[wv][lane] = q0 + lane < ms ? x[sidx[f.sof + q0 + lane]] : s_zero<S>();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        mf_acc16(acc, tv, ysh[wv], q0, ms);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    // later pivot blocks of this front as their flags rise (the last block first)
+    for (int c = nblk - 1; c > rb; --c) {
+        const int c0 = 64 * c + 16 * wv;
+        S tv[16];
+        const S* tile = A + row;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) tv[t] = tile[(int64_t)min(c0 + t, ns - 1) * d];
+        if (lane == 0) mf_wait(flag + f.flag0 + c, epoch, err, bo);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_ld(x + f.c0 + c0 + lane) : s_zero<S>();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        mf_acc16(acc, tv, ysh[wv], c0, ns);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    part[wv][lane] = acc;
+    __syncthreads();
+    if (wv == 0) {
+        const S sum = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+        vsh[lane] = lane < rn ? sub(w[f.c0 + r0 + lane], sum) : s_zero<S>();
+    }
+    __syncthreads();
+    S p = s_zero<S>();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) p = add(p, mul(iv[t], vsh[16 * wv + t]));
+    part[wv][lane] = p;
+    __syncthreads();
+    if (wv != 0) return;
+    const S xv = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+    if (lane < rn) mf_st(x + f.c0 + r0 + lane, xv);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace dev
 
 // ================================================================== host side
@@ -365,7 +622,21 @@ struct MfFactor {
     void* w = nullptr;
     void* x = nullptr;
     std::vector<int64_t> hstart;      // lists[hstart[h] .. hstart[h + 1])
-    std::vector<int32_t> lds_fwd, lds_bwd;   // dynamic LDS bytes per height
+    std::vector<int32_t> lds_fwd, lds_bwd;   // dynamic LDS bytes per height (one-workgroup fronts)
+    // solve: per height the one-workgroup fronts (slists[sstart[h] .. + nsmall[h])), then the
+    // large fronts (the next nbig[h] entries: their assembly launch); the large fronts' row-block
+    // tables (front, block) for the forward / backward launches at tabf / tabb + off[h], cnt[h] pairs
+    int32_t* slists = nullptr;
+    int32_t* tabf = nullptr;
+    int32_t* tabb = nullptr;
+    int32_t* flags = nullptr;         // one per pivot block of the large fronts (epoch words)
+    int32_t* err = nullptr;           // a flag wait that timed out
+    void* z = nullptr;                // large fronts' assembled right-hand sides
+    void* tinv = nullptr;             // inverted diagonal blocks of the large fronts (8192 scalars each)
+    int32_t epoch = 0;
+    int backoff = 0;                  // EIGSOL_MF_BACKOFF
+    std::vector<int64_t> sstart, nsmall, nbig, foff, fcnt, boff, bcnt;
+    std::vector<int32_t> lds_asm;
     MfStats st;
 };
 
@@ -374,7 +645,8 @@ void mf_free(MfFactor* f) {
     hipSetDevice(f->ctx->device);
     hipStreamSynchronize(f->ctx->stream);
     for (void* p : {(void*)f->fronts, (void*)f->chl, (void*)f->sidx, (void*)f->cmap, (void*)f->perm, (void*)f->pinv,
-                    (void*)f->lists, f->F, f->u, f->w, f->x})
+                    (void*)f->lists, f->F, f->u, f->w, f->x, (void*)f->slists, (void*)f->tabf, (void*)f->tabb,
+                    (void*)f->flags, (void*)f->err, f->z, f->tinv})
         if (p) hipFree(p);
     ctx_release(f->ctx);
     delete f;
@@ -878,7 +1150,51 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
             if (k) plan.push_back(Launch{2, h, q, o, k});
         }
     }
+    // solve plan: fronts with many pivots or rows are solved by one workgroup per 64-row block
+    // (mf_big_*), the others by one workgroup each (mf_fwd / mf_bwd)
+    int big_ns = 128, big_d = 512;
+    if (const char* e = std::getenv("EIGSOL_MF_BIG_NS")) big_ns = std::atoi(e);
+    if (const char* e = std::getenv("EIGSOL_MF_BIG_D")) big_d = std::atoi(e);
+    std::vector<int32_t> slists, tabf, tabb;
+    std::vector<int64_t> sstart(H + 2, 0), nsmall(H + 1, 0), nbig(H + 1, 0), foff(H + 1, 0), fcnt(H + 1, 0),
+        boff(H + 1, 0), bcnt(H + 1, 0);
+    std::vector<int32_t> lds_asm(H + 1, 0);
+    int32_t nflag = 0;
+    int64_t zsz = 0;
+    for (int32_t h = 0; h <= H; ++h) {
+        std::vector<int32_t> big;
+        for (int64_t t = hstart[h]; t < hstart[h + 1]; ++t) {
+            dev::MfFront& q = fr[lists[t]];
+            const bool is_big = big_ns > 0 && (q.ns >= big_ns || q.d >= big_d);
+            q.flag0 = -1;
+            q.zoff = 0;
+            if (is_big) big.push_back(lists[t]);
+            else slists.push_back(lists[t]);
+        }
+        nsmall[h] = (int64_t)slists.size() - sstart[h];
+        nbig[h] = (int64_t)big.size();
+        slists.insert(slists.end(), big.begin(), big.end());
+        sstart[h + 1] = (int64_t)slists.size();
+        foff[h] = (int64_t)tabf.size() / 2;
+        boff[h] = (int64_t)tabb.size() / 2;
+        for (int32_t b : big) {
+            dev::MfFront& q = fr[b];
+            const int32_t nblk = (q.ns + 63) / 64, nsb = (q.ms + 63) / 64;
+            q.flag0 = nflag;
+            q.zoff = zsz;
+            nflag += nblk;
+            zsz += q.d;
+            for (int32_t k = 0; k < nblk + nsb; ++k) { tabf.push_back(b); tabf.push_back(k); }
+            for (int32_t k = nblk - 1; k >= 0; --k) { tabb.push_back(b); tabb.push_back(k); }
+            lds_asm[h] = std::max<int32_t>(lds_asm[h], (int32_t)(q.ns * sb));
+        }
+        fcnt[h] = (int64_t)tabf.size() / 2 - foff[h];
+        bcnt[h] = (int64_t)tabb.size() / 2 - boff[h];
+    }
     stt.order_seconds = std::chrono::duration<double>(clk::now() - t0).count();
+    if (std::getenv("EIGSOL_MF_DEBUG"))
+        std::fprintf(stderr, "[mf] plan + maps + tables %.3f s; fronts %lld, heights %d, factor entries %.3g, flops %.3g\n",
+                     stt.order_seconds, (long long)nt, H + 1, fac, P.flops);
     // ---- device
     auto* f = new MfFactor();
     f->ctx = ctx;
@@ -888,11 +1204,20 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
     f->nb = NB;
     f->nfront = nt;
     f->hstart = hstart;
+    f->sstart = sstart;
+    f->nsmall = nsmall;
+    f->nbig = nbig;
+    f->foff = foff;
+    f->fcnt = fcnt;
+    f->boff = boff;
+    f->bcnt = bcnt;
+    f->lds_asm = lds_asm;
+    if (const char* e = std::getenv("EIGSOL_MF_BACKOFF")) f->backoff = std::atoi(e);
     f->lds_fwd.assign(H + 1, 0);
     f->lds_bwd.assign(H + 1, 0);
     for (int32_t h = 0; h <= H; ++h)
-        for (int64_t t = hstart[h]; t < hstart[h + 1]; ++t) {
-            const dev::MfFront& q = fr[lists[t]];
+        for (int64_t t = sstart[h]; t < sstart[h] + nsmall[h]; ++t) {
+            const dev::MfFront& q = fr[slists[t]];
             f->lds_fwd[h] = std::max<int32_t>(f->lds_fwd[h], (int32_t)((2 * q.ns + q.ms) * sb));
             f->lds_bwd[h] = std::max<int32_t>(f->lds_bwd[h], (int32_t)((q.ns + q.ms) * sb));
         }
@@ -912,6 +1237,13 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
     dm((void**)&f->perm, n * 4);
     dm((void**)&f->pinv, n * 4);
     dm((void**)&f->lists, lists.size() * 4);
+    dm((void**)&f->slists, slists.size() * 4);
+    dm((void**)&f->tabf, tabf.size() * 4);
+    dm((void**)&f->tabb, tabb.size() * 4);
+    dm((void**)&f->flags, (size_t)nflag * 4);
+    dm((void**)&f->err, 4);
+    dm(&f->z, (size_t)zsz * sb);
+    dm(&f->tinv, (size_t)nflag * 8192 * sb);
     dm(&f->F, (size_t)fe * sb);
     dm(&f->u, (size_t)uo * sb);
     dm(&f->w, n * sb);
@@ -934,6 +1266,11 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
         up(f->cmap, P.cmap.data(), P.cmap.size() * 4);
         up(f->perm, P.perm.data(), n * 4);
         up(f->lists, lists.data(), lists.size() * 4);
+        up(f->slists, slists.data(), slists.size() * 4);
+        up(f->tabf, tabf.data(), tabf.size() * 4);
+        up(f->tabb, tabb.data(), tabb.size() * 4);
+        hipMemsetAsync(f->flags, 0, std::max<size_t>((size_t)nflag * 4, 4), st);
+        hipMemsetAsync(f->err, 0, 4, st);
         up(d_tab, tab.data(), tab.size() * 4);
         up(d_dst, dst.data(), nnz * 8);
         up(d_v, vals, nnz * sb);
@@ -953,11 +1290,15 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
                 hipLaunchKernelGGL((dev::mf_gemm_kernel<S, NB>), dim3(l.cnt), dim3(256), 0, st, f->fronts, d_tab + l.off,
                                    l.q, F);
         }
+        if (!tabb.empty())
+            hipLaunchKernelGGL((dev::mf_inv_kernel<S>), dim3(tabb.size() / 2), dim3(256), 0, st, f->fronts, f->tabb, F,
+                               static_cast<S*>(f->tinv));
         hipMemcpyAsync(hpiv.data(), d_piv, n * 4, hipMemcpyDeviceToHost, st);
         hipMemcpyAsync(&hz, d_z, 4, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal factorization");
         stt.numeric_seconds = std::chrono::duration<double>(clk::now() - t1).count();
+        if (std::getenv("EIGSOL_MF_DEBUG")) std::fprintf(stderr, "[mf] upload + numeric %.3f s\n", stt.numeric_seconds);
     }
     for (void* p : {(void*)d_tab, (void*)d_piv, (void*)d_z, (void*)d_dst, (void*)d_v})
         if (p) hipFree(p);
@@ -979,9 +1320,12 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
         int32_t mx = 0;
         for (int32_t b : f->lds_fwd) mx = std::max(mx, b);
         for (int32_t b : f->lds_bwd) mx = std::max(mx, b);
+        for (int32_t b : f->lds_asm) mx = std::max(mx, b);
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_big_asm_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal solve LDS");
     }
@@ -1005,15 +1349,31 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     const S* F = static_cast<const S*>(f->F);
     hipLaunchKernelGGL((dev::mf_gather_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, b, w, n);
     const int32_t H = (int32_t)f->hstart.size() - 2;
+    S* u = static_cast<S*>(f->u);
+    S* z = static_cast<S*>(f->z);
+    const int32_t ef = ++f->epoch, eb = ++f->epoch;   // flag words: forward, then backward values
     for (int32_t h = 0; h <= H; ++h) {
-        const int64_t cnt = f->hstart[h + 1] - f->hstart[h];
-        hipLaunchKernelGGL((dev::mf_fwd_kernel<S>), dim3(cnt), dim3(256), f->lds_fwd[h], st, f->fronts,
-                           f->lists + f->hstart[h], f->chl, F, f->cmap, f->pinv, w, static_cast<S*>(f->u));
+        const int32_t* L = f->slists + f->sstart[h];
+        if (f->nsmall[h])
+            hipLaunchKernelGGL((dev::mf_fwd_kernel<S>), dim3(f->nsmall[h]), dim3(256), f->lds_fwd[h], st, f->fronts, L,
+                               f->chl, F, f->cmap, f->pinv, w, u);
+        if (f->nbig[h]) {
+            hipLaunchKernelGGL((dev::mf_big_asm_kernel<S>), dim3(f->nbig[h]), dim3(256), f->lds_asm[h], st, f->fronts,
+                               L + f->nsmall[h], f->chl, f->cmap, f->pinv, (const S*)w, (const S*)u, z);
+            hipLaunchKernelGGL((dev::mf_big_fwd_kernel<S>), dim3(f->fcnt[h]), dim3(256), 0, st, f->fronts,
+                               f->tabf + 2 * f->foff[h], F, (const S*)f->tinv, (const S*)z, w, u, f->flags, ef, f->err,
+                               f->backoff);
+        }
     }
     for (int32_t h = H; h >= 0; --h) {
-        const int64_t cnt = f->hstart[h + 1] - f->hstart[h];
-        hipLaunchKernelGGL((dev::mf_bwd_kernel<S>), dim3(cnt), dim3(256), f->lds_bwd[h], st, f->fronts,
-                           f->lists + f->hstart[h], F, f->sidx, w, x);
+        const int32_t* L = f->slists + f->sstart[h];
+        if (f->nbig[h])
+            hipLaunchKernelGGL((dev::mf_big_bwd_kernel<S>), dim3(f->bcnt[h]), dim3(256), 0, st, f->fronts,
+                               f->tabb + 2 * f->boff[h], F, (const S*)f->tinv, f->sidx, (const S*)w, x, f->flags, eb,
+                               f->err, f->backoff);
+        if (f->nsmall[h])
+            hipLaunchKernelGGL((dev::mf_bwd_kernel<S>), dim3(f->nsmall[h]), dim3(256), f->lds_bwd[h], st, f->fronts, L,
+                               F, f->sidx, w, x);
     }
     hipLaunchKernelGGL((dev::mf_scatter_out_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, x, out, n);
     EIGSOL_HIP(hipGetLastError());

@@ -221,3 +221,31 @@ def test_multifrontal_singular_falls_back_or_fails(ctx, env):
         E.solve_shifted(A, sigma, np.ones(400, np.complex128))
     assert ei.value.status == 6
     A.close()
+
+
+@pytest.mark.parametrize("big", ["1", "0", "64"])
+def test_multifrontal_block_row_solve_kernels(ctx, env, big):
+    """Fronts solved by one workgroup per 64-row block (sync-free, flags; EIGSOL_MF_BIG_NS=1: every
+    front), by one workgroup each (=0), or split at 64 pivots: the same solution within the
+    residual bound, bitwise repeatable for each split."""
+    _mf_env(env)
+    env("EIGSOL_MF_BIG_NS", big)
+    env("EIGSOL_MF_LEAF", "24")
+    rp, ci, v = S.convdiff_complex(45, seed=12)
+    n = 45 * 45
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 3.0 - 0.2j
+    assert _variant(A, sigma) == 19
+    b = S.start_vector(n, np.complex128, seed=21)
+    y = E.solve_shifted(A, sigma, b)
+    assert np.linalg.norm(M @ y - sigma * y - b) <= 1e-11 * np.linalg.norm(b)
+    assert np.array_equal(y, E.solve_shifted(A, sigma, b))
+    import scipy.sparse.linalg as sla
+    lam = complex(sla.eigs(M.tocsc(), k=1, sigma=sigma, return_eigenvectors=False)[0])
+    s2 = lam + 1e-5 * (1 + 1j)
+    r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(200, 1e-12, s2), S.start_vector(n, np.complex128))
+    assert r.converged
+    assert abs(r.eigenvalue - lam) <= 1e-10 * (1 + abs(lam)), (r.eigenvalue, lam)
+    assert np.linalg.norm(M @ r.eigenvector - r.eigenvalue * r.eigenvector) <= 1e-9
+    A.close()

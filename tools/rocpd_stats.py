@@ -1,39 +1,25 @@
-"""Per-kernel stats from a rocprofv3 rocpd database (the default output format).
+"""Kernel statistics from a rocprofv3 rocpd database (run_results.db): per kernel name the call
+count, total and average duration; optional name filter and start-time window.
+Usage: python tools/rocpd_stats.py DB [substring] [--top N]"""
+import sqlite3
+import sys
 
-rocprofv3 7.2 segfaults in its exit-time finaliser after a hipLaunchCooperativeKernel (standalone
-repro: tools/coop_prof_repro.hip, no eigsol code involved), so its --stats CSV is never written
-for the cooperative kernels; the rocpd database is complete before that point.  This prints the
-same summary: name, calls, total / average / min / max ns, percentage.
 
-usage: python tools/rocpd_stats.py <dir-or-db> [--csv out.csv] [--filter substring]
-"""
-import argparse, csv, glob, os, sqlite3, sys
-
-ap = argparse.ArgumentParser()
-ap.add_argument("path")
-ap.add_argument("--csv")
-ap.add_argument("--filter", default="")
-args = ap.parse_args()
-dbs = [args.path] if args.path.endswith(".db") else sorted(glob.glob(os.path.join(args.path, "**", "*.db"), recursive=True))
-if not dbs:
-    sys.exit(f"no .db under {args.path}")
-agg = {}
-for db in dbs:
+def main():
+    db = sys.argv[1]
+    filt = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else ""
+    top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 40
     c = sqlite3.connect(db)
-    for name, dur in c.execute("select name, duration from kernels"):
-        a = agg.setdefault(name, [0, 0, None, None])
-        a[0] += 1
-        a[1] += dur
-        a[2] = dur if a[2] is None else min(a[2], dur)
-        a[3] = dur if a[3] is None else max(a[3], dur)
-tot = sum(v[1] for v in agg.values()) or 1
-rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
-out = [["Name", "Calls", "TotalDurationNs", "AverageNs", "MinNs", "MaxNs", "Percentage"]]
-for name, (n, s, lo, hi) in rows:
-    if args.filter in name:
-        out.append([name, n, s, round(s / n, 1), lo, hi, round(100.0 * s / tot, 3)])
-for r in out:
-    print(",".join(str(x) for x in r) if r is out[0] else f"{r[1]:6d} {r[3]:12.1f} ns {r[6]:7.2f}%  {r[0][:120]}")
-if args.csv:
-    with open(args.csv, "w", newline="") as f:
-        csv.writer(f).writerows(out)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    name = "kernel_name" if "kernel_name" in cols else "name"
+    rows = c.execute(f"select {name}, count(*), sum(end - start), avg(end - start) from kernels "
+                     f"where {name} like ? group by {name} order by sum(end - start) desc", (f"%{filt}%",)).fetchall()
+    tot = sum(r[2] for r in rows)
+    print(f"{'calls':>7} {'total_ms':>10} {'avg_us':>10} {'pct':>6}  kernel")
+    for r in rows[:top]:
+        print(f"{r[1]:7d} {r[2] / 1e6:10.3f} {r[3] / 1e3:10.2f} {100 * r[2] / tot:6.1f}  {r[0][:150]}")
+    print(f"total {tot / 1e6:.3f} ms over {sum(r[1] for r in rows)} dispatches")
+
+
+if __name__ == "__main__":
+    main()
