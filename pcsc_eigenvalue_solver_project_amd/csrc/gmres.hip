@@ -27,6 +27,7 @@
 // EIGSOL_E_SOLVER as SparseLU's failed solve (solve_shifted.hpp:112-114); shifted.hip then falls
 // back to the densified LU wherever it fits the device.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <complex>
@@ -35,6 +36,7 @@
 #include <cstring>
 #include <exception>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels_common.hpp"
@@ -228,13 +230,15 @@ static S h_sub(S a, S b) {
 // sorted, the diagonal present.  Returns false (and stops early) once the pattern would exceed cap
 // entries.
 static bool lu_fill_pattern(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int64_t cap,
-                            std::vector<int32_t>& frp, std::vector<int32_t>& fci, std::vector<int32_t>& fdpos) {
+                            std::vector<int32_t>& frp, std::vector<int32_t>& fci, std::vector<int32_t>& fdpos,
+                            const std::atomic<bool>* stop = nullptr) {
     frp.assign(n + 1, 0);
     fci.clear();
     fdpos.assign(n, 0);
     std::vector<int32_t> mark(n, -1), lcols, ucols, heap;
     auto cmp = [](int32_t a, int32_t b) { return a > b; };   // min-heap
     for (int64_t i = 0; i < n; ++i) {
+        if (stop && (i & 1023) == 0 && stop->load(std::memory_order_relaxed)) return false;
         lcols.clear();
         ucols.clear();
         heap.clear();
@@ -335,14 +339,52 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     // 7-10 over ILU(0)).  M's own pattern is kept aside: the exact LU without pivoting meets a zero
     // pivot whenever a leading minor of M is singular, where ILU(0)'s (dropped-fill) pivots may all
     // be nonzero, so that case retries ILU(0) before reporting SparseLU's failure
+    //
+    // The multifrontal plan (host only: nested dissection, symbolic structure, tables) runs on a
+    // second host thread beside the fill attempt; it is used where the fill passes the cap and is
+    // abandoned (stop flag) where the exact LU wins.  EIGSOL_MF=0 skips it; a fill cap below 1
+    // (ILU(0) forced) skips both.
     std::vector<int32_t> orp, oci, odpos;
     std::vector<S> ov;
+    double ratio = 3.0;
+    if (const char* e = std::getenv("EIGSOL_LU_FILL_CAP")) ratio = std::atof(e);
+    MfHost* mfh = nullptr;
+    int mf_prc = EIGSOL_E_UNSUPPORTED;
+    std::atomic<bool> mf_stop{false}, fill_stop{false};
+    std::thread mft;
+    size_t fb = 0;
     {
-        double ratio = 3.0;
-        if (const char* e = std::getenv("EIGSOL_LU_FILL_CAP")) ratio = std::atof(e);
+        const char* me = std::getenv("EIGSOL_MF");
+        size_t tb = 0;
+        if (rc == EIGSOL_OK && ratio >= 1.0 && !(me && !std::strcmp(me, "0"))) {
+            if (hipMemGetInfo(&fb, &tb) == hipSuccess) {
+                mfh = mf_host_new();
+                try {
+                    // a plan whose fronts store more than 6 x nnz(M) is a mesh-like pattern: the
+                    // natural-order fill (capped at 3 x nnz) is then all but certain to pass its cap,
+                    // so the attempt is cut short
+                    mft = std::thread([&] {
+                        mf_prc = mf_prepare(n, mrp, mci, dtype, (double)fb, mfh, &mf_stop);
+                        if (mf_prc == EIGSOL_OK && mf_host_stats(mfh).factor_entries > 6.0 * (double)g->nnzM)
+                            fill_stop.store(true);
+                    });
+                } catch (const std::exception&) {   // no thread: plan on this one after the fill attempt
+                    mf_prc = -1;
+                }
+            }
+        }
+    }
+    {
         std::vector<int32_t> frp, fci, fdpos;
-        if (ratio >= 1.0 && lu_fill_pattern(n, mrp, mci, std::min<int64_t>(INT32_MAX - 1, (int64_t)(ratio * (double)g->nnzM)),
-                                            frp, fci, fdpos)) {
+        const bool filled = ratio >= 1.0 && lu_fill_pattern(n, mrp, mci,
+                                                            std::min<int64_t>(INT32_MAX - 1, (int64_t)(ratio * (double)g->nnzM)),
+                                                            frp, fci, fdpos, &fill_stop);
+        lap("exact-LU fill attempt");
+        if (filled) mf_stop.store(true);
+        if (mft.joinable()) mft.join();
+        if (mf_prc == -1 && !filled) mf_prc = mf_prepare(n, mrp, mci, dtype, (double)fb, mfh);
+        lap("multifrontal plan (joined)");
+        if (filled) {
             std::vector<S> fv(fci.size(), s_zero<S>());
             for (int64_t i = 0; i < n; ++i) {   // both rows sorted: merge M's entries into the pattern
                 int32_t p = frp[i];
@@ -363,20 +405,14 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
         }
     }
     // the exact LU's fill passes the cap: the nested-dissection multifrontal LU (its own ordering,
-    // dense fronts on the matrix cores) where its plan fits the device; ILU(0) otherwise.
-    // EIGSOL_MF=0 skips it; a fill cap below 1 (ILU(0) forced) skips it too
-    {
-        double ratio = 3.0;
-        if (const char* e = std::getenv("EIGSOL_LU_FILL_CAP")) ratio = std::atof(e);
-        const char* me = std::getenv("EIGSOL_MF");
-        if (rc == EIGSOL_OK && !g->complete && ratio >= 1.0 && !(me && !std::strcmp(me, "0"))) {
-            lap("exact-LU fill attempt");
-            const int mrc = mf_create(ctx, dtype, n, mrp, mci, mv.data(), &g->mf);
-            lap("multifrontal create");
-            if (mrc == EIGSOL_OK) g->complete = 2;
-            else if (mrc == EIGSOL_E_HIP) rc = mrc;   // a zero pivot or a declined plan: ILU(0) below
-        }
+    // dense fronts on the matrix cores) where its plan fits the device; ILU(0) otherwise
+    if (rc == EIGSOL_OK && !g->complete && mfh && mf_prc == EIGSOL_OK) {
+        const int mrc = mf_create(ctx, dtype, mfh, mv.data(), &g->mf);
+        lap("multifrontal factor");
+        if (mrc == EIGSOL_OK) g->complete = 2;
+        else if (mrc == EIGSOL_E_HIP) rc = mrc;   // a zero pivot: ILU(0) below
     }
+    if (mfh) mf_host_free(mfh);
     int32_t zpiv = 0;
     std::vector<S> lu;
     // IKJ factorization on the current pattern (mrp/mci/mv/dpos), level by level on the device

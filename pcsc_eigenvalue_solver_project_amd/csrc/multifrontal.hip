@@ -36,12 +36,16 @@
 // only when no pivot is tiny; gmres.hip therefore treats it like the no-pivot exact LU: the solve
 // is checked by its true residual and refined by GMRES cycles on the same factor when it misses.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include "kernels_common.hpp"
@@ -662,44 +666,88 @@ struct SymGraph {
 };
 
 // pattern of M + M^T without the diagonal, each list sorted and unique
+// fn(begin, end) over [0, n) in contiguous chunks on up to nth host threads
+template <class Fn>
+void par_for(int64_t n, int nth, Fn fn) {
+    if (nth <= 1 || n < 4096) { fn((int64_t)0, n); return; }
+    std::vector<std::thread> th;
+    const int64_t chunk = (n + nth - 1) / nth;
+    try {
+        for (int t = 1; t < nth; ++t) {
+            const int64_t b = t * chunk, e = std::min(n, b + chunk);
+            if (b < e) th.emplace_back(fn, b, e);
+        }
+    } catch (const std::exception&) {
+        for (auto& x : th) x.join();
+        fn(chunk, n);   // no more threads: the rest on this one
+        fn((int64_t)0, std::min(n, chunk));
+        return;
+    }
+    fn((int64_t)0, std::min(n, chunk));
+    for (auto& x : th) x.join();
+}
+
+int host_threads() {
+    int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char* e = std::getenv("EIGSOL_MF_THREADS")) nth = std::max(1, std::atoi(e));
+    return nth;
+}
+
+// pattern of M + M^T without the diagonal, each list sorted and unique: M's rows merged with the
+// rows of its transpose (a counting-sort transpose keeps them sorted)
 void sym_graph(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, SymGraph& g) {
-    std::vector<int64_t> deg(n + 1, 0);
-    for (int64_t i = 0; i < n; ++i)
-        for (int32_t e = rp[i]; e < rp[i + 1]; ++e)
-            if (ci[e] != i) { ++deg[i + 1]; ++deg[ci[e] + 1]; }
-    std::vector<int64_t> p(n + 1, 0);
-    for (int64_t i = 0; i < n; ++i) p[i + 1] = p[i] + deg[i + 1];
-    std::vector<int32_t> adj(p[n]);
+    const int nth = host_threads();
+    std::vector<int64_t> tp(n + 1, 0);
+    for (int64_t e = 0; e < (int64_t)rp[n]; ++e) ++tp[ci[e] + 1];
+    for (int64_t i = 0; i < n; ++i) tp[i + 1] += tp[i];
+    std::vector<int32_t> tc(rp[n]);
     {
-        std::vector<int64_t> fill(p.begin(), p.end() - 1);
+        std::vector<int64_t> fill(tp.begin(), tp.end() - 1);
         for (int64_t i = 0; i < n; ++i)
-            for (int32_t e = rp[i]; e < rp[i + 1]; ++e)
-                if (ci[e] != i) { adj[fill[i]++] = ci[e]; adj[fill[ci[e]]++] = (int32_t)i; }
+            for (int32_t e = rp[i]; e < rp[i + 1]; ++e) tc[fill[ci[e]]++] = (int32_t)i;
     }
+    // merge row i of M and of M^T (both ascending), without i and repeats; count, then fill
+    auto merge = [&](int64_t i, int32_t* out) -> int64_t {
+        int64_t a = rp[i], ae = rp[i + 1], b = tp[i], be = tp[i + 1], k = 0;
+        int32_t last = -1;
+        while (a < ae || b < be) {
+            int32_t c;
+            if (b >= be || (a < ae && ci[a] <= tc[b])) c = ci[a++];
+            else c = tc[b++];
+            if (c == i || c == last) continue;
+            last = c;
+            if (out) out[k] = c;
+            ++k;
+        }
+        return k;
+    };
     g.ptr.assign(n + 1, 0);
-    int64_t o = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        auto b = adj.begin() + p[i], e = adj.begin() + p[i + 1];
-        std::sort(b, e);
-        const int64_t u = std::unique(b, e) - b;
-        std::copy(b, b + u, adj.begin() + o);
-        o += u;
-        g.ptr[i + 1] = o;
-    }
-    adj.resize(o);
-    g.adj.swap(adj);
+    par_for(n, nth, [&](int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) g.ptr[i + 1] = merge(i, nullptr);
+    });
+    for (int64_t i = 0; i < n; ++i) g.ptr[i + 1] += g.ptr[i];
+    g.adj.resize(g.ptr[n]);
+    par_for(n, nth, [&](int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) merge(i, g.adj.data() + g.ptr[i]);
+    });
 }
 
 struct NdNode {
     std::vector<int32_t> members;
     int32_t parent;
+    std::vector<int32_t> key;   // position in the dissection (independent of thread timing)
 };
 
-// Nested dissection of the vertices of g: tree nodes (leaves and separators) with parents.
-void nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNode>& tree) {
+// Nested dissection of the vertices of g: tree nodes (leaves and separators) with parents, in a
+// canonical order (sorted by key: the path of choices from the whole graph to the node's piece).
+// Pieces are dissected by a pool of host threads (they touch disjoint vertex sets; a piece's BFS
+// reads its neighbours' set tags with relaxed atomics); the tree does not depend on the timing.
+bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNode>& tree,
+                       const std::atomic<bool>* stop) {
     struct Task {
         std::vector<int32_t> nodes;
         int32_t parent;
+        std::vector<int32_t> key;
     };
     std::vector<Task> stack;
     {
@@ -710,127 +758,205 @@ void nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
         stack.push_back(std::move(t));
     }
     std::vector<int64_t> inset(n, -1), seen(n, -1);
-    std::vector<int32_t> level(n, 0), q;
-    int64_t stamp = 0, bstamp = 0;
-    // BFS inside the current task's set from root: q holds the visit order, level[] the levels
-    auto bfs = [&](int32_t root, int64_t tag) -> int32_t {
-        const int64_t b = ++bstamp;
-        q.clear();
-        q.push_back(root);
-        seen[root] = b;
-        level[root] = 0;
-        int32_t depth = 0;
-        for (size_t h = 0; h < q.size(); ++h) {
-            const int32_t v = q[h];
-            for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
-                const int32_t w = g.adj[e];
-                if (inset[w] != tag || seen[w] == b) continue;
-                seen[w] = b;
-                level[w] = level[v] + 1;
-                depth = std::max(depth, level[w]);
-                q.push_back(w);
-            }
-        }
-        return depth;
+    std::vector<int32_t> level(n, 0);
+    std::atomic<int64_t> stamp{0}, bstamp{0};
+    std::mutex mu;
+    std::condition_variable cv;
+    int active = 0;
+    bool aborted = false;
+    auto tag_of = [&](int32_t v) { return __atomic_load_n(&inset[v], __ATOMIC_RELAXED); };
+    auto add_node = [&](std::vector<int32_t>&& members, int32_t parent, std::vector<int32_t> key) -> int32_t {
+        std::lock_guard<std::mutex> lk(mu);
+        tree.push_back(NdNode{std::move(members), parent, std::move(key)});
+        return (int32_t)tree.size() - 1;
     };
-    auto sub_degree = [&](int32_t v, int64_t tag) {
-        int32_t dgr = 0;
-        for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) dgr += inset[g.adj[e]] == tag;
-        return dgr;
+    auto push_task = [&](Task&& t) {
+        std::lock_guard<std::mutex> lk(mu);
+        stack.push_back(std::move(t));
+        cv.notify_one();
     };
-    while (!stack.empty()) {
-        Task t = std::move(stack.back());
-        stack.pop_back();
-        const int64_t sz = (int64_t)t.nodes.size();
-        if (sz == 0) continue;
-        if (sz <= leaf) {
-            tree.push_back(NdNode{std::move(t.nodes), t.parent});
-            continue;
-        }
-        const int64_t tag = ++stamp;
-        for (int32_t v : t.nodes) inset[v] = tag;
-        bfs(t.nodes[0], tag);
-        if ((int64_t)q.size() < sz) {
-            // disconnected: components; the small ones packed into leaves, the others new tasks
-            std::vector<std::vector<int32_t>> comps;
-            const int64_t b0 = bstamp;   // the first component's BFS; every later one has a larger stamp
-            comps.push_back(q);
-            for (int32_t v : t.nodes) {
-                if (seen[v] >= b0) continue;
-                bfs(v, tag);
-                comps.push_back(q);
-            }
-            std::vector<int32_t> pack;
-            for (auto& c : comps) {
-                if ((int64_t)c.size() > leaf) {
-                    stack.push_back(Task{std::move(c), t.parent});
-                    continue;
-                }
-                if ((int64_t)(pack.size() + c.size()) > leaf) {
-                    tree.push_back(NdNode{std::move(pack), t.parent});
-                    pack.clear();
-                }
-                pack.insert(pack.end(), c.begin(), c.end());
-            }
-            if (!pack.empty()) tree.push_back(NdNode{std::move(pack), t.parent});
-            continue;
-        }
-        // pseudo-peripheral root (George-Liu): restart from a minimum-degree vertex of the last
-        // level while the eccentricity grows
-        int32_t root = t.nodes[0];
-        int32_t ecc = bfs(root, tag);
-        for (int round = 0; round < 2; ++round) {
-            int32_t best = -1, bd = INT32_MAX;
-            for (size_t h = q.size(); h-- > 0;) {
+    auto work = [&]() {
+        std::vector<int32_t> q;
+        // BFS inside the piece tagged `tag` from root: q holds the visit order, level[] the levels
+        auto bfs = [&](int32_t root, int64_t tag) -> int32_t {
+            const int64_t b = ++bstamp;
+            q.clear();
+            q.push_back(root);
+            seen[root] = b;
+            level[root] = 0;
+            int32_t depth = 0;
+            for (size_t h = 0; h < q.size(); ++h) {
                 const int32_t v = q[h];
-                if (level[v] != ecc) break;
-                const int32_t dv = sub_degree(v, tag);
-                if (dv < bd) { bd = dv; best = v; }
+                for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
+                    const int32_t w = g.adj[e];
+                    if (tag_of(w) != tag || seen[w] == b) continue;
+                    seen[w] = b;
+                    level[w] = level[v] + 1;
+                    depth = std::max(depth, level[w]);
+                    q.push_back(w);
+                }
             }
-            const int32_t e2 = bfs(best, tag);
-            if (e2 <= ecc) {
-                if (e2 < ecc) ecc = bfs(root, tag);   // restore the levels of the better root
-                break;
+            return depth;
+        };
+        auto sub_degree = [&](int32_t v, int64_t tag) {
+            int32_t dgr = 0;
+            for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) dgr += tag_of(g.adj[e]) == tag;
+            return dgr;
+        };
+        for (;;) {
+            Task t;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return aborted || !stack.empty() || active == 0; });
+                if (aborted || stack.empty()) { cv.notify_all(); return; }
+                t = std::move(stack.back());
+                stack.pop_back();
+                ++active;
             }
-            root = best;
-            ecc = e2;
-        }
-        const int32_t nlev = ecc + 1;
-        if (nlev < 3) {   // no level structure to cut: one dense front
-            tree.push_back(NdNode{std::move(t.nodes), t.parent});
-            continue;
-        }
-        std::vector<int64_t> cnt(nlev, 0);
-        for (int32_t v : t.nodes) ++cnt[level[v]];
-        int32_t m = 1;
-        {
-            int64_t cum = 0;
-            for (int32_t l = 0; l < nlev; ++l) {
-                if (2 * (cum + cnt[l] / 2) >= sz) { m = l; break; }
-                cum += cnt[l];
+            auto done = [&]() {
+                std::lock_guard<std::mutex> lk(mu);
+                --active;
+                if (active == 0 && stack.empty()) cv.notify_all();
+            };
+            if (stop && stop->load(std::memory_order_relaxed)) {
+                std::lock_guard<std::mutex> lk(mu);
+                aborted = true;
+                --active;
+                cv.notify_all();
+                return;
             }
-            m = std::max(1, std::min(nlev - 2, m));
-        }
-        // separator: the vertices of level m that touch level m + 1; the rest of level m joins A
-        std::vector<int32_t> A, B, Sep;
-        for (int32_t v : t.nodes) {
-            const int32_t l = level[v];
-            if (l < m) A.push_back(v);
-            else if (l > m) B.push_back(v);
-            else {
-                bool touch = false;
-                for (int64_t e = g.ptr[v]; e < g.ptr[v + 1] && !touch; ++e)
-                    touch = inset[g.adj[e]] == tag && level[g.adj[e]] == m + 1;
-                (touch ? Sep : A).push_back(v);
+            const int64_t sz = (int64_t)t.nodes.size();
+            if (sz == 0) { done(); continue; }
+            if (sz <= leaf) {
+                add_node(std::move(t.nodes), t.parent, std::move(t.key));
+                done();
+                continue;
             }
+            const int64_t tag = ++stamp;
+            for (int32_t v : t.nodes) __atomic_store_n(&inset[v], tag, __ATOMIC_RELAXED);
+            bfs(t.nodes[0], tag);
+            if ((int64_t)q.size() < sz) {
+                // disconnected: components (in the order of their first vertex in the piece); the
+                // small ones packed into leaves, the others new pieces
+                std::vector<std::vector<int32_t>> comps;
+                const int64_t b0 = seen[t.nodes[0]];   // this piece's first BFS; later ones are larger
+                comps.push_back(q);
+                for (int32_t v : t.nodes) {
+                    if (seen[v] >= b0) continue;
+                    bfs(v, tag);
+                    comps.push_back(q);
+                }
+                std::vector<int32_t> pack;
+                int32_t slot = 0;
+                auto key_at = [&](int32_t k) {
+                    std::vector<int32_t> kk = t.key;
+                    kk.push_back(k);
+                    return kk;
+                };
+                for (auto& c : comps) {
+                    if ((int64_t)c.size() > leaf) {
+                        push_task(Task{std::move(c), t.parent, key_at(slot++)});
+                        continue;
+                    }
+                    if ((int64_t)(pack.size() + c.size()) > leaf) {
+                        add_node(std::move(pack), t.parent, key_at(slot++));
+                        pack.clear();
+                    }
+                    pack.insert(pack.end(), c.begin(), c.end());
+                }
+                if (!pack.empty()) add_node(std::move(pack), t.parent, key_at(slot++));
+                done();
+                continue;
+            }
+            // pseudo-peripheral root (George-Liu): restart from a minimum-degree vertex of the last
+            // level while the eccentricity grows
+            int32_t root = t.nodes[0];
+            int32_t ecc = bfs(root, tag);
+            for (int round = 0; round < 2; ++round) {
+                int32_t best = -1, bd = INT32_MAX;
+                for (size_t h = q.size(); h-- > 0;) {
+                    const int32_t v = q[h];
+                    if (level[v] != ecc) break;
+                    const int32_t dv = sub_degree(v, tag);
+                    if (dv < bd || (dv == bd && v < best)) { bd = dv; best = v; }
+                }
+                const int32_t e2 = bfs(best, tag);
+                if (e2 <= ecc) {
+                    if (e2 < ecc) ecc = bfs(root, tag);   // restore the levels of the better root
+                    break;
+                }
+                root = best;
+                ecc = e2;
+            }
+            const int32_t nlev = ecc + 1;
+            if (nlev < 3) {   // no level structure to cut: one dense front
+                add_node(std::move(t.nodes), t.parent, std::move(t.key));
+                done();
+                continue;
+            }
+            std::vector<int64_t> cnt(nlev, 0);
+            for (int32_t v : t.nodes) ++cnt[level[v]];
+            int32_t m = 1;
+            {
+                int64_t cum = 0;
+                for (int32_t l = 0; l < nlev; ++l) {
+                    if (2 * (cum + cnt[l] / 2) >= sz) { m = l; break; }
+                    cum += cnt[l];
+                }
+                m = std::max(1, std::min(nlev - 2, m));
+            }
+            // separator: the vertices of level m that touch level m + 1; the rest of level m joins A
+            std::vector<int32_t> A, B, Sep;
+            for (int32_t v : t.nodes) {
+                const int32_t l = level[v];
+                if (l < m) A.push_back(v);
+                else if (l > m) B.push_back(v);
+                else {
+                    bool touch = false;
+                    for (int64_t e = g.ptr[v]; e < g.ptr[v + 1] && !touch; ++e)
+                        touch = tag_of(g.adj[e]) == tag && level[g.adj[e]] == m + 1;
+                    (touch ? Sep : A).push_back(v);
+                }
+            }
+            std::vector<int32_t>().swap(t.nodes);
+            std::vector<int32_t> ka = t.key, kb = t.key;
+            ka.push_back(0);
+            kb.push_back(1);
+            const int32_t id = add_node(std::move(Sep), t.parent, std::move(t.key));
+            push_task(Task{std::move(A), id, std::move(ka)});
+            push_task(Task{std::move(B), id, std::move(kb)});
+            done();
         }
-        const int32_t id = (int32_t)tree.size();
-        tree.push_back(NdNode{std::move(Sep), t.parent});
-        std::vector<int32_t>().swap(t.nodes);
-        stack.push_back(Task{std::move(A), id});
-        stack.push_back(Task{std::move(B), id});
+    };
+    int nth = host_threads();
+    if (n < 20000) nth = 1;
+    std::vector<std::thread> pool;
+    try {
+        for (int i = 1; i < nth; ++i) pool.emplace_back(work);
+    } catch (const std::exception&) {   // fewer threads: the others do the work
     }
+    work();
+    for (auto& th : pool) th.join();
+    if (aborted) return false;
+    // canonical order: by key; parents renumbered
+    std::vector<int32_t> ord(tree.size());
+    std::iota(ord.begin(), ord.end(), 0);
+    std::sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return tree[x].key < tree[y].key; });
+    std::vector<int32_t> newid(tree.size());
+    for (size_t i = 0; i < ord.size(); ++i) newid[ord[i]] = (int32_t)i;
+    std::vector<NdNode> sorted;
+    sorted.reserve(tree.size());
+    for (int32_t o : ord) {
+        NdNode nd = std::move(tree[o]);
+        if (nd.parent >= 0) nd.parent = newid[nd.parent];
+        std::vector<int32_t>().swap(nd.key);
+        sorted.push_back(std::move(nd));
+    }
+    tree.swap(sorted);
+    return true;
 }
+
+}  // namespace
 
 // The ordering and symbolic structure (host only): fronts in postorder with their columns,
 // structs, children, parent maps; per-height lists; work and size figures.
@@ -845,8 +971,11 @@ struct MfPlan {
 };
 
 // returns false on an internal inconsistency (a struct entry outside the ancestors)
+// max_front_entries: the plan is abandoned once the fronts' sum of d^2 passes it (a pattern
+// without small separators, e.g. a random graph); stop: abandoned when raised (another thread's
+// factor won)
 bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int leaf, bool cplx_flops,
-             MfPlan& P) {
+             MfPlan& P, double max_front_entries = 1e300, const std::atomic<bool>* stop = nullptr) {
     static const bool dbg = std::getenv("EIGSOL_MF_DEBUG") != nullptr;
     auto tp = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
@@ -877,18 +1006,20 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
         std::vector<int32_t> lab(n);
         for (int64_t k = 0; k < n; ++k) lab[ord[k]] = (int32_t)k;
         g.ptr.assign(n + 1, 0);
+        for (int64_t k = 0; k < n; ++k) g.ptr[k + 1] = g.ptr[k] + (g0.ptr[ord[k] + 1] - g0.ptr[ord[k]]);
         g.adj.resize(g0.adj.size());
-        for (int64_t k = 0; k < n; ++k) {
-            const int32_t v = ord[k];
-            int64_t o = g.ptr[k];
-            for (int64_t e = g0.ptr[v]; e < g0.ptr[v + 1]; ++e) g.adj[o++] = lab[g0.adj[e]];
-            std::sort(g.adj.begin() + g.ptr[k], g.adj.begin() + o);
-            g.ptr[k + 1] = o;
-        }
+        par_for(n, host_threads(), [&](int64_t b, int64_t e) {
+            for (int64_t k = b; k < e; ++k) {
+                const int32_t v = ord[k];
+                int64_t o = g.ptr[k];
+                for (int64_t x = g0.ptr[v]; x < g0.ptr[v + 1]; ++x) g.adj[o++] = lab[g0.adj[x]];
+                std::sort(g.adj.begin() + g.ptr[k], g.adj.begin() + o);
+            }
+        });
     }
     lap("graph");
     std::vector<NdNode> tree;
-    nested_dissection(n, g, leaf, tree);
+    if (!nested_dissection(n, g, leaf, tree, stop)) return false;
     lap("dissection");
     // postorder numbering: children before parents, each tree node one contiguous column range
     const int64_t nt = (int64_t)tree.size();
@@ -959,6 +1090,7 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
     {
         std::vector<int64_t> mark(n, -1);
         std::vector<int32_t> lst;
+        double fe_run = 0.0;
         for (int64_t s = 0; s < nt; ++s) {
             const int32_t c0 = fr[s].c0, c1 = c0 + fr[s].ns;
             lst.clear();
@@ -982,6 +1114,8 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
             fr[s].ms = (int32_t)lst.size();
             fr[s].sof = sof[s];
             fr[s].d = fr[s].ns + fr[s].ms;
+            fe_run += (double)fr[s].d * (double)fr[s].d;
+            if (fe_run > max_front_entries || (stop && stop->load(std::memory_order_relaxed))) return false;
         }
     }
     std::vector<int64_t>().swap(g.ptr);
@@ -1050,18 +1184,44 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
     return true;
 }
 
-template <class S>
-int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
-                const S* vals, MfFactor** out) {
-    *out = nullptr;
+struct MfLaunch {
+    int kind;   // 0 extend, 1 panel, 2 gemm
+    int32_t h, q;
+    int64_t off, cnt;
+};
+
+struct MfHost {
+    MfPlan P;
+    int64_t n = 0, nnz = 0;
+    int nb = 32;
+    int64_t sb = 16;
+    std::vector<int64_t> dst;              // M's entries -> front offsets
+    std::vector<MfLaunch> plan;            // factorization launches
+    std::vector<int32_t> tab, slists, tabf, tabb, lds_asm;
+    std::vector<int64_t> sstart, nsmall, nbig, foff, fcnt, boff, bcnt;
+    int32_t nflag = 0;
+    int64_t zsz = 0;
+    MfStats stt;
+};
+
+// The host half of the factor: plan, bounds, entry destinations, launch and solve tables.  Needs
+// no device (free_bytes: the device memory the fronts may take), so gmres.hip runs it on a second
+// host thread beside the natural-order fill attempt.
+int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, bool cplx_s,
+                    double free_bytes, MfHost& X, const std::atomic<bool>* stop) {
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    constexpr int NB = dev::RankKMax<S>::value;
-    const int64_t sb = (int64_t)sizeof(S);
+    const int NB = cplx_s ? dev::RankKMax<cplx>::value : dev::RankKMax<double>::value;
+    const int64_t sb = cplx_s ? 16 : 8;
+    X.n = n;
+    X.nb = NB;
+    X.sb = sb;
     int leaf = 64;
     if (const char* e = std::getenv("EIGSOL_MF_LEAF")) leaf = std::max(4, std::atoi(e));
-    MfPlan P;
-    if (!mf_plan(n, rp, ci, leaf, is_cplx_v<S>, P)) return EIGSOL_E_UNSUPPORTED;
+    MfPlan& P = X.P;
+    double cap = 0.45 * free_bytes;
+    if (const char* e = std::getenv("EIGSOL_MF_MAX_GB")) cap = std::min(cap, std::atof(e) * 1073741824.0);
+    if (!mf_plan(n, rp, ci, leaf, cplx_s, P, cap / (double)sb, stop)) return EIGSOL_E_UNSUPPORTED;
     const int64_t nt = P.nt;
     auto& fr = P.fr;
     const auto& chl = P.chl;
@@ -1071,8 +1231,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
     const auto& hstart = P.hstart;
     const int32_t H = P.H;
     const double fe = P.fe, fac = P.fac;
-    const int64_t uo = P.uo;
-    MfStats stt;
+    MfStats& stt = X.stt;
     stt.fronts = nt;
     stt.heights = H + 1;
     stt.max_front = P.maxd;
@@ -1081,16 +1240,14 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
     stt.factor_entries = fac;
     stt.flops = P.flops;
     // bounds: device memory for the fronts, the solve kernels' LDS, the work
-    size_t fr_b = 0, tot_b = 0;
-    hipMemGetInfo(&fr_b, &tot_b);
-    double cap = 0.45 * (double)fr_b;
-    if (const char* e = std::getenv("EIGSOL_MF_MAX_GB")) cap = std::min(cap, std::atof(e) * 1073741824.0);
     const double lds_max = 120.0 * 1024.0;
     if (fe * (double)sb > cap || (double)(P.maxns + P.maxd) * (double)sb > lds_max || P.flops > 4e13)
         return EIGSOL_E_UNSUPPORTED;
     // destinations of M's entries (the caller's numbering) in the fronts
     const int64_t nnz = rp[n];
-    std::vector<int64_t> dst(nnz);
+    X.nnz = nnz;
+    auto& dst = X.dst;
+    dst.assign(nnz, 0);
     auto pos_in = [&](int32_t s, int32_t j) -> int64_t {
         const int32_t c0 = fr[s].c0;
         if (j < c0 + fr[s].ns) return j - c0;
@@ -1108,13 +1265,9 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
         }
     // launch tables: extend-add (child, first column) per (height, child rank); trailing-update
     // tiles (front, tile row, tile column) per (height, panel)
-    struct Launch {
-        int kind;   // 0 extend, 1 panel, 2 gemm
-        int32_t h, q;
-        int64_t off, cnt;
-    };
-    std::vector<Launch> plan;
-    std::vector<int32_t> tab;
+    using Launch = MfLaunch;
+    auto& plan = X.plan;
+    auto& tab = X.tab;
     for (int32_t h = 0; h <= H; ++h) {
         const int32_t* L = lists.data() + hstart[h];
         const int64_t cnt = hstart[h + 1] - hstart[h];
@@ -1155,12 +1308,14 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
     int big_ns = 128, big_d = 512;
     if (const char* e = std::getenv("EIGSOL_MF_BIG_NS")) big_ns = std::atoi(e);
     if (const char* e = std::getenv("EIGSOL_MF_BIG_D")) big_d = std::atoi(e);
-    std::vector<int32_t> slists, tabf, tabb;
-    std::vector<int64_t> sstart(H + 2, 0), nsmall(H + 1, 0), nbig(H + 1, 0), foff(H + 1, 0), fcnt(H + 1, 0),
-        boff(H + 1, 0), bcnt(H + 1, 0);
-    std::vector<int32_t> lds_asm(H + 1, 0);
-    int32_t nflag = 0;
-    int64_t zsz = 0;
+    auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &lds_asm = X.lds_asm;
+    auto &sstart = X.sstart, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff, &fcnt = X.fcnt, &boff = X.boff,
+         &bcnt = X.bcnt;
+    sstart.assign(H + 2, 0);
+    for (auto* v : {&nsmall, &nbig, &foff, &fcnt, &boff, &bcnt}) v->assign(H + 1, 0);
+    lds_asm.assign(H + 1, 0);
+    int32_t& nflag = X.nflag;
+    int64_t& zsz = X.zsz;
     for (int32_t h = 0; h <= H; ++h) {
         std::vector<int32_t> big;
         for (int64_t t = hstart[h]; t < hstart[h + 1]; ++t) {
@@ -1195,6 +1350,38 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t
     if (std::getenv("EIGSOL_MF_DEBUG"))
         std::fprintf(stderr, "[mf] plan + maps + tables %.3f s; fronts %lld, heights %d, factor entries %.3g, flops %.3g\n",
                      stt.order_seconds, (long long)nt, H + 1, fac, P.flops);
+    return EIGSOL_OK;
+}
+
+template <class S>
+int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor** out) {
+    *out = nullptr;
+    using clk = std::chrono::steady_clock;
+    constexpr int NB = dev::RankKMax<S>::value;
+    const int64_t sb = (int64_t)sizeof(S);
+    if (X.nb != NB || X.sb != sb) return fail(EIGSOL_E_INVALID, "solve_shifted: multifrontal plan of another scalar type");
+    const int64_t n = X.n, nnz = X.nnz;
+    MfPlan& P = X.P;
+    const int64_t nt = P.nt;
+    auto& fr = P.fr;
+    const auto& chl = P.chl;
+    const auto& sidx = P.sidx;
+    const auto& lists = P.lists;
+    const auto& hstart = P.hstart;
+    const int32_t H = P.H;
+    const double fe = P.fe, fac = P.fac;
+    const int64_t uo = P.uo;
+    MfStats& stt = X.stt;
+    using Launch = MfLaunch;
+    const auto& dst = X.dst;
+    const auto& plan = X.plan;
+    const auto& tab = X.tab;
+    const auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &lds_asm = X.lds_asm;
+    const auto &sstart = X.sstart, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff, &fcnt = X.fcnt,
+               &boff = X.boff, &bcnt = X.bcnt;
+    const int32_t nflag = X.nflag;
+    const int64_t zsz = X.zsz;
+    (void)plan;
     // ---- device
     auto* f = new MfFactor();
     f->ctx = ctx;
@@ -1380,16 +1567,27 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     return EIGSOL_OK;
 }
 
-}  // namespace
+MfHost* mf_host_new() { return new MfHost(); }
+const MfStats& mf_host_stats(const MfHost* X) { return X->stt; }
+void mf_host_free(MfHost* X) { delete X; }
 
-int mf_create(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
-              const void* v, MfFactor** out) {
+int mf_prepare(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int dtype, double free_bytes,
+               MfHost* X, const std::atomic<bool>* stop) {
+    if (dtype != EIGSOL_C128 && dtype != EIGSOL_F64) return EIGSOL_E_UNSUPPORTED;
+    try {
+        return mf_prepare_host(n, rp, ci, dtype == EIGSOL_C128, free_bytes, *X, stop);
+    } catch (const std::exception&) {   // host allocation of the plan: decline
+        return EIGSOL_E_UNSUPPORTED;
+    }
+}
+
+int mf_create(eigsol_ctx* ctx, int dtype, MfHost* X, const void* v, MfFactor** out) {
     *out = nullptr;
     try {
-        if (dtype == EIGSOL_C128) return mf_create_t<cplx>(ctx, dtype, n, rp, ci, static_cast<const cplx*>(v), out);
-        if (dtype == EIGSOL_F64) return mf_create_t<double>(ctx, dtype, n, rp, ci, static_cast<const double*>(v), out);
-    } catch (const std::exception& ex) {   // host allocation of the plan
-        return fail(EIGSOL_E_UNSUPPORTED, std::string("solve_shifted: multifrontal plan: ") + ex.what());
+        if (dtype == EIGSOL_C128) return mf_create_t<cplx>(ctx, dtype, *X, static_cast<const cplx*>(v), out);
+        if (dtype == EIGSOL_F64) return mf_create_t<double>(ctx, dtype, *X, static_cast<const double*>(v), out);
+    } catch (const std::exception& ex) {
+        return fail(EIGSOL_E_UNSUPPORTED, std::string("solve_shifted: multifrontal factor: ") + ex.what());
     }
     return EIGSOL_E_UNSUPPORTED;
 }

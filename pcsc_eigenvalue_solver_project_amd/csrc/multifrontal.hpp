@@ -3,6 +3,7 @@
 // symbolic LU passes its fill cap (round 5: the permuted 1M convection-diffusion matrix).
 #pragma once
 
+#include <atomic>
 #include <vector>
 
 #include "internal.hpp"
@@ -21,12 +22,19 @@ struct MfStats {
     double solve_bytes = 0.0;      // algorithmic bytes of one solve (factor entries + vectors)
 };
 
-// M (n x n, CSR with sorted rows and every diagonal stored; values S = double or cplx per dtype).
-// Returns EIGSOL_OK with *out, EIGSOL_E_UNSUPPORTED when the plan exceeds its bounds (memory,
-// LDS, work; the caller keeps another path; no error text is kept), EIGSOL_E_SOLVER on a zero
-// pivot, or EIGSOL_E_HIP.
-int mf_create(eigsol_ctx* ctx, int dtype, int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
-              const void* v, MfFactor** out);
+struct MfHost;   // the host half of a factor (ordering, symbolic structure, launch tables)
+MfHost* mf_host_new();
+void mf_host_free(MfHost* X);
+const MfStats& mf_host_stats(const MfHost* X);   // after a successful mf_prepare
+// Host only (thread-safe, no device call): the plan for the pattern of M (n x n, CSR with sorted
+// rows and every diagonal stored), dtype EIGSOL_F64 or EIGSOL_C128, its fronts bounded by
+// free_bytes of device memory.  EIGSOL_OK, or EIGSOL_E_UNSUPPORTED when the plan exceeds its
+// bounds (memory, LDS, work; no error text is kept) or *stop was raised while it ran.
+int mf_prepare(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int dtype, double free_bytes,
+               MfHost* X, const std::atomic<bool>* stop = nullptr);
+// The device half on a prepared plan with M's values: EIGSOL_OK with *out, EIGSOL_E_SOLVER on a
+// zero pivot, or EIGSOL_E_HIP.
+int mf_create(eigsol_ctx* ctx, int dtype, MfHost* X, const void* v, MfFactor** out);
 // x = M^-1 b (device vectors, the caller's numbering), stream-ordered on ctx's stream
 int mf_solve(MfFactor* f, const void* b, void* x);
 void mf_free(MfFactor* f);

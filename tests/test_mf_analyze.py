@@ -123,3 +123,17 @@ def test_argument_errors():
     assert lib().eigsol_mf_analyze(100, rp2.ctypes.data, ci2.ctypes.data, 0, 1, None, None, 0, st) == 9
     fr = np.empty((1, 4), np.int32)
     assert lib().eigsol_mf_analyze(100, rp2.ctypes.data, ci2.ctypes.data, 4, 1, None, fr.ctypes.data, 1, st) == 9
+
+
+def test_plan_independent_of_host_threads(monkeypatch):
+    """The dissection runs on a pool of host threads past n = 20000; the tree is put in a canonical
+    order, so the plan is identical for any thread count."""
+    rp, ci, _ = S.convdiff_complex(160, seed=9)
+    n = 160 * 160
+    out = []
+    for t in ("1", "3", "8"):
+        monkeypatch.setenv("EIGSOL_MF_THREADS", t)
+        out.append(analyze(rp, ci, n, leaf=64))
+    for st, perm, fr in out[1:]:
+        assert st == out[0][0] and np.array_equal(perm, out[0][1]) and np.array_equal(fr, out[0][2])
+    check_plan(rp, ci, n, 64)
