@@ -592,9 +592,30 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
     // r0 = b / bdiv (x0 = 0)
     hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, (const S*)nullptr, w, n);
     double beta = 0.0;
-    EIGSOL_TRY(norm_of(w, beta));
+    bool direct_done = false;
+    if (g->complete && !guess) {
+        // exact factor: ||r0||, x = K^-1 r0, r = r0 - M x and ||r|| with one host wait
+        hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
+        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev);
+        EIGSOL_TRY(precond(w, x));
+        EIGSOL_TRY(eigsol_csr_spmv(g->M, x, t1));
+        hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, t1, w, n);
+        hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
+        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev + 2);
+        EIGSOL_HIP(hipMemcpyAsync(g->hpin, g->hdev, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(stream_wait(st));
+        beta = std::sqrt(g->hpin[0]);
+        direct_done = true;
+    } else {
+        EIGSOL_TRY(norm_of(w, beta));
+    }
     const double bnorm = beta;
-    EIGSOL_HIP(hipMemsetAsync(x, 0, n * sizeof(S), st));
+    if (direct_done) {
+        beta = bnorm > 0.0 ? std::sqrt(g->hpin[2]) : 0.0;
+        bytes += lb + ub + mb + 3.0 * sb * (double)n;
+    } else {
+        EIGSOL_HIP(hipMemsetAsync(x, 0, n * sizeof(S), st));
+    }
     // Warm start for the shifted inverse iteration: once x_t is close to the eigenvector v
     // ((A - sigma I) v = (lambda - sigma) v), y_t = (A - sigma I)^{-1} x_t is close to
     // x_t / (lambda_{t-1} - sigma): x0 = guess * b / bdiv leaves a residual that shrinks with the
@@ -615,13 +636,7 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
     }
     // exact LU (complete fill): x = U^-1 L^-1 r0 directly; GMRES cycles below only if its true
     // residual misses rtol_true (iterative refinement on the same factors)
-    if (g->complete && !guess && bnorm > 0.0) {
-        EIGSOL_TRY(precond(w, x));
-        EIGSOL_TRY(eigsol_csr_spmv(g->M, x, t1));
-        hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, t1, w, n);
-        EIGSOL_TRY(norm_of(w, beta));
-        bytes += lb + ub + mb + 3.0 * sb * (double)n;
-    }
+    // (exact LU: done above, before the first host wait)
     double relres = beta / (bnorm > 0.0 ? bnorm : 1.0);
     int cycles = 0;
     if (bnorm > 0.0 && beta > 0.0 && relres > g->rtol_true) {

@@ -350,6 +350,125 @@ __global__ __launch_bounds__(256) void mf_bwd_kernel(const MfFront* fr, const in
     for (int k = tid; k < ns; k += 256) x[f.c0 + k] = t[k];
 }
 
+// ---- small fronts (ns <= 64 pivots, ms <= 192 struct rows): one wave per front, four fronts per
+// workgroup, no workgroup barrier (each wave's LDS slice is its own), so a CU keeps up to 32
+// fronts in flight.  Same arithmetic order as mf_fwd_kernel / mf_bwd_kernel's single block.
+constexpr int kWaveNs = 64, kWaveMs = 192;
+
+__device__ __forceinline__ void mf_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void mf_fwd_wave_kernel(const MfFront* fr, const int32_t* list, int32_t cnt,
+                                                          const int32_t* chl, const S* F, const int32_t* cmap,
+                                                          const int32_t* pinv, S* w, S* u) {
+    __shared__ S sh[4][2 * kWaveNs + kWaveMs];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int t = blockIdx.x * 4 + wv;
+    if (t >= cnt) return;
+    const MfFront f = fr[list[t]];
+    const int d = f.d, ns = f.ns, ms = f.ms;
+    S* r = sh[wv];
+    S* y = r + kWaveNs;
+    S* acc = y + kWaveNs;
+    if (lane < ns) r[lane] = w[f.c0 + lane];
+    for (int k = lane; k < ms; k += 64) acc[k] = s_zero<S>();
+    mf_wave_sync();
+    for (int k = f.ch0; k < f.ch1; ++k) {
+        const MfFront c = fr[chl[k]];
+        const int32_t* map = cmap + c.sof;
+        const S* uc = u + c.uoff;
+        for (int q = lane; q < c.ms; q += 64) {
+            const int pos = map[q];
+            const S v = uc[q];
+            if (pos < ns) r[pos] = sub(r[pos], v);
+            else acc[pos - ns] = add(acc[pos - ns], v);
+        }
+        mf_wave_sync();
+    }
+    const S* A = F + f.off;
+    S v = lane < ns ? r[pinv[f.c0 + lane]] : s_zero<S>();
+    const int row = min(lane, ns - 1);
+    for (int j0 = 0; j0 < ns; j0 += 16) {
+        S lv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) lv[q] = A[row + (int64_t)min(j0 + q, ns - 1) * d];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int j = j0 + q;
+            if (j < ns) {
+                const S yj = mf_rl(v, j);
+                if (lane > j) v = sub(v, mul(lv[q], yj));
+            }
+        }
+    }
+    if (lane < ns) {
+        y[lane] = v;
+        w[f.c0 + lane] = v;
+    }
+    mf_wave_sync();
+    for (int i = ns + lane; i < d; i += 64) {
+        S sacc = s_zero<S>();
+        const S* Ai = A + i;
+        for (int j0 = 0; j0 < ns; j0 += 16) {
+            S lv[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) lv[q] = Ai[(int64_t)min(j0 + q, ns - 1) * d];
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (j0 + q < ns) sacc = add(sacc, mul(lv[q], y[j0 + q]));
+        }
+        u[f.uoff + (i - ns)] = add(acc[i - ns], sacc);
+    }
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void mf_bwd_wave_kernel(const MfFront* fr, const int32_t* list, int32_t cnt,
+                                                          const S* F, const int32_t* sidx, const S* w, S* x) {
+    __shared__ S sh[4][kWaveMs];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int t = blockIdx.x * 4 + wv;
+    if (t >= cnt) return;
+    const MfFront f = fr[list[t]];
+    const int d = f.d, ns = f.ns, ms = f.ms;
+    S* xs = sh[wv];
+    for (int q = lane; q < ms; q += 64) xs[q] = x[sidx[f.sof + q]];
+    mf_wave_sync();
+    const S* A = F + f.off;
+    const int row = min(lane, ns - 1);
+    S s = s_zero<S>();
+    {
+        const S* Ak = A + row + (int64_t)ns * d;
+        for (int q0 = 0; q0 < ms; q0 += 16) {
+            S uv[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) uv[e] = Ak[(int64_t)min(q0 + e, ms - 1) * d];
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+                if (q0 + e < ms) s = add(s, mul(uv[e], xs[q0 + e]));
+        }
+    }
+    S v = lane < ns ? sub(w[f.c0 + lane], s) : s_zero<S>();
+    for (int j1 = ns; j1 > 0; j1 -= 16) {
+        S uv[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) uv[e] = A[row + (int64_t)max(j1 - 1 - e, 0) * d];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int j = j1 - 1 - e;
+            if (j >= 0) {
+                if (lane == j) v = sdiv(v, uv[e]);
+                const S xj = mf_rl(v, j);
+                if (lane < j) v = sub(v, mul(uv[e], xj));
+            }
+        }
+    }
+    if (lane < ns) x[f.c0 + lane] = v;
+}
+
 // ---- large fronts: one workgroup per 64-row block, sync-free (the dense path's blocked TRSV,
 // shifted.hip dense_trsv_kernel, on a front).  Pivot block k of a front publishes its solved 64
 // values with write-through stores and raises flag[flag0 + k] to the solve's epoch; a row block
@@ -360,8 +479,11 @@ __global__ __launch_bounds__(256) void mf_bwd_kernel(const MfFront* fr, const in
 // a few hundred workgroups), or the dense TRSV's growing sleeps (EIGSOL_MF_BACKOFF=1)
 __device__ __forceinline__ void mf_wait(const int32_t* f, int32_t epoch, int32_t* err, int bo) {
     int spins = 0;
-    while (__hip_atomic_load(const_cast<int32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-        if (!bo) __builtin_amdgcn_s_sleep(1);
+    for (;;) {
+        const int32_t v = (bo & 2) ? __hip_atomic_load(const_cast<int32_t*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : __hip_atomic_load(const_cast<int32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == epoch) break;
+        if (!(bo & 1)) __builtin_amdgcn_s_sleep(1);
         else if (spins < 4) __builtin_amdgcn_s_sleep(2);
         else if (spins < 16) __builtin_amdgcn_s_sleep(8);
         else __builtin_amdgcn_s_sleep(32);
@@ -499,7 +621,7 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
         for (int t = 0; t < 16; ++t) tv[t] = tile[(int64_t)min(c0 + t, ns - 1) * d];
         if (lane == 0) mf_wait(flag + f.flag0 + c, epoch, err, bo);
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (!(bo & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_ld(w + f.c0 + c0 + lane) : s_zero<S>();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -527,7 +649,10 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
     const S y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
     if (lane < rn) mf_st(w + f.c0 + r0 + lane, y);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        if (bo & 4) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // backward, large fronts: tab = (front, pivot block) pairs, blocks descending within a front:
@@ -577,7 +702,7 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
         for (int t = 0; t < 16; ++t) tv[t] = tile[(int64_t)min(c0 + t, ns - 1) * d];
         if (lane == 0) mf_wait(flag + f.flag0 + c, epoch, err, bo);
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (!(bo & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_ld(x + f.c0 + c0 + lane) : s_zero<S>();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -602,7 +727,10 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
     const S xv = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
     if (lane < rn) mf_st(x + f.c0 + r0 + lane, xv);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        if (bo & 4) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 }  // namespace dev
@@ -638,8 +766,8 @@ struct MfFactor {
     void* z = nullptr;                // large fronts' assembled right-hand sides
     void* tinv = nullptr;             // inverted diagonal blocks of the large fronts (8192 scalars each)
     int32_t epoch = 0;
-    int backoff = 0;                  // EIGSOL_MF_BACKOFF
-    std::vector<int64_t> sstart, nsmall, nbig, foff, fcnt, boff, bcnt;
+    int backoff = 2;                  // EIGSOL_MF_BACKOFF: 1 growing sleeps, 2 relaxed polls, 4 relaxed flag stores
+    std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt;
     std::vector<int32_t> lds_asm;
     MfStats st;
 };
@@ -1198,7 +1326,7 @@ struct MfHost {
     std::vector<int64_t> dst;              // M's entries -> front offsets
     std::vector<MfLaunch> plan;            // factorization launches
     std::vector<int32_t> tab, slists, tabf, tabb, lds_asm;
-    std::vector<int64_t> sstart, nsmall, nbig, foff, fcnt, boff, bcnt;
+    std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt;
     int32_t nflag = 0;
     int64_t zsz = 0;
     MfStats stt;
@@ -1305,28 +1433,36 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
     }
     // solve plan: fronts with many pivots or rows are solved by one workgroup per 64-row block
     // (mf_big_*), the others by one workgroup each (mf_fwd / mf_bwd)
-    int big_ns = 128, big_d = 512;
+    int big_ns = 96, big_d = 256;
     if (const char* e = std::getenv("EIGSOL_MF_BIG_NS")) big_ns = std::atoi(e);
     if (const char* e = std::getenv("EIGSOL_MF_BIG_D")) big_d = std::atoi(e);
     auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &lds_asm = X.lds_asm;
-    auto &sstart = X.sstart, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff, &fcnt = X.fcnt, &boff = X.boff,
-         &bcnt = X.bcnt;
+    auto &sstart = X.sstart, &nwave = X.nwave, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff, &fcnt = X.fcnt,
+         &boff = X.boff, &bcnt = X.bcnt;
     sstart.assign(H + 2, 0);
-    for (auto* v : {&nsmall, &nbig, &foff, &fcnt, &boff, &bcnt}) v->assign(H + 1, 0);
+    for (auto* v : {&nwave, &nsmall, &nbig, &foff, &fcnt, &boff, &bcnt}) v->assign(H + 1, 0);
+    // one wave per small front (EIGSOL_MF_WAVE=1): measured 2.21 against 2.01 ms per 1M iteration
+    // with one workgroup per front - the same loads in flight per CU, and the struct rows' GEMV on
+    // one wave instead of four
+    bool wave_ok = false;
+    if (const char* e = std::getenv("EIGSOL_MF_WAVE")) wave_ok = std::atoi(e) != 0;
     lds_asm.assign(H + 1, 0);
     int32_t& nflag = X.nflag;
     int64_t& zsz = X.zsz;
     for (int32_t h = 0; h <= H; ++h) {
-        std::vector<int32_t> big;
+        std::vector<int32_t> big, wg;
         for (int64_t t = hstart[h]; t < hstart[h + 1]; ++t) {
             dev::MfFront& q = fr[lists[t]];
             const bool is_big = big_ns > 0 && (q.ns >= big_ns || q.d >= big_d);
             q.flag0 = -1;
             q.zoff = 0;
             if (is_big) big.push_back(lists[t]);
-            else slists.push_back(lists[t]);
+            else if (wave_ok && q.ns <= dev::kWaveNs && q.ms <= dev::kWaveMs) slists.push_back(lists[t]);
+            else wg.push_back(lists[t]);
         }
-        nsmall[h] = (int64_t)slists.size() - sstart[h];
+        nwave[h] = (int64_t)slists.size() - sstart[h];
+        slists.insert(slists.end(), wg.begin(), wg.end());
+        nsmall[h] = (int64_t)wg.size();
         nbig[h] = (int64_t)big.size();
         slists.insert(slists.end(), big.begin(), big.end());
         sstart[h + 1] = (int64_t)slists.size();
@@ -1377,8 +1513,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     const auto& plan = X.plan;
     const auto& tab = X.tab;
     const auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &lds_asm = X.lds_asm;
-    const auto &sstart = X.sstart, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff, &fcnt = X.fcnt,
-               &boff = X.boff, &bcnt = X.bcnt;
+    const auto &sstart = X.sstart, &nwave = X.nwave, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff,
+               &fcnt = X.fcnt, &boff = X.boff, &bcnt = X.bcnt;
     const int32_t nflag = X.nflag;
     const int64_t zsz = X.zsz;
     (void)plan;
@@ -1392,6 +1528,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     f->nfront = nt;
     f->hstart = hstart;
     f->sstart = sstart;
+    f->nwave = nwave;
     f->nsmall = nsmall;
     f->nbig = nbig;
     f->foff = foff;
@@ -1403,7 +1540,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     f->lds_fwd.assign(H + 1, 0);
     f->lds_bwd.assign(H + 1, 0);
     for (int32_t h = 0; h <= H; ++h)
-        for (int64_t t = sstart[h]; t < sstart[h] + nsmall[h]; ++t) {
+        for (int64_t t = sstart[h] + nwave[h]; t < sstart[h] + nwave[h] + nsmall[h]; ++t) {
             const dev::MfFront& q = fr[slists[t]];
             f->lds_fwd[h] = std::max<int32_t>(f->lds_fwd[h], (int32_t)((2 * q.ns + q.ms) * sb));
             f->lds_bwd[h] = std::max<int32_t>(f->lds_bwd[h], (int32_t)((q.ns + q.ms) * sb));
@@ -1541,12 +1678,16 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     const int32_t ef = ++f->epoch, eb = ++f->epoch;   // flag words: forward, then backward values
     for (int32_t h = 0; h <= H; ++h) {
         const int32_t* L = f->slists + f->sstart[h];
+        const int64_t nw = f->nwave[h];
+        if (nw)
+            hipLaunchKernelGGL((dev::mf_fwd_wave_kernel<S>), dim3((nw + 3) / 4), dim3(256), 0, st, f->fronts, L,
+                               (int32_t)nw, f->chl, F, f->cmap, f->pinv, w, u);
         if (f->nsmall[h])
-            hipLaunchKernelGGL((dev::mf_fwd_kernel<S>), dim3(f->nsmall[h]), dim3(256), f->lds_fwd[h], st, f->fronts, L,
-                               f->chl, F, f->cmap, f->pinv, w, u);
+            hipLaunchKernelGGL((dev::mf_fwd_kernel<S>), dim3(f->nsmall[h]), dim3(256), f->lds_fwd[h], st, f->fronts,
+                               L + nw, f->chl, F, f->cmap, f->pinv, w, u);
         if (f->nbig[h]) {
             hipLaunchKernelGGL((dev::mf_big_asm_kernel<S>), dim3(f->nbig[h]), dim3(256), f->lds_asm[h], st, f->fronts,
-                               L + f->nsmall[h], f->chl, f->cmap, f->pinv, (const S*)w, (const S*)u, z);
+                               L + nw + f->nsmall[h], f->chl, f->cmap, f->pinv, (const S*)w, (const S*)u, z);
             hipLaunchKernelGGL((dev::mf_big_fwd_kernel<S>), dim3(f->fcnt[h]), dim3(256), 0, st, f->fronts,
                                f->tabf + 2 * f->foff[h], F, (const S*)f->tinv, (const S*)z, w, u, f->flags, ef, f->err,
                                f->backoff);
@@ -1558,9 +1699,13 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
             hipLaunchKernelGGL((dev::mf_big_bwd_kernel<S>), dim3(f->bcnt[h]), dim3(256), 0, st, f->fronts,
                                f->tabb + 2 * f->boff[h], F, (const S*)f->tinv, f->sidx, (const S*)w, x, f->flags, eb,
                                f->err, f->backoff);
+        const int64_t nw = f->nwave[h];
         if (f->nsmall[h])
-            hipLaunchKernelGGL((dev::mf_bwd_kernel<S>), dim3(f->nsmall[h]), dim3(256), f->lds_bwd[h], st, f->fronts, L,
-                               F, f->sidx, w, x);
+            hipLaunchKernelGGL((dev::mf_bwd_kernel<S>), dim3(f->nsmall[h]), dim3(256), f->lds_bwd[h], st, f->fronts,
+                               L + nw, F, f->sidx, w, x);
+        if (nw)
+            hipLaunchKernelGGL((dev::mf_bwd_wave_kernel<S>), dim3((nw + 3) / 4), dim3(256), 0, st, f->fronts, L,
+                               (int32_t)nw, F, f->sidx, w, x);
     }
     hipLaunchKernelGGL((dev::mf_scatter_out_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, x, out, n);
     EIGSOL_HIP(hipGetLastError());
