@@ -47,6 +47,9 @@ namespace eigsol {
 struct ShiftFactor;
 int shift_factor_tri(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<int32_t>& rp, std::vector<int32_t>& ci,
                      const void* vals, bool up, ShiftFactor** out);
+int shift_factor_tri_dev(eigsol_ctx* ctx, int dtype, int64_t n, int32_t* rp, int32_t* ci, void* vals, int64_t nnz,
+                         bool up, ShiftFactor** out);
+hipError_t tri_exclusive_scan(hipStream_t st, const int32_t* in, int32_t* out, int64_t n);
 int shift_solve_launch(ShiftFactor* f, const void* b_dev, void* y_dev);
 int shift_error(ShiftFactor* f);
 void shift_factor_free(ShiftFactor* f);
@@ -83,6 +86,42 @@ __global__ __launch_bounds__(256) void ilu0_level_kernel(const int32_t* rp, cons
     if constexpr (std::is_same_v<S, double>) z = d == 0.0;
     else z = d.re == 0.0 && d.im == 0.0;
     if (z) atomicOr(zpiv, 1);
+}
+
+// L / U split of the factored pattern: row counts (lcnt[n] = ucnt[n] = 0 for the exclusive scan)
+__global__ __launch_bounds__(256) void gm_split_count_kernel(const int32_t* rp, const int32_t* dpos, int64_t n,
+                                                             int32_t* lcnt, int32_t* ucnt) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        lcnt[i] = dpos[i] - rp[i] + 1;
+        ucnt[i] = rp[i + 1] - dpos[i];
+    } else if (i == n) {
+        lcnt[n] = 0;
+        ucnt[n] = 0;
+    }
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void gm_split_fill_kernel(const int32_t* rp, const int32_t* ci, const S* v,
+                                                            const int32_t* dpos, int64_t n, const int32_t* lrp,
+                                                            const int32_t* urp, int32_t* lci, S* lv, int32_t* uci,
+                                                            S* uv) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    int32_t o = lrp[i];
+    for (int32_t e = rp[i]; e < dpos[i]; ++e, ++o) {
+        lci[o] = ci[e];
+        lv[o] = v[e];
+    }
+    lci[o] = (int32_t)i;
+    S one;
+    set_re_im(one, 1.0, 0.0);
+    lv[o] = one;
+    o = urp[i];
+    for (int32_t e = dpos[i]; e < rp[i + 1]; ++e, ++o) {
+        uci[o] = ci[e];
+        uv[o] = v[e];
+    }
 }
 
 // part[(blk * k + c) * 2 + {0, 1}] = block partial of sum_i conj(V(i, c)) w(i)
@@ -414,9 +453,20 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     }
     if (mfh) mf_host_free(mfh);
     int32_t zpiv = 0;
-    std::vector<S> lu;
+    // the factored pattern stays on the device: L and U are split from it there (round 5: the host
+    // split of the 1M general-sparse factor took 0.26 s plus a 0.4 GB round trip)
+    int32_t *k_rp = nullptr, *k_ci = nullptr, *k_dpos = nullptr;
+    S* k_v = nullptr;
+    auto free_k = [&]() {
+        hipStreamSynchronize(st);
+        for (void* p : {(void*)k_rp, (void*)k_ci, (void*)k_v, (void*)k_dpos})
+            if (p) hipFree(p);
+        k_rp = k_ci = k_dpos = nullptr;
+        k_v = nullptr;
+    };
     // IKJ factorization on the current pattern (mrp/mci/mv/dpos), level by level on the device
     auto factor = [&]() -> int {
+        free_k();
         g->nnzK = (int64_t)mci.size();
         // ILU(0) levels: level(i) = 1 + max level of the rows its strict lower part reads
         std::vector<int32_t> lev(n, 0), lcount;
@@ -434,36 +484,34 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
             for (int64_t i = 0; i < n; ++i) rows[fill[lev[i]]++] = (int32_t)i;
         }
         int frc = EIGSOL_OK;
-        int32_t *d_rp = nullptr, *d_ci = nullptr, *d_dpos = nullptr, *d_rows = nullptr, *d_z = nullptr;
-        S* d_v = nullptr;
-        if (hipMalloc(&d_rp, (n + 1) * 4) != hipSuccess || hipMalloc(&d_ci, std::max<int64_t>(1, g->nnzK) * 4) != hipSuccess ||
-            hipMalloc(&d_v, std::max<int64_t>(1, g->nnzK) * sizeof(S)) != hipSuccess ||
-            hipMalloc(&d_dpos, n * 4) != hipSuccess || hipMalloc(&d_rows, n * 4) != hipSuccess ||
+        int32_t *d_rows = nullptr, *d_z = nullptr;
+        if (hipMalloc(&k_rp, (n + 1) * 4) != hipSuccess || hipMalloc(&k_ci, std::max<int64_t>(1, g->nnzK) * 4) != hipSuccess ||
+            hipMalloc(&k_v, std::max<int64_t>(1, g->nnzK) * sizeof(S)) != hipSuccess ||
+            hipMalloc(&k_dpos, n * 4) != hipSuccess || hipMalloc(&d_rows, n * 4) != hipSuccess ||
             hipMalloc(&d_z, 4) != hipSuccess)
             frc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) buffers");
         zpiv = 0;
-        lu.assign(g->nnzK, s_zero<S>());
         if (frc == EIGSOL_OK) {
-            hipMemcpyAsync(d_rp, mrp.data(), (n + 1) * 4, hipMemcpyHostToDevice, st);
-            hipMemcpyAsync(d_ci, mci.data(), g->nnzK * 4, hipMemcpyHostToDevice, st);
-            hipMemcpyAsync(d_v, mv.data(), g->nnzK * sizeof(S), hipMemcpyHostToDevice, st);
-            hipMemcpyAsync(d_dpos, dpos.data(), n * 4, hipMemcpyHostToDevice, st);
+            hipMemcpyAsync(k_rp, mrp.data(), (n + 1) * 4, hipMemcpyHostToDevice, st);
+            hipMemcpyAsync(k_ci, mci.data(), g->nnzK * 4, hipMemcpyHostToDevice, st);
+            hipMemcpyAsync(k_v, mv.data(), g->nnzK * sizeof(S), hipMemcpyHostToDevice, st);
+            hipMemcpyAsync(k_dpos, dpos.data(), n * 4, hipMemcpyHostToDevice, st);
             hipMemcpyAsync(d_rows, rows.data(), n * 4, hipMemcpyHostToDevice, st);
             hipMemsetAsync(d_z, 0, 4, st);
             for (size_t l = 0; l < lcount.size(); ++l) {
                 const int32_t cnt = lcount[l];
-                hipLaunchKernelGGL((dev::ilu0_level_kernel<S>), dim3((cnt + 255) / 256), dim3(256), 0, st, d_rp, d_ci,
-                                   d_dpos, d_v, d_rows + lstart[l], cnt, d_z);
+                hipLaunchKernelGGL((dev::ilu0_level_kernel<S>), dim3((cnt + 255) / 256), dim3(256), 0, st, k_rp, k_ci,
+                                   k_dpos, k_v, d_rows + lstart[l], cnt, d_z);
             }
             hipMemcpyAsync(&zpiv, d_z, 4, hipMemcpyDeviceToHost, st);
-            hipMemcpyAsync(lu.data(), d_v, g->nnzK * sizeof(S), hipMemcpyDeviceToHost, st);
             if (stream_wait(st) != hipSuccess) frc = fail(EIGSOL_E_HIP, "solve_shifted: ILU(0) factorization");
         }
-        for (void* p : {(void*)d_rp, (void*)d_ci, (void*)d_v, (void*)d_dpos, (void*)d_rows, (void*)d_z})
+        for (void* p : {(void*)d_rows, (void*)d_z})
             if (p) hipFree(p);
         return frc;
     };
     if (rc == EIGSOL_OK && !g->mf) rc = factor();
+    lap("numeric factor (IKJ levels)");
     if (rc == EIGSOL_OK && zpiv && g->complete) {
         // the exact LU met a zero pivot: ILU(0) on M's own pattern (GMRES then iterates over it)
         mrp.swap(orp);
@@ -481,24 +529,43 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
         rc = fail(EIGSOL_E_SOLVER, g->complete ? "solve_shifted: sparse LU (complete fill, no pivoting) met a zero pivot"
                                                : "solve_shifted: ILU(0) factorization met a zero pivot");
     if (rc == EIGSOL_OK && !g->mf) {
-        // split: L = strict lower + unit diagonal (columns ascending: the lower part, then i), U =
-        // diagonal + strict upper
-        std::vector<int32_t> lrp(n + 1, 0), lci, urp(n + 1, 0), uci;
-        std::vector<S> lv, uv;
-        S one;
-        if constexpr (std::is_same_v<S, double>) one = 1.0;
-        else one = S{1.0, 0.0};
-        for (int64_t i = 0; i < n; ++i) {
-            for (int32_t e = mrp[i]; e < dpos[i]; ++e) { lci.push_back(mci[e]); lv.push_back(lu[e]); }
-            lci.push_back((int32_t)i);
-            lv.push_back(one);
-            lrp[i + 1] = (int32_t)lci.size();
-            for (int32_t e = dpos[i]; e < mrp[i + 1]; ++e) { uci.push_back(mci[e]); uv.push_back(lu[e]); }
-            urp[i + 1] = (int32_t)uci.size();
+        // split on the device: L = strict lower + unit diagonal (columns ascending: the lower part,
+        // then i), U = diagonal + strict upper
+        int32_t *lrp = nullptr, *urp = nullptr, *lci = nullptr, *uci = nullptr, *lcnt = nullptr, *ucnt = nullptr;
+        S *lv = nullptr, *uv = nullptr;
+        int32_t tot[2] = {0, 0};
+        if (hipMalloc(&lrp, (n + 1) * 4) != hipSuccess || hipMalloc(&urp, (n + 1) * 4) != hipSuccess ||
+            hipMalloc(&lcnt, (n + 1) * 4) != hipSuccess || hipMalloc(&ucnt, (n + 1) * 4) != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "solve_shifted: L / U split");
+        if (rc == EIGSOL_OK) {
+            hipLaunchKernelGGL(dev::gm_split_count_kernel, dim3((n + 256) / 256), dim3(256), 0, st, k_rp, k_dpos, n,
+                               lcnt, ucnt);
+            if (tri_exclusive_scan(st, lcnt, lrp, n) != hipSuccess || tri_exclusive_scan(st, ucnt, urp, n) != hipSuccess)
+                rc = fail(EIGSOL_E_HIP, "solve_shifted: L / U split scan");
         }
-        rc = shift_factor_tri(ctx, dtype, n, lrp, lci, lv.data(), false, &g->L);
-        if (rc == EIGSOL_OK) rc = shift_factor_tri(ctx, dtype, n, urp, uci, uv.data(), true, &g->U);
+        if (rc == EIGSOL_OK) {
+            hipMemcpyAsync(&tot[0], lrp + n, 4, hipMemcpyDeviceToHost, st);
+            hipMemcpyAsync(&tot[1], urp + n, 4, hipMemcpyDeviceToHost, st);
+            if (hipStreamSynchronize(st) != hipSuccess || hipMalloc(&lci, std::max(1, tot[0]) * 4) != hipSuccess ||
+                hipMalloc(&lv, std::max(1, tot[0]) * sizeof(S)) != hipSuccess ||
+                hipMalloc(&uci, std::max(1, tot[1]) * 4) != hipSuccess ||
+                hipMalloc(&uv, std::max(1, tot[1]) * sizeof(S)) != hipSuccess)
+                rc = fail(EIGSOL_E_HIP, "solve_shifted: L / U split buffers");
+        }
+        if (rc == EIGSOL_OK)
+            hipLaunchKernelGGL((dev::gm_split_fill_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, k_rp, k_ci, k_v,
+                               k_dpos, n, lrp, urp, lci, lv, uci, uv);
+        free_k();
+        lap("split L / U");
+        if (rc == EIGSOL_OK) rc = shift_factor_tri_dev(ctx, dtype, n, lrp, lci, lv, tot[0], false, &g->L);
+        lap("triangular layout L");
+        if (rc == EIGSOL_OK) rc = shift_factor_tri_dev(ctx, dtype, n, urp, uci, uv, tot[1], true, &g->U);
+        lap("triangular layout U");
+        hipStreamSynchronize(st);
+        for (void* p : {(void*)lrp, (void*)urp, (void*)lci, (void*)uci, (void*)lv, (void*)uv, (void*)lcnt, (void*)ucnt})
+            if (p) hipFree(p);
     }
+    free_k();
     const size_t sb = sizeof(S);
     g->G = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 2047) / 2048));
     if (rc == EIGSOL_OK &&

@@ -823,16 +823,21 @@ int host_threads() {
 
 // pattern of M + M^T without the diagonal, each list sorted and unique: M's rows merged with the
 // rows of its transpose (a counting-sort transpose keeps them sorted)
-void sym_graph(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, SymGraph& g) {
+bool sym_graph(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, SymGraph& g,
+               const std::atomic<bool>* stop = nullptr) {
     const int nth = host_threads();
+    auto stopped = [&]() { return stop && stop->load(std::memory_order_relaxed); };
     std::vector<int64_t> tp(n + 1, 0);
     for (int64_t e = 0; e < (int64_t)rp[n]; ++e) ++tp[ci[e] + 1];
     for (int64_t i = 0; i < n; ++i) tp[i + 1] += tp[i];
+    if (stopped()) return false;
     std::vector<int32_t> tc(rp[n]);
     {
         std::vector<int64_t> fill(tp.begin(), tp.end() - 1);
-        for (int64_t i = 0; i < n; ++i)
+        for (int64_t i = 0; i < n; ++i) {
+            if ((i & 65535) == 0 && stopped()) return false;
             for (int32_t e = rp[i]; e < rp[i + 1]; ++e) tc[fill[ci[e]]++] = (int32_t)i;
+        }
     }
     // merge row i of M and of M^T (both ascending), without i and repeats; count, then fill
     auto merge = [&](int64_t i, int32_t* out) -> int64_t {
@@ -851,13 +856,22 @@ void sym_graph(int64_t n, const std::vector<int32_t>& rp, const std::vector<int3
     };
     g.ptr.assign(n + 1, 0);
     par_for(n, nth, [&](int64_t b, int64_t e) {
-        for (int64_t i = b; i < e; ++i) g.ptr[i + 1] = merge(i, nullptr);
+        for (int64_t i = b; i < e; ++i) {
+            if ((i & 65535) == 0 && stopped()) return;
+            g.ptr[i + 1] = merge(i, nullptr);
+        }
     });
+    if (stopped()) return false;
     for (int64_t i = 0; i < n; ++i) g.ptr[i + 1] += g.ptr[i];
+    if (stopped()) return false;
     g.adj.resize(g.ptr[n]);
     par_for(n, nth, [&](int64_t b, int64_t e) {
-        for (int64_t i = b; i < e; ++i) merge(i, g.adj.data() + g.ptr[i]);
+        for (int64_t i = b; i < e; ++i) {
+            if ((i & 65535) == 0 && stopped()) return;
+            merge(i, g.adj.data() + g.ptr[i]);
+        }
     });
+    return !stopped();
 }
 
 struct NdNode {
@@ -1116,9 +1130,10 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
     // passes of the dissection then walk memory locally whatever the caller's numbering)
     SymGraph g;
     std::vector<int32_t> ord(n);   // label -> caller's index
+    auto stopped = [&]() { return stop && stop->load(std::memory_order_relaxed); };
     {
         SymGraph g0;
-        sym_graph(n, rp, ci, g0);
+        if (!sym_graph(n, rp, ci, g0, stop)) return false;
         std::vector<char> done(n, 0);
         int64_t head = 0, tail = 0;
         for (int64_t s0 = 0; s0 < n; ++s0) {
@@ -1126,11 +1141,13 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
             done[s0] = 1;
             ord[tail++] = (int32_t)s0;
             while (head < tail) {
+                if ((head & 65535) == 0 && stopped()) return false;
                 const int32_t v = ord[head++];
                 for (int64_t e = g0.ptr[v]; e < g0.ptr[v + 1]; ++e)
                     if (!done[g0.adj[e]]) { done[g0.adj[e]] = 1; ord[tail++] = g0.adj[e]; }
             }
         }
+        if (stopped()) return false;
         std::vector<int32_t> lab(n);
         for (int64_t k = 0; k < n; ++k) lab[ord[k]] = (int32_t)k;
         g.ptr.assign(n + 1, 0);

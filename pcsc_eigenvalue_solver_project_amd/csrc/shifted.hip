@@ -2801,10 +2801,82 @@ static int factor_tri_device(eigsol_csr* A, double sre, double sim, ShiftFactor*
 // triangular factor from host CSR arrays (the ILU(0) factors of the GMRES path, gmres.hip)
 int shift_factor_tri(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<int32_t>& rp, std::vector<int32_t>& ci,
                      const void* vals, bool up, ShiftFactor** out) {
+    // the GMRES path's L / U (host arrays): uploaded once and analysed and laid out on the device
+    // like a triangular A (round 5: the 1M general-sparse factor's two host layouts took ~0.8 s);
+    // EIGSOL_TRSV_HOST=1 or a declined device analysis keeps the host build (the same bytes)
     auto run = [&](auto tag) {
         using S = decltype(tag);
+        const char* host_env = std::getenv("EIGSOL_TRSV_HOST");
+        if (n > 0 && !(host_env && std::atoi(host_env))) {
+            // a bare device CSR (row pointers, columns, values): all the device analysis reads
+            eigsol_csr A;
+            A.ctx = ctx;
+            A.dtype = dtype;
+            A.nrows = A.ncols = n;
+            A.nnz = rp[n];
+            hipStream_t st = ctx->stream;
+            int rc = EIGSOL_OK;
+            if (hipMalloc(&A.rowptr, (n + 1) * 4) != hipSuccess || hipMalloc(&A.col, std::max<int64_t>(1, A.nnz) * 4) != hipSuccess ||
+                hipMalloc(&A.val, std::max<int64_t>(1, A.nnz) * sizeof(S)) != hipSuccess)
+                rc = fail(EIGSOL_E_HIP, "solve_shifted: triangular factor upload");
+            if (rc == EIGSOL_OK) {
+                hipMemcpyAsync(A.rowptr, rp.data(), (n + 1) * 4, hipMemcpyHostToDevice, st);
+                hipMemcpyAsync(A.col, ci.data(), A.nnz * 4, hipMemcpyHostToDevice, st);
+                hipMemcpyAsync(A.val, vals, A.nnz * sizeof(S), hipMemcpyHostToDevice, st);
+            }
+            bool declined = false;
+            if (rc == EIGSOL_OK) rc = factor_tri_device<S>(&A, 0.0, 0.0, out, declined);
+            hipStreamSynchronize(st);
+            for (void* p : {(void*)A.rowptr, (void*)A.col, A.val})
+                if (p) hipFree(p);
+            A.rowptr = nullptr;
+            A.col = nullptr;
+            A.val = nullptr;
+            if (!declined || rc != EIGSOL_OK) return rc;
+        }
         std::vector<S> v(static_cast<const S*>(vals), static_cast<const S*>(vals) + rp[n]);
         return factor_tri_host<S>(ctx, dtype, n, rp, ci, v, up, 0.0, 0.0, out);
+    };
+    switch (dtype) {
+        case EIGSOL_C128: return run(cplx{});
+        case EIGSOL_F32: return run(0.0f);
+        case EIGSOL_C64: return run(cplxf{});
+        default: return run(0.0);
+    }
+}
+
+// A triangular factor given as device CSR arrays (the GMRES path's L / U, split on the device):
+// analysed and laid out on the device; a declined analysis or EIGSOL_TRSV_HOST=1 takes the host
+// build on a downloaded copy (the same bytes).  The arrays stay the caller's.
+int shift_factor_tri_dev(eigsol_ctx* ctx, int dtype, int64_t n, int32_t* rp, int32_t* ci, void* vals, int64_t nnz,
+                         bool up, ShiftFactor** out) {
+    auto run = [&](auto tag) -> int {
+        using S = decltype(tag);
+        hipStream_t st = ctx->stream;
+        const char* host_env = std::getenv("EIGSOL_TRSV_HOST");
+        if (n > 0 && !(host_env && std::atoi(host_env))) {
+            eigsol_csr A;
+            A.ctx = ctx;
+            A.dtype = dtype;
+            A.nrows = A.ncols = n;
+            A.nnz = nnz;
+            A.rowptr = rp;
+            A.col = ci;
+            A.val = vals;
+            bool declined = false;
+            const int rc = factor_tri_device<S>(&A, 0.0, 0.0, out, declined);
+            A.rowptr = nullptr;
+            A.col = nullptr;
+            A.val = nullptr;
+            if (!declined || rc != EIGSOL_OK) return rc;
+        }
+        std::vector<int32_t> hrp(n + 1), hci(nnz);
+        std::vector<S> hv(nnz);
+        EIGSOL_HIP(hipMemcpyAsync(hrp.data(), rp, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipMemcpyAsync(hci.data(), ci, nnz * 4, hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipMemcpyAsync(hv.data(), vals, nnz * sizeof(S), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        return factor_tri_host<S>(ctx, dtype, n, hrp, hci, hv, up, 0.0, 0.0, out);
     };
     switch (dtype) {
         case EIGSOL_C128: return run(cplx{});
