@@ -74,6 +74,14 @@ __device__ __forceinline__ double mf_rl(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 __device__ __forceinline__ cplx mf_rl(cplx v, int src) { return cplx{mf_rl(v.re, src), mf_rl(v.im, src)}; }
+// write-through stores / agent-scope loads of values handed between workgroups of one launch
+__device__ __forceinline__ void mf_st(double* p, double v) { st_agent(p, v); }
+__device__ __forceinline__ void mf_st(cplx* p, cplx v) {
+    st_agent(&p->re, v.re);
+    st_agent(&p->im, v.im);
+}
+__device__ __forceinline__ double mf_ld(const double* p) { return ld_agent(p); }
+__device__ __forceinline__ cplx mf_ld(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
 
 // M's entries into their fronts: F[dst[e]] = v[e] (every destination distinct)
 template <class S>
@@ -469,6 +477,188 @@ __global__ __launch_bounds__(256) void mf_bwd_wave_kernel(const MfFront* fr, con
     if (lane < ns) x[f.c0 + lane] = v;
 }
 
+// ---- the lower heights in one launch each way (dataflow, opt-in EIGSOL_MF_FLOW=1): one workgroup
+// per front in height order (forward ascending, backward descending), waiting for the fronts it
+// reads - the children's contributions (forward) or the parent's solution (backward) - through
+// per-front epoch flags; a front only waits for fronts of lower workgroup index (in-order
+// dispatch), values are handed over write-through and loaded at agent scope.  Same arithmetic, in
+// the same order, as mf_fwd_kernel / mf_bwd_kernel.  Measured and rejected as the default: 2.01 ->
+// 4.5 ms per 1M iteration (waiting workgroups hold the CU slots the producers need, and the
+// acquire polls invalidate L2).  A ticket-ordered persistent variant hung in a way that device
+// printf made disappear; not kept.
+__device__ __forceinline__ void mf_wait_flag(const int32_t* f, int32_t epoch, int32_t* err, int who = -1) {
+    (void)who;
+    int spins = 0;
+    while (__hip_atomic_load(const_cast<int32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 22)) {
+            atomicOr(err, 2);
+            break;
+        }
+    }
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void mf_fwd_flow_kernel(const MfFront* fr, const int32_t* order, int32_t cnt,
+                                                          int32_t* done, int32_t epoch, const int32_t* chl,
+                                                          const S* F, const int32_t* cmap, const int32_t* pinv, S* w,
+                                                          S* u, int32_t* err) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    {
+        const int32_t t = (int32_t)blockIdx.x;
+        if (t >= cnt) return;
+        const int32_t sidx_f = order[t];
+        const MfFront f = fr[sidx_f];
+        const int d = f.d, ns = f.ns, ms = f.ms;
+        S* r = reinterpret_cast<S*>(lds_raw);
+        S* y = r + ns;
+        S* acc = y + ns;
+        for (int k = f.ch0 + tid; k < f.ch1; k += 256) mf_wait_flag(done + chl[k], epoch, err, sidx_f);
+        for (int q = tid; q < ns; q += 256) r[q] = w[f.c0 + q];
+        for (int q = tid; q < ms; q += 256) acc[q] = s_zero<S>();
+        __syncthreads();
+        for (int k = f.ch0; k < f.ch1; ++k) {
+            const MfFront c = fr[chl[k]];
+            const int32_t* map = cmap + c.sof;
+            const S* uc = u + c.uoff;
+            for (int q = tid; q < c.ms; q += 256) {
+                const int pos = map[q];
+                const S v = mf_ld(uc + q);
+                if (pos < ns) r[pos] = sub(r[pos], v);
+                else acc[pos - ns] = add(acc[pos - ns], v);
+            }
+            __syncthreads();
+        }
+        for (int q = tid; q < ns; q += 256) y[q] = r[pinv[f.c0 + q]];
+        __syncthreads();
+        const S* A = F + f.off;
+        for (int jb = 0; jb < ns; jb += 64) {
+            const int bw = min(64, ns - jb);
+            if (wv == 0) {
+                S v = lane < bw ? y[jb + lane] : s_zero<S>();
+                const int row = jb + min(lane, bw - 1);
+                for (int j0 = 0; j0 < bw; j0 += 16) {
+                    S lv[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) lv[q] = A[row + (int64_t)(jb + min(j0 + q, bw - 1)) * d];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int j = j0 + q;
+                        if (j < bw) {
+                            const S yj = mf_rl(v, j);
+                            if (lane > j) v = sub(v, mul(lv[q], yj));
+                        }
+                    }
+                }
+                if (lane < bw) y[jb + lane] = v;
+            }
+            __syncthreads();
+            for (int i = jb + bw + tid; i < d; i += 256) {
+                S sacc = s_zero<S>();
+                const S* Ai = A + i + (int64_t)jb * d;
+                for (int j0 = 0; j0 < bw; j0 += 16) {
+                    S lv[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) lv[q] = Ai[(int64_t)min(j0 + q, bw - 1) * d];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q)
+                        if (j0 + q < bw) sacc = add(sacc, mul(lv[q], y[jb + j0 + q]));
+                }
+                if (i < ns) y[i] = sub(y[i], sacc);
+                else acc[i - ns] = add(acc[i - ns], sacc);
+            }
+            __syncthreads();
+        }
+        for (int q = tid; q < ns; q += 256) w[f.c0 + q] = y[q];
+        for (int q = tid; q < ms; q += 256) mf_st(u + f.uoff + q, acc[q]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // release: writes the XCD's L2 back, so pollers on other XCDs see the flag and the values
+        // (a relaxed agent-scope store was measured never to reach them)
+        if (tid == 0) __hip_atomic_store(done + sidx_f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void mf_bwd_flow_kernel(const MfFront* fr, const int32_t* order, int32_t cnt,
+                                                          int32_t* done, int32_t epoch, int32_t hflow,
+                                                          const int32_t* height, const S* F, const int32_t* sidx,
+                                                          const S* w, S* x, int32_t* err) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    {
+        const int32_t t = (int32_t)blockIdx.x;
+        if (t >= cnt) return;
+        const int32_t sf = order[t];
+        const MfFront f = fr[sf];
+        const int d = f.d, ns = f.ns, ms = f.ms;
+        S* tv_ = reinterpret_cast<S*>(lds_raw);
+        S* xs = tv_ + ns;
+        if (tid == 0 && f.parent >= 0 && height[f.parent] < hflow) mf_wait_flag(done + f.parent, epoch, err, sf);
+        __syncthreads();
+        for (int q = tid; q < ms; q += 256) xs[q] = mf_ld(x + sidx[f.sof + q]);
+        __syncthreads();
+        const S* A = F + f.off;
+        for (int k = tid; k < ns; k += 256) {
+            S sacc = s_zero<S>();
+            const S* Ak = A + k + (int64_t)ns * d;
+            int q0 = 0;
+            for (; q0 + 8 <= ms; q0 += 8) {
+                S uv[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) uv[e] = Ak[(int64_t)(q0 + e) * d];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sacc = add(sacc, mul(uv[e], xs[q0 + e]));
+            }
+            for (; q0 < ms; ++q0) sacc = add(sacc, mul(Ak[(int64_t)q0 * d], xs[q0]));
+            tv_[k] = sub(w[f.c0 + k], sacc);
+        }
+        __syncthreads();
+        for (int jb = ((ns - 1) / 64) * 64; jb >= 0; jb -= 64) {
+            const int bw = min(64, ns - jb);
+            if (wv == 0) {
+                S v = lane < bw ? tv_[jb + lane] : s_zero<S>();
+                const int row = jb + min(lane, bw - 1);
+                for (int j1 = bw; j1 > 0; j1 -= 16) {
+                    S uv[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) uv[e] = A[row + (int64_t)(jb + max(j1 - 1 - e, 0)) * d];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        const int j = j1 - 1 - e;
+                        if (j >= 0) {
+                            if (lane == j) v = sdiv(v, uv[e]);
+                            const S xj = mf_rl(v, j);
+                            if (lane < j) v = sub(v, mul(uv[e], xj));
+                        }
+                    }
+                }
+                if (lane < bw) tv_[jb + lane] = v;
+            }
+            __syncthreads();
+            for (int i = tid; i < jb; i += 256) {
+                S sacc = s_zero<S>();
+                const S* Ai = A + i + (int64_t)jb * d;
+                for (int j0 = 0; j0 < bw; j0 += 16) {
+                    S uv[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) uv[e] = Ai[(int64_t)min(j0 + e, bw - 1) * d];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        if (j0 + e < bw) sacc = add(sacc, mul(uv[e], tv_[jb + j0 + e]));
+                }
+                tv_[i] = sub(tv_[i], sacc);
+            }
+            __syncthreads();
+        }
+        for (int k = tid; k < ns; k += 256) mf_st(x + f.c0 + k, tv_[k]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(done + sf, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ---- large fronts: one workgroup per 64-row block, sync-free (the dense path's blocked TRSV,
 // shifted.hip dense_trsv_kernel, on a front).  Pivot block k of a front publishes its solved 64
 // values with write-through stores and raises flag[flag0 + k] to the solve's epoch; a row block
@@ -490,13 +680,6 @@ __device__ __forceinline__ void mf_wait(const int32_t* f, int32_t epoch, int32_t
         if (++spins > (1 << 24)) { atomicOr(err, 1); break; }
     }
 }
-__device__ __forceinline__ void mf_st(double* p, double v) { st_agent(p, v); }
-__device__ __forceinline__ void mf_st(cplx* p, cplx v) {
-    st_agent(&p->re, v.re);
-    st_agent(&p->im, v.im);
-}
-__device__ __forceinline__ double mf_ld(const double* p) { return ld_agent(p); }
-__device__ __forceinline__ cplx mf_ld(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
 
 // z (d entries per large front) = the permuted pivot right-hand side, then the children's
 // contributions to the struct rows; one workgroup per front.  LDS: r (ns)
@@ -649,10 +832,7 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
     const S y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
     if (lane < rn) mf_st(w + f.c0 + r0 + lane, y);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        if (bo & 4) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // backward, large fronts: tab = (front, pivot block) pairs, blocks descending within a front:
@@ -727,10 +907,7 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
     const S xv = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
     if (lane < rn) mf_st(x + f.c0 + r0 + lane, xv);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        if (bo & 4) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace dev
@@ -766,7 +943,14 @@ struct MfFactor {
     void* z = nullptr;                // large fronts' assembled right-hand sides
     void* tinv = nullptr;             // inverted diagonal blocks of the large fronts (8192 scalars each)
     int32_t epoch = 0;
-    int backoff = 2;                  // EIGSOL_MF_BACKOFF: 1 growing sleeps, 2 relaxed polls, 4 relaxed flag stores
+    int32_t hflow = 0;
+    int32_t* flow_f = nullptr;
+    int32_t* flow_b = nullptr;
+    int32_t* fheight = nullptr;
+    int32_t* done = nullptr;
+    int32_t nflow = 0, lds_flow_f = 0, lds_flow_b = 0;
+    int flow_mode = 3;                // bit 0 forward, bit 1 backward (EIGSOL_MF_FLOW_MODE, debugging)
+    int backoff = 2;                  // EIGSOL_MF_BACKOFF: 1 growing sleeps, 2 relaxed polls (flag stores: release)
     std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt;
     std::vector<int32_t> lds_asm;
     MfStats st;
@@ -778,7 +962,8 @@ void mf_free(MfFactor* f) {
     hipStreamSynchronize(f->ctx->stream);
     for (void* p : {(void*)f->fronts, (void*)f->chl, (void*)f->sidx, (void*)f->cmap, (void*)f->perm, (void*)f->pinv,
                     (void*)f->lists, f->F, f->u, f->w, f->x, (void*)f->slists, (void*)f->tabf, (void*)f->tabb,
-                    (void*)f->flags, (void*)f->err, f->z, f->tinv})
+                    (void*)f->flags, (void*)f->err, f->z, f->tinv, (void*)f->flow_f, (void*)f->flow_b,
+                    (void*)f->fheight, (void*)f->done})
         if (p) hipFree(p);
     ctx_release(f->ctx);
     delete f;
@@ -1346,6 +1531,9 @@ struct MfHost {
     std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt;
     int32_t nflag = 0;
     int64_t zsz = 0;
+    int32_t hflow = 0;                     // heights below it: the dataflow launches (0: off)
+    std::vector<int32_t> flow_f, flow_b;   // their fronts, ascending / descending height
+    int32_t lds_flow_f = 0, lds_flow_b = 0;
     MfStats stt;
 };
 
@@ -1499,6 +1687,26 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
         fcnt[h] = (int64_t)tabf.size() / 2 - foff[h];
         bcnt[h] = (int64_t)tabb.size() / 2 - boff[h];
     }
+    // dataflow launches for the heights below the first one with a large front (EIGSOL_MF_FLOW=0: off)
+    {
+        bool flow = false;
+        if (const char* e = std::getenv("EIGSOL_MF_FLOW")) flow = std::atoi(e) != 0;
+        int32_t hf = H + 1;
+        for (int32_t h = 0; h <= H; ++h)
+            if (nbig[h]) { hf = h; break; }
+        X.hflow = flow ? hf : 0;
+        X.flow_f.clear();
+        X.flow_b.clear();
+        for (int32_t h = 0; h < X.hflow; ++h)
+            for (int64_t t = hstart[h]; t < hstart[h + 1]; ++t) {
+                const dev::MfFront& q = fr[lists[t]];
+                X.flow_f.push_back(lists[t]);
+                X.lds_flow_f = std::max<int32_t>(X.lds_flow_f, (int32_t)((2 * q.ns + q.ms) * sb));
+                X.lds_flow_b = std::max<int32_t>(X.lds_flow_b, (int32_t)((q.ns + q.ms) * sb));
+            }
+        for (int32_t h = X.hflow - 1; h >= 0; --h)
+            for (int64_t t = hstart[h]; t < hstart[h + 1]; ++t) X.flow_b.push_back(lists[t]);
+    }
     stt.order_seconds = std::chrono::duration<double>(clk::now() - t0).count();
     if (std::getenv("EIGSOL_MF_DEBUG"))
         std::fprintf(stderr, "[mf] plan + maps + tables %.3f s; fronts %lld, heights %d, factor entries %.3g, flops %.3g\n",
@@ -1585,6 +1793,15 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     dm((void**)&f->err, 4);
     dm(&f->z, (size_t)zsz * sb);
     dm(&f->tinv, (size_t)nflag * 8192 * sb);
+    f->hflow = X.hflow;
+    f->nflow = (int32_t)X.flow_f.size();
+    f->lds_flow_f = X.lds_flow_f;
+    f->lds_flow_b = X.lds_flow_b;
+    if (const char* e = std::getenv("EIGSOL_MF_FLOW_MODE")) f->flow_mode = std::atoi(e) & 3;
+    dm((void**)&f->flow_f, X.flow_f.size() * 4);
+    dm((void**)&f->flow_b, X.flow_b.size() * 4);
+    dm((void**)&f->fheight, nt * 4);
+    dm((void**)&f->done, nt * 4);
     dm(&f->F, (size_t)fe * sb);
     dm(&f->u, (size_t)uo * sb);
     dm(&f->w, n * sb);
@@ -1611,6 +1828,10 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         up(f->tabf, tabf.data(), tabf.size() * 4);
         up(f->tabb, tabb.data(), tabb.size() * 4);
         hipMemsetAsync(f->flags, 0, std::max<size_t>((size_t)nflag * 4, 4), st);
+        up(f->flow_f, X.flow_f.data(), X.flow_f.size() * 4);
+        up(f->flow_b, X.flow_b.data(), X.flow_b.size() * 4);
+        up(f->fheight, P.height.data(), nt * 4);
+        hipMemsetAsync(f->done, 0, nt * 4, st);
         hipMemsetAsync(f->err, 0, 4, st);
         up(d_tab, tab.data(), tab.size() * 4);
         up(d_dst, dst.data(), nnz * 8);
@@ -1662,11 +1883,16 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         for (int32_t b : f->lds_fwd) mx = std::max(mx, b);
         for (int32_t b : f->lds_bwd) mx = std::max(mx, b);
         for (int32_t b : f->lds_asm) mx = std::max(mx, b);
+        mx = std::max(mx, std::max(f->lds_flow_f, f->lds_flow_b));
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_big_asm_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_flow_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_flow_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal solve LDS");
     }
@@ -1693,7 +1919,13 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     S* u = static_cast<S*>(f->u);
     S* z = static_cast<S*>(f->z);
     const int32_t ef = ++f->epoch, eb = ++f->epoch;   // flag words: forward, then backward values
-    for (int32_t h = 0; h <= H; ++h) {
+    const int flow_grid = (int)std::max<int64_t>(1, f->nflow);   // one workgroup per front, in order
+    const bool ff = f->nflow && (f->flow_mode & 1), fb = f->nflow && (f->flow_mode & 2);
+    if (ff) {
+        hipLaunchKernelGGL((dev::mf_fwd_flow_kernel<S>), dim3(flow_grid), dim3(256), f->lds_flow_f, st, f->fronts,
+                           f->flow_f, f->nflow, f->done, ef, f->chl, F, f->cmap, f->pinv, w, u, f->err);
+    }
+    for (int32_t h = ff ? f->hflow : 0; h <= H; ++h) {
         const int32_t* L = f->slists + f->sstart[h];
         const int64_t nw = f->nwave[h];
         if (nw)
@@ -1710,7 +1942,7 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
                                f->backoff);
         }
     }
-    for (int32_t h = H; h >= 0; --h) {
+    for (int32_t h = H; h >= (fb ? f->hflow : 0); --h) {
         const int32_t* L = f->slists + f->sstart[h];
         if (f->nbig[h])
             hipLaunchKernelGGL((dev::mf_big_bwd_kernel<S>), dim3(f->bcnt[h]), dim3(256), 0, st, f->fronts,
@@ -1724,8 +1956,18 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
             hipLaunchKernelGGL((dev::mf_bwd_wave_kernel<S>), dim3((nw + 3) / 4), dim3(256), 0, st, f->fronts, L,
                                (int32_t)nw, F, f->sidx, w, x);
     }
+    if (fb)
+        hipLaunchKernelGGL((dev::mf_bwd_flow_kernel<S>), dim3(flow_grid), dim3(256), f->lds_flow_b, st, f->fronts,
+                           f->flow_b, f->nflow, f->done, eb, f->hflow, f->fheight, F, f->sidx, (const S*)w, x, f->err);
     hipLaunchKernelGGL((dev::mf_scatter_out_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, x, out, n);
     EIGSOL_HIP(hipGetLastError());
+    static const bool dbg = std::getenv("EIGSOL_MF_DEBUG") != nullptr;
+    if (dbg) {
+        int32_t e = 0;
+        EIGSOL_HIP(hipMemcpyAsync(&e, f->err, 4, hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+        std::fprintf(stderr, "[mf] solve epoch %d err %d nflow %d hflow %d\n", f->epoch, e, f->nflow, f->hflow);
+    }
     return EIGSOL_OK;
 }
 
