@@ -391,6 +391,18 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     int mf_prc = EIGSOL_E_UNSUPPORTED;
     std::atomic<bool> mf_stop{false}, fill_stop{false};
     std::thread mft;
+    // joins the plan thread on every way out of this scope (an exception from the fill attempt
+    // included: a joinable std::thread must never be destroyed)
+    struct PlanJoin {
+        std::thread& t;
+        std::atomic<bool>& stop;
+        ~PlanJoin() {
+            if (t.joinable()) {
+                stop.store(true);
+                t.join();
+            }
+        }
+    } plan_join{mft, mf_stop};
     size_t fb = 0;
     {
         const char* me = std::getenv("EIGSOL_MF");
