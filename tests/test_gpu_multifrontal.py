@@ -93,7 +93,10 @@ def test_multifrontal_solve_residual_and_determinism(ctx, nx):
     n = nx * nx
     A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
     M = sp.csr_matrix((v, ci, rp), shape=(n, n))
-    for sigma in (4.0 + 0.5j, 0.5 - 0.25j, 7.9 + 0.0j):
+    # 7.9 lies next to an eigenvalue at nx = 141 (||y|| ~ 1e8); at nx = 300 every shift near the
+    # spectrum's edge is singular to working precision (SuperLU: ||y|| ~ 1e18, relative residual ~ 5),
+    # which only the densified-LU fallback would attempt - so the larger grid keeps interior shifts
+    for sigma in (4.0 + 0.5j, 0.5 - 0.25j) + ((7.9 + 0.0j,) if nx == 141 else ()):
         assert _variant(A, sigma) == 19
         b = S.start_vector(n, np.complex128, seed=11)
         y = E.solve_shifted(A, sigma, b)
