@@ -221,11 +221,9 @@ __global__ __launch_bounds__(256) void mf_scatter_out_kernel(const int32_t* perm
 
 // forward: fronts list[0 .. gridDim.x) of one height.  LDS: r (ns), y (ns), acc (ms).
 template <class S>
-__global__ __launch_bounds__(256) void mf_fwd_kernel(const MfFront* fr, const int32_t* list, const int32_t* chl,
-                                                     const S* F, const int32_t* cmap, const int32_t* pinv, S* w,
-                                                     S* u) {
-    extern __shared__ __align__(16) unsigned char lds_raw[];
-    const MfFront f = fr[list[blockIdx.x]];
+__device__ __forceinline__ void mf_fwd_front(const MfFront f, unsigned char* lds_raw, const MfFront* fr,
+                                             const int32_t* chl, const S* F, const int32_t* cmap, const int32_t* pinv,
+                                             S* w, S* u) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int d = f.d, ns = f.ns, ms = f.ms;
     S* r = reinterpret_cast<S*>(lds_raw);
@@ -290,12 +288,33 @@ __global__ __launch_bounds__(256) void mf_fwd_kernel(const MfFront* fr, const in
     for (int t = tid; t < ms; t += 256) u[f.uoff + t] = acc[t];
 }
 
+template <class S>
+__global__ __launch_bounds__(256) void mf_fwd_kernel(const MfFront* fr, const int32_t* list, const int32_t* chl,
+                                                     const S* F, const int32_t* cmap, const int32_t* pinv, S* w,
+                                                     S* u) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    mf_fwd_front<S>(fr[list[blockIdx.x]], lds_raw, fr, chl, F, cmap, pinv, w, u);
+}
+
+// a whole small subtree per workgroup: its fronts are the postorder range [lo, hi], children
+// before parents, so the forward pass walks it upward without any other workgroup (the children's
+// contributions were written by this workgroup, visible after its barrier)
+template <class S>
+__global__ __launch_bounds__(256) void mf_fwd_sub_kernel(const MfFront* fr, const int32_t* ranges, const int32_t* chl,
+                                                         const S* F, const int32_t* cmap, const int32_t* pinv, S* w,
+                                                         S* u) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const int32_t lo = ranges[2 * blockIdx.x], hi = ranges[2 * blockIdx.x + 1];
+    for (int32_t s = lo; s <= hi; ++s) {
+        mf_fwd_front<S>(fr[s], lds_raw, fr, chl, F, cmap, pinv, w, u);
+        __syncthreads();
+    }
+}
+
 // backward: fronts list[0 .. gridDim.x) of one height (their ancestors solved).  LDS: t (ns), xs (ms).
 template <class S>
-__global__ __launch_bounds__(256) void mf_bwd_kernel(const MfFront* fr, const int32_t* list, const S* F,
-                                                     const int32_t* sidx, const S* w, S* x) {
-    extern __shared__ __align__(16) unsigned char lds_raw[];
-    const MfFront f = fr[list[blockIdx.x]];
+__device__ __forceinline__ void mf_bwd_front(const MfFront f, unsigned char* lds_raw, const S* F,
+                                             const int32_t* sidx, const S* w, S* x) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int d = f.d, ns = f.ns, ms = f.ms;
     S* t = reinterpret_cast<S*>(lds_raw);
@@ -356,6 +375,26 @@ __global__ __launch_bounds__(256) void mf_bwd_kernel(const MfFront* fr, const in
         __syncthreads();
     }
     for (int k = tid; k < ns; k += 256) x[f.c0 + k] = t[k];
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void mf_bwd_kernel(const MfFront* fr, const int32_t* list, const S* F,
+                                                     const int32_t* sidx, const S* w, S* x) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    mf_bwd_front<S>(fr[list[blockIdx.x]], lds_raw, F, sidx, w, x);
+}
+
+// the backward pass over a small subtree: parents before children (the subtree root's ancestors
+// were solved by earlier launches)
+template <class S>
+__global__ __launch_bounds__(256) void mf_bwd_sub_kernel(const MfFront* fr, const int32_t* ranges, const S* F,
+                                                         const int32_t* sidx, const S* w, S* x) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const int32_t lo = ranges[2 * blockIdx.x], hi = ranges[2 * blockIdx.x + 1];
+    for (int32_t s = hi; s >= lo; --s) {
+        mf_bwd_front<S>(fr[s], lds_raw, F, sidx, w, x);
+        __syncthreads();
+    }
 }
 
 // ---- small fronts (ns <= 64 pivots, ms <= 192 struct rows): one wave per front, four fronts per
@@ -949,7 +988,9 @@ struct MfFactor {
     int32_t* fheight = nullptr;
     int32_t* done = nullptr;
     int32_t nflow = 0, lds_flow_f = 0, lds_flow_b = 0;
-    int flow_mode = 3;                // bit 0 forward, bit 1 backward (EIGSOL_MF_FLOW_MODE, debugging)
+    int flow_mode = 3;
+    int32_t* sub_ranges = nullptr;
+    int32_t nsub = 0, lds_sub_f = 0, lds_sub_b = 0;                // bit 0 forward, bit 1 backward (EIGSOL_MF_FLOW_MODE, debugging)
     int backoff = 2;                  // EIGSOL_MF_BACKOFF: 1 growing sleeps, 2 relaxed polls (flag stores: release)
     std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt;
     std::vector<int32_t> lds_asm;
@@ -963,7 +1004,7 @@ void mf_free(MfFactor* f) {
     for (void* p : {(void*)f->fronts, (void*)f->chl, (void*)f->sidx, (void*)f->cmap, (void*)f->perm, (void*)f->pinv,
                     (void*)f->lists, f->F, f->u, f->w, f->x, (void*)f->slists, (void*)f->tabf, (void*)f->tabb,
                     (void*)f->flags, (void*)f->err, f->z, f->tinv, (void*)f->flow_f, (void*)f->flow_b,
-                    (void*)f->fheight, (void*)f->done})
+                    (void*)f->fheight, (void*)f->done, (void*)f->sub_ranges})
         if (p) hipFree(p);
     ctx_release(f->ctx);
     delete f;
@@ -1534,6 +1575,8 @@ struct MfHost {
     int32_t hflow = 0;                     // heights below it: the dataflow launches (0: off)
     std::vector<int32_t> flow_f, flow_b;   // their fronts, ascending / descending height
     int32_t lds_flow_f = 0, lds_flow_b = 0;
+    std::vector<int32_t> sub_ranges;       // small subtrees solved by one workgroup each: (lo, hi) fronts
+    int32_t lds_sub_f = 0, lds_sub_b = 0;
     MfStats stt;
 };
 
@@ -1588,14 +1631,18 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
         const int64_t k = std::lower_bound(b, b + fr[s].ms, j) - b;
         return (k < fr[s].ms && b[k] == j) ? fr[s].ns + k : -1;
     };
-    for (int64_t r = 0; r < n; ++r)
-        for (int32_t e = rp[r]; e < rp[r + 1]; ++e) {
-            const int32_t i = P.iperm[r], j = P.iperm[ci[e]];
-            const int32_t s = P.snode[std::min(i, j)];
-            const int64_t pi = pos_in(s, i), pj = pos_in(s, j);
-            if (pi < 0 || pj < 0) return EIGSOL_E_UNSUPPORTED;   // not in the front: an inconsistent plan
-            dst[e] = fr[s].off + pi + pj * (int64_t)fr[s].d;
-        }
+    std::atomic<bool> bad{false};
+    par_for(n, host_threads(), [&](int64_t rb, int64_t re) {
+        for (int64_t r = rb; r < re; ++r)
+            for (int32_t e = rp[r]; e < rp[r + 1]; ++e) {
+                const int32_t i = P.iperm[r], j = P.iperm[ci[e]];
+                const int32_t s = P.snode[std::min(i, j)];
+                const int64_t pi = pos_in(s, i), pj = pos_in(s, j);
+                if (pi < 0 || pj < 0) { bad.store(true); return; }   // not in the front: an inconsistent plan
+                dst[e] = fr[s].off + pi + pj * (int64_t)fr[s].d;
+            }
+    });
+    if (bad.load()) return EIGSOL_E_UNSUPPORTED;
     // launch tables: extend-add (child, first column) per (height, child rank); trailing-update
     // tiles (front, tile row, tile column) per (height, panel)
     using Launch = MfLaunch;
@@ -1651,6 +1698,43 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
     // one wave instead of four
     bool wave_ok = false;
     if (const char* e = std::getenv("EIGSOL_MF_WAVE")) wave_ok = std::atoi(e) != 0;
+    // small subtrees (at most sub_cap pivots, EIGSOL_MF_SUB; 0: off) solved whole by one workgroup
+    // each: their fronts are a contiguous postorder range, so a workgroup walks it up (forward) and
+    // down (backward) with no hand-off between workgroups and no per-height launch.  Measured and
+    // left off (1M convection-diffusion, tools/mf_grid.sh): caps 256 / 512 / 1024 / 2048 pivots
+    // 2.21 / 2.33 / 2.63 / 2.70 ms per iteration against 2.00 - the per-height launches keep every
+    // front of a height in flight, a subtree's fronts run one after the other
+    int sub_cap = 0;
+    if (const char* e = std::getenv("EIGSOL_MF_SUB")) sub_cap = std::atoi(e);
+    if (const char* e = std::getenv("EIGSOL_MF_FLOW"))
+        if (std::atoi(e) != 0) sub_cap = 0;   // the dataflow experiment takes the lower heights itself
+    std::vector<char> insub(nt, 0);
+    X.sub_ranges.clear();
+    if (sub_cap > 0) {
+        std::vector<int64_t> subp(nt, 0);
+        std::vector<int32_t> lo(nt);
+        for (int64_t s2 = 0; s2 < nt; ++s2) {   // postorder: children first
+            subp[s2] += fr[s2].ns;
+            if (fr[s2].ch0 == fr[s2].ch1) lo[s2] = (int32_t)s2;
+            else {
+                int32_t m = (int32_t)s2;
+                for (int32_t k = fr[s2].ch0; k < fr[s2].ch1; ++k) m = std::min(m, lo[chl[k]]);
+                lo[s2] = m;
+            }
+            if (fr[s2].parent >= 0) subp[fr[s2].parent] += subp[s2];
+            insub[s2] = subp[s2] <= sub_cap;
+        }
+        for (int64_t s2 = 0; s2 < nt; ++s2)
+            if (insub[s2] && (fr[s2].parent < 0 || !insub[fr[s2].parent])) {
+                X.sub_ranges.push_back(lo[s2]);
+                X.sub_ranges.push_back((int32_t)s2);
+            }
+        for (int64_t s2 = 0; s2 < nt; ++s2)
+            if (insub[s2]) {
+                X.lds_sub_f = std::max<int32_t>(X.lds_sub_f, (int32_t)((2 * fr[s2].ns + fr[s2].ms) * sb));
+                X.lds_sub_b = std::max<int32_t>(X.lds_sub_b, (int32_t)((fr[s2].ns + fr[s2].ms) * sb));
+            }
+    }
     lds_asm.assign(H + 1, 0);
     int32_t& nflag = X.nflag;
     int64_t& zsz = X.zsz;
@@ -1658,9 +1742,10 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
         std::vector<int32_t> big, wg;
         for (int64_t t = hstart[h]; t < hstart[h + 1]; ++t) {
             dev::MfFront& q = fr[lists[t]];
-            const bool is_big = big_ns > 0 && (q.ns >= big_ns || q.d >= big_d);
             q.flag0 = -1;
             q.zoff = 0;
+            if (insub[lists[t]]) continue;
+            const bool is_big = big_ns > 0 && (q.ns >= big_ns || q.d >= big_d);
             if (is_big) big.push_back(lists[t]);
             else if (wave_ok && q.ns <= dev::kWaveNs && q.ms <= dev::kWaveMs) slists.push_back(lists[t]);
             else wg.push_back(lists[t]);
@@ -1802,6 +1887,10 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     dm((void**)&f->flow_b, X.flow_b.size() * 4);
     dm((void**)&f->fheight, nt * 4);
     dm((void**)&f->done, nt * 4);
+    f->nsub = (int32_t)(X.sub_ranges.size() / 2);
+    f->lds_sub_f = X.lds_sub_f;
+    f->lds_sub_b = X.lds_sub_b;
+    dm((void**)&f->sub_ranges, X.sub_ranges.size() * 4);
     dm(&f->F, (size_t)fe * sb);
     dm(&f->u, (size_t)uo * sb);
     dm(&f->w, n * sb);
@@ -1831,6 +1920,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         up(f->flow_f, X.flow_f.data(), X.flow_f.size() * 4);
         up(f->flow_b, X.flow_b.data(), X.flow_b.size() * 4);
         up(f->fheight, P.height.data(), nt * 4);
+        up(f->sub_ranges, X.sub_ranges.data(), X.sub_ranges.size() * 4);
         hipMemsetAsync(f->done, 0, nt * 4, st);
         hipMemsetAsync(f->err, 0, 4, st);
         up(d_tab, tab.data(), tab.size() * 4);
@@ -1884,6 +1974,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         for (int32_t b : f->lds_bwd) mx = std::max(mx, b);
         for (int32_t b : f->lds_asm) mx = std::max(mx, b);
         mx = std::max(mx, std::max(f->lds_flow_f, f->lds_flow_b));
+        mx = std::max(mx, std::max(f->lds_sub_f, f->lds_sub_b));
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_kernel<S>),
@@ -1893,6 +1984,10 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_flow_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_flow_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_sub_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_sub_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal solve LDS");
     }
@@ -1921,6 +2016,9 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     const int32_t ef = ++f->epoch, eb = ++f->epoch;   // flag words: forward, then backward values
     const int flow_grid = (int)std::max<int64_t>(1, f->nflow);   // one workgroup per front, in order
     const bool ff = f->nflow && (f->flow_mode & 1), fb = f->nflow && (f->flow_mode & 2);
+    if (f->nsub)
+        hipLaunchKernelGGL((dev::mf_fwd_sub_kernel<S>), dim3(f->nsub), dim3(256), f->lds_sub_f, st, f->fronts,
+                           f->sub_ranges, f->chl, F, f->cmap, f->pinv, w, u);
     if (ff) {
         hipLaunchKernelGGL((dev::mf_fwd_flow_kernel<S>), dim3(flow_grid), dim3(256), f->lds_flow_f, st, f->fronts,
                            f->flow_f, f->nflow, f->done, ef, f->chl, F, f->cmap, f->pinv, w, u, f->err);
@@ -1956,6 +2054,9 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
             hipLaunchKernelGGL((dev::mf_bwd_wave_kernel<S>), dim3((nw + 3) / 4), dim3(256), 0, st, f->fronts, L,
                                (int32_t)nw, F, f->sidx, w, x);
     }
+    if (f->nsub)
+        hipLaunchKernelGGL((dev::mf_bwd_sub_kernel<S>), dim3(f->nsub), dim3(256), f->lds_sub_b, st, f->fronts,
+                           f->sub_ranges, F, f->sidx, (const S*)w, x);
     if (fb)
         hipLaunchKernelGGL((dev::mf_bwd_flow_kernel<S>), dim3(flow_grid), dim3(256), f->lds_flow_b, st, f->fronts,
                            f->flow_b, f->nflow, f->done, eb, f->hflow, f->fheight, F, f->sidx, (const S*)w, x, f->err);
