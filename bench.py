@@ -424,6 +424,7 @@ def run_config5_convdiff(E, S, ctx, torch, stream, nx=1000, max_iter=8):
     nested-dissection multifrontal LU, multifrontal.hip; round 5's first figure was the RCM band LU:
     13.8 s set-up, 1.37 s per iteration) and for ILU(0) + GMRES forced (EIGSOL_LU_FILL_CAP=0): set-up
     time, steady-state ms per iteration, Arnoldi steps / band width, and the end-to-end time of a run
+    (plus the default path on the values rounded to complex<float>)
     of at most max_iter iterations (sigma sits inside a clustered spectrum, so the iteration itself
     converges slowly: `converged` says whether it did).  solve_shifted.hpp:85-117 is the reference
     path (SparseLU, refactored every iteration)."""
@@ -451,6 +452,13 @@ def run_config5_convdiff(E, S, ctx, torch, stream, nx=1000, max_iter=8):
         d["eigen_residual"] = float(np.linalg.norm(M @ x - res.eigenvalue * x) / np.linalg.norm(x))
         out[label] = d
     A.close()
+    # complex<float>: the same family on the values widened to double, the iterate in complex<float>
+    A32 = E.CsrMatrix(ctx, rp, ci, v.astype(np.complex64), (n, n))
+    res, d = _convdiff_run(E, ctx, torch, stream, A32, np.complex64(sigma), x0.astype(np.complex64), max_iter)
+    x = res.eigenvector.astype(np.complex128)
+    d["eigen_residual"] = float(np.linalg.norm(M @ x - res.eigenvalue * x) / np.linalg.norm(x))
+    out["complex64_default"] = d
+    A32.close()
     return out
 
 

@@ -52,6 +52,8 @@ struct ShiftFactor {
     int64_t n = 0;
     int kind = 0;                 // 0 triangular CSR, 1 dense LU, 2 ILU(0)-preconditioned GMRES, 3 band LU
     GmresSolver* gm = nullptr;    // kind 2 (gmres.hip)
+    void* promo = nullptr;        // kind 2 in single precision: [2][n] double-precision right-hand side and
+                                  // solution of the GMRES family's solve (its factors are built in double)
     BandFactor* band = nullptr;   // kind 3 (band_lu.hip)
     void* hpin = nullptr;         // pinned host scratch for per-solve readbacks (pageable copies sleep ~1 ms)
     eigsol_csr* src = nullptr;    // kind 2: A, retained for the densified-LU fallback
@@ -1734,6 +1736,14 @@ __global__ __launch_bounds__(256) void fill_kernel(T* __restrict__ a, int64_t n,
     for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) a[k] = v;
 }
 
+template <class S, class W>
+__global__ __launch_bounds__(256) void convert_kernel(const S* __restrict__ in, W* __restrict__ out, int64_t n) {
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        if constexpr (is_real_v<S>) out[i] = static_cast<W>(in[i]);
+        else out[i] = W{static_cast<decltype(W{}.re)>(in[i].re), static_cast<decltype(W{}.im)>(in[i].im)};
+    }
+}
+
 }  // namespace dev
 
 // ================================================================== host side
@@ -1742,6 +1752,10 @@ __global__ __launch_bounds__(256) void fill_kernel(T* __restrict__ a, int64_t n,
 // stays double-only
 template <class S> inline constexpr bool kDenseLU = true;
 template <class S> inline constexpr bool kGmres = std::is_same_v<S, double> || std::is_same_v<S, cplx>;
+// single-precision matrices take the GMRES family (exact / multifrontal LU, ILU(0) + GMRES) on their
+// values widened to double: the factor, the residual checks and the refinement run in double, the
+// iterate stays in the matrix's precision (dtype >= the reference's SparseLU<float>)
+template <class S> using GmresScalar = std::conditional_t<is_real_v<S>, double, cplx>;
 int resident_blocks(eigsol_ctx* ctx, const void* kernel, int threads, size_t dyn_lds, int* grid);
 
 template <class S>
@@ -1779,7 +1793,7 @@ static void shift_free(ShiftFactor* f) {
                     f->ppiv,
                     (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
                     (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf,
-                    f->kpart, f->kblk})
+                    f->kpart, f->kblk, f->promo})
         if (p) hipFree(p);
     for (int j = 0; j < dev::kMaxMulti; ++j) {
         if (j < dev::kMaxMulti - 1 && f->aux[j]) hipFree(f->aux[j]);
@@ -2134,11 +2148,12 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         // factors (exact no-pivot LU where the fill stays within 3 x nnz, else the nested-dissection
         // multifrontal LU, gmres.hip / multifrontal.hip; ILU(0) + GMRES when neither fits): the band
         // factor runs one panel kernel per 64 columns on one workgroup (round 5, config5_convdiff_1M:
-        // 13.8 s, 1.37 s per solve).  The band stays for smaller orders, single precision, or forced.
+        // 13.8 s, 1.37 s per solve).  Single precision takes the same family on values widened to
+        // double (gm_solve_s).  The band stays for smaller orders, or forced.
         BandPlan plan;
         SparseSolver fs = kSolverBand;
         const bool pre_forced = general_sparse_forced(fs);
-        const bool large_gmres = !pre_forced && n > 16384 && kGmres<S>;
+        const bool large_gmres = !pre_forced && n > 16384;
         if (!large_gmres && !(pre_forced && fs != kSolverBand)) band_plan(A->dtype, n, rp.data(), ci.data(), plan);
         bool forced = false;
         const SparseSolver solver = large_gmres ? kSolverGMRES : general_sparse_solver(n, sizeof(S), plan, forced);
@@ -2155,9 +2170,21 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
             *out = f;
             return EIGSOL_OK;
         }
-        // single precision has no GMRES: the densified LU (below) where it fits the device
-        if (solver == kSolverGMRES && kGmres<S>) {
-            rc = gmres_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, &f->gm);
+        if (solver == kSolverGMRES) {
+            if constexpr (kGmres<S>) {
+                rc = gmres_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, &f->gm);
+            } else {
+                using W = GmresScalar<S>;
+                std::vector<W> vw(v.size());
+                for (size_t e = 0; e < v.size(); ++e) {
+                    if constexpr (is_real_v<S>) vw[e] = static_cast<double>(v[e]);
+                    else vw[e] = W{static_cast<double>(v[e].re), static_cast<double>(v[e].im)};
+                }
+                rc = gmres_create(A->ctx, dtype_complex(A->dtype) ? EIGSOL_C128 : EIGSOL_F64, n, rp.data(), ci.data(),
+                                  vw.data(), sre, sim, &f->gm);
+                if (rc == EIGSOL_OK && hipMalloc(&f->promo, 2 * (size_t)n * sizeof(W)) != hipSuccess)
+                    rc = fail(EIGSOL_E_HIP, "solve_shifted: hipMalloc(single-precision GMRES vectors)");
+            }
             f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 1023) / 1024));
             if (rc == EIGSOL_OK && (hipMalloc(&f->work, 64) != hipSuccess ||
                                     hipMalloc(&f->wave_part, (size_t)f->red_grid * sizeof(dev::part4)) != hipSuccess ||
@@ -2940,6 +2967,27 @@ static int multi_alloc(ShiftFactor* f) {
 // the final iterate of a multi-solve launch that stopped on solve j < K - 1 (final_parity 2 + j)
 void* shift_aux(const ShiftFactor* f, int j) { return (j >= 0 && j < dev::kMaxMulti - 1) ? f->aux[j] : nullptr; }
 
+// x = M^-1 (b / bdiv) by the GMRES family; single precision through f->promo (widen, solve, narrow)
+template <class S>
+static int gm_solve_s(ShiftFactor* f, const void* b, double bdiv, void* y, const double* guess) {
+    if constexpr (kGmres<S>) {
+        return gmres_solve(f->gm, b, bdiv, y, guess);
+    } else {
+        using W = GmresScalar<S>;
+        hipStream_t st = f->ctx->stream;
+        W* wb = static_cast<W*>(f->promo);
+        W* wy = wb + f->n;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (f->n + 255) / 256));
+        hipLaunchKernelGGL((dev::convert_kernel<S, W>), dim3(grid), dim3(256), 0, st, static_cast<const S*>(b), wb, f->n);
+        EIGSOL_HIP(hipGetLastError());
+        const int rc = gmres_solve(f->gm, wb, bdiv, wy, guess);
+        if (rc != EIGSOL_OK) return rc;
+        hipLaunchKernelGGL((dev::convert_kernel<W, S>), dim3(grid), dim3(256), 0, st, wy, static_cast<S*>(y), f->n);
+        EIGSOL_HIP(hipGetLastError());
+        return EIGSOL_OK;
+    }
+}
+
 template <class S>
 static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, void* buf0, void* buf1,
                           PowerCtl* ctl, const void* rank_part, void* my_part, void* trace, int parity,
@@ -2949,7 +2997,7 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         // ILU(0)-preconditioned GMRES: host-driven (one sync per Arnoldi step), so the iteration is
         // prologue launch -> host reads the stop decision -> solve -> partials launch
         if (!iter) {
-            const int rc = gmres_solve(f->gm, b, 0.0, y);
+            const int rc = gm_solve_s<S>(f, b, 0.0, y, nullptr);
             if (rc != EIGSOL_E_SOLVER) return rc;
             EIGSOL_TRY(gmres_dense_fallback<S>(f, rc));
             return shift_launch_t<S>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
@@ -3000,7 +3048,7 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
                 use_guess = true;
             }
         }
-        const int rc = gmres_solve(f->gm, parity ? buf0 : buf1, cr.nrm, parity ? buf1 : buf0, use_guess ? guess : nullptr);
+        const int rc = gm_solve_s<S>(f, parity ? buf0 : buf1, cr.nrm, parity ? buf1 : buf0, use_guess ? guess : nullptr);
         if (rc == EIGSOL_E_SOLVER) {
             // switch to the densified LU and redo this launch on it: the dense kernel's prologue
             // re-evaluates the same decision from the same carry record (idempotent)

@@ -260,3 +260,62 @@ def test_multifrontal_block_row_solve_kernels(ctx, env, big, wave, flow, sub):
     assert abs(r.eigenvalue - lam) <= 1e-10 * (1 + abs(lam)), (r.eigenvalue, lam)
     assert np.linalg.norm(M @ r.eigenvector - r.eigenvalue * r.eigenvector) <= 1e-9
     A.close()
+
+
+def test_single_precision_complex_default_is_multifrontal(ctx):
+    """complex<float> past n = 16384 takes the GMRES family on values widened to double (the factor,
+    residual check and refinement in double, the iterate in complex<float>): on the SuperLU fixture's
+    matrix rounded to complex<float> the eigenvalue agrees with the complex<double> run on the same
+    rounded values within single-precision tolerance (1e-5 relative), the eigenvector is complex64,
+    and a single solve has a single-precision backward error."""
+    fx = json.load(open(os.path.join(GOLD, "convdiff141.json")))
+    rp, ci, v = S.convdiff_complex(fx["nx"], seed=fx["seed"])
+    n = fx["n"]
+    v32 = v.astype(np.complex64)
+    sigma = complex(*fx["sigma"])
+    out = {}
+    for dt, vals in ((np.complex64, v32), (np.complex128, v32.astype(np.complex128))):
+        A = E.CsrMatrix(ctx, rp, ci, vals, (n, n))
+        assert _variant(A, dt(sigma)) == 19
+        r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(fx["max_iter"], 1e-6, dt(sigma)),
+                                           S.start_vector(n, dt))
+        assert r.converged
+        assert np.asarray(r.eigenvector).dtype == dt
+        out[dt] = r
+        if dt is np.complex64:
+            b = S.start_vector(n, np.complex64, seed=11)
+            y = E.solve_shifted(A, np.complex64(sigma), b)
+            assert y.dtype == np.complex64
+            M = sp.csr_matrix((vals.astype(np.complex128), ci, rp), shape=(n, n))
+            res = M @ y.astype(np.complex128) - sigma * y.astype(np.complex128) - b
+            assert np.linalg.norm(res) <= 1e-5 * (abs(M).sum(0).max() + abs(sigma)) * np.linalg.norm(y)
+        A.close()
+    l32, l64 = out[np.complex64].eigenvalue, out[np.complex128].eigenvalue
+    assert abs(l32 - l64) <= 1e-5 * (1 + abs(l64)), (l32, l64)
+    assert abs(abs(np.vdot(out[np.complex64].eigenvector.astype(np.complex128),
+                           out[np.complex128].eigenvector)) - 1) <= 1e-4
+
+
+def test_single_precision_real_multifrontal_parity(ctx, env):
+    """float on the multifrontal path (forced at n = 900): the eigenvalue of the oracle's dense
+    restatement of the reference loop on the float values within 1e-5 relative."""
+    _mf_env(env)
+    rp, ci, v = S.convdiff_complex(30, seed=5)
+    v = np.ascontiguousarray(v.real).astype(np.float32)
+    n = 900
+    D = sp.csr_matrix((v.astype(np.float64), ci, rp), shape=(n, n)).toarray()
+    ev = np.linalg.eigvals(D)
+    re = np.sort(ev.real[np.abs(ev.imag) < 1e-12])
+    i = len(re) // 3
+    sigma = re[i] + 0.1 * min(re[i + 1] - re[i], re[i] - re[i - 1])
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    assert _variant(A, np.float32(sigma)) == 19
+    x0 = S.start_vector(n, np.float32)
+    r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(500, 1e-6, np.float32(sigma)), x0)
+    ref = O.shifted_dense(D, float(np.float32(sigma)), x0.astype(np.float64), 500, 1e-12)
+    assert r.converged and ref["converged"]
+    assert np.asarray(r.eigenvector).dtype == np.float32
+    lam = ref["eigenvalue"]
+    assert abs(r.eigenvalue - lam) <= 1e-5 * (1 + abs(lam)), (r.eigenvalue, lam)
+    assert abs(abs(np.vdot(r.eigenvector.astype(np.float64), ref["eigenvector"])) - 1) <= 1e-4
+    A.close()

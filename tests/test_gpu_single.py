@@ -203,7 +203,8 @@ def test_single_algorithmic_bytes_and_band_solve(ctx):
     # SURVEY §8d accounting with 4-byte values: (4 + 4) nnz + 4 (n + 1) + 2 * 4 n
     assert info["bytes_per_iteration"] == 8 * nnz + 4 * (n + 1) + 8 * n
     s.close()
-    # a general (non-triangular) single-precision sparse shifted solve: the RCM band LU in float
+    # a general (non-triangular) single-precision sparse shifted solve past n = 16384: the GMRES family
+    # (here the exact no-pivot LU) on the values widened to double, the solution rounded to float
     # (solve_shifted.hpp:85-117's SparseLU branch); backward error at single precision
     b = S.start_vector(n, np.float32, seed=3)
     y = E.solve_shifted(A, np.float32(0.5), b)
