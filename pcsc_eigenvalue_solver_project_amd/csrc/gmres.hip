@@ -205,6 +205,14 @@ __global__ __launch_bounds__(kThreads) void gm_cscale_kernel(const S* src, doubl
         dst[i] = mul(src[i], from_re_im<S>(gre, gim));
 }
 
+// y -= sigma x: M x = A x - sigma x on the caller's matrix A
+template <class S>
+__global__ __launch_bounds__(kThreads) void gm_shift_sub_kernel(const S* x, double sre, double sim, S* y, int64_t n) {
+    const S sig = from_re_im<S>(sre, sim);
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads)
+        y[i] = sub(y[i], mul(sig, x[i]));
+}
+
 template <class S>
 __global__ __launch_bounds__(kThreads) void gm_axpy_kernel(S* x, const S* t, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads)
@@ -224,7 +232,9 @@ struct GmresSolver {
     double rtol_accept = 1e-10; // worst final residual reported as a success (EIGSOL_GMRES_ACCEPT)
     double normM = 0.0;         // max(||M||_1, ||M||_inf): the backward-error scale of a direct solve
     double be_accept = 1e-14;   // a direct solve whose normwise backward error is below this is accepted
-    eigsol_csr* M = nullptr;
+    eigsol_csr* M = nullptr;    // M = A - sigma I uploaded (single-precision A only), else
+    eigsol_csr* A = nullptr;    // the caller's device matrix: M x = A x - sigma x (no second copy of M)
+    double sre = 0.0, sim = 0.0;
     ShiftFactor* L = nullptr;
     ShiftFactor* U = nullptr;
     void* V = nullptr;          // n x (m + 1), column-major
@@ -253,6 +263,7 @@ void gmres_free(GmresSolver* g) {
     if (g->U) shift_factor_free(g->U);
     if (g->mf) mf_free(g->mf);
     if (g->M) csr_release(g->M);
+    if (g->A) csr_release(g->A);
     for (void* p : {g->V, g->Z, g->t1, g->w, g->x, (void*)g->part, (void*)g->hdev})
         if (p) hipFree(p);
     if (g->hpin) hipHostFree(g->hpin);
@@ -321,7 +332,7 @@ static bool lu_fill_pattern(int64_t n, const std::vector<int32_t>& rp, const std
 
 template <class S>
 static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const int32_t* ci, const S* v,
-                          double sre, double sim, GmresSolver** out) {
+                          double sre, double sim, eigsol_csr* Adev, GmresSolver** out) {
     hipStream_t st = ctx->stream;
     static const bool dbg = std::getenv("EIGSOL_MF_DEBUG") != nullptr;
     auto tp = std::chrono::steady_clock::now();
@@ -390,7 +401,17 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
         for (double c : colsum) g->normM = std::max(g->normM, c);
     }
     lap("build M");
-    int rc = csr_upload(ctx, dtype, n, n, g->nnzM, mrp.data(), mci.data(), mv.data(), &g->M, 0);
+    // products with M: on the caller's device matrix A when it is given (M x = A x - sigma x; round
+    // 5: the host layout build and pageable upload of a second copy took 0.19 s of the 1M set-up)
+    int rc = EIGSOL_OK;
+    g->sre = sre;
+    g->sim = sim;
+    if (Adev) {
+        g->A = Adev;
+        csr_retain(Adev);
+    } else {
+        rc = csr_upload(ctx, dtype, n, n, g->nnzM, mrp.data(), mci.data(), mv.data(), &g->M, 0);
+    }
     lap("upload M");
     // complete fill where affordable: M's values on the closed pattern, zeros at the fill
     // positions; the factorization below then produces the exact LU (round 4: the 1M config-5
@@ -618,11 +639,12 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
 }
 
 int gmres_create(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const int32_t* ci, const void* v,
-                 double sre, double sim, GmresSolver** out) {
+                 double sre, double sim, GmresSolver** out, eigsol_csr* Adev) {
+    if (Adev && (Adev->dtype != dtype || Adev->nrows != n || Adev->ncols != n || Adev->xoff != 0)) Adev = nullptr;
     if (dtype == EIGSOL_C128)
-        return gmres_create_t<cplx>(ctx, dtype, n, rp, ci, static_cast<const cplx*>(v), sre, sim, out);
+        return gmres_create_t<cplx>(ctx, dtype, n, rp, ci, static_cast<const cplx*>(v), sre, sim, Adev, out);
     if (dtype == EIGSOL_F64)
-        return gmres_create_t<double>(ctx, dtype, n, rp, ci, static_cast<const double*>(v), sre, sim, out);
+        return gmres_create_t<double>(ctx, dtype, n, rp, ci, static_cast<const double*>(v), sre, sim, Adev, out);
     return fail(EIGSOL_E_UNSUPPORTED, "solve_shifted: the GMRES path is built for double and complex<double>");
 }
 
@@ -654,6 +676,18 @@ static int cgs2(GmresSolver* g, S* V, int k, S* w, std::vector<hc>& h, double& w
     return EIGSOL_OK;
 }
 
+// y = M x
+template <class S>
+static int apply_M(GmresSolver* g, const S* x, S* y) {
+    if (g->M) return eigsol_csr_spmv(g->M, x, y);
+    EIGSOL_TRY(eigsol_csr_spmv(g->A, x, y));
+    const int gb = (int)std::min<int64_t>(2048, (g->n + dev::kThreads - 1) / dev::kThreads);
+    hipLaunchKernelGGL((dev::gm_shift_sub_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, g->ctx->stream, x, g->sre,
+                       g->sim, y, g->n);
+    EIGSOL_HIP(hipGetLastError());
+    return EIGSOL_OK;
+}
+
 template <class S>
 static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const double* guess) {
     hipStream_t st = g->ctx->stream;
@@ -672,7 +706,7 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
         shift_info(g->U, &ub, nullptr, nullptr);
     }
     const double sb = (double)sizeof(S);
-    mb = (sb + 4.0) * (double)g->nnzM + 4.0 * (double)(n + 1) + 2.0 * sb * (double)n;
+    mb = (sb + 4.0) * (double)(g->A ? g->A->nnz : g->nnzM) + 4.0 * (double)(n + 1) + (g->A ? 5.0 : 2.0) * sb * (double)n;
     double bytes = 0.0;
     int steps = 0;
     auto norm_of = [&](S* v, double& out) -> int {
@@ -697,7 +731,7 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
         hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
         hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev);
         EIGSOL_TRY(precond(w, x));
-        EIGSOL_TRY(eigsol_csr_spmv(g->M, x, t1));
+        EIGSOL_TRY(apply_M<S>(g, x, t1));
         hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, t1, w, n);
         hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
         hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev + 2);
@@ -731,7 +765,7 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
     // (kept only when it beats x0 = 0).
     if (guess && bnorm > 0.0) {
         hipLaunchKernelGGL((dev::gm_cscale_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, w, guess[0], guess[1], x, n);
-        EIGSOL_TRY(eigsol_csr_spmv(g->M, x, t1));
+        EIGSOL_TRY(apply_M<S>(g, x, t1));
         hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, t1, w, n);
         EIGSOL_TRY(norm_of(w, beta));
         bytes += mb + 4.0 * sb * (double)n;
@@ -759,7 +793,7 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
                 S* vj = V + (int64_t)j * n;
                 S* zj = Z + (int64_t)j * n;
                 EIGSOL_TRY(precond(vj, zj));   // kept: x += Z y at the cycle's end needs no preconditioner
-                EIGSOL_TRY(eigsol_csr_spmv(g->M, zj, w));
+                EIGSOL_TRY(apply_M<S>(g, zj, w));
                 double hn = 0.0;
                 EIGSOL_TRY(cgs2<S>(g, V, j + 1, w, h, hn));
                 bytes += lb + ub + mb + 2.0 * (3.0 * (j + 1) + 2.0) * sb * (double)n;
@@ -808,7 +842,7 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
             hipLaunchKernelGGL((dev::gm_combine_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, Z, n, k, g->hdev, w, n, 1);
             hipLaunchKernelGGL((dev::gm_axpy_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, x, w, n);
             // true residual r = b - M x (the next cycle's start)
-            EIGSOL_TRY(eigsol_csr_spmv(g->M, x, t1));
+            EIGSOL_TRY(apply_M<S>(g, x, t1));
             hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, t1, w, n);
             EIGSOL_TRY(norm_of(w, beta));
             bytes += mb + 2.0 * (double)k * sb * (double)n;

@@ -1145,6 +1145,9 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
     };
     auto work = [&]() {
         std::vector<int32_t> q;
+        // raised inside a BFS once *stop is seen (checked every 64K visits: a whole-graph BFS of the
+        // top piece takes tens of ms), the task then abandons the dissection
+        bool cut = false;
         // BFS inside the piece tagged `tag` from root: q holds the visit order, level[] the levels
         auto bfs = [&](int32_t root, int64_t tag) -> int32_t {
             const int64_t b = ++bstamp;
@@ -1155,6 +1158,10 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
             int32_t depth = 0;
             for (size_t h = 0; h < q.size(); ++h) {
                 const int32_t v = q[h];
+                if ((h & 65535) == 65535 && stop && stop->load(std::memory_order_relaxed)) {
+                    cut = true;
+                    return depth;
+                }
                 for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
                     const int32_t w = g.adj[e];
                     if (tag_of(w) != tag || seen[w] == b) continue;
@@ -1186,11 +1193,14 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
                 --active;
                 if (active == 0 && stack.empty()) cv.notify_all();
             };
-            if (stop && stop->load(std::memory_order_relaxed)) {
+            auto abort_task = [&]() {
                 std::lock_guard<std::mutex> lk(mu);
                 aborted = true;
                 --active;
                 cv.notify_all();
+            };
+            if (cut || (stop && stop->load(std::memory_order_relaxed))) {
+                abort_task();
                 return;
             }
             const int64_t sz = (int64_t)t.nodes.size();
@@ -1203,6 +1213,10 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
             const int64_t tag = ++stamp;
             for (int32_t v : t.nodes) __atomic_store_n(&inset[v], tag, __ATOMIC_RELAXED);
             bfs(t.nodes[0], tag);
+            if (cut) {
+                abort_task();
+                return;
+            }
             if ((int64_t)q.size() < sz) {
                 // disconnected: components (in the order of their first vertex in the piece); the
                 // small ones packed into leaves, the others new pieces
@@ -1212,7 +1226,12 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
                 for (int32_t v : t.nodes) {
                     if (seen[v] >= b0) continue;
                     bfs(v, tag);
+                    if (cut) break;
                     comps.push_back(q);
+                }
+                if (cut) {
+                    abort_task();
+                    return;
                 }
                 std::vector<int32_t> pack;
                 int32_t slot = 0;
@@ -1255,6 +1274,10 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
                 }
                 root = best;
                 ecc = e2;
+            }
+            if (cut) {
+                abort_task();
+                return;
             }
             const int32_t nlev = ecc + 1;
             if (nlev < 3) {   // no level structure to cut: one dense front

@@ -32,8 +32,9 @@
 namespace eigsol {
 
 struct GmresSolver;
+// Adev: the device matrix A itself (same dtype and order), used for the products with M = A - sigma I
 int gmres_create(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const int32_t* ci, const void* v,
-                 double sre, double sim, GmresSolver** out);
+                 double sre, double sim, GmresSolver** out, eigsol_csr* Adev = nullptr);
 void gmres_free(GmresSolver* g);
 int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev, const double* guess = nullptr);
 void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps);
@@ -2172,7 +2173,7 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         }
         if (solver == kSolverGMRES) {
             if constexpr (kGmres<S>) {
-                rc = gmres_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, &f->gm);
+                rc = gmres_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, &f->gm, A);
             } else {
                 using W = GmresScalar<S>;
                 std::vector<W> vw(v.size());
