@@ -65,6 +65,8 @@ struct MfFront {
     int32_t parent;
     int32_t flag0;  // large fronts: first of the front's pivot-block flags; -1: solved by one workgroup
     int64_t zoff;   // large fronts: assembled right-hand side (d entries) at z + zoff
+    int64_t goff;   // inverse form (ns <= 64, d <= 256; -1: none) at F + goff: [inv(L11); L21 inv(L11)]
+                    // (d x ns, ld d), then [inv(U11), -inv(U11) U12] (ns x d, ld ns)
 };
 
 __device__ __forceinline__ double mf_rl(double v, int src) {
@@ -246,6 +248,29 @@ __device__ __forceinline__ void mf_fwd_front(const MfFront f, unsigned char* lds
     }
     for (int t = tid; t < ns; t += 256) y[t] = r[pinv[f.c0 + t]];
     __syncthreads();
+    if (f.goff >= 0) {
+        // one product over the d rows, tpr threads per row (columns interleaved), partials summed
+        // in a fixed order
+        const S* G = F + f.goff;
+        S* part = acc + ms;
+        const int R = d <= 64 ? 64 : d <= 128 ? 128 : 256, tpr = 256 / R;
+        const int i = tid % R, p = tid / R;
+        S sacc = s_zero<S>();
+        if (i < d) {
+            const S* Gi = G + i;
+#pragma unroll 8
+            for (int j = p; j < ns; j += tpr) sacc = add(sacc, mul(Gi[(int64_t)j * d], y[j]));
+        }
+        part[p * R + i] = sacc;
+        __syncthreads();
+        if (tid < d) {
+            S v = part[tid];
+            for (int q = 1; q < tpr; ++q) v = add(v, part[q * R + tid]);
+            if (tid < ns) w[f.c0 + tid] = v;
+            else u[f.uoff + tid - ns] = add(acc[tid - ns], v);
+        }
+        return;
+    }
     const S* A = F + f.off;
     for (int jb = 0; jb < ns; jb += 64) {
         const int bw = min(64, ns - jb);
@@ -320,6 +345,24 @@ __device__ __forceinline__ void mf_bwd_front(const MfFront f, unsigned char* lds
     S* t = reinterpret_cast<S*>(lds_raw);
     S* xs = t + ns;
     for (int q = tid; q < ms; q += 256) xs[q] = x[sidx[f.sof + q]];
+    if (f.goff >= 0) {
+        // x(pivots) = [inv(U11), -inv(U11) U12] [w(pivots); x(struct)]: wave p takes columns p, p + 4, ...
+        for (int q = tid; q < ns; q += 256) t[q] = w[f.c0 + q];
+        __syncthreads();
+        const S* G = F + f.goff + (int64_t)d * ns;
+        S* part = xs + ms;
+        const int k = lane, p = wv;
+        S sacc = s_zero<S>();
+        if (k < ns) {
+            const S* Gk = G + k;
+#pragma unroll 8
+            for (int c = p; c < d; c += 4) sacc = add(sacc, mul(Gk[(int64_t)c * ns], c < ns ? t[c] : xs[c - ns]));
+        }
+        part[p * 64 + k] = sacc;
+        __syncthreads();
+        if (tid < ns) x[f.c0 + tid] = add(add(add(part[tid], part[64 + tid]), part[128 + tid]), part[192 + tid]);
+        return;
+    }
     __syncthreads();
     const S* A = F + f.off;
     for (int k = tid; k < ns; k += 256) {
@@ -796,6 +839,72 @@ __global__ __launch_bounds__(256) void mf_inv_kernel(const MfFront* fr, const in
     }
     __syncthreads();
     for (int e = tid; e < 64 * 64; e += 256) out[4096 + e] = X[(e & 63) + (e >> 6) * 65];
+}
+
+// Inverse form of a one-workgroup front (after the factorization; EIGSOL_MF_INVFORM=0: off): the
+// forward solve of the front becomes one product [inv(L11); L21 inv(L11)] (P r) and the backward one
+// [inv(U11), -inv(U11) U12] [t; x(struct)], every load independent, instead of a dependent chain
+// over the pivot columns on one wave followed by the struct rows (the diagonal blocks of the large
+// fronts are inverted the same way, mf_inv_kernel).
+template <class S>
+__global__ __launch_bounds__(256) void mf_invform_kernel(const MfFront* fr, const int32_t* list, S* F) {
+    __shared__ S T[64 * 65];
+    __shared__ S X[64 * 65];
+    const MfFront f = fr[list[blockIdx.x]];
+    const int tid = threadIdx.x, d = f.d, ns = f.ns;
+    const S* A = F + f.off;
+    S* Gf = F + f.goff;
+    S* Gb = Gf + (int64_t)d * ns;
+    S one;
+    set_re_im(one, 1.0, 0.0);
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int i = e & 63, j = e >> 6;
+        T[i + j * 65] = (i < ns && j < ns) ? A[i + (int64_t)j * d] : (i == j ? one : s_zero<S>());
+    }
+    __syncthreads();
+    if (tid < 64) {   // inv(L11), column t (unit lower)
+        const int t = tid;
+        for (int i = 0; i < 64; ++i) {
+            S v = i == t ? one : s_zero<S>();
+            for (int j = t; j < i; ++j) v = sub(v, mul(T[i + j * 65], X[j + t * 65]));
+            X[i + t * 65] = i < t ? s_zero<S>() : v;
+        }
+    }
+    __syncthreads();
+    // rows < ns: inv(L11); rows ns .. d: W = L21 inv(L11), W(i, j) = sum_{k >= j} L21(i, k) inv(L11)(k, j)
+    for (int e = tid; e < d * ns; e += 256) {
+        const int i = e % d, j = e / d;
+        S v;
+        if (i < ns) {
+            v = X[i + j * 65];
+        } else {
+            v = s_zero<S>();
+            for (int k = j; k < ns; ++k) v = add(v, mul(A[i + (int64_t)k * d], X[k + j * 65]));
+        }
+        Gf[i + (int64_t)j * d] = v;
+    }
+    __syncthreads();
+    if (tid < 64) {   // inv(U11), column t
+        const int t = tid;
+        for (int i = 63; i >= 0; --i) {
+            S v = i == t ? one : s_zero<S>();
+            for (int j = i + 1; j <= t; ++j) v = sub(v, mul(T[i + j * 65], X[j + t * 65]));
+            X[i + t * 65] = i > t ? s_zero<S>() : sdiv(v, T[i + i * 65]);
+        }
+    }
+    __syncthreads();
+    // columns < ns: inv(U11); columns ns + q: -inv(U11) U12(:, q), U12(k, q) = A(k, ns + q)
+    for (int e = tid; e < ns * d; e += 256) {
+        const int i = e % ns, c = e / ns;
+        S v;
+        if (c < ns) {
+            v = X[i + c * 65];
+        } else {
+            v = s_zero<S>();
+            for (int k = i; k < ns; ++k) v = sub(v, mul(X[i + k * 65], A[k + (int64_t)c * d]));
+        }
+        Gb[i + (int64_t)c * ns] = v;
+    }
 }
 
 // acc += tile(row, c0 .. c0 + 16) * yv over the columns below lim (tile values already loaded)
@@ -1600,6 +1709,8 @@ struct MfHost {
     int32_t lds_flow_f = 0, lds_flow_b = 0;
     std::vector<int32_t> sub_ranges;       // small subtrees solved by one workgroup each: (lo, hi) fronts
     int32_t lds_sub_f = 0, lds_sub_b = 0;
+    std::vector<int32_t> inv_list;         // fronts with an inverse form (MfFront::goff)
+    int64_t gsz = 0;                       // its scalars, stored after the fronts in F
     MfStats stt;
 };
 
@@ -1795,6 +1906,28 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
         fcnt[h] = (int64_t)tabf.size() / 2 - foff[h];
         bcnt[h] = (int64_t)tabb.size() / 2 - boff[h];
     }
+    // inverse forms of the one-workgroup fronts with at most 64 pivots and 256 rows (mf_invform_kernel;
+    // EIGSOL_MF_INVFORM=0: off), kept only while the fronts and the forms fit 0.6 of the device memory
+    X.inv_list.clear();
+    X.gsz = 0;
+    {
+        const char* e = std::getenv("EIGSOL_MF_INVFORM");
+        const bool on = !(e && std::atoi(e) == 0);
+        for (int64_t s2 = 0; s2 < nt; ++s2) {
+            dev::MfFront& q = fr[s2];
+            q.goff = -1;
+            if (on && q.flag0 < 0 && q.ns <= 64 && q.d <= 256) {
+                q.goff = (int64_t)fe + X.gsz;
+                X.gsz += 2 * (int64_t)q.d * q.ns;
+                X.inv_list.push_back((int32_t)s2);
+            }
+        }
+        if (((double)fe + (double)X.gsz) * (double)sb > 0.6 * free_bytes) {
+            for (int32_t s2 : X.inv_list) fr[s2].goff = -1;
+            X.inv_list.clear();
+            X.gsz = 0;
+        }
+    }
     // dataflow launches for the heights below the first one with a large front (EIGSOL_MF_FLOW=0: off)
     {
         bool flow = false;
@@ -1872,11 +2005,13 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     if (const char* e = std::getenv("EIGSOL_MF_BACKOFF")) f->backoff = std::atoi(e);
     f->lds_fwd.assign(H + 1, 0);
     f->lds_bwd.assign(H + 1, 0);
+    // the inverse-form branch keeps 256 partial sums after the front's vectors
+    const int32_t inv_lds = X.gsz ? (int32_t)(256 * sb) : 0;
     for (int32_t h = 0; h <= H; ++h)
         for (int64_t t = sstart[h] + nwave[h]; t < sstart[h] + nwave[h] + nsmall[h]; ++t) {
             const dev::MfFront& q = fr[slists[t]];
-            f->lds_fwd[h] = std::max<int32_t>(f->lds_fwd[h], (int32_t)((2 * q.ns + q.ms) * sb));
-            f->lds_bwd[h] = std::max<int32_t>(f->lds_bwd[h], (int32_t)((q.ns + q.ms) * sb));
+            f->lds_fwd[h] = std::max<int32_t>(f->lds_fwd[h], (int32_t)((2 * q.ns + q.ms) * sb) + inv_lds);
+            f->lds_bwd[h] = std::max<int32_t>(f->lds_bwd[h], (int32_t)((q.ns + q.ms) * sb) + inv_lds);
         }
     hipStream_t st = ctx->stream;
     int rc = EIGSOL_OK;
@@ -1911,10 +2046,12 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     dm((void**)&f->fheight, nt * 4);
     dm((void**)&f->done, nt * 4);
     f->nsub = (int32_t)(X.sub_ranges.size() / 2);
-    f->lds_sub_f = X.lds_sub_f;
-    f->lds_sub_b = X.lds_sub_b;
+    f->lds_sub_f = X.lds_sub_f ? X.lds_sub_f + inv_lds : 0;
+    f->lds_sub_b = X.lds_sub_b ? X.lds_sub_b + inv_lds : 0;
     dm((void**)&f->sub_ranges, X.sub_ranges.size() * 4);
-    dm(&f->F, (size_t)fe * sb);
+    dm(&f->F, ((size_t)fe + (size_t)X.gsz) * sb);
+    int32_t* d_inv = nullptr;
+    if (!X.inv_list.empty()) dm((void**)&d_inv, X.inv_list.size() * 4);
     dm(&f->u, (size_t)uo * sb);
     dm(&f->w, n * sb);
     dm(&f->x, n * sb);
@@ -1947,6 +2084,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         hipMemsetAsync(f->done, 0, nt * 4, st);
         hipMemsetAsync(f->err, 0, 4, st);
         up(d_tab, tab.data(), tab.size() * 4);
+        if (d_inv) up(d_inv, X.inv_list.data(), X.inv_list.size() * 4);
         up(d_dst, dst.data(), nnz * 8);
         up(d_v, vals, nnz * sb);
         hipMemsetAsync(f->F, 0, (size_t)fe * sb, st);
@@ -1968,6 +2106,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         if (!tabb.empty())
             hipLaunchKernelGGL((dev::mf_inv_kernel<S>), dim3(tabb.size() / 2), dim3(256), 0, st, f->fronts, f->tabb, F,
                                static_cast<S*>(f->tinv));
+        if (d_inv)
+            hipLaunchKernelGGL((dev::mf_invform_kernel<S>), dim3(X.inv_list.size()), dim3(256), 0, st, f->fronts, d_inv, F);
         hipMemcpyAsync(hpiv.data(), d_piv, n * 4, hipMemcpyDeviceToHost, st);
         hipMemcpyAsync(&hz, d_z, 4, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess)
@@ -1975,7 +2115,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         stt.numeric_seconds = std::chrono::duration<double>(clk::now() - t1).count();
         if (std::getenv("EIGSOL_MF_DEBUG")) std::fprintf(stderr, "[mf] upload + numeric %.3f s\n", stt.numeric_seconds);
     }
-    for (void* p : {(void*)d_tab, (void*)d_piv, (void*)d_z, (void*)d_dst, (void*)d_v})
+    for (void* p : {(void*)d_tab, (void*)d_piv, (void*)d_z, (void*)d_dst, (void*)d_v, (void*)d_inv})
         if (p) hipFree(p);
     if (rc == EIGSOL_OK && hz) rc = fail(EIGSOL_E_SOLVER, "solve_shifted: multifrontal LU met a zero pivot");
     if (rc == EIGSOL_OK) {
