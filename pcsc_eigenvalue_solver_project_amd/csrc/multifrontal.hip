@@ -252,8 +252,19 @@ __device__ __forceinline__ void mf_fwd_front(const MfFront f, unsigned char* lds
         // one product over the d rows, tpr threads per row (columns interleaved), partials summed
         // in a fixed order
         const S* G = F + f.goff;
+        if (d > 128) {   // one thread per row
+            for (int i = tid; i < d; i += 256) {
+                S v = s_zero<S>();
+                const S* Gi = G + i;
+#pragma unroll 8
+                for (int j = 0; j < ns; ++j) v = add(v, mul(Gi[(int64_t)j * d], y[j]));
+                if (i < ns) w[f.c0 + i] = v;
+                else u[f.uoff + i - ns] = add(acc[i - ns], v);
+            }
+            return;
+        }
         S* part = acc + ms;
-        const int R = d <= 64 ? 64 : d <= 128 ? 128 : 256, tpr = 256 / R;
+        const int R = d <= 64 ? 64 : 128, tpr = 256 / R;
         const int i = tid % R, p = tid / R;
         S sacc = s_zero<S>();
         if (i < d) {
@@ -841,7 +852,8 @@ __global__ __launch_bounds__(256) void mf_inv_kernel(const MfFront* fr, const in
     for (int e = tid; e < 64 * 64; e += 256) out[4096 + e] = X[(e & 63) + (e >> 6) * 65];
 }
 
-// Inverse form of a one-workgroup front (after the factorization; EIGSOL_MF_INVFORM=0: off): the
+// Inverse form of a one-workgroup front with at most 64 pivots (after the factorization;
+// EIGSOL_MF_INVFORM=0: off, EIGSOL_MF_INV_D: most rows, default 256): the
 // forward solve of the front becomes one product [inv(L11); L21 inv(L11)] (P r) and the backward one
 // [inv(U11), -inv(U11) U12] [t; x(struct)], every load independent, instead of a dependent chain
 // over the pivot columns on one wave followed by the struct rows (the diagonal blocks of the large
@@ -1870,6 +1882,10 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
             }
     }
     lds_asm.assign(H + 1, 0);
+    bool inv_on = true;
+    int inv_d = 256;   // 256 / 384 / 512: 1.71 / 1.72 / 1.72 ms per 1M iteration (tools/mf_grid.sh)
+    if (const char* e = std::getenv("EIGSOL_MF_INVFORM")) inv_on = std::atoi(e) != 0;
+    if (const char* e = std::getenv("EIGSOL_MF_INV_D")) inv_d = std::max(1, std::atoi(e));
     int32_t& nflag = X.nflag;
     int64_t& zsz = X.zsz;
     for (int32_t h = 0; h <= H; ++h) {
@@ -1879,7 +1895,9 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
             q.flag0 = -1;
             q.zoff = 0;
             if (insub[lists[t]]) continue;
-            const bool is_big = big_ns > 0 && (q.ns >= big_ns || q.d >= big_d);
+            // fronts of at most 64 pivots and inv_d rows stay one-workgroup fronts (inverse form)
+            const bool inv_ok = inv_on && q.ns <= 64 && q.d <= inv_d;
+            const bool is_big = big_ns > 0 && (q.ns >= big_ns || (q.d >= big_d && !inv_ok));
             if (is_big) big.push_back(lists[t]);
             else if (wave_ok && q.ns <= dev::kWaveNs && q.ms <= dev::kWaveMs) slists.push_back(lists[t]);
             else wg.push_back(lists[t]);
@@ -1906,17 +1924,16 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
         fcnt[h] = (int64_t)tabf.size() / 2 - foff[h];
         bcnt[h] = (int64_t)tabb.size() / 2 - boff[h];
     }
-    // inverse forms of the one-workgroup fronts with at most 64 pivots and 256 rows (mf_invform_kernel;
-    // EIGSOL_MF_INVFORM=0: off), kept only while the fronts and the forms fit 0.6 of the device memory
+    // inverse forms of the one-workgroup fronts with at most 64 pivots and inv_d rows
+    // (mf_invform_kernel), kept only while the fronts and the forms fit 0.6 of the device memory
     X.inv_list.clear();
     X.gsz = 0;
     {
-        const char* e = std::getenv("EIGSOL_MF_INVFORM");
-        const bool on = !(e && std::atoi(e) == 0);
+        const bool on = inv_on;
         for (int64_t s2 = 0; s2 < nt; ++s2) {
             dev::MfFront& q = fr[s2];
             q.goff = -1;
-            if (on && q.flag0 < 0 && q.ns <= 64 && q.d <= 256) {
+            if (on && q.flag0 < 0 && q.ns <= 64 && q.d <= inv_d) {
                 q.goff = (int64_t)fe + X.gsz;
                 X.gsz += 2 * (int64_t)q.d * q.ns;
                 X.inv_list.push_back((int32_t)s2);
