@@ -1004,6 +1004,8 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
     __shared__ S part[4][64];
     __shared__ S ysh[4][16];
     __shared__ S vsh[64];
+    extern __shared__ __align__(16) unsigned char xs_raw[];
+    S* xsh = reinterpret_cast<S*>(xs_raw);   // x(struct), ms entries
     const int s = tab[2 * blockIdx.x], rb = tab[2 * blockIdx.x + 1];
     const MfFront f = fr[s];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1019,19 +1021,29 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
         for (int t = 0; t < 16; ++t) iv[t] = ti[t * 64];
     }
     S acc = s_zero<S>();
-    // U12 x(struct): 16-column chunks, wave wv every 4th (the ancestors' x: earlier launches)
-    for (int q0 = 16 * wv; q0 < ms; q0 += 64) {
-        S tv[16];
+    // U12 x(struct): x(struct) (the ancestors' x: earlier launches) gathered into LDS once, then
+    // 16-column chunks, wave wv every 4th, two chunks' tiles in flight (the gather and the tile
+    // loads used to chain one round trip per chunk: ms = 1000 took ~50 us of a 68 us launch)
+    for (int q = tid; q < ms; q += 256) xsh[q] = x[sidx[f.sof + q]];
+    __syncthreads();
+    {
         const S* tile = A + row + (int64_t)ns * d;
+        int q0 = 16 * wv;
+        for (; q0 + 64 < ms; q0 += 128) {
+            S ta[16], tb[16];
 #pragma unroll
-        for (int t = 0; t < 16; ++t) tv[t] = tile[(int64_t)min(q0 + t, ms - 1) * d];
-        if (lane < 16) ysh[wv][lane] = q0 + lane < ms ? x[sidx[f.sof + q0 + lane]] : s_zero<S>();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        mf_acc16(acc, tv, ysh[wv], q0, ms);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+            for (int t = 0; t < 16; ++t) ta[t] = tile[(int64_t)(q0 + t) * d];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) tb[t] = tile[(int64_t)min(q0 + 64 + t, ms - 1) * d];
+            mf_acc16(acc, ta, xsh + q0, q0, ms);
+            mf_acc16(acc, tb, xsh + q0 + 64, q0 + 64, ms);
+        }
+        if (q0 < ms) {
+            S ta[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) ta[t] = tile[(int64_t)min(q0 + t, ms - 1) * d];
+            mf_acc16(acc, ta, xsh + q0, q0, ms);
+        }
     }
     // later pivot blocks of this front as their flags rise (the last block first)
     for (int c = nblk - 1; c > rb; --c) {
@@ -1092,6 +1104,7 @@ struct MfFactor {
     void* x = nullptr;
     std::vector<int64_t> hstart;      // lists[hstart[h] .. hstart[h + 1])
     std::vector<int32_t> lds_fwd, lds_bwd;   // dynamic LDS bytes per height (one-workgroup fronts)
+    std::vector<int32_t> lds_bbig;           // per height: x(struct) of the large fronts (mf_big_bwd_kernel)
     // solve: per height the one-workgroup fronts (slists[sstart[h] .. + nsmall[h])), then the
     // large fronts (the next nbig[h] entries: their assembly launch); the large fronts' row-block
     // tables (front, block) for the forward / backward launches at tabf / tabb + off[h], cnt[h] pairs
@@ -2063,6 +2076,10 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     dm((void**)&f->fheight, nt * 4);
     dm((void**)&f->done, nt * 4);
     f->nsub = (int32_t)(X.sub_ranges.size() / 2);
+    f->lds_bbig.assign(H + 1, 0);
+    for (int32_t h = 0; h <= H; ++h)
+        for (int64_t t = sstart[h] + nwave[h] + nsmall[h]; t < sstart[h] + nwave[h] + nsmall[h] + nbig[h]; ++t)
+            f->lds_bbig[h] = std::max<int32_t>(f->lds_bbig[h], (int32_t)(fr[slists[t]].ms * sb));
     f->lds_sub_f = X.lds_sub_f ? X.lds_sub_f + inv_lds : 0;
     f->lds_sub_b = X.lds_sub_b ? X.lds_sub_b + inv_lds : 0;
     dm((void**)&f->sub_ranges, X.sub_ranges.size() * 4);
@@ -2168,7 +2185,10 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_sub_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_sub_kernel<S>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess)
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_big_bwd_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                *std::max_element(f->lds_bbig.begin(), f->lds_bbig.end())) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal solve LDS");
     }
     if (rc != EIGSOL_OK) {
@@ -2223,7 +2243,7 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     for (int32_t h = H; h >= (fb ? f->hflow : 0); --h) {
         const int32_t* L = f->slists + f->sstart[h];
         if (f->nbig[h])
-            hipLaunchKernelGGL((dev::mf_big_bwd_kernel<S>), dim3(f->bcnt[h]), dim3(256), 0, st, f->fronts,
+            hipLaunchKernelGGL((dev::mf_big_bwd_kernel<S>), dim3(f->bcnt[h]), dim3(256), f->lds_bbig[h], st, f->fronts,
                                f->tabb + 2 * f->boff[h], F, (const S*)f->tinv, f->sidx, (const S*)w, x, f->flags, eb,
                                f->err, f->backoff);
         const int64_t nw = f->nwave[h];
