@@ -273,6 +273,34 @@ def run_single_band10m(E, S, ctx, torch, stream):
     return out
 
 
+def run_long_double_power(E, S, ctx, torch, n=1_000_000, k=10):
+    """long double (x87 in the reference, double-double on the device, wide.hip): powerMethod's
+    fused step on a 1M band matrix with 10 entries per row.  One reference iteration is the
+    double-double pass (x = y / normY, A x, the norm / Rayleigh partials) and the host's stopping
+    test (one host wait).  Algorithmic bytes per iteration (kernel_info): (16 + 4) nnz + 4 (n + 1)
+    + 48 n (y read, x and A x written)."""
+    rp, ci, v = S.band(n, k)
+    A = E.CsrMatrix(ctx, rp, ci, v.astype(np.longdouble), (n, n))
+    del v
+    sess = E.PowerSession(A)
+    sess.begin(E.SolverOptions(2**31 - 1, -1.0), S.start_vector(n).astype(np.longdouble))
+    sess.step(3)
+    torch.cuda.synchronize()
+    iters = 30
+    t = time.perf_counter()
+    sess.step(iters)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / iters * 1e3
+    nnz = len(ci)
+    info = sess.kernel_info()
+    b = info["bytes_per_iteration"]
+    sess.close()
+    A.close()
+    return {"n": n, "nnz": nnz, "dtype": "double-double", "ms_per_iteration": round(ms, 4),
+            "GB/s": round(b / (ms / 1e3) / 1e9, 1), "roofline_frac": round(b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel": info["kernel"]}
+
+
 def run_uniform10m(E, S, ctx, torch, stream, opts):
     """Config 4's honest gather figure (SURVEY §8d "uniform also reported"): the same fused
     iteration on a 10M x 10M matrix with 10 uniform random columns per row, one GPU."""
@@ -792,6 +820,7 @@ def main():
             "config3_csr_1Mx16": run_config3(E, S, ctx, torch, torch_stream, opts),
             "config4_uniform10m": run_uniform10m(E, S, ctx, torch, torch_stream, opts),
             "band10m_float32": run_single_band10m(E, S, ctx, torch, torch_stream),
+            "long_double_band1m": run_long_double_power(E, S, ctx, torch),
             "config1_A_txt": run_config1(E, S, ctx),
             "config2_qr_4096": run_config2(E, ctx, args.no_cpu_baseline),
             "qr_complex_1024": run_qr_complex(E, ctx, args.no_cpu_baseline),

@@ -23,9 +23,11 @@
 // iteration: this is the precision path, not the headline path).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <type_traits>
 #include <vector>
 
 #include "internal.hpp"
@@ -100,6 +102,67 @@ __global__ __launch_bounds__(kT) void spmv_kernel(int64_t nrows, const int32_t* 
     if (sgn < 0) s = O::sub(O::zero(), s);
     if (b) s = O::add(b[i], s);
     y[i] = s;
+}
+
+__device__ __forceinline__ cdd shfl_cdd(cdd v, int off) { return cdd{shfl_dd(v.re, off), shfl_dd(v.im, off)}; }
+template <class T> __device__ __forceinline__ T shfl_w(T v, int off);
+template <> __device__ __forceinline__ dd shfl_w<dd>(dd v, int off) { return shfl_dd(v, off); }
+template <> __device__ __forceinline__ cdd shfl_w<cdd>(cdd v, int off) { return shfl_cdd(v, off); }
+
+// One power iteration of the CSR session in one pass (power_method.hpp:78-81): z = A x as (A y) /
+// normY (two double-double divisions per row instead of one per entry: a 1e-32-relative rounding
+// difference from A (y / normY), far inside the x87 reference's own), A y by G lanes per row
+// (entries strided over the group, a butterfly in fixed order), x = y / normY and z written by the
+// row's first lane,
+// and the block partials of {|z|^2, Re x^H z, Im x^H z} (rows in a fixed order per block; the host
+// sums the blocks in order).  Replaces scale + one-row-per-lane product + dot pass: the vectors are
+// read once and the matrix stream is coalesced across a group.
+template <class T, int G>
+__global__ __launch_bounds__(kT) void power_fused_kernel(int64_t n, const int32_t* __restrict__ rp,
+                                                         const int32_t* __restrict__ ci, const T* __restrict__ val,
+                                                         const T* __restrict__ y, dd nrm, T* __restrict__ x,
+                                                         T* __restrict__ z, dd* __restrict__ part) {
+    using O = wide_ops<T>;
+    __shared__ dd sm[3 * 16];
+    constexpr int RB = kT / G;   // rows per block tile
+    const int g = threadIdx.x % G;
+    dd acc[3] = {dd{0.0, 0.0}, dd{0.0, 0.0}, dd{0.0, 0.0}};
+    for (int64_t base = (int64_t)blockIdx.x * RB; base < n; base += (int64_t)gridDim.x * RB) {
+        const int64_t i = base + threadIdx.x / G;
+        T sum = O::zero();
+        if (i < n) {
+            const int32_t e1 = rp[i + 1];
+            for (int32_t e = rp[i] + g; e < e1; e += G) sum = O::add(sum, O::mul(val[e], y[ci[e]]));
+        }
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) sum = O::add(sum, shfl_w<T>(sum, off));
+        if (i < n && g == 0) {
+            const T xi = O::div_r(y[i], nrm);
+            sum = O::div_r(sum, nrm);
+            x[i] = xi;
+            z[i] = sum;
+            acc[0] = dd_add(acc[0], O::abs2(sum));
+            const T pr = O::mul(O::conj(xi), sum);
+            acc[1] = dd_add(acc[1], O::real(pr));
+            acc[2] = dd_add(acc[2], O::imag(pr));
+        }
+    }
+    block_sum<3>(acc, sm);
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 3; ++q) part[3 * blockIdx.x + q] = acc[q];
+}
+
+// out[q] = sum of the nb block partials part[3 b + q] (thread t: blocks t, t + kT, ... in order, then
+// the block sum in wave order): deterministic for a given nb
+__global__ __launch_bounds__(kT) void sum3_kernel(const dd* __restrict__ part, int nb, dd* __restrict__ out) {
+    __shared__ dd sm[3 * 16];
+    dd v[3] = {dd{0.0, 0.0}, dd{0.0, 0.0}, dd{0.0, 0.0}};
+    for (int b = threadIdx.x; b < nb; b += kT)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[q] = dd_add(v[q], part[3 * b + q]);
+    block_sum<3>(v, sm);
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 3; ++q) out[q] = v[q];
 }
 
 // dense, column-major m x n: part[c * m + i] = sum over the columns of chunk c of A(i, j) x_j
@@ -569,6 +632,7 @@ struct WideSession {
     double* r64 = nullptr;  // residual rounded to fp64
     double* d64 = nullptr;  // fp64 correction
     dd* part = nullptr;     // reduction partials (3 per block)
+    dd* fpart = nullptr;    // power_fused_kernel's block partials and their sum
     double* dpart = nullptr;
     dd* hpart = nullptr;       // pinned host copies of part / dpart (a pageable copy sleeps ~1 ms)
     double* hdpart = nullptr;
@@ -589,7 +653,7 @@ void wide_session_free(WideSession* s) {
     if (!s) return;
     hipSetDevice(s->ctx->device);
     hipStreamSynchronize(s->ctx->stream);
-    for (void* p : {s->x, s->y, s->z, s->r, (void*)s->r64, (void*)s->d64, (void*)s->part, (void*)s->dpart})
+    for (void* p : {s->x, s->y, s->z, s->r, (void*)s->r64, (void*)s->d64, (void*)s->part, (void*)s->dpart, (void*)s->fpart})
         if (p) hipFree(p);
     for (void* p : {(void*)s->hpart, (void*)s->hdpart})
         if (p) hipHostFree(p);
@@ -622,6 +686,43 @@ static int reduce(WideSession* s, const void* a, const void* w, dd& n2, cdd& dot
         dot.re = dd_add(dot.re, s->hpart[3 * b + 1]);
         dot.im = dd_add(dot.im, s->hpart[3 * b + 2]);
     }
+    return EIGSOL_OK;
+}
+
+// x = y / normY, z = A x, {||z||^2, x^H z}: one launch, lanes per row from the mean row length
+// (one block per kT / G rows up to kFusedBlocks, so every CU keeps many rows' dependent loads in
+// flight; the block partials are reduced on the device in a fixed order and three values come back)
+constexpr int kFusedBlocks = 16384;   // cap of EIGSOL_DD_BLOCKS (default 2048: 1024 / 2048 / 4096 blocks 0.151 / 0.142 / 0.144 ms, band 1M)
+template <class T>
+static int power_fused(WideSession* s, dd nrm, dd& n2, cdd& dot) {
+    hipStream_t st = s->ctx->stream;
+    eigsol_csr* A = s->csr;
+    const double avg = s->n ? (double)A->nnz / (double)s->n : 0.0;
+    if (!s->fpart) EIGSOL_HIP(hipMalloc(&s->fpart, (3 * (size_t)kFusedBlocks + 3) * sizeof(dd)));
+    unsigned g = 1;
+    auto go = [&](auto gtag) {
+        constexpr int G = decltype(gtag)::value;
+        static const int64_t cap = [] {
+            const char* e = std::getenv("EIGSOL_DD_BLOCKS");
+            return e ? std::max<int64_t>(1, std::min<int64_t>(kFusedBlocks, std::atoll(e))) : (int64_t)2048;
+        }();
+        g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cap, (s->n + wdev::kT / G - 1) / (wdev::kT / G)));
+        hipLaunchKernelGGL((wdev::power_fused_kernel<T, G>), dim3(g), dim3(wdev::kT), 0, st, s->n, A->rowptr, A->col,
+                           static_cast<const T*>(A->val), static_cast<const T*>(s->y), nrm, static_cast<T*>(s->x),
+                           static_cast<T*>(s->z), s->fpart);
+    };
+    if (avg <= 6.0) go(std::integral_constant<int, 4>{});
+    else if (avg <= 12.0) go(std::integral_constant<int, 8>{});
+    else if (avg <= 24.0) go(std::integral_constant<int, 16>{});
+    else go(std::integral_constant<int, 32>{});
+    EIGSOL_HIP(hipGetLastError());
+    hipLaunchKernelGGL(wdev::sum3_kernel, dim3(1), dim3(wdev::kT), 0, st, s->fpart, (int)g,
+                       s->fpart + 3 * (size_t)kFusedBlocks);
+    EIGSOL_HIP(hipGetLastError());
+    EIGSOL_HIP(hipMemcpyAsync(s->hpart, s->fpart + 3 * (size_t)kFusedBlocks, 3 * sizeof(dd), hipMemcpyDeviceToHost, st));
+    EIGSOL_HIP(stream_wait(st));
+    n2 = s->hpart[0];
+    dot = cdd{s->hpart[1], s->hpart[2]};
     return EIGSOL_OK;
 }
 
@@ -758,12 +859,17 @@ static int iterate_t(WideSession* s) {
         s->done = true;
         return EIGSOL_OK;
     }
-    hipLaunchKernelGGL((wdev::scale_kernel<T>), dim3(nblk(s->n)), dim3(wdev::kT), 0, st, s->n,
-                       static_cast<const T*>(s->y), normY, static_cast<T*>(s->x));   // x = y / normY
-    EIGSOL_TRY(apply<T>(s, s->x, s->z, nullptr, W<T>::zero(), 1));                  // A x
     dd nz;
     cdd dot;
-    EIGSOL_TRY(reduce<T>(s, s->z, s->x, nz, dot));                                    // x.dot(A x)
+    if (s->csr && !s->shifted) {
+        // x = y / normY, A x and x.dot(A x) in one pass (power_fused_kernel)
+        EIGSOL_TRY(power_fused<T>(s, normY, nz, dot));
+    } else {
+        hipLaunchKernelGGL((wdev::scale_kernel<T>), dim3(nblk(s->n)), dim3(wdev::kT), 0, st, s->n,
+                           static_cast<const T*>(s->y), normY, static_cast<T*>(s->x));   // x = y / normY
+        EIGSOL_TRY(apply<T>(s, s->x, s->z, nullptr, W<T>::zero(), 1));                  // A x
+        EIGSOL_TRY(reduce<T>(s, s->z, s->x, nz, dot));                                    // x.dot(A x)
+    }
     const cdd lam = W<T>::complex ? dot : cdd{dot.re, dd{0.0, 0.0}};
     if ((int32_t)s->trace.size() < s->trace_cap) s->trace.push_back(lam);
     s->iters = s->k + 1;
@@ -836,7 +942,7 @@ void wide_info(const WideSession* s, double* bytes, int32_t* variant, int32_t* t
         if (variant) *variant = 17;
         if (tiles) *tiles = s->refine_steps;
     } else if (s->csr) {
-        if (bytes) *bytes = (sb + 4.0) * (double)s->csr->nnz + 4.0 * (n + 1.0) + 2.0 * sb * n;
+        if (bytes) *bytes = (sb + 4.0) * (double)s->csr->nnz + 4.0 * (n + 1.0) + 3.0 * sb * n;   // y read, x and z written
         if (variant) *variant = 15;
         if (tiles) *tiles = 0;
     } else {
