@@ -256,8 +256,9 @@ __device__ __forceinline__ void mf_fwd_front(const MfFront f, unsigned char* lds
             for (int i = tid; i < d; i += 256) {
                 S v = s_zero<S>();
                 const S* Gi = G + i;
+                const int jn = i < ns ? i + 1 : ns;   // inv(L11) is lower triangular: skip its zeros
 #pragma unroll 8
-                for (int j = 0; j < ns; ++j) v = add(v, mul(Gi[(int64_t)j * d], y[j]));
+                for (int j = 0; j < jn; ++j) v = add(v, mul(Gi[(int64_t)j * d], y[j]));
                 if (i < ns) w[f.c0 + i] = v;
                 else u[f.uoff + i - ns] = add(acc[i - ns], v);
             }
@@ -269,8 +270,9 @@ __device__ __forceinline__ void mf_fwd_front(const MfFront f, unsigned char* lds
         S sacc = s_zero<S>();
         if (i < d) {
             const S* Gi = G + i;
+            const int jn = i < ns ? i + 1 : ns;   // inv(L11) is lower triangular: skip its zeros
 #pragma unroll 8
-            for (int j = p; j < ns; j += tpr) sacc = add(sacc, mul(Gi[(int64_t)j * d], y[j]));
+            for (int j = p; j < jn; j += tpr) sacc = add(sacc, mul(Gi[(int64_t)j * d], y[j]));
         }
         part[p * R + i] = sacc;
         __syncthreads();
@@ -366,8 +368,10 @@ __device__ __forceinline__ void mf_bwd_front(const MfFront f, unsigned char* lds
         S sacc = s_zero<S>();
         if (k < ns) {
             const S* Gk = G + k;
+            // inv(U11) is upper triangular: columns from k on (the first of them congruent to p mod 4)
+            const int c0 = k > p ? p + ((k - p + 3) / 4) * 4 : p;
 #pragma unroll 8
-            for (int c = p; c < d; c += 4) sacc = add(sacc, mul(Gk[(int64_t)c * ns], c < ns ? t[c] : xs[c - ns]));
+            for (int c = c0; c < d; c += 4) sacc = add(sacc, mul(Gk[(int64_t)c * ns], c < ns ? t[c] : xs[c - ns]));
         }
         part[p * 64 + k] = sacc;
         __syncthreads();
