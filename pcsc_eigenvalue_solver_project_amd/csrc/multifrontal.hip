@@ -85,6 +85,33 @@ __device__ __forceinline__ void mf_st(cplx* p, cplx v) {
 __device__ __forceinline__ double mf_ld(const double* p) { return ld_agent(p); }
 __device__ __forceinline__ cplx mf_ld(const cplx* p) { return cplx{ld_agent(&p->re), ld_agent(&p->im)}; }
 
+// value flags of the row-block solve (EIGSOL_MF_VALFLAG): an unsolved pivot value holds this NaN in
+// every 8-byte word, a solved one never does (a NaN result is stored as the default quiet NaN), so a
+// waiting block polls the values themselves instead of a flag and then the values
+constexpr unsigned long long kMfSent = 0x7FF4DEAD7FF4DEADull;
+__device__ __forceinline__ bool mf_unready(double v) { return (unsigned long long)__double_as_longlong(v) == kMfSent; }
+__device__ __forceinline__ bool mf_unready(cplx v) { return mf_unready(v.re) || mf_unready(v.im); }
+__device__ __forceinline__ double mf_sent(double) { return __longlong_as_double((long long)kMfSent); }
+__device__ __forceinline__ cplx mf_sent(cplx) { return cplx{mf_sent(0.0), mf_sent(0.0)}; }
+__device__ __forceinline__ double mf_clean(double v) { return v != v ? __longlong_as_double(0x7FF8000000000000ll) : v; }
+__device__ __forceinline__ cplx mf_clean(cplx v) { return cplx{mf_clean(v.re), mf_clean(v.im)}; }
+template <class S>
+__device__ __forceinline__ S mf_poll(const S* p, int32_t* err, int bo) {
+    S v = mf_ld(p);
+    int spins = 0;
+    while (mf_unready(v)) {
+        if (!(bo & 1)) __builtin_amdgcn_s_sleep(1);
+        else if (spins < 4) __builtin_amdgcn_s_sleep(2);
+        else __builtin_amdgcn_s_sleep(8);
+        v = mf_ld(p);
+        if (++spins > (1 << 22)) {
+            atomicOr(err, 4);
+            break;
+        }
+    }
+    return v;
+}
+
 // M's entries into their fronts: F[dst[e]] = v[e] (every destination distinct)
 template <class S>
 __global__ __launch_bounds__(256) void mf_scatter_kernel(const int64_t* dst, const S* v, int64_t nnz, S* F) {
@@ -782,8 +809,8 @@ __device__ __forceinline__ void mf_wait(const int32_t* f, int32_t epoch, int32_t
 // contributions to the struct rows; one workgroup per front.  LDS: r (ns)
 template <class S>
 __global__ __launch_bounds__(256) void mf_big_asm_kernel(const MfFront* fr, const int32_t* list, const int32_t* chl,
-                                                         const int32_t* cmap, const int32_t* pinv, const S* w,
-                                                         const S* u, S* z) {
+                                                         const int32_t* cmap, const int32_t* pinv, S* w,
+                                                         const S* u, S* z, int bo) {
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const MfFront f = fr[list[blockIdx.x]];
     const int tid = threadIdx.x, ns = f.ns, ms = f.ms;
@@ -805,6 +832,10 @@ __global__ __launch_bounds__(256) void mf_big_asm_kernel(const MfFront* fr, cons
         __syncthreads();
     }
     for (int t = tid; t < ns; t += 256) zs[t] = r[pinv[f.c0 + t]];
+    // value flags: the pivot rows' w (read above, before the barrier) becomes "unsolved" for
+    // mf_big_fwd_kernel, the next launch
+    if (bo & 4)
+        for (int t = tid; t < ns; t += 256) mf_st(w + f.c0 + t, mf_sent(s_zero<S>()));
 }
 
 template <class S>
@@ -938,7 +969,7 @@ __device__ __forceinline__ void mf_acc16(S& acc, const S (&tv)[16], const S* yv,
 template <class S>
 __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, const int32_t* tab, const S* F,
                                                          const S* Tinv, const S* z, S* w, S* u, int32_t* flag,
-                                                         int32_t epoch, int32_t* err, int bo) {
+                                                         int32_t epoch, int32_t* err, int bo, S* x) {
     __shared__ S part[4][64];
     __shared__ S ysh[4][16];
     __shared__ S vsh[64];
@@ -966,10 +997,14 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
         const S* tile = A + row;
 #pragma unroll
         for (int t = 0; t < 16; ++t) tv[t] = tile[(int64_t)min(c0 + t, ns - 1) * d];
-        if (lane == 0) mf_wait(flag + f.flag0 + c, epoch, err, bo);
-        __builtin_amdgcn_wave_barrier();
-        if (!(bo & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_ld(w + f.c0 + c0 + lane) : s_zero<S>();
+        if (bo & 4) {
+            if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_poll(w + f.c0 + c0 + lane, err, bo) : s_zero<S>();
+        } else {
+            if (lane == 0) mf_wait(flag + f.flag0 + c, epoch, err, bo);
+            __builtin_amdgcn_wave_barrier();
+            if (!(bo & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_ld(w + f.c0 + c0 + lane) : s_zero<S>();
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -994,6 +1029,14 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
     __syncthreads();
     if (wv != 0) return;
     const S y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+    if (bo & 4) {
+        // publish (the value is its own flag); x of these rows becomes "unsolved" for the backward pass
+        if (lane < rn) {
+            mf_st(w + f.c0 + r0 + lane, mf_clean(y));
+            mf_st(x + f.c0 + r0 + lane, mf_sent(y));
+        }
+        return;
+    }
     if (lane < rn) mf_st(w + f.c0 + r0 + lane, y);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -1056,10 +1099,14 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
         const S* tile = A + row;
 #pragma unroll
         for (int t = 0; t < 16; ++t) tv[t] = tile[(int64_t)min(c0 + t, ns - 1) * d];
-        if (lane == 0) mf_wait(flag + f.flag0 + c, epoch, err, bo);
-        __builtin_amdgcn_wave_barrier();
-        if (!(bo & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_ld(x + f.c0 + c0 + lane) : s_zero<S>();
+        if (bo & 4) {
+            if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_poll(x + f.c0 + c0 + lane, err, bo) : s_zero<S>();
+        } else {
+            if (lane == 0) mf_wait(flag + f.flag0 + c, epoch, err, bo);
+            __builtin_amdgcn_wave_barrier();
+            if (!(bo & 2)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_ld(x + f.c0 + c0 + lane) : s_zero<S>();
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1081,6 +1128,10 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
     __syncthreads();
     if (wv != 0) return;
     const S xv = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+    if (bo & 4) {
+        if (lane < rn) mf_st(x + f.c0 + r0 + lane, mf_clean(xv));
+        return;
+    }
     if (lane < rn) mf_st(x + f.c0 + r0 + lane, xv);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -2036,7 +2087,12 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     f->boff = boff;
     f->bcnt = bcnt;
     f->lds_asm = lds_asm;
-    if (const char* e = std::getenv("EIGSOL_MF_BACKOFF")) f->backoff = std::atoi(e);
+    if (const char* e = std::getenv("EIGSOL_MF_BACKOFF")) f->backoff = std::atoi(e) & 3;
+    // value flags (bit 4; EIGSOL_MF_VALFLAG=0: epoch flags): 1M convection-diffusion 1.657 -> 1.567 ms
+    {
+        const char* e = std::getenv("EIGSOL_MF_VALFLAG");
+        if (!(e && std::atoi(e) == 0)) f->backoff |= 4;
+    }
     f->lds_fwd.assign(H + 1, 0);
     f->lds_bwd.assign(H + 1, 0);
     // the inverse-form branch keeps 256 partial sums after the front's vectors
@@ -2238,10 +2294,10 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
                                L + nw, f->chl, F, f->cmap, f->pinv, w, u);
         if (f->nbig[h]) {
             hipLaunchKernelGGL((dev::mf_big_asm_kernel<S>), dim3(f->nbig[h]), dim3(256), f->lds_asm[h], st, f->fronts,
-                               L + nw + f->nsmall[h], f->chl, f->cmap, f->pinv, (const S*)w, (const S*)u, z);
+                               L + nw + f->nsmall[h], f->chl, f->cmap, f->pinv, w, (const S*)u, z, f->backoff);
             hipLaunchKernelGGL((dev::mf_big_fwd_kernel<S>), dim3(f->fcnt[h]), dim3(256), 0, st, f->fronts,
                                f->tabf + 2 * f->foff[h], F, (const S*)f->tinv, (const S*)z, w, u, f->flags, ef, f->err,
-                               f->backoff);
+                               f->backoff, x);
         }
     }
     for (int32_t h = H; h >= (fb ? f->hflow : 0); --h) {

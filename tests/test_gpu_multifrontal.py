@@ -226,21 +226,27 @@ def test_multifrontal_singular_falls_back_or_fails(ctx, env):
     A.close()
 
 
-@pytest.mark.parametrize("big,wave,flow,sub", [("1", "0", "0", "0"), ("0", "0", "0", "0"), ("64", "0", "0", "0"),
-                                               ("0", "1", "0", "0"), ("96", "1", "0", "0"), ("0", "0", "1", "0"),
-                                               ("64", "0", "1", "0"), ("96", "0", "0", "512"), ("1", "0", "0", "200"),
-                                               ("0", "0", "0", "100000")])
-def test_multifrontal_block_row_solve_kernels(ctx, env, big, wave, flow, sub):
-    """Fronts solved by one workgroup per 64-row block (sync-free, flags; EIGSOL_MF_BIG_NS=1: every
-    front), by one workgroup each (=0), split at 64 / 96 pivots, and the small fronts by one wave
-    each (EIGSOL_MF_WAVE=1), the lower heights in one dataflow launch each way (EIGSOL_MF_FLOW=1),
-    small subtrees whole on one workgroup (EIGSOL_MF_SUB pivots; 100000: the whole tree): the same
-    solution within the residual bound, bitwise repeatable for each split."""
+@pytest.mark.parametrize("big,wave,flow,sub,inv,vf", [
+    ("1", "0", "0", "0", "1", "1"), ("1", "0", "0", "0", "1", "0"), ("0", "0", "0", "0", "1", "1"),
+    ("0", "0", "0", "0", "0", "1"), ("64", "0", "0", "0", "1", "1"), ("64", "0", "0", "0", "0", "0"),
+    ("0", "1", "0", "0", "1", "1"), ("96", "1", "0", "0", "1", "1"), ("0", "0", "1", "0", "1", "1"),
+    ("64", "0", "1", "0", "1", "0"), ("96", "0", "0", "512", "1", "1"), ("1", "0", "0", "200", "0", "1"),
+    ("0", "0", "0", "100000", "1", "1")])
+def test_multifrontal_block_row_solve_kernels(ctx, env, big, wave, flow, sub, inv, vf):
+    """Fronts solved by one workgroup per 64-row block (sync-free; EIGSOL_MF_BIG_NS=1: every front;
+    the pivot values polled as their own flags, EIGSOL_MF_VALFLAG=1, or epoch flags, =0), by one
+    workgroup each (=0), split at 64 / 96 pivots, and the small fronts by one wave each
+    (EIGSOL_MF_WAVE=1), the lower heights in one dataflow launch each way (EIGSOL_MF_FLOW=1), small
+    subtrees whole on one workgroup (EIGSOL_MF_SUB pivots; 100000: the whole tree), with or without
+    the inverse forms (EIGSOL_MF_INVFORM): the same solution within the residual bound, bitwise
+    repeatable for each split."""
     _mf_env(env)
     env("EIGSOL_MF_BIG_NS", big)
     env("EIGSOL_MF_WAVE", wave)
     env("EIGSOL_MF_FLOW", flow)
     env("EIGSOL_MF_SUB", sub)
+    env("EIGSOL_MF_INVFORM", inv)
+    env("EIGSOL_MF_VALFLAG", vf)
     env("EIGSOL_MF_LEAF", "24")
     rp, ci, v = S.convdiff_complex(45, seed=12)
     n = 45 * 45
