@@ -258,22 +258,60 @@ __device__ __forceinline__ void mf_fwd_front(const MfFront f, unsigned char* lds
     S* r = reinterpret_cast<S*>(lds_raw);
     S* y = r + ns;
     S* acc = y + ns;
+    // up to KC children: every child's header, its first 256 (position, value) pairs and this
+    // thread's pivot index are loaded before anything waits on them (one chain of dependent loads
+    // instead of one per child); the contributions are then applied child by child in the fixed
+    // order, as before
+    constexpr int KC = 4;
+    const int nch = f.ch1 - f.ch0;
+    const bool pre = nch <= KC;
+    int cms[KC], cpos[KC];
+    const int32_t* cmp[KC];
+    const S* cup[KC];
+    S cval[KC];
+    if (pre) {
+#pragma unroll
+        for (int q = 0; q < KC; ++q)
+            if (q < nch) {
+                const MfFront c = fr[chl[f.ch0 + q]];
+                cms[q] = c.ms;
+                cmp[q] = cmap + c.sof;
+                cup[q] = u + c.uoff;
+            }
+#pragma unroll
+        for (int q = 0; q < KC; ++q)
+            if (q < nch && tid < cms[q]) {
+                cpos[q] = cmp[q][tid];
+                cval[q] = cup[q][tid];
+            }
+    }
+    const int pv = tid < ns ? pinv[f.c0 + tid] : 0;
     for (int t = tid; t < ns; t += 256) r[t] = w[f.c0 + t];
     for (int t = tid; t < ms; t += 256) acc[t] = s_zero<S>();
     __syncthreads();
-    for (int k = f.ch0; k < f.ch1; ++k) {
-        const MfFront c = fr[chl[k]];
-        const int32_t* map = cmap + c.sof;
-        const S* uc = u + c.uoff;
-        for (int t = tid; t < c.ms; t += 256) {
-            const int pos = map[t];
-            const S v = uc[t];
-            if (pos < ns) r[pos] = sub(r[pos], v);
-            else acc[pos - ns] = add(acc[pos - ns], v);
+    auto apply = [&](int pos, S v) {
+        if (pos < ns) r[pos] = sub(r[pos], v);
+        else acc[pos - ns] = add(acc[pos - ns], v);
+    };
+    if (pre) {
+#pragma unroll
+        for (int q = 0; q < KC; ++q)
+            if (q < nch) {
+                if (tid < cms[q]) apply(cpos[q], cval[q]);
+                for (int t = tid + 256; t < cms[q]; t += 256) apply(cmp[q][t], cup[q][t]);
+                __syncthreads();
+            }
+    } else {
+        for (int k = f.ch0; k < f.ch1; ++k) {
+            const MfFront c = fr[chl[k]];
+            const int32_t* map = cmap + c.sof;
+            const S* uc = u + c.uoff;
+            for (int t = tid; t < c.ms; t += 256) apply(map[t], uc[t]);
+            __syncthreads();
         }
-        __syncthreads();
     }
-    for (int t = tid; t < ns; t += 256) y[t] = r[pinv[f.c0 + t]];
+    if (tid < ns) y[tid] = r[pv];
+    for (int t = tid + 256; t < ns; t += 256) y[t] = r[pinv[f.c0 + t]];
     __syncthreads();
     if (f.goff >= 0) {
         // one product over the d rows, tpr threads per row (columns interleaved), partials summed
@@ -384,10 +422,12 @@ __device__ __forceinline__ void mf_bwd_front(const MfFront f, unsigned char* lds
     const int d = f.d, ns = f.ns, ms = f.ms;
     S* t = reinterpret_cast<S*>(lds_raw);
     S* xs = t + ns;
+    const S w0 = tid < ns ? w[f.c0 + tid] : s_zero<S>();   // issued before the struct gather waits
     for (int q = tid; q < ms; q += 256) xs[q] = x[sidx[f.sof + q]];
     if (f.goff >= 0) {
         // x(pivots) = [inv(U11), -inv(U11) U12] [w(pivots); x(struct)]: wave p takes columns p, p + 4, ...
-        for (int q = tid; q < ns; q += 256) t[q] = w[f.c0 + q];
+        if (tid < ns) t[tid] = w0;
+        for (int q = tid + 256; q < ns; q += 256) t[q] = w[f.c0 + q];
         __syncthreads();
         const S* G = F + f.goff + (int64_t)d * ns;
         S* part = xs + ms;
