@@ -738,7 +738,10 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
         hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, x, n, 1, x, n, g->part);
         hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev + 4);
         EIGSOL_HIP(hipMemcpyAsync(g->hpin, g->hdev, 6 * sizeof(double), hipMemcpyDeviceToHost, st));
+        int32_t* mf_err = reinterpret_cast<int32_t*>(g->hpin + 6);   // the multifrontal solve's wait-error word
+        if (g->mf) EIGSOL_HIP(hipMemcpyAsync(mf_err, mf_err_word(g->mf), sizeof(int32_t), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(stream_wait(st));
+        if (g->mf && *mf_err) return fail(EIGSOL_E_HIP, "solve_shifted: a multifrontal solve wait did not complete");
         beta = std::sqrt(g->hpin[0]);
         direct_done = true;
     } else {

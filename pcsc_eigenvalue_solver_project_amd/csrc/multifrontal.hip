@@ -2372,6 +2372,8 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     return EIGSOL_OK;
 }
 
+const int32_t* mf_err_word(const MfFactor* f) { return f->err; }
+
 MfHost* mf_host_new() { return new MfHost(); }
 const MfStats& mf_host_stats(const MfHost* X) { return X->stt; }
 void mf_host_free(MfHost* X) { delete X; }

@@ -38,6 +38,8 @@ int mf_create(eigsol_ctx* ctx, int dtype, MfHost* X, const void* v, MfFactor** o
 // x = M^-1 b (device vectors, the caller's numbering), stream-ordered on ctx's stream
 int mf_solve(MfFactor* f, const void* b, void* x);
 void mf_free(MfFactor* f);
+// device word a solve's flag / value waits set when one gives up (bounded spin): non-zero = broken solve
+const int32_t* mf_err_word(const MfFactor* f);
 const MfStats& mf_stats(const MfFactor* f);
 
 }  // namespace eigsol
