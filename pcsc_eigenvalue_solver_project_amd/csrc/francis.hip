@@ -1034,9 +1034,13 @@ int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double*
         const int v = e ? std::atoi(e) : 0;
         return (v == 32 || v == 64) ? v : 0;
     }();
-    static const int kNibble = [] {   // % of the AED window deflated that skips the sweep (LAPACK's NIBBLE)
+    // % of the AED window deflated that skips the sweep (LAPACK's NIBBLE).  Round 5, after the
+    // concurrent shifts (tools/qr_nibble_r5.sh, 4096^2, seeds 42 / 7 / 20251226): 30 / 25 / 20 / 15 / 10
+    // -> 0.941 / 0.920 / 0.904 / 0.889 / 0.911 s (seed 42), 0.931 / 0.895 / 0.909 / 0.889 / 0.900,
+    // 0.927 / 0.913 / 0.904 / 0.884 / 0.919: 15
+    static const int kNibble = [] {
         const char* e = std::getenv("EIGSOL_QR_NIBBLE");
-        return e ? std::max(1, std::atoi(e)) : 30;
+        return e ? std::max(1, std::atoi(e)) : 15;
     }();
     int st_sweeps = 0, st_windows = 0, st_small = 0, st_small_rows = 0, st_aed = 0, st_aed_defl = 0, st_conc = 0;
     // concurrent shifts (EIGSOL_QR_CONC): 0 off (the shift QR after the AED, one wave), 1 when the AED
