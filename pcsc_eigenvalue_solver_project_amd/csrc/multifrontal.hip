@@ -1356,6 +1356,13 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
     }
     std::vector<int64_t> inset(n, -1), seen(n, -1);
     std::vector<int32_t> level(n, 0);
+    // pseudo-peripheral restarts per piece (EIGSOL_MF_PP_ROUNDS).  1M convection-diffusion: 2 / 1 / 0
+    // rounds -> 1.374e8 / 1.368e8 / 1.47e8 factor entries, 1.13e11 / 1.12e11 / 1.83e11 flops; on the box
+    // the set-up is the same for 1 and 2 (0.63-0.67 s) and the solve 1.55 against 1.57 ms: 2 stays
+    static const int pp_rounds = [] {
+        const char* e = std::getenv("EIGSOL_MF_PP_ROUNDS");
+        return e ? std::max(0, std::atoi(e)) : 2;
+    }();
     std::atomic<int64_t> stamp{0}, bstamp{0};
     std::mutex mu;
     std::condition_variable cv;
@@ -1488,7 +1495,7 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
             // level while the eccentricity grows
             int32_t root = t.nodes[0];
             int32_t ecc = bfs(root, tag);
-            for (int round = 0; round < 2; ++round) {
+            for (int round = 0; round < pp_rounds; ++round) {
                 int32_t best = -1, bd = INT32_MAX;
                 for (size_t h = q.size(); h-- > 0;) {
                     const int32_t v = q[h];
