@@ -1030,6 +1030,9 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
         for (int t = 0; t < 16; ++t) iv[t] = ti[t * 64];
     }
     S acc = s_zero<S>();
+    // the assembled right-hand side of these rows, loaded before the chain of waits (it was a
+    // dependent round trip after the last one, on every hand-off's critical path)
+    const S zr = lane < rn ? z[f.zoff + r0 + lane] : s_zero<S>();
     const int cend = piv ? rb : nblk;
     for (int c = 0; c < cend; ++c) {
         const int c0 = 64 * c + 16 * wv;
@@ -1055,7 +1058,6 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
     part[wv][lane] = acc;
     __syncthreads();
     const S sum = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
-    const S zr = lane < rn ? z[f.zoff + r0 + lane] : s_zero<S>();
     if (!piv) {
         if (wv == 0 && lane < rn) u[f.uoff + (r0 - ns) + lane] = add(zr, sum);
         return;
@@ -1108,6 +1110,7 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
         for (int t = 0; t < 16; ++t) iv[t] = ti[t * 64];
     }
     S acc = s_zero<S>();
+    const S wr = lane < rn ? w[f.c0 + r0 + lane] : s_zero<S>();   // loaded before the waits (see forward)
     // U12 x(struct): x(struct) (the ancestors' x: earlier launches) gathered into LDS once, then
     // 16-column chunks, wave wv every 4th, two chunks' tiles in flight (the gather and the tile
     // loads used to chain one round trip per chunk: ms = 1000 took ~50 us of a 68 us launch)
@@ -1158,7 +1161,7 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
     __syncthreads();
     if (wv == 0) {
         const S sum = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
-        vsh[lane] = lane < rn ? sub(w[f.c0 + r0 + lane], sum) : s_zero<S>();
+        vsh[lane] = lane < rn ? sub(wr, sum) : s_zero<S>();
     }
     __syncthreads();
     S p = s_zero<S>();
