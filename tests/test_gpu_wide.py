@@ -369,3 +369,36 @@ def test_wide_qr_eigenvalues_reference_iteration(ctx):
     st = E.lib().eigsol_qr_eigenvalues_dense(ctx.handle, 4, 3, aw.ctypes.data_as(C.c_void_p), C.byref(o), 0,
                                              eig.ctypes.data_as(C.c_void_p), None, C.byref(it), C.byref(cv))
     assert st == 12   # EIGSOL_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("k", [3, 20, 40])
+def test_wide_power_fused_group_widths(ctx, k):
+    """The one-pass double-double power iteration (power_fused_kernel) picks 4 / 16 / 32 lanes per row
+    from the mean row length: uniform matrices of 3, 20 and 40 entries per row, with 50 empty rows
+    and one 3000-entry row, against the x87 oracle (lambda within 1e-17 (1 + |lambda|), equal
+    iteration counts, the same eigenvector)."""
+    n = 20000
+    rp, ci, v = S.uniform(n, k, seed=k)
+    M = sp.csr_matrix((np.abs(v), ci, rp), shape=(n, n)).tolil()
+    rng = np.random.default_rng(k)
+    for r in rng.choice(n, 50, replace=False):
+        M.rows[r] = []
+        M.data[r] = []
+    long_cols = np.sort(rng.choice(n, 3000, replace=False))
+    M.rows[7] = list(long_cols)
+    M.data[7] = list(rng.uniform(0.1, 1.0, 3000))
+    M = M.tocsr()
+    M.sort_indices()
+    rp, ci = M.indptr.astype(np.int64), M.indices.astype(np.int64)
+    vals = _wide(M.data, LD)
+    A = E.CsrMatrix(ctx, rp, ci, vals, (n, n))
+    x0 = _wide(S.start_vector(n), LD, seed=9)
+    tol = 1e-12
+    res = E.power_method(A, E.SolverOptions(500, tol), x0)
+    cp, ri, vv = O.csr_to_csc(rp, ci, vals, n)
+    ref = O.power_csc(cp, ri, vv, x0, 500, tol)
+    assert res.converged and ref["converged"] and res.iterations == ref["iterations"]
+    lr = ref["eigenvalue"]
+    assert abs(res.eigenvalue - lr) <= 1e-17 * (1 + abs(lr)), (res.eigenvalue, lr)
+    assert abs(abs(_cdot(res.eigenvector, ref["eigenvector"])) - 1) <= 1e-17
+    A.close()
