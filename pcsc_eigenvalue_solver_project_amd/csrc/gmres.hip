@@ -168,6 +168,40 @@ __device__ __forceinline__ S from_re_im(double re, double im) {
     else return S{re, im};
 }
 
+// The checked direct solve's epilogue in one pass: r = b / bdiv - M x with M x = t (M uploaded) or
+// t - sigma x (t = A x on the caller's matrix), and the block partials of ||r||^2 and ||x||^2 in
+// gm_dots_kernel's layout for k = 2 (the same chunks and per-thread order: the sums are bitwise
+// those of the separate shift / residual / two dot passes it replaces)
+template <class S>
+__global__ __launch_bounds__(kThreads) void gm_resid_norms_kernel(const S* b, double bdiv, const S* t, const S* x,
+                                                                  double sre, double sim, int shift, S* r, int64_t n,
+                                                                  double* part) {
+    __shared__ double sm[3 * kWaves];
+    const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = std::min<int64_t>(n, i0 + chunk);
+    const S sig = from_re_im<S>(sre, sim);
+    double rr = 0.0, ri = 0.0, xr = 0.0, xi = 0.0, dummy = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kThreads) {
+        const S xv = x[i];
+        const S mx = shift ? sub(t[i], mul(sig, xv)) : t[i];
+        const S rv = sub(scale_in(b[i], bdiv), mx);
+        r[i] = rv;
+        acc_dot(rr, ri, rv, rv);
+        acc_dot(xr, xi, xv, xv);
+    }
+    block_sum3(rr, ri, dummy, sm);
+    if (threadIdx.x == 0) {
+        part[((int64_t)blockIdx.x * 2) * 2] = rr;
+        part[((int64_t)blockIdx.x * 2) * 2 + 1] = ri;
+    }
+    dummy = 0.0;
+    block_sum3(xr, xi, dummy, sm);
+    if (threadIdx.x == 0) {
+        part[((int64_t)blockIdx.x * 2 + 1) * 2] = xr;
+        part[((int64_t)blockIdx.x * 2 + 1) * 2 + 1] = xi;
+    }
+}
+
 // mode 0: w -= V(:, 0:k) h;  mode 1: w = V(:, 0:k) h   (h: k (re, im) pairs on the device)
 template <class S>
 __global__ __launch_bounds__(kThreads) void gm_combine_kernel(const S* V, int64_t ldv, int k, const double* h, S* w,
@@ -731,12 +765,11 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
         hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
         hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev);
         EIGSOL_TRY(precond(w, x));
-        EIGSOL_TRY(apply_M<S>(g, x, t1));
-        hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, t1, w, n);
-        hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
-        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev + 2);
-        hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, x, n, 1, x, n, g->part);
-        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev + 4);
+        // t1 = M x (or A x), then r, ||r||^2 and ||x||^2 in one pass and one reduction launch
+        EIGSOL_TRY(eigsol_csr_spmv(g->M ? g->M : g->A, x, t1));
+        hipLaunchKernelGGL((dev::gm_resid_norms_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, b, bdiv, t1, x,
+                           g->sre, g->sim, g->M ? 0 : 1, w, n, g->part);
+        hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(2), dim3(dev::kThreads), 0, st, g->part, g->G, 2, g->hdev + 2);
         EIGSOL_HIP(hipMemcpyAsync(g->hpin, g->hdev, 6 * sizeof(double), hipMemcpyDeviceToHost, st));
         int32_t* mf_err = reinterpret_cast<int32_t*>(g->hpin + 6);   // the multifrontal solve's wait-error word
         if (g->mf) EIGSOL_HIP(hipMemcpyAsync(mf_err, mf_err_word(g->mf), sizeof(int32_t), hipMemcpyDeviceToHost, st));
