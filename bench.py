@@ -58,7 +58,27 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-extras", action="store_true",
                    help="skip configs 2 (QR 4096^2), 3 (1M x 16 CSR) and 5 (shifted inverse, 1M complex)")
+    p.add_argument("--check", action="store_true",
+                   help="after the timed region, run the power method to convergence (tol 1e-12, at most 300 "
+                        "iterations) on the same sharded matrix and report lambda / iterations in the line")
+    p.add_argument("--bootstrap", default="auto", choices=["auto", "rccl", "host"],
+                   help="N > 1: the library's communicator. rccl: an RCCL communicator (one GPU per rank); "
+                        "host: set-up over torch.distributed (gloo), per-iteration exchange device to device. "
+                        "auto: rccl unless ranks share a GPU (RCCL refuses duplicate devices)")
     return p.parse_args()
+
+
+def device_map(world, local_world=None):
+    """GPU of each local rank: EIGSOL_BENCH_DEVICES="0,0,1,1" when set (rehearsing N ranks on fewer
+    GPUs), else local rank r on GPU r.  torch.cuda.device_count() does not initialise the GPU."""
+    spec = os.environ.get("EIGSOL_BENCH_DEVICES")
+    n = local_world or world
+    if spec:
+        devs = [int(t) for t in spec.split(",") if t.strip()]
+        if len(devs) < n:
+            raise SystemExit(f"EIGSOL_BENCH_DEVICES names {len(devs)} devices for {n} local ranks")
+        return devs[:n]
+    return list(range(n))
 
 
 def gen(kind, n_global, k, row0, nrows):
@@ -674,7 +694,15 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
+    devs = device_map(world, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    device = devs[local_rank]
+    shared = len(set(devs)) < len(devs)
+    bootstrap = args.bootstrap
+    if bootstrap == "auto":
+        bootstrap = "host" if shared else "rccl"
+    if world > 1 and shared and bootstrap == "rccl":
+        raise SystemExit("--bootstrap rccl with ranks sharing a GPU: RCCL refuses duplicate devices")
+    torch.cuda.set_device(device)
 
     import pcsc_eigenvalue_solver_project_amd as E
     from pcsc_eigenvalue_solver_project_amd import synthetic as S
@@ -692,13 +720,17 @@ def main():
     torch.cuda.set_stream(torch_stream)
     rp, ci, v = gen(kind, n_global, k, row0, rows)
     if world > 1:
-        # one communicator per rank owned by the library (RCCL over xGMI); gloo only ships the id
         from pcsc_eigenvalue_solver_project_amd import dist as D
-        ctx = D.torch_dist_context(local_rank, stream=torch_stream.cuda_stream)
+        if bootstrap == "rccl":
+            # one communicator per rank owned by the library (RCCL over xGMI); gloo only ships the id
+            ctx = D.torch_dist_context(device, stream=torch_stream.cuda_stream)
+        else:
+            # set-up all-gathers over gloo; the exchange itself is the same device-side peer push
+            ctx = D.torch_host_context(device, stream=torch_stream.cuda_stream)
         A = D.DistCsrMatrix(ctx, rb, rp, ci, v)
         sess = E.PowerSession(A)
     else:
-        ctx = E.Context(local_rank, stream=torch_stream.cuda_stream)
+        ctx = E.Context(device, stream=torch_stream.cuda_stream)
         A = E.CsrMatrix(ctx, rp, ci, v, (rows, rows))
         sess = E.PowerSession(A)
     nnz = len(ci)
@@ -739,6 +771,25 @@ def main():
     if world > 1:
         transports = [None] * world
         dist.all_gather_object(transports, transport_names[transport])
+    check = None
+    if args.check:
+        # untimed: the same session run to convergence (every rank takes part: the exchange is per
+        # iteration); lambda of every rank gathered so the line shows they are bitwise identical
+        sess.begin(E.SolverOptions(300, 1e-12), x0)
+        done = False
+        while not done:
+            sess.step(16)
+            done = sess.query()[0]
+        res = sess.finish()
+        mine = [float(res.eigenvalue), int(res.iterations), bool(res.converged)]
+        per_rank = [mine]
+        if world > 1:
+            per_rank = [None] * world
+            dist.all_gather_object(per_rank, mine)
+        check = {"eigenvalue": per_rank[0][0], "iterations": per_rank[0][1], "converged": per_rank[0][2],
+                 "tolerance": 1e-12, "max_iterations": 300,
+                 "ranks_bitwise_equal": all(p == per_rank[0] for p in per_rank),
+                 "eigenvector_norm2_rank0": float(np.linalg.norm(res.eigenvector))}
 
     bytes_iter = info["bytes_per_iteration"]          # this rank's algorithmic bytes
     total_bytes = float(tot[0]) * args.steps          # all ranks' blocks
@@ -792,12 +843,24 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if check is not None:
+            out["check"] = check
+        out["config"]["bootstrap"] = bootstrap if world > 1 else "none"
+        out["config"]["devices"] = devs if world > 1 else [device]
     if rank == 0:
         pmc = pmc_traffic(args.workload, kname)
         if pmc:
-            out["roofline"]["traffic"] = pmc["hbm_traffic_bytes_per_launch"]
+            t = pmc["hbm_traffic_bytes_per_launch"]
+            out["roofline"]["traffic"] = t
             out["roofline"]["traffic_source"] = pmc["source"]
             out["roofline"]["traffic_kernel"] = pmc["kernel"]
+            # frac is EFFECTIVE: algorithmic bytes count int32 columns, the sliced layout
+            # streams 8-bit window offsets; frac_dram is what the DRAM actually moved per launch
+            out["roofline"]["frac_basis"] = (
+                "effective: algorithmic CSR bytes (12 B per f64 nonzero with an int32 column, SURVEY §8d) / kernel "
+                "time; the shipped slices stream 8-bit column offsets, so fewer bytes reach DRAM — frac_dram is the "
+                "PMC traffic (FETCH_SIZE x 2 + WRITE_SIZE, profiles/) / the same kernel time / 8 TB/s")
+            out["roofline"]["frac_dram"] = round(t / (ev_ms / 1e3 / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
     if rank == 0:
         import ctypes as C
         dv, rk, nr, ck = C.c_int(), C.c_int(), C.c_int(), C.c_int()
