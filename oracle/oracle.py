@@ -52,6 +52,19 @@ def as_shipped():
         _lib = saved
 
 
+@contextlib.contextmanager
+def single_accumulation():
+    """Inside the block, float / complex<float> norms and dots accumulate in the scalar type itself,
+    one sequential single-precision sum (a scalar Eigen reduction over Vector<float>,
+    power_method.hpp:72,81) instead of in double then rounded (the default)."""
+    L = lib()
+    old = L.orc_set_single_accum(1)
+    try:
+        yield
+    finally:
+        L.orc_set_single_accum(old)
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -76,6 +89,8 @@ def _configure(L):
             f = getattr(L, "orc_" + name)
             f.argtypes = [_i64, _p, _p, _int, _dbl, _p, _p, _p, _p]
             f.restype = _int
+        L.orc_set_single_accum.argtypes = [_int]
+        L.orc_set_single_accum.restype = _int
         L.orc_power_csr_omp_f64.argtypes = [_i64, _p, _p, _p, _p, _int, _int]
         L.orc_power_csr_omp_f64.restype = _dbl
         L.orc_solve_shifted_dense_f64.argtypes = [_i64, _p, _dbl, _p, _p]
@@ -103,6 +118,8 @@ def _configure(L):
             f.restype = _int
         L.orc_hqr_francis_f64.argtypes = [_i64, _p, _p, _p]
         L.orc_hqr_francis_f64.restype = _int
+        L.orc_hqr_francis_f80.argtypes = [_i64, _p, _p, _p]
+        L.orc_hqr_francis_f80.restype = _int
         # long double / std::complex<long double> (x87): the same restatements at extended precision
         for sfx in ("f80", "c80"):
             getattr(L, "orc_spmv_csc_" + sfx).argtypes = [_i64, _i64, _p, _p, _p, _p, _p]
@@ -341,8 +358,16 @@ def qr_eigenvalues(A, max_iterations=1000, tolerance=1e-10):
 
 
 def hqr_francis(H):
-    """Francis double-shift QR on an upper Hessenberg matrix; returns complex eigenvalues."""
+    """Francis double-shift QR on an upper Hessenberg matrix; returns complex eigenvalues.  A long
+    double H runs the same restatement in x87 long double (clongdouble eigenvalues)."""
     n = H.shape[0]
+    if _wide(np.asarray(H).dtype):
+        Hf = np.array(H, dtype=np.longdouble, order="F", copy=True)
+        wr = np.zeros(n, dtype=np.longdouble)
+        wi = np.zeros(n, dtype=np.longdouble)
+        if lib().orc_hqr_francis_f80(n, _ptr(Hf), _ptr(wr), _ptr(wi)) != 0:
+            raise RuntimeError("hqr_francis: no convergence")
+        return wr + np.clongdouble(1j) * wi
     Hf = np.array(H, dtype=np.float64, order="F", copy=True)
     wr = np.zeros(n)
     wi = np.zeros(n)

@@ -328,3 +328,43 @@ def test_single_qr_eigenvalues(ctx, dtype):
     got = np.asarray(r.eigenvalues_complex, np.complex128)
     d = np.abs(got[:, None] - ref[None, :]).min(axis=1)
     assert d.max() <= 1e-5 * np.linalg.norm(B.astype(np.complex128))
+
+
+@pytest.mark.parametrize("dtype", SINGLE)
+@pytest.mark.parametrize("kind", ["band", "uniform"])
+def test_single_power_distance_to_both_float_semantics(ctx, dtype, kind):
+    """The device's float / complex<float> power method against BOTH oracle variants: the default
+    (norm and dot accumulated in double, rounded) and O.single_accumulation() (one sequential sum in
+    the scalar type: the reference's float Eigen instantiation, power_method.hpp:72,81; pinned
+    bitwise to a numpy float32 restatement in tests/test_oracle_golden.py).  The two variants differ
+    by ~1e-6 relative here; the device must be within 1e-5 (1 + |lambda|) of each with the same
+    iteration count (+-1), |x^H x_ref| >= 1 - 1e-5.  The distances are appended to
+    gpurun_out/single_accum_distances.jsonl as evidence."""
+    import json
+    import os
+    n = 40000
+    rp, ci, v = S.band(n, 10) if kind == "band" else S.uniform(n, 16)
+    v = _with_imag(v, dtype)
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    x0 = S.start_vector(n, dtype)
+    tol = 1e-5
+    res = E.power_method(A, E.SolverOptions(500, tol), x0)
+    A.close()
+    cp, ri, vv = O.csr_to_csc(rp, ci, v, n)
+    ref_d = O.power_csc(cp, ri, vv, x0, 500, tol)
+    with O.single_accumulation():
+        ref_f = O.power_csc(cp, ri, vv, x0, 500, tol)
+    lam = complex(res.eigenvalue)
+    rec = {"kind": kind, "dtype": np.dtype(dtype).name, "device": [lam.real, lam.imag], "iterations": res.iterations}
+    xd = res.eigenvector.astype(np.complex128)
+    for name, ref in (("double_acc", ref_d), ("float_acc", ref_f)):
+        lr = complex(ref["eigenvalue"])
+        dist = abs(lam - lr) / (1 + abs(lr))
+        rec[name] = {"rel_dist": dist, "iterations": ref["iterations"]}
+        assert dist <= 1e-5, (name, lam, lr)
+        assert abs(res.iterations - ref["iterations"]) <= 1, (name, res.iterations, ref["iterations"])
+        assert abs(abs(np.vdot(xd, ref["eigenvector"].astype(np.complex128))) - 1) <= 1e-5
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "single_accum_distances.jsonl"), "a") as f:
+            f.write(json.dumps(rec) + "\n")
