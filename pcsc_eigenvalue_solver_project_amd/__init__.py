@@ -98,8 +98,10 @@ def to_wire(a, dtype) -> np.ndarray:
         if np.any(np.isinf(hi) & np.isfinite(p)):
             raise EigSolError(EIGSOL_E_INVALID, "long double value outside the double exponent range "
                                                 "(double-double carries |v| < 1.8e308)")
-        lo = (p - hi.astype(np.longdouble)).astype(np.float64)
-        if np.any(hi.astype(np.longdouble) + lo.astype(np.longdouble) != p):
+        fin = np.isfinite(p)
+        with np.errstate(invalid="ignore"):
+            lo = np.where(fin, (p - hi.astype(np.longdouble)), 0).astype(np.float64)   # inf / NaN: lo = 0
+        if np.any(fin & (hi.astype(np.longdouble) + lo.astype(np.longdouble) != p)):
             import warnings
             warnings.warn("long double values below ~2^-1010 (1e-304) lose low bits in the double-double wire format "
                           "(the low part falls under the subnormal grid)", RuntimeWarning, stacklevel=2)
@@ -543,14 +545,22 @@ def qr_eigenvalues(ctx: Context, A, opts: SolverOptions = SolverOptions(), varia
     n = A.shape[0]
     v = 1 if variant == "unshifted" else 0
     if is_wide(A.dtype):
-        # long double: the reference's unshifted iteration in double-double (the multishift sweeps
-        # are fp64 kernels; the C++ facade makes the same choice)
+        # long double: "unshifted" = the reference's iteration in double-double; "francis" = the fp64
+        # multishift sweeps on the rounded double-double Hessenberg matrix, every eigenvalue then
+        # refined in double-double by Newton's method on det(H - mu I) (wide.hip)
         eig = wire_buffer(A.dtype, max(n, 1))
+        eim = np.zeros((max(n, 1), 2)) if (v == 0 and A.dtype == np.longdouble) else None
         it, conv = C.c_int32(0), C.c_int32(0)
         o = opts.to_c()
         call("eigsol_qr_eigenvalues_dense", ctx.handle, code, n, _ptr(to_wire(A.ravel(order="F"), A.dtype)),
-             C.byref(o), 1, _ptr(eig), None, C.byref(it), C.byref(conv))
-        return QRResult(from_wire(eig, A.dtype)[:n], int(it.value), bool(conv.value), None)
+             C.byref(o), v, _ptr(eig), None if eim is None else _ptr(eim), C.byref(it), C.byref(conv))
+        ev = from_wire(eig, A.dtype)[:n]
+        full = None
+        if v == 0:
+            full = ev.astype(np.clongdouble)
+            if eim is not None:
+                full = full + np.clongdouble(1j) * from_wire(eim, np.longdouble)[:n]
+        return QRResult(ev, int(it.value), bool(conv.value), full)
     if v == 0 and A.dtype in (np.float32, np.complex64):
         # single precision: the multishift sweeps are double kernels (as in the C++ facade, the
         # matrix is promoted and the eigenvalues rounded back); "unshifted" runs natively in float

@@ -532,11 +532,14 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     }
     // the exact LU's fill passes the cap: the nested-dissection multifrontal LU (its own ordering,
     // dense fronts on the matrix cores) where its plan fits the device; ILU(0) otherwise
+    // mf_create: EIGSOL_E_SOLVER = a zero pivot inside a front, EIGSOL_E_UNSUPPORTED = declined (a
+    // front buffer allocation failed after the plan's estimate): both continue with ILU(0) below;
+    // EIGSOL_E_HIP = a device fault, reported
     if (rc == EIGSOL_OK && !g->complete && mfh && mf_prc == EIGSOL_OK) {
         const int mrc = mf_create(ctx, dtype, mfh, mv.data(), &g->mf);
         lap("multifrontal factor");
         if (mrc == EIGSOL_OK) g->complete = 2;
-        else if (mrc == EIGSOL_E_HIP) rc = mrc;   // a zero pivot: ILU(0) below
+        else if (mrc == EIGSOL_E_HIP) rc = mrc;
     }
     if (mfh) mf_host_free(mfh);
     int32_t zpiv = 0;
@@ -599,8 +602,32 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     };
     if (rc == EIGSOL_OK && !g->mf) rc = factor();
     lap("numeric factor (IKJ levels)");
-    if (rc == EIGSOL_OK && zpiv && g->complete) {
-        // the exact LU met a zero pivot: ILU(0) on M's own pattern (GMRES then iterates over it)
+    if (rc == EIGSOL_OK && zpiv && g->complete == 1) {
+        // the exact LU without pivoting met a zero pivot (a singular leading minor of M): the
+        // multifrontal LU, whose nested-dissection order and partial pivoting inside each front
+        // avoid it where M itself is regular (the reference's SparseLU pivots, solve_shifted.hpp:
+        // 104-106); its plan was abandoned when the fill fitted, so it is made now on M's own pattern
+        const char* me = std::getenv("EIGSOL_MF");
+        size_t fb2 = 0, tb2 = 0;
+        if (!(me && !std::strcmp(me, "0")) && hipMemGetInfo(&fb2, &tb2) == hipSuccess) {
+            free_k();
+            MfHost* h2 = mf_host_new();
+            if (mf_prepare(n, orp, oci, dtype, (double)fb2, h2) == EIGSOL_OK) {
+                const int mrc = mf_create(ctx, dtype, h2, ov.data(), &g->mf);
+                lap("multifrontal factor (after the exact LU's zero pivot)");
+                if (mrc == EIGSOL_OK) {
+                    g->complete = 2;
+                    zpiv = 0;
+                } else if (mrc == EIGSOL_E_HIP) {
+                    rc = mrc;
+                }
+            }
+            mf_host_free(h2);
+        }
+    }
+    if (rc == EIGSOL_OK && zpiv && g->complete == 1) {
+        // the exact LU met a zero pivot (and the multifrontal LU did not help): ILU(0) on M's own
+        // pattern (GMRES then iterates over it)
         mrp.swap(orp);
         mci.swap(oci);
         mv.swap(ov);
@@ -891,6 +918,14 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
         }
     }
     EIGSOL_HIP(hipMemcpyAsync(y, x, n * sizeof(S), hipMemcpyDeviceToDevice, st));
+    if (g->mf && (!direct_done || cycles > 0 || guess)) {
+        // multifrontal solves after the first pass (refinement cycles, a warm-start guess): their
+        // wait-error word, read once in one host wait
+        int32_t* mf_err = reinterpret_cast<int32_t*>(g->hpin + 6);
+        EIGSOL_HIP(hipMemcpyAsync(mf_err, mf_err_word(g->mf), sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(stream_wait(st));
+        if (*mf_err) return fail(EIGSOL_E_HIP, "solve_shifted: a multifrontal solve wait did not complete");
+    }
     if (g->L) EIGSOL_TRY(shift_error(g->L));
     if (g->U) EIGSOL_TRY(shift_error(g->U));
     g->last_steps = steps;

@@ -167,6 +167,11 @@ __host__ __device__ inline double cabs_(double re, double im) {
 #endif
 }
 
+// modulus that does not underflow where sq_abs does (|a| below ~1e-162 squares to 0): pivot
+// searches and zero-pivot tests (the ordering is sq_abs's, up to rounding)
+__host__ __device__ inline double mod_abs(double a) { return a < 0 ? -a : a; }
+__host__ __device__ inline double mod_abs(cplx a) { return cabs_(a.re, a.im); }
+
 // tolerance.hpp:28-33: |a - b| <= tol * (1 + |a|), a = lambdaNew (power_method.hpp:84).
 __host__ __device__ inline bool close_rel(double are, double aim, double bre, double bim,
                                           double tol, bool is_complex) {

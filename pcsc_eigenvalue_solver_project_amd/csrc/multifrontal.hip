@@ -141,6 +141,13 @@ __global__ __launch_bounds__(256) void mf_extend_kernel(const MfFront* fr, const
     }
 }
 
+// a / b for a pivot b whose squared modulus underflows (exact power-of-two scaling of b)
+__device__ inline double sdiv_tiny(double a, double b) { return a / b; }
+__device__ inline cplx sdiv_tiny(cplx a, cplx b) {
+    const cplx q = cdiv(a, cplx{ldexp(b.re, 600), ldexp(b.im, 600)});
+    return cplx{ldexp(q.re, 600), ldexp(q.im, 600)};
+}
+
 // Panel q of every front in list[0 .. gridDim.x): pivots k0 .. k0 + kb - 1 (k0 = q NB), each the
 // first row of largest modulus among the front's remaining pivot rows [k, ns); the whole row
 // swapped (all d columns), the column below the diagonal scaled, the panel's other columns
@@ -161,7 +168,7 @@ __global__ __launch_bounds__(256) void mf_panel_kernel(const MfFront* fr, const 
         double best = -1.0;
         int bi = k;
         for (int i = k + tid; i < ns; i += 256) {
-            const double s = sq_abs(A[i + (int64_t)k * d]);
+            const double s = mod_abs(A[i + (int64_t)k * d]);   // no underflow below |a| ~ 1e-162
             if (s > best) { best = s; bi = i; }
         }
 #pragma unroll
@@ -191,8 +198,13 @@ __global__ __launch_bounds__(256) void mf_panel_kernel(const MfFront* fr, const 
             }
         __syncthreads();
         const S dk = A[k + (int64_t)k * d];
-        if (sq_abs(dk) > 0.0)
+        if (sq_abs(dk) >= 1e-280) {
             for (int i = k + 1 + tid; i < d; i += 256) A[i + (int64_t)k * d] = sdiv(A[i + (int64_t)k * d], dk);
+        } else if (mod_abs(dk) > 0.0) {
+            // |pivot| below ~1e-140: its squared modulus (the textbook complex quotient's
+            // denominator) would underflow; divide by the pivot scaled by 2^600, then rescale
+            for (int i = k + 1 + tid; i < d; i += 256) A[i + (int64_t)k * d] = sdiv_tiny(A[i + (int64_t)k * d], dk);
+        }
         __syncthreads();
         const int m = d - k - 1, w = c1 - k - 1;
         for (int e = tid; e < m * w; e += 256) {
@@ -2158,9 +2170,15 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     int32_t *d_tab = nullptr, *d_piv = nullptr, *d_z = nullptr;
     int64_t* d_dst = nullptr;
     S* d_v = nullptr;
+    // an allocation that fails after the plan's free-memory estimate declines the factor
+    // (EIGSOL_E_UNSUPPORTED: the caller goes on with ILU(0)); the out-of-memory status is cleared
     auto dm = [&](void** p, size_t bytes) {
-        if (rc == EIGSOL_OK && hipMalloc(p, std::max<size_t>(bytes, 16)) != hipSuccess)
-            rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal buffers (" + std::to_string(bytes >> 20) + " MiB)");
+        if (rc == EIGSOL_OK && hipMalloc(p, std::max<size_t>(bytes, 16)) != hipSuccess) {
+            (void)hipGetLastError();
+            *p = nullptr;
+            rc = fail(EIGSOL_E_UNSUPPORTED,
+                      "solve_shifted: multifrontal buffers (" + std::to_string(bytes >> 20) + " MiB) declined");
+        }
     };
     dm((void**)&f->fronts, nt * sizeof(dev::MfFront));
     dm((void**)&f->chl, chl.size() * 4);

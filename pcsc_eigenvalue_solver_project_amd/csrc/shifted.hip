@@ -2194,6 +2194,34 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
             f->kind = 2;
             f->src = A;
             csr_retain(A);
+            if (rc == EIGSOL_E_SOLVER && large_gmres) {
+                // every factor of the family met a zero pivot (the no-pivot exact LU, the
+                // multifrontal LU's front pivoting, ILU(0)): the partial-pivoting RCM band LU where
+                // its band fits, as the reference's pivoting SparseLU would (solve_shifted.hpp:104-106)
+                const std::string why = eigsol_last_error();
+                BandPlan bp;
+                band_plan(A->dtype, n, rp.data(), ci.data(), bp);
+                if (bp.ok) {
+                    auto* fb = new ShiftFactor();
+                    fb->ctx = A->ctx;
+                    ctx_retain(fb->ctx);
+                    fb->dtype = A->dtype;
+                    fb->n = n;
+                    fb->sig_re = sre;
+                    fb->sig_im = sim;
+                    fb->nnz_total = nnz;
+                    if (band_create(A->ctx, A->dtype, n, rp.data(), ci.data(), v.data(), sre, sim, bp, &fb->band) ==
+                        EIGSOL_OK) {
+                        fb->kind = 3;
+                        shift_free(f);
+                        *out = fb;
+                        return EIGSOL_OK;
+                    }
+                    shift_free(fb);
+                    (void)hipGetLastError();
+                }
+                rc = fail(EIGSOL_E_SOLVER, why);
+            }
             if (rc == EIGSOL_E_SOLVER) rc = gmres_dense_fallback<S>(f, rc);   // ILU(0) zero pivot
             if (rc != EIGSOL_OK) { shift_free(f); return rc; }
             *out = f;

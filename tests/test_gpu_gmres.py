@@ -177,6 +177,7 @@ def test_exact_lu_zero_pivot_retries_ilu0(ctx, gmres_env, monkeypatch):
     retry ILU(0) on M's own pattern (variant 7) and GMRES must still solve to 1e-10 ||b|| and drive
     the shifted inverse iteration to the block's exact eigenvalue."""
     monkeypatch.setenv("EIGSOL_GMRES_FALLBACK", "0")
+    monkeypatch.setenv("EIGSOL_MF", "0")         # the multifrontal retry (next test) off: ILU(0)
     nb = 6000
     n = 4 * nb                                   # > 16384: no densified LU either
     sigma = 0.25
@@ -239,3 +240,81 @@ def test_exact_lu_small_and_zero_pivots(ctx, gmres_env, pivot):
     assert abs(r.eigenvalue - lam) <= 1e-10 * (1 + abs(lam)), (r.eigenvalue, lam)
     assert abs(r.iterations - ref["iterations"]) <= 1
     A.close()
+
+
+def _zero_pivot_blocks(sigma=0.25, nb=6000):
+    M1 = np.array([[1, 0, 1, 0], [1, 1, 0, 0], [0, 1, -1, 1], [0, 0, 0.5, 3]], float)
+    scale = np.r_[1.0, 4.0 + np.random.default_rng(3).random(nb - 1)]
+    A = sp.block_diag([s * M1 for s in scale], format="csr") + sigma * sp.identity(4 * nb, format="csr")
+    A = sp.csr_matrix(A)
+    A.eliminate_zeros()
+    A.sort_indices()
+    return A, M1
+
+
+def _run_shifted(D, sigma, n, x0=None):
+    s = E.ShiftedSession(D, sigma)
+    s.begin(E.ShiftedSolverOptions(200, 1e-12, sigma), S.start_vector(n) if x0 is None else x0)
+    done = False
+    while not done:
+        s.step(1)
+        done, _ = s.query()
+    info = s.kernel_info()
+    r = s.finish()
+    s.close()
+    return info, r
+
+
+def test_exact_lu_zero_pivot_retries_multifrontal(ctx, gmres_env, monkeypatch):
+    """The matrix of the previous test with the multifrontal LU allowed (the default): after the
+    exact LU's zero pivot the factor is the nested-dissection multifrontal LU (variant 19), whose
+    partial pivoting inside each 4 x 4 front is the reference SparseLU's pivoting
+    (solve_shifted.hpp:104-106); direct solve to 1e-10 ||b||, the block's exact eigenvalue."""
+    monkeypatch.setenv("EIGSOL_GMRES_FALLBACK", "0")
+    sigma = 0.25
+    A, M1 = _zero_pivot_blocks(sigma)
+    n = A.shape[0]
+    D = E.CsrMatrix.from_scipy(ctx, A)
+    b = np.random.default_rng(4).standard_normal(n)
+    y = E.solve_shifted(D, sigma, b)
+    assert np.linalg.norm(A @ y - sigma * y - b) <= 1e-10 * np.linalg.norm(b)
+    info, r = _run_shifted(D, sigma, n)
+    assert info["variant"] == 19, info
+    ev = np.linalg.eigvals(M1)
+    exact = sigma + ev[np.argmin(np.abs(ev))].real
+    assert r.converged and abs(r.eigenvalue - exact) <= 1e-9, (r.eigenvalue, exact)
+    D.close()
+
+
+@pytest.mark.parametrize("mf", ["1", "0"])
+def test_zero_diagonal_band_past_16384(ctx, monkeypatch, mf):
+    """a banded A - sigma I past n = 16384 with exactly zero diagonal entries
+    (rows 0 and 9000: a_ii = sigma), nonsingular.  The natural-order exact LU (its fill fits) and
+    ILU(0) both meet the zero pivot at row 0.  Default: the multifrontal LU pivots inside the front
+    (variant 19); with EIGSOL_MF=0 the RCM band LU with partial pivoting takes over (variant 8) —
+    where before the call failed with "SparseLU factorization failed".  Either way the solve meets
+    1e-10 ||b|| and the shifted inverse iteration converges to an eigenvalue of A (residual check,
+    scipy's eigenvalue nearest sigma)."""
+    monkeypatch.setenv("EIGSOL_MF", mf)
+    monkeypatch.setenv("EIGSOL_GMRES_FALLBACK", "0")
+    n, sigma = 20000, 0.3
+    rng = np.random.default_rng(11)
+    off = [rng.uniform(-1, 1, n - k) for k in (1, 2, 3)]          # symmetric: a real spectrum
+    A = sp.diags(off[::-1] + off, [-3, -2, -1, 1, 2, 3], shape=(n, n), format="csr")
+    d = 2.5 + rng.uniform(0, 1, n)
+    d[0] = d[9000] = sigma
+    A = sp.csr_matrix(A + sp.diags(d))
+    A.sort_indices()
+    D = E.CsrMatrix.from_scipy(ctx, A)
+    b = rng.standard_normal(n)
+    y = E.solve_shifted(D, sigma, b)
+    M = A - sigma * sp.identity(n, format="csr")
+    assert np.linalg.norm(M @ y - b) <= 1e-10 * np.linalg.norm(b)
+    info, r = _run_shifted(D, sigma, n)
+    assert info["variant"] == (19 if mf == "1" else 8), info
+    x = r.eigenvector
+    assert r.converged and np.linalg.norm(A @ x - r.eigenvalue * x) <= 1e-8 * np.linalg.norm(x)
+    import scipy.sparse.linalg as spl
+    ev = spl.eigsh(A.astype(np.float64), k=1, sigma=sigma, return_eigenvectors=False)
+    assert abs(r.eigenvalue - ev[0]) <= 1e-8 * (1 + abs(ev[0])), (r.eigenvalue, ev)
+    D.close()

@@ -43,3 +43,20 @@ def test_out_of_range_refused():
         pytest.skip("long double is not the x87 format here")
     with pytest.raises(E.EigSolError):
         E.to_wire(np.array([LD(10) ** 400], LD), LD)
+
+
+@pytest.mark.skipif(not x87, reason="long double is not the x87 format here")
+def test_inf_and_nan_carry_without_warning():
+    """inf / NaN entries: hi carries them, lo = 0, and no 'below 2^-1010' warning (inf - inf
+    gave a NaN low part that failed the exactness check)."""
+    x = np.array([np.inf, -np.inf, np.nan, 1.0, LD(1) + LD(2) ** -60], dtype=LD)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        w = E.to_wire(x, LD)
+    assert np.all(w[:3, 1] == 0.0) and np.isposinf(w[0, 0]) and np.isneginf(w[1, 0]) and np.isnan(w[2, 0])
+    back = E.from_wire(w, LD)
+    assert np.isposinf(back[0]) and np.isneginf(back[1]) and np.isnan(back[2]) and np.all(back[3:] == x[3:])
+    z = np.array([complex(np.inf, 1.0), complex(2.0, np.nan)], dtype=CLD)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        E.to_wire(z, CLD)
