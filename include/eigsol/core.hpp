@@ -527,6 +527,10 @@ struct QRResult {
     bool converged = false;
     // Francis variant on a real matrix: the complex eigenvalues (eigenvalues = their real parts)
     std::vector<std::complex<double>> eigenvalues_complex;
+    // Francis variant, long double / std::complex<long double>: the eigenvalues at extended
+    // precision (double-double refined, rounded to long double); eigenvalues_complex holds them
+    // rounded to double
+    std::vector<std::complex<long double>> eigenvalues_complex_extended;
     QRResult() = default;
     QRResult(const Vector<S>& ev, int iters, bool conv) : eigenvalues(ev), iterations(iters), converged(conv) {}
 };

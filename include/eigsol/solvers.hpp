@@ -11,8 +11,8 @@
 // Scalars: double and std::complex<double> natively; float and std::complex<float> natively for the
 // power method and the triangular-CSR shifted inverse, promoted to fp64 for the other solvers
 // (core.hpp, PromotedScalar); long double / std::complex<long double> in double-double on the
-// device (core.hpp, WideScalar: every solver; qr_eigenvalues runs the reference's unshifted
-// iteration for them).
+// device (core.hpp, WideScalar: every solver; qr_eigenvalues' Francis variant refines the fp64
+// sweeps' eigenvalues in double-double).
 //
 // Start vector: the reference draws x0 with Eigen's Vector::Random (std::rand, not reproducible
 // across Eigen versions).  Here x0 comes from a documented generator
@@ -352,20 +352,36 @@ QRResult<S> qr_eigenvalues_dense(const DenseMatrix<S>& A, const SolverOptions& o
     if (n == 0) return QRResult<S>(Vector<S>(), 0, true);   // qr_eigenvalues.hpp:55-57
     detail::require_device_scalar<S>("qr_eigenvalues_dense");
     if constexpr (WideScalar<S>) {
-        // long double: the reference's own algorithm (unshifted H <- R Q, qr_eigenvalues.hpp:62-105)
-        // in double-double, for either variant: the multishift sweeps are fp64 kernels, and running
-        // them would round the matrix to double
-        (void)variant;
+        // long double: Unshifted = the reference's own algorithm (H <- R Q, qr_eigenvalues.hpp:62-105)
+        // in double-double; Francis = the fp64 multishift sweeps on the rounded double-double
+        // Hessenberg matrix, every eigenvalue then refined in double-double by Newton's method on
+        // det(H - mu I) (wide.hip), so no eigenvalue keeps fp64 accuracy only
         const auto aw = to_wire_vec(A.data(), static_cast<std::size_t>(A.size()));
         std::vector<wire_t<S>> ew(static_cast<std::size_t>(n));
+        std::vector<double> eim(2 * static_cast<std::size_t>(n), 0.0);   // real long double: imaginary dd parts
         std::int32_t it = 0, conv = 0;
         const eigsol_solver_options o = detail::copts(opts);
+        const bool francis = variant == QRVariant::Francis;
         detail::check(eigsol_qr_eigenvalues_dense(detail::ctx(), detail::dtype_of<S>(), n, aw.data(), &o,
-                                                  EIGSOL_QR_UNSHIFTED, ew.data(), nullptr, &it, &conv),
+                                                  static_cast<int>(variant), ew.data(),
+                                                  francis ? eim.data() : nullptr, &it, &conv),
                       "qr_eigenvalues_dense");
         Vector<S> ev(static_cast<std::size_t>(n));
         for (std::int64_t i = 0; i < n; ++i) ev(i) = from_wire(ew[static_cast<std::size_t>(i)]);
-        return QRResult<S>(ev, it, conv != 0);
+        QRResult<S> r(ev, it, conv != 0);
+        if (francis) {
+            r.eigenvalues_complex_extended.resize(static_cast<std::size_t>(n));
+            r.eigenvalues_complex.resize(static_cast<std::size_t>(n));
+            for (std::int64_t i = 0; i < n; ++i) {
+                std::complex<long double> z;
+                if constexpr (std::is_same_v<S, long double>)
+                    z = {ev(i), static_cast<long double>(eim[2 * i]) + static_cast<long double>(eim[2 * i + 1])};
+                else z = ev(i);
+                r.eigenvalues_complex_extended[i] = z;
+                r.eigenvalues_complex[i] = {static_cast<double>(z.real()), static_cast<double>(z.imag())};
+            }
+        }
+        return r;
     }
     // single precision: the reference's unshifted iteration natively in float; the Francis sweeps
     // (double kernels) on the fp64 promotion, eigenvalues rounded back

@@ -239,7 +239,12 @@ int eigsol_solve_shifted_dense(eigsol_dense* A, const void* sigma, const void* b
  *     receives the real parts (= diag of the standardised real Schur form), eig_im (optional) the
  *     imaginary parts; iterations = the most sweeps any single deflation needed (>= 1), and
  *     converged = 0 when that exceeded maxIterations (so iterations <= maxIterations exactly when
- *     converged, as in the reference).  Complex matrices use the unshifted variant.
+ *     converged, as in the reference).  Complex matrices (EIGSOL_C128) run complex multishift
+ *     sweeps and return the eigenvalues themselves in eig_re_or_c.
+ *     EIGSOL_DD / EIGSOL_CDD (long double): the fp64 sweeps on the rounded double-double Hessenberg
+ *     matrix, then every eigenvalue refined in double-double by Newton's method on det(H - mu I)
+ *     (Hyman's recurrence, n <= 8192); eig_re_or_c receives n dd (real parts) / n cdd values, and
+ *     for EIGSOL_DD eig_im (optional) the imaginary parts as n {hi, lo} pairs (2n doubles).
  * n == 0: iterations 0, converged 1 (qr_eigenvalues.hpp:55-57). */
 #define EIGSOL_QR_FRANCIS 0
 #define EIGSOL_QR_UNSHIFTED 1

@@ -738,7 +738,7 @@ int hqr_lds(hipStream_t st, const double* H, int64_t ld, int n, int maxits, doub
 int wide_hessenberg(eigsol_ctx* ctx, int dtype, int64_t n, const void* A, void* H);   // wide.hip
 int wide_qr_decompose(eigsol_ctx* ctx, int dtype, int64_t m, int64_t n, const void* A, void* Q, void* R);
 int wide_qr_eigenvalues(eigsol_ctx* ctx, int dtype, int64_t n, const void* A, const eigsol_solver_options* opts,
-                        int variant, void* eig, int32_t* iters, int32_t* conv);
+                        int variant, void* eig, double* eig_im, int32_t* iters, int32_t* conv);
 
 }  // namespace eigsol
 
@@ -788,7 +788,7 @@ int eigsol_qr_eigenvalues_dense(eigsol_ctx* ctx, int dtype, int64_t n, const voi
     if (!A_colmajor || !eig_re_or_c) return fail(EIGSOL_E_INVALID, "eigsol_qr_eigenvalues_dense: null pointer");
     EIGSOL_HIP(hipSetDevice(ctx->device));
     if (dtype_wide(dtype))
-        return wide_qr_eigenvalues(ctx, dtype, n, A_colmajor, opts, variant, eig_re_or_c, iterations, converged);
+        return wide_qr_eigenvalues(ctx, dtype, n, A_colmajor, opts, variant, eig_re_or_c, eig_im, iterations, converged);
     if (!dtype_valid(dtype)) return fail(EIGSOL_E_INVALID, "eigsol_qr_eigenvalues_dense: unknown dtype");
     if (dtype == EIGSOL_F32 || dtype == EIGSOL_C64) {
         // single precision: the reference's unshifted iteration natively (blocked QR decompositions

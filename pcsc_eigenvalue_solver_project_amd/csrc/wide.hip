@@ -1125,6 +1125,302 @@ int wqr_unshifted_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_iter, 
     return rc;
 }
 
+// ---------------------------------------------------------------- long double Francis QR
+// qr_eigenvalues<long double> with the implicit-shift variant (north_star's algorithm class; the
+// reference's ScalarConcept admits long double, types.hpp:28-30): the double-double Hessenberg
+// matrix H is rounded to fp64 and its eigenvalues found by the fp64 multishift sweeps
+// (francis.hip / zfrancis.hip); then every eigenvalue is refined on H ITSELF, in double-double, by
+// Newton's method on det(H - mu I).  For an unreduced Hessenberg matrix Hyman's recurrence gives
+// det(H - mu I) = +-c(mu) prod h(i, i-1) from the vector x with x(n-1) = 1 solving rows 1 .. n-1 of
+// (H - mu I) x = c e_0 (back substitution through the subdiagonal), c = row 0's residual; the
+// same recurrence differentiated gives c'(mu), and mu <- mu - c / c' converges quadratically from
+// the fp64 eigenvalue (error ~1e-16 cond) to the double-double floor in two or three steps.
+// Exact zeros on the subdiagonal split H into blocks; each block has its own recurrence and the
+// eigenvalue is refined on the block whose Newton step from the fp64 value is the smallest.  x and
+// its derivative are rescaled by powers of two when they leave [2^-300, 2^300] (the ratio c / c'
+// is scale-invariant).  A refinement that moves the eigenvalue by more than 1e-8 (1 + |lambda|)
+// (a Newton step that left the fp64 eigenvalue's basin) is discarded and the fp64 value kept.
+namespace wqdev {
+
+template <class T> __device__ __forceinline__ cdd as_cdd(const T& a);
+template <> __device__ __forceinline__ cdd as_cdd<dd>(const dd& a) { EIGSOL_EXACT return cdd{a, dd{0.0, 0.0}}; }
+template <> __device__ __forceinline__ cdd as_cdd<cdd>(const cdd& a) { return a; }
+
+__device__ __forceinline__ double cdd_maxhi(const cdd& a) { return fmax(fabs(a.re.hi), fabs(a.im.hi)); }
+
+constexpr int kHyT = 1024;   // threads of the refinement (one workgroup per eigenvalue)
+
+// One workgroup per eigenvalue; thread t owns rows t + kHyT k, k < R (n <= kHyT R).  Per column j
+// (descending): every owned row i <= j adds (h(i, j) - mu [i = j]) x_j to r_i and the same with
+// x'_j (minus x_j at i = j) to r'_i; the owner of row j then forms x_{j-1} = -r_j / h(j, j-1) (and
+// x'_{j-1}), or closes the block at a zero subdiagonal.  One barrier per column, two LDS slots
+// alternating by column parity.
+template <class T, int R>
+__global__ __launch_bounds__(kHyT) void hyman_newton_kernel(const T* __restrict__ H, int n, const cdd* __restrict__ lam0,
+                                                            cdd* __restrict__ lam_out, int32_t* __restrict__ steps_out,
+                                                            int max_newton) {
+    EIGSOL_EXACT
+    __shared__ cdd sx[2][2];      // [parity] {x_j, x'_j}
+    __shared__ int sflag[2][2];   // [parity] {reset rows < j+1 (block closed), scale exponent}
+    __shared__ cdd s_delta;       // Newton step of the selected block
+    __shared__ double s_best;     // |step| of the best block (first pass)
+    __shared__ int s_hi, s_cur_hi, s_done, s_upd;
+    const int t = threadIdx.x;
+    const int64_t ld = n;
+    const cdd zero = cdd{dd{0.0, 0.0}, dd{0.0, 0.0}};
+    const cdd one = cdd{dd{1.0, 0.0}, dd{0.0, 0.0}};
+    const cdd l0 = lam0[blockIdx.x];
+    cdd mu = l0;
+    int steps = 0;
+    if (t == 0) { s_hi = -1; s_done = 0; }
+    for (int it = 0; it < max_newton; ++it) {
+        cdd r[R], rp[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) { r[k] = zero; rp[k] = zero; }
+        if (t == 0) {
+            sx[(n - 1) & 1][0] = one;
+            sx[(n - 1) & 1][1] = zero;
+            sflag[(n - 1) & 1][0] = 0;
+            sflag[(n - 1) & 1][1] = 0;
+            s_cur_hi = n;
+            s_best = -1.0;
+        }
+        __syncthreads();
+        for (int j = n - 1; j >= 0; --j) {
+            const int par = j & 1;
+            const cdd xj = sx[par][0], xpj = sx[par][1];
+            const int reset = sflag[par][0], esc = sflag[par][1];
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const int i = t + kHyT * k;
+                if (i <= j) {
+                    if (reset) { r[k] = zero; rp[k] = zero; }   // rows of the next block start afresh
+                    else if (esc) { r[k] = cdd_ldexp(r[k], esc); rp[k] = cdd_ldexp(rp[k], esc); }
+                    cdd a = as_cdd<T>(H[i + (int64_t)j * ld]);
+                    if (i == j) a = cdd_sub(a, mu);
+                    r[k] = cdd_add(r[k], cdd_mul(a, xj));
+                    rp[k] = cdd_add(rp[k], cdd_mul(a, xpj));
+                    if (i == j) rp[k] = cdd_sub(rp[k], xj);
+                }
+            }
+            // the owner of row j: next x, or the block [j, cur_hi) closes
+            if (t == (j % kHyT)) {
+                const int k = j / kHyT;
+                cdd rj = r[0], rpj = rp[0];
+#pragma unroll
+                for (int q = 1; q < R; ++q)
+                    if (q == k) { rj = r[q]; rpj = rp[q]; }
+                const cdd sub_h = j > 0 ? as_cdd<T>(H[j + (int64_t)(j - 1) * ld]) : zero;
+                const int np = (j - 1) & 1;
+                if (j == 0 || cdd_is_zero(sub_h)) {
+                    // block [j, cur_hi): c = r_j, c' = r'_j, Newton step c / c'
+                    const cdd d = cdd_div(rj, rpj);
+                    const double ad = cdd_maxhi(d);
+                    const bool ok = ad == ad && ad <= 1.7976931348623157e308;
+                    if (it == 0) {
+                        if (ok && (s_best < 0.0 || ad < s_best)) { s_best = ad; s_delta = d; s_hi = s_cur_hi; }
+                    } else if (s_cur_hi == s_hi) {
+                        s_delta = ok ? d : zero;
+                        s_best = ok ? ad : -1.0;
+                    }
+                    if (j > 0) {
+                        sx[np][0] = one;
+                        sx[np][1] = zero;
+                        sflag[np][0] = 1;
+                        sflag[np][1] = 0;
+                        s_cur_hi = j;
+                    }
+                } else {
+                    cdd xn = cdd_neg(cdd_div(rj, sub_h));
+                    cdd xpn = cdd_neg(cdd_div(rpj, sub_h));
+                    const double m = fmax(cdd_maxhi(xn), cdd_maxhi(xpn));
+                    int e = 0;
+                    if (m > 0x1p300 || (m > 0.0 && m < 0x1p-300)) e = -ilogb(m);
+                    if (e) { xn = cdd_ldexp(xn, e); xpn = cdd_ldexp(xpn, e); }
+                    sx[np][0] = xn;
+                    sx[np][1] = xpn;
+                    sflag[np][0] = 0;
+                    sflag[np][1] = e;
+                }
+            }
+            __syncthreads();
+        }
+        // Newton update (thread 0 decides, everyone reads mu): mu <- mu - c / c' of the selected
+        // block; stop after a step at the double-double floor, or without a usable step
+        if (t == 0) {
+            s_upd = 0;
+            if (s_best < 0.0) {
+                s_done = 1;
+            } else {
+                const cdd mn = cdd_sub(mu, s_delta);
+                ++steps;
+                const double am = fmax(cdd_maxhi(mn), 1e-300);
+                if (s_best <= 0x1p-104 * am || it + 1 == max_newton) s_done = 1;
+                sx[0][0] = mn;   // hand mu over through LDS (slot free until the next pass starts)
+                s_upd = 1;
+            }
+        }
+        __syncthreads();
+        if (s_upd) mu = sx[0][0];
+        const int done = s_done;
+        __syncthreads();
+        if (done) break;
+    }
+    if (t == 0) {
+        // discard a refinement that left the fp64 eigenvalue's neighbourhood
+        const cdd dm = cdd_sub(mu, l0);
+        const double move = cdd_maxhi(dm), scale = 1.0 + cdd_maxhi(l0);
+        const bool keep = move == move && move <= 1e-8 * scale;
+        lam_out[blockIdx.x] = keep ? mu : l0;
+        steps_out[blockIdx.x] = keep ? steps : -1;
+    }
+}
+
+// hi parts of the double-double Hessenberg matrix (fp64 / complex fp64) and max |hi| (bits)
+template <class T>
+__global__ __launch_bounds__(wdev::kT) void hi_parts_kernel(const T* __restrict__ H, int64_t cnt, double* __restrict__ out,
+                                                      unsigned long long* __restrict__ amax) {
+    double m = 0.0;
+    for (int64_t e = (int64_t)blockIdx.x * wdev::kT + threadIdx.x; e < cnt; e += (int64_t)gridDim.x * wdev::kT) {
+        if constexpr (std::is_same_v<T, dd>) {
+            out[e] = H[e].hi;
+            m = fmax(m, fabs(H[e].hi));
+        } else {
+            out[2 * e] = H[e].re.hi;
+            out[2 * e + 1] = H[e].im.hi;
+            m = fmax(m, fmax(fabs(H[e].re.hi), fabs(H[e].im.hi)));
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0 && m > 0.0) atomicMax(amax, (unsigned long long)__double_as_longlong(m));
+}
+
+__global__ __launch_bounds__(wdev::kT) void ldexp_kernel(double* __restrict__ a, int64_t cnt, int e) {
+    for (int64_t i = (int64_t)blockIdx.x * wdev::kT + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * wdev::kT)
+        a[i] = ldexp(a[i], e);
+}
+
+}  // namespace wqdev
+
+}  // namespace
+
+int francis_large_f64(eigsol_ctx* ctx, double* H, int64_t n, int maxits, double* wr, double* wi, int32_t* sweeps,
+                      int32_t* fail_out);
+int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_host, int32_t* sweeps_out,
+                       int32_t* fail_out);
+
+namespace {
+
+constexpr int kHyMaxRows = 8;   // refinement: n <= kHyT * 8 = 8192
+
+template <class T, int R>
+static void hyman_launch(hipStream_t st, const T* H, int n, const cdd* l0, cdd* l1, int32_t* steps, int64_t count) {
+    hipLaunchKernelGGL((wqdev::hyman_newton_kernel<T, R>), dim3((unsigned)count), dim3(wqdev::kHyT), 0, st, H, n, l0,
+                       l1, steps, 4);
+}
+
+// eig: n scalars of T (DD: the real parts); eig_im (DD only, may be null): n dd imaginary parts
+template <class T>
+int wqr_francis_host(eigsol_ctx* ctx, int64_t n, const void* A, int max_iter, void* eig, double* eig_im,
+                     int32_t* iters, int32_t* conv) {
+    if (n > (int64_t)wqdev::kHyT * kHyMaxRows)
+        return fail(EIGSOL_E_UNSUPPORTED, "qr_eigenvalues: the double-double Francis refinement handles n <= 8192");
+    constexpr bool cx = std::is_same_v<T, cdd>;
+    hipStream_t st = ctx->stream;
+    T* H = nullptr;
+    double* H64 = nullptr;
+    cdd *dl0 = nullptr, *dl1 = nullptr;
+    int32_t* dsteps = nullptr;
+    unsigned long long* damax = nullptr;
+    int rc = EIGSOL_OK;
+    if (hipMalloc(&H, n * n * sizeof(T)) != hipSuccess || hipMalloc(&H64, n * n * (cx ? 16 : 8)) != hipSuccess ||
+        hipMalloc(&dl0, n * sizeof(cdd)) != hipSuccess || hipMalloc(&dl1, n * sizeof(cdd)) != hipSuccess ||
+        hipMalloc(&dsteps, n * sizeof(int32_t)) != hipSuccess || hipMalloc(&damax, 64) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: hipMalloc");
+    WQr<T> w;
+    if (rc == EIGSOL_OK) rc = wqr_alloc(w, n);
+    if (rc == EIGSOL_OK && hipMemcpyAsync(H, A, n * n * sizeof(T), hipMemcpyHostToDevice, st) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: upload");
+    if (rc == EIGSOL_OK) rc = whessenberg<T>(st, H, n, w);
+    // fp64 rounding of H, with LAPACK xGEEV's range guard (max |h| outside [smlnum, 1 / smlnum]:
+    // exact power-of-two scaling for the sweeps, eigenvalues scaled back)
+    unsigned long long bits = 0;
+    if (rc == EIGSOL_OK) {
+        hipMemsetAsync(damax, 0, 8, st);
+        hipLaunchKernelGGL((wqdev::hi_parts_kernel<T>), dim3(rgrid(n * n)), dim3(wdev::kT), 0, st, H, n * n, H64, damax);
+        if (hipMemcpyAsync(&bits, damax, 8, hipMemcpyDeviceToHost, st) != hipSuccess || stream_wait(st) != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: fp64 rounding");
+    }
+    int escale = 0;
+    if (rc == EIGSOL_OK) {
+        double amax;
+        std::memcpy(&amax, &bits, sizeof(amax));
+        const double smlnum = std::sqrt(std::numeric_limits<double>::min()) / std::numeric_limits<double>::epsilon();
+        if (std::isfinite(amax) && amax > 0.0 && (amax < smlnum || amax > 1.0 / smlnum)) {
+            escale = -std::ilogb(amax);
+            hipLaunchKernelGGL(wqdev::ldexp_kernel, dim3(rgrid(n * n * (cx ? 2 : 1))), dim3(wdev::kT), 0, st, H64,
+                               n * n * (cx ? 2 : 1), escale);
+        }
+    }
+    std::vector<cdd> l0(n);
+    int32_t sweeps = 0, failed = 0;
+    if (rc == EIGSOL_OK) {
+        if constexpr (cx) {
+            std::vector<cplx> wv(n);
+            rc = francis_large_c128(ctx, reinterpret_cast<cplx*>(H64), n, max_iter, wv.data(), &sweeps, &failed);
+            for (int64_t i = 0; i < n && rc == EIGSOL_OK; ++i)
+                l0[i] = cdd{dd{std::ldexp(wv[i].re, -escale), 0.0}, dd{std::ldexp(wv[i].im, -escale), 0.0}};
+        } else {
+            std::vector<double> wr(n), wi(n);
+            rc = francis_large_f64(ctx, H64, n, max_iter, wr.data(), wi.data(), &sweeps, &failed);
+            for (int64_t i = 0; i < n && rc == EIGSOL_OK; ++i)
+                l0[i] = cdd{dd{std::ldexp(wr[i], -escale), 0.0}, dd{std::ldexp(wi[i], -escale), 0.0}};
+        }
+    }
+    std::vector<cdd> l1(n);
+    std::vector<int32_t> steps(n, 0);
+    if (rc == EIGSOL_OK && hipMemcpyAsync(dl0, l0.data(), n * sizeof(cdd), hipMemcpyHostToDevice, st) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: upload eigenvalues");
+    if (rc == EIGSOL_OK) {
+        const int R = (int)((n + wqdev::kHyT - 1) / wqdev::kHyT);
+        const int ni = (int)n;
+        if (R <= 1) hyman_launch<T, 1>(st, H, ni, dl0, dl1, dsteps, n);
+        else if (R <= 2) hyman_launch<T, 2>(st, H, ni, dl0, dl1, dsteps, n);
+        else if (R <= 4) hyman_launch<T, 4>(st, H, ni, dl0, dl1, dsteps, n);
+        else hyman_launch<T, 8>(st, H, ni, dl0, dl1, dsteps, n);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(l1.data(), dl1, n * sizeof(cdd), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(steps.data(), dsteps, n * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            stream_wait(st) != hipSuccess)
+            rc = fail(EIGSOL_E_HIP, "qr_eigenvalues: double-double refinement");
+    }
+    if (rc == EIGSOL_OK) {
+        if (std::getenv("EIGSOL_WIDE_QR_DEBUG")) {
+            int kept = 0, mx = 0;
+            for (int32_t s : steps) { kept += s < 0; mx = std::max(mx, s); }
+            std::fprintf(stderr, "[wide-qr] n %lld sweeps %d refinement: %d kept fp64, max Newton steps %d\n",
+                         (long long)n, sweeps, kept, mx);
+        }
+        for (int64_t i = 0; i < n; ++i) {
+            if constexpr (cx) {
+                static_cast<cdd*>(eig)[i] = l1[i];
+            } else {
+                static_cast<dd*>(eig)[i] = l1[i].re;
+                if (eig_im) {
+                    eig_im[2 * i] = l1[i].im.hi;
+                    eig_im[2 * i + 1] = l1[i].im.lo;
+                }
+            }
+        }
+    }
+    if (iters) *iters = sweeps;
+    if (conv) *conv = failed ? 0 : 1;
+    wqr_free(w);
+    for (void* p : {(void*)H, (void*)H64, (void*)dl0, (void*)dl1, (void*)dsteps, (void*)damax})
+        if (p) (void)hipFree(p);
+    return rc;
+}
+
 }  // namespace
 
 int wide_hessenberg(eigsol_ctx* ctx, int dtype, int64_t n, const void* A, void* H) {
@@ -1134,10 +1430,11 @@ int wide_qr_decompose(eigsol_ctx* ctx, int dtype, int64_t m, int64_t n, const vo
     return by_wide(dtype, [&](auto tag) { return wqr_decompose_host<decltype(tag)>(ctx, m, n, A, Q, R); });
 }
 int wide_qr_eigenvalues(eigsol_ctx* ctx, int dtype, int64_t n, const void* A, const eigsol_solver_options* opts,
-                        int variant, void* eig, int32_t* iters, int32_t* conv) {
+                        int variant, void* eig, double* eig_im, int32_t* iters, int32_t* conv) {
     if (variant != EIGSOL_QR_UNSHIFTED)
-        return fail(EIGSOL_E_UNSUPPORTED, "qr_eigenvalues: the Francis sweeps are fp64 kernels; double-double "
-                                          "(long double) runs the reference's unshifted iteration (EIGSOL_QR_UNSHIFTED)");
+        return by_wide(dtype, [&](auto tag) {
+            return wqr_francis_host<decltype(tag)>(ctx, n, A, opts->max_iterations, eig, eig_im, iters, conv);
+        });
     return by_wide(dtype, [&](auto tag) {
         return wqr_unshifted_host<decltype(tag)>(ctx, n, A, opts->max_iterations, opts->tolerance, eig, iters, conv);
     });

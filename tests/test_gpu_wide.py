@@ -341,16 +341,23 @@ def test_wide_hessenberg_qr_extreme_scales(ctx, scale):
 
 def test_wide_qr_eigenvalues_reference_iteration(ctx):
     """qr_eigenvalues<long double>: the reference's unshifted iteration (qr_eigenvalues.hpp:62-105)
-    with its iteration counts; the Francis variant is refused at the C ABI (fp64 kernels) and the
-    Python view (like the C++ facade) runs the reference iteration for long double."""
+    with its iteration counts; the Francis variant (fp64 sweeps + double-double Newton refinement)
+    on the reference test's 3 x 3, whose Hessenberg form splits (h(2, 1) = 0): eigenvalues 2 and
+    1 +- sqrt(15) to long double precision."""
     r = E.qr_eigenvalues(ctx, np.array([[2, 1], [1, 2]], LD), E.SolverOptions(1000, 1e-12), "unshifted")
     assert r.converged and r.iterations == 25
     assert float(np.max(np.abs(np.sort(r.eigenvalues) - np.array([1, 3], LD)))) <= 1e-18
     A = np.array([[1, 3, 3], [5, 1, 4], [0, 0, 2]], LD)
-    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-10), "francis")
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-10), "unshifted")
     ref = O.qr_eigenvalues(A, 1000, 1e-10)
     assert r.converged and r.iterations == 44 == ref["iterations"]
     assert float(np.max(np.abs(r.eigenvalues - ref["eigenvalues"]))) <= 1e-17 * 8
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-10), "francis")
+    s15 = np.sqrt(LD(15))
+    exact = np.sort(np.array([1 - s15, 2, 1 + s15], LD))
+    assert r.converged and r.eigenvalues_complex.dtype == np.clongdouble
+    assert float(np.max(np.abs(np.sort(r.eigenvalues) - exact))) <= 4e-19 * 8
+    assert float(np.max(np.abs(r.eigenvalues_complex.imag))) == 0.0
     n = 12
     rng = np.random.default_rng(5)
     B = rng.standard_normal((n, n))
@@ -361,14 +368,94 @@ def test_wide_qr_eigenvalues_reference_iteration(ctx):
     assert r.converged == ref["converged"] and r.iterations == ref["iterations"]
     nrm = float(np.linalg.norm(S_.astype(np.float64)))
     assert float(np.max(np.abs(r.eigenvalues - ref["eigenvalues"]))) <= 1e-17 * nrm
-    # C ABI: the Francis variant has no double-double kernels
+    # C ABI: the Francis variant with no imaginary-part buffer (optional)
     o = E.SolverOptions(100, 1e-10).to_c()
     aw = E.to_wire(A.ravel(order="F"), LD)
     eig = E.wire_buffer(LD, 3)
     it, cv = C.c_int32(0), C.c_int32(0)
     st = E.lib().eigsol_qr_eigenvalues_dense(ctx.handle, 4, 3, aw.ctypes.data_as(C.c_void_p), C.byref(o), 0,
                                              eig.ctypes.data_as(C.c_void_p), None, C.byref(it), C.byref(cv))
-    assert st == 12   # EIGSOL_E_UNSUPPORTED
+    assert st == 0 and cv.value == 1
+    assert float(np.max(np.abs(np.sort(E.from_wire(eig, LD)) - exact))) <= 4e-19 * 8
+
+
+def _match(ev, ref):
+    """one-to-one nearest matching of two eigenvalue sets (complex, compared in long double)"""
+    from scipy.spatial import cKDTree
+    d, j = cKDTree(np.c_[ref.real.astype(float), ref.imag.astype(float)]).query(
+        np.c_[ev.real.astype(float), ev.imag.astype(float)], k=1)
+    assert len(np.unique(j)) == len(ev)
+    return np.abs((ev - ref[j]).astype(np.clongdouble))
+
+
+def test_wide_francis_random_256_vs_x87_francis(ctx):
+    """qr_eigenvalues<long double> (Francis) on a 256^2 N(0,1) matrix, against
+    the x87 oracle's Francis restatement at long double (oracle hqr_francis_t<long double> on the
+    x87 Hessenberg form, qr_eigenvalues.hpp:126-147 / types.hpp:28-30): one-to-one, every
+    eigenvalue within 1e-17 ||A||_F; the fp64 Francis path misses that bound by orders of magnitude
+    (its eigenvalues are off by ~1e-13), so the refinement is what meets it."""
+    n = 256
+    A = np.random.default_rng(256).standard_normal((n, n)).astype(LD)
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12), "francis")
+    assert r.converged
+    ref = O.hqr_francis(O.hessenberg(A))
+    nrm = float(np.linalg.norm(A.astype(np.float64)))
+    err = _match(r.eigenvalues_complex, ref)
+    assert float(err.max()) <= 1e-17 * nrm, float(err.max())
+    r64 = E.qr_eigenvalues(ctx, A.astype(np.float64), E.SolverOptions(1000, 1e-12), "francis")
+    err64 = _match(r64.eigenvalues_complex.astype(np.clongdouble), ref)
+    assert float(err64.max()) > 10 * float(err.max())
+    # conjugate pairs stay exact pairs (the refinement is conjugation-symmetric)
+    z = r.eigenvalues_complex
+    cz = np.sort_complex(z[z.imag != 0].astype(np.complex128))
+    assert len(cz) % 2 == 0
+
+
+@pytest.mark.parametrize("n", [64, 200])
+def test_wide_francis_complex_planted(ctx, n):
+    """complex<long double> Francis: A = U T U^H with T upper triangular (planted diagonal, well
+    separated) and U a product of Householder reflectors, all formed in x87 long double, so A's
+    eigenvalues are diag(T) to ~1e-19 ||T||.  Every device eigenvalue within 1e-17 ||A||_F of its
+    planted value (the complex fp64 sweeps alone: ~1e-15)."""
+    rng = np.random.default_rng(n)
+    d = (rng.uniform(1, 3, n) * np.exp(2j * np.pi * rng.random(n))).astype(np.clongdouble)
+    T = np.triu(0.1 * (rng.standard_normal((n, n)) + 1j * rng.standard_normal((n, n))), 1).astype(np.clongdouble)
+    T[np.arange(n), np.arange(n)] = d
+    A = T.copy()
+    for _ in range(3):
+        v = (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.clongdouble)
+        v /= np.sqrt(np.sum(np.abs(v) ** 2))
+        P = np.eye(n, dtype=np.clongdouble) - 2 * np.outer(v, v.conj())
+        A = P @ A @ P
+    r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12), "francis")
+    assert r.converged
+    nrm = float(np.sqrt(np.sum(np.abs(A.astype(np.complex128)) ** 2)))
+    err = _match(r.eigenvalues, d)
+    assert float(err.max()) <= 1e-17 * nrm, float(err.max())
+
+
+def test_wide_francis_split_and_triangular(ctx):
+    """Hessenberg forms with exact zero subdiagonals (the refinement runs on each diagonal block):
+    an upper-triangular long double matrix (eigenvalues = its diagonal, exactly) and a block-diagonal
+    one whose 2 x 2 blocks [[a, b], [-b, a]] have eigenvalues a +- i b."""
+    n = 40
+    rng = np.random.default_rng(3)
+    T = np.triu(rng.standard_normal((n, n))).astype(LD)
+    T[np.arange(n), np.arange(n)] = (np.arange(n) + 1).astype(LD) / 3
+    r = E.qr_eigenvalues(ctx, T, E.SolverOptions(1000, 1e-12), "francis")
+    assert r.converged
+    assert float(np.max(np.abs(np.sort(r.eigenvalues) - np.sort(np.diag(T))))) <= 2e-19 * n
+    m = 10
+    a = (np.arange(m) + 1).astype(LD) / 7
+    b = (np.arange(m) + 2).astype(LD) / 11
+    B = np.zeros((2 * m, 2 * m), LD)
+    for k in range(m):
+        B[2 * k, 2 * k] = B[2 * k + 1, 2 * k + 1] = a[k]
+        B[2 * k, 2 * k + 1], B[2 * k + 1, 2 * k] = b[k], -b[k]
+    r = E.qr_eigenvalues(ctx, B, E.SolverOptions(1000, 1e-12), "francis")
+    exact = np.concatenate([a + np.clongdouble(1j) * b, a - np.clongdouble(1j) * b])
+    assert r.converged
+    assert float(_match(r.eigenvalues_complex, exact).max()) <= 1e-18 * 4
 
 
 @pytest.mark.parametrize("k", [3, 20, 40])
