@@ -63,8 +63,9 @@ def parse():
                         "iterations) on the same sharded matrix and report lambda / iterations in the line")
     p.add_argument("--bootstrap", default="auto", choices=["auto", "rccl", "host"],
                    help="N > 1: the library's communicator. rccl: an RCCL communicator (one GPU per rank); "
-                        "host: set-up over torch.distributed (gloo), per-iteration exchange device to device. "
-                        "auto: rccl unless ranks share a GPU (RCCL refuses duplicate devices)")
+                        "host: set-up over torch.distributed (gloo), per-iteration exchange device to device "
+                        "(peer inboxes). auto: rccl on distinct GPUs (a rank whose peer set-up fails falls back to "
+                        "RCCL's collective exchange), host when ranks share a GPU (RCCL refuses duplicate devices)")
     return p.parse_args()
 
 
@@ -235,6 +236,11 @@ def measured_hbm(torch, stream, ctx=None):
                         "kernel_write_GBps": round(wr.value, 1), "kernel_read_blocks_per_cu": bpc.value,
                         "kernel": "eigsol::pdev::read_kernel, read8_kernel / copy_kernel / write_kernel (probe.hip, "
                                   "libeigsol_hip.so)"})
+        mx, mb = C.c_double(), C.c_int()
+        if lib().eigsol_hbm_probe_mix(ctx.handle, C.c_size_t(2 << 30), 10, C.byref(mx), C.byref(mb)) == 0:
+            out.update({"kernel_mix12_GBps": round(mx.value, 1), "kernel_mix12_blocks_per_cu": mb.value,
+                        "mix12_kernel": "eigsol::pdev::mix_kernel: the headline's read/write mix, 12 16-byte "
+                                        "non-temporal reads per 16-byte write"})
     out["note"] = ("practical ceilings of this box; the roofline peak stays the 8 TB/s spec.  kernel_read_GBps is "
                    "the better of the 16-byte and the 8-byte non-temporal read kernels (each at 1/2/4/8 workgroups "
                    "per CU).  The headline's actual DRAM rate (PMC traffic / event time) is compared against it below")
@@ -878,6 +884,9 @@ def main():
             actual = t / (ev_ms / 1e3 / args.steps) / 1e9
             out["roofline"]["actual_dram_GBps"] = round(actual, 1)
             out["roofline"]["actual_over_kernel_read_ceiling"] = round(actual / kr, 4)
+            km = out["roofline"]["measured_hbm"].get("kernel_mix12_GBps")
+            if km:
+                out["roofline"]["actual_over_kernel_mix12_ceiling"] = round(actual / km, 4)
     if not args.no_extras and world == 1:
         out["extras"] = {
             "config3_csr_1Mx16": run_config3(E, S, ctx, torch, torch_stream, opts),

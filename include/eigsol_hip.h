@@ -66,7 +66,8 @@ typedef enum eigsol_status {
  * device: CSR / dense products, the power method, the shifted inverse and solve_shifted (the fp64
  * factor of A - sigma I refined to double-double accuracy by residuals computed in double-double),
  * to_hessenberg, qr_decompose and the reference's unshifted qr_eigenvalues; the Francis variant
- * (fp64 kernels) and the row-sharded path return EIGSOL_E_UNSUPPORTED. */
+ * runs the fp64 sweeps and refines every eigenvalue in double-double (eigsol_qr_eigenvalues_dense);
+ * the row-sharded path returns EIGSOL_E_UNSUPPORTED. */
 typedef enum eigsol_dtype {
     EIGSOL_F64 = 0,
     EIGSOL_C128 = 1,
@@ -343,6 +344,9 @@ int eigsol_ctx_info(eigsol_ctx* ctx, int* device, int* rank, int* nranks, int* c
  * counted), write = store only (GB/s). */
 int eigsol_hbm_probe(eigsol_ctx* ctx, size_t bytes, int reps, double* read_gbps, double* copy_gbps,
                      double* write_gbps, int* best_blocks_per_cu);
+/* The headline SpMV's read / write mix (12 reads : 1 write of 16-byte non-temporal words) over
+ * `bytes` of reads: GB/s of both directions, best over 1/2/4/8 workgroups per CU. */
+int eigsol_hbm_probe_mix(eigsol_ctx* ctx, size_t bytes, int reps, double* mix_gbps, int* best_blocks_per_cu);
 
 /* ---------------------------------------------------------------- sparse LU analysis (host only)
  * The symbolic factorization the general-sparse shifted solve runs before choosing the exact LU

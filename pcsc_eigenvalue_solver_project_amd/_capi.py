@@ -124,6 +124,7 @@ SIGNATURES = {
     "eigsol_qr_eigenvalues_dense": [_vp, C.c_int, _i64, _vp, C.POINTER(SolverOptionsC), C.c_int, _vp,
                                     _vp, _pi32, _pi32],
     "eigsol_hbm_probe": [_vp, C.c_size_t, C.c_int, _pd, _pd, _pd, _pint],
+    "eigsol_hbm_probe_mix": [_vp, C.c_size_t, C.c_int, _pd, _pint],
     "eigsol_ctx_info": [_vp, _pint, _pint, _pint, _pint],
     "eigsol_sparse_lu_fill": [_i64, _vp, _vp, _i64, _pi64, _pi32],
     "eigsol_mf_analyze": [_i64, _vp, _vp, _i32, _i32, _vp, _vp, _i64, _pd],

@@ -1239,6 +1239,15 @@ struct MfFactor {
     std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt;
     std::vector<int32_t> lds_asm;
     MfStats st;
+    // solves replayed as a hipGraph per (b, out) pair seen twice (value flags, no flow kernels:
+    // the launches' arguments are then the same for every solve of that pair)
+    struct Graph {
+        const void* b;
+        void* out;
+        int uses;
+        hipGraphExec_t exec;
+    };
+    std::vector<Graph> graphs;
 };
 
 void mf_free(MfFactor* f) {
@@ -1250,6 +1259,8 @@ void mf_free(MfFactor* f) {
                     (void*)f->flags, (void*)f->err, f->z, f->tinv, (void*)f->flow_f, (void*)f->flow_b,
                     (void*)f->fheight, (void*)f->done, (void*)f->sub_ranges})
         if (p) hipFree(p);
+    for (auto& g : f->graphs)
+        if (g.exec) hipGraphExecDestroy(g.exec);
     ctx_release(f->ctx);
     delete f;
 }
@@ -2329,11 +2340,10 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     return EIGSOL_OK;
 }
 
+// Every launch of one solve, enqueued on st (direct, or inside a stream capture)
 template <class S>
-int mf_solve_t(MfFactor* f, const S* b, S* out) {
-    hipStream_t st = f->ctx->stream;
+static void mf_solve_enqueue(MfFactor* f, hipStream_t st, const S* b, S* out, int32_t ef, int32_t eb) {
     const int64_t n = f->n;
-    if (n == 0) return EIGSOL_OK;
     S* w = static_cast<S*>(f->w);
     S* x = static_cast<S*>(f->x);
     const S* F = static_cast<const S*>(f->F);
@@ -2341,7 +2351,6 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     const int32_t H = (int32_t)f->hstart.size() - 2;
     S* u = static_cast<S*>(f->u);
     S* z = static_cast<S*>(f->z);
-    const int32_t ef = ++f->epoch, eb = ++f->epoch;   // flag words: forward, then backward values
     const int flow_grid = (int)std::max<int64_t>(1, f->nflow);   // one workgroup per front, in order
     const bool ff = f->nflow && (f->flow_mode & 1), fb = f->nflow && (f->flow_mode & 2);
     if (f->nsub)
@@ -2389,6 +2398,51 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
         hipLaunchKernelGGL((dev::mf_bwd_flow_kernel<S>), dim3(flow_grid), dim3(256), f->lds_flow_b, st, f->fronts,
                            f->flow_b, f->nflow, f->done, eb, f->hflow, f->fheight, F, f->sidx, (const S*)w, x, f->err);
     hipLaunchKernelGGL((dev::mf_scatter_out_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, x, out, n);
+}
+
+template <class S>
+int mf_solve_t(MfFactor* f, const S* b, S* out) {
+    hipStream_t st = f->ctx->stream;
+    const int64_t n = f->n;
+    if (n == 0) return EIGSOL_OK;
+    const int32_t ef = ++f->epoch, eb = ++f->epoch;   // flag words: forward, then backward values
+    // ~50 dependent launches per solve (the tree's heights, forward and backward): replayed as one
+    // hipGraph once a (b, out) pair repeats (the shifted inverse iteration's checked direct solve
+    // uses one pair every iteration).  Only where no launch argument changes between solves:
+    // value flags (the epoch words are unused) and no flow kernels.  EIGSOL_MF_GRAPH=0: direct.
+    static const bool graph_on = [] {
+        const char* e = std::getenv("EIGSOL_MF_GRAPH");
+        return !(e && std::atoi(e) == 0);
+    }();
+    const bool ff = f->nflow && (f->flow_mode & 1), fb = f->nflow && (f->flow_mode & 2);
+    bool done = false;
+    if (graph_on && (f->backoff & 4) && !ff && !fb && st != nullptr) {
+        MfFactor::Graph* gr = nullptr;
+        for (auto& g : f->graphs)
+            if (g.b == b && g.out == out) gr = &g;
+        if (!gr) {
+            if (f->graphs.size() >= 8) {   // keep the most recent pairs
+                if (f->graphs.front().exec) (void)hipGraphExecDestroy(f->graphs.front().exec);
+                f->graphs.erase(f->graphs.begin());
+            }
+            f->graphs.push_back({b, out, 1, nullptr});
+        } else if (!gr->exec && ++gr->uses >= 2) {
+            hipGraph_t g = nullptr;
+            if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+                mf_solve_enqueue<S>(f, st, b, out, ef, eb);
+                if (hipStreamEndCapture(st, &g) != hipSuccess || !g ||
+                    hipGraphInstantiate(&gr->exec, g, nullptr, nullptr, 0) != hipSuccess)
+                    gr->exec = nullptr;
+                if (g) (void)hipGraphDestroy(g);
+            }
+            (void)hipGetLastError();   // a failed capture leaves the direct launches below
+        }
+        if (gr && gr->exec) {
+            EIGSOL_HIP(hipGraphLaunch(gr->exec, st));
+            done = true;
+        }
+    }
+    if (!done) mf_solve_enqueue<S>(f, st, b, out, ef, eb);
     EIGSOL_HIP(hipGetLastError());
     static const bool dbg = std::getenv("EIGSOL_MF_DEBUG") != nullptr;
     if (dbg) {

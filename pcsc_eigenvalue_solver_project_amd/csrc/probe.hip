@@ -88,6 +88,20 @@ __global__ __launch_bounds__(kT) void write_kernel(u4* __restrict__ b, size_t n1
         }
 }
 
+// read / write mix of the headline SpMV (reads 1.0 GB, writes y's 80 MB: ~12.5 : 1): every lane
+// loads kMixR 16-byte words from `a` (kU in flight) and stores their xor as one 16-byte word to
+// `b`, non-temporal like the other shapes
+constexpr int kMixR = 12;
+__global__ __launch_bounds__(kT) void mix_kernel(const u4* __restrict__ a, u4* __restrict__ b, size_t nout) {
+    for (size_t o = (size_t)blockIdx.x * kT + threadIdx.x; o < nout; o += (size_t)gridDim.x * kT) {
+        const size_t blk = (o / kT) * (size_t)kT * kMixR + (o % kT);   // coalesced: 12 wave-wide loads
+        u4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int r = 0; r < kMixR; ++r) acc ^= __builtin_nontemporal_load(a + blk + (size_t)r * kT);
+        __builtin_nontemporal_store(acc, b + o);
+    }
+}
+
 }  // namespace pdev
 }  // namespace eigsol
 
@@ -156,6 +170,60 @@ int eigsol_hbm_probe(eigsol_ctx* ctx, size_t bytes, int reps, double* read_gbps,
     if (best_blocks_per_cu) *best_blocks_per_cu = best_bpc;
     (void)hipStreamSynchronize(st);
     for (void* p : {a, b, o})
+        if (p) (void)hipFree(p);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return rc;
+}
+
+// The read / write mix of the headline (12 reads : 1 write, 16-byte non-temporal accesses) over
+// `bytes` of reads, best of 1/2/4/8 workgroups per CU: the practical ceiling for a kernel that
+// streams a matrix and writes a vector, next to the read-only ceiling of eigsol_hbm_probe.
+int eigsol_hbm_probe_mix(eigsol_ctx* ctx, size_t bytes, int reps, double* mix_gbps, int* best_blocks_per_cu) {
+    if (!ctx || bytes < 16 * pdev::kMixR * pdev::kT) return fail(EIGSOL_E_INVALID, "eigsol_hbm_probe_mix: bad arguments");
+    reps = std::max(1, reps);
+    EIGSOL_HIP(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const size_t per = (size_t)16 * pdev::kMixR * pdev::kT;
+    const size_t nblk = bytes / per;
+    const size_t nin = nblk * pdev::kMixR * pdev::kT, nout = nblk * pdev::kT;
+    void *a = nullptr, *b = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = EIGSOL_OK;
+    if (hipMalloc(&a, nin * 16) != hipSuccess || hipMalloc(&b, nout * 16) != hipSuccess ||
+        hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+        rc = fail(EIGSOL_E_HIP, "eigsol_hbm_probe_mix: allocation");
+    double best = 0.0;
+    int best_bpc = 0;
+    if (rc == EIGSOL_OK) {
+        (void)hipMemsetAsync(a, 0, nin * 16, st);
+        for (int bpc : {1, 2, 4, 8}) {
+            const unsigned grid = (unsigned)(bpc * ctx->num_cus);
+            auto launch = [&]() {
+                hipLaunchKernelGGL(pdev::mix_kernel, dim3(grid), dim3(pdev::kT), 0, st, static_cast<const pdev::u4*>(a),
+                                   static_cast<pdev::u4*>(b), nout);
+            };
+            launch();
+            (void)hipEventRecord(e0, st);
+            for (int r = 0; r < reps; ++r) launch();
+            (void)hipEventRecord(e1, st);
+            float ms = 0.0f;
+            if (hipGetLastError() != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                hipEventElapsedTime(&ms, e0, e1) != hipSuccess || ms <= 0.0f) {
+                rc = fail(EIGSOL_E_HIP, "eigsol_hbm_probe_mix: timing");
+                break;
+            }
+            const double gbps = (double)(nin + nout) * 16.0 * reps / (ms * 1e-3) / 1e9;
+            if (gbps > best) {
+                best = gbps;
+                best_bpc = bpc;
+            }
+        }
+    }
+    if (mix_gbps) *mix_gbps = best;
+    if (best_blocks_per_cu) *best_blocks_per_cu = best_bpc;
+    (void)hipStreamSynchronize(st);
+    for (void* p : {a, b})
         if (p) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);

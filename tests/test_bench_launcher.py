@@ -88,3 +88,19 @@ def test_under_torchrun_no_relaunch():
         "bench.main()\n")
     r = _run(code, {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 42, (r.returncode, r.stderr)   # went on to the rank path (imports torch)
+
+
+def test_device_map_for_shared_gpus(monkeypatch):
+    """EIGSOL_BENCH_DEVICES maps local ranks to GPUs (rehearsing N ranks on fewer GPUs: bench.py then
+    bootstraps over gloo, RCCL refusing duplicate devices); unset: local rank r on GPU r."""
+    import bench
+    monkeypatch.delenv("EIGSOL_BENCH_DEVICES", raising=False)
+    assert bench.device_map(4) == [0, 1, 2, 3]
+    monkeypatch.setenv("EIGSOL_BENCH_DEVICES", "0,0")
+    assert bench.device_map(2) == [0, 0]
+    monkeypatch.setenv("EIGSOL_BENCH_DEVICES", "0,0,1,1,2")
+    assert bench.device_map(4, 4) == [0, 0, 1, 1]
+    monkeypatch.setenv("EIGSOL_BENCH_DEVICES", "0")
+    import pytest
+    with pytest.raises(SystemExit):
+        bench.device_map(2)
