@@ -365,7 +365,7 @@ def run_config2(E, ctx, no_cpu):
         ev = r.eigenvalues_complex
         d, j = cKDTree(np.c_[ref.real, ref.imag]).query(np.c_[ev.real, ev.imag], k=1)
         out["vs_lapack_fixture"] = {"max_abs_diff": float(d.max()), "one_to_one": bool(len(np.unique(j)) == n)}
-    prof = os.path.join(ROOT, "profiles", "r04_qr4096_mfma.json")
+    prof = os.path.join(ROOT, "profiles", "r06_qr4096_mfma.json")
     if os.path.exists(prof):
         d = json.load(open(prof))
         out["mfma"] = {"gemm_TFLOPs": round(d["gemm_TFLOPs"], 2), "peak_TFLOPs": d["mfma_peak_TFLOPs"],
@@ -373,7 +373,7 @@ def run_config2(E, ctx, no_cpu):
                        "rank_update_TFLOPs": round(d.get("rank_update_TFLOPs") or 0.0, 2),
                        "rank_update_utilisation": round(d.get("rank_update_mfma_utilisation") or 0.0, 4),
                        "francis_window_gemm_share": round(d.get("francis_window_gemm_share") or 0.0, 4),
-                       "source": "profiles/r04_qr4096_mfma.json from profiles/r04_qr4096_kernel_stats.csv "
+                       "source": "profiles/r06_qr4096_mfma.json from profiles/r06_qr4096_kernel_stats.csv "
                                  "(rocprofv3 kernel times of the shipped path: hess_panel_coop<double, 1> issued by "
                                  "an ordinary launch of the same kernel, gemm_mfma_f64 / gemm_reduce / "
                                  "rankk_mfma<double, false> on v_mfma_f64_16x16x4_f64 - the whole trailing-update "

@@ -2406,13 +2406,15 @@ int mf_solve_t(MfFactor* f, const S* b, S* out) {
     const int64_t n = f->n;
     if (n == 0) return EIGSOL_OK;
     const int32_t ef = ++f->epoch, eb = ++f->epoch;   // flag words: forward, then backward values
-    // ~50 dependent launches per solve (the tree's heights, forward and backward): replayed as one
-    // hipGraph once a (b, out) pair repeats (the shifted inverse iteration's checked direct solve
-    // uses one pair every iteration).  Only where no launch argument changes between solves:
-    // value flags (the epoch words are unused) and no flow kernels.  EIGSOL_MF_GRAPH=0: direct.
+    // EIGSOL_MF_GRAPH=1 (opt-in): the ~50 dependent launches of a solve replayed as one hipGraph
+    // once a (b, out) pair repeats.  Only where no launch argument changes between solves: value
+    // flags (the epoch words are unused) and no flow kernels.  Measured and rejected (round 6,
+    // tools/r06_mf_graph_ab.sh, 1M convection-diffusion, two A/B pairs): 1.51 ms per iteration with
+    // direct launches, 2.82 / 2.86 ms replayed - the replay serialises the nodes behind more than the
+    // stream's own launch gaps
     static const bool graph_on = [] {
         const char* e = std::getenv("EIGSOL_MF_GRAPH");
-        return !(e && std::atoi(e) == 0);
+        return e && std::atoi(e) != 0;
     }();
     const bool ff = f->nflow && (f->flow_mode & 1), fb = f->nflow && (f->flow_mode & 2);
     bool done = false;
