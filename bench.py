@@ -436,13 +436,13 @@ def run_qr_complex(E, ctx, no_cpu, n=1024):
     return out
 
 
-def _convdiff_run(E, ctx, torch, stream, A, sigma, x0, max_iter):
+def _convdiff_run(E, ctx, torch, stream, A, sigma, x0, max_iter, tol=1e-10):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     sess = E.ShiftedSession(A, sigma)
     t_factor = time.perf_counter() - t0
     info0 = sess.kernel_info()
-    sess.begin(E.ShiftedSolverOptions(max_iter, 1e-10, sigma), x0)
+    sess.begin(E.ShiftedSolverOptions(max_iter, tol, sigma), x0)
     t = time.perf_counter()
     done = False
     while not done:
@@ -504,6 +504,15 @@ def run_config5_convdiff(E, S, ctx, torch, stream, nx=1000, max_iter=8):
                     os.environ[k] = val
         x = res.eigenvector
         d["eigen_residual"] = float(np.linalg.norm(M @ x - res.eigenvalue * x) / np.linalg.norm(x))
+        # the same 8 iterations of the reference loop run with SciPy's SuperLU on the host
+        # (tests/golden/convdiff1000_fixed.json): lambda after them, and the iteration count
+        fxp = os.path.join(ROOT, "tests", "golden", "convdiff1000_fixed.json")
+        if os.path.exists(fxp) and nx == 1000 and max_iter == 8:
+            fx = json.load(open(fxp))
+            if complex(*fx["sigma"]) == sigma:
+                d["vs_superlu_fixture"] = {"abs_error": float(abs(res.eigenvalue - complex(*fx["lambda"]))),
+                                           "fixture_iterations": fx["iterations"],
+                                           "source": "tests/golden/convdiff1000_fixed.json"}
         out[label] = d
     A.close()
     # complex<float>: the same family on the values widened to double, the iterate in complex<float>

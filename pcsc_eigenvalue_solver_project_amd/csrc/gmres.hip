@@ -266,6 +266,7 @@ struct GmresSolver {
     double rtol_accept = 1e-10; // worst final residual reported as a success (EIGSOL_GMRES_ACCEPT)
     double normM = 0.0;         // max(||M||_1, ||M||_inf): the backward-error scale of a direct solve
     double be_accept = 1e-14;   // a direct solve whose normwise backward error is below this is accepted
+    int64_t mf_static = 0;      // static pivots of the multifrontal factor (its zero-pivot retry)
     eigsol_csr* M = nullptr;    // M = A - sigma I uploaded (single-precision A only), else
     eigsol_csr* A = nullptr;    // the caller's device matrix: M x = A x - sigma x (no second copy of M)
     double sre = 0.0, sim = 0.0;
@@ -535,9 +536,31 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     // mf_create: EIGSOL_E_SOLVER = a zero pivot inside a front, EIGSOL_E_UNSUPPORTED = declined (a
     // front buffer allocation failed after the plan's estimate): both continue with ILU(0) below;
     // EIGSOL_E_HIP = a device fault, reported
+    // a front whose pivot column is zero in all of its rows (the pivot would have to come from a
+    // later front: SparseLU's pivoting would take it, the front-restricted one cannot) is retried with
+    // static pivots tau = sqrt(eps) max |m_ij| on such columns (SuperLU_DIST's remedy): K is then
+    // the LU of a perturbation of M, and the checked direct solve's GMRES cycles refine it away
+    auto static_tau = [&]() {
+        double mx = 0.0;
+        for (const S& e : mv) mx = std::max(mx, sq_abs(e));
+        return std::sqrt(mx) * 1.4901161193847656e-08;
+    };
+    auto mf_try = [&](MfHost* h, const S* vals, const char* what) -> int {
+        int mrc = mf_create(ctx, dtype, h, vals, &g->mf);
+        lap(what);
+        if (mrc == EIGSOL_E_SOLVER) {
+            const char* se = std::getenv("EIGSOL_MF_STATIC");
+            if (!(se && !std::strcmp(se, "0"))) {
+                int64_t ns = 0;
+                mrc = mf_create(ctx, dtype, h, vals, &g->mf, static_tau(), &ns);
+                g->mf_static = ns;
+                lap("multifrontal factor, static pivots");
+            }
+        }
+        return mrc;
+    };
     if (rc == EIGSOL_OK && !g->complete && mfh && mf_prc == EIGSOL_OK) {
-        const int mrc = mf_create(ctx, dtype, mfh, mv.data(), &g->mf);
-        lap("multifrontal factor");
+        const int mrc = mf_try(mfh, mv.data(), "multifrontal factor");
         if (mrc == EIGSOL_OK) g->complete = 2;
         else if (mrc == EIGSOL_E_HIP) rc = mrc;
     }
@@ -613,8 +636,7 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
             free_k();
             MfHost* h2 = mf_host_new();
             if (mf_prepare(n, orp, oci, dtype, (double)fb2, h2) == EIGSOL_OK) {
-                const int mrc = mf_create(ctx, dtype, h2, ov.data(), &g->mf);
-                lap("multifrontal factor (after the exact LU's zero pivot)");
+                const int mrc = mf_try(h2, ov.data(), "multifrontal factor (after the exact LU's zero pivot)");
                 if (mrc == EIGSOL_OK) {
                     g->complete = 2;
                     zpiv = 0;

@@ -152,12 +152,15 @@ __device__ inline cplx sdiv_tiny(cplx a, cplx b) {
 // first row of largest modulus among the front's remaining pivot rows [k, ns); the whole row
 // swapped (all d columns), the column below the diagonal scaled, the panel's other columns
 // rank-1 updated; then U12 = L11^-1 A12 on the columns right of the panel (one column per thread).
+// tau > 0 (static pivoting, the retry after a zero pivot): a pivot column whose remaining front
+// rows are all exactly zero gets the pivot tau on its diagonal (counted in *nstat) instead of
+// failing - a perturbation of M that the checked solve's GMRES refinement then removes.
 template <class S, int NB>
 __global__ __launch_bounds__(256) void mf_panel_kernel(const MfFront* fr, const int32_t* list, int q, S* F,
-                                                       int32_t* piv, int32_t* zpiv) {
+                                                       int32_t* piv, int32_t* zpiv, double tau, int32_t* nstat) {
     __shared__ double sv[4];
     __shared__ int si[4];
-    __shared__ int s_p;
+    __shared__ int s_p, s_fix;
     __shared__ S l11[NB * NB];
     const MfFront f = fr[list[blockIdx.x]];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -186,10 +189,22 @@ __global__ __launch_bounds__(256) void mf_panel_kernel(const MfFront* fr, const 
                 if (sv[w] > b || (sv[w] == b && si[w] < p)) { b = sv[w]; p = si[w]; }
             s_p = p;
             piv[f.c0 + k] = p;
-            if (!(b > 0.0)) atomicOr(zpiv, 1);
+            s_fix = 0;
+            if (!(b > 0.0)) {
+                if (tau > 0.0) {
+                    s_fix = 1;
+                    atomicAdd(nstat, 1);
+                } else {
+                    atomicOr(zpiv, 1);
+                }
+            }
         }
         __syncthreads();
         const int p = s_p;
+        if (s_fix) {   // the whole column is zero in the front's rows: p == k, no interchange
+            if (tid == 0) set_re_im(A[k + (int64_t)k * d], tau, 0.0);
+            __syncthreads();
+        }
         if (p != k)
             for (int j = tid; j < d; j += 256) {
                 const S t = A[k + (int64_t)j * d];
@@ -1248,6 +1263,7 @@ struct MfFactor {
         hipGraphExec_t exec;
     };
     std::vector<Graph> graphs;
+    int64_t nstatic = 0;   // static pivots of the factorization (0 unless the retry set them)
 };
 
 void mf_free(MfFactor* f) {
@@ -2114,7 +2130,7 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
 }
 
 template <class S>
-int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor** out) {
+int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor** out, double tau, int64_t* nstatic) {
     *out = nullptr;
     using clk = std::chrono::steady_clock;
     constexpr int NB = dev::RankKMax<S>::value;
@@ -2230,11 +2246,12 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     dm(&f->x, n * sb);
     dm((void**)&d_tab, tab.size() * 4);
     dm((void**)&d_piv, n * 4);
-    dm((void**)&d_z, 4);
+    dm((void**)&d_z, 8);   // [0] zero-pivot flag, [1] static pivots
     dm((void**)&d_dst, nnz * 8);
     dm((void**)&d_v, nnz * sb);
     std::vector<int32_t> hpiv(n);
-    int32_t hz = 0;
+    int32_t hz2[2] = {0, 0};
+    const int32_t& hz = hz2[0];
     if (rc == EIGSOL_OK) {
         const auto t1 = clk::now();
         auto up = [&](void* d, const void* h, size_t b) {
@@ -2261,7 +2278,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         up(d_dst, dst.data(), nnz * 8);
         up(d_v, vals, nnz * sb);
         hipMemsetAsync(f->F, 0, (size_t)fe * sb, st);
-        hipMemsetAsync(d_z, 0, 4, st);
+        hipMemsetAsync(d_z, 0, 8, st);
         S* F = static_cast<S*>(f->F);
         if (nnz)
             hipLaunchKernelGGL((dev::mf_scatter_kernel<S>), dim3((nnz + 255) / 256), dim3(256), 0, st, d_dst, d_v, nnz, F);
@@ -2271,7 +2288,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
                                    f->cmap, F);
             else if (l.kind == 1)
                 hipLaunchKernelGGL((dev::mf_panel_kernel<S, NB>), dim3(l.cnt), dim3(256), 0, st, f->fronts,
-                                   f->lists + l.off, l.q, F, d_piv, d_z);
+                                   f->lists + l.off, l.q, F, d_piv, d_z, tau, d_z + 1);
             else
                 hipLaunchKernelGGL((dev::mf_gemm_kernel<S, NB>), dim3(l.cnt), dim3(256), 0, st, f->fronts, d_tab + l.off,
                                    l.q, F);
@@ -2282,7 +2299,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         if (d_inv)
             hipLaunchKernelGGL((dev::mf_invform_kernel<S>), dim3(X.inv_list.size()), dim3(256), 0, st, f->fronts, d_inv, F);
         hipMemcpyAsync(hpiv.data(), d_piv, n * 4, hipMemcpyDeviceToHost, st);
-        hipMemcpyAsync(&hz, d_z, 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(hz2, d_z, 8, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal factorization");
         stt.numeric_seconds = std::chrono::duration<double>(clk::now() - t1).count();
@@ -2291,6 +2308,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     for (void* p : {(void*)d_tab, (void*)d_piv, (void*)d_z, (void*)d_dst, (void*)d_v, (void*)d_inv})
         if (p) hipFree(p);
     if (rc == EIGSOL_OK && hz) rc = fail(EIGSOL_E_SOLVER, "solve_shifted: multifrontal LU met a zero pivot");
+    if (nstatic) *nstatic = hz2[1];
+    f->nstatic = hz2[1];
     if (rc == EIGSOL_OK) {
         // composite interchange of every front: row t of the factored front is row q[t] of the assembled one
         std::vector<int32_t> pinv(n);
@@ -2472,11 +2491,15 @@ int mf_prepare(int64_t n, const std::vector<int32_t>& rp, const std::vector<int3
     }
 }
 
-int mf_create(eigsol_ctx* ctx, int dtype, MfHost* X, const void* v, MfFactor** out) {
+int mf_create(eigsol_ctx* ctx, int dtype, MfHost* X, const void* v, MfFactor** out, double static_pivot,
+              int64_t* nstatic) {
     *out = nullptr;
+    if (nstatic) *nstatic = 0;
     try {
-        if (dtype == EIGSOL_C128) return mf_create_t<cplx>(ctx, dtype, *X, static_cast<const cplx*>(v), out);
-        if (dtype == EIGSOL_F64) return mf_create_t<double>(ctx, dtype, *X, static_cast<const double*>(v), out);
+        if (dtype == EIGSOL_C128)
+            return mf_create_t<cplx>(ctx, dtype, *X, static_cast<const cplx*>(v), out, static_pivot, nstatic);
+        if (dtype == EIGSOL_F64)
+            return mf_create_t<double>(ctx, dtype, *X, static_cast<const double*>(v), out, static_pivot, nstatic);
     } catch (const std::exception& ex) {
         return fail(EIGSOL_E_UNSUPPORTED, std::string("solve_shifted: multifrontal factor: ") + ex.what());
     }

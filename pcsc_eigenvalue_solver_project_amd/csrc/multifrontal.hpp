@@ -33,8 +33,12 @@ const MfStats& mf_host_stats(const MfHost* X);   // after a successful mf_prepar
 int mf_prepare(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci, int dtype, double free_bytes,
                MfHost* X, const std::atomic<bool>* stop = nullptr);
 // The device half on a prepared plan with M's values: EIGSOL_OK with *out, EIGSOL_E_SOLVER on a
-// zero pivot, or EIGSOL_E_HIP.
-int mf_create(eigsol_ctx* ctx, int dtype, MfHost* X, const void* v, MfFactor** out);
+// zero pivot, EIGSOL_E_UNSUPPORTED when a front buffer cannot be allocated, or EIGSOL_E_HIP.
+// static_pivot > 0: a pivot column that is exactly zero in every remaining row of its front (its
+// pivot would have to come from outside the front) gets static_pivot on the diagonal instead - a
+// perturbation of M (*nstatic counts them) that the caller's checked solve refines away.
+int mf_create(eigsol_ctx* ctx, int dtype, MfHost* X, const void* v, MfFactor** out, double static_pivot = 0.0,
+              int64_t* nstatic = nullptr);
 // x = M^-1 b (device vectors, the caller's numbering), stream-ordered on ctx's stream
 int mf_solve(MfFactor* f, const void* b, void* x);
 void mf_free(MfFactor* f);

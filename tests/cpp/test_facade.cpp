@@ -449,13 +449,22 @@ TEST(WidePrecision, LongDoubleInDoubleDouble) {
     EXPECT_NEAR(std::abs(rsc.eigenvalue - CLD(2.0L, 4.0L)), 0.0L, 1e-18L);
     EigSol::Matrix::Dense<CLD> Dc(2, 2);
     Dc << CLD(1, 1), CLD(2, 0), CLD(0, 0), CLD(3, -1);
-    // long double runs the reference's unshifted iteration for either variant (triangular input:
-    // converged at the first check, the diagonal)
+    // long double Francis: fp64 sweeps, then each eigenvalue refined in double-double (triangular
+    // input: the diagonal, exactly)
     auto qc = EigSol::qr_eigenvalues<CLD>(EigSol::Matrix(Dc), EigSol::SolverOptions{}, EigSol::QRVariant::Francis);
     EXPECT_TRUE(qc.converged);
     EXPECT_EQ(qc.iterations, 1);
     EXPECT_NEAR(std::abs(qc.eigenvalues(0) - CLD(1, 1)), 0.0L, 1e-18L);
     EXPECT_NEAR(std::abs(qc.eigenvalues(1) - CLD(3, -1)), 0.0L, 1e-18L);
+    // real long double Francis: eigenvalues 1 and 3 of [[2, 1], [1, 2]] at extended precision, the
+    // complex form in eigenvalues_complex_extended
+    auto qf = EigSol::qr_eigenvalues<LD>(EigSol::Matrix(B), EigSol::SolverOptions{1000, 1e-12});
+    EXPECT_TRUE(qf.converged);
+    EXPECT_EQ(qf.eigenvalues_complex_extended.size(), 2u);
+    const LD lo = std::min(qf.eigenvalues(0), qf.eigenvalues(1)), hi = std::max(qf.eigenvalues(0), qf.eigenvalues(1));
+    EXPECT_NEAR(lo, 1.0L, 1e-18L);
+    EXPECT_NEAR(hi, 3.0L, 1e-18L);
+    EXPECT_NEAR(std::abs(qf.eigenvalues_complex_extended[0].imag()), 0.0L, 0.0L);
 }
 
 // ---------------------------------------------------------------- reference caller shapes
