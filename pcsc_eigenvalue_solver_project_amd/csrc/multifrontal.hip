@@ -1661,6 +1661,7 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
     {
         SymGraph g0;
         if (!sym_graph(n, rp, ci, g0, stop)) return false;
+        lap("graph: symmetric pattern");
         std::vector<char> done(n, 0);
         int64_t head = 0, tail = 0;
         for (int64_t s0 = 0; s0 < n; ++s0) {
@@ -1675,6 +1676,7 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
             }
         }
         if (stopped()) return false;
+        lap("graph: breadth-first labels");
         std::vector<int32_t> lab(n);
         for (int64_t k = 0; k < n; ++k) lab[ord[k]] = (int32_t)k;
         g.ptr.assign(n + 1, 0);
