@@ -1396,8 +1396,13 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
         t.parent = -1;
         stack.push_back(std::move(t));
     }
-    std::vector<int64_t> inset(n, -1), seen(n, -1);
-    std::vector<int32_t> level(n, 0);
+    // per-vertex state in one record, so a neighbour test touches one cache line: the piece tag
+    // (written by the piece's owner, read by the neighbouring pieces' BFS), the BFS stamp and level
+    struct Vs {
+        int64_t tag, seen;
+        int32_t level;
+    };
+    std::vector<Vs> vs(n, Vs{-1, -1, 0});
     // pseudo-peripheral restarts per piece (EIGSOL_MF_PP_ROUNDS).  1M convection-diffusion: 2 / 1 / 0
     // rounds -> 1.374e8 / 1.368e8 / 1.47e8 factor entries, 1.13e11 / 1.12e11 / 1.83e11 flops; on the box
     // the set-up is the same for 1 and 2 (0.63-0.67 s) and the solve 1.55 against 1.57 ms: 2 stays
@@ -1410,7 +1415,7 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
     std::condition_variable cv;
     int active = 0;
     bool aborted = false;
-    auto tag_of = [&](int32_t v) { return __atomic_load_n(&inset[v], __ATOMIC_RELAXED); };
+    auto tag_of = [&](int32_t v) { return __atomic_load_n(&vs[v].tag, __ATOMIC_RELAXED); };
     auto add_node = [&](std::vector<int32_t>&& members, int32_t parent, std::vector<int32_t> key) -> int32_t {
         std::lock_guard<std::mutex> lk(mu);
         tree.push_back(NdNode{std::move(members), parent, std::move(key)});
@@ -1426,13 +1431,13 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
         // raised inside a BFS once *stop is seen (checked every 64K visits: a whole-graph BFS of the
         // top piece takes tens of ms), the task then abandons the dissection
         bool cut = false;
-        // BFS inside the piece tagged `tag` from root: q holds the visit order, level[] the levels
+        // BFS inside the piece tagged `tag` from root: q holds the visit order, vs[].level the levels
         auto bfs = [&](int32_t root, int64_t tag) -> int32_t {
             const int64_t b = ++bstamp;
             q.clear();
             q.push_back(root);
-            seen[root] = b;
-            level[root] = 0;
+            vs[root].seen = b;
+            vs[root].level = 0;
             int32_t depth = 0;
             for (size_t h = 0; h < q.size(); ++h) {
                 const int32_t v = q[h];
@@ -1440,12 +1445,13 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
                     cut = true;
                     return depth;
                 }
+                const int32_t lw = vs[v].level + 1;
                 for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
                     const int32_t w = g.adj[e];
-                    if (tag_of(w) != tag || seen[w] == b) continue;
-                    seen[w] = b;
-                    level[w] = level[v] + 1;
-                    depth = std::max(depth, level[w]);
+                    if (tag_of(w) != tag || vs[w].seen == b) continue;
+                    vs[w].seen = b;
+                    vs[w].level = lw;
+                    depth = std::max(depth, lw);
                     q.push_back(w);
                 }
             }
@@ -1489,8 +1495,9 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
                 continue;
             }
             const int64_t tag = ++stamp;
-            for (int32_t v : t.nodes) __atomic_store_n(&inset[v], tag, __ATOMIC_RELAXED);
-            bfs(t.nodes[0], tag);
+            for (int32_t v : t.nodes) __atomic_store_n(&vs[v].tag, tag, __ATOMIC_RELAXED);
+            // from the piece's first vertex: connectivity, and the first pseudo-peripheral level set
+            const int32_t depth0 = bfs(t.nodes[0], tag);
             if (cut) {
                 abort_task();
                 return;
@@ -1499,10 +1506,10 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
                 // disconnected: components (in the order of their first vertex in the piece); the
                 // small ones packed into leaves, the others new pieces
                 std::vector<std::vector<int32_t>> comps;
-                const int64_t b0 = seen[t.nodes[0]];   // this piece's first BFS; later ones are larger
+                const int64_t b0 = vs[t.nodes[0]].seen;   // this piece's first BFS; later ones are larger
                 comps.push_back(q);
                 for (int32_t v : t.nodes) {
-                    if (seen[v] >= b0) continue;
+                    if (vs[v].seen >= b0) continue;
                     bfs(v, tag);
                     if (cut) break;
                     comps.push_back(q);
@@ -1536,12 +1543,12 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
             // pseudo-peripheral root (George-Liu): restart from a minimum-degree vertex of the last
             // level while the eccentricity grows
             int32_t root = t.nodes[0];
-            int32_t ecc = bfs(root, tag);
+            int32_t ecc = depth0;   // q and the levels are still those of the BFS from root
             for (int round = 0; round < pp_rounds; ++round) {
                 int32_t best = -1, bd = INT32_MAX;
                 for (size_t h = q.size(); h-- > 0;) {
                     const int32_t v = q[h];
-                    if (level[v] != ecc) break;
+                    if (vs[v].level != ecc) break;
                     const int32_t dv = sub_degree(v, tag);
                     if (dv < bd || (dv == bd && v < best)) { bd = dv; best = v; }
                 }
@@ -1564,7 +1571,7 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
                 continue;
             }
             std::vector<int64_t> cnt(nlev, 0);
-            for (int32_t v : t.nodes) ++cnt[level[v]];
+            for (int32_t v : t.nodes) ++cnt[vs[v].level];
             int32_t m = 1;
             {
                 int64_t cum = 0;
@@ -1577,13 +1584,13 @@ bool nested_dissection(int64_t n, const SymGraph& g, int leaf, std::vector<NdNod
             // separator: the vertices of level m that touch level m + 1; the rest of level m joins A
             std::vector<int32_t> A, B, Sep;
             for (int32_t v : t.nodes) {
-                const int32_t l = level[v];
+                const int32_t l = vs[v].level;
                 if (l < m) A.push_back(v);
                 else if (l > m) B.push_back(v);
                 else {
                     bool touch = false;
                     for (int64_t e = g.ptr[v]; e < g.ptr[v + 1] && !touch; ++e)
-                        touch = tag_of(g.adj[e]) == tag && level[g.adj[e]] == m + 1;
+                        touch = tag_of(g.adj[e]) == tag && vs[g.adj[e]].level == m + 1;
                     (touch ? Sep : A).push_back(v);
                 }
             }
@@ -1757,17 +1764,40 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
             fr[s].ch1 = (int32_t)chl.size();
         }
     }
-    // symbolic: struct(s) = indices >= c1 reached from s's rows in M + M^T or through a child's struct
+    // heights (a leaf 0, a parent one above its highest child) and the per-height front lists
+    // (descending ns: each panel's fronts are a prefix)
+    P.height.assign(nt, 0);
+    P.H = 0;
+    for (int64_t s = 0; s < nt; ++s) {
+        for (int32_t k = fr[s].ch0; k < fr[s].ch1; ++k) P.height[s] = std::max(P.height[s], P.height[chl[k]] + 1);
+        P.H = std::max(P.H, P.height[s]);
+    }
+    P.hstart.assign(P.H + 2, 0);
+    {
+        std::vector<std::vector<int32_t>> byh(P.H + 1);
+        for (int64_t s = 0; s < nt; ++s) byh[P.height[s]].push_back((int32_t)s);
+        for (int32_t h = 0; h <= P.H; ++h) {
+            std::stable_sort(byh[h].begin(), byh[h].end(), [&](int32_t a, int32_t b) { return fr[a].ns > fr[b].ns; });
+            P.lists.insert(P.lists.end(), byh[h].begin(), byh[h].end());
+            P.hstart[h + 1] = (int64_t)P.lists.size();
+        }
+    }
+    // symbolic: struct(s) = indices >= c1 reached from s's rows in M + M^T or through a child's
+    // struct (each list ascending).  A front needs only its children's lists, so the fronts of one
+    // height are independent: they run on the host threads (a mark array per thread), height after
+    // height, and the lists are concatenated in front order -- the same arrays as a serial pass.
     auto& sidx = P.sidx;
     auto& sof = P.sof;
     sof.assign(nt + 1, 0);
     {
-        std::vector<int64_t> mark(n, -1);
-        std::vector<int32_t> lst;
-        double fe_run = 0.0;
-        for (int64_t s = 0; s < nt; ++s) {
+        std::vector<std::vector<int32_t>> lists(nt);
+        std::atomic<bool> over{false};
+        std::atomic<double> fe_run{0.0};
+        const int nth = host_threads();
+        std::vector<std::vector<int32_t>> marks(std::max(1, nth));
+        auto one = [&](int32_t s, std::vector<int32_t>& mark) {
             const int32_t c0 = fr[s].c0, c1 = c0 + fr[s].ns;
-            lst.clear();
+            std::vector<int32_t>& lst = lists[s];
             for (int32_t i = c0; i < c1; ++i) {
                 const int32_t v = P.perm[i];
                 for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
@@ -1775,21 +1805,52 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
                     if (j >= c1 && mark[j] != s) { mark[j] = s; lst.push_back(j); }
                 }
             }
-            for (int32_t k = fr[s].ch0; k < fr[s].ch1; ++k) {
-                const int32_t c = chl[k];
-                for (int64_t e = sof[c]; e < sof[c + 1]; ++e) {
-                    const int32_t j = sidx[e];
+            for (int32_t k = fr[s].ch0; k < fr[s].ch1; ++k)
+                for (int32_t j : lists[chl[k]])
                     if (j >= c1 && mark[j] != s) { mark[j] = s; lst.push_back(j); }
-                }
-            }
             std::sort(lst.begin(), lst.end());
-            sidx.insert(sidx.end(), lst.begin(), lst.end());
+            const double d = (double)fr[s].ns + (double)lst.size();
+            double cur = fe_run.load(std::memory_order_relaxed);
+            while (!fe_run.compare_exchange_weak(cur, cur + d * d, std::memory_order_relaxed)) {}
+            if (cur + d * d > max_front_entries) over.store(true, std::memory_order_relaxed);
+        };
+        for (int32_t h = 0; h <= P.H; ++h) {
+            const int64_t b = P.hstart[h], m = P.hstart[h + 1] - b;
+            const int use = m < 8 ? 1 : (int)std::min<int64_t>(std::max(1, nth), m);
+            auto run = [&](int t) {
+                std::vector<int32_t>& mark = marks[t];
+                if (mark.empty()) mark.assign(n, -1);
+                for (int64_t k = t; k < m; k += use) {   // fronts dealt round-robin: sizes vary by position
+                    if (over.load(std::memory_order_relaxed) || stopped()) return;
+                    one(P.lists[b + k], mark);
+                }
+            };
+            if (use <= 1) {
+                run(0);
+            } else {
+                std::vector<std::thread> th;
+                try {
+                    for (int t = 1; t < use; ++t) th.emplace_back(run, t);
+                } catch (const std::exception&) {
+                    for (auto& x : th) x.join();
+                    th.clear();
+                    for (int t = 1; t < use; ++t) run(t);   // no more threads: this one does the rest
+                }
+                run(0);
+                for (auto& x : th) x.join();
+            }
+            if (over.load() || stopped()) return false;
+        }
+        int64_t tot = 0;
+        for (int64_t s = 0; s < nt; ++s) tot += (int64_t)lists[s].size();
+        sidx.reserve(tot);
+        for (int64_t s = 0; s < nt; ++s) {
+            sidx.insert(sidx.end(), lists[s].begin(), lists[s].end());
+            std::vector<int32_t>().swap(lists[s]);
             sof[s + 1] = (int64_t)sidx.size();
-            fr[s].ms = (int32_t)lst.size();
+            fr[s].ms = (int32_t)(sof[s + 1] - sof[s]);
             fr[s].sof = sof[s];
             fr[s].d = fr[s].ns + fr[s].ms;
-            fe_run += (double)fr[s].d * (double)fr[s].d;
-            if (fe_run > max_front_entries || (stop && stop->load(std::memory_order_relaxed))) return false;
         }
     }
     std::vector<int64_t>().swap(g.ptr);
@@ -1814,24 +1875,7 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
         P.maxns = std::max<int64_t>(P.maxns, fr[s].ns);
     }
     if (cplx_flops) P.flops *= 4.0;
-    // heights and the per-height front lists (descending ns: each panel's fronts are a prefix)
-    P.height.assign(nt, 0);
-    P.H = 0;
-    for (int64_t s = 0; s < nt; ++s) {
-        for (int32_t k = fr[s].ch0; k < fr[s].ch1; ++k) P.height[s] = std::max(P.height[s], P.height[chl[k]] + 1);
-        P.H = std::max(P.H, P.height[s]);
-    }
-    P.hstart.assign(P.H + 2, 0);
-    {
-        std::vector<std::vector<int32_t>> byh(P.H + 1);
-        for (int64_t s = 0; s < nt; ++s) byh[P.height[s]].push_back((int32_t)s);
-        for (int32_t h = 0; h <= P.H; ++h) {
-            std::stable_sort(byh[h].begin(), byh[h].end(), [&](int32_t a, int32_t b) { return fr[a].ns > fr[b].ns; });
-            P.lists.insert(P.lists.end(), byh[h].begin(), byh[h].end());
-            P.hstart[h + 1] = (int64_t)P.lists.size();
-        }
-    }
-    lap("heights");
+    lap("sizes");
     // parent positions of every child's struct entries
     P.cmap.assign(sidx.size(), 0);
     for (int64_t s = 0; s < nt; ++s) {
@@ -1855,6 +1899,7 @@ bool mf_plan(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_
             }
         }
     }
+    lap("parent maps");
     return true;
 }
 
