@@ -98,6 +98,50 @@ __device__ __forceinline__ void zhouse(cplx a, cplx x1, cplx x2, bool three, dou
     v2 = three ? qt(x2) : cplx{0.0, 0.0};
 }
 
+// sqrt of a in [2^-4, 2^4] (no range reduction): hardware reciprocal square root, then Goldschmidt /
+// Newton corrections to full double precision (francis.hip's, restated for this translation unit)
+__device__ __forceinline__ double sqrt_nr(double a) {
+    const double y = __builtin_amdgcn_rsq(a);
+    double s = a * y, h = 0.5 * y;
+    const double r = __builtin_fma(-h, s, 0.5);
+    s = __builtin_fma(s, r, s);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-s, s, a);
+    s = __builtin_fma(d, h, s);
+    d = __builtin_fma(-s, s, a);
+    return __builtin_fma(d, h, s);
+}
+
+// zhouse for the 2 x 2 reflectors of the one-wave QR, on any scale: (alpha, x1) is scaled by a power
+// of two (exact) so that its largest component lies in [1/2, 1), which puts the norm's square in
+// [1/4, 4] and lets the hardware square root seed replace the IEEE sequence; tau and v are
+// scale-free, beta is scaled back.  The same reflector as zhouse up to the rounding of the square
+// root and reciprocals.
+__device__ __forceinline__ void zhouse2_scaled(cplx a, cplx x1, double& beta, cplx& tau, cplx& v1) {
+    const double m = fmax(fmax(fabs(a.re), fabs(a.im)), fmax(fabs(x1.re), fabs(x1.im)));
+    const int ex = m > 0.0 ? __builtin_amdgcn_frexp_exp(m) : 0;
+    const cplx as{__builtin_amdgcn_ldexp(a.re, -ex), __builtin_amdgcn_ldexp(a.im, -ex)};
+    const cplx xs{__builtin_amdgcn_ldexp(x1.re, -ex), __builtin_amdgcn_ldexp(x1.im, -ex)};
+    const double xn2 = sq_abs(xs);
+    if (xn2 == 0.0 && as.im == 0.0) {
+        beta = a.re;
+        tau = cplx{0.0, 0.0};
+        v1 = cplx{0.0, 0.0};
+        return;
+    }
+    const double an = sqrt_nr(__builtin_fma(as.re, as.re, __builtin_fma(as.im, as.im, xn2)));
+    const double bs = as.re >= 0.0 ? -an : an;
+    const double ib = rcp_nr(bs);
+    tau = cplx{(bs - as.re) * ib, -as.im * ib};
+    const cplx d = cplx{as.re - bs, as.im};   // |d| >= |bs| > 0
+    const bool re_big = fabs(d.re) >= fabs(d.im);
+    const double r = re_big ? d.im * rcp_nr(d.re) : d.re * rcp_nr(d.im);
+    const double id = rcp_nr(re_big ? __builtin_fma(d.im, r, d.re) : __builtin_fma(d.re, r, d.im));
+    v1 = re_big ? cplx{__builtin_fma(xs.im, r, xs.re) * id, __builtin_fma(-xs.re, r, xs.im) * id}
+                : cplx{__builtin_fma(xs.re, r, xs.im) * id, __builtin_fma(xs.im, r, -xs.re) * id};
+    beta = __builtin_amdgcn_ldexp(bs, ex);
+}
+
 // ---------------------------------------------------------------- one-wave single-shift QR (n <= 64)
 // Eigenvalues of an n x n Hessenberg block (ZLAHQR without Schur vectors; updates confined to the
 // active block).  info[0] = 1 if some eigenvalue needed more than 30 max(10, n) iterations,
@@ -115,7 +159,7 @@ __device__ __forceinline__ void zhouse(cplx a, cplx x1, cplx x2, bool three, dou
 // factorisation (stop = i; the rows above stay unreduced).  stop = -1: ran to completion.
 // dtol: relative subdiagonal at which the block splits (ulp: ZLAHQR's test; the sweeps' shifts are
 // computed with a looser one, EIGSOL_ZQR_SHIFT_TOL)
-template <bool kSchur>
+template <bool kSchur, bool kFast = true>
 __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& maxits, int& steps,
                           double spk = -1.0, int* stop = nullptr, double dtol = 2.220446049250313e-16) {
     constexpr int lh = kZSmall + 1;
@@ -186,6 +230,16 @@ __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& ma
             // single-shift sweep from l
             steps += i - l;
             for (int kk = l; kk < i; ++kk) {
+                // kFast: the left update's rows kk, kk+1 (columns >= kk: this step's own stores go to
+                // column kk-1) and V's columns kk, kk+1 are loaded first, so their LDS latency
+                // overlaps the reflector's chain; the reflector is zhouse2_scaled's
+                const int c = kk + ln;
+                const bool cl = c <= (kSchur ? n - 1 : i);
+                cplx a0{0.0, 0.0}, a1{0.0, 0.0}, w0{0.0, 0.0}, w1{0.0, 0.0};
+                if (kFast) {
+                    if (cl) { a0 = H(kk, c); a1 = H(kk + 1, c); }
+                    if (kSchur && ln < n) { w0 = V(ln, kk); w1 = V(ln, kk + 1); }
+                }
                 cplx v0, v1;
                 if (kk == l) {
                     const cplx h11s = sub(H(l, l), t);
@@ -199,7 +253,8 @@ __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& ma
                 }
                 double beta;
                 cplx tau, vv, unused;
-                zhouse(v0, v1, cplx{0.0, 0.0}, false, beta, tau, vv, unused);
+                if (kFast) zhouse2_scaled(v0, v1, beta, tau, vv);
+                else zhouse(v0, v1, cplx{0.0, 0.0}, false, beta, tau, vv, unused);
                 EIGSOL_ZWAVE_ORDER();
                 if (kk > l && ln == 0) {
                     H(kk, kk - 1) = cplx{beta, 0.0};
@@ -207,9 +262,8 @@ __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& ma
                 }
                 const cplx ct = cconj(tau);
                 {   // left: rows kk, kk+1, columns kk..i (Schur: ..n-1)
-                    const int c = kk + ln;
-                    if (c <= (kSchur ? n - 1 : i)) {
-                        const cplx a0 = H(kk, c), a1 = H(kk + 1, c);
+                    if (cl) {
+                        if (!kFast) { a0 = H(kk, c); a1 = H(kk + 1, c); }
                         const cplx s = mul(ct, add(a0, cmul_conj(vv, a1)));
                         H(kk, c) = sub(a0, s);
                         H(kk + 1, c) = sub(a1, mul(s, vv));
@@ -219,16 +273,16 @@ __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& ma
                 {   // right: columns kk, kk+1, rows l..min(kk+2, i) (Schur: from row 0; and V)
                     const int r = (kSchur ? 0 : l) + ln;
                     if (r <= min(kk + 2, i)) {
-                        const cplx a0 = H(r, kk), a1 = H(r, kk + 1);
-                        const cplx s = mul(tau, add(a0, mul(a1, vv)));
-                        H(r, kk) = sub(a0, s);
-                        H(r, kk + 1) = sub(a1, mul(s, cconj(vv)));
+                        const cplx b0 = H(r, kk), b1 = H(r, kk + 1);
+                        const cplx s = mul(tau, add(b0, mul(b1, vv)));
+                        H(r, kk) = sub(b0, s);
+                        H(r, kk + 1) = sub(b1, mul(s, cconj(vv)));
                     }
                     if (kSchur && ln < n) {
-                        const cplx a0 = V(ln, kk), a1 = V(ln, kk + 1);
-                        const cplx s = mul(tau, add(a0, mul(a1, vv)));
-                        V(ln, kk) = sub(a0, s);
-                        V(ln, kk + 1) = sub(a1, mul(s, cconj(vv)));
+                        if (!kFast) { w0 = V(ln, kk); w1 = V(ln, kk + 1); }
+                        const cplx s = mul(tau, add(w0, mul(w1, vv)));
+                        V(ln, kk) = sub(w0, s);
+                        V(ln, kk + 1) = sub(w1, mul(s, cconj(vv)));
                     }
                 }
                 EIGSOL_ZWAVE_ORDER();
@@ -257,7 +311,8 @@ __device__ void zwave_hqr(cplx* h, cplx* v, int n, cplx* w, int& failed, int& ma
     }
 }
 
-// Eigenvalues of an n x n Hessenberg block (n <= 64) in LDS.
+// Eigenvalues of an n x n Hessenberg block (n <= 64) in LDS.  kFast: zwave_hqr's step (EIGSOL_ZQR_STEP)
+template <bool kFast>
 __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t ld, int n, cplx* w, int* info,
                                                        double dtol) {
     __shared__ cplx h[kZSmall * (kZSmall + 1)];
@@ -266,7 +321,7 @@ __global__ __launch_bounds__(64) void zhqr_wave_kernel(const cplx* Hin, int64_t 
     for (int idx = ln; idx < n * n; idx += 64) h[(idx % n) + (idx / n) * lh] = Hin[(idx % n) + (int64_t)(idx / n) * ld];
     __syncthreads();
     int failed, maxits, steps;
-    zwave_hqr<false>(h, nullptr, n, w, failed, maxits, steps, -1.0, nullptr, dtol);
+    zwave_hqr<false, kFast>(h, nullptr, n, w, failed, maxits, steps, -1.0, nullptr, dtol);
     if (ln == 0) {
         info[0] = failed;
         info[1] = maxits;
@@ -315,6 +370,7 @@ struct ZShiftJob {
     unsigned epoch;
 };
 
+template <bool kFast>
 __global__ __launch_bounds__(kZAedThreads) void zaed_kernel(cplx* Hg, int64_t n, int kw, int nw, int spike_valid,
                                                             int early, cplx* w, cplx* Vout, int* info, ZShiftJob sj) {
     constexpr int lh = kZSmall + 1;
@@ -332,7 +388,7 @@ __global__ __launch_bounds__(kZAedThreads) void zaed_kernel(cplx* Hg, int64_t n,
         if (tid == 0) __hip_atomic_store(sj.flag, sj.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         if (wv0) {
             int fail, maxsw, steps;
-            zwave_hqr<false>(t, nullptr, ns, sj.w, fail, maxsw, steps, -1.0, nullptr, sj.dtol);
+            zwave_hqr<false, kFast>(t, nullptr, ns, sj.w, fail, maxsw, steps, -1.0, nullptr, sj.dtol);
             if (ln == 0) {
                 sj.info[0] = fail;
                 sj.info[1] = maxsw;
@@ -352,7 +408,7 @@ __global__ __launch_bounds__(kZAedThreads) void zaed_kernel(cplx* Hg, int64_t n,
     __syncthreads();
     if (wv0) {
         int fail, maxsw, steps, stop = -1;
-        zwave_hqr<true>(t, v, nw, w + kw, fail, maxsw, steps, early ? cabs1(spike) : -1.0, &stop);
+        zwave_hqr<true, kFast>(t, v, nw, w + kw, fail, maxsw, steps, early ? cabs1(spike) : -1.0, &stop);
         // spike test, one window row per lane; deflated = the trailing run of negligible entries
         const double ulp = 2.220446049250313e-16, smlnum = 2.2250738585072014e-308 * ((double)nw / ulp);
         int nd = 0;
@@ -899,6 +955,12 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         return e ? std::atoi(e) : 0;
     }();
     static const bool stats = std::getenv("EIGSOL_QR_STATS") != nullptr;
+    // the one-wave QR's step (zwave_hqr kFast, EIGSOL_ZQR_STEP): 1 loads ahead and takes the scaled
+    // reflector (default), 0 the round-5 step
+    static const bool fast_step = [] {
+        const char* e = std::getenv("EIGSOL_ZQR_STEP");
+        return !(e && !std::strcmp(e, "0"));
+    }();
     int ihi = (int)n - 1;
     const int max_stall = std::max(1, maxits);
     // the shifts' QR splits at a looser relative subdiagonal than the eigenvalues' (EIGSOL_ZQR_SHIFT_TOL;
@@ -908,8 +970,8 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
         return e ? std::max(2.220446049250313e-16, std::atof(e)) : 2.220446049250313e-16;
     }();
     auto small = [&](int l, int hi, cplx* wdst, int info[2], double dtol = 2.220446049250313e-16) -> int {
-        hipLaunchKernelGGL(dev::zhqr_wave_kernel, dim3(1), dim3(64), 0, st, H + l + (int64_t)l * n, (int64_t)n,
-                           hi - l + 1, wdst, dinfo, dtol);
+        hipLaunchKernelGGL(fast_step ? dev::zhqr_wave_kernel<true> : dev::zhqr_wave_kernel<false>, dim3(1), dim3(64), 0,
+                           st, H + l + (int64_t)l * n, (int64_t)n, hi - l + 1, wdst, dinfo, dtol);
         EIGSOL_HIP(hipMemcpyAsync(hp->info, dinfo, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(stream_wait(st));
         info[0] = hp->info[0];
@@ -990,7 +1052,8 @@ int francis_large_c128(eigsol_ctx* ctx, cplx* H, int64_t n, int maxits, cplx* w_
             const int ns0 = 2 * plan(N, 0, C0, nbg0);   // the shift block if the AED deflates nothing
             const bool conc = conc_mode > 0 && !aed_full && ns0 >= 2 && ns0 <= dev::kZSmall;
             dev::ZShiftJob sj{ihi - ns0 + 1, ns0, shift_tol, dsw, dsinfo, dflag, ++flag_epoch};
-            hipLaunchKernelGGL(dev::zaed_kernel, dim3(conc ? 2 : 1), dim3(dev::kZAedThreads), 0, st, H, (int64_t)n, kw, nw,
+            hipLaunchKernelGGL(fast_step ? dev::zaed_kernel<true> : dev::zaed_kernel<false>, dim3(conc ? 2 : 1),
+                               dim3(dev::kZAedThreads), 0, st, H, (int64_t)n, kw, nw,
                                kw > l ? 1 : 0, aed_full ? 0 : 1, dw, dV, dinfo, sj);
             int* info = hp->info;
             if (hipMemcpyAsync(info, dinfo, 5 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
