@@ -1207,6 +1207,240 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
     if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- large fronts, two pivot blocks per workgroup (EIGSOL_MF_PAIR=1, value flags only; off by
+// default: measured slower, see MfFactor::pair).  A chain of
+// 64-row blocks pays one cross-CU hand-off per block (the producer's write-through store, the
+// consumer's poll: ~2-3 us with the chip busy).  Here a workgroup owns pivot blocks 2u and 2u + 1:
+// it awaits the dependencies the two share once, solves block 2u, and hands its values to block
+// 2u + 1 in LDS, so a front's chain crosses CUs once per pair.  Every row's sum keeps
+// mf_big_fwd_kernel's / mf_big_bwd_kernel's order (the column blocks in the same sequence, the
+// handed-over block last), so the solution is bitwise the same.
+// Reduction of the four waves' partial row sums, then the inverted diagonal block: returns the
+// block's solution in wave 0 (lane = row); part / vsh are the caller's LDS, synchronised here.
+template <class S>
+__device__ __forceinline__ S mf_pair_finish(S acc, S rhs, int rn, const S (&iv)[16], S (&part)[4][64], S* vsh) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    part[wv][lane] = acc;
+    __syncthreads();
+    if (wv == 0) {
+        const S sum = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+        vsh[lane] = lane < rn ? sub(rhs, sum) : s_zero<S>();
+    }
+    __syncthreads();
+    S p = s_zero<S>();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) p = add(p, mul(iv[t], vsh[16 * wv + t]));
+    part[wv][lane] = p;
+    __syncthreads();
+    return add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+}
+
+// forward: tab = (front, unit); unit < npair = ceil(nblk / 2) covers pivot blocks 2 unit and
+// 2 unit + 1, the others are struct row blocks (nblk + unit - npair, as mf_big_fwd_kernel)
+template <class S>
+__global__ __launch_bounds__(256) void mf_big_fwd2_kernel(const MfFront* fr, const int32_t* tab, const S* F,
+                                                          const S* Tinv, const S* z, S* w, S* u, int32_t* err, int bo,
+                                                          S* x) {
+    __shared__ S part[4][64];
+    __shared__ S ysh[4][16];
+    __shared__ S vsh[64];
+    __shared__ S ya[64];
+    const int s = tab[2 * blockIdx.x], un = tab[2 * blockIdx.x + 1];
+    const MfFront f = fr[s];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int d = f.d, ns = f.ns;
+    const int nblk = (ns + 63) / 64, npair = (nblk + 1) / 2;
+    const bool piv = un < npair;
+    const int ba = piv ? 2 * un : nblk + (un - npair);   // the (first) row block
+    const bool hasb = piv && ba + 1 < nblk;
+    const int ra0 = piv ? 64 * ba : ns + 64 * (ba - nblk);
+    const int rna = min(64, (piv ? ns : d) - ra0);
+    const int rnb = hasb ? min(64, ns - (ra0 + 64)) : 0;
+    const S* A = F + f.off;
+    const int rowa = ra0 + min(lane, rna - 1);
+    const int rowb = hasb ? ra0 + 64 + min(lane, rnb - 1) : rowa;
+    S iva[16], ivb[16];
+    if (piv) {
+        const S* ti = Tinv + (int64_t)(f.flag0 + ba) * 8192 + lane + (16 * wv) * 64;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) iva[t] = ti[t * 64];
+    }
+    if (hasb) {
+        const S* ti = Tinv + (int64_t)(f.flag0 + ba + 1) * 8192 + lane + (16 * wv) * 64;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) ivb[t] = ti[t * 64];
+    }
+    const S zra = lane < rna ? z[f.zoff + ra0 + lane] : s_zero<S>();
+    const S zrb = (hasb && lane < rnb) ? z[f.zoff + ra0 + 64 + lane] : s_zero<S>();
+    // block 2u + 1's tile over block 2u's columns: loaded before the chain of waits
+    S th[16];
+    if (hasb) {
+        const int c0 = 64 * ba + 16 * wv;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) th[t] = A[rowb + (int64_t)min(c0 + t, ns - 1) * d];
+    }
+    S acca = s_zero<S>(), accb = s_zero<S>();
+    const int cend = piv ? ba : nblk;
+    for (int c = 0; c < cend; ++c) {
+        const int c0 = 64 * c + 16 * wv;
+        S tva[16], tvb[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) tva[t] = A[rowa + (int64_t)min(c0 + t, ns - 1) * d];
+        if (hasb) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) tvb[t] = A[rowb + (int64_t)min(c0 + t, ns - 1) * d];
+        }
+        if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_poll(w + f.c0 + c0 + lane, err, bo) : s_zero<S>();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        mf_acc16(acca, tva, ysh[wv], c0, ns);
+        if (hasb) mf_acc16(accb, tvb, ysh[wv], c0, ns);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (!piv) {
+        part[wv][lane] = acca;
+        __syncthreads();
+        const S sum = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+        if (wv == 0 && lane < rna) u[f.uoff + (ra0 - ns) + lane] = add(zra, sum);
+        return;
+    }
+    const S y = mf_pair_finish(acca, zra, rna, iva, part, vsh);
+    if (wv == 0) {
+        // publish (the value is its own flag); x of these rows becomes "unsolved" for the backward pass
+        const S yc = mf_clean(y);
+        if (lane < rna) {
+            mf_st(w + f.c0 + ra0 + lane, yc);
+            mf_st(x + f.c0 + ra0 + lane, mf_sent(y));
+        }
+        ya[lane] = yc;   // what block 2u + 1 would have polled
+    }
+    if (!hasb) return;
+    __syncthreads();
+    mf_acc16(accb, th, ya + 16 * wv, 64 * ba + 16 * wv, ns);
+    const S yb = mf_pair_finish(accb, zrb, rnb, ivb, part, vsh);
+    if (wv == 0 && lane < rnb) {
+        mf_st(w + f.c0 + ra0 + 64 + lane, mf_clean(yb));
+        mf_st(x + f.c0 + ra0 + 64 + lane, mf_sent(yb));
+    }
+}
+
+// backward: tab = (front, unit), units descending; unit u covers pivot blocks 2u + 1 (when it
+// exists, solved first) and 2u
+template <class S>
+__global__ __launch_bounds__(256) void mf_big_bwd2_kernel(const MfFront* fr, const int32_t* tab, const S* F,
+                                                          const S* Tinv, const int32_t* sidx, const S* w, S* x,
+                                                          int32_t* err, int bo) {
+    __shared__ S part[4][64];
+    __shared__ S ysh[4][16];
+    __shared__ S vsh[64];
+    __shared__ S xa[64];
+    extern __shared__ __align__(16) unsigned char xs_raw[];
+    S* xsh = reinterpret_cast<S*>(xs_raw);   // x(struct), ms entries
+    const int s = tab[2 * blockIdx.x], un = tab[2 * blockIdx.x + 1];
+    const MfFront f = fr[s];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int d = f.d, ns = f.ns, ms = f.ms;
+    const int nblk = (ns + 63) / 64;
+    const int bl = 2 * un;                   // the lower block (always present)
+    const bool hash = bl + 1 < nblk;         // the higher block, solved first
+    const int rl0 = 64 * bl, rnl = min(64, ns - rl0);
+    const int rh0 = rl0 + 64, rnh = hash ? min(64, ns - rh0) : 0;
+    const S* A = F + f.off;
+    const int rowl = rl0 + min(lane, rnl - 1);
+    const int rowh = hash ? rh0 + min(lane, rnh - 1) : rowl;
+    S ivl[16], ivh[16];
+    {
+        const S* ti = Tinv + (int64_t)(f.flag0 + bl) * 8192 + 4096 + lane + (16 * wv) * 64;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) ivl[t] = ti[t * 64];
+    }
+    if (hash) {
+        const S* ti = Tinv + (int64_t)(f.flag0 + bl + 1) * 8192 + 4096 + lane + (16 * wv) * 64;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) ivh[t] = ti[t * 64];
+    }
+    const S wl = lane < rnl ? w[f.c0 + rl0 + lane] : s_zero<S>();
+    const S wh = (hash && lane < rnh) ? w[f.c0 + rh0 + lane] : s_zero<S>();
+    // the lower block's tile over the higher block's columns (used after the higher block is solved)
+    S tl[16];
+    if (hash) {
+        const int c0 = rh0 + 16 * wv;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) tl[t] = A[rowl + (int64_t)min(c0 + t, ns - 1) * d];
+    }
+    S accl = s_zero<S>(), acch = s_zero<S>();
+    // U12 x(struct) for both blocks' rows (x(struct) gathered into LDS once)
+    for (int q = tid; q < ms; q += 256) xsh[q] = x[sidx[f.sof + q]];
+    __syncthreads();
+    {
+        const S* tile_l = A + rowl + (int64_t)ns * d;
+        const S* tile_h = A + rowh + (int64_t)ns * d;
+        int q0 = 16 * wv;
+        for (; q0 + 64 < ms; q0 += 128) {
+            S ta[16], tb[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) ta[t] = tile_l[(int64_t)(q0 + t) * d];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) tb[t] = tile_l[(int64_t)min(q0 + 64 + t, ms - 1) * d];
+            mf_acc16(accl, ta, xsh + q0, q0, ms);
+            mf_acc16(accl, tb, xsh + q0 + 64, q0 + 64, ms);
+            if (hash) {
+#pragma unroll
+                for (int t = 0; t < 16; ++t) ta[t] = tile_h[(int64_t)(q0 + t) * d];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) tb[t] = tile_h[(int64_t)min(q0 + 64 + t, ms - 1) * d];
+                mf_acc16(acch, ta, xsh + q0, q0, ms);
+                mf_acc16(acch, tb, xsh + q0 + 64, q0 + 64, ms);
+            }
+        }
+        if (q0 < ms) {
+            S ta[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) ta[t] = tile_l[(int64_t)min(q0 + t, ms - 1) * d];
+            mf_acc16(accl, ta, xsh + q0, q0, ms);
+            if (hash) {
+#pragma unroll
+                for (int t = 0; t < 16; ++t) ta[t] = tile_h[(int64_t)min(q0 + t, ms - 1) * d];
+                mf_acc16(acch, ta, xsh + q0, q0, ms);
+            }
+        }
+    }
+    // later pivot blocks (the last first) as their values arrive
+    const int clow = hash ? bl + 1 : bl;
+    for (int c = nblk - 1; c > clow; --c) {
+        const int c0 = 64 * c + 16 * wv;
+        S tvl[16], tvh[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) tvl[t] = A[rowl + (int64_t)min(c0 + t, ns - 1) * d];
+        if (hash) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) tvh[t] = A[rowh + (int64_t)min(c0 + t, ns - 1) * d];
+        }
+        if (lane < 16) ysh[wv][lane] = c0 + lane < ns ? mf_poll(x + f.c0 + c0 + lane, err, bo) : s_zero<S>();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        mf_acc16(accl, tvl, ysh[wv], c0, ns);
+        if (hash) mf_acc16(acch, tvh, ysh[wv], c0, ns);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (hash) {
+        const S xh = mf_pair_finish(acch, wh, rnh, ivh, part, vsh);
+        if (wv == 0) {
+            const S xc = mf_clean(xh);
+            if (lane < rnh) mf_st(x + f.c0 + rh0 + lane, xc);
+            xa[lane] = xc;
+        }
+        __syncthreads();
+        mf_acc16(accl, tl, xa + 16 * wv, rh0 + 16 * wv, ns);
+    }
+    const S xl = mf_pair_finish(accl, wl, rnl, ivl, part, vsh);
+    if (wv == 0 && lane < rnl) mf_st(x + f.c0 + rl0 + lane, mf_clean(xl));
+}
+
 }  // namespace dev
 
 // ================================================================== host side
@@ -1236,6 +1470,13 @@ struct MfFactor {
     int32_t* slists = nullptr;
     int32_t* tabf = nullptr;
     int32_t* tabb = nullptr;
+    int32_t* tabf2 = nullptr;         // the same with two pivot blocks per entry (mf_big_fwd2 / bwd2_kernel)
+    int32_t* tabb2 = nullptr;
+    // EIGSOL_MF_PAIR=1 (value flags only; measured and left off, round 6, tools/r06_mf_pair_ab.sh):
+    // 1M convection-diffusion 1.495 / 1.509 -> 1.776 / 1.793 ms per iteration, bitwise the same
+    // solution - a workgroup holding two blocks' tiles (256 VGPRs + AGPRs, one wave per SIMD) loads
+    // them at half the rate, and that, not the hand-off count, is what the chain waits on
+    bool pair = false;
     int32_t* flags = nullptr;         // one per pivot block of the large fronts (epoch words)
     int32_t* err = nullptr;           // a flag wait that timed out
     void* z = nullptr;                // large fronts' assembled right-hand sides
@@ -1251,7 +1492,7 @@ struct MfFactor {
     int32_t* sub_ranges = nullptr;
     int32_t nsub = 0, lds_sub_f = 0, lds_sub_b = 0;                // bit 0 forward, bit 1 backward (EIGSOL_MF_FLOW_MODE, debugging)
     int backoff = 2;                  // EIGSOL_MF_BACKOFF: 1 growing sleeps, 2 relaxed polls (flag stores: release)
-    std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt;
+    std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt, foff2, fcnt2, boff2, bcnt2;
     std::vector<int32_t> lds_asm;
     MfStats st;
     // solves replayed as a hipGraph per (b, out) pair seen twice (value flags, no flow kernels:
@@ -1272,7 +1513,7 @@ void mf_free(MfFactor* f) {
     hipStreamSynchronize(f->ctx->stream);
     for (void* p : {(void*)f->fronts, (void*)f->chl, (void*)f->sidx, (void*)f->cmap, (void*)f->perm, (void*)f->pinv,
                     (void*)f->lists, f->F, f->u, f->w, f->x, (void*)f->slists, (void*)f->tabf, (void*)f->tabb,
-                    (void*)f->flags, (void*)f->err, f->z, f->tinv, (void*)f->flow_f, (void*)f->flow_b,
+                    (void*)f->tabf2, (void*)f->tabb2, (void*)f->flags, (void*)f->err, f->z, f->tinv, (void*)f->flow_f, (void*)f->flow_b,
                     (void*)f->fheight, (void*)f->done, (void*)f->sub_ranges})
         if (p) hipFree(p);
     for (auto& g : f->graphs)
@@ -1916,8 +2157,8 @@ struct MfHost {
     int64_t sb = 16;
     std::vector<int64_t> dst;              // M's entries -> front offsets
     std::vector<MfLaunch> plan;            // factorization launches
-    std::vector<int32_t> tab, slists, tabf, tabb, lds_asm;
-    std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt;
+    std::vector<int32_t> tab, slists, tabf, tabb, tabf2, tabb2, lds_asm;
+    std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt, foff2, fcnt2, boff2, bcnt2;
     int32_t nflag = 0;
     int64_t zsz = 0;
     int32_t hflow = 0;                     // heights below it: the dataflow launches (0: off)
@@ -2038,11 +2279,11 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
     int big_ns = 96, big_d = 256;
     if (const char* e = std::getenv("EIGSOL_MF_BIG_NS")) big_ns = std::atoi(e);
     if (const char* e = std::getenv("EIGSOL_MF_BIG_D")) big_d = std::atoi(e);
-    auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &lds_asm = X.lds_asm;
+    auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &tabf2 = X.tabf2, &tabb2 = X.tabb2, &lds_asm = X.lds_asm;
     auto &sstart = X.sstart, &nwave = X.nwave, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff, &fcnt = X.fcnt,
-         &boff = X.boff, &bcnt = X.bcnt;
+         &boff = X.boff, &bcnt = X.bcnt, &foff2 = X.foff2, &fcnt2 = X.fcnt2, &boff2 = X.boff2, &bcnt2 = X.bcnt2;
     sstart.assign(H + 2, 0);
-    for (auto* v : {&nwave, &nsmall, &nbig, &foff, &fcnt, &boff, &bcnt}) v->assign(H + 1, 0);
+    for (auto* v : {&nwave, &nsmall, &nbig, &foff, &fcnt, &boff, &bcnt, &foff2, &fcnt2, &boff2, &bcnt2}) v->assign(H + 1, 0);
     // one wave per small front (EIGSOL_MF_WAVE=1): measured 2.21 against 2.01 ms per 1M iteration
     // with one workgroup per front - the same loads in flight per CU, and the struct rows' GEMV on
     // one wave instead of four
@@ -2114,6 +2355,8 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
         sstart[h + 1] = (int64_t)slists.size();
         foff[h] = (int64_t)tabf.size() / 2;
         boff[h] = (int64_t)tabb.size() / 2;
+        foff2[h] = (int64_t)tabf2.size() / 2;
+        boff2[h] = (int64_t)tabb2.size() / 2;
         for (int32_t b : big) {
             dev::MfFront& q = fr[b];
             const int32_t nblk = (q.ns + 63) / 64, nsb = (q.ms + 63) / 64;
@@ -2123,10 +2366,15 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
             zsz += q.d;
             for (int32_t k = 0; k < nblk + nsb; ++k) { tabf.push_back(b); tabf.push_back(k); }
             for (int32_t k = nblk - 1; k >= 0; --k) { tabb.push_back(b); tabb.push_back(k); }
+            const int32_t npair = (nblk + 1) / 2;
+            for (int32_t k = 0; k < npair + nsb; ++k) { tabf2.push_back(b); tabf2.push_back(k); }
+            for (int32_t k = npair - 1; k >= 0; --k) { tabb2.push_back(b); tabb2.push_back(k); }
             lds_asm[h] = std::max<int32_t>(lds_asm[h], (int32_t)(q.ns * sb));
         }
         fcnt[h] = (int64_t)tabf.size() / 2 - foff[h];
         bcnt[h] = (int64_t)tabb.size() / 2 - boff[h];
+        fcnt2[h] = (int64_t)tabf2.size() / 2 - foff2[h];
+        bcnt2[h] = (int64_t)tabb2.size() / 2 - boff2[h];
     }
     // inverse forms of the one-workgroup fronts with at most 64 pivots and inv_d rows
     // (mf_invform_kernel), kept only while the fronts and the forms fit 0.6 of the device memory
@@ -2199,7 +2447,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     const auto& dst = X.dst;
     const auto& plan = X.plan;
     const auto& tab = X.tab;
-    const auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &lds_asm = X.lds_asm;
+    const auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &tabf2 = X.tabf2, &tabb2 = X.tabb2,
+               &lds_asm = X.lds_asm;
     const auto &sstart = X.sstart, &nwave = X.nwave, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff,
                &fcnt = X.fcnt, &boff = X.boff, &bcnt = X.bcnt;
     const int32_t nflag = X.nflag;
@@ -2222,7 +2471,12 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     f->fcnt = fcnt;
     f->boff = boff;
     f->bcnt = bcnt;
+    f->foff2 = X.foff2;
+    f->fcnt2 = X.fcnt2;
+    f->boff2 = X.boff2;
+    f->bcnt2 = X.bcnt2;
     f->lds_asm = lds_asm;
+    if (const char* e = std::getenv("EIGSOL_MF_PAIR")) f->pair = std::atoi(e) != 0;
     if (const char* e = std::getenv("EIGSOL_MF_BACKOFF")) f->backoff = std::atoi(e) & 3;
     // value flags (bit 4; EIGSOL_MF_VALFLAG=0: epoch flags): 1M convection-diffusion 1.657 -> 1.567 ms
     {
@@ -2264,6 +2518,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     dm((void**)&f->slists, slists.size() * 4);
     dm((void**)&f->tabf, tabf.size() * 4);
     dm((void**)&f->tabb, tabb.size() * 4);
+    dm((void**)&f->tabf2, tabf2.size() * 4);
+    dm((void**)&f->tabb2, tabb2.size() * 4);
     dm((void**)&f->flags, (size_t)nflag * 4);
     dm((void**)&f->err, 4);
     dm(&f->z, (size_t)zsz * sb);
@@ -2313,6 +2569,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         up(f->slists, slists.data(), slists.size() * 4);
         up(f->tabf, tabf.data(), tabf.size() * 4);
         up(f->tabb, tabb.data(), tabb.size() * 4);
+        up(f->tabf2, tabf2.data(), tabf2.size() * 4);
+        up(f->tabb2, tabb2.data(), tabb2.size() * 4);
         hipMemsetAsync(f->flags, 0, std::max<size_t>((size_t)nflag * 4, 4), st);
         up(f->flow_f, X.flow_f.data(), X.flow_f.size() * 4);
         up(f->flow_b, X.flow_b.data(), X.flow_b.size() * 4);
@@ -2393,6 +2651,9 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_big_bwd_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                *std::max_element(f->lds_bbig.begin(), f->lds_bbig.end())) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_big_bwd2_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                 *std::max_element(f->lds_bbig.begin(), f->lds_bbig.end())) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal solve LDS");
     }
@@ -2419,6 +2680,8 @@ static void mf_solve_enqueue(MfFactor* f, hipStream_t st, const S* b, S* out, in
     S* z = static_cast<S*>(f->z);
     const int flow_grid = (int)std::max<int64_t>(1, f->nflow);   // one workgroup per front, in order
     const bool ff = f->nflow && (f->flow_mode & 1), fb = f->nflow && (f->flow_mode & 2);
+    // two pivot blocks per workgroup (mf_big_fwd2 / bwd2_kernel): value flags only
+    const bool pair = f->pair && (f->backoff & 4);
     if (f->nsub)
         hipLaunchKernelGGL((dev::mf_fwd_sub_kernel<S>), dim3(f->nsub), dim3(256), f->lds_sub_f, st, f->fronts,
                            f->sub_ranges, f->chl, F, f->cmap, f->pinv, w, u);
@@ -2438,14 +2701,23 @@ static void mf_solve_enqueue(MfFactor* f, hipStream_t st, const S* b, S* out, in
         if (f->nbig[h]) {
             hipLaunchKernelGGL((dev::mf_big_asm_kernel<S>), dim3(f->nbig[h]), dim3(256), f->lds_asm[h], st, f->fronts,
                                L + nw + f->nsmall[h], f->chl, f->cmap, f->pinv, w, (const S*)u, z, f->backoff);
-            hipLaunchKernelGGL((dev::mf_big_fwd_kernel<S>), dim3(f->fcnt[h]), dim3(256), 0, st, f->fronts,
-                               f->tabf + 2 * f->foff[h], F, (const S*)f->tinv, (const S*)z, w, u, f->flags, ef, f->err,
-                               f->backoff, x);
+            if (pair)
+                hipLaunchKernelGGL((dev::mf_big_fwd2_kernel<S>), dim3(f->fcnt2[h]), dim3(256), 0, st, f->fronts,
+                                   f->tabf2 + 2 * f->foff2[h], F, (const S*)f->tinv, (const S*)z, w, u, f->err,
+                                   f->backoff, x);
+            else
+                hipLaunchKernelGGL((dev::mf_big_fwd_kernel<S>), dim3(f->fcnt[h]), dim3(256), 0, st, f->fronts,
+                                   f->tabf + 2 * f->foff[h], F, (const S*)f->tinv, (const S*)z, w, u, f->flags, ef,
+                                   f->err, f->backoff, x);
         }
     }
     for (int32_t h = H; h >= (fb ? f->hflow : 0); --h) {
         const int32_t* L = f->slists + f->sstart[h];
-        if (f->nbig[h])
+        if (f->nbig[h] && pair)
+            hipLaunchKernelGGL((dev::mf_big_bwd2_kernel<S>), dim3(f->bcnt2[h]), dim3(256), f->lds_bbig[h], st,
+                               f->fronts, f->tabb2 + 2 * f->boff2[h], F, (const S*)f->tinv, f->sidx, (const S*)w, x,
+                               f->err, f->backoff);
+        else if (f->nbig[h])
             hipLaunchKernelGGL((dev::mf_big_bwd_kernel<S>), dim3(f->bcnt[h]), dim3(256), f->lds_bbig[h], st, f->fronts,
                                f->tabb + 2 * f->boff[h], F, (const S*)f->tinv, f->sidx, (const S*)w, x, f->flags, eb,
                                f->err, f->backoff);

@@ -308,6 +308,34 @@ def test_multifrontal_block_row_solve_kernels(ctx, env, big, wave, flow, sub, in
     A.close()
 
 
+@pytest.mark.parametrize("nx,big,real", [(45, "1", False), (45, "1", True), (300, None, False), (120, "64", True)])
+def test_row_block_pairs_bitwise(ctx, env, nx, big, real):
+    """Two pivot blocks per workgroup (mf_big_fwd2 / bwd2_kernel, EIGSOL_MF_PAIR=1, opt-in) against
+    one per workgroup (=0, the default): the same sums in the same order, so the solutions are bitwise
+    equal — fronts with odd and even block counts, partial last blocks, struct rows, real and
+    complex."""
+    _mf_env(env)
+    env("EIGSOL_MF_LEAF", "24" if nx == 45 else "64")
+    if big is not None:
+        env("EIGSOL_MF_BIG_NS", big)
+    rp, ci, v = S.convdiff_complex(nx, seed=13)
+    if real:
+        v = np.ascontiguousarray(v.real)
+    n = nx * nx
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 8.5 if real else 3.0 - 0.2j   # real: outside the stencil's spectrum (0, 8), not next to an eigenvalue
+    b = S.start_vector(n, np.complex128 if not real else np.float64, seed=5)
+    ys = {}
+    for pair in ("0", "1"):
+        env("EIGSOL_MF_PAIR", pair)
+        assert _variant(A, sigma) == 19
+        ys[pair] = E.solve_shifted(A, sigma, b)
+    assert np.linalg.norm(M @ ys["1"] - sigma * ys["1"] - b) <= 1e-10 * np.linalg.norm(b) * max(1.0, np.linalg.norm(ys["1"]))
+    assert np.array_equal(ys["0"], ys["1"])
+    A.close()
+
+
 def test_single_precision_complex_default_is_multifrontal(ctx):
     """complex<float> past n = 16384 takes the GMRES family on values widened to double (the factor,
     residual check and refinement in double, the iterate in complex<float>): on the SuperLU fixture's
