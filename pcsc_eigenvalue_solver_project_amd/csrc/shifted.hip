@@ -94,7 +94,12 @@ struct ShiftFactor {
     void* pval = nullptr;
     void* ppiv = nullptr;
     int32_t chunk0 = 0;
-    int poll_fast = 0;            // tail polls without back-off (EIGSOL_TRSV_POLL_FAST)
+    // tail polls without back-off (EIGSOL_TRSV_POLL_FAST, low 16 bits) and the back-off schedule
+    // (EIGSOL_TRSV_POLL_SLOW, bits 16-18; poll_backoff).  Round 6 (tools/r06_trsv_backoff_ab.sh,
+    // profiles/r06_trsv_backoff_ab.log, config 5 at K = 4): sleeps of 2 / 8 / 32 x 64 cycles
+    // (growing with the spins) 0.4127-0.4134 ms per iteration; a constant 4 / 6 / 8 / 12 / 16:
+    // 0.4072-0.4083 (the long sleeps woke late); 32: 0.415.  Default: a constant 8
+    int poll_fast = 4 << 16;
     int poll_mode = 2;            // EIGSOL_TRSV_POLL_MODE (bit 0: slice tail, one re-poll per lane; bit 1: chunk tails, the second chunk's first polls after the first chunk: config 5 0.698 -> 0.674 ms, K = 4 0.419 -> 0.414)
     // multi-solve launches (sptrsv_chunk_role_kernel; EIGSOL_TRSV_MULTI=K, 1 disables): K reference
     // iterations per launch, solve j one dependency round behind solve j - 1
@@ -582,15 +587,36 @@ __global__ __launch_bounds__(kWHeadThreads) void sptrsv_whead_kernel(TriArgs<S> 
   }
 }
 
+// the chunk tails' back-off between re-polls of an unsolved value: pf = EIGSOL_TRSV_POLL_FAST in
+// the low 16 bits (re-polls without a sleep), EIGSOL_TRSV_POLL_SLOW in bits 16-18 (the sleep
+// schedule below, in units of 64 cycles: fewer re-poll requests against later wake-ups)
+__device__ __forceinline__ void poll_backoff(int spins, int pf) {
+    const int fast = pf & 0xffff, slow = pf >> 16;
+    if (spins < fast) return;         // re-poll at once: the value is due within a round trip
+    const int s = spins - fast;
+    const int step = s < 4 ? 0 : (s < 16 ? 1 : 2);
+    switch (slow * 3 + step) {        // s_sleep takes an immediate
+        case 0: __builtin_amdgcn_s_sleep(2); break;     // 0: 2 / 8 / 32
+        case 1: __builtin_amdgcn_s_sleep(8); break;
+        case 2: __builtin_amdgcn_s_sleep(32); break;
+        case 3: case 4: case 5: __builtin_amdgcn_s_sleep(4); break;       // 1: 4
+        case 6: case 7: case 8: __builtin_amdgcn_s_sleep(6); break;       // 2: 6
+        case 9: case 10: case 11: __builtin_amdgcn_s_sleep(16); break;    // 3: 16
+        case 12: case 13: case 14: __builtin_amdgcn_s_sleep(8); break;    // 4: 8
+        case 15: case 16: case 17: __builtin_amdgcn_s_sleep(32); break;   // 5: 32
+        case 18: case 19: case 20: __builtin_amdgcn_s_sleep(12); break;   // 6: 12
+        case 21: __builtin_amdgcn_s_sleep(16); break;   // 7: 16 / 24 / 32
+        case 22: __builtin_amdgcn_s_sleep(24); break;
+        default: __builtin_amdgcn_s_sleep(32); break;
+    }
+}
+
 // first poll of a dependency is issued early (ld_coh); this finishes the wait
 template <class S>
-__device__ __forceinline__ S finish_wait(S y, const S* z, int j, int32_t* err, int fast) {
+__device__ __forceinline__ S finish_wait(S y, const S* z, int j, int32_t* err, int pf) {
     int spins = 0;
     while (unready(y)) {
-        if (spins < fast) {}          // re-poll at once: the value is due within a round trip
-        else if (spins < fast + 4) __builtin_amdgcn_s_sleep(2);
-        else if (spins < fast + 16) __builtin_amdgcn_s_sleep(8);
-        else __builtin_amdgcn_s_sleep(32);
+        poll_backoff(spins, pf);
         y = ld_cohi(z, j);
         if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(err) != 0)) {
             atomicOr(err, 1);
@@ -681,8 +707,8 @@ __global__ __launch_bounds__(kThreads) void sptrsv_slice_kernel(TriArgs<S> a, in
         for (int k = 0; k < B; ++k) pend = pend || unready(z[k]);
         int spins = 0;
         while (pend) {
-            if (spins >= a.poll_fast) {
-                if (spins < a.poll_fast + 8) __builtin_amdgcn_s_sleep(2);
+            if (spins >= (a.poll_fast & 0xffff)) {
+                if (spins < (a.poll_fast & 0xffff) + 8) __builtin_amdgcn_s_sleep(2);
                 else __builtin_amdgcn_s_sleep(16);
             }
             if (!(a.poll_mode & 1)) {
@@ -920,9 +946,7 @@ __global__ __launch_bounds__(kThreads) void sptrsv_chunk_role_kernel(TriArgs<S> 
             S zv = m.j >= 0 ? z0 : s_zero<S>();
             int spins = 0;
             while (unready(zv) || (nb && unready(bv))) {
-                if (spins < 4) __builtin_amdgcn_s_sleep(2);
-                else if (spins < 16) __builtin_amdgcn_s_sleep(8);
-                else __builtin_amdgcn_s_sleep(32);
+                poll_backoff(spins, a.poll_fast & ~0xffff);
                 if (unready(zv)) zv = ld_cohi(zdep, m.j);
                 if (nb && unready(bv)) bv = ld_cohi(zrhs, m.i);
                 if ((++spins & 255) == 0 && (spins > kSpinLimit || ld_flag_err(a.err) != 0)) {
@@ -2386,7 +2410,10 @@ static int factor_tri_host(eigsol_ctx* ctx, int dtype, int64_t n, std::vector<in
             lmaxlen[l] = std::max(lmaxlen[l], orp[order[p] + 1] - orp[order[p]]);
     if (const char* e = std::getenv("EIGSOL_TRSV_HEAD")) f->wave_head = std::strcmp(e, "block") ? 1 : 0;
     f->hlevels = head_levels<S>(lstart, lcount, lmaxlen, f->nlevels, f->wave_head != 0);
-    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_FAST")) f->poll_fast = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_FAST"))
+        f->poll_fast = (f->poll_fast & ~0xffff) | std::min(0xffff, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_SLOW"))
+        f->poll_fast = (f->poll_fast & 0xffff) | (std::min(7, std::max(0, std::atoi(e))) << 16);
     if (const char* e = std::getenv("EIGSOL_TRSV_POLL_MODE")) f->poll_mode = std::atoi(e);
     f->hpos = (int32_t)lstart[f->hlevels];
     std::vector<int2> passes;
@@ -2723,7 +2750,10 @@ static int factor_tri_device(eigsol_csr* A, double sre, double sim, ShiftFactor*
     f->npos = (int32_t)lstart[nlevels];
     if (const char* e = std::getenv("EIGSOL_TRSV_HEAD")) f->wave_head = std::strcmp(e, "block") ? 1 : 0;
     f->hlevels = head_levels<S>(lstart, lcount, hmax, f->nlevels, f->wave_head != 0);
-    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_FAST")) f->poll_fast = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_FAST"))
+        f->poll_fast = (f->poll_fast & ~0xffff) | std::min(0xffff, std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("EIGSOL_TRSV_POLL_SLOW"))
+        f->poll_fast = (f->poll_fast & 0xffff) | (std::min(7, std::max(0, std::atoi(e))) << 16);
     if (const char* e = std::getenv("EIGSOL_TRSV_POLL_MODE")) f->poll_mode = std::atoi(e);
     f->hpos = (int32_t)lstart[f->hlevels];
     {   // tail variant: the rule of factor_tri_host
