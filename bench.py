@@ -715,7 +715,8 @@ def main():
     bootstrap = args.bootstrap
     if bootstrap == "auto":
         bootstrap = "host" if shared else "rccl"
-    if world > 1 and shared and bootstrap == "rccl":
+    if world > 1 and shared and bootstrap == "rccl" and os.environ.get("EIGSOL_BENCH_FORCE_RCCL") != "1":
+        # (EIGSOL_BENCH_FORCE_RCCL=1, tests only: let RCCL refuse them, exercising the host fallback)
         raise SystemExit("--bootstrap rccl with ranks sharing a GPU: RCCL refuses duplicate devices")
     torch.cuda.set_device(device)
 
@@ -736,10 +737,22 @@ def main():
     rp, ci, v = gen(kind, n_global, k, row0, rows)
     if world > 1:
         from pcsc_eigenvalue_solver_project_amd import dist as D
+        ctx = None
         if bootstrap == "rccl":
             # one communicator per rank owned by the library (RCCL over xGMI); gloo only ships the id
-            ctx = D.torch_dist_context(device, stream=torch_stream.cuda_stream)
-        else:
+            try:
+                ctx = D.torch_dist_context(device, stream=torch_stream.cuda_stream)
+            except E.EigSolError as e:
+                sys.stderr.write(f"[bench] rank {rank}: RCCL bootstrap failed ({e}); trying the host bootstrap\n")
+            # every rank takes the same bootstrap: RCCL only where all of them have a communicator
+            ok = torch.tensor([1 if ctx is not None else 0], dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok[0]) == 0:
+                if ctx is not None:
+                    ctx.close()
+                ctx = None
+                bootstrap = "host (RCCL bootstrap failed)"
+        if ctx is None:
             # set-up all-gathers over gloo; the exchange itself is the same device-side peer push
             ctx = D.torch_host_context(device, stream=torch_stream.cuda_stream)
         A = D.DistCsrMatrix(ctx, rb, rp, ci, v)

@@ -132,11 +132,20 @@ def torch_dist_context(device: int, stream=None) -> DistContext:
     import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
     n = lib().eigsol_dist_unique_id_bytes()
-    t = torch.zeros(n, dtype=torch.uint8)
+    # byte 0: rank 0 obtained the id (a failure there is reported on every rank instead of leaving
+    # the others in the broadcast)
+    t = torch.zeros(n + 1, dtype=torch.uint8)
+    why = ""
     if rank == 0:
-        t[:] = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
+        try:
+            t[1:] = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
+            t[0] = 1
+        except EigSolError as e:
+            why = str(e)
     dist.broadcast(t, src=0)
-    return DistContext(device, rank, world, bytes(t.numpy().tobytes()), stream=stream)
+    if int(t[0]) != 1:
+        raise EigSolError(8, "RCCL unique id unavailable on rank 0" + (": " + why if why else ""))
+    return DistContext(device, rank, world, bytes(t[1:].numpy().tobytes()), stream=stream)
 
 
 class DistCsrMatrix(CsrMatrix):

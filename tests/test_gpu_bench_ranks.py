@@ -12,6 +12,7 @@ the timed region; its lambda must be within 1e-10 (1 + |lambda|) of the unsharde
 """
 import json
 import os
+import signal
 import subprocess
 import sys
 import time
@@ -25,14 +26,22 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(args, devices):
+def _bench(args, devices, extra_env=None, timeout=110):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["EIGSOL_BENCH_DEVICES"] = devices
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.update(extra_env or {})
     t = time.perf_counter()
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=110)
-    return r, time.perf_counter() - t
+    # its own process group: on a timeout the launcher's rank processes go too
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        raise AssertionError("bench timed out: " + err[-3000:])
+    return subprocess.CompletedProcess(p.args, p.returncode, out, err), time.perf_counter() - t
 
 
 def test_bench_two_ranks_one_gpu_end_to_end():
@@ -77,3 +86,16 @@ def test_bench_one_rank_check_matches_sharded():
     ref = O.power_csc(cp, ri, vv, S.start_vector(n), 300, 1e-12)
     assert abs(d["check"]["eigenvalue"] - ref["eigenvalue"]) <= 1e-10 * (1 + abs(ref["eigenvalue"]))
     assert abs(d["check"]["iterations"] - ref["iterations"]) <= 1
+
+
+def test_bench_rccl_bootstrap_failure_falls_back_to_host():
+    """A rank set whose RCCL communicator cannot be built (here: two ranks on one GPU, which RCCL
+    refuses; EIGSOL_BENCH_FORCE_RCCL=1 lets bench.py try) agrees on the host bootstrap instead of
+    failing the run: the line reports it, the exchange is still the peer push."""
+    r, _ = _bench(["--gpus", "2", "--workload", "band1m", "--steps", "3", "--warmup", "1", "--no-extras",
+                   "--no-cpu-baseline", "--bootstrap", "rccl"], "0,0", {"EIGSOL_BENCH_FORCE_RCCL": "1"}, timeout=90)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-5000:]
+    d = json.loads([s for s in r.stdout.splitlines() if s.strip()][-1])
+    assert d["config"]["bootstrap"] == "host (RCCL bootstrap failed)"
+    assert d["config"]["communicator"]["transport_per_rank"] == ["peer", "peer"]
+    assert d["value"] > 0
