@@ -766,11 +766,38 @@ def main():
     x0 = S.start_vector(rows, np.float64, row0=row0)
     transport = sess.transport()
     opts = E.SolverOptions(2**31 - 1, -1.0)   # tol < 0: the reference loop never stops early
-    sess.begin(opts, x0)
+
+    def warm(s):
+        s.begin(opts, x0)
+        s.step(args.warmup)
+        torch.cuda.synchronize()
+        s.query()   # raises on a peer-wait fault (bounded waits: every rank gets here)
+
+    werr = None
+    try:
+        warm(sess)
+    except E.EigSolError as e:
+        werr = e
+    if world > 1:
+        # a device-side peer exchange that does not work between these GPUs (every wait is bounded,
+        # so all ranks return): all ranks rebuild the session on RCCL's collective exchange together
+        okt = torch.tensor([0 if werr is not None else 1], dtype=torch.int32)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        if int(okt[0]) == 0 and transport == 2 and bootstrap == "rccl":
+            sys.stderr.write(f"[bench] rank {rank}: peer exchange failed in the warm-up ({werr}); "
+                             "rebuilding the session on the collective transport\n")
+            sess.close()
+            os.environ["EIGSOL_DIST_TRANSPORT"] = "collective"
+            sess = E.PowerSession(A)
+            transport = sess.transport()
+            bootstrap = "rccl (peer exchange failed: collective transport)"
+            warm(sess)
+        elif int(okt[0]) == 0:
+            raise werr if werr is not None else SystemExit("another rank failed its warm-up")
+    elif werr is not None:
+        raise werr
     info = sess.kernel_info()
     kname = sess.kernel_name()
-    sess.step(args.warmup)
-    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
