@@ -2329,7 +2329,11 @@ static int tri_launch_setup(ShiftFactor* f) {
                         (size_t)K * (size_t)(f->hpos + 1) * sizeof(S) + 16 + static_lds <= (size_t)160 * 1024) ? 1 : 0;
         }
     }
-    int64_t red_cap = 1024;   // EIGSOL_TRSV_PART_GRID: A/B of the partials kernels' grid
+    // EIGSOL_TRSV_PART_GRID: the partials kernels' grid.  Round 6 (tools/r06_c5_partgrid_ab.sh,
+    // profiles/r06_c5_partgrid_ab.log, config 5 at K = 4): 2048 / 977 (n / 1024, the old cap) / 512 /
+    // 256 / 192 / 128 / 64 blocks -> 0.4077 / 0.4076 / 0.4026 / 0.4010 / 0.4016 / 0.4049 / 0.4159 ms per
+    // iteration: one block per CU, the last arriver sums fewer block partials per solve
+    int64_t red_cap = 256;
     if (const char* e = std::getenv("EIGSOL_TRSV_PART_GRID")) red_cap = std::max<int64_t>(8, std::atoll(e));
     // never above grid * kWaves: wave_part (below) holds that many block partials
     f->red_grid = (int)std::max<int64_t>(1, std::min<int64_t>(f->grid * dev::kWaves,
