@@ -436,6 +436,7 @@ struct CoopArgs {
     S* x0;              // a(j+1)
     unsigned* bar;      // barrier counter (zeroed by the host before the launch)
     int* err;
+    S* xu;              // kMerge: the column below row j + 1 before normalisation (n scalars)
 };
 
 __device__ __forceinline__ unsigned ld_agent_u32(const unsigned* p) {
@@ -457,7 +458,15 @@ __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned& target, in
     __syncthreads();
 }
 
-template <class S, int kCoopRowsPerLane>
+// kMerge (default; EIGSOL_HESS_MERGE=0: off): two grid barriers per column instead of three.  P2 also publishes
+// the updated column below row j + 1 unnormalised (xu) with the partials of V^H over those rows;
+// after its barrier every block forms the reflector from the reduced norm, scales xu into the GEMV's
+// v on the fly, and t = V^H v = rv (conj(V(j+1, :)) v0 + the reduced partials) - no barrier between
+// the reflector and the GEMV.  V(:, i) is then stored by each block for its own rows after that
+// barrier, so the next column's P1 takes the one entry it reads from another block, V(j + 1, i),
+// from the block's own copy (every block forms rv v0 itself).  The same reflectors; t and T round
+// differently.
+template <class S, int kCoopRowsPerLane, bool kMerge = false>
 __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
     constexpr int NB = HessCfg<S>::NB;
     extern __shared__ double vsh_raw[];      // v (n scalars) for the GEMV
@@ -470,6 +479,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
     __shared__ S s_scal[3];
     __shared__ double s_rv;
     __shared__ int s_sk;
+    __shared__ S s_vrow;   // kMerge: V(j + 1, i) of the previous column (rv v0, or 0 when skipped)
     // Block partials of another phase: all threads load them at once (independent sc1 loads),
     // then thread c sums column c in block order (deterministic).
     auto gather = [&](const S* src, int cnt, S* dst) {
@@ -501,7 +511,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
     for (int i = 0; i < a.nbp; ++i) {
         const int j = k + i;
         // ---------------- P1
-        if (tid < i) sv[tid] = cj(ld_ag(&a.V[j + (int64_t)tid * n]));
+        if (tid < i) sv[tid] = cj((kMerge && tid == i - 1) ? s_vrow : ld_ag(&a.V[j + (int64_t)tid * n]));
         __syncthreads();
         if (wv == 0)
             for (int q = 0; q < kCoopRowsPerLane; ++q) {
@@ -524,94 +534,192 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
             if (lane == 0) st_ag(&a.part[grp * NB + c], p);
         }
         grid_barrier(a.bar, target, a.err);
-        // ---------------- P2
-        gather(a.part, i, sw);
-        if (tid < i) {
-            S s = s_zero<S>();
-            for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(Tl[c + tid * NB]), sw[c]));   // (T^H w)_tid
-            st[tid] = s;
-        }
-        __syncthreads();
-        double tl = 0.0;
-        if (wv == 0)
-            for (int q = 0; q < kCoopRowsPerLane; ++q) {
-                const int r = r0 + lane + 64 * q;
-                if (r < r1) {
-                    S x = xs[lane + 64 * q];
-                    if (r >= k + 1)
-                        for (int c = 0; c < i; ++c) x = sub(x, mul(a.V[r + (int64_t)c * n], st[c]));
-                    xs[lane + 64 * q] = x;
-                    if (r >= j + 2) tl += sq_abs(x);
-                    if (r == j + 1) st_ag(a.x0, x);
+        bool sk;
+        if constexpr (kMerge) {
+            // ---------------- P2 (merged): left update, norm partials, x0, xu, partials of V^H xu
+            gather(a.part, i, sw);
+            if (tid < i) {
+                S s = s_zero<S>();
+                for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(Tl[c + tid * NB]), sw[c]));   // (T^H w)_tid
+                st[tid] = s;
+            }
+            __syncthreads();
+            double tl = 0.0;
+            if (wv == 0)
+                for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                    const int r = r0 + lane + 64 * q;
+                    if (r < r1) {
+                        S x = xs[lane + 64 * q];
+                        if (r >= k + 1)
+                            for (int c = 0; c < i; ++c) x = sub(x, mul(a.V[r + (int64_t)c * n], st[c]));
+                        xs[lane + 64 * q] = x;
+                        if (r >= j + 2) {
+                            tl += sq_abs(x);
+                            st_ag(&a.xu[r], x);
+                        }
+                        if (r == j + 1) st_ag(a.x0, x);
+                    }
+                }
+            if (wv == 0) {
+                tl = wave_sum(tl);
+                if (lane == 0) st_agent(&a.tpart[grp], tl);
+            }
+            __syncthreads();
+            for (int c = wv; c < i; c += 16) {
+                S p = s_zero<S>();
+                for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                    const int r = r0 + lane + 64 * q;
+                    if (r < r1 && r >= j + 2) p = add(p, mul(cj(a.V[r + (int64_t)c * n]), xs[lane + 64 * q]));
+                }
+                p = wsum(p);
+                if (lane == 0) st_ag(&a.part[(G + grp) * NB + c], p);
+            }
+            grid_barrier(a.bar, target, a.err);
+            // ---------------- P3 + P4: reflector (every block), own rows of V and the reduced column,
+            // v for the GEMV from xu, t from the reduced partials
+            double* redd = reinterpret_cast<double*>(red);
+            if (tid < G) redd[tid] = ld_agent(&a.tpart[tid]);
+            __syncthreads();
+            if (tid == 0) {
+                double tail = 0.0;
+                for (int b = 0; b < G; ++b) tail += redd[b];
+                const S x0 = ld_ag(a.x0);
+                bool skr;
+                S v0, alpha;
+                double rv;
+                hess_reflector(x0, tail, skr, v0, rv, alpha);
+                s_sk = skr ? 1 : 0;
+                s_scal[1] = v0;
+                s_rv = rv;
+                s_scal[2] = alpha;
+                s_vrow = skr ? s_zero<S>() : scal(v0, rv);
+            }
+            __syncthreads();
+            sk = s_sk != 0;
+            const S v0 = s_scal[1], alpha = s_scal[2];
+            const double rv = s_rv;
+            if (wv == 0)
+                for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                    const int r = r0 + lane + 64 * q;
+                    if (r < r1) {
+                        const S x = xs[lane + 64 * q];
+                        S v = s_zero<S>();
+                        if (!sk && r > j) v = scal(r == j + 1 ? v0 : x, rv);
+                        st_ag(&a.V[r + (int64_t)i * n], v);
+                        S red_col = x;
+                        if (!sk && r == j + 1) red_col = alpha;
+                        if (!sk && r > j + 1) red_col = s_zero<S>();
+                        a.A[r + (int64_t)j * n] = red_col;
+                    }
+                }
+            // v into LDS for every row: zero above row j + 1, rv v0 at j + 1, rv xu below
+            for (int rb = tid; rb < n; rb += 4 * kCoopThreads) {
+                S t4[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) t4[u] = ld_ag(&a.xu[min(max(rb + u * kCoopThreads, j + 2), n - 1)]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int r = rb + u * kCoopThreads;
+                    if (r < n) vsh[r] = (sk || r <= j) ? s_zero<S>() : scal(r == j + 1 ? v0 : t4[u], rv);
                 }
             }
-        if (wv == 0) {
-            tl = wave_sum(tl);
-            if (lane == 0) st_agent(&a.tpart[grp], tl);
-        }
-        grid_barrier(a.bar, target, a.err);
-        // ---------------- P3
-        double* redd = reinterpret_cast<double*>(red);
-        if (tid < G) redd[tid] = ld_agent(&a.tpart[tid]);
-        __syncthreads();
-        if (tid == 0) {
-            double tail = 0.0;
-            for (int b = 0; b < G; ++b) tail += redd[b];
-            const S x0 = ld_ag(a.x0);
-            bool sk;
-            S v0, alpha;
-            double rv;
-            hess_reflector(x0, tail, sk, v0, rv, alpha);
-            s_sk = sk ? 1 : 0;
-            s_scal[1] = v0;
-            s_rv = rv;
-            s_scal[2] = alpha;
-        }
-        __syncthreads();
-        const bool sk = s_sk != 0;
-        const S v0 = s_scal[1], alpha = s_scal[2];
-        const double rv = s_rv;
-        if (wv == 0)
-            for (int q = 0; q < kCoopRowsPerLane; ++q) {
-                const int r = r0 + lane + 64 * q;
-                if (r < r1) {
-                    const S x = xs[lane + 64 * q];
-                    S v = s_zero<S>();
-                    if (!sk && r > j) v = scal(r == j + 1 ? v0 : x, rv);
-                    st_ag(&a.V[r + (int64_t)i * n], v);
-                    xs[lane + 64 * q] = v;           // keep v for the t partials
-                    S red_col = x;
-                    if (!sk && r == j + 1) red_col = alpha;
-                    if (!sk && r > j + 1) red_col = s_zero<S>();
-                    a.A[r + (int64_t)j * n] = red_col;
+            __syncthreads();
+            gather(a.part + (size_t)G * NB, i, sv);
+            if (tid < i) {
+                const S u = add(mul(cj(ld_ag(&a.V[(j + 1) + (int64_t)tid * n])), v0), sv[tid]);
+                sv[tid] = sk ? s_zero<S>() : scal(u, rv);
+            }
+            __syncthreads();
+        } else {
+            // ---------------- P2
+            gather(a.part, i, sw);
+            if (tid < i) {
+                S s = s_zero<S>();
+                for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(Tl[c + tid * NB]), sw[c]));   // (T^H w)_tid
+                st[tid] = s;
+            }
+            __syncthreads();
+            double tl = 0.0;
+            if (wv == 0)
+                for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                    const int r = r0 + lane + 64 * q;
+                    if (r < r1) {
+                        S x = xs[lane + 64 * q];
+                        if (r >= k + 1)
+                            for (int c = 0; c < i; ++c) x = sub(x, mul(a.V[r + (int64_t)c * n], st[c]));
+                        xs[lane + 64 * q] = x;
+                        if (r >= j + 2) tl += sq_abs(x);
+                        if (r == j + 1) st_ag(a.x0, x);
+                    }
                 }
+            if (wv == 0) {
+                tl = wave_sum(tl);
+                if (lane == 0) st_agent(&a.tpart[grp], tl);
             }
-        __syncthreads();
-        for (int c = wv; c < i; c += 16) {
-            S p = s_zero<S>();
-            for (int q = 0; q < kCoopRowsPerLane; ++q) {
-                const int r = r0 + lane + 64 * q;
-                if (r < r1) p = add(p, mul(cj(a.V[r + (int64_t)c * n]), xs[lane + 64 * q]));
+            grid_barrier(a.bar, target, a.err);
+            // ---------------- P3
+            double* redd = reinterpret_cast<double*>(red);
+            if (tid < G) redd[tid] = ld_agent(&a.tpart[tid]);
+            __syncthreads();
+            if (tid == 0) {
+                double tail = 0.0;
+                for (int b = 0; b < G; ++b) tail += redd[b];
+                const S x0 = ld_ag(a.x0);
+                bool sk;
+                S v0, alpha;
+                double rv;
+                hess_reflector(x0, tail, sk, v0, rv, alpha);
+                s_sk = sk ? 1 : 0;
+                s_scal[1] = v0;
+                s_rv = rv;
+                s_scal[2] = alpha;
             }
-            p = wsum(p);
-            if (lane == 0) st_ag(&a.part[(G + grp) * NB + c], p);
+            __syncthreads();
+            sk = s_sk != 0;
+            const S v0 = s_scal[1], alpha = s_scal[2];
+            const double rv = s_rv;
+            if (wv == 0)
+                for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                    const int r = r0 + lane + 64 * q;
+                    if (r < r1) {
+                        const S x = xs[lane + 64 * q];
+                        S v = s_zero<S>();
+                        if (!sk && r > j) v = scal(r == j + 1 ? v0 : x, rv);
+                        st_ag(&a.V[r + (int64_t)i * n], v);
+                        xs[lane + 64 * q] = v;           // keep v for the t partials
+                        S red_col = x;
+                        if (!sk && r == j + 1) red_col = alpha;
+                        if (!sk && r > j + 1) red_col = s_zero<S>();
+                        a.A[r + (int64_t)j * n] = red_col;
+                    }
+                }
+            __syncthreads();
+            for (int c = wv; c < i; c += 16) {
+                S p = s_zero<S>();
+                for (int q = 0; q < kCoopRowsPerLane; ++q) {
+                    const int r = r0 + lane + 64 * q;
+                    if (r < r1) p = add(p, mul(cj(a.V[r + (int64_t)c * n]), xs[lane + 64 * q]));
+                }
+                p = wsum(p);
+                if (lane == 0) st_ag(&a.part[(G + grp) * NB + c], p);
+            }
+            grid_barrier(a.bar, target, a.err);
+            // ---------------- P4
+            // v into LDS: four independent coherent loads per thread in flight (clamped rows, so no
+            // predicated load waits for the one before it)
+            for (int rb = tid; rb < n; rb += 4 * kCoopThreads) {
+                S t4[4];
+    #pragma unroll
+                for (int u = 0; u < 4; ++u) t4[u] = ld_ag(&a.V[min(rb + u * kCoopThreads, n - 1) + (int64_t)i * n]);
+    #pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (rb + u * kCoopThreads < n) vsh[rb + u * kCoopThreads] = sk ? s_zero<S>() : t4[u];
+            }
+            __syncthreads();
+            gather(a.part + (size_t)G * NB, i, sv);
+            if (sk && tid < i) sv[tid] = s_zero<S>();
+            __syncthreads();
         }
-        grid_barrier(a.bar, target, a.err);
-        // ---------------- P4
-        // v into LDS: four independent coherent loads per thread in flight (clamped rows, so no
-        // predicated load waits for the one before it)
-        for (int rb = tid; rb < n; rb += 4 * kCoopThreads) {
-            S t4[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) t4[u] = ld_ag(&a.V[min(rb + u * kCoopThreads, n - 1) + (int64_t)i * n]);
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (rb + u * kCoopThreads < n) vsh[rb + u * kCoopThreads] = sk ? s_zero<S>() : t4[u];
-        }
-        __syncthreads();
-        gather(a.part + (size_t)G * NB, i, sv);
-        if (sk && tid < i) sv[tid] = s_zero<S>();
-        __syncthreads();
         S yacc[kCoopRowsPerLane];
 #pragma unroll
         for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] = s_zero<S>();
@@ -995,9 +1103,21 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
     EIGSOL_HIP(hipDeviceGetAttribute(&coop_ok, hipDeviceAttributeCooperativeLaunch, dev_id));
     bool coop = coop_ok && n <= Cfg::kCoopMaxN && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
     const size_t coop_lds = (size_t)n * sizeof(S);
-    const void* coop_kernel = n <= 64 * dev::kCoopBlocks ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1>)
-                                                         : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 2>);
-    S *part = nullptr, *x0s = nullptr;
+    // two grid barriers per panel column (hess_panel_coop kMerge; EIGSOL_HESS_MERGE=0: three).  Round 6
+    // (tools/r06_hess_merge_ab.sh, profiles/r06_hess_merge_ab.log): to_hessenberg 4096^2 0.184 / 0.185 ->
+    // 0.182 / 0.176 s; QR 4096^2 unchanged within noise (0.885 / 0.885 against 0.888 / 0.882 s), complex
+    // 1.551 -> 1.545 s; eigenvalues one-to-one with the LAPACK fixtures
+    static const bool merge = [] {
+        const char* e = std::getenv("EIGSOL_HESS_MERGE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    const void* coop_kernel =
+        n <= 64 * dev::kCoopBlocks
+            ? (merge ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1, true>)
+                     : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1>))
+            : (merge ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 2, true>)
+                     : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 2>));
+    S *part = nullptr, *x0s = nullptr, *xu = nullptr;
     double* tpart = nullptr;
     unsigned* bar = nullptr;
     int* err = nullptr;
@@ -1005,6 +1125,7 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         EIGSOL_HIP(hipMalloc(&part, 2 * dev::kCoopBlocks * NB * sizeof(S)));
         EIGSOL_HIP(hipMalloc(&tpart, dev::kCoopBlocks * sizeof(double)));
         EIGSOL_HIP(hipMalloc(&x0s, 64));
+        EIGSOL_HIP(hipMalloc(&xu, (size_t)n * sizeof(S)));
         EIGSOL_HIP(hipMalloc(&bar, 64));
         EIGSOL_HIP(hipMalloc(&err, 64));
         EIGSOL_HIP(hipMemsetAsync(err, 0, 64, st));
@@ -1018,7 +1139,7 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         EIGSOL_HIP(hipMemsetAsync(T, 0, NB * NB * sizeof(S), st));
         if (coop) {
             EIGSOL_HIP(hipMemsetAsync(bar, 0, 64, st));
-            dev::CoopArgs<S> ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err};
+            dev::CoopArgs<S> ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err, xu};
             void* kargs[] = {&ca};
             // EIGSOL_HESS_COOP_PLAIN=1: the SAME panel kernel through an ordinary launch, for profiling
             // only (rocprofv3 7.2 crashes at exit after any cooperative launch, tools/coop_prof_repro.hip);
@@ -1082,7 +1203,7 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         EIGSOL_HIP(hipStreamSynchronize(st));
     }
     for (void* p : {(void*)V, (void*)L, (void*)R, (void*)M, (void*)T, (void*)tv, (void*)yp, (void*)W, (void*)skip,
-                    (void*)part, (void*)tpart, (void*)x0s, (void*)bar, (void*)err, (void*)SK})
+                    (void*)part, (void*)tpart, (void*)x0s, (void*)xu, (void*)bar, (void*)err, (void*)SK})
         if (p) (void)hipFree(p);
     if (errh) return fail(EIGSOL_E_HIP, "blocked Hessenberg: grid barrier timed out (internal error)");
     return EIGSOL_OK;
