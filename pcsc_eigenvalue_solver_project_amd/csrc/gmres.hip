@@ -35,6 +35,7 @@
 #include <cstdio>
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -390,50 +391,114 @@ static int gmres_create_t(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* 
     S sig;
     if constexpr (std::is_same_v<S, double>) { (void)sim; sig = sre; }
     else sig = S{sre, sim};
+    // built on the host threads (rows in contiguous chunks): the same arrays and row sums as a serial
+    // pass; the column sums are formed per row chunk and then added chunk by chunk, so ||M||_1 can
+    // differ from a serial sum in its last bits (it only scales the direct solve's acceptance test).
+    // 1M general-sparse matrix: 0.28 -> 0.10 s (round 6, tools/r06_buildM_ab.py: solutions bitwise
+    // the serial build's)
     std::vector<int32_t> mrp(n + 1, 0), mci, dpos(n);
     std::vector<S> mv;
-    mci.reserve(rp[n] + n);
-    mv.reserve(rp[n] + n);
-    for (int64_t i = 0; i < n; ++i) {
-        bool have = false;
-        for (int32_t e = rp[i]; e <= rp[i + 1]; ++e) {
-            const bool end = e == rp[i + 1];
-            if (!have && (end || ci[e] > i)) {   // diagonal slot before the first column past i
-                dpos[i] = (int32_t)mci.size();
-                mci.push_back((int32_t)i);
-                mv.push_back(h_sub(s_zero<S>(), sig));
-                have = true;
-            }
-            if (end) break;
-            if (ci[e] == i) {
-                dpos[i] = (int32_t)mci.size();
-                mci.push_back((int32_t)i);
-                mv.push_back(h_sub(v[e], sig));
-                have = true;
-            } else {
-                mci.push_back(ci[e]);
-                mv.push_back(v[e]);
-            }
+    const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    auto par = [&](int64_t cnt, auto fn) {   // fn(t, begin, end) over nth contiguous chunks
+        const int T = cnt < 65536 ? 1 : nth;
+        const int64_t ch = (cnt + T - 1) / T;
+        std::vector<std::thread> th;
+        int t = 1;
+        try {
+            for (; t < T; ++t) th.emplace_back(fn, t, std::min(cnt, t * ch), std::min(cnt, (t + 1) * ch));
+        } catch (const std::exception&) {
         }
-        mrp[i + 1] = (int32_t)mci.size();
-    }
-    g->nnzM = (int64_t)mci.size();
-    {
-        std::vector<double> colsum(n, 0.0);
+        for (int r = t; r < T; ++r) fn(r, std::min(cnt, r * ch), std::min(cnt, (r + 1) * ch));
+        fn(0, (int64_t)0, std::min(cnt, ch));
+        for (auto& x : th) x.join();
+        return T;
+    };
+    par(n, [&](int, int64_t b, int64_t e) {   // row lengths of M: a missing diagonal is inserted
+        for (int64_t r = b; r < e; ++r) {
+            bool has = false;
+            for (int32_t q = rp[r]; q < rp[r + 1]; ++q) has = has || ci[q] == r;
+            mrp[r + 1] = rp[r + 1] - rp[r] + (has ? 0 : 1);
+        }
+    });
+    for (int64_t r = 0; r < n; ++r) mrp[r + 1] += mrp[r];
+    g->nnzM = mrp[n];
+    mci.resize(g->nnzM);
+    mv.resize(g->nnzM);
+    std::unique_ptr<double[]> am(new double[g->nnzM]);    // |m_e|
+    std::vector<double> rmaxs(nth, 0.0);
+    par(n, [&](int t, int64_t b, int64_t e) {
         double rmax = 0.0;
-        for (int64_t i = 0; i < n; ++i) {
-            double rs = 0.0;
-            for (int32_t e = mrp[i]; e < mrp[i + 1]; ++e) {
-                double a;
-                if constexpr (std::is_same_v<S, double>) a = std::fabs(mv[e]);
-                else a = std::hypot(mv[e].re, mv[e].im);
-                rs += a;
-                colsum[mci[e]] += a;
+        for (int64_t i = b; i < e; ++i) {
+            int32_t o = mrp[i];
+            bool have = false;
+            auto put = [&](int32_t c, S val) {
+                mci[o] = c;
+                mv[o] = val;
+                if constexpr (std::is_same_v<S, double>) am[o] = std::fabs(val);
+                else am[o] = std::hypot(val.re, val.im);
+                ++o;
+            };
+            for (int32_t q = rp[i]; q <= rp[i + 1]; ++q) {
+                const bool end = q == rp[i + 1];
+                if (!have && (end || ci[q] > i)) {   // diagonal slot before the first column past i
+                    dpos[i] = o;
+                    put((int32_t)i, h_sub(s_zero<S>(), sig));
+                    have = true;
+                }
+                if (end) break;
+                if (ci[q] == i) {
+                    dpos[i] = o;
+                    put((int32_t)i, h_sub(v[q], sig));
+                    have = true;
+                } else {
+                    put(ci[q], v[q]);
+                }
             }
+            double rs = 0.0;
+            for (int32_t q = mrp[i]; q < mrp[i + 1]; ++q) rs += am[q];
             rmax = std::max(rmax, rs);
         }
-        g->normM = rmax;
-        for (double c : colsum) g->normM = std::max(g->normM, c);
+        rmaxs[t] = rmax;
+    });
+    {
+        // column sums: each thread sums its row chunk into its own column array, the arrays are then
+        // added column by column in thread order (at most 512 MB of them)
+        const int T = (int)std::max<int64_t>(1, std::min<int64_t>(n < 65536 ? 1 : nth, ((int64_t)1 << 29) / (8 * std::max<int64_t>(n, 1))));
+        std::vector<std::vector<double>> cs(T);
+        const int64_t rch = (n + T - 1) / T;
+        auto rows = [&](int t) {
+            cs[t].assign(n, 0.0);
+            const int64_t b = std::min<int64_t>(n, t * rch), e = std::min<int64_t>(n, (t + 1) * rch);
+            for (int64_t q = mrp[b]; q < mrp[e]; ++q) cs[t][mci[q]] += am[q];
+        };
+        std::vector<double> cmaxs(T, 0.0);
+        const int64_t cw = (n + T - 1) / T;
+        auto cols = [&](int t) {
+            const int64_t lo = std::min<int64_t>(n, t * cw), hi = std::min<int64_t>(n, (t + 1) * cw);
+            double m = 0.0;
+            for (int64_t c = lo; c < hi; ++c) {
+                double sum = 0.0;
+                for (int u = 0; u < T; ++u) sum += cs[u][c];
+                m = std::max(m, sum);
+            }
+            cmaxs[t] = m;
+        };
+        auto run = [&](auto& fn) {
+            std::vector<std::thread> th;
+            int t = 1;
+            try {
+                for (; t < T; ++t) th.emplace_back([&fn, t] { fn(t); });
+            } catch (const std::exception&) {
+            }
+            for (int r = t; r < T; ++r) fn(r);
+            fn(0);
+            for (auto& x : th) x.join();
+        };
+        run(rows);
+        run(cols);
+        g->normM = 0.0;
+        for (double r : rmaxs) g->normM = std::max(g->normM, r);
+        for (double c : cmaxs) g->normM = std::max(g->normM, c);
     }
     lap("build M");
     // products with M: on the caller's device matrix A when it is given (M x = A x - sigma x; round
