@@ -152,6 +152,54 @@ __global__ __launch_bounds__(kT) void power_fused_kernel(int64_t n, const int32_
         for (int q = 0; q < 3; ++q) part[3 * blockIdx.x + q] = acc[q];
 }
 
+// Two-phase variant (EIGSOL_DD_FUSED2, default): the per-row epilogue (two double-double divisions,
+// |z|^2 and conj(x) z: most of a row's instructions) ran on one lane of every group of G, i.e. at
+// 1 / G of the wave.  Here a block first forms the row sums of kT rows (G passes of kT / G rows, G
+// lanes per row, the same strided order and butterfly) into LDS, then every thread finishes one row:
+// the same x and z values, the partials summed per thread over its rows (a different order).
+template <class T, int G>
+__global__ __launch_bounds__(kT) void power_fused2_kernel(int64_t n, const int32_t* __restrict__ rp,
+                                                          const int32_t* __restrict__ ci, const T* __restrict__ val,
+                                                          const T* __restrict__ y, dd nrm, T* __restrict__ x,
+                                                          T* __restrict__ z, dd* __restrict__ part) {
+    using O = wide_ops<T>;
+    __shared__ dd sm[3 * 16];
+    __shared__ T srow[kT];
+    constexpr int RB = kT / G;   // rows per pass
+    const int g = threadIdx.x % G, r = threadIdx.x / G;
+    dd acc[3] = {dd{0.0, 0.0}, dd{0.0, 0.0}, dd{0.0, 0.0}};
+    for (int64_t base = (int64_t)blockIdx.x * kT; base < n; base += (int64_t)gridDim.x * kT) {
+#pragma unroll
+        for (int p = 0; p < G; ++p) {
+            const int64_t i = base + p * RB + r;
+            T sum = O::zero();
+            if (i < n) {
+                const int32_t e1 = rp[i + 1];
+                for (int32_t e = rp[i] + g; e < e1; e += G) sum = O::add(sum, O::mul(val[e], y[ci[e]]));
+            }
+#pragma unroll
+            for (int off = G / 2; off > 0; off >>= 1) sum = O::add(sum, shfl_w<T>(sum, off));
+            if (g == 0) srow[p * RB + r] = sum;
+        }
+        __syncthreads();
+        const int64_t i = base + threadIdx.x;
+        if (i < n) {
+            const T xi = O::div_r(y[i], nrm);
+            const T zi = O::div_r(srow[threadIdx.x], nrm);
+            x[i] = xi;
+            z[i] = zi;
+            acc[0] = dd_add(acc[0], O::abs2(zi));
+            const T pr = O::mul(O::conj(xi), zi);
+            acc[1] = dd_add(acc[1], O::real(pr));
+            acc[2] = dd_add(acc[2], O::imag(pr));
+        }
+        __syncthreads();
+    }
+    block_sum<3>(acc, sm);
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 3; ++q) part[3 * blockIdx.x + q] = acc[q];
+}
+
 // out[q] = sum of the nb block partials part[3 b + q] (thread t: blocks t, t + kT, ... in order, then
 // the block sum in wave order): deterministic for a given nb
 __global__ __launch_bounds__(kT) void sum3_kernel(const dd* __restrict__ part, int nb, dd* __restrict__ out) {
@@ -699,6 +747,10 @@ static int power_fused(WideSession* s, dd nrm, dd& n2, cdd& dot) {
     eigsol_csr* A = s->csr;
     const double avg = s->n ? (double)A->nnz / (double)s->n : 0.0;
     if (!s->fpart) EIGSOL_HIP(hipMalloc(&s->fpart, (3 * (size_t)kFusedBlocks + 3) * sizeof(dd)));
+    static const bool two = [] {
+        const char* e = std::getenv("EIGSOL_DD_FUSED2");
+        return !(e && std::atoi(e) == 0);
+    }();
     unsigned g = 1;
     auto go = [&](auto gtag) {
         constexpr int G = decltype(gtag)::value;
@@ -706,14 +758,31 @@ static int power_fused(WideSession* s, dd nrm, dd& n2, cdd& dot) {
             const char* e = std::getenv("EIGSOL_DD_BLOCKS");
             return e ? std::max<int64_t>(1, std::min<int64_t>(kFusedBlocks, std::atoll(e))) : (int64_t)2048;
         }();
-        g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cap, (s->n + wdev::kT / G - 1) / (wdev::kT / G)));
-        hipLaunchKernelGGL((wdev::power_fused_kernel<T, G>), dim3(g), dim3(wdev::kT), 0, st, s->n, A->rowptr, A->col,
-                           static_cast<const T*>(A->val), static_cast<const T*>(s->y), nrm, static_cast<T*>(s->x),
-                           static_cast<T*>(s->z), s->fpart);
+        // EIGSOL_DD_FUSED2=0: the one-phase kernel (the row epilogue on one lane of G)
+        const int64_t rows = two ? wdev::kT : wdev::kT / G;   // rows per block tile
+        g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cap, (s->n + rows - 1) / rows));
+        if (two)
+            hipLaunchKernelGGL((wdev::power_fused2_kernel<T, G>), dim3(g), dim3(wdev::kT), 0, st, s->n, A->rowptr,
+                               A->col, static_cast<const T*>(A->val), static_cast<const T*>(s->y), nrm,
+                               static_cast<T*>(s->x), static_cast<T*>(s->z), s->fpart);
+        else
+            hipLaunchKernelGGL((wdev::power_fused_kernel<T, G>), dim3(g), dim3(wdev::kT), 0, st, s->n, A->rowptr,
+                               A->col, static_cast<const T*>(A->val), static_cast<const T*>(s->y), nrm,
+                               static_cast<T*>(s->x), static_cast<T*>(s->z), s->fpart);
     };
-    if (avg <= 6.0) go(std::integral_constant<int, 4>{});
-    else if (avg <= 12.0) go(std::integral_constant<int, 8>{});
-    else if (avg <= 24.0) go(std::integral_constant<int, 16>{});
+    static const int force_g = [] {   // EIGSOL_DD_G: lanes per row (2 / 4 / 8 / 16 / 32), A/B only
+        const char* e = std::getenv("EIGSOL_DD_G");
+        return e ? std::atoi(e) : 0;
+    }();
+    // lanes per row from the mean row length.  Two-phase kernel (round 6, tools/r06_dd_power_prof.py,
+    // band matrices of 1M rows): 4 entries per row G = 2 / 4: 0.057 / 0.059 ms; 10: G = 2 / 4 / 8
+    // 0.137 / 0.080 / 0.091 ms; 32: G = 4 / 8 / 16 0.228 / 0.178 / 0.197 ms; 64: G = 8 / 16 / 32
+    // 0.300 / 0.304 / 0.421 ms (profiles/r06_dd_power_ab.log)
+    const double lim[4] = {two ? 5.0 : 0.0, two ? 20.0 : 6.0, two ? 48.0 : 12.0, two ? 96.0 : 24.0};
+    if (force_g == 2 || (!force_g && avg <= lim[0])) go(std::integral_constant<int, 2>{});
+    else if (force_g == 4 || (!force_g && avg <= lim[1])) go(std::integral_constant<int, 4>{});
+    else if (force_g == 8 || (!force_g && avg <= lim[2])) go(std::integral_constant<int, 8>{});
+    else if (force_g == 16 || (!force_g && avg <= lim[3])) go(std::integral_constant<int, 16>{});
     else go(std::integral_constant<int, 32>{});
     EIGSOL_HIP(hipGetLastError());
     hipLaunchKernelGGL(wdev::sum3_kernel, dim3(1), dim3(wdev::kT), 0, st, s->fpart, (int)g,
