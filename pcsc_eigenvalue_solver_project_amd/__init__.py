@@ -378,7 +378,7 @@ class PowerSession:
                      "solve j one dependency round behind solve j-1)",
                  14: "sptrsv multi-solve kernel (sync-free triangular solves, 4 iterations per launch, "
                      "solve j one dependency round behind solve j-1)",
-                 15: "wide power_fused_kernel (double-double: x = y / normY, A x and the norm / Rayleigh partials in one pass, 4-32 lanes per row)",
+                 15: "wide power_fused2_kernel (double-double: x = y / normY, A x and the norm / Rayleigh partials in one pass; a tile's row sums by 2-32 lanes per row into LDS, then one row's epilogue per thread)",
                  16: "wide gemv kernels (double-double dense product)",
                  17: "wide shifted inverse (fp64 factor + double-double residual refinement; "
                      "tiles = refinement steps of the last solve)",
