@@ -289,6 +289,8 @@ struct GmresSolver {
     int64_t nnzK = 0;           // entries of the factored pattern
     double last_bytes = 0.0;
     double last_relres = 0.0;
+    bool lag_pending = false;   // a lagged direct solve whose check (lagpin) is still to be read
+    int64_t lag_off() const { return 4 * (int64_t)m + 6; }   // its slot in hpin, past the cycles' use
 };
 
 void gmres_free(GmresSolver* g) {
@@ -1026,6 +1028,82 @@ static int gmres_solve_t(GmresSolver* g, const S* b, double bdiv, S* y, const do
         return fail(EIGSOL_E_SOLVER, msg);
     }
     return EIGSOL_OK;
+}
+
+// The shifted inverse iteration's direct solve with its check lagged (gmres_solve_lag): y = K^-1 (b /
+// bdiv), then the true residual r = b / bdiv - M y and ||b / bdiv||, ||r||, ||y|| reduced and copied to
+// the pinned slot without a host wait; the session reads them at its next decision wait
+// (gmres_lag_verdict) and redoes the iteration with the checked solve if they miss the test.  Only
+// for a complete factor without static pivots (the solve itself is then the reference's).
+template <class S>
+static int gmres_solve_lag_t(GmresSolver* g, const S* b, double bdiv, S* y) {
+    hipStream_t st = g->ctx->stream;
+    const int64_t n = g->n;
+    const int gb = (int)std::min<int64_t>(2048, (n + dev::kThreads - 1) / dev::kThreads);
+    S* w = static_cast<S*>(g->w);
+    S* t1 = static_cast<S*>(g->t1);
+    hipLaunchKernelGGL((dev::gm_resid_kernel<S>), dim3(gb), dim3(dev::kThreads), 0, st, b, bdiv, (const S*)nullptr, w, n);
+    hipLaunchKernelGGL((dev::gm_dots_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, w, n, 1, w, n, g->part);
+    hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(1), dim3(dev::kThreads), 0, st, g->part, g->G, 1, g->hdev);
+    if (g->mf) EIGSOL_TRY(mf_solve(g->mf, w, y));
+    else {
+        EIGSOL_TRY(shift_solve_launch(g->L, w, t1));
+        EIGSOL_TRY(shift_solve_launch(g->U, t1, y));
+    }
+    EIGSOL_TRY(eigsol_csr_spmv(g->M ? g->M : g->A, y, t1));
+    hipLaunchKernelGGL((dev::gm_resid_norms_kernel<S>), dim3(g->G), dim3(dev::kThreads), 0, st, b, bdiv, t1, y,
+                       g->sre, g->sim, g->M ? 0 : 1, w, n, g->part);
+    hipLaunchKernelGGL(dev::gm_reduce_kernel, dim3(2), dim3(dev::kThreads), 0, st, g->part, g->G, 2, g->hdev + 2);
+    double* slot = g->hpin + g->lag_off();
+    EIGSOL_HIP(hipMemcpyAsync(slot, g->hdev, 6 * sizeof(double), hipMemcpyDeviceToHost, st));
+    int32_t* err = reinterpret_cast<int32_t*>(slot + 6);
+    *err = 0;
+    if (g->mf) EIGSOL_HIP(hipMemcpyAsync(err, mf_err_word(g->mf), sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    g->lag_pending = true;
+    double lb = 0.0, ub = 0.0;
+    if (g->mf) lb = mf_stats(g->mf).solve_bytes;
+    else {
+        shift_info(g->L, &lb, nullptr, nullptr);
+        shift_info(g->U, &ub, nullptr, nullptr);
+    }
+    const double sb = (double)sizeof(S);
+    g->last_steps = 0;
+    g->last_bytes = lb + ub + (sb + 4.0) * (double)(g->A ? g->A->nnz : g->nnzM) + 4.0 * (double)(n + 1) +
+                    (g->A ? 5.0 : 2.0) * sb * (double)n + 4.0 * sb * (double)n;
+    return EIGSOL_OK;
+}
+
+int gmres_can_lag(const GmresSolver* g) {
+    const char* e = std::getenv("EIGSOL_GMRES_LAG");   // read per call: tests switch it inside one process
+    const bool off = e && std::atoi(e) == 0;
+    return !off && g->complete && g->mf_static == 0 && g->hpin ? 1 : 0;
+}
+
+int gmres_solve_lag(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev) {
+    if (g->dtype == EIGSOL_C128)
+        return gmres_solve_lag_t<cplx>(g, static_cast<const cplx*>(b_dev), bdiv, static_cast<cplx*>(y_dev));
+    return gmres_solve_lag_t<double>(g, static_cast<const double*>(b_dev), bdiv, static_cast<double*>(y_dev));
+}
+
+// the pending lagged check (its copy done: the caller has waited on the stream since): EIGSOL_OK,
+// EIGSOL_E_SOLVER (redo the iteration with the checked solve) or EIGSOL_E_HIP (a multifrontal solve
+// wait timed out).  EIGSOL_GMRES_LAG_REDO=1 (tests) reports every check as missed.
+int gmres_lag_verdict(GmresSolver* g) {
+    if (!g->lag_pending) return EIGSOL_OK;
+    g->lag_pending = false;
+    const double* l = g->hpin + g->lag_off();
+    if (*reinterpret_cast<const int32_t*>(l + 6))
+        return fail(EIGSOL_E_HIP, "solve_shifted: a multifrontal solve wait did not complete");
+    for (ShiftFactor* t : {g->L, g->U})   // the triangular solves' wait-error words
+        if (t && shift_error(t) != EIGSOL_OK) return EIGSOL_E_HIP;
+    const char* fe = std::getenv("EIGSOL_GMRES_LAG_REDO");
+    const bool force = fe && std::atoi(fe) != 0;
+    const double bnorm = std::sqrt(l[0]), beta = std::sqrt(l[2]), xnorm = std::sqrt(l[4]);
+    const double relres = bnorm > 0.0 ? beta / bnorm : 0.0;
+    g->last_relres = relres;
+    const bool ok = bnorm == 0.0 || beta == 0.0 || relres <= g->rtol_true ||
+                    beta <= g->be_accept * (g->normM * xnorm + bnorm);
+    return (ok && !force) ? EIGSOL_OK : EIGSOL_E_SOLVER;
 }
 
 int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev, const double* guess) {

@@ -37,6 +37,9 @@ int gmres_create(eigsol_ctx* ctx, int dtype, int64_t n, const int32_t* rp, const
                  double sre, double sim, GmresSolver** out, eigsol_csr* Adev = nullptr);
 void gmres_free(GmresSolver* g);
 int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev, const double* guess = nullptr);
+int gmres_can_lag(const GmresSolver* g);
+int gmres_solve_lag(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev);
+int gmres_lag_verdict(GmresSolver* g);
 void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps);
 int gmres_complete(const GmresSolver* g);
 
@@ -53,6 +56,8 @@ struct ShiftFactor {
     int64_t n = 0;
     int kind = 0;                 // 0 triangular CSR, 1 dense LU, 2 ILU(0)-preconditioned GMRES, 3 band LU
     GmresSolver* gm = nullptr;    // kind 2 (gmres.hip)
+    bool lag_prev = false;        // kind 2 iteration: the previous launch's solve check is still to be read
+    double lag_bdiv = 0.0;        // ... and that solve's divisor (||y_{t-1}||)
     void* promo = nullptr;        // kind 2 in single precision: [2][n] double-precision right-hand side and
                                   // solution of the GMRES family's solve (its factors are built in double)
     BandFactor* band = nullptr;   // kind 3 (band_lu.hip)
@@ -3032,9 +3037,9 @@ void* shift_aux(const ShiftFactor* f, int j) { return (j >= 0 && j < dev::kMaxMu
 
 // x = M^-1 (b / bdiv) by the GMRES family; single precision through f->promo (widen, solve, narrow)
 template <class S>
-static int gm_solve_s(ShiftFactor* f, const void* b, double bdiv, void* y, const double* guess) {
+static int gm_solve_s(ShiftFactor* f, const void* b, double bdiv, void* y, const double* guess, bool lag = false) {
     if constexpr (kGmres<S>) {
-        return gmres_solve(f->gm, b, bdiv, y, guess);
+        return lag ? gmres_solve_lag(f->gm, b, bdiv, y) : gmres_solve(f->gm, b, bdiv, y, guess);
     } else {
         using W = GmresScalar<S>;
         hipStream_t st = f->ctx->stream;
@@ -3043,7 +3048,7 @@ static int gm_solve_s(ShiftFactor* f, const void* b, double bdiv, void* y, const
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (f->n + 255) / 256));
         hipLaunchKernelGGL((dev::convert_kernel<S, W>), dim3(grid), dim3(256), 0, st, static_cast<const S*>(b), wb, f->n);
         EIGSOL_HIP(hipGetLastError());
-        const int rc = gmres_solve(f->gm, wb, bdiv, wy, guess);
+        const int rc = lag ? gmres_solve_lag(f->gm, wb, bdiv, wy) : gmres_solve(f->gm, wb, bdiv, wy, guess);
         if (rc != EIGSOL_OK) return rc;
         hipLaunchKernelGGL((dev::convert_kernel<W, S>), dim3(grid), dim3(256), 0, st, wy, static_cast<S*>(y), f->n);
         EIGSOL_HIP(hipGetLastError());
@@ -3088,6 +3093,38 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         EIGSOL_HIP(hipMemcpyAsync(&hd->done, &ctl->done, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(hipMemcpyAsync(&hd->cr, &ctl->st[parity ^ 1], sizeof(PowerCarry), hipMemcpyDeviceToHost, st));
         EIGSOL_HIP(stream_wait(st));
+        if (f->lag_prev) {
+            // the previous launch's direct solve was checked without a host wait (gmres_solve_lag): read
+            // the check now; a miss redoes that iteration with the checked solve (and GMRES refinement),
+            // its partials, and this launch's decision.  The previous launch read B[parity] and wrote
+            // B[parity ^ 1]... in its own parity: it solved from buffer (parity ? buf1 : buf0) into
+            // (parity ? buf0 : buf1), and neither has been touched since.
+            f->lag_prev = false;
+            const int v = gmres_lag_verdict(f->gm);
+            if (v != EIGSOL_OK && v != EIGSOL_E_SOLVER) return v;
+            if (v == EIGSOL_E_SOLVER) {
+                const int pp = parity ^ 1;
+                const int rc = gm_solve_s<S>(f, pp ? buf0 : buf1, f->lag_bdiv, pp ? buf1 : buf0, nullptr);
+                if (rc == EIGSOL_E_SOLVER) {
+                    // the checked solve failed too: the densified LU redoes the previous launch (its
+                    // prologue re-takes that launch's decision from the same carry), then this one
+                    EIGSOL_TRY(gmres_dense_fallback<S>(f, rc));
+                    EIGSOL_HIP(hipMemsetAsync(&ctl->done, 0, sizeof(int32_t), st));
+                    EIGSOL_TRY(shift_launch_t<S>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, pp));
+                    return shift_launch_t<S>(f, iter, b, y, buf0, buf1, ctl, rank_part, my_part, trace, parity);
+                }
+                EIGSOL_TRY(rc);
+                hipLaunchKernelGGL((dev::shift_part_kernel<S>), dim3(f->red_grid), dim3(dev::kThreads), 0, st, a, pp);
+                EIGSOL_HIP(hipGetLastError());
+                // this launch's decision again, from the corrected partials (the prologue writes the
+                // same carry slot and trace entry; a stop it had decided is undone first)
+                EIGSOL_HIP(hipMemsetAsync(&ctl->done, 0, sizeof(int32_t), st));
+                hipLaunchKernelGGL((dev::shift_decide_kernel<S>), dim3(1), dim3(64), 0, st, a, parity);
+                EIGSOL_HIP(hipMemcpyAsync(&hd->done, &ctl->done, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+                EIGSOL_HIP(hipMemcpyAsync(&hd->cr, &ctl->st[parity ^ 1], sizeof(PowerCarry), hipMemcpyDeviceToHost, st));
+                EIGSOL_HIP(stream_wait(st));
+            }
+        }
         const int32_t done = hd->done;
         const PowerCarry cr = hd->cr;
         if (done) return EIGSOL_OK;
@@ -3111,7 +3148,15 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
                 use_guess = true;
             }
         }
-        const int rc = gm_solve_s<S>(f, parity ? buf0 : buf1, cr.nrm, parity ? buf1 : buf0, use_guess ? guess : nullptr);
+        // the direct solve's check is read at the next launch's decision wait (one host wait per
+        // iteration instead of two) where the factor is complete and needs no refinement by design
+        const bool lag = !use_guess && gmres_can_lag(f->gm);
+        const int rc = gm_solve_s<S>(f, parity ? buf0 : buf1, cr.nrm, parity ? buf1 : buf0, use_guess ? guess : nullptr,
+                                     lag);
+        if (lag && rc == EIGSOL_OK) {
+            f->lag_prev = true;
+            f->lag_bdiv = cr.nrm;
+        }
         if (rc == EIGSOL_E_SOLVER) {
             // switch to the densified LU and redo this launch on it: the dense kernel's prologue
             // re-evaluates the same decision from the same carry record (idempotent)

@@ -318,3 +318,51 @@ def test_zero_diagonal_band_past_16384(ctx, monkeypatch, mf):
     ev = spl.eigsh(A.astype(np.float64), k=1, sigma=sigma, return_eigenvectors=False)
     assert abs(r.eigenvalue - ev[0]) <= 1e-8 * (1 + abs(ev[0])), (r.eigenvalue, ev)
     D.close()
+
+
+@pytest.mark.parametrize("kind", ["exact", "multifrontal"])
+def test_lagged_direct_solve_check_bitwise(ctx, gmres_env, monkeypatch, kind):
+    """The iteration's direct solve over a complete factor is checked one launch late (its true
+    residual read at the next decision wait, gmres.hip gmres_solve_lag): the same λ trace, iteration
+    count and eigenvector, bit for bit, as the checked solve with its own host wait
+    (EIGSOL_GMRES_LAG=0), and as a run whose every lagged check is treated as missed
+    (EIGSOL_GMRES_LAG_REDO=1: each iteration redone with the checked solve, its partials and the
+    next decision recomputed)."""
+    if kind == "exact":
+        n = 600
+        rp, ci, v, d = S.general_complex(n, 12)
+        sigma = TARGET + 1e-3
+        monkeypatch.setenv("EIGSOL_LU_FILL_CAP", "3")
+        variant = 18
+    else:
+        nx = 45
+        n = nx * nx
+        rp, ci, v = S.convdiff_complex(nx, seed=12)
+        sigma = 3.0 - 0.2j
+        monkeypatch.setenv("EIGSOL_LU_FILL_CAP", "1")
+        monkeypatch.setenv("EIGSOL_GMRES_FALLBACK", "0")
+        variant = 19
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    x0 = S.start_vector(n, np.complex128)
+    runs = {}
+    for mode, envs in (("sync", {"EIGSOL_GMRES_LAG": "0"}), ("lag", {}), ("redo", {"EIGSOL_GMRES_LAG_REDO": "1"})):
+        for k in ("EIGSOL_GMRES_LAG", "EIGSOL_GMRES_LAG_REDO"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in envs.items():
+            monkeypatch.setenv(k, val)
+        s = E.ShiftedSession(A, sigma, trace_capacity=64)
+        assert s.kernel_info()["variant"] == variant
+        s.begin(E.ShiftedSolverOptions(40, 1e-12, sigma), x0)
+        done = False
+        while not done:
+            s.step(1)
+            done, _ = s.query()
+        r = s.finish()
+        runs[mode] = (r.eigenvalue, r.iterations, r.converged, r.eigenvector.copy(), s.trace(64).copy())
+        s.close()
+    for mode in ("lag", "redo"):
+        a, b = runs["sync"], runs[mode]
+        assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2], (mode, a[:3], b[:3])
+        assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4]), mode
+    assert runs["sync"][1] >= 2
+    A.close()
