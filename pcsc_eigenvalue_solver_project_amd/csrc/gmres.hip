@@ -1079,6 +1079,8 @@ int gmres_can_lag(const GmresSolver* g) {
     return !off && g->complete && g->mf_static == 0 && g->hpin ? 1 : 0;
 }
 
+void gmres_lag_reset(GmresSolver* g) { g->lag_pending = false; }
+
 int gmres_solve_lag(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev) {
     if (g->dtype == EIGSOL_C128)
         return gmres_solve_lag_t<cplx>(g, static_cast<const cplx*>(b_dev), bdiv, static_cast<cplx*>(y_dev));

@@ -46,6 +46,7 @@ void shift_factor_free(ShiftFactor* f);
 int shift_grid(const ShiftFactor* f);
 void* shift_aux(const ShiftFactor* f, int j);
 int shift_error(ShiftFactor* f);
+void shift_lag_reset(ShiftFactor* f);
 int shift_iter_launch(ShiftFactor* f, void* buf0, void* buf1, PowerCtl* ctl, const void* rank_part,
                       void* my_part, void* trace, int parity, int first);
 int shift_solve_launch(ShiftFactor* f, const void* b_dev, void* y_dev);
@@ -495,6 +496,7 @@ int eigsol_power_begin(eigsol_power* s, const eigsol_solver_options* opts, const
     EIGSOL_HIP(hipSetDevice(s->ctx->device));
     hipStream_t st = s->ctx->stream;
     const size_t sb = scalar_bytes(s->dtype);
+    if (s->shift) shift_lag_reset(s->shift);
     s->opts = *opts;
     s->trivial = opts->max_iterations <= 0;
     // y_{-1} = x0 lives in buf[1] (launch t reads buf[(t-1)&1]); own rows at x-space offset xoff

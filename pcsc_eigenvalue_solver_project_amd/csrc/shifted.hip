@@ -40,6 +40,7 @@ int gmres_solve(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev, con
 int gmres_can_lag(const GmresSolver* g);
 int gmres_solve_lag(GmresSolver* g, const void* b_dev, double bdiv, void* y_dev);
 int gmres_lag_verdict(GmresSolver* g);
+void gmres_lag_reset(GmresSolver* g);
 void gmres_info(const GmresSolver* g, double* bytes, int32_t* steps);
 int gmres_complete(const GmresSolver* g);
 
@@ -2995,6 +2996,12 @@ int shift_factor_csr(eigsol_csr* A, const void* sigma, ShiftFactor** out) {
 }
 
 int shift_grid(const ShiftFactor* f) { return (f->kind == 0 || f->dense_multi) ? f->grid : 1; }
+
+// a new run of the iteration (session begin): no lagged check of the previous run is carried over
+void shift_lag_reset(ShiftFactor* f) {
+    f->lag_prev = false;
+    if (f->gm) gmres_lag_reset(f->gm);
+}
 
 int shift_error(ShiftFactor* f) {
     if (f->kind != 0 && !f->dense_multi) return EIGSOL_OK;

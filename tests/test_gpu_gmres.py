@@ -327,7 +327,8 @@ def test_lagged_direct_solve_check_bitwise(ctx, gmres_env, monkeypatch, kind):
     count and eigenvector, bit for bit, as the checked solve with its own host wait
     (EIGSOL_GMRES_LAG=0), and as a run whose every lagged check is treated as missed
     (EIGSOL_GMRES_LAG_REDO=1: each iteration redone with the checked solve, its partials and the
-    next decision recomputed)."""
+    next decision recomputed; that run is begun after an abandoned one, whose pending check must be
+    dropped at begin)."""
     if kind == "exact":
         n = 600
         rp, ci, v, d = S.general_complex(n, 12)
@@ -352,6 +353,9 @@ def test_lagged_direct_solve_check_bitwise(ctx, gmres_env, monkeypatch, kind):
             monkeypatch.setenv(k, val)
         s = E.ShiftedSession(A, sigma, trace_capacity=64)
         assert s.kernel_info()["variant"] == variant
+        if mode == "redo":   # an abandoned run first: its pending check must not reach the next one
+            s.begin(E.ShiftedSolverOptions(40, 1e-12, sigma), S.start_vector(n, np.complex128, seed=9))
+            s.step(2)
         s.begin(E.ShiftedSolverOptions(40, 1e-12, sigma), x0)
         done = False
         while not done:
