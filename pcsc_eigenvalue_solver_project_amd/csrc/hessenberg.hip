@@ -396,7 +396,7 @@ __global__ __launch_bounds__(1024) void qr_panel_col(S* R, int m, int k, int j, 
 }
 
 // ------------------------------------------------------------------ cooperative panel (one launch)
-// The whole panel (32 columns) in ONE cooperative launch of kCoopBlocks co-resident blocks; block
+// The whole panel (32 columns) in ONE cooperative launch of G co-resident blocks (host: ~32 rows each); block
 // b owns rows [b R, (b+1) R).  Per column, three grid barriers separate
 //   P1  right update of column j (own rows, kept in LDS) + partials of V^T a
 //   P2  w = T^T (sum of partials); left update; partial of ||a(j+2:)||^2; x0 = a(j+1)
@@ -411,10 +411,6 @@ __global__ __launch_bounds__(1024) void qr_panel_col(S* R, int m, int k, int j, 
 // so no L2 writeback/invalidate is needed; partial sums are combined in block order
 // (deterministic).  The barrier spins are bounded: on expiry the kernel sets an error word and
 // drains (the host then reports EIGSOL_E_HIP).
-#ifndef EIGSOL_COOP_BLOCKS
-#define EIGSOL_COOP_BLOCKS 64
-#endif
-constexpr int kCoopBlocks = EIGSOL_COOP_BLOCKS;
 constexpr int kCoopThreads = 1024;
 #ifndef EIGSOL_GEMV_BATCH
 #define EIGSOL_GEMV_BATCH 16
@@ -473,25 +469,41 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
     S* vsh = reinterpret_cast<S*>(vsh_raw);
     __shared__ S xs[kCoopRowsPerLane * 64];    // own rows of the current column
     __shared__ S ysum[16][kCoopRowsPerLane * 64];
-    __shared__ S red[kCoopBlocks * NB];   // gathered block partials
+    __shared__ S red[kCoopThreads];   // per-thread sums of block partials (and the norm partials as doubles)
     __shared__ S sv[NB], sw[NB], st[NB];
     __shared__ S Tl[NB * NB];   // this block's copy of T (every block forms each column from the same sums)
     __shared__ S s_scal[3];
     __shared__ double s_rv;
     __shared__ int s_sk;
     __shared__ S s_vrow;   // kMerge: V(j + 1, i) of the previous column (rv v0, or 0 when skipped)
-    // Block partials of another phase: all threads load them at once (independent sc1 loads),
-    // then thread c sums column c in block order (deterministic).
+    // Block partials of another phase: thread (s, c) loads blocks s, s + kSl, ... of column c at once
+    // (independent sc1 loads) and sums them in that order; thread c then sums the kSl slices in order
+    // (deterministic, the same in every block, for any grid size).
+    constexpr int kSl = kCoopThreads / NB;
     auto gather = [&](const S* src, int cnt, S* dst) {
         const int nb = (int)gridDim.x;
-        for (int e = threadIdx.x; e < nb * NB; e += kCoopThreads) {
-            const int b = e / NB, c = e % NB;
-            red[e] = c < cnt ? ld_ag(&src[b * NB + c]) : s_zero<S>();
+        {
+            const int c = threadIdx.x % NB, sl = threadIdx.x / NB;
+            S acc = s_zero<S>();
+            if (c < cnt) {
+                constexpr int kU = 4;
+                for (int b0 = sl; b0 < nb; b0 += kU * kSl) {
+                    S t4[kU];
+#pragma unroll
+                    for (int u = 0; u < kU; ++u) {
+                        const int b = b0 + u * kSl;
+                        t4[u] = b < nb ? ld_ag(&src[b * NB + c]) : s_zero<S>();
+                    }
+#pragma unroll
+                    for (int u = 0; u < kU; ++u) acc = add(acc, t4[u]);
+                }
+            }
+            red[threadIdx.x] = acc;
         }
         __syncthreads();
         if ((int)threadIdx.x < cnt) {
             S acc = s_zero<S>();
-            for (int b = 0; b < nb; ++b) acc = add(acc, red[b * NB + threadIdx.x]);
+            for (int sl = 0; sl < kSl; ++sl) acc = add(acc, red[sl * NB + threadIdx.x]);
             dst[threadIdx.x] = acc;
         }
         __syncthreads();
@@ -506,6 +518,9 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
     // (4096^2: panels 151 -> 141 ms per reduction, rocprofv3 kernel trace, tools/hess_prof.sh)
     const int grp = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
     const int r0 = grp * R, r1 = min(n, r0 + R);
+    int rp = 64;   // lanes per column in the GEMV (a power of two >= R when R < 64; one row per lane)
+    if (kCoopRowsPerLane == 1)
+        while (rp > 8 && rp / 2 >= R) rp /= 2;
     unsigned target = 0;
     for (int e = tid; e < NB * NB; e += kCoopThreads) Tl[e] = s_zero<S>();
     for (int i = 0; i < a.nbp; ++i) {
@@ -726,30 +741,34 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
         if (!sk && !EIGSOL_HESS_SKIP_GEMV) {
             // kB columns per step with every load issued before the FMAs (bytes in flight: the
             // GEMV streams the trailing matrix once per column)
+            // rp lanes per row group of a column, sub = 64 / rp columns per wave step: with fewer than
+            // 64 rows per block (a larger grid) the wave's other lanes take the next columns
             const int nq = (r1 - r0 + 63) / 64;
-            int c = j + 1 + wv;
+            const int rl = lane & (rp - 1), sub = 64 / rp;
+            const int cs = 16 * sub;
+            int c = j + 1 + wv * sub + lane / rp;
             constexpr int kB = kGemvBatch * (int)sizeof(double) / (int)sizeof(S) / kCoopRowsPerLane;
-            for (; c + 16 * (kB - 1) < n; c += 16 * kB) {
+            for (; c + cs * (kB - 1) < n; c += cs * kB) {
                 S av[kB][kCoopRowsPerLane];
 #pragma unroll
                 for (int u = 0; u < kB; ++u)
 #pragma unroll
                     for (int q = 0; q < kCoopRowsPerLane; ++q) {
-                        const int r = min(r0 + lane + 64 * q, r1 - 1);
-                        av[u][q] = q < nq ? a.A[r + (int64_t)(c + 16 * u) * n] : s_zero<S>();
+                        const int r = min(r0 + rl + 64 * q, r1 - 1);
+                        av[u][q] = q < nq ? a.A[r + (int64_t)(c + cs * u) * n] : s_zero<S>();
                     }
 #pragma unroll
                 for (int u = 0; u < kB; ++u) {
-                    const S vc = vsh[c + 16 * u];
+                    const S vc = vsh[c + cs * u];
 #pragma unroll
                     for (int q = 0; q < kCoopRowsPerLane; ++q) yacc[q] = add(yacc[q], mul(av[u][q], vc));
                 }
             }
-            for (; c < n; c += 16) {
+            for (; c < n; c += cs) {
                 const S vc = vsh[c];
 #pragma unroll
                 for (int q = 0; q < kCoopRowsPerLane; ++q) {
-                    const int r = min(r0 + lane + 64 * q, r1 - 1);
+                    const int r = min(r0 + rl + 64 * q, r1 - 1);
                     if (q < nq) yacc[q] = add(yacc[q], mul(a.A[r + (int64_t)c * n], vc));
                 }
             }
@@ -763,7 +782,8 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
                 const int r = r0 + lane + 64 * q;
                 if (r < r1) {
                     S y = s_zero<S>();
-                    for (int w = 0; w < 16; ++w) y = add(y, ysum[w][lane + 64 * q]);
+                    for (int w = 0; w < 16; ++w)
+                        for (int l = lane + 64 * q; l < 64 * (q + 1); l += rp) y = add(y, ysum[w][l]);
                     for (int c = 0; c < i; ++c) y = sub(y, mul(a.Y[r + (int64_t)c * n], sv[c]));
                     a.Y[r + (int64_t)i * n] = sk ? s_zero<S>() : two_x(y);
                 }
@@ -1101,7 +1121,18 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
     int coop_ok = 0, dev_id = 0;
     EIGSOL_HIP(hipGetDevice(&dev_id));
     EIGSOL_HIP(hipDeviceGetAttribute(&coop_ok, hipDeviceAttributeCooperativeLaunch, dev_id));
-    bool coop = coop_ok && n <= Cfg::kCoopMaxN && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
+    // panel grid: about 32 rows per block, 16 .. 256 blocks (EIGSOL_HESS_G overrides: 8 .. 256, a multiple of
+    // 8).  The panel's GEMV streams the trailing matrix once per column from the grid's CUs, its two grid
+    // barriers per column grow with the grid; round 6 (tools/r06_hess_grid_ab.sh, profiles/r06_hess_grid_ab.log,
+    // host in/out): 512^2 16 blocks 0.011 s (64: 0.014), 1024^2 32 0.024 (64: 0.026), 4096^2 128 0.167 (64:
+    // 0.184, 256: 0.193), 8192^2 256 0.73 (64: 1.11)
+    static const int g_env = [] {
+        const char* e = std::getenv("EIGSOL_HESS_G");
+        const int g = e ? std::atoi(e) : 0;
+        return (g >= 8 && g <= 256 && g % 8 == 0) ? g : 0;
+    }();
+    const int G = g_env ? g_env : std::min(256, std::max(16, (n / 32 + 7) / 8 * 8));
+    bool coop = coop_ok && n <= Cfg::kCoopMaxN && n <= 128 * G && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
     const size_t coop_lds = (size_t)n * sizeof(S);
     // two grid barriers per panel column (hess_panel_coop kMerge; EIGSOL_HESS_MERGE=0: three).  Round 6
     // (tools/r06_hess_merge_ab.sh, profiles/r06_hess_merge_ab.log): to_hessenberg 4096^2 0.184 / 0.185 ->
@@ -1112,7 +1143,7 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         return !(e && std::atoi(e) == 0);
     }();
     const void* coop_kernel =
-        n <= 64 * dev::kCoopBlocks
+        n <= 64 * G
             ? (merge ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1, true>)
                      : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1>))
             : (merge ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 2, true>)
@@ -1122,8 +1153,8 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
     unsigned* bar = nullptr;
     int* err = nullptr;
     if (coop) {
-        EIGSOL_HIP(hipMalloc(&part, 2 * dev::kCoopBlocks * NB * sizeof(S)));
-        EIGSOL_HIP(hipMalloc(&tpart, dev::kCoopBlocks * sizeof(double)));
+        EIGSOL_HIP(hipMalloc(&part, 2 * G * NB * sizeof(S)));
+        EIGSOL_HIP(hipMalloc(&tpart, G * sizeof(double)));
         EIGSOL_HIP(hipMalloc(&x0s, 64));
         EIGSOL_HIP(hipMalloc(&xu, (size_t)n * sizeof(S)));
         EIGSOL_HIP(hipMalloc(&bar, 64));
@@ -1143,13 +1174,13 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
             void* kargs[] = {&ca};
             // EIGSOL_HESS_COOP_PLAIN=1: the SAME panel kernel through an ordinary launch, for profiling
             // only (rocprofv3 7.2 crashes at exit after any cooperative launch, tools/coop_prof_repro.hip);
-            // its kCoopBlocks blocks are far fewer than the CUs, so on an idle device all are resident,
+            // its G blocks are at most the CUs, so on an idle device all are resident,
             // and the grid barrier's bounded spin reports a failure instead of hanging otherwise
             static const bool plain = std::getenv("EIGSOL_HESS_COOP_PLAIN") != nullptr;
             if (plain)
-                EIGSOL_HIP(hipLaunchKernel(coop_kernel, dim3(dev::kCoopBlocks), dim3(dev::kCoopThreads), kargs, coop_lds, st));
+                EIGSOL_HIP(hipLaunchKernel(coop_kernel, dim3(G), dim3(dev::kCoopThreads), kargs, coop_lds, st));
             else
-                EIGSOL_HIP(hipLaunchCooperativeKernel(coop_kernel, dim3(dev::kCoopBlocks), dim3(dev::kCoopThreads), kargs,
+                EIGSOL_HIP(hipLaunchCooperativeKernel(coop_kernel, dim3(G), dim3(dev::kCoopThreads), kargs,
                                                       coop_lds, st));
         }
         for (int i = 0; !coop && i < nbp; ++i) {
