@@ -430,21 +430,33 @@ struct CoopArgs {
     S* part;            // [2][G][NB]: P1 -> P2 partials in the first half, P3 -> P4 in the second
     double* tpart;      // [G]
     S* x0;              // a(j+1)
-    unsigned* bar;      // barrier counter (zeroed by the host before the launch)
+    unsigned* bar;      // barrier counters, 9 x 64 bytes (zeroed by the host before the launch)
     int* err;
     S* xu;              // kMerge: the column below row j + 1 before normalisation (n scalars)
+    bool hier;          // two-level grid barrier (gridDim.x % 8 == 0)
 };
 
 __device__ __forceinline__ unsigned ld_agent_u32(const unsigned* p) {
     return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned& target, int* err) {
+// bar[0] counts arrivals of the whole grid; with hier (a grid that is a multiple of 8 blocks), block b
+// first counts itself in its group's word bar[16 (1 + b % 8)] (the blocks one XCD holds, each group word on
+// its own 64-byte line) and the group's last arriver adds the group to bar[0]: 8 + G / 8 serialised atomics
+// per line instead of G on one
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned& target, int* err, bool hier = false) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's sc1 stores are complete
     __syncthreads();
     target += gridDim.x;
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (hier) {
+            const unsigned gs = gridDim.x / 8;
+            const unsigned old =
+                __hip_atomic_fetch_add(bar + 16 * (1 + blockIdx.x % 8), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((old + 1) % gs == 0) __hip_atomic_fetch_add(bar, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         int spins = 0;
         while (ld_agent_u32(bar) < target) {
             __builtin_amdgcn_s_sleep(1);
@@ -548,7 +560,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
             p = wsum(p);
             if (lane == 0) st_ag(&a.part[grp * NB + c], p);
         }
-        grid_barrier(a.bar, target, a.err);
+        grid_barrier(a.bar, target, a.err, a.hier);
         bool sk;
         if constexpr (kMerge) {
             // ---------------- P2 (merged): left update, norm partials, x0, xu, partials of V^H xu
@@ -589,7 +601,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
                 p = wsum(p);
                 if (lane == 0) st_ag(&a.part[(G + grp) * NB + c], p);
             }
-            grid_barrier(a.bar, target, a.err);
+            grid_barrier(a.bar, target, a.err, a.hier);
             // ---------------- P3 + P4: reflector (every block), own rows of V and the reduced column,
             // v for the GEMV from xu, t from the reduced partials
             double* redd = reinterpret_cast<double*>(red);
@@ -671,7 +683,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
                 tl = wave_sum(tl);
                 if (lane == 0) st_agent(&a.tpart[grp], tl);
             }
-            grid_barrier(a.bar, target, a.err);
+            grid_barrier(a.bar, target, a.err, a.hier);
             // ---------------- P3
             double* redd = reinterpret_cast<double*>(red);
             if (tid < G) redd[tid] = ld_agent(&a.tpart[tid]);
@@ -718,7 +730,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
                 p = wsum(p);
                 if (lane == 0) st_ag(&a.part[(G + grp) * NB + c], p);
             }
-            grid_barrier(a.bar, target, a.err);
+            grid_barrier(a.bar, target, a.err, a.hier);
             // ---------------- P4
             // v into LDS: four independent coherent loads per thread in flight (clamped rows, so no
             // predicated load waits for the one before it)
@@ -1132,6 +1144,14 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         return (g >= 8 && g <= 256 && g % 8 == 0) ? g : 0;
     }();
     const int G = g_env ? g_env : std::min(256, std::max(16, (n / 32 + 7) / 8 * 8));
+    // two-level grid barrier from 64 blocks (EIGSOL_HESS_BAR=0: one counter).  Round 6
+    // (tools/r06_hess_bar_ab.sh, profiles/r06_hess_bar_ab.log, host in/out): 4096^2 0.169 / 0.172 -> 0.161 /
+    // 0.162 s, 8192^2 0.730 -> 0.689 s; at 32 blocks (1024^2) one counter stays (0.0240 against 0.0248 s)
+    static const bool hier = [] {
+        const char* e = std::getenv("EIGSOL_HESS_BAR");
+        return !(e && std::atoi(e) == 0);
+    }();
+    constexpr size_t kBarBytes = 9 * 64;
     bool coop = coop_ok && n <= Cfg::kCoopMaxN && n <= 128 * G && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
     const size_t coop_lds = (size_t)n * sizeof(S);
     // two grid barriers per panel column (hess_panel_coop kMerge; EIGSOL_HESS_MERGE=0: three).  Round 6
@@ -1157,7 +1177,7 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         EIGSOL_HIP(hipMalloc(&tpart, G * sizeof(double)));
         EIGSOL_HIP(hipMalloc(&x0s, 64));
         EIGSOL_HIP(hipMalloc(&xu, (size_t)n * sizeof(S)));
-        EIGSOL_HIP(hipMalloc(&bar, 64));
+        EIGSOL_HIP(hipMalloc(&bar, kBarBytes));
         EIGSOL_HIP(hipMalloc(&err, 64));
         EIGSOL_HIP(hipMemsetAsync(err, 0, 64, st));
         EIGSOL_HIP(hipFuncSetAttribute(coop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)coop_lds));
@@ -1169,8 +1189,8 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         const int nbp = std::min(NB, last - k + 1);
         EIGSOL_HIP(hipMemsetAsync(T, 0, NB * NB * sizeof(S), st));
         if (coop) {
-            EIGSOL_HIP(hipMemsetAsync(bar, 0, 64, st));
-            dev::CoopArgs<S> ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err, xu};
+            EIGSOL_HIP(hipMemsetAsync(bar, 0, kBarBytes, st));
+            dev::CoopArgs<S> ca{A, n, k, nbp, V, Y, T, part, tpart, x0s, bar, err, xu, hier && G % 8 == 0 && G >= 64};
             void* kargs[] = {&ca};
             // EIGSOL_HESS_COOP_PLAIN=1: the SAME panel kernel through an ordinary launch, for profiling
             // only (rocprofv3 7.2 crashes at exit after any cooperative launch, tools/coop_prof_repro.hip);
