@@ -817,6 +817,233 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
     }
 }
 
+// The merged panel (two grid barriers per column) with fewer dependent round trips to memory: one row per
+// lane (a grid of >= n / 64 blocks), the block's own rows of V(:, 0:i) and Y(:, 0:i) kept in LDS (the
+// right and left updates and the partials of V^H a read no global memory), the own rows of A(:, j + 1)
+// loaded before the second barrier, and everything the reflector and the GEMV need after that barrier
+// (the norm partials, x0, xu, the partials of V^H xu and V(j + 1, 0:i)) loaded in one batch; V(j + 1, :)
+// is also the next column's V(j, :).  The same operations in the same order as hess_panel_coop<S, 1, true>:
+// bitwise its results (tests/test_gpu_qr.py::test_hessenberg_panel2_bitwise).
+template <class S>
+__global__ __launch_bounds__(kCoopThreads) void hess_panel_coop2(CoopArgs<S> a) {
+    constexpr int NB = HessCfg<S>::NB;
+    constexpr int kSl = kCoopThreads / NB;               // gather slices
+    constexpr int kGU = 256 / kSl;                       // gather loads per thread (grid <= 256)
+    constexpr int kXU = HessCfg<S>::kCoopMaxN / kCoopThreads;   // xu loads per thread
+    extern __shared__ double vsh_raw[];
+    S* vsh = reinterpret_cast<S*>(vsh_raw);
+    __shared__ S xs[64];
+    __shared__ S ysum[16][64];
+    __shared__ S red[kCoopThreads];
+    __shared__ S vc[NB][64];     // own rows of V(:, c)
+    __shared__ S yc[NB][64];     // own rows of Y(:, c)
+    __shared__ double tps[256];
+    __shared__ S sv[NB], sw[NB], st[NB], s_vj[NB];
+    __shared__ S Tl[NB * NB];
+    __shared__ S s_scal[3];
+    __shared__ double s_rv;
+    __shared__ int s_sk;
+    auto gather2 = [&](const S* src, int cnt, S* dst) {   // hess_panel_coop's gather, the same order
+        const int nb = (int)gridDim.x;
+        {
+            const int c = threadIdx.x % NB, sl = threadIdx.x / NB;
+            S acc = s_zero<S>();
+            if (c < cnt) {
+                S t[kGU];
+#pragma unroll
+                for (int u = 0; u < kGU; ++u) {
+                    const int b = sl + u * kSl;
+                    t[u] = b < nb ? ld_ag(&src[b * NB + c]) : s_zero<S>();
+                }
+#pragma unroll
+                for (int u = 0; u < kGU; ++u) acc = add(acc, t[u]);
+            }
+            red[threadIdx.x] = acc;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < cnt) {
+            S acc = s_zero<S>();
+            for (int sl = 0; sl < kSl; ++sl) acc = add(acc, red[sl * NB + threadIdx.x]);
+            dst[threadIdx.x] = acc;
+        }
+        __syncthreads();
+    };
+    const int n = a.n, k = a.k;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int G = gridDim.x;
+    const int R = (n + G - 1) / G;
+    const int grp = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int r0 = grp * R, r1 = min(n, r0 + R);
+    int rp = 64;
+    while (rp > 8 && rp / 2 >= R) rp /= 2;
+    const int rown = r0 + lane;                 // wave 0: this lane's row
+    const bool own = rown < r1;
+    unsigned target = 0;
+    for (int e = tid; e < NB * NB; e += kCoopThreads) Tl[e] = s_zero<S>();
+    S acol = s_zero<S>();                       // wave 0: A(rown, j), loaded a column ahead
+    if (wv == 0 && own) acol = a.A[rown + (int64_t)k * n];
+    for (int i = 0; i < a.nbp; ++i) {
+        const int j = k + i;
+        // ---------------- P1 (no global loads)
+        if (tid < i) sv[tid] = cj(s_vj[tid]);
+        __syncthreads();
+        if (wv == 0 && own) {
+            S x = acol;
+            for (int c = 0; c < i; ++c) x = sub(x, mul(yc[c][lane], sv[c]));
+            xs[lane] = x;
+        }
+        __syncthreads();
+        for (int c = wv; c < i; c += 16) {
+            S p = s_zero<S>();
+            if (own && rown >= k + 1) p = add(p, mul(cj(vc[c][lane]), xs[lane]));
+            p = wsum(p);
+            if (lane == 0) st_ag(&a.part[grp * NB + c], p);
+        }
+        grid_barrier(a.bar, target, a.err, a.hier);
+        // ---------------- P2
+        gather2(a.part, i, sw);
+        if (tid < i) {
+            S s = s_zero<S>();
+            for (int c = 0; c <= tid; ++c) s = add(s, mul(cj(Tl[c + tid * NB]), sw[c]));
+            st[tid] = s;
+        }
+        __syncthreads();
+        if (wv == 0) {
+            double tl = 0.0;
+            if (own) {
+                S x = xs[lane];
+                if (rown >= k + 1)
+                    for (int c = 0; c < i; ++c) x = sub(x, mul(vc[c][lane], st[c]));
+                xs[lane] = x;
+                if (rown >= j + 2) {
+                    tl += sq_abs(x);
+                    st_ag(&a.xu[rown], x);
+                }
+                if (rown == j + 1) st_ag(a.x0, x);
+                if (i + 1 < a.nbp) acol = a.A[rown + (int64_t)(j + 1) * n];
+            }
+            tl = wave_sum(tl);
+            if (lane == 0) st_agent(&a.tpart[grp], tl);
+        }
+        __syncthreads();
+        for (int c = wv; c < i; c += 16) {
+            S p = s_zero<S>();
+            if (own && rown >= j + 2) p = add(p, mul(cj(vc[c][lane]), xs[lane]));
+            p = wsum(p);
+            if (lane == 0) st_ag(&a.part[(G + grp) * NB + c], p);
+        }
+        grid_barrier(a.bar, target, a.err, a.hier);
+        // ---------------- P3 + P4: one batch of loads
+        S xt[kXU];
+#pragma unroll
+        for (int u = 0; u < kXU; ++u) xt[u] = ld_ag(&a.xu[min(max(tid + u * kCoopThreads, j + 2), n - 1)]);
+        S gt[kGU];
+        const int gc = tid % NB, gsl = tid / NB;
+#pragma unroll
+        for (int u = 0; u < kGU; ++u) {
+            const int b = gsl + u * kSl;
+            gt[u] = (gc < i && b < G) ? ld_ag(&a.part[(G + b) * NB + gc]) : s_zero<S>();
+        }
+        const double tpv = tid < G ? ld_agent(&a.tpart[tid]) : 0.0;
+        const S vrow = tid < i ? ld_ag(&a.V[(j + 1) + (int64_t)tid * n]) : s_zero<S>();
+        const S x0 = ld_ag(a.x0);
+        {
+            S acc = s_zero<S>();
+#pragma unroll
+            for (int u = 0; u < kGU; ++u) acc = add(acc, gt[u]);
+            red[tid] = acc;
+        }
+#pragma unroll
+        for (int u = 0; u < kXU; ++u)
+            if (tid + u * kCoopThreads < n) vsh[tid + u * kCoopThreads] = xt[u];   // scaled below
+        if (tid < G) tps[tid] = tpv;
+        __syncthreads();
+        if (tid == 0) {
+            double tail = 0.0;
+            for (int b = 0; b < G; ++b) tail += tps[b];
+            bool skr;
+            S v0, alpha;
+            double rv;
+            hess_reflector(x0, tail, skr, v0, rv, alpha);
+            s_sk = skr ? 1 : 0;
+            s_scal[1] = v0;
+            s_rv = rv;
+            s_scal[2] = alpha;
+        }
+        if (tid < i) {
+            S acc = s_zero<S>();
+            for (int sl = 0; sl < kSl; ++sl) acc = add(acc, red[sl * NB + tid]);
+            sw[tid] = acc;   // the reduced partials of V^H xu
+        }
+        __syncthreads();
+        const bool sk = s_sk != 0;
+        const S v0 = s_scal[1], alpha = s_scal[2];
+        const double rv = s_rv;
+        if (wv == 0 && own) {
+            const S x = xs[lane];
+            S v = s_zero<S>();
+            if (!sk && rown > j) v = scal(rown == j + 1 ? v0 : x, rv);
+            st_ag(&a.V[rown + (int64_t)i * n], v);
+            vc[i][lane] = v;
+            S red_col = x;
+            if (!sk && rown == j + 1) red_col = alpha;
+            if (!sk && rown > j + 1) red_col = s_zero<S>();
+            a.A[rown + (int64_t)j * n] = red_col;
+        }
+#pragma unroll
+        for (int u = 0; u < kXU; ++u) {
+            const int r = tid + u * kCoopThreads;
+            if (r < n) vsh[r] = (sk || r <= j) ? s_zero<S>() : scal(r == j + 1 ? v0 : vsh[r], rv);
+        }
+        if (tid < i) {
+            const S u = add(mul(cj(vrow), v0), sw[tid]);
+            sv[tid] = sk ? s_zero<S>() : scal(u, rv);
+            s_vj[tid] = vrow;
+        }
+        if (tid == i) s_vj[i] = sk ? s_zero<S>() : scal(v0, rv);
+        __syncthreads();
+        S yacc = s_zero<S>();
+        if (!sk) {
+            const int rl = lane & (rp - 1), sub = 64 / rp;
+            const int cs = 16 * sub;
+            const int r = min(r0 + rl, r1 - 1);
+            int c = j + 1 + wv * sub + lane / rp;
+            constexpr int kB = kGemvBatch * (int)sizeof(double) / (int)sizeof(S);
+            for (; c + cs * (kB - 1) < n; c += cs * kB) {
+                S av[kB];
+#pragma unroll
+                for (int u = 0; u < kB; ++u) av[u] = a.A[r + (int64_t)(c + cs * u) * n];
+#pragma unroll
+                for (int u = 0; u < kB; ++u) yacc = add(yacc, mul(av[u], vsh[c + cs * u]));
+            }
+            for (; c < n; c += cs) yacc = add(yacc, mul(a.A[r + (int64_t)c * n], vsh[c]));
+        }
+        ysum[wv][lane] = yacc;
+        __syncthreads();
+        if (wv == 0 && own) {
+            S y = s_zero<S>();
+            for (int w = 0; w < 16; ++w)
+                for (int l = lane; l < 64; l += rp) y = add(y, ysum[w][l]);
+            for (int c = 0; c < i; ++c) y = sub(y, mul(yc[c][lane], sv[c]));
+            const S yv = sk ? s_zero<S>() : two_x(y);
+            a.Y[rown + (int64_t)i * n] = yv;
+            yc[i][lane] = yv;
+        }
+        if (tid <= i) {
+            S tc;
+            set_re_im(tc, 2.0, 0.0);
+            if (tid < i) {
+                S s = s_zero<S>();
+                for (int q = tid; q < i; ++q) s = add(s, mul(Tl[tid + q * NB], sv[q]));
+                tc = neg2(s);
+            }
+            Tl[tid + i * NB] = tc;
+            if (blockIdx.x == 0) a.T[tid + i * NB] = tc;
+        }
+        __syncthreads();
+    }
+}
+
 // C (m x nn, ldc) += alpha * op(A) op(B); op = transpose when TA / TB.  64x64 tiles, 4x4/thread.
 // Split-K: blockIdx.z takes rows [z kc, (z+1) kc) of the K range and, when gridDim.z > 1, writes its
 // partial product to C + z * zstride (beta must be 0 then; gemm_reduce adds the partials in z order).
@@ -1162,9 +1389,15 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         const char* e = std::getenv("EIGSOL_HESS_MERGE");
         return !(e && std::atoi(e) == 0);
     }();
+    // EIGSOL_HESS_PANEL2=0: the merged panel without the LDS caches and the batched loads
+    const bool panel2 = [] {   // read per call (the bitwise test switches it)
+        const char* e = std::getenv("EIGSOL_HESS_PANEL2");
+        return !(e && std::atoi(e) == 0);
+    }();
     const void* coop_kernel =
         n <= 64 * G
-            ? (merge ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1, true>)
+            ? (merge ? (panel2 ? reinterpret_cast<const void*>(dev::hess_panel_coop2<S>)
+                               : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1, true>))
                      : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1>))
             : (merge ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 2, true>)
                      : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 2>));

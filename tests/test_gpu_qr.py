@@ -334,6 +334,25 @@ def test_complex_hessenberg_blocked(ctx, coop, monkeypatch):
     assert np.abs(np.tril(H, -2)).max() == 0.0
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+@pytest.mark.parametrize("n", [300, 1000, 2100])
+def test_hessenberg_panel2_bitwise(ctx, dtype, n, monkeypatch):
+    """The cooperative panel with LDS-cached own rows and one batch of loads after the second grid
+    barrier (hess_panel_coop2, the default) performs the merged panel's operations in the same order:
+    H bitwise equal to EIGSOL_HESS_PANEL2=0's, for grids of 16, 32 and 72 blocks (the last with the
+    two-level barrier), and within the oracle's tolerance (to_hessenberg.hpp:38-77)."""
+    rng = np.random.default_rng(n)
+    A = rng.standard_normal((n, n))
+    if dtype == np.complex128:
+        A = A + 1j * rng.standard_normal((n, n))
+    H2 = E.to_hessenberg(ctx, A)
+    monkeypatch.setenv("EIGSOL_HESS_PANEL2", "0")
+    H1 = E.to_hessenberg(ctx, A)
+    assert H1.tobytes() == H2.tobytes()
+    if n == 300:
+        assert np.abs(H2 - O.hessenberg(A)).max() <= 1e-12 * np.linalg.norm(A)
+
+
 def test_complex_francis_4096_fixture(ctx):
     """Complex QR at the config-2 order: blocked complex Hessenberg, complex AED and multishift
     sweeps, matched one-to-one against LAPACK zgeev (tests/golden/qr_c4096_eigvals.npy)."""
