@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop2(CoopArgs<S> a) 
         if (tid == i) s_vj[i] = sk ? s_zero<S>() : scal(v0, rv);
         __syncthreads();
         S yacc = s_zero<S>();
-        if (!sk) {
+        if (!sk && !EIGSOL_HESS_SKIP_GEMV) {
             const int rl = lane & (rp - 1), sub = 64 / rp;
             const int cs = 16 * sub;
             const int r = min(r0 + rl, r1 - 1);
