@@ -1,5 +1,6 @@
 #!/bin/bash
 # f64 MFMA GEMM K-step (EIGSOL_GEMM_KT 16 / 32 / 64): kernel trace of to_hessenberg 4096^2 (tools/hess_prof.sh),
+# (the EIGSOL_GEMM_KT switch was measured flat and removed; the script documents profiles/r06_gemm_kt_ab.log)
 # summed GEMM kernel time of the last reduction, then QR 4096^2 (tools/bench_qr.py)
 set -o pipefail
 mkdir -p gpurun_out/r6
