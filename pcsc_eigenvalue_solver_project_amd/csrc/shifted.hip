@@ -132,6 +132,8 @@ struct ShiftFactor {
     int32_t* flag_f = nullptr;
     int32_t* flag_b = nullptr;
     void* zf = nullptr;
+    void* tinv = nullptr;         // [nblk][2] inverted diagonal blocks inv(L_kk), inv(U_kk), 64 x 64 column-major
+    int dense_v = 2;              // substitution kernel: 2 = dense_trsv2_kernel, 1 = dense_trsv_kernel (EIGSOL_DENSE_TRSV=1)
 };
 
 namespace dev {
@@ -1335,6 +1337,7 @@ struct DenseTriArgs {
     int32_t epoch;
     int32_t* flag_f;     // [nblk] epoch when z of the block row is published
     int32_t* flag_b;     // [nblk] epoch when y of the block row is published
+    const S* tinv;       // dense_trsv2_kernel: [nblk][2] inv(L_kk), inv(U_kk), 64 x 64 column-major
     S* z;                // forward results (n)
     const S* b_plain;
     S* y_plain;
@@ -1511,6 +1514,216 @@ __global__ __launch_bounds__(256) void dense_trsv_kernel(DenseTriArgs<S> a, int 
             st_agent(&p->a, n2);
             st_agent(&p->b, pr);
             st_agent(&p->c, pi);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t tk = __hip_atomic_fetch_add(&a.work[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (tk == gridDim.x - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if constexpr (kIter) {
+        if (tid == 0) {
+            double sa = 0.0, sb = 0.0, sc = 0.0;
+            for (int i = 0; i < G; ++i) {
+                sa += ld_agent(&a.wave_part[i].a);
+                sb += ld_agent(&a.wave_part[i].b);
+                sc += ld_agent(&a.wave_part[i].c);
+            }
+            a.my_part->a = sa;
+            a.my_part->b = sb;
+            a.my_part->c = sc;
+            a.my_part->d = 0.0;
+        }
+    }
+    if (tid == 0) __hip_atomic_store(&a.work[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Inverted diagonal blocks of a dense LU factor (after the factorization; one workgroup per block and
+// triangle): tinv + 4096 (2 k) = inv(L_kk) (unit lower), tinv + 4096 (2 k + 1) = inv(U_kk), 64 x 64
+// column-major, the identity past a partial last block.  Wave w solves for the 16 unit vectors
+// e_{16 w} .. e_{16 w + 15} at once, lane = row, the solved entry broadcast by v_readlane.
+template <class S>
+__global__ __launch_bounds__(256) void dense_tinv_kernel(const S* lu, int64_t n, S* tinv) {
+    __shared__ S tri[kDB * (kDB + 1)];
+    const int k = blockIdx.x, upper = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t r0 = (int64_t)k * kDB;
+    const int rn = (int)min<int64_t>(kDB, n - r0);
+    for (int e = tid; e < kDB * kDB; e += 256) {
+        const int i = e % kDB, j = e / kDB;
+        S v = s_zero<S>();
+        if (i < rn && j < rn) v = lu[(r0 + i) + (r0 + j) * n];
+        else if (i == j) set_re_im(v, 1.0, 0.0);
+        tri[i + j * (kDB + 1)] = v;
+    }
+    __syncthreads();
+    S v[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        v[t] = s_zero<S>();
+        if (lane == 16 * wv + t) set_re_im(v[t], 1.0, 0.0);
+    }
+    if (!upper) {
+        for (int j = 0; j < kDB; ++j) {
+            const S lij = tri[lane + j * (kDB + 1)];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const S zj = readlane_s(v[t], j);
+                if (lane > j) v[t] = sub(v[t], mul(lij, zj));
+            }
+        }
+    } else {
+        for (int j = kDB - 1; j >= 0; --j) {
+            const S ujj = tri[j + j * (kDB + 1)];
+            const S uij = tri[lane + j * (kDB + 1)];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                if (lane == j) v[t] = sdiv(v[t], ujj);
+                const S zj = readlane_s(v[t], j);
+                if (lane < j) v[t] = sub(v[t], mul(uij, zj));
+            }
+        }
+    }
+    S* out = tinv + (int64_t)(2 * k + upper) * kDB * kDB;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) out[(16 * wv + t) * kDB + lane] = v[t];
+}
+
+// The multi-CU substitution with the diagonal blocks applied as products with their inverses
+// (dense_tinv_kernel) and every off-diagonal tile loaded before its block's flag is awaited (the
+// multifrontal row-block solve's scheme, mf_big_fwd_kernel).  A block row: each wave takes 16 columns
+// of every column block - forward c = 0 .. r - 1, backward c = nblk - 1 .. r + 1 - loads its 64 x 16
+// piece of the tile, waits for the block's flag (relaxed polls; the published values are read with
+// coherent loads), and accumulates; then t = rhs - sum, y = inv(T_rr) t as four 64 x 16 products
+// from registers, published with one flag.  The per-block hand-off is a few round trips instead of
+// the 64-step triangle of dense_trsv_kernel.  Workgroups take block rows round-robin like it.
+__device__ __forceinline__ void wait_flag_relaxed(const int32_t* f, int32_t epoch, int32_t* err) {
+    int spins = 0;
+    while (__hip_atomic_load(const_cast<int32_t*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 24)) { atomicOr(err, 1); break; }
+    }
+}
+
+template <class S, bool kIter>
+__global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int parity) {
+    __shared__ S part[4][kDB];
+    __shared__ S zsh[4][16];
+    __shared__ S vec[kDB];
+    __shared__ Prologue pro;
+    __shared__ int s_last;
+    const S* xin;
+    S* yout;
+    double nrm = 0.0;
+    if constexpr (kIter) {
+        shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // epoch flags: nothing to reset
+        nrm = pro.nrm;
+        xin = parity ? a.buf0 : a.buf1;
+        yout = parity ? a.buf1 : a.buf0;
+    } else {
+        xin = a.b_plain;
+        yout = a.y_plain;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t n = a.n;
+    const int G = gridDim.x;
+    double n2 = 0.0, pr = 0.0, pi = 0.0;
+    for (int phase = 0; phase < 2; ++phase) {
+        const bool fwd = phase == 0;
+        const int cnt = a.nblk > (int)blockIdx.x ? (a.nblk - 1 - (int)blockIdx.x) / G + 1 : 0;
+        for (int q = 0; q < cnt; ++q) {
+            const int r = fwd ? (int)blockIdx.x + q * G : (int)blockIdx.x + (cnt - 1 - q) * G;
+            const int64_t r0 = (int64_t)r * kDB;
+            const int rn = (int)min<int64_t>(kDB, n - r0);
+            const int64_t row = r0 + min(lane, rn - 1);
+            // this wave's 16 columns of the inverted diagonal block, and the block row's right-hand side
+            S iv[16];
+            {
+                const S* ti = a.tinv + (int64_t)(2 * r + (fwd ? 0 : 1)) * kDB * kDB + (16 * wv) * kDB + lane;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) iv[t] = ti[t * kDB];
+            }
+            S rhs = s_zero<S>();
+            if (wv == 0 && lane < rn) {
+                if (fwd) {
+                    rhs = xin[a.perm[r0 + lane]];
+                    if constexpr (kIter) rhs = scale_in(rhs, nrm);
+                } else {
+                    rhs = ld_coh(a.z + r0 + lane);   // published by this workgroup in the forward phase
+                }
+            }
+            S acc = s_zero<S>();
+            const int nc = fwd ? r : a.nblk - 1 - r;
+            const S* src = fwd ? a.z : yout;
+            const int32_t* fl = fwd ? a.flag_f : a.flag_b;
+            for (int m = 0; m < nc; ++m) {
+                const int c = fwd ? m : a.nblk - 1 - m;
+                const int64_t c0 = (int64_t)c * kDB;
+                const int cn = (int)min<int64_t>(kDB, n - c0);
+                const int j0 = 16 * wv;
+                S tv[16];
+                const S* tile = a.lu + row;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) tv[t] = tile[(c0 + min(j0 + t, cn - 1)) * n];
+                if (lane == 0) wait_flag_relaxed(fl + c, a.epoch, a.err);
+                __builtin_amdgcn_wave_barrier();
+                if (lane < 16) zsh[wv][lane] = j0 + lane < cn ? ld_coh(src + c0 + j0 + lane) : s_zero<S>();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int t = 0; t < 16; ++t) acc = add(acc, mul(tv[t], zsh[wv][t]));
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
+            part[wv][lane] = acc;
+            __syncthreads();
+            if (wv == 0)
+                vec[lane] = lane < rn ? sub(rhs, add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane])))
+                                      : s_zero<S>();
+            __syncthreads();
+            S p = s_zero<S>();
+#pragma unroll
+            for (int t = 0; t < 16; ++t) p = add(p, mul(iv[t], vec[16 * wv + t]));
+            part[wv][lane] = p;
+            __syncthreads();
+            if (wv == 0) {
+                const S y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+                if (lane < rn) {
+                    if (fwd) {
+                        st_coh(a.z + r0 + lane, y);
+                    } else {
+                        st_coh(yout + r0 + lane, y);
+                        if constexpr (kIter) {
+                            S xi = xin[r0 + lane];
+                            xi = scale_in(xi, nrm);
+                            n2 += sq_abs(y);
+                            acc_dot(pr, pi, xi, y);
+                        }
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store(fwd ? a.flag_f + r : a.flag_b + r, a.epoch, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+        }
+    }
+    // workgroup partials (wave 0 holds them), then the last arriver sums them in workgroup order
+    if (wv == 0) {
+        n2 = wave_sum(n2);
+        pr = wave_sum(pr);
+        pi = wave_sum(pi);
+        if (lane == 0) {
+            part4* pp = a.wave_part + blockIdx.x;
+            st_agent(&pp->a, n2);
+            st_agent(&pp->b, pr);
+            st_agent(&pp->c, pi);
         }
     }
     __syncthreads();
@@ -1823,7 +2036,7 @@ static void shift_free(ShiftFactor* f) {
                     f->tpiv, (void*)f->tcol, f->tval, (void*)f->porder, (void*)f->pptr, (void*)f->pcol, f->pval,
                     f->ppiv,
                     (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
-                    (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf,
+                    (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf, f->tinv,
                     f->kpart, f->kblk, f->promo})
         if (p) hipFree(p);
     for (int j = 0; j < dev::kMaxMulti; ++j) {
@@ -1914,6 +2127,24 @@ static int dense_lu_factor(ShiftFactor* f, bool from_sparse) {
         EIGSOL_HIP(hipMemsetAsync(f->flag_b, 0, sizeof(int32_t) * nblk, st));
         EIGSOL_HIP(hipMemsetAsync(f->work, 0, 64, st));
         EIGSOL_HIP(hipMemsetAsync(f->err, 0, 64, st));
+        // EIGSOL_DENSE_TRSV=1: round 5's substitution (64-step triangles on one wave, 32 workgroups)
+        const char* dv = std::getenv("EIGSOL_DENSE_TRSV");
+        f->dense_v = (dv && std::atoi(dv) == 1) ? 1 : 2;
+        if (f->dense_v == 2) {
+            EIGSOL_HIP(hipMalloc(&f->tinv, sizeof(S) * (size_t)nblk * 2 * dev::kDB * dev::kDB));
+            hipLaunchKernelGGL((dev::dense_tinv_kernel<S>), dim3(nblk, 2), dim3(256), 0, st, static_cast<const S*>(f->lu),
+                               n, static_cast<S*>(f->tinv));
+            EIGSOL_HIP(hipGetLastError());
+            // one block row per workgroup while they all fit on the device at once (a cooperative launch)
+            int per_cu = 1;
+            EIGSOL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu, reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, true>), 256, 0));
+            f->grid = std::max(1, std::min(nblk, std::max(1, per_cu) * f->ctx->num_cus));
+            if (const char* e = std::getenv("EIGSOL_DENSE_TRSV_GRID")) f->grid = std::max(1, std::min(nblk, std::atoi(e)));
+            hipFree(f->wave_part);
+            f->wave_part = nullptr;
+            EIGSOL_HIP(hipMalloc(&f->wave_part, sizeof(dev::part4) * f->grid));
+        }
         EIGSOL_HIP(hipStreamSynchronize(st));
     }
     return EIGSOL_OK;
@@ -2116,6 +2347,8 @@ static int gmres_dense_fallback(ShiftFactor* f, int rc_gmres) {
         f->flag_f = g->flag_f;
         f->flag_b = g->flag_b;
         f->zf = g->zf;
+        f->tinv = g->tinv;
+        f->dense_v = g->dense_v;
         f->work = g->work;
         f->err = g->err;
         f->wave_part = g->wave_part;
@@ -3299,6 +3532,7 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.epoch = ++f->epoch;
         a.flag_f = f->flag_f;
         a.flag_b = f->flag_b;
+        a.tinv = static_cast<const S*>(f->tinv);
         a.z = static_cast<S*>(f->zf);
         a.b_plain = static_cast<const S*>(b);
         a.y_plain = static_cast<S*>(y);
@@ -3315,8 +3549,11 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.sig_im = f->sig_im;
         // cooperative: the persistent block-row workgroups wait on each other's epoch flags
         void* kargs[] = {&a, &parity};
-        const void* dk = iter ? reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, true>)
-                              : reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, false>);
+        const void* dk = f->dense_v == 2
+                             ? (iter ? reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, true>)
+                                     : reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, false>))
+                             : (iter ? reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, true>)
+                                     : reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, false>));
         EIGSOL_HIP(hipLaunchCooperativeKernel(dk, dim3(f->grid), dim3(256), kargs, 0, st));
     } else {
         dev::DenseSolveArgs<S> a{};

@@ -316,6 +316,33 @@ def test_dense_multi_cu_substitution_matches_single_cu(ctx, dtype, monkeypatch):
     assert np.linalg.norm(M @ x - b) <= 1e-12 * n * np.linalg.norm(M, 2) * np.linalg.norm(x)
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+@pytest.mark.parametrize("grid", [None, "7"])
+def test_dense_trsv2_matches_round5_substitution(ctx, dtype, grid, monkeypatch):
+    """The multi-CU substitution with inverted diagonal blocks (dense_trsv2_kernel, default) against
+    round 5's triangle substitution (EIGSOL_DENSE_TRSV=1) on the same factor: solve_shifted within
+    1e-12 relative, both backward stable, with a partial last block (n = 3000) and with fewer
+    workgroups than block rows (EIGSOL_DENSE_TRSV_GRID=7: rows taken round-robin).  Reference:
+    solve_shifted.hpp:85-96 (PartialPivLU solve)."""
+    rng = np.random.default_rng(33)
+    n = 3000
+    A = rng.standard_normal((n, n))
+    if dtype == np.complex128:
+        A = A + 1j * rng.standard_normal((n, n))
+    A = (A / np.sqrt(n) + np.diag(np.linspace(1.0, 4.0, n))).astype(dtype)
+    sigma = 2.501 if dtype == np.float64 else 2.501 + 0.01j
+    b = rng.standard_normal(n).astype(dtype)
+    if grid:
+        monkeypatch.setenv("EIGSOL_DENSE_TRSV_GRID", grid)
+    x2 = E.solve_shifted(E.DenseMatrix(ctx, A), sigma, b)
+    monkeypatch.setenv("EIGSOL_DENSE_TRSV", "1")
+    x1 = E.solve_shifted(E.DenseMatrix(ctx, A), sigma, b)
+    M = A - sigma * np.eye(n)
+    for x in (x1, x2):
+        assert np.linalg.norm(M @ x - b) <= 1e-12 * n * np.linalg.norm(M, 2) * np.linalg.norm(x)
+    assert np.linalg.norm(x2 - x1) <= 1e-12 * np.linalg.cond(M) * np.linalg.norm(x1)
+
+
 def test_dense_shifted_above_single_cu_limit(ctx):
     """n = 20000 f64 (3.2 GB): beyond the former single-CU LDS limit (18432); residual check."""
     rng = np.random.default_rng(5)
