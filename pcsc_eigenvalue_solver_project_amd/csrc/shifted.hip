@@ -1596,16 +1596,45 @@ __global__ __launch_bounds__(256) void dense_tinv_kernel(const S* lu, int64_t n,
 // (dense_tinv_kernel) and every off-diagonal tile loaded before its block's flag is awaited (the
 // multifrontal row-block solve's scheme, mf_big_fwd_kernel).  A block row: each wave takes 16 columns
 // of every column block - forward c = 0 .. r - 1, backward c = nblk - 1 .. r + 1 - loads its 64 x 16
-// piece of the tile, waits for the block's flag (relaxed polls; the published values are read with
-// coherent loads), and accumulates; then t = rhs - sum, y = inv(T_rr) t as four 64 x 16 products
-// from registers, published with one flag.  The per-block hand-off is a few round trips instead of
-// the 64-step triangle of dense_trsv_kernel.  Workgroups take block rows round-robin like it.
-__device__ __forceinline__ void wait_flag_relaxed(const int32_t* f, int32_t epoch, int32_t* err) {
+// piece of the tile, polls the block's 16 published values (value flags, below), and accumulates;
+// then t = rhs - sum, y = inv(T_rr) t as four 64 x 16 products from registers, published by 64
+// write-through stores.  The per-block hand-off is one store and one poll instead of the 64-step
+// triangle of dense_trsv_kernel and its epoch flag.  Workgroups take block rows round-robin like it.
+// value flags of dense_trsv2_kernel: an unsolved entry holds this NaN in every 8-byte word, a solved one
+// never does (a NaN result is stored as the default quiet NaN), so a waiting wave polls the values
+// themselves.  Two buffers alternate by the launch's epoch: a launch solves in one and resets its own
+// rows of the other for the next launch (no reader of the other buffer is running).
+constexpr unsigned long long kDnSent = 0x7FF4DEAD7FF4DEADull;
+__device__ __forceinline__ bool dn_unready(double v) { return (unsigned long long)__double_as_longlong(v) == kDnSent; }
+__device__ __forceinline__ bool dn_unready(cplx v) { return dn_unready(v.re) || dn_unready(v.im); }
+__device__ __forceinline__ bool dn_unready(float v) { return (unsigned)__float_as_int(v) == (unsigned)(kDnSent & 0xffffffffu); }
+__device__ __forceinline__ bool dn_unready(cplxf v) { return dn_unready(v.re) || dn_unready(v.im); }
+template <class S>
+__device__ __forceinline__ S dn_sent() {
+    S v;
+    if constexpr (std::is_same_v<S, double>) v = __longlong_as_double((long long)kDnSent);
+    else if constexpr (std::is_same_v<S, cplx>) v = cplx{__longlong_as_double((long long)kDnSent), __longlong_as_double((long long)kDnSent)};
+    else if constexpr (std::is_same_v<S, float>) v = __int_as_float((int)(kDnSent & 0xffffffffu));
+    else v = cplxf{__int_as_float((int)(kDnSent & 0xffffffffu)), __int_as_float((int)(kDnSent & 0xffffffffu))};
+    return v;
+}
+__device__ __forceinline__ double dn_clean(double v) { return v != v ? __longlong_as_double(0x7FF8000000000000ll) : v; }
+__device__ __forceinline__ cplx dn_clean(cplx v) { return cplx{dn_clean(v.re), dn_clean(v.im)}; }
+__device__ __forceinline__ float dn_clean(float v) { return v != v ? __int_as_float(0x7FC00000) : v; }
+__device__ __forceinline__ cplxf dn_clean(cplxf v) { return cplxf{dn_clean(v.re), dn_clean(v.im)}; }
+template <class S>
+__device__ __forceinline__ S dn_poll(const S* p, int32_t* err) {
+    S v = ld_coh(p);
     int spins = 0;
-    while (__hip_atomic_load(const_cast<int32_t*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    while (dn_unready(v)) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1 << 24)) { atomicOr(err, 1); break; }
+        v = ld_coh(p);
+        if (++spins > (1 << 24)) {
+            atomicOr(err, 1);
+            break;
+        }
     }
+    return v;
 }
 
 template <class S, bool kIter>
@@ -1618,9 +1647,30 @@ __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int
     const S* xin;
     S* yout;
     double nrm = 0.0;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t n = a.n;
+    const int G = gridDim.x;
+    const int cnt = a.nblk > (int)blockIdx.x ? (a.nblk - 1 - (int)blockIdx.x) / G + 1 : 0;
+    // a.z: [z | z' | y | y'] value buffers; this launch solves in (z, y) of its epoch's parity and
+    // resets its own rows of the other pair for the next launch (also when the iteration has stopped)
+    const int64_t pp = a.epoch & 1;
+    S* zcur = a.z + pp * n;
+    S* ycur = a.z + (2 + pp) * n;
+    {
+        S* znext = a.z + (1 - pp) * n;
+        S* ynext = a.z + (3 - pp) * n;
+        const S sent = dn_sent<S>();
+        for (int q = 0; q < cnt; ++q) {
+            const int64_t r0 = (int64_t)((int)blockIdx.x + q * G) * kDB;
+            if (tid < kDB && r0 + tid < n) {
+                st_coh(znext + r0 + tid, sent);
+                st_coh(ynext + r0 + tid, sent);
+            }
+        }
+    }
     if constexpr (kIter) {
         shift_prologue<S>(a.ctl, a.rank_part, parity, a.trace, a.sig_re, a.sig_im, &pro);
-        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;   // epoch flags: nothing to reset
+        if (!__builtin_amdgcn_readfirstlane(pro.go)) return;
         nrm = pro.nrm;
         xin = parity ? a.buf0 : a.buf1;
         yout = parity ? a.buf1 : a.buf0;
@@ -1628,13 +1678,9 @@ __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int
         xin = a.b_plain;
         yout = a.y_plain;
     }
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int64_t n = a.n;
-    const int G = gridDim.x;
     double n2 = 0.0, pr = 0.0, pi = 0.0;
     for (int phase = 0; phase < 2; ++phase) {
         const bool fwd = phase == 0;
-        const int cnt = a.nblk > (int)blockIdx.x ? (a.nblk - 1 - (int)blockIdx.x) / G + 1 : 0;
         for (int q = 0; q < cnt; ++q) {
             const int r = fwd ? (int)blockIdx.x + q * G : (int)blockIdx.x + (cnt - 1 - q) * G;
             const int64_t r0 = (int64_t)r * kDB;
@@ -1653,13 +1699,12 @@ __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int
                     rhs = xin[a.perm[r0 + lane]];
                     if constexpr (kIter) rhs = scale_in(rhs, nrm);
                 } else {
-                    rhs = ld_coh(a.z + r0 + lane);   // published by this workgroup in the forward phase
+                    rhs = dn_poll(zcur + r0 + lane, a.err);   // published by this workgroup in the forward phase
                 }
             }
             S acc = s_zero<S>();
             const int nc = fwd ? r : a.nblk - 1 - r;
-            const S* src = fwd ? a.z : yout;
-            const int32_t* fl = fwd ? a.flag_f : a.flag_b;
+            const S* src = fwd ? zcur : ycur;
             for (int m = 0; m < nc; ++m) {
                 const int c = fwd ? m : a.nblk - 1 - m;
                 const int64_t c0 = (int64_t)c * kDB;
@@ -1669,9 +1714,7 @@ __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int
                 const S* tile = a.lu + row;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) tv[t] = tile[(c0 + min(j0 + t, cn - 1)) * n];
-                if (lane == 0) wait_flag_relaxed(fl + c, a.epoch, a.err);
-                __builtin_amdgcn_wave_barrier();
-                if (lane < 16) zsh[wv][lane] = j0 + lane < cn ? ld_coh(src + c0 + j0 + lane) : s_zero<S>();
+                if (lane < 16) zsh[wv][lane] = j0 + lane < cn ? dn_poll(src + c0 + j0 + lane, a.err) : s_zero<S>();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1694,10 +1737,12 @@ __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int
             if (wv == 0) {
                 const S y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
                 if (lane < rn) {
+                    // publish (the value is its own flag)
                     if (fwd) {
-                        st_coh(a.z + r0 + lane, y);
+                        st_coh(zcur + r0 + lane, dn_clean(y));
                     } else {
-                        st_coh(yout + r0 + lane, y);
+                        st_coh(ycur + r0 + lane, dn_clean(y));
+                        yout[r0 + lane] = y;
                         if constexpr (kIter) {
                             S xi = xin[r0 + lane];
                             xi = scale_in(xi, nrm);
@@ -1706,10 +1751,6 @@ __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int
                         }
                     }
                 }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0)
-                    __hip_atomic_store(fwd ? a.flag_f + r : a.flag_b + r, a.epoch, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
             }
             __syncthreads();
         }
@@ -2131,6 +2172,11 @@ static int dense_lu_factor(ShiftFactor* f, bool from_sparse) {
         const char* dv = std::getenv("EIGSOL_DENSE_TRSV");
         f->dense_v = (dv && std::atoi(dv) == 1) ? 1 : 2;
         if (f->dense_v == 2) {
+            // value buffers [z | z' | y | y'] (dense_trsv2_kernel), all unsolved
+            hipFree(f->zf);
+            f->zf = nullptr;
+            EIGSOL_HIP(hipMalloc(&f->zf, sizeof(S) * 4 * n));
+            EIGSOL_HIP(hipMemsetD32Async(static_cast<hipDeviceptr_t>(f->zf), 0x7FF4DEADu, sizeof(S) * n, st));
             EIGSOL_HIP(hipMalloc(&f->tinv, sizeof(S) * (size_t)nblk * 2 * dev::kDB * dev::kDB));
             hipLaunchKernelGGL((dev::dense_tinv_kernel<S>), dim3(nblk, 2), dim3(256), 0, st, static_cast<const S*>(f->lu),
                                n, static_cast<S*>(f->tinv));
