@@ -540,9 +540,25 @@ def run_dense_power(E, S, ctx, torch, stream):
     info = s.kernel_info()
     gbs = info["bytes_per_iteration"] / (ms / 1e3) / 1e9
     s.close()
+    # the same matrix through the dense shifted inverse (shifted_inverse_power_solver.hpp:49-76): the
+    # partial-pivot LU once, then per iteration both triangular solves (dense_trsv2_kernel) and the
+    # partials; steady state with tol < 0, like the power method above
+    t = time.perf_counter()
+    sh = E.ShiftedSession(D, 0.5)
+    t_factor = time.perf_counter() - t
+    sh.begin(E.ShiftedSolverOptions(2**31 - 1, -1.0, 0.5), S.start_vector(n))
+    sh.step(3)
+    torch.cuda.synchronize()
+    ms_sh = _events(torch, stream, lambda: sh.step(20)) / 20
+    info_sh = sh.kernel_info()
+    sh.close()
     D.close()
     return {"n": n, "dtype": "f64", "ms_per_iteration": round(ms, 4), "GB/s": round(gbs, 1),
-            "roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "kernel": info["kernel"]}
+            "roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "kernel": info["kernel"],
+            "shifted_inverse": {"sigma": 0.5, "factor_seconds": round(t_factor, 3),
+                                "ms_per_iteration": round(ms_sh, 4),
+                                "GB/s": round(info_sh["bytes_per_iteration"] / (ms_sh / 1e3) / 1e9, 1),
+                                "kernel": info_sh["kernel"]}}
 
 
 def run_config1(E, S, ctx):
