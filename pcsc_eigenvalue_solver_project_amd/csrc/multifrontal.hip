@@ -875,11 +875,9 @@ __device__ __forceinline__ void mf_wait(const int32_t* f, int32_t epoch, int32_t
 // z (d entries per large front) = the permuted pivot right-hand side, then the children's
 // contributions to the struct rows; one workgroup per front.  LDS: r (ns)
 template <class S>
-__global__ __launch_bounds__(256) void mf_big_asm_kernel(const MfFront* fr, const int32_t* list, const int32_t* chl,
-                                                         const int32_t* cmap, const int32_t* pinv, S* w,
-                                                         const S* u, S* z, int bo) {
-    extern __shared__ __align__(16) unsigned char lds_raw[];
-    const MfFront f = fr[list[blockIdx.x]];
+__device__ __forceinline__ void mf_big_asm_front(const MfFront& f, unsigned char* lds_raw, const MfFront* fr,
+                                                 const int32_t* chl, const int32_t* cmap, const int32_t* pinv, S* w,
+                                                 const S* u, S* z, int bo) {
     const int tid = threadIdx.x, ns = f.ns, ms = f.ms;
     S* r = reinterpret_cast<S*>(lds_raw);
     S* zs = z + f.zoff;
@@ -903,6 +901,27 @@ __global__ __launch_bounds__(256) void mf_big_asm_kernel(const MfFront* fr, cons
     // mf_big_fwd_kernel, the next launch
     if (bo & 4)
         for (int t = tid; t < ns; t += 256) mf_st(w + f.c0 + t, mf_sent(s_zero<S>()));
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void mf_big_asm_kernel(const MfFront* fr, const int32_t* list, const int32_t* chl,
+                                                         const int32_t* cmap, const int32_t* pinv, S* w,
+                                                         const S* u, S* z, int bo) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    mf_big_asm_front<S>(fr[list[blockIdx.x]], lds_raw, fr, chl, cmap, pinv, w, u, z, bo);
+}
+
+// one launch for a height's small fronts (workgroups [0, nsmall): mf_fwd_kernel) and its large fronts'
+// assembly (the rest: mf_big_asm_kernel); list = the small fronts, then the large ones.  They touch
+// disjoint rows of w and read only lower heights' contributions, so they need no order between them.
+template <class S>
+__global__ __launch_bounds__(256) void mf_fwd_asm_kernel(const MfFront* fr, const int32_t* list, int32_t nsmall,
+                                                         const int32_t* chl, const S* F, const int32_t* cmap,
+                                                         const int32_t* pinv, S* w, S* u, S* z, int bo) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const MfFront f = fr[list[blockIdx.x]];
+    if ((int32_t)blockIdx.x < nsmall) mf_fwd_front<S>(f, lds_raw, fr, chl, F, cmap, pinv, w, u);
+    else mf_big_asm_front<S>(f, lds_raw, fr, chl, cmap, pinv, w, u, z, bo);
 }
 
 template <class S>
@@ -1114,15 +1133,15 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
 // backward, large fronts: tab = (front, pivot block) pairs, blocks descending within a front:
 // t = y - U12 x(struct) - U[rows, later blocks] x, then inv(U_kk) t (publish, flag)
 template <class S>
-__global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, const int32_t* tab, const S* F,
-                                                         const S* Tinv, const int32_t* sidx, const S* w, S* x,
-                                                         int32_t* flag, int32_t epoch, int32_t* err, int bo) {
+__device__ __forceinline__ void mf_big_bwd_block(const int bid, const MfFront* fr, const int32_t* tab, const S* F,
+                                                 const S* Tinv, const int32_t* sidx, const S* w, S* x,
+                                                 int32_t* flag, int32_t epoch, int32_t* err, int bo) {
     __shared__ S part[4][64];
     __shared__ S ysh[4][16];
     __shared__ S vsh[64];
     extern __shared__ __align__(16) unsigned char xs_raw[];
     S* xsh = reinterpret_cast<S*>(xs_raw);   // x(struct), ms entries
-    const int s = tab[2 * blockIdx.x], rb = tab[2 * blockIdx.x + 1];
+    const int s = tab[2 * bid], rb = tab[2 * bid + 1];
     const MfFront f = fr[s];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int d = f.d, ns = f.ns, ms = f.ms;
@@ -1205,6 +1224,28 @@ __global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, cons
     if (lane < rn) mf_st(x + f.c0 + r0 + lane, xv);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void mf_big_bwd_kernel(const MfFront* fr, const int32_t* tab, const S* F,
+                                                         const S* Tinv, const int32_t* sidx, const S* w, S* x,
+                                                         int32_t* flag, int32_t epoch, int32_t* err, int bo) {
+    mf_big_bwd_block<S>((int)blockIdx.x, fr, tab, F, Tinv, sidx, w, x, flag, epoch, err, bo);
+}
+
+// one launch for a height's large-front row blocks (workgroups [0, nbb), waiting on each other's values;
+// dispatched first) and its small fronts (the rest, mf_bwd_kernel's; they read only their ancestors' x)
+template <class S>
+__global__ __launch_bounds__(256) void mf_bwd_big_small_kernel(const MfFront* fr, const int32_t* tab, int32_t nbb,
+                                                               const int32_t* list, const S* F, const S* Tinv,
+                                                               const int32_t* sidx, const S* w, S* x,
+                                                               int32_t* flag, int32_t epoch, int32_t* err, int bo) {
+    if ((int32_t)blockIdx.x < nbb) {
+        mf_big_bwd_block<S>((int)blockIdx.x, fr, tab, F, Tinv, sidx, w, x, flag, epoch, err, bo);
+    } else {
+        extern __shared__ __align__(16) unsigned char lds_raw[];
+        mf_bwd_front<S>(fr[list[blockIdx.x - nbb]], lds_raw, F, sidx, w, x);
+    }
 }
 
 // ---- large fronts, two pivot blocks per workgroup (EIGSOL_MF_PAIR=1, value flags only; off by
@@ -1492,6 +1533,7 @@ struct MfFactor {
     int32_t* sub_ranges = nullptr;
     int32_t nsub = 0, lds_sub_f = 0, lds_sub_b = 0;                // bit 0 forward, bit 1 backward (EIGSOL_MF_FLOW_MODE, debugging)
     int backoff = 2;                  // EIGSOL_MF_BACKOFF: 1 growing sleeps, 2 relaxed polls (flag stores: release)
+    bool fuse_asm = true;             // EIGSOL_MF_FUSE_ASM=0: small fronts and large-front assembly as two launches
     std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt, foff2, fcnt2, boff2, bcnt2;
     std::vector<int32_t> lds_asm;
     MfStats st;
@@ -2478,6 +2520,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     f->lds_asm = lds_asm;
     if (const char* e = std::getenv("EIGSOL_MF_PAIR")) f->pair = std::atoi(e) != 0;
     if (const char* e = std::getenv("EIGSOL_MF_BACKOFF")) f->backoff = std::atoi(e) & 3;
+    if (const char* e = std::getenv("EIGSOL_MF_FUSE_ASM")) f->fuse_asm = std::atoi(e) != 0;
     // value flags (bit 4; EIGSOL_MF_VALFLAG=0: epoch flags): 1M convection-diffusion 1.657 -> 1.567 ms
     {
         const char* e = std::getenv("EIGSOL_MF_VALFLAG");
@@ -2641,6 +2684,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_big_asm_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_asm_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_flow_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_flow_kernel<S>),
@@ -2654,7 +2699,10 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
                                 *std::max_element(f->lds_bbig.begin(), f->lds_bbig.end())) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_big_bwd2_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                *std::max_element(f->lds_bbig.begin(), f->lds_bbig.end())) != hipSuccess)
+                                *std::max_element(f->lds_bbig.begin(), f->lds_bbig.end())) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_bwd_big_small_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                std::max(mx, *std::max_element(f->lds_bbig.begin(), f->lds_bbig.end()))) != hipSuccess)
             rc = fail(EIGSOL_E_HIP, "solve_shifted: multifrontal solve LDS");
     }
     if (rc != EIGSOL_OK) {
@@ -2695,12 +2743,20 @@ static void mf_solve_enqueue(MfFactor* f, hipStream_t st, const S* b, S* out, in
         if (nw)
             hipLaunchKernelGGL((dev::mf_fwd_wave_kernel<S>), dim3((nw + 3) / 4), dim3(256), 0, st, f->fronts, L,
                                (int32_t)nw, f->chl, F, f->cmap, f->pinv, w, u);
-        if (f->nsmall[h])
+        // EIGSOL_MF_FUSE_ASM=0: the small fronts and the large fronts' assembly as two launches
+        const bool fuse = f->fuse_asm && f->nsmall[h] && f->nbig[h];
+        if (fuse)
+            hipLaunchKernelGGL((dev::mf_fwd_asm_kernel<S>), dim3(f->nsmall[h] + f->nbig[h]), dim3(256),
+                               std::max(f->lds_fwd[h], f->lds_asm[h]), st, f->fronts, L + nw, f->nsmall[h], f->chl, F,
+                               f->cmap, f->pinv, w, u, z, f->backoff);
+        else if (f->nsmall[h])
             hipLaunchKernelGGL((dev::mf_fwd_kernel<S>), dim3(f->nsmall[h]), dim3(256), f->lds_fwd[h], st, f->fronts,
                                L + nw, f->chl, F, f->cmap, f->pinv, w, u);
         if (f->nbig[h]) {
-            hipLaunchKernelGGL((dev::mf_big_asm_kernel<S>), dim3(f->nbig[h]), dim3(256), f->lds_asm[h], st, f->fronts,
-                               L + nw + f->nsmall[h], f->chl, f->cmap, f->pinv, w, (const S*)u, z, f->backoff);
+            if (!fuse)
+                hipLaunchKernelGGL((dev::mf_big_asm_kernel<S>), dim3(f->nbig[h]), dim3(256), f->lds_asm[h], st,
+                                   f->fronts, L + nw + f->nsmall[h], f->chl, f->cmap, f->pinv, w, (const S*)u, z,
+                                   f->backoff);
             if (pair)
                 hipLaunchKernelGGL((dev::mf_big_fwd2_kernel<S>), dim3(f->fcnt2[h]), dim3(256), 0, st, f->fronts,
                                    f->tabf2 + 2 * f->foff2[h], F, (const S*)f->tinv, (const S*)z, w, u, f->err,
@@ -2717,12 +2773,18 @@ static void mf_solve_enqueue(MfFactor* f, hipStream_t st, const S* b, S* out, in
             hipLaunchKernelGGL((dev::mf_big_bwd2_kernel<S>), dim3(f->bcnt2[h]), dim3(256), f->lds_bbig[h], st,
                                f->fronts, f->tabb2 + 2 * f->boff2[h], F, (const S*)f->tinv, f->sidx, (const S*)w, x,
                                f->err, f->backoff);
-        else if (f->nbig[h])
+        const bool fuse = f->fuse_asm && !pair && f->nbig[h] && f->nsmall[h];
+        if (fuse)
+            hipLaunchKernelGGL((dev::mf_bwd_big_small_kernel<S>), dim3(f->bcnt[h] + f->nsmall[h]), dim3(256),
+                               std::max(f->lds_bbig[h], f->lds_bwd[h]), st, f->fronts, f->tabb + 2 * f->boff[h],
+                               f->bcnt[h], L + f->nwave[h], F, (const S*)f->tinv, f->sidx, (const S*)w, x, f->flags, eb,
+                               f->err, f->backoff);
+        else if (f->nbig[h] && !pair)
             hipLaunchKernelGGL((dev::mf_big_bwd_kernel<S>), dim3(f->bcnt[h]), dim3(256), f->lds_bbig[h], st, f->fronts,
                                f->tabb + 2 * f->boff[h], F, (const S*)f->tinv, f->sidx, (const S*)w, x, f->flags, eb,
                                f->err, f->backoff);
         const int64_t nw = f->nwave[h];
-        if (f->nsmall[h])
+        if (f->nsmall[h] && !fuse)
             hipLaunchKernelGGL((dev::mf_bwd_kernel<S>), dim3(f->nsmall[h]), dim3(256), f->lds_bwd[h], st, f->fronts,
                                L + nw, F, f->sidx, w, x);
         if (nw)

@@ -336,6 +336,34 @@ def test_row_block_pairs_bitwise(ctx, env, nx, big, real):
     A.close()
 
 
+@pytest.mark.parametrize("nx,big,real", [(45, "1", False), (300, None, False), (120, "64", True)])
+def test_fused_height_launches_bitwise(ctx, env, nx, big, real):
+    """A height's small fronts and its large fronts' assembly in one forward launch, and its large-front
+    row blocks and small fronts in one backward launch (mf_fwd_asm_kernel / mf_bwd_big_small_kernel,
+    the default) against separate launches (EIGSOL_MF_FUSE_ASM=0): the same operations, bitwise the
+    same solution, and a backward-stable solve (solve_shifted.hpp:96-115)."""
+    _mf_env(env)
+    env("EIGSOL_MF_LEAF", "24" if nx == 45 else "64")
+    if big is not None:
+        env("EIGSOL_MF_BIG_NS", big)
+    rp, ci, v = S.convdiff_complex(nx, seed=13)
+    if real:
+        v = np.ascontiguousarray(v.real)
+    n = nx * nx
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 8.5 if real else 3.0 - 0.2j
+    b = S.start_vector(n, np.complex128 if not real else np.float64, seed=5)
+    ys = {}
+    for fuse in ("0", "1"):
+        env("EIGSOL_MF_FUSE_ASM", fuse)
+        assert _variant(A, sigma) == 19
+        ys[fuse] = E.solve_shifted(A, sigma, b)
+    assert np.linalg.norm(M @ ys["1"] - sigma * ys["1"] - b) <= 1e-10 * np.linalg.norm(b) * max(1.0, np.linalg.norm(ys["1"]))
+    assert np.array_equal(ys["0"], ys["1"])
+    A.close()
+
+
 def test_single_precision_complex_default_is_multifrontal(ctx):
     """complex<float> past n = 16384 takes the GMRES family on values widened to double (the factor,
     residual check and refinement in double, the iterate in complex<float>): on the SuperLU fixture's
