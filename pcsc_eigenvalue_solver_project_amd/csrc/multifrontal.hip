@@ -265,9 +265,10 @@ __global__ __launch_bounds__(256) void mf_gemm_kernel(const MfFront* fr, const i
 // ---------------------------------------------------------------- solve
 // w = b in the new numbering
 template <class S>
-__global__ __launch_bounds__(256) void mf_gather_kernel(const int32_t* perm, const S* b, S* w, int64_t n) {
+__global__ __launch_bounds__(256) void mf_gather_kernel(const int32_t* perm, const S* b, S* w, int64_t n,
+                                                        const uint8_t* bigm) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) w[i] = b[perm[i]];
+    if (i < n) w[i] = (bigm && bigm[i]) ? mf_sent(s_zero<S>()) : b[perm[i]];   // bigm: large fronts' pivot rows
 }
 template <class S>
 __global__ __launch_bounds__(256) void mf_scatter_out_kernel(const int32_t* perm, const S* x, S* out, int64_t n) {
@@ -911,6 +912,35 @@ __global__ __launch_bounds__(256) void mf_big_asm_kernel(const MfFront* fr, cons
     mf_big_asm_front<S>(fr[list[blockIdx.x]], lds_raw, fr, chl, cmap, pinv, w, u, z, bo);
 }
 
+// mf_big_asm_front for mf_fwd_height_kernel: the pivot right-hand side read from b through perm (the
+// gather left these rows of w unsolved), the struct rows summed in LDS too, and every z entry stored
+// once with its value as its flag.  The same sums in the same order.  LDS: r (d)
+template <class S>
+__device__ __forceinline__ void mf_big_asm_front2(const MfFront& f, unsigned char* lds_raw, const MfFront* fr,
+                                                  const int32_t* chl, const int32_t* cmap, const int32_t* pinv,
+                                                  const int32_t* perm, const S* bin, const S* u, S* z) {
+    const int tid = threadIdx.x, ns = f.ns, ms = f.ms;
+    S* r = reinterpret_cast<S*>(lds_raw);
+    for (int t = tid; t < ns; t += 256) r[t] = bin[perm[f.c0 + t]];
+    for (int t = tid; t < ms; t += 256) r[ns + t] = s_zero<S>();
+    __syncthreads();
+    for (int k = f.ch0; k < f.ch1; ++k) {
+        const MfFront c = fr[chl[k]];
+        const int32_t* map = cmap + c.sof;
+        const S* uc = u + c.uoff;
+        for (int t = tid; t < c.ms; t += 256) {
+            const int pos = map[t];
+            const S v = uc[t];
+            if (pos < ns) r[pos] = sub(r[pos], v);
+            else r[pos] = add(r[pos], v);   // each position once per child: no race
+        }
+        __syncthreads();
+    }
+    S* zs = z + f.zoff;
+    for (int t = tid; t < ns; t += 256) mf_st(zs + t, mf_clean(r[pinv[f.c0 + t]]));
+    for (int t = tid; t < ms; t += 256) mf_st(zs + ns + t, mf_clean(r[ns + t]));
+}
+
 // one launch for a height's small fronts (workgroups [0, nsmall): mf_fwd_kernel) and its large fronts'
 // assembly (the rest: mf_big_asm_kernel); list = the small fronts, then the large ones.  They touch
 // disjoint rows of w and read only lower heights' contributions, so they need no order between them.
@@ -1053,13 +1083,13 @@ __device__ __forceinline__ void mf_acc16(S& acc, const S (&tv)[16], const S* yv,
 // contribution u = children's part + L21 y).  Every wave takes 16 columns of each column block:
 // its tile values are loaded before the block's flag is awaited.
 template <class S>
-__global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, const int32_t* tab, const S* F,
-                                                         const S* Tinv, const S* z, S* w, S* u, int32_t* flag,
-                                                         int32_t epoch, int32_t* err, int bo, S* x) {
+__device__ __forceinline__ void mf_big_fwd_block(const int bid, const MfFront* fr, const int32_t* tab, const S* F,
+                                                 const S* Tinv, S* z, S* w, S* u, int32_t* flag, int32_t epoch,
+                                                 int32_t* err, int bo, S* x, const bool zpoll) {
     __shared__ S part[4][64];
     __shared__ S ysh[4][16];
     __shared__ S vsh[64];
-    const int s = tab[2 * blockIdx.x], rb = tab[2 * blockIdx.x + 1];
+    const int s = tab[2 * bid], rb = tab[2 * bid + 1];
     const MfFront f = fr[s];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int d = f.d, ns = f.ns;
@@ -1078,7 +1108,9 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
     S acc = s_zero<S>();
     // the assembled right-hand side of these rows, loaded before the chain of waits (it was a
     // dependent round trip after the last one, on every hand-off's critical path)
-    const S zr = lane < rn ? z[f.zoff + r0 + lane] : s_zero<S>();
+    // zpoll (mf_fwd_height_kernel): z is assembled in this launch and value-flagged; wave 0 polls it after
+    // the chain and hands the slot back to the sentinel (this workgroup is its only reader)
+    S zr = (!zpoll && lane < rn) ? z[f.zoff + r0 + lane] : s_zero<S>();
     const int cend = piv ? rb : nblk;
     for (int c = 0; c < cend; ++c) {
         const int c0 = 64 * c + 16 * wv;
@@ -1100,6 +1132,10 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
         mf_acc16(acc, tv, ysh[wv], c0, ns);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+    }
+    if (zpoll && wv == 0 && lane < rn) {
+        zr = mf_poll(z + f.zoff + r0 + lane, err, bo);
+        mf_st(z + f.zoff + r0 + lane, mf_sent(s_zero<S>()));
     }
     part[wv][lane] = acc;
     __syncthreads();
@@ -1128,6 +1164,31 @@ __global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, cons
     if (lane < rn) mf_st(w + f.c0 + r0 + lane, y);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(flag + f.flag0 + rb, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class S>
+__global__ __launch_bounds__(256) void mf_big_fwd_kernel(const MfFront* fr, const int32_t* tab, const S* F,
+                                                         const S* Tinv, S* z, S* w, S* u, int32_t* flag,
+                                                         int32_t epoch, int32_t* err, int bo, S* x) {
+    mf_big_fwd_block<S>((int)blockIdx.x, fr, tab, F, Tinv, z, w, u, flag, epoch, err, bo, x, false);
+}
+
+// One forward launch per height with large fronts (value flags): workgroups [0, nsmall) the small fronts,
+// [nsmall, nsmall + nbig) the large fronts' assembly (mf_big_asm_front2: z written once per entry,
+// value-flagged), the rest the large fronts' row blocks (mf_big_fwd_block, polling z after their chain).
+// Every workgroup waits only on lower-indexed ones; the large fronts' pivot rows of w were set to the
+// sentinel by mf_gather_kernel.
+template <class S>
+__global__ __launch_bounds__(256) void mf_fwd_height_kernel(const MfFront* fr, const int32_t* list, int32_t nsmall,
+                                                            int32_t nbig, const int32_t* tab, const int32_t* chl,
+                                                            const S* F, const S* Tinv, const int32_t* cmap,
+                                                            const int32_t* pinv, const int32_t* perm, const S* bin,
+                                                            S* w, S* u, S* z, int32_t* err, int bo, S* x) {
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const int32_t b = (int32_t)blockIdx.x;
+    if (b < nsmall) mf_fwd_front<S>(fr[list[b]], lds_raw, fr, chl, F, cmap, pinv, w, u);
+    else if (b < nsmall + nbig) mf_big_asm_front2<S>(fr[list[b]], lds_raw, fr, chl, cmap, pinv, perm, bin, u, z);
+    else mf_big_fwd_block<S>((int)(b - nsmall - nbig), fr, tab, F, Tinv, z, w, u, nullptr, 0, err, bo, x, true);
 }
 
 // backward, large fronts: tab = (front, pivot block) pairs, blocks descending within a front:
@@ -1534,8 +1595,11 @@ struct MfFactor {
     int32_t nsub = 0, lds_sub_f = 0, lds_sub_b = 0;                // bit 0 forward, bit 1 backward (EIGSOL_MF_FLOW_MODE, debugging)
     int backoff = 2;                  // EIGSOL_MF_BACKOFF: 1 growing sleeps, 2 relaxed polls (flag stores: release)
     bool fuse_asm = true;             // EIGSOL_MF_FUSE_ASM=0: small fronts and large-front assembly as two launches
+    bool fuse_big = true;             // EIGSOL_MF_FUSE_BIG=0: no mf_fwd_height_kernel
+    uint8_t* bigm = nullptr;          // [n] 1 on the large fronts' pivot rows (mf_fwd_height_kernel's gather)
     std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt, foff2, fcnt2, boff2, bcnt2;
     std::vector<int32_t> lds_asm;
+    std::vector<int32_t> lds_asm2;    // mf_fwd_height_kernel's assembly: d entries per large front
     MfStats st;
     // solves replayed as a hipGraph per (b, out) pair seen twice (value flags, no flow kernels:
     // the launches' arguments are then the same for every solve of that pair)
@@ -1556,7 +1620,7 @@ void mf_free(MfFactor* f) {
     for (void* p : {(void*)f->fronts, (void*)f->chl, (void*)f->sidx, (void*)f->cmap, (void*)f->perm, (void*)f->pinv,
                     (void*)f->lists, f->F, f->u, f->w, f->x, (void*)f->slists, (void*)f->tabf, (void*)f->tabb,
                     (void*)f->tabf2, (void*)f->tabb2, (void*)f->flags, (void*)f->err, f->z, f->tinv, (void*)f->flow_f, (void*)f->flow_b,
-                    (void*)f->fheight, (void*)f->done, (void*)f->sub_ranges})
+                    (void*)f->fheight, (void*)f->done, (void*)f->sub_ranges, (void*)f->bigm})
         if (p) hipFree(p);
     for (auto& g : f->graphs)
         if (g.exec) hipGraphExecDestroy(g.exec);
@@ -2199,7 +2263,7 @@ struct MfHost {
     int64_t sb = 16;
     std::vector<int64_t> dst;              // M's entries -> front offsets
     std::vector<MfLaunch> plan;            // factorization launches
-    std::vector<int32_t> tab, slists, tabf, tabb, tabf2, tabb2, lds_asm;
+    std::vector<int32_t> tab, slists, tabf, tabb, tabf2, tabb2, lds_asm, lds_asm2;
     std::vector<int64_t> sstart, nwave, nsmall, nbig, foff, fcnt, boff, bcnt, foff2, fcnt2, boff2, bcnt2;
     int32_t nflag = 0;
     int64_t zsz = 0;
@@ -2322,6 +2386,7 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
     if (const char* e = std::getenv("EIGSOL_MF_BIG_NS")) big_ns = std::atoi(e);
     if (const char* e = std::getenv("EIGSOL_MF_BIG_D")) big_d = std::atoi(e);
     auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &tabf2 = X.tabf2, &tabb2 = X.tabb2, &lds_asm = X.lds_asm;
+    auto& lds_asm2 = X.lds_asm2;
     auto &sstart = X.sstart, &nwave = X.nwave, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff, &fcnt = X.fcnt,
          &boff = X.boff, &bcnt = X.bcnt, &foff2 = X.foff2, &fcnt2 = X.fcnt2, &boff2 = X.boff2, &bcnt2 = X.bcnt2;
     sstart.assign(H + 2, 0);
@@ -2369,6 +2434,7 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
             }
     }
     lds_asm.assign(H + 1, 0);
+    lds_asm2.assign(H + 1, 0);
     bool inv_on = true;
     int inv_d = 256;   // 256 / 384 / 512: 1.71 / 1.72 / 1.72 ms per 1M iteration (tools/mf_grid.sh)
     if (const char* e = std::getenv("EIGSOL_MF_INVFORM")) inv_on = std::atoi(e) != 0;
@@ -2412,6 +2478,7 @@ int mf_prepare_host(int64_t n, const std::vector<int32_t>& rp, const std::vector
             for (int32_t k = 0; k < npair + nsb; ++k) { tabf2.push_back(b); tabf2.push_back(k); }
             for (int32_t k = npair - 1; k >= 0; --k) { tabb2.push_back(b); tabb2.push_back(k); }
             lds_asm[h] = std::max<int32_t>(lds_asm[h], (int32_t)(q.ns * sb));
+            lds_asm2[h] = std::max<int32_t>(lds_asm2[h], (int32_t)((q.ns + q.ms) * sb));   // d: mf_big_asm_front2
         }
         fcnt[h] = (int64_t)tabf.size() / 2 - foff[h];
         bcnt[h] = (int64_t)tabb.size() / 2 - boff[h];
@@ -2491,6 +2558,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     const auto& tab = X.tab;
     const auto &slists = X.slists, &tabf = X.tabf, &tabb = X.tabb, &tabf2 = X.tabf2, &tabb2 = X.tabb2,
                &lds_asm = X.lds_asm;
+    auto& lds_asm2 = X.lds_asm2;
     const auto &sstart = X.sstart, &nwave = X.nwave, &nsmall = X.nsmall, &nbig = X.nbig, &foff = X.foff,
                &fcnt = X.fcnt, &boff = X.boff, &bcnt = X.bcnt;
     const int32_t nflag = X.nflag;
@@ -2518,9 +2586,15 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     f->boff2 = X.boff2;
     f->bcnt2 = X.bcnt2;
     f->lds_asm = lds_asm;
+    f->lds_asm2 = lds_asm2;
+    // the fused forward launch's assembly holds a whole front's right-hand side in LDS
+    for (int32_t b : lds_asm2)
+        if (b > 120 * 1024) f->fuse_big = false;
     if (const char* e = std::getenv("EIGSOL_MF_PAIR")) f->pair = std::atoi(e) != 0;
     if (const char* e = std::getenv("EIGSOL_MF_BACKOFF")) f->backoff = std::atoi(e) & 3;
     if (const char* e = std::getenv("EIGSOL_MF_FUSE_ASM")) f->fuse_asm = std::atoi(e) != 0;
+    if (const char* e = std::getenv("EIGSOL_MF_FUSE_BIG"))
+        if (std::atoi(e) == 0) f->fuse_big = false;
     // value flags (bit 4; EIGSOL_MF_VALFLAG=0: epoch flags): 1M convection-diffusion 1.657 -> 1.567 ms
     {
         const char* e = std::getenv("EIGSOL_MF_VALFLAG");
@@ -2566,6 +2640,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     dm((void**)&f->flags, (size_t)nflag * 4);
     dm((void**)&f->err, 4);
     dm(&f->z, (size_t)zsz * sb);
+    dm((void**)&f->bigm, (size_t)n);
     dm(&f->tinv, (size_t)nflag * 8192 * sb);
     f->hflow = X.hflow;
     f->nflow = (int32_t)X.flow_f.size();
@@ -2619,6 +2694,17 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         up(f->flow_b, X.flow_b.data(), X.flow_b.size() * 4);
         up(f->fheight, P.height.data(), nt * 4);
         up(f->sub_ranges, X.sub_ranges.data(), X.sub_ranges.size() * 4);
+        {
+            // the large fronts' pivot rows (mf_fwd_height_kernel's gather) and an all-unsolved z
+            std::vector<uint8_t> bm((size_t)n, 0);
+            for (int32_t h = 0; h <= H; ++h)
+                for (int64_t t = sstart[h] + nwave[h] + nsmall[h]; t < sstart[h] + nwave[h] + nsmall[h] + nbig[h]; ++t) {
+                    const dev::MfFront& q = fr[slists[t]];
+                    for (int32_t r = 0; r < q.ns; ++r) bm[(size_t)q.c0 + r] = 1;
+                }
+            up(f->bigm, bm.data(), (size_t)n);
+            hipMemsetD32Async(static_cast<hipDeviceptr_t>(f->z), 0x7FF4DEADu, std::max<size_t>((size_t)zsz * sb / 4, 1), st);
+        }
         hipMemsetAsync(f->done, 0, nt * 4, st);
         hipMemsetAsync(f->err, 0, 4, st);
         up(d_tab, tab.data(), tab.size() * 4);
@@ -2676,6 +2762,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         for (int32_t b : f->lds_fwd) mx = std::max(mx, b);
         for (int32_t b : f->lds_bwd) mx = std::max(mx, b);
         for (int32_t b : f->lds_asm) mx = std::max(mx, b);
+        if (f->fuse_big)
+            for (int32_t b : f->lds_asm2) mx = std::max(mx, b);
         mx = std::max(mx, std::max(f->lds_flow_f, f->lds_flow_b));
         mx = std::max(mx, std::max(f->lds_sub_f, f->lds_sub_b));
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_kernel<S>),
@@ -2685,6 +2773,8 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_big_asm_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_asm_kernel<S>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
+            hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_height_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
             hipFuncSetAttribute(reinterpret_cast<const void*>(dev::mf_fwd_flow_kernel<S>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess ||
@@ -2722,7 +2812,11 @@ static void mf_solve_enqueue(MfFactor* f, hipStream_t st, const S* b, S* out, in
     S* w = static_cast<S*>(f->w);
     S* x = static_cast<S*>(f->x);
     const S* F = static_cast<const S*>(f->F);
-    hipLaunchKernelGGL((dev::mf_gather_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, b, w, n);
+    // one forward launch per height with large fronts (mf_fwd_height_kernel; value flags, no pairs,
+    // EIGSOL_MF_FUSE_BIG=0 off): the gather leaves those fronts' pivot rows of w unsolved
+    const bool hfuse = f->bigm && f->fuse_big && (f->backoff & 4) && !f->pair;
+    hipLaunchKernelGGL((dev::mf_gather_kernel<S>), dim3((n + 255) / 256), dim3(256), 0, st, f->perm, b, w, n,
+                       hfuse ? f->bigm : (const uint8_t*)nullptr);
     const int32_t H = (int32_t)f->hstart.size() - 2;
     S* u = static_cast<S*>(f->u);
     S* z = static_cast<S*>(f->z);
@@ -2743,6 +2837,13 @@ static void mf_solve_enqueue(MfFactor* f, hipStream_t st, const S* b, S* out, in
         if (nw)
             hipLaunchKernelGGL((dev::mf_fwd_wave_kernel<S>), dim3((nw + 3) / 4), dim3(256), 0, st, f->fronts, L,
                                (int32_t)nw, f->chl, F, f->cmap, f->pinv, w, u);
+        if (hfuse && f->nbig[h]) {
+            hipLaunchKernelGGL((dev::mf_fwd_height_kernel<S>), dim3(f->nsmall[h] + f->nbig[h] + f->fcnt[h]), dim3(256),
+                               std::max(f->lds_fwd[h], f->lds_asm2[h]), st, f->fronts, L + nw, (int32_t)f->nsmall[h],
+                               (int32_t)f->nbig[h], f->tabf + 2 * f->foff[h], f->chl, F, (const S*)f->tinv, f->cmap,
+                               f->pinv, f->perm, b, w, u, z, f->err, f->backoff, x);
+            continue;
+        }
         // EIGSOL_MF_FUSE_ASM=0: the small fronts and the large fronts' assembly as two launches
         const bool fuse = f->fuse_asm && f->nsmall[h] && f->nbig[h];
         if (fuse)
@@ -2763,7 +2864,7 @@ static void mf_solve_enqueue(MfFactor* f, hipStream_t st, const S* b, S* out, in
                                    f->backoff, x);
             else
                 hipLaunchKernelGGL((dev::mf_big_fwd_kernel<S>), dim3(f->fcnt[h]), dim3(256), 0, st, f->fronts,
-                                   f->tabf + 2 * f->foff[h], F, (const S*)f->tinv, (const S*)z, w, u, f->flags, ef,
+                                   f->tabf + 2 * f->foff[h], F, (const S*)f->tinv, z, w, u, f->flags, ef,
                                    f->err, f->backoff, x);
         }
     }

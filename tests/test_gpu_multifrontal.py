@@ -339,9 +339,11 @@ def test_row_block_pairs_bitwise(ctx, env, nx, big, real):
 @pytest.mark.parametrize("nx,big,real", [(45, "1", False), (300, None, False), (120, "64", True)])
 def test_fused_height_launches_bitwise(ctx, env, nx, big, real):
     """A height's small fronts and its large fronts' assembly in one forward launch, and its large-front
-    row blocks and small fronts in one backward launch (mf_fwd_asm_kernel / mf_bwd_big_small_kernel,
-    the default) against separate launches (EIGSOL_MF_FUSE_ASM=0): the same operations, bitwise the
-    same solution, and a backward-stable solve (solve_shifted.hpp:96-115)."""
+    row blocks and small fronts in one backward launch (mf_fwd_asm_kernel / mf_bwd_big_small_kernel),
+    and a height's whole forward pass in one launch (mf_fwd_height_kernel: small fronts, assembly and
+    row blocks, the default) against separate launches (EIGSOL_MF_FUSE_ASM / _BIG = 0): the same
+    operations, bitwise the same solution and six-iteration shifted-inverse run, and a backward-stable
+    solve (solve_shifted.hpp:96-115, shifted_inverse_power_solver.hpp:49-76)."""
     _mf_env(env)
     env("EIGSOL_MF_LEAF", "24" if nx == 45 else "64")
     if big is not None:
@@ -355,12 +357,19 @@ def test_fused_height_launches_bitwise(ctx, env, nx, big, real):
     sigma = 8.5 if real else 3.0 - 0.2j
     b = S.start_vector(n, np.complex128 if not real else np.float64, seed=5)
     ys = {}
-    for fuse in ("0", "1"):
-        env("EIGSOL_MF_FUSE_ASM", fuse)
+    for fuse in ("00", "10", "11"):   # EIGSOL_MF_FUSE_ASM, EIGSOL_MF_FUSE_BIG (mf_fwd_height_kernel)
+        env("EIGSOL_MF_FUSE_ASM", fuse[0])
+        env("EIGSOL_MF_FUSE_BIG", fuse[1])
         assert _variant(A, sigma) == 19
         ys[fuse] = E.solve_shifted(A, sigma, b)
-    assert np.linalg.norm(M @ ys["1"] - sigma * ys["1"] - b) <= 1e-10 * np.linalg.norm(b) * max(1.0, np.linalg.norm(ys["1"]))
-    assert np.array_equal(ys["0"], ys["1"])
+    y = ys["11"]
+    assert np.linalg.norm(M @ y - sigma * y - b) <= 1e-10 * np.linalg.norm(b) * max(1.0, np.linalg.norm(y))
+    assert np.array_equal(ys["00"], ys["10"]) and np.array_equal(ys["00"], y)
+    # repeated solves on one factor (the value-flagged z is handed back to the sentinel each solve)
+    r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(6, -1.0, sigma), b)
+    env("EIGSOL_MF_FUSE_BIG", "0")
+    r0 = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(6, -1.0, sigma), b)
+    assert np.array_equal(r.eigenvector, r0.eigenvector) and r.eigenvalue == r0.eigenvalue
     A.close()
 
 
