@@ -1069,6 +1069,89 @@ __global__ __launch_bounds__(256) void mf_invform_kernel(const MfFront* fr, cons
         Gb[i + (int64_t)c * ns] = v;
     }
 }
+template <class S>
+__global__ __launch_bounds__(256) void mf_invform2_kernel(const MfFront* fr, const int32_t* list, S* F) {
+    // mf_invform_kernel's forms with the same operations in the same order, restructured for latency:
+    // inv(L11) (wave 0) and inv(U11) (wave 1) concurrently into one LDS array X (strictly below the
+    // diagonal inv(L11), whose unit diagonal is implicit; on and above it inv(U11)), and L21 / U12 read
+    // from HBM once, 64-row / 64-column tiles staged in T (free after the inversions), instead of one
+    // HBM load per multiply-add.
+    __shared__ S T[64 * 65];
+    __shared__ S X[64 * 65];
+    const MfFront f = fr[list[blockIdx.x]];
+    const int tid = threadIdx.x, d = f.d, ns = f.ns, wv = tid >> 6, lane = tid & 63;
+    const S* A = F + f.off;
+    S* Gf = F + f.goff;
+    S* Gb = Gf + (int64_t)d * ns;
+    S one;
+    set_re_im(one, 1.0, 0.0);
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int i = e & 63, j = e >> 6;
+        T[i + j * 65] = (i < ns && j < ns) ? A[i + (int64_t)j * d] : (i == j ? one : s_zero<S>());
+    }
+    __syncthreads();
+    // XL(k, j) / XU(i, k) as the old kernel's X held them
+    auto xl = [&](int k, int j) { return k == j ? one : (k < j ? s_zero<S>() : X[k + j * 65]); };
+    if (wv == 0) {   // inv(L11), column t (unit lower)
+        const int t = lane;
+        for (int i = t + 1; i < 64; ++i) {
+            S v = s_zero<S>();
+            for (int j = t; j < i; ++j) v = sub(v, mul(T[i + j * 65], xl(j, t)));
+            X[i + t * 65] = v;
+        }
+    } else if (wv == 1) {   // inv(U11), column t
+        const int t = lane;
+        for (int i = t; i >= 0; --i) {
+            S v = i == t ? one : s_zero<S>();
+            for (int j = i + 1; j <= t; ++j) v = sub(v, mul(T[i + j * 65], X[j + t * 65]));
+            X[i + t * 65] = sdiv(v, T[i + i * 65]);
+        }
+    }
+    __syncthreads();
+    // rows < ns of the forward form: inv(L11)
+    for (int e = tid; e < ns * ns; e += 256) {
+        const int i = e % ns, j = e / ns;
+        Gf[i + (int64_t)j * d] = xl(i, j);
+    }
+    // columns < ns of the backward form: inv(U11)
+    for (int e = tid; e < ns * ns; e += 256) {
+        const int i = e % ns, c = e / ns;
+        Gb[i + (int64_t)c * ns] = i <= c ? X[i + c * 65] : s_zero<S>();
+    }
+    // W = L21 inv(L11), 64 rows of L21 at a time through T
+    for (int i0 = ns; i0 < d; i0 += 64) {
+        const int rn = min(64, d - i0);
+        __syncthreads();
+        for (int e = tid; e < 64 * ns; e += 256) {
+            const int i = e & 63, k = e >> 6;
+            if (i < rn) T[i + k * 65] = A[(i0 + i) + (int64_t)k * d];
+        }
+        __syncthreads();
+        for (int e = tid; e < rn * ns; e += 256) {
+            const int i = e % rn, j = e / rn;
+            S v = s_zero<S>();
+            for (int k = j; k < ns; ++k) v = add(v, mul(T[i + k * 65], xl(k, j)));
+            Gf[(i0 + i) + (int64_t)j * d] = v;
+        }
+    }
+    // -inv(U11) U12, 64 columns of U12 at a time through T
+    for (int c0 = ns; c0 < d; c0 += 64) {
+        const int cn = min(64, d - c0);
+        __syncthreads();
+        for (int e = tid; e < ns * 64; e += 256) {
+            const int k = e % ns, c = e / ns;
+            if (c < cn) T[k + c * 65] = A[k + (int64_t)(c0 + c) * d];
+        }
+        __syncthreads();
+        for (int e = tid; e < ns * cn; e += 256) {
+            const int i = e % ns, c = e / ns;
+            S v = s_zero<S>();
+            for (int k = i; k < ns; ++k) v = sub(v, mul(X[i + k * 65], T[k + c * 65]));
+            Gb[i + (int64_t)(c0 + c) * ns] = v;
+        }
+    }
+}
+
 
 // acc += tile(row, c0 .. c0 + 16) * yv over the columns below lim (tile values already loaded)
 template <class S>
@@ -2731,7 +2814,14 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
             hipLaunchKernelGGL((dev::mf_inv_kernel<S>), dim3(tabb.size() / 2), dim3(256), 0, st, f->fronts, f->tabb, F,
                                static_cast<S*>(f->tinv));
         if (d_inv)
-            hipLaunchKernelGGL((dev::mf_invform_kernel<S>), dim3(X.inv_list.size()), dim3(256), 0, st, f->fronts, d_inv, F);
+        {
+            // EIGSOL_MF_INVFORM=1: round 5's kernel (one HBM load per multiply-add of L21 inv(L11) and inv(U11) U12)
+            const char* ie = std::getenv("EIGSOL_MF_INVFORM");
+            if (ie && std::atoi(ie) == 1)
+                hipLaunchKernelGGL((dev::mf_invform_kernel<S>), dim3(X.inv_list.size()), dim3(256), 0, st, f->fronts, d_inv, F);
+            else
+                hipLaunchKernelGGL((dev::mf_invform2_kernel<S>), dim3(X.inv_list.size()), dim3(256), 0, st, f->fronts, d_inv, F);
+        }
         hipMemcpyAsync(hpiv.data(), d_piv, n * 4, hipMemcpyDeviceToHost, st);
         hipMemcpyAsync(hz2, d_z, 8, hipMemcpyDeviceToHost, st);
         if (hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess)

@@ -373,6 +373,30 @@ def test_fused_height_launches_bitwise(ctx, env, nx, big, real):
     A.close()
 
 
+@pytest.mark.parametrize("nx,real", [(120, False), (120, True), (300, False)])
+def test_inverse_forms_bitwise(ctx, env, nx, real):
+    """The small fronts' inverse forms built by mf_invform2_kernel (both inversions at once, L21 / U12
+    staged through LDS, the default) against round 5's mf_invform_kernel (EIGSOL_MF_INVFORM=1): the
+    same operations in the same order, so bitwise the same solution (solve_shifted.hpp:96-115)."""
+    _mf_env(env)
+    rp, ci, v = S.convdiff_complex(nx, seed=17)
+    if real:
+        v = np.ascontiguousarray(v.real)
+    n = nx * nx
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 8.5 if real else 3.0 - 0.2j
+    b = S.start_vector(n, np.complex128 if not real else np.float64, seed=7)
+    ys = {}
+    for k in ("1", "2"):
+        env("EIGSOL_MF_INVFORM", k)
+        assert _variant(A, sigma) == 19
+        ys[k] = E.solve_shifted(A, sigma, b)
+    assert np.linalg.norm(M @ ys["2"] - sigma * ys["2"] - b) <= 1e-10 * np.linalg.norm(b) * max(1.0, np.linalg.norm(ys["2"]))
+    assert np.array_equal(ys["1"], ys["2"])
+    A.close()
+
+
 def test_single_precision_complex_default_is_multifrontal(ctx):
     """complex<float> past n = 16384 takes the GMRES family on values widened to double (the factor,
     residual check and refinement in double, the iterate in complex<float>): on the SuperLU fixture's
