@@ -88,6 +88,9 @@ __device__ __forceinline__ cplx mf_ld(const cplx* p) { return cplx{ld_agent(&p->
 // value flags of the row-block solve (EIGSOL_MF_VALFLAG): an unsolved pivot value holds this NaN in
 // every 8-byte word, a solved one never does (a NaN result is stored as the default quiet NaN), so a
 // waiting block polls the values themselves instead of a flag and then the values
+#ifndef EIGSOL_MF_UNROLL
+#define EIGSOL_MF_UNROLL 8   // loads in flight per thread in the small fronts' inverse-form products
+#endif
 constexpr unsigned long long kMfSent = 0x7FF4DEAD7FF4DEADull;
 __device__ __forceinline__ bool mf_unready(double v) { return (unsigned long long)__double_as_longlong(v) == kMfSent; }
 __device__ __forceinline__ bool mf_unready(cplx v) { return mf_unready(v.re) || mf_unready(v.im); }
@@ -350,7 +353,7 @@ __device__ __forceinline__ void mf_fwd_front(const MfFront f, unsigned char* lds
                 S v = s_zero<S>();
                 const S* Gi = G + i;
                 const int jn = i < ns ? i + 1 : ns;   // inv(L11) is lower triangular: skip its zeros
-#pragma unroll 8
+#pragma unroll EIGSOL_MF_UNROLL
                 for (int j = 0; j < jn; ++j) v = add(v, mul(Gi[(int64_t)j * d], y[j]));
                 if (i < ns) w[f.c0 + i] = v;
                 else u[f.uoff + i - ns] = add(acc[i - ns], v);
@@ -364,7 +367,7 @@ __device__ __forceinline__ void mf_fwd_front(const MfFront f, unsigned char* lds
         if (i < d) {
             const S* Gi = G + i;
             const int jn = i < ns ? i + 1 : ns;   // inv(L11) is lower triangular: skip its zeros
-#pragma unroll 8
+#pragma unroll EIGSOL_MF_UNROLL
             for (int j = p; j < jn; j += tpr) sacc = add(sacc, mul(Gi[(int64_t)j * d], y[j]));
         }
         part[p * R + i] = sacc;
@@ -465,7 +468,7 @@ __device__ __forceinline__ void mf_bwd_front(const MfFront f, unsigned char* lds
             const S* Gk = G + k;
             // inv(U11) is upper triangular: columns from k on (the first of them congruent to p mod 4)
             const int c0 = k > p ? p + ((k - p + 3) / 4) * 4 : p;
-#pragma unroll 8
+#pragma unroll EIGSOL_MF_UNROLL
             for (int c = c0; c < d; c += 4) sacc = add(sacc, mul(Gk[(int64_t)c * ns], c < ns ? t[c] : xs[c - ns]));
         }
         part[p * 64 + k] = sacc;
