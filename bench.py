@@ -374,7 +374,7 @@ def run_config2(E, ctx, no_cpu):
                        "rank_update_utilisation": round(d.get("rank_update_mfma_utilisation") or 0.0, 4),
                        "francis_window_gemm_share": round(d.get("francis_window_gemm_share") or 0.0, 4),
                        "source": "profiles/r06_qr4096_mfma.json from profiles/r06_qr4096_kernel_stats.csv "
-                                 "(rocprofv3 kernel times of the shipped path: hess_panel_coop<double, 1> issued by "
+                                 "(rocprofv3 kernel times of the shipped path: hess_panel_coop2<double> issued by "
                                  "an ordinary launch of the same kernel, gemm_mfma_f64 / gemm_reduce / "
                                  "rankk_mfma<double, false> on v_mfma_f64_16x16x4_f64 - the whole trailing-update "
                                  "set incl. the split-K W = V^T A, and the single rank-2nb update alone; "
