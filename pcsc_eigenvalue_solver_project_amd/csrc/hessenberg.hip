@@ -1044,6 +1044,188 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop2(CoopArgs<S> a) 
     }
 }
 
+// ------------------------------------------------------------------ cooperative QR panel
+// qr_blocked's panel (32 Householder columns of R, qr_decompose.hpp:46-85, with the compact-WY T of the
+// panel) in ONE cooperative launch of G blocks, block b owning rows [b R, (b+1) R) (R <= 64: one row per
+// lane of wave 0), instead of one single-workgroup launch per column that streams V three times through
+// one CU.  Per column, two grid barriers:
+//   P1  the column's own rows (kept in LDS) and the partials of V^H a over rows >= k
+//   P2  p = sum of the partials, T's previous column from the previous column's t partials, w = T^H p,
+//       a -= V w (own rows), partial of ||a(j+1:)||^2, x0 = a(j)
+//   P3  the reflector (every block, from the same sums), V(:, i) and R(:, j) for own rows, partials of
+//       t = V^H v (gathered after the next column's first barrier; the last column's after one more)
+// The block's own rows of V are cached in LDS; partial sums are combined in block order (deterministic).
+template <class S>
+struct QrCoopArgs {
+    S* R;
+    int m, k, nbp;
+    S* V;
+    S* T;
+    S* part;        // [2][G][32]: P1 partials, then the t partials
+    double* tpart;  // [G]
+    S* x0;
+    unsigned* bar;
+    int* err;
+    bool hier;
+};
+
+template <class S>
+__global__ __launch_bounds__(kCoopThreads) void qr_panel_coop(QrCoopArgs<S> a) {
+    constexpr int NB = 32;
+    constexpr int kSl = kCoopThreads / NB;
+    constexpr int kGU = 256 / kSl;
+    __shared__ S xs[64];
+    __shared__ S vc[NB][64];
+    __shared__ S red[kCoopThreads];
+    __shared__ double tps[256];
+    __shared__ S sp[NB], stt[NB], sw2[NB];
+    __shared__ S Tl[NB * NB];
+    __shared__ S s_scal[3];
+    __shared__ double s_rv;
+    __shared__ int s_sk, s_skprev;
+    auto gather = [&](const S* src, int cnt, S* dst) {
+        const int nb = (int)gridDim.x;
+        {
+            const int c = threadIdx.x % NB, sl = threadIdx.x / NB;
+            S acc = s_zero<S>();
+            if (c < cnt) {
+                S t[kGU];
+#pragma unroll
+                for (int u = 0; u < kGU; ++u) {
+                    const int b = sl + u * kSl;
+                    t[u] = b < nb ? ld_ag(&src[b * NB + c]) : s_zero<S>();
+                }
+#pragma unroll
+                for (int u = 0; u < kGU; ++u) acc = add(acc, t[u]);
+            }
+            red[threadIdx.x] = acc;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < cnt) {
+            S acc = s_zero<S>();
+            for (int sl = 0; sl < kSl; ++sl) acc = add(acc, red[sl * NB + threadIdx.x]);
+            dst[threadIdx.x] = acc;
+        }
+        __syncthreads();
+    };
+    // T column c from the gathered t = V(:, 0:c)^H v_c (stt), as qr_panel_col forms it
+    auto t_column = [&](int c, bool skc) {
+        if ((int)threadIdx.x <= c) {
+            S tc;
+            set_re_im(tc, 2.0, 0.0);
+            if ((int)threadIdx.x < c) {
+                S s2 = s_zero<S>();
+                if (!skc)
+                    for (int q = threadIdx.x; q < c; ++q) s2 = add(s2, mul(Tl[threadIdx.x + q * NB], stt[q]));
+                tc = neg2(s2);
+            }
+            Tl[threadIdx.x + c * NB] = tc;
+        }
+        __syncthreads();
+    };
+    const int m = a.m, k = a.k;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int G = gridDim.x;
+    const int R = (m + G - 1) / G;
+    const int grp = (G % 8 == 0) ? ((int)blockIdx.x % 8) * (G / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
+    const int r0 = grp * R, r1 = min(m, r0 + R);
+    const int rown = r0 + lane;
+    const bool own = rown < r1;
+    unsigned target = 0;
+    for (int e = tid; e < NB * NB; e += kCoopThreads) Tl[e] = s_zero<S>();
+    if (tid == 0) s_skprev = 0;
+    for (int i = 0; i < a.nbp; ++i) {
+        const int j = k + i;
+        // ---------------- P1
+        if (wv == 0 && own) xs[lane] = a.R[rown + (int64_t)j * m];
+        __syncthreads();
+        for (int c = wv; c < i; c += 16) {
+            S p = s_zero<S>();
+            if (own && rown >= k) p = add(p, mul(cj(vc[c][lane]), xs[lane]));
+            p = wsum(p);
+            if (lane == 0) st_ag(&a.part[grp * NB + c], p);
+        }
+        grid_barrier(a.bar, target, a.err, a.hier);
+        // ---------------- P2
+        if (i > 0) {
+            gather(a.part, i, sp);
+            gather(a.part + (size_t)G * NB, i - 1, stt);
+            t_column(i - 1, s_skprev != 0);
+            if (tid < i) {
+                S sacc = s_zero<S>();
+                for (int c = 0; c <= tid; ++c) sacc = add(sacc, mul(cj(Tl[c + tid * NB]), sp[c]));
+                sw2[tid] = sacc;
+            }
+            __syncthreads();
+        }
+        if (wv == 0) {
+            double tl = 0.0;
+            if (own) {
+                S x = xs[lane];
+                if (rown >= k)
+                    for (int c = 0; c < i; ++c) x = sub(x, mul(vc[c][lane], sw2[c]));
+                xs[lane] = x;
+                if (rown >= j + 1) tl += sq_abs(x);
+                if (rown == j) st_ag(a.x0, x);
+            }
+            tl = wave_sum(tl);
+            if (lane == 0) st_agent(&a.tpart[grp], tl);
+        }
+        grid_barrier(a.bar, target, a.err, a.hier);
+        // ---------------- P3
+        {
+            const double tpv = tid < G ? ld_agent(&a.tpart[tid]) : 0.0;
+            const S x0 = ld_ag(a.x0);
+            if (tid < G) tps[tid] = tpv;
+            __syncthreads();
+            if (tid == 0) {
+                double tail = 0.0;
+                for (int b = 0; b < G; ++b) tail += tps[b];
+                bool skr;
+                S v0, alpha;
+                double rv;
+                hess_reflector(x0, tail, skr, v0, rv, alpha);
+                s_sk = skr ? 1 : 0;
+                s_scal[1] = v0;
+                s_rv = rv;
+                s_scal[2] = alpha;
+            }
+            __syncthreads();
+        }
+        const bool sk = s_sk != 0;
+        const S v0 = s_scal[1], alpha = s_scal[2];
+        const double rv = s_rv;
+        if (wv == 0 && own) {
+            const S x = xs[lane];
+            S v = s_zero<S>();
+            if (!sk && rown >= j) v = scal(rown == j ? v0 : x, rv);
+            st_ag(&a.V[rown + (int64_t)i * m], v);
+            vc[i][lane] = v;
+            S xr = x;
+            if (!sk && rown == j) xr = alpha;
+            if (!sk && rown > j) xr = s_zero<S>();
+            a.R[rown + (int64_t)j * m] = xr;
+        }
+        __syncthreads();
+        for (int c = wv; c < i; c += 16) {
+            S p = s_zero<S>();
+            if (!sk && own && rown >= j) p = add(p, mul(cj(vc[c][lane]), vc[i][lane]));
+            p = wsum(p);
+            if (lane == 0) st_ag(&a.part[(G + grp) * NB + c], p);
+        }
+        if (tid == 0) s_skprev = s_sk;
+    }
+    // the last column's T column, then block 0 publishes T
+    grid_barrier(a.bar, target, a.err, a.hier);
+    const int il = a.nbp - 1;
+    if (il >= 0) {
+        gather(a.part + (size_t)G * NB, il, stt);
+        t_column(il, s_skprev != 0);
+    }
+    if (blockIdx.x == 0)
+        for (int e = tid; e < NB * NB; e += kCoopThreads) a.T[e] = Tl[e];
+}
+
 // C (m x nn, ldc) += alpha * op(A) op(B); op = transpose when TA / TB.  64x64 tiles, 4x4/thread.
 // Split-K: blockIdx.z takes rows [z kc, (z+1) kc) of the K range and, when gridDim.z > 1, writes its
 // partial product to C + z * zstride (beta must be 0 then; gemm_reduce adds the partials in z order).
@@ -1514,10 +1696,44 @@ int qr_blocked(hipStream_t st, S* R, int m, int n, S* Q) {
     EIGSOL_HIP(hipMalloc(&SK, sk_elems * sizeof(S)));
     EIGSOL_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dev::qr_panel_col<S>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(m * sizeof(S))));
+    // the panel as one cooperative launch (qr_panel_coop) from m >= 256 when the device supports it
+    // (EIGSOL_QR_COOP=0: one qr_panel_col launch per column); its grid: about 32 rows per block, 16 .. 256
+    // blocks, like the Hessenberg panel's
+    int coop_ok = 0, dev_id = 0;
+    EIGSOL_HIP(hipGetDevice(&dev_id));
+    EIGSOL_HIP(hipDeviceGetAttribute(&coop_ok, hipDeviceAttributeCooperativeLaunch, dev_id));
+    const char* qce = std::getenv("EIGSOL_QR_COOP");
+    const int G = std::min(256, std::max(16, (m / 32 + 7) / 8 * 8));
+    const bool coop = coop_ok && m >= 256 && m <= 64 * G && !(qce && std::atoi(qce) == 0);
+    S *part = nullptr, *x0s = nullptr;
+    double* tpart = nullptr;
+    unsigned* bar = nullptr;
+    int* err = nullptr;
+    constexpr size_t kBarBytes = 9 * 64;
+    if (coop) {
+        EIGSOL_HIP(hipMalloc(&part, 2 * (size_t)G * NB * sizeof(S)));
+        EIGSOL_HIP(hipMalloc(&tpart, G * sizeof(double)));
+        EIGSOL_HIP(hipMalloc(&x0s, 64));
+        EIGSOL_HIP(hipMalloc(&bar, kBarBytes));
+        EIGSOL_HIP(hipMalloc(&err, 64));
+        EIGSOL_HIP(hipMemsetAsync(err, 0, 64, st));
+    }
     for (int k = 0; k < kmax; k += NB) {
         const int nbp = std::min(NB, kmax - k);
         EIGSOL_HIP(hipMemsetAsync(T, 0, NB * NB * sizeof(S), st));
-        for (int i = 0; i < nbp; ++i)
+        if (coop) {
+            EIGSOL_HIP(hipMemsetAsync(bar, 0, kBarBytes, st));
+            dev::QrCoopArgs<S> ca{R, m, k, nbp, V, T, part, tpart, x0s, bar, err, G >= 64};
+            void* kargs[] = {&ca};
+            static const bool plain = std::getenv("EIGSOL_HESS_COOP_PLAIN") != nullptr;   // profiling only
+            if (plain)
+                EIGSOL_HIP(hipLaunchKernel(reinterpret_cast<const void*>(dev::qr_panel_coop<S>), dim3(G),
+                                           dim3(dev::kCoopThreads), kargs, 0, st));
+            else
+                EIGSOL_HIP(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(dev::qr_panel_coop<S>), dim3(G),
+                                                      dim3(dev::kCoopThreads), kargs, 0, st));
+        }
+        for (int i = 0; !coop && i < nbp; ++i)
             hipLaunchKernelGGL(dev::qr_panel_col<S>, dim3(1), dim3(1024), m * sizeof(S), st, R, m, k, k + i, i, V, T);
         const int rows = m - k, c1 = k + nbp, mt = n - c1;
         if (mt > 0) {   // R(k:, c1:) <- (I - V T^H V^H) R(k:, c1:)
@@ -1538,8 +1754,15 @@ int qr_blocked(hipStream_t st, S* R, int m, int n, S* Q) {
         rankk_update<S, false>(st, m, rows, nbp, -1.0, Z2, m, Vr + k, m, Q + (int64_t)k * m, m);
     }
     EIGSOL_HIP(hipGetLastError());
-    for (void* p : {(void*)V, (void*)Vc, (void*)T, (void*)W, (void*)W2, (void*)Z, (void*)Z2, (void*)SK})
+    int errh = 0;
+    if (coop) {
+        EIGSOL_HIP(hipMemcpyAsync(&errh, err, sizeof(int), hipMemcpyDeviceToHost, st));
+        EIGSOL_HIP(hipStreamSynchronize(st));
+    }
+    for (void* p : {(void*)V, (void*)Vc, (void*)T, (void*)W, (void*)W2, (void*)Z, (void*)Z2, (void*)SK, (void*)part,
+                    (void*)tpart, (void*)x0s, (void*)bar, (void*)err})
         if (p) (void)hipFree(p);
+    if (errh) return fail(EIGSOL_E_HIP, "blocked QR: grid barrier timed out (internal error)");
     return EIGSOL_OK;
 }
 }  // namespace

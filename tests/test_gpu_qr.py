@@ -115,6 +115,29 @@ def test_qr_decompose_blocked_parity(ctx, shape, cplx):
     assert np.abs(Q.conj().T @ Q - np.eye(m)).max() <= 1e-12 * m
 
 
+@pytest.mark.parametrize("shape,dtype", [((2000, 1200), np.float64), ((1500, 1500), np.complex128),
+                                         ((600, 900), np.float64), ((1100, 700), np.float32)])
+def test_qr_decompose_coop_panel(ctx, shape, dtype, monkeypatch):
+    """The cooperative QR panel (qr_panel_coop: G blocks of rows, two grid barriers per column, the
+    two-level barrier from 64 blocks; the default from m = 256) against the one-launch-per-column panel
+    (EIGSOL_QR_COOP=0): Q and R agree to rounding, Q R = A and Q^H Q = I to the working precision
+    (qr_decompose.hpp:46-85)."""
+    rng = np.random.default_rng(sum(shape))
+    m, n = shape
+    A = rng.standard_normal((m, n))
+    if np.iscomplexobj(np.zeros(1, dtype)):
+        A = A + 1j * rng.standard_normal((m, n))
+    A = A.astype(dtype)
+    Q, R = E.qr_decompose(ctx, A)
+    monkeypatch.setenv("EIGSOL_QR_COOP", "0")
+    Q0, R0 = E.qr_decompose(ctx, A)
+    eps = np.finfo(dtype).eps
+    sc = np.linalg.norm(A)
+    assert np.abs(R - R0).max() <= 50 * eps * sc and np.abs(Q - Q0).max() <= 50 * eps * m
+    assert np.abs(Q @ R - A).max() <= 50 * eps * sc
+    assert np.abs(Q.conj().T @ Q - np.eye(m)).max() <= 50 * eps * m
+
+
 def test_kat_qr_eigenvalues_unshifted_matches_reference_counts(ctx):
     A = np.array([[2.0, 1.0], [1.0, 2.0]])
     r = E.qr_eigenvalues(ctx, A, E.SolverOptions(1000, 1e-12), variant="unshifted")
