@@ -384,7 +384,9 @@ class PowerSession:
                  17: "wide shifted inverse (fp64 factor + double-double residual refinement; "
                      "tiles = refinement steps of the last solve)",
                  18: "GMRES over the exact sparse LU (complete fill, no pivoting; tiles = Arnoldi "
-                     "steps of the last solve)"}
+                     "steps of the last solve)",
+                 19: "GMRES over the nested-dissection multifrontal LU (dense fronts, pivoting inside each "
+                     "front; tiles = Arnoldi steps of the last solve)"}
         return {"bytes_per_iteration": b.value, "grid": g.value, "tiles": t.value,
                 "variant": v.value, "kernel": names.get(v.value, "?"),
                 "iterations_per_launch": v.value - 10 if 12 <= v.value <= 14 else 1}

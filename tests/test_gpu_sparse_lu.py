@@ -195,3 +195,25 @@ def test_gmres_stagnation_falls_back_to_dense_lu(ctx, convdiff, env):
                                        S.start_vector(n, np.complex128))
     _check_fixture(r, fx, xref)
     A.close()
+
+
+def test_mid_size_general_sparse_defaults_to_the_direct_family(ctx, env):
+    """From n = 2048 (EIGSOL_SPARSE_FAMILY_MIN_N) a general sparse shifted factor takes the GMRES family's
+    direct factors (here the nested-dissection multifrontal LU, variant 19) instead of the RCM band LU,
+    whose one-workgroup solve was 15-40x slower per iteration at n = 4096-16384: the solution agrees with
+    the band LU's (EIGSOL_SPARSE_SOLVER=band) and is backward stable (solve_shifted.hpp:96-115)."""
+    rp, ci, v = S.convdiff_complex(64, seed=7)
+    n = 4096
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 3.0 - 0.2j
+    b = S.start_vector(n, np.complex128, seed=5)
+    s = E.ShiftedSession(A, sigma)
+    assert s.kernel_info()["variant"] == 19, s.kernel_info()
+    s.close()
+    y = E.solve_shifted(A, sigma, b)
+    env("EIGSOL_SPARSE_SOLVER", "band")
+    yb = E.solve_shifted(A, sigma, b)
+    assert np.linalg.norm(M @ y - sigma * y - b) <= 1e-11 * np.linalg.norm(b) * max(1.0, np.linalg.norm(y))
+    assert np.linalg.norm(y - yb) <= 1e-10 * np.linalg.norm(yb)
+    A.close()
