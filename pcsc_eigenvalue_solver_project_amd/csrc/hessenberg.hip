@@ -824,12 +824,14 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop(CoopArgs<S> a) {
 // (the norm partials, x0, xu, the partials of V^H xu and V(j + 1, 0:i)) loaded in one batch; V(j + 1, :)
 // is also the next column's V(j, :).  The same operations in the same order as hess_panel_coop<S, 1, true>:
 // bitwise its results (tests/test_gpu_qr.py::test_hessenberg_panel2_bitwise).
-template <class S>
+// kVG (orders past HessCfg<S>::kCoopMaxN, up to 64 rows per block x 256 blocks): v is not staged in LDS;
+// the GEMV reads the published column xu and scales it on the fly (the same value as the staged v).
+template <class S, bool kVG = false>
 __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop2(CoopArgs<S> a) {
     constexpr int NB = HessCfg<S>::NB;
     constexpr int kSl = kCoopThreads / NB;               // gather slices
     constexpr int kGU = 256 / kSl;                       // gather loads per thread (grid <= 256)
-    constexpr int kXU = HessCfg<S>::kCoopMaxN / kCoopThreads;   // xu loads per thread
+    constexpr int kXU = kVG ? 0 : HessCfg<S>::kCoopMaxN / kCoopThreads;   // xu loads per thread
     extern __shared__ double vsh_raw[];
     S* vsh = reinterpret_cast<S*>(vsh_raw);
     __shared__ S xs[64];
@@ -934,7 +936,7 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop2(CoopArgs<S> a) 
         }
         grid_barrier(a.bar, target, a.err, a.hier);
         // ---------------- P3 + P4: one batch of loads
-        S xt[kXU];
+        S xt[kXU > 0 ? kXU : 1];
 #pragma unroll
         for (int u = 0; u < kXU; ++u) xt[u] = ld_ag(&a.xu[min(max(tid + u * kCoopThreads, j + 2), n - 1)]);
         S gt[kGU];
@@ -1008,15 +1010,33 @@ __global__ __launch_bounds__(kCoopThreads) void hess_panel_coop2(CoopArgs<S> a) 
             const int cs = 16 * sub;
             const int r = min(r0 + rl, r1 - 1);
             int c = j + 1 + wv * sub + lane / rp;
-            constexpr int kB = kGemvBatch * (int)sizeof(double) / (int)sizeof(S);
-            for (; c + cs * (kB - 1) < n; c += cs * kB) {
-                S av[kB];
+            if constexpr (kVG) {
+                const S v0s = scal(v0, rv);
+                constexpr int kB = kGemvBatch * (int)sizeof(double) / (int)sizeof(S) / 2;
+                for (; c + cs * (kB - 1) < n; c += cs * kB) {
+                    S av[kB], xv[kB];
 #pragma unroll
-                for (int u = 0; u < kB; ++u) av[u] = a.A[r + (int64_t)(c + cs * u) * n];
+                    for (int u = 0; u < kB; ++u) {
+                        av[u] = a.A[r + (int64_t)(c + cs * u) * n];
+                        xv[u] = ld_ag(&a.xu[max(c + cs * u, j + 2)]);
+                    }
 #pragma unroll
-                for (int u = 0; u < kB; ++u) yacc = add(yacc, mul(av[u], vsh[c + cs * u]));
+                    for (int u = 0; u < kB; ++u)
+                        yacc = add(yacc, mul(av[u], c + cs * u == j + 1 ? v0s : scal(xv[u], rv)));
+                }
+                for (; c < n; c += cs)
+                    yacc = add(yacc, mul(a.A[r + (int64_t)c * n], c == j + 1 ? v0s : scal(ld_ag(&a.xu[max(c, j + 2)]), rv)));
+            } else {
+                constexpr int kB = kGemvBatch * (int)sizeof(double) / (int)sizeof(S);
+                for (; c + cs * (kB - 1) < n; c += cs * kB) {
+                    S av[kB];
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) av[u] = a.A[r + (int64_t)(c + cs * u) * n];
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) yacc = add(yacc, mul(av[u], vsh[c + cs * u]));
+                }
+                for (; c < n; c += cs) yacc = add(yacc, mul(a.A[r + (int64_t)c * n], vsh[c]));
             }
-            for (; c < n; c += cs) yacc = add(yacc, mul(a.A[r + (int64_t)c * n], vsh[c]));
         }
         ysum[wv][lane] = yacc;
         __syncthreads();
@@ -1561,8 +1581,14 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         return !(e && std::atoi(e) == 0);
     }();
     constexpr size_t kBarBytes = 9 * 64;
-    bool coop = coop_ok && n <= Cfg::kCoopMaxN && n <= 128 * G && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
-    const size_t coop_lds = (size_t)n * sizeof(S);
+    // past Cfg::kCoopMaxN (v no longer fits the panel's LDS) the merged panel reads v from the published
+    // column (hess_panel_coop2<S, true>), up to 64 rows per block (n <= 16384); EIGSOL_HESS_VG=0 keeps such
+    // orders on the per-column kernels
+    // (EIGSOL_HESS_VG=2 also below the limit: the bitwise test of the global-v form)
+    const char* vge = std::getenv("EIGSOL_HESS_VG");
+    const bool vg = (n > Cfg::kCoopMaxN || (vge && std::atoi(vge) == 2)) && n <= 64 * G && !(vge && std::atoi(vge) == 0);
+    bool coop = coop_ok && (n <= Cfg::kCoopMaxN || vg) && n <= 128 * G && std::getenv("EIGSOL_HESS_NO_COOP") == nullptr;
+    const size_t coop_lds = vg ? 0 : (size_t)n * sizeof(S);
     // two grid barriers per panel column (hess_panel_coop kMerge; EIGSOL_HESS_MERGE=0: three).  Round 6
     // (tools/r06_hess_merge_ab.sh, profiles/r06_hess_merge_ab.log): to_hessenberg 4096^2 0.184 / 0.185 ->
     // 0.182 / 0.176 s; QR 4096^2 unchanged within noise (0.885 / 0.885 against 0.888 / 0.882 s), complex
@@ -1576,9 +1602,11 @@ int hessenberg_blocked(hipStream_t st, S* A, int64_t n64) {
         const char* e = std::getenv("EIGSOL_HESS_PANEL2");
         return !(e && std::atoi(e) == 0);
     }();
+    if (vg && !(merge && panel2)) coop = false;   // only the merged LDS-cached panel has the global-v form
     const void* coop_kernel =
         n <= 64 * G
-            ? (merge ? (panel2 ? reinterpret_cast<const void*>(dev::hess_panel_coop2<S>)
+            ? (merge ? (panel2 ? (vg ? reinterpret_cast<const void*>(dev::hess_panel_coop2<S, true>)
+                                     : reinterpret_cast<const void*>(dev::hess_panel_coop2<S>))
                                : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1, true>))
                      : reinterpret_cast<const void*>(dev::hess_panel_coop<S, 1>))
             : (merge ? reinterpret_cast<const void*>(dev::hess_panel_coop<S, 2, true>)

@@ -376,6 +376,40 @@ def test_hessenberg_panel2_bitwise(ctx, dtype, n, monkeypatch):
         assert np.abs(H2 - O.hessenberg(A)).max() <= 1e-12 * np.linalg.norm(A)
 
 
+@pytest.mark.parametrize("dtype,n", [(np.complex128, 4500), (np.float64, 8400)])
+def test_hessenberg_coop_past_lds_limit(ctx, dtype, n, monkeypatch):
+    """Past the cooperative panel's LDS limit for v (complex 4096, real 8192) the merged panel reads v from
+    the published column (hess_panel_coop2<S, true>, default) instead of falling to the per-column kernels
+    (EIGSOL_HESS_VG=0): the same reflectors up to rounding (to_hessenberg.hpp:38-77)."""
+    rng = np.random.default_rng(n)
+    A = rng.standard_normal((n, n))
+    if dtype == np.complex128:
+        A = A + 1j * rng.standard_normal((n, n))
+    A = np.asfortranarray(A)
+    H = E.to_hessenberg(ctx, A)
+    monkeypatch.setenv("EIGSOL_HESS_VG", "0")
+    H0 = E.to_hessenberg(ctx, A)
+    scale = np.linalg.norm(A)
+    # two summation orders over thousands of dependent reflectors: agreement to ~1e-10 of the norm
+    assert np.abs(H - H0).max() <= 1e-9 * scale
+    assert np.abs(np.tril(H, -2)).max() == 0.0
+    assert abs(np.trace(H) - np.trace(A)) <= 1e-9 * scale
+    assert abs(np.linalg.norm(H) - scale) <= 1e-9 * scale
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_hessenberg_global_v_bitwise(ctx, dtype, monkeypatch):
+    """The global-v panel form (EIGSOL_HESS_VG=2 forces it below the LDS limit) scales the published column
+    on the fly to the same v the LDS form stages: bitwise the same H (n = 2100, 72 blocks)."""
+    rng = np.random.default_rng(2100)
+    A = rng.standard_normal((2100, 2100))
+    if dtype == np.complex128:
+        A = A + 1j * rng.standard_normal((2100, 2100))
+    H = E.to_hessenberg(ctx, A)
+    monkeypatch.setenv("EIGSOL_HESS_VG", "2")
+    assert E.to_hessenberg(ctx, A).tobytes() == H.tobytes()
+
+
 def test_complex_francis_4096_fixture(ctx):
     """Complex QR at the config-2 order: blocked complex Hessenberg, complex AED and multishift
     sweeps, matched one-to-one against LAPACK zgeev (tests/golden/qr_c4096_eigvals.npy)."""
