@@ -363,7 +363,7 @@ class PowerSession:
         call("eigsol_power_kernel_info", self.handle, C.byref(b), C.byref(g), C.byref(t), C.byref(v))
         names = {0: "csr_kernel (x gathered from HBM)", 1: "csr_win_kernel (x window staged in LDS)",
                  2: "dense_kernel (GEMV)", 3: "sptrsv_kernel (sync-free triangular solve)",
-                 4: "dense LU substitution (dense_lu_solve_kernel on one CU up to n = 512, else "
+                 4: "dense LU substitution (dense_lu_solve_kernel on one CU up to n = 64, else "
                     "dense_trsv2_kernel: 64-row block rows, inverted diagonal blocks, value flags)",
                  5: "csr_slice_kernel (64-row slices, one row per lane)",
                  6: "csr_row_kernel (one row per lane, single-precision fallback layout)",

@@ -2095,7 +2095,9 @@ template <class S>
 static int64_t kDenseSingleMax() {
     const char* e = std::getenv("EIGSOL_DENSE_TRSV_SINGLE_MAX");   // A/B: substitution crossover
     if (e) return std::atoll(e);
-    return 512;
+    // round 6 (profiles/r06_dense_small.log): the block-row substitution beats the one-workgroup one from
+    // n = 128 on (0.080 -> 0.030 ms per iteration at 128, 0.332 -> 0.047 ms at 512)
+    return 64;
 }
 
 template <class S>
