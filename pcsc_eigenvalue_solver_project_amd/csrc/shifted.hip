@@ -2465,13 +2465,13 @@ static int factor_csr_t(eigsol_csr* A, double sre, double sim, ShiftFactor** out
         BandPlan plan;
         SparseSolver fs = kSolverBand;
         const bool pre_forced = general_sparse_forced(fs);
-        // from n = 2048 (EIGSOL_SPARSE_FAMILY_MIN_N) too: on a 2-D stencil the band solve (one workgroup
-        // walking the band) took 2.2 ms per iteration at n = 4096 and 9.5 ms at 16384, the multifrontal
-        // LU 0.15 / 0.21 ms with a shorter set-up (round 6, tools/r06_small_sparse_paths.py,
+        // from n = 1024 (EIGSOL_SPARSE_FAMILY_MIN_N) too: on a 2-D stencil the band solve (one workgroup
+        // walking the band) took 0.50 ms per iteration at n = 1024, 2.2 ms at 4096 and 9.5 ms at 16384, the
+        // multifrontal LU 0.11 / 0.15 / 0.21 ms with a shorter set-up (round 6, tools/r06_small_sparse_paths.py,
         // profiles/r06_small_sparse_paths.log); the band LU stays the fallback for zero pivots
         static const int64_t family_min = [] {
             const char* e = std::getenv("EIGSOL_SPARSE_FAMILY_MIN_N");
-            return e ? (int64_t)std::atoll(e) : (int64_t)2048;
+            return e ? (int64_t)std::atoll(e) : (int64_t)1024;
         }();
         const bool large_gmres = !pre_forced && (n > 16384 || n >= family_min);
         if (!large_gmres && !(pre_forced && fs != kSolverBand)) band_plan(A->dtype, n, rp.data(), ci.data(), plan);

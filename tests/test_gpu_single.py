@@ -17,6 +17,8 @@ Tolerances (fp32):
   * dense and general-sparse (RCM band LU) shifted inverse in float: planted / numpy eigenvalues
     within 1e-4, solve backward errors at single precision (1e-4 ||M|| ||y||).
 """
+import os
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -247,8 +249,9 @@ def test_single_dense_shifted_native(ctx, dtype, n):
 
 def test_single_general_sparse_shifted_band(ctx):
     """complex<float> general sparse shifted inverse on the permuted convection-diffusion matrix
-    (nx = 40): the RCM band LU in single precision, the eigenvalue nearest the shift (numpy, fp64)
-    within 1e-4 relative."""
+    (nx = 40, n = 1600): the direct GMRES family on the values widened to double (the default from
+    n = 1024; the RCM band LU in single precision with EIGSOL_SPARSE_SOLVER=band, the second run), the
+    eigenvalue nearest the shift (numpy, fp64) within 1e-4 relative."""
     rp, ci, v = S.convdiff_complex(40)
     n = len(rp) - 1
     Md = sp.csr_matrix((v, ci, rp), shape=(n, n)).toarray()
@@ -259,10 +262,16 @@ def test_single_general_sparse_shifted_band(ctx):
     gap = np.min(np.abs(np.delete(ev, order[k]) - lam))
     sigma = np.complex64(lam + 0.1 * gap)
     A = E.CsrMatrix(ctx, rp, ci, v.astype(np.complex64), (n, n))
-    r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(300, 1e-6, sigma),
-                                       S.start_vector(n, np.complex64))
-    assert r.converged and abs(r.eigenvalue - lam) <= 1e-4 * (1 + abs(lam)), (r.eigenvalue, lam)
-    assert np.asarray(r.eigenvector).dtype == np.complex64
+    for band in (False, True):
+        if band:
+            os.environ["EIGSOL_SPARSE_SOLVER"] = "band"
+        try:
+            r = E.shifted_inverse_power_method(A, E.ShiftedSolverOptions(300, 1e-6, sigma),
+                                               S.start_vector(n, np.complex64))
+        finally:
+            os.environ.pop("EIGSOL_SPARSE_SOLVER", None)
+        assert r.converged and abs(r.eigenvalue - lam) <= 1e-4 * (1 + abs(lam)), (band, r.eigenvalue, lam)
+        assert np.asarray(r.eigenvector).dtype == np.complex64
 
 
 @pytest.mark.parametrize("dtype", SINGLE)
