@@ -133,6 +133,7 @@ struct ShiftFactor {
     int32_t* flag_b = nullptr;
     void* zf = nullptr;
     void* tinv = nullptr;         // [nblk][2] inverted diagonal blocks inv(L_kk), inv(U_kk), 64 x 64 column-major
+    void* tmul = nullptr;         // [nblk][2] premultiplied next-to-diagonal tiles (dense_tmul_kernel)
     int dense_v = 2;              // substitution kernel: 2 = dense_trsv2_kernel, 1 = dense_trsv_kernel (EIGSOL_DENSE_TRSV=1)
 };
 
@@ -1338,6 +1339,7 @@ struct DenseTriArgs {
     int32_t* flag_f;     // [nblk] epoch when z of the block row is published
     int32_t* flag_b;     // [nblk] epoch when y of the block row is published
     const S* tinv;       // dense_trsv2_kernel: [nblk][2] inv(L_kk), inv(U_kk), 64 x 64 column-major
+    const S* tmul;       // [nblk][2] inv(L_rr) L_{r,r-1}, inv(U_rr) U_{r,r+1} (dense_tmul_kernel)
     S* z;                // forward results (n)
     const S* b_plain;
     S* y_plain;
@@ -1592,6 +1594,44 @@ __global__ __launch_bounds__(256) void dense_tinv_kernel(const S* lu, int64_t n,
     for (int t = 0; t < 16; ++t) out[(16 * wv + t) * kDB + lane] = v[t];
 }
 
+// The premultiplied next-to-diagonal tiles of dense_trsv2_kernel's dense_pf 2: tmul + 4096 (2 r) =
+// inv(L_rr) L_{r,r-1} (r >= 1), tmul + 4096 (2 r + 1) = inv(U_rr) U_{r,r+1} (r <= nblk - 2), 64 x 64
+// column-major, rows past a partial last block and columns past a partial next block zero.  Thread =
+// one column, 16 rows.
+template <class S>
+__global__ __launch_bounds__(256) void dense_tmul_kernel(const S* lu, const S* tinv, int64_t n, int nblk, S* tmul) {
+    __shared__ S ti[kDB * (kDB + 1)];
+    __shared__ S tl[kDB * (kDB + 1)];
+    const int r = blockIdx.x, upper = blockIdx.y;
+    const int tid = threadIdx.x;
+    S* out = tmul + (int64_t)(2 * r + upper) * kDB * kDB;
+    const int c = upper ? r + 1 : r - 1;
+    if (c < 0 || c >= nblk) {
+        for (int e = tid; e < kDB * kDB; e += 256) out[e] = s_zero<S>();
+        return;
+    }
+    const int64_t r0 = (int64_t)r * kDB, c0 = (int64_t)c * kDB;
+    const int rn = (int)min<int64_t>(kDB, n - r0), cn = (int)min<int64_t>(kDB, n - c0);
+    const S* tv = tinv + (int64_t)(2 * r + upper) * kDB * kDB;
+    for (int e = tid; e < kDB * kDB; e += 256) {
+        const int i = e % kDB, j = e / kDB;
+        ti[i + j * (kDB + 1)] = tv[e];
+        tl[i + j * (kDB + 1)] = (i < rn && j < cn) ? lu[(r0 + i) + (c0 + j) * n] : s_zero<S>();
+    }
+    __syncthreads();
+    const int j = tid & 63, i0 = (tid >> 6) * 16;
+    S o[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) o[t] = s_zero<S>();
+    for (int k = 0; k < kDB; ++k) {
+        const S b = tl[k + j * (kDB + 1)];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) o[t] = add(o[t], mul(ti[(i0 + t) + k * (kDB + 1)], b));
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) out[(i0 + t) + j * kDB] = o[t];
+}
+
 // The multi-CU substitution with the diagonal blocks applied as products with their inverses
 // (dense_tinv_kernel) and every off-diagonal tile loaded before its block's flag is awaited (the
 // multifrontal row-block solve's scheme, mf_big_fwd_kernel).  A block row: each wave takes 16 columns
@@ -1637,9 +1677,10 @@ __device__ __forceinline__ S dn_poll(const S* p, int32_t* err) {
     return v;
 }
 
-template <class S, bool kIter>
+template <class S, bool kIter, int kPf>
 __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int parity) {
     __shared__ S part[4][kDB];
+    __shared__ S part2[4][kDB];
     __shared__ S zsh[4][16];
     __shared__ S vec[kDB];
     __shared__ Prologue pro;
@@ -1704,24 +1745,91 @@ __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int
             }
             S acc = s_zero<S>();
             const int nc = fwd ? r : a.nblk - 1 - r;
+            // dense_pf 2: the block next to the diagonal enters as a product with the premultiplied tile
+            // inv(T_rr) T_{r, r -/+ 1} (dense_tmul_kernel) after y' = inv(T_rr) (rhs - the other blocks)
+            // is formed, so the chain's hand-off is followed by one 64 x 64 product instead of two
+            const bool premul = kPf == 2 && nc > 0;
+            const int nacc = premul ? nc - 1 : nc;
             const S* src = fwd ? zcur : ycur;
-            for (int m = 0; m < nc; ++m) {
+            const int j0 = 16 * wv;
+            const S* tile = a.lu + row;
+            // this wave's 64 x 16 piece of column block m's tile
+            auto load_tile = [&](int m, S* tv) {
                 const int c = fwd ? m : a.nblk - 1 - m;
                 const int64_t c0 = (int64_t)c * kDB;
                 const int cn = (int)min<int64_t>(kDB, n - c0);
-                const int j0 = 16 * wv;
-                S tv[16];
-                const S* tile = a.lu + row;
 #pragma unroll
                 for (int t = 0; t < 16; ++t) tv[t] = tile[(c0 + min(j0 + t, cn - 1)) * n];
-                if (lane < 16) zsh[wv][lane] = j0 + lane < cn ? dn_poll(src + c0 + j0 + lane, a.err) : s_zero<S>();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            };
+            if constexpr (kPf >= 1) {
+                // software-pipelined (default): the first poll of block m's values is issued before the
+                // loads of tile m + 1, so the poll's wait leaves those in flight and a wave behind the
+                // chain streams its tiles instead of paying one load latency per block; the same
+                // products in the same order (bitwise the unpipelined loop)
+                S tv[16], tn[16];
+                if (nacc > 0) load_tile(0, tv);
+                for (int m = 0; m < nacc; ++m) {
+                    const int c = fwd ? m : a.nblk - 1 - m;
+                    const int64_t c0 = (int64_t)c * kDB;
+                    const int cn = (int)min<int64_t>(kDB, n - c0);
+                    const bool mine = lane < 16 && j0 + lane < cn;
+                    S zv = s_zero<S>();
+                    if (mine) zv = ld_coh(src + c0 + j0 + lane);
+                    if (m + 1 < nacc) load_tile(m + 1, tn);
+                    if (mine) {
+                        int spins = 0;
+                        while (dn_unready(zv)) {
+                            __builtin_amdgcn_s_sleep(1);
+                            zv = ld_coh(src + c0 + j0 + lane);
+                            if (++spins > (1 << 24)) {
+                                atomicOr(a.err, 1);
+                                break;
+                            }
+                        }
+                    }
+                    if (lane < 16) zsh[wv][lane] = zv;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-                for (int t = 0; t < 16; ++t) acc = add(acc, mul(tv[t], zsh[wv][t]));
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
+                    for (int t = 0; t < 16; ++t) acc = add(acc, mul(tv[t], zsh[wv][t]));
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) tv[t] = tn[t];
+                }
+            } else {
+                for (int m = 0; m < nc; ++m) {
+                    const int c = fwd ? m : a.nblk - 1 - m;
+                    const int64_t c0 = (int64_t)c * kDB;
+                    const int cn = (int)min<int64_t>(kDB, n - c0);
+                    S tv[16];
+                    load_tile(m, tv);
+                    if (lane < 16) zsh[wv][lane] = j0 + lane < cn ? dn_poll(src + c0 + j0 + lane, a.err) : s_zero<S>();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                    for (int t = 0; t < 16; ++t) acc = add(acc, mul(tv[t], zsh[wv][t]));
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            // premultiplied step: its tile piece and the first poll of its values issued now, under the
+            // reductions below
+            S tm[16];
+            S zl = s_zero<S>();
+            int64_t lc0 = 0;
+            bool lmine = false;
+            if (premul) {
+                const int c = fwd ? r - 1 : r + 1;
+                lc0 = (int64_t)c * kDB;
+                const int cn = (int)min<int64_t>(kDB, n - lc0);
+                lmine = lane < 16 && j0 + lane < cn;
+                if (lmine) zl = ld_coh(src + lc0 + j0 + lane);
+                const S* tmp = a.tmul + (int64_t)(2 * r + (fwd ? 0 : 1)) * kDB * kDB + j0 * kDB + lane;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) tm[t] = tmp[t * kDB];
             }
             part[wv][lane] = acc;
             __syncthreads();
@@ -1734,8 +1842,32 @@ __global__ __launch_bounds__(256) void dense_trsv2_kernel(DenseTriArgs<S> a, int
             for (int t = 0; t < 16; ++t) p = add(p, mul(iv[t], vec[16 * wv + t]));
             part[wv][lane] = p;
             __syncthreads();
+            S y = s_zero<S>();
+            if (wv == 0) y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+            if (premul) {
+                if (lmine) {
+                    int spins = 0;
+                    while (dn_unready(zl)) {
+                        __builtin_amdgcn_s_sleep(1);
+                        zl = ld_coh(src + lc0 + j0 + lane);
+                        if (++spins > (1 << 24)) {
+                            atomicOr(a.err, 1);
+                            break;
+                        }
+                    }
+                }
+                if (lane < 16) zsh[wv][lane] = zl;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                S q = s_zero<S>();
+#pragma unroll
+                for (int t = 0; t < 16; ++t) q = add(q, mul(tm[t], zsh[wv][t]));
+                part2[wv][lane] = q;
+                __syncthreads();
+                if (wv == 0) y = sub(y, add(add(part2[0][lane], part2[1][lane]), add(part2[2][lane], part2[3][lane])));
+            }
             if (wv == 0) {
-                const S y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
                 if (lane < rn) {
                     // publish (the value is its own flag)
                     if (fwd) {
@@ -2032,6 +2164,23 @@ __global__ __launch_bounds__(256) void convert_kernel(const S* __restrict__ in, 
 }  // namespace dev
 
 // ================================================================== host side
+// dense_trsv2_kernel's loop form (EIGSOL_DENSE_PF, read per call): 0 one tile load per block, 1 tile
+// loads one block ahead, 2 (default) also the premultiplied next-to-diagonal block; each form is its own
+// instantiation so the others' registers do not bound it
+template <class S>
+static const void* dense_trsv2_ptr(bool iter, int pf) {
+    if (pf <= 0) return iter ? reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, true, 0>)
+                             : reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, false, 0>);
+    if (pf == 1) return iter ? reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, true, 1>)
+                             : reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, false, 1>);
+    return iter ? reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, true, 2>)
+                : reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, false, 2>);
+}
+template <class S>
+static int dense_pf_mode() {
+    const char* e = std::getenv("EIGSOL_DENSE_PF");
+    return e ? std::max(0, std::min(2, std::atoi(e))) : 2;
+}
 // the dense LU (and the densified / banded general-sparse paths) is built for every scalar: single
 // precision factors and solves in float (rank-NB updates on v_mfma_f32_16x16x4_f32); ILU(0)-GMRES
 // stays double-only
@@ -2077,7 +2226,7 @@ static void shift_free(ShiftFactor* f) {
                     f->tpiv, (void*)f->tcol, f->tval, (void*)f->porder, (void*)f->pptr, (void*)f->pcol, f->pval,
                     f->ppiv,
                     (void*)f->work, (void*)f->err, f->wave_part, f->lu, (void*)f->perm,
-                    (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf, f->tinv,
+                    (void*)f->zero_pivot, (void*)f->flag_f, (void*)f->flag_b, f->zf, f->tinv, f->tmul,
                     f->kpart, f->kblk, f->promo})
         if (p) hipFree(p);
     for (int j = 0; j < dev::kMaxMulti; ++j) {
@@ -2183,10 +2332,19 @@ static int dense_lu_factor(ShiftFactor* f, bool from_sparse) {
             hipLaunchKernelGGL((dev::dense_tinv_kernel<S>), dim3(nblk, 2), dim3(256), 0, st, static_cast<const S*>(f->lu),
                                n, static_cast<S*>(f->tinv));
             EIGSOL_HIP(hipGetLastError());
+            EIGSOL_HIP(hipMalloc(&f->tmul, sizeof(S) * (size_t)nblk * 2 * dev::kDB * dev::kDB));
+            hipLaunchKernelGGL((dev::dense_tmul_kernel<S>), dim3(nblk, 2), dim3(256), 0, st, static_cast<const S*>(f->lu),
+                               static_cast<const S*>(f->tinv), n, nblk, static_cast<S*>(f->tmul));
+            EIGSOL_HIP(hipGetLastError());
             // one block row per workgroup while they all fit on the device at once (a cooperative launch)
-            int per_cu = 1;
-            EIGSOL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, true>), 256, 0));
+            // (the fewest resident over the loop forms, so a later EIGSOL_DENSE_PF still fits the grid)
+            int per_cu = 1 << 20;
+            for (int pf = 0; pf < 3; ++pf)
+                for (int it = 0; it < 2; ++it) {
+                    int o = 1;
+                    EIGSOL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, dense_trsv2_ptr<S>(it != 0, pf), 256, 0));
+                    per_cu = std::min(per_cu, o);
+                }
             f->grid = std::max(1, std::min(nblk, std::max(1, per_cu) * f->ctx->num_cus));
             if (const char* e = std::getenv("EIGSOL_DENSE_TRSV_GRID")) f->grid = std::max(1, std::min(nblk, std::atoi(e)));
             hipFree(f->wave_part);
@@ -2396,6 +2554,7 @@ static int gmres_dense_fallback(ShiftFactor* f, int rc_gmres) {
         f->flag_b = g->flag_b;
         f->zf = g->zf;
         f->tinv = g->tinv;
+        f->tmul = g->tmul;
         f->dense_v = g->dense_v;
         f->work = g->work;
         f->err = g->err;
@@ -3589,6 +3748,7 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.flag_f = f->flag_f;
         a.flag_b = f->flag_b;
         a.tinv = static_cast<const S*>(f->tinv);
+        a.tmul = static_cast<const S*>(f->tmul);
         a.z = static_cast<S*>(f->zf);
         a.b_plain = static_cast<const S*>(b);
         a.y_plain = static_cast<S*>(y);
@@ -3605,11 +3765,9 @@ static int shift_launch_t(ShiftFactor* f, bool iter, const void* b, void* y, voi
         a.sig_im = f->sig_im;
         // cooperative: the persistent block-row workgroups wait on each other's epoch flags
         void* kargs[] = {&a, &parity};
-        const void* dk = f->dense_v == 2
-                             ? (iter ? reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, true>)
-                                     : reinterpret_cast<const void*>(dev::dense_trsv2_kernel<S, false>))
-                             : (iter ? reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, true>)
-                                     : reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, false>));
+        const void* dk = f->dense_v == 2 ? dense_trsv2_ptr<S>(iter, dense_pf_mode<S>())
+                                         : (iter ? reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, true>)
+                                                 : reinterpret_cast<const void*>(dev::dense_trsv_kernel<S, false>));
         EIGSOL_HIP(hipLaunchCooperativeKernel(dk, dim3(f->grid), dim3(256), kargs, 0, st));
     } else {
         dev::DenseSolveArgs<S> a{};
