@@ -960,8 +960,12 @@ __global__ __launch_bounds__(256) void mf_fwd_asm_kernel(const MfFront* fr, cons
 template <class S>
 __device__ __forceinline__ S mf_rls(S v, int j) { return mf_rl(v, j); }
 
+// scalars per pivot block of the large fronts in Tinv: inv(L_kk), inv(U_kk) (mf_inv_kernel), then the
+// premultiplied next-to-diagonal tiles inv(L_kk) L_{k,k-1}, inv(U_kk) U_{k,k+1} (mf_premul_kernel)
+constexpr int kMfTinv = 16384;
+
 // Inverted diagonal blocks of the large fronts (one workgroup per pivot block, after the
-// factorization): Tinv + 8192 k holds inv(L_kk) (unit lower), then inv(U_kk), 64 x 64 column-major,
+// factorization): Tinv + kMfTinv k holds inv(L_kk) (unit lower), then inv(U_kk), 64 x 64 column-major,
 // the identity past a partial block's rn rows.  The solves then apply a diagonal block as a
 // 64 x 64 product split over the four waves instead of a 64-step dependent chain on one wave.
 template <class S>
@@ -980,7 +984,7 @@ __global__ __launch_bounds__(256) void mf_inv_kernel(const MfFront* fr, const in
         T[i + j * 65] = (i < rn && j < rn) ? A[(r0 + i) + (int64_t)(r0 + j) * d] : (i == j ? one : s_zero<S>());
     }
     __syncthreads();
-    S* out = Tinv + (int64_t)(f.flag0 + k) * 8192;
+    S* out = Tinv + (int64_t)(f.flag0 + k) * kMfTinv;
     // inv(L): thread t < 64 solves column t by forward substitution (unit diagonal)
     if (tid < 64) {
         const int t = tid;
@@ -1156,6 +1160,50 @@ __global__ __launch_bounds__(256) void mf_invform2_kernel(const MfFront* fr, con
 }
 
 
+// The premultiplied next-to-diagonal tiles of the large fronts' row-block solves (bo & 8), one
+// workgroup per pivot block after mf_inv_kernel: Tinv + kMfTinv k + 8192 = inv(L_kk) L_{k,k-1} (k >= 1;
+// rows past a partial block zero), + 12288 = inv(U_kk) U_{k,k+1} (k <= nblk - 2; columns past a partial
+// next block zero), 64 x 64 column-major.  Thread = one column, 16 rows.
+template <class S>
+__global__ __launch_bounds__(256) void mf_premul_kernel(const MfFront* fr, const int32_t* tab, const S* F, S* Tinv) {
+    __shared__ S ti[64 * 65];
+    __shared__ S tl[64 * 65];
+    const int s = tab[2 * blockIdx.x], k = tab[2 * blockIdx.x + 1];
+    const MfFront f = fr[s];
+    const int tid = threadIdx.x, d = f.d, ns = f.ns;
+    const int nblk = (ns + 63) / 64;
+    const int r0 = 64 * k, rn = min(64, ns - r0);
+    const S* A = F + f.off;
+    S* base = Tinv + (int64_t)(f.flag0 + k) * kMfTinv;
+    for (int up = 0; up < 2; ++up) {
+        S* out = base + 8192 + 4096 * up;
+        const int c = up ? k + 1 : k - 1;
+        if (c < 0 || c >= nblk) {
+            for (int e = tid; e < 4096; e += 256) out[e] = s_zero<S>();
+            continue;
+        }
+        const int c0 = 64 * c, cn = min(64, ns - c0);
+        __syncthreads();
+        for (int e = tid; e < 4096; e += 256) {
+            const int i = e & 63, j = e >> 6;
+            ti[i + j * 65] = base[4096 * up + e];
+            tl[i + j * 65] = (i < rn && j < cn) ? A[(r0 + i) + (int64_t)(c0 + j) * d] : s_zero<S>();
+        }
+        __syncthreads();
+        const int j = tid & 63, i0 = (tid >> 6) * 16;
+        S o[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) o[t] = s_zero<S>();
+        for (int q = 0; q < 64; ++q) {
+            const S b = tl[q + j * 65];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) o[t] = add(o[t], mul(ti[(i0 + t) + q * 65], b));
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) out[(i0 + t) + j * 64] = o[t];
+    }
+}
+
 // acc += tile(row, c0 .. c0 + 16) * yv over the columns below lim (tile values already loaded)
 template <class S>
 __device__ __forceinline__ void mf_acc16(S& acc, const S (&tv)[16], const S* yv, int c0, int lim) {
@@ -1187,7 +1235,7 @@ __device__ __forceinline__ void mf_big_fwd_block(const int bid, const MfFront* f
     const int row = r0 + min(lane, rn - 1);
     S iv[16];
     if (piv) {
-        const S* ti = Tinv + (int64_t)(f.flag0 + rb) * 8192 + lane + (16 * wv) * 64;
+        const S* ti = Tinv + (int64_t)(f.flag0 + rb) * kMfTinv + lane + (16 * wv) * 64;
 #pragma unroll
         for (int t = 0; t < 16; ++t) iv[t] = ti[t * 64];
     }
@@ -1197,7 +1245,11 @@ __device__ __forceinline__ void mf_big_fwd_block(const int bid, const MfFront* f
     // zpoll (mf_fwd_height_kernel): z is assembled in this launch and value-flagged; wave 0 polls it after
     // the chain and hands the slot back to the sentinel (this workgroup is its only reader)
     S zr = (!zpoll && lane < rn) ? z[f.zoff + r0 + lane] : s_zero<S>();
-    const int cend = piv ? rb : nblk;
+    // bo & 8 (value flags only): block rb - 1 enters last, as a product with the premultiplied tile
+    // inv(L_rr) L_{r,r-1} after y' = inv(L_rr) (z - the other blocks), so a hand-off is followed by one
+    // 64 x 64 product instead of two
+    const bool premul = (bo & 12) == 12 && piv && rb >= 1;
+    const int cend = piv ? (premul ? rb - 1 : rb) : nblk;
     for (int c = 0; c < cend; ++c) {
         const int c0 = 64 * c + 16 * wv;
         S tv[16];
@@ -1219,6 +1271,15 @@ __device__ __forceinline__ void mf_big_fwd_block(const int bid, const MfFront* f
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
+    S tm[16];
+    S yl = s_zero<S>();
+    const int lc0 = 64 * (rb - 1) + 16 * wv;
+    if (premul) {
+        if (lane < 16) yl = mf_ld(w + f.c0 + lc0 + lane);   // first poll, under the reductions
+        const S* tp = Tinv + (int64_t)(f.flag0 + rb) * kMfTinv + 8192 + lane + (16 * wv) * 64;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) tm[t] = tp[t * 64];
+    }
     if (zpoll && wv == 0 && lane < rn) {
         zr = mf_poll(z + f.zoff + r0 + lane, err, bo);
         mf_st(z + f.zoff + r0 + lane, mf_sent(s_zero<S>()));
@@ -1237,8 +1298,25 @@ __device__ __forceinline__ void mf_big_fwd_block(const int bid, const MfFront* f
     for (int t = 0; t < 16; ++t) p = add(p, mul(iv[t], vsh[16 * wv + t]));
     part[wv][lane] = p;
     __syncthreads();
+    S y = s_zero<S>();
+    if (wv == 0) y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+    if (premul) {
+        __shared__ S part2[4][64];
+        if (lane < 16) {
+            if (mf_unready(yl)) yl = mf_poll(w + f.c0 + lc0 + lane, err, bo);
+            ysh[wv][lane] = yl;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        S q = s_zero<S>();
+#pragma unroll
+        for (int t = 0; t < 16; ++t) q = add(q, mul(tm[t], ysh[wv][t]));
+        part2[wv][lane] = q;
+        __syncthreads();
+        if (wv == 0) y = sub(y, add(add(part2[0][lane], part2[1][lane]), add(part2[2][lane], part2[3][lane])));
+    }
     if (wv != 0) return;
-    const S y = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
     if (bo & 4) {
         // publish (the value is its own flag); x of these rows becomes "unsolved" for the backward pass
         if (lane < rn) {
@@ -1298,7 +1376,7 @@ __device__ __forceinline__ void mf_big_bwd_block(const int bid, const MfFront* f
     const int row = r0 + min(lane, rn - 1);
     S iv[16];
     {
-        const S* ti = Tinv + (int64_t)(f.flag0 + rb) * 8192 + 4096 + lane + (16 * wv) * 64;
+        const S* ti = Tinv + (int64_t)(f.flag0 + rb) * kMfTinv + 4096 + lane + (16 * wv) * 64;
 #pragma unroll
         for (int t = 0; t < 16; ++t) iv[t] = ti[t * 64];
     }
@@ -1328,8 +1406,10 @@ __device__ __forceinline__ void mf_big_bwd_block(const int bid, const MfFront* f
             mf_acc16(acc, ta, xsh + q0, q0, ms);
         }
     }
-    // later pivot blocks of this front as their flags rise (the last block first)
-    for (int c = nblk - 1; c > rb; --c) {
+    // later pivot blocks of this front as their flags rise (the last block first); bo & 8: block rb + 1
+    // last, as a product with the premultiplied inv(U_rr) U_{r,r+1} (see the forward block)
+    const bool premul = (bo & 12) == 12 && rb + 1 < nblk;
+    for (int c = nblk - 1; c > (premul ? rb + 1 : rb); --c) {
         const int c0 = 64 * c + 16 * wv;
         S tv[16];
         const S* tile = A + row;
@@ -1350,6 +1430,15 @@ __device__ __forceinline__ void mf_big_bwd_block(const int bid, const MfFront* f
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
+    S tm[16];
+    S xl = s_zero<S>();
+    const int lc0 = 64 * (rb + 1) + 16 * wv;
+    if (premul) {
+        if (lane < 16 && lc0 + lane < ns) xl = mf_ld(x + f.c0 + lc0 + lane);
+        const S* tp = Tinv + (int64_t)(f.flag0 + rb) * kMfTinv + 12288 + lane + (16 * wv) * 64;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) tm[t] = tp[t * 64];
+    }
     part[wv][lane] = acc;
     __syncthreads();
     if (wv == 0) {
@@ -1362,8 +1451,29 @@ __device__ __forceinline__ void mf_big_bwd_block(const int bid, const MfFront* f
     for (int t = 0; t < 16; ++t) p = add(p, mul(iv[t], vsh[16 * wv + t]));
     part[wv][lane] = p;
     __syncthreads();
+    S xv = s_zero<S>();
+    if (wv == 0) xv = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
+    if (premul) {
+        __shared__ S part2[4][64];
+        if (lane < 16) {
+            if (lc0 + lane < ns) {
+                if (mf_unready(xl)) xl = mf_poll(x + f.c0 + lc0 + lane, err, bo);
+            } else {
+                xl = s_zero<S>();
+            }
+            ysh[wv][lane] = xl;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        S q = s_zero<S>();
+#pragma unroll
+        for (int t = 0; t < 16; ++t) q = add(q, mul(tm[t], ysh[wv][t]));
+        part2[wv][lane] = q;
+        __syncthreads();
+        if (wv == 0) xv = sub(xv, add(add(part2[0][lane], part2[1][lane]), add(part2[2][lane], part2[3][lane])));
+    }
     if (wv != 0) return;
-    const S xv = add(add(part[0][lane], part[1][lane]), add(part[2][lane], part[3][lane]));
     if (bo & 4) {
         if (lane < rn) mf_st(x + f.c0 + r0 + lane, mf_clean(xv));
         return;
@@ -1449,12 +1559,12 @@ __global__ __launch_bounds__(256) void mf_big_fwd2_kernel(const MfFront* fr, con
     const int rowb = hasb ? ra0 + 64 + min(lane, rnb - 1) : rowa;
     S iva[16], ivb[16];
     if (piv) {
-        const S* ti = Tinv + (int64_t)(f.flag0 + ba) * 8192 + lane + (16 * wv) * 64;
+        const S* ti = Tinv + (int64_t)(f.flag0 + ba) * kMfTinv + lane + (16 * wv) * 64;
 #pragma unroll
         for (int t = 0; t < 16; ++t) iva[t] = ti[t * 64];
     }
     if (hasb) {
-        const S* ti = Tinv + (int64_t)(f.flag0 + ba + 1) * 8192 + lane + (16 * wv) * 64;
+        const S* ti = Tinv + (int64_t)(f.flag0 + ba + 1) * kMfTinv + lane + (16 * wv) * 64;
 #pragma unroll
         for (int t = 0; t < 16; ++t) ivb[t] = ti[t * 64];
     }
@@ -1540,12 +1650,12 @@ __global__ __launch_bounds__(256) void mf_big_bwd2_kernel(const MfFront* fr, con
     const int rowh = hash ? rh0 + min(lane, rnh - 1) : rowl;
     S ivl[16], ivh[16];
     {
-        const S* ti = Tinv + (int64_t)(f.flag0 + bl) * 8192 + 4096 + lane + (16 * wv) * 64;
+        const S* ti = Tinv + (int64_t)(f.flag0 + bl) * kMfTinv + 4096 + lane + (16 * wv) * 64;
 #pragma unroll
         for (int t = 0; t < 16; ++t) ivl[t] = ti[t * 64];
     }
     if (hash) {
-        const S* ti = Tinv + (int64_t)(f.flag0 + bl + 1) * 8192 + 4096 + lane + (16 * wv) * 64;
+        const S* ti = Tinv + (int64_t)(f.flag0 + bl + 1) * kMfTinv + 4096 + lane + (16 * wv) * 64;
 #pragma unroll
         for (int t = 0; t < 16; ++t) ivh[t] = ti[t * 64];
     }
@@ -1668,7 +1778,7 @@ struct MfFactor {
     int32_t* flags = nullptr;         // one per pivot block of the large fronts (epoch words)
     int32_t* err = nullptr;           // a flag wait that timed out
     void* z = nullptr;                // large fronts' assembled right-hand sides
-    void* tinv = nullptr;             // inverted diagonal blocks of the large fronts (8192 scalars each)
+    void* tinv = nullptr;             // inverted diagonal blocks of the large fronts and premultiplied tiles (kMfTinv scalars each)
     int32_t epoch = 0;
     int32_t hflow = 0;
     int32_t* flow_f = nullptr;
@@ -2686,6 +2796,12 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
         const char* e = std::getenv("EIGSOL_MF_VALFLAG");
         if (!(e && std::atoi(e) == 0)) f->backoff |= 4;
     }
+    // the large fronts' row-block solves take their next-to-diagonal block premultiplied (bit 8, with
+    // value flags; EIGSOL_MF_PREMUL=0: off)
+    {
+        const char* e = std::getenv("EIGSOL_MF_PREMUL");
+        if (!(e && std::atoi(e) == 0)) f->backoff |= 8;
+    }
     f->lds_fwd.assign(H + 1, 0);
     f->lds_bwd.assign(H + 1, 0);
     // the inverse-form branch keeps 256 partial sums after the front's vectors
@@ -2727,7 +2843,7 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
     dm((void**)&f->err, 4);
     dm(&f->z, (size_t)zsz * sb);
     dm((void**)&f->bigm, (size_t)n);
-    dm(&f->tinv, (size_t)nflag * 8192 * sb);
+    dm(&f->tinv, (size_t)nflag * dev::kMfTinv * sb);
     f->hflow = X.hflow;
     f->nflow = (int32_t)X.flow_f.size();
     f->lds_flow_f = X.lds_flow_f;
@@ -2813,9 +2929,13 @@ int mf_create_t(eigsol_ctx* ctx, int dtype, MfHost& X, const S* vals, MfFactor**
                 hipLaunchKernelGGL((dev::mf_gemm_kernel<S, NB>), dim3(l.cnt), dim3(256), 0, st, f->fronts, d_tab + l.off,
                                    l.q, F);
         }
-        if (!tabb.empty())
+        if (!tabb.empty()) {
             hipLaunchKernelGGL((dev::mf_inv_kernel<S>), dim3(tabb.size() / 2), dim3(256), 0, st, f->fronts, f->tabb, F,
                                static_cast<S*>(f->tinv));
+            if ((f->backoff & 12) == 12)
+                hipLaunchKernelGGL((dev::mf_premul_kernel<S>), dim3(tabb.size() / 2), dim3(256), 0, st, f->fronts,
+                                   f->tabb, F, static_cast<S*>(f->tinv));
+        }
         if (d_inv)
         {
             // EIGSOL_MF_INVFORM=1: round 5's kernel (one HBM load per multiply-add of L21 inv(L11) and inv(U11) U12)

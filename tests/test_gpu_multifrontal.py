@@ -316,6 +316,7 @@ def test_row_block_pairs_bitwise(ctx, env, nx, big, real):
     complex."""
     _mf_env(env)
     env("EIGSOL_MF_LEAF", "24" if nx == 45 else "64")
+    env("EIGSOL_MF_PREMUL", "0")   # the pairs keep the plain chain's order
     if big is not None:
         env("EIGSOL_MF_BIG_NS", big)
     rp, ci, v = S.convdiff_complex(nx, seed=13)
@@ -333,6 +334,35 @@ def test_row_block_pairs_bitwise(ctx, env, nx, big, real):
         ys[pair] = E.solve_shifted(A, sigma, b)
     assert np.linalg.norm(M @ ys["1"] - sigma * ys["1"] - b) <= 1e-10 * np.linalg.norm(b) * max(1.0, np.linalg.norm(ys["1"]))
     assert np.array_equal(ys["0"], ys["1"])
+    A.close()
+
+
+@pytest.mark.parametrize("nx,big,real", [(45, "1", False), (300, None, False), (120, "64", True)])
+def test_premultiplied_next_block(ctx, env, nx, big, real):
+    """The large fronts' row-block solves with the block next to the diagonal premultiplied by the
+    inverted diagonal block (mf_premul_kernel; EIGSOL_MF_PREMUL, default on) against the plain chain
+    (=0): both solve M x = b to 1e-10 and agree within 1e-9 relative — fronts with odd and even block
+    counts, partial last blocks, struct rows, real and complex."""
+    _mf_env(env)
+    env("EIGSOL_MF_LEAF", "24" if nx == 45 else "64")
+    if big is not None:
+        env("EIGSOL_MF_BIG_NS", big)
+    rp, ci, v = S.convdiff_complex(nx, seed=13)
+    if real:
+        v = np.ascontiguousarray(v.real)
+    n = nx * nx
+    M = sp.csr_matrix((v, ci, rp), shape=(n, n))
+    A = E.CsrMatrix(ctx, rp, ci, v, (n, n))
+    sigma = 8.5 if real else 3.0 - 0.2j
+    b = S.start_vector(n, np.complex128 if not real else np.float64, seed=5)
+    ys = {}
+    for pm in ("1", "0"):
+        env("EIGSOL_MF_PREMUL", pm)
+        assert _variant(A, sigma) == 19
+        ys[pm] = E.solve_shifted(A, sigma, b)
+        y = ys[pm]
+        assert np.linalg.norm(M @ y - sigma * y - b) <= 1e-10 * np.linalg.norm(b) * max(1.0, np.linalg.norm(y))
+    assert np.linalg.norm(ys["1"] - ys["0"]) <= 1e-9 * np.linalg.norm(ys["0"])
     A.close()
 
 
