@@ -16,6 +16,18 @@
 
 #include "kernels_common.hpp"
 
+// columns per load batch of dense_kernel (EIGSOL_DENSE_KU overrides at build time).  Round 6
+// (tools/r06_dense_ku_ab.sh, 16384^2): f64 4 / 8 / 12 / 16 -> 0.324 / 0.324 / 0.343 / 0.334 ms,
+// c128 0.660-0.667 / 0.661 / 0.663-0.667 / 0.647-0.649 ms: 8 for f64, 16 for 16-byte scalars
+template <class S>
+constexpr int dense_ku() {
+#ifdef EIGSOL_DENSE_KU
+    return EIGSOL_DENSE_KU;
+#else
+    return sizeof(S) == 16 ? 16 : 8;
+#endif
+}
+
 namespace eigsol {
 namespace dev {
 
@@ -136,7 +148,7 @@ __global__ __launch_bounds__(kThreads) void dense_kernel(DenseArgs<S> a, int par
     {
         // batches of kU columns, all loads issued before the products (A read once: non-temporal),
         // the same per-row summation order as the one-column loop below
-        constexpr int kU = 8;
+        constexpr int kU = dense_ku<S>();
         if (vec) {
             for (; j + kU <= wc1; j += kU) {
                 S xj[kU];
